@@ -1,0 +1,272 @@
+"""Benchmark: env-steps/s of the fused racing-env step at 65 536 envs per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--num-envs 65536]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A "step" is one pass of the hot path (ManagerBasedDiffRLEnv.step equivalent:
+action processing, CTBR controller, integrator, collision, gate progress,
+reward, termination, in-lane reset, observation, log reduction) over all envs
+of a rank, with pre-generated synthetic actions already resident in HBM.
+Envs shard one shard per GPU with no data-path collective ("scaling": "weak");
+`value` = envs * world_size * K / max-over-ranks wall time.
+
+Also reported (same JSON line): the fused kernel's roofline (HIP events
+around every env-kernel launch of an eager pass, algorithmic bytes from
+gr_bytes_per_env_step), the policy-in-the-loop rate (step + actor MLP), one
+PPO training iteration's Perf/total_fps at 4 096 envs (config C2), and the
+CPU oracle timed on the host ("port", rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from generalizableracing_amd.envs.racing_cfg import RacingEnvCfg, SceneCfg, SimCfg, TerrainCfg  # noqa: E402
+from generalizableracing_amd.envs.racing_env import RacingEnv  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+ACTION_RING = 64
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=1024)
+    p.add_argument("--warmup", type=int, default=64)
+    p.add_argument("--num-envs", type=int, default=65536)
+    p.add_argument("--gates", type=int, default=8)
+    p.add_argument("--integrator", default="dd_explicit")
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--no-extras", action="store_true", help="skip policy/train/cpu legs (profiling runs)")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    return p.parse_args()
+
+
+def barrier():
+    if dist.is_initialized():
+        dist.barrier()
+
+
+def max_over_ranks(x: float, device) -> float:
+    if not dist.is_initialized():
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def make_env(n, rank, device, gates, integrator):
+    cfg = RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=device), stage=1, integrator=integrator,
+                       terrain=TerrainCfg(num_gates=gates), env_id_offset=rank * n, track_seed_offset=rank)
+    env = RacingEnv(cfg)
+    env.reset()
+    g = torch.Generator(device="cpu").manual_seed(1234 + rank)
+    env.episode_length_buf = torch.randint(0, env.max_episode_length, (n,), generator=g, dtype=torch.int32).to(device)
+    return env
+
+
+def time_env_steps(env, actions, steps, use_graph):
+    """Returns (seconds for exactly `steps` env steps, launch mode)."""
+    mode = "eager"
+    graph = None
+    if use_graph and steps >= ACTION_RING:
+        try:
+            # capture ACTION_RING consecutive steps (buffer bindings and action pointers baked in)
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for k in range(2):  # stream warm-up outside capture
+                    env.step(actions[k % ACTION_RING])
+            torch.cuda.current_stream().wait_stream(s)
+            # realign the host-side call counter to a multiple of the ring
+            while env._calls % ACTION_RING != 0:
+                env.step(actions[env._calls % ACTION_RING])
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                for k in range(ACTION_RING):
+                    env.step(actions[k])
+            torch.cuda.synchronize()
+            graph.replay()
+            torch.cuda.synchronize()
+            mode = "hipgraph"
+        except Exception as e:  # graph capture unavailable: fall back to eager launches
+            print(f"[bench] hipGraph capture failed ({e}); timing eager launches", file=sys.stderr)
+            graph = None
+    reps, rem = (steps // ACTION_RING, steps % ACTION_RING) if graph is not None else (0, steps)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        graph.replay()
+    for k in range(rem):
+        env.step(actions[k % ACTION_RING])
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    return t1 - t0, mode
+
+
+def kernel_timing(env, actions, steps):
+    """HIP events around every fused-kernel launch (eager pass), on the launch stream."""
+    import ctypes as C
+
+    lib, ctx = env._lib, env._ctx
+    n = min(steps, 4096)
+    assert lib.gr_set_timing(ctx, 1) == 0
+    for k in range(n):
+        env.step(actions[k % ACTION_RING])
+    tot, cnt = C.c_double(), C.c_int64()
+    assert lib.gr_read_timing(ctx, C.byref(tot), C.byref(cnt)) == 0
+    lib.gr_set_timing(ctx, 0)
+    return tot.value / cnt.value  # ms per launch
+
+
+def policy_in_loop(env, steps, device):
+    """env step + actor MLP(16->256->256->4) inference per step (rollout without learning)."""
+    from generalizableracing_amd.rsl_rl import ActorCritic
+
+    pol = ActorCritic(16, 16, 4, [256, 256], [256, 256], "lrelu").to(device).eval()
+    obs = env.observe()["policy"]
+    with torch.inference_mode():
+        for _ in range(8):
+            obs = env.step(pol.act_inference(obs))[0]["policy"]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            obs = env.step(pol.act_inference(obs))[0]["policy"]
+        torch.cuda.synchronize()
+    return env.num_envs * steps / (time.perf_counter() - t0)
+
+
+def train_fps(device, n=4096, iters=3):
+    """Config C2: 4 096 envs, rsl_rl PPO MLP(256,256) fp32, the reference's Perf/total_fps."""
+    from generalizableracing_amd.envs.racing_env import RslRlVecEnvWrapper
+    from generalizableracing_amd.rsl_rl import OnPolicyRunner, QuadcopterPPORunnerCfg
+
+    venv = RslRlVecEnvWrapper(RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=device))))
+    runner = OnPolicyRunner(venv, QuadcopterPPORunnerCfg(device=device).to_dict(), log_dir=None, device=device)
+    runner.learn(1, init_at_random_ep_len=True)  # warm-up iteration
+    fps = []
+    for _ in range(iters):
+        runner.learn(1)
+        fps.append(runner.last_log["fps"])
+    venv.close()
+    return float(np.median(fps))
+
+
+def cpu_baseline(seconds: float):
+    """The CPU oracle (C restatement of the reference step, 1 thread) on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    from generalizableracing_amd.envs.tracks import build_track_table
+
+    n = 4096
+    cfg = RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device="cpu"), stage=1).to_gr_config()
+    gates, recs = build_track_table()
+    orc = oracle.Oracle(cfg, gates, recs)
+    orc.init()
+    orc.reset(None)
+    rng = np.random.default_rng(0)
+    acts = rng.standard_normal((16, n, 4)).astype(np.float32)
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        orc.step(acts[steps % 16])
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n} envs x {steps} steps of the C oracle (oracle/gr_oracle.c), single thread, "
+                      f"{dt:.1f} s; the Isaac-Lab/PhysX reference cannot run here (SURVEY §8d)"}
+
+
+def load_traffic(n, gates):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        if d.get("num_envs") == n and d.get("gates", 8) == gates:
+            return d.get("bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+def main():
+    a = parse()
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=ws)
+    device = f"cuda:{local}"
+    n = a.num_envs
+    env = make_env(n, rank, device, a.gates, a.integrator)
+    g = torch.Generator(device=device).manual_seed(1234 + rank)
+    actions = torch.randn(ACTION_RING, n, 4, device=device, generator=g)
+    for k in range(a.warmup):
+        env.step(actions[k % ACTION_RING])
+    torch.cuda.synchronize()
+    secs, mode = time_env_steps(env, actions, a.steps, not a.no_graph)
+    secs = max_over_ranks(secs, device)
+    value = n * ws * a.steps / secs
+    ms_kernel = kernel_timing(env, actions, a.steps)
+    rd, wr = env.bytes_per_env_step()
+    achieved = (rd + wr) * n / (ms_kernel * 1e-3) / 1e9
+    extra = {}
+    if not a.no_extras:
+        extra["policy_in_loop_env_steps_per_s"] = policy_in_loop(env, 256, device)
+    env.close()
+    if not a.no_extras:
+        extra["train_total_fps_4096_envs"] = train_fps(device)
+    cpu = None
+    if rank == 0 and ws == 1 and not a.no_extras:
+        cpu = cpu_baseline(a.cpu_seconds)
+    traffic = load_traffic(n, a.gates)
+    if rank == 0:
+        line = {
+            "metric": "env-steps/sec whole-node @65536 envs/GPU; 1/2/4/8-GPU scaling",
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": ws,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": secs * 1e3 / a.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: procedural zigzag/circular/ellipse tracks (20 types x 10 levels), "
+                    "N(0,1) pre-tanh actions resident in HBM",
+            "config": {"workload": f"racing env step, {n} envs/GPU, TRAINING_STAGE=1, {a.gates}-gate tracks, "
+                                   f"{a.integrator} integrator (BASELINE config C3/C4)",
+                       "num_envs_per_gpu": n, "launch": mode, "parallelism": f"env-shard x{ws}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "gr::env_kernel<0,true> (fused step)", "kernel_us": ms_kernel * 1e3,
+                         "bytes_per_env_step": {"read": rd, "written": wr},
+                         "read_frac": rd * n / (ms_kernel * 1e-3) / 1e9 / HBM_PEAK_GBS},
+            "cpu_baseline": cpu,
+            **extra,
+        }
+        print(json.dumps(line))
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,247 @@
+"""ctypes mirror of include/gr.h and the loader for libgr.so.
+
+The product path talks to the HIP step only through this C ABI (plain
+pointers, sizes and a hipStream_t; no torch types cross it).  `load()` fails
+loudly when the in-tree libgr.so is missing — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must be imported first: libgr.so binds to torch's libamdhip64)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgr.so")
+
+# ---- constants (include/gr.h) ----
+GR_ABI_VERSION = 1
+GR_INTEGRATOR_DD_EXPLICIT = 0
+GR_INTEGRATOR_SEMI_IMPLICIT = 1
+
+P_POSQ, P_QV, P_VW, P_WA, P_CTRL, P_LAG, P_RST0, P_RST1, P_EP0, P_EP1, P_PAR0, P_PAR1, P_PAR2, P_PAR3, P_MOTOR = range(15)
+NUM_PLANES = 15
+I_EPLEN, I_ACC, I_EPOCH, I_PACKED = range(4)
+OBS_DIM = 16
+GATE_FLOATS = 20
+TRACK_FLOATS = 4
+
+LOG_NRESET = 0
+LOG_EPSUM0 = 1
+LOG_ACC = 8
+LOG_M_ACTRATE = 9
+LOG_M_LINSPD = 10
+LOG_M_ANGSPD = 11
+LOG_T_TIMEOUT = 12
+LOG_T_CONTACT = 13
+LOG_T_BADPOSE = 14
+LOG_LEVEL = 15
+LOG_NOISE = 16
+LOG_SLOTS = 20
+
+# named fields of the float planes: name -> (plane, first component, count)
+STATE_FIELDS = {
+    "pos": [(P_POSQ, 0, 3)],
+    "quat": [(P_POSQ, 3, 1), (P_QV, 0, 3)],
+    "lin_vel_w": [(P_QV, 3, 1), (P_VW, 0, 2)],
+    "ang_vel_b": [(P_VW, 2, 2), (P_WA, 0, 1)],
+    "ang_acc_b": [(P_WA, 1, 3)],
+    "ctrl": [(P_CTRL, 0, 4)],
+    "lag": [(P_LAG, 0, 4)],
+    "thr_est_error": [(P_RST0, 0, 1)],
+    "noise_level": [(P_RST0, 1, 1)],
+    "drag2": [(P_RST0, 2, 2), (P_RST1, 0, 1)],
+    "drag1": [(P_RST1, 1, 3)],
+    "episode_sums": [(P_EP0, 0, 4), (P_EP1, 0, 3)],
+    "metric_action_rate": [(P_EP1, 3, 1)],
+    "rate_gain_p": [(P_PAR0, 0, 3)],
+    "thrust_filter": [(P_PAR0, 3, 1)],
+    "rate_gain_d": [(P_PAR1, 0, 3)],
+    "mass_plant": [(P_PAR1, 3, 1)],
+    "torque_filter": [(P_PAR2, 0, 3)],
+    "mass_ctrl": [(P_PAR2, 3, 1)],
+    "inertia_plant": [(P_PAR3, 0, 3)],
+    "motor_omega": [(P_MOTOR, 0, 4)],
+}
+
+
+class GrConfig(C.Structure):
+    _fields_ = [
+        ("num_envs", C.c_int32),
+        ("env_id_offset", C.c_int32),
+        ("seed_lo", C.c_uint32),
+        ("seed_hi", C.c_uint32),
+        ("num_types", C.c_int32),
+        ("num_levels", C.c_int32),
+        ("max_gates", C.c_int32),
+        ("max_init_level", C.c_int32),
+        ("stage", C.c_int32),
+        ("integrator", C.c_int32),
+        ("decimation", C.c_int32),
+        ("max_episode_length", C.c_int32),
+        ("sim_dt", C.c_float),
+        ("step_dt", C.c_float),
+        ("episode_length_s", C.c_float),
+        ("gravity", C.c_float),
+        ("mass", C.c_float),
+        ("inertia", C.c_float * 3),
+        ("arm_length", C.c_float),
+        ("kappa", C.c_float),
+        ("motor_tau", C.c_float),
+        ("motor_omega", C.c_float * 2),
+        ("thrustmap", C.c_float * 3),
+        ("max_thrust_weight_ratio", C.c_float),
+        ("body_rate_bound", C.c_float),
+        ("rate_gain_p", C.c_float * 3),
+        ("rate_gain_d", C.c_float * 3),
+        ("thrust_ctrl_delay", C.c_float),
+        ("torque_ctrl_delay", C.c_float * 3),
+        ("use_motor_model", C.c_int32),
+        ("action_lag", C.c_int32),
+        ("drag1", C.c_float * 3),
+        ("drag1_rand", C.c_float),
+        ("drag2", C.c_float * 3),
+        ("drag2_rand", C.c_float),
+        ("z_drag", C.c_float),
+        ("z_drag_rand", C.c_float),
+        ("random_drag", C.c_int32),
+        ("mass_add_range", C.c_float * 2),
+        ("inertia_scale_range", C.c_float * 2),
+        ("pid_scale_range", C.c_float * 2),
+        ("delay_scale_range", C.c_float * 2),
+        ("dr_startup", C.c_int32),
+        ("dr_plant", C.c_int32),
+        ("spawn_pos", C.c_float * 3),
+        ("reset_pos_half", C.c_float * 3),
+        ("reset_att_half", C.c_float * 3),
+        ("reset_vel_half", C.c_float * 6),
+        ("gate_threshold", C.c_float),
+        ("gate_noise_pos", C.c_float * 3),
+        ("add_gate_noise", C.c_int32),
+        ("level_up_threshold", C.c_int32),
+        ("level_down_threshold", C.c_int32),
+        ("noise_curriculum", C.c_int32),
+        ("noise_enhance_threshold", C.c_int32),
+        ("noise_decay_threshold", C.c_int32),
+        ("noise_enhance", C.c_float),
+        ("noise_decay", C.c_float),
+        ("obs_noise", C.c_int32),
+        ("obs_lin_vel_noise", C.c_float),
+        ("obs_att_noise", C.c_float),
+        ("w_progress", C.c_float),
+        ("w_body_rate", C.c_float),
+        ("w_action_rate", C.c_float),
+        ("w_collision", C.c_float),
+        ("w_perception", C.c_float),
+        ("w_success", C.c_float),
+        ("w_bad_pose", C.c_float),
+        ("collider_half", C.c_float * 3),
+        ("collision_count_threshold", C.c_int32),
+        ("out_of_bound", C.c_float * 2),
+        ("term_contact", C.c_int32),
+        ("term_bad_pose", C.c_int32),
+        ("reserved", C.c_int32 * 8),
+    ]
+
+    def to_dict(self) -> dict:
+        out = {}
+        for name, _ in self._fields_:
+            v = getattr(self, name)
+            out[name] = list(v) if hasattr(v, "__len__") else v
+        return out
+
+
+class GrBuffers(C.Structure):
+    _fields_ = [
+        ("state", C.c_void_p),
+        ("istate", C.c_void_p),
+        ("obs_policy", C.c_void_p),
+        ("obs_critic", C.c_void_p),
+        ("obs_aux", C.c_void_p),
+        ("reward", C.c_void_p),
+        ("terminated", C.c_void_p),
+        ("time_out", C.c_void_p),
+        ("dones", C.c_void_p),
+        ("prev_obs_critic", C.c_void_p),
+        ("prev_obs_aux", C.c_void_p),
+        ("prev_time_out", C.c_void_p),
+        ("log_partial", C.c_void_p),
+        ("log_out", C.c_void_p),
+        ("log_prev", C.c_void_p),
+        ("counters", C.c_void_p),
+    ]
+
+
+EXPORTS = [
+    "gr_abi_version", "gr_config_default", "gr_config_size", "gr_create", "gr_destroy", "gr_last_error",
+    "gr_num_blocks", "gr_bytes_per_env_step", "gr_bind_tracks", "gr_bind_buffers", "gr_init", "gr_reset",
+    "gr_step", "gr_observe", "gr_set_timing", "gr_read_timing", "gr_test_dynamics", "gr_test_math",
+    "gr_test_philox",
+]
+
+_lib = None
+
+
+def _declare(lib):
+    vp = C.c_void_p
+    sig = {
+        "gr_abi_version": (C.c_int, []),
+        "gr_config_default": (C.c_int, [C.POINTER(GrConfig)]),
+        "gr_config_size": (C.c_size_t, []),
+        "gr_create": (C.c_int, [C.POINTER(GrConfig), C.POINTER(vp)]),
+        "gr_destroy": (C.c_int, [vp]),
+        "gr_last_error": (C.c_char_p, [vp]),
+        "gr_num_blocks": (C.c_int, [vp]),
+        "gr_bytes_per_env_step": (C.c_int, [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+        "gr_bind_tracks": (C.c_int, [vp, vp, vp]),
+        "gr_bind_buffers": (C.c_int, [vp, C.POINTER(GrBuffers)]),
+        "gr_init": (C.c_int, [vp, vp]),
+        "gr_reset": (C.c_int, [vp, vp, vp]),
+        "gr_step": (C.c_int, [vp, vp, vp]),
+        "gr_observe": (C.c_int, [vp, vp]),
+        "gr_set_timing": (C.c_int, [vp, C.c_int]),
+        "gr_read_timing": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
+        "gr_test_dynamics": (C.c_int, [vp, C.c_int, C.c_int] + [vp] * 9 + [vp]),
+        "gr_test_math": (C.c_int, [vp, C.c_int, C.c_int, vp, vp, vp, vp]),
+        "gr_test_philox": (C.c_int, [vp, C.c_int] + [C.c_uint32] * 4 + [vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+
+
+def load(path: str | None = None):
+    """Load libgr.so (the HIP step).  Raises if it is missing: no fallback."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(
+            f"libgr.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `make -C generalizableracing_amd/csrc`.  The racing env has no CPU fallback."
+        )
+    lib = C.CDLL(p, mode=C.RTLD_GLOBAL)
+    _declare(lib)
+    if lib.gr_abi_version() != GR_ABI_VERSION:
+        raise RuntimeError(f"libgr.so ABI {lib.gr_abi_version()} != expected {GR_ABI_VERSION}")
+    if lib.gr_config_size() != C.sizeof(GrConfig):
+        raise RuntimeError(f"gr_config size mismatch: C {lib.gr_config_size()} vs ctypes {C.sizeof(GrConfig)}")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def default_config() -> GrConfig:
+    cfg = GrConfig()
+    rc = load().gr_config_default(C.byref(cfg))
+    if rc != 0:
+        raise RuntimeError("gr_config_default failed")
+    return cfg
+
+
+def check(lib, ctx, rc: int, what: str):
+    if rc != 0:
+        msg = lib.gr_last_error(ctx) if ctx else b""
+        raise RuntimeError(f"{what} failed (status {rc}): {msg.decode() if msg else ''}")

@@ -1,0 +1,369 @@
+// gr_capi.cpp — C ABI of libgr.so (declared in include/gr.h).
+//
+// Host side only: validates arguments, derives per-config constants once,
+// owns the packed copy of the track table, and launches the kernels of
+// gr_kernels.hip on the caller's stream.  No allocation, host sync or
+// exception crosses gr_step / gr_reset / gr_observe.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/gr.h"
+#include "gr_kernels.h"
+#include "gr_math.h"
+
+struct gr_ctx {
+  gr_config cfg;
+  gr_buffers buf;
+  bool have_buf = false;
+  float* table = nullptr;  // packed [T*L][stride]
+  bool have_tracks = false;
+  gr::KArgs args;
+  std::string err;
+  // optional kernel timing (gr_set_timing)
+  std::vector<hipEvent_t> ev;  // [2 * GR_TIMING_RING]
+  int ev_next = 0;
+  bool timing = false;
+};
+
+#define GR_TIMING_RING 4096
+
+namespace {
+
+int fail(gr_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+int hip_fail(gr_ctx* c, hipError_t e, const char* what) {
+  return fail(c, GR_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+void derive(gr_ctx* c) {
+  const gr_config& g = c->cfg;
+  gr::KArgs& a = c->args;
+  std::memset(&a, 0, sizeof(a));
+  a.cfg = g;
+  a.track_stride = g.max_gates * GR_GATE_FLOATS + GR_TRACK_FLOATS;
+  // env -> terrain type: IL floor(arange(N) / (N / num_cols)) with an fp32 divisor
+  const float s = (float)((double)g.num_envs / (double)g.num_types);
+  for (int t = 0; t <= g.num_types; ++t) {
+    double lim = (double)t * (double)s;
+    int i = (int)std::ceil(lim);
+    a.type_start[t] = i > g.num_envs ? g.num_envs : i;
+  }
+  // gross thrust bounds, controller_diff.py:96-99 (python double, cast at clamp)
+  const double k2 = g.thrustmap[0], k1 = g.thrustmap[1], k0 = g.thrustmap[2];
+  const double w0 = g.motor_omega[0], w1 = g.motor_omega[1];
+  const double tmin = k2 * w0 * w0 + k1 * w0 + k0, tmax = k2 * w1 * w1 + k1 * w1 + k0;
+  a.thrust_lo = (float)(tmin * 4.0);
+  a.thrust_hi = (float)(tmax * 4.0);
+  const double reach = std::sqrt((double)g.collider_half[0] * g.collider_half[0] +
+                                 (double)g.collider_half[1] * g.collider_half[1] +
+                                 (double)g.collider_half[2] * g.collider_half[2]);
+  a.lat_reach = (float)(reach * 1.001 + 1e-5);
+  const float w[7] = {g.w_progress, g.w_body_rate, g.w_action_rate, g.w_collision,
+                      g.w_perception, g.w_success, g.w_bad_pose};
+  for (int k = 0; k < 7; ++k) a.w[k] = w[k];
+  // motor model constants (same expressions as the oracle)
+  const float l = g.arm_length * 0.707106769f, kap = g.kappa;
+  const float sx[4] = {1, -1, -1, 1}, sy[4] = {-1, -1, 1, 1}, sz[4] = {1, -1, 1, -1};
+  for (int j = 0; j < 4; ++j) {
+    a.B[0][j] = 1.0f; a.B[1][j] = l * sx[j]; a.B[2][j] = l * sy[j]; a.B[3][j] = kap * sz[j];
+    a.Bi[j][0] = 0.25f; a.Bi[j][1] = sx[j] / (4.0f * l); a.Bi[j][2] = sy[j] / (4.0f * l);
+    a.Bi[j][3] = sz[j] / (4.0f * kap);
+  }
+  a.motor_fmax = (float)tmax;
+  a.motor_c = gr_expf(-(float)(1.0 / (double)g.motor_tau) * g.step_dt);
+  a.tm_k2 = (float)k2; a.tm_k1 = (float)k1; a.tm_k0 = (float)k0;
+  a.tm_k1sq = (float)(k1 * k1); a.tm_4k2 = (float)(4.0 * k2);
+  a.tm_inv2k2 = (float)(1.0 / (2.0 * k2)); a.tm_negk1 = (float)(-k1);
+  // LDS: the widest terrain-type span of any workgroup, all levels
+  int span = 1;
+  const int nb = (g.num_envs + GR_BLOCK - 1) / GR_BLOCK;
+  for (int b = 0; b < nb; ++b) {
+    int f = b * GR_BLOCK, last = std::min(f + GR_BLOCK, g.num_envs) - 1, t0 = 0, t1 = 0;
+    for (int t = 1; t < g.num_types; ++t) { t0 += f >= a.type_start[t]; t1 += last >= a.type_start[t]; }
+    span = std::max(span, t1 - t0 + 1);
+  }
+  const long bytes = (long)span * g.num_levels * a.track_stride * 4;
+  a.lds_bytes = bytes <= 60 * 1024 ? (int)bytes : 0;  // beyond 60 KiB: read the (L2-resident) table directly
+}
+
+}  // namespace
+
+extern "C" {
+
+int gr_abi_version(void) { return GR_ABI_VERSION; }
+size_t gr_config_size(void) { return sizeof(gr_config); }
+
+int gr_config_default(gr_config* c) {
+  if (!c) return GR_ERR_ARG;
+  std::memset(c, 0, sizeof(*c));
+  c->num_envs = 2048;  // racing_ctbr_env.py:357
+  c->seed_lo = 42;
+  c->num_types = 20;   // RacingComplexTerrainCfg num_cols (racing_terrains.py:137-147)
+  c->num_levels = 10;  // num_rows
+  c->max_gates = 8;
+  c->max_init_level = 5;
+  c->stage = 1;
+  c->integrator = GR_INTEGRATOR_DD_EXPLICIT;
+  c->decimation = 3;
+  c->sim_dt = 0.01f;
+  c->step_dt = (float)(0.01 * 3);
+  c->episode_length_s = 6.0f;
+  c->max_episode_length = (int)std::ceil(6.0 / (0.01 * 3));  // 200 (manager_based_diff_rl_env.py:99-102)
+  c->gravity = 9.81f;
+  c->mass = 0.6f;  // ASSUMPTION: drone_175_v8.usd (defines the mass) is not in the reference
+  c->inertia[0] = 0.0015f; c->inertia[1] = 0.002f; c->inertia[2] = 0.004f;
+  c->arm_length = 0.09f;
+  c->kappa = 0.016f;
+  c->motor_tau = 0.0001f;
+  c->motor_omega[0] = 150.0f; c->motor_omega[1] = 3000.0f;
+  c->thrustmap[0] = 1.3298253500372892e-06f;
+  c->thrustmap[1] = 0.0038360810526746033f;
+  c->thrustmap[2] = -1.7689986848125325f;
+  c->max_thrust_weight_ratio = 3.0f;
+  c->body_rate_bound = 6.0f;
+  for (int k = 0; k < 3; ++k) c->rate_gain_p[k] = 35.0f;
+  c->rate_gain_d[0] = 0.0005f; c->rate_gain_d[1] = 0.0005f; c->rate_gain_d[2] = 0.0003f;
+  c->thrust_ctrl_delay = 0.03f;
+  for (int k = 0; k < 3; ++k) c->torque_ctrl_delay[k] = 0.03f;
+  c->use_motor_model = 0;
+  c->action_lag = 1;
+  for (int k = 0; k < 3; ++k) { c->drag1[k] = 0.18f; c->drag2[k] = 0.01f; }
+  c->drag1_rand = 0.1f;
+  c->drag2_rand = 0.005f;
+  c->z_drag = 4.0f;
+  c->z_drag_rand = 0.4f;
+  c->random_drag = 1;
+  c->mass_add_range[0] = -0.02f; c->mass_add_range[1] = 0.02f;
+  c->inertia_scale_range[0] = 0.9f; c->inertia_scale_range[1] = 1.1f;
+  c->pid_scale_range[0] = 0.9f; c->pid_scale_range[1] = 1.1f;
+  c->delay_scale_range[0] = 0.8f; c->delay_scale_range[1] = 1.3f;
+  c->dr_startup = 1;
+  c->dr_plant = 1;
+  c->spawn_pos[2] = 0.5f;  // DRONE_CFG init_state.pos (quadcopter.py:30-31)
+  for (int k = 0; k < 3; ++k) c->reset_pos_half[k] = 0.5f;
+  c->reset_att_half[0] = 0.2f; c->reset_att_half[1] = 0.2f; c->reset_att_half[2] = 0.7f;
+  for (int k = 0; k < 6; ++k) c->reset_vel_half[k] = 0.1f;
+  c->gate_threshold = 0.35f;
+  for (int k = 0; k < 3; ++k) c->gate_noise_pos[k] = 0.1f;
+  c->add_gate_noise = 1;
+  c->level_up_threshold = 3;
+  c->level_down_threshold = 2;
+  c->noise_curriculum = 1;
+  c->noise_enhance_threshold = 4;
+  c->noise_decay_threshold = 3;
+  c->noise_enhance = 0.02f;
+  c->noise_decay = 0.03f;
+  c->obs_noise = 1;
+  c->obs_lin_vel_noise = 0.03f;
+  c->obs_att_noise = 0.05f;
+  c->w_progress = 1.0f;
+  c->w_body_rate = -0.1f;
+  c->w_action_rate = -0.05f;
+  c->w_collision = -100.0f;
+  c->w_perception = 0.1f;
+  c->w_success = 20.0f;
+  c->w_bad_pose = -30.0f;
+  c->collider_half[0] = 0.707f * 0.09f;
+  c->collider_half[1] = 0.707f * 0.09f;
+  c->collider_half[2] = 0.5f * 0.05f;
+  c->collision_count_threshold = 0;
+  c->out_of_bound[0] = 0.0f; c->out_of_bound[1] = 10.0f;
+  c->term_contact = 1;
+  c->term_bad_pose = 1;
+  return GR_OK;
+}
+
+int gr_create(const gr_config* cfg, gr_ctx** out) {
+  if (!cfg || !out) return GR_ERR_ARG;
+  *out = nullptr;
+  const gr_config& g = *cfg;
+  if (g.num_envs <= 0 || g.num_types <= 0 || g.num_types > GR_MAX_TYPES || g.num_levels <= 0 ||
+      g.num_levels > 255 || g.max_gates <= 0 || g.max_gates > 255 || g.decimation <= 0 ||
+      (g.action_lag != 0 && g.action_lag != 1) || g.max_episode_length <= 0 || !(g.mass > 0.0f) ||
+      (g.integrator != GR_INTEGRATOR_DD_EXPLICIT && g.integrator != GR_INTEGRATOR_SEMI_IMPLICIT) ||
+      g.num_types > g.num_envs || g.max_init_level < 0)
+    return GR_ERR_ARG;
+  gr_ctx* c = new (std::nothrow) gr_ctx();
+  if (!c) return GR_ERR_STATE;
+  c->cfg = g;
+  derive(c);
+  *out = c;
+  return GR_OK;
+}
+
+int gr_destroy(gr_ctx* c) {
+  if (!c) return GR_ERR_ARG;
+  for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+  if (c->table) (void)hipFree(c->table);
+  delete c;
+  return GR_OK;
+}
+
+const char* gr_last_error(const gr_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int gr_num_blocks(const gr_ctx* c) { return c ? (c->cfg.num_envs + GR_BLOCK - 1) / GR_BLOCK : GR_ERR_ARG; }
+
+int gr_bytes_per_env_step(const gr_ctx* c, int64_t* rd, int64_t* wr) {
+  if (!c || !rd || !wr) return GR_ERR_ARG;
+  const int motor = c->cfg.use_motor_model ? 1 : 0;
+  // read: planes POSQ..PAR3 (14 x 16 B) [+ MOTOR], int plane 16 B, action 16 B
+  *rd = (14 + motor) * 16 + 16 + 16;
+  // written: POSQ..LAG, EP0, EP1 (8 x 16 B) [+ MOTOR], int plane, obs policy+critic (2 x 64 B),
+  // aux 4, reward 4, terminated 1, time_out 1, dones 8.  RST0/RST1 (only on reset) not counted.
+  *wr = (8 + motor) * 16 + 16 + 128 + 4 + 4 + 1 + 1 + 8;
+  return GR_OK;
+}
+
+int gr_bind_tracks(gr_ctx* c, const float* gates, const float* tracks) {
+  if (!c || !gates || !tracks) return fail(c, GR_ERR_ARG, "gr_bind_tracks: null pointer");
+  const gr_config& g = c->cfg;
+  const int ntr = g.num_types * g.num_levels;
+  std::vector<float> h((size_t)ntr * GR_TRACK_FLOATS);
+  hipError_t e = hipMemcpy(h.data(), tracks, h.size() * sizeof(float), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(c, e, "gr_bind_tracks: copy track records");
+  for (int t = 0; t < ntr; ++t) {
+    const float* r = &h[(size_t)t * GR_TRACK_FLOATS];
+    const int start = (int)r[2], ng = (int)r[3];
+    if (!(std::isfinite(r[0]) && std::isfinite(r[1])) || ng < 2 || ng > g.max_gates || start < 0 || start >= ng ||
+        (float)start != r[2] || (float)ng != r[3])
+      return fail(c, GR_ERR_ARG, "gr_bind_tracks: invalid track record " + std::to_string(t));
+  }
+  const size_t stride = (size_t)c->args.track_stride;
+  if (!c->table) {
+    e = hipMalloc(&c->table, (size_t)ntr * stride * sizeof(float));
+    if (e != hipSuccess) return hip_fail(c, e, "gr_bind_tracks: hipMalloc");
+  }
+  const size_t gb = (size_t)g.max_gates * GR_GATE_FLOATS * sizeof(float);
+  e = hipMemcpy2D(c->table, stride * sizeof(float), gates, gb, gb, ntr, hipMemcpyDeviceToDevice);
+  if (e != hipSuccess) return hip_fail(c, e, "gr_bind_tracks: pack gates");
+  e = hipMemcpy2D(c->table + (size_t)g.max_gates * GR_GATE_FLOATS, stride * sizeof(float), tracks,
+                  GR_TRACK_FLOATS * sizeof(float), GR_TRACK_FLOATS * sizeof(float), ntr, hipMemcpyDeviceToDevice);
+  if (e != hipSuccess) return hip_fail(c, e, "gr_bind_tracks: pack track records");
+  e = hipDeviceSynchronize();
+  if (e != hipSuccess) return hip_fail(c, e, "gr_bind_tracks: sync");
+  c->args.table = c->table;
+  c->have_tracks = true;
+  return GR_OK;
+}
+
+int gr_bind_buffers(gr_ctx* c, const gr_buffers* b) {
+  if (!c || !b) return fail(c, GR_ERR_ARG, "gr_bind_buffers: null pointer");
+  const void* ptrs[] = {b->state,      b->istate,          b->obs_policy,   b->obs_critic,    b->obs_aux,
+                        b->reward,     b->terminated,      b->time_out,     b->dones,         b->prev_obs_critic,
+                        b->prev_obs_aux, b->prev_time_out, b->log_partial,  b->log_out,       b->counters};
+  for (const void* p : ptrs)
+    if (!p) return fail(c, GR_ERR_ARG, "gr_bind_buffers: null buffer");
+  if (!aligned16(b->state) || !aligned16(b->istate) || !aligned16(b->obs_policy) || !aligned16(b->obs_critic) ||
+      !aligned16(b->prev_obs_critic))
+    return fail(c, GR_ERR_ARG, "gr_bind_buffers: state/obs buffers must be 16-byte aligned");
+  c->buf = *b;
+  c->args.buf = *b;
+  c->have_buf = true;
+  return GR_OK;
+}
+
+static int ready(gr_ctx* c, const char* what) {
+  if (!c) return GR_ERR_ARG;
+  if (!c->have_buf || !c->have_tracks)
+    return fail(c, GR_ERR_STATE, std::string(what) + ": buffers and tracks must be bound first");
+  return GR_OK;
+}
+
+int gr_init(gr_ctx* c, void* stream) {
+  int r = ready(c, "gr_init");
+  if (r) return r;
+  hipError_t e = gr::launch_init(c->args, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(c, e, "gr_init");
+  e = hipMemsetAsync(c->buf.counters, 0, 4 * sizeof(uint32_t), (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(c, e, "gr_init: counters");
+  return GR_OK;
+}
+
+int gr_reset(gr_ctx* c, const uint8_t* mask, void* stream) {
+  int r = ready(c, "gr_reset");
+  if (r) return r;
+  hipError_t e = gr::launch_env(gr::KMODE_RESET, c->args, nullptr, mask, (hipStream_t)stream, nullptr, nullptr);
+  return e == hipSuccess ? GR_OK : hip_fail(c, e, "gr_reset");
+}
+
+int gr_step(gr_ctx* c, const float* actions, void* stream) {
+  int r = ready(c, "gr_step");
+  if (r) return r;
+  if (!actions || !aligned16(actions)) return fail(c, GR_ERR_ARG, "gr_step: actions must be a 16-byte aligned [N][4] fp32 buffer");
+  hipEvent_t t0 = nullptr, t1 = nullptr;
+  if (c->timing && c->ev_next < GR_TIMING_RING) {
+    t0 = c->ev[2 * c->ev_next];
+    t1 = c->ev[2 * c->ev_next + 1];
+    c->ev_next++;
+  }
+  hipError_t e = gr::launch_env(gr::KMODE_STEP, c->args, actions, nullptr, (hipStream_t)stream, t0, t1);
+  return e == hipSuccess ? GR_OK : hip_fail(c, e, "gr_step");
+}
+
+int gr_set_timing(gr_ctx* c, int enable) {
+  if (!c) return GR_ERR_ARG;
+  if (enable && c->ev.empty()) {
+    c->ev.resize(2 * GR_TIMING_RING, nullptr);
+    for (auto& e : c->ev) {
+      hipError_t r = hipEventCreate(&e);
+      if (r != hipSuccess) return hip_fail(c, r, "gr_set_timing: hipEventCreate");
+    }
+  }
+  c->timing = enable != 0;
+  c->ev_next = 0;
+  return GR_OK;
+}
+
+int gr_read_timing(gr_ctx* c, double* total_ms, int64_t* launches) {
+  if (!c || !total_ms || !launches) return GR_ERR_ARG;
+  double tot = 0.0;
+  for (int i = 0; i < c->ev_next; ++i) {
+    hipError_t r = hipEventSynchronize(c->ev[2 * i + 1]);
+    if (r != hipSuccess) return hip_fail(c, r, "gr_read_timing: sync");
+    float ms = 0.0f;
+    r = hipEventElapsedTime(&ms, c->ev[2 * i], c->ev[2 * i + 1]);
+    if (r != hipSuccess) return hip_fail(c, r, "gr_read_timing: elapsed");
+    tot += ms;
+  }
+  *total_ms = tot;
+  *launches = c->ev_next;
+  c->ev_next = 0;
+  return GR_OK;
+}
+
+int gr_observe(gr_ctx* c, void* stream) {
+  int r = ready(c, "gr_observe");
+  if (r) return r;
+  hipError_t e = gr::launch_env(gr::KMODE_OBSERVE, c->args, nullptr, nullptr, (hipStream_t)stream, nullptr, nullptr);
+  return e == hipSuccess ? GR_OK : hip_fail(c, e, "gr_observe");
+}
+
+int gr_test_dynamics(gr_ctx* c, int n, int mode, const float* si, const float* ab, const float* cmd, const float* ci,
+                     const float* par, const float* drag, float* so, float* co, float* xo, void* stream) {
+  if (!c || n <= 0 || !si || !ab || !cmd || !ci || !par || !drag || !so || !co || !xo) return GR_ERR_ARG;
+  hipError_t e = gr::launch_test_dynamics(c->args, n, mode, si, ab, cmd, ci, par, drag, so, co, xo, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : hip_fail(c, e, "gr_test_dynamics");
+}
+
+int gr_test_math(gr_ctx* c, int fn, int n, const float* x, const float* y, float* out, void* stream) {
+  if (!c || n <= 0 || !x || !y || !out) return GR_ERR_ARG;
+  hipError_t e = gr::launch_test_math(fn, n, x, y, out, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : hip_fail(c, e, "gr_test_math");
+}
+
+int gr_test_philox(gr_ctx* c, int n, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t* out4, void* stream) {
+  if (!c || n <= 0 || !out4) return GR_ERR_ARG;
+  hipError_t e = gr::launch_test_philox(n, c0, c1, c2, c3, c->cfg.seed_lo, c->cfg.seed_hi, out4, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : hip_fail(c, e, "gr_test_philox");
+}
+
+}  // extern "C"

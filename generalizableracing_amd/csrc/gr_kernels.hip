@@ -1,0 +1,862 @@
+// gr_kernels.hip — fused racing-env step for MI355X (gfx950, CDNA4).
+//
+// One lane per env, 256-lane workgroups (4 wave64).  Env state is
+// struct-of-float4-planes in HBM (GR_P_* in include/gr.h): every field group
+// is one coalesced 16-B-per-lane load / store (1 KiB per wave instruction).
+// The gate geometry of the tracks a workgroup's envs can reference (its
+// terrain-type range x all levels) is staged into LDS once per launch.
+//
+// Kernel == the reference step (manager_based_diff_rl_env.py:160-267) in the
+// reference's op order, bit-identical to oracle/gr_oracle.c (built with
+// -ffp-contract=off and the shared gr_math.h / gr_rng.h).  Reset is mask-based
+// and in-lane: no host synchronisation, hipGraph-capturable.
+#include <hip/hip_runtime.h>
+
+#include "../../include/gr.h"
+#include "gr_kernels.h"
+#include "gr_math.h"
+#include "gr_rng.h"
+
+namespace gr {
+
+#define DEV __device__ __forceinline__
+
+// ------------------------------------------------------------- IL math
+// Isaac Lab omni.isaac.lab.utils.math restated (see oracle/gr_oracle.c).
+DEV void quat_rotate(const float q[4], const float v[3], float o[3]) {
+  float s = 2.0f * (q[0] * q[0]) - 1.0f;
+  float cx = q[2] * v[2] - q[3] * v[1];
+  float cy = q[3] * v[0] - q[1] * v[2];
+  float cz = q[1] * v[1] - q[2] * v[0];
+  float d = (q[1] * v[0] + q[2] * v[1]) + q[3] * v[2];
+  o[0] = (v[0] * s + (cx * q[0]) * 2.0f) + (q[1] * d) * 2.0f;
+  o[1] = (v[1] * s + (cy * q[0]) * 2.0f) + (q[2] * d) * 2.0f;
+  o[2] = (v[2] * s + (cz * q[0]) * 2.0f) + (q[3] * d) * 2.0f;
+}
+DEV void quat_rotate_inverse(const float q[4], const float v[3], float o[3]) {
+  float s = 2.0f * (q[0] * q[0]) - 1.0f;
+  float cx = q[2] * v[2] - q[3] * v[1];
+  float cy = q[3] * v[0] - q[1] * v[2];
+  float cz = q[1] * v[1] - q[2] * v[0];
+  float d = (q[1] * v[0] + q[2] * v[1]) + q[3] * v[2];
+  o[0] = (v[0] * s - (cx * q[0]) * 2.0f) + (q[1] * d) * 2.0f;
+  o[1] = (v[1] * s - (cy * q[0]) * 2.0f) + (q[2] * d) * 2.0f;
+  o[2] = (v[2] * s - (cz * q[0]) * 2.0f) + (q[3] * d) * 2.0f;
+}
+DEV void quat_mul(const float a[4], const float b[4], float o[4]) {
+  float ww = (a[3] + a[1]) * (b[1] + b[2]);
+  float yy = (a[0] - a[2]) * (b[0] + b[3]);
+  float zz = (a[0] + a[2]) * (b[0] - b[3]);
+  float xx = (ww + yy) + zz;
+  float qq = 0.5f * (xx + (a[3] - a[1]) * (b[1] - b[2]));
+  o[0] = (qq - ww) + (a[3] - a[2]) * (b[2] - b[3]);
+  o[1] = (qq - xx) + (a[1] + a[0]) * (b[1] + b[0]);
+  o[2] = (qq - yy) + (a[0] - a[1]) * (b[2] + b[3]);
+  o[3] = (qq - zz) + (a[3] + a[2]) * (b[0] - b[1]);
+}
+DEV void quat_from_euler_xyz(float roll, float pitch, float yaw, float o[4]) {
+  float sy, cy, sr, cr, sp, cp;
+  gr_sincosf(yaw * 0.5f, &sy, &cy);
+  gr_sincosf(roll * 0.5f, &sr, &cr);
+  gr_sincosf(pitch * 0.5f, &sp, &cp);
+  o[0] = (cy * cr) * cp + (sy * sr) * sp;
+  o[1] = (cy * sr) * cp - (sy * cr) * sp;
+  o[2] = (cy * cr) * sp + (sy * sr) * cp;
+  o[3] = (sy * cr) * cp - (cy * sr) * sp;
+}
+DEV void matrix_row2(const float q[4], float o[3]) {
+  float two_s = 2.0f / (((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3]);
+  o[0] = two_s * (q[1] * q[3] - q[2] * q[0]);
+  o[1] = two_s * (q[2] * q[3] + q[1] * q[0]);
+  o[2] = 1.0f - two_s * (q[1] * q[1] + q[2] * q[2]);
+}
+DEV void cross3(const float a[3], const float b[3], float o[3]) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+DEV float norm3(const float a[3]) { return gr_sqrtf((a[0] * a[0] + a[1] * a[1]) + a[2] * a[2]); }
+DEV float cosine_similarity(const float a[3], const float b[3]) {
+  float na = gr_maxf(norm3(a), 1e-8f), nb = gr_maxf(norm3(b), 1e-8f);
+  return ((a[0] / na) * (b[0] / nb) + (a[1] / na) * (b[1] / nb)) + (a[2] / na) * (b[2] / nb);
+}
+
+// ------------------------------------------------------------- env registers
+struct Env {
+  float p[3], q[4], v[3], w[3], al[3], T, tau[3], lag[4];
+  float thr, nl, k2[3], k1[3], es[7], mar;
+  float Kp[3], cT, Kd[3], mp, ct[3], mc, J[3], mw[4];
+  int ep, acc, epoch, gate, lvl, type, azero;
+};
+
+DEV void load_env(const KArgs& a, int i, Env& e) {
+  const float4* S = reinterpret_cast<const float4*>(a.buf.state);
+  const size_t n = (size_t)a.cfg.num_envs;
+  float4 s0 = S[GR_P_POSQ * n + i], s1 = S[GR_P_QV * n + i], s2 = S[GR_P_VW * n + i], s3 = S[GR_P_WA * n + i];
+  float4 s4 = S[GR_P_CTRL * n + i], s5 = S[GR_P_LAG * n + i], s6 = S[GR_P_RST0 * n + i], s7 = S[GR_P_RST1 * n + i];
+  float4 s8 = S[GR_P_EP0 * n + i], s9 = S[GR_P_EP1 * n + i];
+  float4 p0 = S[GR_P_PAR0 * n + i], p1 = S[GR_P_PAR1 * n + i], p2 = S[GR_P_PAR2 * n + i], p3 = S[GR_P_PAR3 * n + i];
+  int4 ii = reinterpret_cast<const int4*>(a.buf.istate)[i];
+  e.p[0] = s0.x; e.p[1] = s0.y; e.p[2] = s0.z; e.q[0] = s0.w;
+  e.q[1] = s1.x; e.q[2] = s1.y; e.q[3] = s1.z; e.v[0] = s1.w;
+  e.v[1] = s2.x; e.v[2] = s2.y; e.w[0] = s2.z; e.w[1] = s2.w;
+  e.w[2] = s3.x; e.al[0] = s3.y; e.al[1] = s3.z; e.al[2] = s3.w;
+  e.T = s4.x; e.tau[0] = s4.y; e.tau[1] = s4.z; e.tau[2] = s4.w;
+  e.lag[0] = s5.x; e.lag[1] = s5.y; e.lag[2] = s5.z; e.lag[3] = s5.w;
+  e.thr = s6.x; e.nl = s6.y; e.k2[0] = s6.z; e.k2[1] = s6.w;
+  e.k2[2] = s7.x; e.k1[0] = s7.y; e.k1[1] = s7.z; e.k1[2] = s7.w;
+  e.es[0] = s8.x; e.es[1] = s8.y; e.es[2] = s8.z; e.es[3] = s8.w;
+  e.es[4] = s9.x; e.es[5] = s9.y; e.es[6] = s9.z; e.mar = s9.w;
+  e.Kp[0] = p0.x; e.Kp[1] = p0.y; e.Kp[2] = p0.z; e.cT = p0.w;
+  e.Kd[0] = p1.x; e.Kd[1] = p1.y; e.Kd[2] = p1.z; e.mp = p1.w;
+  e.ct[0] = p2.x; e.ct[1] = p2.y; e.ct[2] = p2.z; e.mc = p2.w;
+  e.J[0] = p3.x; e.J[1] = p3.y; e.J[2] = p3.z;
+  if (a.cfg.use_motor_model) {
+    float4 m = S[GR_P_MOTOR * n + i];
+    e.mw[0] = m.x; e.mw[1] = m.y; e.mw[2] = m.z; e.mw[3] = m.w;
+  } else {
+    e.mw[0] = e.mw[1] = e.mw[2] = e.mw[3] = 0.0f;
+  }
+  e.ep = ii.x; e.acc = ii.y; e.epoch = ii.z;
+  e.gate = ii.w & 0xff; e.lvl = (ii.w >> 8) & 0xff; e.azero = (ii.w >> 16) & 1; e.type = (ii.w >> 24) & 0xff;
+}
+
+// Dynamic planes (and, when `rst` is set, the per-episode DR planes) back to HBM.
+DEV void store_env(const KArgs& a, int i, const Env& e, bool rst, bool params) {
+  float4* S = reinterpret_cast<float4*>(a.buf.state);
+  const size_t n = (size_t)a.cfg.num_envs;
+  S[GR_P_POSQ * n + i] = make_float4(e.p[0], e.p[1], e.p[2], e.q[0]);
+  S[GR_P_QV * n + i] = make_float4(e.q[1], e.q[2], e.q[3], e.v[0]);
+  S[GR_P_VW * n + i] = make_float4(e.v[1], e.v[2], e.w[0], e.w[1]);
+  S[GR_P_WA * n + i] = make_float4(e.w[2], e.al[0], e.al[1], e.al[2]);
+  S[GR_P_CTRL * n + i] = make_float4(e.T, e.tau[0], e.tau[1], e.tau[2]);
+  S[GR_P_LAG * n + i] = make_float4(e.lag[0], e.lag[1], e.lag[2], e.lag[3]);
+  S[GR_P_EP0 * n + i] = make_float4(e.es[0], e.es[1], e.es[2], e.es[3]);
+  S[GR_P_EP1 * n + i] = make_float4(e.es[4], e.es[5], e.es[6], e.mar);
+  if (rst) {
+    S[GR_P_RST0 * n + i] = make_float4(e.thr, e.nl, e.k2[0], e.k2[1]);
+    S[GR_P_RST1 * n + i] = make_float4(e.k2[2], e.k1[0], e.k1[1], e.k1[2]);
+  }
+  if (params) {
+    S[GR_P_PAR0 * n + i] = make_float4(e.Kp[0], e.Kp[1], e.Kp[2], e.cT);
+    S[GR_P_PAR1 * n + i] = make_float4(e.Kd[0], e.Kd[1], e.Kd[2], e.mp);
+    S[GR_P_PAR2 * n + i] = make_float4(e.ct[0], e.ct[1], e.ct[2], e.mc);
+    S[GR_P_PAR3 * n + i] = make_float4(e.J[0], e.J[1], e.J[2], 0.0f);
+  }
+  if (a.cfg.use_motor_model) S[GR_P_MOTOR * n + i] = make_float4(e.mw[0], e.mw[1], e.mw[2], e.mw[3]);
+  int packed = (e.gate & 0xff) | ((e.lvl & 0xff) << 8) | ((e.azero & 1) << 16) | ((e.type & 0xff) << 24);
+  reinterpret_cast<int4*>(a.buf.istate)[i] = make_int4(e.ep, e.acc, e.epoch, packed);
+}
+
+// ------------------------------------------------------------- track table view
+// Packed table: per track [max_gates * GR_GATE_FLOATS gate records | GR_TRACK_FLOATS track record].
+// `base` points at the first track of type t0 (LDS copy or the global table).
+struct Tab {
+  const float* base;
+  int t0, L, G, stride;
+  DEV const float* track_base(int type, int lvl) const { return base + ((type - t0) * L + lvl) * stride; }
+  DEV const float* gate(int type, int lvl, int g) const { return track_base(type, lvl) + g * GR_GATE_FLOATS; }
+  DEV const float* rec(int type, int lvl) const { return track_base(type, lvl) + G * GR_GATE_FLOATS; }
+};
+
+DEV uint32_t gid_of(const KArgs& a, int i) { return (uint32_t)(a.cfg.env_id_offset + i); }
+DEV gr_u32x4 draw(const KArgs& a, uint32_t gid, uint32_t c1, uint32_t tag, uint32_t c3) {
+  return gr_philox4x32_10(gid, c1, tag, c3, a.cfg.seed_lo, a.cfg.seed_hi);
+}
+
+DEV void action_scale(const KArgs& a, float m_ctrl, float sc[4], float of[4]) {
+  float weight = m_ctrl * a.cfg.gravity;
+  float s0 = (weight * a.cfg.max_thrust_weight_ratio) / 2.0f;
+  sc[0] = s0; of[0] = s0;
+  for (int k = 1; k < 4; ++k) { sc[k] = a.cfg.body_rate_bound; of[k] = 0.0f; }
+}
+
+// ------------------------------------------------------------- collision
+__constant__ float c_lattice[17][3] = {
+    {0, 0, 0},          {1, 1, 1},         {1, -1, 1},        {-1, 1, 1},       {-1, -1, 1},     {1, 1, -1},
+    {1, -1, -1},        {-1, 1, -1},       {-1, -1, -1},      {0.5f, 0.5f, 0.5f}, {0.5f, -0.5f, 0.5f},
+    {-0.5f, 0.5f, 0.5f}, {-0.5f, -0.5f, 0.5f}, {0.5f, 0.5f, -0.5f}, {0.5f, -0.5f, -0.5f}, {-0.5f, 0.5f, -0.5f},
+    {-0.5f, -0.5f, -0.5f}};
+
+DEV void lattice_point(const KArgs& a, int k, const float p[3], const float q[4], float pt[3]) {
+  float o[3] = {c_lattice[k][0] * a.cfg.collider_half[0], c_lattice[k][1] * a.cfg.collider_half[1],
+                c_lattice[k][2] * a.cfg.collider_half[2]};
+  float r[3];
+  quat_rotate(q, o, r);
+  pt[0] = p[0] + r[0]; pt[1] = p[1] + r[1]; pt[2] = p[2] + r[2];
+}
+
+DEV bool point_in_gate(const float* g, const float pt[3]) {
+  float d0 = pt[0] - g[0], d1 = pt[1] - g[1], d2 = pt[2] - g[2];
+  float l0 = (g[4] * d0 + g[5] * d1) + g[6] * d2;
+  float l1 = (g[8] * d0 + g[9] * d1) + g[10] * d2;
+  float l2 = (g[12] * d0 + g[13] * d1) + g[14] * d2;
+  float a0 = gr_fabsf(l0), a1 = gr_fabsf(l1), a2 = gr_fabsf(l2);
+  bool in_outer = (a0 <= g[16]) & (a1 <= g[17]) & (a2 <= g[15]);
+  bool in_hole = (a0 < g[7]) & (a1 < g[11]);
+  return in_outer & !in_hole;
+}
+
+// number of the 17 lattice points inside a gate frame or under the ground
+// (replaces PhysX contact / Warp mesh_tools.py:128-233; see oracle)
+DEV int collision_count(const KArgs& a, const Tab& tab, int type, int lvl, const float p[3], const float q[4]) {
+  const float* rec = tab.rec(type, lvl);
+  const float ground = rec[0];
+  const int ng = (int)rec[3];
+  uint32_t inside = 0u;
+  // the lattice reaches at most |collider_half| (< lat_reach) from p: skip the
+  // per-point ground test when no point can be below the plane (conservative)
+  if (p[2] - ground < a.lat_reach) {
+    for (int k = 0; k < 17; ++k) {
+      float pt[3];
+      lattice_point(a, k, p, q, pt);
+      if (pt[2] < ground) inside |= 1u << k;
+    }
+  }
+  for (int g = 0; g < ng; ++g) {
+    const float* gr = tab.gate(type, lvl, g);
+    float d0 = p[0] - gr[0], d1 = p[1] - gr[1], d2 = p[2] - gr[2];
+    if ((d0 * d0 + d1 * d1) + d2 * d2 <= gr[3]) {
+      for (int k = 0; k < 17; ++k) {
+        float pt[3];
+        lattice_point(a, k, p, q, pt);
+        if (point_in_gate(gr, pt)) inside |= 1u << k;
+      }
+    }
+  }
+  return __builtin_popcount(inside);
+}
+
+// ------------------------------------------------------------- controller
+// CTBRController.compute (controller_diff.py:120-144)
+DEV void ctbr_compute(const KArgs& a, const float cmd[4], const float wb[3], const float ab[3], const float Kp[3],
+                      const float Kd[3], float cT, const float ct[3], float& T, float tau[3], float mw[4],
+                      float tt[4]) {
+  float T_des = gr_clampf(cmd[0], a.thrust_lo, a.thrust_hi);
+  T = (1.0f - cT) * T_des + cT * T;
+  const float* J = a.cfg.inertia;
+  float err[3], Jw[3], cr[3];
+  for (int i = 0; i < 3; ++i) err[i] = gr_clampf(cmd[i + 1], -a.cfg.body_rate_bound, a.cfg.body_rate_bound) - wb[i];
+  for (int i = 0; i < 3; ++i) Jw[i] = J[i] * wb[i];
+  cross3(wb, Jw, cr);
+  for (int i = 0; i < 3; ++i) {
+    float tdes = (J[i] * (Kp[i] * err[i]) + cr[i]) - Kd[i] * ab[i];
+    tau[i] = (1.0f - ct[i]) * tdes + ct[i] * tau[i];
+  }
+  tt[0] = T; tt[1] = tau[0]; tt[2] = tau[1]; tt[3] = tau[2];
+  if (!a.cfg.use_motor_model) return;
+  float f[4];
+  for (int r = 0; r < 4; ++r)
+    f[r] = ((tt[0] * a.Bi[r][0] + tt[1] * a.Bi[r][1]) + tt[2] * a.Bi[r][2]) + tt[3] * a.Bi[r][3];
+  for (int i = 0; i < 4; ++i) {
+    float fd = gr_clampf(f[i], 0.0f, a.motor_fmax);
+    float t3 = a.tm_k1sq - a.tm_4k2 * (a.tm_k0 - fd);
+    float wdes = a.tm_inv2k2 * (a.tm_negk1 + gr_sqrtf(t3));
+    mw[i] = a.motor_c * mw[i] + (1.0f - a.motor_c) * wdes;
+    f[i] = (a.tm_k2 * mw[i] * mw[i] + a.tm_k1 * mw[i]) + a.tm_k0;
+  }
+  for (int r = 0; r < 4; ++r) tt[r] = ((f[0] * a.B[r][0] + f[1] * a.B[r][1]) + f[2] * a.B[r][2]) + f[3] * a.B[r][3];
+}
+
+// ------------------------------------------------------------- integrators
+// DroneDynamics.step (droneDynamics.py:119-135)
+DEV void dd_explicit(float m, const float J[3], const float k2[3], const float k1[3], const float tt[4], float dt,
+                     float gz, float p[3], float q[4], float v[3], float w[3], float a_out[3], float al_out[3]) {
+  float vb[3];
+  quat_rotate_inverse(q, v, vb);
+  float thr[3] = {0.0f, 0.0f, tt[0]};
+  for (int i = 0; i < 3; ++i) thr[i] = (thr[i] - (k2[i] * vb[i]) * gr_fabsf(vb[i])) - k1[i] * vb[i];
+  float tw[3];
+  quat_rotate(q, thr, tw);
+  float acc[3] = {0.0f + tw[0] / m, 0.0f + tw[1] / m, -gz + tw[2] / m};
+  float Jw[3] = {J[0] * w[0], J[1] * w[1], J[2] * w[2]}, cr[3];
+  cross3(w, Jw, cr);
+  float al[3];
+  for (int i = 0; i < 3; ++i) {
+    float ji = 1.0f / J[i];
+    al[i] = ji * tt[i + 1] - ji * cr[i];
+  }
+  for (int i = 0; i < 3; ++i) p[i] = (p[i] + v[i] * dt) + ((0.5f * acc[i]) * dt) * dt;
+  float wq[4] = {0.0f, w[0], w[1], w[2]}, qd[4];
+  quat_mul(q, wq, qd);
+  for (int i = 0; i < 4; ++i) q[i] = q[i] + (0.5f * qd[i]) * dt;
+  float nq = gr_sqrtf(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3]);
+  for (int i = 0; i < 4; ++i) q[i] = q[i] / nq;
+  for (int i = 0; i < 3; ++i) v[i] = v[i] + acc[i] * dt;
+  for (int i = 0; i < 3; ++i) w[i] = w[i] + al[i] * dt;
+  for (int i = 0; i < 3; ++i) { a_out[i] = acc[i]; al_out[i] = al[i]; }
+}
+
+// semi-implicit Euler substep (PhysX role), wrench held over the substep
+DEV void si_substep(float m, const float J[3], const float fb[3], const float tb[3], float h, float gz, float p[3],
+                    float q[4], float v[3], float w[3], float a_out[3], float al_out[3]) {
+  float tw[3];
+  quat_rotate(q, fb, tw);
+  float acc[3] = {0.0f + tw[0] / m, 0.0f + tw[1] / m, -gz + tw[2] / m};
+  float Jw[3] = {J[0] * w[0], J[1] * w[1], J[2] * w[2]}, cr[3];
+  cross3(w, Jw, cr);
+  float al[3];
+  for (int i = 0; i < 3; ++i) al[i] = (tb[i] - cr[i]) / J[i];
+  for (int i = 0; i < 3; ++i) v[i] = v[i] + acc[i] * h;
+  for (int i = 0; i < 3; ++i) w[i] = w[i] + al[i] * h;
+  for (int i = 0; i < 3; ++i) p[i] = p[i] + v[i] * h;
+  float wq[4] = {0.0f, w[0], w[1], w[2]}, qd[4];
+  quat_mul(q, wq, qd);
+  for (int i = 0; i < 4; ++i) q[i] = q[i] + (0.5f * qd[i]) * h;
+  float nq = gr_sqrtf(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3]);
+  for (int i = 0; i < 4; ++i) q[i] = q[i] / nq;
+  for (int i = 0; i < 3; ++i) { a_out[i] = acc[i]; al_out[i] = al[i]; }
+}
+
+// ------------------------------------------------------------- reset
+DEV void reset_env(const KArgs& a, const Tab& tab, Env& e, uint32_t gid) {
+  const gr_config& c = a.cfg;
+  int up = e.acc >= c.level_up_threshold, down = e.acc < c.level_down_threshold;
+  int lvl = e.lvl + up - down;
+  uint32_t ep = (uint32_t)e.epoch + 1u;
+  gr_u32x4 r0 = draw(a, gid, ep, GR_TAG_RESET, 0), r1 = draw(a, gid, ep, GR_TAG_RESET, 1);
+  gr_u32x4 r2 = draw(a, gid, ep, GR_TAG_RESET, 2), r3 = draw(a, gid, ep, GR_TAG_RESET, 3);
+  gr_u32x4 r4 = draw(a, gid, ep, GR_TAG_RESET, 4), r5 = draw(a, gid, ep, GR_TAG_RESET, 5);
+  if (lvl >= c.num_levels) lvl = (int)gr_floorf(gr_u01(r4.w) * (float)c.num_levels);
+  else if (lvl < 0) lvl = 0;
+  if (c.noise_curriculum) {
+    float upf = e.acc >= c.noise_enhance_threshold ? 1.0f + c.noise_enhance : 1.0f;
+    float dnf = e.acc < c.noise_decay_threshold ? 1.0f - c.noise_decay : 1.0f;
+    e.nl = e.nl * upf;
+    e.nl = e.nl * dnf;
+  }
+  e.lvl = lvl;
+  float rp[6] = {gr_uniform(r0.x, -c.reset_pos_half[0], c.reset_pos_half[0]),
+                 gr_uniform(r0.y, -c.reset_pos_half[1], c.reset_pos_half[1]),
+                 gr_uniform(r0.z, -c.reset_pos_half[2], c.reset_pos_half[2]),
+                 gr_uniform(r0.w, -c.reset_att_half[0], c.reset_att_half[0]),
+                 gr_uniform(r1.x, -c.reset_att_half[1], c.reset_att_half[1]),
+                 gr_uniform(r1.y, -c.reset_att_half[2], c.reset_att_half[2])};
+  float rv[6] = {gr_uniform(r1.z, -c.reset_vel_half[0], c.reset_vel_half[0]),
+                 gr_uniform(r1.w, -c.reset_vel_half[1], c.reset_vel_half[1]),
+                 gr_uniform(r2.x, -c.reset_vel_half[2], c.reset_vel_half[2]),
+                 gr_uniform(r2.y, -c.reset_vel_half[3], c.reset_vel_half[3]),
+                 gr_uniform(r2.z, -c.reset_vel_half[4], c.reset_vel_half[4]),
+                 gr_uniform(r2.w, -c.reset_vel_half[5], c.reset_vel_half[5])};
+  for (int k = 0; k < 3; ++k) e.p[k] = c.spawn_pos[k] + rp[k];
+  const float* rec = tab.rec(e.type, lvl);
+  int start = (int)rec[2];
+  const float* g0 = tab.gate(e.type, lvl, start);
+  float tx = g0[0] - e.p[0], ty = g0[1] - e.p[1];
+  float yaw = gr_wrap_to_pi(gr_atan2f(ty, tx)) + rp[5];
+  float qd[4], qid[4] = {1.0f, 0.0f, 0.0f, 0.0f};
+  quat_from_euler_xyz(rp[3], rp[4], yaw, qd);
+  quat_mul(qid, qd, e.q);
+  for (int k = 0; k < 3; ++k) e.v[k] = 0.0f + rv[k];
+  float ww[3] = {0.0f + rv[3], 0.0f + rv[4], 0.0f + rv[5]};
+  quat_rotate_inverse(e.q, ww, e.w);
+  e.azero = 1;
+  e.T = 0.0f;
+  for (int k = 0; k < 3; ++k) { e.tau[k] = 0.0f; e.al[k] = 0.0f; }
+  for (int k = 0; k < 4; ++k) e.mw[k] = 0.0f;
+  if (c.random_drag) {
+    float z = c.z_drag + gr_u01(r3.x) * c.z_drag_rand;
+    float u2[3] = {gr_u01(r3.y), gr_u01(r3.z), gr_u01(r3.w)};
+    float u1[3] = {gr_u01(r4.x), gr_u01(r4.y), gr_u01(r4.z)};
+    for (int k = 0; k < 3; ++k) {
+      e.k2[k] = c.drag2[k] * e.mc + u2[k] * c.drag2_rand;
+      e.k1[k] = c.drag1[k] * e.mc + u1[k] * c.drag1_rand;
+    }
+    e.k2[2] = e.k2[2] * z;
+    e.k1[2] = e.k1[2] * z;
+  }
+  float z0, z1;
+  gr_box_muller(r5.x, r5.y, &z0, &z1);
+  e.thr = 1.0f + z0 * 0.01f;
+  for (int k = 0; k < 7; ++k) e.es[k] = 0.0f;
+  e.mar = 0.0f;
+  e.acc = 0;
+  e.gate = start;
+  e.ep = 0;
+  e.epoch = (int)ep;
+}
+
+// ------------------------------------------------------------- observations
+DEV void gate_noise(const KArgs& a, const Env& e, uint32_t gid, int which, float out[3]) {
+  if (!a.cfg.add_gate_noise) { out[0] = out[1] = out[2] = 0.0f; return; }
+  gr_u32x4 b = draw(a, gid, (uint32_t)e.epoch, GR_TAG_GATE, (uint32_t)(2 * e.acc + which));
+  uint32_t wv[3] = {b.x, b.y, b.z};
+  for (int k = 0; k < 3; ++k) {
+    float lo = (-a.cfg.gate_noise_pos[k]) * e.nl, hi = a.cfg.gate_noise_pos[k] * e.nl;
+    out[k] = lo + gr_u01(wv[k]) * (hi - lo);
+  }
+}
+
+DEV void write_obs(const KArgs& a, const Tab& tab, const Env& e, int i, uint32_t gid, uint32_t cnt,
+                   const float lc[4], float aux) {
+  const float* rec = tab.rec(e.type, e.lvl);
+  int ng = (int)rec[3];
+  const float* g = tab.gate(e.type, e.lvl, e.gate);
+  int gnext = e.gate + 1;
+  if (gnext >= ng) gnext -= ng;
+  const float* gn = tab.gate(e.type, e.lvl, gnext);
+  float g0[3] = {g[0], g[1], g[2]}, gn0[3] = {gn[0], gn[1], gn[2]};
+  float vb[3], r2[3];
+  quat_rotate_inverse(e.q, e.v, vb);
+  matrix_row2(e.q, r2);
+  float d[3] = {g0[0] - e.p[0], g0[1] - e.p[1], g0[2] - e.p[2]};
+  float dn[3] = {gn0[0] - g0[0], gn0[1] - g0[1], gn0[2] - g0[2]};
+  float cg[3], cn[3];
+  quat_rotate_inverse(e.q, d, cg);
+  quat_rotate_inverse(e.q, dn, cn);
+  float4* C = reinterpret_cast<float4*>(a.buf.obs_critic) + (size_t)i * 4;
+  C[0] = make_float4(vb[0], vb[1], vb[2], r2[0]);
+  C[1] = make_float4(r2[1], r2[2], cg[0], cg[1]);
+  C[2] = make_float4(cg[2], cn[0], cn[1], cn[2]);
+  C[3] = make_float4(lc[0], lc[1], lc[2], lc[3]);
+  float nz[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (a.cfg.obs_noise) {
+    gr_u32x4 b0 = draw(a, gid, cnt, GR_TAG_OBS, 0), b1 = draw(a, gid, cnt, GR_TAG_OBS, 1);
+    gr_box_muller(b0.x, b0.y, &nz[0], &nz[1]);
+    gr_box_muller(b0.z, b0.w, &nz[2], &nz[3]);
+    gr_box_muller(b1.x, b1.y, &nz[4], &nz[5]);
+    gr_box_muller(b1.z, b1.w, &nz[6], &nz[7]);
+  }
+  float qn[4], qq[4], r2n[3];
+  quat_from_euler_xyz(nz[3] * a.cfg.obs_att_noise, nz[4] * a.cfg.obs_att_noise, nz[5] * a.cfg.obs_att_noise, qn);
+  quat_mul(e.q, qn, qq);
+  matrix_row2(qq, r2n);
+  float ng0[3], ng1[3];
+  gate_noise(a, e, gid, 0, ng0);
+  gate_noise(a, e, gid, 1, ng1);
+  float gw[3] = {g0[0] + ng0[0], g0[1] + ng0[1], g0[2] + ng0[2]};
+  float gnw[3] = {gn0[0] + ng1[0], gn0[1] + ng1[1], gn0[2] + ng1[2]};
+  float dp[3] = {gw[0] - e.p[0], gw[1] - e.p[1], gw[2] - e.p[2]};
+  float dnp[3] = {gnw[0] - gw[0], gnw[1] - gw[1], gnw[2] - gw[2]};
+  float pg[3], pn[3];
+  quat_rotate_inverse(e.q, dp, pg);
+  quat_rotate_inverse(e.q, dnp, pn);
+  float vn[3];
+  for (int k = 0; k < 3; ++k) vn[k] = vb[k] * (1.0f + nz[k] * a.cfg.obs_lin_vel_noise);
+  float4* P = reinterpret_cast<float4*>(a.buf.obs_policy) + (size_t)i * 4;
+  P[0] = make_float4(vn[0], vn[1], vn[2], r2n[0]);
+  P[1] = make_float4(r2n[1], r2n[2], pg[0], pg[1]);
+  P[2] = make_float4(pg[2], pn[0], pn[1], pn[2]);
+  P[3] = make_float4(lc[0], lc[1], lc[2], lc[3]);
+  a.buf.obs_aux[i] = aux;
+}
+
+// ------------------------------------------------------------- log reduction
+// Sum the GR_LOG_SLOTS values of the workgroup into log_partial[block][:].
+DEV void block_log(const KArgs& a, float* vals, float* lds_red, bool any) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int first = any ? 0 : GR_LOG_LEVEL;
+  for (int s = first; s < GR_LOG_SLOTS; ++s) {
+    float v = vals[s];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (lane == 0) lds_red[wave * GR_LOG_SLOTS + s] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < GR_LOG_SLOTS) {
+    int s = threadIdx.x;
+    float t = 0.0f;
+    if (s >= first)
+      for (int wv = 0; wv < GR_BLOCK / 64; ++wv) t += lds_red[wv * GR_LOG_SLOTS + s];
+    a.buf.log_partial[(size_t)blockIdx.x * GR_LOG_SLOTS + s] = t;
+  }
+}
+
+// ------------------------------------------------------------- the kernel
+template <int MODE, bool USE_LDS>
+__global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const float* __restrict__ actions,
+                                                        const uint8_t* __restrict__ mask) {
+  extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+  __shared__ float lds_red[(GR_BLOCK / 64) * GR_LOG_SLOTS];
+  const int n = a.cfg.num_envs;
+  const int i = blockIdx.x * GR_BLOCK + threadIdx.x;
+  const bool live = i < n;
+
+  // ---- stage the gate geometry of this workgroup's terrain types ----
+  const int first_env = blockIdx.x * GR_BLOCK;
+  const int last_env = min(first_env + GR_BLOCK, n) - 1;
+  int t0 = 0, t1 = 0;
+  for (int t = 1; t < a.cfg.num_types; ++t) {
+    t0 += first_env >= a.type_start[t];
+    t1 += last_env >= a.type_start[t];
+  }
+  Tab tab;
+  tab.L = a.cfg.num_levels;
+  tab.G = a.cfg.max_gates;
+  tab.stride = a.track_stride;
+  tab.t0 = t0;
+  if (USE_LDS) {
+    const float4* src = reinterpret_cast<const float4*>(a.table + (size_t)t0 * tab.L * tab.stride);
+    const int nvec = (t1 - t0 + 1) * tab.L * tab.stride / 4;
+    for (int k = threadIdx.x; k < nvec; k += GR_BLOCK) lds_tab[k] = src[k];
+    __syncthreads();
+    tab.base = reinterpret_cast<const float*>(lds_tab);
+  } else {
+    tab.base = a.table + (size_t)t0 * tab.L * tab.stride;
+  }
+
+  const uint32_t cnt = a.buf.counters[0];
+  float lg[GR_LOG_SLOTS];
+  for (int s = 0; s < GR_LOG_SLOTS; ++s) lg[s] = 0.0f;
+  bool any_reset = false;
+
+  if (live) {
+    const gr_config& c = a.cfg;
+    const uint32_t gid = gid_of(a, i);
+    Env e;
+    load_env(a, i, e);
+    if (MODE == KMODE_STEP) {
+      const float4 act = reinterpret_cast<const float4*>(actions)[i];
+      const float dt = c.step_dt;
+      float lin_prev = norm3(e.v), ang_prev = norm3(e.w), mar_prev = e.mar;
+      float cur[4] = {act.x, act.y, act.z, act.w}, prev[4], raw[4];
+      for (int k = 0; k < 4; ++k) prev[k] = e.azero ? 0.0f : e.lag[k];
+      e.azero = 0;
+      for (int k = 0; k < 4; ++k) { raw[k] = c.action_lag ? e.lag[k] : cur[k]; e.lag[k] = cur[k]; }
+      float sc[4], of[4], cmd[4], th_raw[4];
+      action_scale(a, e.mc, sc, of);
+      for (int k = 0; k < 4; ++k) { th_raw[k] = gr_tanhf(raw[k]); cmd[k] = th_raw[k] * sc[k] + of[k]; }
+      cmd[0] = cmd[0] * e.thr;
+      float tt[4];
+      ctbr_compute(a, cmd, e.w, e.al, e.Kp, e.Kd, e.cT, e.ct, e.T, e.tau, e.mw, tt);
+      const float m = c.dr_plant ? e.mp : e.mc;
+      float Jp[3];
+      for (int k = 0; k < 3; ++k) Jp[k] = c.dr_plant ? e.J[k] : c.inertia[k];
+      float accl[3], al[3];
+      int ccount = 0;
+      if (c.integrator == GR_INTEGRATOR_DD_EXPLICIT) {
+        dd_explicit(m, Jp, e.k2, e.k1, tt, dt, c.gravity, e.p, e.q, e.v, e.w, accl, al);
+        ccount = collision_count(a, tab, e.type, e.lvl, e.p, e.q);
+      } else {
+        float vb[3], fb[3] = {0.0f, 0.0f, tt[0]};
+        quat_rotate_inverse(e.q, e.v, vb);
+        for (int k = 0; k < 3; ++k) fb[k] = (fb[k] - (e.k2[k] * vb[k]) * gr_fabsf(vb[k])) - e.k1[k] * vb[k];
+        for (int s = 0; s < c.decimation; ++s) {
+          si_substep(m, Jp, fb, tt + 1, c.sim_dt, c.gravity, e.p, e.q, e.v, e.w, accl, al);
+          int cc = collision_count(a, tab, e.type, e.lvl, e.p, e.q);
+          ccount = cc > ccount ? cc : ccount;
+        }
+      }
+      for (int k = 0; k < 3; ++k) e.al[k] = al[k];
+      e.ep += 1;
+      const int time_out = e.ep >= c.max_episode_length;
+      const int contact = ccount > c.collision_count_threshold;
+      const float* rec = tab.rec(e.type, e.lvl);
+      const float zw = e.p[2] + rec[1];
+      const int oob = (zw < c.out_of_bound[0]) | (zw > c.out_of_bound[1]);
+      const int bad = (1.0f - 2.0f * (e.q[1] * e.q[1] + e.q[2] * e.q[2])) < 0.0f;
+      const int c_term = c.stage == 0 ? oob : contact;
+      const int terminated = (c.term_contact && c_term) | (c.term_bad_pose && bad);
+      // rewards
+      const float* g = tab.gate(e.type, e.lvl, e.gate);
+      float vb[3], dg[3] = {g[0] - e.p[0], g[1] - e.p[1], g[2] - e.p[2]}, gb[3];
+      quat_rotate_inverse(e.q, e.v, vb);
+      quat_rotate_inverse(e.q, dg, gb);
+      float f[7];
+      f[0] = cosine_similarity(vb, gb);
+      float th_cur[4], th_prev[4], br[3];
+      for (int k = 0; k < 4; ++k) { th_cur[k] = gr_tanhf(cur[k]); th_prev[k] = gr_tanhf(prev[k]); }
+      for (int k = 0; k < 3; ++k) br[k] = th_cur[k + 1] * sc[k + 1];
+      f[1] = norm3(br);
+      float sq[4];
+      for (int k = 0; k < 4; ++k) {
+        float dd = (th_cur[k] * sc[k] + of[k]) - (th_prev[k] * sc[k] + of[k]);
+        sq[k] = dd * dd;
+      }
+      f[2] = ((sq[0] + sq[1]) + sq[2]) + sq[3];
+      f[3] = (float)contact;
+      float nb = gr_maxf(norm3(gb), 1e-12f);
+      float gh[3] = {gb[0] / nb, gb[1] / nb, gb[2] / nb}, fx[3] = {1.0f, 0.0f, 0.0f};
+      f[4] = cosine_similarity(gh, fx);
+      float dist = norm3(dg);
+      const int near_gate = dist < c.gate_threshold;
+      f[5] = (float)near_gate * (1.0f / (dist * dist + 1.0f));
+      f[6] = (float)bad;
+      float rew = 0.0f;
+      for (int k = 0; k < 7; ++k) {
+        const float wk = a.w[k];
+        if (wk == 0.0f) continue;
+        float v = (f[k] * wk) * dt;
+        rew = rew + v;
+        e.es[k] = e.es[k] + v;
+      }
+      a.buf.reward[i] = rew;
+      const float aux = near_gate ? 1.0f : 0.0f;
+      e.mar = f[2];
+      const int done = terminated | time_out;
+      a.buf.terminated[i] = (uint8_t)terminated;
+      a.buf.time_out[i] = (uint8_t)time_out;
+      a.buf.dones[i] = (int64_t)done;
+      if (done) {
+        any_reset = true;
+        lg[GR_LOG_NRESET] = 1.0f;
+        for (int k = 0; k < 7; ++k) lg[GR_LOG_EPSUM0 + k] = e.es[k];
+        lg[GR_LOG_ACC] = (float)e.acc;
+        lg[GR_LOG_M_ACTRATE] = mar_prev;
+        lg[GR_LOG_M_LINSPD] = lin_prev;
+        lg[GR_LOG_M_ANGSPD] = ang_prev;
+        lg[GR_LOG_T_TIMEOUT] = (float)time_out;
+        lg[GR_LOG_T_CONTACT] = (float)c_term;
+        lg[GR_LOG_T_BADPOSE] = (float)bad;
+        reset_env(a, tab, e, gid);
+      }
+      // command compute: _update_metrics + _update_command (commands.py:247-260, 308-350)
+      {
+        const float* gg = tab.gate(e.type, e.lvl, e.gate);
+        float dd[3] = {gg[0] - e.p[0], gg[1] - e.p[1], gg[2] - e.p[2]};
+        if (norm3(dd) < c.gate_threshold) {
+          const int ngt = (int)tab.rec(e.type, e.lvl)[3];
+          e.acc += 1;
+          e.gate = e.gate + 1;
+          if (e.gate >= ngt) e.gate -= ngt;
+        }
+      }
+      float lc[4];
+      for (int k = 0; k < 4; ++k) lc[k] = th_raw[k] * sc[k] + of[k];
+      lc[0] = lc[0] / e.mc;
+      write_obs(a, tab, e, i, gid, cnt, lc, aux);
+      store_env(a, i, e, done != 0, false);
+    } else {
+      // MODE_RESET / MODE_OBSERVE: last_ctbr and aux carry over from the previous observation
+      const float4 lcv = reinterpret_cast<const float4*>(a.buf.prev_obs_critic)[(size_t)i * 4 + 3];
+      float lc[4] = {lcv.x, lcv.y, lcv.z, lcv.w};
+      const float aux = a.buf.prev_obs_aux[i];
+      bool did = false;
+      if (MODE == KMODE_RESET && (mask == nullptr || mask[i])) {
+        did = true;
+        any_reset = true;
+        lg[GR_LOG_NRESET] = 1.0f;
+        for (int k = 0; k < 7; ++k) lg[GR_LOG_EPSUM0 + k] = e.es[k];
+        lg[GR_LOG_ACC] = (float)e.acc;
+        lg[GR_LOG_M_ACTRATE] = e.mar;
+        lg[GR_LOG_M_LINSPD] = norm3(e.v);
+        lg[GR_LOG_M_ANGSPD] = norm3(e.w);
+        lg[GR_LOG_T_TIMEOUT] = a.buf.prev_time_out[i] ? 1.0f : 0.0f;
+        reset_env(a, tab, e, gid);
+      }
+      write_obs(a, tab, e, i, gid, cnt, lc, aux);
+      if (did) store_env(a, i, e, true, false);
+    }
+    lg[GR_LOG_LEVEL] = (float)e.lvl;
+    lg[GR_LOG_NOISE] = e.nl;
+  }
+  if (MODE != KMODE_OBSERVE) {
+    const bool any = __syncthreads_or(any_reset);
+    block_log(a, lg, lds_red, any);
+  }
+}
+
+// ------------------------------------------------------------- init (startup events)
+__global__ __launch_bounds__(GR_BLOCK) void init_kernel(KArgs a) {
+  const int i = blockIdx.x * GR_BLOCK + threadIdx.x;
+  const gr_config& c = a.cfg;
+  if (i >= c.num_envs) return;
+  const uint32_t gid = gid_of(a, i);
+  Env e;
+  gr_u32x4 b0 = draw(a, gid, 0, GR_TAG_STATIC, 0), b1 = draw(a, gid, 0, GR_TAG_STATIC, 1);
+  gr_u32x4 b2 = draw(a, gid, 0, GR_TAG_STATIC, 2), b3 = draw(a, gid, 0, GR_TAG_STATIC, 3);
+  gr_u32x4 b4 = draw(a, gid, 0, GR_TAG_STATIC, 4);
+  const int dr = c.dr_startup;
+  const float plo = c.pid_scale_range[0], phi = c.pid_scale_range[1];
+  const float dlo = c.delay_scale_range[0], dhi = c.delay_scale_range[1];
+  float skp[3] = {gr_uniform(b0.x, plo, phi), gr_uniform(b0.y, plo, phi), gr_uniform(b0.z, plo, phi)};
+  float skd[3] = {gr_uniform(b0.w, plo, phi), gr_uniform(b1.x, plo, phi), gr_uniform(b1.y, plo, phi)};
+  float sdt = gr_uniform(b1.z, dlo, dhi);
+  float sdq[3] = {gr_uniform(b1.w, dlo, dhi), gr_uniform(b2.x, dlo, dhi), gr_uniform(b2.y, dlo, dhi)};
+  float madd = gr_uniform(b2.z, c.mass_add_range[0], c.mass_add_range[1]);
+  float sj[3] = {gr_uniform(b2.w, c.inertia_scale_range[0], c.inertia_scale_range[1]),
+                 gr_uniform(b3.x, c.inertia_scale_range[0], c.inertia_scale_range[1]),
+                 gr_uniform(b3.y, c.inertia_scale_range[0], c.inertia_scale_range[1])};
+  for (int k = 0; k < 3; ++k) {
+    e.Kp[k] = dr ? c.rate_gain_p[k] * skp[k] : c.rate_gain_p[k];
+    e.Kd[k] = dr ? c.rate_gain_d[k] * skd[k] : c.rate_gain_d[k];
+  }
+  float tauT = dr ? c.thrust_ctrl_delay * sdt : c.thrust_ctrl_delay;
+  e.cT = gr_expf(-c.step_dt / tauT);
+  for (int k = 0; k < 3; ++k) {
+    float tq = dr ? c.torque_ctrl_delay[k] * sdq[k] : c.torque_ctrl_delay[k];
+    e.ct[k] = gr_expf(-c.step_dt / tq);
+  }
+  e.mc = c.mass;
+  float mp = (dr && c.dr_plant) ? c.mass + madd : c.mass;
+  e.mp = mp;
+  for (int k = 0; k < 3; ++k) e.J[k] = (dr && c.dr_plant) ? (c.inertia[k] * (mp / c.mass)) * sj[k] : c.inertia[k];
+  e.lvl = (int)gr_floorf(gr_u01(b3.z) * (float)(c.max_init_level + 1));
+  float z0, z1;
+  gr_box_muller(b3.w, b4.x, &z0, &z1);
+  e.thr = 1.0f + z0 * 0.02f;
+  e.nl = 1.0f;
+  for (int k = 0; k < 3; ++k) { e.k2[k] = c.drag2[k] * c.mass; e.k1[k] = c.drag1[k] * c.mass; }
+  e.k2[2] = e.k2[2] * c.z_drag;
+  e.k1[2] = e.k1[2] * c.z_drag;
+  for (int k = 0; k < 3; ++k) { e.p[k] = c.spawn_pos[k]; e.v[k] = 0.0f; e.w[k] = 0.0f; e.al[k] = 0.0f; e.tau[k] = 0.0f; }
+  e.q[0] = 1.0f; e.q[1] = e.q[2] = e.q[3] = 0.0f;
+  e.T = 0.0f;
+  for (int k = 0; k < 4; ++k) { e.lag[k] = 0.0f; e.mw[k] = 0.0f; }
+  for (int k = 0; k < 7; ++k) e.es[k] = 0.0f;
+  e.mar = 0.0f;
+  e.ep = 0; e.acc = 0; e.epoch = 0; e.gate = 0; e.azero = 1;
+  int type = 0;
+  for (int t = 1; t < c.num_types; ++t) type += (i >= a.type_start[t]);
+  e.type = type;
+  store_env(a, i, e, true, true);
+  // initial observation buffers: last action = ctbr(0) (DiffActions._raw_actions starts at zero)
+  float sc[4], of[4];
+  action_scale(a, e.mc, sc, of);
+  float4* C = reinterpret_cast<float4*>(a.buf.obs_critic) + (size_t)i * 4;
+  float4* P = reinterpret_cast<float4*>(a.buf.obs_policy) + (size_t)i * 4;
+  const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  float4 l4 = make_float4((gr_tanhf(0.0f) * sc[0] + of[0]) / e.mc, gr_tanhf(0.0f) * sc[1] + of[1],
+                          gr_tanhf(0.0f) * sc[2] + of[2], gr_tanhf(0.0f) * sc[3] + of[3]);
+  C[0] = z4; C[1] = z4; C[2] = z4; C[3] = l4;
+  P[0] = z4; P[1] = z4; P[2] = z4; P[3] = l4;
+  a.buf.obs_aux[i] = 0.0f;
+  a.buf.reward[i] = 0.0f;
+  a.buf.terminated[i] = 0;
+  a.buf.time_out[i] = 0;
+  a.buf.dones[i] = 0;
+}
+
+// ------------------------------------------------------------- finalize
+// One workgroup: sums log_partial over the step kernel's workgroups, turns sums
+// into the means IL's managers log (reward_manager / command / curriculum),
+// and advances the observation-noise call counter.
+__global__ __launch_bounds__(256) void finalize_kernel(KArgs a, int nblocks, int with_log) {
+  __shared__ float red[256];
+  if (with_log) {
+    for (int s = 0; s < GR_LOG_SLOTS; ++s) {
+      float t = 0.0f;
+      for (int b = threadIdx.x; b < nblocks; b += 256) t += a.buf.log_partial[(size_t)b * GR_LOG_SLOTS + s];
+      red[threadIdx.x] = t;
+      __syncthreads();
+      for (int off = 128; off > 0; off >>= 1) {
+        if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) a.buf.log_out[s] = red[0];  // raw sums, converted below
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      float* o = a.buf.log_out;
+      const float nr = o[GR_LOG_NRESET];
+      if (nr == 0.0f && a.buf.log_prev != nullptr) {
+        // no env reset this call: the reference leaves extras["log"] untouched (stale), keep it
+        for (int s = 0; s < GR_LOG_SLOTS; ++s) o[s] = a.buf.log_prev[s];
+      } else {
+        for (int k = 0; k < 7; ++k) o[GR_LOG_EPSUM0 + k] = o[GR_LOG_EPSUM0 + k] / nr / a.cfg.episode_length_s;
+        for (int k = GR_LOG_ACC; k <= GR_LOG_M_ANGSPD; ++k) o[k] = o[k] / nr;
+        o[GR_LOG_LEVEL] = o[GR_LOG_LEVEL] / (float)a.cfg.num_envs;
+        o[GR_LOG_NOISE] = o[GR_LOG_NOISE] / (float)a.cfg.num_envs;
+      }
+    }
+  }
+  if (threadIdx.x == 0) a.buf.counters[0] = a.buf.counters[0] + 1u;
+}
+
+// ------------------------------------------------------------- test kernels
+__global__ void test_dynamics_kernel(KArgs a, int n, int mode, const float* si, const float* ab, const float* cmd,
+                                     const float* ci, const float* par, const float* drag, float* so, float* co,
+                                     float* xo) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float p[3], q[4], v[3], w[3], acc[3], al[3], tt[4], T = ci[i * 4], tau[3] = {ci[i * 4 + 1], ci[i * 4 + 2], ci[i * 4 + 3]};
+  float mw[4] = {0, 0, 0, 0};
+  for (int k = 0; k < 3; ++k) { p[k] = si[i * 13 + k]; v[k] = si[i * 13 + 7 + k]; w[k] = si[i * 13 + 10 + k]; }
+  for (int k = 0; k < 4; ++k) q[k] = si[i * 13 + 3 + k];
+  const float* pr = par + i * 16;
+  if (mode == 0) {
+    ctbr_compute(a, cmd + i * 4, w, ab + i * 3, pr + 0, pr + 4, pr[3], pr + 8, T, tau, mw, tt);
+  } else {
+    for (int k = 0; k < 4; ++k) tt[k] = cmd[i * 4 + k];
+  }
+  dd_explicit(pr[7], pr + 12, drag + i * 6, drag + i * 6 + 3, tt, a.cfg.step_dt, a.cfg.gravity, p, q, v, w, acc, al);
+  for (int k = 0; k < 3; ++k) { so[i * 13 + k] = p[k]; so[i * 13 + 7 + k] = v[k]; so[i * 13 + 10 + k] = w[k]; }
+  for (int k = 0; k < 4; ++k) so[i * 13 + 3 + k] = q[k];
+  co[i * 4] = T;
+  for (int k = 0; k < 3; ++k) co[i * 4 + 1 + k] = tau[k];
+  float ww[3];
+  quat_rotate(q, w, ww);
+  for (int k = 0; k < 3; ++k) { xo[i * 9 + k] = acc[k]; xo[i * 9 + 3 + k] = al[k]; xo[i * 9 + 6 + k] = ww[k]; }
+}
+
+__global__ void test_math_kernel(int fn, int n, const float* x, const float* y, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s, c;
+  switch (fn) {
+    case 0: out[i] = gr_expf(x[i]); break;
+    case 1: out[i] = gr_tanhf(x[i]); break;
+    case 2: out[i] = gr_logf(x[i]); break;
+    case 3: gr_sincosf(x[i], &s, &c); out[i] = s; break;
+    case 4: gr_sincosf(x[i], &s, &c); out[i] = c; break;
+    case 5: out[i] = gr_atan2f(x[i], y[i]); break;
+    case 6: out[i] = gr_sqrtf(x[i]); break;
+    default: out[i] = x[i] / y[i]; break;
+  }
+}
+
+__global__ void test_philox_kernel(int n, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                   uint32_t k1, uint32_t* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  gr_u32x4 r = gr_philox4x32_10(c0 + (uint32_t)i, c1, c2, c3, k0, k1);
+  out[i * 4] = r.x; out[i * 4 + 1] = r.y; out[i * 4 + 2] = r.z; out[i * 4 + 3] = r.w;
+}
+
+// ------------------------------------------------------------- launchers
+static int grid_of(int n) { return (n + GR_BLOCK - 1) / GR_BLOCK; }
+
+template <int MODE>
+static hipError_t launch_env_mode(const KArgs& a, const float* actions, const uint8_t* mask, hipStream_t s) {
+  const int g = grid_of(a.cfg.num_envs);
+  if (a.lds_bytes > 0) {
+    hipLaunchKernelGGL((env_kernel<MODE, true>), dim3(g), dim3(GR_BLOCK), a.lds_bytes, s, a, actions, mask);
+  } else {
+    hipLaunchKernelGGL((env_kernel<MODE, false>), dim3(g), dim3(GR_BLOCK), 0, s, a, actions, mask);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_env(int mode, const KArgs& a, const float* actions, const uint8_t* mask, hipStream_t s,
+                      hipEvent_t t0, hipEvent_t t1) {
+  hipError_t err;
+  if (t0) {
+    err = hipEventRecord(t0, s);
+    if (err != hipSuccess) return err;
+  }
+  if (mode == KMODE_STEP) err = launch_env_mode<KMODE_STEP>(a, actions, mask, s);
+  else if (mode == KMODE_RESET) err = launch_env_mode<KMODE_RESET>(a, actions, mask, s);
+  else err = launch_env_mode<KMODE_OBSERVE>(a, actions, mask, s);
+  if (err != hipSuccess) return err;
+  if (t1) {
+    err = hipEventRecord(t1, s);
+    if (err != hipSuccess) return err;
+  }
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, a, grid_of(a.cfg.num_envs), mode != KMODE_OBSERVE ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_init(const KArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(init_kernel, dim3(grid_of(a.cfg.num_envs)), dim3(GR_BLOCK), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_test_dynamics(const KArgs& a, int n, int mode, const float* si, const float* ab, const float* cmd,
+                                const float* ci, const float* par, const float* drag, float* so, float* co, float* xo,
+                                hipStream_t s) {
+  hipLaunchKernelGGL(test_dynamics_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, n, mode, si, ab, cmd, ci, par,
+                     drag, so, co, xo);
+  return hipGetLastError();
+}
+
+hipError_t launch_test_math(int fn, int n, const float* x, const float* y, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(test_math_kernel, dim3((n + 255) / 256), dim3(256), 0, s, fn, n, x, y, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_test_philox(int n, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
+                              uint32_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(test_philox_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, c0, c1, c2, c3, k0, k1, out);
+  return hipGetLastError();
+}
+
+}  // namespace gr

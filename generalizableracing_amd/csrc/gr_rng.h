@@ -1,0 +1,61 @@
+/*
+ * gr_rng.h — counter-based RNG (Philox4x32-10, Salmon et al. SC'11) and the
+ * mapping of its words to the uniform / Gaussian draws the racing env needs.
+ *
+ * Every random draw of the env step is a pure function of
+ *   key     = (seed_lo, seed_hi)
+ *   counter = (global env id, epoch-or-step, stream tag, block index)
+ * so the HIP kernel, the CPU oracle and any number of ranks reproduce the same
+ * stream without storing RNG state in HBM (the reference uses torch's stateful
+ * generator; its exact stream is not reproducible anyway — see DESIGN.md).
+ * Shared verbatim by the kernel and the oracle; compiles as C and HIP C++.
+ */
+#ifndef GR_RNG_H
+#define GR_RNG_H
+
+#include "gr_math.h"
+
+typedef struct { uint32_t x, y, z, w; } gr_u32x4;
+
+GR_HD gr_u32x4 gr_philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                uint32_t k0, uint32_t k1) {
+  for (int i = 0; i < 10; ++i) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c2;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c1 ^ k0;
+    uint32_t n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  gr_u32x4 r = {c0, c1, c2, c3};
+  return r;
+}
+
+/* uniform in [0, 1): 24 random bits, exact in fp32 */
+GR_HD float gr_u01(uint32_t w) { return (float)(w >> 8) * 5.9604645e-08f; }
+/* uniform in (0, 1]: for log() in Box-Muller */
+GR_HD float gr_u01_open0(uint32_t w) { return (float)((w >> 8) + 1u) * 5.9604645e-08f; }
+/* torch-style  U(lo, hi) = u * (hi - lo) + lo  (Isaac Lab sample_uniform op order) */
+GR_HD float gr_uniform(uint32_t w, float lo, float hi) { return gr_u01(w) * (hi - lo) + lo; }
+
+/* Box-Muller: two standard normals from two words */
+GR_HD void gr_box_muller(uint32_t w0, uint32_t w1, float* z0, float* z1) {
+  float u1 = gr_u01_open0(w0);
+  float u2 = gr_u01(w1);
+  float rad = gr_sqrtf(-2.0f * gr_logf(u1));
+  float s, c;
+  gr_sincosf(6.28318548f * u2, &s, &c);
+  *z0 = rad * c;
+  *z1 = rad * s;
+}
+
+/* stream tags (counter word 2) */
+#define GR_TAG_STATIC 0x53544154u /* startup DR: gains, delays, mass, inertia, initial level */
+#define GR_TAG_RESET 0x52535421u  /* per-episode reset draws, counter1 = epoch */
+#define GR_TAG_GATE 0x47415445u   /* gate-pose noise, counter1 = epoch, counter3 = 2*pass+j */
+#define GR_TAG_OBS 0x4f425321u    /* observation noise, counter1 = call counter */
+
+#endif /* GR_RNG_H */

@@ -1,0 +1,341 @@
+"""The racing env on the device: Python surface over libgr.so.
+
+`RacingEnv` mirrors `ManagerBasedDiffRLEnv` (extensions/diff.lab/diff/lab/envs/
+manager_based_diff_rl_env.py): `step(action) -> (obs_dict, reward, terminated,
+time_outs, extras)`, `reset()`, `episode_length_buf`, `max_episode_length`, …
+`RslRlVecEnvWrapper` mirrors Isaac Lab's rsl_rl wrapper, the VecEnv the
+runner drives (standalone/rsl_rl/ext/runners/on_policy_runner.py:38,119-143).
+
+Every step is ONE fused HIP launch (+ a one-workgroup log finalize) on the
+current torch stream, with no host synchronisation.  Output tensors alternate
+between two buffer sets (ping-pong) because rsl_rl keeps step t's `obs`
+while step t+1 runs; a tensor returned by step t stays valid until step t+2.
+`extras["log"]` entries come from a ring of 64 steps (the runner reads them at
+the end of its 24-step rollout).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from collections.abc import Mapping
+
+import torch
+
+from .. import _abi
+from .racing_cfg import RacingEnvCfg
+from .tracks import build_track_table
+
+LOG_RING = 64
+
+
+class _EpisodeLog(Mapping):
+    """extras["log"]: lazily materialised 0-dim device tensors (no host sync)."""
+
+    __slots__ = ("_row", "_keys")
+
+    def __init__(self, row: torch.Tensor, keys: dict):
+        self._row = row
+        self._keys = keys
+
+    def __getitem__(self, k):
+        return self._row[self._keys[k]]
+
+    def __iter__(self):
+        return iter(self._keys)
+
+    def __len__(self):
+        return len(self._keys)
+
+
+class RacingEnv:
+    """Vectorised drone-racing env (one shard of envs on one GPU)."""
+
+    metadata = {"render_modes": [None]}
+
+    def __init__(self, cfg: RacingEnvCfg, render_mode=None, **kwargs):
+        self.cfg = cfg
+        self.render_mode = render_mode
+        self.device = torch.device(cfg.sim.device)
+        if self.device.type != "cuda":
+            raise RuntimeError(
+                "RacingEnv runs on an MI355X (torch 'cuda' device on ROCm); got device "
+                f"{self.device}.  The env step is HIP-only, there is no CPU path."
+            )
+        if not torch.cuda.is_available():
+            raise RuntimeError("RacingEnv needs a GPU: torch.cuda.is_available() is False")
+        self._lib = _abi.load()
+        self._gcfg = cfg.to_gr_config()
+        self.num_envs = int(cfg.scene.num_envs)
+        self.num_actions = 4
+        self.step_dt = cfg.step_dt
+        self.physics_dt = cfg.sim.dt
+        self.common_step_counter = 0
+        dev = self.device
+
+        ctx = C.c_void_p()
+        _abi.check(self._lib, None, self._lib.gr_create(C.byref(self._gcfg), C.byref(ctx)), "gr_create")
+        self._ctx = ctx
+
+        # ---- track table (host-generated once, then device-resident) ----
+        gates, recs = build_track_table(num_types=cfg.terrain.num_cols, num_levels=cfg.terrain.num_rows,
+                                        num_gates=cfg.terrain.num_gates,
+                                        seed=cfg.terrain.seed + cfg.track_seed_offset)
+        self.track_gates = torch.from_numpy(gates).to(dev).contiguous()
+        self.track_records = torch.from_numpy(recs).to(dev).contiguous()
+        self._call("gr_bind_tracks", self.track_gates.data_ptr(), self.track_records.data_ptr())
+
+        # ---- state (SoA float4 planes) and outputs ----
+        n = self.num_envs
+        self.state = torch.zeros(_abi.NUM_PLANES, n, 4, dtype=torch.float32, device=dev)
+        self.istate = torch.zeros(n, 4, dtype=torch.int32, device=dev)
+        self._sets = [self._alloc_outputs(n, dev) for _ in range(2)]
+        self._nblocks = self._lib.gr_num_blocks(ctx)
+        self._log_partial = torch.zeros(self._nblocks, _abi.LOG_SLOTS, dtype=torch.float32, device=dev)
+        self._log_ring = torch.zeros(LOG_RING, _abi.LOG_SLOTS, dtype=torch.float32, device=dev)
+        self._counters = torch.zeros(4, dtype=torch.int32, device=dev)
+        self._calls = 0
+        self._cur = 0  # index of the output set written by the last call
+        self._bufs = [self._make_buffers(k) for k in range(LOG_RING)]
+        self._log_keys = self._build_log_keys()
+        self.extras: dict = {}
+        # startup (gr_init): nominal state, startup DR events, initial terrain levels
+        self._bind(0)
+        self._call("gr_init", self._stream())
+        self._calls, self._cur = 1, 1  # gr_init wrote output set 1
+
+    # ------------------------------------------------------------------ plumbing
+    @staticmethod
+    def _alloc_outputs(n, dev):
+        return {
+            "policy": torch.zeros(n, _abi.OBS_DIM, dtype=torch.float32, device=dev),
+            "critic": torch.zeros(n, _abi.OBS_DIM, dtype=torch.float32, device=dev),
+            "auxiliary": torch.zeros(n, 1, dtype=torch.float32, device=dev),
+            "reward": torch.zeros(n, dtype=torch.float32, device=dev),
+            "terminated": torch.zeros(n, dtype=torch.bool, device=dev),
+            "time_out": torch.zeros(n, dtype=torch.bool, device=dev),
+            "dones": torch.zeros(n, dtype=torch.int64, device=dev),
+        }
+
+    def _make_buffers(self, k: int) -> _abi.GrBuffers:
+        """Buffers for call number k: outputs -> set (k+1)%2, previous -> set k%2, log ring slot k."""
+        out, prev = self._sets[(k + 1) % 2], self._sets[k % 2]
+        b = _abi.GrBuffers()
+        b.state = self.state.data_ptr()
+        b.istate = self.istate.data_ptr()
+        b.obs_policy = out["policy"].data_ptr()
+        b.obs_critic = out["critic"].data_ptr()
+        b.obs_aux = out["auxiliary"].data_ptr()
+        b.reward = out["reward"].data_ptr()
+        b.terminated = out["terminated"].data_ptr()
+        b.time_out = out["time_out"].data_ptr()
+        b.dones = out["dones"].data_ptr()
+        b.prev_obs_critic = prev["critic"].data_ptr()
+        b.prev_obs_aux = prev["auxiliary"].data_ptr()
+        b.prev_time_out = prev["time_out"].data_ptr()
+        b.log_partial = self._log_partial.data_ptr()
+        b.log_out = self._log_ring[(k + 1) % LOG_RING].data_ptr()
+        b.log_prev = self._log_ring[k % LOG_RING].data_ptr()
+        b.counters = self._counters.data_ptr()
+        return b
+
+    def _bind(self, k: int):
+        self._call("gr_bind_buffers", C.byref(self._bufs[k % LOG_RING]))
+
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _call(self, name, *args):
+        rc = getattr(self._lib, name)(self._ctx, *args)
+        if rc != 0:
+            raise RuntimeError(f"{name} failed (status {rc}): {self._lib.gr_last_error(self._ctx).decode()}")
+
+    def _advance(self):
+        """Bind the next output set + log slot; returns the set that will be written."""
+        k = self._calls
+        self._bind(k)
+        self._calls += 1
+        self._cur = (k + 1) % 2
+        return self._sets[self._cur], self._log_ring[(k + 1) % LOG_RING]
+
+    def _build_log_keys(self) -> dict:
+        c = self.cfg
+        keys = {}
+        for j, name in enumerate(c.reward_term_names()):
+            keys[f"Episode_Reward/{name}"] = _abi.LOG_EPSUM0 + j
+        cur = c.curriculum_term_names()
+        keys[f"Curriculum/{cur[0]}"] = _abi.LOG_LEVEL
+        if len(cur) > 1:
+            keys[f"Curriculum/{cur[1]}"] = _abi.LOG_NOISE
+        for name, slot in (("accumulate_gates", _abi.LOG_ACC), ("action_rate", _abi.LOG_M_ACTRATE),
+                           ("avg_lin_spd", _abi.LOG_M_LINSPD), ("avg_ang_spd", _abi.LOG_M_ANGSPD)):
+            keys[f"Metrics/next_gate_pose/{name}"] = slot
+        tnames = c.termination_term_names()
+        slots = [_abi.LOG_T_TIMEOUT, _abi.LOG_T_CONTACT, _abi.LOG_T_BADPOSE]
+        for name, slot in zip(tnames, slots):
+            keys[f"Episode_Termination/{name}"] = slot
+        return keys
+
+    def _obs_dict(self, s):
+        return {"policy": s["policy"], "critic": s["critic"], "auxiliary": s["auxiliary"]}
+
+    # ------------------------------------------------------------------ properties
+    @property
+    def unwrapped(self):
+        return self
+
+    @property
+    def max_episode_length_s(self) -> float:
+        return self.cfg.episode_length_s
+
+    @property
+    def max_episode_length(self) -> int:
+        return self.cfg.max_episode_length
+
+    @property
+    def episode_length_buf(self) -> torch.Tensor:
+        return self.istate[:, _abi.I_EPLEN]
+
+    @episode_length_buf.setter
+    def episode_length_buf(self, value: torch.Tensor):
+        self.istate[:, _abi.I_EPLEN].copy_(value.to(self.device))
+
+    @property
+    def obs_buf(self) -> dict:
+        return self._obs_dict(self._sets[self._cur])
+
+    @property
+    def gr_config(self) -> _abi.GrConfig:
+        return self._gcfg
+
+    def bytes_per_env_step(self) -> tuple[int, int]:
+        r, w = C.c_int64(), C.c_int64()
+        self._call("gr_bytes_per_env_step", C.byref(r), C.byref(w))
+        return r.value, w.value
+
+    def state_field(self, name: str) -> torch.Tensor:
+        """Gather a named per-env state field ([N, k] copy) from the SoA planes."""
+        parts = [self.state[p, :, c0:c0 + k] for p, c0, k in _abi.STATE_FIELDS[name]]
+        return torch.cat(parts, dim=1)
+
+    def set_state_field(self, name: str, value: torch.Tensor):
+        j = 0
+        for p, c0, k in _abi.STATE_FIELDS[name]:
+            self.state[p, :, c0:c0 + k].copy_(value[:, j:j + k])
+            j += k
+
+    @property
+    def gate_id(self) -> torch.Tensor:
+        return self.istate[:, _abi.I_PACKED] & 0xFF
+
+    @property
+    def terrain_levels(self) -> torch.Tensor:
+        return (self.istate[:, _abi.I_PACKED] >> 8) & 0xFF
+
+    @property
+    def terrain_types(self) -> torch.Tensor:
+        return (self.istate[:, _abi.I_PACKED] >> 24) & 0xFF
+
+    # ------------------------------------------------------------------ MDP
+    def step(self, action: torch.Tensor):
+        """ManagerBasedDiffRLEnv.step (manager_based_diff_rl_env.py:160-267)."""
+        if action.dim() != 2 or action.shape[1] != self.num_actions:
+            raise ValueError(f"Invalid action shape, expected: {self.num_actions}, received: {action.shape[-1]}.")
+        if action.shape[0] != self.num_envs:
+            raise ValueError(f"Invalid action batch {action.shape[0]}, expected {self.num_envs}")
+        a = action
+        if a.device != self.device or a.dtype != torch.float32 or not a.is_contiguous() or a.data_ptr() % 16:
+            a = a.to(device=self.device, dtype=torch.float32).contiguous()
+        out, log_row = self._advance()
+        self._call("gr_step", a.data_ptr(), self._stream())
+        self.common_step_counter += 1
+        self.extras = {"log": _EpisodeLog(log_row, self._log_keys)}
+        return self._obs_dict(out), out["reward"], out["terminated"], out["time_out"], self.extras
+
+    def reset(self, seed: int | None = None, env_ids=None, options=None):
+        """ManagerBasedEnv.reset -> _reset_idx(env_ids) (+ curriculum), then observations."""
+        mask_t = None
+        if env_ids is not None:
+            ids = torch.as_tensor(env_ids, device=self.device, dtype=torch.long)
+            mask_t = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
+            mask_t[ids] = 1
+        out, log_row = self._advance()
+        self._call("gr_reset", mask_t.data_ptr() if mask_t is not None else None, self._stream())
+        self.extras = {"log": _EpisodeLog(log_row, self._log_keys)}
+        return self._obs_dict(out), self.extras
+
+    def observe(self) -> dict:
+        """ObservationManager.compute(): fresh observation noise, no state change."""
+        out, _ = self._advance()
+        self._call("gr_observe", self._stream())
+        return self._obs_dict(out)
+
+    def seed(self, seed: int = -1) -> int:
+        return seed
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._lib.gr_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class RslRlVecEnvWrapper:
+    """Isaac Lab's omni.isaac.lab_tasks.utils.wrappers.rsl_rl.RslRlVecEnvWrapper surface
+    (call sites: standalone/rsl_rl/train.py:120, on_policy_runner.py:38,119-122,143)."""
+
+    def __init__(self, env: RacingEnv):
+        self.env = env
+        self.num_envs = env.num_envs
+        self.device = env.device
+        self.max_episode_length = env.max_episode_length
+        self.num_actions = env.num_actions
+        self.num_obs = _abi.OBS_DIM
+        self.num_privileged_obs = _abi.OBS_DIM
+        self.env.reset()
+
+    @property
+    def cfg(self):
+        return self.env.cfg
+
+    @property
+    def unwrapped(self) -> RacingEnv:
+        return self.env
+
+    @property
+    def render_mode(self):
+        return self.env.render_mode
+
+    @property
+    def episode_length_buf(self) -> torch.Tensor:
+        return self.env.episode_length_buf
+
+    @episode_length_buf.setter
+    def episode_length_buf(self, value: torch.Tensor):
+        self.env.episode_length_buf = value
+
+    def seed(self, seed: int = -1) -> int:
+        return self.env.seed(seed)
+
+    def get_observations(self):
+        obs_dict = self.env.observe()
+        return obs_dict["policy"], {"observations": obs_dict}
+
+    def reset(self):
+        obs_dict, _ = self.env.reset()
+        return obs_dict["policy"], {"observations": obs_dict}
+
+    def step(self, actions: torch.Tensor):
+        obs_dict, rew, terminated, truncated, extras = self.env.step(actions)
+        extras["observations"] = obs_dict
+        if not self.env.cfg.is_finite_horizon:
+            extras["time_outs"] = truncated
+        # dones = (terminated | truncated).long(), written by the kernel directly
+        dones = self.env._sets[self.env._cur]["dones"]
+        return obs_dict["policy"], rew, dones, extras
+
+    def close(self):
+        return self.env.close()

@@ -1,0 +1,7 @@
+"""rsl_rl surface (runner / PPO / storage / ActorCritic) in PyTorch-ROCm, mirroring
+standalone/rsl_rl/ext of the reference, with RCCL data parallelism."""
+from .actor_critic import ActorCritic, EmpiricalNormalization  # noqa: F401
+from .config import QuadcopterPPORunnerCfg, RslRlPpoActorCriticCfg, RslRlPpoAlgorithmCfg  # noqa: F401
+from .on_policy_runner import OnPolicyRunner  # noqa: F401
+from .ppo import PPO  # noqa: F401
+from .rollout_storage import RolloutStorage  # noqa: F401

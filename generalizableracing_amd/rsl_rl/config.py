@@ -1,0 +1,57 @@
+"""Runner configuration (rsl_rl_ppo_cfg.py:15-41, QuadcopterPPORunnerCfg) as plain dataclasses.
+
+`to_dict()` produces the dict layout Isaac Lab's RslRlOnPolicyRunnerCfg.to_dict()
+hands to OnPolicyRunner (keys "policy", "algorithm", "num_steps_per_env", …).
+Hidden dims are 256x256 (BASELINE.json); the reference's state-only cfg uses 128x128.
+"""
+from __future__ import annotations
+
+from dataclasses import asdict, dataclass, field
+
+
+@dataclass
+class RslRlPpoActorCriticCfg:
+    class_name: str = "ActorCritic"
+    init_noise_std: float = 1.0
+    noise_std_type: str = "scalar"
+    actor_hidden_dims: list = field(default_factory=lambda: [256, 256])
+    critic_hidden_dims: list = field(default_factory=lambda: [256, 256])
+    activation: str = "lrelu"
+
+
+@dataclass
+class RslRlPpoAlgorithmCfg:
+    class_name: str = "PPO"
+    value_loss_coef: float = 1.0
+    use_clipped_value_loss: bool = True
+    clip_param: float = 0.2
+    entropy_coef: float = 0.0
+    num_learning_epochs: int = 5
+    num_mini_batches: int = 4
+    learning_rate: float = 5.0e-4
+    schedule: str = "adaptive"
+    gamma: float = 0.99
+    lam: float = 0.95
+    desired_kl: float = 0.01
+    max_grad_norm: float = 1.0
+
+
+@dataclass
+class QuadcopterPPORunnerCfg:
+    seed: int = 42
+    device: str = "cuda:0"
+    num_steps_per_env: int = 24
+    max_iterations: int = 5000
+    empirical_normalization: bool = False
+    policy: RslRlPpoActorCriticCfg = field(default_factory=RslRlPpoActorCriticCfg)
+    algorithm: RslRlPpoAlgorithmCfg = field(default_factory=RslRlPpoAlgorithmCfg)
+    save_interval: int = 500
+    experiment_name: str = "racing_ppo"
+    run_name: str = ""
+    logger: str = "tensorboard"
+    resume: bool = False
+    load_run: str = ".*"
+    load_checkpoint: str = "model_.*.pt"
+
+    def to_dict(self) -> dict:
+        return asdict(self)

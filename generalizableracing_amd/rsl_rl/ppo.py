@@ -1,0 +1,139 @@
+"""PPO (standalone/rsl_rl/ext/algorithms/ppo.py:14-190) + data parallelism.
+
+Same act / process_env_step (time-out bootstrap) / compute_returns / update
+as the reference: clipped surrogate, clipped value loss, adaptive-KL learning
+rate, grad-norm clipping, Adam.  Added for the multi-GPU path:
+the KL mean is averaged across ranks before the learning-rate decision and
+gradients are averaged in one flat all-reduce before clipping, so every rank
+applies the identical update.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.optim as optim
+
+from . import distributed as gdist
+from .rollout_storage import RolloutStorage
+
+
+class PPO:
+    def __init__(self, policy, env=None, num_learning_epochs=1, num_mini_batches=1, clip_param=0.2, gamma=0.998,
+                 lam=0.95, value_loss_coef=1.0, entropy_coef=0.0, learning_rate=1e-3, max_grad_norm=1.0,
+                 use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu",
+                 normalize_advantage=True, storage_obs_dtype=torch.float32, **kwargs):
+        self.env = env
+        self.device = device
+        self.desired_kl = desired_kl
+        self.schedule = schedule
+        self.learning_rate = learning_rate
+        self.policy = policy
+        self.policy.to(self.device)
+        gdist.broadcast_params(self.policy)
+        self.storage: RolloutStorage | None = None
+        self.optimizer = optim.Adam(self.policy.parameters(), lr=learning_rate)
+        self.transition = RolloutStorage.Transition()
+        self.clip_param = clip_param
+        self.num_learning_epochs = num_learning_epochs
+        self.num_mini_batches = num_mini_batches
+        self.value_loss_coef = value_loss_coef
+        self.entropy_coef = entropy_coef
+        self.gamma = gamma
+        self.lam = lam
+        self.max_grad_norm = max_grad_norm
+        self.use_clipped_value_loss = use_clipped_value_loss
+        self.normalize_advantage = normalize_advantage
+        self.storage_obs_dtype = storage_obs_dtype
+
+    def init_storage(self, training_type, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape,
+                     action_shape):
+        self.storage = RolloutStorage(training_type, num_envs, num_transitions_per_env, actor_obs_shape,
+                                      critic_obs_shape, action_shape, self.device, obs_dtype=self.storage_obs_dtype)
+
+    def test_mode(self):
+        self.policy.eval()
+
+    def train_mode(self):
+        self.policy.train()
+
+    def act(self, obs, critic_obs):
+        self.transition.actions = self.policy.act(obs).detach()
+        self.transition.values = self.policy.evaluate(critic_obs).detach()
+        self.transition.actions_log_prob = self.policy.get_actions_log_prob(self.transition.actions).detach()
+        self.transition.action_mean = self.policy.action_mean.detach()
+        self.transition.action_sigma = self.policy.action_std.detach()
+        self.transition.observations = obs
+        self.transition.privileged_observations = critic_obs
+        return self.transition.actions
+
+    def process_env_step(self, rewards, dones, infos):
+        self.transition.rewards = rewards.clone()
+        self.transition.dones = dones
+        if "time_outs" in infos:  # bootstrapping on time outs (ppo.py:88-92)
+            self.transition.rewards += self.gamma * torch.squeeze(
+                self.transition.values * infos["time_outs"].unsqueeze(1).to(self.device), 1)
+        self.storage.add_transitions(self.transition)
+        self.transition.clear()
+        self.policy.reset(dones)
+
+    def compute_returns(self, last_critic_obs):
+        last_values = self.policy.evaluate(last_critic_obs).detach()
+        self.storage.compute_returns(last_values, self.gamma, self.lam, self.normalize_advantage)
+
+    def update(self):
+        mean_value_loss = torch.zeros((), device=self.device)
+        mean_surrogate_loss = torch.zeros((), device=self.device)
+        generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
+        params = list(self.policy.parameters())
+        for (obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch, returns_batch,
+             old_actions_log_prob_batch, old_mu_batch, old_sigma_batch, hid_states_batch, masks_batch) in generator:
+            self.policy.act(obs_batch)
+            actions_log_prob_batch = self.policy.get_actions_log_prob(actions_batch)
+            value_batch = self.policy.evaluate(critic_obs_batch)
+            mu_batch = self.policy.action_mean
+            sigma_batch = self.policy.action_std
+            entropy_batch = self.policy.entropy
+            # adaptive KL learning rate (ppo.py:133-150)
+            if self.desired_kl is not None and self.schedule == "adaptive":
+                with torch.inference_mode():
+                    kl = torch.sum(
+                        torch.log(sigma_batch / old_sigma_batch + 1.0e-5)
+                        + (torch.square(old_sigma_batch) + torch.square(old_mu_batch - mu_batch))
+                        / (2.0 * torch.square(sigma_batch)) - 0.5, axis=-1)
+                    kl_mean = gdist.allreduce_mean(torch.mean(kl))
+                    kl_val = float(kl_mean)  # host decision, as in the reference
+                    if kl_val > self.desired_kl * 2.0:
+                        self.learning_rate = max(1e-5, self.learning_rate / 1.5)
+                    elif self.desired_kl / 2.0 > kl_val > 0.0:
+                        self.learning_rate = min(1e-2, self.learning_rate * 1.5)
+                    for g in self.optimizer.param_groups:
+                        g["lr"] = self.learning_rate
+            # surrogate (ppo.py:152-158)
+            ratio = torch.exp(actions_log_prob_batch - torch.squeeze(old_actions_log_prob_batch))
+            surrogate = -torch.squeeze(advantages_batch) * ratio
+            surrogate_clipped = -torch.squeeze(advantages_batch) * torch.clamp(ratio, 1.0 - self.clip_param,
+                                                                               1.0 + self.clip_param)
+            surrogate_loss = torch.max(surrogate, surrogate_clipped).mean()
+            # value loss (ppo.py:160-169)
+            if self.use_clipped_value_loss:
+                value_clipped = target_values_batch + (value_batch - target_values_batch).clamp(-self.clip_param,
+                                                                                                self.clip_param)
+                value_losses = (value_batch - returns_batch).pow(2)
+                value_losses_clipped = (value_clipped - returns_batch).pow(2)
+                value_loss = torch.max(value_losses, value_losses_clipped).mean()
+            else:
+                value_loss = (returns_batch - value_batch).pow(2).mean()
+            loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_batch.mean()
+            self.optimizer.zero_grad()
+            loss.backward()
+            gdist.allreduce_grads(params)
+            nn.utils.clip_grad_norm_(params, self.max_grad_norm)
+            self.optimizer.step()
+            mean_value_loss += value_loss.detach()
+            mean_surrogate_loss += surrogate_loss.detach()
+        num_updates = self.num_learning_epochs * self.num_mini_batches
+        self.storage.clear()
+        return {
+            "value_function": float(mean_value_loss) / num_updates,
+            "surrogate": float(mean_surrogate_loss) / num_updates,
+        }

@@ -1,0 +1,128 @@
+"""RolloutStorage (standalone/rsl_rl/ext/storage/rollout_storage.py:12-191).
+
+(T, N, .) device buffers, GAE, advantage normalisation and the shuffled
+mini-batch generator.  Multi-GPU: advantages are normalised with the GLOBAL
+mean / std over all ranks (two all-reduces), so a k-rank run normalises
+exactly like one rank holding all k shards.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import distributed as gdist
+
+
+class RolloutStorage:
+    class Transition:
+        def __init__(self):
+            self.observations = None
+            self.privileged_observations = None
+            self.actions = None
+            self.privileged_actions = None
+            self.rewards = None
+            self.dones = None
+            self.values = None
+            self.actions_log_prob = None
+            self.action_mean = None
+            self.action_sigma = None
+            self.hidden_states = None
+
+        def clear(self):
+            self.__init__()
+
+    def __init__(self, training_type, num_envs, num_transitions_per_env, obs_shape, privileged_obs_shape,
+                 actions_shape, device="cpu", obs_dtype=torch.float32):
+        self.device = device
+        self.training_type = training_type
+        self.obs_shape = obs_shape
+        self.privileged_obs_shape = privileged_obs_shape
+        self.actions_shape = actions_shape
+        T, N = num_transitions_per_env, num_envs
+        self.observations = torch.zeros(T, N, *obs_shape, device=device, dtype=obs_dtype)
+        if privileged_obs_shape[0] is not None:
+            self.privileged_observations = torch.zeros(T, N, *privileged_obs_shape, device=device, dtype=obs_dtype)
+        else:
+            self.privileged_observations = None
+        self.rewards = torch.zeros(T, N, 1, device=device)
+        self.actions = torch.zeros(T, N, *actions_shape, device=device)
+        self.dones = torch.zeros(T, N, 1, device=device).byte()
+        if training_type == "distillation":
+            self.privileged_actions = torch.zeros(T, N, *actions_shape, device=device)
+        if training_type == "rl":
+            self.actions_log_prob = torch.zeros(T, N, 1, device=device)
+            self.values = torch.zeros(T, N, 1, device=device)
+            self.returns = torch.zeros(T, N, 1, device=device)
+            self.advantages = torch.zeros(T, N, 1, device=device)
+            self.mu = torch.zeros(T, N, *actions_shape, device=device)
+            self.sigma = torch.zeros(T, N, *actions_shape, device=device)
+        self.num_transitions_per_env = T
+        self.num_envs = N
+        self.saved_hidden_states_a = None
+        self.saved_hidden_states_c = None
+        self.step = 0
+
+    def add_transitions(self, transition: "RolloutStorage.Transition"):
+        if self.step >= self.num_transitions_per_env:
+            raise AssertionError("Rollout buffer overflow")
+        self.observations[self.step].copy_(transition.observations)
+        if self.privileged_observations is not None:
+            self.privileged_observations[self.step].copy_(transition.privileged_observations)
+        self.actions[self.step].copy_(transition.actions)
+        self.rewards[self.step].copy_(transition.rewards.view(-1, 1))
+        self.dones[self.step].copy_(transition.dones.view(-1, 1))
+        if self.training_type == "distillation":
+            self.privileged_actions[self.step].copy_(transition.privileged_actions)
+        if self.training_type == "rl":
+            self.values[self.step].copy_(transition.values)
+            self.actions_log_prob[self.step].copy_(transition.actions_log_prob.view(-1, 1))
+            self.mu[self.step].copy_(transition.action_mean)
+            self.sigma[self.step].copy_(transition.action_sigma)
+        self.step += 1
+
+    def clear(self):
+        self.step = 0
+
+    def compute_returns(self, last_values, gamma, lam, normalize_advantage: bool = True):
+        """GAE, rollout_storage.py:113-127."""
+        advantage = 0
+        for step in reversed(range(self.num_transitions_per_env)):
+            next_values = last_values if step == self.num_transitions_per_env - 1 else self.values[step + 1]
+            next_is_not_terminal = 1.0 - self.dones[step].float()
+            delta = self.rewards[step] + next_is_not_terminal * gamma * next_values - self.values[step]
+            advantage = delta + next_is_not_terminal * gamma * lam * advantage
+            self.returns[step] = advantage + self.values[step]
+        self.advantages = self.returns - self.values
+        if normalize_advantage:
+            mean, std = gdist.global_mean_std(self.advantages)
+            self.advantages = (self.advantages - mean) / (std + 1e-8)
+
+    def get_statistics(self):
+        done = self.dones.clone()
+        done[-1] = 1
+        flat_dones = done.permute(1, 0, 2).reshape(-1, 1)
+        done_indices = torch.cat((flat_dones.new_tensor([-1], dtype=torch.int64),
+                                  flat_dones.nonzero(as_tuple=False)[:, 0]))
+        trajectory_lengths = done_indices[1:] - done_indices[:-1]
+        return trajectory_lengths.float().mean(), self.rewards.mean()
+
+    def mini_batch_generator(self, num_mini_batches, num_epochs=8):
+        """rollout_storage.py:152-191: one randperm, `num_epochs` passes of `num_mini_batches` chunks."""
+        if self.training_type != "rl":
+            raise ValueError("This function is only available for reinforcement learning training.")
+        batch_size = self.num_envs * self.num_transitions_per_env
+        mini_batch_size = batch_size // num_mini_batches
+        indices = torch.randperm(num_mini_batches * mini_batch_size, requires_grad=False, device=self.device)
+        observations = self.observations.flatten(0, 1)
+        privileged = self.privileged_observations.flatten(0, 1) if self.privileged_observations is not None else observations
+        actions = self.actions.flatten(0, 1)
+        values = self.values.flatten(0, 1)
+        returns = self.returns.flatten(0, 1)
+        old_logp = self.actions_log_prob.flatten(0, 1)
+        advantages = self.advantages.flatten(0, 1)
+        old_mu = self.mu.flatten(0, 1)
+        old_sigma = self.sigma.flatten(0, 1)
+        for _ in range(num_epochs):
+            for i in range(num_mini_batches):
+                idx = indices[i * mini_batch_size:(i + 1) * mini_batch_size]
+                yield (observations[idx].float(), privileged[idx].float(), actions[idx], values[idx], advantages[idx],
+                       returns[idx], old_logp[idx], old_mu[idx], old_sigma[idx], (None, None), None)

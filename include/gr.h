@@ -1,0 +1,262 @@
+/*
+ * gr.h — C ABI of libgr.so, the MI355X-native step of the drone-racing task
+ * `DiffLab-Quadcopter-CTBR-Racing-v0` (yufengsjtu/GeneralizableRacing).
+ *
+ * The reference has no native boundary of its own: the env step is Python
+ * (Isaac Lab managers + PhysX).  The entry points below are what its Python
+ * layer would bind to replace that step; each cites the reference code it
+ * replaces (paths relative to the reference repo root):
+ *
+ *   gr_create / gr_bind_* / gr_init   ManagerBasedDiffRLEnv.__init__ + load_managers
+ *                                     (extensions/diff.lab/diff/lab/envs/manager_based_diff_rl_env.py:108-141)
+ *                                     + startup events (.../quadcopter_diff/mdp/events.py:30-137)
+ *   gr_reset                          ManagerBasedEnv.reset -> _reset_idx
+ *                                     (manager_based_diff_rl_env.py:362-410)
+ *   gr_step                           ManagerBasedDiffRLEnv.step (manager_based_diff_rl_env.py:160-267)
+ *   gr_observe                        RslRlVecEnvWrapper.get_observations -> ObservationManager.compute
+ *   gr_test_dynamics                  DroneDynamics.step / CTBRController.compute in isolation
+ *                                     (.../mdp/dynamics/droneDynamics.py:119-135,
+ *                                      extensions/diff.lab/diff/lab/controllers/controller_diff.py:120-144)
+ *
+ * Conventions: plain C, no exceptions cross the ABI, every function returns 0
+ * on success and a negative code on failure (gr_last_error() has the text).
+ * All per-env buffers are allocated by the caller (PyTorch) on the device;
+ * the library never allocates inside gr_step/gr_reset/gr_observe, never
+ * synchronises the host, and launches only on the caller's stream, so the
+ * calls are hipGraph-capturable.
+ */
+#ifndef GR_H
+#define GR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GR_ABI_VERSION 1
+
+/* ---- status codes ---- */
+#define GR_OK 0
+#define GR_ERR_ARG -1
+#define GR_ERR_HIP -2
+#define GR_ERR_STATE -3
+
+/* ---- integrators ---- */
+#define GR_INTEGRATOR_DD_EXPLICIT 0   /* DroneDynamics.step order, one explicit step of step_dt */
+#define GR_INTEGRATOR_SEMI_IMPLICIT 1 /* `decimation` semi-implicit Euler substeps of sim_dt (PhysX-like) */
+
+/* ---- state layout: float planes, each [num_envs][4] fp32, plane-major ---- */
+#define GR_P_POSQ 0   /* px py pz qw            (env-local frame: world - env_origin) */
+#define GR_P_QV 1     /* qx qy qz vwx           (q = w,x,y,z body->world; v world frame) */
+#define GR_P_VW 2     /* vwy vwz wbx wby        (w = body angular rate) */
+#define GR_P_WA 3     /* wbz abx aby abz        (a = last body angular acceleration) */
+#define GR_P_CTRL 4   /* T tx ty tz             (CTBR thrust/torque delay-filter state) */
+#define GR_P_LAG 5    /* action-lag buffer (previous raw action) */
+#define GR_P_RST0 6   /* thr_est_err noise_level k2x k2y */
+#define GR_P_RST1 7   /* k2z k1x k1y k1z        (quadratic / linear drag) */
+#define GR_P_EP0 8    /* episode reward sums 0..3 */
+#define GR_P_EP1 9    /* episode reward sums 4..6, last action_rate metric */
+#define GR_P_PAR0 10  /* Kp xyz, thrust filter coefficient exp(-dt/tau_T) */
+#define GR_P_PAR1 11  /* Kd xyz, plant mass */
+#define GR_P_PAR2 12  /* torque filter coefficients exp(-dt/tau_tau) xyz, controller mass */
+#define GR_P_PAR3 13  /* plant inertia diag xyz, spare */
+#define GR_P_MOTOR 14 /* rotor speeds (motor model only) */
+#define GR_NUM_PLANES 15
+/* int plane [num_envs][4] int32: episode_length, accumulate_gates, epoch, packed */
+#define GR_I_EPLEN 0
+#define GR_I_ACC 1
+#define GR_I_EPOCH 2
+#define GR_I_PACKED 3 /* bits 0-7 gate_id, 8-15 terrain level, bit 16: action-manager buffers zeroed */
+
+#define GR_OBS_DIM 16
+#define GR_GATE_FLOATS 20 /* per-gate record, see DESIGN.md "track table" */
+#define GR_TRACK_FLOATS 4 /* per-track record: ground_z, origin_z, start_gate, num_gates */
+
+/* ---- log slots (extras["log"]) ---- */
+#define GR_LOG_NRESET 0
+#define GR_LOG_EPSUM0 1 /* 7 reward terms, declaration order of RewardsCfg */
+#define GR_LOG_ACC 8
+#define GR_LOG_M_ACTRATE 9
+#define GR_LOG_M_LINSPD 10
+#define GR_LOG_M_ANGSPD 11
+#define GR_LOG_T_TIMEOUT 12
+#define GR_LOG_T_CONTACT 13 /* base_contact (stage 1/2) or outofbound (stage 0) */
+#define GR_LOG_T_BADPOSE 14
+#define GR_LOG_LEVEL 15
+#define GR_LOG_NOISE 16
+#define GR_LOG_SLOTS 20
+
+/*
+ * Task configuration.  Field meanings follow the reference cfg classes; the
+ * defaults (gr_config_default) are those of QuadcopterRacingCTBREnvCfg with
+ * TRAINING_STAGE=1 (racing_ctbr_env.py:97-398) and CTBRControllerCfg
+ * (controller_diff_cfg.py:22-54).  All fields are 4 bytes: no padding.
+ */
+typedef struct gr_config {
+  int32_t num_envs;
+  int32_t env_id_offset; /* rank * num_envs: distinct RNG streams per shard */
+  uint32_t seed_lo, seed_hi;
+  int32_t num_types;      /* terrain columns (20) */
+  int32_t num_levels;     /* terrain rows (10) */
+  int32_t max_gates;      /* gates per track (8; 32 for config C5) */
+  int32_t max_init_level; /* max_init_terrain_level (5) */
+  int32_t stage;          /* TRAINING_STAGE 0/1/2 */
+  int32_t integrator;
+  int32_t decimation;         /* 3 */
+  int32_t max_episode_length; /* ceil(episode_length_s / step_dt) */
+  float sim_dt;               /* 0.01 */
+  float step_dt;              /* sim_dt * decimation */
+  float episode_length_s;     /* 6.0 */
+  float gravity;              /* 9.81 */
+  /* vehicle */
+  float mass;        /* nominal (USD) mass: ASSUMPTION 0.6 kg, the USD is not in the reference */
+  float inertia[3];  /* diag(0.0015, 0.002, 0.004) diff_action.py:59 */
+  float arm_length;  /* 0.09 */
+  float kappa;       /* 0.016 */
+  float motor_tau;   /* 1e-4 */
+  float motor_omega[2];
+  float thrustmap[3];
+  float max_thrust_weight_ratio; /* 3 */
+  float body_rate_bound;         /* 6 */
+  float rate_gain_p[3];
+  float rate_gain_d[3];
+  float thrust_ctrl_delay;
+  float torque_ctrl_delay[3];
+  int32_t use_motor_model;
+  int32_t action_lag; /* 0 or 1 */
+  /* drag, dynamics.yaml */
+  float drag1[3];
+  float drag1_rand;
+  float drag2[3];
+  float drag2_rand;
+  float z_drag;
+  float z_drag_rand;
+  int32_t random_drag;
+  /* startup domain randomisation (EventCfg) */
+  float mass_add_range[2];
+  float inertia_scale_range[2];
+  float pid_scale_range[2];
+  float delay_scale_range[2];
+  int32_t dr_startup; /* apply the startup events */
+  int32_t dr_plant;   /* integrate with the randomised plant mass/inertia (PhysX role) */
+  /* reset (reset_root_state_racing) */
+  float spawn_pos[3];       /* default root pos (0,0,0.5) */
+  float reset_pos_half[3];  /* U(-h, h) */
+  float reset_att_half[3];  /* roll, pitch, yaw offset */
+  float reset_vel_half[6];
+  /* command (RacingCommandCfg) */
+  float gate_threshold; /* 0.35 */
+  float gate_noise_pos[3]; /* half ranges */
+  int32_t add_gate_noise;
+  /* curriculum */
+  int32_t level_up_threshold;   /* 3 */
+  int32_t level_down_threshold; /* 2 */
+  int32_t noise_curriculum;     /* stage 1 */
+  int32_t noise_enhance_threshold; /* 4 */
+  int32_t noise_decay_threshold;   /* 3 */
+  float noise_enhance;  /* 0.02 */
+  float noise_decay;    /* 0.03 */
+  /* observation noise */
+  int32_t obs_noise;
+  float obs_lin_vel_noise; /* 0.03 */
+  float obs_att_noise;     /* 0.05 */
+  /* reward weights in RewardsCfg order (0 disables a term) */
+  float w_progress, w_body_rate, w_action_rate, w_collision, w_perception, w_success, w_bad_pose;
+  /* collision body: lattice half extents (0.707*0.09, 0.707*0.09, 0.5*0.05) */
+  float collider_half[3];
+  int32_t collision_count_threshold; /* contact if #lattice points inside > this (stage1: 0, stage0: 2) */
+  float out_of_bound[2];             /* stage 0 world-z bounds (0, 10) */
+  int32_t term_contact;  /* base_contact / outofbound termination enabled */
+  int32_t term_bad_pose;
+  int32_t reserved[8];
+} gr_config;
+
+/*
+ * Output buffers are written by every call; callers that keep the previous
+ * call's tensors alive (rsl_rl stores `obs` from step t while step t+1 runs)
+ * rebind a second output set each call and point the prev_* fields at the
+ * set written last (ping-pong).  prev_* may alias the outputs.
+ */
+typedef struct gr_buffers {
+  float* state;        /* [GR_NUM_PLANES][num_envs][4] */
+  int32_t* istate;     /* [num_envs][4] */
+  float* obs_policy;   /* [num_envs][16] */
+  float* obs_critic;   /* [num_envs][16] */
+  float* obs_aux;      /* [num_envs] */
+  float* reward;       /* [num_envs] */
+  uint8_t* terminated; /* [num_envs] (bool) */
+  uint8_t* time_out;   /* [num_envs] (bool) */
+  int64_t* dones;      /* [num_envs] */
+  const float* prev_obs_critic; /* last action (cols 12-15) carried by gr_reset/gr_observe */
+  const float* prev_obs_aux;
+  const uint8_t* prev_time_out;
+  float* log_partial;    /* [gr_num_blocks()][GR_LOG_SLOTS] scratch */
+  float* log_out;        /* [GR_LOG_SLOTS] */
+  const float* log_prev; /* previous log_out: kept when no env reset (the reference keeps the stale dict) */
+  uint32_t* counters;    /* [4]: [0] observation-noise call counter */
+} gr_buffers;
+
+typedef struct gr_ctx gr_ctx;
+
+int gr_abi_version(void);
+int gr_config_default(gr_config* cfg);
+size_t gr_config_size(void);
+int gr_create(const gr_config* cfg, gr_ctx** out);
+int gr_destroy(gr_ctx* ctx);
+const char* gr_last_error(const gr_ctx* ctx);
+/* number of workgroups of the step kernel (rows of log_partial) */
+int gr_num_blocks(const gr_ctx* ctx);
+/* algorithmic HBM bytes per env-step of the fused step kernel (read, written) */
+int gr_bytes_per_env_step(const gr_ctx* ctx, int64_t* read_bytes, int64_t* written_bytes);
+
+/* Track table on the device (caller-owned):
+ *   gates  [num_types*num_levels][max_gates][GR_GATE_FLOATS] fp32
+ *   tracks [num_types*num_levels][GR_TRACK_FLOATS] fp32
+ * track index = type * num_levels + level (the reference stores gate_pose as
+ * [col=type][row=level], terrain_importer.py:150-153). */
+int gr_bind_tracks(gr_ctx* ctx, const float* gates, const float* tracks);
+int gr_bind_buffers(gr_ctx* ctx, const gr_buffers* bufs);
+
+/* startup: nominal state, startup DR (gains/delays/mass/inertia), initial levels */
+int gr_init(gr_ctx* ctx, void* stream);
+/* reset envs whose mask byte is non-zero (mask == NULL: all), then observe all */
+int gr_reset(gr_ctx* ctx, const uint8_t* mask, void* stream);
+/* one policy step: actions [num_envs][4] fp32 pre-tanh, device memory */
+int gr_step(gr_ctx* ctx, const float* actions, void* stream);
+/* recompute observations (fresh observation noise), no state change */
+int gr_observe(gr_ctx* ctx, void* stream);
+
+/* In-library HIP-event timing of the fused step kernel alone (not the log
+ * finalize): when enabled, gr_step brackets the env kernel with a pair of
+ * events on the caller's stream (ring of 4096 pairs; do not capture into a
+ * graph while enabled).  gr_read_timing synchronises, sums the elapsed times
+ * of the recorded launches and clears the ring. */
+int gr_set_timing(gr_ctx* ctx, int enable);
+int gr_read_timing(gr_ctx* ctx, double* total_ms, int64_t* launches);
+
+/* Standalone controller + integrator on n envs, for parity against the
+ * reference's DroneDynamics / CTBRController golden vectors.
+ *   state_in/out [n][13] p(3) q(4) v_w(3) w_b(3)  (DroneDynamics keeps w in the body frame)
+ *   ang_acc_b [n][3] controller D-term input
+ *   cmd [n][4] scaled CTBR command (mode 0) or (thrust, torque) (mode 1)
+ *   ctrl_in/out [n][4] CTBR filter state (T, tau)
+ *   par [n][16] = PAR0..PAR3 planes of one env (Kp3 cT Kd3 m_plant ctau3 m_ctrl J3 pad)
+ *   drag [n][6] k2(3) k1(3)
+ *   extra_out [n][9] = DD.step linear acceleration a(3), angular acceleration alpha(3), w_world(3)
+ *   mode: 0 CTBR controller then integrator ; 1 integrator only */
+int gr_test_dynamics(gr_ctx* ctx, int n, int mode, const float* state_in, const float* ang_acc_b,
+                     const float* cmd, const float* ctrl_in, const float* par, const float* drag,
+                     float* state_out, float* ctrl_out, float* extra_out, void* stream);
+/* Elementwise portable math on the device (parity of gr_math.h host vs device).
+ * fn: 0 exp 1 tanh 2 log 3 sin 4 cos 5 atan2(x, y2) 6 sqrt 7 div(x/y2) */
+int gr_test_math(gr_ctx* ctx, int fn, int n, const float* x, const float* y2, float* out, void* stream);
+/* Philox words for counters (c0+i, c1, c2, c3), key = ctx seed */
+int gr_test_philox(gr_ctx* ctx, int n, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t* out4,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GR_H */

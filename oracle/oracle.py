@@ -1,0 +1,205 @@
+"""ctypes front-end of the CPU oracle (oracle/gr_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg — never by the generalizableracing_amd package.
+Also converts between the oracle's array-of-structs env records and the HIP
+kernel's struct-of-float4-planes state so both can be driven from one state.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "liboracle.so")
+
+_F = np.float32
+_I = np.int32
+ENV_DTYPE = np.dtype([
+    ("p", _F, 3), ("q", _F, 4), ("v", _F, 3), ("w", _F, 3), ("alpha", _F, 3), ("T", _F), ("tau", _F, 3),
+    ("lag", _F, 4), ("thr_err", _F), ("noise_level", _F), ("k2", _F, 3), ("k1", _F, 3), ("ep_sum", _F, 7),
+    ("m_actrate", _F), ("Kp", _F, 3), ("cT", _F), ("Kd", _F, 3), ("m_plant", _F), ("ctau", _F, 3),
+    ("m_ctrl", _F), ("J", _F, 3), ("motor_w", _F, 4),
+    ("ep_len", _I), ("acc", _I), ("epoch", _I), ("gate_id", _I), ("level", _I), ("type", _I), ("azero", _I),
+])
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        lib = C.CDLL(LIB)
+        vp = C.c_void_p
+        lib.gro_env_size.restype = C.c_size_t
+        for name, args in {
+            "gro_type_starts": [vp, vp],
+            "gro_init": [vp, vp, C.c_int, vp],
+            "gro_reset": [vp, vp, C.c_int, vp, vp, vp, vp],
+            "gro_step": [vp, vp, C.c_int, vp, vp, vp, vp],
+            "gro_observe": [vp, vp, C.c_int, vp, vp, vp],
+            "gro_test_dynamics": [vp, C.c_int, C.c_int] + [vp] * 9,
+            "gro_test_math": [C.c_int, C.c_int, vp, vp, vp],
+            "gro_test_philox": [C.c_int] + [C.c_uint32] * 6 + [vp],
+        }.items():
+            f = getattr(lib, name)
+            f.restype = None
+            f.argtypes = args
+        lib.gro_collision_count.restype = C.c_int
+        lib.gro_collision_count.argtypes = [vp, vp, C.c_int, vp, vp]
+        if lib.gro_env_size() != ENV_DTYPE.itemsize:
+            raise RuntimeError(f"gro_env size {lib.gro_env_size()} != numpy {ENV_DTYPE.itemsize}")
+        _lib = lib
+    return _lib
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class GroOut(C.Structure):
+    _fields_ = [("obs_policy", C.c_void_p), ("obs_critic", C.c_void_p), ("obs_aux", C.c_void_p),
+                ("reward", C.c_void_p), ("terminated", C.c_void_p), ("time_out", C.c_void_p),
+                ("dones", C.c_void_p), ("log_out", C.c_void_p)]
+
+
+class GroTracks(C.Structure):
+    _fields_ = [("gates", C.c_void_p), ("tracks", C.c_void_p)]
+
+
+class Oracle:
+    """Stateful CPU env mirroring the device env (same config struct, same track table)."""
+
+    def __init__(self, cfg, gates: np.ndarray, recs: np.ndarray):
+        self.lib = load()
+        self.cfg = cfg  # generalizableracing_amd._abi.GrConfig (plain ctypes struct)
+        n = cfg.num_envs
+        self.n = n
+        self.gates = np.ascontiguousarray(gates, dtype=np.float32)
+        self.recs = np.ascontiguousarray(recs, dtype=np.float32)
+        self.tracks = GroTracks(_p(self.gates), _p(self.recs))
+        self.envs = np.zeros(n, dtype=ENV_DTYPE)
+        self.obs_policy = np.zeros((n, 16), np.float32)
+        self.obs_critic = np.zeros((n, 16), np.float32)
+        self.obs_aux = np.zeros(n, np.float32)
+        self.reward = np.zeros(n, np.float32)
+        self.terminated = np.zeros(n, np.uint8)
+        self.time_out = np.zeros(n, np.uint8)
+        self.dones = np.zeros(n, np.int64)
+        self.log = np.zeros(20, np.float32)
+        self.counter = np.zeros(1, np.uint32)
+        self.out = GroOut(_p(self.obs_policy), _p(self.obs_critic), _p(self.obs_aux), _p(self.reward),
+                          _p(self.terminated), _p(self.time_out), _p(self.dones), _p(self.log))
+
+    def init(self):
+        self.lib.gro_init(C.byref(self.cfg), _p(self.envs), self.n, C.byref(self.out))
+        self.counter[0] = 0
+
+    def reset(self, mask: np.ndarray | None = None):
+        mp = None if mask is None else _p(np.ascontiguousarray(mask, dtype=np.uint8))
+        self.lib.gro_reset(C.byref(self.cfg), _p(self.envs), self.n, mp, C.byref(self.tracks), _p(self.counter),
+                           C.byref(self.out))
+
+    def step(self, actions: np.ndarray):
+        a = np.ascontiguousarray(actions, dtype=np.float32)
+        self.lib.gro_step(C.byref(self.cfg), _p(self.envs), self.n, _p(a), C.byref(self.tracks), _p(self.counter),
+                          C.byref(self.out))
+
+    def observe(self):
+        self.lib.gro_observe(C.byref(self.cfg), _p(self.envs), self.n, C.byref(self.tracks), _p(self.counter),
+                             C.byref(self.out))
+
+    def collision_count(self, track: int, p, q) -> int:
+        p = np.ascontiguousarray(p, dtype=np.float32)
+        q = np.ascontiguousarray(q, dtype=np.float32)
+        return self.lib.gro_collision_count(C.byref(self.cfg), C.byref(self.tracks), track, _p(p), _p(q))
+
+
+def test_dynamics(cfg, mode, state_in, ab, cmd, ctrl_in, par, drag):
+    lib = load()
+    n = state_in.shape[0]
+    arrs = [np.ascontiguousarray(x, dtype=np.float32) for x in (state_in, ab, cmd, ctrl_in, par, drag)]
+    so = np.zeros((n, 13), np.float32)
+    co = np.zeros((n, 4), np.float32)
+    xo = np.zeros((n, 9), np.float32)
+    lib.gro_test_dynamics(C.byref(cfg), n, mode, *[_p(a) for a in arrs], _p(so), _p(co), _p(xo))
+    return so, co, xo
+
+
+def test_math(fn, x, y=None):
+    lib = load()
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.ascontiguousarray(np.ones_like(x) if y is None else y, dtype=np.float32)
+    out = np.zeros_like(x)
+    lib.gro_test_math(fn, x.size, _p(x), _p(y), _p(out))
+    return out
+
+
+def test_philox(n, c0, c1, c2, c3, k0, k1):
+    lib = load()
+    out = np.zeros((n, 4), np.uint32)
+    lib.gro_test_philox(n, c0, c1, c2, c3, k0, k1, _p(out))
+    return out
+
+
+def type_starts(cfg):
+    lib = load()
+    out = np.zeros(cfg.num_types + 1, np.int32)
+    lib.gro_type_starts(C.byref(cfg), _p(out))
+    return out
+
+
+# ---------------------------------------------------------------- layout bridge
+# kernel planes (include/gr.h GR_P_*) <-> oracle records
+_PLANE_MAP = [  # (plane, comp) for each float of the kernel state, in ENV_DTYPE field order
+    ("p", [(0, 0), (0, 1), (0, 2)]), ("q", [(0, 3), (1, 0), (1, 1), (1, 2)]), ("v", [(1, 3), (2, 0), (2, 1)]),
+    ("w", [(2, 2), (2, 3), (3, 0)]), ("alpha", [(3, 1), (3, 2), (3, 3)]), ("T", [(4, 0)]),
+    ("tau", [(4, 1), (4, 2), (4, 3)]), ("lag", [(5, 0), (5, 1), (5, 2), (5, 3)]), ("thr_err", [(6, 0)]),
+    ("noise_level", [(6, 1)]), ("k2", [(6, 2), (6, 3), (7, 0)]), ("k1", [(7, 1), (7, 2), (7, 3)]),
+    ("ep_sum", [(8, 0), (8, 1), (8, 2), (8, 3), (9, 0), (9, 1), (9, 2)]), ("m_actrate", [(9, 3)]),
+    ("Kp", [(10, 0), (10, 1), (10, 2)]), ("cT", [(10, 3)]), ("Kd", [(11, 0), (11, 1), (11, 2)]),
+    ("m_plant", [(11, 3)]), ("ctau", [(12, 0), (12, 1), (12, 2)]), ("m_ctrl", [(12, 3)]),
+    ("J", [(13, 0), (13, 1), (13, 2)]), ("motor_w", [(14, 0), (14, 1), (14, 2), (14, 3)]),
+]
+
+
+def planes_to_envs(state: np.ndarray, istate: np.ndarray) -> np.ndarray:
+    n = state.shape[1]
+    envs = np.zeros(n, dtype=ENV_DTYPE)
+    for name, comps in _PLANE_MAP:
+        vals = np.stack([state[p, :, c] for p, c in comps], axis=1)
+        envs[name] = vals if len(comps) > 1 else vals[:, 0]
+    envs["ep_len"] = istate[:, 0]
+    envs["acc"] = istate[:, 1]
+    envs["epoch"] = istate[:, 2]
+    packed = istate[:, 3]
+    envs["gate_id"] = packed & 0xFF
+    envs["level"] = (packed >> 8) & 0xFF
+    envs["azero"] = (packed >> 16) & 1
+    envs["type"] = (packed >> 24) & 0xFF
+    return envs
+
+
+def envs_to_planes(envs: np.ndarray, num_planes: int = 15):
+    n = envs.shape[0]
+    state = np.zeros((num_planes, n, 4), np.float32)
+    for name, comps in _PLANE_MAP:
+        vals = envs[name].reshape(n, -1)
+        for j, (p, c) in enumerate(comps):
+            state[p, :, c] = vals[:, j]
+    istate = np.zeros((n, 4), np.int32)
+    istate[:, 0] = envs["ep_len"]
+    istate[:, 1] = envs["acc"]
+    istate[:, 2] = envs["epoch"]
+    istate[:, 3] = (envs["gate_id"] & 0xFF) | ((envs["level"] & 0xFF) << 8) | ((envs["azero"] & 1) << 16) | \
+        ((envs["type"] & 0xFF) << 24)
+    return state, istate

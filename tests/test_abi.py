@@ -1,0 +1,69 @@
+"""C-ABI surface of libgr.so: loads, exports every symbol include/gr.h declares,
+config struct layout matches the ctypes mirror.  No device compute here."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from generalizableracing_amd import _abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "gr.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gr_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_header_declares_all_exports():
+    assert declared_symbols() == sorted(_abi.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _abi.load()
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+
+
+def test_config_layout_and_defaults():
+    lib = _abi.load()
+    assert lib.gr_config_size() == C.sizeof(_abi.GrConfig)
+    assert lib.gr_abi_version() == _abi.GR_ABI_VERSION
+    c = _abi.default_config()
+    assert c.num_envs == 2048 and c.num_types == 20 and c.num_levels == 10 and c.max_gates == 8
+    assert c.max_episode_length == 200  # ceil(6.0 / 0.03)
+    assert abs(c.step_dt - 0.03) < 1e-9 and c.decimation == 3
+    assert list(c.rate_gain_p) == [35.0] * 3
+    assert c.w_collision == -100.0 and c.w_success == 20.0 and c.w_bad_pose == -30.0
+
+
+def test_create_destroy_and_bytes():
+    lib = _abi.load()
+    c = _abi.default_config()
+    c.num_envs = 65536
+    ctx = C.c_void_p()
+    assert lib.gr_create(C.byref(c), C.byref(ctx)) == 0
+    assert lib.gr_num_blocks(ctx) == 256
+    r, w = C.c_int64(), C.c_int64()
+    assert lib.gr_bytes_per_env_step(ctx, C.byref(r), C.byref(w)) == 0
+    assert r.value == 256 and w.value == 290
+    # calls before binding fail loudly with a message, never crash
+    assert lib.gr_step(ctx, None, None) != 0
+    assert b"bound" in lib.gr_last_error(ctx)
+    assert lib.gr_destroy(ctx) == 0
+
+
+@pytest.mark.parametrize("field,value", [("num_envs", 0), ("num_types", 65), ("action_lag", 2), ("integrator", 7)])
+def test_create_rejects_bad_config(field, value):
+    lib = _abi.load()
+    c = _abi.default_config()
+    setattr(c, field, value)
+    ctx = C.c_void_p()
+    assert lib.gr_create(C.byref(c), C.byref(ctx)) == _abi.__dict__.get("GR_ERR_ARG", -1)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        _abi.load(str(tmp_path / "libgr.so"))
