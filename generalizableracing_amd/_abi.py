@@ -47,7 +47,7 @@ STATE_FIELDS = {
     "ang_vel_b": [(P_VW, 2, 2), (P_WA, 0, 1)],
     "ang_acc_b": [(P_WA, 1, 3)],
     "ctrl": [(P_CTRL, 0, 4)],
-    "lag": [(P_LAG, 0, 4)],
+    "lag": [(P_LAG, 0, 4)],  # tanh(previous raw action): the lag buffer, squashed once
     "thr_est_error": [(P_RST0, 0, 1)],
     "noise_level": [(P_RST0, 1, 1)],
     "drag2": [(P_RST0, 2, 2), (P_RST1, 0, 1)],
@@ -166,15 +166,15 @@ class GrBuffers(C.Structure):
         ("prev_obs_aux", C.c_void_p),
         ("prev_time_out", C.c_void_p),
         ("log_partial", C.c_void_p),
-        ("log_out", C.c_void_p),
-        ("log_prev", C.c_void_p),
         ("counters", C.c_void_p),
+        ("counter_index", C.c_int32),
+        ("reserved", C.c_int32),
     ]
 
 
 EXPORTS = [
     "gr_abi_version", "gr_config_default", "gr_config_size", "gr_create", "gr_destroy", "gr_last_error",
-    "gr_num_blocks", "gr_bytes_per_env_step", "gr_bind_tracks", "gr_bind_buffers", "gr_init", "gr_reset",
+    "gr_num_blocks", "gr_num_log_rows", "gr_log_finalize", "gr_bytes_per_env_step", "gr_bind_tracks", "gr_bind_buffers", "gr_init", "gr_reset",
     "gr_step", "gr_observe", "gr_set_timing", "gr_read_timing", "gr_test_dynamics", "gr_test_math",
     "gr_test_philox",
 ]
@@ -192,6 +192,8 @@ def _declare(lib):
         "gr_destroy": (C.c_int, [vp]),
         "gr_last_error": (C.c_char_p, [vp]),
         "gr_num_blocks": (C.c_int, [vp]),
+        "gr_num_log_rows": (C.c_int, [vp]),
+        "gr_log_finalize": (C.c_int, [vp, vp, vp, vp, vp]),
         "gr_bytes_per_env_step": (C.c_int, [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
         "gr_bind_tracks": (C.c_int, [vp, vp, vp]),
         "gr_bind_buffers": (C.c_int, [vp, C.POINTER(GrBuffers)]),

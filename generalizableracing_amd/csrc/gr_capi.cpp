@@ -211,6 +211,14 @@ int gr_destroy(gr_ctx* c) {
 const char* gr_last_error(const gr_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 int gr_num_blocks(const gr_ctx* c) { return c ? (c->cfg.num_envs + GR_BLOCK - 1) / GR_BLOCK : GR_ERR_ARG; }
+int gr_num_log_rows(const gr_ctx* c) { return c ? gr_num_blocks(c) * (GR_BLOCK / 64) : GR_ERR_ARG; }
+
+int gr_log_finalize(gr_ctx* c, const float* rows, const float* prev, float* out, void* stream) {
+  if (!c || !rows || !out) return GR_ERR_ARG;
+  hipError_t e = gr::launch_log_finalize(rows, gr_num_log_rows(c), prev, out, c->cfg.episode_length_s,
+                                         (float)c->cfg.num_envs, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : hip_fail(c, e, "gr_log_finalize");
+}
 
 int gr_bytes_per_env_step(const gr_ctx* c, int64_t* rd, int64_t* wr) {
   if (!c || !rd || !wr) return GR_ERR_ARG;
@@ -259,7 +267,10 @@ int gr_bind_buffers(gr_ctx* c, const gr_buffers* b) {
   if (!c || !b) return fail(c, GR_ERR_ARG, "gr_bind_buffers: null pointer");
   const void* ptrs[] = {b->state,      b->istate,          b->obs_policy,   b->obs_critic,    b->obs_aux,
                         b->reward,     b->terminated,      b->time_out,     b->dones,         b->prev_obs_critic,
-                        b->prev_obs_aux, b->prev_time_out, b->log_partial,  b->log_out,       b->counters};
+                        b->prev_obs_aux, b->prev_time_out, b->log_partial,  b->counters};
+  if (b->counter_index != 0 && b->counter_index != 1)
+    return fail(c, GR_ERR_ARG, "gr_bind_buffers: counter_index must be 0 or 1");
+  if (!aligned16(b->log_partial)) return fail(c, GR_ERR_ARG, "gr_bind_buffers: log_partial must be 16-byte aligned");
   for (const void* p : ptrs)
     if (!p) return fail(c, GR_ERR_ARG, "gr_bind_buffers: null buffer");
   if (!aligned16(b->state) || !aligned16(b->istate) || !aligned16(b->obs_policy) || !aligned16(b->obs_critic) ||
@@ -283,7 +294,7 @@ int gr_init(gr_ctx* c, void* stream) {
   if (r) return r;
   hipError_t e = gr::launch_init(c->args, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(c, e, "gr_init");
-  e = hipMemsetAsync(c->buf.counters, 0, 4 * sizeof(uint32_t), (hipStream_t)stream);
+  e = hipMemsetAsync(c->buf.counters, 0, 2 * sizeof(uint32_t), (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(c, e, "gr_init: counters");
   return GR_OK;
 }

@@ -32,6 +32,8 @@ struct KArgs {
 hipError_t launch_env(int mode, const KArgs& a, const float* actions, const uint8_t* mask, hipStream_t s,
                       hipEvent_t t0, hipEvent_t t1);
 hipError_t launch_init(const KArgs& a, hipStream_t s);
+hipError_t launch_log_finalize(const float* rows, int nrows, const float* prev, float* out, float ep_len_s,
+                               float num_envs, hipStream_t s);
 hipError_t launch_test_dynamics(const KArgs& a, int n, int mode, const float* si, const float* ab, const float* cmd,
                                 const float* ci, const float* par, const float* drag, float* so, float* co, float* xo,
                                 hipStream_t s);

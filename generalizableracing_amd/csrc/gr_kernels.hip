@@ -387,7 +387,26 @@ DEV void gate_noise(const KArgs& a, const Env& e, uint32_t gid, int which, float
   }
 }
 
-DEV void write_obs(const KArgs& a, const Tab& tab, const Env& e, int i, uint32_t gid, uint32_t cnt,
+// Observation noise depends only on (env, call counter): drawn before the state
+// loads land, so its Philox / Box-Muller work hides under the load latency.
+struct ObsNoise {
+  float vfac[3];  // 1 + N(0,1) * 0.03        (observation.py:52)
+  float qn[4];    // quat_from_euler_xyz(N(0,1) * 0.05) (observation.py:27-28)
+};
+
+DEV void obs_noise(const KArgs& a, uint32_t gid, uint32_t cnt, ObsNoise& on) {
+  float nz[6] = {0, 0, 0, 0, 0, 0};
+  if (a.cfg.obs_noise) {
+    gr_u32x4 b0 = draw(a, gid, cnt, GR_TAG_OBS, 0), b1 = draw(a, gid, cnt, GR_TAG_OBS, 1);
+    gr_box_muller(b0.x, b0.y, &nz[0], &nz[1]);
+    gr_box_muller(b0.z, b0.w, &nz[2], &nz[3]);
+    gr_box_muller(b1.x, b1.y, &nz[4], &nz[5]);
+  }
+  for (int k = 0; k < 3; ++k) on.vfac[k] = 1.0f + nz[k] * a.cfg.obs_lin_vel_noise;
+  quat_from_euler_xyz(nz[3] * a.cfg.obs_att_noise, nz[4] * a.cfg.obs_att_noise, nz[5] * a.cfg.obs_att_noise, on.qn);
+}
+
+DEV void write_obs(const KArgs& a, const Tab& tab, const Env& e, int i, uint32_t gid, const ObsNoise& on,
                    const float lc[4], float aux) {
   const float* rec = tab.rec(e.type, e.lvl);
   int ng = (int)rec[3];
@@ -409,17 +428,8 @@ DEV void write_obs(const KArgs& a, const Tab& tab, const Env& e, int i, uint32_t
   C[1] = make_float4(r2[1], r2[2], cg[0], cg[1]);
   C[2] = make_float4(cg[2], cn[0], cn[1], cn[2]);
   C[3] = make_float4(lc[0], lc[1], lc[2], lc[3]);
-  float nz[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (a.cfg.obs_noise) {
-    gr_u32x4 b0 = draw(a, gid, cnt, GR_TAG_OBS, 0), b1 = draw(a, gid, cnt, GR_TAG_OBS, 1);
-    gr_box_muller(b0.x, b0.y, &nz[0], &nz[1]);
-    gr_box_muller(b0.z, b0.w, &nz[2], &nz[3]);
-    gr_box_muller(b1.x, b1.y, &nz[4], &nz[5]);
-    gr_box_muller(b1.z, b1.w, &nz[6], &nz[7]);
-  }
-  float qn[4], qq[4], r2n[3];
-  quat_from_euler_xyz(nz[3] * a.cfg.obs_att_noise, nz[4] * a.cfg.obs_att_noise, nz[5] * a.cfg.obs_att_noise, qn);
-  quat_mul(e.q, qn, qq);
+  float qq[4], r2n[3];
+  quat_mul(e.q, on.qn, qq);
   matrix_row2(qq, r2n);
   float ng0[3], ng1[3];
   gate_noise(a, e, gid, 0, ng0);
@@ -432,7 +442,7 @@ DEV void write_obs(const KArgs& a, const Tab& tab, const Env& e, int i, uint32_t
   quat_rotate_inverse(e.q, dp, pg);
   quat_rotate_inverse(e.q, dnp, pn);
   float vn[3];
-  for (int k = 0; k < 3; ++k) vn[k] = vb[k] * (1.0f + nz[k] * a.cfg.obs_lin_vel_noise);
+  for (int k = 0; k < 3; ++k) vn[k] = vb[k] * on.vfac[k];
   float4* P = reinterpret_cast<float4*>(a.buf.obs_policy) + (size_t)i * 4;
   P[0] = make_float4(vn[0], vn[1], vn[2], r2n[0]);
   P[1] = make_float4(r2n[1], r2n[2], pg[0], pg[1]);
@@ -442,22 +452,33 @@ DEV void write_obs(const KArgs& a, const Tab& tab, const Env& e, int i, uint32_t
 }
 
 // ------------------------------------------------------------- log reduction
-// Sum the GR_LOG_SLOTS values of the workgroup into log_partial[block][:].
-DEV void block_log(const KArgs& a, float* vals, float* lds_red, bool any) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int first = any ? 0 : GR_LOG_LEVEL;
-  for (int s = first; s < GR_LOG_SLOTS; ++s) {
-    float v = vals[s];
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    if (lane == 0) lds_red[wave * GR_LOG_SLOTS + s] = v;
+// Per-wave partial sums into log_partial[wave][GR_LOG_SLOTS] (no workgroup
+// barrier).  Resets are sparse (~1 % of envs per step): the reset slots are
+// accumulated over the set bits of the wave's reset ballot with wave-uniform
+// lane reads; only the two all-env sums (terrain level, noise level) use a
+// full butterfly.  Means are formed on demand from these rows.
+DEV void wave_log(const KArgs& a, const float lg[GR_LOG_SLOTS], bool reset_lane, float level, float noise) {
+  const int lane = threadIdx.x & 63;
+  float acc[GR_LOG_LEVEL];
+  for (int s = 0; s < GR_LOG_LEVEL; ++s) acc[s] = 0.0f;
+  uint64_t m = __ballot(reset_lane);
+  while (m) {
+    const int l = __builtin_ctzll(m);
+    m &= m - 1;
+    for (int s = 0; s < GR_LOG_LEVEL; ++s) acc[s] += __shfl(lg[s], l, 64);
   }
-  __syncthreads();
-  if (threadIdx.x < GR_LOG_SLOTS) {
-    int s = threadIdx.x;
-    float t = 0.0f;
-    if (s >= first)
-      for (int wv = 0; wv < GR_BLOCK / 64; ++wv) t += lds_red[wv * GR_LOG_SLOTS + s];
-    a.buf.log_partial[(size_t)blockIdx.x * GR_LOG_SLOTS + s] = t;
+  for (int off = 32; off > 0; off >>= 1) {
+    level += __shfl_xor(level, off, 64);
+    noise += __shfl_xor(noise, off, 64);
+  }
+  if (lane == 0) {
+    float4* row = reinterpret_cast<float4*>(a.buf.log_partial +
+                                            ((size_t)blockIdx.x * (GR_BLOCK / 64) + (threadIdx.x >> 6)) * GR_LOG_SLOTS);
+    row[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    row[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    row[2] = make_float4(acc[8], acc[9], acc[10], acc[11]);
+    row[3] = make_float4(acc[12], acc[13], acc[14], level);
+    row[4] = make_float4(noise, 0.0f, 0.0f, 0.0f);
   }
 }
 
@@ -466,22 +487,35 @@ template <int MODE, bool USE_LDS>
 __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const float* __restrict__ actions,
                                                         const uint8_t* __restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
-  __shared__ float lds_red[(GR_BLOCK / 64) * GR_LOG_SLOTS];
   const int n = a.cfg.num_envs;
   const int i = blockIdx.x * GR_BLOCK + threadIdx.x;
   const bool live = i < n;
+  const int ii = live ? i : n - 1;  // dead lanes mirror the last env (loads stay in bounds, no stores)
+  const gr_config& c = a.cfg;
+  const uint32_t gid = gid_of(a, ii);
 
-  // ---- stage the gate geometry of this workgroup's terrain types ----
+  // ---- 1. issue every HBM load of this lane first ----
+  Env e;
+  load_env(a, ii, e);
+  float4 act = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if (MODE == KMODE_STEP) act = reinterpret_cast<const float4*>(actions)[ii];
+  const uint32_t cnt = a.buf.counters[a.buf.counter_index];
+
+  // ---- 2. load-independent work: observation noise (Philox + Box-Muller) ----
+  ObsNoise on;
+  obs_noise(a, gid, cnt, on);
+
+  // ---- 3. stage the gate geometry of this workgroup's terrain types in LDS ----
   const int first_env = blockIdx.x * GR_BLOCK;
   const int last_env = min(first_env + GR_BLOCK, n) - 1;
   int t0 = 0, t1 = 0;
-  for (int t = 1; t < a.cfg.num_types; ++t) {
+  for (int t = 1; t < c.num_types; ++t) {
     t0 += first_env >= a.type_start[t];
     t1 += last_env >= a.type_start[t];
   }
   Tab tab;
-  tab.L = a.cfg.num_levels;
-  tab.G = a.cfg.max_gates;
+  tab.L = c.num_levels;
+  tab.G = c.max_gates;
   tab.stride = a.track_stride;
   tab.t0 = t0;
   if (USE_LDS) {
@@ -493,156 +527,157 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const float* __r
   } else {
     tab.base = a.table + (size_t)t0 * tab.L * tab.stride;
   }
+  // call counter for the observation-noise stream: double-buffered by call parity,
+  // so this write never races with the reads of the current launch
+  if (threadIdx.x == 0 && blockIdx.x == 0) a.buf.counters[a.buf.counter_index ^ 1] = cnt + 1u;
 
-  const uint32_t cnt = a.buf.counters[0];
   float lg[GR_LOG_SLOTS];
   for (int s = 0; s < GR_LOG_SLOTS; ++s) lg[s] = 0.0f;
-  bool any_reset = false;
+  bool reset_lane = false;
 
-  if (live) {
-    const gr_config& c = a.cfg;
-    const uint32_t gid = gid_of(a, i);
-    Env e;
-    load_env(a, i, e);
-    if (MODE == KMODE_STEP) {
-      const float4 act = reinterpret_cast<const float4*>(actions)[i];
-      const float dt = c.step_dt;
-      float lin_prev = norm3(e.v), ang_prev = norm3(e.w), mar_prev = e.mar;
-      float cur[4] = {act.x, act.y, act.z, act.w}, prev[4], raw[4];
-      for (int k = 0; k < 4; ++k) prev[k] = e.azero ? 0.0f : e.lag[k];
-      e.azero = 0;
-      for (int k = 0; k < 4; ++k) { raw[k] = c.action_lag ? e.lag[k] : cur[k]; e.lag[k] = cur[k]; }
-      float sc[4], of[4], cmd[4], th_raw[4];
-      action_scale(a, e.mc, sc, of);
-      for (int k = 0; k < 4; ++k) { th_raw[k] = gr_tanhf(raw[k]); cmd[k] = th_raw[k] * sc[k] + of[k]; }
-      cmd[0] = cmd[0] * e.thr;
-      float tt[4];
-      ctbr_compute(a, cmd, e.w, e.al, e.Kp, e.Kd, e.cT, e.ct, e.T, e.tau, e.mw, tt);
-      const float m = c.dr_plant ? e.mp : e.mc;
-      float Jp[3];
-      for (int k = 0; k < 3; ++k) Jp[k] = c.dr_plant ? e.J[k] : c.inertia[k];
-      float accl[3], al[3];
-      int ccount = 0;
-      if (c.integrator == GR_INTEGRATOR_DD_EXPLICIT) {
-        dd_explicit(m, Jp, e.k2, e.k1, tt, dt, c.gravity, e.p, e.q, e.v, e.w, accl, al);
-        ccount = collision_count(a, tab, e.type, e.lvl, e.p, e.q);
-      } else {
-        float vb[3], fb[3] = {0.0f, 0.0f, tt[0]};
-        quat_rotate_inverse(e.q, e.v, vb);
-        for (int k = 0; k < 3; ++k) fb[k] = (fb[k] - (e.k2[k] * vb[k]) * gr_fabsf(vb[k])) - e.k1[k] * vb[k];
-        for (int s = 0; s < c.decimation; ++s) {
-          si_substep(m, Jp, fb, tt + 1, c.sim_dt, c.gravity, e.p, e.q, e.v, e.w, accl, al);
-          int cc = collision_count(a, tab, e.type, e.lvl, e.p, e.q);
-          ccount = cc > ccount ? cc : ccount;
-        }
-      }
-      for (int k = 0; k < 3; ++k) e.al[k] = al[k];
-      e.ep += 1;
-      const int time_out = e.ep >= c.max_episode_length;
-      const int contact = ccount > c.collision_count_threshold;
-      const float* rec = tab.rec(e.type, e.lvl);
-      const float zw = e.p[2] + rec[1];
-      const int oob = (zw < c.out_of_bound[0]) | (zw > c.out_of_bound[1]);
-      const int bad = (1.0f - 2.0f * (e.q[1] * e.q[1] + e.q[2] * e.q[2])) < 0.0f;
-      const int c_term = c.stage == 0 ? oob : contact;
-      const int terminated = (c.term_contact && c_term) | (c.term_bad_pose && bad);
-      // rewards
-      const float* g = tab.gate(e.type, e.lvl, e.gate);
-      float vb[3], dg[3] = {g[0] - e.p[0], g[1] - e.p[1], g[2] - e.p[2]}, gb[3];
+  if (MODE == KMODE_STEP) {
+    const float dt = c.step_dt;
+    const float lin_prev = norm3(e.v), ang_prev = norm3(e.w), mar_prev = e.mar;
+    // DiffActionManager.process_action + one-step lag.  The lag plane holds the
+    // *squashed* previous action tanh(a_{t-1}): the reference only ever uses
+    // tanh() of the lagged / previous raw action, so each action is squashed once.
+    float th_cur[4], th_prev[4], th_raw[4];
+    th_cur[0] = gr_tanhf(act.x); th_cur[1] = gr_tanhf(act.y); th_cur[2] = gr_tanhf(act.z); th_cur[3] = gr_tanhf(act.w);
+    for (int k = 0; k < 4; ++k) {
+      th_prev[k] = e.azero ? 0.0f : e.lag[k];
+      th_raw[k] = c.action_lag ? e.lag[k] : th_cur[k];
+      e.lag[k] = th_cur[k];
+    }
+    e.azero = 0;
+    float sc[4], of[4], cmd[4];
+    action_scale(a, e.mc, sc, of);
+    for (int k = 0; k < 4; ++k) cmd[k] = th_raw[k] * sc[k] + of[k];
+    cmd[0] = cmd[0] * e.thr;
+    float tt[4];
+    ctbr_compute(a, cmd, e.w, e.al, e.Kp, e.Kd, e.cT, e.ct, e.T, e.tau, e.mw, tt);
+    const float m = c.dr_plant ? e.mp : e.mc;
+    float Jp[3];
+    for (int k = 0; k < 3; ++k) Jp[k] = c.dr_plant ? e.J[k] : c.inertia[k];
+    float accl[3], al[3];
+    int ccount = 0;
+    if (c.integrator == GR_INTEGRATOR_DD_EXPLICIT) {
+      dd_explicit(m, Jp, e.k2, e.k1, tt, dt, c.gravity, e.p, e.q, e.v, e.w, accl, al);
+      ccount = collision_count(a, tab, e.type, e.lvl, e.p, e.q);
+    } else {
+      float vb[3], fb[3] = {0.0f, 0.0f, tt[0]};
       quat_rotate_inverse(e.q, e.v, vb);
-      quat_rotate_inverse(e.q, dg, gb);
-      float f[7];
-      f[0] = cosine_similarity(vb, gb);
-      float th_cur[4], th_prev[4], br[3];
-      for (int k = 0; k < 4; ++k) { th_cur[k] = gr_tanhf(cur[k]); th_prev[k] = gr_tanhf(prev[k]); }
-      for (int k = 0; k < 3; ++k) br[k] = th_cur[k + 1] * sc[k + 1];
-      f[1] = norm3(br);
-      float sq[4];
-      for (int k = 0; k < 4; ++k) {
-        float dd = (th_cur[k] * sc[k] + of[k]) - (th_prev[k] * sc[k] + of[k]);
-        sq[k] = dd * dd;
+      for (int k = 0; k < 3; ++k) fb[k] = (fb[k] - (e.k2[k] * vb[k]) * gr_fabsf(vb[k])) - e.k1[k] * vb[k];
+      for (int s = 0; s < c.decimation; ++s) {
+        si_substep(m, Jp, fb, tt + 1, c.sim_dt, c.gravity, e.p, e.q, e.v, e.w, accl, al);
+        int cc = collision_count(a, tab, e.type, e.lvl, e.p, e.q);
+        ccount = cc > ccount ? cc : ccount;
       }
-      f[2] = ((sq[0] + sq[1]) + sq[2]) + sq[3];
-      f[3] = (float)contact;
-      float nb = gr_maxf(norm3(gb), 1e-12f);
-      float gh[3] = {gb[0] / nb, gb[1] / nb, gb[2] / nb}, fx[3] = {1.0f, 0.0f, 0.0f};
-      f[4] = cosine_similarity(gh, fx);
-      float dist = norm3(dg);
-      const int near_gate = dist < c.gate_threshold;
-      f[5] = (float)near_gate * (1.0f / (dist * dist + 1.0f));
-      f[6] = (float)bad;
-      float rew = 0.0f;
-      for (int k = 0; k < 7; ++k) {
-        const float wk = a.w[k];
-        if (wk == 0.0f) continue;
-        float v = (f[k] * wk) * dt;
-        rew = rew + v;
-        e.es[k] = e.es[k] + v;
-      }
+    }
+    for (int k = 0; k < 3; ++k) e.al[k] = al[k];
+    e.ep += 1;
+    const int time_out = e.ep >= c.max_episode_length;
+    const int contact = ccount > c.collision_count_threshold;
+    const float* rec = tab.rec(e.type, e.lvl);
+    const float zw = e.p[2] + rec[1];
+    const int oob = (zw < c.out_of_bound[0]) | (zw > c.out_of_bound[1]);
+    const int bad = (1.0f - 2.0f * (e.q[1] * e.q[1] + e.q[2] * e.q[2])) < 0.0f;
+    const int c_term = c.stage == 0 ? oob : contact;
+    const int terminated = (c.term_contact && c_term) | (c.term_bad_pose && bad);
+    // rewards (rewards.py:154-253), IL RewardManager: f * w * dt, declaration order
+    const float* g = tab.gate(e.type, e.lvl, e.gate);
+    float vb[3], dg[3] = {g[0] - e.p[0], g[1] - e.p[1], g[2] - e.p[2]}, gb[3];
+    quat_rotate_inverse(e.q, e.v, vb);
+    quat_rotate_inverse(e.q, dg, gb);
+    float f[7];
+    f[0] = cosine_similarity(vb, gb);
+    float br[3];
+    for (int k = 0; k < 3; ++k) br[k] = th_cur[k + 1] * sc[k + 1];
+    f[1] = norm3(br);
+    float sq[4];
+    for (int k = 0; k < 4; ++k) {
+      float dd = (th_cur[k] * sc[k] + of[k]) - (th_prev[k] * sc[k] + of[k]);
+      sq[k] = dd * dd;
+    }
+    f[2] = ((sq[0] + sq[1]) + sq[2]) + sq[3];
+    f[3] = (float)contact;
+    float nb = gr_maxf(norm3(gb), 1e-12f);
+    float gh[3] = {gb[0] / nb, gb[1] / nb, gb[2] / nb}, fx[3] = {1.0f, 0.0f, 0.0f};
+    f[4] = cosine_similarity(gh, fx);
+    float dist = norm3(dg);
+    const int near_gate = dist < c.gate_threshold;
+    f[5] = (float)near_gate * (1.0f / (dist * dist + 1.0f));
+    f[6] = (float)bad;
+    float rew = 0.0f;
+    for (int k = 0; k < 7; ++k) {
+      const float wk = a.w[k];
+      if (wk == 0.0f) continue;
+      float v = (f[k] * wk) * dt;
+      rew = rew + v;
+      e.es[k] = e.es[k] + v;
+    }
+    const float aux = near_gate ? 1.0f : 0.0f;
+    e.mar = f[2];
+    const int done = terminated | time_out;
+    if (live) {
       a.buf.reward[i] = rew;
-      const float aux = near_gate ? 1.0f : 0.0f;
-      e.mar = f[2];
-      const int done = terminated | time_out;
       a.buf.terminated[i] = (uint8_t)terminated;
       a.buf.time_out[i] = (uint8_t)time_out;
       a.buf.dones[i] = (int64_t)done;
-      if (done) {
-        any_reset = true;
-        lg[GR_LOG_NRESET] = 1.0f;
-        for (int k = 0; k < 7; ++k) lg[GR_LOG_EPSUM0 + k] = e.es[k];
-        lg[GR_LOG_ACC] = (float)e.acc;
-        lg[GR_LOG_M_ACTRATE] = mar_prev;
-        lg[GR_LOG_M_LINSPD] = lin_prev;
-        lg[GR_LOG_M_ANGSPD] = ang_prev;
-        lg[GR_LOG_T_TIMEOUT] = (float)time_out;
-        lg[GR_LOG_T_CONTACT] = (float)c_term;
-        lg[GR_LOG_T_BADPOSE] = (float)bad;
-        reset_env(a, tab, e, gid);
-      }
-      // command compute: _update_metrics + _update_command (commands.py:247-260, 308-350)
-      {
-        const float* gg = tab.gate(e.type, e.lvl, e.gate);
-        float dd[3] = {gg[0] - e.p[0], gg[1] - e.p[1], gg[2] - e.p[2]};
-        if (norm3(dd) < c.gate_threshold) {
-          const int ngt = (int)tab.rec(e.type, e.lvl)[3];
-          e.acc += 1;
-          e.gate = e.gate + 1;
-          if (e.gate >= ngt) e.gate -= ngt;
-        }
-      }
-      float lc[4];
-      for (int k = 0; k < 4; ++k) lc[k] = th_raw[k] * sc[k] + of[k];
-      lc[0] = lc[0] / e.mc;
-      write_obs(a, tab, e, i, gid, cnt, lc, aux);
-      store_env(a, i, e, done != 0, false);
-    } else {
-      // MODE_RESET / MODE_OBSERVE: last_ctbr and aux carry over from the previous observation
-      const float4 lcv = reinterpret_cast<const float4*>(a.buf.prev_obs_critic)[(size_t)i * 4 + 3];
-      float lc[4] = {lcv.x, lcv.y, lcv.z, lcv.w};
-      const float aux = a.buf.prev_obs_aux[i];
-      bool did = false;
-      if (MODE == KMODE_RESET && (mask == nullptr || mask[i])) {
-        did = true;
-        any_reset = true;
-        lg[GR_LOG_NRESET] = 1.0f;
-        for (int k = 0; k < 7; ++k) lg[GR_LOG_EPSUM0 + k] = e.es[k];
-        lg[GR_LOG_ACC] = (float)e.acc;
-        lg[GR_LOG_M_ACTRATE] = e.mar;
-        lg[GR_LOG_M_LINSPD] = norm3(e.v);
-        lg[GR_LOG_M_ANGSPD] = norm3(e.w);
-        lg[GR_LOG_T_TIMEOUT] = a.buf.prev_time_out[i] ? 1.0f : 0.0f;
-        reset_env(a, tab, e, gid);
-      }
-      write_obs(a, tab, e, i, gid, cnt, lc, aux);
-      if (did) store_env(a, i, e, true, false);
     }
-    lg[GR_LOG_LEVEL] = (float)e.lvl;
-    lg[GR_LOG_NOISE] = e.nl;
+    if (done && live) {
+      reset_lane = true;
+      for (int k = 0; k < 7; ++k) lg[GR_LOG_EPSUM0 + k] = e.es[k];
+      lg[GR_LOG_NRESET] = 1.0f;
+      lg[GR_LOG_ACC] = (float)e.acc;
+      lg[GR_LOG_M_ACTRATE] = mar_prev;
+      lg[GR_LOG_M_LINSPD] = lin_prev;
+      lg[GR_LOG_M_ANGSPD] = ang_prev;
+      lg[GR_LOG_T_TIMEOUT] = (float)time_out;
+      lg[GR_LOG_T_CONTACT] = (float)c_term;
+      lg[GR_LOG_T_BADPOSE] = (float)bad;
+      reset_env(a, tab, e, gid);
+    }
+    // command compute: _update_metrics + _update_command (commands.py:247-260, 308-350)
+    {
+      const float* gg = tab.gate(e.type, e.lvl, e.gate);
+      float dd[3] = {gg[0] - e.p[0], gg[1] - e.p[1], gg[2] - e.p[2]};
+      if (norm3(dd) < c.gate_threshold) {
+        const int ngt = (int)tab.rec(e.type, e.lvl)[3];
+        e.acc += 1;
+        e.gate = e.gate + 1;
+        if (e.gate >= ngt) e.gate -= ngt;
+      }
+    }
+    float lc[4];
+    for (int k = 0; k < 4; ++k) lc[k] = th_raw[k] * sc[k] + of[k];
+    lc[0] = lc[0] / e.mc;
+    if (live) {
+      write_obs(a, tab, e, i, gid, on, lc, aux);
+      store_env(a, i, e, done != 0, false);
+    }
+  } else {
+    // MODE_RESET / MODE_OBSERVE: last action and aux carry over from the previous observation
+    const float4 lcv = reinterpret_cast<const float4*>(a.buf.prev_obs_critic)[(size_t)ii * 4 + 3];
+    float lc[4] = {lcv.x, lcv.y, lcv.z, lcv.w};
+    const float aux = a.buf.prev_obs_aux[ii];
+    if (MODE == KMODE_RESET && live && (mask == nullptr || mask[i])) {
+      reset_lane = true;
+      lg[GR_LOG_NRESET] = 1.0f;
+      for (int k = 0; k < 7; ++k) lg[GR_LOG_EPSUM0 + k] = e.es[k];
+      lg[GR_LOG_ACC] = (float)e.acc;
+      lg[GR_LOG_M_ACTRATE] = e.mar;
+      lg[GR_LOG_M_LINSPD] = norm3(e.v);
+      lg[GR_LOG_M_ANGSPD] = norm3(e.w);
+      lg[GR_LOG_T_TIMEOUT] = a.buf.prev_time_out[i] ? 1.0f : 0.0f;
+      reset_env(a, tab, e, gid);
+    }
+    if (live) {
+      write_obs(a, tab, e, i, gid, on, lc, aux);
+      if (reset_lane) store_env(a, i, e, true, false);
+    }
   }
-  if (MODE != KMODE_OBSERVE) {
-    const bool any = __syncthreads_or(any_reset);
-    block_log(a, lg, lds_red, any);
-  }
+  // (observe calls reset nothing: their rows say so, and the finalized log repeats the previous one)
+  wave_log(a, lg, reset_lane, live ? (float)e.lvl : 0.0f, live ? e.nl : 0.0f);
 }
 
 // ------------------------------------------------------------- init (startup events)
@@ -716,40 +751,46 @@ __global__ __launch_bounds__(GR_BLOCK) void init_kernel(KArgs a) {
   a.buf.dones[i] = 0;
 }
 
-// ------------------------------------------------------------- finalize
-// One workgroup: sums log_partial over the step kernel's workgroups, turns sums
-// into the means IL's managers log (reward_manager / command / curriculum),
-// and advances the observation-noise call counter.
-__global__ __launch_bounds__(256) void finalize_kernel(KArgs a, int nblocks, int with_log) {
-  __shared__ float red[256];
-  if (with_log) {
-    for (int s = 0; s < GR_LOG_SLOTS; ++s) {
-      float t = 0.0f;
-      for (int b = threadIdx.x; b < nblocks; b += 256) t += a.buf.log_partial[(size_t)b * GR_LOG_SLOTS + s];
-      red[threadIdx.x] = t;
-      __syncthreads();
-      for (int off = 128; off > 0; off >>= 1) {
-        if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
-        __syncthreads();
-      }
-      if (threadIdx.x == 0) a.buf.log_out[s] = red[0];  // raw sums, converted below
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-      float* o = a.buf.log_out;
-      const float nr = o[GR_LOG_NRESET];
-      if (nr == 0.0f && a.buf.log_prev != nullptr) {
-        // no env reset this call: the reference leaves extras["log"] untouched (stale), keep it
-        for (int s = 0; s < GR_LOG_SLOTS; ++s) o[s] = a.buf.log_prev[s];
-      } else {
-        for (int k = 0; k < 7; ++k) o[GR_LOG_EPSUM0 + k] = o[GR_LOG_EPSUM0 + k] / nr / a.cfg.episode_length_s;
-        for (int k = GR_LOG_ACC; k <= GR_LOG_M_ANGSPD; ++k) o[k] = o[k] / nr;
-        o[GR_LOG_LEVEL] = o[GR_LOG_LEVEL] / (float)a.cfg.num_envs;
-        o[GR_LOG_NOISE] = o[GR_LOG_NOISE] / (float)a.cfg.num_envs;
-      }
-    }
+// ------------------------------------------------------------- log finalize (on demand)
+// Sums the per-wave rows of one call's log slab and forms the means Isaac Lab's
+// managers log (RewardManager.reset: episode sum / episode_length_s; command
+// metrics and curriculum: means; termination terms: counts).  No env reset in
+// that call -> the previous values are kept (the reference leaves extras["log"]
+// untouched).  One 256-thread workgroup, all loads issued before any reduction.
+__global__ __launch_bounds__(256) void log_finalize_kernel(const float* __restrict__ rows, int nrows,
+                                                           const float* __restrict__ prev, float* __restrict__ out,
+                                                           float ep_len_s, float num_envs) {
+  __shared__ float red[GR_LOG_SLOTS][8];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float acc[GR_LOG_SLOTS];
+  for (int s = 0; s < GR_LOG_SLOTS; ++s) acc[s] = 0.0f;
+  for (int r = threadIdx.x; r < nrows; r += 256) {
+    const float4* row = reinterpret_cast<const float4*>(rows + (size_t)r * GR_LOG_SLOTS);
+    float4 v0 = row[0], v1 = row[1], v2 = row[2], v3 = row[3], v4 = row[4];
+    float v[GR_LOG_SLOTS] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y,
+                             v2.z, v2.w, v3.x, v3.y, v3.z, v3.w, v4.x, v4.y, v4.z, v4.w};
+    for (int s = 0; s < GR_LOG_SLOTS; ++s) acc[s] += v[s];
   }
-  if (threadIdx.x == 0) a.buf.counters[0] = a.buf.counters[0] + 1u;
+  for (int s = 0; s < GR_LOG_SLOTS; ++s) {
+    float v = acc[s];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (lane == 0) red[s][wave] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t[GR_LOG_SLOTS];
+    for (int s = 0; s < GR_LOG_SLOTS; ++s) t[s] = ((red[s][0] + red[s][1]) + red[s][2]) + red[s][3];
+    const float nr = t[GR_LOG_NRESET];
+    if (nr == 0.0f && prev != nullptr) {
+      for (int s = 0; s < GR_LOG_SLOTS; ++s) out[s] = prev[s];
+      return;
+    }
+    for (int s = 0; s < GR_LOG_SLOTS; ++s) out[s] = t[s];
+    for (int k = 0; k < 7; ++k) out[GR_LOG_EPSUM0 + k] = t[GR_LOG_EPSUM0 + k] / nr / ep_len_s;
+    for (int k = GR_LOG_ACC; k <= GR_LOG_M_ANGSPD; ++k) out[k] = t[k] / nr;
+    out[GR_LOG_LEVEL] = t[GR_LOG_LEVEL] / num_envs;
+    out[GR_LOG_NOISE] = t[GR_LOG_NOISE] / num_envs;
+  }
 }
 
 // ------------------------------------------------------------- test kernels
@@ -827,11 +868,13 @@ hipError_t launch_env(int mode, const KArgs& a, const float* actions, const uint
   else if (mode == KMODE_RESET) err = launch_env_mode<KMODE_RESET>(a, actions, mask, s);
   else err = launch_env_mode<KMODE_OBSERVE>(a, actions, mask, s);
   if (err != hipSuccess) return err;
-  if (t1) {
-    err = hipEventRecord(t1, s);
-    if (err != hipSuccess) return err;
-  }
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, a, grid_of(a.cfg.num_envs), mode != KMODE_OBSERVE ? 1 : 0);
+  if (t1) err = hipEventRecord(t1, s);
+  return err;
+}
+
+hipError_t launch_log_finalize(const float* rows, int nrows, const float* prev, float* out, float ep_len_s,
+                               float num_envs, hipStream_t s) {
+  hipLaunchKernelGGL(log_finalize_kernel, dim3(1), dim3(256), 0, s, rows, nrows, prev, out, ep_len_s, num_envs);
   return hipGetLastError();
 }
 

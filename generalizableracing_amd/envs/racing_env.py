@@ -28,16 +28,39 @@ LOG_RING = 64
 
 
 class _EpisodeLog(Mapping):
-    """extras["log"]: lazily materialised 0-dim device tensors (no host sync)."""
+    """extras["log"] of one call: the kernel leaves per-wave partial sums in a
+    ring slot; the means Isaac Lab's managers log are formed on first access
+    (gr_log_finalize, one small launch, no host sync).  Valid for LOG_RING calls."""
 
-    __slots__ = ("_row", "_keys")
+    __slots__ = ("_env", "_k", "_vals", "_keys")
 
-    def __init__(self, row: torch.Tensor, keys: dict):
-        self._row = row
+    def __init__(self, env: "RacingEnv", k: int, keys: dict):
+        self._env = env
+        self._k = k
+        self._vals = None
         self._keys = keys
 
+    def values(self) -> torch.Tensor:  # type: ignore[override]
+        if self._vals is None:
+            env = self._env
+            if env._calls - self._k > LOG_RING:
+                raise RuntimeError("extras['log'] read more than LOG_RING calls after its step")
+            chain = [self]
+            prev = env._log_at(self._k - 1)
+            while prev is not None and prev._vals is None and len(chain) < LOG_RING:
+                chain.append(prev)
+                prev = env._log_at(prev._k - 1)
+            for lg in reversed(chain):
+                out = torch.empty(_abi.LOG_SLOTS, dtype=torch.float32, device=env.device)
+                pv = prev._vals.data_ptr() if prev is not None and prev._vals is not None else None
+                env._call("gr_log_finalize", env._log_slab[lg._k % LOG_RING].data_ptr(), pv, out.data_ptr(),
+                          env._stream())
+                lg._vals = out
+                prev = lg
+        return self._vals
+
     def __getitem__(self, k):
-        return self._row[self._keys[k]]
+        return self.values()[self._keys[k]]
 
     def __iter__(self):
         return iter(self._keys)
@@ -88,10 +111,10 @@ class RacingEnv:
         self.state = torch.zeros(_abi.NUM_PLANES, n, 4, dtype=torch.float32, device=dev)
         self.istate = torch.zeros(n, 4, dtype=torch.int32, device=dev)
         self._sets = [self._alloc_outputs(n, dev) for _ in range(2)]
-        self._nblocks = self._lib.gr_num_blocks(ctx)
-        self._log_partial = torch.zeros(self._nblocks, _abi.LOG_SLOTS, dtype=torch.float32, device=dev)
-        self._log_ring = torch.zeros(LOG_RING, _abi.LOG_SLOTS, dtype=torch.float32, device=dev)
-        self._counters = torch.zeros(4, dtype=torch.int32, device=dev)
+        self._nrows = self._lib.gr_num_log_rows(ctx)
+        self._log_slab = torch.zeros(LOG_RING, self._nrows, _abi.LOG_SLOTS, dtype=torch.float32, device=dev)
+        self._logs: list = [None] * LOG_RING
+        self._counters = torch.zeros(2, dtype=torch.int32, device=dev)
         self._calls = 0
         self._cur = 0  # index of the output set written by the last call
         self._bufs = [self._make_buffers(k) for k in range(LOG_RING)]
@@ -100,7 +123,7 @@ class RacingEnv:
         # startup (gr_init): nominal state, startup DR events, initial terrain levels
         self._bind(0)
         self._call("gr_init", self._stream())
-        self._calls, self._cur = 1, 1  # gr_init wrote output set 1
+        self._calls, self._cur = 1, 1  # gr_init wrote output set 1 (binding 0); counters zeroed
 
     # ------------------------------------------------------------------ plumbing
     @staticmethod
@@ -116,7 +139,8 @@ class RacingEnv:
         }
 
     def _make_buffers(self, k: int) -> _abi.GrBuffers:
-        """Buffers for call number k: outputs -> set (k+1)%2, previous -> set k%2, log ring slot k."""
+        """Buffers for call number k: outputs -> set (k+1)%2, previous -> set k%2, log slab k % LOG_RING,
+        observation-noise counter parity k % 2."""
         out, prev = self._sets[(k + 1) % 2], self._sets[k % 2]
         b = _abi.GrBuffers()
         b.state = self.state.data_ptr()
@@ -131,10 +155,9 @@ class RacingEnv:
         b.prev_obs_critic = prev["critic"].data_ptr()
         b.prev_obs_aux = prev["auxiliary"].data_ptr()
         b.prev_time_out = prev["time_out"].data_ptr()
-        b.log_partial = self._log_partial.data_ptr()
-        b.log_out = self._log_ring[(k + 1) % LOG_RING].data_ptr()
-        b.log_prev = self._log_ring[k % LOG_RING].data_ptr()
+        b.log_partial = self._log_slab[k % LOG_RING].data_ptr()
         b.counters = self._counters.data_ptr()
+        b.counter_index = k % 2
         return b
 
     def _bind(self, k: int):
@@ -149,12 +172,20 @@ class RacingEnv:
             raise RuntimeError(f"{name} failed (status {rc}): {self._lib.gr_last_error(self._ctx).decode()}")
 
     def _advance(self):
-        """Bind the next output set + log slot; returns the set that will be written."""
+        """Bind the next output set + log slab; returns (output set, extras["log"] of this call)."""
         k = self._calls
         self._bind(k)
         self._calls += 1
         self._cur = (k + 1) % 2
-        return self._sets[self._cur], self._log_ring[(k + 1) % LOG_RING]
+        lg = _EpisodeLog(self, k, self._log_keys)
+        self._logs[k % LOG_RING] = lg
+        return self._sets[self._cur], lg
+
+    def _log_at(self, k: int):
+        if k < 0:
+            return None
+        lg = self._logs[k % LOG_RING]
+        return lg if lg is not None and lg._k == k else None
 
     def _build_log_keys(self) -> dict:
         c = self.cfg
@@ -244,10 +275,10 @@ class RacingEnv:
         a = action
         if a.device != self.device or a.dtype != torch.float32 or not a.is_contiguous() or a.data_ptr() % 16:
             a = a.to(device=self.device, dtype=torch.float32).contiguous()
-        out, log_row = self._advance()
+        out, log = self._advance()
         self._call("gr_step", a.data_ptr(), self._stream())
         self.common_step_counter += 1
-        self.extras = {"log": _EpisodeLog(log_row, self._log_keys)}
+        self.extras = {"log": log}
         return self._obs_dict(out), out["reward"], out["terminated"], out["time_out"], self.extras
 
     def reset(self, seed: int | None = None, env_ids=None, options=None):
@@ -257,9 +288,9 @@ class RacingEnv:
             ids = torch.as_tensor(env_ids, device=self.device, dtype=torch.long)
             mask_t = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
             mask_t[ids] = 1
-        out, log_row = self._advance()
+        out, log = self._advance()
         self._call("gr_reset", mask_t.data_ptr() if mask_t is not None else None, self._stream())
-        self.extras = {"log": _EpisodeLog(log_row, self._log_keys)}
+        self.extras = {"log": log}
         return self._obs_dict(out), self.extras
 
     def observe(self) -> dict:

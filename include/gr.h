@@ -53,7 +53,7 @@ extern "C" {
 #define GR_P_VW 2     /* vwy vwz wbx wby        (w = body angular rate) */
 #define GR_P_WA 3     /* wbz abx aby abz        (a = last body angular acceleration) */
 #define GR_P_CTRL 4   /* T tx ty tz             (CTBR thrust/torque delay-filter state) */
-#define GR_P_LAG 5    /* action-lag buffer (previous raw action) */
+#define GR_P_LAG 5    /* action-lag buffer: tanh(previous raw action) (only its tanh is ever used) */
 #define GR_P_RST0 6   /* thr_est_err noise_level k2x k2y */
 #define GR_P_RST1 7   /* k2z k1x k1y k1z        (quadratic / linear drag) */
 #define GR_P_EP0 8    /* episode reward sums 0..3 */
@@ -192,10 +192,10 @@ typedef struct gr_buffers {
   const float* prev_obs_critic; /* last action (cols 12-15) carried by gr_reset/gr_observe */
   const float* prev_obs_aux;
   const uint8_t* prev_time_out;
-  float* log_partial;    /* [gr_num_blocks()][GR_LOG_SLOTS] scratch */
-  float* log_out;        /* [GR_LOG_SLOTS] */
-  const float* log_prev; /* previous log_out: kept when no env reset (the reference keeps the stale dict) */
-  uint32_t* counters;    /* [4]: [0] observation-noise call counter */
+  float* log_partial;    /* [gr_num_log_rows()][GR_LOG_SLOTS]: this call's per-wave log sums */
+  uint32_t* counters;    /* [2]: observation-noise call counter, double-buffered by call parity */
+  int32_t counter_index; /* 0/1: this call reads counters[i] and writes counters[i^1] = counters[i] + 1 */
+  int32_t reserved;
 } gr_buffers;
 
 typedef struct gr_ctx gr_ctx;
@@ -206,8 +206,13 @@ size_t gr_config_size(void);
 int gr_create(const gr_config* cfg, gr_ctx** out);
 int gr_destroy(gr_ctx* ctx);
 const char* gr_last_error(const gr_ctx* ctx);
-/* number of workgroups of the step kernel (rows of log_partial) */
+/* number of workgroups of the step kernel */
 int gr_num_blocks(const gr_ctx* ctx);
+/* rows of a call's log slab (one per wave) */
+int gr_num_log_rows(const gr_ctx* ctx);
+/* extras["log"] on demand: reduce one call's log slab into GR_LOG_SLOTS means
+ * (prev: the previous call's finalized values, kept when no env reset; may be NULL) */
+int gr_log_finalize(gr_ctx* ctx, const float* log_partial, const float* prev, float* out, void* stream);
 /* algorithmic HBM bytes per env-step of the fused step kernel (read, written) */
 int gr_bytes_per_env_step(const gr_ctx* ctx, int64_t* read_bytes, int64_t* written_bytes);
 

@@ -479,13 +479,12 @@ static void compute_obs(const gr_config* c, gro_env* e, uint32_t gid, uint32_t c
   for (int k = 0; k < 3; ++k) { cri[k] = vb[k]; cri[3 + k] = r2[k]; cri[6 + k] = cg[k]; cri[9 + k] = cn[k]; }
   for (int k = 0; k < 4; ++k) cri[12 + k] = last_ctbr[k];
   /* policy: observation.py:47-53 (lin vel noise), :22-32 (attitude noise), commands.py:208-221 (noisy gates) */
-  float nz[8] = {0};
-  if (c->obs_noise) {
+  float nz[6] = {0};
+  if (c->obs_noise) { /* randn(N,3) for the velocity and for the attitude noise */
     gr_u32x4 b0 = draw(c, gid, cnt, GR_TAG_OBS, 0), b1 = draw(c, gid, cnt, GR_TAG_OBS, 1);
     gr_box_muller(b0.x, b0.y, &nz[0], &nz[1]);
     gr_box_muller(b0.z, b0.w, &nz[2], &nz[3]);
     gr_box_muller(b1.x, b1.y, &nz[4], &nz[5]);
-    gr_box_muller(b1.z, b1.w, &nz[6], &nz[7]);
   }
   float qn[4], qq[4], r2n[3];
   quat_from_euler_xyz(nz[3] * c->obs_att_noise, nz[4] * c->obs_att_noise, nz[5] * c->obs_att_noise, qn);
@@ -579,16 +578,23 @@ void gro_step(const gr_config* c, gro_env* envs, int n, const float* actions, co
     uint32_t gid = gid_of(c, i);
     const float* a = actions + (size_t)i * 4;
     float lin_prev = norm3(e->v), ang_prev = norm3(e->w), mar_prev = e->m_actrate;
-    /* 1. DiffActionManager.process_action (action_manager.py:44-45) */
-    float prev[4], cur[4], raw[4];
-    for (int k = 0; k < 4; ++k) { prev[k] = e->azero ? 0.0f : e->lag[k]; cur[k] = a[k]; }
+    /* 1. DiffActionManager.process_action (action_manager.py:44-45): prev <- action <- a.
+     * 2. DiffActions.process_actions: one-step lag (diff_action.py:160-163).
+     * Every use of the lagged / previous raw action goes through tanh() (:174,
+     * rewards.py:194,201-202, observation.py:61), so the lag record stores
+     * tanh(a) and each action is squashed once (bit-identical values). */
+    float th_cur[4], th_prev[4], th_raw[4];
+    for (int k = 0; k < 4; ++k) th_cur[k] = gr_tanhf(a[k]);
+    for (int k = 0; k < 4; ++k) {
+      th_prev[k] = e->azero ? 0.0f : e->lag[k]; /* IL ActionManager.reset zeroes _action (tanh(0) = 0) */
+      th_raw[k] = c->action_lag ? e->lag[k] : th_cur[k];
+      e->lag[k] = th_cur[k];
+    }
     e->azero = 0;
-    /* 2. DiffActions.process_actions: one-step lag (diff_action.py:160-163) */
-    for (int k = 0; k < 4; ++k) { raw[k] = c->action_lag ? e->lag[k] : a[k]; e->lag[k] = a[k]; }
     /* tanh -> scale/offset -> thrust-estimate error (:174-176) */
-    float sc[4], of[4], cmd[4], th_raw[4];
+    float sc[4], of[4], cmd[4];
     action_scale(c, e->m_ctrl, sc, of);
-    for (int k = 0; k < 4; ++k) { th_raw[k] = gr_tanhf(raw[k]); cmd[k] = th_raw[k] * sc[k] + of[k]; }
+    for (int k = 0; k < 4; ++k) cmd[k] = th_raw[k] * sc[k] + of[k];
     cmd[0] = cmd[0] * e->thr_err;
     /* 3. controller (:182) with the state "read from sim" (:126-154) */
     float tt[4];
@@ -632,8 +638,7 @@ void gro_step(const gr_config* c, gro_env* envs, int n, const float* actions, co
     quat_rotate_inverse(e->q, dg, gb);
     float f[7];
     f[0] = cosine_similarity(vb, gb);
-    float th_cur[4], th_prev[4], br[3];
-    for (int k = 0; k < 4; ++k) { th_cur[k] = gr_tanhf(cur[k]); th_prev[k] = gr_tanhf(prev[k]); }
+    float br[3];
     for (int k = 0; k < 3; ++k) br[k] = th_cur[k + 1] * sc[k + 1];
     f[1] = norm3(br);
     float sq[4];

@@ -135,7 +135,7 @@ def test_full_size_teacher_forced_slices():
         torch.cuda.synchronize()
         pre = oracle.planes_to_envs(env.state[:, i0:i0 + m].cpu().numpy(), env.istate[i0:i0 + m].cpu().numpy())
         prev_crit = env.obs_buf["critic"][i0:i0 + m].cpu().numpy()
-        cnt = int(env._counters[0].item())
+        cnt = int(env._counters[env._calls % 2].item())
         env.step(torch.from_numpy(a).to(DEV))
         c = _abi.GrConfig.from_buffer_copy(base)
         c.num_envs = m
