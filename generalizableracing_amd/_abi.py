@@ -218,7 +218,7 @@ def load(path: str | None = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("GR_LIB_PATH") or LIB_PATH  # override: timing-only ablation builds
     if not os.path.exists(p):
         raise RuntimeError(
             f"libgr.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "

@@ -93,6 +93,9 @@ void derive(gr_ctx* c) {
   }
   const long bytes = (long)span * g.num_levels * a.track_stride * 4;
   a.lds_bytes = bytes <= 60 * 1024 ? (int)bytes : 0;  // beyond 60 KiB: read the (L2-resident) table directly
+#ifdef GR_ABL_NOLDS
+  a.lds_bytes = 0;
+#endif
 }
 
 }  // namespace

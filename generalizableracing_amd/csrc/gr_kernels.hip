@@ -172,29 +172,32 @@ DEV void action_scale(const KArgs& a, float m_ctrl, float sc[4], float of[4]) {
 }
 
 // ------------------------------------------------------------- collision
+// Lattice of the drone box (diff.lab/utils/__init__.py:19-37): offsets
+// (lx*hx, ly*hy, lz*hz) with l in {0, +-1, +-0.5}.  quat_rotate is linear, so a
+// lattice point is p + (lx*A + ly*B) + lz*C with A, B, C the rotated scaled body
+// axes (3 rotations instead of 17); in a gate frame M (rows of R_gate^T) the same
+// point is d_g + (lx*A_g + ly*B_g) + lz*C_g with d_g = M(p - c), A_g = M A, ...
+// Oracle and kernel evaluate exactly these expressions; the kernel adds
+// conservative culls (sphere, plane slab, outer box, hole) that can only skip
+// gates where no lattice point can be inside, so the count is unchanged.
 __constant__ float c_lattice[17][3] = {
     {0, 0, 0},          {1, 1, 1},         {1, -1, 1},        {-1, 1, 1},       {-1, -1, 1},     {1, 1, -1},
     {1, -1, -1},        {-1, 1, -1},       {-1, -1, -1},      {0.5f, 0.5f, 0.5f}, {0.5f, -0.5f, 0.5f},
     {-0.5f, 0.5f, 0.5f}, {-0.5f, -0.5f, 0.5f}, {0.5f, 0.5f, -0.5f}, {0.5f, -0.5f, -0.5f}, {-0.5f, 0.5f, -0.5f},
     {-0.5f, -0.5f, -0.5f}};
 
-DEV void lattice_point(const KArgs& a, int k, const float p[3], const float q[4], float pt[3]) {
-  float o[3] = {c_lattice[k][0] * a.cfg.collider_half[0], c_lattice[k][1] * a.cfg.collider_half[1],
-                c_lattice[k][2] * a.cfg.collider_half[2]};
-  float r[3];
-  quat_rotate(q, o, r);
-  pt[0] = p[0] + r[0]; pt[1] = p[1] + r[1]; pt[2] = p[2] + r[2];
+DEV void body_axes(const KArgs& a, const float q[4], float A[3], float B[3], float Cz[3]) {
+  const float ex[3] = {a.cfg.collider_half[0], 0.0f, 0.0f}, ey[3] = {0.0f, a.cfg.collider_half[1], 0.0f},
+              ez[3] = {0.0f, 0.0f, a.cfg.collider_half[2]};
+  quat_rotate(q, ex, A);
+  quat_rotate(q, ey, B);
+  quat_rotate(q, ez, Cz);
 }
 
-DEV bool point_in_gate(const float* g, const float pt[3]) {
-  float d0 = pt[0] - g[0], d1 = pt[1] - g[1], d2 = pt[2] - g[2];
-  float l0 = (g[4] * d0 + g[5] * d1) + g[6] * d2;
-  float l1 = (g[8] * d0 + g[9] * d1) + g[10] * d2;
-  float l2 = (g[12] * d0 + g[13] * d1) + g[14] * d2;
-  float a0 = gr_fabsf(l0), a1 = gr_fabsf(l1), a2 = gr_fabsf(l2);
-  bool in_outer = (a0 <= g[16]) & (a1 <= g[17]) & (a2 <= g[15]);
-  bool in_hole = (a0 < g[7]) & (a1 < g[11]);
-  return in_outer & !in_hole;
+DEV void gate_frame(const float* g, const float v[3], float o[3]) {
+  o[0] = (g[4] * v[0] + g[5] * v[1]) + g[6] * v[2];
+  o[1] = (g[8] * v[0] + g[9] * v[1]) + g[10] * v[2];
+  o[2] = (g[12] * v[0] + g[13] * v[1]) + g[14] * v[2];
 }
 
 // number of the 17 lattice points inside a gate frame or under the ground
@@ -203,25 +206,52 @@ DEV int collision_count(const KArgs& a, const Tab& tab, int type, int lvl, const
   const float* rec = tab.rec(type, lvl);
   const float ground = rec[0];
   const int ng = (int)rec[3];
-  uint32_t inside = 0u;
-  // the lattice reaches at most |collider_half| (< lat_reach) from p: skip the
-  // per-point ground test when no point can be below the plane (conservative)
-  if (p[2] - ground < a.lat_reach) {
-    for (int k = 0; k < 17; ++k) {
-      float pt[3];
-      lattice_point(a, k, p, q, pt);
-      if (pt[2] < ground) inside |= 1u << k;
-    }
-  }
+  const float reach = a.lat_reach;  // > max |lattice offset| incl. rounding
+  // ---- conservative culls: which gates can contain a lattice point ----
+  uint32_t near = 0u;
   for (int g = 0; g < ng; ++g) {
     const float* gr = tab.gate(type, lvl, g);
-    float d0 = p[0] - gr[0], d1 = p[1] - gr[1], d2 = p[2] - gr[2];
-    if ((d0 * d0 + d1 * d1) + d2 * d2 <= gr[3]) {
-      for (int k = 0; k < 17; ++k) {
-        float pt[3];
-        lattice_point(a, k, p, q, pt);
-        if (point_in_gate(gr, pt)) inside |= 1u << k;
-      }
+    float d[3] = {p[0] - gr[0], p[1] - gr[1], p[2] - gr[2]};
+    if ((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2] <= gr[3]) {
+      float dg[3];
+      gate_frame(gr, d, dg);
+      float x = gr_fabsf(dg[0]), y = gr_fabsf(dg[1]), z = gr_fabsf(dg[2]);
+      bool slab = z <= gr[15] + reach;
+      bool outer = (x <= gr[16] + reach) & (y <= gr[17] + reach);
+      bool hole = (x < gr[7] - reach) & (y < gr[11] - reach);
+      if (slab & outer & !hole) near |= 1u << g;
+    }
+  }
+  const bool ground_near = p[2] - ground < reach;
+  if (!near && !ground_near) return 0;
+  float A[3], B[3], Cz[3];
+  body_axes(a, q, A, B, Cz);
+  uint32_t inside = 0u;
+  if (ground_near) {
+    for (int k = 0; k < 17; ++k) {
+      float oz = (c_lattice[k][0] * A[2] + c_lattice[k][1] * B[2]) + c_lattice[k][2] * Cz[2];
+      if (p[2] + oz < ground) inside |= 1u << k;
+    }
+  }
+  while (near) {
+    const int g = __builtin_ctz(near);
+    near &= near - 1u;
+    const float* gr = tab.gate(type, lvl, g);
+    float d[3] = {p[0] - gr[0], p[1] - gr[1], p[2] - gr[2]};
+    float dg[3], Ag[3], Bg[3], Cg[3];
+    gate_frame(gr, d, dg);
+    gate_frame(gr, A, Ag);
+    gate_frame(gr, B, Bg);
+    gate_frame(gr, Cz, Cg);
+    for (int k = 0; k < 17; ++k) {
+      const float lx = c_lattice[k][0], ly = c_lattice[k][1], lz = c_lattice[k][2];
+      float l0 = dg[0] + ((lx * Ag[0] + ly * Bg[0]) + lz * Cg[0]);
+      float l1 = dg[1] + ((lx * Ag[1] + ly * Bg[1]) + lz * Cg[1]);
+      float l2 = dg[2] + ((lx * Ag[2] + ly * Bg[2]) + lz * Cg[2]);
+      float a0 = gr_fabsf(l0), a1 = gr_fabsf(l1), a2 = gr_fabsf(l2);
+      bool in_outer = (a0 <= gr[16]) & (a1 <= gr[17]) & (a2 <= gr[15]);
+      bool in_hole = (a0 < gr[7]) & (a1 < gr[11]);
+      if (in_outer & !in_hole) inside |= 1u << k;
     }
   }
   return __builtin_popcount(inside);
@@ -378,6 +408,9 @@ DEV void reset_env(const KArgs& a, const Tab& tab, Env& e, uint32_t gid) {
 
 // ------------------------------------------------------------- observations
 DEV void gate_noise(const KArgs& a, const Env& e, uint32_t gid, int which, float out[3]) {
+#ifdef GR_ABL_NOGATENOISE
+  if (true) { out[0] = out[1] = out[2] = 0.0f; return; }
+#endif
   if (!a.cfg.add_gate_noise) { out[0] = out[1] = out[2] = 0.0f; return; }
   gr_u32x4 b = draw(a, gid, (uint32_t)e.epoch, GR_TAG_GATE, (uint32_t)(2 * e.acc + which));
   uint32_t wv[3] = {b.x, b.y, b.z};
@@ -503,7 +536,12 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const float* __r
 
   // ---- 2. load-independent work: observation noise (Philox + Box-Muller) ----
   ObsNoise on;
+#ifndef GR_ABL_NOOBSNOISE
   obs_noise(a, gid, cnt, on);
+#else
+  for (int k = 0; k < 3; ++k) on.vfac[k] = 1.0f;
+  on.qn[0] = 1.0f; on.qn[1] = on.qn[2] = on.qn[3] = 0.0f;
+#endif
 
   // ---- 3. stage the gate geometry of this workgroup's terrain types in LDS ----
   const int first_env = blockIdx.x * GR_BLOCK;
@@ -562,7 +600,9 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const float* __r
     int ccount = 0;
     if (c.integrator == GR_INTEGRATOR_DD_EXPLICIT) {
       dd_explicit(m, Jp, e.k2, e.k1, tt, dt, c.gravity, e.p, e.q, e.v, e.w, accl, al);
+#ifndef GR_ABL_NOCOLL
       ccount = collision_count(a, tab, e.type, e.lvl, e.p, e.q);
+#endif
     } else {
       float vb[3], fb[3] = {0.0f, 0.0f, tt[0]};
       quat_rotate_inverse(e.q, e.v, vb);
@@ -624,7 +664,11 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const float* __r
       a.buf.time_out[i] = (uint8_t)time_out;
       a.buf.dones[i] = (int64_t)done;
     }
+#ifndef GR_ABL_NORESET
     if (done && live) {
+#else
+    if (false) {
+#endif
       reset_lane = true;
       for (int k = 0; k < 7; ++k) lg[GR_LOG_EPSUM0 + k] = e.es[k];
       lg[GR_LOG_NRESET] = 1.0f;
@@ -652,7 +696,9 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const float* __r
     for (int k = 0; k < 4; ++k) lc[k] = th_raw[k] * sc[k] + of[k];
     lc[0] = lc[0] / e.mc;
     if (live) {
+#ifndef GR_ABL_NOOBS
       write_obs(a, tab, e, i, gid, on, lc, aux);
+#endif
       store_env(a, i, e, done != 0, false);
     }
   } else {
@@ -677,7 +723,9 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const float* __r
     }
   }
   // (observe calls reset nothing: their rows say so, and the finalized log repeats the previous one)
+#ifndef GR_ABL_NOLOG
   wave_log(a, lg, reset_lane, live ? (float)e.lvl : 0.0f, live ? e.nl : 0.0f);
+#endif
 }
 
 // ------------------------------------------------------------- init (startup events)

@@ -143,36 +143,45 @@ static const float LATTICE[17][3] = {
     {-0.5f, 0.5f, 0.5f}, {-0.5f, -0.5f, 0.5f}, {0.5f, 0.5f, -0.5f}, {0.5f, -0.5f, -0.5f}, {-0.5f, 0.5f, -0.5f},
     {-0.5f, -0.5f, -0.5f}};
 
-static int point_in_gate(const float* g, const float pt[3]) {
-  float d0 = pt[0] - g[0], d1 = pt[1] - g[1], d2 = pt[2] - g[2];
-  float l0 = (g[4] * d0 + g[5] * d1) + g[6] * d2;
-  float l1 = (g[8] * d0 + g[9] * d1) + g[10] * d2;
-  float l2 = (g[12] * d0 + g[13] * d1) + g[14] * d2;
-  float a0 = gr_fabsf(l0), a1 = gr_fabsf(l1), a2 = gr_fabsf(l2);
-  int in_outer = (a0 <= g[16]) & (a1 <= g[17]) & (a2 <= g[15]);
-  int in_hole = (a0 < g[7]) & (a1 < g[11]);
-  return in_outer & !in_hole;
+/* Lattice point k = p + (lx*A + ly*B) + lz*C with A, B, C = quat_rotate(q, scaled body
+ * axes) — quat_rotate is linear, so this is the reference's center + quat_rotate(q, vec)
+ * (mesh_tools.py:187-189) evaluated as a fixed sum.  Inside a gate frame M (rows of
+ * R_gate^T) the point is d_g + (lx*A_g + ly*B_g) + lz*C_g, d_g = M(p - c), A_g = M A, ... */
+static void gate_frame(const float* g, const float v[3], float o[3]) {
+  o[0] = (g[4] * v[0] + g[5] * v[1]) + g[6] * v[2];
+  o[1] = (g[8] * v[0] + g[9] * v[1]) + g[10] * v[2];
+  o[2] = (g[12] * v[0] + g[13] * v[1]) + g[14] * v[2];
 }
 
 int gro_collision_count(const gr_config* c, const gro_tracks* tr, int track, const float p[3], const float q[4]) {
   const float ground = track_rec(tr, track)[0];
   int ng = track_num_gates(tr, track);
-  int near[64];
-  int nnear = 0;
-  for (int g = 0; g < ng && g < 64; ++g) {
-    const float* gr = gate_rec(c, tr, track, g);
-    float d0 = p[0] - gr[0], d1 = p[1] - gr[1], d2 = p[2] - gr[2];
-    if ((d0 * d0 + d1 * d1) + d2 * d2 <= gr[3]) near[nnear++] = g;
-  }
+  const float ex[3] = {c->collider_half[0], 0.0f, 0.0f}, ey[3] = {0.0f, c->collider_half[1], 0.0f},
+              ez[3] = {0.0f, 0.0f, c->collider_half[2]};
+  float A[3], B[3], Cz[3];
+  quat_rotate(q, ex, A);
+  quat_rotate(q, ey, B);
+  quat_rotate(q, ez, Cz);
   int count = 0;
   for (int k = 0; k < 17; ++k) {
-    float o[3] = {LATTICE[k][0] * c->collider_half[0], LATTICE[k][1] * c->collider_half[1],
-                  LATTICE[k][2] * c->collider_half[2]};
-    float r[3];
-    quat_rotate(q, o, r);
-    float pt[3] = {p[0] + r[0], p[1] + r[1], p[2] + r[2]};
-    int inside = pt[2] < ground;
-    for (int j = 0; j < nnear && !inside; ++j) inside = point_in_gate(gate_rec(c, tr, track, near[j]), pt);
+    const float lx = LATTICE[k][0], ly = LATTICE[k][1], lz = LATTICE[k][2];
+    float oz = (lx * A[2] + ly * B[2]) + lz * Cz[2];
+    int inside = p[2] + oz < ground; /* below the ground plane (ground box top) */
+    for (int g = 0; g < ng && !inside; ++g) {
+      const float* gr = gate_rec(c, tr, track, g);
+      float d[3] = {p[0] - gr[0], p[1] - gr[1], p[2] - gr[2]}, dg[3], Ag[3], Bg[3], Cg[3];
+      gate_frame(gr, d, dg);
+      gate_frame(gr, A, Ag);
+      gate_frame(gr, B, Bg);
+      gate_frame(gr, Cz, Cg);
+      float l0 = dg[0] + ((lx * Ag[0] + ly * Bg[0]) + lz * Cg[0]);
+      float l1 = dg[1] + ((lx * Ag[1] + ly * Bg[1]) + lz * Cg[1]);
+      float l2 = dg[2] + ((lx * Ag[2] + ly * Bg[2]) + lz * Cg[2]);
+      float a0 = gr_fabsf(l0), a1 = gr_fabsf(l1), a2 = gr_fabsf(l2);
+      int in_outer = (a0 <= gr[16]) & (a1 <= gr[17]) & (a2 <= gr[15]);
+      int in_hole = (a0 < gr[7]) & (a1 < gr[11]);
+      inside = in_outer & !in_hole; /* frame = outer box minus the through-hole */
+    }
     count += inside;
   }
   return count;
