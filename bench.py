@@ -76,30 +76,35 @@ def make_env(n, rank, device, gates, integrator):
     return env
 
 
+def capture_graph(env, actions):
+    """hipGraph of ACTION_RING consecutive env steps (buffer bindings and action pointers baked in)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for k in range(2):  # stream warm-up outside capture
+            env.step(actions[k % ACTION_RING])
+    torch.cuda.current_stream().wait_stream(s)
+    # realign the host-side call counter to a multiple of the ring
+    while env._calls % ACTION_RING != 0:
+        env.step(actions[env._calls % ACTION_RING])
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for k in range(ACTION_RING):
+            env.step(actions[k])
+    torch.cuda.synchronize()
+    graph.replay()
+    torch.cuda.synchronize()
+    return graph
+
+
 def time_env_steps(env, actions, steps, use_graph):
-    """Returns (seconds for exactly `steps` env steps, launch mode)."""
+    """Returns (seconds for exactly `steps` env steps, launch mode, graph or None)."""
     mode = "eager"
     graph = None
     if use_graph and steps >= ACTION_RING:
         try:
-            # capture ACTION_RING consecutive steps (buffer bindings and action pointers baked in)
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                for k in range(2):  # stream warm-up outside capture
-                    env.step(actions[k % ACTION_RING])
-            torch.cuda.current_stream().wait_stream(s)
-            # realign the host-side call counter to a multiple of the ring
-            while env._calls % ACTION_RING != 0:
-                env.step(actions[env._calls % ACTION_RING])
-            torch.cuda.synchronize()
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                for k in range(ACTION_RING):
-                    env.step(actions[k])
-            torch.cuda.synchronize()
-            graph.replay()
-            torch.cuda.synchronize()
+            graph = capture_graph(env, actions)
             mode = "hipgraph"
         except Exception as e:  # graph capture unavailable: fall back to eager launches
             print(f"[bench] hipGraph capture failed ({e}); timing eager launches", file=sys.stderr)
@@ -115,22 +120,42 @@ def time_env_steps(env, actions, steps, use_graph):
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
-    return t1 - t0, mode
+    return t1 - t0, mode, graph
 
 
-def kernel_timing(env, actions, steps):
-    """HIP events around every fused-kernel launch (eager pass), on the launch stream."""
+def kernel_timing(env, actions, steps, graph):
+    """Average duration of one fused-kernel launch, from HIP events on the launch stream.
+
+    Graph mode: one event pair around back-to-back replays of the 64-launch graph (each replay is
+    exactly 64 env-kernel launches on torch's current stream, which is the stream gr_step launches
+    on), so the per-launch figure includes the graph's inter-kernel gaps — the same quantity
+    rocprofv3's kernel-trace average approximates from below.  Also returned: the C ABI's own
+    per-launch event pairs (gr_set_timing) from an eager pass, which add event-record overhead."""
     import ctypes as C
 
+    out = {}
+    if graph is not None:
+        reps = max(1, min(steps, 4096) // ACTION_RING)
+        stream = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for _ in range(reps):
+            graph.replay()
+        e1.record(stream)
+        e1.synchronize()
+        out["graph_event_us"] = e0.elapsed_time(e1) * 1e3 / (reps * ACTION_RING)
     lib, ctx = env._lib, env._ctx
-    n = min(steps, 4096)
+    n = min(steps, 1024)
     assert lib.gr_set_timing(ctx, 1) == 0
     for k in range(n):
         env.step(actions[k % ACTION_RING])
     tot, cnt = C.c_double(), C.c_int64()
     assert lib.gr_read_timing(ctx, C.byref(tot), C.byref(cnt)) == 0
     lib.gr_set_timing(ctx, 0)
-    return tot.value / cnt.value  # ms per launch
+    out["eager_event_us"] = tot.value * 1e3 / cnt.value
+    out["kernel_us"] = out.get("graph_event_us", out["eager_event_us"])
+    return out
 
 
 def policy_in_loop(env, steps, device):
@@ -221,12 +246,14 @@ def main():
     for k in range(a.warmup):
         env.step(actions[k % ACTION_RING])
     torch.cuda.synchronize()
-    secs, mode = time_env_steps(env, actions, a.steps, not a.no_graph)
+    secs, mode, graph = time_env_steps(env, actions, a.steps, not a.no_graph)
     secs = max_over_ranks(secs, device)
     value = n * ws * a.steps / secs
-    ms_kernel = kernel_timing(env, actions, a.steps)
+    kt = kernel_timing(env, actions, a.steps, graph)
+    del graph
+    us = kt["kernel_us"]
     rd, wr = env.bytes_per_env_step()
-    achieved = (rd + wr) * n / (ms_kernel * 1e-3) / 1e9
+    achieved = (rd + wr) * n / (us * 1e-6) / 1e9
     extra = {}
     if not a.no_extras:
         extra["policy_in_loop_env_steps_per_s"] = policy_in_loop(env, 256, device)
@@ -257,9 +284,9 @@ def main():
                        "num_envs_per_gpu": n, "launch": mode, "parallelism": f"env-shard x{ws}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "gr::env_kernel<0,true> (fused step)", "kernel_us": ms_kernel * 1e3,
-                         "bytes_per_env_step": {"read": rd, "written": wr},
-                         "read_frac": rd * n / (ms_kernel * 1e-3) / 1e9 / HBM_PEAK_GBS},
+                         "kernel": "gr::env_kernel<0,true> (fused step)", **kt,
+                         "algorithmic_bytes_per_launch": (rd + wr) * n,
+                         "bytes_per_env_step": {"read": rd, "written": wr}},
             "cpu_baseline": cpu,
             **extra,
         }

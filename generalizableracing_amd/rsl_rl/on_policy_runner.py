@@ -191,7 +191,8 @@ class OnPolicyRunner:
                 v = v if isinstance(v, torch.Tensor) else torch.tensor([float(v)])
                 vals.append(v.reshape(-1).to(self.device))
             ep_vals[key] = float(torch.cat(vals).float().mean())
-        mean_std = float(self.alg.policy._std(torch.zeros(1, self.env.num_actions, device=self.device)).mean())
+        with torch.no_grad():
+            mean_std = float(self.alg.policy._std(torch.zeros(1, self.env.num_actions, device=self.device)).mean())
         self.last_log = {"fps": fps, "collection_time": locs["collection_time"], "learn_time": locs["learn_time"],
                          "mean_reward": means[0] if means else None, "mean_episode_length": means[1] if means else None,
                          "learning_rate": self.alg.learning_rate, **locs["loss_dict"], **ep_vals}

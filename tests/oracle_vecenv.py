@@ -1,0 +1,71 @@
+"""Test-only VecEnv backed by the CPU oracle (never used by the product path).
+
+Lets the rsl_rl runner / PPO / distributed plumbing be exercised on CPU with
+the same `RslRlVecEnvWrapper` surface the HIP env exposes (get_observations,
+reset, step -> (obs, rew, dones long, extras{observations, time_outs, log}),
+settable episode_length_buf)."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+import oracle
+from generalizableracing_amd.envs.racing_cfg import RacingEnvCfg, SceneCfg, SimCfg, TerrainCfg
+from generalizableracing_amd.envs.tracks import build_track_table
+
+
+class OracleVecEnv:
+    def __init__(self, num_envs=64, stage=1, env_id_offset=0, track_seed_offset=0, seed=42, types=4, levels=10):
+        self.cfg = RacingEnvCfg(scene=SceneCfg(num_envs=num_envs), sim=SimCfg(device="cpu"), stage=stage,
+                                terrain=TerrainCfg(num_cols=types, num_rows=levels), seed=seed,
+                                env_id_offset=env_id_offset, track_seed_offset=track_seed_offset)
+        c = self.cfg.to_gr_config()
+        gates, recs = build_track_table(num_types=types, num_levels=levels, num_gates=8, seed=42 + track_seed_offset)
+        self.orc = oracle.Oracle(c, gates, recs)
+        self.orc.init()
+        self.orc.reset(None)
+        self.num_envs = num_envs
+        self.num_actions = 4
+        self.num_obs = 16
+        self.num_privileged_obs = 16
+        self.max_episode_length = self.cfg.max_episode_length
+        self.device = "cpu"
+        self.render_mode = None
+
+    @property
+    def unwrapped(self):
+        return self
+
+    @property
+    def episode_length_buf(self) -> torch.Tensor:
+        return torch.from_numpy(self.orc.envs["ep_len"].astype(np.int64))
+
+    @episode_length_buf.setter
+    def episode_length_buf(self, value: torch.Tensor):
+        self.orc.envs["ep_len"] = value.cpu().numpy().astype(np.int32)
+
+    def _obs(self):
+        return {"policy": torch.from_numpy(self.orc.obs_policy.copy()),
+                "critic": torch.from_numpy(self.orc.obs_critic.copy()),
+                "auxiliary": torch.from_numpy(self.orc.obs_aux.copy()).unsqueeze(1)}
+
+    def get_observations(self):
+        self.orc.observe()
+        o = self._obs()
+        return o["policy"], {"observations": o}
+
+    def reset(self):
+        self.orc.reset(None)
+        o = self._obs()
+        return o["policy"], {"observations": o}
+
+    def step(self, actions: torch.Tensor):
+        self.orc.step(actions.detach().cpu().numpy().astype(np.float32))
+        o = self._obs()
+        extras = {"observations": o, "time_outs": torch.from_numpy(self.orc.time_out.astype(bool)),
+                  "log": {"Episode_Termination/time_out": float(self.orc.log[12])}}
+        return (o["policy"], torch.from_numpy(self.orc.reward.copy()),
+                torch.from_numpy(self.orc.dones.copy()), extras)
+
+    def close(self):
+        pass

@@ -1,0 +1,25 @@
+"""standalone/rsl_rl/train.py end to end on the HIP env (reference train.sh command line)."""
+import os
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_train_cli_two_iterations(tmp_path):
+    sys.path.insert(0, os.path.join(ROOT, "standalone", "rsl_rl"))
+    import train
+
+    runner = train.main(["--task", "DiffLab-Quadcopter-CTBR-Racing-v0", "--num_envs", "1024", "--headless",
+                         "--max_iterations", "2", "--log_root", str(tmp_path)])
+    assert runner.last_log["fps"] > 0
+    runs = list((tmp_path / "rsl_rl" / "racing_ppo").iterdir())
+    assert len(runs) == 1 and (runs[0] / "params" / "env.yaml").exists()
+    assert any(f.name.startswith("model_") for f in runs[0].iterdir())
+    # resume from the latest checkpoint of the latest run
+    r2 = train.main(["--task", "DiffLab-Quadcopter-CTBR-Racing-v0", "--num_envs", "1024", "--max_iterations", "1",
+                     "--log_root", str(tmp_path), "--resume", "1"])
+    assert r2.current_learning_iteration >= 1
