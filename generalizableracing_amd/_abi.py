@@ -177,6 +177,7 @@ EXPORTS = [
     "gr_num_blocks", "gr_num_log_rows", "gr_log_finalize", "gr_bytes_per_env_step", "gr_bind_tracks", "gr_bind_buffers", "gr_init", "gr_reset",
     "gr_step", "gr_observe", "gr_set_timing", "gr_read_timing", "gr_test_dynamics", "gr_test_math",
     "gr_test_philox",
+    "gr_debug_read_stamps",
 ]
 
 _lib = None
@@ -206,6 +207,7 @@ def _declare(lib):
         "gr_test_dynamics": (C.c_int, [vp, C.c_int, C.c_int] + [vp] * 9 + [vp]),
         "gr_test_math": (C.c_int, [vp, C.c_int, C.c_int, vp, vp, vp, vp]),
         "gr_test_philox": (C.c_int, [vp, C.c_int] + [C.c_uint32] * 4 + [vp, vp]),
+        "gr_debug_read_stamps": (C.c_int, [vp, C.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

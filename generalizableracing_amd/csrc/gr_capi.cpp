@@ -24,6 +24,10 @@ struct gr_ctx {
   float* table = nullptr;  // packed [T*L][stride]
   bool have_tracks = false;
   gr::KArgs args;
+  gr::KConst kc;                   // host copy of the per-context constants
+  gr::KConst* kc_dev = nullptr;    // device copy read by the kernels
+  std::vector<int> blk_types;      // per workgroup: first | last terrain type << 16
+  int* blk_dev = nullptr;
   std::string err;
   // optional kernel timing (gr_set_timing)
   std::vector<hipEvent_t> ev;  // [2 * GR_TIMING_RING]
@@ -44,10 +48,31 @@ int hip_fail(gr_ctx* c, hipError_t e, const char* what) {
 }
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// device copy of the constants, made on first device use (gr_create stays host-only)
+int ensure_dev(gr_ctx* c, const char* what) {
+  if (c->kc_dev) return GR_OK;
+  const size_t nbt = c->blk_types.size() * sizeof(int);
+  hipError_t e = hipMalloc(&c->kc_dev, sizeof(gr::KConst));
+  if (e == hipSuccess) e = hipMalloc(&c->blk_dev, nbt);
+  if (e == hipSuccess) e = hipMemcpy(c->kc_dev, &c->kc, sizeof(gr::KConst), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c->blk_dev, c->blk_types.data(), nbt, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    if (c->kc_dev) (void)hipFree(c->kc_dev);
+    if (c->blk_dev) (void)hipFree(c->blk_dev);
+    c->kc_dev = nullptr;
+    c->blk_dev = nullptr;
+    return hip_fail(c, e, what);
+  }
+  c->args.kc = c->kc_dev;
+  c->args.blk_types = c->blk_dev;
+  return GR_OK;
+}
+
 void derive(gr_ctx* c) {
   const gr_config& g = c->cfg;
-  gr::KArgs& a = c->args;
+  gr::KConst& a = c->kc;
   std::memset(&a, 0, sizeof(a));
+  std::memset(&c->args, 0, sizeof(c->args));
   a.cfg = g;
   a.track_stride = g.max_gates * GR_GATE_FLOATS + GR_TRACK_FLOATS;
   // env -> terrain type: IL floor(arange(N) / (N / num_cols)) with an fp32 divisor
@@ -83,19 +108,34 @@ void derive(gr_ctx* c) {
   a.tm_k2 = (float)k2; a.tm_k1 = (float)k1; a.tm_k0 = (float)k0;
   a.tm_k1sq = (float)(k1 * k1); a.tm_4k2 = (float)(4.0 * k2);
   a.tm_inv2k2 = (float)(1.0 / (2.0 * k2)); a.tm_negk1 = (float)(-k1);
-  // LDS: the widest terrain-type span of any workgroup, all levels
+  // per-workgroup terrain-type range; LDS = the widest span of any workgroup, all levels
   int span = 1;
   const int nb = (g.num_envs + GR_BLOCK - 1) / GR_BLOCK;
+  c->blk_types.assign(nb, 0);
   for (int b = 0; b < nb; ++b) {
     int f = b * GR_BLOCK, last = std::min(f + GR_BLOCK, g.num_envs) - 1, t0 = 0, t1 = 0;
     for (int t = 1; t < g.num_types; ++t) { t0 += f >= a.type_start[t]; t1 += last >= a.type_start[t]; }
     span = std::max(span, t1 - t0 + 1);
+    c->blk_types[b] = t0 | (t1 << 16);
   }
   const long bytes = (long)span * g.num_levels * a.track_stride * 4;
   a.lds_bytes = bytes <= 60 * 1024 ? (int)bytes : 0;  // beyond 60 KiB: read the (L2-resident) table directly
 #ifdef GR_ABL_NOLDS
   a.lds_bytes = 0;
 #endif
+  gr::KHot& h = c->args.h;
+  h.num_envs = g.num_envs;
+  h.num_levels = g.num_levels;
+  h.max_gates = g.max_gates;
+  h.track_stride = a.track_stride;
+  h.env_id_offset = g.env_id_offset;
+  h.use_motor_model = g.use_motor_model;
+  h.obs_noise = g.obs_noise;
+  h.lds_bytes = a.lds_bytes;
+  h.seed_lo = g.seed_lo;
+  h.seed_hi = g.seed_hi;
+  h.obs_lin_vel_noise = g.obs_lin_vel_noise;
+  h.obs_att_noise = g.obs_att_noise;
 }
 
 }  // namespace
@@ -207,6 +247,8 @@ int gr_destroy(gr_ctx* c) {
   if (!c) return GR_ERR_ARG;
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->table) (void)hipFree(c->table);
+  if (c->kc_dev) (void)hipFree(c->kc_dev);
+  if (c->blk_dev) (void)hipFree(c->blk_dev);
   delete c;
   return GR_OK;
 }
@@ -248,7 +290,7 @@ int gr_bind_tracks(gr_ctx* c, const float* gates, const float* tracks) {
         (float)start != r[2] || (float)ng != r[3])
       return fail(c, GR_ERR_ARG, "gr_bind_tracks: invalid track record " + std::to_string(t));
   }
-  const size_t stride = (size_t)c->args.track_stride;
+  const size_t stride = (size_t)c->kc.track_stride;
   if (!c->table) {
     e = hipMalloc(&c->table, (size_t)ntr * stride * sizeof(float));
     if (e != hipSuccess) return hip_fail(c, e, "gr_bind_tracks: hipMalloc");
@@ -289,7 +331,7 @@ static int ready(gr_ctx* c, const char* what) {
   if (!c) return GR_ERR_ARG;
   if (!c->have_buf || !c->have_tracks)
     return fail(c, GR_ERR_STATE, std::string(what) + ": buffers and tracks must be bound first");
-  return GR_OK;
+  return ensure_dev(c, what);
 }
 
 int gr_init(gr_ctx* c, void* stream) {
@@ -364,6 +406,7 @@ int gr_observe(gr_ctx* c, void* stream) {
 int gr_test_dynamics(gr_ctx* c, int n, int mode, const float* si, const float* ab, const float* cmd, const float* ci,
                      const float* par, const float* drag, float* so, float* co, float* xo, void* stream) {
   if (!c || n <= 0 || !si || !ab || !cmd || !ci || !par || !drag || !so || !co || !xo) return GR_ERR_ARG;
+  if (int r = ensure_dev(c, "gr_test_dynamics")) return r;
   hipError_t e = gr::launch_test_dynamics(c->args, n, mode, si, ab, cmd, ci, par, drag, so, co, xo, (hipStream_t)stream);
   return e == hipSuccess ? GR_OK : hip_fail(c, e, "gr_test_dynamics");
 }
@@ -378,6 +421,12 @@ int gr_test_philox(gr_ctx* c, int n, uint32_t c0, uint32_t c1, uint32_t c2, uint
   if (!c || n <= 0 || !out4) return GR_ERR_ARG;
   hipError_t e = gr::launch_test_philox(n, c0, c1, c2, c3, c->cfg.seed_lo, c->cfg.seed_hi, out4, (hipStream_t)stream);
   return e == hipSuccess ? GR_OK : hip_fail(c, e, "gr_test_philox");
+}
+
+int gr_debug_read_stamps(uint64_t* host, int n) {
+  if (!host || n <= 0) return GR_ERR_ARG;
+  hipError_t e = gr::read_stamps(reinterpret_cast<unsigned long long*>(host), n);
+  return e == hipSuccess ? GR_OK : (e == hipErrorNotSupported ? GR_ERR_STATE : GR_ERR_HIP);
 }
 
 }  // extern "C"

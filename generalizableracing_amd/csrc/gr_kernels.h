@@ -6,17 +6,19 @@
 
 #define GR_BLOCK 256
 #define GR_MAX_TYPES 64
+#define GR_STAMP_WAVES 4096  // diagnostic stamps (GR_STAMPS builds only)
+#define GR_STAMP_SLOTS 16
 
 namespace gr {
 
 enum { KMODE_STEP = 0, KMODE_RESET = 1, KMODE_OBSERVE = 2 };
 
-// Passed by value (kernarg segment -> scalar registers).  Everything derived
-// from the config that would otherwise be recomputed per lane lives here.
-struct KArgs {
+// Per-context constants: the config and everything derived from it once on the
+// host.  Lives in device memory and is read through a __restrict__ kernel
+// argument, so the compiler emits scalar loads next to each use instead of
+// hoisting ~150 kernarg dwords into SGPRs at entry (which spilled into VGPR lanes).
+struct KConst {
   gr_config cfg;
-  gr_buffers buf;
-  const float* table;  // packed track table [T*L][track_stride]
   int track_stride;    // floats per track: max_gates*GR_GATE_FLOATS + GR_TRACK_FLOATS
   int lds_bytes;       // dynamic LDS per workgroup (0: read the table from global memory)
   int type_start[GR_MAX_TYPES + 1];
@@ -29,6 +31,24 @@ struct KArgs {
   float tm_k2, tm_k1, tm_k0, tm_k1sq, tm_4k2, tm_inv2k2, tm_negk1;
 };
 
+// Constants every wave needs before its first loads / RNG draws: passed by value
+// (one kernarg fetch at entry) instead of through the KConst pointer chain.
+struct KHot {
+  int num_envs, num_levels, max_gates, track_stride;
+  int env_id_offset, use_motor_model, obs_noise, lds_bytes;
+  uint32_t seed_lo, seed_hi;
+  float obs_lin_vel_noise, obs_att_noise;
+};
+
+// Passed by value (kernarg): per-binding pointers + the constants pointer.
+struct KArgs {
+  const KConst* kc;      // device copy (set from the kernel's __restrict__ argument)
+  gr_buffers buf;
+  const float* table;    // packed track table [T*L][track_stride]
+  const int* blk_types;  // per workgroup: first | last terrain type << 16 (host-derived)
+  KHot h;
+};
+
 hipError_t launch_env(int mode, const KArgs& a, const float* actions, const uint8_t* mask, hipStream_t s,
                       hipEvent_t t0, hipEvent_t t1);
 hipError_t launch_init(const KArgs& a, hipStream_t s);
@@ -38,6 +58,7 @@ hipError_t launch_test_dynamics(const KArgs& a, int n, int mode, const float* si
                                 const float* ci, const float* par, const float* drag, float* so, float* co, float* xo,
                                 hipStream_t s);
 hipError_t launch_test_math(int fn, int n, const float* x, const float* y, float* out, hipStream_t s);
+hipError_t read_stamps(unsigned long long* host, int n);
 hipError_t launch_test_philox(int n, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
                               uint32_t* out, hipStream_t s);
 

@@ -90,13 +90,15 @@ struct Env {
 };
 
 DEV void load_env(const KArgs& a, int i, Env& e) {
+  // issue order = order of first use (the waitcnt counters retire in order)
   const float4* S = reinterpret_cast<const float4*>(a.buf.state);
-  const size_t n = (size_t)a.cfg.num_envs;
-  float4 s0 = S[GR_P_POSQ * n + i], s1 = S[GR_P_QV * n + i], s2 = S[GR_P_VW * n + i], s3 = S[GR_P_WA * n + i];
-  float4 s4 = S[GR_P_CTRL * n + i], s5 = S[GR_P_LAG * n + i], s6 = S[GR_P_RST0 * n + i], s7 = S[GR_P_RST1 * n + i];
-  float4 s8 = S[GR_P_EP0 * n + i], s9 = S[GR_P_EP1 * n + i];
-  float4 p0 = S[GR_P_PAR0 * n + i], p1 = S[GR_P_PAR1 * n + i], p2 = S[GR_P_PAR2 * n + i], p3 = S[GR_P_PAR3 * n + i];
+  const size_t n = (size_t)a.h.num_envs;
   int4 ii = reinterpret_cast<const int4*>(a.buf.istate)[i];
+  float4 s5 = S[GR_P_LAG * n + i], s6 = S[GR_P_RST0 * n + i], p2 = S[GR_P_PAR2 * n + i];
+  float4 s2 = S[GR_P_VW * n + i], s3 = S[GR_P_WA * n + i], s4 = S[GR_P_CTRL * n + i];
+  float4 p0 = S[GR_P_PAR0 * n + i], p1 = S[GR_P_PAR1 * n + i], p3 = S[GR_P_PAR3 * n + i];
+  float4 s0 = S[GR_P_POSQ * n + i], s1 = S[GR_P_QV * n + i], s7 = S[GR_P_RST1 * n + i];
+  float4 s8 = S[GR_P_EP0 * n + i], s9 = S[GR_P_EP1 * n + i];
   e.p[0] = s0.x; e.p[1] = s0.y; e.p[2] = s0.z; e.q[0] = s0.w;
   e.q[1] = s1.x; e.q[2] = s1.y; e.q[3] = s1.z; e.v[0] = s1.w;
   e.v[1] = s2.x; e.v[2] = s2.y; e.w[0] = s2.z; e.w[1] = s2.w;
@@ -111,7 +113,7 @@ DEV void load_env(const KArgs& a, int i, Env& e) {
   e.Kd[0] = p1.x; e.Kd[1] = p1.y; e.Kd[2] = p1.z; e.mp = p1.w;
   e.ct[0] = p2.x; e.ct[1] = p2.y; e.ct[2] = p2.z; e.mc = p2.w;
   e.J[0] = p3.x; e.J[1] = p3.y; e.J[2] = p3.z;
-  if (a.cfg.use_motor_model) {
+  if (a.h.use_motor_model) {
     float4 m = S[GR_P_MOTOR * n + i];
     e.mw[0] = m.x; e.mw[1] = m.y; e.mw[2] = m.z; e.mw[3] = m.w;
   } else {
@@ -121,10 +123,10 @@ DEV void load_env(const KArgs& a, int i, Env& e) {
   e.gate = ii.w & 0xff; e.lvl = (ii.w >> 8) & 0xff; e.azero = (ii.w >> 16) & 1; e.type = (ii.w >> 24) & 0xff;
 }
 
-// Dynamic planes (and, when `rst` is set, the per-episode DR planes) back to HBM.
-DEV void store_env(const KArgs& a, int i, const Env& e, bool rst, bool params) {
+// Per-step planes: kinematics, controller filters, lag, episode sums (+ motor speeds).
+DEV void store_dyn(const KArgs& a, int i, const Env& e) {
   float4* S = reinterpret_cast<float4*>(a.buf.state);
-  const size_t n = (size_t)a.cfg.num_envs;
+  const size_t n = (size_t)a.h.num_envs;
   S[GR_P_POSQ * n + i] = make_float4(e.p[0], e.p[1], e.p[2], e.q[0]);
   S[GR_P_QV * n + i] = make_float4(e.q[1], e.q[2], e.q[3], e.v[0]);
   S[GR_P_VW * n + i] = make_float4(e.v[1], e.v[2], e.w[0], e.w[1]);
@@ -133,17 +135,18 @@ DEV void store_env(const KArgs& a, int i, const Env& e, bool rst, bool params) {
   S[GR_P_LAG * n + i] = make_float4(e.lag[0], e.lag[1], e.lag[2], e.lag[3]);
   S[GR_P_EP0 * n + i] = make_float4(e.es[0], e.es[1], e.es[2], e.es[3]);
   S[GR_P_EP1 * n + i] = make_float4(e.es[4], e.es[5], e.es[6], e.mar);
-  if (rst) {
-    S[GR_P_RST0 * n + i] = make_float4(e.thr, e.nl, e.k2[0], e.k2[1]);
-    S[GR_P_RST1 * n + i] = make_float4(e.k2[2], e.k1[0], e.k1[1], e.k1[2]);
-  }
-  if (params) {
-    S[GR_P_PAR0 * n + i] = make_float4(e.Kp[0], e.Kp[1], e.Kp[2], e.cT);
-    S[GR_P_PAR1 * n + i] = make_float4(e.Kd[0], e.Kd[1], e.Kd[2], e.mp);
-    S[GR_P_PAR2 * n + i] = make_float4(e.ct[0], e.ct[1], e.ct[2], e.mc);
-    S[GR_P_PAR3 * n + i] = make_float4(e.J[0], e.J[1], e.J[2], 0.0f);
-  }
-  if (a.cfg.use_motor_model) S[GR_P_MOTOR * n + i] = make_float4(e.mw[0], e.mw[1], e.mw[2], e.mw[3]);
+  if (a.h.use_motor_model) S[GR_P_MOTOR * n + i] = make_float4(e.mw[0], e.mw[1], e.mw[2], e.mw[3]);
+}
+
+// Per-episode domain-randomisation planes (written at reset only).
+DEV void store_rst(const KArgs& a, int i, const Env& e) {
+  float4* S = reinterpret_cast<float4*>(a.buf.state);
+  const size_t n = (size_t)a.h.num_envs;
+  S[GR_P_RST0 * n + i] = make_float4(e.thr, e.nl, e.k2[0], e.k2[1]);
+  S[GR_P_RST1 * n + i] = make_float4(e.k2[2], e.k1[0], e.k1[1], e.k1[2]);
+}
+
+DEV void store_istate(const KArgs& a, int i, const Env& e) {
   int packed = (e.gate & 0xff) | ((e.lvl & 0xff) << 8) | ((e.azero & 1) << 16) | ((e.type & 0xff) << 24);
   reinterpret_cast<int4*>(a.buf.istate)[i] = make_int4(e.ep, e.acc, e.epoch, packed);
 }
@@ -159,16 +162,16 @@ struct Tab {
   DEV const float* rec(int type, int lvl) const { return track_base(type, lvl) + G * GR_GATE_FLOATS; }
 };
 
-DEV uint32_t gid_of(const KArgs& a, int i) { return (uint32_t)(a.cfg.env_id_offset + i); }
+DEV uint32_t gid_of(const KArgs& a, int i) { return (uint32_t)(a.h.env_id_offset + i); }
 DEV gr_u32x4 draw(const KArgs& a, uint32_t gid, uint32_t c1, uint32_t tag, uint32_t c3) {
-  return gr_philox4x32_10(gid, c1, tag, c3, a.cfg.seed_lo, a.cfg.seed_hi);
+  return gr_philox4x32_10(gid, c1, tag, c3, a.h.seed_lo, a.h.seed_hi);
 }
 
 DEV void action_scale(const KArgs& a, float m_ctrl, float sc[4], float of[4]) {
-  float weight = m_ctrl * a.cfg.gravity;
-  float s0 = (weight * a.cfg.max_thrust_weight_ratio) / 2.0f;
+  float weight = m_ctrl * a.kc->cfg.gravity;
+  float s0 = (weight * a.kc->cfg.max_thrust_weight_ratio) / 2.0f;
   sc[0] = s0; of[0] = s0;
-  for (int k = 1; k < 4; ++k) { sc[k] = a.cfg.body_rate_bound; of[k] = 0.0f; }
+  for (int k = 1; k < 4; ++k) { sc[k] = a.kc->cfg.body_rate_bound; of[k] = 0.0f; }
 }
 
 // ------------------------------------------------------------- collision
@@ -180,15 +183,16 @@ DEV void action_scale(const KArgs& a, float m_ctrl, float sc[4], float of[4]) {
 // Oracle and kernel evaluate exactly these expressions; the kernel adds
 // conservative culls (sphere, plane slab, outer box, hole) that can only skip
 // gates where no lattice point can be inside, so the count is unchanged.
-__constant__ float c_lattice[17][3] = {
+// compile-time lattice: after unrolling every offset is an inline constant (0, +-1, +-0.5)
+constexpr float c_lattice[17][3] = {
     {0, 0, 0},          {1, 1, 1},         {1, -1, 1},        {-1, 1, 1},       {-1, -1, 1},     {1, 1, -1},
     {1, -1, -1},        {-1, 1, -1},       {-1, -1, -1},      {0.5f, 0.5f, 0.5f}, {0.5f, -0.5f, 0.5f},
     {-0.5f, 0.5f, 0.5f}, {-0.5f, -0.5f, 0.5f}, {0.5f, 0.5f, -0.5f}, {0.5f, -0.5f, -0.5f}, {-0.5f, 0.5f, -0.5f},
     {-0.5f, -0.5f, -0.5f}};
 
 DEV void body_axes(const KArgs& a, const float q[4], float A[3], float B[3], float Cz[3]) {
-  const float ex[3] = {a.cfg.collider_half[0], 0.0f, 0.0f}, ey[3] = {0.0f, a.cfg.collider_half[1], 0.0f},
-              ez[3] = {0.0f, 0.0f, a.cfg.collider_half[2]};
+  const float ex[3] = {a.kc->cfg.collider_half[0], 0.0f, 0.0f}, ey[3] = {0.0f, a.kc->cfg.collider_half[1], 0.0f},
+              ez[3] = {0.0f, 0.0f, a.kc->cfg.collider_half[2]};
   quat_rotate(q, ex, A);
   quat_rotate(q, ey, B);
   quat_rotate(q, ez, Cz);
@@ -206,43 +210,45 @@ DEV int collision_count(const KArgs& a, const Tab& tab, int type, int lvl, const
   const float* rec = tab.rec(type, lvl);
   const float ground = rec[0];
   const int ng = (int)rec[3];
-  const float reach = a.lat_reach;  // > max |lattice offset| incl. rounding
-  // ---- conservative culls: which gates can contain a lattice point ----
-  uint32_t near = 0u;
+  const float reach = a.kc->lat_reach;  // > max |lattice offset| incl. rounding
+  // ---- pass 1: bounding-sphere cull, one 16-byte read (centre, r^2) per gate ----
+  uint32_t sph = 0u;
+#pragma unroll 8
   for (int g = 0; g < ng; ++g) {
-    const float* gr = tab.gate(type, lvl, g);
-    float d[3] = {p[0] - gr[0], p[1] - gr[1], p[2] - gr[2]};
-    if ((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2] <= gr[3]) {
-      float dg[3];
-      gate_frame(gr, d, dg);
-      float x = gr_fabsf(dg[0]), y = gr_fabsf(dg[1]), z = gr_fabsf(dg[2]);
-      bool slab = z <= gr[15] + reach;
-      bool outer = (x <= gr[16] + reach) & (y <= gr[17] + reach);
-      bool hole = (x < gr[7] - reach) & (y < gr[11] - reach);
-      if (slab & outer & !hole) near |= 1u << g;
-    }
+    const float4 c4 = *reinterpret_cast<const float4*>(tab.gate(type, lvl, g));
+    const float dx = p[0] - c4.x, dy = p[1] - c4.y, dz = p[2] - c4.z;
+    if ((dx * dx + dy * dy) + dz * dz <= c4.w) sph |= 1u << g;
   }
   const bool ground_near = p[2] - ground < reach;
-  if (!near && !ground_near) return 0;
+  if (!sph && !ground_near) return 0;
   float A[3], B[3], Cz[3];
   body_axes(a, q, A, B, Cz);
   uint32_t inside = 0u;
   if (ground_near) {
+#pragma unroll
     for (int k = 0; k < 17; ++k) {
       float oz = (c_lattice[k][0] * A[2] + c_lattice[k][1] * B[2]) + c_lattice[k][2] * Cz[2];
       if (p[2] + oz < ground) inside |= 1u << k;
     }
   }
-  while (near) {
-    const int g = __builtin_ctz(near);
-    near &= near - 1u;
+  // ---- pass 2: gates inside the sphere: plane-slab / outer-box / hole culls, then the lattice ----
+  while (sph) {
+    const int g = __builtin_ctz(sph);
+    sph &= sph - 1u;
     const float* gr = tab.gate(type, lvl, g);
     float d[3] = {p[0] - gr[0], p[1] - gr[1], p[2] - gr[2]};
-    float dg[3], Ag[3], Bg[3], Cg[3];
+    float dg[3];
     gate_frame(gr, d, dg);
+    const float x = gr_fabsf(dg[0]), y = gr_fabsf(dg[1]), z = gr_fabsf(dg[2]);
+    const bool slab = z <= gr[15] + reach;
+    const bool outer = (x <= gr[16] + reach) & (y <= gr[17] + reach);
+    const bool hole = (x < gr[7] - reach) & (y < gr[11] - reach);
+    if (!(slab & outer & !hole)) continue;
+    float Ag[3], Bg[3], Cg[3];
     gate_frame(gr, A, Ag);
     gate_frame(gr, B, Bg);
     gate_frame(gr, Cz, Cg);
+#pragma unroll
     for (int k = 0; k < 17; ++k) {
       const float lx = c_lattice[k][0], ly = c_lattice[k][1], lz = c_lattice[k][2];
       float l0 = dg[0] + ((lx * Ag[0] + ly * Bg[0]) + lz * Cg[0]);
@@ -262,11 +268,11 @@ DEV int collision_count(const KArgs& a, const Tab& tab, int type, int lvl, const
 DEV void ctbr_compute(const KArgs& a, const float cmd[4], const float wb[3], const float ab[3], const float Kp[3],
                       const float Kd[3], float cT, const float ct[3], float& T, float tau[3], float mw[4],
                       float tt[4]) {
-  float T_des = gr_clampf(cmd[0], a.thrust_lo, a.thrust_hi);
+  float T_des = gr_clampf(cmd[0], a.kc->thrust_lo, a.kc->thrust_hi);
   T = (1.0f - cT) * T_des + cT * T;
-  const float* J = a.cfg.inertia;
+  const float* J = a.kc->cfg.inertia;
   float err[3], Jw[3], cr[3];
-  for (int i = 0; i < 3; ++i) err[i] = gr_clampf(cmd[i + 1], -a.cfg.body_rate_bound, a.cfg.body_rate_bound) - wb[i];
+  for (int i = 0; i < 3; ++i) err[i] = gr_clampf(cmd[i + 1], -a.kc->cfg.body_rate_bound, a.kc->cfg.body_rate_bound) - wb[i];
   for (int i = 0; i < 3; ++i) Jw[i] = J[i] * wb[i];
   cross3(wb, Jw, cr);
   for (int i = 0; i < 3; ++i) {
@@ -274,18 +280,18 @@ DEV void ctbr_compute(const KArgs& a, const float cmd[4], const float wb[3], con
     tau[i] = (1.0f - ct[i]) * tdes + ct[i] * tau[i];
   }
   tt[0] = T; tt[1] = tau[0]; tt[2] = tau[1]; tt[3] = tau[2];
-  if (!a.cfg.use_motor_model) return;
+  if (!a.h.use_motor_model) return;
   float f[4];
   for (int r = 0; r < 4; ++r)
-    f[r] = ((tt[0] * a.Bi[r][0] + tt[1] * a.Bi[r][1]) + tt[2] * a.Bi[r][2]) + tt[3] * a.Bi[r][3];
+    f[r] = ((tt[0] * a.kc->Bi[r][0] + tt[1] * a.kc->Bi[r][1]) + tt[2] * a.kc->Bi[r][2]) + tt[3] * a.kc->Bi[r][3];
   for (int i = 0; i < 4; ++i) {
-    float fd = gr_clampf(f[i], 0.0f, a.motor_fmax);
-    float t3 = a.tm_k1sq - a.tm_4k2 * (a.tm_k0 - fd);
-    float wdes = a.tm_inv2k2 * (a.tm_negk1 + gr_sqrtf(t3));
-    mw[i] = a.motor_c * mw[i] + (1.0f - a.motor_c) * wdes;
-    f[i] = (a.tm_k2 * mw[i] * mw[i] + a.tm_k1 * mw[i]) + a.tm_k0;
+    float fd = gr_clampf(f[i], 0.0f, a.kc->motor_fmax);
+    float t3 = a.kc->tm_k1sq - a.kc->tm_4k2 * (a.kc->tm_k0 - fd);
+    float wdes = a.kc->tm_inv2k2 * (a.kc->tm_negk1 + gr_sqrtf(t3));
+    mw[i] = a.kc->motor_c * mw[i] + (1.0f - a.kc->motor_c) * wdes;
+    f[i] = (a.kc->tm_k2 * mw[i] * mw[i] + a.kc->tm_k1 * mw[i]) + a.kc->tm_k0;
   }
-  for (int r = 0; r < 4; ++r) tt[r] = ((f[0] * a.B[r][0] + f[1] * a.B[r][1]) + f[2] * a.B[r][2]) + f[3] * a.B[r][3];
+  for (int r = 0; r < 4; ++r) tt[r] = ((f[0] * a.kc->B[r][0] + f[1] * a.kc->B[r][1]) + f[2] * a.kc->B[r][2]) + f[3] * a.kc->B[r][3];
 }
 
 // ------------------------------------------------------------- integrators
@@ -340,14 +346,17 @@ DEV void si_substep(float m, const float J[3], const float fb[3], const float tb
 
 // ------------------------------------------------------------- reset
 DEV void reset_env(const KArgs& a, const Tab& tab, Env& e, uint32_t gid) {
-  const gr_config& c = a.cfg;
+  const gr_config& c = a.kc->cfg;
   int up = e.acc >= c.level_up_threshold, down = e.acc < c.level_down_threshold;
   int lvl = e.lvl + up - down;
   uint32_t ep = (uint32_t)e.epoch + 1u;
-  gr_u32x4 r0 = draw(a, gid, ep, GR_TAG_RESET, 0), r1 = draw(a, gid, ep, GR_TAG_RESET, 1);
-  gr_u32x4 r2 = draw(a, gid, ep, GR_TAG_RESET, 2), r3 = draw(a, gid, ep, GR_TAG_RESET, 3);
-  gr_u32x4 r4 = draw(a, gid, ep, GR_TAG_RESET, 4), r5 = draw(a, gid, ep, GR_TAG_RESET, 5);
-  if (lvl >= c.num_levels) lvl = (int)gr_floorf(gr_u01(r4.w) * (float)c.num_levels);
+  // 24 x 21-bit fields: pos 0-2, att 3-5, vel 6-11, z-drag 12, k2 13-15, k1 16-18, level 19, thr 20-21
+  uint32_t f[24];
+  gr_fields6(draw(a, gid, ep, GR_TAG_RESET, 0), f);
+  gr_fields6(draw(a, gid, ep, GR_TAG_RESET, 1), f + 6);
+  gr_fields6(draw(a, gid, ep, GR_TAG_RESET, 2), f + 12);
+  gr_fields6(draw(a, gid, ep, GR_TAG_RESET, 3), f + 18);
+  if (lvl >= c.num_levels) lvl = (int)gr_floorf(gr_f21(f[19]) * (float)c.num_levels);
   else if (lvl < 0) lvl = 0;
   if (c.noise_curriculum) {
     float upf = e.acc >= c.noise_enhance_threshold ? 1.0f + c.noise_enhance : 1.0f;
@@ -356,18 +365,12 @@ DEV void reset_env(const KArgs& a, const Tab& tab, Env& e, uint32_t gid) {
     e.nl = e.nl * dnf;
   }
   e.lvl = lvl;
-  float rp[6] = {gr_uniform(r0.x, -c.reset_pos_half[0], c.reset_pos_half[0]),
-                 gr_uniform(r0.y, -c.reset_pos_half[1], c.reset_pos_half[1]),
-                 gr_uniform(r0.z, -c.reset_pos_half[2], c.reset_pos_half[2]),
-                 gr_uniform(r0.w, -c.reset_att_half[0], c.reset_att_half[0]),
-                 gr_uniform(r1.x, -c.reset_att_half[1], c.reset_att_half[1]),
-                 gr_uniform(r1.y, -c.reset_att_half[2], c.reset_att_half[2])};
-  float rv[6] = {gr_uniform(r1.z, -c.reset_vel_half[0], c.reset_vel_half[0]),
-                 gr_uniform(r1.w, -c.reset_vel_half[1], c.reset_vel_half[1]),
-                 gr_uniform(r2.x, -c.reset_vel_half[2], c.reset_vel_half[2]),
-                 gr_uniform(r2.y, -c.reset_vel_half[3], c.reset_vel_half[3]),
-                 gr_uniform(r2.z, -c.reset_vel_half[4], c.reset_vel_half[4]),
-                 gr_uniform(r2.w, -c.reset_vel_half[5], c.reset_vel_half[5])};
+  float rp[6], rv[6];
+  for (int k = 0; k < 3; ++k) {
+    rp[k] = gr_uniform21(f[k], -c.reset_pos_half[k], c.reset_pos_half[k]);
+    rp[3 + k] = gr_uniform21(f[3 + k], -c.reset_att_half[k], c.reset_att_half[k]);
+  }
+  for (int k = 0; k < 6; ++k) rv[k] = gr_uniform21(f[6 + k], -c.reset_vel_half[k], c.reset_vel_half[k]);
   for (int k = 0; k < 3; ++k) e.p[k] = c.spawn_pos[k] + rp[k];
   const float* rec = tab.rec(e.type, lvl);
   int start = (int)rec[2];
@@ -385,9 +388,9 @@ DEV void reset_env(const KArgs& a, const Tab& tab, Env& e, uint32_t gid) {
   for (int k = 0; k < 3; ++k) { e.tau[k] = 0.0f; e.al[k] = 0.0f; }
   for (int k = 0; k < 4; ++k) e.mw[k] = 0.0f;
   if (c.random_drag) {
-    float z = c.z_drag + gr_u01(r3.x) * c.z_drag_rand;
-    float u2[3] = {gr_u01(r3.y), gr_u01(r3.z), gr_u01(r3.w)};
-    float u1[3] = {gr_u01(r4.x), gr_u01(r4.y), gr_u01(r4.z)};
+    float z = c.z_drag + gr_f21(f[12]) * c.z_drag_rand;
+    float u2[3] = {gr_f21(f[13]), gr_f21(f[14]), gr_f21(f[15])};
+    float u1[3] = {gr_f21(f[16]), gr_f21(f[17]), gr_f21(f[18])};
     for (int k = 0; k < 3; ++k) {
       e.k2[k] = c.drag2[k] * e.mc + u2[k] * c.drag2_rand;
       e.k1[k] = c.drag1[k] * e.mc + u1[k] * c.drag1_rand;
@@ -396,7 +399,7 @@ DEV void reset_env(const KArgs& a, const Tab& tab, Env& e, uint32_t gid) {
     e.k1[2] = e.k1[2] * z;
   }
   float z0, z1;
-  gr_box_muller(r5.x, r5.y, &z0, &z1);
+  gr_box_muller21(f[20], f[21], &z0, &z1);
   e.thr = 1.0f + z0 * 0.01f;
   for (int k = 0; k < 7; ++k) e.es[k] = 0.0f;
   e.mar = 0.0f;
@@ -407,16 +410,18 @@ DEV void reset_env(const KArgs& a, const Tab& tab, Env& e, uint32_t gid) {
 }
 
 // ------------------------------------------------------------- observations
-DEV void gate_noise(const KArgs& a, const Env& e, uint32_t gid, int which, float out[3]) {
+// gate-pose noise of the current (out[0..2]) and next (out[3..5]) gate: one draw
+// per (episode, gates passed), commands.py:287-289,329-350
+DEV void gate_noise(const KArgs& a, const Env& e, uint32_t gid, float out[6]) {
 #ifdef GR_ABL_NOGATENOISE
-  if (true) { out[0] = out[1] = out[2] = 0.0f; return; }
+  if (true) { for (int k = 0; k < 6; ++k) out[k] = 0.0f; return; }
 #endif
-  if (!a.cfg.add_gate_noise) { out[0] = out[1] = out[2] = 0.0f; return; }
-  gr_u32x4 b = draw(a, gid, (uint32_t)e.epoch, GR_TAG_GATE, (uint32_t)(2 * e.acc + which));
-  uint32_t wv[3] = {b.x, b.y, b.z};
-  for (int k = 0; k < 3; ++k) {
-    float lo = (-a.cfg.gate_noise_pos[k]) * e.nl, hi = a.cfg.gate_noise_pos[k] * e.nl;
-    out[k] = lo + gr_u01(wv[k]) * (hi - lo);
+  if (!a.kc->cfg.add_gate_noise) { for (int k = 0; k < 6; ++k) out[k] = 0.0f; return; }
+  uint32_t f[6];
+  gr_fields6(draw(a, gid, (uint32_t)e.epoch, GR_TAG_GATE, (uint32_t)e.acc), f);
+  for (int k = 0; k < 6; ++k) {
+    float lo = (-a.kc->cfg.gate_noise_pos[k % 3]) * e.nl, hi = a.kc->cfg.gate_noise_pos[k % 3] * e.nl;
+    out[k] = lo + gr_f21(f[k]) * (hi - lo);
   }
 }
 
@@ -429,14 +434,15 @@ struct ObsNoise {
 
 DEV void obs_noise(const KArgs& a, uint32_t gid, uint32_t cnt, ObsNoise& on) {
   float nz[6] = {0, 0, 0, 0, 0, 0};
-  if (a.cfg.obs_noise) {
-    gr_u32x4 b0 = draw(a, gid, cnt, GR_TAG_OBS, 0), b1 = draw(a, gid, cnt, GR_TAG_OBS, 1);
-    gr_box_muller(b0.x, b0.y, &nz[0], &nz[1]);
-    gr_box_muller(b0.z, b0.w, &nz[2], &nz[3]);
-    gr_box_muller(b1.x, b1.y, &nz[4], &nz[5]);
+  if (a.h.obs_noise) {
+    uint32_t f[6];
+    gr_fields6(draw(a, gid, cnt, GR_TAG_OBS, 0), f);
+    gr_box_muller21(f[0], f[1], &nz[0], &nz[1]);
+    gr_box_muller21(f[2], f[3], &nz[2], &nz[3]);
+    gr_box_muller21(f[4], f[5], &nz[4], &nz[5]);
   }
-  for (int k = 0; k < 3; ++k) on.vfac[k] = 1.0f + nz[k] * a.cfg.obs_lin_vel_noise;
-  quat_from_euler_xyz(nz[3] * a.cfg.obs_att_noise, nz[4] * a.cfg.obs_att_noise, nz[5] * a.cfg.obs_att_noise, on.qn);
+  for (int k = 0; k < 3; ++k) on.vfac[k] = 1.0f + nz[k] * a.h.obs_lin_vel_noise;
+  quat_from_euler_xyz(nz[3] * a.h.obs_att_noise, nz[4] * a.h.obs_att_noise, nz[5] * a.h.obs_att_noise, on.qn);
 }
 
 DEV void write_obs(const KArgs& a, const Tab& tab, const Env& e, int i, uint32_t gid, const ObsNoise& on,
@@ -464,11 +470,10 @@ DEV void write_obs(const KArgs& a, const Tab& tab, const Env& e, int i, uint32_t
   float qq[4], r2n[3];
   quat_mul(e.q, on.qn, qq);
   matrix_row2(qq, r2n);
-  float ng0[3], ng1[3];
-  gate_noise(a, e, gid, 0, ng0);
-  gate_noise(a, e, gid, 1, ng1);
-  float gw[3] = {g0[0] + ng0[0], g0[1] + ng0[1], g0[2] + ng0[2]};
-  float gnw[3] = {gn0[0] + ng1[0], gn0[1] + ng1[1], gn0[2] + ng1[2]};
+  float gnz[6];
+  gate_noise(a, e, gid, gnz);
+  float gw[3] = {g0[0] + gnz[0], g0[1] + gnz[1], g0[2] + gnz[2]};
+  float gnw[3] = {gn0[0] + gnz[3], gn0[1] + gnz[4], gn0[2] + gnz[5]};
   float dp[3] = {gw[0] - e.p[0], gw[1] - e.p[1], gw[2] - e.p[2]};
   float dnp[3] = {gnw[0] - gw[0], gnw[1] - gw[1], gnw[2] - gw[2]};
   float pg[3], pn[3];
@@ -515,25 +520,92 @@ DEV void wave_log(const KArgs& a, const float lg[GR_LOG_SLOTS], bool reset_lane,
   }
 }
 
+// ------------------------------------------------------------- gate table staging
+// The workgroup's slice of the track table (its terrain types x all levels) is
+// loaded into registers together with the state loads, and written to LDS only
+// when the collision test needs it: the barrier then waits for loads that have
+// long landed, while the controller and integrator run under the load latency.
+constexpr int GR_TREG = 2;  // float4 per thread held in registers (one 8-gate type: 410 float4)
+
+__device__ __forceinline__ void table_commit(const float4* src, int nvec, float4 r0, float4 r1, float4* lds) {
+  const int t = threadIdx.x;
+  if (t < nvec) lds[t] = r0;
+  if (t + GR_BLOCK < nvec) lds[t + GR_BLOCK] = r1;
+  for (int idx = t + GR_TREG * GR_BLOCK; idx < nvec; idx += GR_BLOCK) lds[idx] = src[idx];
+  __syncthreads();
+}
+
+// ------------------------------------------------------------- diagnostic stamps
+// -DGR_STAMPS (diagnostic build only, scripts/stamps.py): lane 0 of every wave
+// records s_memtime at phase boundaries and s_memrealtime at entry/exit into a
+// buffer nothing else reads.  The product build compiles these away.
+#ifdef GR_STAMPS
+__device__ unsigned long long g_stamps[GR_STAMP_WAVES * GR_STAMP_SLOTS];
+#define STAMP(k)                                                                              \
+  do {                                                                                        \
+    unsigned long long t_ = __builtin_amdgcn_s_memtime();                                    \
+    const unsigned w_ = blockIdx.x * (GR_BLOCK / 64) + (threadIdx.x >> 6);                    \
+    if ((threadIdx.x & 63) == 0 && w_ < GR_STAMP_WAVES) g_stamps[w_ * GR_STAMP_SLOTS + (k)] = t_; \
+  } while (0)
+#define RSTAMP(k)                                                                             \
+  do {                                                                                        \
+    unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                \
+    const unsigned w_ = blockIdx.x * (GR_BLOCK / 64) + (threadIdx.x >> 6);                    \
+    if ((threadIdx.x & 63) == 0 && w_ < GR_STAMP_WAVES) g_stamps[w_ * GR_STAMP_SLOTS + (k)] = t_; \
+  } while (0)
+#else
+#define STAMP(k)
+#define RSTAMP(k)
+#endif
+
 // ------------------------------------------------------------- the kernel
 template <int MODE, bool USE_LDS>
-__global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const float* __restrict__ actions,
+__global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const KConst* __restrict__ kc,
+                                                        const float* __restrict__ actions,
                                                         const uint8_t* __restrict__ mask) {
+  a.kc = kc;  // constants through the noalias argument: scalar loads at their uses
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
-  const int n = a.cfg.num_envs;
+  const int n = a.h.num_envs;
   const int i = blockIdx.x * GR_BLOCK + threadIdx.x;
   const bool live = i < n;
   const int ii = live ? i : n - 1;  // dead lanes mirror the last env (loads stay in bounds, no stores)
-  const gr_config& c = a.cfg;
+  const gr_config& c = a.kc->cfg;
   const uint32_t gid = gid_of(a, ii);
+  RSTAMP(9);
+  STAMP(0);
 
-  // ---- 1. issue every HBM load of this lane first ----
-  Env e;
-  load_env(a, ii, e);
+  // ---- 1. issue every load of this lane first, in order of use ----
+  const uint32_t cnt = a.buf.counters[a.buf.counter_index];  // wave-uniform (scalar) load
   float4 act = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (MODE == KMODE_STEP) act = reinterpret_cast<const float4*>(actions)[ii];
-  const uint32_t cnt = a.buf.counters[a.buf.counter_index];
+  Env e;
+  load_env(a, ii, e);
+  // this workgroup's terrain types (type = floor(i / (N / T)), IL TerrainImporter layout),
+  // derived on the host per workgroup: one scalar load
+  const int bt = a.blk_types[blockIdx.x];
+  const int t0 = bt & 0xffff, t1 = bt >> 16;
+  Tab tab;
+  tab.L = a.h.num_levels;
+  tab.G = a.h.max_gates;
+  tab.stride = a.h.track_stride;
+  tab.t0 = t0;
+  tab.base = USE_LDS ? reinterpret_cast<const float*>(lds_tab) : a.table + (size_t)t0 * tab.L * tab.stride;
+  // table slice loads (clamped, always in bounds; the commit skips the extras)
+  const float4* tsrc = reinterpret_cast<const float4*>(a.table + (size_t)t0 * tab.L * tab.stride);
+  const int tnvec = (t1 - t0 + 1) * tab.L * tab.stride / 4;
+  float4 tr0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), tr1 = tr0;
+  if (USE_LDS) {
+    tr0 = tsrc[min((int)threadIdx.x, tnvec - 1)];
+    tr1 = tsrc[min((int)threadIdx.x + GR_BLOCK, tnvec - 1)];
+  }
 
+  STAMP(12);
+#ifdef GR_STAMPS
+  __asm__ volatile("" ::"s"(cnt));  // diagnostic: when the counter load has landed
+  STAMP(13);
+  __asm__ volatile("" ::"v"(e.ep));  // diagnostic: when the first vector load (istate) has landed
+  STAMP(14);
+#endif
   // ---- 2. load-independent work: observation noise (Philox + Box-Muller) ----
   ObsNoise on;
 #ifndef GR_ABL_NOOBSNOISE
@@ -542,32 +614,14 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const float* __r
   for (int k = 0; k < 3; ++k) on.vfac[k] = 1.0f;
   on.qn[0] = 1.0f; on.qn[1] = on.qn[2] = on.qn[3] = 0.0f;
 #endif
-
-  // ---- 3. stage the gate geometry of this workgroup's terrain types in LDS ----
-  const int first_env = blockIdx.x * GR_BLOCK;
-  const int last_env = min(first_env + GR_BLOCK, n) - 1;
-  int t0 = 0, t1 = 0;
-  for (int t = 1; t < c.num_types; ++t) {
-    t0 += first_env >= a.type_start[t];
-    t1 += last_env >= a.type_start[t];
-  }
-  Tab tab;
-  tab.L = c.num_levels;
-  tab.G = c.max_gates;
-  tab.stride = a.track_stride;
-  tab.t0 = t0;
-  if (USE_LDS) {
-    const float4* src = reinterpret_cast<const float4*>(a.table + (size_t)t0 * tab.L * tab.stride);
-    const int nvec = (t1 - t0 + 1) * tab.L * tab.stride / 4;
-    for (int k = threadIdx.x; k < nvec; k += GR_BLOCK) lds_tab[k] = src[k];
-    __syncthreads();
-    tab.base = reinterpret_cast<const float*>(lds_tab);
-  } else {
-    tab.base = a.table + (size_t)t0 * tab.L * tab.stride;
-  }
+  STAMP(1);
   // call counter for the observation-noise stream: double-buffered by call parity,
   // so this write never races with the reads of the current launch
   if (threadIdx.x == 0 && blockIdx.x == 0) a.buf.counters[a.buf.counter_index ^ 1] = cnt + 1u;
+  // the table is needed first by the collision test (step + explicit integrator) or right away
+  const bool late_table = MODE == KMODE_STEP && c.integrator == GR_INTEGRATOR_DD_EXPLICIT;
+  if (USE_LDS && !late_table) table_commit(tsrc, tnvec, tr0, tr1, lds_tab);
+  STAMP(2);
 
   float lg[GR_LOG_SLOTS];
   for (int s = 0; s < GR_LOG_SLOTS; ++s) lg[s] = 0.0f;
@@ -575,7 +629,9 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const float* __r
 
   if (MODE == KMODE_STEP) {
     const float dt = c.step_dt;
-    const float lin_prev = norm3(e.v), ang_prev = norm3(e.w), mar_prev = e.mar;
+    // pre-step speeds for the episode metrics (commands.py:247-260): norms taken only for resets
+    const float v_prev[3] = {e.v[0], e.v[1], e.v[2]}, w_prev[3] = {e.w[0], e.w[1], e.w[2]};
+    const float mar_prev = e.mar;
     // DiffActionManager.process_action + one-step lag.  The lag plane holds the
     // *squashed* previous action tanh(a_{t-1}): the reference only ever uses
     // tanh() of the lagged / previous raw action, so each action is squashed once.
@@ -600,9 +656,12 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const float* __r
     int ccount = 0;
     if (c.integrator == GR_INTEGRATOR_DD_EXPLICIT) {
       dd_explicit(m, Jp, e.k2, e.k1, tt, dt, c.gravity, e.p, e.q, e.v, e.w, accl, al);
+      STAMP(3);
+      if (USE_LDS) table_commit(tsrc, tnvec, tr0, tr1, lds_tab);
 #ifndef GR_ABL_NOCOLL
       ccount = collision_count(a, tab, e.type, e.lvl, e.p, e.q);
 #endif
+      STAMP(4);
     } else {
       float vb[3], fb[3] = {0.0f, 0.0f, tt[0]};
       quat_rotate_inverse(e.q, e.v, vb);
@@ -649,7 +708,7 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const float* __r
     f[6] = (float)bad;
     float rew = 0.0f;
     for (int k = 0; k < 7; ++k) {
-      const float wk = a.w[k];
+      const float wk = a.kc->w[k];
       if (wk == 0.0f) continue;
       float v = (f[k] * wk) * dt;
       rew = rew + v;
@@ -658,11 +717,14 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const float* __r
     const float aux = near_gate ? 1.0f : 0.0f;
     e.mar = f[2];
     const int done = terminated | time_out;
+    STAMP(5);
     if (live) {
       a.buf.reward[i] = rew;
       a.buf.terminated[i] = (uint8_t)terminated;
       a.buf.time_out[i] = (uint8_t)time_out;
       a.buf.dones[i] = (int64_t)done;
+      // continuing envs: the per-step planes are final now; let them drain while the rest runs
+      if (!done) store_dyn(a, i, e);
     }
 #ifndef GR_ABL_NORESET
     if (done && live) {
@@ -674,12 +736,14 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const float* __r
       lg[GR_LOG_NRESET] = 1.0f;
       lg[GR_LOG_ACC] = (float)e.acc;
       lg[GR_LOG_M_ACTRATE] = mar_prev;
-      lg[GR_LOG_M_LINSPD] = lin_prev;
-      lg[GR_LOG_M_ANGSPD] = ang_prev;
+      lg[GR_LOG_M_LINSPD] = norm3(v_prev);
+      lg[GR_LOG_M_ANGSPD] = norm3(w_prev);
       lg[GR_LOG_T_TIMEOUT] = (float)time_out;
       lg[GR_LOG_T_CONTACT] = (float)c_term;
       lg[GR_LOG_T_BADPOSE] = (float)bad;
       reset_env(a, tab, e, gid);
+      store_dyn(a, i, e);
+      store_rst(a, i, e);
     }
     // command compute: _update_metrics + _update_command (commands.py:247-260, 308-350)
     {
@@ -695,12 +759,14 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const float* __r
     float lc[4];
     for (int k = 0; k < 4; ++k) lc[k] = th_raw[k] * sc[k] + of[k];
     lc[0] = lc[0] / e.mc;
+    STAMP(6);
     if (live) {
+      store_istate(a, i, e);
 #ifndef GR_ABL_NOOBS
       write_obs(a, tab, e, i, gid, on, lc, aux);
 #endif
-      store_env(a, i, e, done != 0, false);
     }
+    STAMP(7);
   } else {
     // MODE_RESET / MODE_OBSERVE: last action and aux carry over from the previous observation
     const float4 lcv = reinterpret_cast<const float4*>(a.buf.prev_obs_critic)[(size_t)ii * 4 + 3];
@@ -719,19 +785,34 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const float* __r
     }
     if (live) {
       write_obs(a, tab, e, i, gid, on, lc, aux);
-      if (reset_lane) store_env(a, i, e, true, false);
+      if (reset_lane) {
+        store_dyn(a, i, e);
+        store_rst(a, i, e);
+        store_istate(a, i, e);
+      }
     }
   }
   // (observe calls reset nothing: their rows say so, and the finalized log repeats the previous one)
 #ifndef GR_ABL_NOLOG
   wave_log(a, lg, reset_lane, live ? (float)e.lvl : 0.0f, live ? e.nl : 0.0f);
 #endif
+  STAMP(8);
+  RSTAMP(10);
+#ifdef GR_STAMPS
+  if ((threadIdx.x & 63) == 0 && blockIdx.x * (GR_BLOCK / 64) + (threadIdx.x >> 6) < GR_STAMP_WAVES) {
+    unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));  // HW_ID (hwreg 4), all 32 bits
+    unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));  // XCC_ID (hwreg 20), 16 bits
+    g_stamps[(blockIdx.x * (GR_BLOCK / 64) + (threadIdx.x >> 6)) * GR_STAMP_SLOTS + 11] =
+        ((unsigned long long)xcc << 32) | hw;
+  }
+#endif
 }
 
 // ------------------------------------------------------------- init (startup events)
-__global__ __launch_bounds__(GR_BLOCK) void init_kernel(KArgs a) {
+__global__ __launch_bounds__(GR_BLOCK) void init_kernel(KArgs a, const KConst* __restrict__ kc) {
+  a.kc = kc;
   const int i = blockIdx.x * GR_BLOCK + threadIdx.x;
-  const gr_config& c = a.cfg;
+  const gr_config& c = a.kc->cfg;
   if (i >= c.num_envs) return;
   const uint32_t gid = gid_of(a, i);
   Env e;
@@ -779,9 +860,19 @@ __global__ __launch_bounds__(GR_BLOCK) void init_kernel(KArgs a) {
   e.mar = 0.0f;
   e.ep = 0; e.acc = 0; e.epoch = 0; e.gate = 0; e.azero = 1;
   int type = 0;
-  for (int t = 1; t < c.num_types; ++t) type += (i >= a.type_start[t]);
+  for (int t = 1; t < c.num_types; ++t) type += (i >= a.kc->type_start[t]);
   e.type = type;
-  store_env(a, i, e, true, true);
+  store_dyn(a, i, e);
+  store_rst(a, i, e);
+  store_istate(a, i, e);
+  {  // startup-DR parameter planes (written once)
+    float4* S = reinterpret_cast<float4*>(a.buf.state);
+    const size_t n = (size_t)c.num_envs;
+    S[GR_P_PAR0 * n + i] = make_float4(e.Kp[0], e.Kp[1], e.Kp[2], e.cT);
+    S[GR_P_PAR1 * n + i] = make_float4(e.Kd[0], e.Kd[1], e.Kd[2], e.mp);
+    S[GR_P_PAR2 * n + i] = make_float4(e.ct[0], e.ct[1], e.ct[2], e.mc);
+    S[GR_P_PAR3 * n + i] = make_float4(e.J[0], e.J[1], e.J[2], 0.0f);
+  }
   // initial observation buffers: last action = ctbr(0) (DiffActions._raw_actions starts at zero)
   float sc[4], of[4];
   action_scale(a, e.mc, sc, of);
@@ -842,9 +933,10 @@ __global__ __launch_bounds__(256) void log_finalize_kernel(const float* __restri
 }
 
 // ------------------------------------------------------------- test kernels
-__global__ void test_dynamics_kernel(KArgs a, int n, int mode, const float* si, const float* ab, const float* cmd,
-                                     const float* ci, const float* par, const float* drag, float* so, float* co,
-                                     float* xo) {
+__global__ void test_dynamics_kernel(KArgs a, const KConst* __restrict__ kc, int n, int mode, const float* si,
+                                     const float* ab, const float* cmd, const float* ci, const float* par,
+                                     const float* drag, float* so, float* co, float* xo) {
+  a.kc = kc;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float p[3], q[4], v[3], w[3], acc[3], al[3], tt[4], T = ci[i * 4], tau[3] = {ci[i * 4 + 1], ci[i * 4 + 2], ci[i * 4 + 3]};
@@ -857,7 +949,7 @@ __global__ void test_dynamics_kernel(KArgs a, int n, int mode, const float* si, 
   } else {
     for (int k = 0; k < 4; ++k) tt[k] = cmd[i * 4 + k];
   }
-  dd_explicit(pr[7], pr + 12, drag + i * 6, drag + i * 6 + 3, tt, a.cfg.step_dt, a.cfg.gravity, p, q, v, w, acc, al);
+  dd_explicit(pr[7], pr + 12, drag + i * 6, drag + i * 6 + 3, tt, a.kc->cfg.step_dt, a.kc->cfg.gravity, p, q, v, w, acc, al);
   for (int k = 0; k < 3; ++k) { so[i * 13 + k] = p[k]; so[i * 13 + 7 + k] = v[k]; so[i * 13 + 10 + k] = w[k]; }
   for (int k = 0; k < 4; ++k) so[i * 13 + 3 + k] = q[k];
   co[i * 4] = T;
@@ -896,11 +988,11 @@ static int grid_of(int n) { return (n + GR_BLOCK - 1) / GR_BLOCK; }
 
 template <int MODE>
 static hipError_t launch_env_mode(const KArgs& a, const float* actions, const uint8_t* mask, hipStream_t s) {
-  const int g = grid_of(a.cfg.num_envs);
-  if (a.lds_bytes > 0) {
-    hipLaunchKernelGGL((env_kernel<MODE, true>), dim3(g), dim3(GR_BLOCK), a.lds_bytes, s, a, actions, mask);
+  const int g = grid_of(a.h.num_envs);
+  if (a.h.lds_bytes > 0) {
+    hipLaunchKernelGGL((env_kernel<MODE, true>), dim3(g), dim3(GR_BLOCK), a.h.lds_bytes, s, a, a.kc, actions, mask);
   } else {
-    hipLaunchKernelGGL((env_kernel<MODE, false>), dim3(g), dim3(GR_BLOCK), 0, s, a, actions, mask);
+    hipLaunchKernelGGL((env_kernel<MODE, false>), dim3(g), dim3(GR_BLOCK), 0, s, a, a.kc, actions, mask);
   }
   return hipGetLastError();
 }
@@ -927,15 +1019,15 @@ hipError_t launch_log_finalize(const float* rows, int nrows, const float* prev, 
 }
 
 hipError_t launch_init(const KArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(init_kernel, dim3(grid_of(a.cfg.num_envs)), dim3(GR_BLOCK), 0, s, a);
+  hipLaunchKernelGGL(init_kernel, dim3(grid_of(a.h.num_envs)), dim3(GR_BLOCK), 0, s, a, a.kc);
   return hipGetLastError();
 }
 
 hipError_t launch_test_dynamics(const KArgs& a, int n, int mode, const float* si, const float* ab, const float* cmd,
                                 const float* ci, const float* par, const float* drag, float* so, float* co, float* xo,
                                 hipStream_t s) {
-  hipLaunchKernelGGL(test_dynamics_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, n, mode, si, ab, cmd, ci, par,
-                     drag, so, co, xo);
+  hipLaunchKernelGGL(test_dynamics_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, a.kc, n, mode, si, ab, cmd, ci,
+                     par, drag, so, co, xo);
   return hipGetLastError();
 }
 
@@ -948,6 +1040,18 @@ hipError_t launch_test_philox(int n, uint32_t c0, uint32_t c1, uint32_t c2, uint
                               uint32_t* out, hipStream_t s) {
   hipLaunchKernelGGL(test_philox_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, c0, c1, c2, c3, k0, k1, out);
   return hipGetLastError();
+}
+
+hipError_t read_stamps(unsigned long long* host, int n) {
+#ifdef GR_STAMPS
+  if (n > GR_STAMP_WAVES * GR_STAMP_SLOTS) n = GR_STAMP_WAVES * GR_STAMP_SLOTS;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), (size_t)n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost);
+#else
+  (void)host;
+  (void)n;
+  return hipErrorNotSupported;
+#endif
 }
 
 }  // namespace gr

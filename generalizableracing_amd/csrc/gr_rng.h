@@ -19,6 +19,14 @@ typedef struct { uint32_t x, y, z, w; } gr_u32x4;
 
 GR_HD gr_u32x4 gr_philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                 uint32_t k0, uint32_t k1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  /* opaque key: the round-key schedule is recomputed per draw (two scalar adds per
+   * round) instead of being shared across every inlined draw and kept live in SGPRs */
+  __asm__ volatile("" : "+s"(k0), "+s"(k1));
+  /* fully unrolled: 262 vs 647 cycles per draw, and independent draws interleave
+   * (4 draws: ~175 cycles each) — tools/mathbench.hip on gfx950 */
+#pragma unroll
+#endif
   for (int i = 0; i < 10; ++i) {
     uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c0;
     uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c2;
@@ -52,10 +60,37 @@ GR_HD void gr_box_muller(uint32_t w0, uint32_t w1, float* z0, float* z1) {
   *z1 = rad * s;
 }
 
+/* Six 21-bit fields from one 128-bit draw (bits 0..125; 126-127 unused).  The
+ * per-step streams take 21-bit uniforms so one Philox block feeds six draws
+ * (a block costs ~650 cycles on gfx950, tools/mathbench.hip). */
+GR_HD void gr_fields6(gr_u32x4 r, uint32_t f[6]) {
+  f[0] = r.x & 0x1FFFFFu;
+  f[1] = (r.x >> 21) | ((r.y & 0x3FFu) << 11);
+  f[2] = (r.y >> 10) & 0x1FFFFFu;
+  f[3] = (r.y >> 31) | ((r.z & 0xFFFFFu) << 1);
+  f[4] = (r.z >> 20) | ((r.w & 0x1FFu) << 12);
+  f[5] = (r.w >> 9) & 0x1FFFFFu;
+}
+/* uniform in [0, 1) / (0, 1] from a 21-bit field (exact in fp32) */
+GR_HD float gr_f21(uint32_t f) { return (float)f * 4.76837158e-07f; }
+GR_HD float gr_f21_open0(uint32_t f) { return (float)(f + 1u) * 4.76837158e-07f; }
+/* torch-style U(lo, hi) = u * (hi - lo) + lo */
+GR_HD float gr_uniform21(uint32_t f, float lo, float hi) { return gr_f21(f) * (hi - lo) + lo; }
+/* Box-Muller from two 21-bit fields (radius tail truncated at 5.4 sigma) */
+GR_HD void gr_box_muller21(uint32_t f1, uint32_t f2, float* z0, float* z1) {
+  float u1 = gr_f21_open0(f1);
+  float u2 = gr_f21(f2);
+  float rad = gr_sqrtf(-2.0f * gr_logf(u1));
+  float s, c;
+  gr_sincosf(6.28318548f * u2, &s, &c);
+  *z0 = rad * c;
+  *z1 = rad * s;
+}
+
 /* stream tags (counter word 2) */
 #define GR_TAG_STATIC 0x53544154u /* startup DR: gains, delays, mass, inertia, initial level */
 #define GR_TAG_RESET 0x52535421u  /* per-episode reset draws, counter1 = epoch */
-#define GR_TAG_GATE 0x47415445u   /* gate-pose noise, counter1 = epoch, counter3 = 2*pass+j */
+#define GR_TAG_GATE 0x47415445u   /* gate-pose noise, counter1 = epoch, counter3 = gates passed */
 #define GR_TAG_OBS 0x4f425321u    /* observation noise, counter1 = call counter */
 
 #endif /* GR_RNG_H */

@@ -260,6 +260,10 @@ int gr_test_math(gr_ctx* ctx, int fn, int n, const float* x, const float* y2, fl
 /* Philox words for counters (c0+i, c1, c2, c3), key = ctx seed */
 int gr_test_philox(gr_ctx* ctx, int n, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t* out4,
                    void* stream);
+/* Diagnostic builds only (-DGR_STAMPS, scripts/stamps.py): copy the per-wave phase
+ * timestamps of the most recent step launch (12 u64 per wave).  Product builds
+ * return GR_ERR_STATE. */
+int gr_debug_read_stamps(uint64_t* host, int n);
 
 #ifdef __cplusplus
 }

@@ -388,13 +388,15 @@ void gro_init(const gr_config* c, gro_env* envs, int n, gro_out* out) {
 /* ------------------------------------------------------------------ reset */
 typedef struct logacc { double s[GR_LOG_SLOTS]; } logacc;
 
-static void gate_noise(const gr_config* c, const gro_env* e, uint32_t gid, int which, float out[3]) {
-  if (!c->add_gate_noise) { out[0] = out[1] = out[2] = 0.0f; return; }
-  gr_u32x4 b = draw(c, gid, (uint32_t)e->epoch, GR_TAG_GATE, (uint32_t)(2 * e->acc + which));
-  uint32_t wv[3] = {b.x, b.y, b.z};
-  for (int k = 0; k < 3; ++k) {
-    float lo = (-c->gate_noise_pos[k]) * e->noise_level, hi = c->gate_noise_pos[k] * e->noise_level;
-    out[k] = lo + gr_u01(wv[k]) * (hi - lo); /* commands.py:287-289 */
+/* noise of the current (out[0..2]) and next (out[3..5]) gate pose: one draw per
+ * (episode, gates passed); U(-r, r) * noise_level per axis, commands.py:287-289,329-350 */
+static void gate_noise(const gr_config* c, const gro_env* e, uint32_t gid, float out[6]) {
+  if (!c->add_gate_noise) { for (int k = 0; k < 6; ++k) out[k] = 0.0f; return; }
+  uint32_t f[6];
+  gr_fields6(draw(c, gid, (uint32_t)e->epoch, GR_TAG_GATE, (uint32_t)e->acc), f);
+  for (int k = 0; k < 6; ++k) {
+    float lo = (-c->gate_noise_pos[k % 3]) * e->noise_level, hi = c->gate_noise_pos[k % 3] * e->noise_level;
+    out[k] = lo + gr_f21(f[k]) * (hi - lo);
   }
 }
 
@@ -404,10 +406,13 @@ static void reset_env(const gr_config* c, gro_env* e, uint32_t gid, const gro_tr
   int up = e->acc >= c->level_up_threshold, down = e->acc < c->level_down_threshold;
   int lvl = e->level + up - down;
   uint32_t ep = (uint32_t)e->epoch + 1u;
-  gr_u32x4 r0 = draw(c, gid, ep, GR_TAG_RESET, 0), r1 = draw(c, gid, ep, GR_TAG_RESET, 1);
-  gr_u32x4 r2 = draw(c, gid, ep, GR_TAG_RESET, 2), r3 = draw(c, gid, ep, GR_TAG_RESET, 3);
-  gr_u32x4 r4 = draw(c, gid, ep, GR_TAG_RESET, 4), r5 = draw(c, gid, ep, GR_TAG_RESET, 5);
-  if (lvl >= c->num_levels) lvl = (int)gr_floorf(gr_u01(r4.w) * (float)c->num_levels);
+  /* 24 x 21-bit fields: pos 0-2, att 3-5, vel 6-11, z-drag 12, k2 13-15, k1 16-18, level 19, thr 20-21 */
+  uint32_t f[24];
+  gr_fields6(draw(c, gid, ep, GR_TAG_RESET, 0), f);
+  gr_fields6(draw(c, gid, ep, GR_TAG_RESET, 1), f + 6);
+  gr_fields6(draw(c, gid, ep, GR_TAG_RESET, 2), f + 12);
+  gr_fields6(draw(c, gid, ep, GR_TAG_RESET, 3), f + 18);
+  if (lvl >= c->num_levels) lvl = (int)gr_floorf(gr_f21(f[19]) * (float)c->num_levels);
   else if (lvl < 0) lvl = 0;
   if (c->noise_curriculum) { /* curriculums.py:40-54 + commands.py:385-402 */
     float upf = e->acc >= c->noise_enhance_threshold ? 1.0f + c->noise_enhance : 1.0f;
@@ -418,18 +423,12 @@ static void reset_env(const gr_config* c, gro_env* e, uint32_t gid, const gro_tr
   e->level = lvl;
   int track = track_index(c, e->type, lvl);
   /* reset_root_state_racing, events.py:139-177 (env-local frame: world - env_origin) */
-  float rp[6] = {gr_uniform(r0.x, -c->reset_pos_half[0], c->reset_pos_half[0]),
-                 gr_uniform(r0.y, -c->reset_pos_half[1], c->reset_pos_half[1]),
-                 gr_uniform(r0.z, -c->reset_pos_half[2], c->reset_pos_half[2]),
-                 gr_uniform(r0.w, -c->reset_att_half[0], c->reset_att_half[0]),
-                 gr_uniform(r1.x, -c->reset_att_half[1], c->reset_att_half[1]),
-                 gr_uniform(r1.y, -c->reset_att_half[2], c->reset_att_half[2])};
-  float rv[6] = {gr_uniform(r1.z, -c->reset_vel_half[0], c->reset_vel_half[0]),
-                 gr_uniform(r1.w, -c->reset_vel_half[1], c->reset_vel_half[1]),
-                 gr_uniform(r2.x, -c->reset_vel_half[2], c->reset_vel_half[2]),
-                 gr_uniform(r2.y, -c->reset_vel_half[3], c->reset_vel_half[3]),
-                 gr_uniform(r2.z, -c->reset_vel_half[4], c->reset_vel_half[4]),
-                 gr_uniform(r2.w, -c->reset_vel_half[5], c->reset_vel_half[5])};
+  float rp[6], rv[6];
+  for (int k = 0; k < 3; ++k) {
+    rp[k] = gr_uniform21(f[k], -c->reset_pos_half[k], c->reset_pos_half[k]);
+    rp[3 + k] = gr_uniform21(f[3 + k], -c->reset_att_half[k], c->reset_att_half[k]);
+  }
+  for (int k = 0; k < 6; ++k) rv[k] = gr_uniform21(f[6 + k], -c->reset_vel_half[k], c->reset_vel_half[k]);
   for (int k = 0; k < 3; ++k) e->p[k] = c->spawn_pos[k] + rp[k];
   int start = track_start(tr, track);
   const float* g0 = gate_rec(c, tr, track, start);
@@ -448,9 +447,9 @@ static void reset_env(const gr_config* c, gro_env* e, uint32_t gid, const gro_tr
   for (int k = 0; k < 3; ++k) { e->tau[k] = 0.0f; e->alpha[k] = 0.0f; }
   for (int k = 0; k < 4; ++k) e->motor_w[k] = 0.0f;
   if (c->random_drag) { /* droneDynamics.py:50-57 */
-    float z = c->z_drag + gr_u01(r3.x) * c->z_drag_rand;
-    float u2[3] = {gr_u01(r3.y), gr_u01(r3.z), gr_u01(r3.w)};
-    float u1[3] = {gr_u01(r4.x), gr_u01(r4.y), gr_u01(r4.z)};
+    float z = c->z_drag + gr_f21(f[12]) * c->z_drag_rand;
+    float u2[3] = {gr_f21(f[13]), gr_f21(f[14]), gr_f21(f[15])};
+    float u1[3] = {gr_f21(f[16]), gr_f21(f[17]), gr_f21(f[18])};
     for (int k = 0; k < 3; ++k) {
       e->k2[k] = c->drag2[k] * e->m_ctrl + u2[k] * c->drag2_rand;
       e->k1[k] = c->drag1[k] * e->m_ctrl + u1[k] * c->drag1_rand;
@@ -459,7 +458,7 @@ static void reset_env(const gr_config* c, gro_env* e, uint32_t gid, const gro_tr
     e->k1[2] = e->k1[2] * z;
   }
   float z0, z1;
-  gr_box_muller(r5.x, r5.y, &z0, &z1);
+  gr_box_muller21(f[20], f[21], &z0, &z1);
   e->thr_err = 1.0f + z0 * 0.01f;
   /* reward manager: episode sums; command manager: metrics + _resample_command (commands.py:262-306) */
   for (int k = 0; k < 7; ++k) e->ep_sum[k] = 0.0f;
@@ -490,20 +489,20 @@ static void compute_obs(const gr_config* c, gro_env* e, uint32_t gid, uint32_t c
   /* policy: observation.py:47-53 (lin vel noise), :22-32 (attitude noise), commands.py:208-221 (noisy gates) */
   float nz[6] = {0};
   if (c->obs_noise) { /* randn(N,3) for the velocity and for the attitude noise */
-    gr_u32x4 b0 = draw(c, gid, cnt, GR_TAG_OBS, 0), b1 = draw(c, gid, cnt, GR_TAG_OBS, 1);
-    gr_box_muller(b0.x, b0.y, &nz[0], &nz[1]);
-    gr_box_muller(b0.z, b0.w, &nz[2], &nz[3]);
-    gr_box_muller(b1.x, b1.y, &nz[4], &nz[5]);
+    uint32_t f[6];
+    gr_fields6(draw(c, gid, cnt, GR_TAG_OBS, 0), f);
+    gr_box_muller21(f[0], f[1], &nz[0], &nz[1]);
+    gr_box_muller21(f[2], f[3], &nz[2], &nz[3]);
+    gr_box_muller21(f[4], f[5], &nz[4], &nz[5]);
   }
   float qn[4], qq[4], r2n[3];
   quat_from_euler_xyz(nz[3] * c->obs_att_noise, nz[4] * c->obs_att_noise, nz[5] * c->obs_att_noise, qn);
   quat_mul(e->q, qn, qq);
   matrix_row2(qq, r2n);
-  float ng0[3], ng1[3];
-  gate_noise(c, e, gid, 0, ng0);
-  gate_noise(c, e, gid, 1, ng1);
-  float gw[3] = {g[0] + ng0[0], g[1] + ng0[1], g[2] + ng0[2]};
-  float gnw[3] = {gn[0] + ng1[0], gn[1] + ng1[1], gn[2] + ng1[2]};
+  float gnz[6];
+  gate_noise(c, e, gid, gnz);
+  float gw[3] = {g[0] + gnz[0], g[1] + gnz[1], g[2] + gnz[2]};
+  float gnw[3] = {gn[0] + gnz[3], gn[1] + gnz[4], gn[2] + gnz[5]};
   float dp[3] = {gw[0] - e->p[0], gw[1] - e->p[1], gw[2] - e->p[2]};
   float dnp[3] = {gnw[0] - gw[0], gnw[1] - gw[1], gnw[2] - gw[2]};
   float pg[3], pn[3];
@@ -760,5 +759,12 @@ void gro_test_philox(int n, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, 
   for (int i = 0; i < n; ++i) {
     gr_u32x4 r = gr_philox4x32_10(c0 + (uint32_t)i, c1, c2, c3, k0, k1);
     out4[i * 4] = r.x; out4[i * 4 + 1] = r.y; out4[i * 4 + 2] = r.z; out4[i * 4 + 3] = r.w;
+  }
+}
+
+void gro_test_fields6(int n, const uint32_t* in4, uint32_t* out6) {
+  for (int i = 0; i < n; ++i) {
+    gr_u32x4 r = {in4[i * 4], in4[i * 4 + 1], in4[i * 4 + 2], in4[i * 4 + 3]};
+    gr_fields6(r, out6 + i * 6);
   }
 }

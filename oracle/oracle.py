@@ -50,6 +50,7 @@ def load():
             "gro_test_dynamics": [vp, C.c_int, C.c_int] + [vp] * 9,
             "gro_test_math": [C.c_int, C.c_int, vp, vp, vp],
             "gro_test_philox": [C.c_int] + [C.c_uint32] * 6 + [vp],
+            "gro_test_fields6": [C.c_int, vp, vp],
         }.items():
             f = getattr(lib, name)
             f.restype = None
@@ -148,6 +149,14 @@ def test_philox(n, c0, c1, c2, c3, k0, k1):
     lib = load()
     out = np.zeros((n, 4), np.uint32)
     lib.gro_test_philox(n, c0, c1, c2, c3, k0, k1, _p(out))
+    return out
+
+
+def test_fields6(words: np.ndarray) -> np.ndarray:
+    lib = load()
+    w = np.ascontiguousarray(words, dtype=np.uint32).reshape(-1, 4)
+    out = np.zeros((w.shape[0], 6), np.uint32)
+    lib.gro_test_fields6(w.shape[0], _p(w), _p(out))
     return out
 
 

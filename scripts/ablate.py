@@ -11,7 +11,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "build", "abl")
 CSRC = os.path.join(ROOT, "generalizableracing_amd", "csrc")
+BASE_FLAGS = "-fno-slp-vectorize"  # as the Makefile
+EXTRA = {"slp": ""}  # compiler-flag variants (no source ablation): replace BASE_FLAGS
 VARIANTS = {
+    "slp": [],
     "base": [], "noreset": ["GR_ABL_NORESET"], "nocoll": ["GR_ABL_NOCOLL"], "noobsnoise": ["GR_ABL_NOOBSNOISE"],
     "nogatenoise": ["GR_ABL_NOGATENOISE"], "nolog": ["GR_ABL_NOLOG"], "noobs": ["GR_ABL_NOOBS"],
     "nolds": ["GR_ABL_NOLDS"],
@@ -24,6 +27,7 @@ def build():
     procs = []
     for name, flags in VARIANTS.items():
         d = " ".join(f"-D{f}" for f in flags)
+        d += " " + EXTRA.get(name, BASE_FLAGS)
         cmd = (f"/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off "
                f"-fhip-fp32-correctly-rounded-divide-sqrt {d} -shared -o {OUT}/libgr_{name}.so "
                f"{CSRC}/gr_kernels.hip -x hip {CSRC}/gr_capi.cpp")
@@ -43,7 +47,8 @@ def time_one(n=65536, steps=512):
     acts = torch.randn(bench.ACTION_RING, n, 4, device="cuda:0", generator=g)
     for k in range(32):
         env.step(acts[k % bench.ACTION_RING])
-    return bench.kernel_timing(env, acts, steps) * 1e3
+    graph = bench.capture_graph(env, acts)
+    return bench.kernel_timing(env, acts, steps, graph)["kernel_us"]
 
 
 def modes(n=65536, reps=200):
@@ -59,7 +64,7 @@ def modes(n=65536, reps=200):
     acts = torch.randn(bench.ACTION_RING, n, 4, device="cuda:0", generator=g)
     for k in range(32):
         env.step(acts[k % bench.ACTION_RING])
-    res = {"step": bench.kernel_timing(env, acts, reps) * 1e3}
+    res = {"step": bench.kernel_timing(env, acts, reps, None)["eager_event_us"]}
     none = np.zeros(0, np.int64)
     for name, fn in (("reset_all", lambda: env.reset()), ("reset_none", lambda: env.reset(env_ids=none)),
                      ("observe", lambda: env.observe())):

@@ -67,7 +67,9 @@ def main(argv=None):
     import torch
     import yaml
 
-    from generalizableracing_amd import registry
+    import importlib
+
+    registry = importlib.import_module("generalizableracing_amd.registry")
     from generalizableracing_amd.envs.racing_env import RslRlVecEnvWrapper
     from generalizableracing_amd.rsl_rl import OnPolicyRunner
     from generalizableracing_amd.rsl_rl import distributed as gdist

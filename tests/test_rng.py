@@ -21,3 +21,20 @@ def test_uniform_words_look_uniform():
     w = oracle.test_philox(50000, 0, 1, 2, 3, 42, 0).reshape(-1)
     u = (w >> 8).astype(np.float64) / 2**24
     assert abs(u.mean() - 0.5) < 0.005 and abs(u.var() - 1 / 12) < 0.002
+
+
+def test_fields6_partition_126_bits():
+    """gr_fields6: six 21-bit fields = bits [21j, 21j+21) of the little-endian 128-bit draw."""
+    rng = np.random.default_rng(7)
+    w = rng.integers(0, 2**32, size=(256, 4), dtype=np.uint64).astype(np.uint32)
+    got = oracle.test_fields6(w)
+    for r in range(w.shape[0]):
+        big = sum(int(w[r, k]) << (32 * k) for k in range(4))
+        want = [(big >> (21 * j)) & ((1 << 21) - 1) for j in range(6)]
+        assert got[r].tolist() == want
+    # single-bit probes: every bit 0..125 lands in exactly one field, 126/127 in none
+    for b in range(128):
+        big = 1 << b
+        ww = np.array([[(big >> (32 * k)) & 0xFFFFFFFF for k in range(4)]], np.uint32)
+        f = oracle.test_fields6(ww)[0]
+        assert int((f != 0).sum()) == (1 if b < 126 else 0)
