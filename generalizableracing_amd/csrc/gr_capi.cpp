@@ -119,7 +119,8 @@ void derive(gr_ctx* c) {
     c->blk_types[b] = t0 | (t1 << 16);
   }
   const long bytes = (long)span * g.num_levels * a.track_stride * 4;
-  a.lds_bytes = bytes <= 60 * 1024 ? (int)bytes : 0;  // beyond 60 KiB: read the (L2-resident) table directly
+  // table + handover within 64 KiB per workgroup; beyond that the (L2-resident) table is read directly
+  a.lds_bytes = bytes + GR_XCH_BYTES <= 64 * 1024 ? (int)bytes : 0;
 #ifdef GR_ABL_NOLDS
   a.lds_bytes = 0;
 #endif
@@ -131,7 +132,7 @@ void derive(gr_ctx* c) {
   h.env_id_offset = g.env_id_offset;
   h.use_motor_model = g.use_motor_model;
   h.obs_noise = g.obs_noise;
-  h.lds_bytes = a.lds_bytes;
+  h.lds_tab_vec = a.lds_bytes / 16;
   h.seed_lo = g.seed_lo;
   h.seed_hi = g.seed_hi;
   h.obs_lin_vel_noise = g.obs_lin_vel_noise;
@@ -256,7 +257,7 @@ int gr_destroy(gr_ctx* c) {
 const char* gr_last_error(const gr_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 int gr_num_blocks(const gr_ctx* c) { return c ? (c->cfg.num_envs + GR_BLOCK - 1) / GR_BLOCK : GR_ERR_ARG; }
-int gr_num_log_rows(const gr_ctx* c) { return c ? gr_num_blocks(c) * (GR_BLOCK / 64) : GR_ERR_ARG; }
+int gr_num_log_rows(const gr_ctx* c) { return c ? gr_num_blocks(c) * GR_LOG_ROWS_PER_BLOCK : GR_ERR_ARG; }
 
 int gr_log_finalize(gr_ctx* c, const float* rows, const float* prev, float* out, void* stream) {
   if (!c || !rows || !out) return GR_ERR_ARG;

@@ -6,6 +6,8 @@
 
 #define GR_BLOCK 256
 #define GR_MAX_TYPES 64
+#define GR_LOG_ROWS_PER_BLOCK 8  // log rows per workgroup (the step kernel has 8 waves)
+#define GR_XCH_BYTES (20 * GR_BLOCK * 4)  // step kernel: physics -> observation handover in LDS
 #define GR_STAMP_WAVES 4096  // diagnostic stamps (GR_STAMPS builds only)
 #define GR_STAMP_SLOTS 16
 
@@ -35,7 +37,7 @@ struct KConst {
 // (one kernarg fetch at entry) instead of through the KConst pointer chain.
 struct KHot {
   int num_envs, num_levels, max_gates, track_stride;
-  int env_id_offset, use_motor_model, obs_noise, lds_bytes;
+  int env_id_offset, use_motor_model, obs_noise, lds_tab_vec;  // lds_tab_vec: float4 of LDS table (0: global)
   uint32_t seed_lo, seed_hi;
   float obs_lin_vel_noise, obs_att_noise;
 };

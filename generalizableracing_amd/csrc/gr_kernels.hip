@@ -123,8 +123,8 @@ DEV void load_env(const KArgs& a, int i, Env& e) {
   e.gate = ii.w & 0xff; e.lvl = (ii.w >> 8) & 0xff; e.azero = (ii.w >> 16) & 1; e.type = (ii.w >> 24) & 0xff;
 }
 
-// Per-step planes: kinematics, controller filters, lag, episode sums (+ motor speeds).
-DEV void store_dyn(const KArgs& a, int i, const Env& e) {
+// Per-step planes: kinematics, controller filters, lag (+ motor speeds) ...
+DEV void store_kin(const KArgs& a, int i, const Env& e) {
   float4* S = reinterpret_cast<float4*>(a.buf.state);
   const size_t n = (size_t)a.h.num_envs;
   S[GR_P_POSQ * n + i] = make_float4(e.p[0], e.p[1], e.p[2], e.q[0]);
@@ -133,9 +133,18 @@ DEV void store_dyn(const KArgs& a, int i, const Env& e) {
   S[GR_P_WA * n + i] = make_float4(e.w[2], e.al[0], e.al[1], e.al[2]);
   S[GR_P_CTRL * n + i] = make_float4(e.T, e.tau[0], e.tau[1], e.tau[2]);
   S[GR_P_LAG * n + i] = make_float4(e.lag[0], e.lag[1], e.lag[2], e.lag[3]);
+  if (a.h.use_motor_model) S[GR_P_MOTOR * n + i] = make_float4(e.mw[0], e.mw[1], e.mw[2], e.mw[3]);
+}
+// ... and episode sums
+DEV void store_eps(const KArgs& a, int i, const Env& e) {
+  float4* S = reinterpret_cast<float4*>(a.buf.state);
+  const size_t n = (size_t)a.h.num_envs;
   S[GR_P_EP0 * n + i] = make_float4(e.es[0], e.es[1], e.es[2], e.es[3]);
   S[GR_P_EP1 * n + i] = make_float4(e.es[4], e.es[5], e.es[6], e.mar);
-  if (a.h.use_motor_model) S[GR_P_MOTOR * n + i] = make_float4(e.mw[0], e.mw[1], e.mw[2], e.mw[3]);
+}
+DEV void store_dyn(const KArgs& a, int i, const Env& e) {
+  store_kin(a, i, e);
+  store_eps(a, i, e);
 }
 
 // Per-episode domain-randomisation planes (written at reset only).
@@ -345,18 +354,51 @@ DEV void si_substep(float m, const float J[3], const float fb[3], const float tb
 }
 
 // ------------------------------------------------------------- reset
-DEV void reset_env(const KArgs& a, const Tab& tab, Env& e, uint32_t gid) {
+// reset_root_state_racing (events.py:139-177) + drag DR (droneDynamics.py:50-57) +
+// thrust-estimate error (diff_action.py:223-233) + curriculum (curriculums.py:25-54).
+// Split in two: everything that depends only on (env, next episode) — the four
+// Philox blocks, uniforms, Box-Muller, drag — can be drawn before it is known
+// whether the env resets; the rest (level, yaw to the start gate) is applied then.
+struct ResetDraws {
+  float p[3], att[3], v[3], wv[3];  // spawn position, roll/pitch/yaw offsets, linear / angular velocity
+  float k2[3], k1[3];               // drag (random_drag)
+  float lvl_u, thr;                 // random level for "beyond the last level", thrust-estimate error
+};
+
+// 24 x 21-bit fields: pos 0-2, att 3-5, vel 6-11, z-drag 12, k2 13-15, k1 16-18, level 19, thr 20-21
+DEV void reset_draws(const KArgs& a, uint32_t gid, uint32_t ep, float m_ctrl, ResetDraws& r) {
   const gr_config& c = a.kc->cfg;
-  int up = e.acc >= c.level_up_threshold, down = e.acc < c.level_down_threshold;
-  int lvl = e.lvl + up - down;
-  uint32_t ep = (uint32_t)e.epoch + 1u;
-  // 24 x 21-bit fields: pos 0-2, att 3-5, vel 6-11, z-drag 12, k2 13-15, k1 16-18, level 19, thr 20-21
   uint32_t f[24];
   gr_fields6(draw(a, gid, ep, GR_TAG_RESET, 0), f);
   gr_fields6(draw(a, gid, ep, GR_TAG_RESET, 1), f + 6);
   gr_fields6(draw(a, gid, ep, GR_TAG_RESET, 2), f + 12);
   gr_fields6(draw(a, gid, ep, GR_TAG_RESET, 3), f + 18);
-  if (lvl >= c.num_levels) lvl = (int)gr_floorf(gr_f21(f[19]) * (float)c.num_levels);
+  r.lvl_u = gr_f21(f[19]);
+  for (int k = 0; k < 3; ++k) {
+    r.p[k] = c.spawn_pos[k] + gr_uniform21(f[k], -c.reset_pos_half[k], c.reset_pos_half[k]);
+    r.att[k] = gr_uniform21(f[3 + k], -c.reset_att_half[k], c.reset_att_half[k]);
+    r.v[k] = 0.0f + gr_uniform21(f[6 + k], -c.reset_vel_half[k], c.reset_vel_half[k]);
+    r.wv[k] = 0.0f + gr_uniform21(f[9 + k], -c.reset_vel_half[3 + k], c.reset_vel_half[3 + k]);
+  }
+  if (c.random_drag) {
+    float z = c.z_drag + gr_f21(f[12]) * c.z_drag_rand;
+    for (int k = 0; k < 3; ++k) {
+      r.k2[k] = c.drag2[k] * m_ctrl + gr_f21(f[13 + k]) * c.drag2_rand;
+      r.k1[k] = c.drag1[k] * m_ctrl + gr_f21(f[16 + k]) * c.drag1_rand;
+    }
+    r.k2[2] = r.k2[2] * z;
+    r.k1[2] = r.k1[2] * z;
+  }
+  float z0, z1;
+  gr_box_muller21(f[20], f[21], &z0, &z1);
+  r.thr = 1.0f + z0 * 0.01f;
+}
+
+DEV void reset_apply(const KArgs& a, const Tab& tab, Env& e, const ResetDraws& r) {
+  const gr_config& c = a.kc->cfg;
+  int up = e.acc >= c.level_up_threshold, down = e.acc < c.level_down_threshold;
+  int lvl = e.lvl + up - down;
+  if (lvl >= c.num_levels) lvl = (int)gr_floorf(r.lvl_u * (float)c.num_levels);
   else if (lvl < 0) lvl = 0;
   if (c.noise_curriculum) {
     float upf = e.acc >= c.noise_enhance_threshold ? 1.0f + c.noise_enhance : 1.0f;
@@ -365,48 +407,36 @@ DEV void reset_env(const KArgs& a, const Tab& tab, Env& e, uint32_t gid) {
     e.nl = e.nl * dnf;
   }
   e.lvl = lvl;
-  float rp[6], rv[6];
-  for (int k = 0; k < 3; ++k) {
-    rp[k] = gr_uniform21(f[k], -c.reset_pos_half[k], c.reset_pos_half[k]);
-    rp[3 + k] = gr_uniform21(f[3 + k], -c.reset_att_half[k], c.reset_att_half[k]);
-  }
-  for (int k = 0; k < 6; ++k) rv[k] = gr_uniform21(f[6 + k], -c.reset_vel_half[k], c.reset_vel_half[k]);
-  for (int k = 0; k < 3; ++k) e.p[k] = c.spawn_pos[k] + rp[k];
+  for (int k = 0; k < 3; ++k) e.p[k] = r.p[k];
   const float* rec = tab.rec(e.type, lvl);
   int start = (int)rec[2];
   const float* g0 = tab.gate(e.type, lvl, start);
   float tx = g0[0] - e.p[0], ty = g0[1] - e.p[1];
-  float yaw = gr_wrap_to_pi(gr_atan2f(ty, tx)) + rp[5];
+  float yaw = gr_wrap_to_pi(gr_atan2f(ty, tx)) + r.att[2];
   float qd[4], qid[4] = {1.0f, 0.0f, 0.0f, 0.0f};
-  quat_from_euler_xyz(rp[3], rp[4], yaw, qd);
+  quat_from_euler_xyz(r.att[0], r.att[1], yaw, qd);
   quat_mul(qid, qd, e.q);
-  for (int k = 0; k < 3; ++k) e.v[k] = 0.0f + rv[k];
-  float ww[3] = {0.0f + rv[3], 0.0f + rv[4], 0.0f + rv[5]};
-  quat_rotate_inverse(e.q, ww, e.w);
+  for (int k = 0; k < 3; ++k) e.v[k] = r.v[k];
+  quat_rotate_inverse(e.q, r.wv, e.w);
   e.azero = 1;
   e.T = 0.0f;
   for (int k = 0; k < 3; ++k) { e.tau[k] = 0.0f; e.al[k] = 0.0f; }
   for (int k = 0; k < 4; ++k) e.mw[k] = 0.0f;
-  if (c.random_drag) {
-    float z = c.z_drag + gr_f21(f[12]) * c.z_drag_rand;
-    float u2[3] = {gr_f21(f[13]), gr_f21(f[14]), gr_f21(f[15])};
-    float u1[3] = {gr_f21(f[16]), gr_f21(f[17]), gr_f21(f[18])};
-    for (int k = 0; k < 3; ++k) {
-      e.k2[k] = c.drag2[k] * e.mc + u2[k] * c.drag2_rand;
-      e.k1[k] = c.drag1[k] * e.mc + u1[k] * c.drag1_rand;
-    }
-    e.k2[2] = e.k2[2] * z;
-    e.k1[2] = e.k1[2] * z;
-  }
-  float z0, z1;
-  gr_box_muller21(f[20], f[21], &z0, &z1);
-  e.thr = 1.0f + z0 * 0.01f;
+  if (c.random_drag)
+    for (int k = 0; k < 3; ++k) { e.k2[k] = r.k2[k]; e.k1[k] = r.k1[k]; }
+  e.thr = r.thr;
   for (int k = 0; k < 7; ++k) e.es[k] = 0.0f;
   e.mar = 0.0f;
   e.acc = 0;
   e.gate = start;
   e.ep = 0;
-  e.epoch = (int)ep;
+  e.epoch = e.epoch + 1;
+}
+
+DEV void reset_env(const KArgs& a, const Tab& tab, Env& e, uint32_t gid) {
+  ResetDraws r;
+  reset_draws(a, gid, (uint32_t)e.epoch + 1u, e.mc, r);
+  reset_apply(a, tab, e, r);
 }
 
 // ------------------------------------------------------------- observations
@@ -490,34 +520,46 @@ DEV void write_obs(const KArgs& a, const Tab& tab, const Env& e, int i, uint32_t
 }
 
 // ------------------------------------------------------------- log reduction
-// Per-wave partial sums into log_partial[wave][GR_LOG_SLOTS] (no workgroup
-// barrier).  Resets are sparse (~1 % of envs per step): the reset slots are
-// accumulated over the set bits of the wave's reset ballot with wave-uniform
-// lane reads; only the two all-env sums (terrain level, noise level) use a
-// full butterfly.  Means are formed on demand from these rows.
-DEV void wave_log(const KArgs& a, const float lg[GR_LOG_SLOTS], bool reset_lane, float level, float noise) {
-  const int lane = threadIdx.x & 63;
-  float acc[GR_LOG_LEVEL];
-  for (int s = 0; s < GR_LOG_LEVEL; ++s) acc[s] = 0.0f;
+// Per-wave partial sums into log_partial[row][GR_LOG_SLOTS] (no workgroup
+// barrier); a workgroup owns GR_LOG_ROWS_PER_BLOCK rows.  Resets are sparse
+// (~1 % of envs per step): the reset slots are accumulated over the set bits of
+// the wave's reset ballot with wave-uniform lane reads; the two all-env sums
+// (terrain level, noise level) use a butterfly.  Means are formed on demand.
+
+DEV void log_row_store(const KArgs& a, int row, const float v[GR_LOG_SLOTS]) {
+  float4* r = reinterpret_cast<float4*>(a.buf.log_partial + ((size_t)blockIdx.x * GR_LOG_ROWS_PER_BLOCK + row) *
+                                                                GR_LOG_SLOTS);
+  r[0] = make_float4(v[0], v[1], v[2], v[3]);
+  r[1] = make_float4(v[4], v[5], v[6], v[7]);
+  r[2] = make_float4(v[8], v[9], v[10], v[11]);
+  r[3] = make_float4(v[12], v[13], v[14], v[15]);
+  r[4] = make_float4(v[16], v[17], v[18], v[19]);
+}
+
+// reset-lane slots (GR_LOG_NRESET .. GR_LOG_T_BADPOSE) of this wave -> row
+DEV void wave_log_resets(const KArgs& a, int row, const float lg[GR_LOG_SLOTS], bool reset_lane) {
+  float acc[GR_LOG_SLOTS];
+  for (int s = 0; s < GR_LOG_SLOTS; ++s) acc[s] = 0.0f;
   uint64_t m = __ballot(reset_lane);
   while (m) {
     const int l = __builtin_ctzll(m);
     m &= m - 1;
     for (int s = 0; s < GR_LOG_LEVEL; ++s) acc[s] += __shfl(lg[s], l, 64);
   }
+  if ((threadIdx.x & 63) == 0) log_row_store(a, row, acc);
+}
+
+// all-env slots (terrain level, noise level) of this wave -> row
+DEV void wave_log_levels(const KArgs& a, int row, float level, float noise) {
   for (int off = 32; off > 0; off >>= 1) {
     level += __shfl_xor(level, off, 64);
     noise += __shfl_xor(noise, off, 64);
   }
-  if (lane == 0) {
-    float4* row = reinterpret_cast<float4*>(a.buf.log_partial +
-                                            ((size_t)blockIdx.x * (GR_BLOCK / 64) + (threadIdx.x >> 6)) * GR_LOG_SLOTS);
-    row[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-    row[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
-    row[2] = make_float4(acc[8], acc[9], acc[10], acc[11]);
-    row[3] = make_float4(acc[12], acc[13], acc[14], level);
-    row[4] = make_float4(noise, 0.0f, 0.0f, 0.0f);
-  }
+  float v[GR_LOG_SLOTS];
+  for (int s = 0; s < GR_LOG_SLOTS; ++s) v[s] = 0.0f;
+  v[GR_LOG_LEVEL] = level;
+  v[GR_LOG_NOISE] = noise;
+  if ((threadIdx.x & 63) == 0) log_row_store(a, row, v);
 }
 
 // ------------------------------------------------------------- gate table staging
@@ -544,13 +586,13 @@ __device__ unsigned long long g_stamps[GR_STAMP_WAVES * GR_STAMP_SLOTS];
 #define STAMP(k)                                                                              \
   do {                                                                                        \
     unsigned long long t_ = __builtin_amdgcn_s_memtime();                                    \
-    const unsigned w_ = blockIdx.x * (GR_BLOCK / 64) + (threadIdx.x >> 6);                    \
+    const unsigned w_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);                  \
     if ((threadIdx.x & 63) == 0 && w_ < GR_STAMP_WAVES) g_stamps[w_ * GR_STAMP_SLOTS + (k)] = t_; \
   } while (0)
 #define RSTAMP(k)                                                                             \
   do {                                                                                        \
     unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                \
-    const unsigned w_ = blockIdx.x * (GR_BLOCK / 64) + (threadIdx.x >> 6);                    \
+    const unsigned w_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);                  \
     if ((threadIdx.x & 63) == 0 && w_ < GR_STAMP_WAVES) g_stamps[w_ * GR_STAMP_SLOTS + (k)] = t_; \
   } while (0)
 #else
@@ -558,78 +600,132 @@ __device__ unsigned long long g_stamps[GR_STAMP_WAVES * GR_STAMP_SLOTS];
 #define RSTAMP(k)
 #endif
 
-// ------------------------------------------------------------- the kernel
+// ------------------------------------------------------------- table slice view
+struct Slice {
+  Tab tab;
+  const float4* src;  // global copy of this workgroup's slice
+  int nvec;           // float4 in the slice
+};
+
+template <bool USE_LDS>
+DEV Slice block_slice(const KArgs& a, const float4* lds) {
+  // terrain types of this workgroup (type = floor(i / (N / T)), IL TerrainImporter layout),
+  // derived on the host per workgroup: one scalar load
+  const int bt = a.blk_types[blockIdx.x];
+  const int t0 = bt & 0xffff, t1 = bt >> 16;
+  Slice s;
+  s.tab.L = a.h.num_levels;
+  s.tab.G = a.h.max_gates;
+  s.tab.stride = a.h.track_stride;
+  s.tab.t0 = t0;
+  s.src = reinterpret_cast<const float4*>(a.table + (size_t)t0 * s.tab.L * s.tab.stride);
+  s.nvec = (t1 - t0 + 1) * s.tab.L * s.tab.stride / 4;
+  s.tab.base = USE_LDS ? reinterpret_cast<const float*>(lds) : reinterpret_cast<const float*>(s.src);
+  return s;
+}
+
+// ------------------------------------------------------------- reset / observe kernel
+// gr_reset / gr_observe: observations for every env, reset for the masked ones.
 template <int MODE, bool USE_LDS>
 __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const KConst* __restrict__ kc,
-                                                        const float* __restrict__ actions,
                                                         const uint8_t* __restrict__ mask) {
-  a.kc = kc;  // constants through the noalias argument: scalar loads at their uses
+  a.kc = kc;
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
   const int n = a.h.num_envs;
   const int i = blockIdx.x * GR_BLOCK + threadIdx.x;
+  const bool live = i < n;
+  const int ii = live ? i : n - 1;  // dead lanes mirror the last env (loads stay in bounds, no stores)
+  const uint32_t gid = gid_of(a, ii);
+  const uint32_t cnt = a.buf.counters[a.buf.counter_index];
+  Env e;
+  load_env(a, ii, e);
+  const Slice sl = block_slice<USE_LDS>(a, lds_tab);
+  if (USE_LDS) {
+    for (int idx = threadIdx.x; idx < sl.nvec; idx += GR_BLOCK) lds_tab[idx] = sl.src[idx];
+    __syncthreads();
+  }
+  ObsNoise on;
+  obs_noise(a, gid, cnt, on);
+  if (threadIdx.x == 0 && blockIdx.x == 0) a.buf.counters[a.buf.counter_index ^ 1] = cnt + 1u;
+  float lg[GR_LOG_SLOTS];
+  for (int s = 0; s < GR_LOG_SLOTS; ++s) lg[s] = 0.0f;
+  bool reset_lane = false;
+  // last action and aux carry over from the previous observation
+  const float4 lcv = reinterpret_cast<const float4*>(a.buf.prev_obs_critic)[(size_t)ii * 4 + 3];
+  const float lc[4] = {lcv.x, lcv.y, lcv.z, lcv.w};
+  const float aux = a.buf.prev_obs_aux[ii];
+  if (MODE == KMODE_RESET && live && (mask == nullptr || mask[i])) {
+    reset_lane = true;
+    lg[GR_LOG_NRESET] = 1.0f;
+    for (int k = 0; k < 7; ++k) lg[GR_LOG_EPSUM0 + k] = e.es[k];
+    lg[GR_LOG_ACC] = (float)e.acc;
+    lg[GR_LOG_M_ACTRATE] = e.mar;
+    lg[GR_LOG_M_LINSPD] = norm3(e.v);
+    lg[GR_LOG_M_ANGSPD] = norm3(e.w);
+    lg[GR_LOG_T_TIMEOUT] = a.buf.prev_time_out[i] ? 1.0f : 0.0f;
+    reset_env(a, sl.tab, e, gid);
+  }
+  if (live) {
+    write_obs(a, sl.tab, e, i, gid, on, lc, aux);
+    if (reset_lane) {
+      store_dyn(a, i, e);
+      store_rst(a, i, e);
+      store_istate(a, i, e);
+    }
+  }
+  // (observe calls reset nothing: their rows say so, and the finalized log repeats the previous one)
+  const int w = threadIdx.x >> 6;
+  wave_log_resets(a, w, lg, reset_lane);
+  wave_log_levels(a, 4 + w, live ? (float)e.lvl : 0.0f, live ? e.nl : 0.0f);
+}
+
+// ------------------------------------------------------------- the step kernel
+// One workgroup = 256 envs and 8 waves: waves 0-3 run the physics of the 256 envs
+// (controller, integrator, collision, termination, reward), waves 4-7 run their
+// observation noise and the reset draws meanwhile, then — after the physics hands
+// over the post-step pose through LDS — the resets, gate progress and the
+// observations.  At 65 536 envs this puts two waves on every SIMD: a single
+// wave can issue a VALU op only every 4 cycles, two can use the SIMD every 2,
+// and one wave's memory / LDS / transcendental latency hides under the other's
+// work.  (ManagerBasedDiffRLEnv.step, manager_based_diff_rl_env.py:160-267.)
+// handover rows (float4 per env): p + aux, q, v + done, lag, last ctbr
+enum { X_PA = 0, X_Q = 1, X_VD = 2, X_LAG = 3, X_LC = 4, GR_XF4 = 5, GR_XF = 4 * GR_XF4 };
+
+template <bool USE_LDS>
+__global__ __launch_bounds__(2 * GR_BLOCK) void step_kernel(KArgs a, const KConst* __restrict__ kc,
+                                                             const float* __restrict__ actions) {
+  a.kc = kc;
+  extern __shared__ __attribute__((aligned(16))) float4 lds[];
+  float4* xch = lds + a.h.lds_tab_vec;  // [GR_XF4][GR_BLOCK] handover, after the table
+  const int role = threadIdx.x >> 8;                             // wave-uniform: 0 physics, 1 observation
+  const int t = threadIdx.x & (GR_BLOCK - 1);
+  const int n = a.h.num_envs;
+  const int i = blockIdx.x * GR_BLOCK + t;
   const bool live = i < n;
   const int ii = live ? i : n - 1;  // dead lanes mirror the last env (loads stay in bounds, no stores)
   const gr_config& c = a.kc->cfg;
   const uint32_t gid = gid_of(a, ii);
   RSTAMP(9);
   STAMP(0);
+  const Slice sl = block_slice<USE_LDS>(a, lds);
+  // each of the 512 threads stages one float4 of the table slice (clamped loads; extras are not stored)
+  float4 tr = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if (USE_LDS) tr = sl.src[min((int)threadIdx.x, sl.nvec - 1)];
+  auto commit = [&]() {
+    if (USE_LDS) {
+      if ((int)threadIdx.x < sl.nvec) lds[threadIdx.x] = tr;
+      for (int idx = threadIdx.x + 2 * GR_BLOCK; idx < sl.nvec; idx += 2 * GR_BLOCK) lds[idx] = sl.src[idx];
+    }
+    __syncthreads();  // barrier 1: table staged
+  };
 
-  // ---- 1. issue every load of this lane first, in order of use ----
-  const uint32_t cnt = a.buf.counters[a.buf.counter_index];  // wave-uniform (scalar) load
-  float4 act = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  if (MODE == KMODE_STEP) act = reinterpret_cast<const float4*>(actions)[ii];
-  Env e;
-  load_env(a, ii, e);
-  // this workgroup's terrain types (type = floor(i / (N / T)), IL TerrainImporter layout),
-  // derived on the host per workgroup: one scalar load
-  const int bt = a.blk_types[blockIdx.x];
-  const int t0 = bt & 0xffff, t1 = bt >> 16;
-  Tab tab;
-  tab.L = a.h.num_levels;
-  tab.G = a.h.max_gates;
-  tab.stride = a.h.track_stride;
-  tab.t0 = t0;
-  tab.base = USE_LDS ? reinterpret_cast<const float*>(lds_tab) : a.table + (size_t)t0 * tab.L * tab.stride;
-  // table slice loads (clamped, always in bounds; the commit skips the extras)
-  const float4* tsrc = reinterpret_cast<const float4*>(a.table + (size_t)t0 * tab.L * tab.stride);
-  const int tnvec = (t1 - t0 + 1) * tab.L * tab.stride / 4;
-  float4 tr0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), tr1 = tr0;
-  if (USE_LDS) {
-    tr0 = tsrc[min((int)threadIdx.x, tnvec - 1)];
-    tr1 = tsrc[min((int)threadIdx.x + GR_BLOCK, tnvec - 1)];
-  }
-
-  STAMP(12);
-#ifdef GR_STAMPS
-  __asm__ volatile("" ::"s"(cnt));  // diagnostic: when the counter load has landed
-  STAMP(13);
-  __asm__ volatile("" ::"v"(e.ep));  // diagnostic: when the first vector load (istate) has landed
-  STAMP(14);
-#endif
-  // ---- 2. load-independent work: observation noise (Philox + Box-Muller) ----
-  ObsNoise on;
-#ifndef GR_ABL_NOOBSNOISE
-  obs_noise(a, gid, cnt, on);
-#else
-  for (int k = 0; k < 3; ++k) on.vfac[k] = 1.0f;
-  on.qn[0] = 1.0f; on.qn[1] = on.qn[2] = on.qn[3] = 0.0f;
-#endif
-  STAMP(1);
-  // call counter for the observation-noise stream: double-buffered by call parity,
-  // so this write never races with the reads of the current launch
-  if (threadIdx.x == 0 && blockIdx.x == 0) a.buf.counters[a.buf.counter_index ^ 1] = cnt + 1u;
-  // the table is needed first by the collision test (step + explicit integrator) or right away
-  const bool late_table = MODE == KMODE_STEP && c.integrator == GR_INTEGRATOR_DD_EXPLICIT;
-  if (USE_LDS && !late_table) table_commit(tsrc, tnvec, tr0, tr1, lds_tab);
-  STAMP(2);
-
-  float lg[GR_LOG_SLOTS];
-  for (int s = 0; s < GR_LOG_SLOTS; ++s) lg[s] = 0.0f;
-  bool reset_lane = false;
-
-  if (MODE == KMODE_STEP) {
+  if (role == 0) {
+    // ======================= physics waves =======================
+    const float4 act = reinterpret_cast<const float4*>(actions)[ii];
+    Env e;
+    load_env(a, ii, e);
+    commit();  // barrier 1 early: the slice loads were issued first and land first
     const float dt = c.step_dt;
-    // pre-step speeds for the episode metrics (commands.py:247-260): norms taken only for resets
     const float v_prev[3] = {e.v[0], e.v[1], e.v[2]}, w_prev[3] = {e.w[0], e.w[1], e.w[2]};
     const float mar_prev = e.mar;
     // DiffActionManager.process_action + one-step lag.  The lag plane holds the
@@ -642,7 +738,6 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const KConst* __
       th_raw[k] = c.action_lag ? e.lag[k] : th_cur[k];
       e.lag[k] = th_cur[k];
     }
-    e.azero = 0;
     float sc[4], of[4], cmd[4];
     action_scale(a, e.mc, sc, of);
     for (int k = 0; k < 4; ++k) cmd[k] = th_raw[k] * sc[k] + of[k];
@@ -657,34 +752,53 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const KConst* __
     if (c.integrator == GR_INTEGRATOR_DD_EXPLICIT) {
       dd_explicit(m, Jp, e.k2, e.k1, tt, dt, c.gravity, e.p, e.q, e.v, e.w, accl, al);
       STAMP(3);
-      if (USE_LDS) table_commit(tsrc, tnvec, tr0, tr1, lds_tab);
 #ifndef GR_ABL_NOCOLL
-      ccount = collision_count(a, tab, e.type, e.lvl, e.p, e.q);
+      ccount = collision_count(a, sl.tab, e.type, e.lvl, e.p, e.q);
 #endif
-      STAMP(4);
     } else {
       float vb[3], fb[3] = {0.0f, 0.0f, tt[0]};
       quat_rotate_inverse(e.q, e.v, vb);
       for (int k = 0; k < 3; ++k) fb[k] = (fb[k] - (e.k2[k] * vb[k]) * gr_fabsf(vb[k])) - e.k1[k] * vb[k];
       for (int s = 0; s < c.decimation; ++s) {
         si_substep(m, Jp, fb, tt + 1, c.sim_dt, c.gravity, e.p, e.q, e.v, e.w, accl, al);
-        int cc = collision_count(a, tab, e.type, e.lvl, e.p, e.q);
+        int cc = collision_count(a, sl.tab, e.type, e.lvl, e.p, e.q);
         ccount = cc > ccount ? cc : ccount;
       }
     }
+    STAMP(4);
     for (int k = 0; k < 3; ++k) e.al[k] = al[k];
+    // terminations first (termination.py:24-33, IL time_out / illegal contact): the observation
+    // waves need `done` for the resets; the reward is computed after the handover, in their shadow
     e.ep += 1;
     const int time_out = e.ep >= c.max_episode_length;
     const int contact = ccount > c.collision_count_threshold;
-    const float* rec = tab.rec(e.type, e.lvl);
+    const float* rec = sl.tab.rec(e.type, e.lvl);
     const float zw = e.p[2] + rec[1];
     const int oob = (zw < c.out_of_bound[0]) | (zw > c.out_of_bound[1]);
     const int bad = (1.0f - 2.0f * (e.q[1] * e.q[1] + e.q[2] * e.q[2])) < 0.0f;
     const int c_term = c.stage == 0 ? oob : contact;
     const int terminated = (c.term_contact && c_term) | (c.term_bad_pose && bad);
+    const float* g = sl.tab.gate(e.type, e.lvl, e.gate);
+    float dg[3] = {g[0] - e.p[0], g[1] - e.p[1], g[2] - e.p[2]};
+    const float dist = norm3(dg);
+    const int near_gate = dist < c.gate_threshold;
+    int done = terminated | time_out;
+#ifdef GR_ABL_NORESET
+    done = 0;
+#endif
+    float lc[4];
+    for (int k = 0; k < 4; ++k) lc[k] = th_raw[k] * sc[k] + of[k];
+    lc[0] = lc[0] / e.mc;
+    // hand the post-step pose over to the observation waves
+    xch[X_PA * GR_BLOCK + t] = make_float4(e.p[0], e.p[1], e.p[2], near_gate ? 1.0f : 0.0f);
+    xch[X_Q * GR_BLOCK + t] = make_float4(e.q[0], e.q[1], e.q[2], e.q[3]);
+    xch[X_VD * GR_BLOCK + t] = make_float4(e.v[0], e.v[1], e.v[2], done ? 1.0f : 0.0f);
+    xch[X_LAG * GR_BLOCK + t] = make_float4(e.lag[0], e.lag[1], e.lag[2], e.lag[3]);
+    xch[X_LC * GR_BLOCK + t] = make_float4(lc[0], lc[1], lc[2], lc[3]);
+    STAMP(5);
+    __syncthreads();  // barrier 2: handover
     // rewards (rewards.py:154-253), IL RewardManager: f * w * dt, declaration order
-    const float* g = tab.gate(e.type, e.lvl, e.gate);
-    float vb[3], dg[3] = {g[0] - e.p[0], g[1] - e.p[1], g[2] - e.p[2]}, gb[3];
+    float vb[3], gb[3];
     quat_rotate_inverse(e.q, e.v, vb);
     quat_rotate_inverse(e.q, dg, gb);
     float f[7];
@@ -702,8 +816,6 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const KConst* __
     float nb = gr_maxf(norm3(gb), 1e-12f);
     float gh[3] = {gb[0] / nb, gb[1] / nb, gb[2] / nb}, fx[3] = {1.0f, 0.0f, 0.0f};
     f[4] = cosine_similarity(gh, fx);
-    float dist = norm3(dg);
-    const int near_gate = dist < c.gate_threshold;
     f[5] = (float)near_gate * (1.0f / (dist * dist + 1.0f));
     f[6] = (float)bad;
     float rew = 0.0f;
@@ -714,24 +826,20 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const KConst* __
       rew = rew + v;
       e.es[k] = e.es[k] + v;
     }
-    const float aux = near_gate ? 1.0f : 0.0f;
     e.mar = f[2];
-    const int done = terminated | time_out;
-    STAMP(5);
     if (live) {
       a.buf.reward[i] = rew;
       a.buf.terminated[i] = (uint8_t)terminated;
       a.buf.time_out[i] = (uint8_t)time_out;
-      a.buf.dones[i] = (int64_t)done;
-      // continuing envs: the per-step planes are final now; let them drain while the rest runs
-      if (!done) store_dyn(a, i, e);
+      a.buf.dones[i] = (int64_t)(terminated | time_out);
+      if (!done) store_dyn(a, i, e);  // resetting envs: written by the observation waves
     }
-#ifndef GR_ABL_NORESET
-    if (done && live) {
-#else
-    if (false) {
-#endif
-      reset_lane = true;
+    STAMP(12);
+    // episode metrics of the resetting envs (reward / termination / command managers' reset logs)
+    float lg[GR_LOG_SLOTS];
+    for (int s = 0; s < GR_LOG_SLOTS; ++s) lg[s] = 0.0f;
+    const bool reset_lane = done && live;
+    if (reset_lane) {
       for (int k = 0; k < 7; ++k) lg[GR_LOG_EPSUM0 + k] = e.es[k];
       lg[GR_LOG_NRESET] = 1.0f;
       lg[GR_LOG_ACC] = (float)e.acc;
@@ -741,68 +849,90 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const KConst* __
       lg[GR_LOG_T_TIMEOUT] = (float)time_out;
       lg[GR_LOG_T_CONTACT] = (float)c_term;
       lg[GR_LOG_T_BADPOSE] = (float)bad;
-      reset_env(a, tab, e, gid);
+    }
+#ifndef GR_ABL_NOLOG
+    wave_log_resets(a, threadIdx.x >> 6, lg, reset_lane);
+#endif
+    STAMP(8);
+    RSTAMP(10);
+  } else {
+    // ======================= observation / reset waves =======================
+    const uint32_t cnt = a.buf.counters[a.buf.counter_index];
+    const float4* S = reinterpret_cast<const float4*>(a.buf.state);
+    const size_t ns = (size_t)n;
+    const int4 is = reinterpret_cast<const int4*>(a.buf.istate)[ii];
+    const float4 r0 = S[GR_P_RST0 * ns + ii], r1 = S[GR_P_RST1 * ns + ii], p2 = S[GR_P_PAR2 * ns + ii];
+    Env e;
+    e.ep = is.x; e.acc = is.y; e.epoch = is.z;
+    e.gate = is.w & 0xff; e.lvl = (is.w >> 8) & 0xff; e.type = (is.w >> 24) & 0xff;
+    e.thr = r0.x; e.nl = r0.y; e.k2[0] = r0.z; e.k2[1] = r0.w;
+    e.k2[2] = r1.x; e.k1[0] = r1.y; e.k1[1] = r1.z; e.k1[2] = r1.w;
+    e.mc = p2.w;
+    commit();  // barrier 1
+    STAMP(1);
+    ObsNoise on;
+#ifndef GR_ABL_NOOBSNOISE
+    obs_noise(a, gid, cnt, on);
+#else
+    for (int k = 0; k < 3; ++k) on.vfac[k] = 1.0f;
+    on.qn[0] = 1.0f; on.qn[1] = on.qn[2] = on.qn[3] = 0.0f;
+#endif
+    STAMP(2);
+    // call counter for the observation-noise stream: double-buffered by call parity,
+    // so this write never races with the reads of the current launch
+    if (t == 0 && blockIdx.x == 0) a.buf.counters[a.buf.counter_index ^ 1] = cnt + 1u;
+    // the next episode's draws, for every env (only the resetting ones use them)
+    ResetDraws rd;
+    reset_draws(a, gid, (uint32_t)e.epoch + 1u, e.mc, rd);
+    STAMP(6);
+    __syncthreads();  // barrier 2: handover
+    STAMP(13);
+    const float4 xpa = xch[X_PA * GR_BLOCK + t], xq = xch[X_Q * GR_BLOCK + t], xvd = xch[X_VD * GR_BLOCK + t];
+    const float4 xlag = xch[X_LAG * GR_BLOCK + t], xlc = xch[X_LC * GR_BLOCK + t];
+    e.p[0] = xpa.x; e.p[1] = xpa.y; e.p[2] = xpa.z;
+    e.q[0] = xq.x; e.q[1] = xq.y; e.q[2] = xq.z; e.q[3] = xq.w;
+    e.v[0] = xvd.x; e.v[1] = xvd.y; e.v[2] = xvd.z;
+    e.lag[0] = xlag.x; e.lag[1] = xlag.y; e.lag[2] = xlag.z; e.lag[3] = xlag.w;
+    const float lc[4] = {xlc.x, xlc.y, xlc.z, xlc.w};
+    const float aux = xpa.w;
+    const bool done = xvd.w != 0.0f;
+    e.ep += 1;
+    e.azero = 0;
+    if (done && live) {
+      reset_apply(a, sl.tab, e, rd);
       store_dyn(a, i, e);
       store_rst(a, i, e);
     }
+    STAMP(14);
     // command compute: _update_metrics + _update_command (commands.py:247-260, 308-350)
     {
-      const float* gg = tab.gate(e.type, e.lvl, e.gate);
+      const float* gg = sl.tab.gate(e.type, e.lvl, e.gate);
       float dd[3] = {gg[0] - e.p[0], gg[1] - e.p[1], gg[2] - e.p[2]};
       if (norm3(dd) < c.gate_threshold) {
-        const int ngt = (int)tab.rec(e.type, e.lvl)[3];
+        const int ngt = (int)sl.tab.rec(e.type, e.lvl)[3];
         e.acc += 1;
         e.gate = e.gate + 1;
         if (e.gate >= ngt) e.gate -= ngt;
       }
     }
-    float lc[4];
-    for (int k = 0; k < 4; ++k) lc[k] = th_raw[k] * sc[k] + of[k];
-    lc[0] = lc[0] / e.mc;
-    STAMP(6);
+    STAMP(7);
     if (live) {
       store_istate(a, i, e);
 #ifndef GR_ABL_NOOBS
-      write_obs(a, tab, e, i, gid, on, lc, aux);
+      write_obs(a, sl.tab, e, i, gid, on, lc, aux);
 #endif
     }
-    STAMP(7);
-  } else {
-    // MODE_RESET / MODE_OBSERVE: last action and aux carry over from the previous observation
-    const float4 lcv = reinterpret_cast<const float4*>(a.buf.prev_obs_critic)[(size_t)ii * 4 + 3];
-    float lc[4] = {lcv.x, lcv.y, lcv.z, lcv.w};
-    const float aux = a.buf.prev_obs_aux[ii];
-    if (MODE == KMODE_RESET && live && (mask == nullptr || mask[i])) {
-      reset_lane = true;
-      lg[GR_LOG_NRESET] = 1.0f;
-      for (int k = 0; k < 7; ++k) lg[GR_LOG_EPSUM0 + k] = e.es[k];
-      lg[GR_LOG_ACC] = (float)e.acc;
-      lg[GR_LOG_M_ACTRATE] = e.mar;
-      lg[GR_LOG_M_LINSPD] = norm3(e.v);
-      lg[GR_LOG_M_ANGSPD] = norm3(e.w);
-      lg[GR_LOG_T_TIMEOUT] = a.buf.prev_time_out[i] ? 1.0f : 0.0f;
-      reset_env(a, tab, e, gid);
-    }
-    if (live) {
-      write_obs(a, tab, e, i, gid, on, lc, aux);
-      if (reset_lane) {
-        store_dyn(a, i, e);
-        store_rst(a, i, e);
-        store_istate(a, i, e);
-      }
-    }
-  }
-  // (observe calls reset nothing: their rows say so, and the finalized log repeats the previous one)
 #ifndef GR_ABL_NOLOG
-  wave_log(a, lg, reset_lane, live ? (float)e.lvl : 0.0f, live ? e.nl : 0.0f);
+    wave_log_levels(a, threadIdx.x >> 6, live ? (float)e.lvl : 0.0f, live ? e.nl : 0.0f);
 #endif
-  STAMP(8);
-  RSTAMP(10);
+    STAMP(8);
+    RSTAMP(10);
+  }
 #ifdef GR_STAMPS
-  if ((threadIdx.x & 63) == 0 && blockIdx.x * (GR_BLOCK / 64) + (threadIdx.x >> 6) < GR_STAMP_WAVES) {
+  if ((threadIdx.x & 63) == 0 && blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6) < GR_STAMP_WAVES) {
     unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));  // HW_ID (hwreg 4), all 32 bits
     unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));  // XCC_ID (hwreg 20), 16 bits
-    g_stamps[(blockIdx.x * (GR_BLOCK / 64) + (threadIdx.x >> 6)) * GR_STAMP_SLOTS + 11] =
+    g_stamps[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * GR_STAMP_SLOTS + 11] =
         ((unsigned long long)xcc << 32) | hw;
   }
 #endif
@@ -989,10 +1119,19 @@ static int grid_of(int n) { return (n + GR_BLOCK - 1) / GR_BLOCK; }
 template <int MODE>
 static hipError_t launch_env_mode(const KArgs& a, const float* actions, const uint8_t* mask, hipStream_t s) {
   const int g = grid_of(a.h.num_envs);
-  if (a.h.lds_bytes > 0) {
-    hipLaunchKernelGGL((env_kernel<MODE, true>), dim3(g), dim3(GR_BLOCK), a.h.lds_bytes, s, a, a.kc, actions, mask);
+  const bool lds = a.h.lds_tab_vec > 0;
+  if constexpr (MODE == KMODE_STEP) {
+    const size_t bytes = (size_t)a.h.lds_tab_vec * 16 + (size_t)GR_XF * GR_BLOCK * 4;
+    if (lds)
+      hipLaunchKernelGGL(step_kernel<true>, dim3(g), dim3(2 * GR_BLOCK), bytes, s, a, a.kc, actions);
+    else
+      hipLaunchKernelGGL(step_kernel<false>, dim3(g), dim3(2 * GR_BLOCK), bytes, s, a, a.kc, actions);
   } else {
-    hipLaunchKernelGGL((env_kernel<MODE, false>), dim3(g), dim3(GR_BLOCK), 0, s, a, a.kc, actions, mask);
+    const size_t bytes = (size_t)a.h.lds_tab_vec * 16;
+    if (lds)
+      hipLaunchKernelGGL((env_kernel<MODE, true>), dim3(g), dim3(GR_BLOCK), bytes, s, a, a.kc, mask);
+    else
+      hipLaunchKernelGGL((env_kernel<MODE, false>), dim3(g), dim3(GR_BLOCK), 0, s, a, a.kc, mask);
   }
   return hipGetLastError();
 }

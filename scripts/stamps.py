@@ -3,10 +3,12 @@
   python scripts/stamps.py build     # here: build/stamps/libgr.so
   python scripts/stamps.py run       # GPU box: GR_LIB_PATH=build/stamps/libgr.so, prints a JSON summary
 
-Stamps (lane 0 of each wave, s_memtime shader cycles): 0 entry, 1 obs noise done,
-2 gate table staged (barrier), 3 controller+integrator, 4 collision, 5 reward/termination,
-6 reset+gate advance, 7 obs+state stores issued, 8 log rows; 9/10 s_memrealtime (100 MHz)
-at entry/exit; 11 XCC_ID<<32 | HW_ID; 12 loads issued (before the obs noise).
+Stamps of the step kernel (lane 0 of each wave, s_memtime shader cycles; 9/10 s_memrealtime
+(100 MHz) at entry/exit; 11 XCC_ID<<32 | HW_ID):
+  physics waves:     0 entry, 3 controller+integrator, 4 table barrier + collision,
+                     5 reward + handover written, 8 after barrier 2, stores and log rows
+  observation waves: 0 entry, 1 loads + obs noise, 2 table barrier, 6 reset draws,
+                     7 barrier 2 + resets + gate progress, 8 observations + log rows
 """
 import json
 import os
@@ -28,6 +30,15 @@ def build():
     subprocess.run(cmd, shell=True, check=True)
 
 
+ROLE_PHASES = {
+    "physics": [("loads+barrier1+integrate", 0, 3), ("collision", 3, 4), ("termination+handover", 4, 5),
+                ("barrier2+reward+stores", 5, 12), ("log", 12, 8)],
+    "observation": [("loads+barrier1", 0, 1), ("obs_noise", 1, 2), ("reset_draws", 2, 6),
+                    ("barrier2_wait", 6, 13), ("reset_apply+stores", 13, 14), ("advance", 14, 7),
+                    ("obs+log", 7, 8)],
+}
+
+
 def run(n=65536, steps=200):
     os.environ["GR_LIB_PATH"] = os.path.join(OUT, "libgr.so")
     import ctypes as C
@@ -41,39 +52,32 @@ def run(n=65536, steps=200):
     env = bench.make_env(n, 0, "cuda:0", 8, "dd_explicit")
     g = torch.Generator(device="cuda:0").manual_seed(0)
     acts = torch.randn(bench.ACTION_RING, n, 4, device="cuda:0", generator=g)
-    res = []
-    for rep in range(3):
-        for k in range(steps):
-            env.step(acts[k % bench.ACTION_RING])
-        torch.cuda.synchronize()
-        waves = n // 64
-        buf = np.zeros(waves * 16, np.uint64)
-        assert env._lib.gr_debug_read_stamps(buf.ctypes.data_as(C.c_void_p), buf.size) == 0
-        st = buf.reshape(waves, 16).astype(np.int64)
-        cyc = st[:, :9]
-        d = np.diff(cyc, axis=1)
-        life = cyc[:, 8] - cyc[:, 0]
-        rt0, rt1 = st[:, 9], st[:, 10]
-        xcc = (st[:, 11] >> 32) & 0xF
-        span_ns = (rt1.max() - rt0.min()) * 10
-        summary = {
-            "kernel_span_us(realtime)": span_ns / 1e3,
-            "wave_start_spread_us": (rt0.max() - rt0.min()) * 10 / 1e3,
-            "wave_end_spread_us": (rt1.max() - rt1.min()) * 10 / 1e3,
-            "wave_life_us(realtime) p50/p90/max": [float(np.percentile((rt1 - rt0) * 10 / 1e3, q)) for q in (50, 90, 100)],
-            "wave_life_cycles p50/p90/max": [float(np.percentile(life, q)) for q in (50, 90, 100)],
-            "clock_ghz(median)": float(np.median(life / ((rt1 - rt0) * 10.0 + 1e-9))),
-            "phase_cycles_mean": {PHASES[j]: float(d[:, j].mean()) for j in range(8)},
-            "load_issue_cycles_mean": float((st[:, 12] - st[:, 0]).mean()),
-            "counter_landed_cycles_mean": float((st[:, 13] - st[:, 0]).mean()),
-            "istate_landed_cycles_mean": float((st[:, 14] - st[:, 0]).mean()),
-            "phase_cycles_p90": {PHASES[j]: float(np.percentile(d[:, j], 90)) for j in range(8)},
-            "xcc_counts": np.bincount(xcc, minlength=8).tolist(),
-            "start_us_hist": np.histogram((rt0 - rt0.min()) * 10 / 1e3, bins=8)[0].tolist(),
-            "end_us_pcts": [float(np.percentile((rt1 - rt0.min()) * 10 / 1e3, q)) for q in (10, 50, 90, 99, 100)],
+    for k in range(steps):
+        env.step(acts[k % bench.ACTION_RING])
+    torch.cuda.synchronize()
+    waves = (n // 256) * 8  # step kernel: 8 waves per 256-env workgroup
+    buf = np.zeros(waves * 16, np.uint64)
+    assert env._lib.gr_debug_read_stamps(buf.ctypes.data_as(C.c_void_p), buf.size) == 0
+    st = buf.reshape(waves, 16).astype(np.int64)
+    role = (np.arange(waves) % 8) // 4  # waves 0-3 physics, 4-7 observation
+    rt0, rt1 = st[:, 9], st[:, 10]
+    out = {
+        "kernel_span_us(realtime)": float((rt1.max() - rt0.min()) * 10 / 1e3),
+        "wave_start_spread_us": float((rt0.max() - rt0.min()) * 10 / 1e3),
+        "end_us_pcts(10,50,90,99,100)": [float(np.percentile((rt1 - rt0.min()) * 10 / 1e3, q))
+                                         for q in (10, 50, 90, 99, 100)],
+    }
+    for r, name in enumerate(("physics", "observation")):
+        sel = st[role == r]
+        life = sel[:, 8] - sel[:, 0]
+        out[name] = {
+            "life_cycles p50/p90/max": [float(np.percentile(life, q)) for q in (50, 90, 100)],
+            "end_us p50/p90/max": [float(np.percentile((sel[:, 10] - rt0.min()) * 10 / 1e3, q)) for q in (50, 90, 100)],
+            "phase_cycles_mean": {ph: float((sel[:, b_] - sel[:, a_]).mean()) for ph, a_, b_ in ROLE_PHASES[name]},
+            "phase_cycles_p90": {ph: float(np.percentile(sel[:, b_] - sel[:, a_], 90))
+                                 for ph, a_, b_ in ROLE_PHASES[name]},
         }
-        res.append(summary)
-    print(json.dumps(res[-1], indent=1))
+    print(json.dumps(out, indent=1))
     env.close()
 
 
