@@ -65,6 +65,8 @@ int ensure_dev(gr_ctx* c, const char* what) {
   }
   c->args.kc = c->kc_dev;
   c->args.blk_types = c->blk_dev;
+  e = gr::allow_large_lds();
+  if (e != hipSuccess) return hip_fail(c, e, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
   return GR_OK;
 }
 
@@ -119,8 +121,9 @@ void derive(gr_ctx* c) {
     c->blk_types[b] = t0 | (t1 << 16);
   }
   const long bytes = (long)span * g.num_levels * a.track_stride * 4;
-  // table + handover within 64 KiB per workgroup; beyond that the (L2-resident) table is read directly
-  a.lds_bytes = bytes + GR_XCH_BYTES <= 64 * 1024 ? (int)bytes : 0;
+  // table + handovers within the CU's LDS (one workgroup per CU at the bench size); beyond that the
+  // (L2-resident) table is read directly
+  a.lds_bytes = bytes + GR_XCH_BYTES <= 128 * 1024 ? (int)bytes : 0;
 #ifdef GR_ABL_NOLDS
   a.lds_bytes = 0;
 #endif

@@ -7,7 +7,8 @@
 #define GR_BLOCK 256
 #define GR_MAX_TYPES 64
 #define GR_LOG_ROWS_PER_BLOCK 8  // log rows per workgroup (the step kernel has 8 waves)
-#define GR_XCH_BYTES (20 * GR_BLOCK * 4)  // step kernel: physics -> observation handover in LDS
+#define GR_XCH_BYTES ((5 + 6) * GR_BLOCK * 16)  // step kernel handovers in LDS (both directions)
+#define GR_LDS_MAX (160 * 1024)                 // LDS a gfx950 workgroup may allocate
 #define GR_STAMP_WAVES 4096  // diagnostic stamps (GR_STAMPS builds only)
 #define GR_STAMP_SLOTS 16
 
@@ -61,6 +62,7 @@ hipError_t launch_test_dynamics(const KArgs& a, int n, int mode, const float* si
                                 hipStream_t s);
 hipError_t launch_test_math(int fn, int n, const float* x, const float* y, float* out, hipStream_t s);
 hipError_t read_stamps(unsigned long long* host, int n);
+hipError_t allow_large_lds();  // lift the default dynamic-LDS cap of the env kernels
 hipError_t launch_test_philox(int n, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
                               uint32_t* out, hipStream_t s);
 

@@ -475,8 +475,14 @@ DEV void obs_noise(const KArgs& a, uint32_t gid, uint32_t cnt, ObsNoise& on) {
   quat_from_euler_xyz(nz[3] * a.h.obs_att_noise, nz[4] * a.h.obs_att_noise, nz[5] * a.h.obs_att_noise, on.qn);
 }
 
-DEV void write_obs(const KArgs& a, const Tab& tab, const Env& e, int i, uint32_t gid, const ObsNoise& on,
-                   const float lc[4], float aux) {
+// policy / critic observation rows of one env (observation.py:22-63, commands.py:208-245;
+// group order racing_ctbr_env.py:141-169)
+struct ObsRows {
+  float4 c[4], p[4];
+};
+
+DEV void compute_obs(const KArgs& a, const Tab& tab, const Env& e, uint32_t gid, const ObsNoise& on,
+                     const float lc[4], ObsRows& o) {
   const float* rec = tab.rec(e.type, e.lvl);
   int ng = (int)rec[3];
   const float* g = tab.gate(e.type, e.lvl, e.gate);
@@ -492,11 +498,10 @@ DEV void write_obs(const KArgs& a, const Tab& tab, const Env& e, int i, uint32_t
   float cg[3], cn[3];
   quat_rotate_inverse(e.q, d, cg);
   quat_rotate_inverse(e.q, dn, cn);
-  float4* C = reinterpret_cast<float4*>(a.buf.obs_critic) + (size_t)i * 4;
-  C[0] = make_float4(vb[0], vb[1], vb[2], r2[0]);
-  C[1] = make_float4(r2[1], r2[2], cg[0], cg[1]);
-  C[2] = make_float4(cg[2], cn[0], cn[1], cn[2]);
-  C[3] = make_float4(lc[0], lc[1], lc[2], lc[3]);
+  o.c[0] = make_float4(vb[0], vb[1], vb[2], r2[0]);
+  o.c[1] = make_float4(r2[1], r2[2], cg[0], cg[1]);
+  o.c[2] = make_float4(cg[2], cn[0], cn[1], cn[2]);
+  o.c[3] = make_float4(lc[0], lc[1], lc[2], lc[3]);
   float qq[4], r2n[3];
   quat_mul(e.q, on.qn, qq);
   matrix_row2(qq, r2n);
@@ -511,12 +516,35 @@ DEV void write_obs(const KArgs& a, const Tab& tab, const Env& e, int i, uint32_t
   quat_rotate_inverse(e.q, dnp, pn);
   float vn[3];
   for (int k = 0; k < 3; ++k) vn[k] = vb[k] * on.vfac[k];
+  o.p[0] = make_float4(vn[0], vn[1], vn[2], r2n[0]);
+  o.p[1] = make_float4(r2n[1], r2n[2], pg[0], pg[1]);
+  o.p[2] = make_float4(pg[2], pn[0], pn[1], pn[2]);
+  o.p[3] = make_float4(lc[0], lc[1], lc[2], lc[3]);
+}
+
+// one lane writes its env's 64-byte rows (4 x 16 B, 64-byte lane stride)
+DEV void store_obs_direct(const KArgs& a, int i, const ObsRows& o, float aux) {
+  float4* C = reinterpret_cast<float4*>(a.buf.obs_critic) + (size_t)i * 4;
   float4* P = reinterpret_cast<float4*>(a.buf.obs_policy) + (size_t)i * 4;
-  P[0] = make_float4(vn[0], vn[1], vn[2], r2n[0]);
-  P[1] = make_float4(r2n[1], r2n[2], pg[0], pg[1]);
-  P[2] = make_float4(pg[2], pn[0], pn[1], pn[2]);
-  P[3] = make_float4(lc[0], lc[1], lc[2], lc[3]);
+  for (int k = 0; k < 4; ++k) C[k] = o.c[k];
+  for (int k = 0; k < 4; ++k) P[k] = o.p[k];
   a.buf.obs_aux[i] = aux;
+}
+
+// The same rows written by a whole wave through an LDS transpose, so each store
+// instruction covers 1 KiB of consecutive bytes (16 envs x 64 B) instead of 64
+// scattered 16-byte pieces: the store path of a CU is the tail of the step.
+// `stage` = this wave's 4 x 64 float4 LDS slots (quad-major: conflict-free writes).
+DEV void store_rows_staged(float4* dst, int env0, int n, const float4 rows[4], float4* stage) {
+  const int l = threadIdx.x & 63;
+  for (int q = 0; q < 4; ++q) stage[q * GR_BLOCK + l] = rows[q];
+  __asm__ volatile("" ::: "memory");  // LDS ops of a wave retire in order; keep the compiler from reordering
+  for (int j = 0; j < 4; ++j) {
+    const int env = 16 * j + (l >> 2), q = l & 3;
+    const float4 v = stage[q * GR_BLOCK + env];
+    if (env0 + env < n) dst[(size_t)(env0 + env) * 4 + q] = v;
+  }
+  __asm__ volatile("" ::: "memory");
 }
 
 // ------------------------------------------------------------- log reduction
@@ -526,7 +554,10 @@ DEV void write_obs(const KArgs& a, const Tab& tab, const Env& e, int i, uint32_t
 // the wave's reset ballot with wave-uniform lane reads; the two all-env sums
 // (terrain level, noise level) use a butterfly.  Means are formed on demand.
 
+// a wave-uniform row of GR_LOG_SLOTS floats, written by lane 0 (five 16-byte stores).  (Spreading
+// the row over lanes 0-4 in one store instruction measured 2 us SLOWER per step on gfx950.)
 DEV void log_row_store(const KArgs& a, int row, const float v[GR_LOG_SLOTS]) {
+  if ((threadIdx.x & 63) != 0) return;
   float4* r = reinterpret_cast<float4*>(a.buf.log_partial + ((size_t)blockIdx.x * GR_LOG_ROWS_PER_BLOCK + row) *
                                                                 GR_LOG_SLOTS);
   r[0] = make_float4(v[0], v[1], v[2], v[3]);
@@ -544,22 +575,35 @@ DEV void wave_log_resets(const KArgs& a, int row, const float lg[GR_LOG_SLOTS], 
   while (m) {
     const int l = __builtin_ctzll(m);
     m &= m - 1;
-    for (int s = 0; s < GR_LOG_LEVEL; ++s) acc[s] += __shfl(lg[s], l, 64);
+    for (int s = 0; s < GR_LOG_LEVEL; ++s) acc[s] += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lg[s]), l));
   }
-  if ((threadIdx.x & 63) == 0) log_row_store(a, row, acc);
+  log_row_store(a, row, acc);
+}
+
+// wave-wide float sum by DPP (no LDS round trips); the total lands in lane 63
+template <int CTRL, int ROWS>
+DEV float dpp_term(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xF, false));
+}
+DEV float wave_sum63(float v) {
+  v = v + dpp_term<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+  v = v + dpp_term<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+  v = v + dpp_term<0x141, 0xF>(v);  // row_half_mirror
+  v = v + dpp_term<0x140, 0xF>(v);  // row_mirror: every lane of a row holds the row sum
+  v = v + dpp_term<0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3
+  v = v + dpp_term<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
+  return v;
 }
 
 // all-env slots (terrain level, noise level) of this wave -> row
 DEV void wave_log_levels(const KArgs& a, int row, float level, float noise) {
-  for (int off = 32; off > 0; off >>= 1) {
-    level += __shfl_xor(level, off, 64);
-    noise += __shfl_xor(noise, off, 64);
-  }
+  level = __shfl(wave_sum63(level), 63, 64);
+  noise = __shfl(wave_sum63(noise), 63, 64);
   float v[GR_LOG_SLOTS];
   for (int s = 0; s < GR_LOG_SLOTS; ++s) v[s] = 0.0f;
   v[GR_LOG_LEVEL] = level;
   v[GR_LOG_NOISE] = noise;
-  if ((threadIdx.x & 63) == 0) log_row_store(a, row, v);
+  log_row_store(a, row, v);
 }
 
 // ------------------------------------------------------------- gate table staging
@@ -666,7 +710,9 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const KConst* __
     reset_env(a, sl.tab, e, gid);
   }
   if (live) {
-    write_obs(a, sl.tab, e, i, gid, on, lc, aux);
+    ObsRows o;
+    compute_obs(a, sl.tab, e, gid, on, lc, o);
+    store_obs_direct(a, i, o, aux);
     if (reset_lane) {
       store_dyn(a, i, e);
       store_rst(a, i, e);
@@ -688,8 +734,10 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const KConst* __
 // wave can issue a VALU op only every 4 cycles, two can use the SIMD every 2,
 // and one wave's memory / LDS / transcendental latency hides under the other's
 // work.  (ManagerBasedDiffRLEnv.step, manager_based_diff_rl_env.py:160-267.)
-// handover rows (float4 per env): p + aux, q, v + done, lag, last ctbr
+// handover rows (float4 per env), physics -> observation: p + aux, q, v + done, lag, last ctbr;
+// then observation -> physics: the next episode's start state (state-plane layout)
 enum { X_PA = 0, X_Q = 1, X_VD = 2, X_LAG = 3, X_LC = 4, GR_XF4 = 5, GR_XF = 4 * GR_XF4 };
+enum { R_POSQ = 0, R_QV = 1, R_VW = 2, R_W = 3, R_RST0 = 4, R_RST1 = 5, GR_RF4 = 6 };
 
 template <bool USE_LDS>
 __global__ __launch_bounds__(2 * GR_BLOCK) void step_kernel(KArgs a, const KConst* __restrict__ kc,
@@ -827,14 +875,6 @@ __global__ __launch_bounds__(2 * GR_BLOCK) void step_kernel(KArgs a, const KCons
       e.es[k] = e.es[k] + v;
     }
     e.mar = f[2];
-    if (live) {
-      a.buf.reward[i] = rew;
-      a.buf.terminated[i] = (uint8_t)terminated;
-      a.buf.time_out[i] = (uint8_t)time_out;
-      a.buf.dones[i] = (int64_t)(terminated | time_out);
-      if (!done) store_dyn(a, i, e);  // resetting envs: written by the observation waves
-    }
-    STAMP(12);
     // episode metrics of the resetting envs (reward / termination / command managers' reset logs)
     float lg[GR_LOG_SLOTS];
     for (int s = 0; s < GR_LOG_SLOTS; ++s) lg[s] = 0.0f;
@@ -849,7 +889,31 @@ __global__ __launch_bounds__(2 * GR_BLOCK) void step_kernel(KArgs a, const KCons
       lg[GR_LOG_T_TIMEOUT] = (float)time_out;
       lg[GR_LOG_T_CONTACT] = (float)c_term;
       lg[GR_LOG_T_BADPOSE] = (float)bad;
+      // the next episode's start state, from the observation waves (events.py:139-177 et al.)
+      const float4* xr = xch + GR_XF4 * GR_BLOCK;
+      const float4 r0 = xr[R_POSQ * GR_BLOCK + t], r1 = xr[R_QV * GR_BLOCK + t], r2 = xr[R_VW * GR_BLOCK + t];
+      const float4 r3 = xr[R_W * GR_BLOCK + t], r4 = xr[R_RST0 * GR_BLOCK + t], r5 = xr[R_RST1 * GR_BLOCK + t];
+      e.p[0] = r0.x; e.p[1] = r0.y; e.p[2] = r0.z; e.q[0] = r0.w;
+      e.q[1] = r1.x; e.q[2] = r1.y; e.q[3] = r1.z; e.v[0] = r1.w;
+      e.v[1] = r2.x; e.v[2] = r2.y; e.w[0] = r2.z; e.w[1] = r2.w;
+      e.w[2] = r3.x;
+      for (int k = 0; k < 3; ++k) { e.al[k] = 0.0f; e.tau[k] = 0.0f; }
+      e.T = 0.0f;
+      for (int k = 0; k < 4; ++k) e.mw[k] = 0.0f;
+      for (int k = 0; k < 7; ++k) e.es[k] = 0.0f;
+      e.mar = 0.0f;
+      e.thr = r4.x; e.nl = r4.y; e.k2[0] = r4.z; e.k2[1] = r4.w;
+      e.k2[2] = r5.x; e.k1[0] = r5.y; e.k1[1] = r5.z; e.k1[2] = r5.w;
     }
+    if (live) {
+      a.buf.reward[i] = rew;
+      a.buf.terminated[i] = (uint8_t)terminated;
+      a.buf.time_out[i] = (uint8_t)time_out;
+      a.buf.dones[i] = (int64_t)(terminated | time_out);
+      store_dyn(a, i, e);
+      if (done) store_rst(a, i, e);
+    }
+    STAMP(12);
 #ifndef GR_ABL_NOLOG
     wave_log_resets(a, threadIdx.x >> 6, lg, reset_lane);
 #endif
@@ -881,28 +945,39 @@ __global__ __launch_bounds__(2 * GR_BLOCK) void step_kernel(KArgs a, const KCons
     // call counter for the observation-noise stream: double-buffered by call parity,
     // so this write never races with the reads of the current launch
     if (t == 0 && blockIdx.x == 0) a.buf.counters[a.buf.counter_index ^ 1] = cnt + 1u;
-    // the next episode's draws, for every env (only the resetting ones use them)
+    // the next episode's start state, for every env (only the resetting ones use it): a reset
+    // depends only on the episode bookkeeping loaded above, not on this step's physics
     ResetDraws rd;
     reset_draws(a, gid, (uint32_t)e.epoch + 1u, e.mc, rd);
+    Env er = e;
+    reset_apply(a, sl.tab, er, rd);
+    {  // hand the candidates to the physics waves, which write the state planes of every env
+      float4* xr = xch + GR_XF4 * GR_BLOCK;
+      xr[R_POSQ * GR_BLOCK + t] = make_float4(er.p[0], er.p[1], er.p[2], er.q[0]);
+      xr[R_QV * GR_BLOCK + t] = make_float4(er.q[1], er.q[2], er.q[3], er.v[0]);
+      xr[R_VW * GR_BLOCK + t] = make_float4(er.v[1], er.v[2], er.w[0], er.w[1]);
+      xr[R_W * GR_BLOCK + t] = make_float4(er.w[2], 0.0f, 0.0f, 0.0f);
+      xr[R_RST0 * GR_BLOCK + t] = make_float4(er.thr, er.nl, er.k2[0], er.k2[1]);
+      xr[R_RST1 * GR_BLOCK + t] = make_float4(er.k2[2], er.k1[0], er.k1[1], er.k1[2]);
+    }
     STAMP(6);
     __syncthreads();  // barrier 2: handover
     STAMP(13);
     const float4 xpa = xch[X_PA * GR_BLOCK + t], xq = xch[X_Q * GR_BLOCK + t], xvd = xch[X_VD * GR_BLOCK + t];
     const float4 xlag = xch[X_LAG * GR_BLOCK + t], xlc = xch[X_LC * GR_BLOCK + t];
-    e.p[0] = xpa.x; e.p[1] = xpa.y; e.p[2] = xpa.z;
-    e.q[0] = xq.x; e.q[1] = xq.y; e.q[2] = xq.z; e.q[3] = xq.w;
-    e.v[0] = xvd.x; e.v[1] = xvd.y; e.v[2] = xvd.z;
-    e.lag[0] = xlag.x; e.lag[1] = xlag.y; e.lag[2] = xlag.z; e.lag[3] = xlag.w;
     const float lc[4] = {xlc.x, xlc.y, xlc.z, xlc.w};
     const float aux = xpa.w;
     const bool done = xvd.w != 0.0f;
-    e.ep += 1;
-    e.azero = 0;
     if (done && live) {
-      reset_apply(a, sl.tab, e, rd);
-      store_dyn(a, i, e);
-      store_rst(a, i, e);
+      e = er;
+    } else {
+      e.p[0] = xpa.x; e.p[1] = xpa.y; e.p[2] = xpa.z;
+      e.q[0] = xq.x; e.q[1] = xq.y; e.q[2] = xq.z; e.q[3] = xq.w;
+      e.v[0] = xvd.x; e.v[1] = xvd.y; e.v[2] = xvd.z;
+      e.ep += 1;
+      e.azero = 0;
     }
+    e.lag[0] = xlag.x; e.lag[1] = xlag.y; e.lag[2] = xlag.z; e.lag[3] = xlag.w;
     STAMP(14);
     // command compute: _update_metrics + _update_command (commands.py:247-260, 308-350)
     {
@@ -916,12 +991,19 @@ __global__ __launch_bounds__(2 * GR_BLOCK) void step_kernel(KArgs a, const KCons
       }
     }
     STAMP(7);
-    if (live) {
-      store_istate(a, i, e);
+    if (live) store_istate(a, i, e);
 #ifndef GR_ABL_NOOBS
-      write_obs(a, sl.tab, e, i, gid, on, lc, aux);
-#endif
+    {
+      ObsRows o;
+      compute_obs(a, sl.tab, e, gid, on, lc, o);
+      // this wave's handover slots are free once read (rows X_PA.. of its own 64 envs)
+      float4* stage = xch + (t & ~63);
+      const int env0 = blockIdx.x * GR_BLOCK + (t & ~63);
+      store_rows_staged(reinterpret_cast<float4*>(a.buf.obs_critic), env0, n, o.c, stage);
+      store_rows_staged(reinterpret_cast<float4*>(a.buf.obs_policy), env0, n, o.p, stage);
+      if (live) a.buf.obs_aux[i] = aux;
     }
+#endif
 #ifndef GR_ABL_NOLOG
     wave_log_levels(a, threadIdx.x >> 6, live ? (float)e.lvl : 0.0f, live ? e.nl : 0.0f);
 #endif
@@ -1121,7 +1203,7 @@ static hipError_t launch_env_mode(const KArgs& a, const float* actions, const ui
   const int g = grid_of(a.h.num_envs);
   const bool lds = a.h.lds_tab_vec > 0;
   if constexpr (MODE == KMODE_STEP) {
-    const size_t bytes = (size_t)a.h.lds_tab_vec * 16 + (size_t)GR_XF * GR_BLOCK * 4;
+    const size_t bytes = (size_t)a.h.lds_tab_vec * 16 + (size_t)(GR_XF4 + GR_RF4) * GR_BLOCK * 16;
     if (lds)
       hipLaunchKernelGGL(step_kernel<true>, dim3(g), dim3(2 * GR_BLOCK), bytes, s, a, a.kc, actions);
     else
@@ -1179,6 +1261,20 @@ hipError_t launch_test_philox(int n, uint32_t c0, uint32_t c1, uint32_t c2, uint
                               uint32_t* out, hipStream_t s) {
   hipLaunchKernelGGL(test_philox_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, c0, c1, c2, c3, k0, k1, out);
   return hipGetLastError();
+}
+
+hipError_t allow_large_lds() {
+#ifdef GR_ABL_NO_LDS_ATTR
+  return hipSuccess;
+#endif
+  const void* ks[] = {reinterpret_cast<const void*>(&step_kernel<true>),
+                      reinterpret_cast<const void*>(&env_kernel<KMODE_RESET, true>),
+                      reinterpret_cast<const void*>(&env_kernel<KMODE_OBSERVE, true>)};
+  for (const void* k : ks) {
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t read_stamps(unsigned long long* host, int n) {

@@ -2,6 +2,9 @@
  * gr_math.h — portable fp32 elementary functions (exp, tanh, log, sincos,
  * atan2) built only from IEEE-754 correctly-rounded +,-,*,/ and sqrt.
  *
+ * Polynomial steps use an explicit fused multiply-add (gr_fmaf), correctly rounded
+ * on both sides, so they stay bit-identical with -ffp-contract=off elsewhere.
+ *
  * Why this exists: the env step draws Gaussian noise (Box-Muller: log, sin,
  * cos), squashes actions (tanh) and samples reset yaw (atan2).  If the HIP
  * kernel used the device's hardware approximations (v_exp_f32, v_sin_f32 …)
@@ -31,6 +34,9 @@ GR_HD float gr_copysignf(float m, float s) {
   return gr_u2f((gr_f2u(m) & 0x7fffffffu) | (gr_f2u(s) & 0x80000000u));
 }
 GR_HD float gr_sqrtf(float x) { return __builtin_sqrtf(x); }
+/* fused multiply-add, correctly rounded on both sides (v_fma_f32 / x86 vfmadd, the
+ * oracle is built with -mfma): one rounding per polynomial step, half the instructions */
+GR_HD float gr_fmaf(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 GR_HD float gr_floorf(float x) { return __builtin_floorf(x); }
 GR_HD float gr_minf(float a, float b) { return a < b ? a : b; }
 GR_HD float gr_maxf(float a, float b) { return a > b ? a : b; }
@@ -44,17 +50,17 @@ GR_HD float gr_exp2i(int k) { return gr_u2f((uint32_t)(k + 127) << 23); }
 GR_HD float gr_expf(float x) {
   if (x < -87.0f) return 0.0f;
   if (x > 88.0f) x = 88.0f;
-  float kf = gr_floorf(x * 1.44269502f + 0.5f);
+  float kf = gr_floorf(gr_fmaf(x, 1.44269502f, 0.5f));
   int k = (int)kf;
-  float r = (x - kf * 0.693115234375f) - kf * 3.19461833e-05f; /* Cody-Waite ln2 */
-  float p = 1.98412698e-04f;                                   /* 1/5040 */
-  p = p * r + 1.38888889e-03f;                                 /* 1/720 */
-  p = p * r + 8.33333333e-03f;                                 /* 1/120 */
-  p = p * r + 4.16666667e-02f;                                 /* 1/24 */
-  p = p * r + 1.66666667e-01f;                                 /* 1/6 */
-  p = p * r + 0.5f;
-  p = p * r + 1.0f;
-  p = p * r + 1.0f;
+  float r = gr_fmaf(-kf, 3.19461833e-05f, gr_fmaf(-kf, 0.693115234375f, x)); /* Cody-Waite ln2 */
+  float p = 1.98412698e-04f;                                                 /* 1/5040 */
+  p = gr_fmaf(p, r, 1.38888889e-03f);                                        /* 1/720 */
+  p = gr_fmaf(p, r, 8.33333333e-03f);                                        /* 1/120 */
+  p = gr_fmaf(p, r, 4.16666667e-02f);                                        /* 1/24 */
+  p = gr_fmaf(p, r, 1.66666667e-01f);                                        /* 1/6 */
+  p = gr_fmaf(p, r, 0.5f);
+  p = gr_fmaf(p, r, 1.0f);
+  p = gr_fmaf(p, r, 1.0f);
   return p * gr_exp2i(k);
 }
 
@@ -65,11 +71,11 @@ GR_HD float gr_tanhf(float x) {
   if (ax < 0.3f) {
     float x2 = x * x;
     float p = -8.86323552e-03f;          /* -1382/155925 */
-    p = p * x2 + 2.18694885e-02f;        /* 62/2835 */
-    p = p * x2 + -5.39682540e-02f;       /* -17/315 */
-    p = p * x2 + 1.33333333e-01f;        /* 2/15 */
-    p = p * x2 + -3.33333333e-01f;       /* -1/3 */
-    return x + x * (x2 * p);
+    p = gr_fmaf(p, x2, 2.18694885e-02f); /* 62/2835 */
+    p = gr_fmaf(p, x2, -5.39682540e-02f); /* -17/315 */
+    p = gr_fmaf(p, x2, 1.33333333e-01f); /* 2/15 */
+    p = gr_fmaf(p, x2, -3.33333333e-01f); /* -1/3 */
+    return gr_fmaf(x, x2 * p, x);
   }
   if (ax > 9.0f) {
     r = 1.0f;
@@ -89,33 +95,33 @@ GR_HD float gr_logf(float x) {
   float f = (m - 1.0f) / (m + 1.0f);
   float f2 = f * f;
   float s = 1.53846154e-01f;             /* 2/13 */
-  s = s * f2 + 1.81818182e-01f;          /* 2/11 */
-  s = s * f2 + 2.22222222e-01f;          /* 2/9 */
-  s = s * f2 + 2.85714286e-01f;          /* 2/7 */
-  s = s * f2 + 4.00000000e-01f;          /* 2/5 */
-  s = s * f2 + 6.66666667e-01f;          /* 2/3 */
+  s = gr_fmaf(s, f2, 1.81818182e-01f);   /* 2/11 */
+  s = gr_fmaf(s, f2, 2.22222222e-01f);   /* 2/9 */
+  s = gr_fmaf(s, f2, 2.85714286e-01f);   /* 2/7 */
+  s = gr_fmaf(s, f2, 4.00000000e-01f);   /* 2/5 */
+  s = gr_fmaf(s, f2, 6.66666667e-01f);   /* 2/3 */
   float ef = (float)e;
-  float lo = f * (f2 * s) + ef * 3.19461833e-05f;
-  return (ef * 0.693115234375f + 2.0f * f) + lo;
+  float lo = gr_fmaf(f, f2 * s, ef * 3.19461833e-05f);
+  return gr_fmaf(ef, 0.693115234375f, 2.0f * f) + lo;
 }
 
 /* sin and cos of x for |x| < ~1e3 (Cody-Waite by pi/2), <= 2 ulp away from 0 */
 GR_HD void gr_sincosf(float x, float* s_out, float* c_out) {
-  float kf = gr_floorf(x * 0.636619747f + 0.5f);
+  float kf = gr_floorf(gr_fmaf(x, 0.636619747f, 0.5f));
   int k = (int)kf;
-  float r = ((x - kf * 1.5703125f) - kf * 4.83751297e-04f) - kf * 7.54979013e-08f;
+  float r = gr_fmaf(-kf, 7.54979013e-08f, gr_fmaf(-kf, 4.83751297e-04f, gr_fmaf(-kf, 1.5703125f, x)));
   float r2 = r * r;
   float sp = 2.75573192e-06f;            /* 1/9! */
-  sp = sp * r2 + -1.98412698e-04f;       /* -1/7! */
-  sp = sp * r2 + 8.33333333e-03f;        /* 1/5! */
-  sp = sp * r2 + -1.66666667e-01f;       /* -1/3! */
-  float s = r + r * (r2 * sp);
+  sp = gr_fmaf(sp, r2, -1.98412698e-04f); /* -1/7! */
+  sp = gr_fmaf(sp, r2, 8.33333333e-03f); /* 1/5! */
+  sp = gr_fmaf(sp, r2, -1.66666667e-01f); /* -1/3! */
+  float s = gr_fmaf(r, r2 * sp, r);
   float cp = -2.75573192e-07f;           /* -1/10! */
-  cp = cp * r2 + 2.48015873e-05f;        /* 1/8! */
-  cp = cp * r2 + -1.38888889e-03f;       /* -1/6! */
-  cp = cp * r2 + 4.16666667e-02f;        /* 1/4! */
-  cp = cp * r2 + -0.5f;
-  float c = 1.0f + r2 * cp;
+  cp = gr_fmaf(cp, r2, 2.48015873e-05f); /* 1/8! */
+  cp = gr_fmaf(cp, r2, -1.38888889e-03f); /* -1/6! */
+  cp = gr_fmaf(cp, r2, 4.16666667e-02f); /* 1/4! */
+  cp = gr_fmaf(cp, r2, -0.5f);
+  float c = gr_fmaf(r2, cp, 1.0f);
   switch (k & 3) {
     case 0: *s_out = s; *c_out = c; break;
     case 1: *s_out = c; *c_out = -s; break;
@@ -133,16 +139,16 @@ GR_HD float gr_atan_unit(float t) {
   }
   float t2 = t * t;
   float p = -4.76190476e-02f;            /* -1/21 */
-  p = p * t2 + 5.26315789e-02f;          /* 1/19 */
-  p = p * t2 + -5.88235294e-02f;         /* -1/17 */
-  p = p * t2 + 6.66666667e-02f;          /* 1/15 */
-  p = p * t2 + -7.69230769e-02f;         /* -1/13 */
-  p = p * t2 + 9.09090909e-02f;          /* 1/11 */
-  p = p * t2 + -1.11111111e-01f;         /* -1/9 */
-  p = p * t2 + 1.42857143e-01f;          /* 1/7 */
-  p = p * t2 + -2.00000000e-01f;         /* -1/5 */
-  p = p * t2 + 3.33333333e-01f;          /* 1/3 */
-  return base + (t - t * (t2 * p));
+  p = gr_fmaf(p, t2, 5.26315789e-02f);   /* 1/19 */
+  p = gr_fmaf(p, t2, -5.88235294e-02f);  /* -1/17 */
+  p = gr_fmaf(p, t2, 6.66666667e-02f);   /* 1/15 */
+  p = gr_fmaf(p, t2, -7.69230769e-02f);  /* -1/13 */
+  p = gr_fmaf(p, t2, 9.09090909e-02f);   /* 1/11 */
+  p = gr_fmaf(p, t2, -1.11111111e-01f);  /* -1/9 */
+  p = gr_fmaf(p, t2, 1.42857143e-01f);   /* 1/7 */
+  p = gr_fmaf(p, t2, -2.00000000e-01f);  /* -1/5 */
+  p = gr_fmaf(p, t2, 3.33333333e-01f);   /* 1/3 */
+  return base + gr_fmaf(-t, t2 * p, t);
 }
 
 /* atan2(y, x) with C semantics for finite inputs (atan2(0,0)=0) */

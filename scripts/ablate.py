@@ -18,6 +18,7 @@ VARIANTS = {
     "base": [], "noreset": ["GR_ABL_NORESET"], "nocoll": ["GR_ABL_NOCOLL"], "noobsnoise": ["GR_ABL_NOOBSNOISE"],
     "nogatenoise": ["GR_ABL_NOGATENOISE"], "nolog": ["GR_ABL_NOLOG"], "noobs": ["GR_ABL_NOOBS"],
     "nolds": ["GR_ABL_NOLDS"],
+    "noldsattr": ["GR_ABL_NO_LDS_ATTR"],
     "all": ["GR_ABL_NORESET", "GR_ABL_NOCOLL", "GR_ABL_NOOBSNOISE", "GR_ABL_NOGATENOISE", "GR_ABL_NOLOG", "GR_ABL_NOOBS"],
 }
 
