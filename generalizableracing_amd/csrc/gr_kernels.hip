@@ -363,16 +363,16 @@ struct ResetDraws {
   float p[3], att[3], v[3], wv[3];  // spawn position, roll/pitch/yaw offsets, linear / angular velocity
   float k2[3], k1[3];               // drag (random_drag)
   float lvl_u, thr;                 // random level for "beyond the last level", thrust-estimate error
+  float sr, cr, sp, cp;             // sin/cos of roll/2 and pitch/2 (quat_from_euler_xyz)
 };
 
 // 24 x 21-bit fields: pos 0-2, att 3-5, vel 6-11, z-drag 12, k2 13-15, k1 16-18, level 19, thr 20-21
 DEV void reset_draws(const KArgs& a, uint32_t gid, uint32_t ep, float m_ctrl, ResetDraws& r) {
   const gr_config& c = a.kc->cfg;
   uint32_t f[24];
-  gr_fields6(draw(a, gid, ep, GR_TAG_RESET, 0), f);
-  gr_fields6(draw(a, gid, ep, GR_TAG_RESET, 1), f + 6);
-  gr_fields6(draw(a, gid, ep, GR_TAG_RESET, 2), f + 12);
-  gr_fields6(draw(a, gid, ep, GR_TAG_RESET, 3), f + 18);
+  gr_u32x4 w4[4];
+  gr_philox4x32_10_x4(gid, ep, GR_TAG_RESET, 0u, a.h.seed_lo, a.h.seed_hi, w4);
+  for (int j = 0; j < 4; ++j) gr_fields6(w4[j], f + 6 * j);
   r.lvl_u = gr_f21(f[19]);
   for (int k = 0; k < 3; ++k) {
     r.p[k] = c.spawn_pos[k] + gr_uniform21(f[k], -c.reset_pos_half[k], c.reset_pos_half[k]);
@@ -380,7 +380,7 @@ DEV void reset_draws(const KArgs& a, uint32_t gid, uint32_t ep, float m_ctrl, Re
     r.v[k] = 0.0f + gr_uniform21(f[6 + k], -c.reset_vel_half[k], c.reset_vel_half[k]);
     r.wv[k] = 0.0f + gr_uniform21(f[9 + k], -c.reset_vel_half[3 + k], c.reset_vel_half[3 + k]);
   }
-  if (c.random_drag) {
+  {  // drag DR (applied only with random_drag; computed unconditionally to keep one basic block)
     float z = c.z_drag + gr_f21(f[12]) * c.z_drag_rand;
     for (int k = 0; k < 3; ++k) {
       r.k2[k] = c.drag2[k] * m_ctrl + gr_f21(f[13 + k]) * c.drag2_rand;
@@ -392,6 +392,8 @@ DEV void reset_draws(const KArgs& a, uint32_t gid, uint32_t ep, float m_ctrl, Re
   float z0, z1;
   gr_box_muller21(f[20], f[21], &z0, &z1);
   r.thr = 1.0f + z0 * 0.01f;
+  gr_sincosf(r.att[0] * 0.5f, &r.sr, &r.cr);
+  gr_sincosf(r.att[1] * 0.5f, &r.sp, &r.cp);
 }
 
 DEV void reset_apply(const KArgs& a, const Tab& tab, Env& e, const ResetDraws& r) {
@@ -400,11 +402,12 @@ DEV void reset_apply(const KArgs& a, const Tab& tab, Env& e, const ResetDraws& r
   int lvl = e.lvl + up - down;
   if (lvl >= c.num_levels) lvl = (int)gr_floorf(r.lvl_u * (float)c.num_levels);
   else if (lvl < 0) lvl = 0;
-  if (c.noise_curriculum) {
+  {
     float upf = e.acc >= c.noise_enhance_threshold ? 1.0f + c.noise_enhance : 1.0f;
     float dnf = e.acc < c.noise_decay_threshold ? 1.0f - c.noise_decay : 1.0f;
-    e.nl = e.nl * upf;
-    e.nl = e.nl * dnf;
+    float nl = e.nl * upf;
+    nl = nl * dnf;
+    e.nl = c.noise_curriculum ? nl : e.nl;
   }
   e.lvl = lvl;
   for (int k = 0; k < 3; ++k) e.p[k] = r.p[k];
@@ -414,7 +417,15 @@ DEV void reset_apply(const KArgs& a, const Tab& tab, Env& e, const ResetDraws& r
   float tx = g0[0] - e.p[0], ty = g0[1] - e.p[1];
   float yaw = gr_wrap_to_pi(gr_atan2f(ty, tx)) + r.att[2];
   float qd[4], qid[4] = {1.0f, 0.0f, 0.0f, 0.0f};
-  quat_from_euler_xyz(r.att[0], r.att[1], yaw, qd);
+  {  // quat_from_euler_xyz(roll, pitch, yaw) with the roll/pitch half-angle sincos drawn ahead
+    float sy, cy;
+    gr_sincosf(yaw * 0.5f, &sy, &cy);
+    const float sr = r.sr, cr = r.cr, sp = r.sp, cp = r.cp;
+    qd[0] = (cy * cr) * cp + (sy * sr) * sp;
+    qd[1] = (cy * sr) * cp - (sy * cr) * sp;
+    qd[2] = (cy * cr) * sp + (sy * sr) * cp;
+    qd[3] = (sy * cr) * cp - (cy * sr) * sp;
+  }
   quat_mul(qid, qd, e.q);
   for (int k = 0; k < 3; ++k) e.v[k] = r.v[k];
   quat_rotate_inverse(e.q, r.wv, e.w);
@@ -422,8 +433,10 @@ DEV void reset_apply(const KArgs& a, const Tab& tab, Env& e, const ResetDraws& r
   e.T = 0.0f;
   for (int k = 0; k < 3; ++k) { e.tau[k] = 0.0f; e.al[k] = 0.0f; }
   for (int k = 0; k < 4; ++k) e.mw[k] = 0.0f;
-  if (c.random_drag)
-    for (int k = 0; k < 3; ++k) { e.k2[k] = r.k2[k]; e.k1[k] = r.k1[k]; }
+  for (int k = 0; k < 3; ++k) {
+    e.k2[k] = c.random_drag ? r.k2[k] : e.k2[k];
+    e.k1[k] = c.random_drag ? r.k1[k] : e.k1[k];
+  }
   e.thr = r.thr;
   for (int k = 0; k < 7; ++k) e.es[k] = 0.0f;
   e.mar = 0.0f;
@@ -463,13 +476,14 @@ struct ObsNoise {
 };
 
 DEV void obs_noise(const KArgs& a, uint32_t gid, uint32_t cnt, ObsNoise& on) {
-  float nz[6] = {0, 0, 0, 0, 0, 0};
-  if (a.h.obs_noise) {
+  float nz[6];
+  {  // drawn unconditionally (one basic block for the scheduler), zeroed without obs noise
     uint32_t f[6];
     gr_fields6(draw(a, gid, cnt, GR_TAG_OBS, 0), f);
     gr_box_muller21(f[0], f[1], &nz[0], &nz[1]);
     gr_box_muller21(f[2], f[3], &nz[2], &nz[3]);
     gr_box_muller21(f[4], f[5], &nz[4], &nz[5]);
+    for (int k = 0; k < 6; ++k) nz[k] = a.h.obs_noise ? nz[k] : 0.0f;
   }
   for (int k = 0; k < 3; ++k) on.vfac[k] = 1.0f + nz[k] * a.h.obs_lin_vel_noise;
   quat_from_euler_xyz(nz[3] * a.h.obs_att_noise, nz[4] * a.h.obs_att_noise, nz[5] * a.h.obs_att_noise, on.qn);
@@ -481,15 +495,21 @@ struct ObsRows {
   float4 c[4], p[4];
 };
 
-DEV void compute_obs(const KArgs& a, const Tab& tab, const Env& e, uint32_t gid, const ObsNoise& on,
-                     const float lc[4], ObsRows& o) {
+// the gates an observation refers to: current and next of the env's track
+DEV void obs_gates(const Tab& tab, const Env& e, float g0[3], float gn0[3]) {
   const float* rec = tab.rec(e.type, e.lvl);
   int ng = (int)rec[3];
   const float* g = tab.gate(e.type, e.lvl, e.gate);
   int gnext = e.gate + 1;
   if (gnext >= ng) gnext -= ng;
   const float* gn = tab.gate(e.type, e.lvl, gnext);
-  float g0[3] = {g[0], g[1], g[2]}, gn0[3] = {gn[0], gn[1], gn[2]};
+  for (int k = 0; k < 3; ++k) { g0[k] = g[k]; gn0[k] = gn[k]; }
+}
+
+// critic row: noise-free (observation.py:97-104, commands.py:233-245)
+DEV void compute_critic(const Tab& tab, const Env& e, const float lc[4], float4 c[4]) {
+  float g0[3], gn0[3];
+  obs_gates(tab, e, g0, gn0);
   float vb[3], r2[3];
   quat_rotate_inverse(e.q, e.v, vb);
   matrix_row2(e.q, r2);
@@ -498,10 +518,19 @@ DEV void compute_obs(const KArgs& a, const Tab& tab, const Env& e, uint32_t gid,
   float cg[3], cn[3];
   quat_rotate_inverse(e.q, d, cg);
   quat_rotate_inverse(e.q, dn, cn);
-  o.c[0] = make_float4(vb[0], vb[1], vb[2], r2[0]);
-  o.c[1] = make_float4(r2[1], r2[2], cg[0], cg[1]);
-  o.c[2] = make_float4(cg[2], cn[0], cn[1], cn[2]);
-  o.c[3] = make_float4(lc[0], lc[1], lc[2], lc[3]);
+  c[0] = make_float4(vb[0], vb[1], vb[2], r2[0]);
+  c[1] = make_float4(r2[1], r2[2], cg[0], cg[1]);
+  c[2] = make_float4(cg[2], cn[0], cn[1], cn[2]);
+  c[3] = make_float4(lc[0], lc[1], lc[2], lc[3]);
+}
+
+// policy row: velocity and attitude noise (observation.py:22-63), noisy gate poses (commands.py:208-221)
+DEV void compute_policy(const KArgs& a, const Tab& tab, const Env& e, uint32_t gid, const ObsNoise& on,
+                        const float lc[4], float4 p[4]) {
+  float g0[3], gn0[3];
+  obs_gates(tab, e, g0, gn0);
+  float vb[3];
+  quat_rotate_inverse(e.q, e.v, vb);
   float qq[4], r2n[3];
   quat_mul(e.q, on.qn, qq);
   matrix_row2(qq, r2n);
@@ -516,10 +545,28 @@ DEV void compute_obs(const KArgs& a, const Tab& tab, const Env& e, uint32_t gid,
   quat_rotate_inverse(e.q, dnp, pn);
   float vn[3];
   for (int k = 0; k < 3; ++k) vn[k] = vb[k] * on.vfac[k];
-  o.p[0] = make_float4(vn[0], vn[1], vn[2], r2n[0]);
-  o.p[1] = make_float4(r2n[1], r2n[2], pg[0], pg[1]);
-  o.p[2] = make_float4(pg[2], pn[0], pn[1], pn[2]);
-  o.p[3] = make_float4(lc[0], lc[1], lc[2], lc[3]);
+  p[0] = make_float4(vn[0], vn[1], vn[2], r2n[0]);
+  p[1] = make_float4(r2n[1], r2n[2], pg[0], pg[1]);
+  p[2] = make_float4(pg[2], pn[0], pn[1], pn[2]);
+  p[3] = make_float4(lc[0], lc[1], lc[2], lc[3]);
+}
+
+DEV void compute_obs(const KArgs& a, const Tab& tab, const Env& e, uint32_t gid, const ObsNoise& on,
+                     const float lc[4], ObsRows& o) {
+  compute_critic(tab, e, lc, o.c);
+  compute_policy(a, tab, e, gid, on, lc, o.p);
+}
+
+// command compute: _update_metrics + _update_command (commands.py:247-260, 308-350)
+DEV void gate_advance(const KArgs& a, const Tab& tab, Env& e) {
+  const float* gg = tab.gate(e.type, e.lvl, e.gate);
+  float dd[3] = {gg[0] - e.p[0], gg[1] - e.p[1], gg[2] - e.p[2]};
+  if (norm3(dd) < a.kc->cfg.gate_threshold) {
+    const int ngt = (int)tab.rec(e.type, e.lvl)[3];
+    e.acc += 1;
+    e.gate = e.gate + 1;
+    if (e.gate >= ngt) e.gate -= ngt;
+  }
 }
 
 // one lane writes its env's 64-byte rows (4 x 16 B, 64-byte lane stride)
@@ -897,6 +944,9 @@ __global__ __launch_bounds__(2 * GR_BLOCK) void step_kernel(KArgs a, const KCons
       e.q[1] = r1.x; e.q[2] = r1.y; e.q[3] = r1.z; e.v[0] = r1.w;
       e.v[1] = r2.x; e.v[2] = r2.y; e.w[0] = r2.z; e.w[1] = r2.w;
       e.w[2] = r3.x;
+      e.lvl = __float_as_int(r3.y);
+      e.gate = __float_as_int(r3.z);
+      e.acc = 0;
       for (int k = 0; k < 3; ++k) { e.al[k] = 0.0f; e.tau[k] = 0.0f; }
       e.T = 0.0f;
       for (int k = 0; k < 4; ++k) e.mw[k] = 0.0f;
@@ -913,6 +963,17 @@ __global__ __launch_bounds__(2 * GR_BLOCK) void step_kernel(KArgs a, const KCons
       store_dyn(a, i, e);
       if (done) store_rst(a, i, e);
     }
+#ifndef GR_ABL_NOOBS
+    {  // critic observation (noise-free) of the post-reset, post-gate-progress state
+      gate_advance(a, sl.tab, e);
+      float4 crow[4];
+      compute_critic(sl.tab, e, lc, crow);
+      // this wave's reset-candidate slots are free once read (only done lanes read them, above)
+      float4* stage = xch + GR_XF4 * GR_BLOCK + (t & ~63);
+      store_rows_staged(reinterpret_cast<float4*>(a.buf.obs_critic), blockIdx.x * GR_BLOCK + (t & ~63), n, crow,
+                        stage);
+    }
+#endif
     STAMP(12);
 #ifndef GR_ABL_NOLOG
     wave_log_resets(a, threadIdx.x >> 6, lg, reset_lane);
@@ -949,6 +1010,7 @@ __global__ __launch_bounds__(2 * GR_BLOCK) void step_kernel(KArgs a, const KCons
     // depends only on the episode bookkeeping loaded above, not on this step's physics
     ResetDraws rd;
     reset_draws(a, gid, (uint32_t)e.epoch + 1u, e.mc, rd);
+    STAMP(15);
     Env er = e;
     reset_apply(a, sl.tab, er, rd);
     {  // hand the candidates to the physics waves, which write the state planes of every env
@@ -956,7 +1018,7 @@ __global__ __launch_bounds__(2 * GR_BLOCK) void step_kernel(KArgs a, const KCons
       xr[R_POSQ * GR_BLOCK + t] = make_float4(er.p[0], er.p[1], er.p[2], er.q[0]);
       xr[R_QV * GR_BLOCK + t] = make_float4(er.q[1], er.q[2], er.q[3], er.v[0]);
       xr[R_VW * GR_BLOCK + t] = make_float4(er.v[1], er.v[2], er.w[0], er.w[1]);
-      xr[R_W * GR_BLOCK + t] = make_float4(er.w[2], 0.0f, 0.0f, 0.0f);
+      xr[R_W * GR_BLOCK + t] = make_float4(er.w[2], __int_as_float(er.lvl), __int_as_float(er.gate), 0.0f);
       xr[R_RST0 * GR_BLOCK + t] = make_float4(er.thr, er.nl, er.k2[0], er.k2[1]);
       xr[R_RST1 * GR_BLOCK + t] = make_float4(er.k2[2], er.k1[0], er.k1[1], er.k1[2]);
     }
@@ -979,28 +1041,17 @@ __global__ __launch_bounds__(2 * GR_BLOCK) void step_kernel(KArgs a, const KCons
     }
     e.lag[0] = xlag.x; e.lag[1] = xlag.y; e.lag[2] = xlag.z; e.lag[3] = xlag.w;
     STAMP(14);
-    // command compute: _update_metrics + _update_command (commands.py:247-260, 308-350)
-    {
-      const float* gg = sl.tab.gate(e.type, e.lvl, e.gate);
-      float dd[3] = {gg[0] - e.p[0], gg[1] - e.p[1], gg[2] - e.p[2]};
-      if (norm3(dd) < c.gate_threshold) {
-        const int ngt = (int)sl.tab.rec(e.type, e.lvl)[3];
-        e.acc += 1;
-        e.gate = e.gate + 1;
-        if (e.gate >= ngt) e.gate -= ngt;
-      }
-    }
+    gate_advance(a, sl.tab, e);
     STAMP(7);
     if (live) store_istate(a, i, e);
 #ifndef GR_ABL_NOOBS
-    {
-      ObsRows o;
-      compute_obs(a, sl.tab, e, gid, on, lc, o);
+    {  // policy observation (the physics waves write the critic one)
+      float4 prow[4];
+      compute_policy(a, sl.tab, e, gid, on, lc, prow);
       // this wave's handover slots are free once read (rows X_PA.. of its own 64 envs)
       float4* stage = xch + (t & ~63);
-      const int env0 = blockIdx.x * GR_BLOCK + (t & ~63);
-      store_rows_staged(reinterpret_cast<float4*>(a.buf.obs_critic), env0, n, o.c, stage);
-      store_rows_staged(reinterpret_cast<float4*>(a.buf.obs_policy), env0, n, o.p, stage);
+      store_rows_staged(reinterpret_cast<float4*>(a.buf.obs_policy), blockIdx.x * GR_BLOCK + (t & ~63), n, prow,
+                        stage);
       if (live) a.buf.obs_aux[i] = aux;
     }
 #endif

@@ -42,6 +42,35 @@ GR_HD gr_u32x4 gr_philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t 
   return r;
 }
 
+/* Four draws that differ only in the last counter word, rounds interleaved so the
+ * four dependency chains overlap (same words as four gr_philox4x32_10 calls). */
+GR_HD void gr_philox4x32_10_x4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
+                               gr_u32x4 out[4]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __asm__ volatile("" : "+s"(k0), "+s"(k1));
+#endif
+  uint32_t x0[4], x1[4], x2[4], x3[4];
+  for (int j = 0; j < 4; ++j) { x0[j] = c0; x1[j] = c1; x2[j] = c2; x3[j] = c3 + (uint32_t)j; }
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+  for (int i = 0; i < 10; ++i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int j = 0; j < 4; ++j) {
+      uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)x0[j];
+      uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)x2[j];
+      uint32_t n0 = (uint32_t)(p1 >> 32) ^ x1[j] ^ k0;
+      uint32_t n2 = (uint32_t)(p0 >> 32) ^ x3[j] ^ k1;
+      x1[j] = (uint32_t)p1; x3[j] = (uint32_t)p0; x0[j] = n0; x2[j] = n2;
+    }
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  for (int j = 0; j < 4; ++j) { out[j].x = x0[j]; out[j].y = x1[j]; out[j].z = x2[j]; out[j].w = x3[j]; }
+}
+
 /* uniform in [0, 1): 24 random bits, exact in fp32 */
 GR_HD float gr_u01(uint32_t w) { return (float)(w >> 8) * 5.9604645e-08f; }
 /* uniform in (0, 1]: for log() in Box-Muller */

@@ -33,7 +33,7 @@ def build():
 ROLE_PHASES = {
     "physics": [("loads+barrier1+integrate", 0, 3), ("collision", 3, 4), ("termination+handover", 4, 5),
                 ("barrier2+reward+stores", 5, 12), ("log", 12, 8)],
-    "observation": [("loads+barrier1", 0, 1), ("obs_noise", 1, 2), ("speculative_reset", 2, 6),
+    "observation": [("loads+barrier1", 0, 1), ("obs_noise", 1, 2), ("reset_draws", 2, 15), ("reset_apply+xr", 15, 6),
                     ("barrier2_wait", 6, 13), ("select+reset_stores", 13, 14), ("advance", 14, 7),
                     ("obs+log", 7, 8)],
 }

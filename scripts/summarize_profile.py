@@ -18,7 +18,7 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "gr::env_kernel<0"
+KERNEL = "gr::step_kernel<true>"
 
 
 def pmc_means(prof):
@@ -58,7 +58,7 @@ def main():
             avg_ns = float(r["AverageNs"])
     m, counts, meta = pmc_means(prof)
     n = a.num_envs
-    d = {"kernel": "gr::env_kernel<0,true> (fused step)", "num_envs": n, "gates": a.gates,
+    d = {"kernel": "gr::step_kernel<true> (fused step)", "num_envs": n, "gates": a.gates,
          "launches_per_counter": counts, "dispatch": meta, "raw_means": m, "trace_avg_ns": avg_ns}
     if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
         rd = m["FETCH_SIZE"] * 1024 * 2  # KB; gfx950 reports half of a coalesced streaming read
