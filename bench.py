@@ -50,6 +50,9 @@ def parse():
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="skip policy/train/cpu legs (profiling runs)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--dist-backend", default="nccl",
+                   help="nccl (= RCCL, one GPU per rank); gloo only to rehearse the multi-rank path with ranks "
+                        "sharing one GPU")
     return p.parse_args()
 
 
@@ -61,7 +64,8 @@ def barrier():
 def max_over_ranks(x: float, device) -> float:
     if not dist.is_initialized():
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dev = device if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -235,9 +239,11 @@ def main():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.dist_backend != "nccl":  # rehearsal: ranks may share a device
+        local = local % max(1, torch.cuda.device_count())
     if ws > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=ws)
+        dist.init_process_group(a.dist_backend, rank=rank, world_size=ws)
     device = f"cuda:{local}"
     n = a.num_envs
     env = make_env(n, rank, device, a.gates, a.integrator)
@@ -284,7 +290,7 @@ def main():
                        "num_envs_per_gpu": n, "launch": mode, "parallelism": f"env-shard x{ws}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "gr::env_kernel<0,true> (fused step)", **kt,
+                         "kernel": "gr::step_kernel<true> (fused step)", **kt,
                          "algorithmic_bytes_per_launch": (rd + wr) * n,
                          "bytes_per_env_step": {"read": rd, "written": wr}},
             "cpu_baseline": cpu,

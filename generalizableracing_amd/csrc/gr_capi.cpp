@@ -123,7 +123,7 @@ void derive(gr_ctx* c) {
   const long bytes = (long)span * g.num_levels * a.track_stride * 4;
   // table + handovers within the CU's LDS (one workgroup per CU at the bench size); beyond that the
   // (L2-resident) table is read directly
-  a.lds_bytes = bytes + GR_XCH_BYTES <= 128 * 1024 ? (int)bytes : 0;
+  a.lds_bytes = bytes + GR_XCH_BYTES <= GR_LDS_MAX ? (int)bytes : 0;
 #ifdef GR_ABL_NOLDS
   a.lds_bytes = 0;
 #endif

@@ -6,10 +6,10 @@
 
 #define GR_BLOCK 256
 #define GR_MAX_TYPES 64
-#define GR_LOG_ROWS_PER_BLOCK 8  // log rows per workgroup (the step kernel has 8 waves)
-#define GR_XCH_BYTES ((5 + 6) * GR_BLOCK * 16)  // step kernel handovers in LDS (both directions)
+#define GR_LOG_ROWS_PER_BLOCK 8  // log rows per workgroup (physics and policy waves of the step kernel)
+#define GR_XCH_BYTES ((5 + 6 + 8) * GR_BLOCK * 16)  // step kernel handovers + store staging in LDS
 #define GR_LDS_MAX (160 * 1024)                 // LDS a gfx950 workgroup may allocate
-#define GR_STAMP_WAVES 4096  // diagnostic stamps (GR_STAMPS builds only)
+#define GR_STAMP_WAVES 8192  // diagnostic stamps (GR_STAMPS builds only)
 #define GR_STAMP_SLOTS 16
 
 namespace gr {

@@ -561,12 +561,12 @@ DEV void compute_obs(const KArgs& a, const Tab& tab, const Env& e, uint32_t gid,
 DEV void gate_advance(const KArgs& a, const Tab& tab, Env& e) {
   const float* gg = tab.gate(e.type, e.lvl, e.gate);
   float dd[3] = {gg[0] - e.p[0], gg[1] - e.p[1], gg[2] - e.p[2]};
-  if (norm3(dd) < a.kc->cfg.gate_threshold) {
-    const int ngt = (int)tab.rec(e.type, e.lvl)[3];
-    e.acc += 1;
-    e.gate = e.gate + 1;
-    if (e.gate >= ngt) e.gate -= ngt;
-  }
+  const bool pass = norm3(dd) < a.kc->cfg.gate_threshold;
+  const int ngt = (int)tab.rec(e.type, e.lvl)[3];
+  int g = e.gate + 1;
+  if (g >= ngt) g -= ngt;
+  e.acc = pass ? e.acc + 1 : e.acc;
+  e.gate = pass ? g : e.gate;
 }
 
 // one lane writes its env's 64-byte rows (4 x 16 B, 64-byte lane stride)
@@ -773,26 +773,65 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const KConst* __
 }
 
 // ------------------------------------------------------------- the step kernel
-// One workgroup = 256 envs and 8 waves: waves 0-3 run the physics of the 256 envs
-// (controller, integrator, collision, termination, reward), waves 4-7 run their
-// observation noise and the reset draws meanwhile, then — after the physics hands
-// over the post-step pose through LDS — the resets, gate progress and the
-// observations.  At 65 536 envs this puts two waves on every SIMD: a single
-// wave can issue a VALU op only every 4 cycles, two can use the SIMD every 2,
-// and one wave's memory / LDS / transcendental latency hides under the other's
-// work.  (ManagerBasedDiffRLEnv.step, manager_based_diff_rl_env.py:160-267.)
-// handover rows (float4 per env), physics -> observation: p + aux, q, v + done, lag, last ctbr;
-// then observation -> physics: the next episode's start state (state-plane layout)
+// One workgroup = 256 envs and 12 waves in three roles (wave-uniform):
+//   physics (waves 0-3):   controller, integrator, collision, termination -> handover;
+//                          then reward, state planes, step outputs, reset logs
+//   policy  (waves 4-7):   observation noise while the physics runs; then the noisy
+//                          policy observation, per-env gate progress, level logs
+//   episode (waves 8-11):  the next episode's start state for every env (a reset
+//                          depends only on the episode bookkeeping, not on this
+//                          step's physics) -> handover; then gate progress, the
+//                          critic observation and the episode counters
+// At 65 536 envs this puts three waves on every SIMD: a single wave issues a VALU
+// op at most every 4 cycles (the SIMD could take one every 2), and the waves'
+// memory / LDS / transcendental latencies overlap.  Two workgroup barriers: the
+// LDS track slice (1), the physics handover (2).
+// (ManagerBasedDiffRLEnv.step, manager_based_diff_rl_env.py:160-267.)
+// handover rows (float4 per env), physics -> others: p + aux, q, v + done, lag, last ctbr;
+// episode -> others: the next episode's start state (state-plane layout)
 enum { X_PA = 0, X_Q = 1, X_VD = 2, X_LAG = 3, X_LC = 4, GR_XF4 = 5, GR_XF = 4 * GR_XF4 };
 enum { R_POSQ = 0, R_QV = 1, R_VW = 2, R_W = 3, R_RST0 = 4, R_RST1 = 5, GR_RF4 = 6 };
+enum { GR_SF4 = 8 };  // staging rows for the coalesced observation stores (policy 4, critic 4)
+
+// environment as the policy / episode waves see it after the handover: the post-step pose,
+// or for resetting envs the next episode's start state
+DEV void merge_handover(const float4* xch, int t, bool reset, Env& e) {
+  // (field-wise selects: branch-dependent writes to different fields made the compiler
+  // address the struct through scratch memory)
+  float4 p4 = xch[X_PA * GR_BLOCK + t], q4 = xch[X_Q * GR_BLOCK + t], v4 = xch[X_VD * GR_BLOCK + t];
+  int lvl = e.lvl, gate = e.gate;
+  float nl = e.nl;
+  if (reset) {
+    const float4* xr = xch + GR_XF4 * GR_BLOCK;
+    const float4 r0 = xr[R_POSQ * GR_BLOCK + t], r1 = xr[R_QV * GR_BLOCK + t], r2 = xr[R_VW * GR_BLOCK + t];
+    const float4 r3 = xr[R_W * GR_BLOCK + t], r4 = xr[R_RST0 * GR_BLOCK + t];
+    p4 = make_float4(r0.x, r0.y, r0.z, 0.0f);
+    q4 = make_float4(r0.w, r1.x, r1.y, r1.z);
+    v4 = make_float4(r1.w, r2.x, r2.y, 0.0f);
+    lvl = __float_as_int(r3.y);
+    gate = __float_as_int(r3.z);
+    nl = r4.y;
+  }
+  e.p[0] = p4.x; e.p[1] = p4.y; e.p[2] = p4.z;
+  e.q[0] = q4.x; e.q[1] = q4.y; e.q[2] = q4.z; e.q[3] = q4.w;
+  e.v[0] = v4.x; e.v[1] = v4.y; e.v[2] = v4.z;
+  e.lvl = lvl;
+  e.gate = gate;
+  e.nl = nl;
+  e.acc = reset ? 0 : e.acc;
+  e.ep = reset ? 0 : e.ep + 1;
+  e.epoch = reset ? e.epoch + 1 : e.epoch;
+  e.azero = reset ? 1 : 0;
+}
 
 template <bool USE_LDS>
-__global__ __launch_bounds__(2 * GR_BLOCK) void step_kernel(KArgs a, const KConst* __restrict__ kc,
+__global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KConst* __restrict__ kc,
                                                              const float* __restrict__ actions) {
   a.kc = kc;
   extern __shared__ __attribute__((aligned(16))) float4 lds[];
-  float4* xch = lds + a.h.lds_tab_vec;  // [GR_XF4][GR_BLOCK] handover, after the table
-  const int role = threadIdx.x >> 8;                             // wave-uniform: 0 physics, 1 observation
+  float4* xch = lds + a.h.lds_tab_vec;                      // [GR_XF4 + GR_RF4][GR_BLOCK] handovers
+  float4* stg = xch + (GR_XF4 + GR_RF4) * GR_BLOCK;         // [GR_SF4][GR_BLOCK] store staging
+  const int role = threadIdx.x >> 8;                        // wave-uniform: 0 physics, 1 policy, 2 episode
   const int t = threadIdx.x & (GR_BLOCK - 1);
   const int n = a.h.num_envs;
   const int i = blockIdx.x * GR_BLOCK + t;
@@ -803,15 +842,15 @@ __global__ __launch_bounds__(2 * GR_BLOCK) void step_kernel(KArgs a, const KCons
   RSTAMP(9);
   STAMP(0);
   const Slice sl = block_slice<USE_LDS>(a, lds);
-  // each of the 512 threads stages one float4 of the table slice (clamped loads; extras are not stored)
+  // each of the 768 threads stages one float4 of the table slice (clamped loads; extras are not stored)
   float4 tr = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (USE_LDS) tr = sl.src[min((int)threadIdx.x, sl.nvec - 1)];
   auto commit = [&]() {
     if (USE_LDS) {
       if ((int)threadIdx.x < sl.nvec) lds[threadIdx.x] = tr;
-      for (int idx = threadIdx.x + 2 * GR_BLOCK; idx < sl.nvec; idx += 2 * GR_BLOCK) lds[idx] = sl.src[idx];
+      for (int idx = threadIdx.x + 3 * GR_BLOCK; idx < sl.nvec; idx += 3 * GR_BLOCK) lds[idx] = sl.src[idx];
+      __syncthreads();  // barrier 1: table staged
     }
-    __syncthreads();  // barrier 1: table staged
   };
 
   if (role == 0) {
@@ -819,7 +858,6 @@ __global__ __launch_bounds__(2 * GR_BLOCK) void step_kernel(KArgs a, const KCons
     const float4 act = reinterpret_cast<const float4*>(actions)[ii];
     Env e;
     load_env(a, ii, e);
-    commit();  // barrier 1 early: the slice loads were issued first and land first
     const float dt = c.step_dt;
     const float v_prev[3] = {e.v[0], e.v[1], e.v[2]}, w_prev[3] = {e.w[0], e.w[1], e.w[2]};
     const float mar_prev = e.mar;
@@ -847,10 +885,12 @@ __global__ __launch_bounds__(2 * GR_BLOCK) void step_kernel(KArgs a, const KCons
     if (c.integrator == GR_INTEGRATOR_DD_EXPLICIT) {
       dd_explicit(m, Jp, e.k2, e.k1, tt, dt, c.gravity, e.p, e.q, e.v, e.w, accl, al);
       STAMP(3);
+      commit();  // barrier 1: the table is first needed by the collision test
 #ifndef GR_ABL_NOCOLL
       ccount = collision_count(a, sl.tab, e.type, e.lvl, e.p, e.q);
 #endif
     } else {
+      commit();  // barrier 1: contacts are tested every substep
       float vb[3], fb[3] = {0.0f, 0.0f, tt[0]};
       quat_rotate_inverse(e.q, e.v, vb);
       for (int k = 0; k < 3; ++k) fb[k] = (fb[k] - (e.k2[k] * vb[k]) * gr_fabsf(vb[k])) - e.k1[k] * vb[k];
@@ -963,38 +1003,24 @@ __global__ __launch_bounds__(2 * GR_BLOCK) void step_kernel(KArgs a, const KCons
       store_dyn(a, i, e);
       if (done) store_rst(a, i, e);
     }
-#ifndef GR_ABL_NOOBS
-    {  // critic observation (noise-free) of the post-reset, post-gate-progress state
-      gate_advance(a, sl.tab, e);
-      float4 crow[4];
-      compute_critic(sl.tab, e, lc, crow);
-      // this wave's reset-candidate slots are free once read (only done lanes read them, above)
-      float4* stage = xch + GR_XF4 * GR_BLOCK + (t & ~63);
-      store_rows_staged(reinterpret_cast<float4*>(a.buf.obs_critic), blockIdx.x * GR_BLOCK + (t & ~63), n, crow,
-                        stage);
-    }
-#endif
     STAMP(12);
 #ifndef GR_ABL_NOLOG
     wave_log_resets(a, threadIdx.x >> 6, lg, reset_lane);
 #endif
     STAMP(8);
     RSTAMP(10);
-  } else {
-    // ======================= observation / reset waves =======================
+  } else if (role == 1) {
+    // ======================= policy-observation waves =======================
     const uint32_t cnt = a.buf.counters[a.buf.counter_index];
-    const float4* S = reinterpret_cast<const float4*>(a.buf.state);
-    const size_t ns = (size_t)n;
     const int4 is = reinterpret_cast<const int4*>(a.buf.istate)[ii];
-    const float4 r0 = S[GR_P_RST0 * ns + ii], r1 = S[GR_P_RST1 * ns + ii], p2 = S[GR_P_PAR2 * ns + ii];
+    const float4 r0 = reinterpret_cast<const float4*>(a.buf.state)[GR_P_RST0 * (size_t)n + ii];
     Env e;
     e.ep = is.x; e.acc = is.y; e.epoch = is.z;
     e.gate = is.w & 0xff; e.lvl = (is.w >> 8) & 0xff; e.type = (is.w >> 24) & 0xff;
-    e.thr = r0.x; e.nl = r0.y; e.k2[0] = r0.z; e.k2[1] = r0.w;
-    e.k2[2] = r1.x; e.k1[0] = r1.y; e.k1[1] = r1.z; e.k1[2] = r1.w;
-    e.mc = p2.w;
-    commit();  // barrier 1
+    e.nl = r0.y;
+    commit();  // barrier 1 (joined at once: the physics and episode waves set its time)
     STAMP(1);
+    // observation noise needs only the call counter: it runs while the physics waves collide
     ObsNoise on;
 #ifndef GR_ABL_NOOBSNOISE
     obs_noise(a, gid, cnt, on);
@@ -1006,14 +1032,50 @@ __global__ __launch_bounds__(2 * GR_BLOCK) void step_kernel(KArgs a, const KCons
     // call counter for the observation-noise stream: double-buffered by call parity,
     // so this write never races with the reads of the current launch
     if (t == 0 && blockIdx.x == 0) a.buf.counters[a.buf.counter_index ^ 1] = cnt + 1u;
-    // the next episode's start state, for every env (only the resetting ones use it): a reset
-    // depends only on the episode bookkeeping loaded above, not on this step's physics
+    __syncthreads();  // barrier 2: handover
+    STAMP(13);
+    const float4 xvd = xch[X_VD * GR_BLOCK + t], xlc = xch[X_LC * GR_BLOCK + t];
+    const float aux = xch[X_PA * GR_BLOCK + t].w;
+    const bool reset = xvd.w != 0.0f && live;
+    merge_handover(xch, t, reset, e);
+    const float lc[4] = {xlc.x, xlc.y, xlc.z, xlc.w};
+    gate_advance(a, sl.tab, e);
+    STAMP(7);
+#ifndef GR_ABL_NOOBS
+    {
+      float4 prow[4];
+      compute_policy(a, sl.tab, e, gid, on, lc, prow);
+      store_rows_staged(reinterpret_cast<float4*>(a.buf.obs_policy), blockIdx.x * GR_BLOCK + (t & ~63), n, prow,
+                        stg + (t & ~63));
+      if (live) a.buf.obs_aux[i] = aux;
+    }
+#endif
+#ifndef GR_ABL_NOLOG
+    wave_log_levels(a, threadIdx.x >> 6, live ? (float)e.lvl : 0.0f, live ? e.nl : 0.0f);
+#endif
+    STAMP(8);
+    RSTAMP(10);
+  } else {
+    // ======================= episode waves =======================
+    const float4* S = reinterpret_cast<const float4*>(a.buf.state);
+    const size_t ns = (size_t)n;
+    const int4 is = reinterpret_cast<const int4*>(a.buf.istate)[ii];
+    const float4 r0 = S[GR_P_RST0 * ns + ii], r1 = S[GR_P_RST1 * ns + ii], p2 = S[GR_P_PAR2 * ns + ii];
+    Env e;
+    e.ep = is.x; e.acc = is.y; e.epoch = is.z;
+    e.gate = is.w & 0xff; e.lvl = (is.w >> 8) & 0xff; e.type = (is.w >> 24) & 0xff;
+    e.thr = r0.x; e.nl = r0.y; e.k2[0] = r0.z; e.k2[1] = r0.w;
+    e.k2[2] = r1.x; e.k1[0] = r1.y; e.k1[1] = r1.z; e.k1[2] = r1.w;
+    e.mc = p2.w;
+    // the next episode's start state, for every env (only the resetting ones use it)
     ResetDraws rd;
     reset_draws(a, gid, (uint32_t)e.epoch + 1u, e.mc, rd);
-    STAMP(15);
-    Env er = e;
-    reset_apply(a, sl.tab, er, rd);
-    {  // hand the candidates to the physics waves, which write the state planes of every env
+    STAMP(1);
+    commit();  // barrier 1 (the start gate of the next episode's track is read from the slice)
+    STAMP(2);
+    {
+      Env er = e;
+      reset_apply(a, sl.tab, er, rd);
       float4* xr = xch + GR_XF4 * GR_BLOCK;
       xr[R_POSQ * GR_BLOCK + t] = make_float4(er.p[0], er.p[1], er.p[2], er.q[0]);
       xr[R_QV * GR_BLOCK + t] = make_float4(er.q[1], er.q[2], er.q[3], er.v[0]);
@@ -1025,38 +1087,20 @@ __global__ __launch_bounds__(2 * GR_BLOCK) void step_kernel(KArgs a, const KCons
     STAMP(6);
     __syncthreads();  // barrier 2: handover
     STAMP(13);
-    const float4 xpa = xch[X_PA * GR_BLOCK + t], xq = xch[X_Q * GR_BLOCK + t], xvd = xch[X_VD * GR_BLOCK + t];
-    const float4 xlag = xch[X_LAG * GR_BLOCK + t], xlc = xch[X_LC * GR_BLOCK + t];
+    const float4 xlc = xch[X_LC * GR_BLOCK + t];
+    const bool reset = xch[X_VD * GR_BLOCK + t].w != 0.0f && live;
+    merge_handover(xch, t, reset, e);
     const float lc[4] = {xlc.x, xlc.y, xlc.z, xlc.w};
-    const float aux = xpa.w;
-    const bool done = xvd.w != 0.0f;
-    if (done && live) {
-      e = er;
-    } else {
-      e.p[0] = xpa.x; e.p[1] = xpa.y; e.p[2] = xpa.z;
-      e.q[0] = xq.x; e.q[1] = xq.y; e.q[2] = xq.z; e.q[3] = xq.w;
-      e.v[0] = xvd.x; e.v[1] = xvd.y; e.v[2] = xvd.z;
-      e.ep += 1;
-      e.azero = 0;
-    }
-    e.lag[0] = xlag.x; e.lag[1] = xlag.y; e.lag[2] = xlag.z; e.lag[3] = xlag.w;
-    STAMP(14);
     gate_advance(a, sl.tab, e);
-    STAMP(7);
+    STAMP(14);
     if (live) store_istate(a, i, e);
 #ifndef GR_ABL_NOOBS
-    {  // policy observation (the physics waves write the critic one)
-      float4 prow[4];
-      compute_policy(a, sl.tab, e, gid, on, lc, prow);
-      // this wave's handover slots are free once read (rows X_PA.. of its own 64 envs)
-      float4* stage = xch + (t & ~63);
-      store_rows_staged(reinterpret_cast<float4*>(a.buf.obs_policy), blockIdx.x * GR_BLOCK + (t & ~63), n, prow,
-                        stage);
-      if (live) a.buf.obs_aux[i] = aux;
+    {  // critic observation (noise-free) of the post-reset, post-gate-progress state
+      float4 crow[4];
+      compute_critic(sl.tab, e, lc, crow);
+      store_rows_staged(reinterpret_cast<float4*>(a.buf.obs_critic), blockIdx.x * GR_BLOCK + (t & ~63), n, crow,
+                        stg + 4 * GR_BLOCK + (t & ~63));
     }
-#endif
-#ifndef GR_ABL_NOLOG
-    wave_log_levels(a, threadIdx.x >> 6, live ? (float)e.lvl : 0.0f, live ? e.nl : 0.0f);
 #endif
     STAMP(8);
     RSTAMP(10);
@@ -1254,11 +1298,11 @@ static hipError_t launch_env_mode(const KArgs& a, const float* actions, const ui
   const int g = grid_of(a.h.num_envs);
   const bool lds = a.h.lds_tab_vec > 0;
   if constexpr (MODE == KMODE_STEP) {
-    const size_t bytes = (size_t)a.h.lds_tab_vec * 16 + (size_t)(GR_XF4 + GR_RF4) * GR_BLOCK * 16;
+    const size_t bytes = (size_t)a.h.lds_tab_vec * 16 + (size_t)(GR_XF4 + GR_RF4 + GR_SF4) * GR_BLOCK * 16;
     if (lds)
-      hipLaunchKernelGGL(step_kernel<true>, dim3(g), dim3(2 * GR_BLOCK), bytes, s, a, a.kc, actions);
+      hipLaunchKernelGGL(step_kernel<true>, dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
     else
-      hipLaunchKernelGGL(step_kernel<false>, dim3(g), dim3(2 * GR_BLOCK), bytes, s, a, a.kc, actions);
+      hipLaunchKernelGGL(step_kernel<false>, dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
   } else {
     const size_t bytes = (size_t)a.h.lds_tab_vec * 16;
     if (lds)
@@ -1322,7 +1366,7 @@ hipError_t allow_large_lds() {
                       reinterpret_cast<const void*>(&env_kernel<KMODE_RESET, true>),
                       reinterpret_cast<const void*>(&env_kernel<KMODE_OBSERVE, true>)};
   for (const void* k : ks) {
-    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, GR_LDS_MAX);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;

@@ -31,11 +31,12 @@ def build():
 
 
 ROLE_PHASES = {
-    "physics": [("loads+barrier1+integrate", 0, 3), ("collision", 3, 4), ("termination+handover", 4, 5),
+    "physics": [("loads+integrate", 0, 3), ("barrier1+collision", 3, 4), ("termination+handover", 4, 5),
                 ("barrier2+reward+stores", 5, 12), ("log", 12, 8)],
-    "observation": [("loads+barrier1", 0, 1), ("obs_noise", 1, 2), ("reset_draws", 2, 15), ("reset_apply+xr", 15, 6),
-                    ("barrier2_wait", 6, 13), ("select+reset_stores", 13, 14), ("advance", 14, 7),
-                    ("obs+log", 7, 8)],
+    "policy": [("loads+barrier1", 0, 1), ("obs_noise", 1, 2), ("barrier2_wait", 2, 13),
+               ("merge+advance", 13, 7), ("policy_obs+log", 7, 8)],
+    "episode": [("loads+reset_draws", 0, 1), ("barrier1", 1, 2), ("reset_apply+xr", 2, 6),
+                ("barrier2_wait", 6, 13), ("merge+advance+istate", 13, 14), ("critic_obs", 14, 8)],
 }
 
 
@@ -55,11 +56,11 @@ def run(n=65536, steps=200):
     for k in range(steps):
         env.step(acts[k % bench.ACTION_RING])
     torch.cuda.synchronize()
-    waves = (n // 256) * 8  # step kernel: 8 waves per 256-env workgroup
+    waves = (n // 256) * 12  # step kernel: 12 waves per 256-env workgroup
     buf = np.zeros(waves * 16, np.uint64)
     assert env._lib.gr_debug_read_stamps(buf.ctypes.data_as(C.c_void_p), buf.size) == 0
     st = buf.reshape(waves, 16).astype(np.int64)
-    role = (np.arange(waves) % 8) // 4  # waves 0-3 physics, 4-7 observation
+    role = (np.arange(waves) % 12) // 4  # waves 0-3 physics, 4-7 policy, 8-11 episode
     rt0, rt1 = st[:, 9], st[:, 10]
     out = {
         "kernel_span_us(realtime)": float((rt1.max() - rt0.min()) * 10 / 1e3),
@@ -67,7 +68,7 @@ def run(n=65536, steps=200):
         "end_us_pcts(10,50,90,99,100)": [float(np.percentile((rt1 - rt0.min()) * 10 / 1e3, q))
                                          for q in (10, 50, 90, 99, 100)],
     }
-    for r, name in enumerate(("physics", "observation")):
+    for r, name in enumerate(("physics", "policy", "episode")):
         sel = st[role == r]
         life = sel[:, 8] - sel[:, 0]
         out[name] = {
