@@ -195,14 +195,14 @@ def train_fps(device, n=4096, iters=3):
     return float(np.median(fps))
 
 
-def cpu_baseline(seconds: float):
-    """The CPU oracle (C restatement of the reference step, 1 thread) on a bounded sample."""
+def cpu_baseline(seconds: float, n: int = 65536):
+    """The CPU oracle (C restatement of the reference step, OpenMP over envs) on a bounded sample
+    of the same workload: n envs stepped for about `seconds`."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
 
     from generalizableracing_amd.envs.tracks import build_track_table
 
-    n = 4096
     cfg = RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device="cpu"), stage=1).to_gr_config()
     gates, recs = build_track_table()
     orc = oracle.Oracle(cfg, gates, recs)
@@ -216,9 +216,11 @@ def cpu_baseline(seconds: float):
         orc.step(acts[steps % 16])
         steps += 1
     dt = time.perf_counter() - t0
-    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n} envs x {steps} steps of the C oracle (oracle/gr_oracle.c), single thread, "
-                      f"{dt:.1f} s; the Isaac-Lab/PhysX reference cannot run here (SURVEY §8d)"}
+    threads = oracle.num_threads()
+    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{n} envs x {steps} steps of the C oracle (oracle/gr_oracle.c, gcc -O2, OpenMP "
+                      f"{threads} threads = OMP_NUM_THREADS), {dt:.1f} s; the Isaac-Lab/PhysX reference cannot "
+                      f"run here (SURVEY §8d)"}
 
 
 def load_traffic(n, gates):

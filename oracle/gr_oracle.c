@@ -21,6 +21,9 @@
 
 #include <math.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #include "../generalizableracing_amd/csrc/gr_math.h"
 #include "../generalizableracing_amd/csrc/gr_rng.h"
@@ -575,12 +578,19 @@ void gro_observe(const gr_config* c, gro_env* envs, int n, const gro_tracks* tr,
 /* -------------------------------------------------------------------- step */
 void gro_step(const gr_config* c, gro_env* envs, int n, const float* actions, const gro_tracks* tr, uint32_t* counter,
               gro_out* out) {
-  logacc L;
-  memset(&L, 0, sizeof(L));
+  logacc Lsum;
+  memset(&Lsum, 0, sizeof(Lsum));
   uint32_t cnt = *counter;
   const float dt = c->step_dt;
   const float w[7] = {c->w_progress, c->w_body_rate, c->w_action_rate, c->w_collision,
                       c->w_perception, c->w_success, c->w_bad_pose};
+  /* envs are independent: one OpenMP team over them (OMP_NUM_THREADS; per-env results do not
+   * depend on the thread count, only the summation order of the log means does) */
+#pragma omp parallel
+  {
+  logacc L;
+  memset(&L, 0, sizeof(L));
+#pragma omp for schedule(static)
   for (int i = 0; i < n; ++i) {
     gro_env* e = &envs[i];
     uint32_t gid = gid_of(c, i);
@@ -709,8 +719,19 @@ void gro_step(const gr_config* c, gro_env* envs, int n, const float* actions, co
     compute_obs(c, e, gid, cnt, tr, lc, aux, out->obs_policy + (size_t)i * 16, out->obs_critic + (size_t)i * 16,
                 &out->obs_aux[i]);
   }
-  finalize_log(c, &L, out->log_out);
+#pragma omp critical
+  for (int k = 0; k < GR_LOG_SLOTS; ++k) Lsum.s[k] += L.s[k];
+  }
+  finalize_log(c, &Lsum, out->log_out);
   *counter = cnt + 1u;
+}
+
+int gro_num_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
 }
 
 /* ------------------------------------------------------------ test hooks */

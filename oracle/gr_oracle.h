@@ -64,5 +64,7 @@ void gro_test_math(int fn, int n, const float* x, const float* y, float* out);
 void gro_test_philox(int n, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
                      uint32_t* out4);
 void gro_test_fields6(int n, const uint32_t* in4, uint32_t* out6);
+/* OpenMP threads gro_step uses (1 without OpenMP) */
+int gro_num_threads(void);
 
 #endif

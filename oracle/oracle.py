@@ -51,6 +51,7 @@ def load():
             "gro_test_math": [C.c_int, C.c_int, vp, vp, vp],
             "gro_test_philox": [C.c_int] + [C.c_uint32] * 6 + [vp],
             "gro_test_fields6": [C.c_int, vp, vp],
+            "gro_num_threads": [],
         }.items():
             f = getattr(lib, name)
             f.restype = None
@@ -150,6 +151,12 @@ def test_philox(n, c0, c1, c2, c3, k0, k1):
     out = np.zeros((n, 4), np.uint32)
     lib.gro_test_philox(n, c0, c1, c2, c3, k0, k1, _p(out))
     return out
+
+
+def num_threads() -> int:
+    lib = load()
+    lib.gro_num_threads.restype = C.c_int
+    return int(lib.gro_num_threads())
 
 
 def test_fields6(words: np.ndarray) -> np.ndarray:
