@@ -842,13 +842,19 @@ __global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KCons
   RSTAMP(9);
   STAMP(0);
   const Slice sl = block_slice<USE_LDS>(a, lds);
-  // each of the 768 threads stages one float4 of the table slice (clamped loads; extras are not stored)
-  float4 tr = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  if (USE_LDS) tr = sl.src[min((int)threadIdx.x, sl.nvec - 1)];
+  // each of the 768 threads stages up to two float4 of the table slice, loaded at entry (clamped
+  // loads; extras are not stored): a two-type slice of 8-gate tracks (820 float4) needs no load later
+  float4 tr = make_float4(0.0f, 0.0f, 0.0f, 0.0f), tr2 = tr;
+  const bool two = sl.nvec > 3 * GR_BLOCK;
+  if (USE_LDS) {
+    tr = sl.src[min((int)threadIdx.x, sl.nvec - 1)];
+    if (two) tr2 = sl.src[min((int)threadIdx.x + 3 * GR_BLOCK, sl.nvec - 1)];
+  }
   auto commit = [&]() {
     if (USE_LDS) {
       if ((int)threadIdx.x < sl.nvec) lds[threadIdx.x] = tr;
-      for (int idx = threadIdx.x + 3 * GR_BLOCK; idx < sl.nvec; idx += 3 * GR_BLOCK) lds[idx] = sl.src[idx];
+      if (two && (int)threadIdx.x + 3 * GR_BLOCK < sl.nvec) lds[threadIdx.x + 3 * GR_BLOCK] = tr2;
+      for (int idx = threadIdx.x + 6 * GR_BLOCK; idx < sl.nvec; idx += 3 * GR_BLOCK) lds[idx] = sl.src[idx];
       __syncthreads();  // barrier 1: table staged
     }
   };
