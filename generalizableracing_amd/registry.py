@@ -11,11 +11,12 @@ from __future__ import annotations
 _REGISTRY: dict = {}
 
 
-def register(id: str, entry_point, env_cfg_entry_point, rsl_rl_cfg_entry_point):
+def register(id: str, entry_point, env_cfg_entry_point, rsl_rl_cfg_entry_point, **extra_entry_points):
     _REGISTRY[id] = {
         "entry_point": entry_point,
         "env_cfg_entry_point": env_cfg_entry_point,
         "rsl_rl_cfg_entry_point": rsl_rl_cfg_entry_point,
+        **extra_entry_points,
     }
 
 
@@ -51,4 +52,5 @@ register(
     entry_point="generalizableracing_amd.envs.racing_env:RacingEnv",
     env_cfg_entry_point="generalizableracing_amd.envs.racing_cfg:RacingEnvCfg",
     rsl_rl_cfg_entry_point="generalizableracing_amd.rsl_rl.config:QuadcopterPPORunnerCfg",
+    rsl_rl_l2c2_cfg_entry_point="generalizableracing_amd.rsl_rl.config:QuadcopterL2C2PPORunnerCfg",
 )

@@ -55,3 +55,15 @@ class QuadcopterPPORunnerCfg:
 
     def to_dict(self) -> dict:
         return asdict(self)
+
+
+@dataclass
+class QuadcopterL2C2PPORunnerCfg(QuadcopterPPORunnerCfg):
+    """The reference's racing recipe algorithm (rsl_rl_ppo_cfg.py:80-104: class_name "PPOL2C2",
+    entropy 0.005, 4000 iterations) on the state-only MLP policy.  The L2C2 knobs keep the
+    PPOL2C2 constructor defaults (ppo_l2c2.py:26-28)."""
+
+    max_iterations: int = 4000
+    experiment_name: str = "racing_ppo_l2c2"
+    algorithm: RslRlPpoAlgorithmCfg = field(
+        default_factory=lambda: RslRlPpoAlgorithmCfg(class_name="PPOL2C2", entropy_coef=0.005))

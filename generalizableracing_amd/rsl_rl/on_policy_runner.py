@@ -20,6 +20,10 @@ import torch
 from . import distributed as gdist
 from .actor_critic import ActorCritic, EmpiricalNormalization
 from .ppo import PPO
+from .ppo_l2c2 import PPOL2C2
+
+ALGORITHMS = {"PPO": PPO, "PPOL2C2": PPOL2C2}
+POLICIES = {"ActorCritic": ActorCritic}
 
 
 class _CsvWriter:
@@ -88,18 +92,18 @@ class OnPolicyRunner:
         self.policy_cfg = dict(train_cfg["policy"])
         self.device = device
         self.env = env
-        if self.alg_cfg["class_name"] != "PPO":
-            raise ValueError(f"algorithm {self.alg_cfg['class_name']} not supported (PPO only; PPOL2C2 is SURVEY next-2)")
+        if self.alg_cfg["class_name"] not in ALGORITHMS:  # on_policy_runner.py:31-36
+            raise ValueError(f"Training type not found for algorithm {self.alg_cfg['class_name']}.")
         self.training_type = "rl"
         obs, extras = self.env.get_observations()
         num_obs = obs.shape[1]
         self.privileged_obs_type = "critic" if "critic" in extras["observations"] else None
         num_privileged_obs = (extras["observations"][self.privileged_obs_type].shape[1]
                               if self.privileged_obs_type is not None else num_obs)
-        policy_class = {"ActorCritic": ActorCritic}[self.policy_cfg.pop("class_name")]
+        policy_class = POLICIES[self.policy_cfg.pop("class_name")]
         policy = policy_class(num_obs, num_privileged_obs, self.env.num_actions, **self.policy_cfg).to(self.device)
-        self.alg_cfg.pop("class_name")
-        self.alg = PPO(policy, env=self.env, device=self.device, **self.alg_cfg)
+        alg_class = ALGORITHMS[self.alg_cfg.pop("class_name")]
+        self.alg = alg_class(policy, env=self.env, device=self.device, **self.alg_cfg)
         self.num_steps_per_env = self.cfg["num_steps_per_env"]
         self.save_interval = self.cfg["save_interval"]
         self.empirical_normalization = self.cfg["empirical_normalization"]

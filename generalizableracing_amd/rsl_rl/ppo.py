@@ -80,6 +80,42 @@ class PPO:
         last_values = self.policy.evaluate(last_critic_obs).detach()
         self.storage.compute_returns(last_values, self.gamma, self.lam, self.normalize_advantage)
 
+    def _adapt_learning_rate(self, mu_batch, sigma_batch, old_mu_batch, old_sigma_batch):
+        """Adaptive KL learning rate (ppo.py:133-150); KL mean averaged over ranks."""
+        if self.desired_kl is None or self.schedule != "adaptive":
+            return
+        with torch.inference_mode():
+            kl = torch.sum(
+                torch.log(sigma_batch / old_sigma_batch + 1.0e-5)
+                + (torch.square(old_sigma_batch) + torch.square(old_mu_batch - mu_batch))
+                / (2.0 * torch.square(sigma_batch)) - 0.5, axis=-1)
+            kl_mean = gdist.allreduce_mean(torch.mean(kl))
+            kl_val = float(kl_mean)  # host decision, as in the reference
+            if kl_val > self.desired_kl * 2.0:
+                self.learning_rate = max(1e-5, self.learning_rate / 1.5)
+            elif self.desired_kl / 2.0 > kl_val > 0.0:
+                self.learning_rate = min(1e-2, self.learning_rate * 1.5)
+            for g in self.optimizer.param_groups:
+                g["lr"] = self.learning_rate
+
+    def _ppo_losses(self, actions_log_prob_batch, old_actions_log_prob_batch, advantages_batch, value_batch,
+                    target_values_batch, returns_batch):
+        """Clipped surrogate (ppo.py:152-158) and (clipped) value loss (ppo.py:160-169)."""
+        ratio = torch.exp(actions_log_prob_batch - torch.squeeze(old_actions_log_prob_batch))
+        surrogate = -torch.squeeze(advantages_batch) * ratio
+        surrogate_clipped = -torch.squeeze(advantages_batch) * torch.clamp(ratio, 1.0 - self.clip_param,
+                                                                           1.0 + self.clip_param)
+        surrogate_loss = torch.max(surrogate, surrogate_clipped).mean()
+        if self.use_clipped_value_loss:
+            value_clipped = target_values_batch + (value_batch - target_values_batch).clamp(-self.clip_param,
+                                                                                            self.clip_param)
+            value_losses = (value_batch - returns_batch).pow(2)
+            value_losses_clipped = (value_clipped - returns_batch).pow(2)
+            value_loss = torch.max(value_losses, value_losses_clipped).mean()
+        else:
+            value_loss = (returns_batch - value_batch).pow(2).mean()
+        return surrogate_loss, value_loss
+
     def update(self):
         mean_value_loss = torch.zeros((), device=self.device)
         mean_surrogate_loss = torch.zeros((), device=self.device)
@@ -93,36 +129,10 @@ class PPO:
             mu_batch = self.policy.action_mean
             sigma_batch = self.policy.action_std
             entropy_batch = self.policy.entropy
-            # adaptive KL learning rate (ppo.py:133-150)
-            if self.desired_kl is not None and self.schedule == "adaptive":
-                with torch.inference_mode():
-                    kl = torch.sum(
-                        torch.log(sigma_batch / old_sigma_batch + 1.0e-5)
-                        + (torch.square(old_sigma_batch) + torch.square(old_mu_batch - mu_batch))
-                        / (2.0 * torch.square(sigma_batch)) - 0.5, axis=-1)
-                    kl_mean = gdist.allreduce_mean(torch.mean(kl))
-                    kl_val = float(kl_mean)  # host decision, as in the reference
-                    if kl_val > self.desired_kl * 2.0:
-                        self.learning_rate = max(1e-5, self.learning_rate / 1.5)
-                    elif self.desired_kl / 2.0 > kl_val > 0.0:
-                        self.learning_rate = min(1e-2, self.learning_rate * 1.5)
-                    for g in self.optimizer.param_groups:
-                        g["lr"] = self.learning_rate
-            # surrogate (ppo.py:152-158)
-            ratio = torch.exp(actions_log_prob_batch - torch.squeeze(old_actions_log_prob_batch))
-            surrogate = -torch.squeeze(advantages_batch) * ratio
-            surrogate_clipped = -torch.squeeze(advantages_batch) * torch.clamp(ratio, 1.0 - self.clip_param,
-                                                                               1.0 + self.clip_param)
-            surrogate_loss = torch.max(surrogate, surrogate_clipped).mean()
-            # value loss (ppo.py:160-169)
-            if self.use_clipped_value_loss:
-                value_clipped = target_values_batch + (value_batch - target_values_batch).clamp(-self.clip_param,
-                                                                                                self.clip_param)
-                value_losses = (value_batch - returns_batch).pow(2)
-                value_losses_clipped = (value_clipped - returns_batch).pow(2)
-                value_loss = torch.max(value_losses, value_losses_clipped).mean()
-            else:
-                value_loss = (returns_batch - value_batch).pow(2).mean()
+            self._adapt_learning_rate(mu_batch, sigma_batch, old_mu_batch, old_sigma_batch)
+            surrogate_loss, value_loss = self._ppo_losses(actions_log_prob_batch, old_actions_log_prob_batch,
+                                                          advantages_batch, value_batch, target_values_batch,
+                                                          returns_batch)
             loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_batch.mean()
             self.optimizer.zero_grad()
             loss.backward()

@@ -1,0 +1,118 @@
+"""PPOL2C2 — PPO with the L2C2 smoothness regulariser
+(standalone/rsl_rl/ext/algorithms/ppo_l2c2.py:8-212), the algorithm the vision racing
+recipe registers (quadcopter_diff/agents/rsl_rl_ppo_cfg.py:87-101, class_name="PPOL2C2").
+
+Same act / process_env_step / compute_returns / PPO losses as PPO, plus, per
+minibatch (ppo_l2c2.py:176-190):
+    eps   = lb / (ub - lb);   c_pi = ub * eps;   c_v = value_smoothness_coef * c_pi
+    w     = cont * U(-1, 1)                           (one scalar per sample; 0 across a reset)
+    o_mix = o + w * (o_next - o)
+    L_s   = c_pi * mean(|mu(o) - mu(o_mix)|^2) + c_v * mean(|V(o) - V(o_mix)|^2)
+added to the PPO loss.  Multi-GPU as in PPO: KL mean averaged across ranks
+before the learning-rate decision, gradients averaged in one flat all-reduce.
+
+Deviations (documented):
+  * `act_inference` of the reference's VisionActorCritic returns (mean, feat) and
+    ppo_l2c2.py:184,189 take `[0]`; on a plain ActorCritic `[0]` would pick the first
+    ROW of the mean and broadcast it.  Here `_mean_of` takes [0] only of a tuple.
+  * the transition is stored unless the whole observation batch is ~0
+    (ppo_l2c2.py:98), as in the reference; that test costs one host sync per step.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import distributed as gdist
+from .ppo import PPO
+from .rollout_storage_l2c2 import RolloutStorageL2C2
+
+
+def _mean_of(out):
+    return out[0] if isinstance(out, (tuple, list)) else out
+
+
+class PPOL2C2(PPO):
+    def __init__(self, policy, env=None, value_smoothness_coef=0.1, smoothness_upper_bound=1.0,
+                 smoothness_lower_bound=0.1, **kwargs):
+        kwargs.pop("normalize_advantage", None)
+        super().__init__(policy, env=env, normalize_advantage=True, **kwargs)
+        self.transition = RolloutStorageL2C2.Transition()
+        self.value_smoothness_coef = value_smoothness_coef
+        self.smoothness_upper_bound = smoothness_upper_bound
+        self.smoothness_lower_bound = smoothness_lower_bound
+
+    def init_storage(self, training_type, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape,
+                     action_shape):
+        self.storage = RolloutStorageL2C2(training_type, num_envs, num_transitions_per_env, actor_obs_shape,
+                                          critic_obs_shape, action_shape, self.device,
+                                          obs_dtype=self.storage_obs_dtype)
+
+    def smooth_coefs(self):
+        """ppo_l2c2.py:176-178."""
+        eps = self.smoothness_lower_bound / (self.smoothness_upper_bound - self.smoothness_lower_bound)
+        policy_coef = self.smoothness_upper_bound * eps
+        return policy_coef, self.value_smoothness_coef * policy_coef
+
+    def process_env_step(self, rewards, dones, infos):
+        self.transition.rewards = rewards.clone()
+        self.transition.dones = dones
+        if "time_outs" in infos:  # ppo_l2c2.py:91-95
+            self.transition.rewards += self.gamma * torch.squeeze(
+                self.transition.values * infos["time_outs"].unsqueeze(1).to(self.device), 1)
+        if torch.norm(self.transition.observations).mean() > 1e-4:  # ppo_l2c2.py:98
+            self.storage.add_transitions(self.transition)
+        self.transition.clear()
+        self.policy.reset(dones)
+
+    def smooth_loss(self, obs_batch, next_obs_batch, cont_batch, mu_batch, value_batch):
+        """ppo_l2c2.py:176-188; returns (smooth_loss, action_smoothness)."""
+        policy_coef, value_coef = self.smooth_coefs()
+        mix_weights = cont_batch * (torch.rand_like(cont_batch) - 0.5) * 2.0
+        mix_obs_batch = obs_batch + mix_weights * (next_obs_batch - obs_batch)
+        policy_smooth = torch.square(torch.norm(mu_batch - _mean_of(self.policy.act_inference(mix_obs_batch)),
+                                                dim=-1)).mean()
+        value_smooth = torch.square(torch.norm(value_batch - self.policy.evaluate(mix_obs_batch), dim=-1)).mean()
+        loss = policy_coef * policy_smooth + value_coef * value_smooth
+        with torch.inference_mode():
+            action_smoothness = torch.norm(mu_batch - _mean_of(self.policy.act_inference(next_obs_batch)),
+                                           dim=-1).mean()
+        return loss, action_smoothness
+
+    def update(self):
+        mean_value_loss = torch.zeros((), device=self.device)
+        mean_surrogate_loss = torch.zeros((), device=self.device)
+        mean_smooth_loss = torch.zeros((), device=self.device)
+        generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
+        params = list(self.policy.parameters())
+        for (obs_batch, critic_obs_batch, next_obs_batch, cont_batch, actions_batch, target_values_batch,
+             advantages_batch, returns_batch, old_actions_log_prob_batch, old_mu_batch, old_sigma_batch,
+             hid_states_batch, masks_batch) in generator:
+            self.policy.act(obs_batch)
+            actions_log_prob_batch = self.policy.get_actions_log_prob(actions_batch)
+            value_batch = self.policy.evaluate(critic_obs_batch)
+            mu_batch = self.policy.action_mean
+            sigma_batch = self.policy.action_std
+            entropy_batch = self.policy.entropy
+            self._adapt_learning_rate(mu_batch, sigma_batch, old_mu_batch, old_sigma_batch)
+            surrogate_loss, value_loss = self._ppo_losses(actions_log_prob_batch, old_actions_log_prob_batch,
+                                                          advantages_batch, value_batch, target_values_batch,
+                                                          returns_batch)
+            loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_batch.mean()
+            smooth_loss, _ = self.smooth_loss(obs_batch, next_obs_batch, cont_batch, mu_batch, value_batch)
+            loss = loss + smooth_loss
+            self.optimizer.zero_grad()
+            loss.backward()
+            gdist.allreduce_grads(params)
+            nn.utils.clip_grad_norm_(params, self.max_grad_norm)
+            self.optimizer.step()
+            mean_value_loss += value_loss.detach()
+            mean_surrogate_loss += surrogate_loss.detach()
+            mean_smooth_loss += smooth_loss.detach()
+        num_updates = self.num_learning_epochs * self.num_mini_batches
+        self.storage.clear()
+        return {
+            "value_function": float(mean_value_loss) / num_updates,
+            "surrogate": float(mean_surrogate_loss) / num_updates,
+            "smooth_loss": float(mean_smooth_loss) / num_updates,
+        }

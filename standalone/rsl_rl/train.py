@@ -39,6 +39,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--max_iterations", type=int, default=None, help="RL Policy training iterations.")
     p.add_argument("--device", type=str, default=None, help="cuda:N (default: cuda:LOCAL_RANK)")
     p.add_argument("--log_root", type=str, default="logs", help="Root of logs/rsl_rl/<experiment>.")
+    p.add_argument("--agent", type=str, default="rsl_rl_cfg_entry_point",
+                   help="Registry key of the runner cfg (rsl_rl_l2c2_cfg_entry_point: PPOL2C2 recipe).")
     # AppLauncher flags the reference's train.sh passes; accepted for drop-in compatibility
     p.add_argument("--headless", action="store_true", default=False)
     p.add_argument("--enable_cameras", action="store_true", default=False)
@@ -77,7 +79,7 @@ def main(argv=None):
     task = args.task or "DiffLab-Quadcopter-CTBR-Racing-v0"
     rank, local_rank, world = gdist.init_from_env()
     env_cfg = registry.load_cfg_from_registry(task, "env_cfg_entry_point")
-    agent_cfg = registry.load_cfg_from_registry(task, "rsl_rl_cfg_entry_point")
+    agent_cfg = registry.load_cfg_from_registry(task, args.agent)
     agent_cfg = cli_args.update_rsl_rl_cfg(agent_cfg, args)
     if args.num_envs is not None:
         env_cfg.scene.num_envs = args.num_envs

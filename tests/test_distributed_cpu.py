@@ -22,7 +22,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, algorithm="PPO"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     try:
@@ -39,6 +39,7 @@ def _worker(rank, world, port, q):
         n = 32
         env = OracleVecEnv(num_envs=n, env_id_offset=rank * n, track_seed_offset=rank)
         cfg = QuadcopterPPORunnerCfg(device="cpu", num_steps_per_env=8)
+        cfg.algorithm.class_name = algorithm
         cfg.policy.actor_hidden_dims = [16, 16]
         cfg.policy.critic_hidden_dims = [16, 16]
         runner = OnPolicyRunner(env, cfg.to_dict(), log_dir=None, device="cpu")
@@ -63,11 +64,12 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_gloo_identical_updates():
+@pytest.mark.parametrize("algorithm", ["PPO", "PPOL2C2"])
+def test_two_rank_gloo_identical_updates(algorithm):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, algorithm)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=280) for _ in procs]

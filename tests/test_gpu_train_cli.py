@@ -23,3 +23,15 @@ def test_train_cli_two_iterations(tmp_path):
     r2 = train.main(["--task", "DiffLab-Quadcopter-CTBR-Racing-v0", "--num_envs", "1024", "--max_iterations", "1",
                      "--log_root", str(tmp_path), "--resume", "1"])
     assert r2.current_learning_iteration >= 1
+
+
+def test_train_cli_l2c2_recipe(tmp_path):
+    sys.path.insert(0, os.path.join(ROOT, "standalone", "rsl_rl"))
+    import train
+
+    runner = train.main(["--task", "DiffLab-Quadcopter-CTBR-Racing-v0", "--num_envs", "1024", "--headless",
+                         "--max_iterations", "2", "--log_root", str(tmp_path),
+                         "--agent", "rsl_rl_l2c2_cfg_entry_point"])
+    assert type(runner.alg).__name__ == "PPOL2C2"
+    assert runner.last_log["smooth_loss"] > 0.0
+    assert (tmp_path / "rsl_rl" / "racing_ppo_l2c2").exists()
