@@ -172,12 +172,30 @@ class GrBuffers(C.Structure):
     ]
 
 
+class GrCameraConfig(C.Structure):
+    _fields_ = [
+        ("width", C.c_int32), ("height", C.c_int32),
+        ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+        ("offset_pos", C.c_float * 3), ("offset_rot", C.c_float * 4),
+        ("max_distance", C.c_float), ("update_period", C.c_float), ("noise_std", C.c_float),
+        ("add_noise", C.c_int32), ("obs_scale", C.c_float), ("reserved", C.c_int32 * 6),
+    ]
+
+
+class GrCameraBuffers(C.Structure):
+    _fields_ = [("depth", C.c_void_p), ("age", C.c_void_p), ("obs_policy", C.c_void_p), ("obs_critic", C.c_void_p)]
+
+
+GR_CAM_STEP, GR_CAM_RESET, GR_CAM_OBSERVE = 0, 1, 2
+
 EXPORTS = [
     "gr_abi_version", "gr_config_default", "gr_config_size", "gr_create", "gr_destroy", "gr_last_error",
     "gr_num_blocks", "gr_num_log_rows", "gr_log_finalize", "gr_bytes_per_env_step", "gr_bind_tracks", "gr_bind_buffers", "gr_init", "gr_reset",
     "gr_step", "gr_observe", "gr_set_timing", "gr_read_timing", "gr_test_dynamics", "gr_test_math",
     "gr_test_philox",
     "gr_debug_read_stamps",
+    "gr_camera_config_default", "gr_camera_config_size", "gr_enable_camera", "gr_bind_camera_buffers",
+    "gr_camera_render", "gr_camera_bytes_per_env",
 ]
 
 _lib = None
@@ -208,6 +226,12 @@ def _declare(lib):
         "gr_test_math": (C.c_int, [vp, C.c_int, C.c_int, vp, vp, vp, vp]),
         "gr_test_philox": (C.c_int, [vp, C.c_int] + [C.c_uint32] * 4 + [vp, vp]),
         "gr_debug_read_stamps": (C.c_int, [vp, C.c_int]),
+        "gr_camera_config_default": (C.c_int, [C.POINTER(GrCameraConfig)]),
+        "gr_camera_config_size": (C.c_size_t, []),
+        "gr_enable_camera": (C.c_int, [vp, C.POINTER(GrCameraConfig)]),
+        "gr_bind_camera_buffers": (C.c_int, [vp, C.POINTER(GrCameraBuffers)]),
+        "gr_camera_render": (C.c_int, [vp, C.c_int, vp, vp]),
+        "gr_camera_bytes_per_env": (C.c_int, [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -232,6 +256,8 @@ def load(path: str | None = None):
         raise RuntimeError(f"libgr.so ABI {lib.gr_abi_version()} != expected {GR_ABI_VERSION}")
     if lib.gr_config_size() != C.sizeof(GrConfig):
         raise RuntimeError(f"gr_config size mismatch: C {lib.gr_config_size()} vs ctypes {C.sizeof(GrConfig)}")
+    if lib.gr_camera_config_size() != C.sizeof(GrCameraConfig):
+        raise RuntimeError("gr_camera_config size mismatch between libgr.so and the ctypes mirror")
     if path is None:
         _lib = lib
     return lib
@@ -242,6 +268,14 @@ def default_config() -> GrConfig:
     rc = load().gr_config_default(C.byref(cfg))
     if rc != 0:
         raise RuntimeError("gr_config_default failed")
+    return cfg
+
+
+def default_camera_config() -> GrCameraConfig:
+    cfg = GrCameraConfig()
+    rc = load().gr_camera_config_default(C.byref(cfg))
+    if rc != 0:
+        raise RuntimeError("gr_camera_config_default failed")
     return cfg
 
 

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/gr.h"
+#include "gr_camera.h"
 #include "gr_kernels.h"
 #include "gr_math.h"
 
@@ -29,6 +30,12 @@ struct gr_ctx {
   std::vector<int> blk_types;      // per workgroup: first | last terrain type << 16
   int* blk_dev = nullptr;
   std::string err;
+  // optional depth camera
+  bool cam_enabled = false;
+  gr_cam_const cam_k;
+  gr_cam_const* cam_dev = nullptr;
+  gr_camera_buffers cam_buf;
+  bool have_cam_buf = false;
   // optional kernel timing (gr_set_timing)
   std::vector<hipEvent_t> ev;  // [2 * GR_TIMING_RING]
   int ev_next = 0;
@@ -253,6 +260,7 @@ int gr_destroy(gr_ctx* c) {
   if (c->table) (void)hipFree(c->table);
   if (c->kc_dev) (void)hipFree(c->kc_dev);
   if (c->blk_dev) (void)hipFree(c->blk_dev);
+  if (c->cam_dev) (void)hipFree(c->cam_dev);
   delete c;
   return GR_OK;
 }
@@ -405,6 +413,113 @@ int gr_observe(gr_ctx* c, void* stream) {
   if (r) return r;
   hipError_t e = gr::launch_env(gr::KMODE_OBSERVE, c->args, nullptr, nullptr, (hipStream_t)stream, nullptr, nullptr);
   return e == hipSuccess ? GR_OK : hip_fail(c, e, "gr_observe");
+}
+
+int gr_camera_config_default(gr_camera_config* k) {
+  if (!k) return GR_ERR_ARG;
+  std::memset(k, 0, sizeof(*k));
+  // racing_ctbr_env.py:77-95 (the intrinsics are python doubles there)
+  k->width = 96;
+  k->height = 72;
+  k->fx = (float)(388.963 / (640.0 / 96.0));
+  k->cx = (float)(317.04 / (640.0 / 96.0));
+  k->fy = (float)(388.963 / (480.0 / 72.0));
+  k->cy = (float)(241.99 / (480.0 / 72.0));
+  k->offset_pos[0] = 0.01f;
+  k->offset_rot[0] = 0.991f;
+  k->offset_rot[2] = -0.131f;
+  k->max_distance = 10.0f;
+  k->update_period = 0.04f;  // racing_ctbr_env.py:390-391
+  k->noise_std = 0.02f;      // observation.py:84-85
+  k->add_noise = 1;
+  k->obs_scale = 10.0f;      // observation.py:88-92
+  return GR_OK;
+}
+
+size_t gr_camera_config_size(void) { return sizeof(gr_camera_config); }
+
+int gr_enable_camera(gr_ctx* c, const gr_camera_config* k) {
+  if (!c || !k) return fail(c, GR_ERR_ARG, "gr_enable_camera: null pointer");
+  const float* r = k->offset_rot;
+  const float qn = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
+  if (k->width <= 0 || k->width > GR_CAM_MAX_W || k->width % 4 != 0 || k->height <= 0 || k->height > GR_CAM_MAX_H)
+    return fail(c, GR_ERR_ARG, "gr_enable_camera: width must be a multiple of 4 in [4, 256], height in [1, 256]");
+  if (!(k->fx > 0.0f) || !(k->fy > 0.0f) || !std::isfinite(k->cx) || !std::isfinite(k->cy) || !(qn > 0.0f) ||
+      !(k->max_distance > 0.0f) || !(k->obs_scale > 0.0f) || !(k->update_period >= 0.0f) || !(k->noise_std >= 0.0f))
+    return fail(c, GR_ERR_ARG, "gr_enable_camera: invalid intrinsics / offset / range / noise");
+  if (c->cfg.max_gates > GR_CAM_MAX_GATES)
+    return fail(c, GR_ERR_ARG, "gr_enable_camera: max_gates > 64 (one lane per gate)");
+  gr_cam_derive(k, c->cfg.step_dt, &c->cam_k);
+  if (c->cam_dev) {
+    (void)hipFree(c->cam_dev);
+    c->cam_dev = nullptr;
+  }
+  c->cam_enabled = true;
+  return GR_OK;
+}
+
+int gr_bind_camera_buffers(gr_ctx* c, const gr_camera_buffers* b) {
+  if (!c || !b) return fail(c, GR_ERR_ARG, "gr_bind_camera_buffers: null pointer");
+  if (!b->depth || !b->age || !b->obs_policy || !b->obs_critic)
+    return fail(c, GR_ERR_ARG, "gr_bind_camera_buffers: null buffer");
+  if (!aligned16(b->depth) || !aligned16(b->obs_policy) || !aligned16(b->obs_critic) ||
+      (reinterpret_cast<uintptr_t>(b->age) & 3u))
+    return fail(c, GR_ERR_ARG, "gr_bind_camera_buffers: depth / obs rows must be 16-byte aligned");
+  c->cam_buf = *b;
+  c->have_cam_buf = true;
+  return GR_OK;
+}
+
+int gr_camera_render(gr_ctx* c, int mode, const uint8_t* mask, void* stream) {
+  int r = ready(c, "gr_camera_render");
+  if (r) return r;
+  if (!c->cam_enabled || !c->have_cam_buf)
+    return fail(c, GR_ERR_STATE, "gr_camera_render: gr_enable_camera and gr_bind_camera_buffers first");
+  if (mode != GR_CAM_STEP && mode != GR_CAM_RESET && mode != GR_CAM_OBSERVE)
+    return fail(c, GR_ERR_ARG, "gr_camera_render: unknown mode");
+  if (!c->cam_dev) {
+    hipError_t e = hipMalloc(&c->cam_dev, sizeof(gr_cam_const));
+    if (e == hipSuccess) e = hipMemcpy(c->cam_dev, &c->cam_k, sizeof(gr_cam_const), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(c, e, "gr_camera_render: camera constants");
+  }
+  gr::CamArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.cc = c->cam_dev;
+  a.state = c->buf.state;
+  a.istate = c->buf.istate;
+  a.obs_p16 = c->buf.obs_policy;
+  a.obs_c16 = c->buf.obs_critic;
+  a.terminated = c->buf.terminated;
+  a.time_out = c->buf.time_out;
+  a.mask = mode == GR_CAM_RESET ? mask : nullptr;
+  a.counters = c->buf.counters;
+  a.counter_index = c->buf.counter_index;
+  a.table = c->table;
+  a.track_stride = c->kc.track_stride;
+  a.num_levels = c->cfg.num_levels;
+  a.max_gates = c->cfg.max_gates;
+  a.num_envs = c->cfg.num_envs;
+  a.env_id_offset = c->cfg.env_id_offset;
+  a.mode = mode;
+  a.seed_lo = c->cfg.seed_lo;
+  a.seed_hi = c->cfg.seed_hi;
+  a.depth = c->cam_buf.depth;
+  a.age = c->cam_buf.age;
+  a.out_p = c->cam_buf.obs_policy;
+  a.out_c = c->cam_buf.obs_critic;
+  hipError_t e = gr::launch_camera(a, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : hip_fail(c, e, "gr_camera_render");
+}
+
+int gr_camera_bytes_per_env(const gr_ctx* c, int64_t* render_bytes, int64_t* reuse_bytes) {
+  if (!c || !render_bytes || !reuse_bytes) return GR_ERR_ARG;
+  if (!c->cam_enabled) return GR_ERR_STATE;
+  const int64_t img = (int64_t)c->cam_k.npix * 4, rows = 2 * (16 * 4 + img);
+  // both: state obs read (2 x 64), obs rows written, flags (2), age read + write (8)
+  const int64_t common = 2 * 64 + rows + 2 + 8;
+  *render_bytes = common + img + 2 * 16 + 16;  // depth written; pose planes + istate read
+  *reuse_bytes = common + img;                 // depth read
+  return GR_OK;
 }
 
 int gr_test_dynamics(gr_ctx* c, int n, int mode, const float* si, const float* ab, const float* cmd, const float* ci,

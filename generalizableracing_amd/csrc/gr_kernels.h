@@ -12,6 +12,8 @@
 #define GR_STAMP_WAVES 8192  // diagnostic stamps (GR_STAMPS builds only)
 #define GR_STAMP_SLOTS 16
 
+struct gr_cam_const;  // gr_camera.h
+
 namespace gr {
 
 enum { KMODE_STEP = 0, KMODE_RESET = 1, KMODE_OBSERVE = 2 };
@@ -51,6 +53,28 @@ struct KArgs {
   const int* blk_types;  // per workgroup: first | last terrain type << 16 (host-derived)
   KHot h;
 };
+
+// Depth camera (gr_camera.hip): everything by value except the derived constants.
+struct CamArgs {
+  const ::gr_cam_const* cc;  // device copy
+  const float* state;
+  const int32_t* istate;
+  const float* obs_p16;  // this call's state observations [N][16]
+  const float* obs_c16;
+  const uint8_t* terminated;
+  const uint8_t* time_out;
+  const uint8_t* mask;  // GR_CAM_RESET only (nullptr: all)
+  const uint32_t* counters;
+  int counter_index;
+  const float* table;  // packed track table
+  int track_stride, num_levels, max_gates, num_envs, env_id_offset, mode;
+  uint32_t seed_lo, seed_hi;
+  float* depth;
+  int32_t* age;
+  float* out_p;
+  float* out_c;
+};
+hipError_t launch_camera(const CamArgs& a, hipStream_t s);
 
 hipError_t launch_env(int mode, const KArgs& a, const float* actions, const uint8_t* mask, hipStream_t s,
                       hipEvent_t t0, hipEvent_t t1);

@@ -45,6 +45,45 @@ class SimCfg:
 
 
 @dataclass
+class CameraCfg:
+    """`front_camera` RayCasterCameraCfg (racing_ctbr_env.py:77-95, update_period :390-391)
+    and the `depth_image` observation term (mdp/observation.py:65-94)."""
+
+    width: int = 96
+    height: int = 72
+    # from_intrinsic_matrix([fx, 0, cx, 0, fy, cy, 0, 0, 1]) of the reference (python doubles)
+    intrinsic_matrix: tuple = (388.963 / (640 / 96), 0.0, 317.04 / (640 / 96),
+                               0.0, 388.963 / (480 / 72), 241.99 / (480 / 72), 0.0, 0.0, 1.0)
+    offset_pos: tuple = (0.01, 0.0, 0.0)
+    offset_rot: tuple = (0.991, 0.0, -0.131, 0.0)  # w x y z, convention "world" (normalised)
+    max_distance: float = 10.0
+    update_period: float = 0.04
+    noise_std: float = 0.02      # policy group add_noise=True
+    add_noise: bool = True
+    obs_scale: float = 10.0      # depth_image normalize: > 10 -> 10, / 10
+
+    @property
+    def num_pixels(self) -> int:
+        return self.width * self.height
+
+    def to_gr(self) -> _abi.GrCameraConfig:
+        k = _abi.GrCameraConfig()
+        k.width, k.height = int(self.width), int(self.height)
+        m = self.intrinsic_matrix
+        k.fx, k.cx, k.fy, k.cy = float(m[0]), float(m[2]), float(m[4]), float(m[5])
+        for j in range(3):
+            k.offset_pos[j] = float(self.offset_pos[j])
+        for j in range(4):
+            k.offset_rot[j] = float(self.offset_rot[j])
+        k.max_distance = float(self.max_distance)
+        k.update_period = float(self.update_period)
+        k.noise_std = float(self.noise_std)
+        k.add_noise = int(bool(self.add_noise))
+        k.obs_scale = float(self.obs_scale)
+        return k
+
+
+@dataclass
 class RacingEnvCfg:
     scene: SceneCfg = field(default_factory=SceneCfg)
     terrain: TerrainCfg = field(default_factory=TerrainCfg)
@@ -56,6 +95,9 @@ class RacingEnvCfg:
     integrator: str = "dd_explicit"         # or "semi_implicit"
     mass: float = 0.6                       # ASSUMPTION: USD mass not in the reference
     is_finite_horizon: bool = False
+    # front depth camera: None = the state-only task (obs 16); CameraCfg() = the reference's
+    # vision task (obs 16 + 96*72, racing_ctbr_env.py:141-160)
+    camera: CameraCfg | None = None
     # shard description for multi-GPU runs (env ids offset for the RNG, track seed offset)
     env_id_offset: int = 0
     track_seed_offset: int = 0
@@ -143,3 +185,10 @@ class RacingEnvCfg:
 
 
 QuadcopterRacingCTBREnvCfg = RacingEnvCfg
+
+
+@dataclass
+class RacingVisionEnvCfg(RacingEnvCfg):
+    """The reference task as registered (policy/critic obs carry the depth image)."""
+
+    camera: CameraCfg | None = field(default_factory=CameraCfg)

@@ -119,6 +119,28 @@ class RacingEnv:
         self._cur = 0  # index of the output set written by the last call
         self._bufs = [self._make_buffers(k) for k in range(LOG_RING)]
         self._log_keys = self._build_log_keys()
+        # ---- optional front depth camera (the reference's vision task)
+        self.camera = cfg.camera
+        self.num_obs = _abi.OBS_DIM
+        if self.camera is not None:
+            self._cam_cfg = self.camera.to_gr()
+            self._call("gr_enable_camera", C.byref(self._cam_cfg))
+            npix = self.camera.num_pixels
+            self.num_obs = _abi.OBS_DIM + npix
+            # the sensor's data buffer (distance_to_image_plane) and its age; -1 = outdated
+            self.depth = torch.zeros(n, npix, dtype=torch.float32, device=dev)
+            self.camera_age = torch.full((n,), -1, dtype=torch.int32, device=dev)
+            self._img_sets = [{"policy": torch.zeros(n, self.num_obs, dtype=torch.float32, device=dev),
+                               "critic": torch.zeros(n, self.num_obs, dtype=torch.float32, device=dev)}
+                              for _ in range(2)]
+            self._cam_bufs = []
+            for k in range(2):
+                cb = _abi.GrCameraBuffers()
+                cb.depth = self.depth.data_ptr()
+                cb.age = self.camera_age.data_ptr()
+                cb.obs_policy = self._img_sets[k]["policy"].data_ptr()
+                cb.obs_critic = self._img_sets[k]["critic"].data_ptr()
+                self._cam_bufs.append(cb)
         self.extras: dict = {}
         # startup (gr_init): nominal state, startup DR events, initial terrain levels
         self._bind(0)
@@ -162,6 +184,12 @@ class RacingEnv:
 
     def _bind(self, k: int):
         self._call("gr_bind_buffers", C.byref(self._bufs[k % LOG_RING]))
+        if getattr(self, "camera", None) is not None:
+            self._call("gr_bind_camera_buffers", C.byref(self._cam_bufs[(k + 1) % 2]))
+
+    def _render(self, mode: int, mask_ptr=None):
+        if self.camera is not None:
+            self._call("gr_camera_render", mode, mask_ptr, self._stream())
 
     def _stream(self):
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -206,7 +234,15 @@ class RacingEnv:
         return keys
 
     def _obs_dict(self, s):
+        if self.camera is not None:
+            img = self._img_sets[self._cur]
+            return {"policy": img["policy"], "critic": img["critic"], "auxiliary": s["auxiliary"]}
         return {"policy": s["policy"], "critic": s["critic"], "auxiliary": s["auxiliary"]}
+
+    def state_obs(self) -> dict:
+        """The 16 state terms of the last call (without the image)."""
+        s = self._sets[self._cur]
+        return {"policy": s["policy"], "critic": s["critic"]}
 
     # ------------------------------------------------------------------ properties
     @property
@@ -277,6 +313,7 @@ class RacingEnv:
             a = a.to(device=self.device, dtype=torch.float32).contiguous()
         out, log = self._advance()
         self._call("gr_step", a.data_ptr(), self._stream())
+        self._render(_abi.GR_CAM_STEP)
         self.common_step_counter += 1
         self.extras = {"log": log}
         return self._obs_dict(out), out["reward"], out["terminated"], out["time_out"], self.extras
@@ -289,7 +326,9 @@ class RacingEnv:
             mask_t = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
             mask_t[ids] = 1
         out, log = self._advance()
-        self._call("gr_reset", mask_t.data_ptr() if mask_t is not None else None, self._stream())
+        mp = mask_t.data_ptr() if mask_t is not None else None
+        self._call("gr_reset", mp, self._stream())
+        self._render(_abi.GR_CAM_RESET, mp)
         self.extras = {"log": log}
         return self._obs_dict(out), self.extras
 
@@ -297,6 +336,7 @@ class RacingEnv:
         """ObservationManager.compute(): fresh observation noise, no state change."""
         out, _ = self._advance()
         self._call("gr_observe", self._stream())
+        self._render(_abi.GR_CAM_OBSERVE)
         return self._obs_dict(out)
 
     def seed(self, seed: int = -1) -> int:
@@ -324,8 +364,8 @@ class RslRlVecEnvWrapper:
         self.device = env.device
         self.max_episode_length = env.max_episode_length
         self.num_actions = env.num_actions
-        self.num_obs = _abi.OBS_DIM
-        self.num_privileged_obs = _abi.OBS_DIM
+        self.num_obs = env.num_obs
+        self.num_privileged_obs = env.num_obs
         self.env.reset()
 
     @property

@@ -198,6 +198,40 @@ typedef struct gr_buffers {
   int32_t reserved;
 } gr_buffers;
 
+/*
+ * Front depth camera (optional).  Reference: `front_camera = RayCasterCameraCfg(...)`
+ * (extensions/diff.lab_tasks/diff/lab_tasks/tasks/quadcopter_diff/racing_ctbr_env.py:77-95,
+ * update_period :390-391) and the `depth_image` observation term (.../quadcopter_diff/mdp/
+ * observation.py:65-94), whose output the policy / critic groups concatenate after the 16
+ * state terms (racing_ctbr_env.py:141-160): obs rows are [16 state | H*W image].
+ * Defaults (gr_camera_config_default) are those of the reference cfg.
+ */
+typedef struct gr_camera_config {
+  int32_t width, height;  /* 96, 72 */
+  float fx, fy, cx, cy;   /* pinhole intrinsics in pixels (from_intrinsic_matrix, :87-91) */
+  float offset_pos[3];    /* (0.01, 0, 0) in the body frame */
+  float offset_rot[4];    /* (0.991, 0, -0.131, 0) w,x,y,z, "world" convention; normalised */
+  float max_distance;     /* 10, depth_clipping_behavior "max" */
+  float update_period;    /* 0.04 s */
+  float noise_std;        /* 0.02: policy image x (1 + N(0,1) * std) */
+  int32_t add_noise;      /* policy group add_noise=True (critic: False) */
+  float obs_scale;        /* 10: depth_image normalize (> 10 -> 10, / 10) */
+  int32_t reserved[6];
+} gr_camera_config;
+
+/* Camera buffers (caller-owned device memory, 16-byte aligned). */
+typedef struct gr_camera_buffers {
+  float* depth;      /* [num_envs][H*W] persistent distance_to_image_plane (m), the sensor's data buffer */
+  int32_t* age;      /* [num_envs] env steps since the last render; -1 = outdated (render at next call) */
+  float* obs_policy; /* [num_envs][16 + H*W]: state terms copied from gr_buffers.obs_policy, noisy image */
+  float* obs_critic; /* [num_envs][16 + H*W]: state terms from gr_buffers.obs_critic, clean image */
+} gr_camera_buffers;
+
+/* gr_camera_render modes: which envs are outdated before the image observation is formed */
+#define GR_CAM_STEP 0    /* after gr_step: terminated|time_out envs, and envs whose period elapsed */
+#define GR_CAM_RESET 1   /* after gr_reset(mask): the masked envs (mask NULL: all) */
+#define GR_CAM_OBSERVE 2 /* after gr_observe: only envs still outdated (age -1) */
+
 typedef struct gr_ctx gr_ctx;
 
 int gr_abi_version(void);
@@ -232,6 +266,20 @@ int gr_reset(gr_ctx* ctx, const uint8_t* mask, void* stream);
 int gr_step(gr_ctx* ctx, const float* actions, void* stream);
 /* recompute observations (fresh observation noise), no state change */
 int gr_observe(gr_ctx* ctx, void* stream);
+
+/* Depth camera.  gr_enable_camera validates the cfg and derives its constants (once);
+ * gr_bind_camera_buffers binds the image outputs of the next render (rebind per call like
+ * gr_bind_buffers).  gr_camera_render forms the image observation of the call just made
+ * (gr_step / gr_reset / gr_observe, same gr_buffers binding, same stream): it re-renders the
+ * outdated envs (Isaac Lab RayCasterCamera._update_buffers_impl), then writes both obs rows
+ * (fresh image noise from the call's observation counter).  Graph-capturable. */
+int gr_camera_config_default(gr_camera_config* cfg);
+size_t gr_camera_config_size(void);
+int gr_enable_camera(gr_ctx* ctx, const gr_camera_config* cfg);
+int gr_bind_camera_buffers(gr_ctx* ctx, const gr_camera_buffers* bufs);
+int gr_camera_render(gr_ctx* ctx, int mode, const uint8_t* mask, void* stream);
+/* algorithmic HBM bytes per env of one render call, with and without the re-render */
+int gr_camera_bytes_per_env(const gr_ctx* ctx, int64_t* render_bytes, int64_t* reuse_bytes);
 
 /* In-library HIP-event timing of the fused step kernel alone (not the log
  * finalize): when enabled, gr_step brackets the env kernel with a pair of

@@ -27,6 +27,7 @@
 
 #include "../generalizableracing_amd/csrc/gr_math.h"
 #include "../generalizableracing_amd/csrc/gr_rng.h"
+#include "../generalizableracing_amd/csrc/gr_camera.h"
 
 size_t gro_env_size(void) { return sizeof(gro_env); }
 
@@ -788,4 +789,100 @@ void gro_test_fields6(int n, const uint32_t* in4, uint32_t* out6) {
     gr_u32x4 r = {in4[i * 4], in4[i * 4 + 1], in4[i * 4 + 2], in4[i * 4 + 3]};
     gr_fields6(r, out6 + i * 6);
   }
+}
+
+/* ------------------------------------------------------------ depth camera */
+/* The front camera + depth_image observation (racing_ctbr_env.py:77-95,141-160,390-391;
+ * mdp/observation.py:65-94), pixel by pixel with the shared gr_camera.h functions: one
+ * env at a time, rays in row-major order, gates in index order. */
+void gro_camera(const gr_config* c, const gr_camera_config* kcfg, const gro_env* envs, int n, const gro_tracks* tr,
+                int mode, const uint8_t* mask, const uint8_t* terminated, const uint8_t* time_out, uint32_t cnt,
+                float* depth, int32_t* age, const float* obs_p16, const float* obs_c16, float* out_p, float* out_c) {
+  gr_cam_const K;
+  gr_cam_derive(kcfg, c->step_dt, &K);
+  const int W = K.width, npix = K.npix;
+  const size_t row = (size_t)(16 + npix);
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < n; ++i) {
+    /* SensorBase: outdated after update_period (in whole env steps) or on reset */
+    int outdated = age[i] < 0, aged = age[i] < 0 ? 0 : age[i];
+    if (mode == GR_CAM_STEP) {
+      aged += 1;
+      outdated = outdated || terminated[i] || time_out[i] || aged >= K.period_steps;
+    } else if (mode == GR_CAM_RESET) {
+      outdated = outdated || mask == NULL || mask[i];
+    }
+    age[i] = outdated ? 0 : aged;
+    float* dep = depth + (size_t)i * npix;
+    if (outdated) {
+      const gro_env* e = &envs[i];
+      float o[3], c0[3], c1[3], c2[3];
+      gr_cam_pose(&K, e->p, e->q, o, c0, c1, c2);
+      const int track = track_index(c, e->type, e->level);
+      const float gz = track_rec(tr, track)[0];
+      const int ng = track_num_gates(tr, track);
+      float slot[GR_CAM_MAX_GATES][GR_CAM_SLOT];
+      for (int g = 0; g < ng; ++g) gr_cam_gate_setup(gate_rec(c, tr, track, g), o, c0, c1, c2, K.max_distance, slot[g]);
+      for (int k = 0; k < npix; ++k) {
+        const int v = k / W, u = k % W;
+        const float a = K.ray_a[u], b = K.ray_b[v];
+        const float dz = gr_fmaf(b, c2[2], gr_fmaf(a, c1[2], c0[2]));
+        float d = gr_cam_ground_hit(o[2], gz, dz);
+        for (int g = 0; g < ng; ++g) {
+          const float* sl = slot[g];
+          if (sl[GR_CS_VALID] == 0.0f) continue;
+          if (b >= sl[GR_CS_BMIN] && b <= sl[GR_CS_BMAX] && a >= sl[GR_CS_AMIN] && a <= sl[GR_CS_AMAX])
+            d = gr_minf(d, gr_cam_gate_hit(sl, a, b));
+        }
+        dep[k] = gr_cam_clip(d, K.max_distance);
+      }
+    }
+    float* rp = out_p + (size_t)i * row;
+    float* rc = out_c + (size_t)i * row;
+    for (int k = 0; k < 16; ++k) {
+      rp[k] = obs_p16[(size_t)i * 16 + k];
+      rc[k] = obs_c16[(size_t)i * 16 + k];
+    }
+    const uint32_t gid = gid_of(c, i);
+    for (int q = 0; q < npix / 4; ++q) {
+      float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (K.add_noise) gr_cam_noise4(gid, cnt, (uint32_t)q, c->seed_lo, c->seed_hi, z);
+      for (int j = 0; j < 4; ++j) {
+        const float d = dep[4 * q + j];
+        rp[16 + 4 * q + j] = gr_cam_obs(d, z[j], K.noise_std, K.obs_scale, K.inv_obs_scale);
+        rc[16 + 4 * q + j] = gr_cam_obs_clean(d, K.obs_scale, K.inv_obs_scale);
+      }
+    }
+  }
+}
+
+/* the shared pinhole / pose / gate-slot / hit functions, one ray at a time (known-answer tests) */
+float gro_camera_ray(const gr_config* c, const gr_camera_config* kcfg, const gro_tracks* tr, int track,
+                     const float p[3], const float q[4], int u, int v) {
+  gr_cam_const K;
+  gr_cam_derive(kcfg, c->step_dt, &K);
+  float o[3], c0[3], c1[3], c2[3];
+  gr_cam_pose(&K, p, q, o, c0, c1, c2);
+  const float a = K.ray_a[u], b = K.ray_b[v];
+  const float dz = gr_fmaf(b, c2[2], gr_fmaf(a, c1[2], c0[2]));
+  float d = gr_cam_ground_hit(o[2], track_rec(tr, track)[0], dz);
+  const int ng = track_num_gates(tr, track);
+  for (int g = 0; g < ng; ++g) {
+    float sl[GR_CAM_SLOT];
+    gr_cam_gate_setup(gate_rec(c, tr, track, g), o, c0, c1, c2, K.max_distance, sl);
+    if (sl[GR_CS_VALID] == 0.0f) continue;
+    if (b >= sl[GR_CS_BMIN] && b <= sl[GR_CS_BMAX] && a >= sl[GR_CS_AMIN] && a <= sl[GR_CS_AMAX])
+      d = gr_minf(d, gr_cam_gate_hit(sl, a, b));
+  }
+  return gr_cam_clip(d, K.max_distance);
+}
+
+/* camera pose + per-pixel ray constants, for the independent float64 mesh check */
+void gro_camera_frame(const gr_config* c, const gr_camera_config* kcfg, const float p[3], const float q[4],
+                      float* out /* o3 c0 c1 c2 (12), ray_a[W], ray_b[H] */) {
+  gr_cam_const K;
+  gr_cam_derive(kcfg, c->step_dt, &K);
+  gr_cam_pose(&K, p, q, out, out + 3, out + 6, out + 9);
+  for (int u = 0; u < K.width; ++u) out[12 + u] = K.ray_a[u];
+  for (int v = 0; v < K.height; ++v) out[12 + K.width + v] = K.ray_b[v];
 }

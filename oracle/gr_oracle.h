@@ -64,6 +64,16 @@ void gro_test_math(int fn, int n, const float* x, const float* y, float* out);
 void gro_test_philox(int n, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
                      uint32_t* out4);
 void gro_test_fields6(int n, const uint32_t* in4, uint32_t* out6);
+/* depth camera + depth_image observation, same contract as gr_camera_render (include/gr.h);
+ * cnt = the observation counter of the call the images belong to */
+void gro_camera(const gr_config* cfg, const gr_camera_config* kcfg, const gro_env* envs, int n, const gro_tracks* tr,
+                int mode, const uint8_t* mask, const uint8_t* terminated, const uint8_t* time_out, uint32_t cnt,
+                float* depth, int32_t* age, const float* obs_p16, const float* obs_c16, float* out_p, float* out_c);
+/* one ray: distance_to_image_plane of pixel (u, v) from body pose (p, q) on track `track` */
+float gro_camera_ray(const gr_config* cfg, const gr_camera_config* kcfg, const gro_tracks* tr, int track,
+                     const float p[3], const float q[4], int u, int v);
+void gro_camera_frame(const gr_config* cfg, const gr_camera_config* kcfg, const float p[3], const float q[4],
+                      float* out);
 /* OpenMP threads gro_step uses (1 without OpenMP) */
 int gro_num_threads(void);
 

@@ -52,10 +52,14 @@ def load():
             "gro_test_philox": [C.c_int] + [C.c_uint32] * 6 + [vp],
             "gro_test_fields6": [C.c_int, vp, vp],
             "gro_num_threads": [],
+            "gro_camera": [vp, vp, vp, C.c_int, vp, C.c_int, vp, vp, vp, C.c_uint32, vp, vp, vp, vp, vp, vp],
+            "gro_camera_frame": [vp, vp, vp, vp, vp],
         }.items():
             f = getattr(lib, name)
             f.restype = None
             f.argtypes = args
+        lib.gro_camera_ray.restype = C.c_float
+        lib.gro_camera_ray.argtypes = [vp, vp, vp, C.c_int, vp, vp, C.c_int, C.c_int]
         lib.gro_collision_count.restype = C.c_int
         lib.gro_collision_count.argtypes = [vp, vp, C.c_int, vp, vp]
         if lib.gro_env_size() != ENV_DTYPE.itemsize:
@@ -119,6 +123,39 @@ class Oracle:
     def observe(self):
         self.lib.gro_observe(C.byref(self.cfg), _p(self.envs), self.n, C.byref(self.tracks), _p(self.counter),
                              C.byref(self.out))
+
+    # ---- depth camera (gro_camera): state lives next to the env records
+    def enable_camera(self, cam_cfg):
+        """cam_cfg: generalizableracing_amd._abi.GrCameraConfig."""
+        self.cam_cfg = cam_cfg
+        npix = cam_cfg.width * cam_cfg.height
+        self.depth = np.zeros((self.n, npix), np.float32)
+        self.cam_age = np.full(self.n, -1, np.int32)
+        self.img_policy = np.zeros((self.n, 16 + npix), np.float32)
+        self.img_critic = np.zeros((self.n, 16 + npix), np.float32)
+
+    def camera(self, mode: int, mask: np.ndarray | None = None):
+        """Image observation of the call just made (cnt = the counter that call used)."""
+        mp = None if mask is None else _p(np.ascontiguousarray(mask, dtype=np.uint8))
+        cnt = (int(self.counter[0]) - 1) & 0xFFFFFFFF
+        self.lib.gro_camera(C.byref(self.cfg), C.byref(self.cam_cfg), _p(self.envs), self.n, C.byref(self.tracks),
+                            mode, mp, _p(self.terminated), _p(self.time_out), cnt, _p(self.depth), _p(self.cam_age),
+                            _p(self.obs_policy), _p(self.obs_critic), _p(self.img_policy), _p(self.img_critic))
+
+    def camera_ray(self, track: int, p, q, u: int, v: int) -> float:
+        p = np.ascontiguousarray(p, dtype=np.float32)
+        q = np.ascontiguousarray(q, dtype=np.float32)
+        return float(self.lib.gro_camera_ray(C.byref(self.cfg), C.byref(self.cam_cfg), C.byref(self.tracks), track,
+                                             _p(p), _p(q), u, v))
+
+    def camera_frame(self, p, q):
+        """-> (o[3], c0, c1, c2, ray_a[W], ray_b[H]) as the oracle computes them (fp32)."""
+        W, H = self.cam_cfg.width, self.cam_cfg.height
+        out = np.zeros(12 + W + H, np.float32)
+        self.lib.gro_camera_frame(C.byref(self.cfg), C.byref(self.cam_cfg),
+                                  _p(np.ascontiguousarray(p, np.float32)), _p(np.ascontiguousarray(q, np.float32)),
+                                  _p(out))
+        return out[0:3], out[3:6], out[6:9], out[9:12], out[12:12 + W], out[12 + W:]
 
     def collision_count(self, track: int, p, q) -> int:
         p = np.ascontiguousarray(p, dtype=np.float32)

@@ -1,0 +1,90 @@
+"""Depth-camera throughput on one MI355X: gr_camera_render after gr_step.
+
+Times the camera kernel alone with HIP events on the stream it is launched on (torch's current
+stream), separately for the calls that re-render every sensor (every 2nd step: update_period
+0.04 s at step_dt 0.03 s) and the calls that reuse the depth buffer, and reports algorithmic
+bytes per call (gr_camera_bytes_per_env) / time against the HBM peak.
+
+  python scripts/bench_camera.py --envs 65536 --steps 40
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from generalizableracing_amd import _abi  # noqa: E402
+from generalizableracing_amd.envs.racing_cfg import CameraCfg, RacingEnvCfg, SceneCfg, SimCfg  # noqa: E402
+from generalizableracing_amd.envs.racing_env import RacingEnv  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=6)
+    ap.add_argument("--no-noise", action="store_true", help="ablation: policy image without noise")
+    ap.add_argument("--period", type=float, default=None, help="camera update_period override (0: every step)")
+    args = ap.parse_args(argv)
+    n = args.envs
+    cam = CameraCfg(add_noise=not args.no_noise)
+    if args.period is not None:
+        cam.update_period = args.period
+    env = RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device="cuda:0"), camera=cam))
+    env.reset()
+    g = torch.Generator(device="cuda:0").manual_seed(1234)
+    acts = [torch.randn(n, 4, device="cuda:0", generator=g) for _ in range(8)]
+    rb, ub = C.c_int64(), C.c_int64()
+    env._call("gr_camera_bytes_per_env", C.byref(rb), C.byref(ub))
+    for k in range(args.warmup):
+        env.step(acts[k % 8])
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    rendered = []
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        env._advance()
+        env._call("gr_step", acts[k % 8].data_ptr(), env._stream())
+        ev[k][0].record()
+        env._render(_abi.GR_CAM_STEP)
+        ev[k][1].record()
+        rendered.append(env.camera_age.eq(0).float().mean())  # age 0: rendered by this call
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ms = [a.elapsed_time(b) for a, b in ev]
+    frac = [float(r) for r in rendered]
+    rend = [m for m, f in zip(ms, frac) if f > 0.5]
+    reuse = [m for m, f in zip(ms, frac) if f <= 0.5]
+    avg = lambda xs: sum(xs) / max(len(xs), 1)  # noqa: E731
+    mean_frac = sum(frac) / len(frac)
+    bytes_call = n * (mean_frac * rb.value + (1 - mean_frac) * ub.value)
+    out = {
+        "kernel": "gr::camera_kernel",
+        "noise": not args.no_noise,
+        "envs": n, "steps": args.steps,
+        "image": [env.camera.height, env.camera.width],
+        "render_fraction": mean_frac,
+        "ms_render_call": avg(rend), "ms_reuse_call": avg(reuse), "ms_avg_call": avg(ms),
+        "bytes_per_env_render": rb.value, "bytes_per_env_reuse": ub.value,
+        "gbs_render_call": n * rb.value / (avg(rend) * 1e6) if rend else None,
+        "gbs_reuse_call": n * ub.value / (avg(reuse) * 1e6) if reuse else None,
+        "gbs_avg": bytes_call / (avg(ms) * 1e6),
+        "hbm_frac_avg": bytes_call / (avg(ms) * 1e6) / HBM_PEAK_GBS,
+        "camera_env_steps_per_s": n / (avg(ms) * 1e-3),
+        "wall_env_steps_per_s_step_plus_camera": n * args.steps / wall,
+    }
+    print(json.dumps(out))
+    env.close()
+
+
+if __name__ == "__main__":
+    main()

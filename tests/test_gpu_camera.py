@@ -1,0 +1,134 @@
+"""Depth camera: HIP kernel (gr_camera_render through the C ABI) vs the CPU oracle.
+
+Kernel and oracle share gr_camera.h and are built without FMA contraction, so the depth
+buffer, the sensor ages and both observation rows ([16 state | 96x72 image]) are asserted
+BIT-EXACT after every call of a free run (resets, time-outs, observe, masked reset).  At the
+full 65 536-env size the oracle is not run; size-independent properties are checked instead.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import oracle  # noqa: E402
+from generalizableracing_amd import _abi  # noqa: E402
+from generalizableracing_amd.envs.racing_cfg import CameraCfg, RacingEnvCfg, SceneCfg, SimCfg  # noqa: E402
+from generalizableracing_amd.envs.racing_env import RacingEnv  # noqa: E402
+from test_gpu_parity import assert_envs_equal, bits, kernel_envs  # noqa: E402
+
+DEV = "cuda:0"
+
+
+def make(n, **cam):
+    cfg = RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV), camera=CameraCfg(**cam))
+    env = RacingEnv(cfg)
+    orc = oracle.Oracle(env.gr_config, env.track_gates.cpu().numpy(), env.track_records.cpu().numpy())
+    orc.init()
+    orc.enable_camera(env._cam_cfg)
+    return env, orc
+
+
+def compare(env, orc, where):
+    torch.cuda.synchronize()
+    got_d = env.depth.cpu().numpy()
+    if not np.array_equal(bits(got_d), bits(orc.depth)):
+        idx = np.argwhere(bits(got_d) != bits(orc.depth))[0]
+        raise AssertionError(f"{where}: depth differs at {idx}: kernel {got_d[tuple(idx)]} oracle {orc.depth[tuple(idx)]}"
+                             f" ({(bits(got_d) != bits(orc.depth)).sum()} pixels)")
+    assert np.array_equal(env.camera_age.cpu().numpy(), orc.cam_age), where
+    obs = env.obs_buf
+    for key, want in (("policy", orc.img_policy), ("critic", orc.img_critic)):
+        got = obs[key].cpu().numpy()
+        assert got.shape == want.shape, (where, key)
+        assert np.array_equal(bits(got), bits(want)), (where, key, np.abs(got - want).max())
+
+
+def test_camera_free_run_bit_exact():
+    n, steps = 640, 30
+    env, orc = make(n)
+    env.reset()
+    orc.reset(None)
+    orc.camera(_abi.GR_CAM_RESET)
+    assert_envs_equal(kernel_envs(env), orc.envs, "reset")
+    compare(env, orc, "reset")
+    g = torch.Generator().manual_seed(11)
+    eplen = torch.randint(150, 200, (n,), generator=g, dtype=torch.int32)
+    env.episode_length_buf = eplen.to(DEV)
+    orc.envs["ep_len"] = eplen.numpy()
+    n_done = 0
+    for k in range(steps):
+        a = (torch.randn(n, 4, generator=g) * 1.2).numpy().astype(np.float32)
+        env.step(torch.from_numpy(a).to(DEV))
+        orc.step(a)
+        orc.camera(_abi.GR_CAM_STEP)
+        compare(env, orc, f"step {k}")
+        n_done += int(orc.dones.sum())
+    assert n_done > 20
+    assert (orc.depth < 9.5).mean() > 0.05  # gates / ground in view
+    env.observe()
+    orc.observe()
+    orc.camera(_abi.GR_CAM_OBSERVE)
+    compare(env, orc, "observe")
+    mask = np.zeros(n, np.uint8)
+    mask[::5] = 1
+    env.reset(env_ids=np.nonzero(mask)[0])
+    orc.reset(mask)
+    orc.camera(_abi.GR_CAM_RESET, mask)
+    compare(env, orc, "masked reset")
+    env.close()
+
+
+def test_camera_no_noise_and_every_step_period():
+    env, orc = make(256, add_noise=False, update_period=0.0)
+    env.reset()
+    orc.reset(None)
+    orc.camera(_abi.GR_CAM_RESET)
+    compare(env, orc, "reset")
+    g = torch.Generator().manual_seed(2)
+    for k in range(4):
+        a = torch.randn(256, 4, generator=g).numpy().astype(np.float32)
+        env.step(torch.from_numpy(a).to(DEV))
+        orc.step(a)
+        orc.camera(_abi.GR_CAM_STEP)
+        compare(env, orc, f"step {k}")
+        assert (orc.cam_age == 0).all()
+    obs = env.obs_buf
+    assert torch.equal(obs["policy"][:, 16:], obs["critic"][:, 16:])
+    env.close()
+
+
+def test_camera_full_size_properties():
+    """65 536 envs: rows carry the state terms, the critic image is the clipped depth / 10, the
+    policy image is that times (1 + 0.02 N(0,1)) clipped to 1, and sensors re-render every 2nd step
+    (all in lockstep after the initial reset, as Isaac Lab's timestamps are)."""
+    n = 65536
+    cfg = RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV), camera=CameraCfg())
+    env = RacingEnv(cfg)
+    env.reset()
+    g = torch.Generator(device=DEV).manual_seed(0)
+    prev_depth = env.depth.clone()
+    for k in range(4):
+        env.step(torch.randn(n, 4, device=DEV, generator=g))
+        obs = env.obs_buf
+        st = env.state_obs()
+        assert torch.equal(obs["policy"][:, :16], st["policy"]) and torch.equal(obs["critic"][:, :16], st["critic"])
+        clean = obs["critic"][:, 16:]
+        assert torch.equal(clean, torch.clamp(env.depth, max=10.0) / 10.0)  # torch: x * fp32(1/10), as the kernel
+        noisy = obs["policy"][:, 16:]
+        assert bool(torch.isfinite(noisy).all()) and float(noisy.min()) >= 0.0 and float(noisy.max()) <= 1.0
+        near = env.depth < 8.0
+        r = noisy[near] / clean[near] - 1.0
+        assert abs(float(r.mean())) < 1e-3 and 0.019 < float(r.std()) < 0.021
+        age = env.camera_age
+        rendered = age == 0
+        # not rendered => unchanged depth
+        same = (env.depth == prev_depth).all(dim=1)
+        assert bool(same[~rendered].all())
+        frac = float(rendered.float().mean())
+        if k % 2 == 1:
+            assert frac > 0.99, frac  # 2 steps since the reset render: all outdated
+        else:
+            assert frac < 0.1, frac  # only the envs reset this step
+        prev_depth = env.depth.clone()
+    env.close()
