@@ -18,27 +18,71 @@
 
 namespace gr {
 
+#define DEV_INLINE __device__ __forceinline__
+
+typedef float gr_v4f __attribute__((ext_vector_type(4)));
+// streaming store: the obs rows (2 x 27.7 KB per env) are not re-read by this kernel
+DEV_INLINE void nt_store4(float4* p, float4 v) {
+  const gr_v4f x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<gr_v4f*>(p));
+}
+
 #define CAM_WAVES 4
 #define CAM_SLOT4 (GR_CAM_SLOT / 4)
+#ifndef CAM_BATCH
+#define CAM_BATCH 9  // reuse path: depth quads loaded per lane before any is consumed (27 = 3 x 9 at 96x72)
+#endif
 
-__global__ __launch_bounds__(CAM_WAVES * 64) void camera_kernel(CamArgs a) {
-  __shared__ __attribute__((aligned(16))) float s_ray_a[GR_CAM_MAX_W];
-  __shared__ float s_ray_b[GR_CAM_MAX_H];
-  __shared__ float4 s_slot[CAM_WAVES][GR_CAM_MAX_GATES][CAM_SLOT4];
+// both observation rows of one pixel quad: fresh noise (quad index q), normalisation, streaming stores
+DEV_INLINE void emit_quad(const CamArgs& a, const gr_cam_const* __restrict__ cc, float4* op4, float4* oc4, int q,
+                          float4 d4, uint32_t gid, uint32_t cnt) {
+  const float scale = cc->obs_scale, inv = cc->inv_obs_scale, nstd = cc->noise_std;
+  float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (cc->add_noise) gr_cam_noise4(gid, cnt, (uint32_t)q, a.seed_lo, a.seed_hi, z);
+  float4 op, oc;
+  op.x = gr_cam_obs(d4.x, z[0], nstd, scale, inv); oc.x = gr_cam_obs_clean(d4.x, scale, inv);
+  op.y = gr_cam_obs(d4.y, z[1], nstd, scale, inv); oc.y = gr_cam_obs_clean(d4.y, scale, inv);
+  op.z = gr_cam_obs(d4.z, z[2], nstd, scale, inv); oc.z = gr_cam_obs_clean(d4.z, scale, inv);
+  op.w = gr_cam_obs(d4.w, z[3], nstd, scale, inv); oc.w = gr_cam_obs_clean(d4.w, scale, inv);
+  nt_store4(op4 + q, op);
+  nt_store4(oc4 + q, oc);
+}
 
+DEV_INLINE void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Dynamic LDS: ray tables a_u[W], b_v[H] (padded to 4), then per wave: gate slots [max_gates][24] and an
+// 8-row depth staging band [8][W].
+#ifdef CAM_WAVES_PER_EU
+#define CAM_ATTR __attribute__((amdgpu_waves_per_eu(CAM_WAVES_PER_EU, CAM_WAVES_PER_EU)))
+#else
+#define CAM_ATTR
+#endif
+__global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs a) {
+  extern __shared__ float4 smem4[];
+  float* smem = reinterpret_cast<float*>(smem4);
   const gr_cam_const* __restrict__ cc = a.cc;
-  const int W = cc->width, npix = cc->npix;
+  const int W = a.width, H = a.height, npix = W * H, G = a.max_gates;
+  const int wpad = (W + 3) & ~3, hpad = (H + 3) & ~3;
+  float* s_ray_a = smem;
+  float* s_ray_b = smem + wpad;
   for (int k = threadIdx.x; k < W; k += CAM_WAVES * 64) s_ray_a[k] = cc->ray_a[k];
-  for (int k = threadIdx.x; k < cc->height; k += CAM_WAVES * 64) s_ray_b[k] = cc->ray_b[k];
+  for (int k = threadIdx.x; k < H; k += CAM_WAVES * 64) s_ray_b[k] = cc->ray_b[k];
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int i = blockIdx.x * CAM_WAVES + w;
   const bool active = i < a.num_envs;
   const int N = a.num_envs;
+  float* wave_lds = smem + wpad + hpad + w * (G * GR_CAM_SLOT + 8 * W);
+  float4* s_slot = reinterpret_cast<float4*>(wave_lds);                    // [G][CAM_SLOT4]
+  float4* s_stage = reinterpret_cast<float4*>(wave_lds + G * GR_CAM_SLOT);  // [8 * W / 4]
 
   // ---- is the sensor outdated? (SensorBase.update / reset; wave-uniform)
-  int render = 0, age_new = 0;
+  int render = 0;
   if (active) {
     const int age = a.age[i];
     int outdated = age < 0;
@@ -51,8 +95,7 @@ __global__ __launch_bounds__(CAM_WAVES * 64) void camera_kernel(CamArgs a) {
       outdated = outdated || a.mask == nullptr || a.mask[i] != 0;
     }
     render = __builtin_amdgcn_readfirstlane(outdated);
-    age_new = render ? 0 : aged;
-    if (lane == 0) a.age[i] = age_new;
+    if (lane == 0) a.age[i] = render ? 0 : aged;
   }
 
   // ---- camera pose and the gate slots of this env's track
@@ -68,7 +111,7 @@ __global__ __launch_bounds__(CAM_WAVES * 64) void camera_kernel(CamArgs a) {
     const int packed = a.istate[4 * i + GR_I_PACKED];
     const int track = ((packed >> 24) & 0xff) * a.num_levels + ((packed >> 8) & 0xff);
     const float* tb = a.table + (size_t)track * a.track_stride;
-    const float* rec = tb + a.max_gates * GR_GATE_FLOATS;
+    const float* rec = tb + G * GR_GATE_FLOATS;
     gz = rec[0];
     const int ng = (int)rec[3];
     float s[GR_CAM_SLOT];
@@ -78,83 +121,98 @@ __global__ __launch_bounds__(CAM_WAVES * 64) void camera_kernel(CamArgs a) {
       valid = s[GR_CS_VALID] != 0.0f;
 #pragma unroll
       for (int k = 0; k < CAM_SLOT4; ++k)
-        s_slot[w][lane][k] = make_float4(s[4 * k], s[4 * k + 1], s[4 * k + 2], s[4 * k + 3]);
+        s_slot[lane * CAM_SLOT4 + k] = make_float4(s[4 * k], s[4 * k + 1], s[4 * k + 2], s[4 * k + 3]);
     }
     valid_mask = __ballot(valid);
   }
   __syncthreads();
+  if (!active) return;
 
-  // ---- pixels
+  // ---- the 16 state terms of both rows
   const uint32_t gid = (uint32_t)(a.env_id_offset + i);
   const uint32_t cnt = a.counters[a.counter_index];
   const size_t row = (size_t)(16 + npix);
-  if (active) {
-    if (lane < 4) {
-      const float4 sp = reinterpret_cast<const float4*>(a.obs_p16)[4 * i + lane];
-      const float4 sc = reinterpret_cast<const float4*>(a.obs_c16)[4 * i + lane];
-      reinterpret_cast<float4*>(a.out_p + i * row)[lane] = sp;
-      reinterpret_cast<float4*>(a.out_c + i * row)[lane] = sc;
-    }
-    const float maxd = cc->max_distance, scale = cc->obs_scale, inv_scale = cc->inv_obs_scale;
-    const float nstd = cc->noise_std;
-    const int noise = cc->add_noise, H = cc->height;
-    // 8-row x 32-column tiles: a lane owns one pixel quad (row lane/8, columns 4*(lane%8)..+3), so a
-    // gate's screen window culls whole tiles and each store writes 8 full 128-byte row segments
-    const int tiles_x = (W + 31) >> 5, ntiles = tiles_x * ((H + 7) >> 3);
-    for (int t = 0; t < ntiles; ++t) {
-      const int ty = t / tiles_x, tx = t - ty * tiles_x;
-      const int v = ty * 8 + (lane >> 3), u0 = tx * 32 + 4 * (lane & 7);
-      if (v >= H || u0 >= W) continue;
-      const int k0 = v * W + u0;
-      float d[4];
-      if (render) {
-        const float b = s_ray_b[v];
-        const float4 a4 = *reinterpret_cast<const float4*>(&s_ray_a[u0]);
-        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+  if (lane < 4) {
+    const float4 sp = reinterpret_cast<const float4*>(a.obs_p16)[4 * i + lane];
+    const float4 sc = reinterpret_cast<const float4*>(a.obs_c16)[4 * i + lane];
+    reinterpret_cast<float4*>(a.out_p + i * row)[lane] = sp;
+    reinterpret_cast<float4*>(a.out_c + i * row)[lane] = sc;
+  }
+  float4* op4 = reinterpret_cast<float4*>(a.out_p + i * row + 16);
+  float4* oc4 = reinterpret_cast<float4*>(a.out_c + i * row + 16);
+  float4* dep4 = reinterpret_cast<float4*>(a.depth + (size_t)i * npix);
+  const int nq = npix >> 2;
+
+  if (!render) {
+    // ---- sensor up to date: stream the depth buffer into both rows, CAM_BATCH loads in flight per lane
+    for (int q0 = 0; q0 < nq; q0 += 64 * CAM_BATCH) {
+      float4 dd[CAM_BATCH];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float dz = gr_fmaf(b, c2[2], gr_fmaf(av[j], c1[2], c0[2]));
-          d[j] = gr_cam_ground_hit(o[2], gz, dz);
-        }
-        uint64_t m = valid_mask;
-        while (m) {
-          const int g = __builtin_ctzll(m);
-          m &= m - 1;
-          float s[GR_CAM_SLOT];
-#pragma unroll
-          for (int k = 0; k < CAM_SLOT4; ++k) {
-            const float4 q4 = s_slot[w][g][k];
-            s[4 * k] = q4.x; s[4 * k + 1] = q4.y; s[4 * k + 2] = q4.z; s[4 * k + 3] = q4.w;
-          }
-          if (b >= s[GR_CS_BMIN] && b <= s[GR_CS_BMAX] && av[3] <= s[GR_CS_AMAX] && av[0] >= s[GR_CS_AMIN]) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (av[j] >= s[GR_CS_AMIN] && av[j] <= s[GR_CS_AMAX]) d[j] = gr_minf(d[j], gr_cam_gate_hit(s, av[j], b));
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) d[j] = gr_cam_clip(d[j], maxd);
-        reinterpret_cast<float4*>(a.depth + (size_t)i * npix)[k0 >> 2] = make_float4(d[0], d[1], d[2], d[3]);
-      } else {
-        const float4 q4 = reinterpret_cast<const float4*>(a.depth + (size_t)i * npix)[k0 >> 2];
-        d[0] = q4.x; d[1] = q4.y; d[2] = q4.z; d[3] = q4.w;
+      for (int j = 0; j < CAM_BATCH; ++j) {
+        const int q = q0 + 64 * j + lane;
+        dd[j] = q < nq ? dep4[q] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
       }
-      float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (noise) gr_cam_noise4(gid, cnt, (uint32_t)(k0 >> 2), a.seed_lo, a.seed_hi, z);
-      float4 op, oc;
-      op.x = gr_cam_obs(d[0], z[0], nstd, scale, inv_scale); oc.x = gr_cam_obs_clean(d[0], scale, inv_scale);
-      op.y = gr_cam_obs(d[1], z[1], nstd, scale, inv_scale); oc.y = gr_cam_obs_clean(d[1], scale, inv_scale);
-      op.z = gr_cam_obs(d[2], z[2], nstd, scale, inv_scale); oc.z = gr_cam_obs_clean(d[2], scale, inv_scale);
-      op.w = gr_cam_obs(d[3], z[3], nstd, scale, inv_scale); oc.w = gr_cam_obs_clean(d[3], scale, inv_scale);
-      reinterpret_cast<float4*>(a.out_p + i * row + 16)[k0 >> 2] = op;
-      reinterpret_cast<float4*>(a.out_c + i * row + 16)[k0 >> 2] = oc;
+#pragma unroll
+      for (int j = 0; j < CAM_BATCH; ++j) {
+        const int q = q0 + 64 * j + lane;
+        if (q < nq) emit_quad(a, cc, op4, oc4, q, dd[j], gid, cnt);
+      }
     }
+    return;
+  }
+
+  // ---- render: bands of 8 image rows.  Rays are cast in 8x32 tiles (a lane owns a quad of one tile
+  // row), so a gate's screen window culls whole tiles; the band is staged in LDS and written out in
+  // row-major order (full, contiguous 1 KB stores per wave instruction).
+  const float maxd = cc->max_distance;
+  for (int v0 = 0; v0 < H; v0 += 8) {
+    const int rows = H - v0 < 8 ? H - v0 : 8;
+    for (int u_t = 0; u_t < W; u_t += 32) {
+      const int v = v0 + (lane >> 3), u0 = u_t + 4 * (lane & 7);
+      if (v >= H || u0 >= W) continue;
+      const float b = s_ray_b[v];
+      const float4 a4 = *reinterpret_cast<const float4*>(&s_ray_a[u0]);
+      const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+      float d[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float dz = gr_fmaf(b, c2[2], gr_fmaf(av[j], c1[2], c0[2]));
+        d[j] = gr_cam_ground_hit(o[2], gz, dz);
+      }
+      uint64_t m = valid_mask;
+      while (m) {
+        const int g = __builtin_ctzll(m);
+        m &= m - 1;
+        float s[GR_CAM_SLOT];
+#pragma unroll
+        for (int k = 0; k < CAM_SLOT4; ++k) {
+          const float4 q4 = s_slot[g * CAM_SLOT4 + k];
+          s[4 * k] = q4.x; s[4 * k + 1] = q4.y; s[4 * k + 2] = q4.z; s[4 * k + 3] = q4.w;
+        }
+        if (b >= s[GR_CS_BMIN] && b <= s[GR_CS_BMAX] && av[3] <= s[GR_CS_AMAX] && av[0] >= s[GR_CS_AMIN]) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (av[j] >= s[GR_CS_AMIN] && av[j] <= s[GR_CS_AMAX]) d[j] = gr_minf(d[j], gr_cam_gate_hit(s, av[j], b));
+        }
+      }
+      s_stage[((v - v0) * W + u0) >> 2] =
+          make_float4(gr_cam_clip(d[0], maxd), gr_cam_clip(d[1], maxd), gr_cam_clip(d[2], maxd), gr_cam_clip(d[3], maxd));
+    }
+    wave_lds_sync();
+    const int qb = (v0 * W) >> 2, nqb = (rows * W) >> 2;
+    for (int qq = lane; qq < nqb; qq += 64) {
+      const float4 d4 = s_stage[qq];
+      nt_store4(dep4 + qb + qq, d4);
+      emit_quad(a, cc, op4, oc4, qb + qq, d4, gid, cnt);
+    }
+    wave_lds_sync();
   }
 }
 
 hipError_t launch_camera(const CamArgs& a, hipStream_t s) {
   const int blocks = (a.num_envs + CAM_WAVES - 1) / CAM_WAVES;
-  hipLaunchKernelGGL(camera_kernel, dim3(blocks), dim3(CAM_WAVES * 64), 0, s, a);
+  hipLaunchKernelGGL(camera_kernel, dim3(blocks), dim3(CAM_WAVES * 64), camera_lds_bytes(a.width, a.height, a.max_gates),
+                     s, a);
   return hipGetLastError();
 }
 

@@ -501,6 +501,8 @@ int gr_camera_render(gr_ctx* c, int mode, const uint8_t* mask, void* stream) {
   a.num_envs = c->cfg.num_envs;
   a.env_id_offset = c->cfg.env_id_offset;
   a.mode = mode;
+  a.width = c->cam_k.width;
+  a.height = c->cam_k.height;
   a.seed_lo = c->cfg.seed_lo;
   a.seed_hi = c->cfg.seed_hi;
   a.depth = c->cam_buf.depth;

@@ -67,7 +67,7 @@ struct CamArgs {
   const uint32_t* counters;
   int counter_index;
   const float* table;  // packed track table
-  int track_stride, num_levels, max_gates, num_envs, env_id_offset, mode;
+  int track_stride, num_levels, max_gates, num_envs, env_id_offset, mode, width, height;
   uint32_t seed_lo, seed_hi;
   float* depth;
   int32_t* age;
@@ -75,6 +75,11 @@ struct CamArgs {
   float* out_c;
 };
 hipError_t launch_camera(const CamArgs& a, hipStream_t s);
+// dynamic LDS of the camera kernel: ray tables + per wave (gate slots + an 8-row staging band)
+inline size_t camera_lds_bytes(int width, int height, int max_gates) {
+  const size_t wpad = (size_t)((width + 3) & ~3), hpad = (size_t)((height + 3) & ~3);
+  return 4 * (wpad + hpad + 4 * ((size_t)max_gates * 24 + 8 * (size_t)width));
+}
 
 hipError_t launch_env(int mode, const KArgs& a, const float* actions, const uint8_t* mask, hipStream_t s,
                       hipEvent_t t0, hipEvent_t t1);

@@ -53,4 +53,15 @@ register(
     env_cfg_entry_point="generalizableracing_amd.envs.racing_cfg:RacingEnvCfg",
     rsl_rl_cfg_entry_point="generalizableracing_amd.rsl_rl.config:QuadcopterPPORunnerCfg",
     rsl_rl_l2c2_cfg_entry_point="generalizableracing_amd.rsl_rl.config:QuadcopterL2C2PPORunnerCfg",
+    env_cfg_vision_entry_point="generalizableracing_amd.envs.racing_cfg:RacingVisionEnvCfg",
+    rsl_rl_vision_cfg_entry_point="generalizableracing_amd.rsl_rl.config:QuadcopterVisionPPORunnerCfg",
+)
+
+# the reference's registration of the id above, with the front depth camera and the
+# VisionActorCritic + PPOL2C2 recipe (quadcopter_diff/__init__.py:50-62)
+register(
+    "DiffLab-Quadcopter-CTBR-Racing-Vision-v0",
+    entry_point="generalizableracing_amd.envs.racing_env:RacingEnv",
+    env_cfg_entry_point="generalizableracing_amd.envs.racing_cfg:RacingVisionEnvCfg",
+    rsl_rl_cfg_entry_point="generalizableracing_amd.rsl_rl.config:QuadcopterVisionPPORunnerCfg",
 )

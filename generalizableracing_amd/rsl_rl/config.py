@@ -67,3 +67,26 @@ class QuadcopterL2C2PPORunnerCfg(QuadcopterPPORunnerCfg):
     experiment_name: str = "racing_ppo_l2c2"
     algorithm: RslRlPpoAlgorithmCfg = field(
         default_factory=lambda: RslRlPpoAlgorithmCfg(class_name="PPOL2C2", entropy_coef=0.005))
+
+
+@dataclass
+class RslRlPpoVisionActorCriticCfg(RslRlPpoActorCriticCfg):
+    """rsl_rl_ppo_cfg.py:43-52."""
+
+    class_name: str = "VisionActorCritic"
+    img_res: tuple = (72, 96)
+    dim_hidden_input: int = 192
+    actor_hidden_dims: list = field(default_factory=lambda: [128, 128])
+    critic_hidden_dims: list = field(default_factory=lambda: [128, 128])
+    use_auxiliary_loss: bool = True  # policy.__setattr__("use_auxiliary_loss", True), :104
+
+
+@dataclass
+class QuadcopterVisionPPORunnerCfg(QuadcopterPPORunnerCfg):
+    """The reference's registered racing recipe (rsl_rl_ppo_cfg.py:80-104): VisionActorCritic + PPOL2C2."""
+
+    max_iterations: int = 4000
+    experiment_name: str = "racing_ppo_l2c2_vision"
+    policy: RslRlPpoActorCriticCfg = field(default_factory=RslRlPpoVisionActorCriticCfg)
+    algorithm: RslRlPpoAlgorithmCfg = field(
+        default_factory=lambda: RslRlPpoAlgorithmCfg(class_name="PPOL2C2", entropy_coef=0.005))

@@ -21,9 +21,10 @@ from . import distributed as gdist
 from .actor_critic import ActorCritic, EmpiricalNormalization
 from .ppo import PPO
 from .ppo_l2c2 import PPOL2C2
+from .vision_actor_critic import VisionActorCritic
 
 ALGORITHMS = {"PPO": PPO, "PPOL2C2": PPOL2C2}
-POLICIES = {"ActorCritic": ActorCritic}
+POLICIES = {"ActorCritic": ActorCritic, "VisionActorCritic": VisionActorCritic}
 
 
 class _CsvWriter:

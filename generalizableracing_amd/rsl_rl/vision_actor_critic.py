@@ -1,0 +1,184 @@
+"""VisionActorCritic — the reference's depth-image policy
+(standalone/rsl_rl/ext/modules/vision_actor_critic.py:43-144), used by the registered racing recipe
+(quadcopter_diff/agents/rsl_rl_ppo_cfg.py:43-52,80-104: img_res (72, 96), dim_hidden_input 192,
+128x128 heads, lrelu, PPOL2C2).
+
+Observation rows are [state | H*W depth image] (racing_ctbr_env.py:141-160).  The image goes
+through a strided conv stem (Conv 3x3/3 -> BN -> act, 3x3/3, 2x2/2, flatten, linear), the state
+through one linear layer; their sum, activated, feeds the actor and critic MLPs.  Module names and
+order match the reference so its checkpoints load as-is.  Convs / GEMMs run on MIOpen / hipBLASLt
+through torch.
+
+MI355X path: every stem convolution has stride == kernel and no padding, i.e. it convolves
+non-overlapping patches.  `features()` therefore evaluates the stem as three patch GEMMs on
+channels-last activations (hipBLASLt) instead of MIOpen direct convolutions, with the BatchNorm
+statistics taken over the same (batch, height, width) set and the flatten order of the reference
+(NCHW) kept by permuting the final Linear's columns.  The nn.Conv2d / nn.BatchNorm2d modules hold
+the parameters and running statistics exactly as the reference's, so checkpoints are interchangeable;
+`stem(img)` still runs the reference module as written (tests compare the two).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .actor_critic import ActorCritic, resolve_nn_activation
+
+
+def _conv_out(n: int, k: int, s: int) -> int:
+    return (n - k) // s + 1
+
+
+class _PatchGemm(torch.autograd.Function):
+    """y = x @ w^T for tall-skinny x [M, K] (M = batch * patches, millions) and a small w [N, K].
+
+    The weight gradient w^T-shaped [N, K] = dy^T x reduces over all M rows; as one GEMM hipBLASLt
+    tiles only its tiny N x K output (one or a few workgroups stream millions of rows).  Here it is
+    split over M into chunks of SPLIT rows (a batched GEMM, one workgroup set per chunk) and the
+    partial products are summed."""
+
+    SPLIT = 8192
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return x @ w.t()
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gx = gy @ w if ctx.needs_input_grad[0] else None
+        gw = None
+        if ctx.needs_input_grad[1]:
+            m, c = x.shape[0], _PatchGemm.SPLIT
+            s = m // c
+            if s >= 2:
+                gw = torch.bmm(gy[: s * c].view(s, c, -1).transpose(1, 2), x[: s * c].view(s, c, -1)).sum(0)
+                if m > s * c:
+                    gw = gw + gy[s * c:].t() @ x[s * c:]
+            else:
+                gw = gy.t() @ x
+        return gx, gw
+
+
+def _gemm(x, w):
+    return _PatchGemm.apply(x, w) if torch.is_grad_enabled() else x @ w.t()
+
+
+class VisionActorCritic(ActorCritic):
+    is_recurrent = False
+
+    def __init__(self, num_actor_obs: int, num_critic_obs: int, num_actions: int, img_res=(72, 96),
+                 dim_hidden_input: int = 192, actor_hidden_dims=(256, 256, 256), critic_hidden_dims=(256, 256, 256),
+                 activation="elu", init_noise_std=1.0, noise_std_type: str = "scalar", **kwargs):
+        self.use_auxiliary_loss = bool(kwargs.pop("use_auxiliary_loss", False))
+        super().__init__(dim_hidden_input, dim_hidden_input, num_actions, actor_hidden_dims=actor_hidden_dims,
+                         critic_hidden_dims=critic_hidden_dims, activation=activation,
+                         init_noise_std=init_noise_std, noise_std_type=noise_std_type, **kwargs)
+        self.activation = resolve_nn_activation(activation)
+        self.img_res = tuple(int(x) for x in img_res)
+        h, w = self.img_res
+        h1, w1 = _conv_out(h, 3, 3), _conv_out(w, 3, 3)
+        h2, w2 = _conv_out(h1, 3, 3), _conv_out(w1, 3, 3)
+        h3, w3 = _conv_out(h2, 2, 2), _conv_out(w2, 2, 2)
+        if min(h3, w3) <= 0:
+            raise ValueError(f"image {self.img_res} too small for the conv stem")
+        self.stem = nn.Sequential(
+            nn.Conv2d(1, 16, 3, 3, bias=False),
+            nn.BatchNorm2d(16),
+            self.activation,
+            nn.Conv2d(16, 32, 3, 3, bias=False),
+            nn.BatchNorm2d(32),
+            self.activation,
+            nn.Conv2d(32, 64, 2, 2, bias=False),
+            nn.BatchNorm2d(64),
+            self.activation,
+            nn.Flatten(),
+            nn.Linear(64 * h3 * w3, dim_hidden_input),  # 1280 at 72x96
+        )
+        self._dims = (h1, w1, h2, w2, h3, w3)
+        self._pidx = None
+        self.num_pixels = h * w
+        if num_actor_obs <= self.num_pixels:
+            raise ValueError(f"num_actor_obs {num_actor_obs} must exceed the image size {self.num_pixels}")
+        self.state_enc = nn.Linear(num_actor_obs - self.num_pixels, dim_hidden_input)
+        if self.use_auxiliary_loss:
+            self.aux_decoder = nn.Linear(dim_hidden_input, 1)
+
+    @staticmethod
+    def _bn(bn: nn.BatchNorm2d, x: torch.Tensor) -> torch.Tensor:
+        """nn.BatchNorm2d.forward on channels-last rows [M, C] (M = batch*height*width)."""
+        momentum = 0.0 if bn.momentum is None else bn.momentum
+        if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
+            bn.num_batches_tracked.add_(1)
+            if bn.momentum is None:
+                momentum = 1.0 / float(bn.num_batches_tracked)
+        use_batch = bn.training or (bn.running_mean is None and bn.running_var is None)
+        return F.batch_norm(x, bn.running_mean if not bn.training or bn.track_running_stats else None,
+                            bn.running_var if not bn.training or bn.track_running_stats else None,
+                            bn.weight, bn.bias, use_batch, momentum, bn.eps)
+
+    def _patch_index(self, device):
+        """Pixel indices of conv1's patches, rows ordered so that every later layer's input is a VIEW of
+        the previous layer's output: conv1 rows feeding conv2 come grouped as conv2's 3x3 patches,
+        those grouped as conv3's 2x2 patches; positions a later conv does not cover (conv1 columns
+        30-31 at 72x96) follow at the end — they still enter the BatchNorm statistics."""
+        if getattr(self, "_pidx", None) is not None and self._pidx[0].device == torch.device(device):
+            return self._pidx
+        h, w = self.img_res
+        h1, w1, h2, w2, h3, w3 = self._dims
+        g3 = [(2 * v3 + i, 2 * u3 + j) for v3 in range(h3) for u3 in range(w3) for i in range(2) for j in range(2)]
+        s3 = set(g3)
+        g2 = g3 + [(v, u) for v in range(h2) for u in range(w2) if (v, u) not in s3]
+        l1 = [(3 * v2 + i, 3 * u2 + j) for v2, u2 in g2 for i in range(3) for j in range(3)]
+        s1 = set(l1)
+        l1_left = [(v, u) for v in range(h1) for u in range(w1) if (v, u) not in s1]
+
+        def pix(cells):
+            return torch.tensor([(3 * v + i) * w + 3 * u + j for v, u in cells for i in range(3) for j in range(3)],
+                                dtype=torch.long, device=device)
+
+        self._pidx = (pix(l1), pix(l1_left), len(l1), len(l1_left), len(g3), len(g2))
+        return self._pidx
+
+    def stem_gemm(self, img: torch.Tensor) -> torch.Tensor:
+        """The conv stem as patch GEMMs (identical math to self.stem(img), other summation order)."""
+        conv1, bn1, act, conv2, bn2, _, conv3, bn3, _, _, lin = self.stem
+        h1, w1, h2, w2, h3, w3 = self._dims
+        B = img.shape[0]
+        flat = img.reshape(B, -1)
+        idx, idx_left, n1, n1_left, n3, n2 = self._patch_index(img.device)
+        x = flat.index_select(1, idx).view(B * n1, 9)
+        if n1_left:
+            x = torch.cat([x, flat.index_select(1, idx_left).view(B * n1_left, 9)])
+        y = act(self._bn(bn1, _gemm(x, conv1.weight.reshape(16, 9))))
+        x = y[: B * n1].view(B * n2, 144)  # conv2's 3x3 patches (i, j, c): a view
+        y = act(self._bn(bn2, _gemm(x, conv2.weight.permute(0, 2, 3, 1).reshape(32, 144))))
+        x = y.view(B, n2, 32)[:, :n3].reshape(B * h3 * w3, 128)  # conv3's 2x2 patches: a view at 72x96
+        y = act(self._bn(bn3, _gemm(x, conv3.weight.permute(0, 2, 3, 1).reshape(64, 128)))).view(B, h3 * w3 * 64)
+        # reference flatten is NCHW (c, h, w): permute the Linear's columns to (h, w, c) instead
+        wl = lin.weight.view(-1, 64, h3, w3).permute(0, 2, 3, 1).reshape(lin.weight.shape[0], -1)
+        return _gemm(y, wl) + lin.bias
+
+    def features(self, observations: torch.Tensor) -> torch.Tensor:
+        """act(stem(image) + state_enc(state)), vision_actor_critic.py:119-122."""
+        img = observations[:, -self.num_pixels:].reshape(-1, 1, *self.img_res)
+        state = observations[:, :-self.num_pixels]
+        return self.activation(self.stem_gemm(img) + self.state_enc(state))
+
+    def update_distribution(self, observations):
+        mean = self.actor(self.features(observations))
+        self.distribution = torch.distributions.Normal(mean, self._std(mean))
+
+    def act(self, observations, **kwargs):
+        self.update_distribution(observations)
+        return self.distribution.sample()
+
+    def act_inference(self, observations):
+        """-> (mean, feature), as the reference (its exporters and PPOL2C2 take [0])."""
+        feat = self.features(observations)
+        return self.actor(feat), feat
+
+    def evaluate(self, critic_observations, **kwargs):
+        return self.critic(self.features(critic_observations))

@@ -10,12 +10,14 @@ import numpy as np
 import torch
 
 import oracle
-from generalizableracing_amd.envs.racing_cfg import RacingEnvCfg, SceneCfg, SimCfg, TerrainCfg
+from generalizableracing_amd import _abi
+from generalizableracing_amd.envs.racing_cfg import CameraCfg, RacingEnvCfg, SceneCfg, SimCfg, TerrainCfg
 from generalizableracing_amd.envs.tracks import build_track_table
 
 
 class OracleVecEnv:
-    def __init__(self, num_envs=64, stage=1, env_id_offset=0, track_seed_offset=0, seed=42, types=4, levels=10):
+    def __init__(self, num_envs=64, stage=1, env_id_offset=0, track_seed_offset=0, seed=42, types=4, levels=10,
+                 camera: CameraCfg | None = None):
         self.cfg = RacingEnvCfg(scene=SceneCfg(num_envs=num_envs), sim=SimCfg(device="cpu"), stage=stage,
                                 terrain=TerrainCfg(num_cols=types, num_rows=levels), seed=seed,
                                 env_id_offset=env_id_offset, track_seed_offset=track_seed_offset)
@@ -23,11 +25,15 @@ class OracleVecEnv:
         gates, recs = build_track_table(num_types=types, num_levels=levels, num_gates=8, seed=42 + track_seed_offset)
         self.orc = oracle.Oracle(c, gates, recs)
         self.orc.init()
+        self.camera = camera
+        if camera is not None:
+            self.orc.enable_camera(camera.to_gr())
         self.orc.reset(None)
+        self._cam(_abi.GR_CAM_RESET)
         self.num_envs = num_envs
         self.num_actions = 4
-        self.num_obs = 16
-        self.num_privileged_obs = 16
+        self.num_obs = 16 + (camera.num_pixels if camera is not None else 0)
+        self.num_privileged_obs = self.num_obs
         self.max_episode_length = self.cfg.max_episode_length
         self.device = "cpu"
         self.render_mode = None
@@ -44,23 +50,32 @@ class OracleVecEnv:
     def episode_length_buf(self, value: torch.Tensor):
         self.orc.envs["ep_len"] = value.cpu().numpy().astype(np.int32)
 
+    def _cam(self, mode):
+        if self.camera is not None:
+            self.orc.camera(mode)
+
     def _obs(self):
-        return {"policy": torch.from_numpy(self.orc.obs_policy.copy()),
-                "critic": torch.from_numpy(self.orc.obs_critic.copy()),
+        pol, cri = ((self.orc.img_policy, self.orc.img_critic) if self.camera is not None
+                    else (self.orc.obs_policy, self.orc.obs_critic))
+        return {"policy": torch.from_numpy(pol.copy()),
+                "critic": torch.from_numpy(cri.copy()),
                 "auxiliary": torch.from_numpy(self.orc.obs_aux.copy()).unsqueeze(1)}
 
     def get_observations(self):
         self.orc.observe()
+        self._cam(_abi.GR_CAM_OBSERVE)
         o = self._obs()
         return o["policy"], {"observations": o}
 
     def reset(self):
         self.orc.reset(None)
+        self._cam(_abi.GR_CAM_RESET)
         o = self._obs()
         return o["policy"], {"observations": o}
 
     def step(self, actions: torch.Tensor):
         self.orc.step(actions.detach().cpu().numpy().astype(np.float32))
+        self._cam(_abi.GR_CAM_STEP)
         o = self._obs()
         extras = {"observations": o, "time_outs": torch.from_numpy(self.orc.time_out.astype(bool)),
                   "log": {"Episode_Termination/time_out": float(self.orc.log[12])}}
