@@ -268,6 +268,17 @@ def main():
     env.close()
     if not a.no_extras:
         extra["train_total_fps_4096_envs"] = train_fps(device)
+        # the depth camera of the vision task (separate kernel, same env shard size)
+        sys.path.insert(0, os.path.join(ROOT, "scripts"))
+        import bench_camera
+
+        cam = bench_camera.run(n, steps=24, warmup=4, device=device)
+        extra["vision_camera"] = {
+            "kernel": cam["kernel"], "image": cam["image"], "render_fraction": cam["render_fraction"],
+            "ms_per_call": cam["ms_avg_call"], "ms_render_call": cam["ms_render_call"],
+            "ms_reuse_call": cam["ms_reuse_call"], "achieved_GBps": cam["gbs_avg"], "peak_GBps": HBM_PEAK_GBS,
+            "frac": cam["hbm_frac_avg"], "bytes_per_env_call": [cam["bytes_per_env_render"], cam["bytes_per_env_reuse"]],
+            "env_steps_per_s_step_plus_camera": cam["wall_env_steps_per_s_step_plus_camera"]}
     cpu = None
     if rank == 0 and ws == 1 and not a.no_extras:
         cpu = cpu_baseline(a.cpu_seconds)

@@ -27,22 +27,15 @@ from generalizableracing_amd.envs.racing_env import RacingEnv  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
-def main(argv=None):
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--envs", type=int, default=65536)
-    ap.add_argument("--steps", type=int, default=40)
-    ap.add_argument("--warmup", type=int, default=6)
-    ap.add_argument("--no-noise", action="store_true", help="ablation: policy image without noise")
-    ap.add_argument("--period", type=float, default=None, help="camera update_period override (0: every step)")
-    args = ap.parse_args(argv)
-    n = args.envs
+def run(n=65536, steps=40, warmup=6, no_noise=False, period=None, device="cuda:0") -> dict:
+    args = argparse.Namespace(envs=n, steps=steps, warmup=warmup, no_noise=no_noise, period=period)
     cam = CameraCfg(add_noise=not args.no_noise)
     if args.period is not None:
         cam.update_period = args.period
-    env = RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device="cuda:0"), camera=cam))
+    env = RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=device), camera=cam))
     env.reset()
-    g = torch.Generator(device="cuda:0").manual_seed(1234)
-    acts = [torch.randn(n, 4, device="cuda:0", generator=g) for _ in range(8)]
+    g = torch.Generator(device=device).manual_seed(1234)
+    acts = [torch.randn(n, 4, device=device, generator=g) for _ in range(8)]
     rb, ub = C.c_int64(), C.c_int64()
     env._call("gr_camera_bytes_per_env", C.byref(rb), C.byref(ub))
     for k in range(args.warmup):
@@ -82,8 +75,19 @@ def main(argv=None):
         "camera_env_steps_per_s": n / (avg(ms) * 1e-3),
         "wall_env_steps_per_s_step_plus_camera": n * args.steps / wall,
     }
-    print(json.dumps(out))
     env.close()
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=6)
+    ap.add_argument("--no-noise", action="store_true", help="ablation: policy image without noise")
+    ap.add_argument("--period", type=float, default=None, help="camera update_period override (0: every step)")
+    a = ap.parse_args(argv)
+    print(json.dumps(run(a.envs, a.steps, a.warmup, a.no_noise, a.period)))
 
 
 if __name__ == "__main__":
