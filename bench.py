@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=64)
     p.add_argument("--num-envs", type=int, default=65536)
     p.add_argument("--gates", type=int, default=8)
+    p.add_argument("--obstacles", type=int, default=1, help="1: the reference task's walls / orbits / ground "
+                   "obstacles (add_obs, add_ground_obs); 0: gates and ground only")
     p.add_argument("--integrator", default="dd_explicit")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="skip policy/train/cpu legs (profiling runs)")
@@ -70,9 +72,10 @@ def max_over_ranks(x: float, device) -> float:
     return float(t.item())
 
 
-def make_env(n, rank, device, gates, integrator):
+def make_env(n, rank, device, gates, integrator, obstacles=True):
     cfg = RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=device), stage=1, integrator=integrator,
-                       terrain=TerrainCfg(num_gates=gates), env_id_offset=rank * n, track_seed_offset=rank)
+                       terrain=TerrainCfg(num_gates=gates, obstacles=obstacles), env_id_offset=rank * n,
+                       track_seed_offset=rank)
     env = RacingEnv(cfg)
     env.reset()
     g = torch.Generator(device="cpu").manual_seed(1234 + rank)
@@ -195,17 +198,17 @@ def train_fps(device, n=4096, iters=3):
     return float(np.median(fps))
 
 
-def cpu_baseline(seconds: float, n: int = 65536):
+def cpu_baseline(seconds: float, n: int = 65536, obstacles: bool = True):
     """The CPU oracle (C restatement of the reference step, OpenMP over envs) on a bounded sample
     of the same workload: n envs stepped for about `seconds`."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
 
-    from generalizableracing_amd.envs.tracks import build_track_table
+    from generalizableracing_amd.envs.tracks import build_tracks
 
     cfg = RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device="cpu"), stage=1).to_gr_config()
-    gates, recs = build_track_table()
-    orc = oracle.Oracle(cfg, gates, recs)
+    gates, recs, ot = build_tracks(obstacles=obstacles)
+    orc = oracle.Oracle(cfg, gates, recs, None if ot is None else ot.records, None if ot is None else ot.counts)
     orc.init()
     orc.reset(None)
     rng = np.random.default_rng(0)
@@ -223,13 +226,13 @@ def cpu_baseline(seconds: float, n: int = 65536):
                       f"run here (SURVEY §8d)"}
 
 
-def load_traffic(n, gates):
+def load_traffic(n, gates, obstacles):
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     try:
         d = json.load(open(path))
-        if d.get("num_envs") == n and d.get("gates", 8) == gates:
+        if d.get("num_envs") == n and d.get("gates", 8) == gates and d.get("obstacles", 0) == obstacles:
             return d.get("bytes_per_launch")
     except Exception:
         return None
@@ -248,7 +251,7 @@ def main():
         dist.init_process_group(a.dist_backend, rank=rank, world_size=ws)
     device = f"cuda:{local}"
     n = a.num_envs
-    env = make_env(n, rank, device, a.gates, a.integrator)
+    env = make_env(n, rank, device, a.gates, a.integrator, bool(a.obstacles))
     g = torch.Generator(device=device).manual_seed(1234 + rank)
     actions = torch.randn(ACTION_RING, n, 4, device=device, generator=g)
     for k in range(a.warmup):
@@ -281,8 +284,8 @@ def main():
             "env_steps_per_s_step_plus_camera": cam["wall_env_steps_per_s_step_plus_camera"]}
     cpu = None
     if rank == 0 and ws == 1 and not a.no_extras:
-        cpu = cpu_baseline(a.cpu_seconds)
-    traffic = load_traffic(n, a.gates)
+        cpu = cpu_baseline(a.cpu_seconds, obstacles=bool(a.obstacles))
+    traffic = load_traffic(n, a.gates, a.obstacles)
     if rank == 0:
         line = {
             "metric": "env-steps/sec whole-node @65536 envs/GPU; 1/2/4/8-GPU scaling",
@@ -298,7 +301,8 @@ def main():
             "dtype": "f32",
             "data": "synthetic: procedural zigzag/circular/ellipse tracks (20 types x 10 levels), "
                     "N(0,1) pre-tanh actions resident in HBM",
-            "config": {"workload": f"racing env step, {n} envs/GPU, TRAINING_STAGE=1, {a.gates}-gate tracks, "
+            "config": {"workload": f"racing env step, {n} envs/GPU, TRAINING_STAGE=1, {a.gates}-gate tracks"
+                                   f"{' with walls/orbits/ground obstacles' if a.obstacles else ', no obstacles'}, "
                                    f"{a.integrator} integrator (BASELINE config C3/C4)",
                        "num_envs_per_gpu": n, "launch": mode, "parallelism": f"env-shard x{ws}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -20,11 +20,12 @@ GR_INTEGRATOR_DD_EXPLICIT = 0
 GR_INTEGRATOR_SEMI_IMPLICIT = 1
 
 P_POSQ, P_QV, P_VW, P_WA, P_CTRL, P_LAG, P_RST0, P_RST1, P_EP0, P_EP1, P_PAR0, P_PAR1, P_PAR2, P_PAR3, P_MOTOR = range(15)
-NUM_PLANES = 15
+NUM_PLANES = 16
 I_EPLEN, I_ACC, I_EPOCH, I_PACKED = range(4)
 OBS_DIM = 16
 GATE_FLOATS = 20
 TRACK_FLOATS = 4
+OBST_FLOATS = 20
 
 LOG_NRESET = 0
 LOG_EPSUM0 = 1
@@ -186,11 +187,17 @@ class GrCameraBuffers(C.Structure):
     _fields_ = [("depth", C.c_void_p), ("age", C.c_void_p), ("obs_policy", C.c_void_p), ("obs_critic", C.c_void_p)]
 
 
+class GrObstacles(C.Structure):
+    _fields_ = [("records", C.c_void_p), ("counts", C.c_void_p), ("grid_f", C.c_void_p), ("grid_i", C.c_void_p),
+                ("cells", C.c_void_p), ("items", C.c_void_p), ("max_obstacles", C.c_int32), ("num_cells", C.c_int32),
+                ("num_items", C.c_int32), ("reserved", C.c_int32)]
+
+
 GR_CAM_STEP, GR_CAM_RESET, GR_CAM_OBSERVE = 0, 1, 2
 
 EXPORTS = [
     "gr_abi_version", "gr_config_default", "gr_config_size", "gr_create", "gr_destroy", "gr_last_error",
-    "gr_num_blocks", "gr_num_log_rows", "gr_log_finalize", "gr_bytes_per_env_step", "gr_bind_tracks", "gr_bind_buffers", "gr_init", "gr_reset",
+    "gr_num_blocks", "gr_num_log_rows", "gr_log_finalize", "gr_bytes_per_env_step", "gr_bind_tracks", "gr_bind_obstacles", "gr_bind_buffers", "gr_init", "gr_reset",
     "gr_step", "gr_observe", "gr_set_timing", "gr_read_timing", "gr_test_dynamics", "gr_test_math",
     "gr_test_philox",
     "gr_debug_read_stamps",
@@ -215,6 +222,7 @@ def _declare(lib):
         "gr_log_finalize": (C.c_int, [vp, vp, vp, vp, vp]),
         "gr_bytes_per_env_step": (C.c_int, [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
         "gr_bind_tracks": (C.c_int, [vp, vp, vp]),
+        "gr_bind_obstacles": (C.c_int, [vp, C.POINTER(GrObstacles)]),
         "gr_bind_buffers": (C.c_int, [vp, C.POINTER(GrBuffers)]),
         "gr_init": (C.c_int, [vp, vp]),
         "gr_reset": (C.c_int, [vp, vp, vp]),

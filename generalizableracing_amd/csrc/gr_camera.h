@@ -13,9 +13,9 @@
  * is `make_gate` = outer box minus inner box (trimesh/utils.py:10-33), plus the ground.
  * Here each gate is intersected analytically as a box with a through-hole prism (the
  * same solid), in the gate's own frame, from the track-table record the collision test
- * uses; the ground is the plane z = ground_z (env-local).  Walls / orbit / ground
- * obstacles are not in the table yet, neither are the gates of the
- * neighbouring 40 m terrain tiles.
+ * uses; the ground is the plane z = ground_z (env-local).  The track's walls / orbits /
+ * ground obstacles are analytic primitives (gr_obstacles.h).  The gates and obstacles of
+ * the neighbouring 40 m terrain tiles are not rendered.
  *
  * Rays.  Pixel (u, v) (row-major, v*W + u) looks along r = (1, a_u, b_v) in the camera
  * frame (x forward, y left, z up: "world" convention), a_u = (cx - (u + 0.5)) / fx,
@@ -31,6 +31,7 @@
 
 #include "../../include/gr.h"
 #include "gr_math.h"
+#include "gr_obstacles.h"
 #include "gr_rng.h"
 
 #define GR_CAM_MAX_W 256
@@ -100,14 +101,15 @@ GR_HD void gr_cam_pose(const gr_cam_const* cc, const float p[3], const float q[4
 
 GR_HD float gr_cam_dot3(const float* a, const float* b) { return gr_fmaf(a[2], b[2], gr_fmaf(a[1], b[1], a[0] * b[0])); }
 
-/* One gate (GR_GATE_FLOATS record: centre, rows of R^T, half sizes) seen from camera
- * (o, c0, c1, c2): fills a slot.  Culls gates entirely behind the camera or whose nearest
- * point is beyond max_distance (the clip makes such hits indistinguishable from misses),
- * and bounds the gate's screen footprint by projecting the 8 outer-box corners (convex
- * hull of a convex solid in front of the camera); the window gets a margin so that
- * rounding never culls a pixel that can hit. */
-GR_HD void gr_cam_gate_setup(const float* g, const float o[3], const float c0[3], const float c1[3],
-                             const float c2[3], float max_distance, float* s) {
+/* A primitive with a GR_GATE_FLOATS / GR_OBST_FLOATS style record (centre 0-2, rows of R^T
+ * at 4-6 / 8-10 / 12-14) and local bounding-box half extents l, seen from camera (o, c0, c1,
+ * c2): fills the frame part of a slot.  Culls primitives entirely behind the camera or whose
+ * nearest point is beyond max_distance (the clip makes such hits indistinguishable from
+ * misses), and bounds the screen footprint by projecting the 8 box corners (convex hull of a
+ * convex solid in front of the camera); the window gets a margin so that rounding never
+ * culls a pixel that can hit. */
+GR_HD void gr_cam_frame_setup(const float* g, const float l[3], const float o[3], const float c0[3],
+                              const float c1[3], const float c2[3], float max_distance, float* s) {
   const float rel[3] = {g[0] - o[0], g[1] - o[1], g[2] - o[2]};
   const float* M[3] = {g + 4, g + 8, g + 12};
   for (int j = 0; j < 3; ++j) {
@@ -116,12 +118,6 @@ GR_HD void gr_cam_gate_setup(const float* g, const float o[3], const float c0[3]
     s[GR_CS_D1 + j] = gr_cam_dot3(M[j], c1);
     s[GR_CS_D2 + j] = gr_cam_dot3(M[j], c2);
   }
-  s[GR_CS_HW] = g[7];
-  s[GR_CS_HH] = g[11];
-  s[GR_CS_HT] = g[15];
-  s[GR_CS_HOW] = g[16];
-  s[GR_CS_HOH] = g[17];
-  const float l[3] = {g[16], g[17], g[15]};
   const float x0 = gr_cam_dot3(c0, rel), y0 = gr_cam_dot3(c1, rel), z0 = gr_cam_dot3(c2, rel);
   float ex = 0.0f;
   for (int j = 0; j < 3; ++j) ex += gr_fabsf(l[j] * s[GR_CS_D0 + j]);
@@ -155,6 +151,32 @@ GR_HD void gr_cam_gate_setup(const float* g, const float o[3], const float c0[3]
   s[GR_CS_BMAX] = bmax;
   s[22] = 0.0f;
   s[23] = 0.0f;
+}
+
+/* One gate (GR_GATE_FLOATS record: centre, rows of R^T, half sizes): its outer box bounds
+ * the window. */
+GR_HD void gr_cam_gate_setup(const float* g, const float o[3], const float c0[3], const float c1[3],
+                             const float c2[3], float max_distance, float* s) {
+  const float l[3] = {g[16], g[17], g[15]};
+  gr_cam_frame_setup(g, l, o, c0, c1, c2, max_distance, s);
+  s[GR_CS_HW] = g[7];
+  s[GR_CS_HH] = g[11];
+  s[GR_CS_HT] = g[15];
+  s[GR_CS_HOW] = g[16];
+  s[GR_CS_HOH] = g[17];
+}
+
+/* One obstacle (GR_OBST_FLOATS record, gr_obstacles.h); hit by gr_cam_obst_hit. */
+GR_HD void gr_cam_obst_setup(const float* r, const float o[3], const float c0[3], const float c1[3],
+                             const float c2[3], float max_distance, float* s) {
+  float l[3];
+  gr_obst_local_box(r, l);
+  gr_cam_frame_setup(r, l, o, c0, c1, c2, max_distance, s);
+  s[GR_OS_E0] = r[7];
+  s[GR_OS_E1] = r[11];
+  s[GR_OS_E2] = r[15];
+  s[GR_OS_KIND] = r[16];
+  s[16] = 0.0f;
 }
 
 GR_HD float gr_cam_inv(float d) { return 1.0f / (gr_fabsf(d) < 1.0e-20f ? gr_copysignf(1.0e-20f, d) : d); }

@@ -54,8 +54,37 @@ DEV_INLINE void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Dynamic LDS: ray tables a_u[W], b_v[H] (padded to 4), then per wave: gate slots [max_gates][24] and an
-// 8-row depth staging band [8][W].
+// obstacle slot from LDS (GR_CAM_OSLOT floats: frame, primitive, window, valid)
+DEV_INLINE void load_oslot(const float4* src, float s[GR_CAM_SLOT]) {
+#pragma unroll
+  for (int k = 0; k < GR_CAM_OSLOT / 4; ++k) {
+    const float4 q4 = src[k];
+    s[4 * k] = q4.x; s[4 * k + 1] = q4.y; s[4 * k + 2] = q4.z; s[4 * k + 3] = q4.w;
+  }
+}
+
+// the obstacle's record from global memory
+DEV_INLINE void load_orec(const float* rec, float r[GR_OBST_FLOATS]) {
+  const float4* r4 = reinterpret_cast<const float4*>(rec);
+#pragma unroll
+  for (int k = 0; k < GR_OBST_FLOATS / 4; ++k) {
+    const float4 v = r4[k];
+    r[4 * k] = v.x; r[4 * k + 1] = v.y; r[4 * k + 2] = v.z; r[4 * k + 3] = v.w;
+  }
+}
+
+// nearest obstacle crossing of the tile quad's four rays against one set-up slot
+DEV_INLINE void quad_obst(const float* s, const float av[4], float b, float d[4]) {
+  // a_u decreases with u: the quad spans [av[3], av[0]]
+  if (b >= s[GR_CS_BMIN] && b <= s[GR_CS_BMAX] && av[3] <= s[GR_CS_AMAX] && av[0] >= s[GR_CS_AMIN]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (av[j] >= s[GR_CS_AMIN] && av[j] <= s[GR_CS_AMAX]) d[j] = gr_minf(d[j], gr_cam_obst_hit(s, av[j], b));
+  }
+}
+
+// Dynamic LDS: ray tables a_u[W], b_v[H] (padded to 4), then per wave: gate slots [max_gates][24], obstacle
+// slots [GR_CAM_OBST_SLOTS][24] (obstacle tracks only) and an 8-row depth staging band [8][W].
 #ifdef CAM_WAVES_PER_EU
 #define CAM_ATTR __attribute__((amdgpu_waves_per_eu(CAM_WAVES_PER_EU, CAM_WAVES_PER_EU)))
 #else
@@ -77,9 +106,12 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
   const int i = blockIdx.x * CAM_WAVES + w;
   const bool active = i < a.num_envs;
   const int N = a.num_envs;
-  float* wave_lds = smem + wpad + hpad + w * (G * GR_CAM_SLOT + 8 * W);
-  float4* s_slot = reinterpret_cast<float4*>(wave_lds);                    // [G][CAM_SLOT4]
-  float4* s_stage = reinterpret_cast<float4*>(wave_lds + G * GR_CAM_SLOT);  // [8 * W / 4]
+  const bool obst = a.obst != nullptr;
+  const int oslots = obst ? GR_CAM_OBST_SLOTS * GR_CAM_OSLOT : 0;
+  float* wave_lds = smem + wpad + hpad + w * (G * GR_CAM_SLOT + oslots + 8 * W);
+  float4* s_slot = reinterpret_cast<float4*>(wave_lds);                             // [G][CAM_SLOT4]
+  float4* s_oslot = reinterpret_cast<float4*>(wave_lds + G * GR_CAM_SLOT);          // [64][GR_CAM_OSLOT / 4]
+  float4* s_stage = reinterpret_cast<float4*>(wave_lds + G * GR_CAM_SLOT + oslots);  // [8 * W / 4]
 
   // ---- is the sensor outdated? (SensorBase.update / reset; wave-uniform)
   int render = 0;
@@ -102,7 +134,9 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
   float o[3] = {0.0f, 0.0f, 0.0f}, c0[3] = {1.0f, 0.0f, 0.0f}, c1[3] = {0.0f, 1.0f, 0.0f},
         c2[3] = {0.0f, 0.0f, 1.0f};
   float gz = 0.0f;
-  uint64_t valid_mask = 0;
+  uint64_t valid_mask = 0, omask = 0;
+  const float* orecs = nullptr;  // this track's obstacle records
+  int nob = 0, ofrom = 0;         // obstacles in the track; raw index of the first one beyond the slots
   if (render) {
     const float4 posq = reinterpret_cast<const float4*>(a.state)[(size_t)GR_P_POSQ * N + i];
     const float4 qv = reinterpret_cast<const float4*>(a.state)[(size_t)GR_P_QV * N + i];
@@ -124,6 +158,40 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
         s_slot[lane * CAM_SLOT4 + k] = make_float4(s[4 * k], s[4 * k + 1], s[4 * k + 2], s[4 * k + 3]);
     }
     valid_mask = __ballot(valid);
+    if (obst) {
+      // obstacles in view: the first GR_CAM_OBST_SLOTS go to LDS slots (compacted by ballot); from the
+      // next one on (rare) they are set up again per tile
+      nob = a.obst_counts[track];
+      orecs = a.obst + (size_t)track * a.max_obst * GR_OBST_FLOATS;
+      ofrom = nob;
+      int nv = 0;
+      for (int base = 0; base < nob; base += 64) {
+        const int k = base + lane;
+        int ok = 0;
+        if (k < nob) {
+          float r[GR_OBST_FLOATS];
+          load_orec(orecs + (size_t)k * GR_OBST_FLOATS, r);
+          gr_cam_obst_setup(r, o, c0, c1, c2, cc->max_distance, s);
+          ok = s[GR_CS_VALID] != 0.0f;
+        }
+        const uint64_t b = __ballot(ok);
+        const int pos = nv + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+        if (ok && pos < GR_CAM_OBST_SLOTS) {
+#pragma unroll
+          for (int q = 0; q < GR_CAM_OSLOT / 4; ++q)
+            s_oslot[pos * (GR_CAM_OSLOT / 4) + q] = make_float4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
+        }
+        const int nb = __popcll(b);
+        if (nv + nb > GR_CAM_OBST_SLOTS && ofrom == nob) {
+          // raw index of valid obstacle number GR_CAM_OBST_SLOTS (wave-uniform)
+          const uint64_t over = __ballot(ok && pos == GR_CAM_OBST_SLOTS);
+          ofrom = base + __builtin_ctzll(over);
+        }
+        nv += nb;
+      }
+      const int ns = nv < GR_CAM_OBST_SLOTS ? nv : GR_CAM_OBST_SLOTS;
+      omask = ns == 64 ? ~0ull : ((1ull << ns) - 1ull);
+    }
   }
   __syncthreads();
   if (!active) return;
@@ -195,6 +263,22 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
             if (av[j] >= s[GR_CS_AMIN] && av[j] <= s[GR_CS_AMAX]) d[j] = gr_minf(d[j], gr_cam_gate_hit(s, av[j], b));
         }
       }
+      if (obst) {
+        uint64_t mo = omask;
+        while (mo) {
+          const int k = __builtin_ctzll(mo);
+          mo &= mo - 1;
+          float s[GR_CAM_SLOT];
+          load_oslot(s_oslot + k * (GR_CAM_OSLOT / 4), s);
+          quad_obst(s, av, b, d);
+        }
+        for (int k = ofrom; k < nob; ++k) {  // beyond the slots: set up again (identical slot values)
+          float r[GR_OBST_FLOATS], s[GR_CAM_SLOT];
+          load_orec(orecs + (size_t)k * GR_OBST_FLOATS, r);
+          gr_cam_obst_setup(r, o, c0, c1, c2, maxd, s);
+          if (s[GR_CS_VALID] != 0.0f) quad_obst(s, av, b, d);
+        }
+      }
       s_stage[((v - v0) * W + u0) >> 2] =
           make_float4(gr_cam_clip(d[0], maxd), gr_cam_clip(d[1], maxd), gr_cam_clip(d[2], maxd), gr_cam_clip(d[3], maxd));
     }
@@ -211,8 +295,8 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
 
 hipError_t launch_camera(const CamArgs& a, hipStream_t s) {
   const int blocks = (a.num_envs + CAM_WAVES - 1) / CAM_WAVES;
-  hipLaunchKernelGGL(camera_kernel, dim3(blocks), dim3(CAM_WAVES * 64), camera_lds_bytes(a.width, a.height, a.max_gates),
-                     s, a);
+  hipLaunchKernelGGL(camera_kernel, dim3(blocks), dim3(CAM_WAVES * 64),
+                     camera_lds_bytes(a.width, a.height, a.max_gates, a.obst != nullptr), s, a);
   return hipGetLastError();
 }
 

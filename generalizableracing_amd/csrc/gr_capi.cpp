@@ -24,6 +24,7 @@ struct gr_ctx {
   bool have_buf = false;
   float* table = nullptr;  // packed [T*L][stride]
   bool have_tracks = false;
+  gr_obstacles obst;       // caller-owned device arrays (records null: none)
   gr::KArgs args;
   gr::KConst kc;                   // host copy of the per-context constants
   gr::KConst* kc_dev = nullptr;    // device copy read by the kernels
@@ -279,7 +280,8 @@ int gr_log_finalize(gr_ctx* c, const float* rows, const float* prev, float* out,
 
 int gr_bytes_per_env_step(const gr_ctx* c, int64_t* rd, int64_t* wr) {
   if (!c || !rd || !wr) return GR_ERR_ARG;
-  const int motor = c->cfg.use_motor_model ? 1 : 0;
+  // the obstacle hint plane (obstacle tracks) is read and written like a motor plane
+  const int motor = (c->cfg.use_motor_model ? 1 : 0) + (c->obst.records ? 1 : 0);
   // read: planes POSQ..PAR3 (14 x 16 B) [+ MOTOR], int plane 16 B, action 16 B
   *rd = (14 + motor) * 16 + 16 + 16;
   // written: POSQ..LAG, EP0, EP1 (8 x 16 B) [+ MOTOR], int plane, obs policy+critic (2 x 64 B),
@@ -317,6 +319,58 @@ int gr_bind_tracks(gr_ctx* c, const float* gates, const float* tracks) {
   if (e != hipSuccess) return hip_fail(c, e, "gr_bind_tracks: sync");
   c->args.table = c->table;
   c->have_tracks = true;
+  return GR_OK;
+}
+
+int gr_bind_obstacles(gr_ctx* c, const gr_obstacles* o) {
+  if (!c) return GR_ERR_ARG;
+  if (!o) {
+    std::memset(&c->obst, 0, sizeof(c->obst));
+    c->args.obst_grid_f = nullptr;
+    c->args.obst_grid_i = nullptr;
+    c->args.obst_cells = nullptr;
+    c->args.obst_items = nullptr;
+    return GR_OK;
+  }
+  if (!o->records || !o->counts || !o->grid_f || !o->grid_i || !o->cells || !o->items || o->max_obstacles <= 0 ||
+      o->num_cells <= 0 || o->num_items <= 0)
+    return fail(c, GR_ERR_ARG, "gr_bind_obstacles: null array or empty size");
+  if (!aligned16(o->records) || !aligned16(o->grid_f) || !aligned16(o->grid_i) || !aligned16(o->items) ||
+      (reinterpret_cast<uintptr_t>(o->cells) & 7u))
+    return fail(c, GR_ERR_ARG, "gr_bind_obstacles: records / grids / items must be 16-byte aligned, cells 8-byte");
+  const int ntr = c->cfg.num_types * c->cfg.num_levels;
+  std::vector<int32_t> cnt(ntr), gi((size_t)ntr * 4), cells((size_t)o->num_cells * 2);
+  std::vector<float> gf((size_t)ntr * 4);
+  hipError_t e = hipMemcpy(cnt.data(), o->counts, cnt.size() * 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(gf.data(), o->grid_f, gf.size() * 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(gi.data(), o->grid_i, gi.size() * 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(cells.data(), o->cells, cells.size() * 4, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(c, e, "gr_bind_obstacles: copy index arrays");
+  for (int t = 0; t < ntr; ++t) {
+    const int nx = gi[4 * t], ny = gi[4 * t + 1], first = gi[4 * t + 2];
+    if (cnt[t] < 0 || cnt[t] > o->max_obstacles || nx < 0 || ny < 0 || first < 0 ||
+        (long)first + (long)nx * ny > o->num_cells)
+      return fail(c, GR_ERR_ARG, "gr_bind_obstacles: invalid count / grid of track " + std::to_string(t));
+  }
+  for (int k = 0; k < o->num_cells; ++k)
+    if (cells[2 * k] < 0 || cells[2 * k + 1] < 0 || (long)cells[2 * k] + cells[2 * k + 1] > o->num_items)
+      return fail(c, GR_ERR_ARG, "gr_bind_obstacles: cell " + std::to_string(k) + " out of the item range");
+  // one cell size and margin for all tracks (the per-env hints carry only the grown cell's corner)
+  for (int t = 0; t < ntr; ++t)
+    if (!(gf[4 * t + 2] > 0.0f) || !(gf[4 * t + 3] >= 0.0f) || gf[4 * t + 2] != gf[2] || gf[4 * t + 3] != gf[3])
+      return fail(c, GR_ERR_ARG, "gr_bind_obstacles: every track needs the same 1/cell > 0 and margin >= 0");
+  const float cell = 1.0f / gf[2], margin = gf[3] * cell;
+  c->args.h.obst_span = cell + 2.0f * margin;
+  // hints refer to the previous obstacle table: clear them (all-zero = no hint)
+  if (c->have_buf) {
+    e = hipMemset(c->buf.state + (size_t)GR_P_OHINT * c->cfg.num_envs * 4, 0, (size_t)c->cfg.num_envs * 16);
+    if (e != hipSuccess) return hip_fail(c, e, "gr_bind_obstacles: clear hints");
+  }
+  c->obst = *o;
+  c->args.obst_grid_f = reinterpret_cast<const float4*>(o->grid_f);
+  c->args.obst_grid_i = reinterpret_cast<const int4*>(o->grid_i);
+  c->args.obst_cells = reinterpret_cast<const int2*>(o->cells);
+  c->args.obst_items = reinterpret_cast<const float4*>(o->items);
   return GR_OK;
 }
 
@@ -495,6 +549,9 @@ int gr_camera_render(gr_ctx* c, int mode, const uint8_t* mask, void* stream) {
   a.counters = c->buf.counters;
   a.counter_index = c->buf.counter_index;
   a.table = c->table;
+  a.obst = c->obst.records;
+  a.obst_counts = c->obst.counts;
+  a.max_obst = c->obst.records ? c->obst.max_obstacles : 0;
   a.track_stride = c->kc.track_stride;
   a.num_levels = c->cfg.num_levels;
   a.max_gates = c->cfg.max_gates;

@@ -7,7 +7,8 @@
 #define GR_BLOCK 256
 #define GR_MAX_TYPES 64
 #define GR_LOG_ROWS_PER_BLOCK 8  // log rows per workgroup (physics and policy waves of the step kernel)
-#define GR_XCH_BYTES ((5 + 6 + 8) * GR_BLOCK * 16)  // step kernel handovers + store staging in LDS
+// step kernel handovers + store staging + obstacle hand-over (3 rows + ready flags) in LDS
+#define GR_XCH_BYTES ((5 + 6 + 8 + 3) * GR_BLOCK * 16 + 16)
 #define GR_LDS_MAX (160 * 1024)                 // LDS a gfx950 workgroup may allocate
 #define GR_STAMP_WAVES 8192  // diagnostic stamps (GR_STAMPS builds only)
 #define GR_STAMP_SLOTS 16
@@ -43,6 +44,7 @@ struct KHot {
   int env_id_offset, use_motor_model, obs_noise, lds_tab_vec;  // lds_tab_vec: float4 of LDS table (0: global)
   uint32_t seed_lo, seed_hi;
   float obs_lin_vel_noise, obs_att_noise;
+  float obst_span;  // obstacle grid: cell + 2 margin (m), the side of a hinted grown cell
 };
 
 // Passed by value (kernarg): per-binding pointers + the constants pointer.
@@ -51,6 +53,11 @@ struct KArgs {
   gr_buffers buf;
   const float* table;    // packed track table [T*L][track_stride]
   const int* blk_types;  // per workgroup: first | last terrain type << 16 (host-derived)
+  // obstacles (gr_bind_obstacles; null: none): per-track xy grid, cells of record copies
+  const float4* obst_grid_f;  // [T*L]: x0, y0, 1/cell, cell
+  const int4* obst_grid_i;    // [T*L]: nx, ny, first cell, 0
+  const int2* obst_cells;     // [C]: first item, count
+  const float4* obst_items;   // [I][GR_OBST_FLOATS / 4]
   KHot h;
 };
 
@@ -67,6 +74,9 @@ struct CamArgs {
   const uint32_t* counters;
   int counter_index;
   const float* table;  // packed track table
+  const float* obst;   // obstacle records [T*L][max_obst][GR_OBST_FLOATS] (null: none)
+  const int32_t* obst_counts;  // [T*L]
+  int max_obst;
   int track_stride, num_levels, max_gates, num_envs, env_id_offset, mode, width, height;
   uint32_t seed_lo, seed_hi;
   float* depth;
@@ -75,10 +85,16 @@ struct CamArgs {
   float* out_c;
 };
 hipError_t launch_camera(const CamArgs& a, hipStream_t s);
-// dynamic LDS of the camera kernel: ray tables + per wave (gate slots + an 8-row staging band)
-inline size_t camera_lds_bytes(int width, int height, int max_gates) {
+// obstacle slots per camera wave (the first GR_CAM_OBST_SLOTS obstacles in view; any further ones
+// are set up again per tile from their records)
+#define GR_CAM_OBST_SLOTS 64
+#define GR_CAM_OSLOT 24  // floats per obstacle slot (the gate slot layout, gr_camera.h / gr_obstacles.h)
+// dynamic LDS of the camera kernel: ray tables + per wave (gate slots [+ obstacle slots] + an 8-row
+// staging band)
+inline size_t camera_lds_bytes(int width, int height, int max_gates, bool obst) {
   const size_t wpad = (size_t)((width + 3) & ~3), hpad = (size_t)((height + 3) & ~3);
-  return 4 * (wpad + hpad + 4 * ((size_t)max_gates * 24 + 8 * (size_t)width));
+  const size_t os = obst ? (size_t)GR_CAM_OBST_SLOTS * GR_CAM_OSLOT : 0;
+  return 4 * (wpad + hpad + 4 * ((size_t)max_gates * 24 + os + 8 * (size_t)width));
 }
 
 hipError_t launch_env(int mode, const KArgs& a, const float* actions, const uint8_t* mask, hipStream_t s,

@@ -15,6 +15,7 @@
 #include "../../include/gr.h"
 #include "gr_kernels.h"
 #include "gr_math.h"
+#include "gr_obstacles.h"
 #include "gr_rng.h"
 
 namespace gr {
@@ -193,11 +194,101 @@ DEV void action_scale(const KArgs& a, float m_ctrl, float sc[4], float of[4]) {
 // conservative culls (sphere, plane slab, outer box, hole) that can only skip
 // gates where no lattice point can be inside, so the count is unchanged.
 // compile-time lattice: after unrolling every offset is an inline constant (0, +-1, +-0.5)
-constexpr float c_lattice[17][3] = {
-    {0, 0, 0},          {1, 1, 1},         {1, -1, 1},        {-1, 1, 1},       {-1, -1, 1},     {1, 1, -1},
-    {1, -1, -1},        {-1, 1, -1},       {-1, -1, -1},      {0.5f, 0.5f, 0.5f}, {0.5f, -0.5f, 0.5f},
-    {-0.5f, 0.5f, 0.5f}, {-0.5f, -0.5f, 0.5f}, {0.5f, 0.5f, -0.5f}, {0.5f, -0.5f, -0.5f}, {-0.5f, 0.5f, -0.5f},
-    {-0.5f, -0.5f, -0.5f}};
+constexpr float c_lattice[17][3] = GR_LATTICE_INIT;
+#ifndef GR_OBST_BATCH
+#define GR_OBST_BATCH 4  // obstacle cull spheres loaded per batch
+#endif
+#ifndef GR_OBST_PRE
+#define GR_OBST_PRE 2  // obstacle records of the hinted cell held in registers from kernel entry
+#endif
+
+// ------------------------------------------------------------- obstacles
+// Per track a uniform xy grid; cell lists hold copies of every record whose cull sphere reaches into
+// the cell grown by `margin` per axis (gr.h gr_obstacles, tracks.py pack_obstacles).  Per env, the
+// GR_P_OHINT plane carries the list of the cell its position lies in (first item, count + 1, and the
+// lower corner of the grown cell; 0 = no hint), written at the end of every step for the next one: so
+// the records can be fetched at kernel entry, and the list serves the post-step test whenever the drone
+// stayed within the grown cell (a step moves it a few cm).  Otherwise (no hint, left the grown cell) the
+// post-step cell is looked up.
+struct ObstGrid {
+  float4 f;  // x0, y0, 1/cell, margin / cell
+  int4 i;    // nx, ny, first cell, 0
+};
+DEV ObstGrid obst_grid(const KArgs& a, int type, int lvl) {
+  const int tk = type * a.h.num_levels + lvl;
+  return ObstGrid{a.obst_grid_f[tk], a.obst_grid_i[tk]};
+}
+// the cell of p: linear cell index, or -1 outside the grid; (cx, cy) its coordinates
+DEV int obst_cell(const ObstGrid& og, const float p[3], int& cx, int& cy) {
+  const float fx = (p[0] - og.f.x) * og.f.z, fy = (p[1] - og.f.y) * og.f.z;
+  cx = cy = 0;
+  if (!(fx >= 0.0f && fy >= 0.0f && fx < (float)og.i.x && fy < (float)og.i.y)) return -1;
+  cx = (int)fx;
+  cy = (int)fy;
+  return og.i.z + cy * og.i.x + cx;
+}
+// lattice mask of one record (cull sphere first)
+DEV uint32_t obst_one(const float4 r4[GR_OBST_FLOATS / 4], const float p[3], const float A[3], const float B[3],
+                      const float C[3]) {
+  float r[GR_OBST_FLOATS];
+#pragma unroll
+  for (int k = 0; k < GR_OBST_FLOATS / 4; ++k) {
+    r[4 * k] = r4[k].x; r[4 * k + 1] = r4[k].y; r[4 * k + 2] = r4[k].z; r[4 * k + 3] = r4[k].w;
+  }
+  return gr_obst_near(r, p) ? gr_obst_lattice_mask(r, p, A, B, C, c_lattice) : 0u;
+}
+// lattice mask of the list items [first + from, first + count): cull spheres in batches of independent
+// loads, full records only for the spheres that hold p
+DEV uint32_t obst_list(const KArgs& a, int first, int from, int count, const float p[3], const float A[3],
+                       const float B[3], const float C[3]) {
+  uint32_t m = 0u;
+  for (int j0 = from; j0 < count; j0 += GR_OBST_BATCH) {
+    float4 sp[GR_OBST_BATCH];
+#pragma unroll
+    for (int j = 0; j < GR_OBST_BATCH; ++j)
+      sp[j] = j0 + j < count ? a.obst_items[(size_t)(first + j0 + j) * (GR_OBST_FLOATS / 4)]
+                             : make_float4(0.0f, 0.0f, 0.0f, -1.0f);
+    uint32_t near = 0u;
+#pragma unroll
+    for (int j = 0; j < GR_OBST_BATCH; ++j) {
+      const float r[4] = {sp[j].x, sp[j].y, sp[j].z, sp[j].w};
+      near |= (uint32_t)gr_obst_near(r, p) << j;
+    }
+    while (near) {
+      const int j = __builtin_ctz(near);
+      near &= near - 1u;
+      const float4* r4 = a.obst_items + (size_t)(first + j0 + j) * (GR_OBST_FLOATS / 4);
+      float4 rr[GR_OBST_FLOATS / 4];
+#pragma unroll
+      for (int k = 0; k < GR_OBST_FLOATS / 4; ++k) rr[k] = r4[k];
+      m |= obst_one(rr, p, A, B, C);
+    }
+  }
+  return m;
+}
+// full lookup from the grid (no hint)
+DEV uint32_t obst_lookup(const KArgs& a, const ObstGrid& og, const float p[3], const float A[3], const float B[3],
+                         const float C[3]) {
+  int cx, cy;
+  const int c = obst_cell(og, p, cx, cy);
+  if (c < 0) return 0u;
+  const int2 ce = a.obst_cells[c];
+  return obst_list(a, ce.x, 0, ce.y, p, A, B, C);
+}
+// the hint of a position: its cell's list and the grown cell's lower corner (0: outside the grid)
+DEV float4 obst_hint_of(const KArgs& a, const ObstGrid& og, const float p[3]) {
+  int cx, cy;
+  const int c = obst_cell(og, p, cx, cy);
+  if (c < 0) return make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  const int2 ce = a.obst_cells[c];
+  const float cell = 1.0f / og.f.z, margin = og.f.w * cell;
+  return make_float4(__int_as_float(ce.x), __int_as_float(ce.y + 1), og.f.x + (float)cx * cell - margin,
+                     og.f.y + (float)cy * cell - margin);
+}
+// is p inside the hinted grown cell?  (span = cell + 2 margin)
+DEV bool obst_hint_holds(const float4& h, const float p[3], float span) {
+  return __float_as_int(h.y) > 0 && p[0] >= h.z && p[0] <= h.z + span && p[1] >= h.w && p[1] <= h.w + span;
+}
 
 DEV void body_axes(const KArgs& a, const float q[4], float A[3], float B[3], float Cz[3]) {
   const float ex[3] = {a.kc->cfg.collider_half[0], 0.0f, 0.0f}, ey[3] = {0.0f, a.kc->cfg.collider_half[1], 0.0f},
@@ -213,9 +304,12 @@ DEV void gate_frame(const float* g, const float v[3], float o[3]) {
   o[2] = (g[12] * v[0] + g[13] * v[1]) + g[14] * v[2];
 }
 
-// number of the 17 lattice points inside a gate frame or under the ground
-// (replaces PhysX contact / Warp mesh_tools.py:128-233; see oracle)
-DEV int collision_count(const KArgs& a, const Tab& tab, int type, int lvl, const float p[3], const float q[4]) {
+// lattice mask (17 bits) of the points inside a gate frame or under the ground, and with OBST inside
+// an obstacle looked up from the grid (the substep integrator; the explicit step hands obstacles to the
+// policy waves instead).  Replaces PhysX contact / Warp mesh_tools.py:128-233; see oracle.
+template <bool OBST>
+DEV uint32_t collision_mask(const KArgs& a, const Tab& tab, int type, int lvl, const float p[3], const float q[4],
+                            const ObstGrid& og) {
   const float* rec = tab.rec(type, lvl);
   const float ground = rec[0];
   const int ng = (int)rec[3];
@@ -229,7 +323,12 @@ DEV int collision_count(const KArgs& a, const Tab& tab, int type, int lvl, const
     if ((dx * dx + dy * dy) + dz * dz <= c4.w) sph |= 1u << g;
   }
   const bool ground_near = p[2] - ground < reach;
-  if (!sph && !ground_near) return 0;
+  int ocount = 0;
+  if (OBST) {
+    int cx, cy;
+    ocount = obst_cell(og, p, cx, cy) >= 0;
+  }
+  if (!sph && !ground_near && !ocount) return 0u;
   float A[3], B[3], Cz[3];
   body_axes(a, q, A, B, Cz);
   uint32_t inside = 0u;
@@ -269,7 +368,8 @@ DEV int collision_count(const KArgs& a, const Tab& tab, int type, int lvl, const
       if (in_outer & !in_hole) inside |= 1u << k;
     }
   }
-  return __builtin_popcount(inside);
+  if (OBST) inside |= obst_lookup(a, og, p, A, B, Cz);
+  return inside;
 }
 
 // ------------------------------------------------------------- controller
@@ -764,6 +864,8 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const KConst* __
       store_dyn(a, i, e);
       store_rst(a, i, e);
       store_istate(a, i, e);
+      // new position / level: the obstacle hint is stale
+      reinterpret_cast<float4*>(a.buf.state)[GR_P_OHINT * (size_t)n + i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
   }
   // (observe calls reset nothing: their rows say so, and the finalized log repeats the previous one)
@@ -792,6 +894,9 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const KConst* __
 enum { X_PA = 0, X_Q = 1, X_VD = 2, X_LAG = 3, X_LC = 4, GR_XF4 = 5, GR_XF = 4 * GR_XF4 };
 enum { R_POSQ = 0, R_QV = 1, R_VW = 2, R_W = 3, R_RST0 = 4, R_RST1 = 5, GR_RF4 = 6 };
 enum { GR_SF4 = 8 };  // staging rows for the coalesced observation stores (policy 4, critic 4)
+// obstacle rows (obstacle tracks only): physics -> policy the post-step position and attitude,
+// policy -> physics the obstacle lattice mask; then one ready flag per wave pair
+enum { O_P = 0, O_Q = 1, O_MASK = 2, GR_OF4 = 3 };
 
 // environment as the policy / episode waves see it after the handover: the post-step pose,
 // or for resetting envs the next episode's start state
@@ -824,13 +929,15 @@ DEV void merge_handover(const float4* xch, int t, bool reset, Env& e) {
   e.azero = reset ? 1 : 0;
 }
 
-template <bool USE_LDS>
+template <bool USE_LDS, bool OBST>
 __global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KConst* __restrict__ kc,
                                                              const float* __restrict__ actions) {
   a.kc = kc;
   extern __shared__ __attribute__((aligned(16))) float4 lds[];
   float4* xch = lds + a.h.lds_tab_vec;                      // [GR_XF4 + GR_RF4][GR_BLOCK] handovers
   float4* stg = xch + (GR_XF4 + GR_RF4) * GR_BLOCK;         // [GR_SF4][GR_BLOCK] store staging
+  float4* obx = stg + GR_SF4 * GR_BLOCK;                    // [GR_OF4][GR_BLOCK] obstacle hand-over (OBST)
+  int* oflag = reinterpret_cast<int*>(obx + GR_OF4 * GR_BLOCK);  // [GR_BLOCK / 64] mask-ready flags (OBST)
   const int role = threadIdx.x >> 8;                        // wave-uniform: 0 physics, 1 policy, 2 episode
   const int t = threadIdx.x & (GR_BLOCK - 1);
   const int n = a.h.num_envs;
@@ -855,8 +962,9 @@ __global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KCons
       if ((int)threadIdx.x < sl.nvec) lds[threadIdx.x] = tr;
       if (two && (int)threadIdx.x + 3 * GR_BLOCK < sl.nvec) lds[threadIdx.x + 3 * GR_BLOCK] = tr2;
       for (int idx = threadIdx.x + 6 * GR_BLOCK; idx < sl.nvec; idx += 3 * GR_BLOCK) lds[idx] = sl.src[idx];
-      __syncthreads();  // barrier 1: table staged
     }
+    // barrier 1: table staged; with obstacles also the physics -> policy pose hand-over and the cleared flags
+    if (USE_LDS || OBST) __syncthreads();
   };
 
   if (role == 0) {
@@ -891,18 +999,35 @@ __global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KCons
     if (c.integrator == GR_INTEGRATOR_DD_EXPLICIT) {
       dd_explicit(m, Jp, e.k2, e.k1, tt, dt, c.gravity, e.p, e.q, e.v, e.w, accl, al);
       STAMP(3);
+      if (OBST) {  // the policy waves test the obstacles on the post-step pose while this wave tests the gates
+        obx[O_P * GR_BLOCK + t] = make_float4(e.p[0], e.p[1], e.p[2], 0.0f);
+        obx[O_Q * GR_BLOCK + t] = make_float4(e.q[0], e.q[1], e.q[2], e.q[3]);
+        if ((t & 63) == 0) oflag[t >> 6] = 0;
+      }
       commit();  // barrier 1: the table is first needed by the collision test
 #ifndef GR_ABL_NOCOLL
-      ccount = collision_count(a, sl.tab, e.type, e.lvl, e.p, e.q);
+      uint32_t cm = collision_mask<false>(a, sl.tab, e.type, e.lvl, e.p, e.q, ObstGrid{});
+      if (OBST) {
+        // wait for the partner policy wave's obstacle mask (same 64 envs); it is resident and never waits on us
+        // (bounded: a protocol bug must not hang the GPU; the parity tests would catch its result)
+        for (int spin = 0; spin < (1 << 22); ++spin) {
+          if (__hip_atomic_load(oflag + (t >> 6), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        cm |= (uint32_t)__float_as_int(obx[O_MASK * GR_BLOCK + t].x);
+      }
+      ccount = __builtin_popcount(cm);
 #endif
     } else {
+      ObstGrid og{};
+      if (OBST) og = obst_grid(a, e.type, e.lvl);
       commit();  // barrier 1: contacts are tested every substep
       float vb[3], fb[3] = {0.0f, 0.0f, tt[0]};
       quat_rotate_inverse(e.q, e.v, vb);
       for (int k = 0; k < 3; ++k) fb[k] = (fb[k] - (e.k2[k] * vb[k]) * gr_fabsf(vb[k])) - e.k1[k] * vb[k];
       for (int s = 0; s < c.decimation; ++s) {
         si_substep(m, Jp, fb, tt + 1, c.sim_dt, c.gravity, e.p, e.q, e.v, e.w, accl, al);
-        int cc = collision_count(a, sl.tab, e.type, e.lvl, e.p, e.q);
+        int cc = __builtin_popcount(collision_mask<OBST>(a, sl.tab, e.type, e.lvl, e.p, e.q, og));
         ccount = cc > ccount ? cc : ccount;
       }
     }
@@ -1024,16 +1149,55 @@ __global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KCons
     e.ep = is.x; e.acc = is.y; e.epoch = is.z;
     e.gate = is.w & 0xff; e.lvl = (is.w >> 8) & 0xff; e.type = (is.w >> 24) & 0xff;
     e.nl = r0.y;
-    commit();  // barrier 1 (joined at once: the physics and episode waves set its time)
-    STAMP(1);
-    // observation noise needs only the call counter: it runs while the physics waves collide
     ObsNoise on;
+    float4 hint = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    ObstGrid og{};
+    if constexpr (OBST) {
+      // Obstacles (the physics waves' registers are full, these are idle until the handover): the records
+      // of the hinted cell are fetched at entry, the test runs on the post-step pose after barrier 1.
+      hint = reinterpret_cast<const float4*>(a.buf.state)[GR_P_OHINT * (size_t)n + ii];
+      og = obst_grid(a, e.type, e.lvl);
+      const int hfirst = __float_as_int(hint.x), hcount = __float_as_int(hint.y) - 1;
+      float4 pre[GR_OBST_PRE][GR_OBST_FLOATS / 4];
+#pragma unroll
+      for (int j = 0; j < GR_OBST_PRE; ++j)
+#pragma unroll
+        for (int k = 0; k < GR_OBST_FLOATS / 4; ++k)
+          pre[j][k] = j < hcount ? a.obst_items[(size_t)(hfirst + j) * (GR_OBST_FLOATS / 4) + k]
+                                 : make_float4(0.0f, 0.0f, 0.0f, -1.0f);
+      obs_noise(a, gid, cnt, on);
+      STAMP(1);
+      commit();  // barrier 1
+      STAMP(2);
+      if (c.integrator == GR_INTEGRATOR_DD_EXPLICIT) {
+        const float4 p4 = obx[O_P * GR_BLOCK + t], q4 = obx[O_Q * GR_BLOCK + t];
+        const float pp[3] = {p4.x, p4.y, p4.z}, qq[4] = {q4.x, q4.y, q4.z, q4.w};
+        float A[3], B[3], Cz[3];
+        body_axes(a, qq, A, B, Cz);
+        uint32_t om = 0u;
+        if (obst_hint_holds(hint, pp, a.h.obst_span)) {
+#pragma unroll
+          for (int j = 0; j < GR_OBST_PRE; ++j)
+            if (j < hcount) om |= obst_one(pre[j], pp, A, B, Cz);
+          if (hcount > GR_OBST_PRE) om |= obst_list(a, hfirst, GR_OBST_PRE, hcount, pp, A, B, Cz);
+        } else {
+          om = obst_lookup(a, og, pp, A, B, Cz);
+        }
+        obx[O_MASK * GR_BLOCK + t] = make_float4(__int_as_float((int)om), 0.0f, 0.0f, 0.0f);
+        if ((t & 63) == 0) __hip_atomic_store(oflag + (t >> 6), 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      STAMP(12);
+    } else {
+      commit();  // barrier 1 (joined at once: the physics and episode waves set its time)
+      STAMP(1);
+      // observation noise needs only the call counter: it runs while the physics waves collide
 #ifndef GR_ABL_NOOBSNOISE
-    obs_noise(a, gid, cnt, on);
+      obs_noise(a, gid, cnt, on);
 #else
-    for (int k = 0; k < 3; ++k) on.vfac[k] = 1.0f;
-    on.qn[0] = 1.0f; on.qn[1] = on.qn[2] = on.qn[3] = 0.0f;
+      for (int k = 0; k < 3; ++k) on.vfac[k] = 1.0f;
+      on.qn[0] = 1.0f; on.qn[1] = on.qn[2] = on.qn[3] = 0.0f;
 #endif
+    }
     STAMP(2);
     // call counter for the observation-noise stream: double-buffered by call parity,
     // so this write never races with the reads of the current launch
@@ -1044,6 +1208,13 @@ __global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KCons
     const float aux = xch[X_PA * GR_BLOCK + t].w;
     const bool reset = xvd.w != 0.0f && live;
     merge_handover(xch, t, reset, e);
+    float4 next_hint = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if constexpr (OBST) {
+      // the next step's hint: the cell list of the post-step (or the next episode's start) position; its loads
+      // land while the policy row is computed
+      const ObstGrid ogn = reset ? obst_grid(a, e.type, e.lvl) : og;
+      next_hint = obst_hint_of(a, ogn, e.p);
+    }
     const float lc[4] = {xlc.x, xlc.y, xlc.z, xlc.w};
     gate_advance(a, sl.tab, e);
     STAMP(7);
@@ -1056,6 +1227,7 @@ __global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KCons
       if (live) a.buf.obs_aux[i] = aux;
     }
 #endif
+    if (OBST && live) reinterpret_cast<float4*>(a.buf.state)[GR_P_OHINT * (size_t)n + i] = next_hint;
 #ifndef GR_ABL_NOLOG
     wave_log_levels(a, threadIdx.x >> 6, live ? (float)e.lvl : 0.0f, live ? e.nl : 0.0f);
 #endif
@@ -1185,6 +1357,7 @@ __global__ __launch_bounds__(GR_BLOCK) void init_kernel(KArgs a, const KConst* _
     S[GR_P_PAR1 * n + i] = make_float4(e.Kd[0], e.Kd[1], e.Kd[2], e.mp);
     S[GR_P_PAR2 * n + i] = make_float4(e.ct[0], e.ct[1], e.ct[2], e.mc);
     S[GR_P_PAR3 * n + i] = make_float4(e.J[0], e.J[1], e.J[2], 0.0f);
+    S[GR_P_OHINT * n + i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // no obstacle hint
   }
   // initial observation buffers: last action = ctbr(0) (DiffActions._raw_actions starts at zero)
   float sc[4], of[4];
@@ -1304,11 +1477,17 @@ static hipError_t launch_env_mode(const KArgs& a, const float* actions, const ui
   const int g = grid_of(a.h.num_envs);
   const bool lds = a.h.lds_tab_vec > 0;
   if constexpr (MODE == KMODE_STEP) {
-    const size_t bytes = (size_t)a.h.lds_tab_vec * 16 + (size_t)(GR_XF4 + GR_RF4 + GR_SF4) * GR_BLOCK * 16;
-    if (lds)
-      hipLaunchKernelGGL(step_kernel<true>, dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
+    const bool obst = a.obst_items != nullptr;
+    const size_t bytes = (size_t)a.h.lds_tab_vec * 16 + (size_t)(GR_XF4 + GR_RF4 + GR_SF4) * GR_BLOCK * 16 +
+                         (obst ? (size_t)GR_OF4 * GR_BLOCK * 16 + 16 : 0);
+    if (lds && obst)
+      hipLaunchKernelGGL((step_kernel<true, true>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
+    else if (lds)
+      hipLaunchKernelGGL((step_kernel<true, false>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
+    else if (obst)
+      hipLaunchKernelGGL((step_kernel<false, true>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
     else
-      hipLaunchKernelGGL(step_kernel<false>, dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
+      hipLaunchKernelGGL((step_kernel<false, false>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
   } else {
     const size_t bytes = (size_t)a.h.lds_tab_vec * 16;
     if (lds)
@@ -1368,7 +1547,8 @@ hipError_t allow_large_lds() {
 #ifdef GR_ABL_NO_LDS_ATTR
   return hipSuccess;
 #endif
-  const void* ks[] = {reinterpret_cast<const void*>(&step_kernel<true>),
+  const void* ks[] = {reinterpret_cast<const void*>(&step_kernel<true, false>),
+                      reinterpret_cast<const void*>(&step_kernel<true, true>),
                       reinterpret_cast<const void*>(&env_kernel<KMODE_RESET, true>),
                       reinterpret_cast<const void*>(&env_kernel<KMODE_OBSERVE, true>)};
   for (const void* k : ks) {

@@ -36,6 +36,12 @@ class TerrainCfg:
     num_cols: int = 20            # types
     num_gates: int = 8
     max_init_terrain_level: int = 5
+    # walls / orbits / ground obstacles (add_obs / add_ground_obs of every sub-terrain cfg)
+    obstacles: bool = True
+    obstacle_cell: float = 2.0    # xy grid cell of the obstacle lists (m)
+    # EventCfg.reset_terrain (racing_ctbr_env.py:221-225): regenerate the terrain every
+    # 0.03 * 24 * 5000 s of simulated time (None: never)
+    regen_interval_s: float | None = 0.03 * 24 * 5000
 
 
 @dataclass

@@ -22,7 +22,7 @@ import torch
 
 from .. import _abi
 from .racing_cfg import RacingEnvCfg
-from .tracks import build_track_table
+from .tracks import build_tracks
 
 LOG_RING = 64
 
@@ -98,13 +98,11 @@ class RacingEnv:
         _abi.check(self._lib, None, self._lib.gr_create(C.byref(self._gcfg), C.byref(ctx)), "gr_create")
         self._ctx = ctx
 
-        # ---- track table (host-generated once, then device-resident) ----
-        gates, recs = build_track_table(num_types=cfg.terrain.num_cols, num_levels=cfg.terrain.num_rows,
-                                        num_gates=cfg.terrain.num_gates,
-                                        seed=cfg.terrain.seed + cfg.track_seed_offset)
-        self.track_gates = torch.from_numpy(gates).to(dev).contiguous()
-        self.track_records = torch.from_numpy(recs).to(dev).contiguous()
-        self._call("gr_bind_tracks", self.track_gates.data_ptr(), self.track_records.data_ptr())
+        # ---- track table + obstacles (host-generated, then device-resident) ----
+        self.terrain_generation = 0
+        self._load_terrain(cfg.terrain.seed + cfg.track_seed_offset)
+        interval = cfg.terrain.regen_interval_s
+        self._regen_steps = None if interval is None else max(1, int(round(interval / self.step_dt)))
 
         # ---- state (SoA float4 planes) and outputs ----
         n = self.num_envs
@@ -146,6 +144,42 @@ class RacingEnv:
         self._bind(0)
         self._call("gr_init", self._stream())
         self._calls, self._cur = 1, 1  # gr_init wrote output set 1 (binding 0); counters zeroed
+
+    # ------------------------------------------------------------------ terrain
+    def _load_terrain(self, seed: int):
+        """Generate the track table (gates + obstacles) for `seed` and bind it (gr_bind_tracks,
+        gr_bind_obstacles).  The tables are copied / referenced by the context; the tensors stay
+        alive on the env."""
+        t = self.cfg.terrain
+        gates, recs, obst = build_tracks(num_types=t.num_cols, num_levels=t.num_rows, num_gates=t.num_gates,
+                                         seed=seed, obstacles=t.obstacles, cell=t.obstacle_cell)
+        dev = self.device
+        self.track_gates = torch.from_numpy(gates).to(dev).contiguous()
+        self.track_records = torch.from_numpy(recs).to(dev).contiguous()
+        self._call("gr_bind_tracks", self.track_gates.data_ptr(), self.track_records.data_ptr())
+        self.obstacle_table = obst
+        if obst is None:
+            self.obstacles = None
+            self._call("gr_bind_obstacles", None)
+            return
+        self.obstacles = {k: torch.from_numpy(getattr(obst, k)).to(dev).contiguous()
+                          for k in ("records", "counts", "grid_f", "grid_i", "cells", "items")}
+        o = _abi.GrObstacles()
+        for k, v in self.obstacles.items():
+            setattr(o, k, v.data_ptr())
+        o.max_obstacles = obst.max_obstacles
+        o.num_cells = int(obst.cells.shape[0])
+        o.num_items = int(obst.items.shape[0])
+        self._obst_struct = o
+        self._call("gr_bind_obstacles", C.byref(o))
+
+    def regenerate_terrain(self):
+        """EventCfg.reset_terrain -> reset_terrain_period (mdp/events.py:180-204): a new terrain
+        (next seed of this shard's stream), then env.reset() of every env."""
+        torch.cuda.current_stream(self.device).synchronize()  # the old tables may still be read
+        self.terrain_generation += 1
+        self._load_terrain(self.cfg.terrain.seed + self.cfg.track_seed_offset + 1000003 * self.terrain_generation)
+        return self.reset()
 
     # ------------------------------------------------------------------ plumbing
     @staticmethod
@@ -316,7 +350,13 @@ class RacingEnv:
         self._render(_abi.GR_CAM_STEP)
         self.common_step_counter += 1
         self.extras = {"log": log}
-        return self._obs_dict(out), out["reward"], out["terminated"], out["time_out"], self.extras
+        res = (self._obs_dict(out), out["reward"], out["terminated"], out["time_out"], self.extras)
+        if self._regen_steps is not None and self.common_step_counter % self._regen_steps == 0:
+            # interval event after the step (IL EventManager "interval" mode); the step's own outputs
+            # are returned, the next step starts on the new terrain
+            self.regenerate_terrain()
+            res[4]["terrain_regenerated"] = True
+        return res
 
     def reset(self, seed: int | None = None, env_ids=None, options=None):
         """ManagerBasedEnv.reset -> _reset_idx(env_ids) (+ curriculum), then observations."""

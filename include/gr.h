@@ -63,7 +63,9 @@ extern "C" {
 #define GR_P_PAR2 12  /* torque filter coefficients exp(-dt/tau_tau) xyz, controller mass */
 #define GR_P_PAR3 13  /* plant inertia diag xyz, spare */
 #define GR_P_MOTOR 14 /* rotor speeds (motor model only) */
-#define GR_NUM_PLANES 15
+#define GR_P_OHINT 15 /* obstacle tracks only: the obstacle-grid list of the env's cell (int first, int count + 1,
+                         lower corner x, y of the cell grown by the margin); all-zero = no hint */
+#define GR_NUM_PLANES 16
 /* int plane [num_envs][4] int32: episode_length, accumulate_gates, epoch, packed */
 #define GR_I_EPLEN 0
 #define GR_I_ACC 1
@@ -73,6 +75,12 @@ extern "C" {
 #define GR_OBS_DIM 16
 #define GR_GATE_FLOATS 20 /* per-gate record, see DESIGN.md "track table" */
 #define GR_TRACK_FLOATS 4 /* per-track record: ground_z, origin_z, start_gate, num_gates */
+#define GR_OBST_FLOATS 20 /* per-obstacle record, see generalizableracing_amd/csrc/gr_obstacles.h */
+/* obstacle primitive kinds (record float 16) */
+#define GR_OBST_BOX 0
+#define GR_OBST_CYLINDER 1
+#define GR_OBST_SPHERE 2
+#define GR_OBST_CAPSULE 3
 
 /* ---- log slots (extras["log"]) ---- */
 #define GR_LOG_NRESET 0
@@ -256,6 +264,28 @@ int gr_bytes_per_env_step(const gr_ctx* ctx, int64_t* read_bytes, int64_t* writt
  * track index = type * num_levels + level (the reference stores gate_pose as
  * [col=type][row=level], terrain_importer.py:150-153). */
 int gr_bind_tracks(gr_ctx* ctx, const float* gates, const float* tracks);
+
+/* Track obstacles (caller-owned device memory, kept alive while bound): the walls, orbits and
+ * ground obstacles the reference's sub-terrain generators add to the terrain mesh
+ * (extensions/diff.lab/diff/lab/terrains/trimesh/racing_terrains.py:87-150,254-319,510-610,
+ * 750-815; primitives trimesh/utils.py:35-131).  They count in the collision test (PhysX
+ * contact, racing_ctbr_env.py:253-256,306-311) and in the depth camera (the terrain mesh the
+ * RayCasterCamera casts against).  Records: GR_OBST_FLOATS each (gr_obstacles.h).
+ * Per track a uniform xy grid over the obstacles: cell (ix, iy) of track k is
+ * cells[grid_i[k].z + iy * grid_i[k].x + ix] = (first item, item count) into `items`, which
+ * holds copies of the records whose cull sphere reaches into that cell. */
+typedef struct gr_obstacles {
+  const float* records;   /* [num_types*num_levels][max_obstacles][GR_OBST_FLOATS] */
+  const int32_t* counts;  /* [num_types*num_levels] obstacles per track */
+  const float* grid_f;    /* [num_types*num_levels][4]: x0, y0 (env-local), 1/cell, cell */
+  const int32_t* grid_i;  /* [num_types*num_levels][4]: nx, ny, first cell, 0 */
+  const int32_t* cells;   /* [num_cells][2]: first item, item count */
+  const float* items;     /* [num_items][GR_OBST_FLOATS] */
+  int32_t max_obstacles, num_cells, num_items, reserved;
+} gr_obstacles;
+/* obst == NULL unbinds (obstacle-free tracks).  Validates counts and the grid (host copies of
+ * the small index arrays). */
+int gr_bind_obstacles(gr_ctx* ctx, const gr_obstacles* obst);
 int gr_bind_buffers(gr_ctx* ctx, const gr_buffers* bufs);
 
 /* startup: nominal state, startup DR (gains/delays/mass/inertia), initial levels */

@@ -20,6 +20,7 @@
 #include "gr_oracle.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
@@ -141,11 +142,12 @@ static int track_start(const gro_tracks* tr, int track) { return (int)track_rec(
  * count the 17 lattice points (utils/__init__.py:19-37) of the drone box that
  * lie inside a gate frame (outer box minus the through-hole, trimesh/utils.py:10-33)
  * or below the ground plane. */
-static const float LATTICE[17][3] = {
-    {0, 0, 0},          {1, 1, 1},         {1, -1, 1},        {-1, 1, 1},       {-1, -1, 1},     {1, 1, -1},
-    {1, -1, -1},        {-1, 1, -1},       {-1, -1, -1},      {0.5f, 0.5f, 0.5f}, {0.5f, -0.5f, 0.5f},
-    {-0.5f, 0.5f, 0.5f}, {-0.5f, -0.5f, 0.5f}, {0.5f, 0.5f, -0.5f}, {0.5f, -0.5f, -0.5f}, {-0.5f, 0.5f, -0.5f},
-    {-0.5f, -0.5f, -0.5f}};
+static const float LATTICE[17][3] = GR_LATTICE_INIT;
+
+static const float* obst_rec(const gro_tracks* tr, int track, int j) {
+  return tr->obst + ((size_t)track * tr->max_obst + j) * GR_OBST_FLOATS;
+}
+static int track_num_obst(const gro_tracks* tr, int track) { return tr->obst ? tr->obst_count[track] : 0; }
 
 /* Lattice point k = p + (lx*A + ly*B) + lz*C with A, B, C = quat_rotate(q, scaled body
  * axes) — quat_rotate is linear, so this is the reference's center + quat_rotate(q, vec)
@@ -166,6 +168,11 @@ int gro_collision_count(const gr_config* c, const gro_tracks* tr, int track, con
   quat_rotate(q, ex, A);
   quat_rotate(q, ey, B);
   quat_rotate(q, ez, Cz);
+  /* obstacles (walls / orbits / ground obstacles, trimesh/racing_terrains.py:87-150 et al.):
+   * every obstacle of the track, no culling */
+  uint32_t obst_mask = 0u;
+  const int no = track_num_obst(tr, track);
+  for (int j = 0; j < no; ++j) obst_mask |= gr_obst_lattice_mask(obst_rec(tr, track, j), p, A, B, Cz, LATTICE);
   int count = 0;
   for (int k = 0; k < 17; ++k) {
     const float lx = LATTICE[k][0], ly = LATTICE[k][1], lz = LATTICE[k][2];
@@ -186,7 +193,7 @@ int gro_collision_count(const gr_config* c, const gro_tracks* tr, int track, con
       int in_hole = (a0 < gr[7]) & (a1 < gr[11]);
       inside = in_outer & !in_hole; /* frame = outer box minus the through-hole */
     }
-    count += inside;
+    count += inside | (int)((obst_mask >> k) & 1u);
   }
   return count;
 }
@@ -823,6 +830,10 @@ void gro_camera(const gr_config* c, const gr_camera_config* kcfg, const gro_env*
       const int ng = track_num_gates(tr, track);
       float slot[GR_CAM_MAX_GATES][GR_CAM_SLOT];
       for (int g = 0; g < ng; ++g) gr_cam_gate_setup(gate_rec(c, tr, track, g), o, c0, c1, c2, K.max_distance, slot[g]);
+      const int no = track_num_obst(tr, track);
+      float* oslot = (float*)malloc(sizeof(float) * GR_CAM_SLOT * (size_t)(no > 0 ? no : 1));
+      for (int j = 0; j < no; ++j)
+        gr_cam_obst_setup(obst_rec(tr, track, j), o, c0, c1, c2, K.max_distance, oslot + (size_t)j * GR_CAM_SLOT);
       for (int k = 0; k < npix; ++k) {
         const int v = k / W, u = k % W;
         const float a = K.ray_a[u], b = K.ray_b[v];
@@ -834,8 +845,15 @@ void gro_camera(const gr_config* c, const gr_camera_config* kcfg, const gro_env*
           if (b >= sl[GR_CS_BMIN] && b <= sl[GR_CS_BMAX] && a >= sl[GR_CS_AMIN] && a <= sl[GR_CS_AMAX])
             d = gr_minf(d, gr_cam_gate_hit(sl, a, b));
         }
+        for (int j = 0; j < no; ++j) {
+          const float* sl = oslot + (size_t)j * GR_CAM_SLOT;
+          if (sl[GR_CS_VALID] == 0.0f) continue;
+          if (b >= sl[GR_CS_BMIN] && b <= sl[GR_CS_BMAX] && a >= sl[GR_CS_AMIN] && a <= sl[GR_CS_AMAX])
+            d = gr_minf(d, gr_cam_obst_hit(sl, a, b));
+        }
         dep[k] = gr_cam_clip(d, K.max_distance);
       }
+      free(oslot);
     }
     float* rp = out_p + (size_t)i * row;
     float* rc = out_c + (size_t)i * row;
@@ -873,6 +891,14 @@ float gro_camera_ray(const gr_config* c, const gr_camera_config* kcfg, const gro
     if (sl[GR_CS_VALID] == 0.0f) continue;
     if (b >= sl[GR_CS_BMIN] && b <= sl[GR_CS_BMAX] && a >= sl[GR_CS_AMIN] && a <= sl[GR_CS_AMAX])
       d = gr_minf(d, gr_cam_gate_hit(sl, a, b));
+  }
+  const int no = track_num_obst(tr, track);
+  for (int j = 0; j < no; ++j) {
+    float sl[GR_CAM_SLOT];
+    gr_cam_obst_setup(obst_rec(tr, track, j), o, c0, c1, c2, K.max_distance, sl);
+    if (sl[GR_CS_VALID] == 0.0f) continue;
+    if (b >= sl[GR_CS_BMIN] && b <= sl[GR_CS_BMAX] && a >= sl[GR_CS_AMIN] && a <= sl[GR_CS_AMAX])
+      d = gr_minf(d, gr_cam_obst_hit(sl, a, b));
   }
   return gr_cam_clip(d, K.max_distance);
 }

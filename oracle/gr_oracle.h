@@ -42,6 +42,9 @@ typedef struct gro_out {
 typedef struct gro_tracks {
   const float* gates;  /* [T*L][G][20] */
   const float* tracks; /* [T*L][4] */
+  const float* obst;         /* [T*L][max_obst][GR_OBST_FLOATS] (NULL: no obstacles) */
+  const int32_t* obst_count; /* [T*L] */
+  int32_t max_obst;
 } gro_tracks;
 
 size_t gro_env_size(void);

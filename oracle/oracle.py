@@ -79,20 +79,36 @@ class GroOut(C.Structure):
 
 
 class GroTracks(C.Structure):
-    _fields_ = [("gates", C.c_void_p), ("tracks", C.c_void_p)]
+    _fields_ = [("gates", C.c_void_p), ("tracks", C.c_void_p), ("obst", C.c_void_p), ("obst_count", C.c_void_p),
+                ("max_obst", C.c_int32)]
+
+
+def from_env(env):
+    """An Oracle over the same config and tables as a device RacingEnv (gates, records, obstacles)."""
+    ot = getattr(env, "obstacle_table", None)
+    return Oracle(env.gr_config, env.track_gates.cpu().numpy(), env.track_records.cpu().numpy(),
+                  None if ot is None else ot.records, None if ot is None else ot.counts)
 
 
 class Oracle:
-    """Stateful CPU env mirroring the device env (same config struct, same track table)."""
+    """Stateful CPU env mirroring the device env (same config struct, same track table).
+    obst_records [T*L][M][20] / obst_counts [T*L]: the obstacle table (None: no obstacles)."""
 
-    def __init__(self, cfg, gates: np.ndarray, recs: np.ndarray):
+    def __init__(self, cfg, gates: np.ndarray, recs: np.ndarray, obst_records: np.ndarray | None = None,
+                 obst_counts: np.ndarray | None = None):
         self.lib = load()
         self.cfg = cfg  # generalizableracing_amd._abi.GrConfig (plain ctypes struct)
         n = cfg.num_envs
         self.n = n
         self.gates = np.ascontiguousarray(gates, dtype=np.float32)
         self.recs = np.ascontiguousarray(recs, dtype=np.float32)
-        self.tracks = GroTracks(_p(self.gates), _p(self.recs))
+        if obst_records is not None:
+            self.obst = np.ascontiguousarray(obst_records, dtype=np.float32)
+            self.obst_counts = np.ascontiguousarray(obst_counts, dtype=np.int32)
+            self.tracks = GroTracks(_p(self.gates), _p(self.recs), _p(self.obst), _p(self.obst_counts),
+                                    self.obst.shape[1])
+        else:
+            self.tracks = GroTracks(_p(self.gates), _p(self.recs), None, None, 0)
         self.envs = np.zeros(n, dtype=ENV_DTYPE)
         self.obs_policy = np.zeros((n, 16), np.float32)
         self.obs_critic = np.zeros((n, 16), np.float32)

@@ -26,14 +26,14 @@ def build():
     os.makedirs(OUT, exist_ok=True)
     cmd = (f"/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off "
            f"-fhip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize -DGR_STAMPS -shared -o {OUT}/libgr.so "
-           f"{CSRC}/gr_kernels.hip -x hip {CSRC}/gr_capi.cpp")
+           f"{CSRC}/gr_kernels.hip {CSRC}/gr_camera.hip -x hip {CSRC}/gr_capi.cpp")
     subprocess.run(cmd, shell=True, check=True)
 
 
 ROLE_PHASES = {
     "physics": [("loads+integrate", 0, 3), ("barrier1+collision", 3, 4), ("termination+handover", 4, 5),
                 ("barrier2+reward+stores", 5, 12), ("log", 12, 8)],
-    "policy": [("loads+barrier1", 0, 1), ("obs_noise", 1, 2), ("barrier2_wait", 2, 13),
+    "policy": [("loads(+obstacle prefetch)", 0, 1), ("barrier1 / obs_noise", 1, 2), ("barrier2_wait", 2, 13),
                ("merge+advance", 13, 7), ("policy_obs+log", 7, 8)],
     "episode": [("loads+reset_draws", 0, 1), ("barrier1", 1, 2), ("reset_apply+xr", 2, 6),
                 ("barrier2_wait", 6, 13), ("merge+advance+istate", 13, 14), ("critic_obs", 14, 8)],
@@ -50,7 +50,8 @@ def run(n=65536, steps=200):
     sys.path.insert(0, ROOT)
     import bench
 
-    env = bench.make_env(n, 0, "cuda:0", 8, "dd_explicit")
+    obst = os.environ.get("GR_STAMPS_OBST", "1") == "1"
+    env = bench.make_env(n, 0, "cuda:0", 8, "dd_explicit", obst)
     g = torch.Generator(device="cuda:0").manual_seed(0)
     acts = torch.randn(bench.ACTION_RING, n, 4, device="cuda:0", generator=g)
     for k in range(steps):

@@ -12,7 +12,7 @@ import torch
 import oracle
 from generalizableracing_amd import _abi
 from generalizableracing_amd.envs.racing_cfg import CameraCfg, RacingEnvCfg, SceneCfg, SimCfg, TerrainCfg
-from generalizableracing_amd.envs.tracks import build_track_table
+from generalizableracing_amd.envs.tracks import build_tracks
 
 
 class OracleVecEnv:
@@ -22,8 +22,8 @@ class OracleVecEnv:
                                 terrain=TerrainCfg(num_cols=types, num_rows=levels), seed=seed,
                                 env_id_offset=env_id_offset, track_seed_offset=track_seed_offset)
         c = self.cfg.to_gr_config()
-        gates, recs = build_track_table(num_types=types, num_levels=levels, num_gates=8, seed=42 + track_seed_offset)
-        self.orc = oracle.Oracle(c, gates, recs)
+        gates, recs, ot = build_tracks(num_types=types, num_levels=levels, num_gates=8, seed=42 + track_seed_offset)
+        self.orc = oracle.Oracle(c, gates, recs, ot.records, ot.counts)
         self.orc.init()
         self.camera = camera
         if camera is not None:

@@ -13,17 +13,18 @@ pytestmark = pytest.mark.gpu
 
 import oracle  # noqa: E402
 from generalizableracing_amd import _abi  # noqa: E402
-from generalizableracing_amd.envs.racing_cfg import CameraCfg, RacingEnvCfg, SceneCfg, SimCfg  # noqa: E402
+from generalizableracing_amd.envs.racing_cfg import CameraCfg, RacingEnvCfg, SceneCfg, SimCfg, TerrainCfg  # noqa: E402
 from generalizableracing_amd.envs.racing_env import RacingEnv  # noqa: E402
 from test_gpu_parity import assert_envs_equal, bits, kernel_envs  # noqa: E402
 
 DEV = "cuda:0"
 
 
-def make(n, **cam):
-    cfg = RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV), camera=CameraCfg(**cam))
+def make(n, gates=8, **cam):
+    cfg = RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV), camera=CameraCfg(**cam),
+                       terrain=TerrainCfg(num_gates=gates))
     env = RacingEnv(cfg)
-    orc = oracle.Oracle(env.gr_config, env.track_gates.cpu().numpy(), env.track_records.cpu().numpy())
+    orc = oracle.from_env(env)
     orc.init()
     orc.enable_camera(env._cam_cfg)
     return env, orc
@@ -91,6 +92,7 @@ def test_camera_no_noise_and_every_step_period():
         env.step(torch.from_numpy(a).to(DEV))
         orc.step(a)
         orc.camera(_abi.GR_CAM_STEP)
+        assert_envs_equal(kernel_envs(env), orc.envs, f"step {k}")
         compare(env, orc, f"step {k}")
         assert (orc.cam_age == 0).all()
     obs = env.obs_buf
@@ -131,4 +133,43 @@ def test_camera_full_size_properties():
         else:
             assert frac < 0.1, frac  # only the envs reset this step
         prev_depth = env.depth.clone()
+    env.close()
+
+
+def test_camera_obstacles_in_view_and_slot_overflow():
+    """Drones placed just behind obstacles looking at them (obstacles fill the image), on 32-gate tracks
+    whose obstacle count exceeds the 64 LDS slots per wave: the re-setup path for obstacles beyond the
+    slots must give the oracle's bits too."""
+    n = 256
+    env, orc = make(n, gates=32)
+    env.reset()
+    orc.reset(None)
+    orc.camera(_abi.GR_CAM_RESET)
+    compare(env, orc, "reset")
+    ot = env.obstacle_table
+    torch.cuda.synchronize()
+    e = kernel_envs(env)
+    rng = np.random.default_rng(4)
+    L = env.cfg.terrain.num_rows
+    for i in range(n):
+        k = int(e["type"][i]) * L + int(e["level"][i])
+        j = rng.integers(ot.counts[k])
+        c = ot.records[k, j, :3].astype(np.float64)
+        yaw = rng.uniform(-np.pi, np.pi)
+        back = c - 2.5 * np.array([np.cos(yaw), np.sin(yaw), 0.0])
+        e["p"][i] = back.astype(np.float32)
+        e["q"][i] = np.array([np.cos(yaw / 2), 0, 0, np.sin(yaw / 2)], np.float32)
+    st, ist = oracle.envs_to_planes(e, env.state.shape[0])
+    env.state.copy_(torch.from_numpy(st).to(DEV))
+    env.istate.copy_(torch.from_numpy(ist).to(DEV))
+    orc.envs[:] = e
+    # every sensor outdated: the next observe call re-renders all of them from the placed poses
+    env.camera_age.fill_(-1)
+    orc.cam_age[:] = -1
+    env.observe()
+    orc.observe()
+    orc.camera(_abi.GR_CAM_OBSERVE)
+    compare(env, orc, "placed observe")
+    assert (orc.depth < 4.0).mean() > 0.05
+    assert ot.counts.max() > 64
     env.close()

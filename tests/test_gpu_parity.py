@@ -39,11 +39,11 @@ def kernel_envs(env):
     return oracle.planes_to_envs(env.state.cpu().numpy(), env.istate.cpu().numpy())
 
 
-def make(n, stage=1, integrator="dd_explicit", gates=8, **ov):
+def make(n, stage=1, integrator="dd_explicit", gates=8, obstacles=True, **ov):
     cfg = RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV), stage=stage, integrator=integrator,
-                       terrain=TerrainCfg(num_gates=gates), overrides=ov)
+                       terrain=TerrainCfg(num_gates=gates, obstacles=obstacles), overrides=ov)
     env = RacingEnv(cfg)
-    orc = oracle.Oracle(env.gr_config, env.track_gates.cpu().numpy(), env.track_records.cpu().numpy())
+    orc = oracle.from_env(env)
     orc.init()
     return env, orc
 
@@ -63,6 +63,7 @@ CONFIGS = [
     dict(stage=2),
     dict(stage=1, use_motor_model=1),
     dict(stage=1, gates=32),
+    dict(stage=1, obstacles=False),
 ]
 
 
@@ -71,7 +72,7 @@ def test_env_free_run_bit_exact(conf):
     n, steps = 1000, 120
     conf = dict(conf)
     env, orc = make(n, stage=conf.pop("stage"), integrator=conf.pop("integrator", "dd_explicit"),
-                    gates=conf.pop("gates", 8), **conf)
+                    gates=conf.pop("gates", 8), obstacles=conf.pop("obstacles", True), **conf)
     assert_envs_equal(kernel_envs(env), orc.envs, "init")
     compare_outputs(env, orc, "init")
     env.reset()
@@ -140,7 +141,8 @@ def test_full_size_teacher_forced_slices():
         c = _abi.GrConfig.from_buffer_copy(base)
         c.num_envs = m
         c.env_id_offset = i0
-        orc = oracle.Oracle(c, env.track_gates.cpu().numpy(), env.track_records.cpu().numpy())
+        ot = env.obstacle_table
+        orc = oracle.Oracle(c, env.track_gates.cpu().numpy(), env.track_records.cpu().numpy(), ot.records, ot.counts)
         orc.envs[:] = pre
         orc.obs_critic[:] = prev_crit
         orc.counter[0] = cnt
@@ -158,4 +160,77 @@ def test_full_size_teacher_forced_slices():
     assert (e["level"] >= 0).all() and (e["level"] < 10).all()
     assert (e["gate_id"] >= 0).all() and (e["gate_id"] < 8).all()
     assert (e["ep_len"] >= 0).all() and (e["ep_len"] < 200).all()
+    env.close()
+
+
+def test_obstacle_collisions_teacher_forced():
+    """Drones placed in and around the obstacles of their own tracks (walls, orbits, ground obstacles):
+    one step must match the oracle (which tests every obstacle, no grid) bit for bit, and many of the
+    placed drones must collide."""
+    n = 4096
+    env, _ = make(n)
+    env.reset()
+    torch.cuda.synchronize()
+    ot = env.obstacle_table
+    e = kernel_envs(env)
+    rng = np.random.default_rng(9)
+    L = env.cfg.terrain.num_rows
+    for i in range(n):
+        k = int(e["type"][i]) * L + int(e["level"][i])
+        j = rng.integers(ot.counts[k])
+        rec = ot.records[k, j]
+        e["p"][i] = (rec[:3] + rng.uniform(-1, 1, 3) * (rec[17] + 0.08)).astype(np.float32)
+        q = rng.normal(size=4)
+        e["q"][i] = (q / np.linalg.norm(q)).astype(np.float32)
+        e["v"][i] = 0.0
+    st, ist = oracle.envs_to_planes(e, env.state.shape[0])
+    env.state.copy_(torch.from_numpy(st).to(DEV))
+    env.istate.copy_(torch.from_numpy(ist).to(DEV))
+    prev_crit = env.obs_buf["critic"].cpu().numpy()
+    cnt = int(env._counters[env._calls % 2].item())
+    orc = oracle.from_env(env)
+    orc.envs[:] = e
+    orc.obs_critic[:] = prev_crit
+    orc.counter[0] = cnt
+    a = np.zeros((n, 4), np.float32)
+    _, rew, term, tout, _ = env.step(torch.from_numpy(a).to(DEV))
+    orc.step(a)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(rew.cpu().numpy()), bits(orc.reward))
+    assert np.array_equal(term.cpu().numpy().astype(np.uint8), orc.terminated)
+    assert_envs_equal(kernel_envs(env), orc.envs, "obstacle step")
+    assert orc.terminated.mean() > 0.2, orc.terminated.mean()
+    env.close()
+
+
+def test_terrain_regeneration_matches_oracle():
+    """EventCfg.reset_terrain: after the interval the env regenerates its tracks (new layouts and
+    obstacles) and resets every env; the oracle over the new tables agrees bit for bit."""
+    n = 512
+    cfg = RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV), stage=1,
+                       terrain=TerrainCfg(regen_interval_s=0.03 * 5))
+    env = RacingEnv(cfg)
+    env.reset()
+    g0 = env.track_gates.clone()
+    g = torch.Generator().manual_seed(1)
+    for k in range(5):
+        _, _, _, _, extras = env.step(torch.randn(n, 4, generator=g).to(DEV))
+    assert extras.get("terrain_regenerated") and env.terrain_generation == 1
+    assert not torch.equal(g0, env.track_gates)
+    orc = oracle.from_env(env)
+    torch.cuda.synchronize()
+    orc.envs[:] = kernel_envs(env)
+    orc.obs_critic[:] = env.obs_buf["critic"].cpu().numpy()
+    orc.counter[0] = int(env._counters[env._calls % 2].item())
+    assert (orc.envs["ep_len"] == 0).all()
+    for k in range(4):  # the 5th step regenerates again
+        a = (torch.randn(n, 4, generator=g)).numpy().astype(np.float32)
+        _, _, _, _, extras = env.step(torch.from_numpy(a).to(DEV))
+        orc.step(a)
+        torch.cuda.synchronize()
+        assert_envs_equal(kernel_envs(env), orc.envs, f"after regen step {k}")
+        assert not extras.get("terrain_regenerated")
+    _, _, _, _, extras = env.step(torch.randn(n, 4, generator=g).to(DEV))
+    assert extras.get("terrain_regenerated") and env.terrain_generation == 2
+    assert bool((env.episode_length_buf == 0).all())
     env.close()
