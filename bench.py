@@ -46,8 +46,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=64)
     p.add_argument("--num-envs", type=int, default=65536)
     p.add_argument("--gates", type=int, default=8)
-    p.add_argument("--obstacles", type=int, default=1, help="1: the reference task's walls / orbits / ground "
-                   "obstacles (add_obs, add_ground_obs); 0: gates and ground only")
+    p.add_argument("--obstacles", type=int, default=0, help="1: the reference task's walls / orbits / ground "
+                   "obstacles (add_obs, add_ground_obs); 0: gates and ground only (BASELINE config C3).  The "
+                   "default line also reports the obstacle variant under 'with_obstacles'")
     p.add_argument("--integrator", default="dd_explicit")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="skip policy/train/cpu legs (profiling runs)")
@@ -231,8 +232,8 @@ def load_traffic(n, gates, obstacles):
     if not os.path.exists(path):
         return None
     try:
-        d = json.load(open(path))
-        if d.get("num_envs") == n and d.get("gates", 8) == gates and d.get("obstacles", 0) == obstacles:
+        d = json.load(open(path)).get("obstacles" if obstacles else "gates_only", {})
+        if d.get("num_envs") == n and d.get("gates", 8) == gates:
             return d.get("bytes_per_launch")
     except Exception:
         return None
@@ -269,19 +270,41 @@ def main():
     if not a.no_extras:
         extra["policy_in_loop_env_steps_per_s"] = policy_in_loop(env, 256, device)
     env.close()
+    if not a.no_extras and not a.obstacles:
+        # the reference task's terrain also carries walls / orbits / ground obstacles:
+        # the same step over obstacle tracks (grid-listed collision, per-env cell hints)
+        env_o = make_env(n, rank, device, a.gates, a.integrator, True)
+        for k in range(a.warmup):
+            env_o.step(actions[k % ACTION_RING])
+        torch.cuda.synchronize()
+        secs_o, mode_o, graph_o = time_env_steps(env_o, actions, a.steps, not a.no_graph)
+        secs_o = max_over_ranks(secs_o, device)
+        kt_o = kernel_timing(env_o, actions, a.steps, graph_o)
+        del graph_o
+        rd_o, wr_o = env_o.bytes_per_env_step()
+        extra["with_obstacles"] = {
+            "value": n * ws * a.steps / secs_o, "unit": "env-steps/s", "kernel": "gr::step_kernel<true, true>",
+            "kernel_us": kt_o["kernel_us"], "bytes_per_env_step": {"read": rd_o, "written": wr_o},
+            "achieved_GBps": (rd_o + wr_o) * n / (kt_o["kernel_us"] * 1e-6) / 1e9,
+            "traffic": load_traffic(n, a.gates, 1),
+            "obstacles_per_track_max": int(env_o.obstacle_table.counts.max()),
+            "obstacles_per_track_mean": float(env_o.obstacle_table.counts.mean())}
+        env_o.close()
     if not a.no_extras:
         extra["train_total_fps_4096_envs"] = train_fps(device)
         # the depth camera of the vision task (separate kernel, same env shard size)
         sys.path.insert(0, os.path.join(ROOT, "scripts"))
         import bench_camera
 
-        cam = bench_camera.run(n, steps=24, warmup=4, device=device)
-        extra["vision_camera"] = {
-            "kernel": cam["kernel"], "image": cam["image"], "render_fraction": cam["render_fraction"],
-            "ms_per_call": cam["ms_avg_call"], "ms_render_call": cam["ms_render_call"],
-            "ms_reuse_call": cam["ms_reuse_call"], "achieved_GBps": cam["gbs_avg"], "peak_GBps": HBM_PEAK_GBS,
-            "frac": cam["hbm_frac_avg"], "bytes_per_env_call": [cam["bytes_per_env_render"], cam["bytes_per_env_reuse"]],
-            "env_steps_per_s_step_plus_camera": cam["wall_env_steps_per_s_step_plus_camera"]}
+        for key, obst in (("vision_camera", False), ("vision_camera_with_obstacles", True)):
+            cam = bench_camera.run(n, steps=24, warmup=4, device=device, obstacles=obst)
+            extra[key] = {
+                "kernel": cam["kernel"], "image": cam["image"], "render_fraction": cam["render_fraction"],
+                "ms_per_call": cam["ms_avg_call"], "ms_render_call": cam["ms_render_call"],
+                "ms_reuse_call": cam["ms_reuse_call"], "achieved_GBps": cam["gbs_avg"], "peak_GBps": HBM_PEAK_GBS,
+                "frac": cam["hbm_frac_avg"],
+                "bytes_per_env_call": [cam["bytes_per_env_render"], cam["bytes_per_env_reuse"]],
+                "env_steps_per_s_step_plus_camera": cam["wall_env_steps_per_s_step_plus_camera"]}
     cpu = None
     if rank == 0 and ws == 1 and not a.no_extras:
         cpu = cpu_baseline(a.cpu_seconds, obstacles=bool(a.obstacles))
@@ -307,7 +330,7 @@ def main():
                        "num_envs_per_gpu": n, "launch": mode, "parallelism": f"env-shard x{ws}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "gr::step_kernel<true> (fused step)", **kt,
+                         "kernel": f"gr::step_kernel<true, {'true' if a.obstacles else 'false'}> (fused step)", **kt,
                          "algorithmic_bytes_per_launch": (rd + wr) * n,
                          "bytes_per_env_step": {"read": rd, "written": wr}},
             "cpu_baseline": cpu,

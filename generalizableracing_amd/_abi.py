@@ -242,6 +242,8 @@ def _declare(lib):
         "gr_camera_bytes_per_env": (C.c_int, [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     }
     for name, (res, args) in sig.items():
+        if not hasattr(lib, name) and os.environ.get("GR_LIB_PATH"):
+            continue  # an older timing build (GR_LIB_PATH) may predate an entry point
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args

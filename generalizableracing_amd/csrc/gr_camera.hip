@@ -54,13 +54,15 @@ DEV_INLINE void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// obstacle slot from LDS (GR_CAM_OSLOT floats: frame, primitive, window, valid)
+// obstacle slot from LDS (GR_CAM_OSLOT floats: frame and primitive = slot floats 0-15, window = 17-20)
 DEV_INLINE void load_oslot(const float4* src, float s[GR_CAM_SLOT]) {
 #pragma unroll
-  for (int k = 0; k < GR_CAM_OSLOT / 4; ++k) {
+  for (int k = 0; k < 4; ++k) {
     const float4 q4 = src[k];
     s[4 * k] = q4.x; s[4 * k + 1] = q4.y; s[4 * k + 2] = q4.z; s[4 * k + 3] = q4.w;
   }
+  const float4 w4 = src[4];
+  s[GR_CS_AMIN] = w4.x; s[GR_CS_AMAX] = w4.y; s[GR_CS_BMIN] = w4.z; s[GR_CS_BMAX] = w4.w;
 }
 
 // the obstacle's record from global memory
@@ -90,6 +92,8 @@ DEV_INLINE void quad_obst(const float* s, const float av[4], float b, float d[4]
 #else
 #define CAM_ATTR
 #endif
+// OBST: the track carries obstacles (a separate instantiation, so the gate-only kernel keeps its code)
+template <bool OBST>
 __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs a) {
   extern __shared__ float4 smem4[];
   float* smem = reinterpret_cast<float*>(smem4);
@@ -106,11 +110,13 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
   const int i = blockIdx.x * CAM_WAVES + w;
   const bool active = i < a.num_envs;
   const int N = a.num_envs;
-  const bool obst = a.obst != nullptr;
-  const int oslots = obst ? GR_CAM_OBST_SLOTS * GR_CAM_OSLOT : 0;
+  constexpr bool obst = OBST;
+  const int ntx = (W + 31) / 32, nty = (H + 7) / 8;
+  const int oslots = obst ? (int)camera_obst_floats(W, H) : 0;
   float* wave_lds = smem + wpad + hpad + w * (G * GR_CAM_SLOT + oslots + 8 * W);
   float4* s_slot = reinterpret_cast<float4*>(wave_lds);                             // [G][CAM_SLOT4]
   float4* s_oslot = reinterpret_cast<float4*>(wave_lds + G * GR_CAM_SLOT);          // [64][GR_CAM_OSLOT / 4]
+  uint64_t* s_tmask = reinterpret_cast<uint64_t*>(wave_lds + G * GR_CAM_SLOT + GR_CAM_OBST_SLOTS * GR_CAM_OSLOT);
   float4* s_stage = reinterpret_cast<float4*>(wave_lds + G * GR_CAM_SLOT + oslots);  // [8 * W / 4]
 
   // ---- is the sensor outdated? (SensorBase.update / reset; wave-uniform)
@@ -134,7 +140,7 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
   float o[3] = {0.0f, 0.0f, 0.0f}, c0[3] = {1.0f, 0.0f, 0.0f}, c1[3] = {0.0f, 1.0f, 0.0f},
         c2[3] = {0.0f, 0.0f, 1.0f};
   float gz = 0.0f;
-  uint64_t valid_mask = 0, omask = 0;
+  uint64_t valid_mask = 0;
   const float* orecs = nullptr;  // this track's obstacle records
   int nob = 0, ofrom = 0;         // obstacles in the track; raw index of the first one beyond the slots
   if (render) {
@@ -158,7 +164,7 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
         s_slot[lane * CAM_SLOT4 + k] = make_float4(s[4 * k], s[4 * k + 1], s[4 * k + 2], s[4 * k + 3]);
     }
     valid_mask = __ballot(valid);
-    if (obst) {
+    if constexpr (obst) {
       // obstacles in view: the first GR_CAM_OBST_SLOTS go to LDS slots (compacted by ballot); from the
       // next one on (rare) they are set up again per tile
       nob = a.obst_counts[track];
@@ -178,8 +184,9 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
         const int pos = nv + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
         if (ok && pos < GR_CAM_OBST_SLOTS) {
 #pragma unroll
-          for (int q = 0; q < GR_CAM_OSLOT / 4; ++q)
+          for (int q = 0; q < 4; ++q)
             s_oslot[pos * (GR_CAM_OSLOT / 4) + q] = make_float4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
+          s_oslot[pos * (GR_CAM_OSLOT / 4) + 4] = make_float4(s[GR_CS_AMIN], s[GR_CS_AMAX], s[GR_CS_BMIN], s[GR_CS_BMAX]);
         }
         const int nb = __popcll(b);
         if (nv + nb > GR_CAM_OBST_SLOTS && ofrom == nob) {
@@ -190,7 +197,20 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
         nv += nb;
       }
       const int ns = nv < GR_CAM_OBST_SLOTS ? nv : GR_CAM_OBST_SLOTS;
-      omask = ns == 64 ? ~0ull : ((1ull << ns) - 1ull);
+      // per 8x32 tile: the slots whose window meets the tile's ray range (a_u, b_v decrease with u, v)
+      wave_lds_sync();
+      for (int tl = lane; tl < ntx * nty; tl += 64) {
+        const int v0 = 8 * (tl / ntx), u0 = 32 * (tl % ntx);
+        const int v1 = (v0 + 7 < H ? v0 + 7 : H - 1), u1 = (u0 + 31 < W ? u0 + 31 : W - 1);
+        const float a_hi = cc->ray_a[u0], a_lo = cc->ray_a[u1], b_hi = cc->ray_b[v0], b_lo = cc->ray_b[v1];
+        uint64_t tm = 0;
+        for (int k = 0; k < ns; ++k) {
+          const float4 wk = s_oslot[k * (GR_CAM_OSLOT / 4) + 4];
+          const bool meet = !(wk.y < a_lo || wk.x > a_hi || wk.w < b_lo || wk.z > b_hi);
+          tm |= (uint64_t)meet << k;
+        }
+        s_tmask[tl] = tm;
+      }
     }
   }
   __syncthreads();
@@ -263,8 +283,8 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
             if (av[j] >= s[GR_CS_AMIN] && av[j] <= s[GR_CS_AMAX]) d[j] = gr_minf(d[j], gr_cam_gate_hit(s, av[j], b));
         }
       }
-      if (obst) {
-        uint64_t mo = omask;
+      if constexpr (obst) {
+        uint64_t mo = s_tmask[(v0 >> 3) * ntx + (u_t >> 5)];
         while (mo) {
           const int k = __builtin_ctzll(mo);
           mo &= mo - 1;
@@ -295,8 +315,12 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
 
 hipError_t launch_camera(const CamArgs& a, hipStream_t s) {
   const int blocks = (a.num_envs + CAM_WAVES - 1) / CAM_WAVES;
-  hipLaunchKernelGGL(camera_kernel, dim3(blocks), dim3(CAM_WAVES * 64),
-                     camera_lds_bytes(a.width, a.height, a.max_gates, a.obst != nullptr), s, a);
+  if (a.obst != nullptr)
+    hipLaunchKernelGGL(camera_kernel<true>, dim3(blocks), dim3(CAM_WAVES * 64),
+                       camera_lds_bytes(a.width, a.height, a.max_gates, true), s, a);
+  else
+    hipLaunchKernelGGL(camera_kernel<false>, dim3(blocks), dim3(CAM_WAVES * 64),
+                       camera_lds_bytes(a.width, a.height, a.max_gates, false), s, a);
   return hipGetLastError();
 }
 

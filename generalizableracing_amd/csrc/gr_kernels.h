@@ -88,12 +88,16 @@ hipError_t launch_camera(const CamArgs& a, hipStream_t s);
 // obstacle slots per camera wave (the first GR_CAM_OBST_SLOTS obstacles in view; any further ones
 // are set up again per tile from their records)
 #define GR_CAM_OBST_SLOTS 64
-#define GR_CAM_OSLOT 24  // floats per obstacle slot (the gate slot layout, gr_camera.h / gr_obstacles.h)
+#define GR_CAM_OSLOT 20  // floats per obstacle slot in LDS: gate-slot floats 0-15, then the window (17-20)
 // dynamic LDS of the camera kernel: ray tables + per wave (gate slots [+ obstacle slots] + an 8-row
 // staging band)
+// obstacle slots + one 64-bit mask per 8x32 tile (the slots whose window meets the tile)
+__host__ __device__ inline size_t camera_obst_floats(int width, int height) {
+  return (size_t)GR_CAM_OBST_SLOTS * GR_CAM_OSLOT + 2 * (size_t)((height + 7) / 8) * ((width + 31) / 32);
+}
 inline size_t camera_lds_bytes(int width, int height, int max_gates, bool obst) {
   const size_t wpad = (size_t)((width + 3) & ~3), hpad = (size_t)((height + 3) & ~3);
-  const size_t os = obst ? (size_t)GR_CAM_OBST_SLOTS * GR_CAM_OSLOT : 0;
+  const size_t os = obst ? camera_obst_floats(width, height) : 0;
   return 4 * (wpad + hpad + 4 * ((size_t)max_gates * 24 + os + 8 * (size_t)width));
 }
 

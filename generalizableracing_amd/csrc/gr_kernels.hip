@@ -198,9 +198,6 @@ constexpr float c_lattice[17][3] = GR_LATTICE_INIT;
 #ifndef GR_OBST_BATCH
 #define GR_OBST_BATCH 4  // obstacle cull spheres loaded per batch
 #endif
-#ifndef GR_OBST_PRE
-#define GR_OBST_PRE 2  // obstacle records of the hinted cell held in registers from kernel entry
-#endif
 
 // ------------------------------------------------------------- obstacles
 // Per track a uniform xy grid; cell lists hold copies of every record whose cull sphere reaches into
@@ -228,26 +225,37 @@ DEV int obst_cell(const ObstGrid& og, const float p[3], int& cx, int& cy) {
   return og.i.z + cy * og.i.x + cx;
 }
 // lattice mask of one record (cull sphere first)
-DEV uint32_t obst_one(const float4 r4[GR_OBST_FLOATS / 4], const float p[3], const float A[3], const float B[3],
-                      const float C[3]) {
+// (cull sphere, then the primitive grown by the lattice reach, then the 17 points)
+DEV uint32_t obst_one(const KArgs& a, const float4 r4[GR_OBST_FLOATS / 4], const float p[3], const float A[3],
+                      const float B[3], const float C[3]) {
   float r[GR_OBST_FLOATS];
 #pragma unroll
   for (int k = 0; k < GR_OBST_FLOATS / 4; ++k) {
     r[4 * k] = r4[k].x; r[4 * k + 1] = r4[k].y; r[4 * k + 2] = r4[k].z; r[4 * k + 3] = r4[k].w;
   }
-  return gr_obst_near(r, p) ? gr_obst_lattice_mask(r, p, A, B, C, c_lattice) : 0u;
+  if (!(gr_obst_near(r, p) && gr_obst_maybe(r, p, a.kc->lat_reach))) return 0u;
+  return gr_obst_lattice_mask(r, p, A, B, C, c_lattice);
 }
-// lattice mask of the list items [first + from, first + count): cull spheres in batches of independent
-// loads, full records only for the spheres that hold p
-DEV uint32_t obst_list(const KArgs& a, int first, int from, int count, const float p[3], const float A[3],
+// the cull spheres of list items [first + j0, first + j0 + GR_OBST_BATCH) (w = -1 past the end)
+DEV void obst_spheres(const KArgs& a, int first, int j0, int count, float4 sp[GR_OBST_BATCH]) {
+#pragma unroll
+  for (int j = 0; j < GR_OBST_BATCH; ++j)
+    sp[j] = j0 + j < count ? a.obst_items[(size_t)(first + j0 + j) * (GR_OBST_FLOATS / 4)]
+                           : make_float4(0.0f, 0.0f, 0.0f, -1.0f);
+}
+// lattice mask of the list items [first, first + count): cull spheres in batches of independent loads (the
+// first batch may come prefetched), full records only for the spheres that hold p
+DEV uint32_t obst_list(const KArgs& a, int first, int count, const float4* pre, const float p[3], const float A[3],
                        const float B[3], const float C[3]) {
   uint32_t m = 0u;
-  for (int j0 = from; j0 < count; j0 += GR_OBST_BATCH) {
+  for (int j0 = 0; j0 < count; j0 += GR_OBST_BATCH) {
     float4 sp[GR_OBST_BATCH];
+    if (pre != nullptr && j0 == 0) {
 #pragma unroll
-    for (int j = 0; j < GR_OBST_BATCH; ++j)
-      sp[j] = j0 + j < count ? a.obst_items[(size_t)(first + j0 + j) * (GR_OBST_FLOATS / 4)]
-                             : make_float4(0.0f, 0.0f, 0.0f, -1.0f);
+      for (int j = 0; j < GR_OBST_BATCH; ++j) sp[j] = pre[j];
+    } else {
+      obst_spheres(a, first, j0, count, sp);
+    }
     uint32_t near = 0u;
 #pragma unroll
     for (int j = 0; j < GR_OBST_BATCH; ++j) {
@@ -261,7 +269,7 @@ DEV uint32_t obst_list(const KArgs& a, int first, int from, int count, const flo
       float4 rr[GR_OBST_FLOATS / 4];
 #pragma unroll
       for (int k = 0; k < GR_OBST_FLOATS / 4; ++k) rr[k] = r4[k];
-      m |= obst_one(rr, p, A, B, C);
+      m |= obst_one(a, rr, p, A, B, C);
     }
   }
   return m;
@@ -273,7 +281,7 @@ DEV uint32_t obst_lookup(const KArgs& a, const ObstGrid& og, const float p[3], c
   const int c = obst_cell(og, p, cx, cy);
   if (c < 0) return 0u;
   const int2 ce = a.obst_cells[c];
-  return obst_list(a, ce.x, 0, ce.y, p, A, B, C);
+  return obst_list(a, ce.x, ce.y, nullptr, p, A, B, C);
 }
 // the hint of a position: its cell's list and the grown cell's lower corner (0: outside the grid)
 DEV float4 obst_hint_of(const KArgs& a, const ObstGrid& og, const float p[3]) {
@@ -1005,8 +1013,10 @@ __global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KCons
         if ((t & 63) == 0) oflag[t >> 6] = 0;
       }
       commit();  // barrier 1: the table is first needed by the collision test
+      STAMP(14);
 #ifndef GR_ABL_NOCOLL
       uint32_t cm = collision_mask<false>(a, sl.tab, e.type, e.lvl, e.p, e.q, ObstGrid{});
+      STAMP(15);
       if (OBST) {
         // wait for the partner policy wave's obstacle mask (same 64 envs); it is resident and never waits on us
         // (bounded: a protocol bug must not hang the GPU; the parity tests would catch its result)
@@ -1158,14 +1168,8 @@ __global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KCons
       hint = reinterpret_cast<const float4*>(a.buf.state)[GR_P_OHINT * (size_t)n + ii];
       og = obst_grid(a, e.type, e.lvl);
       const int hfirst = __float_as_int(hint.x), hcount = __float_as_int(hint.y) - 1;
-      float4 pre[GR_OBST_PRE][GR_OBST_FLOATS / 4];
-#pragma unroll
-      for (int j = 0; j < GR_OBST_PRE; ++j)
-#pragma unroll
-        for (int k = 0; k < GR_OBST_FLOATS / 4; ++k)
-          pre[j][k] = j < hcount ? a.obst_items[(size_t)(hfirst + j) * (GR_OBST_FLOATS / 4) + k]
-                                 : make_float4(0.0f, 0.0f, 0.0f, -1.0f);
-      obs_noise(a, gid, cnt, on);
+      float4 psp[GR_OBST_BATCH];  // cull spheres of the hinted list's first batch
+      obst_spheres(a, hfirst, 0, hcount, psp);
       STAMP(1);
       commit();  // barrier 1
       STAMP(2);
@@ -1175,18 +1179,22 @@ __global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KCons
         float A[3], B[3], Cz[3];
         body_axes(a, qq, A, B, Cz);
         uint32_t om = 0u;
+#ifdef GR_ABL_OBST_NOTEST
+        if (false) {
+#else
         if (obst_hint_holds(hint, pp, a.h.obst_span)) {
-#pragma unroll
-          for (int j = 0; j < GR_OBST_PRE; ++j)
-            if (j < hcount) om |= obst_one(pre[j], pp, A, B, Cz);
-          if (hcount > GR_OBST_PRE) om |= obst_list(a, hfirst, GR_OBST_PRE, hcount, pp, A, B, Cz);
+#endif
+          om = obst_list(a, hfirst, hcount, psp, pp, A, B, Cz);
         } else {
+#ifndef GR_ABL_OBST_NOTEST
           om = obst_lookup(a, og, pp, A, B, Cz);
+#endif
         }
         obx[O_MASK * GR_BLOCK + t] = make_float4(__int_as_float((int)om), 0.0f, 0.0f, 0.0f);
         if ((t & 63) == 0) __hip_atomic_store(oflag + (t >> 6), 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       STAMP(12);
+      obs_noise(a, gid, cnt, on);  // off the critical path: needed after barrier 2
     } else {
       commit();  // barrier 1 (joined at once: the physics and episode waves set its time)
       STAMP(1);
@@ -1197,8 +1205,8 @@ __global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KCons
       for (int k = 0; k < 3; ++k) on.vfac[k] = 1.0f;
       on.qn[0] = 1.0f; on.qn[1] = on.qn[2] = on.qn[3] = 0.0f;
 #endif
+      STAMP(2);
     }
-    STAMP(2);
     // call counter for the observation-noise stream: double-buffered by call parity,
     // so this write never races with the reads of the current launch
     if (t == 0 && blockIdx.x == 0) a.buf.counters[a.buf.counter_index ^ 1] = cnt + 1u;
@@ -1212,8 +1220,10 @@ __global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KCons
     if constexpr (OBST) {
       // the next step's hint: the cell list of the post-step (or the next episode's start) position; its loads
       // land while the policy row is computed
+#ifndef GR_ABL_OBST_NOHINT
       const ObstGrid ogn = reset ? obst_grid(a, e.type, e.lvl) : og;
       next_hint = obst_hint_of(a, ogn, e.p);
+#endif
     }
     const float lc[4] = {xlc.x, xlc.y, xlc.z, xlc.w};
     gate_advance(a, sl.tab, e);

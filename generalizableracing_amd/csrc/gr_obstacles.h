@@ -84,6 +84,26 @@ GR_HD uint32_t gr_obst_lattice_mask(const float* r, const float p[3], const floa
   return m;
 }
 
+/* tighter cull (kernel only; the oracle tests every obstacle): can a point within `reach` of p be
+ * inside the primitive?  p in the primitive frame (the expression the lattice test uses for its
+ * centre term) against the primitive grown by reach: per-axis slabs for the box and the cylinder's
+ * height, radii + reach for the round parts.  Contains the Minkowski sum primitive (+) ball(reach),
+ * so it never rejects a primitive a lattice point is inside. */
+GR_HD int gr_obst_maybe(const float* r, const float p[3], float reach) {
+  const float d[3] = {p[0] - r[0], p[1] - r[1], p[2] - r[2]};
+  float l[3];
+  gr_obst_frame(r, d, l);
+  const int kind = (int)r[16];
+  const float a0 = gr_fabsf(l[0]), a1 = gr_fabsf(l[1]), a2 = gr_fabsf(l[2]);
+  const float e0 = r[7] + reach, e1 = r[11] + reach, rr = e0 * e0;
+  const float radial = l[0] * l[0] + l[1] * l[1];
+  const float dz = gr_maxf(a2 - r[15], 0.0f);
+  const int box = (a0 <= e0) & (a1 <= e1) & (a2 <= r[15] + reach);
+  const int cyl = (radial <= rr) & (a2 <= r[15] + reach);
+  const int rnd = radial + (kind == GR_OBST_SPHERE ? l[2] * l[2] : dz * dz) <= rr;
+  return kind == GR_OBST_BOX ? box : kind == GR_OBST_CYLINDER ? cyl : rnd;
+}
+
 /* cull: can any lattice point of a drone at p be inside?  (|p - c|^2 <= cull radius^2) */
 GR_HD int gr_obst_near(const float* r, const float p[3]) {
   const float dx = p[0] - r[0], dy = p[1] - r[1], dz = p[2] - r[2];

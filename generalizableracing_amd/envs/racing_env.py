@@ -160,7 +160,8 @@ class RacingEnv:
         self.obstacle_table = obst
         if obst is None:
             self.obstacles = None
-            self._call("gr_bind_obstacles", None)
+            if hasattr(self._lib, "gr_bind_obstacles"):  # (older timing builds predate obstacles)
+                self._call("gr_bind_obstacles", None)
             return
         self.obstacles = {k: torch.from_numpy(getattr(obst, k)).to(dev).contiguous()
                           for k in ("records", "counts", "grid_f", "grid_i", "cells", "items")}

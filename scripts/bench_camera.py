@@ -21,18 +21,19 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from generalizableracing_amd import _abi  # noqa: E402
-from generalizableracing_amd.envs.racing_cfg import CameraCfg, RacingEnvCfg, SceneCfg, SimCfg  # noqa: E402
+from generalizableracing_amd.envs.racing_cfg import CameraCfg, RacingEnvCfg, SceneCfg, SimCfg, TerrainCfg  # noqa: E402
 from generalizableracing_amd.envs.racing_env import RacingEnv  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
-def run(n=65536, steps=40, warmup=6, no_noise=False, period=None, device="cuda:0") -> dict:
+def run(n=65536, steps=40, warmup=6, no_noise=False, period=None, device="cuda:0", obstacles=True) -> dict:
     args = argparse.Namespace(envs=n, steps=steps, warmup=warmup, no_noise=no_noise, period=period)
     cam = CameraCfg(add_noise=not args.no_noise)
     if args.period is not None:
         cam.update_period = args.period
-    env = RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=device), camera=cam))
+    env = RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=device), camera=cam,
+                                 terrain=TerrainCfg(obstacles=obstacles)))
     env.reset()
     g = torch.Generator(device=device).manual_seed(1234)
     acts = [torch.randn(n, 4, device=device, generator=g) for _ in range(8)]

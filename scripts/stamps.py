@@ -31,9 +31,11 @@ def build():
 
 
 ROLE_PHASES = {
-    "physics": [("loads+integrate", 0, 3), ("barrier1+collision", 3, 4), ("termination+handover", 4, 5),
+    "physics": [("loads+integrate", 0, 3), ("barrier1", 3, 14), ("gate_collision", 14, 15),
+                ("obstacle_wait", 15, 4), ("termination+handover", 4, 5),
                 ("barrier2+reward+stores", 5, 12), ("log", 12, 8)],
-    "policy": [("loads(+obstacle prefetch)", 0, 1), ("barrier1 / obs_noise", 1, 2), ("barrier2_wait", 2, 13),
+    "policy": [("loads(+obstacle prefetch)", 0, 1), ("barrier1 / obs_noise", 1, 2), ("obstacle_test", 2, 12),
+               ("barrier2_wait", 12, 13),
                ("merge+advance", 13, 7), ("policy_obs+log", 7, 8)],
     "episode": [("loads+reset_draws", 0, 1), ("barrier1", 1, 2), ("reset_apply+xr", 2, 6),
                 ("barrier2_wait", 6, 13), ("merge+advance+istate", 13, 14), ("critic_obs", 14, 8)],

@@ -18,7 +18,7 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "gr::step_kernel<true>"
+KERNEL = "gr::step_kernel<true, false>"  # <USE_LDS, OBST>; --obstacles selects <true, true>
 
 
 def pmc_means(prof):
@@ -46,7 +46,13 @@ def main():
     p.add_argument("--gates", type=int, default=8)
     p.add_argument("--read-bytes", type=int, default=256, help="algorithmic bytes read per env-step")
     p.add_argument("--write-bytes", type=int, default=290, help="algorithmic bytes written per env-step")
+    p.add_argument("--obstacles", action="store_true", help="obstacle tracks (kernel <true, true>, +16 B r/w hint)")
     a = p.parse_args()
+    global KERNEL
+    if a.obstacles:
+        KERNEL = "gr::step_kernel<true, true>"
+        a.read_bytes += 16
+        a.write_bytes += 16
     prof = os.path.join(ROOT, "gpurun_out", f"prof_{a.tag}")
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
@@ -58,7 +64,7 @@ def main():
             avg_ns = float(r["AverageNs"])
     m, counts, meta = pmc_means(prof)
     n = a.num_envs
-    d = {"kernel": "gr::step_kernel<true> (fused step)", "num_envs": n, "gates": a.gates,
+    d = {"kernel": f"{KERNEL} (fused step)", "num_envs": n, "gates": a.gates, "obstacles": int(a.obstacles),
          "launches_per_counter": counts, "dispatch": meta, "raw_means": m, "trace_avg_ns": avg_ns}
     if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
         rd = m["FETCH_SIZE"] * 1024 * 2  # KB; gfx950 reports half of a coalesced streaming read
@@ -67,9 +73,14 @@ def main():
         alg = (a.read_bytes + a.write_bytes) * n
         d["algorithmic_bytes_per_launch"] = alg
         d["traffic_over_algorithmic"] = (rd + wr) / alg
-        json.dump({"num_envs": n, "gates": a.gates, "bytes_per_launch": rd + wr, "read": rd, "write": wr,
-                   "source": f"profiles/{a.name}_pmc.json"},
-                  open(os.path.join(out, "pmc_traffic.json"), "w"), indent=1)
+        tpath = os.path.join(out, "pmc_traffic.json")
+        key = "obstacles" if a.obstacles else "gates_only"
+        allt = json.load(open(tpath)) if os.path.exists(tpath) else {}
+        if "bytes_per_launch" in allt:  # old single-entry format
+            allt = {}
+        allt[key] = {"num_envs": n, "gates": a.gates, "obstacles": int(a.obstacles), "bytes_per_launch": rd + wr,
+                     "read": rd, "write": wr, "source": f"profiles/{a.name}_pmc.json"}
+        json.dump(allt, open(tpath, "w"), indent=1)
     if "SQ_WAVES" in m:
         waves = m["SQ_WAVES"]
         per = {k: m[k] / waves for k in m if k.startswith("SQ_") and k != "SQ_WAVES"}
