@@ -183,6 +183,60 @@ def policy_in_loop(env, steps, device):
     return env.num_envs * steps / (time.perf_counter() - t0)
 
 
+def policy_in_loop_fused(env, steps, device):
+    """C5 "hipGraph-captured step + inference": per step, the fused MFMA inference of both MLPs
+    (FusedPolicyInference: actor mean + Gaussian sample + log prob, critic value; bf16 operands, fp32
+    accumulation) on the step's observations, then gr_step on the sampled actions; 64 such steps are
+    captured in one hipGraph and replayed.  Returns (env-steps/s, per-launch us of the inference kernel)."""
+    from generalizableracing_amd.rsl_rl import ActorCritic
+    from generalizableracing_amd.rsl_rl.fused_inference import FusedPolicyInference
+
+    n = env.num_envs
+    pol = ActorCritic(16, 16, 4, [256, 256], [256, 256], "lrelu").to(device)
+    fused = FusedPolicyInference(pol, n, device, env_id_offset=env.cfg.env_id_offset)
+
+    def one_step(obs):
+        acts = fused.act(obs["policy"], obs["critic"])[0]
+        return env.step(acts)[0]
+
+    obs = env.observe()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            obs = one_step(obs)
+    torch.cuda.current_stream().wait_stream(s)
+    while env._calls % ACTION_RING != 0 or fused._calls % 2 != 0:  # align the ping-pong bindings
+        obs = one_step(obs)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        o = obs
+        for _ in range(ACTION_RING):
+            o = one_step(o)
+    g.replay()
+    torch.cuda.synchronize()
+    reps = max(1, steps // ACTION_RING)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        g.replay()
+    torch.cuda.synchronize()
+    rate = n * reps * ACTION_RING / (time.perf_counter() - t0)
+    # the inference kernel alone (events on the current stream, 64 back-to-back launches)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    x = obs["policy"].clone()
+    for _ in range(4):
+        fused.act(x, x)
+    e0.record()
+    for _ in range(64):
+        fused.act(x, x)
+    e1.record()
+    e1.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / 64
+    flops = 2 * n * 2 * (16 * 256 + 256 * 256 + 256 * 4)  # actor + critic (critic out 1, padded rows free)
+    return rate, us, flops / (us * 1e-6) / 1e12
+
+
 def train_fps(device, n=4096, iters=3):
     """Config C2: 4 096 envs, rsl_rl PPO MLP(256,256) fp32, the reference's Perf/total_fps."""
     from generalizableracing_amd.envs.racing_env import RslRlVecEnvWrapper
@@ -269,6 +323,12 @@ def main():
     extra = {}
     if not a.no_extras:
         extra["policy_in_loop_env_steps_per_s"] = policy_in_loop(env, 256, device)
+        rate, us, tfs = policy_in_loop_fused(env, 512, device)
+        extra["policy_in_loop_fused"] = {
+            "env_steps_per_s": rate, "launch": "hipgraph (64 x [fused inference + gr_step])",
+            "inference_kernel": "gr::policy_kernel<256> (MFMA 16x16x32 bf16, fp32 accumulate)",
+            "inference_kernel_us": us, "inference_TFLOPs": tfs,
+            "note": "actor+critic MLP(16-256-256-out), Gaussian sample + log prob; bf16 operands (C5)"}
     env.close()
     if not a.no_extras and not a.obstacles:
         # the reference task's terrain also carries walls / orbits / ground obstacles:

@@ -193,6 +193,20 @@ class GrObstacles(C.Structure):
                 ("num_items", C.c_int32), ("reserved", C.c_int32)]
 
 
+class GrPolicyNet(C.Structure):
+    _fields_ = [("obs", C.c_void_p), ("w1", C.c_void_p), ("b1", C.c_void_p), ("w2", C.c_void_p),
+                ("b2", C.c_void_p), ("w3", C.c_void_p), ("b3", C.c_void_p), ("out", C.c_void_p),
+                ("num_obs", C.c_int32), ("num_out", C.c_int32), ("reserved", C.c_int32 * 2)]
+
+
+class GrPolicyArgs(C.Structure):
+    _fields_ = [("net", GrPolicyNet * 2), ("std", C.c_void_p), ("actions", C.c_void_p), ("log_prob", C.c_void_p),
+                ("counters", C.c_void_p), ("counter_index", C.c_int32), ("num_envs", C.c_int32),
+                ("hidden", C.c_int32), ("activation", C.c_int32), ("env_id_offset", C.c_int32),
+                ("seed_lo", C.c_uint32), ("seed_hi", C.c_uint32)]
+
+
+GR_POLICY_ACT_LRELU, GR_POLICY_ACT_ELU = 0, 1
 GR_CAM_STEP, GR_CAM_RESET, GR_CAM_OBSERVE = 0, 1, 2
 
 EXPORTS = [
@@ -202,7 +216,7 @@ EXPORTS = [
     "gr_test_philox",
     "gr_debug_read_stamps",
     "gr_camera_config_default", "gr_camera_config_size", "gr_enable_camera", "gr_bind_camera_buffers",
-    "gr_camera_render", "gr_camera_bytes_per_env",
+    "gr_camera_render", "gr_camera_bytes_per_env", "gr_policy_forward",
 ]
 
 _lib = None
@@ -240,6 +254,7 @@ def _declare(lib):
         "gr_bind_camera_buffers": (C.c_int, [vp, C.POINTER(GrCameraBuffers)]),
         "gr_camera_render": (C.c_int, [vp, C.c_int, vp, vp]),
         "gr_camera_bytes_per_env": (C.c_int, [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+        "gr_policy_forward": (C.c_int, [C.POINTER(GrPolicyArgs), vp]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name) and os.environ.get("GR_LIB_PATH"):

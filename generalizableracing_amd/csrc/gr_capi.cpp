@@ -581,6 +581,24 @@ int gr_camera_bytes_per_env(const gr_ctx* c, int64_t* render_bytes, int64_t* reu
   return GR_OK;
 }
 
+int gr_policy_forward(const gr_policy_args* a, void* stream) {
+  if (!a || a->num_envs <= 0 || (a->hidden != 128 && a->hidden != 256) ||
+      (a->activation != GR_POLICY_ACT_LRELU && a->activation != GR_POLICY_ACT_ELU))
+    return GR_ERR_ARG;
+  for (int k = 0; k < 2; ++k) {
+    const gr_policy_net& n = a->net[k];
+    if (!n.obs || !n.w1 || !n.b1 || !n.w2 || !n.b2 || !n.w3 || !n.b3 || !n.out || n.num_obs <= 0 || n.num_obs > 32 ||
+        n.num_obs % 4 != 0 || !aligned16(n.obs) ||
+        n.num_out <= 0 || n.num_out > 4 || (k == 1 && n.num_out != 1))
+      return GR_ERR_ARG;
+    if (!aligned16(n.w1) || !aligned16(n.w2) || !aligned16(n.w3)) return GR_ERR_ARG;
+  }
+  if (!a->std || !a->actions || !a->log_prob || !a->counters || (a->counter_index != 0 && a->counter_index != 1))
+    return GR_ERR_ARG;
+  const hipError_t e = gr::launch_policy(*a, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
 int gr_test_dynamics(gr_ctx* c, int n, int mode, const float* si, const float* ab, const float* cmd, const float* ci,
                      const float* par, const float* drag, float* so, float* co, float* xo, void* stream) {
   if (!c || n <= 0 || !si || !ab || !cmd || !ci || !par || !drag || !so || !co || !xo) return GR_ERR_ARG;

@@ -85,6 +85,7 @@ struct CamArgs {
   float* out_c;
 };
 hipError_t launch_camera(const CamArgs& a, hipStream_t s);
+hipError_t launch_policy(const gr_policy_args& a, hipStream_t s);  // gr_policy.hip
 // obstacle slots per camera wave (the first GR_CAM_OBST_SLOTS obstacles in view; any further ones
 // are set up again per tile from their records)
 #define GR_CAM_OBST_SLOTS 64

@@ -122,5 +122,6 @@ GR_HD void gr_box_muller21(uint32_t f1, uint32_t f2, float* z0, float* z1) {
 #define GR_TAG_GATE 0x47415445u   /* gate-pose noise, counter1 = epoch, counter3 = gates passed */
 #define GR_TAG_OBS 0x4f425321u    /* observation noise, counter1 = call counter */
 #define GR_TAG_IMG 0x494d4721u    /* depth-image noise, counter1 = call counter, counter3 = pixel quad */
+#define GR_TAG_POLICY 0x504f4c21u /* action sampling of the fused policy inference, counter1 = call counter */
 
 #endif /* GR_RNG_H */

@@ -311,6 +311,39 @@ int gr_camera_render(gr_ctx* ctx, int mode, const uint8_t* mask, void* stream);
 /* algorithmic HBM bytes per env of one render call, with and without the re-render */
 int gr_camera_bytes_per_env(const gr_ctx* ctx, int64_t* render_bytes, int64_t* reuse_bytes);
 
+/*
+ * Rollout inference of the rsl_rl ActorCritic (PPO.act: standalone/rsl_rl/ext/algorithms/ppo.py:71-85
+ * -> ActorCritic.act / evaluate / get_actions_log_prob) on MFMA, bf16 operands, fp32 accumulation.
+ * Both MLPs (num_obs -> H -> H -> num_out, H = 128 or 256, LeakyReLU(0.01) or ELU) for all envs in
+ * one graph-capturable launch; the actor also samples Normal(mean, std) (Philox, keyed by env and
+ * `counter`) and sums the log prob over the actions.  Weights are packed by the caller into the
+ * kernel's fragment order (generalizableracing_amd/rsl_rl/fused_inference.py).  Context-free.
+ */
+#define GR_POLICY_ACT_LRELU 0
+#define GR_POLICY_ACT_ELU 1
+typedef struct gr_policy_net {
+  const float* obs; /* [num_envs][num_obs] fp32, 16-byte aligned, num_obs <= 32 and a multiple of 4 */
+  const void* w1;   /* bf16 fragments [H/16][64][8] */
+  const float* b1;  /* [H] */
+  const void* w2;   /* bf16 fragments [H/16][H/32][64][8] */
+  const float* b2;  /* [H] */
+  const void* w3;   /* bf16 fragments [H/32][64][8] (rows >= num_out zero) */
+  const float* b3;  /* [num_out] */
+  float* out;       /* actor: action mean [num_envs][num_out]; critic: value [num_envs] */
+  int32_t num_obs, num_out, reserved[2];
+} gr_policy_net;
+typedef struct gr_policy_args {
+  gr_policy_net net[2]; /* 0: actor (num_out = num_actions <= 4), 1: critic (num_out = 1) */
+  const float* std;     /* [num_actions] the policy's std */
+  float* actions;       /* [num_envs][num_actions] sampled actions */
+  float* log_prob;      /* [num_envs] */
+  uint32_t* counters;   /* [2] sampling call counter, double-buffered like gr_buffers.counters: this */
+  int32_t counter_index; /* call reads counters[i] and writes counters[i ^ 1] = counters[i] + 1 */
+  int32_t num_envs, hidden, activation, env_id_offset;
+  uint32_t seed_lo, seed_hi;
+} gr_policy_args;
+int gr_policy_forward(const gr_policy_args* args, void* stream);
+
 /* In-library HIP-event timing of the fused step kernel alone (not the log
  * finalize): when enabled, gr_step brackets the env kernel with a pair of
  * events on the caller's stream (ring of 4096 pairs; do not capture into a

@@ -1,0 +1,11 @@
+#!/bin/bash
+# GPU box: scripts/bench_policy.py for the in-tree libgr.so and every build/var/libgr_*.so.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/${1:-polvar}
+mkdir -p $OUT
+cd $R
+timeout -k 10 200 python scripts/bench_policy.py >> $OUT/pol.jsonl 2>> $OUT/pol.err || exit 3
+for so in build/var/libgr_*.so; do
+  GR_LIB_PATH=$R/$so timeout -k 10 200 python scripts/bench_policy.py >> $OUT/pol.jsonl 2>> $OUT/pol.err || exit 4
+done

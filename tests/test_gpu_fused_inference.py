@@ -1,0 +1,88 @@
+"""Fused MFMA rollout inference (gr_policy_forward) against the fp32 torch ActorCritic on the GPU.
+
+Tolerance: bf16 operands (8-bit mantissa) with fp32 accumulation over K = 16 / 256 / 256: the mean
+and the value must agree with the fp32 module to 2 % of the output scale; the log prob must be the
+one torch's Normal gives for the kernel's own (mean, std, action) to 1e-4."""
+from __future__ import annotations
+
+import os
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from generalizableracing_amd.rsl_rl import ActorCritic  # noqa: E402
+from generalizableracing_amd.rsl_rl.fused_inference import FusedPolicyInference  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.mark.parametrize("hidden,activation,n", [(256, "lrelu", 65536 + 17), (128, "elu", 1000)])
+def test_matches_fp32_module(hidden, activation, n):
+    torch.manual_seed(0)
+    pol = ActorCritic(16, 16, 4, [hidden, hidden], [hidden, hidden], activation, init_noise_std=0.7).to(DEV)
+    fused = FusedPolicyInference(pol, n, DEV, seed=3)
+    obs = torch.randn(n, 16, device=DEV) * 2.0
+    cobs = torch.randn(n, 16, device=DEV) * 2.0
+    act, val, logp, mean, sigma = fused.act(obs, cobs)
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        m_ref, v_ref = pol.actor(obs), pol.critic(cobs)
+    for got, want in ((mean, m_ref), (val, v_ref)):
+        scale = float(want.abs().max()) + 1e-3
+        err = float((got - want).abs().max())
+        assert err < 2e-2 * scale, (err, scale)
+    lp_ref = torch.distributions.Normal(mean, sigma).log_prob(act).sum(-1)
+    assert float((logp - lp_ref).abs().max()) < 1e-4
+    eps = (act - mean) / sigma
+    tol = 5.0 / (4 * n) ** 0.5  # 5 standard errors
+    assert abs(float(eps.mean())) < tol and abs(float(eps.std()) - 1.0) < 2 * tol
+    # a second call draws fresh noise; the same seed and counter reproduce it
+    a1 = act.clone()
+    fused.act(obs, cobs)
+    assert not torch.equal(a1, fused.actions)
+    other = FusedPolicyInference(pol, n, DEV, seed=3)
+    other.act(obs, cobs)
+    torch.cuda.synchronize()
+    assert torch.equal(a1, other.actions)
+
+
+def test_refresh_after_update_and_graph_capture():
+    torch.manual_seed(1)
+    n = 4096
+    pol = ActorCritic(16, 16, 4, [256, 256], [256, 256], "lrelu").to(DEV)
+    fused = FusedPolicyInference(pol, n, DEV)
+    obs = torch.randn(n, 16, device=DEV)
+    fused.act(obs, obs)
+    torch.cuda.synchronize()
+    m0 = fused.action_mean.clone()
+    with torch.no_grad():
+        for p in pol.actor.parameters():
+            p.add_(0.05 * torch.randn_like(p))
+    fused.refresh()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fused.act(obs, obs)  # warm-up outside capture (even call count)
+        fused.act(obs, obs)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fused.act(obs, obs)
+        fused.act(obs, obs)
+    g.replay()
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        want = pol.actor(obs)
+    assert not torch.allclose(m0, fused.action_mean)
+    assert float((fused.action_mean - want).abs().max()) < 2e-2 * (float(want.abs().max()) + 1e-3)
+    c0 = fused.counters.clone()
+    a0 = fused.actions.clone()
+    g.replay()
+    torch.cuda.synchronize()
+    assert int(fused.counters.max()) == int(c0.max()) + 2  # the device counter advances inside the graph
+    assert not torch.equal(a0, fused.actions)
