@@ -37,12 +37,34 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #ifndef POL_TG
 #define POL_TG 2  // layer-2 output row tiles per group: TG x COLS independent accumulator chains
 #endif
+#ifndef POL_PF
+#define POL_PF 1  // k steps of A-fragment prefetch (register ring of POL_PF + 1 fragments per row tile)
+#endif
+#ifdef POL_ABL_NOA
+#define POL_RING_IDX 0
+#else
+#define POL_RING_IDX (s % (PF + 1))
+#endif
+#ifndef POL_PIPE
+#define POL_PIPE 0  // 1: drain group g (activation, pack, layer 3) under group g + 1's first MFMAs
+#endif
+#ifndef POL_SB
+#define POL_SB 1  // scheduling barriers around each k step's MFMAs
+#endif
+#ifndef POL_STAGGER
+#define POL_STAGGER 0  // s_sleep units (64 cycles) by which waves 4-7 (the SIMD partners of 0-3) start late
+#endif
+#ifndef POL_PRIO
+#define POL_PRIO 0  // 1: s_setprio 1 for waves 4-7
+#endif
 #define POL_ENVS_PER_WAVE (16 * POL_COLS)
+static_assert(POL_COLS == 1 || POL_COLS == 2 || POL_COLS == 4, "the epilogue maps a wave's 16 C envs x 4 rows onto 64 lanes");
 
 template <int ACT>
 __device__ __forceinline__ float pol_act(float x) {
   // LeakyReLU (torch default slope 0.01) or ELU (alpha 1); compile-time, so the layer loops stay straight-line
-  if constexpr (ACT == GR_POLICY_ACT_ELU) return x > 0.0f ? x : expm1f(x);
+  // ELU's exp(x) - 1 on the hardware exp2 (absolute error ~1e-7, far below the bf16 rounding that follows)
+  if constexpr (ACT == GR_POLICY_ACT_ELU) return x > 0.0f ? x : __builtin_amdgcn_exp2f(x * 1.44269504f) - 1.0f;
   return fmaxf(x, 0.01f * x);  // = LeakyReLU(0.01) for every finite x: two VALU ops
 }
 
@@ -60,8 +82,16 @@ __device__ __forceinline__ f32x4 bias4(const float* b, int row0, int lane) {
 }
 template <int ACT>
 __device__ __forceinline__ void act4(f32x4& v) {
+  if constexpr (ACT == GR_POLICY_ACT_LRELU) {
+    // max(x, 0.01 x): the products as two packed v_pk_mul_f32; this file is built with -fno-honor-nans, so
+    // v_max_f32 reads the MFMA results without a canonicalizing copy (csrc/Makefile)
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const f32x2 lo = (f32x2){v[0], v[1]} * 0.01f, hi = (f32x2){v[2], v[3]} * 0.01f;
+    v[0] = fmaxf(v[0], lo[0]); v[1] = fmaxf(v[1], lo[1]); v[2] = fmaxf(v[2], hi[0]); v[3] = fmaxf(v[3], hi[1]);
+  } else {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] = pol_act<ACT>(v[r]);
+    for (int r = 0; r < 4; ++r) v[r] = pol_act<ACT>(v[r]);
+  }
 }
 
 // Per workgroup (one network, 8 waves x 64 envs): all weight fragments staged in LDS once
@@ -110,33 +140,53 @@ __global__ __launch_bounds__(POL_WAVES * 64) void policy_kernel(gr_policy_args p
   const uint32_t cnt = pa.counters[pa.counter_index];
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) pa.counters[pa.counter_index ^ 1] = cnt + 1u;
   __syncthreads();  // weights staged
-  // persistent over env tiles: the weights are staged once per workgroup
-  const int envs_per_block = POL_WAVES * POL_ENVS_PER_WAVE;
-  for (int base = blockIdx.x * envs_per_block; base < n; base += gridDim.x * envs_per_block) {
-  const int env0 = base + wave * POL_ENVS_PER_WAVE;
-  // layer-1 B fragments: obs^T, lane l holds obs[env0 + 16c + (l & 15)][8 (l >> 4) + j] (k < D, else 0).
-  // Two unconditional float4 loads per lane and column tile (rows clamped into range, num_obs % 4 == 0),
-  // all issued before the first is used.
-  bf16x8 xb[C];
-  {
-    float4 ld[C][2];
-    const int k0 = 8 * (lane >> 4);
-    const int kc = k0 < D ? k0 : 0;
+  // persistent over env tiles: the weights are staged once per workgroup.  Layer-1 B fragments: obs^T,
+  // lane l holds obs[env0 + 16c + (l & 15)][8 (l >> 4) + j] (k < D, else 0), from two unconditional
+  // float4 loads per lane and column tile (rows clamped into range, num_obs % 4 == 0).  The next tile's
+  // loads are issued before this tile's MLP, so their latency hides behind it.
+  const int envs_per_block = POL_WAVES * POL_ENVS_PER_WAVE, stride = gridDim.x * envs_per_block;
+  const int k0 = 8 * (lane >> 4), kc = k0 < D ? k0 : 0;
+  float4 ld[C][2];
+  auto load_obs = [&](int base) {
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      int env = env0 + 16 * c + (lane & 15);
+      int env = base + wave * POL_ENVS_PER_WAVE + 16 * c + (lane & 15);
       env = env < n ? env : n - 1;
       const float4* row = reinterpret_cast<const float4*>(net.obs + (size_t)env * D + kc);
       ld[c][0] = row[0];
       ld[c][1] = k0 + 4 < D ? row[1] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
+  };
+  // Epilogue lane map: a wave's 16 C envs x 4 output rows on its 64 lanes.  Lane L takes env e = L % (16 C)
+  // of the wave and the RPL = C rows RPL p .. RPL p + RPL - 1 (p = L / (16 C)).  Per-row sampling constants
+  // (actor): std, 1 / (2 var), -log(std) - log(sqrt(2 pi)).
+  constexpr int RPL = C;
+  const int p = lane / (16 * C), e_w = lane % (16 * C);
+  float sdv[RPL], i2v[RPL], lpc[RPL];
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const float v[8] = {ld[c][0].x, ld[c][0].y, ld[c][0].z, ld[c][0].w, ld[c][1].x, ld[c][1].y, ld[c][1].z, ld[c][1].w};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) xb[c][j] = (__bf16)(k0 + j < D ? v[j] : 0.0f);
-    }
+  for (int q = 0; q < RPL; ++q) {
+    const int r = RPL * p + q;
+    sdv[q] = blockIdx.y == 0 && r < net.num_out ? pa.std[r] : 1.0f;
+    i2v[q] = 1.0f / (2.0f * sdv[q] * sdv[q]);
+    lpc[q] = -logf(sdv[q]) - 0.91893853320467274f;
   }
+  load_obs(blockIdx.x * envs_per_block);
+#if POL_PRIO
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
+#if POL_STAGGER
+  if (wave >= 4) __builtin_amdgcn_s_sleep(POL_STAGGER);
+#endif
+  for (int base = blockIdx.x * envs_per_block; base < n; base += stride) {
+  const int env0 = base + wave * POL_ENVS_PER_WAVE;
+  bf16x8 xb[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const float v[8] = {ld[c][0].x, ld[c][0].y, ld[c][0].z, ld[c][0].w, ld[c][1].x, ld[c][1].y, ld[c][1].z, ld[c][1].w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xb[c][j] = (__bf16)(k0 + j < D ? v[j] : 0.0f);
+  }
+  if (base + stride < n) load_obs(base + stride);
   // ---- layer 1: h1^T = act(W1 x^T + b1), two row tiles at a time = one k step of layer 2
   bf16x8 h1[S][C];
 #pragma unroll
@@ -156,6 +206,22 @@ __global__ __launch_bounds__(POL_WAVES * 64) void policy_kernel(gr_policy_args p
 #pragma unroll
   for (int c = 0; c < C; ++c) o[c] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
   constexpr int TG = POL_TG;  // row tiles per group (even): TG x C independent accumulator chains
+  // activation + bf16 pack + layer-3 k step of a finished group's accumulators
+  auto drain = [&](f32x4 (&g)[TG][C], int t0) {
+#pragma unroll
+    for (int u = 0; u < TG; u += 2) {
+      const bf16x8 a3 = w3s[((t0 + u) / 2) * 64 + lane];
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        act4<ACT>(g[u][c]);
+        act4<ACT>(g[u + 1][c]);
+        o[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3, pack8(g[u][c], g[u + 1][c]), o[c], 0, 0, 0);
+      }
+    }
+  };
+#if POL_PIPE
+  f32x4 pend[TG][C];  // the previous group: drained right after the first k step of the next one is issued
+#endif
 #pragma unroll
   for (int t = 0; t < T; t += TG) {
     f32x4 acc[TG][C];
@@ -165,77 +231,122 @@ __global__ __launch_bounds__(POL_WAVES * 64) void policy_kernel(gr_policy_args p
 #pragma unroll
       for (int c = 0; c < C; ++c) acc[u][c] = b;
     }
-    // A fragments double-buffered in registers: the reads of k step s + 1 are issued before the MFMAs of
-    // step s (the scheduling barriers keep the compiler from folding them back into read -> wait -> MFMA)
-    bf16x8 acur[TG], anxt[TG];
+    // A fragments in a register ring POL_PF k steps deep: the reads of k step s + POL_PF are issued before the
+    // MFMAs of step s (the scheduling barriers keep the compiler from folding them back into read -> wait -> MFMA)
+    constexpr int PF = POL_PF;
+    bf16x8 ring[PF + 1][TG];
 #pragma unroll
-    for (int u = 0; u < TG; ++u) acur[u] = w2s[((t + u) * S) * 64 + lane];
+    for (int s = 0; s < PF && s < S; ++s)
+#pragma unroll
+      for (int u = 0; u < TG; ++u) ring[s][u] = w2s[((t + u) * S + s) * 64 + lane];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      if (s + 1 < S) {
+#ifdef POL_ABL_NOA  // timing only: no layer-2 A reads after the first k step (wrong results)
+      if (false) {
+#else
+      if (s + PF < S) {
+#endif
 #pragma unroll
-        for (int u = 0; u < TG; ++u) anxt[u] = w2s[((t + u) * S + s + 1) * 64 + lane];
+        for (int u = 0; u < TG; ++u) ring[(s + PF) % (PF + 1)][u] = w2s[((t + u) * S + s + PF) * 64 + lane];
       }
+#if POL_SB
       __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
       for (int u = 0; u < TG; ++u)
 #pragma unroll
         for (int c = 0; c < C; ++c)
-          acc[u][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(acur[u], h1[s][c], acc[u][c], 0, 0, 0);
+          acc[u][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[POL_RING_IDX][u], h1[s][c], acc[u][c], 0, 0, 0);
+#if POL_SB
       __builtin_amdgcn_sched_barrier(0);
-      if (s + 1 < S) {
-#pragma unroll
-        for (int u = 0; u < TG; ++u) acur[u] = anxt[u];
-      }
+#endif
+#if POL_PIPE
+      if (s == 0 && t > 0) drain(pend, t - TG);
+#endif
     }
+#if POL_PIPE
 #pragma unroll
-    for (int u = 0; u < TG; u += 2) {
-      const bf16x8 a3 = w3s[((t + u) / 2) * 64 + lane];
+    for (int u = 0; u < TG; ++u)
 #pragma unroll
-      for (int c = 0; c < C; ++c) {
-        act4<ACT>(acc[u][c]);
-        act4<ACT>(acc[u + 1][c]);
-        o[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3, pack8(acc[u][c], acc[u + 1][c]), o[c], 0, 0, 0);
+      for (int c = 0; c < C; ++c) pend[u][c] = acc[u][c];
+#else
+    drain(acc, t);
+#endif
+  }
+#if POL_PIPE
+  drain(pend, T - TG);
+#endif
+  // Epilogue on all 64 lanes (lane map above): the accumulator lane e & 15 of column tile e >> 4 holds
+  // output rows 0-3 of env e.
+  const int nout = net.num_out, src = e_w & 15, ct = e_w >> 4;
+  const int env = env0 + e_w;
+  if (blockIdx.y == 1) {  // critic: the value (row 0)
+    float v = 0.0f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const float t = __shfl(o[c][0], src, 64);
+      v = ct == c ? t : v;
+    }
+    if (p == 0 && env < n) net.out[env] = v + net.b3[0];
+    continue;
+  }
+  float y[RPL];
+#pragma unroll
+  for (int q = 0; q < RPL; ++q) {
+    float v = 0.0f;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int pp = 0; pp < 4 / RPL; ++pp) {
+        const float t = __shfl(o[c][RPL * pp + q], src, 64);
+        v = ct == c && p == pp ? t : v;
       }
+    const int r = RPL * p + q;
+    y[q] = v + (r < nout ? net.b3[r] : 0.0f);
+  }
+  // actor: Normal(mean, std) sample and its log prob summed over the actions (torch Normal.log_prob:
+  // -(x - mu)^2 / (2 var) - log(std) - log(sqrt(2 pi))).  One Philox block per env: rows 0, 1 from Box-Muller
+  // on words (x, y), rows 2, 3 on (z, w); the lanes of an env draw the same block.  Box-Muller on the
+  // hardware log2 / sin / cos / sqrt (v_sin / v_cos take revolutions: u2 in [0, 1) is the angle / 2 pi).
+  const gr_u32x4 w = gr_philox4x32_10((uint32_t)(pa.env_id_offset + env), cnt, GR_TAG_POLICY, 0u, pa.seed_lo,
+                                      pa.seed_hi);
+  float z[RPL];
+#pragma unroll
+  for (int b = 0; b < (RPL + 1) / 2; ++b) {
+    const int pair = (RPL * p) / 2 + b;  // 0: rows 0, 1; 1: rows 2, 3
+    const float u1 = gr_u01_open0(pair ? w.z : w.x), u2 = gr_u01(pair ? w.w : w.y);
+    const float rad = __builtin_amdgcn_sqrtf(-1.38629436f * __builtin_amdgcn_logf(u1));  // -2 ln u1
+    const float zc = rad * __builtin_amdgcn_cosf(u2), zs = rad * __builtin_amdgcn_sinf(u2);
+    if (RPL == 1) {
+      z[0] = (p & 1) ? zs : zc;
+    } else {
+      z[2 * b] = zc;
+      z[2 * b + 1] = zs;
     }
   }
-  // Epilogue on all 64 lanes: lane L takes output row r = L >> 4 of env env0 + 16c + (L & 15) from lane L & 15
-  // (which holds rows 0-3 in its accumulator registers).
-  const int nout = net.num_out, r = lane >> 4, l16 = lane & 15;
-  const float br = r < nout ? net.b3[r] : 0.0f;
-  const float sd = blockIdx.y == 0 && r < nout ? pa.std[r] : 1.0f;
+  float act[RPL], lp = 0.0f;
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
-    const float v0 = __shfl(o[c][0], l16, 64), v1 = __shfl(o[c][1], l16, 64);
-    const float v2 = __shfl(o[c][2], l16, 64), v3 = __shfl(o[c][3], l16, 64);
-    const float y = (r == 0 ? v0 : r == 1 ? v1 : r == 2 ? v2 : v3) + br;
-    const int env = env0 + 16 * c + l16;
-    const bool live = env < n && r < nout;
-    if (blockIdx.y == 1) {  // critic: the value
-      if (live) net.out[env] = y;
-      continue;
-    }
-    // actor: Normal(mean, std) sample and its log prob summed over the actions (torch Normal.log_prob:
-    // -(x - mu)^2 / (2 var) - log(std) - log(sqrt(2 pi))).  The env's four lanes draw the same Philox block.
-    const gr_u32x4 w = gr_philox4x32_10((uint32_t)(pa.env_id_offset + env), cnt, GR_TAG_POLICY, 0u, pa.seed_lo,
-                                        pa.seed_hi);
-    float z0, z1;
-    gr_box_muller(r < 2 ? w.x : w.z, r < 2 ? w.y : w.w, &z0, &z1);
-    const float eps = (r & 1) ? z1 : z0;
-    const float a = y + sd * eps;
-    const float dlt = a - y;
-    float lp = r < nout ? -(dlt * dlt) / (2.0f * (sd * sd)) - logf(sd) - 0.91893853320467274f : 0.0f;
-    lp += __shfl_xor(lp, 16, 64);
-    lp += __shfl_xor(lp, 32, 64);
+  for (int q = 0; q < RPL; ++q) {
+    act[q] = y[q] + sdv[q] * z[q];
+    const float dlt = act[q] - y[q];
+    if (RPL * p + q < nout) lp += lpc[q] - dlt * dlt * i2v[q];
+  }
+#pragma unroll
+  for (int m = 16 * C; m < 64; m *= 2) lp += __shfl_xor(lp, m, 64);
 #ifdef POL_ABL_NOEPI
-    if (live && a == 12345.0f) {
+  if (env < n && lp == 12345.0f) {
 #else
-    if (live) {
+  if (env < n) {
 #endif
-      net.out[(size_t)env * nout + r] = y;
-      pa.actions[(size_t)env * nout + r] = a;
-      if (r == 0) pa.log_prob[env] = lp;
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+      const int r = RPL * p + q;
+      if (r < nout) {
+        net.out[(size_t)env * nout + r] = y[q];
+        pa.actions[(size_t)env * nout + r] = act[q];
+      }
     }
+    if (p == 0) pa.log_prob[env] = lp;
   }
   }  // env tiles
 }
