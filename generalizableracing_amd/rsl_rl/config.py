@@ -34,6 +34,9 @@ class RslRlPpoAlgorithmCfg:
     lam: float = 0.95
     desired_kl: float = 0.01
     max_grad_norm: float = 1.0
+    # not in the reference: rollout inference (act / evaluate / log prob) as one bf16 MFMA launch
+    # (rsl_rl/fused_inference.py); the update stays fp32.  MLP ActorCritic with 128 / 256 hidden units only.
+    fused_rollout_inference: bool = False
 
 
 @dataclass

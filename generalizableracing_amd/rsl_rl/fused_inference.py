@@ -96,7 +96,7 @@ def mlp_layers(seq: nn.Sequential):
 class FusedPolicyInference:
     """PPO.act's policy calls for `num_envs` envs in one MFMA launch.  Outputs are persistent device
     tensors (rebind-free, graph-capturable): actions, action_mean [N, A], values [N, 1], log_prob [N],
-    action_sigma [N, A]."""
+    action_sigma [N, A].  Used by PPO when the algorithm cfg sets `fused_rollout_inference` (ppo.py)."""
 
     def __init__(self, policy, num_envs: int, device, seed: int = 0, env_id_offset: int = 0):
         self.policy = policy
@@ -126,7 +126,16 @@ class FusedPolicyInference:
         self.seed = int(seed)
         self.env_id_offset = int(env_id_offset)
         self._packed = {}
+        self._version = None
         self.refresh()
+
+    def _params(self):
+        ps = list(self.policy.actor.parameters()) + list(self.policy.critic.parameters())
+        return ps + [self.policy.std if self.policy.noise_std_type == "scalar" else self.policy.log_std]
+
+    def _param_version(self):
+        # torch bumps a tensor's version on every in-place write (optimizer.step, load_state_dict, copy_)
+        return tuple(p._version for p in self._params())
 
     @torch.no_grad()
     def refresh(self):
@@ -145,6 +154,7 @@ class FusedPolicyInference:
                     self._packed[key] = v
         std = self.policy.std if self.policy.noise_std_type == "scalar" else torch.exp(self.policy.log_std)
         self.std.copy_(std.detach().float())
+        self._version = self._param_version()
 
     def _net(self, name, obs, out, num_obs, num_out):
         p = self._packed
@@ -159,8 +169,11 @@ class FusedPolicyInference:
 
     def act(self, obs: torch.Tensor, critic_obs: torch.Tensor):
         """-> (actions, values, log_prob, action_mean, action_sigma) for all envs (views of persistent
-        buffers, overwritten by the next call)."""
+        buffers, overwritten by the next call).  Weights changed in place since the last packing (a PPO
+        update, a checkpoint load) are repacked first; inside a graph capture they must not change."""
         n = self.num_envs
+        if self._param_version() != self._version:
+            self.refresh()
         for x, d in ((obs, self.num_obs[0]), (critic_obs, self.num_obs[1])):
             if x.shape != (n, d) or x.dtype != torch.float32 or x.device != self.device or not x.is_contiguous():
                 raise ValueError(f"expected contiguous fp32 [{n}, {d}] observations on {self.device}, got "

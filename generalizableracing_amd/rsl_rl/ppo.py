@@ -21,7 +21,7 @@ class PPO:
     def __init__(self, policy, env=None, num_learning_epochs=1, num_mini_batches=1, clip_param=0.2, gamma=0.998,
                  lam=0.95, value_loss_coef=1.0, entropy_coef=0.0, learning_rate=1e-3, max_grad_norm=1.0,
                  use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu",
-                 normalize_advantage=True, storage_obs_dtype=torch.float32, **kwargs):
+                 normalize_advantage=True, storage_obs_dtype=torch.float32, fused_rollout_inference=False, **kwargs):
         self.env = env
         self.device = device
         self.desired_kl = desired_kl
@@ -44,11 +44,26 @@ class PPO:
         self.use_clipped_value_loss = use_clipped_value_loss
         self.normalize_advantage = normalize_advantage
         self.storage_obs_dtype = storage_obs_dtype
+        # rollout inference on MFMA (rsl_rl/fused_inference.py, BASELINE config C5): bf16 operands, fp32
+        # accumulation, one launch for actor + sampling + log prob + critic; the update stays fp32 PyTorch
+        self.fused_rollout_inference = bool(fused_rollout_inference)
+        self.fused = None
 
     def init_storage(self, training_type, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape,
                      action_shape):
         self.storage = RolloutStorage(training_type, num_envs, num_transitions_per_env, actor_obs_shape,
                                       critic_obs_shape, action_shape, self.device, obs_dtype=self.storage_obs_dtype)
+        self._init_fused(num_envs)
+
+    def _init_fused(self, num_envs):
+        if not self.fused_rollout_inference:
+            return
+        from .fused_inference import FusedPolicyInference
+
+        ucfg = getattr(getattr(self.env, "unwrapped", None), "cfg", None)
+        seed = getattr(ucfg, "seed", None)
+        self.fused = FusedPolicyInference(self.policy, num_envs, self.device, seed=42 if seed is None else int(seed),
+                                          env_id_offset=int(getattr(ucfg, "env_id_offset", 0) or 0))
 
     def test_mode(self):
         self.policy.eval()
@@ -57,6 +72,13 @@ class PPO:
         self.policy.train()
 
     def act(self, obs, critic_obs):
+        if self.fused is not None:
+            a, v, lp, mu, sd = self.fused.act(obs, critic_obs)
+            self.transition.actions, self.transition.values, self.transition.actions_log_prob = a, v, lp
+            self.transition.action_mean, self.transition.action_sigma = mu, sd
+            self.transition.observations = obs
+            self.transition.privileged_observations = critic_obs
+            return a
         self.transition.actions = self.policy.act(obs).detach()
         self.transition.values = self.policy.evaluate(critic_obs).detach()
         self.transition.actions_log_prob = self.policy.get_actions_log_prob(self.transition.actions).detach()

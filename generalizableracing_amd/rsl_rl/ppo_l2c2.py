@@ -47,6 +47,7 @@ class PPOL2C2(PPO):
         self.storage = RolloutStorageL2C2(training_type, num_envs, num_transitions_per_env, actor_obs_shape,
                                           critic_obs_shape, action_shape, self.device,
                                           obs_dtype=self.storage_obs_dtype)
+        self._init_fused(num_envs)
 
     def smooth_coefs(self):
         """ppo_l2c2.py:176-178."""

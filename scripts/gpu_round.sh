@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU box, one call: parity tests, the default bench line, kernel-trace + PMC profiles of the step kernel
-# on gate-only and obstacle tracks.  Usage: gpu_round.sh TAG
+# on gate-only and obstacle tracks, kernel trace + SQ counters of the fused policy inference.  Usage: gpu_round.sh TAG
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-round}
@@ -13,4 +13,5 @@ rc=$?; echo "pytest exit $rc" >> $OUT/pytest_gpu.log; fatal $rc && exit 10
 timeout -k 10 400 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err; rc=$?; fatal $rc && exit 11
 bash scripts/gpu_profile.sh ${TAG}_g 65536 0 || exit 12
 bash scripts/gpu_profile.sh ${TAG}_o 65536 1 || exit 13
+bash scripts/prof_policy.sh ${TAG}_p || exit 14
 echo done > $OUT/done

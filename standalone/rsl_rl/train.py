@@ -45,6 +45,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--headless", action="store_true", default=False)
     p.add_argument("--enable_cameras", action="store_true", default=False)
     p.add_argument("--livestream", type=int, default=None)
+    p.add_argument("--fused_rollout", action="store_true", default=False,
+                   help="Rollout inference as one bf16 MFMA launch (algorithm.fused_rollout_inference).")
     cli_args.add_rsl_rl_args(p)
     return p
 
@@ -85,6 +87,8 @@ def main(argv=None):
         env_cfg.scene.num_envs = args.num_envs
     if args.max_iterations is not None:
         agent_cfg.max_iterations = args.max_iterations
+    if args.fused_rollout:
+        agent_cfg.algorithm.fused_rollout_inference = True
     device = args.device or (f"cuda:{local_rank}" if torch.cuda.is_available() else "cpu")
     agent_cfg.device = device
     env_cfg.sim.device = device

@@ -120,3 +120,12 @@ def test_unsupported_policies_rejected():
         mlp_layers(ActorCritic(16, 16, 4, [64, 64], [64, 64], "lrelu").actor)
     with pytest.raises(ValueError):
         mlp_layers(ActorCritic(16, 16, 4, [256, 256], [256, 256], "tanh").actor)
+
+
+def test_fused_rollout_has_no_cpu_path():
+    """algorithm.fused_rollout_inference is HIP-only: on a CPU device PPO refuses it at storage init."""
+    from generalizableracing_amd.rsl_rl.ppo import PPO
+
+    alg = PPO(ActorCritic(16, 16, 4, [256, 256], [256, 256], "lrelu"), device="cpu", fused_rollout_inference=True)
+    with pytest.raises(RuntimeError):
+        alg.init_storage("rl", 8, 4, [16], [16], [4])

@@ -86,3 +86,43 @@ def test_refresh_after_update_and_graph_capture():
     torch.cuda.synchronize()
     assert int(fused.counters.max()) == int(c0.max()) + 2  # the device counter advances inside the graph
     assert not torch.equal(a0, fused.actions)
+
+
+def test_ppo_rollout_with_fused_inference():
+    """PPO with algorithm.fused_rollout_inference on the HIP env: the stored rollout matches the fp32 module,
+    the log probs are those of the stored (mean, sigma, action), and an update is picked up by the next act."""
+    from generalizableracing_amd.envs.racing_cfg import RacingEnvCfg, SceneCfg, SimCfg
+    from generalizableracing_amd.envs.racing_env import RacingEnv, RslRlVecEnvWrapper
+    from generalizableracing_amd.rsl_rl import OnPolicyRunner, QuadcopterPPORunnerCfg
+
+    torch.manual_seed(2)
+    n = 2048
+    env = RslRlVecEnvWrapper(RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV))))
+    cfg = QuadcopterPPORunnerCfg(device=DEV)
+    cfg.algorithm.fused_rollout_inference = True
+    runner = OnPolicyRunner(env, cfg.to_dict(), log_dir=None, device=DEV)
+    alg, pol = runner.alg, runner.alg.policy
+    assert alg.fused is not None
+    obs, extras = env.get_observations()
+    cobs = extras["observations"]["critic"]
+    steps = 3
+    with torch.inference_mode():
+        for k in range(steps):
+            a = alg.act(obs, cobs)
+            m_ref, v_ref = pol.actor(obs), pol.critic(cobs)
+            for got, want in ((alg.fused.action_mean, m_ref), (alg.fused.values, v_ref)):
+                assert float((got - want).abs().max()) < 2e-2 * (float(want.abs().max()) + 1e-3)
+            obs, rew, dones, infos = env.step(a)
+            cobs = infos["observations"]["critic"]
+            alg.process_env_step(rew, dones, infos)
+    st = alg.storage
+    lp = torch.distributions.Normal(st.mu[:steps], st.sigma[:steps]).log_prob(st.actions[:steps]).sum(-1)
+    assert float((lp - st.actions_log_prob[:steps, :, 0]).abs().max()) < 1e-4
+    assert torch.isfinite(st.values[:steps]).all()
+    # a full iteration: the update changes the weights in place, the next act repacks them
+    st.clear()
+    runner.learn(1)
+    with torch.inference_mode():
+        alg.act(obs, cobs)
+        want = pol.actor(obs)
+    assert float((alg.fused.action_mean - want).abs().max()) < 2e-2 * (float(want.abs().max()) + 1e-3)
