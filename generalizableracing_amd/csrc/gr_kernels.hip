@@ -22,6 +22,51 @@ namespace gr {
 
 #define DEV __device__ __forceinline__
 
+// 16-byte stores of the step's outputs (state planes, istate, obs rows).  GR_STORE_POLICY: 0 plain;
+// 1 non-temporal (`nt`, the default: the step's ~19 MB of outputs are not re-read by this launch);
+// 2 write-through (`sc1`, buffer store on the uniform base); 3 `sc1 nt`.  `base` must be wave-uniform (a kernel-argument pointer).
+#ifndef GR_STORE_POLICY
+#define GR_STORE_POLICY 1  // nt measured 0.8 us (7 %) faster per step than plain; sc1 and nt loads slower
+#endif
+#ifndef GR_SCALAR_NT
+#define GR_SCALAR_NT 1  // nt for the scalar outputs as well (measured 0.1 us faster)
+#endif
+template <typename T>
+DEV void st1(T* p, T v) {  // the per-env scalar outputs (reward, flags, dones, aux)
+#if GR_SCALAR_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+// 16-byte loads of planes only the physics waves read (GR_LOAD_POLICY 1: non-temporal).
+#ifndef GR_LOAD_POLICY
+#define GR_LOAD_POLICY 0
+#endif
+DEV float4 ld4(const float4* base, size_t idx) {
+#if GR_LOAD_POLICY == 1
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  const f32x4 w = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(base) + idx);
+  return make_float4(w[0], w[1], w[2], w[3]);
+#else
+  return base[idx];
+#endif
+}
+template <typename T4>
+DEV void st4(T4* base, size_t idx, const T4& v) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 w = {__builtin_bit_cast(unsigned, v.x), __builtin_bit_cast(unsigned, v.y),
+                   __builtin_bit_cast(unsigned, v.z), __builtin_bit_cast(unsigned, v.w)};
+#if GR_STORE_POLICY == 1
+  __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(base) + idx);
+#elif GR_STORE_POLICY >= 2
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, (int)(idx * 16), 0, GR_STORE_POLICY == 2 ? 16 : 18);
+#else
+  *reinterpret_cast<u32x4*>(base + idx) = w;
+#endif
+}
+
 // ------------------------------------------------------------- IL math
 // Isaac Lab omni.isaac.lab.utils.math restated (see oracle/gr_oracle.c).
 DEV void quat_rotate(const float q[4], const float v[3], float o[3]) {
@@ -95,11 +140,11 @@ DEV void load_env(const KArgs& a, int i, Env& e) {
   const float4* S = reinterpret_cast<const float4*>(a.buf.state);
   const size_t n = (size_t)a.h.num_envs;
   int4 ii = reinterpret_cast<const int4*>(a.buf.istate)[i];
-  float4 s5 = S[GR_P_LAG * n + i], s6 = S[GR_P_RST0 * n + i], p2 = S[GR_P_PAR2 * n + i];
-  float4 s2 = S[GR_P_VW * n + i], s3 = S[GR_P_WA * n + i], s4 = S[GR_P_CTRL * n + i];
-  float4 p0 = S[GR_P_PAR0 * n + i], p1 = S[GR_P_PAR1 * n + i], p3 = S[GR_P_PAR3 * n + i];
-  float4 s0 = S[GR_P_POSQ * n + i], s1 = S[GR_P_QV * n + i], s7 = S[GR_P_RST1 * n + i];
-  float4 s8 = S[GR_P_EP0 * n + i], s9 = S[GR_P_EP1 * n + i];
+  float4 s5 = ld4(S, GR_P_LAG * n + i), s6 = S[GR_P_RST0 * n + i], p2 = S[GR_P_PAR2 * n + i];
+  float4 s2 = ld4(S, GR_P_VW * n + i), s3 = ld4(S, GR_P_WA * n + i), s4 = ld4(S, GR_P_CTRL * n + i);
+  float4 p0 = ld4(S, GR_P_PAR0 * n + i), p1 = ld4(S, GR_P_PAR1 * n + i), p3 = ld4(S, GR_P_PAR3 * n + i);
+  float4 s0 = ld4(S, GR_P_POSQ * n + i), s1 = ld4(S, GR_P_QV * n + i), s7 = S[GR_P_RST1 * n + i];
+  float4 s8 = ld4(S, GR_P_EP0 * n + i), s9 = ld4(S, GR_P_EP1 * n + i);
   e.p[0] = s0.x; e.p[1] = s0.y; e.p[2] = s0.z; e.q[0] = s0.w;
   e.q[1] = s1.x; e.q[2] = s1.y; e.q[3] = s1.z; e.v[0] = s1.w;
   e.v[1] = s2.x; e.v[2] = s2.y; e.w[0] = s2.z; e.w[1] = s2.w;
@@ -128,20 +173,20 @@ DEV void load_env(const KArgs& a, int i, Env& e) {
 DEV void store_kin(const KArgs& a, int i, const Env& e) {
   float4* S = reinterpret_cast<float4*>(a.buf.state);
   const size_t n = (size_t)a.h.num_envs;
-  S[GR_P_POSQ * n + i] = make_float4(e.p[0], e.p[1], e.p[2], e.q[0]);
-  S[GR_P_QV * n + i] = make_float4(e.q[1], e.q[2], e.q[3], e.v[0]);
-  S[GR_P_VW * n + i] = make_float4(e.v[1], e.v[2], e.w[0], e.w[1]);
-  S[GR_P_WA * n + i] = make_float4(e.w[2], e.al[0], e.al[1], e.al[2]);
-  S[GR_P_CTRL * n + i] = make_float4(e.T, e.tau[0], e.tau[1], e.tau[2]);
-  S[GR_P_LAG * n + i] = make_float4(e.lag[0], e.lag[1], e.lag[2], e.lag[3]);
-  if (a.h.use_motor_model) S[GR_P_MOTOR * n + i] = make_float4(e.mw[0], e.mw[1], e.mw[2], e.mw[3]);
+  st4(S, GR_P_POSQ * n + i, make_float4(e.p[0], e.p[1], e.p[2], e.q[0]));
+  st4(S, GR_P_QV * n + i, make_float4(e.q[1], e.q[2], e.q[3], e.v[0]));
+  st4(S, GR_P_VW * n + i, make_float4(e.v[1], e.v[2], e.w[0], e.w[1]));
+  st4(S, GR_P_WA * n + i, make_float4(e.w[2], e.al[0], e.al[1], e.al[2]));
+  st4(S, GR_P_CTRL * n + i, make_float4(e.T, e.tau[0], e.tau[1], e.tau[2]));
+  st4(S, GR_P_LAG * n + i, make_float4(e.lag[0], e.lag[1], e.lag[2], e.lag[3]));
+  if (a.h.use_motor_model) st4(S, GR_P_MOTOR * n + i, make_float4(e.mw[0], e.mw[1], e.mw[2], e.mw[3]));
 }
 // ... and episode sums
 DEV void store_eps(const KArgs& a, int i, const Env& e) {
   float4* S = reinterpret_cast<float4*>(a.buf.state);
   const size_t n = (size_t)a.h.num_envs;
-  S[GR_P_EP0 * n + i] = make_float4(e.es[0], e.es[1], e.es[2], e.es[3]);
-  S[GR_P_EP1 * n + i] = make_float4(e.es[4], e.es[5], e.es[6], e.mar);
+  st4(S, GR_P_EP0 * n + i, make_float4(e.es[0], e.es[1], e.es[2], e.es[3]));
+  st4(S, GR_P_EP1 * n + i, make_float4(e.es[4], e.es[5], e.es[6], e.mar));
 }
 DEV void store_dyn(const KArgs& a, int i, const Env& e) {
   store_kin(a, i, e);
@@ -152,13 +197,13 @@ DEV void store_dyn(const KArgs& a, int i, const Env& e) {
 DEV void store_rst(const KArgs& a, int i, const Env& e) {
   float4* S = reinterpret_cast<float4*>(a.buf.state);
   const size_t n = (size_t)a.h.num_envs;
-  S[GR_P_RST0 * n + i] = make_float4(e.thr, e.nl, e.k2[0], e.k2[1]);
-  S[GR_P_RST1 * n + i] = make_float4(e.k2[2], e.k1[0], e.k1[1], e.k1[2]);
+  st4(S, GR_P_RST0 * n + i, make_float4(e.thr, e.nl, e.k2[0], e.k2[1]));
+  st4(S, GR_P_RST1 * n + i, make_float4(e.k2[2], e.k1[0], e.k1[1], e.k1[2]));
 }
 
 DEV void store_istate(const KArgs& a, int i, const Env& e) {
   int packed = (e.gate & 0xff) | ((e.lvl & 0xff) << 8) | ((e.azero & 1) << 16) | ((e.type & 0xff) << 24);
-  reinterpret_cast<int4*>(a.buf.istate)[i] = make_int4(e.ep, e.acc, e.epoch, packed);
+  st4(reinterpret_cast<int4*>(a.buf.istate), (size_t)i, make_int4(e.ep, e.acc, e.epoch, packed));
 }
 
 // ------------------------------------------------------------- track table view
@@ -697,7 +742,7 @@ DEV void store_rows_staged(float4* dst, int env0, int n, const float4 rows[4], f
   for (int j = 0; j < 4; ++j) {
     const int env = 16 * j + (l >> 2), q = l & 3;
     const float4 v = stage[q * GR_BLOCK + env];
-    if (env0 + env < n) dst[(size_t)(env0 + env) * 4 + q] = v;
+    if (env0 + env < n) st4(dst, (size_t)(env0 + env) * 4 + q, v);
   }
   __asm__ volatile("" ::: "memory");
 }
@@ -977,7 +1022,7 @@ __global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KCons
 
   if (role == 0) {
     // ======================= physics waves =======================
-    const float4 act = reinterpret_cast<const float4*>(actions)[ii];
+    const float4 act = ld4(reinterpret_cast<const float4*>(actions), (size_t)ii);
     Env e;
     load_env(a, ii, e);
     const float dt = c.step_dt;
@@ -1137,10 +1182,10 @@ __global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KCons
       e.k2[2] = r5.x; e.k1[0] = r5.y; e.k1[1] = r5.z; e.k1[2] = r5.w;
     }
     if (live) {
-      a.buf.reward[i] = rew;
-      a.buf.terminated[i] = (uint8_t)terminated;
-      a.buf.time_out[i] = (uint8_t)time_out;
-      a.buf.dones[i] = (int64_t)(terminated | time_out);
+      st1(a.buf.reward + i, rew);
+      st1(a.buf.terminated + i, (uint8_t)terminated);
+      st1(a.buf.time_out + i, (uint8_t)time_out);
+      st1(a.buf.dones + i, (int64_t)(terminated | time_out));
       store_dyn(a, i, e);
       if (done) store_rst(a, i, e);
     }
@@ -1234,10 +1279,10 @@ __global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KCons
       compute_policy(a, sl.tab, e, gid, on, lc, prow);
       store_rows_staged(reinterpret_cast<float4*>(a.buf.obs_policy), blockIdx.x * GR_BLOCK + (t & ~63), n, prow,
                         stg + (t & ~63));
-      if (live) a.buf.obs_aux[i] = aux;
+      if (live) st1(a.buf.obs_aux + i, aux);
     }
 #endif
-    if (OBST && live) reinterpret_cast<float4*>(a.buf.state)[GR_P_OHINT * (size_t)n + i] = next_hint;
+    if (OBST && live) st4(reinterpret_cast<float4*>(a.buf.state), GR_P_OHINT * (size_t)n + i, next_hint);
 #ifndef GR_ABL_NOLOG
     wave_log_levels(a, threadIdx.x >> 6, live ? (float)e.lvl : 0.0f, live ? e.nl : 0.0f);
 #endif
