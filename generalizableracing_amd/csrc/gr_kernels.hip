@@ -768,18 +768,6 @@ DEV void log_row_store(const KArgs& a, int row, const float v[GR_LOG_SLOTS]) {
 }
 
 // reset-lane slots (GR_LOG_NRESET .. GR_LOG_T_BADPOSE) of this wave -> row
-DEV void wave_log_resets(const KArgs& a, int row, const float lg[GR_LOG_SLOTS], bool reset_lane) {
-  float acc[GR_LOG_SLOTS];
-  for (int s = 0; s < GR_LOG_SLOTS; ++s) acc[s] = 0.0f;
-  uint64_t m = __ballot(reset_lane);
-  while (m) {
-    const int l = __builtin_ctzll(m);
-    m &= m - 1;
-    for (int s = 0; s < GR_LOG_LEVEL; ++s) acc[s] += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lg[s]), l));
-  }
-  log_row_store(a, row, acc);
-}
-
 // wave-wide float sum by DPP (no LDS round trips); the total lands in lane 63
 template <int CTRL, int ROWS>
 DEV float dpp_term(float v) {
@@ -795,15 +783,20 @@ DEV float wave_sum63(float v) {
   return v;
 }
 
-// all-env slots (terrain level, noise level) of this wave -> row
-DEV void wave_log_levels(const KArgs& a, int row, float level, float noise) {
-  level = __shfl(wave_sum63(level), 63, 64);
-  noise = __shfl(wave_sum63(noise), 63, 64);
-  float v[GR_LOG_SLOTS];
-  for (int s = 0; s < GR_LOG_SLOTS; ++s) v[s] = 0.0f;
-  v[GR_LOG_LEVEL] = level;
-  v[GR_LOG_NOISE] = noise;
-  log_row_store(a, row, v);
+// one row per wave: the reset slots summed over the wave's resetting lanes, and the all-env slots
+// (terrain level, noise level of the post-reset state) summed over its live lanes
+DEV void wave_log(const KArgs& a, int row, const float lg[GR_LOG_SLOTS], bool reset_lane, float level, float noise) {
+  float acc[GR_LOG_SLOTS];
+  for (int s = 0; s < GR_LOG_SLOTS; ++s) acc[s] = 0.0f;
+  uint64_t m = __ballot(reset_lane);
+  while (m) {
+    const int l = __builtin_ctzll(m);
+    m &= m - 1;
+    for (int s = 0; s < GR_LOG_LEVEL; ++s) acc[s] += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lg[s]), l));
+  }
+  acc[GR_LOG_LEVEL] = __shfl(wave_sum63(level), 63, 64);
+  acc[GR_LOG_NOISE] = __shfl(wave_sum63(noise), 63, 64);
+  log_row_store(a, row, acc);
 }
 
 // ------------------------------------------------------------- gate table staging
@@ -923,8 +916,7 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const KConst* __
   }
   // (observe calls reset nothing: their rows say so, and the finalized log repeats the previous one)
   const int w = threadIdx.x >> 6;
-  wave_log_resets(a, w, lg, reset_lane);
-  wave_log_levels(a, 4 + w, live ? (float)e.lvl : 0.0f, live ? e.nl : 0.0f);
+  wave_log(a, w, lg, reset_lane, live ? (float)e.lvl : 0.0f, live ? e.nl : 0.0f);
 }
 
 // ------------------------------------------------------------- the step kernel
@@ -1191,7 +1183,9 @@ __global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KCons
     }
     STAMP(12);
 #ifndef GR_ABL_NOLOG
-    wave_log_resets(a, threadIdx.x >> 6, lg, reset_lane);
+    // the level slots too (post-reset level / noise level are this lane's): the policy waves, whose tail is
+    // the longest of the three roles, write no log row
+    wave_log(a, threadIdx.x >> 6, lg, reset_lane, live ? (float)e.lvl : 0.0f, live ? e.nl : 0.0f);
 #endif
     STAMP(8);
     RSTAMP(10);
@@ -1283,9 +1277,6 @@ __global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KCons
     }
 #endif
     if (OBST && live) st4(reinterpret_cast<float4*>(a.buf.state), GR_P_OHINT * (size_t)n + i, next_hint);
-#ifndef GR_ABL_NOLOG
-    wave_log_levels(a, threadIdx.x >> 6, live ? (float)e.lvl : 0.0f, live ? e.nl : 0.0f);
-#endif
     STAMP(8);
     RSTAMP(10);
   } else {
