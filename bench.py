@@ -237,6 +237,31 @@ def policy_in_loop_fused(env, steps, device):
     return rate, us, flops / (us * 1e-6) / 1e12
 
 
+def env_count_sweep(rank, device, a, sizes=(16384, 262144, 1048576)):
+    """The same step at other env counts per GPU (HBM holds far more than the 65 536 of the headline
+    config): per-launch us from HIP events over graph replays, env-steps/s and algorithmic GB/s."""
+    out = {}
+    for n in sizes:
+        env = make_env(n, rank, device, a.gates, a.integrator, False)
+        g = torch.Generator(device=device).manual_seed(1234 + rank)
+        acts = torch.randn(ACTION_RING, n, 4, device=device, generator=g)
+        for k in range(8):
+            env.step(acts[k % ACTION_RING])
+        torch.cuda.synchronize()
+        graph = capture_graph(env, acts)
+        kt = kernel_timing(env, acts, 2 * ACTION_RING, graph)
+        del graph
+        rd, wr = env.bytes_per_env_step()
+        us = kt["graph_event_us"]
+        out[str(n)] = {"kernel_us": us, "env_steps_per_s": n / (us * 1e-6),
+                       "achieved_GBps": (rd + wr) * n / (us * 1e-6) / 1e9,
+                       "frac_of_8TBps": (rd + wr) * n / (us * 1e-6) / 8e12}
+        env.close()
+        del acts
+        torch.cuda.empty_cache()
+    return out
+
+
 def train_fps(device, n=4096, iters=3):
     """Config C2: 4 096 envs, rsl_rl PPO MLP(256,256) fp32, the reference's Perf/total_fps."""
     from generalizableracing_amd.envs.racing_env import RslRlVecEnvWrapper
@@ -350,6 +375,8 @@ def main():
             "obstacles_per_track_max": int(env_o.obstacle_table.counts.max()),
             "obstacles_per_track_mean": float(env_o.obstacle_table.counts.mean())}
         env_o.close()
+    if not a.no_extras and not a.obstacles:
+        extra["env_count_sweep"] = env_count_sweep(rank, device, a)
     if not a.no_extras:
         extra["train_total_fps_4096_envs"] = train_fps(device)
         # the depth camera of the vision task (separate kernel, same env shard size)
