@@ -327,6 +327,9 @@ def main():
     if a.dist_backend != "nccl":  # rehearsal: ranks may share a device
         local = local % max(1, torch.cuda.device_count())
     if ws > 1:
+        # the scaling lines report the headline step only: the extras (policy, training, camera, sweep legs)
+        # are single-GPU measurements, and a rank-local leg must not hold the others at a collective
+        a.no_extras = True
         torch.cuda.set_device(local)
         dist.init_process_group(a.dist_backend, rank=rank, world_size=ws)
     device = f"cuda:{local}"

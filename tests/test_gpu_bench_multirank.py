@@ -1,0 +1,36 @@
+"""bench.py's multi-rank path (the driver's N = 2, 4, 8 scaling runs launch it under torch.distributed.run):
+two ranks share the one GPU of the test box over gloo, and rank 0 prints one JSON line whose value counts
+both shards.  The RCCL path differs only in the backend and one GPU per rank."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_two_ranks_gloo():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "128", "--warmup", "8", "--num-envs", "8192", "--dist-backend", "gloo"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 only
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["value"] > 0
+    assert line["config"]["parallelism"] == "env-shard x2"
+    # the value counts both shards: 2 x 8192 envs x steps / max-over-ranks time
+    assert abs(line["value"] - 2 * 8192 * 128 / (line["ms_per_step"] * 1e-3 * 128)) < 1e-6 * line["value"]
+    assert line["cpu_baseline"] is None and "policy_in_loop_fused" not in line
