@@ -380,6 +380,20 @@ def main():
         env_o.close()
     if not a.no_extras and not a.obstacles:
         extra["env_count_sweep"] = env_count_sweep(rank, device, a)
+        # BASELINE config C5 on one GPU: 32-gate tracks, startup DR (plant vs controller mass, drag, thrust
+        # error), hipGraph of [fused rollout inference + step]
+        env_c5 = make_env(n, rank, device, 32, a.integrator, False)
+        for k in range(a.warmup):
+            env_c5.step(actions[k % ACTION_RING])
+        torch.cuda.synchronize()
+        _, _, graph_c5 = time_env_steps(env_c5, actions, 2 * ACTION_RING, not a.no_graph)
+        kt_c5 = kernel_timing(env_c5, actions, 2 * ACTION_RING, graph_c5)
+        del graph_c5
+        rate_c5, us_c5, _ = policy_in_loop_fused(env_c5, 512, device)
+        extra["c5_32_gates"] = {"step_kernel_us": kt_c5["kernel_us"], "step_env_steps_per_s": n / (kt_c5["kernel_us"] * 1e-6),
+                                "step_plus_fused_inference_env_steps_per_s": rate_c5, "inference_kernel_us": us_c5,
+                                "launch": "hipgraph (64 x [fused inference + gr_step])"}
+        env_c5.close()
     if not a.no_extras:
         extra["train_total_fps_4096_envs"] = train_fps(device)
         # the depth camera of the vision task (separate kernel, same env shard size)
