@@ -392,7 +392,10 @@ DEV uint32_t collision_mask(const KArgs& a, const Tab& tab, int type, int lvl, c
       if (p[2] + oz < ground) inside |= 1u << k;
     }
   }
-  // ---- pass 2: gates inside the sphere: plane-slab / outer-box / hole culls, then the lattice ----
+  // ---- pass 2: gates inside the sphere: plane-slab / outer-box / hole culls (2a), then the lattice of the
+  // survivors (2b).  Two loops, so a wave runs the lattice as often as its worst lane has survivors, not as
+  // often as its worst lane has sphere hits (dense tracks: several spheres per env) ----
+  uint32_t cand = 0u;
   while (sph) {
     const int g = __builtin_ctz(sph);
     sph &= sph - 1u;
@@ -404,7 +407,15 @@ DEV uint32_t collision_mask(const KArgs& a, const Tab& tab, int type, int lvl, c
     const bool slab = z <= gr[15] + reach;
     const bool outer = (x <= gr[16] + reach) & (y <= gr[17] + reach);
     const bool hole = (x < gr[7] - reach) & (y < gr[11] - reach);
-    if (!(slab & outer & !hole)) continue;
+    if (slab & outer & !hole) cand |= 1u << g;
+  }
+  while (cand) {
+    const int g = __builtin_ctz(cand);
+    cand &= cand - 1u;
+    const float* gr = tab.gate(type, lvl, g);
+    float d[3] = {p[0] - gr[0], p[1] - gr[1], p[2] - gr[2]};
+    float dg[3];
+    gate_frame(gr, d, dg);
     float Ag[3], Bg[3], Cg[3];
     gate_frame(gr, A, Ag);
     gate_frame(gr, B, Bg);
