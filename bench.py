@@ -262,13 +262,18 @@ def env_count_sweep(rank, device, a, sizes=(16384, 262144, 1048576)):
     return out
 
 
-def train_fps(device, n=4096, iters=3):
-    """Config C2: 4 096 envs, rsl_rl PPO MLP(256,256) fp32, the reference's Perf/total_fps."""
+def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False):
+    """The reference's Perf/total_fps (24 steps x N / (collect + learn)) of rsl_rl PPO with MLP(256,256):
+    config C2 at 4 096 envs fp32; at 65 536 envs also with the fused bf16 rollout inference and bf16
+    rollout obs buffers (C5's training options; the update stays fp32)."""
     from generalizableracing_amd.envs.racing_env import RslRlVecEnvWrapper
     from generalizableracing_amd.rsl_rl import OnPolicyRunner, QuadcopterPPORunnerCfg
 
     venv = RslRlVecEnvWrapper(RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=device))))
-    runner = OnPolicyRunner(venv, QuadcopterPPORunnerCfg(device=device).to_dict(), log_dir=None, device=device)
+    cfg = QuadcopterPPORunnerCfg(device=device)
+    cfg.algorithm.fused_rollout_inference = bool(fused)
+    cfg.algorithm.storage_obs_dtype = "bfloat16" if bf16_storage else "float32"
+    runner = OnPolicyRunner(venv, cfg.to_dict(), log_dir=None, device=device)
     runner.learn(1, init_at_random_ep_len=True)  # warm-up iteration
     fps = []
     for _ in range(iters):
@@ -396,6 +401,10 @@ def main():
         env_c5.close()
     if not a.no_extras:
         extra["train_total_fps_4096_envs"] = train_fps(device)
+        extra["train_total_fps_65536_envs"] = {
+            "fp32": train_fps(device, n),
+            "fused_rollout_bf16_storage": train_fps(device, n, fused=True, bf16_storage=True),
+            "note": "Perf/total_fps, PPO 5 epochs x 4 mini-batches per 24-step rollout, obstacle tracks"}
         # the depth camera of the vision task (separate kernel, same env shard size)
         sys.path.insert(0, os.path.join(ROOT, "scripts"))
         import bench_camera

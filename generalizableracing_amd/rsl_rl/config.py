@@ -37,6 +37,9 @@ class RslRlPpoAlgorithmCfg:
     # not in the reference: rollout inference (act / evaluate / log prob) as one bf16 MFMA launch
     # (rsl_rl/fused_inference.py); the update stays fp32.  MLP ActorCritic with 128 / 256 hidden units only.
     fused_rollout_inference: bool = False
+    # not in the reference: dtype of the rollout storage's observation buffers ("bfloat16" halves them;
+    # mini-batches are cast back to fp32 for the update)
+    storage_obs_dtype: str = "float32"
 
 
 @dataclass

@@ -43,7 +43,9 @@ class PPO:
         self.max_grad_norm = max_grad_norm
         self.use_clipped_value_loss = use_clipped_value_loss
         self.normalize_advantage = normalize_advantage
-        self.storage_obs_dtype = storage_obs_dtype
+        # "float32" / "bfloat16" from a cfg dict, or a torch dtype (BASELINE C5: bf16 rollout obs buffers)
+        self.storage_obs_dtype = getattr(torch, storage_obs_dtype) if isinstance(storage_obs_dtype, str) \
+            else storage_obs_dtype
         # rollout inference on MFMA (rsl_rl/fused_inference.py, BASELINE config C5): bf16 operands, fp32
         # accumulation, one launch for actor + sampling + log prob + critic; the update stays fp32 PyTorch
         self.fused_rollout_inference = bool(fused_rollout_inference)
