@@ -12,6 +12,8 @@ import torch
 import torch.nn as nn
 from torch.distributions import Normal
 
+from .linear import TallLinear
+
 
 def resolve_nn_activation(name: str) -> nn.Module:
     table = {
@@ -24,12 +26,13 @@ def resolve_nn_activation(name: str) -> nn.Module:
 
 
 def _mlp(inp: int, hidden: list, out: int, act: str) -> nn.Sequential:
-    layers = [nn.Linear(inp, hidden[0]), resolve_nn_activation(act)]
+    # TallLinear = nn.Linear (same parameters / state_dict keys) with a row-split weight gradient (linear.py)
+    layers = [TallLinear(inp, hidden[0]), resolve_nn_activation(act)]
     for i in range(len(hidden)):
         if i == len(hidden) - 1:
-            layers.append(nn.Linear(hidden[i], out))
+            layers.append(TallLinear(hidden[i], out))
         else:
-            layers.append(nn.Linear(hidden[i], hidden[i + 1]))
+            layers.append(TallLinear(hidden[i], hidden[i + 1]))
             layers.append(resolve_nn_activation(act))
     return nn.Sequential(*layers)
 

@@ -1,0 +1,60 @@
+"""nn.Linear for the PPO update's tall mini-batches (tens of thousands to millions of rows).
+
+The weight gradient dW = dY^T X of a Linear reduces over every row of the mini-batch.  As one GEMM,
+hipBLASLt tiles only its small [out, in] output, so a handful of workgroups stream all rows: at
+65 536 envs (393 216-row mini-batches) the six weight gradients of the 256 x 256 actor + critic took
+~4.9 ms of an ~11 ms update step (`profiles/round01_update65536_nn_linear_kernel_stats.csv`).  Here the rows are
+split into chunks of SPLIT (a batched GEMM: one workgroup set per chunk) and the partial products are
+summed.  Same module tree, parameters and state_dict keys as nn.Linear (the reference's checkpoints
+and exporters are unaffected); small batches, inference and TorchScript take F.linear.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+SPLIT = 4096  # rows per chunk (scripts/prof_update.py --split: 2048-4096 best at 65 536 and 4 096 envs)
+
+
+def split_k_wgrad(gy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """gy^T x for tall gy [M, N], x [M, K]: split over M into chunks of SPLIT rows, summed."""
+    m = x.shape[0]
+    s = m // SPLIT
+    if s < 2:
+        return gy.t() @ x
+    gw = torch.bmm(gy[: s * SPLIT].view(s, SPLIT, -1).transpose(1, 2), x[: s * SPLIT].view(s, SPLIT, -1)).sum(0)
+    if m > s * SPLIT:
+        gw = gw + gy[s * SPLIT:].t() @ x[s * SPLIT:]
+    return gw
+
+
+class _TallLinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = b is not None
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gx = gy @ w if ctx.needs_input_grad[0] else None
+        gw = split_k_wgrad(gy, x) if ctx.needs_input_grad[1] else None
+        gb = gy.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        return gx, gw, gb
+
+
+class TallLinear(nn.Linear):
+    """nn.Linear whose weight gradient is split over the rows for mini-batches of >= 2 * SPLIT rows."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if torch.jit.is_scripting():
+            return F.linear(x, self.weight, self.bias)
+        return self._forward_eager(x)
+
+    @torch.jit.unused
+    def _forward_eager(self, x: torch.Tensor) -> torch.Tensor:
+        if x.dim() == 2 and x.shape[0] >= 2 * SPLIT and torch.is_grad_enabled() and self.weight.requires_grad:
+            return _TallLinearFn.apply(x, self.weight, self.bias)
+        return F.linear(x, self.weight, self.bias)
