@@ -262,7 +262,7 @@ def env_count_sweep(rank, device, a, sizes=(16384, 262144, 1048576)):
     return out
 
 
-def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False):
+def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False, graph_update=False):
     """The reference's Perf/total_fps (24 steps x N / (collect + learn)) of rsl_rl PPO with MLP(256,256):
     config C2 at 4 096 envs fp32; at 65 536 envs also with the fused bf16 rollout inference and bf16
     rollout obs buffers (C5's training options; the update stays fp32)."""
@@ -273,6 +273,7 @@ def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False):
     cfg = QuadcopterPPORunnerCfg(device=device)
     cfg.algorithm.fused_rollout_inference = bool(fused)
     cfg.algorithm.storage_obs_dtype = "bfloat16" if bf16_storage else "float32"
+    cfg.algorithm.graph_update = bool(graph_update)
     runner = OnPolicyRunner(venv, cfg.to_dict(), log_dir=None, device=device)
     runner.learn(1, init_at_random_ep_len=True)  # warm-up iteration
     fps = []
@@ -401,6 +402,7 @@ def main():
         env_c5.close()
     if not a.no_extras:
         extra["train_total_fps_4096_envs"] = train_fps(device)
+        extra["train_total_fps_4096_envs_graph_update"] = train_fps(device, graph_update=True)
         extra["train_total_fps_65536_envs"] = {
             "fp32": train_fps(device, n),
             "fused_rollout_bf16_storage": train_fps(device, n, fused=True, bf16_storage=True),

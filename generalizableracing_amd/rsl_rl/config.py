@@ -40,6 +40,9 @@ class RslRlPpoAlgorithmCfg:
     # not in the reference: dtype of the rollout storage's observation buffers ("bfloat16" halves them;
     # mini-batches are cast back to fp32 for the update)
     storage_obs_dtype: str = "float32"
+    # not in the reference: the update's mini-batch step captured once in a hipGraph and replayed (ppo.py
+    # _GraphedStep; single rank; PPO only)
+    graph_update: bool = False
 
 
 @dataclass

@@ -21,7 +21,8 @@ class PPO:
     def __init__(self, policy, env=None, num_learning_epochs=1, num_mini_batches=1, clip_param=0.2, gamma=0.998,
                  lam=0.95, value_loss_coef=1.0, entropy_coef=0.0, learning_rate=1e-3, max_grad_norm=1.0,
                  use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu",
-                 normalize_advantage=True, storage_obs_dtype=torch.float32, fused_rollout_inference=False, **kwargs):
+                 normalize_advantage=True, storage_obs_dtype=torch.float32, fused_rollout_inference=False,
+                 graph_update=False, **kwargs):
         self.env = env
         self.device = device
         self.desired_kl = desired_kl
@@ -50,6 +51,10 @@ class PPO:
         # accumulation, one launch for actor + sampling + log prob + critic; the update stays fp32 PyTorch
         self.fused_rollout_inference = bool(fused_rollout_inference)
         self.fused = None
+        # the update's mini-batch step (gather, forward, adaptive learning rate, losses, backward, clip,
+        # Adam) captured once in a hipGraph and replayed per mini-batch (single rank, GPU): see _GraphedStep
+        self.graph_update = bool(graph_update)
+        self._graphed = None
 
     def init_storage(self, training_type, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape,
                      action_shape):
@@ -141,6 +146,11 @@ class PPO:
         return surrogate_loss, value_loss
 
     def update(self):
+        if self.graph_update and self.storage is not None and str(self.device).startswith("cuda") \
+                and gdist.world_size() == 1 and type(self).update is PPO.update:
+            if self._graphed is None:
+                self._graphed = _GraphedStep(self)
+            return self._graphed.update()
         mean_value_loss = torch.zeros((), device=self.device)
         mean_surrogate_loss = torch.zeros((), device=self.device)
         generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
@@ -171,3 +181,133 @@ class PPO:
             "value_function": float(mean_value_loss) / num_updates,
             "surrogate": float(mean_surrogate_loss) / num_updates,
         }
+
+
+class _GraphedStep:
+    """PPO.update's mini-batch step as one hipGraph (the same operations as the eager loop, in order).
+
+    Per mini-batch the eager loop launches ~150 small kernels and reads the KL back to the host for the
+    adaptive learning rate (ppo.py:133-150).  Here the learning-rate rule runs on the device (the same
+    comparisons, in fp32), Adam takes the rate as a device tensor (`capturable=True`), and the whole
+    step (mini-batch gathers from the storage by a static index buffer, forward, losses, backward, grad
+    clipping, Adam) is captured once and replayed per mini-batch.  Capture needs warm-up steps; the
+    parameters, the optimizer state and the rate are snapshotted before and restored after, so training
+    is unchanged.  `learning_rate` is read back once per update, for the log."""
+
+    def __init__(self, alg: "PPO"):
+        self.alg = alg
+        st, dev = alg.storage, alg.device
+        self.T, self.N = st.num_transitions_per_env, st.num_envs
+        self.mb = self.T * self.N // alg.num_mini_batches
+        self.params = list(alg.policy.parameters())
+        self.lr = torch.tensor(float(alg.learning_rate), device=dev, dtype=torch.float32)
+        old = alg.optimizer
+        self.opt = optim.Adam(self.params, lr=self.lr, capturable=True)
+        if old.state:  # resumed from a checkpoint: keep Adam's moments and step counts
+            self.opt.load_state_dict(old.state_dict())
+        for g in self.opt.param_groups:  # (load_state_dict brings the eager groups' settings)
+            g["lr"] = self.lr
+            g["capturable"] = True
+        alg.optimizer = self.opt
+        self.idx = torch.zeros(self.mb, dtype=torch.long, device=dev)
+        self.vloss = torch.zeros((), device=dev)
+        self.sloss = torch.zeros((), device=dev)
+        self.graph = None
+
+    def _sources(self):
+        st = self.alg.storage
+        obs = st.observations.flatten(0, 1)
+        priv = st.privileged_observations.flatten(0, 1) if st.privileged_observations is not None else obs
+        return (obs, priv, st.actions.flatten(0, 1), st.values.flatten(0, 1), st.advantages.flatten(0, 1),
+                st.returns.flatten(0, 1), st.actions_log_prob.flatten(0, 1), st.mu.flatten(0, 1),
+                st.sigma.flatten(0, 1))
+
+    def _step(self):
+        alg, pol = self.alg, self.alg.policy
+        obs, priv, act, val, adv, ret, logp, mu, sig = (x.index_select(0, self.idx) for x in self._sources())
+        obs, priv = obs.float(), priv.float()
+        # the eager loop's policy.act also draws a sample it never uses; torch.normal's check of the std
+        # reads back to the host, which a capture forbids, so only the distribution is set here
+        pol.update_distribution(obs)
+        logp_b = pol.get_actions_log_prob(act)
+        value_b = pol.evaluate(priv)
+        mu_b, sigma_b, entropy_b = pol.action_mean, pol.action_std, pol.entropy
+        if alg.desired_kl is not None and alg.schedule == "adaptive":
+            with torch.no_grad():
+                kl = torch.sum(torch.log(sigma_b / sig + 1.0e-5)
+                               + (torch.square(sig) + torch.square(mu - mu_b)) / (2.0 * torch.square(sigma_b)) - 0.5,
+                               axis=-1)
+                k = torch.mean(kl)
+                lr = self.lr
+                up = torch.clamp(lr * 1.5, max=1e-2)
+                down = torch.clamp(lr / 1.5, min=1e-5)
+                lr_new = torch.where(k > alg.desired_kl * 2.0, down,
+                                     torch.where((alg.desired_kl / 2.0 > k) & (k > 0.0), up, lr))
+                self.lr.copy_(lr_new)
+        surrogate_loss, value_loss = alg._ppo_losses(logp_b, logp, adv, value_b, val, ret)
+        loss = surrogate_loss + alg.value_loss_coef * value_loss - alg.entropy_coef * entropy_b.mean()
+        self.opt.zero_grad(set_to_none=False)
+        loss.backward()
+        nn.utils.clip_grad_norm_(self.params, alg.max_grad_norm)
+        self.opt.step()
+        self.vloss.add_(value_loss.detach())
+        self.sloss.add_(surrogate_loss.detach())
+
+    def _capture(self):
+        # snapshot (parameters, optimizer state, rate), warm up on a side stream, capture, restore
+        snap_p = [p.detach().clone() for p in self.params]
+        snap_lr = self.lr.clone()
+        for p in self.params:  # Adam's state tensors must exist (and stay put) before capture
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        snap_o = {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in self.opt.state[p].items()}
+                  for p in self.params}
+        self.idx.copy_(torch.arange(self.mb, device=self.idx.device))
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                self._step()
+        torch.cuda.current_stream().wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._step()
+        with torch.no_grad():
+            for p, v in zip(self.params, snap_p):
+                p.copy_(v)
+            for p in self.params:
+                for k, v in snap_o[id(p)].items():
+                    if torch.is_tensor(v):
+                        self.opt.state[p][k].copy_(v)
+            self.lr.copy_(snap_lr)
+
+    def update(self):
+        alg = self.alg
+        n = alg.num_mini_batches
+        perm = torch.randperm(n * self.mb, device=self.idx.device)  # rollout_storage.py:152-191, drawn first
+        if self.graph is None:
+            had_state = bool(self.opt.state)
+            if not had_state:  # Adam's first step creates its state: take it with zero gradients, then undo
+                snap_p = [p.detach().clone() for p in self.params]
+                for p in self.params:
+                    p.grad = torch.zeros_like(p)
+                self.opt.step()
+                with torch.no_grad():
+                    for p, v in zip(self.params, snap_p):
+                        p.copy_(v)
+                    for p in self.params:
+                        for k, v in self.opt.state[p].items():
+                            if torch.is_tensor(v):
+                                v.zero_()
+            self._capture()
+        self.lr.fill_(float(alg.learning_rate))
+        self.vloss.zero_()
+        self.sloss.zero_()
+        for _ in range(alg.num_learning_epochs):
+            for i in range(n):
+                self.idx.copy_(perm[i * self.mb:(i + 1) * self.mb])
+                self.graph.replay()
+        num_updates = alg.num_learning_epochs * n
+        alg.learning_rate = float(self.lr)
+        alg.storage.clear()
+        return {"value_function": float(self.vloss) / num_updates, "surrogate": float(self.sloss) / num_updates}
