@@ -11,11 +11,14 @@ of a rank, with pre-generated synthetic actions already resident in HBM.
 Envs shard one shard per GPU with no data-path collective ("scaling": "weak");
 `value` = envs * world_size * K / max-over-ranks wall time.
 
-Also reported (same JSON line): the fused kernel's roofline (HIP events
-around every env-kernel launch of an eager pass, algorithmic bytes from
-gr_bytes_per_env_step), the policy-in-the-loop rate (step + actor MLP), one
-PPO training iteration's Perf/total_fps at 4 096 envs (config C2), and the
-CPU oracle timed on the host ("port", rank 0, N=1 only).
+Also reported (same JSON line): the fused kernel's roofline (HIP events over
+graph replays, algorithmic bytes from gr_bytes_per_env_step, PMC traffic from
+profiles/pmc_traffic.json) and the CPU oracle timed on the host ("port", rank 0,
+N=1 only).  Single-GPU extras: policy-in-the-loop rates (PyTorch actor; fused
+MFMA inference in one hipGraph with the step), the step on obstacle tracks, an
+env-count sweep, config C5 (32-gate tracks), Perf/total_fps of PPO training at
+4 096 envs (C2, eager and graph-captured update) and 65 536 envs, and the depth
+camera.  Multi-rank runs report the headline step only.
 """
 from __future__ import annotations
 
