@@ -265,7 +265,7 @@ def env_count_sweep(rank, device, a, sizes=(16384, 262144, 1048576)):
     return out
 
 
-def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False, graph_update=False):
+def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False, graph_update=False, bf16_update=False):
     """The reference's Perf/total_fps (24 steps x N / (collect + learn)) of rsl_rl PPO with MLP(256,256):
     config C2 at 4 096 envs fp32; at 65 536 envs also with the fused bf16 rollout inference and bf16
     rollout obs buffers (C5's training options; the update stays fp32)."""
@@ -277,6 +277,7 @@ def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False, graph_up
     cfg.algorithm.fused_rollout_inference = bool(fused)
     cfg.algorithm.storage_obs_dtype = "bfloat16" if bf16_storage else "float32"
     cfg.algorithm.graph_update = bool(graph_update)
+    cfg.algorithm.update_autocast_bf16 = bool(bf16_update)
     runner = OnPolicyRunner(venv, cfg.to_dict(), log_dir=None, device=device)
     runner.learn(1, init_at_random_ep_len=True)  # warm-up iteration
     fps = []
@@ -409,6 +410,8 @@ def main():
         extra["train_total_fps_65536_envs"] = {
             "fp32": train_fps(device, n),
             "fused_rollout_bf16_storage": train_fps(device, n, fused=True, bf16_storage=True),
+            "fused_bf16_storage_graphed_bf16_update": train_fps(device, n, fused=True, bf16_storage=True,
+                                                                graph_update=True, bf16_update=True),
             "note": "Perf/total_fps, PPO 5 epochs x 4 mini-batches per 24-step rollout, obstacle tracks"}
         # the depth camera of the vision task (separate kernel, same env shard size)
         sys.path.insert(0, os.path.join(ROOT, "scripts"))

@@ -43,6 +43,8 @@ class RslRlPpoAlgorithmCfg:
     # not in the reference: the update's mini-batch step captured once in a hipGraph and replayed (ppo.py
     # _GraphedStep; single rank; PPO only)
     graph_update: bool = False
+    # not in the reference: the update's forward/backward under torch.autocast(bfloat16) (ppo.py)
+    update_autocast_bf16: bool = False
 
 
 @dataclass

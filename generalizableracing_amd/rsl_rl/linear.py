@@ -30,18 +30,24 @@ def split_k_wgrad(gy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
 
 
 class _TallLinearFn(torch.autograd.Function):
+    # custom_fwd / custom_bwd: under torch.autocast (PPO's opt-in bf16 update) the forward GEMM runs in
+    # the autocast dtype and the backward runs under the same autocast state; gradients return in the
+    # parameters' dtype
     @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda")
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
+        ctx.wdtype = w.dtype
         return F.linear(x, w, b)
 
     @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
-        gx = gy @ w if ctx.needs_input_grad[0] else None
-        gw = split_k_wgrad(gy, x) if ctx.needs_input_grad[1] else None
-        gb = gy.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        gx = gy @ w.to(gy.dtype) if ctx.needs_input_grad[0] else None
+        gw = split_k_wgrad(gy, x.to(gy.dtype)).to(ctx.wdtype) if ctx.needs_input_grad[1] else None
+        gb = gy.float().sum(0).to(ctx.wdtype) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return gx, gw, gb
 
 

@@ -22,7 +22,7 @@ class PPO:
                  lam=0.95, value_loss_coef=1.0, entropy_coef=0.0, learning_rate=1e-3, max_grad_norm=1.0,
                  use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu",
                  normalize_advantage=True, storage_obs_dtype=torch.float32, fused_rollout_inference=False,
-                 graph_update=False, **kwargs):
+                 graph_update=False, update_autocast_bf16=False, **kwargs):
         self.env = env
         self.device = device
         self.desired_kl = desired_kl
@@ -55,6 +55,9 @@ class PPO:
         # Adam) captured once in a hipGraph and replayed per mini-batch (single rank, GPU): see _GraphedStep
         self.graph_update = bool(graph_update)
         self._graphed = None
+        # not in the reference (fp32 update): forward/backward of the update under torch.autocast(bf16);
+        # the losses' exp / log / sums stay fp32 (autocast's fp32 list), parameters and Adam stay fp32
+        self.update_autocast_bf16 = bool(update_autocast_bf16)
 
     def init_storage(self, training_type, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape,
                      action_shape):
@@ -155,19 +158,22 @@ class PPO:
         mean_surrogate_loss = torch.zeros((), device=self.device)
         generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
         params = list(self.policy.parameters())
+        ac = torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.update_autocast_bf16 and
+                            str(self.device).startswith("cuda"))
         for (obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch, returns_batch,
              old_actions_log_prob_batch, old_mu_batch, old_sigma_batch, hid_states_batch, masks_batch) in generator:
-            self.policy.act(obs_batch)
-            actions_log_prob_batch = self.policy.get_actions_log_prob(actions_batch)
-            value_batch = self.policy.evaluate(critic_obs_batch)
-            mu_batch = self.policy.action_mean
-            sigma_batch = self.policy.action_std
-            entropy_batch = self.policy.entropy
-            self._adapt_learning_rate(mu_batch, sigma_batch, old_mu_batch, old_sigma_batch)
-            surrogate_loss, value_loss = self._ppo_losses(actions_log_prob_batch, old_actions_log_prob_batch,
-                                                          advantages_batch, value_batch, target_values_batch,
+            with ac:
+                self.policy.act(obs_batch)
+                actions_log_prob_batch = self.policy.get_actions_log_prob(actions_batch)
+                value_batch = self.policy.evaluate(critic_obs_batch)
+                mu_batch = self.policy.action_mean
+                sigma_batch = self.policy.action_std
+                entropy_batch = self.policy.entropy
+            self._adapt_learning_rate(mu_batch.float(), sigma_batch.float(), old_mu_batch, old_sigma_batch)
+            surrogate_loss, value_loss = self._ppo_losses(actions_log_prob_batch.float(), old_actions_log_prob_batch,
+                                                          advantages_batch, value_batch.float(), target_values_batch,
                                                           returns_batch)
-            loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_batch.mean()
+            loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_batch.float().mean()
             self.optimizer.zero_grad()
             loss.backward()
             gdist.allreduce_grads(params)
@@ -228,10 +234,12 @@ class _GraphedStep:
         obs, priv = obs.float(), priv.float()
         # the eager loop's policy.act also draws a sample it never uses; torch.normal's check of the std
         # reads back to the host, which a capture forbids, so only the distribution is set here
-        pol.update_distribution(obs)
-        logp_b = pol.get_actions_log_prob(act)
-        value_b = pol.evaluate(priv)
-        mu_b, sigma_b, entropy_b = pol.action_mean, pol.action_std, pol.entropy
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=alg.update_autocast_bf16):
+            pol.update_distribution(obs)
+            logp_b = pol.get_actions_log_prob(act)
+            value_b = pol.evaluate(priv)
+            mu_b, sigma_b, entropy_b = pol.action_mean, pol.action_std, pol.entropy
+        logp_b, value_b, mu_b, sigma_b, entropy_b = (t.float() for t in (logp_b, value_b, mu_b, sigma_b, entropy_b))
         if alg.desired_kl is not None and alg.schedule == "adaptive":
             with torch.no_grad():
                 kl = torch.sum(torch.log(sigma_b / sig + 1.0e-5)

@@ -49,6 +49,8 @@ def build_parser() -> argparse.ArgumentParser:
                    help="Rollout inference as one bf16 MFMA launch (algorithm.fused_rollout_inference).")
     p.add_argument("--graph_update", action="store_true", default=False,
                    help="PPO mini-batch step as one replayed hipGraph (algorithm.graph_update, single GPU).")
+    p.add_argument("--bf16_update", action="store_true", default=False,
+                   help="PPO update forward/backward under bf16 autocast (algorithm.update_autocast_bf16).")
     p.add_argument("--bf16_storage", action="store_true", default=False,
                    help="bf16 observation buffers in the rollout storage (algorithm.storage_obs_dtype).")
     cli_args.add_rsl_rl_args(p)
@@ -97,6 +99,8 @@ def main(argv=None):
         agent_cfg.algorithm.storage_obs_dtype = "bfloat16"
     if args.graph_update:
         agent_cfg.algorithm.graph_update = True
+    if args.bf16_update:
+        agent_cfg.algorithm.update_autocast_bf16 = True
     device = args.device or (f"cuda:{local_rank}" if torch.cuda.is_available() else "cpu")
     agent_cfg.device = device
     env_cfg.sim.device = device

@@ -71,3 +71,43 @@ def test_graphed_update_matches_eager():
                     sg[key].copy_(se[key])
         alg_g.learning_rate = alg.learning_rate
     assert alg_g._graphed is not None and alg_g._graphed.graph is not None
+
+
+def test_bf16_autocast_update_follows_fp32():
+    """algorithm.update_autocast_bf16 (with the graphed step): not the reference's fp32 arithmetic, so held
+    to the fp32 update's direction: per parameter tensor, the cosine between the two updates > 0.9, and
+    the same adaptive learning rate."""
+    torch.manual_seed(4)
+    n = 4096
+    env = RslRlVecEnvWrapper(RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV))))
+    cfg = QuadcopterPPORunnerCfg(device=DEV)
+    runner = OnPolicyRunner(env, cfg.to_dict(), log_dir=None, device=DEV)
+    alg = runner.alg
+    kw = dict(cfg.to_dict()["algorithm"])
+    kw.pop("class_name")
+    kw.update(graph_update=True, update_autocast_bf16=True)
+    alg_b = PPO(copy.deepcopy(alg.policy), device=DEV, **kw)
+    alg_b.init_storage("rl", n, cfg.num_steps_per_env, [16], [16], [4])
+    obs, extras = env.get_observations()
+    cobs = extras["observations"]["critic"]
+    with torch.inference_mode():
+        for _ in range(cfg.num_steps_per_env):
+            a = alg.act(obs, cobs)
+            obs, rew, dones, infos = env.step(a)
+            cobs = infos["observations"]["critic"]
+            alg.process_env_step(rew, dones, infos)
+        alg.compute_returns(cobs)
+    for name, v in vars(alg.storage).items():
+        if torch.is_tensor(v):
+            getattr(alg_b.storage, name).copy_(v)
+    p0 = [p.detach().clone() for p in alg.policy.parameters()]
+    torch.manual_seed(9)
+    le = alg.update()
+    torch.manual_seed(9)
+    lb = alg_b.update()
+    for pe, pb, q in zip(alg.policy.parameters(), alg_b.policy.parameters(), p0):
+        de, db = (pe - q).flatten(), (pb - q).flatten()
+        cos = float(torch.dot(de, db) / (de.norm() * db.norm() + 1e-20))
+        assert cos > 0.9, cos
+    assert all(torch.isfinite(torch.tensor(list(lb.values()))))
+    assert abs(le["value_function"] - lb["value_function"]) <= 0.05 * abs(le["value_function"])
