@@ -251,6 +251,9 @@ class OnPolicyRunner:
             self.privileged_obs_normalizer.load_state_dict(loaded["privileged_obs_norm_state_dict"])
         if load_optimizer and resumed:
             self.alg.optimizer.load_state_dict(loaded["optimizer_state_dict"])
+            for g in self.alg.optimizer.param_groups:  # a graph-captured update saves its rate as a tensor
+                if torch.is_tensor(g["lr"]):
+                    g["lr"] = float(g["lr"])
         if resumed:
             self.current_learning_iteration = loaded["iter"]
         return loaded["infos"]

@@ -153,7 +153,10 @@ class PPO:
                 and gdist.world_size() == 1 and type(self).update is PPO.update:
             if self._graphed is None:
                 self._graphed = _GraphedStep(self)
-            return self._graphed.update()
+            out = self._graphed.update()
+            if self.fused is not None:  # graph replays write the parameters without bumping their versions
+                self.fused.refresh()
+            return out
         mean_value_loss = torch.zeros((), device=self.device)
         mean_surrogate_loss = torch.zeros((), device=self.device)
         generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)

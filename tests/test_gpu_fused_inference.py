@@ -88,7 +88,8 @@ def test_refresh_after_update_and_graph_capture():
     assert not torch.equal(a0, fused.actions)
 
 
-def test_ppo_rollout_with_fused_inference():
+@pytest.mark.parametrize("graph_update", [False, True])
+def test_ppo_rollout_with_fused_inference(graph_update):
     """PPO with algorithm.fused_rollout_inference on the HIP env: the stored rollout matches the fp32 module,
     the log probs are those of the stored (mean, sigma, action), and an update is picked up by the next act."""
     from generalizableracing_amd.envs.racing_cfg import RacingEnvCfg, SceneCfg, SimCfg
@@ -100,6 +101,7 @@ def test_ppo_rollout_with_fused_inference():
     env = RslRlVecEnvWrapper(RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV))))
     cfg = QuadcopterPPORunnerCfg(device=DEV)
     cfg.algorithm.fused_rollout_inference = True
+    cfg.algorithm.graph_update = graph_update  # replays do not bump parameter versions: PPO refreshes
     runner = OnPolicyRunner(env, cfg.to_dict(), log_dir=None, device=DEV)
     alg, pol = runner.alg, runner.alg.policy
     assert alg.fused is not None
