@@ -4,9 +4,11 @@
 
 #include "../../include/gr.h"
 
-#define GR_BLOCK 256
+#ifndef GR_BLOCK
+#define GR_BLOCK 256  // envs per step workgroup (three roles x GR_BLOCK / 64 waves)
+#endif
 #define GR_MAX_TYPES 64
-#define GR_LOG_ROWS_PER_BLOCK 4  // log rows per workgroup (one per physics wave of the step kernel)
+#define GR_LOG_ROWS_PER_BLOCK (GR_BLOCK / 64)  // log rows per workgroup (one per physics wave of the step kernel)
 // step kernel handovers + store staging + obstacle hand-over (3 rows + ready flags) in LDS
 #define GR_XCH_BYTES ((5 + 6 + 8 + 3) * GR_BLOCK * 16 + 16)
 #define GR_LDS_MAX (160 * 1024)                 // LDS a gfx950 workgroup may allocate

@@ -985,8 +985,13 @@ DEV void merge_handover(const float4* xch, int t, bool reset, Env& e) {
   e.azero = reset ? 1 : 0;
 }
 
+#ifdef GR_STEP_MINB  // timing variants: minimum resident workgroups per CU (caps the VGPRs)
+#define GR_STEP_LB __launch_bounds__(3 * GR_BLOCK, GR_STEP_MINB)
+#else
+#define GR_STEP_LB __launch_bounds__(3 * GR_BLOCK)
+#endif
 template <bool USE_LDS, bool OBST>
-__global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KConst* __restrict__ kc,
+__global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
                                                              const float* __restrict__ actions) {
   a.kc = kc;
   extern __shared__ __attribute__((aligned(16))) float4 lds[];
@@ -994,7 +999,7 @@ __global__ __launch_bounds__(3 * GR_BLOCK) void step_kernel(KArgs a, const KCons
   float4* stg = xch + (GR_XF4 + GR_RF4) * GR_BLOCK;         // [GR_SF4][GR_BLOCK] store staging
   float4* obx = stg + GR_SF4 * GR_BLOCK;                    // [GR_OF4][GR_BLOCK] obstacle hand-over (OBST)
   int* oflag = reinterpret_cast<int*>(obx + GR_OF4 * GR_BLOCK);  // [GR_BLOCK / 64] mask-ready flags (OBST)
-  const int role = threadIdx.x >> 8;                        // wave-uniform: 0 physics, 1 policy, 2 episode
+  const int role = threadIdx.x / GR_BLOCK;                  // wave-uniform: 0 physics, 1 policy, 2 episode
   const int t = threadIdx.x & (GR_BLOCK - 1);
   const int n = a.h.num_envs;
   const int i = blockIdx.x * GR_BLOCK + t;
