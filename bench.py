@@ -87,21 +87,23 @@ def make_env(n, rank, device, gates, integrator, obstacles=True):
     return env
 
 
-def capture_graph(env, actions):
-    """hipGraph of ACTION_RING consecutive env steps (buffer bindings and action pointers baked in)."""
+def capture_graph(env, actions, length=ACTION_RING):
+    """hipGraph of `length` (<= ACTION_RING) consecutive env steps (buffer bindings and action pointers baked
+    in).  The host call counter is realigned to a multiple of the ring first, so every graph starts on the
+    same bindings and replays of several graphs chain like consecutive eager calls."""
+    assert 1 <= length <= ACTION_RING
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
         for k in range(2):  # stream warm-up outside capture
             env.step(actions[k % ACTION_RING])
     torch.cuda.current_stream().wait_stream(s)
-    # realign the host-side call counter to a multiple of the ring
     while env._calls % ACTION_RING != 0:
         env.step(actions[env._calls % ACTION_RING])
     torch.cuda.synchronize()
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
-        for k in range(ACTION_RING):
+        for k in range(length):
             env.step(actions[k])
     torch.cuda.synchronize()
     graph.replay()
@@ -110,63 +112,65 @@ def capture_graph(env, actions):
 
 
 def time_env_steps(env, actions, steps, use_graph):
-    """Returns (seconds for exactly `steps` env steps, launch mode, graph or None)."""
-    mode = "eager"
-    graph = None
-    if use_graph and steps >= ACTION_RING:
-        try:
-            graph = capture_graph(env, actions)
-            mode = "hipgraph"
-        except Exception as e:  # graph capture unavailable: fall back to eager launches
-            print(f"[bench] hipGraph capture failed ({e}); timing eager launches", file=sys.stderr)
-            graph = None
-    reps, rem = (steps // ACTION_RING, steps % ACTION_RING) if graph is not None else (0, steps)
+    """Returns (seconds for exactly `steps` env steps, launch mode, the 64-step graph or None).
+
+    Graph mode times steps // 64 replays of a 64-step graph plus one replay of a graph of the remaining
+    steps % 64 launches, so any K (the driver's K=20 included) is timed as hipGraph launches."""
+    graph = rem_graph = None
+    reps, rem = 0, steps
+    if use_graph:
+        graph = capture_graph(env, actions)
+        reps, rem = divmod(steps, ACTION_RING)
+        if rem:
+            rem_graph = capture_graph(env, actions, rem)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
         graph.replay()
-    for k in range(rem):
-        env.step(actions[k % ACTION_RING])
+    if rem_graph is not None:
+        rem_graph.replay()
+    elif graph is None:
+        for k in range(rem):
+            env.step(actions[k % ACTION_RING])
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
-    return t1 - t0, mode, graph
+    del rem_graph
+    return t1 - t0, ("hipgraph" if graph is not None else "eager"), graph
 
 
-def kernel_timing(env, actions, steps, graph):
-    """Average duration of one fused-kernel launch, from HIP events on the launch stream.
-
-    Graph mode: one event pair around back-to-back replays of the 64-launch graph (each replay is
-    exactly 64 env-kernel launches on torch's current stream, which is the stream gr_step launches
-    on), so the per-launch figure includes the graph's inter-kernel gaps — the same quantity
-    rocprofv3's kernel-trace average approximates from below.  Also returned: the C ABI's own
-    per-launch event pairs (gr_set_timing) from an eager pass, which add event-record overhead."""
-    import ctypes as C
-
-    out = {}
-    if graph is not None:
-        reps = max(1, min(steps, 4096) // ACTION_RING)
-        stream = torch.cuda.current_stream()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+def repeat_median(graph, n, reps=3, length=1024):
+    """SURVEY §8d's steady-state form: `reps` timed runs of `length` steps (64-step graph replays), median
+    env-steps/s of one rank."""
+    rates = []
+    for _ in range(reps):
         torch.cuda.synchronize()
-        e0.record(stream)
-        for _ in range(reps):
+        t0 = time.perf_counter()
+        for _ in range(length // ACTION_RING):
             graph.replay()
-        e1.record(stream)
-        e1.synchronize()
-        out["graph_event_us"] = e0.elapsed_time(e1) * 1e3 / (reps * ACTION_RING)
-    lib, ctx = env._lib, env._ctx
-    n = min(steps, 1024)
-    assert lib.gr_set_timing(ctx, 1) == 0
-    for k in range(n):
-        env.step(actions[k % ACTION_RING])
-    tot, cnt = C.c_double(), C.c_int64()
-    assert lib.gr_read_timing(ctx, C.byref(tot), C.byref(cnt)) == 0
-    lib.gr_set_timing(ctx, 0)
-    out["eager_event_us"] = tot.value * 1e3 / cnt.value
-    out["kernel_us"] = out.get("graph_event_us", out["eager_event_us"])
-    return out
+        torch.cuda.synchronize()
+        rates.append(n * (length // ACTION_RING) * ACTION_RING / (time.perf_counter() - t0))
+    return float(np.median(rates))
+
+
+def kernel_timing(graph, replays=16):
+    """Average duration of one fused-kernel launch: HIP events on the launch stream around back-to-back
+    replays of the 64-launch graph (each replay is exactly 64 env-kernel launches on torch's current stream,
+    the stream gr_step launches on), so the per-launch figure includes the graph's inter-kernel gaps — the
+    quantity rocprofv3's kernel-trace average approximates from below.  Per-launch event pairs are never
+    used: their record overhead exceeds the kernel's own time at this size."""
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    graph.replay()
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for _ in range(replays):
+        graph.replay()
+    e1.record(stream)
+    e1.synchronize()
+    return {"kernel_us": e0.elapsed_time(e1) * 1e3 / (replays * ACTION_RING),
+            "timing": f"HIP events around {replays} back-to-back replays of a {ACTION_RING}-launch hipGraph"}
 
 
 def policy_in_loop(env, steps, device):
@@ -184,6 +188,47 @@ def policy_in_loop(env, steps, device):
             obs = env.step(pol.act_inference(obs))[0]["policy"]
         torch.cuda.synchronize()
     return env.num_envs * steps / (time.perf_counter() - t0)
+
+
+def policy_in_loop_graphed(env, steps, device):
+    """SURVEY §8d env-only rate at the reference's precision: per step the fp32 PyTorch actor MLP
+    (16-256-256-4, LeakyReLU) computes the mean, a Gaussian sample a = mu + std * eps is drawn (what
+    Normal.sample computes; torch.normal itself reads the std back to the host, which a capture forbids),
+    and gr_step runs on it; 64 such steps are captured in one hipGraph and replayed."""
+    from generalizableracing_amd.rsl_rl import ActorCritic
+
+    n = env.num_envs
+    pol = ActorCritic(16, 16, 4, [256, 256], [256, 256], "lrelu").to(device).eval()
+
+    def one_step(obs):
+        with torch.no_grad():
+            mu = pol.actor(obs)
+            a = mu + pol.std * torch.randn_like(mu)
+        return env.step(a)[0]["policy"]
+
+    obs = env.observe()["policy"]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            obs = one_step(obs)
+    torch.cuda.current_stream().wait_stream(s)
+    while env._calls % ACTION_RING != 0:
+        obs = one_step(obs)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        o = obs
+        for _ in range(ACTION_RING):
+            o = one_step(o)
+    g.replay()
+    torch.cuda.synchronize()
+    reps = max(1, steps // ACTION_RING)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        g.replay()
+    torch.cuda.synchronize()
+    return n * reps * ACTION_RING / (time.perf_counter() - t0)
 
 
 def policy_in_loop_fused(env, steps, device):
@@ -252,13 +297,14 @@ def env_count_sweep(rank, device, a, sizes=(16384, 262144, 1048576)):
             env.step(acts[k % ACTION_RING])
         torch.cuda.synchronize()
         graph = capture_graph(env, acts)
-        kt = kernel_timing(env, acts, 2 * ACTION_RING, graph)
+        kt = kernel_timing(graph)
         del graph
         rd, wr = env.bytes_per_env_step()
-        us = kt["graph_event_us"]
+        us = kt["kernel_us"]
         out[str(n)] = {"kernel_us": us, "env_steps_per_s": n / (us * 1e-6),
                        "achieved_GBps": (rd + wr) * n / (us * 1e-6) / 1e9,
-                       "frac_of_8TBps": (rd + wr) * n / (us * 1e-6) / 8e12}
+                       "frac_of_8TBps": (rd + wr) * n / (us * 1e-6) / 8e12,
+                       "read_frac_of_8TBps": rd * n / (us * 1e-6) / 8e12}
         env.close()
         del acts
         torch.cuda.empty_cache()
@@ -353,19 +399,30 @@ def main():
     secs, mode, graph = time_env_steps(env, actions, a.steps, not a.no_graph)
     secs = max_over_ranks(secs, device)
     value = n * ws * a.steps / secs
-    kt = kernel_timing(env, actions, a.steps, graph)
+    if graph is None:  # --no-graph: the timed region ran eager, the kernel is still timed from graph replays
+        graph = capture_graph(env, actions)
+    kt = kernel_timing(graph)
+    steady = repeat_median(graph, n)
     del graph
     us = kt["kernel_us"]
+    ms_per_step = secs * 1e3 / a.steps
+    if us > ms_per_step * 1e3:  # a per-launch kernel time cannot exceed the wall time per step
+        raise RuntimeError(f"kernel_us {us:.2f} > wall us per step {ms_per_step * 1e3:.2f}: timing is inconsistent")
     rd, wr = env.bytes_per_env_step()
     achieved = (rd + wr) * n / (us * 1e-6) / 1e9
-    extra = {}
+    extra = {"steady_state_env_steps_per_s_per_gpu": steady,
+             "steady_state_note": "median of 3 timed runs of 1024 steps (16 replays of the 64-step graph), one rank"}
     if not a.no_extras:
+        extra["env_only_fp32"] = {
+            "env_steps_per_s": policy_in_loop_graphed(env, 1024, device),
+            "launch": "hipgraph (64 x [PyTorch fp32 actor MLP 16-256-256-4 + Gaussian sample + gr_step])",
+            "note": "SURVEY §8d env-only rate: gr_step + policy inference at the reference's fp32"}
         extra["policy_in_loop_env_steps_per_s"] = policy_in_loop(env, 256, device)
-        rate, us, tfs = policy_in_loop_fused(env, 512, device)
+        rate, us_pol, tfs = policy_in_loop_fused(env, 512, device)
         extra["policy_in_loop_fused"] = {
             "env_steps_per_s": rate, "launch": "hipgraph (64 x [fused inference + gr_step])",
             "inference_kernel": "gr::policy_kernel<256> (MFMA 16x16x32 bf16, fp32 accumulate)",
-            "inference_kernel_us": us, "inference_TFLOPs": tfs,
+            "inference_kernel_us": us_pol, "inference_TFLOPs": tfs,
             "note": "actor+critic MLP(16-256-256-out), Gaussian sample + log prob; bf16 operands (C5)"}
     env.close()
     if not a.no_extras and not a.obstacles:
@@ -377,13 +434,17 @@ def main():
         torch.cuda.synchronize()
         secs_o, mode_o, graph_o = time_env_steps(env_o, actions, a.steps, not a.no_graph)
         secs_o = max_over_ranks(secs_o, device)
-        kt_o = kernel_timing(env_o, actions, a.steps, graph_o)
+        if graph_o is None:
+            graph_o = capture_graph(env_o, actions)
+        kt_o = kernel_timing(graph_o)
         del graph_o
         rd_o, wr_o = env_o.bytes_per_env_step()
         extra["with_obstacles"] = {
             "value": n * ws * a.steps / secs_o, "unit": "env-steps/s", "kernel": "gr::step_kernel<true, true>",
             "kernel_us": kt_o["kernel_us"], "bytes_per_env_step": {"read": rd_o, "written": wr_o},
             "achieved_GBps": (rd_o + wr_o) * n / (kt_o["kernel_us"] * 1e-6) / 1e9,
+            "frac": (rd_o + wr_o) * n / (kt_o["kernel_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS,
+            "read_frac": rd_o * n / (kt_o["kernel_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS,
             "traffic": load_traffic(n, a.gates, 1),
             "obstacles_per_track_max": int(env_o.obstacle_table.counts.max()),
             "obstacles_per_track_mean": float(env_o.obstacle_table.counts.mean())}
@@ -396,8 +457,8 @@ def main():
         for k in range(a.warmup):
             env_c5.step(actions[k % ACTION_RING])
         torch.cuda.synchronize()
-        _, _, graph_c5 = time_env_steps(env_c5, actions, 2 * ACTION_RING, not a.no_graph)
-        kt_c5 = kernel_timing(env_c5, actions, 2 * ACTION_RING, graph_c5)
+        graph_c5 = capture_graph(env_c5, actions)
+        kt_c5 = kernel_timing(graph_c5)
         del graph_c5
         rate_c5, us_c5, _ = policy_in_loop_fused(env_c5, 512, device)
         extra["c5_32_gates"] = {"step_kernel_us": kt_c5["kernel_us"], "step_env_steps_per_s": n / (kt_c5["kernel_us"] * 1e-6),
@@ -438,7 +499,7 @@ def main():
             "n_gpus": ws,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": secs * 1e3 / a.steps,
+            "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -451,6 +512,10 @@ def main():
                        "num_envs_per_gpu": n, "launch": mode, "parallelism": f"env-shard x{ws}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac_definition": "(read + written algorithmic bytes) / kernel_us / 8 TB/s",
+                         "read_achieved": rd * n / (us * 1e-6) / 1e9,
+                         "read_frac": rd * n / (us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                         "read_frac_definition": "the north star's HBM-read roofline: read bytes only",
                          "kernel": f"gr::step_kernel<true, {'true' if a.obstacles else 'false'}> (fused step)", **kt,
                          "algorithmic_bytes_per_launch": (rd + wr) * n,
                          "bytes_per_env_step": {"read": rd, "written": wr}},

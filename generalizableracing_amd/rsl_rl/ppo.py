@@ -263,11 +263,15 @@ class _GraphedStep:
         self.opt.step()
         self.vloss.add_(value_loss.detach())
         self.sloss.add_(surrogate_loss.detach())
+        # drop this step's autograd graph (the distribution holds it): an AccumulateGrad node kept alive from a
+        # warm-up step on the side stream would otherwise meet the capture stream's gradients
+        pol.distribution = None
 
     def _capture(self):
         # snapshot (parameters, optimizer state, rate), warm up on a side stream, capture, restore
         snap_p = [p.detach().clone() for p in self.params]
         snap_lr = self.lr.clone()
+        self.alg.policy.distribution = None  # the eager path's last graph (created on another stream)
         for p in self.params:  # Adam's state tensors must exist (and stay put) before capture
             if p.grad is None:
                 p.grad = torch.zeros_like(p)

@@ -91,10 +91,12 @@ class RolloutStorage:
             delta = self.rewards[step] + next_is_not_terminal * gamma * next_values - self.values[step]
             advantage = delta + next_is_not_terminal * gamma * lam * advantage
             self.returns[step] = advantage + self.values[step]
-        self.advantages = self.returns - self.values
+        # in place: the graph-captured update (ppo.py _GraphedStep) gathers from this allocation, so
+        # rebinding the attribute would leave its replays reading the first iteration's freed buffer
+        torch.sub(self.returns, self.values, out=self.advantages)
         if normalize_advantage:
             mean, std = gdist.global_mean_std(self.advantages)
-            self.advantages = (self.advantages - mean) / (std + 1e-8)
+            self.advantages.sub_(mean).div_(std + 1e-8)
 
     def get_statistics(self):
         done = self.dones.clone()

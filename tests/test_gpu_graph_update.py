@@ -111,3 +111,58 @@ def test_bf16_autocast_update_follows_fp32():
         assert cos > 0.9, cos
     assert all(torch.isfinite(torch.tensor(list(lb.values()))))
     assert abs(le["value_function"] - lb["value_function"]) <= 0.05 * abs(le["value_function"])
+
+
+def test_graphed_update_across_iterations():
+    """Three rollout + compute_returns + update iterations, graphed vs eager, each on its own storage.
+    compute_returns runs on the graphed algorithm's storage every iteration, so a graph whose gathers
+    were baked against an earlier iteration's advantages / returns allocation would read stale data
+    (the surrogate loss then disagrees from the second iteration on)."""
+    torch.manual_seed(5)
+    n = 2048
+    env = RslRlVecEnvWrapper(RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV))))
+    cfg = QuadcopterPPORunnerCfg(device=DEV)
+    runner = OnPolicyRunner(env, cfg.to_dict(), log_dir=None, device=DEV)
+    alg = runner.alg
+    kw = dict(cfg.to_dict()["algorithm"])
+    kw.pop("class_name")
+    kw["graph_update"] = True
+    alg_g = PPO(copy.deepcopy(alg.policy), device=DEV, **kw)
+    alg_g.init_storage("rl", n, cfg.num_steps_per_env, [16], [16], [4])
+    raw = ("observations", "privileged_observations", "actions", "rewards", "dones", "values",
+           "actions_log_prob", "mu", "sigma")
+    obs, extras = env.get_observations()
+    cobs = extras["observations"]["critic"]
+    adv_ptr = alg_g.storage.advantages.data_ptr()
+    for it in range(3):
+        with torch.inference_mode():
+            for _ in range(cfg.num_steps_per_env):
+                a = alg.act(obs, cobs)
+                obs, rew, dones, infos = env.step(a)
+                cobs = infos["observations"]["critic"]
+                alg.process_env_step(rew, dones, infos)
+            alg.compute_returns(cobs)
+            for name in raw:
+                getattr(alg_g.storage, name).copy_(getattr(alg.storage, name))
+            alg_g.storage.step = cfg.num_steps_per_env
+            alg_g.compute_returns(cobs)
+        assert alg_g.storage.advantages.data_ptr() == adv_ptr  # written in place every iteration
+        torch.testing.assert_close(alg_g.storage.advantages, alg.storage.advantages, rtol=1e-5, atol=1e-5)
+        p0 = [p.detach().clone() for p in alg.policy.parameters()]
+        torch.manual_seed(11 + it)
+        le = alg.update()
+        torch.manual_seed(11 + it)
+        lg = alg_g.update()
+        for pe, pg, q in zip(alg.policy.parameters(), alg_g.policy.parameters(), p0):
+            moved = float((pe - q).abs().max())
+            diff = float((pe - pg).abs().max())
+            assert moved > 0.0 and diff <= 0.05 * moved, (it, diff, moved)
+        for k in ("value_function", "surrogate"):
+            assert abs(le[k] - lg[k]) <= 1e-4 * (abs(le[k]) + 1e-6), (it, k, le[k], lg[k])
+        with torch.no_grad():
+            for pe, pg in zip(alg.policy.parameters(), alg_g.policy.parameters()):
+                pg.copy_(pe)
+                se, sg = alg.optimizer.state[pe], alg_g.optimizer.state[pg]
+                for key in ("exp_avg", "exp_avg_sq", "step"):
+                    sg[key].copy_(se[key])
+        alg_g.learning_rate = alg.learning_rate
