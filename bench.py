@@ -406,7 +406,11 @@ def main():
     del graph
     us = kt["kernel_us"]
     ms_per_step = secs * 1e3 / a.steps
-    if us > ms_per_step * 1e3:  # a per-launch kernel time cannot exceed the wall time per step
+    # a per-launch kernel time cannot exceed the wall time per step of the same graph launches; only checked
+    # for a graph-timed region on a device of its own (eager launches under a PMC profiler, or rehearsal ranks
+    # sharing one GPU, interleave other work into the event window)
+    shared = ws > torch.cuda.device_count()
+    if mode == "hipgraph" and not shared and us > ms_per_step * 1e3:
         raise RuntimeError(f"kernel_us {us:.2f} > wall us per step {ms_per_step * 1e3:.2f}: timing is inconsistent")
     rd, wr = env.bytes_per_env_step()
     achieved = (rd + wr) * n / (us * 1e-6) / 1e9

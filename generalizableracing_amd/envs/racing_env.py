@@ -351,13 +351,35 @@ class RacingEnv:
         self._render(_abi.GR_CAM_STEP)
         self.common_step_counter += 1
         self.extras = {"log": log}
-        res = (self._obs_dict(out), out["reward"], out["terminated"], out["time_out"], self.extras)
         if self._regen_steps is not None and self.common_step_counter % self._regen_steps == 0:
-            # interval event after the step (IL EventManager "interval" mode); the step's own outputs
-            # are returned, the next step starts on the new terrain
-            self.regenerate_terrain()
-            res[4]["terrain_regenerated"] = True
-        return res
+            self._regenerate_in_step()
+        return self._obs_dict(out), out["reward"], out["terminated"], out["time_out"], self.extras
+
+    def _regenerate_in_step(self):
+        """The terrain interval event inside step (manager_based_diff_rl_env.py:259-264): after the step's
+        resets and command update, reset_terrain_period (mdp/events.py:180-204) rebuilds the terrain and
+        calls env.reset(); the observations are computed after it.  So the step returns its own reward /
+        terminated / time-outs / dones with the post-reset observations and the reset's extras["log"].
+
+        Call k (this step) wrote output set B.  The reset (call k+1) writes set A, which still holds the
+        previous step's observations that the runner keeps in its transition until process_env_step; the
+        observation pass (call k+2) writes the post-reset observations back into set B, over the step's
+        observation rows only; set A's rows are then restored.  The next step (call k+3) writes set A and
+        reads the post-reset rows of set B as its previous observation."""
+        held = self._sets[(self._cur + 1) % 2]
+        keys = ("policy", "critic", "auxiliary")
+        saved = [held[k].clone() for k in keys]
+        if self.camera is not None:
+            held_img = self._img_sets[(self._cur + 1) % 2]
+            saved_img = [held_img[k].clone() for k in ("policy", "critic")]
+        _, extras = self.regenerate_terrain()
+        self.observe()
+        for k, v in zip(keys, saved):
+            held[k].copy_(v)
+        if self.camera is not None:
+            for k, v in zip(("policy", "critic"), saved_img):
+                held_img[k].copy_(v)
+        self.extras = {"log": extras["log"], "terrain_regenerated": True}
 
     def reset(self, seed: int | None = None, env_ids=None, options=None):
         """ManagerBasedEnv.reset -> _reset_idx(env_ids) (+ curriculum), then observations."""

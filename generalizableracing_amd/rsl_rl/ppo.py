@@ -263,9 +263,6 @@ class _GraphedStep:
         self.opt.step()
         self.vloss.add_(value_loss.detach())
         self.sloss.add_(surrogate_loss.detach())
-        # drop this step's autograd graph (the distribution holds it): an AccumulateGrad node kept alive from a
-        # warm-up step on the side stream would otherwise meet the capture stream's gradients
-        pol.distribution = None
 
     def _capture(self):
         # snapshot (parameters, optimizer state, rate), warm up on a side stream, capture, restore
@@ -284,6 +281,11 @@ class _GraphedStep:
             for _ in range(3):
                 self._step()
         torch.cuda.current_stream().wait_stream(s)
+        # the last warm-up's autograd graph (held by the distribution) keeps AccumulateGrad nodes of the side
+        # stream alive into the capture stream; drop it here, outside the capture (dropping it inside the
+        # captured step returns blocks to the graph's pool mid-capture and corrupted the replays)
+        torch.cuda.synchronize()
+        self.alg.policy.distribution = None
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self._step()

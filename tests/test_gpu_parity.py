@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 import oracle  # noqa: E402
 from generalizableracing_amd import _abi  # noqa: E402
 from generalizableracing_amd.envs.racing_cfg import RacingEnvCfg, SceneCfg, SimCfg, TerrainCfg  # noqa: E402
-from generalizableracing_amd.envs.racing_env import RacingEnv  # noqa: E402
+from generalizableracing_amd.envs.racing_env import RacingEnv, RslRlVecEnvWrapper  # noqa: E402
 
 DEV = "cuda:0"
 
@@ -230,7 +230,52 @@ def test_terrain_regeneration_matches_oracle():
         torch.cuda.synchronize()
         assert_envs_equal(kernel_envs(env), orc.envs, f"after regen step {k}")
         assert not extras.get("terrain_regenerated")
-    _, _, _, _, extras = env.step(torch.randn(n, 4, generator=g).to(DEV))
+    # the regenerating step: the step's reward / dones with the post-reset observations (reference order:
+    # interval event, then observation compute), and the previous step's observation tensors untouched
+    prev_obs = {k: v for k, v in env.obs_buf.items()}
+    prev_copy = {k: v.clone() for k, v in prev_obs.items()}
+    a = (torch.randn(n, 4, generator=g)).numpy().astype(np.float32)
+    obs, rew, term, tout, extras = env.step(torch.from_numpy(a).to(DEV))
     assert extras.get("terrain_regenerated") and env.terrain_generation == 2
     assert bool((env.episode_length_buf == 0).all())
+    orc.step(a)
+    want_rew, want_term, want_dones = orc.reward.copy(), orc.terminated.copy(), orc.dones.copy()
+    orc2 = oracle.from_env(env)  # the new terrain's tables
+    orc2.envs[:] = orc.envs
+    orc2.obs_critic[:] = orc.obs_critic
+    orc2.obs_aux[:] = orc.obs_aux
+    orc2.time_out[:] = orc.time_out
+    orc2.counter[0] = orc.counter[0]
+    orc2.reset(None)
+    orc2.observe()
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(rew.cpu().numpy()), bits(want_rew))
+    assert np.array_equal(term.cpu().numpy().astype(np.uint8), want_term)
+    assert np.array_equal(env._sets[env._cur]["dones"].cpu().numpy(), want_dones)
+    assert_envs_equal(kernel_envs(env), orc2.envs, "regenerating step")
+    compare_outputs(env, orc2, "regenerating step")
+    for k, v in prev_obs.items():
+        assert torch.equal(v, prev_copy[k]), k
     env.close()
+
+
+def test_wrapper_across_terrain_regeneration():
+    """RslRlVecEnvWrapper over a regenerating step: dones are the step's, the runner's previous
+    observation tensor still holds the previous step's rows when process_env_step copies it."""
+    n = 256
+    cfg = RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV), stage=1,
+                       terrain=TerrainCfg(regen_interval_s=0.03 * 3))
+    venv = RslRlVecEnvWrapper(RacingEnv(cfg))
+    obs, _ = venv.get_observations()
+    g = torch.Generator().manual_seed(2)
+    for k in range(3):
+        kept = obs.clone()
+        a = torch.randn(n, 4, generator=g).to(DEV)
+        obs_next, rew, dones, extras = venv.step(a)
+        torch.cuda.synchronize()
+        assert torch.equal(obs, kept), k  # the transition's observation tensor is intact
+        want = (extras["time_outs"] | venv.env._sets[venv.env._cur]["terminated"]).long()
+        assert torch.equal(dones, want), k
+        obs = obs_next
+    assert extras.get("terrain_regenerated")
+    venv.close()
