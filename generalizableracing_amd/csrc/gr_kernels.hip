@@ -437,6 +437,17 @@ DEV uint32_t collision_mask(const KArgs& a, const Tab& tab, int type, int lvl, c
 }
 
 // ------------------------------------------------------------- controller
+// ThrustController.update (thrust_controller_diff.py:182-186): desired rotor thrusts -> motor speeds
+// (Thrust2Omega :167-176) -> first-order motor lag -> realised thrusts (Omega2Thrust :178-179), in place
+DEV void motor_update(const KArgs& a, float f[4], float mw[4]) {
+  for (int i = 0; i < 4; ++i) {
+    float t3 = a.kc->tm_k1sq - a.kc->tm_4k2 * (a.kc->tm_k0 - f[i]);
+    float wdes = a.kc->tm_inv2k2 * (a.kc->tm_negk1 + gr_sqrtf(t3));
+    mw[i] = a.kc->motor_c * mw[i] + (1.0f - a.kc->motor_c) * wdes;
+    f[i] = (a.kc->tm_k2 * mw[i] * mw[i] + a.kc->tm_k1 * mw[i]) + a.kc->tm_k0;
+  }
+}
+
 // CTBRController.compute (controller_diff.py:120-144)
 DEV void ctbr_compute(const KArgs& a, const float cmd[4], const float wb[3], const float ab[3], const float Kp[3],
                       const float Kd[3], float cT, const float ct[3], float& T, float tau[3], float mw[4],
@@ -457,13 +468,8 @@ DEV void ctbr_compute(const KArgs& a, const float cmd[4], const float wb[3], con
   float f[4];
   for (int r = 0; r < 4; ++r)
     f[r] = ((tt[0] * a.kc->Bi[r][0] + tt[1] * a.kc->Bi[r][1]) + tt[2] * a.kc->Bi[r][2]) + tt[3] * a.kc->Bi[r][3];
-  for (int i = 0; i < 4; ++i) {
-    float fd = gr_clampf(f[i], 0.0f, a.kc->motor_fmax);
-    float t3 = a.kc->tm_k1sq - a.kc->tm_4k2 * (a.kc->tm_k0 - fd);
-    float wdes = a.kc->tm_inv2k2 * (a.kc->tm_negk1 + gr_sqrtf(t3));
-    mw[i] = a.kc->motor_c * mw[i] + (1.0f - a.kc->motor_c) * wdes;
-    f[i] = (a.kc->tm_k2 * mw[i] * mw[i] + a.kc->tm_k1 * mw[i]) + a.kc->tm_k0;
-  }
+  for (int i = 0; i < 4; ++i) f[i] = gr_clampf(f[i], 0.0f, a.kc->motor_fmax);  // controller_diff.py:142
+  motor_update(a, f, mw);
   for (int r = 0; r < 4; ++r) tt[r] = ((f[0] * a.kc->B[r][0] + f[1] * a.kc->B[r][1]) + f[2] * a.kc->B[r][2]) + f[3] * a.kc->B[r][3];
 }
 
@@ -1492,8 +1498,13 @@ __global__ void test_dynamics_kernel(KArgs a, const KConst* __restrict__ kc, int
   for (int k = 0; k < 3; ++k) { p[k] = si[i * 13 + k]; v[k] = si[i * 13 + 7 + k]; w[k] = si[i * 13 + 10 + k]; }
   for (int k = 0; k < 4; ++k) q[k] = si[i * 13 + 3 + k];
   const float* pr = par + i * 16;
+  float mot[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   if (mode == 0) {
     ctbr_compute(a, cmd + i * 4, w, ab + i * 3, pr + 0, pr + 4, pr[3], pr + 8, T, tau, mw, tt);
+    for (int k = 0; k < 4; ++k) mot[k] = tt[k];
+  } else if (mode == 2) {  // ThrustController.update alone: cmd = desired rotor thrusts
+    for (int k = 0; k < 4; ++k) { mot[k] = cmd[i * 4 + k]; tt[k] = 0.0f; }
+    motor_update(a, mot, mw);
   } else {
     for (int k = 0; k < 4; ++k) tt[k] = cmd[i * 4 + k];
   }
@@ -1504,7 +1515,8 @@ __global__ void test_dynamics_kernel(KArgs a, const KConst* __restrict__ kc, int
   for (int k = 0; k < 3; ++k) co[i * 4 + 1 + k] = tau[k];
   float ww[3];
   quat_rotate(q, w, ww);
-  for (int k = 0; k < 3; ++k) { xo[i * 9 + k] = acc[k]; xo[i * 9 + 3 + k] = al[k]; xo[i * 9 + 6 + k] = ww[k]; }
+  for (int k = 0; k < 3; ++k) { xo[i * 13 + k] = acc[k]; xo[i * 13 + 3 + k] = al[k]; xo[i * 13 + 6 + k] = ww[k]; }
+  for (int k = 0; k < 4; ++k) xo[i * 13 + 9 + k] = mot[k];
 }
 
 __global__ void test_math_kernel(int fn, int n, const float* x, const float* y, float* out) {

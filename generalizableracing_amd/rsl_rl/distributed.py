@@ -50,9 +50,45 @@ def broadcast_params(module: torch.nn.Module, src: int = 0):
         dist.broadcast(b, src=src)
 
 
-def allreduce_grads(params) -> None:
-    """Average gradients over ranks in ONE flat bucket (latency-bound message on xGMI)."""
+class FlatGrads:
+    """One persistent flat gradient buffer; every parameter's `.grad` is a view of it.
+
+    The PPO update zeroes the gradients in place (`zero_grad(set_to_none=False)`, 0 + g == g exactly), so
+    autograd accumulates into the views and the data-parallel exchange is a single in-place all-reduce of
+    `flat` (~566 KB for the 256x256 MLPs: latency-bound on xGMI, one message), with no concatenation or
+    scatter-back.  The graph-captured update writes its gradients into the same views."""
+
+    def __init__(self, params):
+        self.params = list(params)
+        p0 = self.params[0]
+        self.flat = torch.zeros(sum(p.numel() for p in self.params), device=p0.device, dtype=p0.dtype)
+        self.views, off = [], 0
+        for p in self.params:
+            self.views.append(self.flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+        self.bind()
+
+    def bind(self):
+        for p, v in zip(self.params, self.views):
+            p.grad = v
+
+    def bound(self) -> bool:
+        return all(p.grad is not None and p.grad.data_ptr() == v.data_ptr() for p, v in zip(self.params, self.views))
+
+    def allreduce_(self):
+        """Average over ranks in place (the views see the result)."""
+        if is_dist():
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
+            self.flat.div_(world_size())
+
+
+def allreduce_grads(params, flat: FlatGrads | None = None) -> None:
+    """Average gradients over ranks in ONE flat bucket (latency-bound message on xGMI): in place when the
+    gradients are the views of `flat`, else through a concatenated copy."""
     if not is_dist():
+        return
+    if flat is not None and flat.bound():
+        flat.allreduce_()
         return
     grads = [p.grad for p in params if p.grad is not None]
     if not grads:

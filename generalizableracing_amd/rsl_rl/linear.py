@@ -15,6 +15,18 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 SPLIT = 4096  # rows per chunk (scripts/prof_update.py --split: 2048-4096 best at 65 536 and 4 096 envs)
+# set by the graph-captured PPO step (ppo.py _GraphedStep): every Linear takes _TallLinearFn, whose bias
+# gradient is a GEMV (see bias_grad)
+_FORCE_FN = False
+
+
+def bias_grad(gy: torch.Tensor) -> torch.Tensor:
+    """sum over rows of gy [M, N] as a GEMV with a ones vector.  Inside a captured hipGraph this keeps the
+    column sum off PyTorch's multi-block reduction, whose cross-block semaphores live in a buffer that, on
+    this ROCm build, is not held by the graph's pool: eager allocations between replays reused it and the
+    replays' bias gradients came out wrong (scripts/debug_graph_update.py)."""
+    ones = torch.ones(gy.shape[0], 1, device=gy.device, dtype=gy.dtype)
+    return (gy.t() @ ones).squeeze(1)
 
 
 def split_k_wgrad(gy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
@@ -47,7 +59,7 @@ class _TallLinearFn(torch.autograd.Function):
         x, w = ctx.saved_tensors
         gx = gy @ w.to(gy.dtype) if ctx.needs_input_grad[0] else None
         gw = split_k_wgrad(gy, x.to(gy.dtype)).to(ctx.wdtype) if ctx.needs_input_grad[1] else None
-        gb = gy.float().sum(0).to(ctx.wdtype) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        gb = bias_grad(gy.float()).to(ctx.wdtype) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return gx, gw, gb
 
 
@@ -61,6 +73,7 @@ class TallLinear(nn.Linear):
 
     @torch.jit.unused
     def _forward_eager(self, x: torch.Tensor) -> torch.Tensor:
-        if x.dim() == 2 and x.shape[0] >= 2 * SPLIT and torch.is_grad_enabled() and self.weight.requires_grad:
+        if x.dim() == 2 and (x.shape[0] >= 2 * SPLIT or _FORCE_FN) and torch.is_grad_enabled() and \
+                self.weight.requires_grad:
             return _TallLinearFn.apply(x, self.weight, self.bias)
         return F.linear(x, self.weight, self.bias)

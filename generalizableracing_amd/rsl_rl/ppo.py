@@ -12,8 +12,10 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 import torch.optim as optim
+import torch.distributed as dist
 
 from . import distributed as gdist
+from . import linear as _lin
 from .rollout_storage import RolloutStorage
 
 
@@ -58,6 +60,12 @@ class PPO:
         # not in the reference (fp32 update): forward/backward of the update under torch.autocast(bf16);
         # the losses' exp / log / sums stay fp32 (autocast's fp32 list), parameters and Adam stay fp32
         self.update_autocast_bf16 = bool(update_autocast_bf16)
+        self._flat = None  # gdist.FlatGrads: the parameters' gradients as views of one buffer
+
+    def flat_grads(self) -> gdist.FlatGrads:
+        if self._flat is None or self._flat.params[0] is not next(self.policy.parameters()):
+            self._flat = gdist.FlatGrads(self.policy.parameters())
+        return self._flat
 
     def init_storage(self, training_type, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape,
                      action_shape):
@@ -150,7 +158,7 @@ class PPO:
 
     def update(self):
         if self.graph_update and self.storage is not None and str(self.device).startswith("cuda") \
-                and gdist.world_size() == 1 and type(self).update is PPO.update:
+                and _graph_capturable_dist() and type(self).update is PPO.update:
             if self._graphed is None:
                 self._graphed = _GraphedStep(self)
             out = self._graphed.update()
@@ -161,6 +169,8 @@ class PPO:
         mean_surrogate_loss = torch.zeros((), device=self.device)
         generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
         params = list(self.policy.parameters())
+        flat = self.flat_grads()
+        flat.bind()
         ac = torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.update_autocast_bf16 and
                             str(self.device).startswith("cuda"))
         for (obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch, returns_batch,
@@ -177,9 +187,9 @@ class PPO:
                                                           advantages_batch, value_batch.float(), target_values_batch,
                                                           returns_batch)
             loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_batch.float().mean()
-            self.optimizer.zero_grad()
+            self.optimizer.zero_grad(set_to_none=False)  # (in place: the views of the flat buffer stay bound)
             loss.backward()
-            gdist.allreduce_grads(params)
+            gdist.allreduce_grads(params, flat)
             nn.utils.clip_grad_norm_(params, self.max_grad_norm)
             self.optimizer.step()
             mean_value_loss += value_loss.detach()
@@ -192,6 +202,11 @@ class PPO:
         }
 
 
+def _graph_capturable_dist() -> bool:
+    """One rank, or ranks over RCCL (its collectives can be captured in a hipGraph; gloo's cannot)."""
+    return gdist.world_size() == 1 or dist.get_backend() == "nccl"
+
+
 class _GraphedStep:
     """PPO.update's mini-batch step as one hipGraph (the same operations as the eager loop, in order).
 
@@ -201,7 +216,13 @@ class _GraphedStep:
     step (mini-batch gathers from the storage by a static index buffer, forward, losses, backward, grad
     clipping, Adam) is captured once and replayed per mini-batch.  Capture needs warm-up steps; the
     parameters, the optimizer state and the rate are snapshotted before and restored after, so training
-    is unchanged.  `learning_rate` is read back once per update, for the log."""
+    is unchanged.  `learning_rate` is read back once per update, for the log.
+
+    Gradients: `torch.autograd.grad` into the views of one flat buffer (gdist.FlatGrads, bound as the
+    parameters' `.grad` before capture and never rebound), so the captured step does not depend on how
+    autograd's gradient accumulation treats an existing `.grad` (an out-of-place accumulation during
+    capture rebinds `.grad` and leaves the graph writing a buffer nobody holds).  With several ranks (RCCL)
+    the gradient all-reduce and the KL mean of the adaptive learning rate are captured in the graph too."""
 
     def __init__(self, alg: "PPO"):
         self.alg = alg
@@ -218,6 +239,7 @@ class _GraphedStep:
             g["lr"] = self.lr
             g["capturable"] = True
         alg.optimizer = self.opt
+        self.flat = alg.flat_grads()
         self.idx = torch.zeros(self.mb, dtype=torch.long, device=dev)
         self.vloss = torch.zeros((), device=dev)
         self.sloss = torch.zeros((), device=dev)
@@ -249,6 +271,9 @@ class _GraphedStep:
                                + (torch.square(sig) + torch.square(mu - mu_b)) / (2.0 * torch.square(sigma_b)) - 0.5,
                                axis=-1)
                 k = torch.mean(kl)
+                if gdist.is_dist():
+                    dist.all_reduce(k, op=dist.ReduceOp.SUM)
+                    k = k / gdist.world_size()
                 lr = self.lr
                 up = torch.clamp(lr * 1.5, max=1e-2)
                 down = torch.clamp(lr / 1.5, min=1e-5)
@@ -257,8 +282,10 @@ class _GraphedStep:
                 self.lr.copy_(lr_new)
         surrogate_loss, value_loss = alg._ppo_losses(logp_b, logp, adv, value_b, val, ret)
         loss = surrogate_loss + alg.value_loss_coef * value_loss - alg.entropy_coef * entropy_b.mean()
-        self.opt.zero_grad(set_to_none=False)
-        loss.backward()
+        grads = torch.autograd.grad(loss, self.params, allow_unused=True)
+        torch._foreach_copy_(self.flat.views, [g if g is not None else torch.zeros_like(v)
+                                               for g, v in zip(grads, self.flat.views)])
+        self.flat.allreduce_()
         nn.utils.clip_grad_norm_(self.params, alg.max_grad_norm)
         self.opt.step()
         self.vloss.add_(value_loss.detach())
@@ -268,27 +295,23 @@ class _GraphedStep:
         # snapshot (parameters, optimizer state, rate), warm up on a side stream, capture, restore
         snap_p = [p.detach().clone() for p in self.params]
         snap_lr = self.lr.clone()
-        self.alg.policy.distribution = None  # the eager path's last graph (created on another stream)
-        for p in self.params:  # Adam's state tensors must exist (and stay put) before capture
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
+        self.flat.bind()  # Adam and the clip read the gradients from these views (static addresses)
         snap_o = {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in self.opt.state[p].items()}
                   for p in self.params}
         self.idx.copy_(torch.arange(self.mb, device=self.idx.device))
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(3):
+        _lin._FORCE_FN = True  # bias gradients as GEMVs in the captured step (linear.bias_grad)
+        try:
+            with torch.cuda.stream(s):
+                for _ in range(3):
+                    self._step()
+            torch.cuda.current_stream().wait_stream(s)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph, stream=s):
                 self._step()
-        torch.cuda.current_stream().wait_stream(s)
-        # the last warm-up's autograd graph (held by the distribution) keeps AccumulateGrad nodes of the side
-        # stream alive into the capture stream; drop it here, outside the capture (dropping it inside the
-        # captured step returns blocks to the graph's pool mid-capture and corrupted the replays)
-        torch.cuda.synchronize()
-        self.alg.policy.distribution = None
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self._step()
+        finally:
+            _lin._FORCE_FN = False
         with torch.no_grad():
             for p, v in zip(self.params, snap_p):
                 p.copy_(v)
@@ -306,8 +329,8 @@ class _GraphedStep:
             had_state = bool(self.opt.state)
             if not had_state:  # Adam's first step creates its state: take it with zero gradients, then undo
                 snap_p = [p.detach().clone() for p in self.params]
-                for p in self.params:
-                    p.grad = torch.zeros_like(p)
+                self.flat.bind()
+                self.flat.flat.zero_()
                 self.opt.step()
                 with torch.no_grad():
                     for p, v in zip(self.params, snap_p):

@@ -86,6 +86,8 @@ class PPOL2C2(PPO):
         mean_smooth_loss = torch.zeros((), device=self.device)
         generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
         params = list(self.policy.parameters())
+        flat = self.flat_grads()
+        flat.bind()
         for (obs_batch, critic_obs_batch, next_obs_batch, cont_batch, actions_batch, target_values_batch,
              advantages_batch, returns_batch, old_actions_log_prob_batch, old_mu_batch, old_sigma_batch,
              hid_states_batch, masks_batch) in generator:
@@ -102,9 +104,9 @@ class PPOL2C2(PPO):
             loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_batch.mean()
             smooth_loss, _ = self.smooth_loss(obs_batch, next_obs_batch, cont_batch, mu_batch, value_batch)
             loss = loss + smooth_loss
-            self.optimizer.zero_grad()
+            self.optimizer.zero_grad(set_to_none=False)
             loss.backward()
-            gdist.allreduce_grads(params)
+            gdist.allreduce_grads(params, flat)
             nn.utils.clip_grad_norm_(params, self.max_grad_norm)
             self.optimizer.step()
             mean_value_loss += value_loss.detach()

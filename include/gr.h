@@ -360,8 +360,12 @@ int gr_read_timing(gr_ctx* ctx, double* total_ms, int64_t* launches);
  *   ctrl_in/out [n][4] CTBR filter state (T, tau)
  *   par [n][16] = PAR0..PAR3 planes of one env (Kp3 cT Kd3 m_plant ctau3 m_ctrl J3 pad)
  *   drag [n][6] k2(3) k1(3)
- *   extra_out [n][9] = DD.step linear acceleration a(3), angular acceleration alpha(3), w_world(3)
- *   mode: 0 CTBR controller then integrator ; 1 integrator only */
+ *   extra_out [n][13] = DD.step linear acceleration a(3), angular acceleration alpha(3), w_world(3),
+ *                       then mode 0: the controller's output [T, tau] (post motor model when enabled,
+ *                       controller_diff.py:137-144); mode 2: the realised rotor thrusts
+ *   mode: 0 CTBR controller then integrator ; 1 integrator only (cmd = [T, tau]) ;
+ *         2 ThrustController.update alone (cmd = desired rotor thrusts, thrust_controller_diff.py:182-186;
+ *           motor speeds start at 0; the integrator runs with a zero wrench) */
 int gr_test_dynamics(gr_ctx* ctx, int n, int mode, const float* state_in, const float* ang_acc_b,
                      const float* cmd, const float* ctrl_in, const float* par, const float* drag,
                      float* state_out, float* ctrl_out, float* extra_out, void* stream);

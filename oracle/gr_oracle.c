@@ -209,6 +209,20 @@ static void motor_allocation(const gr_config* c, float B[4][4], float Bi[4][4]) 
 }
 
 /* --------------------------------------------------------- controller */
+/* ThrustController.update, thrust_controller_diff.py:182-186, in place: desired rotor thrusts ->
+ * Thrust2Omega (:167-176) -> w <- c w + (1 - c) w_des, c = exp(-(1/tau) dt) (:117-118) ->
+ * Omega2Thrust (:178-179) */
+static void motor_update(const gr_config* c, float f[4], float motor_w[4]) {
+  double k2 = c->thrustmap[0], k1 = c->thrustmap[1], k0 = c->thrustmap[2];
+  float cc = gr_expf(-(float)(1.0 / (double)c->motor_tau) * c->step_dt);
+  for (int i = 0; i < 4; ++i) {
+    float t3 = (float)(k1 * k1) - (float)(4.0 * k2) * ((float)k0 - f[i]);
+    float wdes = (float)(1.0 / (2.0 * k2)) * ((float)(-k1) + gr_sqrtf(t3));
+    motor_w[i] = cc * motor_w[i] + (1.0f - cc) * wdes;
+    f[i] = ((float)k2 * motor_w[i] * motor_w[i] + (float)k1 * motor_w[i]) + (float)k0;
+  }
+}
+
 /* CTBRController.compute, controller_diff.py:120-144 (use_motor_model=False
  * returns (T, tau) at :137-138); motor model :140-144 + thrust_controller_diff.py:83-102 */
 static void ctbr_compute(const gr_config* c, const float cmd[4], const float wb[3], const float ab[3], const float Kp[3],
@@ -236,19 +250,9 @@ static void ctbr_compute(const gr_config* c, const float cmd[4], const float wb[
   float f[4];
   for (int r = 0; r < 4; ++r)
     f[r] = ((out_tt[0] * Bi[r][0] + out_tt[1] * Bi[r][1]) + out_tt[2] * Bi[r][2]) + out_tt[3] * Bi[r][3];
-  double k2 = c->thrustmap[0], k1 = c->thrustmap[1], k0 = c->thrustmap[2];
   float fmax = thrust_of_omega(c, c->motor_omega[1]);
-  /* thrust_controller_diff.py:117-118: c = exp(-(1/tau) * dt) */
-  float cc = gr_expf(-(float)(1.0 / (double)c->motor_tau) * c->step_dt);
-  for (int i = 0; i < 4; ++i) {
-    float fd = gr_clampf(f[i], 0.0f, fmax);
-    /* Thrust2Omega (:167-176) */
-    float t3 = (float)(k1 * k1) - (float)(4.0 * k2) * ((float)k0 - fd);
-    float wdes = (float)(1.0 / (2.0 * k2)) * ((float)(-k1) + gr_sqrtf(t3));
-    /* update (:182-186) and Omega2Thrust (:178-179) */
-    motor_w[i] = cc * motor_w[i] + (1.0f - cc) * wdes;
-    f[i] = ((float)k2 * motor_w[i] * motor_w[i] + (float)k1 * motor_w[i]) + (float)k0;
-  }
+  for (int i = 0; i < 4; ++i) f[i] = gr_clampf(f[i], 0.0f, fmax); /* controller_diff.py:142 */
+  motor_update(c, f, motor_w);
   for (int r = 0; r < 4; ++r) out_tt[r] = ((f[0] * B[r][0] + f[1] * B[r][1]) + f[2] * B[r][2]) + f[3] * B[r][3];
 }
 
@@ -751,8 +755,13 @@ void gro_test_dynamics(const gr_config* c, int n, int mode, const float* si, con
     for (int k = 0; k < 3; ++k) { p[k] = si[i * 13 + k]; v[k] = si[i * 13 + 7 + k]; w[k] = si[i * 13 + 10 + k]; }
     for (int k = 0; k < 4; ++k) q[k] = si[i * 13 + 3 + k];
     const float* pr = par + i * 16;
+    float mot[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     if (mode == 0) {
       ctbr_compute(c, cmd + i * 4, w, ab + i * 3, pr + 0, pr + 4, pr[3], pr + 8, &T, tau, mw, tt);
+      for (int k = 0; k < 4; ++k) mot[k] = tt[k];
+    } else if (mode == 2) { /* ThrustController.update alone: cmd = desired rotor thrusts */
+      for (int k = 0; k < 4; ++k) { mot[k] = cmd[i * 4 + k]; tt[k] = 0.0f; }
+      motor_update(c, mot, mw);
     } else {
       for (int k = 0; k < 4; ++k) tt[k] = cmd[i * 4 + k];
     }
@@ -763,7 +772,8 @@ void gro_test_dynamics(const gr_config* c, int n, int mode, const float* si, con
     for (int k = 0; k < 3; ++k) co[i * 4 + 1 + k] = tau[k];
     float ww[3];
     quat_rotate(q, w, ww);
-    for (int k = 0; k < 3; ++k) { xo[i * 9 + k] = a[k]; xo[i * 9 + 3 + k] = al[k]; xo[i * 9 + 6 + k] = ww[k]; }
+    for (int k = 0; k < 3; ++k) { xo[i * 13 + k] = a[k]; xo[i * 13 + 3 + k] = al[k]; xo[i * 13 + 6 + k] = ww[k]; }
+    for (int k = 0; k < 4; ++k) xo[i * 13 + 9 + k] = mot[k];
   }
 }
 

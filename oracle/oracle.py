@@ -185,7 +185,7 @@ def test_dynamics(cfg, mode, state_in, ab, cmd, ctrl_in, par, drag):
     arrs = [np.ascontiguousarray(x, dtype=np.float32) for x in (state_in, ab, cmd, ctrl_in, par, drag)]
     so = np.zeros((n, 13), np.float32)
     co = np.zeros((n, 4), np.float32)
-    xo = np.zeros((n, 9), np.float32)
+    xo = np.zeros((n, 13), np.float32)
     lib.gro_test_dynamics(C.byref(cfg), n, mode, *[_p(a) for a in arrs], _p(so), _p(co), _p(xo))
     return so, co, xo
 

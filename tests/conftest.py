@@ -18,3 +18,10 @@ def golden():
     import numpy as np
 
     return dict(np.load(os.path.join(ROOT, "tests", "golden", "golden_dynamics.npz")))
+
+
+@pytest.fixture(scope="session")
+def golden_env():
+    import numpy as np
+
+    return dict(np.load(os.path.join(ROOT, "tests", "golden", "golden_env.npz")))

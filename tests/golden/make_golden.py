@@ -20,10 +20,8 @@ filters, drag, explicit Euler order) — not Isaac Lab's helpers, which are
 """
 from __future__ import annotations
 
-import importlib.util
 import os
 import sys
-import types
 
 import numpy as np
 import torch
@@ -32,76 +30,13 @@ REF = os.environ.get("GR_REFERENCE_ROOT", "/root/reference")
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden_dynamics.npz")
 
 
-# --------------------------------------------------------------- IL shim
-def _quat_mul(q1, q2):
-    shape = q1.shape
-    q1 = q1.reshape(-1, 4)
-    q2 = q2.reshape(-1, 4)
-    w1, x1, y1, z1 = q1[:, 0], q1[:, 1], q1[:, 2], q1[:, 3]
-    w2, x2, y2, z2 = q2[:, 0], q2[:, 1], q2[:, 2], q2[:, 3]
-    ww = (z1 + x1) * (x2 + y2)
-    yy = (w1 - y1) * (w2 + z2)
-    zz = (w1 + y1) * (w2 - z2)
-    xx = ww + yy + zz
-    qq = 0.5 * (xx + (z1 - x1) * (x2 - y2))
-    w = qq - ww + (z1 - y1) * (y2 - z2)
-    x = qq - xx + (x1 + w1) * (x2 + w2)
-    y = qq - yy + (w1 - x1) * (y2 + z2)
-    z = qq - zz + (z1 + y1) * (w2 - x2)
-    return torch.stack([w, x, y, z], dim=-1).view(shape)
-
-
-def _quat_rotate(q, v):
-    q_w = q[..., 0]
-    q_vec = q[..., 1:]
-    a = v * (2.0 * q_w**2 - 1.0).unsqueeze(-1)
-    b = torch.cross(q_vec, v, dim=-1) * q_w.unsqueeze(-1) * 2.0
-    c = q_vec * (q_vec * v).sum(-1, keepdim=True) * 2.0
-    return a + b + c
-
-
-def _quat_rotate_inverse(q, v):
-    q_w = q[..., 0]
-    q_vec = q[..., 1:]
-    a = v * (2.0 * q_w**2 - 1.0).unsqueeze(-1)
-    b = torch.cross(q_vec, v, dim=-1) * q_w.unsqueeze(-1) * 2.0
-    c = q_vec * (q_vec * v).sum(-1, keepdim=True) * 2.0
-    return a - b + c
-
-
-def _install_shim():
-    names = ["omni", "omni.isaac", "omni.isaac.lab", "omni.isaac.lab.utils", "omni.isaac.lab.utils.math"]
-    for n in names:
-        if n not in sys.modules:
-            sys.modules[n] = types.ModuleType(n)
-    m = sys.modules["omni.isaac.lab.utils.math"]
-    m.quat_mul = _quat_mul
-    m.quat_rotate = _quat_rotate
-    m.quat_rotate_inverse = _quat_rotate_inverse
-    sys.modules["omni.isaac.lab.utils"].math = m
-
-
-def _load(name, path, package=None):
-    spec = importlib.util.spec_from_file_location(name, path)
-    mod = importlib.util.module_from_spec(spec)
-    if package:
-        mod.__package__ = package
-    sys.modules[name] = mod
-    spec.loader.exec_module(mod)
-    return mod
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import il_shim  # noqa: E402  (Isaac Lab stand-ins: the three quaternion helpers these classes call)
 
 
 def load_reference():
-    _install_shim()
-    ctrl_dir = os.path.join(REF, "extensions/diff.lab/diff/lab/controllers")
-    # synthetic package so `from .thrust_controller_diff import ...` resolves
-    # without executing controllers/__init__.py (which needs Isaac Lab's configclass)
-    pkg = types.ModuleType("grref_ctrl")
-    pkg.__path__ = [ctrl_dir]
-    sys.modules["grref_ctrl"] = pkg
-    thr = _load("grref_ctrl.thrust_controller_diff", os.path.join(ctrl_dir, "thrust_controller_diff.py"), "grref_ctrl")
-    ctl = _load("grref_ctrl.controller_diff", os.path.join(ctrl_dir, "controller_diff.py"), "grref_ctrl")
-    dd = _load(
+    thr, ctl = il_shim.load_controllers()
+    dd = il_shim.load(
         "grref_dd",
         os.path.join(REF, "extensions/diff.lab_tasks/diff/lab_tasks/tasks/quadcopter_diff/mdp/dynamics/droneDynamics.py"),
     )

@@ -55,8 +55,8 @@ def test_graphed_update_matches_eager():
         torch.manual_seed(7 + rep)
         lg = alg_g.update()
         for pe, pg, q in zip(alg.policy.parameters(), alg_g.policy.parameters(), p0):
-            moved = float((pe - q).abs().max())
-            diff = float((pe - pg).abs().max())
+            moved = float((pe.detach() - q).abs().max())
+            diff = float((pe.detach() - pg.detach()).abs().max())
             assert moved > 0.0 and diff <= 0.05 * moved, (rep, diff, moved)
         assert abs(alg.learning_rate - alg_g.learning_rate) <= 1e-6 * alg.learning_rate
         for k in ("value_function", "surrogate"):
@@ -154,8 +154,8 @@ def test_graphed_update_across_iterations():
         torch.manual_seed(11 + it)
         lg = alg_g.update()
         for pe, pg, q in zip(alg.policy.parameters(), alg_g.policy.parameters(), p0):
-            moved = float((pe - q).abs().max())
-            diff = float((pe - pg).abs().max())
+            moved = float((pe.detach() - q).abs().max())
+            diff = float((pe.detach() - pg.detach()).abs().max())
             assert moved > 0.0 and diff <= 0.05 * moved, (it, diff, moved)
         assert abs(le["value_function"] - lg["value_function"]) <= 1e-4 * abs(le["value_function"]), (it, le, lg)
         # the surrogate is a mean of +-A * ratio over normalised advantages (|A| ~ 1) that nearly cancels

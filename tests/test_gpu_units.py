@@ -62,7 +62,7 @@ def test_philox_bitwise(ctx):
 
 def _run_dyn(lib, h, mode, s, ab, cmd, ci, par, drag):
     n = s.shape[0]
-    outs = [torch.zeros(n, k, device=DEV) for k in (13, 4, 9)]
+    outs = [torch.zeros(n, k, device=DEV) for k in (13, 4, 13)]
     ins = [dev(np.asarray(a, np.float32)) for a in (s, ab, cmd, ci, par, drag)]
     rc = lib.gr_test_dynamics(h, n, mode, *[t.data_ptr() for t in ins], *[t.data_ptr() for t in outs], stream())
     assert rc == 0
@@ -94,3 +94,47 @@ def test_dynamics_vs_oracle_and_golden(ctx, golden):
     want = golden["ddr_traj"][-1]
     want = np.concatenate([want[:, :10], want[:, 13:16]], 1)
     assert (np.abs(s - want) / np.maximum(1, np.abs(want))).max() < 1e-5
+
+
+@pytest.mark.parametrize("motor", [0, 1])
+def test_controller_output_vs_oracle_and_golden(ctx, golden, motor):
+    """The controller output [T, tau] (post motor model for motor=1) on the device: bit-identical to the
+    oracle, and within the CPU golden test's tolerance of the reference's CTBRController sequence."""
+    lib, h, _ = ctx
+    from test_oracle_golden import DT, par_rows
+
+    c = _abi.default_config()
+    c.num_envs = 64
+    c.use_motor_model = motor
+    h2 = C.c_void_p()
+    assert lib.gr_create(C.byref(c), C.byref(h2)) == 0
+    t = f"ctbr_motor{motor}"
+    n = golden[t + "_kp"].shape[0]
+    cT = np.exp(-DT / golden[t + "_dT"][:, 0].astype(np.float32)).astype(np.float32)
+    ctau = np.exp(-DT / golden[t + "_dtau"].astype(np.float32)).astype(np.float32)
+    par = par_rows(n, kp=golden[t + "_kp"], kd=golden[t + "_kd"], cT=cT, ctau=ctau)
+    s_in = np.zeros((n, 13), np.float32)
+    s_in[:, 3] = 1.0
+    drag = np.zeros((n, 6), np.float32)
+    for k in range(golden[t + "_cmd"].shape[0]):
+        s_in[:, 10:13] = golden[t + "_wb"][k]
+        filt = np.zeros((n, 4), np.float32) if k == 0 else golden[t + "_filt"][k - 1]
+        args = (s_in, golden[t + "_ab"][k], golden[t + "_cmd"][k], filt, par, drag)
+        so, co, xo = _run_dyn(lib, h2, 0, *args)
+        so2, co2, xo2 = oracle.test_dynamics(c, 0, *args)
+        assert np.array_equal(xo.view(np.uint32), xo2.view(np.uint32)), k
+        assert np.array_equal(co.view(np.uint32), co2.view(np.uint32)), k
+        want = golden[t + "_out"][k]
+        assert np.abs(xo[:, 9:13] - want).max() <= 2e-5 * np.abs(want).max() * 2, k
+    if motor:
+        thr_in = golden["thr_in"][0]
+        n2 = thr_in.shape[0]
+        s2 = np.zeros((n2, 13), np.float32)
+        s2[:, 3] = 1.0
+        args = (s2, np.zeros((n2, 3)), thr_in, np.zeros((n2, 4)), par_rows(n2), np.zeros((n2, 6)))
+        _, _, xo = _run_dyn(lib, h2, 2, *args)
+        _, _, xo2 = oracle.test_dynamics(c, 2, *args)
+        assert np.array_equal(xo.view(np.uint32), xo2.view(np.uint32))
+        np.testing.assert_allclose(xo[:, 9:13], golden["thr_out"][0], rtol=1e-5, atol=1e-5)
+    lib.gr_destroy(h2)
+

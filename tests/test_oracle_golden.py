@@ -86,6 +86,11 @@ def test_ctbr_sequence(golden, motor):
                                                 filt, par, drag)
         ok, e = close(filt_new, golden[t + "_filt"][k], 2e-6, 2e-6)
         assert ok, ("filter", k, e)
+        # the controller's output: [T, tau] (motor 0: the filters, :137-138; motor 1: allocation ->
+        # clamp -> ThrustController.update -> B f, :140-144).  B^-1 is torch.inverse's LU in the reference
+        # and the closed form here, and T(w) = k2 w^2 + k1 w + k0 cancels near f = 0: 2e-5 of the scale
+        ok, e = close(xo[:, 9:13], golden[t + "_out"][k], 2e-5, 2e-5 * np.abs(golden[t + "_out"][k]).max())
+        assert ok, ("output", k, e)
         filt = golden[t + "_filt"][k].copy()  # teacher-forced filter state
 
 
@@ -117,3 +122,29 @@ def test_closed_loop_controller_dynamics(golden):
         scale_w = np.maximum(1.0, np.abs(want))
         worst = max(worst, float((np.abs(s - want) / scale_w).max()))
     assert worst < 1e-5, worst
+
+
+def test_thrust_controller_update(golden):
+    """ThrustController.update on its own (thrust_controller_diff.py:182-186): desired rotor thrusts ->
+    Thrust2Omega -> first-order motor lag (c = exp(-dt / 1e-4) = 0 in fp32) -> Omega2Thrust.  The fixture
+    starts every sequence from zero motor speed; with c = 0 each call is independent of the last."""
+    n = golden["thr_in"].shape[1]
+    s = np.zeros((n, 13), np.float32)
+    s[:, 3] = 1.0
+    for k in range(golden["thr_in"].shape[0]):
+        _, _, xo = oracle.test_dynamics(cfg(True), 2, s, np.zeros((n, 3)), golden["thr_in"][k], np.zeros((n, 4)),
+                                        par_rows(n), np.zeros((n, 6)))
+        ok, e = close(xo[:, 9:13], golden["thr_out"][k], 1e-5, 1e-5)
+        assert ok, (k, e)
+
+
+def test_allocation_matrix(golden):
+    """B and B^-1 of the motor model (controller_diff.py:56-69 / thrust_controller_diff.py:44-55): the
+    closed-form rows the oracle and kernel use, against the reference's torch.vstack / torch.inverse."""
+    l, kap = np.float32(0.09) * np.float32(0.707106769), np.float32(0.016)
+    sx, sy, sz = np.array([1, -1, -1, 1]), np.array([-1, -1, 1, 1]), np.array([1, -1, 1, -1])
+    B = np.stack([np.ones(4), l * sx, l * sy, kap * sz]).astype(np.float32)
+    Bi = np.stack([np.full(4, 0.25), sx / (4 * l), sy / (4 * l), sz / (4 * kap)], 1).astype(np.float32)
+    np.testing.assert_allclose(B, golden["thr_B"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(Bi, golden["thr_Binv"], rtol=1e-5, atol=1e-5)
+
