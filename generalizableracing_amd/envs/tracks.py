@@ -228,7 +228,7 @@ def segment_obstacles(cfg: FamilyCfg, d: float, pts: np.ndarray, segs, scale: fl
 
     for i in segs:
         j = (i + 1) % G
-        p0, p1 = pts[i].astype(np.float64), pts[j].astype(np.float64)
+        p0, p1 = pts[i], pts[j]  # fp32, as the reference's gate_pts: mid and the along-segment shift round there
         mid, vec = (p0 + p1) / 2, p1 - p0
         cnt = 0
         while cnt < n_wall:
@@ -282,10 +282,12 @@ def square_track(d: float, cfg: FamilyCfg, size, rng: np.random.RandomState, prn
     pos_noise = _lerp(cfg.pos_noise_scale, d)
     rot_noise = _lerp(cfg.rot_noise_scale, d)
     theta = np.linspace(0, 2 * np.pi, G, endpoint=False)
-    pts = np.zeros((G, 3), dtype=np.float32)
-    pts[:, 0] = np.cos(theta) * radius + size[0] / 2
-    pts[:, 1] = np.sin(theta) * radius + size[1] / 2
+    pts = np.zeros((G, 3), dtype=np.float32)  # fp32 stores in the reference's order (:190-197)
+    pts[:, 0] = np.cos(theta) * radius
+    pts[:, 1] = np.sin(theta) * radius
     pts[:, 2] = 1.0
+    pts[:, 0] += size[0] / 2
+    pts[:, 1] += size[1] / 2
     eul = np.zeros((G, 3), dtype=np.float32)
     eul[:, 0] = 90.0
     eul[:, 1] = theta / np.pi * 180.0
@@ -337,7 +339,7 @@ def zigzag_track(d: float, cfg: FamilyCfg, size, rng: np.random.RandomState, prn
     eul = np.zeros((G, 3), dtype=np.float32)
     eul[:, 0] = 90.0
     eul[:, 1] = theta / np.pi * 180.0 + 90
-    pts = points.astype(np.float32)
+    pts = points  # fp64 here: the reference rebinds gate_pts to these points (:470)
     pts[:, 0] += size[0] / 2
     pts[:, 1] += size[1] / 2
     pts[:, 2] += 1.0
@@ -378,7 +380,7 @@ def ellipse_track(d: float, cfg: FamilyCfg, size, rng: np.random.RandomState, pr
     te = theta / np.pi * 180.0
     L = np.array([np.cos(theta), np.sin(theta), 0.0])
     S = np.array([-np.sin(theta), np.cos(theta), 0.0])
-    pts = np.zeros((G, 3))
+    pts = np.zeros((G, 3), dtype=np.float32 if G == 8 else np.float64)  # fp32 like the reference's points (:673)
     if G == 8:
         pts[0], pts[4] = -0.5 * a_e * L, 0.5 * a_e * L
         pts[2], pts[6] = 0.5 * b_e * S, -0.5 * b_e * S
@@ -416,7 +418,7 @@ def ellipse_track(d: float, cfg: FamilyCfg, size, rng: np.random.RandomState, pr
     nxt = (start_seg + 1) % G
     seg = pts[nxt] - pts[start_seg]
     seg = seg / np.linalg.norm(seg)
-    origin = pts[start_seg].astype(np.float64) + seg * prng.uniform(2, 3)
+    origin = pts[start_seg] + seg * prng.uniform(2, 3)  # fp32, as the reference's (:746)
     origin[2] = prng.uniform(0.7, 1.5)
     # all segments but the start one, offsets scaled by gate_distance (:750-815)
     obs = segment_obstacles(cfg, d, pts, [i for i in range(G) if i != start_seg], cfg.gate_distance, 10.0,
