@@ -76,10 +76,10 @@ def max_over_ranks(x: float, device) -> float:
     return float(t.item())
 
 
-def make_env(n, rank, device, gates, integrator, obstacles=True):
+def make_env(n, rank, device, gates, integrator, obstacles=True, **overrides):
     cfg = RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=device), stage=1, integrator=integrator,
                        terrain=TerrainCfg(num_gates=gates, obstacles=obstacles), env_id_offset=rank * n,
-                       track_seed_offset=rank)
+                       track_seed_offset=rank, overrides=overrides)
     env = RacingEnv(cfg)
     env.reset()
     g = torch.Generator(device="cpu").manual_seed(1234 + rank)
@@ -456,8 +456,8 @@ def main():
     if not a.no_extras and not a.obstacles:
         extra["env_count_sweep"] = env_count_sweep(rank, device, a)
         # BASELINE config C5 on one GPU: 32-gate tracks, startup DR (plant vs controller mass, drag, thrust
-        # error), hipGraph of [fused rollout inference + step]
-        env_c5 = make_env(n, rank, device, 32, a.integrator, False)
+        # error, rotor constants), hipGraph of [fused rollout inference + step]
+        env_c5 = make_env(n, rank, device, 32, a.integrator, False, dr_rotor=1)
         for k in range(a.warmup):
             env_c5.step(actions[k % ACTION_RING])
         torch.cuda.synchronize()
@@ -465,7 +465,9 @@ def main():
         kt_c5 = kernel_timing(graph_c5)
         del graph_c5
         rate_c5, us_c5, _ = policy_in_loop_fused(env_c5, 512, device)
-        extra["c5_32_gates"] = {"step_kernel_us": kt_c5["kernel_us"], "step_env_steps_per_s": n / (kt_c5["kernel_us"] * 1e-6),
+        extra["c5_32_gates"] = {"dr": "plant/controller mass, inertia, drag, thrust error, rotor constants "
+                                      "(thrust map, kappa x U(0.9, 1.1))",
+                                "step_kernel_us": kt_c5["kernel_us"], "step_env_steps_per_s": n / (kt_c5["kernel_us"] * 1e-6),
                                 "step_plus_fused_inference_env_steps_per_s": rate_c5, "inference_kernel_us": us_c5,
                                 "launch": "hipgraph (64 x [fused inference + gr_step])"}
         env_c5.close()

@@ -20,7 +20,8 @@ GR_INTEGRATOR_DD_EXPLICIT = 0
 GR_INTEGRATOR_SEMI_IMPLICIT = 1
 
 P_POSQ, P_QV, P_VW, P_WA, P_CTRL, P_LAG, P_RST0, P_RST1, P_EP0, P_EP1, P_PAR0, P_PAR1, P_PAR2, P_PAR3, P_MOTOR = range(15)
-NUM_PLANES = 16
+P_OHINT, P_ROTOR = 15, 16
+NUM_PLANES = 17
 I_EPLEN, I_ACC, I_EPOCH, I_PACKED = range(4)
 OBS_DIM = 16
 GATE_FLOATS = 20
@@ -63,6 +64,7 @@ STATE_FIELDS = {
     "mass_ctrl": [(P_PAR2, 3, 1)],
     "inertia_plant": [(P_PAR3, 0, 3)],
     "motor_omega": [(P_MOTOR, 0, 4)],
+    "rotor_constants": [(P_ROTOR, 0, 4)],
 }
 
 
@@ -141,7 +143,9 @@ class GrConfig(C.Structure):
         ("out_of_bound", C.c_float * 2),
         ("term_contact", C.c_int32),
         ("term_bad_pose", C.c_int32),
-        ("reserved", C.c_int32 * 8),
+        ("dr_rotor", C.c_int32),
+        ("rotor_scale_range", C.c_float * 2),
+        ("reserved", C.c_int32 * 5),
     ]
 
     def to_dict(self) -> dict:

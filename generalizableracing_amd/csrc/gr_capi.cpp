@@ -142,6 +142,7 @@ void derive(gr_ctx* c) {
   h.track_stride = a.track_stride;
   h.env_id_offset = g.env_id_offset;
   h.use_motor_model = g.use_motor_model;
+  h.dr_rotor = g.dr_rotor;
   h.obs_noise = g.obs_noise;
   h.lds_tab_vec = a.lds_bytes / 16;
   h.seed_lo = g.seed_lo;
@@ -234,6 +235,8 @@ int gr_config_default(gr_config* c) {
   c->out_of_bound[0] = 0.0f; c->out_of_bound[1] = 10.0f;
   c->term_contact = 1;
   c->term_bad_pose = 1;
+  c->dr_rotor = 0;  // config C5 turns it on
+  c->rotor_scale_range[0] = 0.9f; c->rotor_scale_range[1] = 1.1f;
   return GR_OK;
 }
 
@@ -282,8 +285,8 @@ int gr_bytes_per_env_step(const gr_ctx* c, int64_t* rd, int64_t* wr) {
   if (!c || !rd || !wr) return GR_ERR_ARG;
   // the obstacle hint plane (obstacle tracks) is read and written like a motor plane
   const int motor = (c->cfg.use_motor_model ? 1 : 0) + (c->obst.records ? 1 : 0);
-  // read: planes POSQ..PAR3 (14 x 16 B) [+ MOTOR], int plane 16 B, action 16 B
-  *rd = (14 + motor) * 16 + 16 + 16;
+  // read: planes POSQ..PAR3 (14 x 16 B) [+ MOTOR] [+ ROTOR], int plane 16 B, action 16 B
+  *rd = (14 + motor + (c->cfg.dr_rotor ? 1 : 0)) * 16 + 16 + 16;
   // written: POSQ..LAG, EP0, EP1 (8 x 16 B) [+ MOTOR], int plane, obs policy+critic (2 x 64 B),
   // aux 4, reward 4, terminated 1, time_out 1, dones 8.  RST0/RST1 (only on reset) not counted.
   *wr = (8 + motor) * 16 + 16 + 128 + 4 + 4 + 1 + 1 + 8;

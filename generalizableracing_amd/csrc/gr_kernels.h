@@ -47,6 +47,7 @@ struct KHot {
   uint32_t seed_lo, seed_hi;
   float obs_lin_vel_noise, obs_att_noise;
   float obst_span;  // obstacle grid: cell + 2 margin (m), the side of a hinted grown cell
+  int dr_rotor;     // per-env rotor constants (GR_P_ROTOR)
 };
 
 // Passed by value (kernarg): per-binding pointers + the constants pointer.

@@ -437,22 +437,52 @@ DEV uint32_t collision_mask(const KArgs& a, const Tab& tab, int type, int lvl, c
 }
 
 // ------------------------------------------------------------- controller
+// Rotor constants of one env: the config's (derived once on the host, KConst) or, with config C5's rotor-
+// constant DR, the env's own thrust map and kappa (GR_P_ROTOR: k2 k1 k0 kappa), through the same double-
+// precision expressions as derive() (gr_capi.cpp) and the oracle.
+struct MotorK {
+  float lo, hi;                                  // gross-thrust clamp 4 f(w_min), 4 f(w_max) (controller_diff.py:96-99)
+  float fmax;                                    // rotor thrust cap f(w_max) (:142)
+  float kap, kap_inv4;                           // kappa, 1 / (4 kappa): allocation row / column 3
+  float k2, k1, k0, k1sq, k4k2, inv2k2, negk1;   // thrust map, Thrust2Omega (thrust_controller_diff.py:167-179)
+  bool own;
+};
+DEV void motor_consts(const KArgs& a, const float4* rk, MotorK& m) {
+  m.own = rk != nullptr;
+  if (!rk) {
+    m.lo = a.kc->thrust_lo; m.hi = a.kc->thrust_hi; m.fmax = a.kc->motor_fmax;
+    m.kap = 0.0f; m.kap_inv4 = 0.0f;  // (the KConst matrices are used)
+    m.k2 = a.kc->tm_k2; m.k1 = a.kc->tm_k1; m.k0 = a.kc->tm_k0;
+    m.k1sq = a.kc->tm_k1sq; m.k4k2 = a.kc->tm_4k2; m.inv2k2 = a.kc->tm_inv2k2; m.negk1 = a.kc->tm_negk1;
+    return;
+  }
+  const double k2 = rk->x, k1 = rk->y, k0 = rk->z;
+  const double w0 = a.kc->cfg.motor_omega[0], w1 = a.kc->cfg.motor_omega[1];
+  const double tmin = k2 * w0 * w0 + k1 * w0 + k0, tmax = k2 * w1 * w1 + k1 * w1 + k0;
+  m.lo = (float)(tmin * 4.0); m.hi = (float)(tmax * 4.0); m.fmax = (float)tmax;
+  m.kap = rk->w; m.kap_inv4 = 1.0f / (4.0f * rk->w);
+  m.k2 = (float)k2; m.k1 = (float)k1; m.k0 = (float)k0;
+  m.k1sq = (float)(k1 * k1); m.k4k2 = (float)(4.0 * k2); m.inv2k2 = (float)(1.0 / (2.0 * k2)); m.negk1 = (float)(-k1);
+}
+
 // ThrustController.update (thrust_controller_diff.py:182-186): desired rotor thrusts -> motor speeds
 // (Thrust2Omega :167-176) -> first-order motor lag -> realised thrusts (Omega2Thrust :178-179), in place
-DEV void motor_update(const KArgs& a, float f[4], float mw[4]) {
+DEV void motor_update(const KArgs& a, const MotorK& m, float f[4], float mw[4]) {
   for (int i = 0; i < 4; ++i) {
-    float t3 = a.kc->tm_k1sq - a.kc->tm_4k2 * (a.kc->tm_k0 - f[i]);
-    float wdes = a.kc->tm_inv2k2 * (a.kc->tm_negk1 + gr_sqrtf(t3));
+    float t3 = m.k1sq - m.k4k2 * (m.k0 - f[i]);
+    float wdes = m.inv2k2 * (m.negk1 + gr_sqrtf(t3));
     mw[i] = a.kc->motor_c * mw[i] + (1.0f - a.kc->motor_c) * wdes;
-    f[i] = (a.kc->tm_k2 * mw[i] * mw[i] + a.kc->tm_k1 * mw[i]) + a.kc->tm_k0;
+    f[i] = (m.k2 * mw[i] * mw[i] + m.k1 * mw[i]) + m.k0;
   }
 }
 
-// CTBRController.compute (controller_diff.py:120-144)
+// CTBRController.compute (controller_diff.py:120-144); rk: the env's rotor constants (dr_rotor) or null
 DEV void ctbr_compute(const KArgs& a, const float cmd[4], const float wb[3], const float ab[3], const float Kp[3],
                       const float Kd[3], float cT, const float ct[3], float& T, float tau[3], float mw[4],
-                      float tt[4]) {
-  float T_des = gr_clampf(cmd[0], a.kc->thrust_lo, a.kc->thrust_hi);
+                      float tt[4], const float4* rk = nullptr) {
+  MotorK mk;
+  motor_consts(a, rk, mk);
+  float T_des = gr_clampf(cmd[0], mk.lo, mk.hi);
   T = (1.0f - cT) * T_des + cT * T;
   const float* J = a.kc->cfg.inertia;
   float err[3], Jw[3], cr[3];
@@ -465,12 +495,19 @@ DEV void ctbr_compute(const KArgs& a, const float cmd[4], const float wb[3], con
   }
   tt[0] = T; tt[1] = tau[0]; tt[2] = tau[1]; tt[3] = tau[2];
   if (!a.h.use_motor_model) return;
+  // allocation (controller_diff.py:56-69): rows 0-2 / columns 0-2 do not involve kappa; row / column 3 is
+  // kappa * (1 -1 1 -1) and its inverse (1 -1 1 -1) / (4 kappa)
+  const float sz[4] = {1.0f, -1.0f, 1.0f, -1.0f};
   float f[4];
-  for (int r = 0; r < 4; ++r)
-    f[r] = ((tt[0] * a.kc->Bi[r][0] + tt[1] * a.kc->Bi[r][1]) + tt[2] * a.kc->Bi[r][2]) + tt[3] * a.kc->Bi[r][3];
-  for (int i = 0; i < 4; ++i) f[i] = gr_clampf(f[i], 0.0f, a.kc->motor_fmax);  // controller_diff.py:142
-  motor_update(a, f, mw);
-  for (int r = 0; r < 4; ++r) tt[r] = ((f[0] * a.kc->B[r][0] + f[1] * a.kc->B[r][1]) + f[2] * a.kc->B[r][2]) + f[3] * a.kc->B[r][3];
+  for (int r = 0; r < 4; ++r) {
+    const float bi3 = mk.own ? sz[r] * mk.kap_inv4 : a.kc->Bi[r][3];
+    f[r] = ((tt[0] * a.kc->Bi[r][0] + tt[1] * a.kc->Bi[r][1]) + tt[2] * a.kc->Bi[r][2]) + tt[3] * bi3;
+  }
+  for (int i = 0; i < 4; ++i) f[i] = gr_clampf(f[i], 0.0f, mk.fmax);  // controller_diff.py:142
+  motor_update(a, mk, f, mw);
+  for (int r = 0; r < 3; ++r) tt[r] = ((f[0] * a.kc->B[r][0] + f[1] * a.kc->B[r][1]) + f[2] * a.kc->B[r][2]) + f[3] * a.kc->B[r][3];
+  if (mk.own) tt[3] = ((f[0] * (mk.kap * sz[0]) + f[1] * (mk.kap * sz[1])) + f[2] * (mk.kap * sz[2])) + f[3] * (mk.kap * sz[3]);
+  else tt[3] = ((f[0] * a.kc->B[3][0] + f[1] * a.kc->B[3][1]) + f[2] * a.kc->B[3][2]) + f[3] * a.kc->B[3][3];
 }
 
 // ------------------------------------------------------------- integrators
@@ -1057,7 +1094,12 @@ __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
     for (int k = 0; k < 4; ++k) cmd[k] = th_raw[k] * sc[k] + of[k];
     cmd[0] = cmd[0] * e.thr;
     float tt[4];
-    ctbr_compute(a, cmd, e.w, e.al, e.Kp, e.Kd, e.cT, e.ct, e.T, e.tau, e.mw, tt);
+    if (a.h.dr_rotor) {
+      const float4 rk = reinterpret_cast<const float4*>(a.buf.state)[GR_P_ROTOR * (size_t)n + ii];
+      ctbr_compute(a, cmd, e.w, e.al, e.Kp, e.Kd, e.cT, e.ct, e.T, e.tau, e.mw, tt, &rk);
+    } else {
+      ctbr_compute(a, cmd, e.w, e.al, e.Kp, e.Kd, e.cT, e.ct, e.T, e.tau, e.mw, tt);
+    }
     const float m = c.dr_plant ? e.mp : e.mc;
     float Jp[3];
     for (int k = 0; k < 3; ++k) Jp[k] = c.dr_plant ? e.J[k] : c.inertia[k];
@@ -1373,6 +1415,13 @@ __global__ __launch_bounds__(GR_BLOCK) void init_kernel(KArgs a, const KConst* _
   gr_u32x4 b2 = draw(a, gid, 0, GR_TAG_STATIC, 2), b3 = draw(a, gid, 0, GR_TAG_STATIC, 3);
   gr_u32x4 b4 = draw(a, gid, 0, GR_TAG_STATIC, 4);
   const int dr = c.dr_startup;
+  float4 rotor = make_float4(c.thrustmap[0], c.thrustmap[1], c.thrustmap[2], c.kappa);
+  if (dr && c.dr_rotor) {  // config C5: thrust map and kappa x U(lo, hi) per env, for the env's lifetime
+    const gr_u32x4 b5 = draw(a, gid, 0, GR_TAG_STATIC, 5);
+    const float lo = c.rotor_scale_range[0], hi = c.rotor_scale_range[1];
+    rotor = make_float4(c.thrustmap[0] * gr_uniform(b5.x, lo, hi), c.thrustmap[1] * gr_uniform(b5.y, lo, hi),
+                        c.thrustmap[2] * gr_uniform(b5.z, lo, hi), c.kappa * gr_uniform(b5.w, lo, hi));
+  }
   const float plo = c.pid_scale_range[0], phi = c.pid_scale_range[1];
   const float dlo = c.delay_scale_range[0], dhi = c.delay_scale_range[1];
   float skp[3] = {gr_uniform(b0.x, plo, phi), gr_uniform(b0.y, plo, phi), gr_uniform(b0.z, plo, phi)};
@@ -1426,6 +1475,7 @@ __global__ __launch_bounds__(GR_BLOCK) void init_kernel(KArgs a, const KConst* _
     S[GR_P_PAR2 * n + i] = make_float4(e.ct[0], e.ct[1], e.ct[2], e.mc);
     S[GR_P_PAR3 * n + i] = make_float4(e.J[0], e.J[1], e.J[2], 0.0f);
     S[GR_P_OHINT * n + i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // no obstacle hint
+    S[GR_P_ROTOR * n + i] = rotor;
   }
   // initial observation buffers: last action = ctbr(0) (DiffActions._raw_actions starts at zero)
   float sc[4], of[4];
@@ -1504,7 +1554,9 @@ __global__ void test_dynamics_kernel(KArgs a, const KConst* __restrict__ kc, int
     for (int k = 0; k < 4; ++k) mot[k] = tt[k];
   } else if (mode == 2) {  // ThrustController.update alone: cmd = desired rotor thrusts
     for (int k = 0; k < 4; ++k) { mot[k] = cmd[i * 4 + k]; tt[k] = 0.0f; }
-    motor_update(a, mot, mw);
+    MotorK mk;
+    motor_consts(a, nullptr, mk);
+    motor_update(a, mk, mot, mw);
   } else {
     for (int k = 0; k < 4; ++k) tt[k] = cmd[i * 4 + k];
   }

@@ -65,7 +65,9 @@ extern "C" {
 #define GR_P_MOTOR 14 /* rotor speeds (motor model only) */
 #define GR_P_OHINT 15 /* obstacle tracks only: the obstacle-grid list of the env's cell (int first, int count + 1,
                          lower corner x, y of the cell grown by the margin); all-zero = no hint */
-#define GR_NUM_PLANES 16
+#define GR_P_ROTOR 16 /* rotor constants of the env (thrust map k2 k1 k0, torque ratio kappa): config C5's
+                         rotor-constant DR, read only when dr_rotor */
+#define GR_NUM_PLANES 17
 /* int plane [num_envs][4] int32: episode_length, accumulate_gates, epoch, packed */
 #define GR_I_EPLEN 0
 #define GR_I_ACC 1
@@ -178,7 +180,11 @@ typedef struct gr_config {
   float out_of_bound[2];             /* stage 0 world-z bounds (0, 10) */
   int32_t term_contact;  /* base_contact / outofbound termination enabled */
   int32_t term_bad_pose;
-  int32_t reserved[8];
+  /* config C5: per-env rotor constants (thrust map k2, k1, k0 and kappa, each x U(lo, hi)) drawn at start-up;
+   * the gross-thrust clamp and, with the motor model, the allocation and motor map follow them per env */
+  int32_t dr_rotor;
+  float rotor_scale_range[2]; /* (0.9, 1.1) */
+  int32_t reserved[5];
 } gr_config;
 
 /*

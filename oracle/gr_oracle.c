@@ -105,12 +105,11 @@ static float cosine_similarity(const float a[3], const float b[3]) {
 static float thrust_of_omega(const gr_config* c, double w) {
   return (float)(c->thrustmap[0] * w * w + c->thrustmap[1] * w + c->thrustmap[2]);
 }
-/* controller_diff.py:96-99  gross thrust bounds (python double, cast at clamp) */
-static void thrust_bounds(const gr_config* c, float* lo, float* hi) {
-  double tmin = (double)c->thrustmap[0] * c->motor_omega[0] * c->motor_omega[0] +
-                (double)c->thrustmap[1] * c->motor_omega[0] + (double)c->thrustmap[2];
-  double tmax = (double)c->thrustmap[0] * c->motor_omega[1] * c->motor_omega[1] +
-                (double)c->thrustmap[1] * c->motor_omega[1] + (double)c->thrustmap[2];
+/* controller_diff.py:96-99  gross thrust bounds (python double, cast at clamp), for the rotor constants
+ * k = (k2, k1, k0) of the env (the config's thrust map unless dr_rotor) */
+static void thrust_bounds(const gr_config* c, const float k[3], float* lo, float* hi) {
+  double tmin = (double)k[0] * c->motor_omega[0] * c->motor_omega[0] + (double)k[1] * c->motor_omega[0] + (double)k[2];
+  double tmax = (double)k[0] * c->motor_omega[1] * c->motor_omega[1] + (double)k[1] * c->motor_omega[1] + (double)k[2];
   *lo = (float)(tmin * 4.0);
   *hi = (float)(tmax * 4.0);
   (void)thrust_of_omega;
@@ -198,9 +197,9 @@ int gro_collision_count(const gr_config* c, const gro_tracks* tr, int track, con
   return count;
 }
 
-/* allocation matrix and its inverse (controller_diff.py:56-69; fp32 as torch builds it) */
-static void motor_allocation(const gr_config* c, float B[4][4], float Bi[4][4]) {
-  float l = c->arm_length * 0.707106769f, k = c->kappa;
+/* allocation matrix and its inverse (controller_diff.py:56-69; fp32 as torch builds it) for torque ratio k */
+static void motor_allocation(const gr_config* c, float k, float B[4][4], float Bi[4][4]) {
+  float l = c->arm_length * 0.707106769f;
   static const float sx[4] = {1, -1, -1, 1}, sy[4] = {-1, -1, 1, 1}, sz[4] = {1, -1, 1, -1};
   for (int j = 0; j < 4; ++j) {
     B[0][j] = 1.0f; B[1][j] = l * sx[j]; B[2][j] = l * sy[j]; B[3][j] = k * sz[j];
@@ -212,8 +211,8 @@ static void motor_allocation(const gr_config* c, float B[4][4], float Bi[4][4]) 
 /* ThrustController.update, thrust_controller_diff.py:182-186, in place: desired rotor thrusts ->
  * Thrust2Omega (:167-176) -> w <- c w + (1 - c) w_des, c = exp(-(1/tau) dt) (:117-118) ->
  * Omega2Thrust (:178-179) */
-static void motor_update(const gr_config* c, float f[4], float motor_w[4]) {
-  double k2 = c->thrustmap[0], k1 = c->thrustmap[1], k0 = c->thrustmap[2];
+static void motor_update(const gr_config* c, const float rk[3], float f[4], float motor_w[4]) {
+  double k2 = rk[0], k1 = rk[1], k0 = rk[2];
   float cc = gr_expf(-(float)(1.0 / (double)c->motor_tau) * c->step_dt);
   for (int i = 0; i < 4; ++i) {
     float t3 = (float)(k1 * k1) - (float)(4.0 * k2) * ((float)k0 - f[i]);
@@ -225,11 +224,12 @@ static void motor_update(const gr_config* c, float f[4], float motor_w[4]) {
 
 /* CTBRController.compute, controller_diff.py:120-144 (use_motor_model=False
  * returns (T, tau) at :137-138); motor model :140-144 + thrust_controller_diff.py:83-102 */
+/* rk: the env's rotor constants k2 k1 k0 kappa (config C5's dr_rotor; else the config's) */
 static void ctbr_compute(const gr_config* c, const float cmd[4], const float wb[3], const float ab[3], const float Kp[3],
                          const float Kd[3], float cT, const float ctau[3], float* T, float tau[3], float motor_w[4],
-                         float out_tt[4]) {
+                         const float rk[4], float out_tt[4]) {
   float tlo, thi;
-  thrust_bounds(c, &tlo, &thi);
+  thrust_bounds(c, rk, &tlo, &thi);
   float T_des = gr_clampf(cmd[0], tlo, thi);
   *T = (1.0f - cT) * T_des + cT * (*T);
   const float* J = c->inertia; /* controller inertia: nominal, diff_action.py:59 */
@@ -246,13 +246,14 @@ static void ctbr_compute(const gr_config* c, const float cmd[4], const float wb[
   /* allocation B (controller_diff.py:56-69): rows [1 1 1 1], l/sqrt2 [1 -1 -1 1],
    * l/sqrt2 [-1 -1 1 1], kappa [1 -1 1 -1]; B^-1 entries 1/4, +-1/(4l), +-1/(4 kappa) */
   float B[4][4], Bi[4][4];
-  motor_allocation(c, B, Bi);
+  motor_allocation(c, rk[3], B, Bi);
   float f[4];
   for (int r = 0; r < 4; ++r)
     f[r] = ((out_tt[0] * Bi[r][0] + out_tt[1] * Bi[r][1]) + out_tt[2] * Bi[r][2]) + out_tt[3] * Bi[r][3];
-  float fmax = thrust_of_omega(c, c->motor_omega[1]);
+  double w1 = c->motor_omega[1];
+  float fmax = (float)((double)rk[0] * w1 * w1 + (double)rk[1] * w1 + (double)rk[2]);
   for (int i = 0; i < 4; ++i) f[i] = gr_clampf(f[i], 0.0f, fmax); /* controller_diff.py:142 */
-  motor_update(c, f, motor_w);
+  motor_update(c, rk, f, motor_w);
   for (int r = 0; r < 4; ++r) out_tt[r] = ((f[0] * B[r][0] + f[1] * B[r][1]) + f[2] * B[r][2]) + f[3] * B[r][3];
 }
 
@@ -339,6 +340,17 @@ void gro_init(const gr_config* c, gro_env* envs, int n, gro_out* out) {
     gr_u32x4 b2 = draw(c, gid, 0, GR_TAG_STATIC, 2), b3 = draw(c, gid, 0, GR_TAG_STATIC, 3);
     gr_u32x4 b4 = draw(c, gid, 0, GR_TAG_STATIC, 4);
     int dr = c->dr_startup;
+    /* config C5 (not in the reference): thrust map and kappa x U(lo, hi) per env, for the env's lifetime */
+    e->rotor[0] = c->thrustmap[0]; e->rotor[1] = c->thrustmap[1]; e->rotor[2] = c->thrustmap[2];
+    e->rotor[3] = c->kappa;
+    if (dr && c->dr_rotor) {
+      gr_u32x4 b5 = draw(c, gid, 0, GR_TAG_STATIC, 5);
+      float lo = c->rotor_scale_range[0], hi = c->rotor_scale_range[1];
+      e->rotor[0] = c->thrustmap[0] * gr_uniform(b5.x, lo, hi);
+      e->rotor[1] = c->thrustmap[1] * gr_uniform(b5.y, lo, hi);
+      e->rotor[2] = c->thrustmap[2] * gr_uniform(b5.z, lo, hi);
+      e->rotor[3] = c->kappa * gr_uniform(b5.w, lo, hi);
+    }
     float plo = c->pid_scale_range[0], phi = c->pid_scale_range[1];
     float dlo = c->delay_scale_range[0], dhi = c->delay_scale_range[1];
     /* events.py:105-137 randomize_rate_controller_gain_and_thrust_delay */
@@ -628,7 +640,9 @@ void gro_step(const gr_config* c, gro_env* envs, int n, const float* actions, co
     cmd[0] = cmd[0] * e->thr_err;
     /* 3. controller (:182) with the state "read from sim" (:126-154) */
     float tt[4];
-    ctbr_compute(c, cmd, e->w, e->alpha, e->Kp, e->Kd, e->cT, e->ctau, &e->T, e->tau, e->motor_w, tt);
+    const float nominal[4] = {c->thrustmap[0], c->thrustmap[1], c->thrustmap[2], c->kappa};
+    ctbr_compute(c, cmd, e->w, e->alpha, e->Kp, e->Kd, e->cT, e->ctau, &e->T, e->tau, e->motor_w,
+                 c->dr_rotor ? e->rotor : nominal, tt);
     /* 4. physics (:189-203): wrench held over the substeps */
     int track = track_index(c, e->type, e->level);
     float m = c->dr_plant ? e->m_plant : e->m_ctrl;
@@ -749,6 +763,7 @@ int gro_num_threads(void) {
 /* ------------------------------------------------------------ test hooks */
 void gro_test_dynamics(const gr_config* c, int n, int mode, const float* si, const float* ab, const float* cmd,
                        const float* ci, const float* par, const float* drag, float* so, float* co, float* xo) {
+  const float nominal[4] = {c->thrustmap[0], c->thrustmap[1], c->thrustmap[2], c->kappa};
   for (int i = 0; i < n; ++i) {
     float p[3], q[4], v[3], w[3], a[3], al[3], tt[4], T = ci[i * 4], tau[3] = {ci[i * 4 + 1], ci[i * 4 + 2], ci[i * 4 + 3]};
     float mw[4] = {0, 0, 0, 0};
@@ -757,11 +772,11 @@ void gro_test_dynamics(const gr_config* c, int n, int mode, const float* si, con
     const float* pr = par + i * 16;
     float mot[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     if (mode == 0) {
-      ctbr_compute(c, cmd + i * 4, w, ab + i * 3, pr + 0, pr + 4, pr[3], pr + 8, &T, tau, mw, tt);
+      ctbr_compute(c, cmd + i * 4, w, ab + i * 3, pr + 0, pr + 4, pr[3], pr + 8, &T, tau, mw, nominal, tt);
       for (int k = 0; k < 4; ++k) mot[k] = tt[k];
     } else if (mode == 2) { /* ThrustController.update alone: cmd = desired rotor thrusts */
       for (int k = 0; k < 4; ++k) { mot[k] = cmd[i * 4 + k]; tt[k] = 0.0f; }
-      motor_update(c, mot, mw);
+      motor_update(c, nominal, mot, mw);
     } else {
       for (int k = 0; k < 4; ++k) tt[k] = cmd[i * 4 + k];
     }

@@ -25,6 +25,7 @@ typedef struct gro_env {
   float thr_err, noise_level, k2[3], k1[3];
   float ep_sum[7], m_actrate;
   float Kp[3], cT, Kd[3], m_plant, ctau[3], m_ctrl, J[3], motor_w[4];
+  float rotor[4]; /* k2 k1 k0 kappa (dr_rotor; else the nominal constants) */
   int32_t ep_len, acc, epoch, gate_id, level, type, azero;
 } gro_env;
 

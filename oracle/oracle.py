@@ -22,7 +22,7 @@ ENV_DTYPE = np.dtype([
     ("p", _F, 3), ("q", _F, 4), ("v", _F, 3), ("w", _F, 3), ("alpha", _F, 3), ("T", _F), ("tau", _F, 3),
     ("lag", _F, 4), ("thr_err", _F), ("noise_level", _F), ("k2", _F, 3), ("k1", _F, 3), ("ep_sum", _F, 7),
     ("m_actrate", _F), ("Kp", _F, 3), ("cT", _F), ("Kd", _F, 3), ("m_plant", _F), ("ctau", _F, 3),
-    ("m_ctrl", _F), ("J", _F, 3), ("motor_w", _F, 4),
+    ("m_ctrl", _F), ("J", _F, 3), ("motor_w", _F, 4), ("rotor", _F, 4),
     ("ep_len", _I), ("acc", _I), ("epoch", _I), ("gate_id", _I), ("level", _I), ("type", _I), ("azero", _I),
 ])
 
@@ -238,6 +238,7 @@ _PLANE_MAP = [  # (plane, comp) for each float of the kernel state, in ENV_DTYPE
     ("Kp", [(10, 0), (10, 1), (10, 2)]), ("cT", [(10, 3)]), ("Kd", [(11, 0), (11, 1), (11, 2)]),
     ("m_plant", [(11, 3)]), ("ctau", [(12, 0), (12, 1), (12, 2)]), ("m_ctrl", [(12, 3)]),
     ("J", [(13, 0), (13, 1), (13, 2)]), ("motor_w", [(14, 0), (14, 1), (14, 2), (14, 3)]),
+    ("rotor", [(16, 0), (16, 1), (16, 2), (16, 3)]),
 ]
 
 
@@ -258,7 +259,7 @@ def planes_to_envs(state: np.ndarray, istate: np.ndarray) -> np.ndarray:
     return envs
 
 
-def envs_to_planes(envs: np.ndarray, num_planes: int = 15):
+def envs_to_planes(envs: np.ndarray, num_planes: int = 17):
     n = envs.shape[0]
     state = np.zeros((num_planes, n, 4), np.float32)
     for name, comps in _PLANE_MAP:

@@ -1,7 +1,7 @@
 """Per-phase wave timelines of the fused step kernel (diagnostic build, -DGR_STAMPS).
 
-  python scripts/stamps.py build     # here: build/stamps/libgr.so
-  python scripts/stamps.py run       # GPU box: GR_LIB_PATH=build/stamps/libgr.so, prints a JSON summary
+  python scripts/stamps.py build     # here: variants/stamps/libgr.so
+  python scripts/stamps.py run       # GPU box: GR_LIB_PATH=variants/stamps/libgr.so, prints a JSON summary
 
 Stamps of the step kernel (lane 0 of each wave, s_memtime shader cycles; 9/10 s_memrealtime
 (100 MHz) at entry/exit; 11 XCC_ID<<32 | HW_ID):
@@ -16,7 +16,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(ROOT, "build", "stamps")
+OUT = os.path.join(ROOT, "variants", "stamps")  # (not under build/: .gpurunignore keeps build/ off the box)
 CSRC = os.path.join(ROOT, "generalizableracing_amd", "csrc")
 PHASES = ["obs_noise", "table_barrier", "ctrl_integrate", "collision", "reward_term", "reset_advance",
           "obs_store_issue", "log"]

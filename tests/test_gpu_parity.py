@@ -64,6 +64,8 @@ CONFIGS = [
     dict(stage=1, use_motor_model=1),
     dict(stage=1, gates=32),
     dict(stage=1, obstacles=False),
+    dict(stage=1, dr_rotor=1),                               # config C5: per-env rotor constants
+    dict(stage=1, dr_rotor=1, use_motor_model=1, gates=32),  # ... through the motor model's allocation
 ]
 
 

@@ -202,3 +202,44 @@ def test_critic_observation_layout():
     np.testing.assert_allclose(ob[6:9], R.T @ (np.array(G0) - [0.5, 0.2, 1.2]), atol=1e-6)
     np.testing.assert_allclose(ob[9:12], R.T @ [3.0, 0, 0], atol=1e-6)                # gate -> next gate
     assert np.array_equal(ob[12:16], np.zeros(4))  # last action: zeroed by the action manager reset
+
+
+def test_rotor_constant_dr():
+    """Config C5's rotor-constant DR (not in the reference): the thrust map and kappa of each env are the
+    config's x U(0.9, 1.1), drawn once at start-up (off: the config's exactly); with it the gross-thrust clamp
+    of the CTBR controller follows the env's own map (controller_diff.py:96-99)."""
+    from generalizableracing_amd.envs.racing_cfg import RacingEnvCfg, SceneCfg, SimCfg, TerrainCfg
+    from generalizableracing_amd.envs.tracks import build_tracks
+
+    n = 256
+    gates, recs, _ = build_tracks(num_types=4, num_levels=10, num_gates=8, obstacles=False)
+    nominal = None
+    for on in (0, 1):
+        c = RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device="cpu"),
+                         terrain=TerrainCfg(num_cols=4, obstacles=False), overrides=dict(dr_rotor=on)).to_gr_config()
+        orc = oracle.Oracle(c, gates, recs)
+        orc.init()
+        rot = orc.envs["rotor"].astype(np.float64)
+        base = np.array([c.thrustmap[0], c.thrustmap[1], c.thrustmap[2], c.kappa], np.float32).astype(np.float64)
+        if not on:
+            assert np.array_equal(rot, np.tile(base, (n, 1)))
+            nominal = orc
+            continue
+        ratio = rot / base
+        assert (ratio >= 0.9 - 1e-6).all() and (ratio <= 1.1 + 1e-6).all()
+        assert len(np.unique(ratio[:, 0])) > n // 2 and ratio.std(axis=0).min() > 0.05
+        # full thrust command: each env clamps at 4 f(w_max) of its own map (thrust filter state T = its clamp)
+        for o in (orc, nominal):
+            o.reset(None)
+            o.envs["T"] = 0.0
+            o.envs["cT"] = 0.0  # no filter lag: T = clamp(cmd)
+            o.envs["thr_err"] = 10.0
+            o.envs["azero"] = 0
+            o.envs["lag"] = 1.0
+            o.step(np.full((n, 4), 5.0, np.float32))
+        w1 = np.float64(c.motor_omega[1])
+        want = (rot[:, 0] * w1 * w1 + rot[:, 1] * w1 + rot[:, 2]) * 4.0
+        live = orc.dones == 0
+        np.testing.assert_allclose(orc.envs["T"][live], want[live].astype(np.float32), rtol=1e-6)
+        assert not np.allclose(orc.envs["T"][live], nominal.envs["T"][live])
+
