@@ -311,7 +311,8 @@ def env_count_sweep(rank, device, a, sizes=(16384, 262144, 1048576)):
     return out
 
 
-def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False, graph_update=False, bf16_update=False):
+def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False, graph_update=False, bf16_update=False,
+              obs_sink=True):
     """The reference's Perf/total_fps (24 steps x N / (collect + learn)) of rsl_rl PPO with MLP(256,256):
     config C2 at 4 096 envs fp32; at 65 536 envs also with the fused bf16 rollout inference and bf16
     rollout obs buffers (C5's training options; the update stays fp32)."""
@@ -324,6 +325,7 @@ def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False, graph_up
     cfg.algorithm.storage_obs_dtype = "bfloat16" if bf16_storage else "float32"
     cfg.algorithm.graph_update = bool(graph_update)
     cfg.algorithm.update_autocast_bf16 = bool(bf16_update)
+    cfg.algorithm.obs_sink = bool(obs_sink)
     runner = OnPolicyRunner(venv, cfg.to_dict(), log_dir=None, device=device)
     runner.learn(1, init_at_random_ep_len=True)  # warm-up iteration
     fps = []
@@ -465,11 +467,21 @@ def main():
         kt_c5 = kernel_timing(graph_c5)
         del graph_c5
         rate_c5, us_c5, _ = policy_in_loop_fused(env_c5, 512, device)
+        # the step kernel also writing the bf16 rollout rows (gr_bind_obs_sink: the runner's storage slot)
+        sink = torch.empty(2, n, 16, device=device, dtype=torch.bfloat16)
+        env_c5.set_obs_sink(sink[0], sink[1])
+        graph_c5s = capture_graph(env_c5, actions)
+        kt_c5s = kernel_timing(graph_c5s)
+        del graph_c5s
+        rd_c5s, wr_c5s = env_c5.bytes_per_env_step()
+        env_c5.set_obs_sink(None)
         extra["c5_32_gates"] = {"dr": "plant/controller mass, inertia, drag, thrust error, rotor constants "
                                       "(thrust map, kappa x U(0.9, 1.1))",
                                 "step_kernel_us": kt_c5["kernel_us"], "step_env_steps_per_s": n / (kt_c5["kernel_us"] * 1e-6),
                                 "step_plus_fused_inference_env_steps_per_s": rate_c5, "inference_kernel_us": us_c5,
-                                "launch": "hipgraph (64 x [fused inference + gr_step])"}
+                                "launch": "hipgraph (64 x [fused inference + gr_step])",
+                                "step_kernel_us_bf16_obs_sink": kt_c5s["kernel_us"],
+                                "bytes_per_env_step_bf16_obs_sink": {"read": rd_c5s, "written": wr_c5s}}
         env_c5.close()
     if not a.no_extras:
         extra["train_total_fps_4096_envs"] = train_fps(device)
@@ -477,9 +489,12 @@ def main():
         extra["train_total_fps_65536_envs"] = {
             "fp32": train_fps(device, n),
             "fused_rollout_bf16_storage": train_fps(device, n, fused=True, bf16_storage=True),
+            "fused_rollout_bf16_storage_no_obs_sink": train_fps(device, n, fused=True, bf16_storage=True,
+                                                                obs_sink=False),
             "fused_bf16_storage_graphed_bf16_update": train_fps(device, n, fused=True, bf16_storage=True,
                                                                 graph_update=True, bf16_update=True),
-            "note": "Perf/total_fps, PPO 5 epochs x 4 mini-batches per 24-step rollout, obstacle tracks"}
+            "note": "Perf/total_fps, PPO 5 epochs x 4 mini-batches per 24-step rollout, obstacle tracks; the step "
+                    "kernel writes the rollout storage rows (obs sink) unless marked no_obs_sink"}
         # the depth camera of the vision task (separate kernel, same env shard size)
         sys.path.insert(0, os.path.join(ROOT, "scripts"))
         import bench_camera

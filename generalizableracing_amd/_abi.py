@@ -212,10 +212,11 @@ class GrPolicyArgs(C.Structure):
 
 GR_POLICY_ACT_LRELU, GR_POLICY_ACT_ELU = 0, 1
 GR_CAM_STEP, GR_CAM_RESET, GR_CAM_OBSERVE = 0, 1, 2
+GR_DTYPE_F32, GR_DTYPE_BF16 = 0, 1
 
 EXPORTS = [
     "gr_abi_version", "gr_config_default", "gr_config_size", "gr_create", "gr_destroy", "gr_last_error",
-    "gr_num_blocks", "gr_num_log_rows", "gr_log_finalize", "gr_bytes_per_env_step", "gr_bind_tracks", "gr_bind_obstacles", "gr_bind_buffers", "gr_init", "gr_reset",
+    "gr_num_blocks", "gr_num_log_rows", "gr_log_finalize", "gr_bytes_per_env_step", "gr_bind_tracks", "gr_bind_obstacles", "gr_bind_buffers", "gr_bind_obs_sink", "gr_init", "gr_reset",
     "gr_step", "gr_observe", "gr_set_timing", "gr_read_timing", "gr_test_dynamics", "gr_test_math",
     "gr_test_philox",
     "gr_debug_read_stamps",
@@ -242,6 +243,7 @@ def _declare(lib):
         "gr_bind_tracks": (C.c_int, [vp, vp, vp]),
         "gr_bind_obstacles": (C.c_int, [vp, C.POINTER(GrObstacles)]),
         "gr_bind_buffers": (C.c_int, [vp, C.POINTER(GrBuffers)]),
+        "gr_bind_obs_sink": (C.c_int, [vp, vp, vp, C.c_int]),
         "gr_init": (C.c_int, [vp, vp]),
         "gr_reset": (C.c_int, [vp, vp, vp]),
         "gr_step": (C.c_int, [vp, vp, vp]),

@@ -290,6 +290,8 @@ int gr_bytes_per_env_step(const gr_ctx* c, int64_t* rd, int64_t* wr) {
   // written: POSQ..LAG, EP0, EP1 (8 x 16 B) [+ MOTOR], int plane, obs policy+critic (2 x 64 B),
   // aux 4, reward 4, terminated 1, time_out 1, dones 8.  RST0/RST1 (only on reset) not counted.
   *wr = (8 + motor) * 16 + 16 + 128 + 4 + 4 + 1 + 1 + 8;
+  // the observation sink, when bound: policy + critic rows again (2 x 16 values)
+  if (c->args.sink_policy) *wr += 2 * 16 * (c->args.sink_dtype == GR_DTYPE_BF16 ? 2 : 4);
   return GR_OK;
 }
 
@@ -393,6 +395,23 @@ int gr_bind_buffers(gr_ctx* c, const gr_buffers* b) {
   c->buf = *b;
   c->args.buf = *b;
   c->have_buf = true;
+  return GR_OK;
+}
+
+int gr_bind_obs_sink(gr_ctx* c, void* policy, void* critic, int dtype) {
+  if (!c) return GR_ERR_ARG;
+  if (!policy) {  // unbind
+    c->args.sink_policy = c->args.sink_critic = nullptr;
+    c->args.sink_dtype = GR_DTYPE_F32;
+    return GR_OK;
+  }
+  if (!critic) return fail(c, GR_ERR_ARG, "gr_bind_obs_sink: critic sink is null");
+  if (dtype != GR_DTYPE_F32 && dtype != GR_DTYPE_BF16) return fail(c, GR_ERR_ARG, "gr_bind_obs_sink: dtype");
+  if (!aligned16(policy) || !aligned16(critic))
+    return fail(c, GR_ERR_ARG, "gr_bind_obs_sink: sinks must be 16-byte aligned");
+  c->args.sink_policy = policy;
+  c->args.sink_critic = critic;
+  c->args.sink_dtype = dtype;
   return GR_OK;
 }
 

@@ -61,6 +61,10 @@ struct KArgs {
   const int4* obst_grid_i;    // [T*L]: nx, ny, first cell, 0
   const int2* obst_cells;     // [C]: first item, count
   const float4* obst_items;   // [I][GR_OBST_FLOATS / 4]
+  // observation sink (gr_bind_obs_sink; null: none): the policy / critic rows again, in sink_dtype
+  void* sink_policy;
+  void* sink_critic;
+  int sink_dtype;
   KHot h;
 };
 

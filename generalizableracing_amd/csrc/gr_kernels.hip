@@ -801,6 +801,51 @@ DEV void store_rows_staged(float4* dst, int env0, int n, const float4 rows[4], f
   __asm__ volatile("" ::: "memory");
 }
 
+// Observation sink (gr_bind_obs_sink): the same rows again into the rollout storage's slot, fp32 or bf16.
+// bf16: round to nearest even on the fp32 bits, NaN -> 0x7FC0 (c10::BFloat16's round_to_nearest_even).
+DEV uint32_t bf16_rne(float x) {
+  const uint32_t u = __float_as_uint(x);
+  return (x != x) ? 0x7FC0u : ((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+DEV uint32_t bf16x2(float lo, float hi) { return bf16_rne(lo) | (bf16_rne(hi) << 16); }
+DEV uint4 bf16x8(const float4& u, const float4& v) {
+  return make_uint4(bf16x2(u.x, u.y), bf16x2(u.z, u.w), bf16x2(v.x, v.y), bf16x2(v.z, v.w));
+}
+// from the LDS stage of store_rows_staged (call right after it): bf16 rows are 32 B, two lanes per env, so
+// each store instruction again covers 1 KiB of consecutive bytes
+DEV void store_rows_sink(const KArgs& a, void* dst, int env0, int n, const float4* stage) {
+  const int l = threadIdx.x & 63;
+  if (a.sink_dtype == GR_DTYPE_BF16) {
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    for (int j = 0; j < 2; ++j) {
+      const int env = 32 * j + (l >> 1), h = l & 1;
+      const uint4 w = bf16x8(stage[(2 * h) * GR_BLOCK + env], stage[(2 * h + 1) * GR_BLOCK + env]);
+      if (env0 + env < n) st4(d, (size_t)(env0 + env) * 2 + h, w);
+    }
+  } else {
+    float4* d = reinterpret_cast<float4*>(dst);
+    for (int j = 0; j < 4; ++j) {
+      const int env = 16 * j + (l >> 2), q = l & 3;
+      const float4 v = stage[q * GR_BLOCK + env];
+      if (env0 + env < n) st4(d, (size_t)(env0 + env) * 4 + q, v);
+    }
+  }
+  __asm__ volatile("" ::: "memory");
+}
+// one env's rows (gr_reset / gr_observe)
+DEV void store_obs_sink(const KArgs& a, int i, const ObsRows& o) {
+  if (a.sink_dtype == GR_DTYPE_BF16) {
+    uint4* P = reinterpret_cast<uint4*>(a.sink_policy) + (size_t)i * 2;
+    uint4* C = reinterpret_cast<uint4*>(a.sink_critic) + (size_t)i * 2;
+    P[0] = bf16x8(o.p[0], o.p[1]); P[1] = bf16x8(o.p[2], o.p[3]);
+    C[0] = bf16x8(o.c[0], o.c[1]); C[1] = bf16x8(o.c[2], o.c[3]);
+  } else {
+    float4* P = reinterpret_cast<float4*>(a.sink_policy) + (size_t)i * 4;
+    float4* C = reinterpret_cast<float4*>(a.sink_critic) + (size_t)i * 4;
+    for (int k = 0; k < 4; ++k) { P[k] = o.p[k]; C[k] = o.c[k]; }
+  }
+}
+
 // ------------------------------------------------------------- log reduction
 // Per-wave partial sums into log_partial[row][GR_LOG_SLOTS] (no workgroup
 // barrier); a workgroup owns GR_LOG_ROWS_PER_BLOCK rows.  Resets are sparse
@@ -960,6 +1005,7 @@ __global__ __launch_bounds__(GR_BLOCK) void env_kernel(KArgs a, const KConst* __
     ObsRows o;
     compute_obs(a, sl.tab, e, gid, on, lc, o);
     store_obs_direct(a, i, o, aux);
+    if (a.sink_policy) store_obs_sink(a, i, o);
     if (reset_lane) {
       store_dyn(a, i, e);
       store_rst(a, i, e);
@@ -1337,6 +1383,7 @@ __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
       compute_policy(a, sl.tab, e, gid, on, lc, prow);
       store_rows_staged(reinterpret_cast<float4*>(a.buf.obs_policy), blockIdx.x * GR_BLOCK + (t & ~63), n, prow,
                         stg + (t & ~63));
+      if (a.sink_policy) store_rows_sink(a, a.sink_policy, blockIdx.x * GR_BLOCK + (t & ~63), n, stg + (t & ~63));
       if (live) st1(a.buf.obs_aux + i, aux);
     }
 #endif
@@ -1388,6 +1435,8 @@ __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
       compute_critic(sl.tab, e, lc, crow);
       store_rows_staged(reinterpret_cast<float4*>(a.buf.obs_critic), blockIdx.x * GR_BLOCK + (t & ~63), n, crow,
                         stg + 4 * GR_BLOCK + (t & ~63));
+      if (a.sink_critic)
+        store_rows_sink(a, a.sink_critic, blockIdx.x * GR_BLOCK + (t & ~63), n, stg + 4 * GR_BLOCK + (t & ~63));
     }
 #endif
     STAMP(8);

@@ -140,6 +140,7 @@ class RacingEnv:
                 cb.obs_critic = self._img_sets[k]["critic"].data_ptr()
                 self._cam_bufs.append(cb)
         self.extras: dict = {}
+        self._sink = None  # (policy, critic) tensors of the bound observation sink
         # startup (gr_init): nominal state, startup DR events, initial terrain levels
         self._bind(0)
         self._call("gr_init", self._stream())
@@ -395,6 +396,29 @@ class RacingEnv:
         self.extras = {"log": log}
         return self._obs_dict(out), self.extras
 
+    def set_obs_sink(self, policy: torch.Tensor | None, critic: torch.Tensor | None = None):
+        """gr_bind_obs_sink: the following step / reset / observe calls also write their policy and critic rows
+        into these [num_envs, 16] tensors (float32 or bfloat16; bf16 rounds to nearest even like torch's cast) —
+        the rollout storage's slot for the next transition (config C5's bf16 rollout buffers without a copy-cast
+        pass).  None unbinds.  State task only (the image rows of the camera task are not sunk)."""
+        if policy is None:
+            self._sink = None
+            self._call("gr_bind_obs_sink", None, None, _abi.GR_DTYPE_F32)
+            return
+        if self.camera is not None:
+            raise ValueError("set_obs_sink: the camera task's image observation rows have no sink")
+        for t in (policy, critic):
+            if (t is None or t.device != self.device or tuple(t.shape) != (self.num_envs, _abi.OBS_DIM)
+                    or not t.is_contiguous() or t.dtype not in (torch.float32, torch.bfloat16)
+                    or t.data_ptr() % 16):
+                raise ValueError(f"set_obs_sink: need contiguous 16-byte aligned [{self.num_envs}, {_abi.OBS_DIM}] "
+                                 f"float32 / bfloat16 tensors on {self.device}")
+        if critic.dtype != policy.dtype:
+            raise ValueError("set_obs_sink: policy and critic sinks must share a dtype")
+        dtype = _abi.GR_DTYPE_BF16 if policy.dtype == torch.bfloat16 else _abi.GR_DTYPE_F32
+        self._sink = (policy, critic)  # kept alive while bound
+        self._call("gr_bind_obs_sink", policy.data_ptr(), critic.data_ptr(), dtype)
+
     def observe(self) -> dict:
         """ObservationManager.compute(): fresh observation noise, no state change."""
         out, _ = self._advance()
@@ -453,6 +477,10 @@ class RslRlVecEnvWrapper:
 
     def seed(self, seed: int = -1) -> int:
         return self.env.seed(seed)
+
+    def set_obs_sink(self, policy, critic=None):
+        """RacingEnv.set_obs_sink (rollout storage slots written by the kernel; None unbinds)."""
+        self.env.set_obs_sink(policy, critic)
 
     def get_observations(self):
         obs_dict = self.env.observe()

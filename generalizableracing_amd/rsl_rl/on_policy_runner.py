@@ -104,6 +104,7 @@ class OnPolicyRunner:
         policy_class = POLICIES[self.policy_cfg.pop("class_name")]
         policy = policy_class(num_obs, num_privileged_obs, self.env.num_actions, **self.policy_cfg).to(self.device)
         alg_class = ALGORITHMS[self.alg_cfg.pop("class_name")]
+        want_sink = bool(self.alg_cfg.pop("obs_sink", True))
         self.alg = alg_class(policy, env=self.env, device=self.device, **self.alg_cfg)
         self.num_steps_per_env = self.cfg["num_steps_per_env"]
         self.save_interval = self.cfg["save_interval"]
@@ -116,6 +117,9 @@ class OnPolicyRunner:
             self.privileged_obs_normalizer = torch.nn.Identity().to(self.device)
         self.alg.init_storage(self.training_type, self.env.num_envs, self.num_steps_per_env, [num_obs],
                               [num_privileged_obs], [self.env.num_actions])
+        self.obs_sink = want_sink and self._sink_supported(obs, extras)
+        if self.obs_sink:
+            self.alg.storage.enable_obs_sink()
         self.log_dir = log_dir
         self.writer = None
         self.logger_type = self.cfg.get("logger", "tensorboard")
@@ -124,6 +128,22 @@ class OnPolicyRunner:
         self.current_learning_iteration = 0
         self.is_main = gdist.rank() == 0
         self.last_log: dict = {}
+
+    def _sink_supported(self, obs, extras) -> bool:
+        """The observation sink (RacingEnv.set_obs_sink: the step kernel writes each transition's observations
+        into the rollout storage slot) applies when the stored rows are exactly the env's rows: PPO (PPOL2C2's
+        storage pairs observations with their successors), no empirical normalisation, separate critic rows,
+        the env on the training device, state observations of the kernel's width."""
+        if type(self.alg) is not PPO or self.empirical_normalization or not hasattr(self.env, "set_obs_sink"):
+            return False
+        st = self.alg.storage
+        if st.privileged_observations is None or self.privileged_obs_type is None:
+            return False
+        unwrapped = getattr(self.env, "unwrapped", self.env)
+        if torch.device(self.env.device) != torch.device(self.device) or getattr(unwrapped, "camera", None) is not None:
+            return False
+        crit = extras["observations"][self.privileged_obs_type]
+        return obs.dim() == 2 and obs.shape[1] == 16 and crit.dim() == 2 and crit.shape[1] == 16
 
     def learn(self, num_learning_iterations: int, init_at_random_ep_len: bool = False):
         if self.log_dir is not None and self.writer is None and self.is_main:
@@ -134,6 +154,9 @@ class OnPolicyRunner:
         obs, extras = self.env.get_observations()
         privileged_obs = extras["observations"].get(self.privileged_obs_type, obs)
         obs, privileged_obs = obs.to(self.device), privileged_obs.to(self.device)
+        storage = self.alg.storage
+        if self.obs_sink:
+            storage.discard_sink()  # fresh observations: slot 0 is copied from them
         self.train_mode()
         ep_infos = []
         stats = _EpisodeStats(self.env.num_envs, self.device)
@@ -144,6 +167,8 @@ class OnPolicyRunner:
             with torch.inference_mode():
                 for _ in range(self.num_steps_per_env):
                     actions = self.alg.act(obs, privileged_obs)
+                    if self.obs_sink:  # this step's observations land in the next transition's slot
+                        self.env.set_obs_sink(*storage.sink_slot(storage.step + 1))
                     obs, rewards, dones, infos = self.env.step(actions.to(self.env.device))
                     obs, rewards, dones = obs.to(self.device), rewards.to(self.device), dones.to(self.device)
                     obs = self.obs_normalizer(obs)
@@ -159,6 +184,8 @@ class OnPolicyRunner:
                         elif "log" in infos:
                             ep_infos.append(infos["log"])
                     stats.update(rewards, dones)
+                if self.obs_sink:
+                    self.env.set_obs_sink(None)
                 if torch.cuda.is_available() and str(self.device).startswith("cuda"):
                     torch.cuda.synchronize(self.device)
                 stop = time.time()

@@ -60,13 +60,43 @@ class RolloutStorage:
         self.saved_hidden_states_a = None
         self.saved_hidden_states_c = None
         self.step = 0
+        # observation sink (enable_obs_sink): the env's kernel writes the observations of transition t into
+        # slot t itself; slot T holds the rollout's last observations (transition 0 of the next rollout)
+        self.sink = False
+        self.prefilled = [False] * (T + 1)
+
+    def enable_obs_sink(self):
+        """Observation buffers with one more slot, written by the env (RacingEnv.set_obs_sink) instead of copied
+        by add_transitions.  The mini-batch generators and the GAE read the first T slots only."""
+        if self.sink:
+            return
+        T = self.num_transitions_per_env
+        self.observations = torch.cat([self.observations, torch.zeros_like(self.observations[:1])])
+        if self.privileged_observations is not None:
+            self.privileged_observations = torch.cat([self.privileged_observations,
+                                                      torch.zeros_like(self.privileged_observations[:1])])
+        self.sink = True
+        self.prefilled = [False] * (T + 1)
+
+    def sink_slot(self, t: int):
+        """(policy, critic) observation rows of slot t, marked as filled by the env."""
+        self.prefilled[t] = True
+        priv = self.privileged_observations if self.privileged_observations is not None else self.observations
+        return self.observations[t], priv[t]
+
+    def discard_sink(self):
+        """Slots marked filled by the env are stale (the runner observed afresh): copy on the next adds."""
+        self.prefilled = [False] * (self.num_transitions_per_env + 1)
 
     def add_transitions(self, transition: "RolloutStorage.Transition"):
         if self.step >= self.num_transitions_per_env:
             raise AssertionError("Rollout buffer overflow")
-        self.observations[self.step].copy_(transition.observations)
-        if self.privileged_observations is not None:
-            self.privileged_observations[self.step].copy_(transition.privileged_observations)
+        if self.prefilled[self.step]:  # written by the env's kernel (observation sink)
+            self.prefilled[self.step] = False
+        else:
+            self.observations[self.step].copy_(transition.observations)
+            if self.privileged_observations is not None:
+                self.privileged_observations[self.step].copy_(transition.privileged_observations)
         self.actions[self.step].copy_(transition.actions)
         self.rewards[self.step].copy_(transition.rewards.view(-1, 1))
         self.dones[self.step].copy_(transition.dones.view(-1, 1))
@@ -81,6 +111,13 @@ class RolloutStorage:
 
     def clear(self):
         self.step = 0
+        T = self.num_transitions_per_env
+        if self.sink and self.prefilled[T]:  # the rollout's last observations open the next rollout
+            self.observations[0].copy_(self.observations[T])
+            if self.privileged_observations is not None:
+                self.privileged_observations[0].copy_(self.privileged_observations[T])
+            self.prefilled = [False] * (T + 1)
+            self.prefilled[0] = True
 
     def compute_returns(self, last_values, gamma, lam, normalize_advantage: bool = True):
         """GAE, rollout_storage.py:113-127."""

@@ -32,18 +32,18 @@ class RolloutStorageL2C2(RolloutStorage):
         batch_size = self.num_envs * (T - 1)
         mini_batch_size = batch_size // num_mini_batches
         indices = torch.randperm(num_mini_batches * mini_batch_size, requires_grad=False, device=self.device)
-        observations = self.observations[:-1].flatten(0, 1)
-        critic = (self.privileged_observations[:-1].flatten(0, 1)
+        observations = self.observations[:T - 1].flatten(0, 1)
+        critic = (self.privileged_observations[:T - 1].flatten(0, 1)
                   if self.privileged_observations is not None else observations)
-        next_observations = self.observations[1:].flatten(0, 1)
-        actions = self.actions[:-1].flatten(0, 1)
-        values = self.values[:-1].flatten(0, 1)
-        returns = self.returns[:-1].flatten(0, 1)
-        old_logp = self.actions_log_prob[:-1].flatten(0, 1)
-        advantages = self.advantages[:-1].flatten(0, 1)
-        old_mu = self.mu[:-1].flatten(0, 1)
-        old_sigma = self.sigma[:-1].flatten(0, 1)
-        not_dones = 1 - self.dones[:-1].float().flatten(0, 1)
+        next_observations = self.observations[1:T].flatten(0, 1)
+        actions = self.actions[:T - 1].flatten(0, 1)
+        values = self.values[:T - 1].flatten(0, 1)
+        returns = self.returns[:T - 1].flatten(0, 1)
+        old_logp = self.actions_log_prob[:T - 1].flatten(0, 1)
+        advantages = self.advantages[:T - 1].flatten(0, 1)
+        old_mu = self.mu[:T - 1].flatten(0, 1)
+        old_sigma = self.sigma[:T - 1].flatten(0, 1)
+        not_dones = 1 - self.dones[:T - 1].float().flatten(0, 1)
         for _ in range(num_epochs):
             for i in range(num_mini_batches):
                 idx = indices[i * mini_batch_size:(i + 1) * mini_batch_size]

@@ -261,7 +261,7 @@ int gr_num_log_rows(const gr_ctx* ctx);
 /* extras["log"] on demand: reduce one call's log slab into GR_LOG_SLOTS means
  * (prev: the previous call's finalized values, kept when no env reset; may be NULL) */
 int gr_log_finalize(gr_ctx* ctx, const float* log_partial, const float* prev, float* out, void* stream);
-/* algorithmic HBM bytes per env-step of the fused step kernel (read, written) */
+/* algorithmic HBM bytes per env-step of the fused step kernel (read, written; with the bound observation sink) */
 int gr_bytes_per_env_step(const gr_ctx* ctx, int64_t* read_bytes, int64_t* written_bytes);
 
 /* Track table on the device (caller-owned):
@@ -293,6 +293,16 @@ typedef struct gr_obstacles {
  * the small index arrays). */
 int gr_bind_obstacles(gr_ctx* ctx, const gr_obstacles* obst);
 int gr_bind_buffers(gr_ctx* ctx, const gr_buffers* bufs);
+
+/* Observation sink (config C5's bf16 rollout buffers): every following gr_step / gr_reset / gr_observe also
+ * writes the policy and critic rows it computes into policy[num_envs][16] / critic[num_envs][16] of `dtype`
+ * (GR_DTYPE_BF16: round-to-nearest-even, as torch's float -> bfloat16; GR_DTYPE_F32: the rows as they are)
+ * — the rollout storage's slot for the next transition (standalone/rsl_rl/ext/storage/rollout_storage.py:
+ * 74-88 add_transitions), so the storage takes the observations without a copy / cast pass.  Rebind per
+ * call (each step has its own slot); policy == NULL unbinds.  16-byte aligned device memory. */
+#define GR_DTYPE_F32 0
+#define GR_DTYPE_BF16 1
+int gr_bind_obs_sink(gr_ctx* ctx, void* policy, void* critic, int dtype);
 
 /* startup: nominal state, startup DR (gains/delays/mass/inertia), initial levels */
 int gr_init(gr_ctx* ctx, void* stream);

@@ -37,6 +37,7 @@ class OracleVecEnv:
         self.max_episode_length = self.cfg.max_episode_length
         self.device = "cpu"
         self.render_mode = None
+        self._sink = None
 
     @property
     def unwrapped(self):
@@ -54,9 +55,19 @@ class OracleVecEnv:
         if self.camera is not None:
             self.orc.camera(mode)
 
+    def set_obs_sink(self, policy, critic=None):
+        """RacingEnv.set_obs_sink emulated: the rows are cast into the bound tensors (torch's cast rounds to
+        nearest even, as the kernel's bf16 sink does)."""
+        if policy is not None and self.camera is not None:
+            raise ValueError("set_obs_sink: no sink for the camera task")
+        self._sink = None if policy is None else (policy, critic)
+
     def _obs(self):
         pol, cri = ((self.orc.img_policy, self.orc.img_critic) if self.camera is not None
                     else (self.orc.obs_policy, self.orc.obs_critic))
+        if self._sink is not None:
+            self._sink[0].copy_(torch.from_numpy(pol))
+            self._sink[1].copy_(torch.from_numpy(cri))
         return {"policy": torch.from_numpy(pol.copy()),
                 "critic": torch.from_numpy(cri.copy()),
                 "auxiliary": torch.from_numpy(self.orc.obs_aux.copy()).unsqueeze(1)}

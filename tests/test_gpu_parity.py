@@ -281,3 +281,69 @@ def test_wrapper_across_terrain_regeneration():
         obs = obs_next
     assert extras.get("terrain_regenerated")
     venv.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_obs_sink_rows(dtype):
+    """gr_bind_obs_sink: step / reset / observe also write the policy and critic rows into the bound tensors,
+    bit-equal to torch's round-to-nearest-even cast of the fp32 rows they return (ragged env count, rotor DR,
+    resets inside the run); unbinding stops the writes."""
+    n = 1000
+    cfg = RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV), stage=1, overrides=dict(dr_rotor=1))
+    venv = RslRlVecEnvWrapper(RacingEnv(cfg))
+    sp = torch.full((n, 16), 7.0, device=DEV, dtype=dtype)
+    sc = torch.full((n, 16), 7.0, device=DEV, dtype=dtype)
+    venv.set_obs_sink(sp, sc)
+    obs, ex = venv.get_observations()
+    torch.cuda.synchronize()
+    assert torch.equal(sp, obs.to(dtype)) and torch.equal(sc, ex["observations"]["critic"].to(dtype))
+    g = torch.Generator().manual_seed(4)
+    resets = 0
+    for k in range(40):
+        obs, rew, dones, ex = venv.step((3 * torch.randn(n, 4, generator=g)).to(DEV))
+        torch.cuda.synchronize()
+        resets += int(dones.sum())
+        assert torch.equal(sp, obs.to(dtype)), k
+        assert torch.equal(sc, ex["observations"]["critic"].to(dtype)), k
+    assert resets > 0
+    obs, ex = venv.reset()
+    torch.cuda.synchronize()
+    assert torch.equal(sp, obs.to(dtype)) and torch.equal(sc, ex["observations"]["critic"].to(dtype))
+    venv.set_obs_sink(None)
+    keep = sp.clone()
+    venv.step(torch.zeros(n, 4, device=DEV))
+    torch.cuda.synchronize()
+    assert torch.equal(sp, keep)
+    with pytest.raises(ValueError):
+        venv.set_obs_sink(sp[:, :8].contiguous(), sc[:, :8].contiguous())
+    venv.close()
+
+
+@pytest.mark.gpu
+def test_runner_obs_sink_matches_copy():
+    """OnPolicyRunner with the observation sink (bf16 rollout storage written by the step kernel) trains
+    exactly like the copy path: same stored observations, same parameters after two learn() calls."""
+    from generalizableracing_amd.rsl_rl import OnPolicyRunner, QuadcopterPPORunnerCfg
+
+    runs = []
+    for sink in (True, False):
+        torch.manual_seed(9)
+        cfg = QuadcopterPPORunnerCfg(device=DEV, num_steps_per_env=8)
+        cfg.algorithm.storage_obs_dtype = "bfloat16"
+        cfg.algorithm.obs_sink = sink
+        env = RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=512), sim=SimCfg(device=DEV), stage=1))
+        r = OnPolicyRunner(RslRlVecEnvWrapper(env), cfg.to_dict(), log_dir=None, device=DEV)
+        assert r.obs_sink is sink
+        r.learn(2)
+        r.learn(1)
+        torch.cuda.synchronize()
+        runs.append(r)
+    a, b = runs
+    T = a.num_steps_per_env
+    assert torch.equal(a.alg.storage.observations[1:T], b.alg.storage.observations[1:T])
+    assert torch.equal(a.alg.storage.privileged_observations[1:T], b.alg.storage.privileged_observations[1:T])
+    for (k, x), (_, y) in zip(a.alg.policy.state_dict().items(), b.alg.policy.state_dict().items()):
+        assert torch.equal(x, y), k
+    for r in runs:
+        r.env.close()

@@ -88,7 +88,7 @@ def test_smooth_loss_matches_hand_restatement():
     # a reset between t and t+1 (cont = 0) leaves the sample unmixed: zero smoothness term
     torch.manual_seed(7)
     loss0, _ = alg.smooth_loss(o, o2, torch.zeros(B, 1), mu, v)
-    assert float(loss0) == 0.0
+    assert float(loss0.detach()) == 0.0
     # gradient flows into both heads
     loss.backward()
     assert pol.actor[0].weight.grad is not None and pol.critic[0].weight.grad is not None

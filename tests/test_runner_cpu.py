@@ -106,3 +106,35 @@ def test_runner_other_stages(stage):
     runner = OnPolicyRunner(env, small_cfg().to_dict(), log_dir=None, device="cpu")
     runner.learn(1)
     assert math.isfinite(runner.last_log["value_function"])
+
+
+@pytest.mark.parametrize("obs_dtype", ["float32", "bfloat16"])
+def test_obs_sink_matches_copy(obs_dtype):
+    """The observation sink (the env writes each transition's rows into storage slot t + 1; slot T opens the
+    next rollout) trains exactly like add_transitions copying the rows: same stored observations, same
+    parameters, across two learn() calls (fresh observations at each call's start) of two iterations each."""
+    runs = []
+    for sink in (True, False):
+        torch.manual_seed(5)
+        cfg = small_cfg()
+        cfg.algorithm.storage_obs_dtype = obs_dtype
+        cfg.algorithm.obs_sink = sink
+        r = OnPolicyRunner(OracleVecEnv(num_envs=32), cfg.to_dict(), log_dir=None, device="cpu")
+        assert r.obs_sink is sink
+        r.learn(2)
+        r.learn(2)
+        runs.append(r)
+    a, b = runs
+    T = a.num_steps_per_env
+    assert a.alg.storage.observations.shape[0] == T + 1
+    assert torch.equal(a.alg.storage.observations[1:T], b.alg.storage.observations[1:T])
+    assert torch.equal(a.alg.storage.privileged_observations[1:T], b.alg.storage.privileged_observations[1:T])
+    for (k, x), (_, y) in zip(a.alg.policy.state_dict().items(), b.alg.policy.state_dict().items()):
+        assert torch.equal(x, y), k
+
+
+def test_obs_sink_not_used_for_l2c2():
+    cfg = small_cfg()
+    cfg.algorithm.class_name = "PPOL2C2"
+    r = OnPolicyRunner(OracleVecEnv(num_envs=16), cfg.to_dict(), log_dir=None, device="cpu")
+    assert not r.obs_sink
