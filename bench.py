@@ -76,6 +76,14 @@ def max_over_ranks(x: float, device) -> float:
     return float(t.item())
 
 
+_T0 = time.time()
+
+
+def progress(msg):
+    """One line per finished leg on stderr (the JSON line alone goes to stdout)."""
+    print(f"[bench {time.time() - _T0:6.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def make_env(n, rank, device, gates, integrator, obstacles=True, **overrides):
     cfg = RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=device), stage=1, integrator=integrator,
                        terrain=TerrainCfg(num_gates=gates, obstacles=obstacles), env_id_offset=rank * n,
@@ -254,7 +262,10 @@ def policy_in_loop_fused(env, steps, device):
         for _ in range(2):
             obs = one_step(obs)
     torch.cuda.current_stream().wait_stream(s)
-    while env._calls % ACTION_RING != 0 or fused._calls % 2 != 0:  # align the ping-pong bindings
+    # align the ping-pong bindings (each step advances both call counters by one: fix their parity first)
+    if (env._calls - fused._calls) % 2:
+        obs = env.observe()
+    while env._calls % ACTION_RING != 0 or fused._calls % 2 != 0:
         obs = one_step(obs)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
@@ -332,6 +343,8 @@ def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False, graph_up
     for _ in range(iters):
         runner.learn(1)
         fps.append(runner.last_log["fps"])
+    progress(f"train_fps n={n} fused={fused} bf16_storage={bf16_storage} graph_update={graph_update} "
+             f"obs_sink={obs_sink}: {np.median(fps):.4g}")
     venv.close()
     return float(np.median(fps))
 
@@ -416,6 +429,7 @@ def main():
         raise RuntimeError(f"kernel_us {us:.2f} > wall us per step {ms_per_step * 1e3:.2f}: timing is inconsistent")
     rd, wr = env.bytes_per_env_step()
     achieved = (rd + wr) * n / (us * 1e-6) / 1e9
+    progress(f"headline: {value:.4g} env-steps/s, kernel {us:.2f} us")
     extra = {"steady_state_env_steps_per_s_per_gpu": steady,
              "steady_state_note": "median of 3 timed runs of 1024 steps (16 replays of the 64-step graph), one rank"}
     if not a.no_extras:
@@ -423,7 +437,9 @@ def main():
             "env_steps_per_s": policy_in_loop_graphed(env, 1024, device),
             "launch": "hipgraph (64 x [PyTorch fp32 actor MLP 16-256-256-4 + Gaussian sample + gr_step])",
             "note": "SURVEY §8d env-only rate: gr_step + policy inference at the reference's fp32"}
+        progress("env_only_fp32")
         extra["policy_in_loop_env_steps_per_s"] = policy_in_loop(env, 256, device)
+        progress("policy_in_loop")
         rate, us_pol, tfs = policy_in_loop_fused(env, 512, device)
         extra["policy_in_loop_fused"] = {
             "env_steps_per_s": rate, "launch": "hipgraph (64 x [fused inference + gr_step])",
@@ -454,9 +470,11 @@ def main():
             "traffic": load_traffic(n, a.gates, 1),
             "obstacles_per_track_max": int(env_o.obstacle_table.counts.max()),
             "obstacles_per_track_mean": float(env_o.obstacle_table.counts.mean())}
+        progress("with_obstacles")
         env_o.close()
     if not a.no_extras and not a.obstacles:
         extra["env_count_sweep"] = env_count_sweep(rank, device, a)
+        progress("env_count_sweep")
         # BASELINE config C5 on one GPU: 32-gate tracks, startup DR (plant vs controller mass, drag, thrust
         # error, rotor constants), hipGraph of [fused rollout inference + step]
         env_c5 = make_env(n, rank, device, 32, a.integrator, False, dr_rotor=1)
@@ -483,6 +501,7 @@ def main():
                                 "step_kernel_us_bf16_obs_sink": kt_c5s["kernel_us"],
                                 "bytes_per_env_step_bf16_obs_sink": {"read": rd_c5s, "written": wr_c5s}}
         env_c5.close()
+        progress("c5_32_gates")
     if not a.no_extras:
         extra["train_total_fps_4096_envs"] = train_fps(device)
         extra["train_total_fps_4096_envs_graph_update"] = train_fps(device, graph_update=True)
@@ -501,6 +520,7 @@ def main():
 
         for key, obst in (("vision_camera", False), ("vision_camera_with_obstacles", True)):
             cam = bench_camera.run(n, steps=24, warmup=4, device=device, obstacles=obst)
+            progress(key)
             extra[key] = {
                 "kernel": cam["kernel"], "image": cam["image"], "render_fraction": cam["render_fraction"],
                 "ms_per_call": cam["ms_avg_call"], "ms_render_call": cam["ms_render_call"],
@@ -511,6 +531,7 @@ def main():
     cpu = None
     if rank == 0 and ws == 1 and not a.no_extras:
         cpu = cpu_baseline(a.cpu_seconds, obstacles=bool(a.obstacles))
+        progress("cpu_baseline")
     traffic = load_traffic(n, a.gates, a.obstacles)
     if rank == 0:
         line = {

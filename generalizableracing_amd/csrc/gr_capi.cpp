@@ -30,6 +30,7 @@ struct gr_ctx {
   gr::KConst* kc_dev = nullptr;    // device copy read by the kernels
   std::vector<int> blk_types;      // per workgroup: first | last terrain type << 16
   int* blk_dev = nullptr;
+  unsigned* status_dev = nullptr;  // GR_STATUS_* word the kernels OR into
   std::string err;
   // optional depth camera
   bool cam_enabled = false;
@@ -62,17 +63,22 @@ int ensure_dev(gr_ctx* c, const char* what) {
   const size_t nbt = c->blk_types.size() * sizeof(int);
   hipError_t e = hipMalloc(&c->kc_dev, sizeof(gr::KConst));
   if (e == hipSuccess) e = hipMalloc(&c->blk_dev, nbt);
+  if (e == hipSuccess) e = hipMalloc(&c->status_dev, 16);
+  if (e == hipSuccess) e = hipMemset(c->status_dev, 0, 16);
   if (e == hipSuccess) e = hipMemcpy(c->kc_dev, &c->kc, sizeof(gr::KConst), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->blk_dev, c->blk_types.data(), nbt, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     if (c->kc_dev) (void)hipFree(c->kc_dev);
     if (c->blk_dev) (void)hipFree(c->blk_dev);
+    if (c->status_dev) (void)hipFree(c->status_dev);
     c->kc_dev = nullptr;
     c->blk_dev = nullptr;
+    c->status_dev = nullptr;
     return hip_fail(c, e, what);
   }
   c->args.kc = c->kc_dev;
   c->args.blk_types = c->blk_dev;
+  c->args.status = c->status_dev;
   e = gr::allow_large_lds();
   if (e != hipSuccess) return hip_fail(c, e, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
   return GR_OK;
@@ -132,9 +138,6 @@ void derive(gr_ctx* c) {
   // table + handovers within the CU's LDS (one workgroup per CU at the bench size); beyond that the
   // (L2-resident) table is read directly
   a.lds_bytes = bytes + GR_XCH_BYTES <= GR_LDS_MAX ? (int)bytes : 0;
-#ifdef GR_ABL_NOLDS
-  a.lds_bytes = 0;
-#endif
   gr::KHot& h = c->args.h;
   h.num_envs = g.num_envs;
   h.num_levels = g.num_levels;
@@ -264,6 +267,7 @@ int gr_destroy(gr_ctx* c) {
   if (c->table) (void)hipFree(c->table);
   if (c->kc_dev) (void)hipFree(c->kc_dev);
   if (c->blk_dev) (void)hipFree(c->blk_dev);
+  if (c->status_dev) (void)hipFree(c->status_dev);
   if (c->cam_dev) (void)hipFree(c->cam_dev);
   delete c;
   return GR_OK;
@@ -451,6 +455,28 @@ int gr_step(gr_ctx* c, const float* actions, void* stream) {
   }
   hipError_t e = gr::launch_env(gr::KMODE_STEP, c->args, actions, nullptr, (hipStream_t)stream, t0, t1);
   return e == hipSuccess ? GR_OK : hip_fail(c, e, "gr_step");
+}
+
+int gr_device_status(gr_ctx* c, uint32_t* status, int clear, void* stream) {
+  if (!c || !status) return fail(c, GR_ERR_ARG, "gr_device_status: null argument");
+  *status = 0;
+  if (!c->status_dev) return GR_OK;  // no kernel has run
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  unsigned host = 0;
+  hipError_t e = hipMemcpyAsync(&host, c->status_dev, sizeof(unsigned), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess && clear) e = hipMemsetAsync(c->status_dev, 0, sizeof(unsigned), s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(c, e, "gr_device_status");
+  *status = host;
+  return GR_OK;
+}
+
+int gr_test_inject_fault(gr_ctx* c, int fault) {
+  if (!c) return GR_ERR_ARG;
+  if (fault != GR_FAULT_NONE && fault != GR_FAULT_OBST_NO_SIGNAL)
+    return fail(c, GR_ERR_ARG, "gr_test_inject_fault: unknown fault");
+  c->args.h.test_fault = fault;
+  return GR_OK;
 }
 
 int gr_set_timing(gr_ctx* c, int enable) {

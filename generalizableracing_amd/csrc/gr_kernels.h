@@ -48,6 +48,7 @@ struct KHot {
   float obs_lin_vel_noise, obs_att_noise;
   float obst_span;  // obstacle grid: cell + 2 margin (m), the side of a hinted grown cell
   int dr_rotor;     // per-env rotor constants (GR_P_ROTOR)
+  int test_fault;   // gr_test_inject_fault (0 in production)
 };
 
 // Passed by value (kernarg): per-binding pointers + the constants pointer.
@@ -65,6 +66,7 @@ struct KArgs {
   void* sink_policy;
   void* sink_critic;
   int sink_dtype;
+  unsigned* status;  // device status word (GR_STATUS_* bits, OR-ed by the kernels; gr_device_status)
   KHot h;
 };
 

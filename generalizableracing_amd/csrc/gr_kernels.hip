@@ -663,9 +663,6 @@ DEV void reset_env(const KArgs& a, const Tab& tab, Env& e, uint32_t gid) {
 // gate-pose noise of the current (out[0..2]) and next (out[3..5]) gate: one draw
 // per (episode, gates passed), commands.py:287-289,329-350
 DEV void gate_noise(const KArgs& a, const Env& e, uint32_t gid, float out[6]) {
-#ifdef GR_ABL_NOGATENOISE
-  if (true) { for (int k = 0; k < 6; ++k) out[k] = 0.0f; return; }
-#endif
   if (!a.kc->cfg.add_gate_noise) { for (int k = 0; k < 6; ++k) out[k] = 0.0f; return; }
   uint32_t f[6];
   gr_fields6(draw(a, gid, (uint32_t)e.epoch, GR_TAG_GATE, (uint32_t)e.acc), f);
@@ -1161,20 +1158,25 @@ __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
       }
       commit();  // barrier 1: the table is first needed by the collision test
       STAMP(14);
-#ifndef GR_ABL_NOCOLL
       uint32_t cm = collision_mask<false>(a, sl.tab, e.type, e.lvl, e.p, e.q, ObstGrid{});
       STAMP(15);
       if (OBST) {
         // wait for the partner policy wave's obstacle mask (same 64 envs); it is resident and never waits on us
-        // (bounded: a protocol bug must not hang the GPU; the parity tests would catch its result)
+        // (bounded: a protocol bug must not hang the GPU; a wave that gives up raises GR_STATUS_OBST_WAIT_TIMEOUT
+        // in the context's status word, which gr_device_status reports)
+        bool signalled = false;
         for (int spin = 0; spin < (1 << 22); ++spin) {
-          if (__hip_atomic_load(oflag + (t >> 6), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0) break;
+          if (__hip_atomic_load(oflag + (t >> 6), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0) {
+            signalled = true;
+            break;
+          }
           __builtin_amdgcn_s_sleep(1);
         }
+        if (!signalled && (t & 63) == 0)
+          __hip_atomic_fetch_or(a.status, GR_STATUS_OBST_WAIT_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         cm |= (uint32_t)__float_as_int(obx[O_MASK * GR_BLOCK + t].x);
       }
       ccount = __builtin_popcount(cm);
-#endif
     } else {
       ObstGrid og{};
       if (OBST) og = obst_grid(a, e.type, e.lvl);
@@ -1206,9 +1208,6 @@ __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
     const float dist = norm3(dg);
     const int near_gate = dist < c.gate_threshold;
     int done = terminated | time_out;
-#ifdef GR_ABL_NORESET
-    done = 0;
-#endif
     float lc[4];
     for (int k = 0; k < 4; ++k) lc[k] = th_raw[k] * sc[k] + of[k];
     lc[0] = lc[0] / e.mc;
@@ -1292,11 +1291,9 @@ __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
       if (done) store_rst(a, i, e);
     }
     STAMP(12);
-#ifndef GR_ABL_NOLOG
     // the level slots too (post-reset level / noise level are this lane's): the policy waves, whose tail is
     // the longest of the three roles, write no log row
     wave_log(a, threadIdx.x >> 6, lg, reset_lane, live ? (float)e.lvl : 0.0f, live ? e.nl : 0.0f);
-#endif
     STAMP(8);
     RSTAMP(10);
   } else if (role == 1) {
@@ -1328,19 +1325,14 @@ __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
         float A[3], B[3], Cz[3];
         body_axes(a, qq, A, B, Cz);
         uint32_t om = 0u;
-#ifdef GR_ABL_OBST_NOTEST
-        if (false) {
-#else
         if (obst_hint_holds(hint, pp, a.h.obst_span)) {
-#endif
           om = obst_list(a, hfirst, hcount, psp, pp, A, B, Cz);
         } else {
-#ifndef GR_ABL_OBST_NOTEST
           om = obst_lookup(a, og, pp, A, B, Cz);
-#endif
         }
         obx[O_MASK * GR_BLOCK + t] = make_float4(__int_as_float((int)om), 0.0f, 0.0f, 0.0f);
-        if ((t & 63) == 0) __hip_atomic_store(oflag + (t >> 6), 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if ((t & 63) == 0 && a.h.test_fault != GR_FAULT_OBST_NO_SIGNAL)
+          __hip_atomic_store(oflag + (t >> 6), 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       STAMP(12);
       obs_noise(a, gid, cnt, on);  // off the critical path: needed after barrier 2
@@ -1348,12 +1340,7 @@ __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
       commit();  // barrier 1 (joined at once: the physics and episode waves set its time)
       STAMP(1);
       // observation noise needs only the call counter: it runs while the physics waves collide
-#ifndef GR_ABL_NOOBSNOISE
       obs_noise(a, gid, cnt, on);
-#else
-      for (int k = 0; k < 3; ++k) on.vfac[k] = 1.0f;
-      on.qn[0] = 1.0f; on.qn[1] = on.qn[2] = on.qn[3] = 0.0f;
-#endif
       STAMP(2);
     }
     // call counter for the observation-noise stream: double-buffered by call parity,
@@ -1369,15 +1356,12 @@ __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
     if constexpr (OBST) {
       // the next step's hint: the cell list of the post-step (or the next episode's start) position; its loads
       // land while the policy row is computed
-#ifndef GR_ABL_OBST_NOHINT
       const ObstGrid ogn = reset ? obst_grid(a, e.type, e.lvl) : og;
       next_hint = obst_hint_of(a, ogn, e.p);
-#endif
     }
     const float lc[4] = {xlc.x, xlc.y, xlc.z, xlc.w};
     gate_advance(a, sl.tab, e);
     STAMP(7);
-#ifndef GR_ABL_NOOBS
     {
       float4 prow[4];
       compute_policy(a, sl.tab, e, gid, on, lc, prow);
@@ -1386,7 +1370,6 @@ __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
       if (a.sink_policy) store_rows_sink(a, a.sink_policy, blockIdx.x * GR_BLOCK + (t & ~63), n, stg + (t & ~63));
       if (live) st1(a.buf.obs_aux + i, aux);
     }
-#endif
     if (OBST && live) st4(reinterpret_cast<float4*>(a.buf.state), GR_P_OHINT * (size_t)n + i, next_hint);
     STAMP(8);
     RSTAMP(10);
@@ -1429,7 +1412,6 @@ __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
     gate_advance(a, sl.tab, e);
     STAMP(14);
     if (live) store_istate(a, i, e);
-#ifndef GR_ABL_NOOBS
     {  // critic observation (noise-free) of the post-reset, post-gate-progress state
       float4 crow[4];
       compute_critic(sl.tab, e, lc, crow);
@@ -1438,7 +1420,6 @@ __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
       if (a.sink_critic)
         store_rows_sink(a, a.sink_critic, blockIdx.x * GR_BLOCK + (t & ~63), n, stg + 4 * GR_BLOCK + (t & ~63));
     }
-#endif
     STAMP(8);
     RSTAMP(10);
   }
@@ -1719,9 +1700,6 @@ hipError_t launch_test_philox(int n, uint32_t c0, uint32_t c1, uint32_t c2, uint
 }
 
 hipError_t allow_large_lds() {
-#ifdef GR_ABL_NO_LDS_ATTR
-  return hipSuccess;
-#endif
   const void* ks[] = {reinterpret_cast<const void*>(&step_kernel<true, false>),
                       reinterpret_cast<const void*>(&step_kernel<true, true>),
                       reinterpret_cast<const void*>(&env_kernel<KMODE_RESET, true>),

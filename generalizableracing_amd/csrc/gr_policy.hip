@@ -40,11 +40,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #ifndef POL_PF
 #define POL_PF 1  // k steps of A-fragment prefetch (register ring of POL_PF + 1 fragments per row tile)
 #endif
-#ifdef POL_ABL_NOA
-#define POL_RING_IDX 0
-#else
 #define POL_RING_IDX (s % (PF + 1))
-#endif
 #ifndef POL_PIPE
 #define POL_PIPE 0  // 1: drain group g (activation, pack, layer 3) under group g + 1's first MFMAs
 #endif
@@ -114,7 +110,6 @@ __global__ __launch_bounds__(POL_WAVES * 64) void policy_kernel(gr_policy_args p
     const bf16x8* __restrict__ g1 = reinterpret_cast<const bf16x8*>(net.w1);
     const bf16x8* __restrict__ g2 = reinterpret_cast<const bf16x8*>(net.w2);
     const bf16x8* __restrict__ g3 = reinterpret_cast<const bf16x8*>(net.w3);
-#ifndef POL_ABL_NOSTAGE
     // all of a thread's fragments loaded before any is written: one L2 round trip, not one per fragment
     constexpr int NV = T * 64 + T * S * 64 + S * 64, PER = (NV + POL_WAVES * 64 - 1) / (POL_WAVES * 64);
     bf16x8 st[PER];
@@ -129,7 +124,6 @@ __global__ __launch_bounds__(POL_WAVES * 64) void policy_kernel(gr_policy_args p
       const int i = threadIdx.x + q * POL_WAVES * 64;
       if (i < NV) wl[i] = st[q];  // w1s, w2s, w3s are contiguous
     }
-#endif
     for (int i = threadIdx.x; i < H; i += POL_WAVES * 64) {
       b1s[i] = net.b1[i];
       b2s[i] = net.b2[i];
@@ -241,11 +235,7 @@ __global__ __launch_bounds__(POL_WAVES * 64) void policy_kernel(gr_policy_args p
       for (int u = 0; u < TG; ++u) ring[s][u] = w2s[((t + u) * S + s) * 64 + lane];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-#ifdef POL_ABL_NOA  // timing only: no layer-2 A reads after the first k step (wrong results)
-      if (false) {
-#else
       if (s + PF < S) {
-#endif
 #pragma unroll
         for (int u = 0; u < TG; ++u) ring[(s + PF) % (PF + 1)][u] = w2s[((t + u) * S + s + PF) * 64 + lane];
       }
@@ -333,11 +323,7 @@ __global__ __launch_bounds__(POL_WAVES * 64) void policy_kernel(gr_policy_args p
   }
 #pragma unroll
   for (int m = 16 * C; m < 64; m *= 2) lp += __shfl_xor(lp, m, 64);
-#ifdef POL_ABL_NOEPI
-  if (env < n && lp == 12345.0f) {
-#else
   if (env < n) {
-#endif
 #pragma unroll
     for (int q = 0; q < RPL; ++q) {
       const int r = RPL * p + q;

@@ -314,6 +314,21 @@ class RacingEnv:
         self._call("gr_bytes_per_env_step", C.byref(r), C.byref(w))
         return r.value, w.value
 
+    def device_status(self, clear: bool = True) -> int:
+        """gr_device_status: the GR_STATUS_* bits the step kernels raised since the last clear (synchronises the
+        env's stream)."""
+        st = C.c_uint32()
+        self._call("gr_device_status", C.byref(st), int(bool(clear)), self._stream())
+        return st.value
+
+    def check_device_status(self):
+        """Raise if a kernel flagged an untrustworthy step since the last check (the runner calls this once per
+        rollout, where it synchronises anyway)."""
+        st = self.device_status(clear=True)
+        if st:
+            why = "; ".join(t for b, t in _abi.STATUS_TEXT.items() if st & b) or "unknown"
+            raise RuntimeError(f"gr step kernel status 0x{st:x}: {why}")
+
     def state_field(self, name: str) -> torch.Tensor:
         """Gather a named per-env state field ([N, k] copy) from the SoA planes."""
         parts = [self.state[p, :, c0:c0 + k] for p, c0, k in _abi.STATE_FIELDS[name]]
@@ -477,6 +492,10 @@ class RslRlVecEnvWrapper:
 
     def seed(self, seed: int = -1) -> int:
         return self.env.seed(seed)
+
+    def check_device_status(self):
+        """RacingEnv.check_device_status."""
+        self.env.check_device_status()
 
     def set_obs_sink(self, policy, critic=None):
         """RacingEnv.set_obs_sink (rollout storage slots written by the kernel; None unbinds)."""

@@ -186,6 +186,8 @@ class OnPolicyRunner:
                     stats.update(rewards, dones)
                 if self.obs_sink:
                     self.env.set_obs_sink(None)
+                if hasattr(self.env, "check_device_status"):
+                    self.env.check_device_status()  # a kernel-flagged step fails the iteration loudly
                 if torch.cuda.is_available() and str(self.device).startswith("cuda"):
                     torch.cuda.synchronize(self.device)
                 stop = time.time()

@@ -360,6 +360,16 @@ typedef struct gr_policy_args {
 } gr_policy_args;
 int gr_policy_forward(const gr_policy_args* args, void* stream);
 
+/* Device status: the GR_STATUS_* bits the kernels of this context raised since the last clear (0: none).
+ * Synchronises `stream` (the stream the steps ran on); clear != 0 resets the word.  A raised bit means the
+ * outputs of some step since the last check are not trustworthy. */
+#define GR_STATUS_OBST_WAIT_TIMEOUT 1u /* a physics wave gave up waiting for its obstacle mask (stale mask used) */
+int gr_device_status(gr_ctx* ctx, uint32_t* status, int clear, void* stream);
+/* Fault injection for the status path's tests (0: none, production). */
+#define GR_FAULT_NONE 0
+#define GR_FAULT_OBST_NO_SIGNAL 1 /* the policy waves never signal the obstacle mask */
+int gr_test_inject_fault(gr_ctx* ctx, int fault);
+
 /* In-library HIP-event timing of the fused step kernel alone (not the log
  * finalize): when enabled, gr_step brackets the env kernel with a pair of
  * events on the caller's stream (ring of 4096 pairs; do not capture into a

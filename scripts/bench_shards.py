@@ -51,6 +51,8 @@ def run(n, shards, policy, device="cuda:0", reps=8):
         s.wait_stream(cur)
         with torch.cuda.stream(s):
             chain(k, 2)
+            if fused is not None and (envs[k]._calls - fused[k]._calls) % 2:
+                obs[k] = envs[k].observe()
             while envs[k]._calls % ACTION_RING != 0 or (fused is not None and fused[k]._calls % 2 != 0):
                 chain(k, 1)
         cur.wait_stream(s)

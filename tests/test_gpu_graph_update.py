@@ -28,6 +28,7 @@ def test_graphed_update_matches_eager():
     n = 2048
     env = RslRlVecEnvWrapper(RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV))))
     cfg = QuadcopterPPORunnerCfg(device=DEV)
+    cfg.algorithm.obs_sink = False  # the storages are copied slot for slot
     runner = OnPolicyRunner(env, cfg.to_dict(), log_dir=None, device=DEV)
     alg = runner.alg
     kw = dict(cfg.to_dict()["algorithm"])
@@ -81,6 +82,7 @@ def test_bf16_autocast_update_follows_fp32():
     n = 4096
     env = RslRlVecEnvWrapper(RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV))))
     cfg = QuadcopterPPORunnerCfg(device=DEV)
+    cfg.algorithm.obs_sink = False  # the storages are copied slot for slot
     runner = OnPolicyRunner(env, cfg.to_dict(), log_dir=None, device=DEV)
     alg = runner.alg
     kw = dict(cfg.to_dict()["algorithm"])
@@ -122,6 +124,7 @@ def test_graphed_update_across_iterations():
     n = 2048
     env = RslRlVecEnvWrapper(RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV))))
     cfg = QuadcopterPPORunnerCfg(device=DEV)
+    cfg.algorithm.obs_sink = False  # the storages are copied slot for slot
     runner = OnPolicyRunner(env, cfg.to_dict(), log_dir=None, device=DEV)
     alg = runner.alg
     kw = dict(cfg.to_dict()["algorithm"])
@@ -154,8 +157,10 @@ def test_graphed_update_across_iterations():
         torch.manual_seed(11 + it)
         lg = alg_g.update()
         for pe, pg, q in zip(alg.policy.parameters(), alg_g.policy.parameters(), p0):
-            moved = float((pe.detach() - q).abs().max())
-            diff = float((pe.detach() - pg.detach()).abs().max())
+            # norms, not maxima: Adam turns the round-off of a near-zero gradient element into an update of
+            # up to lr in either direction, so single elements may differ by a learning rate
+            moved = float((pe.detach() - q).norm())
+            diff = float((pe.detach() - pg.detach()).norm())
             assert moved > 0.0 and diff <= 0.05 * moved, (it, diff, moved)
         assert abs(le["value_function"] - lg["value_function"]) <= 1e-4 * abs(le["value_function"]), (it, le, lg)
         # the surrogate is a mean of +-A * ratio over normalised advantages (|A| ~ 1) that nearly cancels

@@ -138,3 +138,29 @@ def test_controller_output_vs_oracle_and_golden(ctx, golden, motor):
         np.testing.assert_allclose(xo[:, 9:13], golden["thr_out"][0], rtol=1e-5, atol=1e-5)
     lib.gr_destroy(h2)
 
+
+
+@pytest.mark.gpu
+def test_device_status_reports_obstacle_wait_timeout():
+    """The bounded obstacle-mask wait of the physics waves: with the partner's signal suppressed
+    (gr_test_inject_fault) the step completes, raises GR_STATUS_OBST_WAIT_TIMEOUT in the status word, and
+    check_device_status fails loudly; without the fault the word stays clear."""
+    from generalizableracing_amd import _abi
+    from generalizableracing_amd.envs.racing_cfg import RacingEnvCfg, SceneCfg, SimCfg, TerrainCfg
+    from generalizableracing_amd.envs.racing_env import RacingEnv
+
+    env = RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=256), sim=SimCfg(device="cuda:0"), stage=1,
+                                 terrain=TerrainCfg(obstacles=True)))
+    a = torch.zeros(256, 4, device="cuda:0")
+    for _ in range(3):
+        env.step(a)
+    assert env.device_status() == 0
+    env._call("gr_test_inject_fault", _abi.GR_FAULT_OBST_NO_SIGNAL)
+    env.step(a)
+    env._call("gr_test_inject_fault", _abi.GR_FAULT_NONE)
+    assert env.device_status(clear=False) & _abi.GR_STATUS_OBST_WAIT_TIMEOUT
+    with pytest.raises(RuntimeError, match="obstacle mask"):
+        env.check_device_status()
+    env.step(a)
+    assert env.device_status() == 0
+    env.close()
