@@ -27,18 +27,24 @@ from .tracks import build_tracks
 LOG_RING = 64
 
 
+_EMPTY_MEAN_SLOTS = [_abi.LOG_EPSUM0 + j for j in range(7)] + [_abi.LOG_ACC, _abi.LOG_M_ACTRATE, _abi.LOG_M_LINSPD,
+                                                               _abi.LOG_M_ANGSPD]
+_EMPTY_COUNT_SLOTS = [_abi.LOG_T_TIMEOUT, _abi.LOG_T_CONTACT, _abi.LOG_T_BADPOSE]
+
+
 class _EpisodeLog(Mapping):
     """extras["log"] of one call: the kernel leaves per-wave partial sums in a
     ring slot; the means Isaac Lab's managers log are formed on first access
     (gr_log_finalize, one small launch, no host sync).  Valid for LOG_RING calls."""
 
-    __slots__ = ("_env", "_k", "_vals", "_keys")
+    __slots__ = ("_env", "_k", "_vals", "_keys", "_empty_reset")
 
     def __init__(self, env: "RacingEnv", k: int, keys: dict):
         self._env = env
         self._k = k
         self._vals = None
         self._keys = keys
+        self._empty_reset = False  # reset(env_ids=[]): _reset_idx over an empty set
 
     def values(self) -> torch.Tensor:  # type: ignore[override]
         if self._vals is None:
@@ -55,6 +61,11 @@ class _EpisodeLog(Mapping):
                 pv = prev._vals.data_ptr() if prev is not None and prev._vals is not None else None
                 env._call("gr_log_finalize", env._log_slab[lg._k % LOG_RING].data_ptr(), pv, out.data_ptr(),
                           env._stream())
+                if lg._empty_reset:
+                    # the reference's _reset_idx over no envs (manager_based_diff_rl_env.py:362-407): the means
+                    # over the reset envs are torch.mean of an empty set (NaN), the termination counts 0
+                    out[_EMPTY_MEAN_SLOTS] = float("nan")
+                    out[_EMPTY_COUNT_SLOTS] = 0.0
                 lg._vals = out
                 prev = lg
         return self._vals
@@ -400,11 +411,14 @@ class RacingEnv:
     def reset(self, seed: int | None = None, env_ids=None, options=None):
         """ManagerBasedEnv.reset -> _reset_idx(env_ids) (+ curriculum), then observations."""
         mask_t = None
+        empty = False
         if env_ids is not None:
             ids = torch.as_tensor(env_ids, device=self.device, dtype=torch.long)
+            empty = ids.numel() == 0
             mask_t = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
             mask_t[ids] = 1
         out, log = self._advance()
+        log._empty_reset = empty
         mp = mask_t.data_ptr() if mask_t is not None else None
         self._call("gr_reset", mp, self._stream())
         self._render(_abi.GR_CAM_RESET, mp)

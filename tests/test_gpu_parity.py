@@ -117,6 +117,17 @@ def test_env_free_run_bit_exact(conf):
     orc.reset(mask)
     assert_envs_equal(kernel_envs(env), orc.envs, "masked reset")
     compare_outputs(env, orc, "masked reset")
+    # reset over no envs: the reference's _reset_idx([]) logs NaN means and zero termination counts
+    _, extras = env.reset(env_ids=np.zeros(0, np.int64))
+    log = extras["log"]
+    for key in log:
+        v = float(log[key])
+        if key.startswith(("Episode_Reward/", "Metrics/")):
+            assert np.isnan(v), key
+        elif key.startswith("Episode_Termination/"):
+            assert v == 0.0, key
+        else:
+            assert np.isfinite(v), key
     env.close()
 
 
