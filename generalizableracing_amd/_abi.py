@@ -224,7 +224,7 @@ EXPORTS = [
     "gr_test_philox",
     "gr_debug_read_stamps",
     "gr_camera_config_default", "gr_camera_config_size", "gr_enable_camera", "gr_bind_camera_buffers",
-    "gr_camera_render", "gr_camera_bytes_per_env", "gr_policy_forward",
+    "gr_camera_render", "gr_camera_bytes_per_env", "gr_policy_forward", "gr_column_sum_partials", "gr_column_sum",
 ]
 
 _lib = None
@@ -266,6 +266,8 @@ def _declare(lib):
         "gr_camera_render": (C.c_int, [vp, C.c_int, vp, vp]),
         "gr_camera_bytes_per_env": (C.c_int, [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
         "gr_policy_forward": (C.c_int, [C.POINTER(GrPolicyArgs), vp]),
+        "gr_column_sum_partials": (C.c_int, [C.c_int64]),
+        "gr_column_sum": (C.c_int, [vp, C.c_int, C.c_int64, C.c_int32, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name) and os.environ.get("GR_LIB_PATH"):

@@ -647,6 +647,15 @@ int gr_policy_forward(const gr_policy_args* a, void* stream) {
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
+int gr_column_sum_partials(int64_t rows) { return rows < 0 ? GR_ERR_ARG : gr::column_sum_blocks(rows); }
+
+int gr_column_sum(const void* x, int dtype, int64_t rows, int32_t cols, float* partial, float* out, void* stream) {
+  if (!x || !partial || !out || rows < 0 || cols <= 0 || (dtype != GR_DTYPE_F32 && dtype != GR_DTYPE_BF16))
+    return GR_ERR_ARG;
+  const hipError_t e = gr::launch_column_sum(x, dtype, (long long)rows, cols, partial, out, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
 int gr_test_dynamics(gr_ctx* c, int n, int mode, const float* si, const float* ab, const float* cmd, const float* ci,
                      const float* par, const float* drag, float* so, float* co, float* xo, void* stream) {
   if (!c || n <= 0 || !si || !ab || !cmd || !ci || !par || !drag || !so || !co || !xo) return GR_ERR_ARG;

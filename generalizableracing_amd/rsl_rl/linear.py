@@ -16,17 +16,36 @@ import torch.nn.functional as F
 
 SPLIT = 4096  # rows per chunk (scripts/prof_update.py --split: 2048-4096 best at 65 536 and 4 096 envs)
 # set by the graph-captured PPO step (ppo.py _GraphedStep): every Linear takes _TallLinearFn, whose bias
-# gradient is a GEMV (see bias_grad)
+# gradient is gr_column_sum (see bias_grad)
 _FORCE_FN = False
 
 
 def bias_grad(gy: torch.Tensor) -> torch.Tensor:
-    """sum over rows of gy [M, N] as a GEMV with a ones vector.  Inside a captured hipGraph this keeps the
-    column sum off PyTorch's multi-block reduction, whose cross-block semaphores live in a buffer that, on
-    this ROCm build, is not held by the graph's pool: eager allocations between replays reused it and the
-    replays' bias gradients came out wrong (scripts/debug_graph_update.py)."""
-    ones = torch.ones(gy.shape[0], 1, device=gy.device, dtype=gy.dtype)
-    return (gy.t() @ ones).squeeze(1)
+    """Sum over the rows of gy [M, N] (fp32 out).  On the GPU: gr_column_sum (libgr.so, gr_update.hip), one
+    HBM pass in a fixed summation order.  Not PyTorch's gy.sum(0): inside a captured hipGraph its multi-block
+    reduction keeps cross-block semaphores in a buffer that, on this ROCm build, is not held by the graph's
+    pool (eager allocations between replays reused it and the replays' bias gradients came out wrong,
+    scripts/debug_graph_update.py); and as a GEMM with a ones vector hipBLASLt tiles only the N x 1 output
+    (1.5 ms at M = 393 216, N = 256, half of the update step)."""
+    if gy.device.type != "cuda":
+        return gy.float().sum(0)
+    from .. import _abi
+
+    lib = _abi.load()
+    gy = gy.contiguous()
+    m, n = gy.shape
+    if gy.dtype == torch.bfloat16:
+        dtype = _abi.GR_DTYPE_BF16
+    else:
+        gy = gy.float()
+        dtype = _abi.GR_DTYPE_F32
+    part = torch.empty(lib.gr_column_sum_partials(m) * n, device=gy.device, dtype=torch.float32)
+    out = torch.empty(n, device=gy.device, dtype=torch.float32)
+    rc = lib.gr_column_sum(gy.data_ptr(), dtype, m, n, part.data_ptr(), out.data_ptr(),
+                           torch.cuda.current_stream(gy.device).cuda_stream)
+    if rc != 0:
+        raise RuntimeError(f"gr_column_sum failed (status {rc})")
+    return out
 
 
 def split_k_wgrad(gy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
@@ -59,7 +78,7 @@ class _TallLinearFn(torch.autograd.Function):
         x, w = ctx.saved_tensors
         gx = gy @ w.to(gy.dtype) if ctx.needs_input_grad[0] else None
         gw = split_k_wgrad(gy, x.to(gy.dtype)).to(ctx.wdtype) if ctx.needs_input_grad[1] else None
-        gb = bias_grad(gy.float()).to(ctx.wdtype) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        gb = bias_grad(gy).to(ctx.wdtype) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return gx, gw, gb
 
 

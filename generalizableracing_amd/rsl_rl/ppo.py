@@ -301,7 +301,7 @@ class _GraphedStep:
         self.idx.copy_(torch.arange(self.mb, device=self.idx.device))
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        _lin._FORCE_FN = True  # bias gradients as GEMVs in the captured step (linear.bias_grad)
+        _lin._FORCE_FN = True  # bias gradients by gr_column_sum in the captured step (linear.bias_grad)
         try:
             with torch.cuda.stream(s):
                 for _ in range(3):

@@ -164,3 +164,24 @@ def test_device_status_reports_obstacle_wait_timeout():
     env.step(a)
     assert env.device_status() == 0
     env.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,cols", [(1, 1), (1000, 3), (393216, 256), (24577, 4), (70000, 1), (5000, 300),
+                                       (3000, 1100)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_column_sum(rows, cols, dtype):
+    """gr_column_sum (the PPO update's bias gradients, rsl_rl/linear.py bias_grad) against a float64 sum of
+    the same elements; two calls are bit-identical (fixed summation order)."""
+    from generalizableracing_amd.rsl_rl.linear import bias_grad
+
+    g = torch.Generator(device="cuda:0").manual_seed(rows + cols)
+    x = torch.randn(rows, cols, device="cuda:0", generator=g).to(dtype)
+    got = bias_grad(x)
+    again = bias_grad(x)
+    torch.cuda.synchronize()
+    want = x.double().sum(0)
+    scale = x.double().abs().sum(0) + 1.0
+    assert got.dtype == torch.float32 and got.shape == (cols,)
+    assert float(((got.double() - want).abs() / scale).max()) < 1e-6
+    assert torch.equal(got, again)
