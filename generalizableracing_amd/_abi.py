@@ -211,6 +211,7 @@ class GrPolicyArgs(C.Structure):
 
 
 GR_POLICY_ACT_LRELU, GR_POLICY_ACT_ELU = 0, 1
+GR_POLICY_LRELU_PRESCALE = 0.505
 GR_CAM_STEP, GR_CAM_RESET, GR_CAM_OBSERVE = 0, 1, 2
 GR_DTYPE_F32, GR_DTYPE_BF16 = 0, 1
 GR_STATUS_OBST_WAIT_TIMEOUT = 1
@@ -222,7 +223,7 @@ EXPORTS = [
     "gr_num_blocks", "gr_num_log_rows", "gr_log_finalize", "gr_bytes_per_env_step", "gr_bind_tracks", "gr_bind_obstacles", "gr_bind_buffers", "gr_bind_obs_sink", "gr_init", "gr_reset",
     "gr_step", "gr_observe", "gr_device_status", "gr_test_inject_fault", "gr_set_timing", "gr_read_timing", "gr_test_dynamics", "gr_test_math",
     "gr_test_philox",
-    "gr_debug_read_stamps",
+    "gr_debug_read_stamps", "gr_debug_read_policy_stamps",
     "gr_camera_config_default", "gr_camera_config_size", "gr_enable_camera", "gr_bind_camera_buffers",
     "gr_camera_render", "gr_camera_bytes_per_env", "gr_policy_forward", "gr_column_sum_partials", "gr_column_sum",
 ]
@@ -259,6 +260,7 @@ def _declare(lib):
         "gr_test_math": (C.c_int, [vp, C.c_int, C.c_int, vp, vp, vp, vp]),
         "gr_test_philox": (C.c_int, [vp, C.c_int] + [C.c_uint32] * 4 + [vp, vp]),
         "gr_debug_read_stamps": (C.c_int, [vp, C.c_int]),
+        "gr_debug_read_policy_stamps": (C.c_int, [vp, C.c_int]),
         "gr_camera_config_default": (C.c_int, [C.POINTER(GrCameraConfig)]),
         "gr_camera_config_size": (C.c_size_t, []),
         "gr_enable_camera": (C.c_int, [vp, C.POINTER(GrCameraConfig)]),

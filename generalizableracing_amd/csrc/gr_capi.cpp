@@ -682,4 +682,10 @@ int gr_debug_read_stamps(uint64_t* host, int n) {
   return e == hipSuccess ? GR_OK : (e == hipErrorNotSupported ? GR_ERR_STATE : GR_ERR_HIP);
 }
 
+int gr_debug_read_policy_stamps(uint64_t* host, int n) {
+  if (!host || n <= 0) return GR_ERR_ARG;
+  hipError_t e = gr::read_policy_stamps(reinterpret_cast<unsigned long long*>(host), n);
+  return e == hipSuccess ? GR_OK : (e == hipErrorNotSupported ? GR_ERR_STATE : GR_ERR_HIP);
+}
+
 }  // extern "C"

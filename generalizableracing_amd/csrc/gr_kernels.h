@@ -123,6 +123,7 @@ hipError_t launch_test_dynamics(const KArgs& a, int n, int mode, const float* si
                                 hipStream_t s);
 hipError_t launch_test_math(int fn, int n, const float* x, const float* y, float* out, hipStream_t s);
 hipError_t read_stamps(unsigned long long* host, int n);
+hipError_t read_policy_stamps(unsigned long long* host, int n);  // gr_policy.hip
 hipError_t allow_large_lds();  // lift the default dynamic-LDS cap of the env kernels
 hipError_t launch_test_philox(int n, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
                               uint32_t* out, hipStream_t s);

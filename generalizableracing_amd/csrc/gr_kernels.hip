@@ -100,11 +100,31 @@ DEV void quat_mul(const float a[4], const float b[4], float o[4]) {
   o[2] = (qq - yy) + (a[0] - a[1]) * (b[2] + b[3]);
   o[3] = (qq - zz) + (a[3] + a[2]) * (b[0] - b[1]);
 }
+// sin / cos with a wave-uniform fast path: when every lane's |x| < pi/4 the Cody-Waite reduction is the
+// identity (k = 0, r = x exactly), so skipping it gives the same bits as gr_sincosf
+DEV void sincos_w(float x, float* s, float* c) {
+  if (__all(gr_fabsf(x) < 0.78f)) {
+    const float r2 = x * x;
+    float sp = 2.75573192e-06f;
+    sp = gr_fmaf(sp, r2, -1.98412698e-04f);
+    sp = gr_fmaf(sp, r2, 8.33333333e-03f);
+    sp = gr_fmaf(sp, r2, -1.66666667e-01f);
+    *s = gr_fmaf(x, r2 * sp, x);
+    float cp = -2.75573192e-07f;
+    cp = gr_fmaf(cp, r2, 2.48015873e-05f);
+    cp = gr_fmaf(cp, r2, -1.38888889e-03f);
+    cp = gr_fmaf(cp, r2, 4.16666667e-02f);
+    cp = gr_fmaf(cp, r2, -0.5f);
+    *c = gr_fmaf(r2, cp, 1.0f);
+    return;
+  }
+  gr_sincosf(x, s, c);
+}
 DEV void quat_from_euler_xyz(float roll, float pitch, float yaw, float o[4]) {
   float sy, cy, sr, cr, sp, cp;
-  gr_sincosf(yaw * 0.5f, &sy, &cy);
-  gr_sincosf(roll * 0.5f, &sr, &cr);
-  gr_sincosf(pitch * 0.5f, &sp, &cp);
+  sincos_w(yaw * 0.5f, &sy, &cy);
+  sincos_w(roll * 0.5f, &sr, &cr);
+  sincos_w(pitch * 0.5f, &sp, &cp);
   o[0] = (cy * cr) * cp + (sy * sr) * sp;
   o[1] = (cy * sr) * cp - (sy * cr) * sp;
   o[2] = (cy * cr) * sp + (sy * sr) * cp;
@@ -599,8 +619,8 @@ DEV void reset_draws(const KArgs& a, uint32_t gid, uint32_t ep, float m_ctrl, Re
   float z0, z1;
   gr_box_muller21(f[20], f[21], &z0, &z1);
   r.thr = 1.0f + z0 * 0.01f;
-  gr_sincosf(r.att[0] * 0.5f, &r.sr, &r.cr);
-  gr_sincosf(r.att[1] * 0.5f, &r.sp, &r.cp);
+  sincos_w(r.att[0] * 0.5f, &r.sr, &r.cr);
+  sincos_w(r.att[1] * 0.5f, &r.sp, &r.cp);
 }
 
 DEV void reset_apply(const KArgs& a, const Tab& tab, Env& e, const ResetDraws& r) {

@@ -56,6 +56,22 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #define POL_ENVS_PER_WAVE (16 * POL_COLS)
 static_assert(POL_COLS == 1 || POL_COLS == 2 || POL_COLS == 4, "the epilogue maps a wave's 16 C envs x 4 rows onto 64 lanes");
 
+// -DGR_STAMPS (diagnostic build only, scripts/stamps.py policy): lane 0 of every wave records s_memtime at
+// phase boundaries (0 entry, 1 weights staged, then per env tile k < 3: 2 + 4k layer 1, 3 + 4k layers 2 + 3,
+// 4 + 4k epilogue stored; 14 / 15 s_memrealtime at entry / exit).  The product build compiles these away.
+#ifdef GR_STAMPS
+#define POL_STAMP_WAVES 4096
+__device__ unsigned long long g_pol_stamps[POL_STAMP_WAVES * 16];
+#define PSTAMP(k, fn)                                                                              \
+  do {                                                                                            \
+    unsigned long long t_ = fn();                                                                 \
+    const unsigned w_ = (blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6); \
+    if ((threadIdx.x & 63) == 0 && w_ < POL_STAMP_WAVES && (k) < 16) g_pol_stamps[w_ * 16 + (k)] = t_; \
+  } while (0)
+#else
+#define PSTAMP(k, fn)
+#endif
+
 template <int ACT>
 __device__ __forceinline__ float pol_act(float x) {
   // LeakyReLU (torch default slope 0.01) or ELU (alpha 1); compile-time, so the layer loops stay straight-line
@@ -79,11 +95,12 @@ __device__ __forceinline__ f32x4 bias4(const float* b, int row0, int lane) {
 template <int ACT>
 __device__ __forceinline__ void act4(f32x4& v) {
   if constexpr (ACT == GR_POLICY_ACT_LRELU) {
-    // max(x, 0.01 x): the products as two packed v_pk_mul_f32; this file is built with -fno-honor-nans, so
-    // v_max_f32 reads the MFMA results without a canonicalizing copy (csrc/Makefile)
-    typedef float f32x2 __attribute__((ext_vector_type(2)));
-    const f32x2 lo = (f32x2){v[0], v[1]} * 0.01f, hi = (f32x2){v[2], v[3]} * 0.01f;
-    v[0] = fmaxf(v[0], lo[0]); v[1] = fmaxf(v[1], lo[1]); v[2] = fmaxf(v[2], hi[0]); v[3] = fmaxf(v[3], hi[1]);
+    // LeakyReLU(y) = 0.505 y + 0.495 |y|.  Layers 1 and 2 arrive pre-scaled by GR_POLICY_LRELU_PRESCALE
+    // (v = 0.505 y, the host scales W and b), so the activation is ONE v_fma_f32 with an |.| source
+    // modifier per element: v + (0.99 / 1.01) |v| (y for y > 0, 0.01 y below).  (max(y, 0.01 y) took a
+    // packed multiply and a max; packed f32 VALU beside MFMAs costs more than its issue slot.)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = __builtin_fmaf(__builtin_fabsf(v[r]), 0.980198019f, v[r]);
   } else {
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = pol_act<ACT>(v[r]);
@@ -100,6 +117,8 @@ __global__ __launch_bounds__(POL_WAVES * 64) void policy_kernel(gr_policy_args p
   constexpr int S = H / 32;  // 32-wide k steps over a hidden layer
   constexpr int C = POL_COLS;
   const gr_policy_net& net = pa.net[blockIdx.y];
+  PSTAMP(14, __builtin_amdgcn_s_memrealtime);
+  PSTAMP(0, __builtin_amdgcn_s_memtime);
   extern __shared__ bf16x8 wl[];
   bf16x8* w1s = wl;                  // [T][64]
   bf16x8* w2s = wl + T * 64;         // [T][S][64]
@@ -165,6 +184,9 @@ __global__ __launch_bounds__(POL_WAVES * 64) void policy_kernel(gr_policy_args p
     lpc[q] = -logf(sdv[q]) - 0.91893853320467274f;
   }
   load_obs(blockIdx.x * envs_per_block);
+  PSTAMP(1, __builtin_amdgcn_s_memtime);
+  int tile_k = 0;
+  (void)tile_k;  // (stamp slot index, GR_STAMPS builds)
 #if POL_PRIO
   if (wave >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
@@ -195,6 +217,7 @@ __global__ __launch_bounds__(POL_WAVES * 64) void policy_kernel(gr_policy_args p
       h1[t / 2][c] = pack8(y0, y1);
     }
   }
+  PSTAMP(2 + 4 * tile_k, __builtin_amdgcn_s_memtime);
   // ---- layer 2 (pairs of row tiles) fused with layer 3: out^T += W3[:, k step t/2] act(W2 h1^T + b2)
   f32x4 o[C];
 #pragma unroll
@@ -266,6 +289,7 @@ __global__ __launch_bounds__(POL_WAVES * 64) void policy_kernel(gr_policy_args p
 #if POL_PIPE
   drain(pend, T - TG);
 #endif
+  PSTAMP(3 + 4 * tile_k, __builtin_amdgcn_s_memtime);
   // Epilogue on all 64 lanes (lane map above): the accumulator lane e & 15 of column tile e >> 4 holds
   // output rows 0-3 of env e.
   const int nout = net.num_out, src = e_w & 15, ct = e_w >> 4;
@@ -278,6 +302,8 @@ __global__ __launch_bounds__(POL_WAVES * 64) void policy_kernel(gr_policy_args p
       v = ct == c ? t : v;
     }
     if (p == 0 && env < n) net.out[env] = v + net.b3[0];
+    PSTAMP(4 + 4 * tile_k, __builtin_amdgcn_s_memtime);
+    ++tile_k;
     continue;
   }
   float y[RPL];
@@ -334,7 +360,10 @@ __global__ __launch_bounds__(POL_WAVES * 64) void policy_kernel(gr_policy_args p
     }
     if (p == 0) pa.log_prob[env] = lp;
   }
+  PSTAMP(4 + 4 * tile_k, __builtin_amdgcn_s_memtime);
+  ++tile_k;
   }  // env tiles
+  PSTAMP(15, __builtin_amdgcn_s_memrealtime);
 }
 
 template <int H, int ACT>
@@ -348,6 +377,18 @@ static hipError_t launch_policy_t(const gr_policy_args& a, dim3 grid, size_t lds
   }
   hipLaunchKernelGGL((policy_kernel<H, ACT>), grid, dim3(POL_WAVES * 64), lds, s, a);
   return hipGetLastError();
+}
+
+hipError_t read_policy_stamps(unsigned long long* host, int n) {
+#ifdef GR_STAMPS
+  if (n > POL_STAMP_WAVES * 16) n = POL_STAMP_WAVES * 16;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pol_stamps), (size_t)n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost);
+#else
+  (void)host;
+  (void)n;
+  return hipErrorNotSupported;
+#endif
 }
 
 hipError_t launch_policy(const gr_policy_args& a, hipStream_t s) {

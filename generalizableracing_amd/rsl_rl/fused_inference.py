@@ -141,9 +141,11 @@ class FusedPolicyInference:
     def refresh(self):
         """Repack the weights (after a PPO update; in place, so captured graphs stay valid)."""
         nets = {"actor": mlp_layers(self.policy.actor)[0], "critic": mlp_layers(self.policy.critic)[0]}
+        # LeakyReLU: layers 1 and 2 pre-scaled (GR_POLICY_LRELU_PRESCALE, include/gr.h)
+        s = _abi.GR_POLICY_LRELU_PRESCALE if self.activation == _abi.GR_POLICY_ACT_LRELU else 1.0
         for name, lin in nets.items():
-            parts = {"w1": pack_w1(lin[0].weight), "b1": lin[0].bias.detach().float(),
-                     "w2": pack_w2(lin[1].weight), "b2": lin[1].bias.detach().float(),
+            parts = {"w1": pack_w1(lin[0].weight * s), "b1": lin[0].bias.detach().float() * s,
+                     "w2": pack_w2(lin[1].weight * s), "b2": lin[1].bias.detach().float() * s,
                      "w3": pack_w3(lin[2].weight), "b3": lin[2].bias.detach().float()}
             for k, v in parts.items():
                 key = f"{name}.{k}"

@@ -337,6 +337,10 @@ int gr_camera_bytes_per_env(const gr_ctx* ctx, int64_t* render_bytes, int64_t* r
  */
 #define GR_POLICY_ACT_LRELU 0
 #define GR_POLICY_ACT_ELU 1
+/* With GR_POLICY_ACT_LRELU, W1, b1, W2 and b2 are packed multiplied by this factor ((1 + 0.01) / 2): the
+ * kernel forms LeakyReLU(y) from v = 0.505 y as v + (0.99 / 1.01) |v| (one fused multiply-add).  W3, b3
+ * are not scaled. */
+#define GR_POLICY_LRELU_PRESCALE 0.505f
 typedef struct gr_policy_net {
   const float* obs; /* [num_envs][num_obs] fp32, 16-byte aligned, num_obs <= 32 and a multiple of 4 */
   const void* w1;   /* bf16 fragments [H/16][64][8] */
@@ -413,6 +417,8 @@ int gr_test_philox(gr_ctx* ctx, int n, uint32_t c0, uint32_t c1, uint32_t c2, ui
  * timestamps of the most recent step launch (12 u64 per wave).  Product builds
  * return GR_ERR_STATE. */
 int gr_debug_read_stamps(uint64_t* host, int n);
+/* The same for the fused policy kernel (16 u64 per wave, gr_policy.hip). */
+int gr_debug_read_policy_stamps(uint64_t* host, int n);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,46 @@
+"""Timing-only variant builds of libgr.so from a patched copy of the sources (the product sources carry no
+ablation switches).  A patch is a JSON list of [file, old, new] text replacements; every `old` must occur
+exactly once.  Output: variants/<name>/libgr.so (GR_LIB_PATH selects it on the GPU box).
+
+    python scripts/build_patched.py NAME PATCH.json
+"""
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def build(name, patch):
+    tmp = tempfile.mkdtemp(prefix="grvar_")
+    src = os.path.join(tmp, "generalizableracing_amd", "csrc")
+    shutil.copytree(os.path.join(ROOT, "generalizableracing_amd", "csrc"), src)
+    shutil.copytree(os.path.join(ROOT, "include"), os.path.join(tmp, "include"))
+    for fname, old, new in patch:
+        p = os.path.join(src, fname)
+        s = open(p).read()
+        if s.count(old) != 1:
+            raise SystemExit(f"{fname}: patch text found {s.count(old)} times: {old[:80]!r}")
+        open(p, "w").write(s.replace(old, new))
+    out = os.path.join(ROOT, "variants", name)
+    os.makedirs(out, exist_ok=True)
+    flags = ("--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt "
+             "-fno-slp-vectorize")
+    objs = []
+    for f in ("gr_kernels.hip", "gr_camera.hip", "gr_policy.hip", "gr_update.hip", "gr_capi.cpp"):
+        o = os.path.join(tmp, f + ".o")
+        extra = " -fno-honor-nans" if f == "gr_policy.hip" else ""
+        lang = " -x hip" if f.endswith(".cpp") else ""
+        subprocess.run(f"/opt/rocm/bin/hipcc {flags}{extra}{lang} -c -o {o} {os.path.join(src, f)}", shell=True, check=True)
+        objs.append(o)
+    subprocess.run(f"/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o {out}/libgr.so {' '.join(objs)}", shell=True,
+                   check=True)
+    shutil.rmtree(tmp)
+    print(f"{out}/libgr.so")
+
+
+if __name__ == "__main__":
+    build(sys.argv[1], json.load(open(sys.argv[2])))

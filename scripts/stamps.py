@@ -42,7 +42,7 @@ ROLE_PHASES = {
 }
 
 
-def run(n=65536, steps=200):
+def run(n=int(os.environ.get("N", "65536")), steps=200):
     os.environ["GR_LIB_PATH"] = os.path.join(OUT, "libgr.so")
     import ctypes as C
 
@@ -59,7 +59,7 @@ def run(n=65536, steps=200):
     for k in range(steps):
         env.step(acts[k % bench.ACTION_RING])
     torch.cuda.synchronize()
-    waves = (n // 256) * 12  # step kernel: 12 waves per 256-env workgroup
+    waves = max(1, n // 256) * 12  # step kernel: 12 waves per 256-env workgroup
     buf = np.zeros(waves * 16, np.uint64)
     assert env._lib.gr_debug_read_stamps(buf.ctypes.data_as(C.c_void_p), buf.size) == 0
     st = buf.reshape(waves, 16).astype(np.int64)
@@ -85,5 +85,44 @@ def run(n=65536, steps=200):
     env.close()
 
 
+def policy(n=65536):
+    """Phase timelines of the fused policy kernel (gr_policy_forward) from its stamps."""
+    os.environ["GR_LIB_PATH"] = os.path.join(OUT, "libgr.so")
+    import ctypes as C
+
+    import numpy as np
+    import torch
+
+    sys.path.insert(0, ROOT)
+    from generalizableracing_amd.rsl_rl import ActorCritic
+    from generalizableracing_amd.rsl_rl.fused_inference import FusedPolicyInference
+
+    pol = ActorCritic(16, 16, 4, [256, 256], [256, 256], "lrelu").to("cuda:0")
+    fused = FusedPolicyInference(pol, n, "cuda:0")
+    obs = torch.randn(n, 16, device="cuda:0")
+    for _ in range(8):
+        fused.act(obs, obs)
+    torch.cuda.synchronize()
+    waves = 4096
+    buf = np.zeros(waves * 16, np.uint64)
+    assert fused._lib.gr_debug_read_policy_stamps(buf.ctypes.data_as(C.c_void_p), buf.size) == 0
+    st = buf.reshape(waves, 16).astype(np.int64)
+    live = st[:, 0] != 0
+    st = st[live]
+    rt0, rt1 = st[:, 14], st[:, 15]
+    out = {"waves": int(live.sum()), "kernel_span_us(realtime)": float((rt1.max() - rt0.min()) * 10 / 1e3),
+           "wave_start_spread_us": float((rt0.max() - rt0.min()) * 10 / 1e3),
+           "end_us_pcts(10,50,90,100)": [float(np.percentile((rt1 - rt0.min()) * 10 / 1e3, q)) for q in (10, 50, 90, 100)],
+           "life_cycles_p50": float(np.percentile(st[:, 4 + 4 * 1] - st[:, 0], 50)),
+           "staging_cycles_mean": float((st[:, 1] - st[:, 0]).mean())}
+    prev = st[:, 1]
+    for k in range(2):
+        l1, l23, ep = st[:, 2 + 4 * k], st[:, 3 + 4 * k], st[:, 4 + 4 * k]
+        out[f"tile{k}"] = {"layer1": float((l1 - prev).mean()), "layer2+3": float((l23 - l1).mean()),
+                           "epilogue": float((ep - l23).mean())}
+        prev = ep
+    print(json.dumps(out, indent=1))
+
+
 if __name__ == "__main__":
-    {"build": build, "run": run}[sys.argv[1]]()
+    {"build": build, "run": run, "policy": policy}[sys.argv[1]]()
