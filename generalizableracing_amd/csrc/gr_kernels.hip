@@ -1184,15 +1184,13 @@ __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
         // wait for the partner policy wave's obstacle mask (same 64 envs); it is resident and never waits on us
         // (bounded: a protocol bug must not hang the GPU; a wave that gives up raises GR_STATUS_OBST_WAIT_TIMEOUT
         // in the context's status word, which gr_device_status reports)
-        bool signalled = false;
-        for (int spin = 0; spin < (1 << 22); ++spin) {
-          if (__hip_atomic_load(oflag + (t >> 6), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0) {
-            signalled = true;
-            break;
-          }
+        int spin = 0;
+        while (__hip_atomic_load(oflag + (t >> 6), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0 &&
+               spin < (1 << 22)) {
           __builtin_amdgcn_s_sleep(1);
+          ++spin;
         }
-        if (!signalled && (t & 63) == 0)
+        if (__builtin_expect(spin >= (1 << 22), 0) && (t & 63) == 0)
           __hip_atomic_fetch_or(a.status, GR_STATUS_OBST_WAIT_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         cm |= (uint32_t)__float_as_int(obx[O_MASK * GR_BLOCK + t].x);
       }
