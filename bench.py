@@ -39,6 +39,7 @@ from generalizableracing_amd.envs.racing_cfg import RacingEnvCfg, SceneCfg, SimC
 from generalizableracing_amd.envs.racing_env import RacingEnv  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_MFMA_PEAK_TFS = 157.3  # MI355X dense fp32 matrix peak (v_mfma_f32_16x16x4_f32; MI355X_MICROARCH.md)
 ACTION_RING = 64
 
 
@@ -239,17 +240,18 @@ def policy_in_loop_graphed(env, steps, device):
     return n * reps * ACTION_RING / (time.perf_counter() - t0)
 
 
-def policy_in_loop_fused(env, steps, device):
+def policy_in_loop_fused(env, steps, device, precision="bf16"):
     """C5 "hipGraph-captured step + inference": per step, the fused MFMA inference of both MLPs
-    (FusedPolicyInference: actor mean + Gaussian sample + log prob, critic value; bf16 operands, fp32
-    accumulation) on the step's observations, then gr_step on the sampled actions; 64 such steps are
-    captured in one hipGraph and replayed.  Returns (env-steps/s, per-launch us of the inference kernel)."""
+    (FusedPolicyInference: actor mean + Gaussian sample + log prob, critic value; bf16 operands with fp32
+    accumulation, or fp32 operands on fp32 MFMA = the reference's precision) on the step's observations,
+    then gr_step on the sampled actions; 64 such steps are captured in one hipGraph and replayed.  Returns
+    (env-steps/s, per-launch us of the inference kernel, its useful TFLOP/s)."""
     from generalizableracing_amd.rsl_rl import ActorCritic
     from generalizableracing_amd.rsl_rl.fused_inference import FusedPolicyInference
 
     n = env.num_envs
     pol = ActorCritic(16, 16, 4, [256, 256], [256, 256], "lrelu").to(device)
-    fused = FusedPolicyInference(pol, n, device, env_id_offset=env.cfg.env_id_offset)
+    fused = FusedPolicyInference(pol, n, device, env_id_offset=env.cfg.env_id_offset, precision=precision)
 
     def one_step(obs):
         acts = fused.act(obs["policy"], obs["critic"])[0]
@@ -446,6 +448,18 @@ def main():
             "inference_kernel": "gr::policy_kernel<256> (MFMA 16x16x32 bf16, fp32 accumulate)",
             "inference_kernel_us": us_pol, "inference_TFLOPs": tfs,
             "note": "actor+critic MLP(16-256-256-out), Gaussian sample + log prob; bf16 operands (C5)"}
+        progress("policy_in_loop_fused")
+        rate32, us32, tfs32 = policy_in_loop_fused(env, 512, device, precision="fp32")
+        extra["policy_in_loop_fused_fp32"] = {
+            "env_steps_per_s": rate32, "launch": "hipgraph (64 x [fused fp32 inference + gr_step])",
+            "inference_kernel": "gr::policy_f32_kernel<256> (MFMA 16x16x4 f32: fp32 operands, the reference's "
+                                "precision)",
+            "inference_kernel_us": us32, "inference_TFLOPs": tfs32,
+            "roofline": {"bound": "mfma", "achieved": tfs32, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                         "frac": tfs32 / FP32_MFMA_PEAK_TFS},
+            "note": "actor+critic MLP(16-256-256-out) in fp32 (mean / value within 1e-5 of the fp32 module), "
+                    "Gaussian sample + log prob: SURVEY §8d env-only rate at the reference's precision"}
+        progress("policy_in_loop_fused_fp32")
     env.close()
     if not a.no_extras and not a.obstacles:
         # the reference task's terrain also carries walls / orbits / ground obstacles:

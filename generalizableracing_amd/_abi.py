@@ -207,10 +207,11 @@ class GrPolicyArgs(C.Structure):
     _fields_ = [("net", GrPolicyNet * 2), ("std", C.c_void_p), ("actions", C.c_void_p), ("log_prob", C.c_void_p),
                 ("counters", C.c_void_p), ("counter_index", C.c_int32), ("num_envs", C.c_int32),
                 ("hidden", C.c_int32), ("activation", C.c_int32), ("env_id_offset", C.c_int32),
-                ("seed_lo", C.c_uint32), ("seed_hi", C.c_uint32)]
+                ("seed_lo", C.c_uint32), ("seed_hi", C.c_uint32), ("precision", C.c_int32), ("reserved", C.c_int32)]
 
 
 GR_POLICY_ACT_LRELU, GR_POLICY_ACT_ELU = 0, 1
+GR_POLICY_BF16, GR_POLICY_FP32 = 0, 1
 GR_POLICY_LRELU_PRESCALE = 0.505
 GR_CAM_STEP, GR_CAM_RESET, GR_CAM_OBSERVE = 0, 1, 2
 GR_DTYPE_F32, GR_DTYPE_BF16 = 0, 1

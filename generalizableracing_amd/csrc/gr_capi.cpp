@@ -631,7 +631,8 @@ int gr_camera_bytes_per_env(const gr_ctx* c, int64_t* render_bytes, int64_t* reu
 
 int gr_policy_forward(const gr_policy_args* a, void* stream) {
   if (!a || a->num_envs <= 0 || (a->hidden != 128 && a->hidden != 256) ||
-      (a->activation != GR_POLICY_ACT_LRELU && a->activation != GR_POLICY_ACT_ELU))
+      (a->activation != GR_POLICY_ACT_LRELU && a->activation != GR_POLICY_ACT_ELU) ||
+      (a->precision != GR_POLICY_BF16 && a->precision != GR_POLICY_FP32))
     return GR_ERR_ARG;
   for (int k = 0; k < 2; ++k) {
     const gr_policy_net& n = a->net[k];
@@ -643,7 +644,8 @@ int gr_policy_forward(const gr_policy_args* a, void* stream) {
   }
   if (!a->std || !a->actions || !a->log_prob || !a->counters || (a->counter_index != 0 && a->counter_index != 1))
     return GR_ERR_ARG;
-  const hipError_t e = gr::launch_policy(*a, (hipStream_t)stream);
+  const hipError_t e = a->precision == GR_POLICY_FP32 ? gr::launch_policy_f32(*a, (hipStream_t)stream)
+                                                       : gr::launch_policy(*a, (hipStream_t)stream);
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 

@@ -37,6 +37,9 @@ class RslRlPpoAlgorithmCfg:
     # not in the reference: rollout inference (act / evaluate / log prob) as one bf16 MFMA launch
     # (rsl_rl/fused_inference.py); the update stays fp32.  MLP ActorCritic with 128 / 256 hidden units only.
     fused_rollout_inference: bool = False
+    # precision of that launch: "bf16" (bf16 operands, BASELINE C5) or "fp32" (fp32 operands on fp32 MFMA, the
+    # reference's arithmetic: the stored old mean / log prob then match the update's fp32 recompute)
+    fused_rollout_precision: str = "bf16"
     # not in the reference: dtype of the rollout storage's observation buffers ("bfloat16" halves them;
     # mini-batches are cast back to fp32 for the update)
     storage_obs_dtype: str = "float32"

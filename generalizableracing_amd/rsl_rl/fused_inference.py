@@ -1,5 +1,9 @@
 """Fused rollout inference of the MLP ActorCritic on MFMA (libgr.so gr_policy_forward).
 
+Two precisions behind the same call: "bf16" (below: bf16 operands, fp32 accumulation, the C5 option) and
+"fp32" (the reference's precision: fp32 operands on v_mfma_f32_16x16x4_f32, each output an fp32 fma
+chain; the kernel reads the module's row-major fp32 weights, gr_policy_f32.hip).
+
 Replaces, for the rollout, the calls PPO.act makes on the policy
 (standalone/rsl_rl/ext/algorithms/ppo.py:71-85): `policy.act(obs)` (sample Normal(actor(obs), std)),
 `policy.evaluate(critic_obs)`, `policy.get_actions_log_prob(actions)`, `action_mean`, `action_std`.
@@ -98,8 +102,12 @@ class FusedPolicyInference:
     tensors (rebind-free, graph-capturable): actions, action_mean [N, A], values [N, 1], log_prob [N],
     action_sigma [N, A].  Used by PPO when the algorithm cfg sets `fused_rollout_inference` (ppo.py)."""
 
-    def __init__(self, policy, num_envs: int, device, seed: int = 0, env_id_offset: int = 0):
+    def __init__(self, policy, num_envs: int, device, seed: int = 0, env_id_offset: int = 0,
+                 precision: str = "bf16"):
         self.policy = policy
+        if precision not in ("bf16", "fp32"):
+            raise ValueError(f"precision must be 'bf16' or 'fp32', got {precision!r}")
+        self.precision = precision
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise RuntimeError("fused policy inference runs on the GPU (HIP); there is no CPU path")
@@ -141,22 +149,30 @@ class FusedPolicyInference:
     def refresh(self):
         """Repack the weights (after a PPO update; in place, so captured graphs stay valid)."""
         nets = {"actor": mlp_layers(self.policy.actor)[0], "critic": mlp_layers(self.policy.critic)[0]}
-        # LeakyReLU: layers 1 and 2 pre-scaled (GR_POLICY_LRELU_PRESCALE, include/gr.h)
-        s = _abi.GR_POLICY_LRELU_PRESCALE if self.activation == _abi.GR_POLICY_ACT_LRELU else 1.0
-        for name, lin in nets.items():
-            parts = {"w1": pack_w1(lin[0].weight * s), "b1": lin[0].bias.detach().float() * s,
-                     "w2": pack_w2(lin[1].weight * s), "b2": lin[1].bias.detach().float() * s,
-                     "w3": pack_w3(lin[2].weight), "b3": lin[2].bias.detach().float()}
+        if self.precision == "fp32":  # the module's own layout: row-major fp32 W [out, in], b [out]
+            packs = {name: {k: lin[i].weight.float() if k[0] == "w" else lin[i].bias.float()
+                            for i, k in ((0, "w1"), (0, "b1"), (1, "w2"), (1, "b2"), (2, "w3"), (2, "b3"))}
+                     for name, lin in nets.items()}
+        else:
+            packs = {name: self._pack_bf16(lin) for name, lin in nets.items()}
+        for name, parts in packs.items():
             for k, v in parts.items():
                 key = f"{name}.{k}"
-                v = v.to(self.device).contiguous()
+                v = v.detach().to(self.device).contiguous()  # fp32 parameters / bf16 fragments as packed
                 if key in self._packed:
                     self._packed[key].copy_(v)
                 else:
-                    self._packed[key] = v
+                    self._packed[key] = v.clone()  # never an alias of the module's parameter
         std = self.policy.std if self.policy.noise_std_type == "scalar" else torch.exp(self.policy.log_std)
         self.std.copy_(std.detach().float())
         self._version = self._param_version()
+
+    def _pack_bf16(self, lin):
+        # LeakyReLU: layers 1 and 2 pre-scaled (GR_POLICY_LRELU_PRESCALE, include/gr.h)
+        s = _abi.GR_POLICY_LRELU_PRESCALE if self.activation == _abi.GR_POLICY_ACT_LRELU else 1.0
+        return {"w1": pack_w1(lin[0].weight * s), "b1": lin[0].bias.detach().float() * s,
+                "w2": pack_w2(lin[1].weight * s), "b2": lin[1].bias.detach().float() * s,
+                "w3": pack_w3(lin[2].weight), "b3": lin[2].bias.detach().float()}
 
     def _net(self, name, obs, out, num_obs, num_out):
         p = self._packed
@@ -187,6 +203,7 @@ class FusedPolicyInference:
         a.counters, a.counter_index = self.counters.data_ptr(), self._calls % 2
         a.num_envs, a.hidden, a.activation, a.env_id_offset = n, self.hidden, self.activation, self.env_id_offset
         a.seed_lo, a.seed_hi = self.seed & 0xFFFFFFFF, (self.seed >> 32) & 0xFFFFFFFF
+        a.precision = _abi.GR_POLICY_FP32 if self.precision == "fp32" else _abi.GR_POLICY_BF16
         rc = self._lib.gr_policy_forward(C.byref(a), C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
         if rc != 0:
             raise RuntimeError(f"gr_policy_forward failed (status {rc})")

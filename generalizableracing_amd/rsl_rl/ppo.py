@@ -24,7 +24,7 @@ class PPO:
                  lam=0.95, value_loss_coef=1.0, entropy_coef=0.0, learning_rate=1e-3, max_grad_norm=1.0,
                  use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu",
                  normalize_advantage=True, storage_obs_dtype=torch.float32, fused_rollout_inference=False,
-                 graph_update=False, update_autocast_bf16=False, **kwargs):
+                 fused_rollout_precision="bf16", graph_update=False, update_autocast_bf16=False, **kwargs):
         self.env = env
         self.device = device
         self.desired_kl = desired_kl
@@ -52,6 +52,7 @@ class PPO:
         # rollout inference on MFMA (rsl_rl/fused_inference.py, BASELINE config C5): bf16 operands, fp32
         # accumulation, one launch for actor + sampling + log prob + critic; the update stays fp32 PyTorch
         self.fused_rollout_inference = bool(fused_rollout_inference)
+        self.fused_rollout_precision = str(fused_rollout_precision)
         self.fused = None
         # the update's mini-batch step (gather, forward, adaptive learning rate, losses, backward, clip,
         # Adam) captured once in a hipGraph and replayed per mini-batch (single rank, GPU): see _GraphedStep
@@ -81,7 +82,8 @@ class PPO:
         ucfg = getattr(getattr(self.env, "unwrapped", None), "cfg", None)
         seed = getattr(ucfg, "seed", None)
         self.fused = FusedPolicyInference(self.policy, num_envs, self.device, seed=42 if seed is None else int(seed),
-                                          env_id_offset=int(getattr(ucfg, "env_id_offset", 0) or 0))
+                                          env_id_offset=int(getattr(ucfg, "env_id_offset", 0) or 0),
+                                          precision=self.fused_rollout_precision)
 
     def test_mode(self):
         self.policy.eval()

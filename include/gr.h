@@ -329,12 +329,18 @@ int gr_camera_bytes_per_env(const gr_ctx* ctx, int64_t* render_bytes, int64_t* r
 
 /*
  * Rollout inference of the rsl_rl ActorCritic (PPO.act: standalone/rsl_rl/ext/algorithms/ppo.py:71-85
- * -> ActorCritic.act / evaluate / get_actions_log_prob) on MFMA, bf16 operands, fp32 accumulation.
+ * -> ActorCritic.act / evaluate / get_actions_log_prob) on MFMA: bf16 operands with fp32 accumulation
+ * (GR_POLICY_BF16, gr_policy.hip), or fp32 operands, the reference's precision (GR_POLICY_FP32,
+ * v_mfma_f32_16x16x4_f32, gr_policy_f32.hip).
  * Both MLPs (num_obs -> H -> H -> num_out, H = 128 or 256, LeakyReLU(0.01) or ELU) for all envs in
  * one graph-capturable launch; the actor also samples Normal(mean, std) (Philox, keyed by env and
- * `counter`) and sums the log prob over the actions.  Weights are packed by the caller into the
- * kernel's fragment order (generalizableracing_amd/rsl_rl/fused_inference.py).  Context-free.
+ * `counter`) and sums the log prob over the actions.  GR_POLICY_BF16: weights packed by the caller into
+ * the kernel's fragment order (generalizableracing_amd/rsl_rl/fused_inference.py).  GR_POLICY_FP32: the
+ * module's own row-major fp32 weights W1 [H][num_obs], W2 [H][H], W3 [num_out][H] (16-byte aligned).
+ * Both precisions draw the same Normal noise for the same (seed, env, counter).  Context-free.
  */
+#define GR_POLICY_BF16 0
+#define GR_POLICY_FP32 1
 #define GR_POLICY_ACT_LRELU 0
 #define GR_POLICY_ACT_ELU 1
 /* With GR_POLICY_ACT_LRELU, W1, b1, W2 and b2 are packed multiplied by this factor ((1 + 0.01) / 2): the
@@ -343,7 +349,7 @@ int gr_camera_bytes_per_env(const gr_ctx* ctx, int64_t* render_bytes, int64_t* r
 #define GR_POLICY_LRELU_PRESCALE 0.505f
 typedef struct gr_policy_net {
   const float* obs; /* [num_envs][num_obs] fp32, 16-byte aligned, num_obs <= 32 and a multiple of 4 */
-  const void* w1;   /* bf16 fragments [H/16][64][8] */
+  const void* w1;   /* bf16 fragments [H/16][64][8] (GR_POLICY_FP32: fp32 [H][num_obs], likewise below) */
   const float* b1;  /* [H] */
   const void* w2;   /* bf16 fragments [H/16][H/32][64][8] */
   const float* b2;  /* [H] */
@@ -361,6 +367,8 @@ typedef struct gr_policy_args {
   int32_t counter_index; /* call reads counters[i] and writes counters[i ^ 1] = counters[i] + 1 */
   int32_t num_envs, hidden, activation, env_id_offset;
   uint32_t seed_lo, seed_hi;
+  int32_t precision; /* GR_POLICY_BF16 or GR_POLICY_FP32 */
+  int32_t reserved;
 } gr_policy_args;
 int gr_policy_forward(const gr_policy_args* args, void* stream);
 

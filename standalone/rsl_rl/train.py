@@ -47,6 +47,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--livestream", type=int, default=None)
     p.add_argument("--fused_rollout", action="store_true", default=False,
                    help="Rollout inference as one bf16 MFMA launch (algorithm.fused_rollout_inference).")
+    p.add_argument("--fused_rollout_fp32", action="store_true", default=False,
+                   help="The same launch with fp32 operands on fp32 MFMA, the reference's precision "
+                        "(algorithm.fused_rollout_precision=fp32).")
     p.add_argument("--graph_update", action="store_true", default=False,
                    help="PPO mini-batch step as one replayed hipGraph (algorithm.graph_update, single GPU).")
     p.add_argument("--bf16_update", action="store_true", default=False,
@@ -93,8 +96,10 @@ def main(argv=None):
         env_cfg.scene.num_envs = args.num_envs
     if args.max_iterations is not None:
         agent_cfg.max_iterations = args.max_iterations
-    if args.fused_rollout:
+    if args.fused_rollout or args.fused_rollout_fp32:
         agent_cfg.algorithm.fused_rollout_inference = True
+    if args.fused_rollout_fp32:
+        agent_cfg.algorithm.fused_rollout_precision = "fp32"
     if args.bf16_storage:
         agent_cfg.algorithm.storage_obs_dtype = "bfloat16"
     if args.graph_update:

@@ -1,0 +1,143 @@
+"""Fused rollout inference at the reference's precision (gr_policy_forward with GR_POLICY_FP32: fp32
+operands on v_mfma_f32_16x16x4_f32) against the fp32 torch ActorCritic on the GPU.
+
+Tolerance: every output is an fp32 fma chain over K = num_obs / H / H, so the mean and the value must
+agree with a float64 evaluation of the same module to 1e-5 of the output scale (fp32 rounding over K = 256
+is ~1e-6 of it), and with torch's own fp32 forward (hipBLASLt, another summation order) to 1e-5 as well.
+The log prob must be torch's Normal.log_prob of the kernel's (mean, std, action) to 1e-5, and the noise
+must be the bf16 kernel's stream (same seed, env and counter)."""
+from __future__ import annotations
+
+import os
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from generalizableracing_amd.rsl_rl import ActorCritic  # noqa: E402
+from generalizableracing_amd.rsl_rl.fused_inference import FusedPolicyInference  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+TOL = 1e-5
+
+
+def _f64(seq, x):
+    return seq.double()(x.double())
+
+
+@pytest.mark.parametrize("hidden,activation,n,nobs", [(256, "lrelu", 65536 + 17, 16), (128, "elu", 1000, 16),
+                                                      (256, "elu", 5000, 32), (128, "lrelu", 333, 8)])
+def test_fp32_matches_module(hidden, activation, n, nobs):
+    torch.manual_seed(0)
+    pol = ActorCritic(nobs, nobs, 4, [hidden, hidden], [hidden, hidden], activation, init_noise_std=0.7).to(DEV)
+    fused = FusedPolicyInference(pol, n, DEV, seed=3, precision="fp32")
+    obs = torch.randn(n, nobs, device=DEV) * 2.0
+    cobs = torch.randn(n, nobs, device=DEV) * 2.0
+    act, val, logp, mean, sigma = fused.act(obs, cobs)
+    torch.cuda.synchronize()
+    mean, val, act, logp = mean.clone(), val.clone(), act.clone(), logp.clone()
+    with torch.no_grad():
+        m32, v32 = pol.actor(obs), pol.critic(cobs)
+        import copy
+
+        p64 = copy.deepcopy(pol)
+        m64, v64 = _f64(p64.actor, obs), _f64(p64.critic, cobs)
+    for got, want64, want32 in ((mean, m64, m32), (val, v64, v32)):
+        scale = float(want64.abs().max()) + 1e-3
+        err64 = float((got.double() - want64).abs().max())
+        err32 = float((got - want32).abs().max())
+        assert err64 < TOL * scale, (err64, scale)
+        assert err32 < TOL * scale, (err32, scale)
+    lp_ref = torch.distributions.Normal(mean, sigma).log_prob(act).sum(-1)
+    assert float((logp - lp_ref).abs().max()) < TOL * (1.0 + float(lp_ref.abs().max()))
+    # the bf16 kernel draws the same noise for the same (seed, env, counter)
+    other = FusedPolicyInference(pol, n, DEV, seed=3, precision="bf16")
+    other.act(obs, cobs)
+    torch.cuda.synchronize()
+    z32 = (act - mean) / sigma
+    z16 = (other.actions - other.action_mean) / sigma
+    assert float((z32 - z16).abs().max()) < 1e-4 * (1.0 + float(z32.abs().max()))
+
+
+def test_fp32_refresh_and_graph_capture():
+    torch.manual_seed(1)
+    n = 4096
+    pol = ActorCritic(16, 16, 4, [256, 256], [256, 256], "lrelu").to(DEV)
+    fused = FusedPolicyInference(pol, n, DEV, precision="fp32")
+    obs = torch.randn(n, 16, device=DEV)
+    fused.act(obs, obs)
+    torch.cuda.synchronize()
+    m0 = fused.action_mean.clone()
+    with torch.no_grad():
+        for p in pol.actor.parameters():
+            p.add_(0.05 * torch.randn_like(p))
+    fused.refresh()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fused.act(obs, obs)
+        fused.act(obs, obs)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fused.act(obs, obs)
+        fused.act(obs, obs)
+    g.replay()
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        want = pol.actor(obs)
+    assert not torch.allclose(m0, fused.action_mean)
+    assert float((fused.action_mean - want).abs().max()) < TOL * (float(want.abs().max()) + 1e-3)
+    a0 = fused.actions.clone()
+    g.replay()
+    torch.cuda.synchronize()
+    assert not torch.equal(a0, fused.actions)
+
+
+def test_ppo_rollout_fp32_old_log_prob_matches_update():
+    """With algorithm.fused_rollout_precision = "fp32" the rollout's stored mean / value / log prob are the
+    ones the update recomputes in fp32 (with bf16 operands the first epoch's KL is not 0): the
+    KL between the stored and the recomputed Normal is ~0 and the ratio is 1 to fp32 rounding."""
+    from generalizableracing_amd.envs.racing_cfg import RacingEnvCfg, SceneCfg, SimCfg
+    from generalizableracing_amd.envs.racing_env import RacingEnv, RslRlVecEnvWrapper
+    from generalizableracing_amd.rsl_rl import OnPolicyRunner, QuadcopterPPORunnerCfg
+
+    torch.manual_seed(2)
+    n = 2048
+    env = RslRlVecEnvWrapper(RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV))))
+    cfg = QuadcopterPPORunnerCfg(device=DEV)
+    cfg.algorithm.fused_rollout_inference = True
+    cfg.algorithm.fused_rollout_precision = "fp32"
+    runner = OnPolicyRunner(env, cfg.to_dict(), log_dir=None, device=DEV)
+    alg, pol = runner.alg, runner.alg.policy
+    assert alg.fused is not None and alg.fused.precision == "fp32"
+    obs, extras = env.get_observations()
+    cobs = extras["observations"]["critic"]
+    steps = 4
+    with torch.inference_mode():
+        for _ in range(steps):
+            a = alg.act(obs, cobs)
+            obs, rew, dones, infos = env.step(a)
+            cobs = infos["observations"]["critic"]
+            alg.process_env_step(rew, dones, infos)
+    st = alg.storage
+    with torch.inference_mode():
+        o = st.observations[:steps].float().flatten(0, 1)
+        co = st.privileged_observations[:steps].float().flatten(0, 1) if st.privileged_observations is not None else o
+        mu = pol.actor(o)
+        v = pol.critic(co)
+        sd = st.sigma[:steps].flatten(0, 1)
+        lp = torch.distributions.Normal(mu, sd).log_prob(st.actions[:steps].flatten(0, 1)).sum(-1)
+    mu_st = st.mu[:steps].flatten(0, 1)
+    scale = float(mu.abs().max()) + 1e-3
+    assert float((mu_st - mu).abs().max()) < TOL * scale
+    assert float((st.values[:steps].flatten(0, 1) - v).abs().max()) < TOL * (float(v.abs().max()) + 1e-3)
+    ratio = torch.exp(lp - st.actions_log_prob[:steps, :, 0].flatten())
+    assert float((ratio - 1.0).abs().max()) < 1e-4
+    kl = torch.sum(torch.log(sd / sd) + (sd**2 + (mu_st - mu) ** 2) / (2.0 * sd**2) - 0.5, dim=-1)
+    assert float(kl.abs().max()) < 1e-9
+    env.close()
