@@ -240,12 +240,13 @@ def policy_in_loop_graphed(env, steps, device):
     return n * reps * ACTION_RING / (time.perf_counter() - t0)
 
 
-def policy_in_loop_fused(env, steps, device, precision="bf16"):
+def policy_in_loop_fused(env, steps, device, precision="bf16", actor_only=False):
     """C5 "hipGraph-captured step + inference": per step, the fused MFMA inference of both MLPs
     (FusedPolicyInference: actor mean + Gaussian sample + log prob, critic value; bf16 operands with fp32
     accumulation, or fp32 operands on fp32 MFMA = the reference's precision) on the step's observations,
-    then gr_step on the sampled actions; 64 such steps are captured in one hipGraph and replayed.  Returns
-    (env-steps/s, per-launch us of the inference kernel, its useful TFLOP/s)."""
+    then gr_step on the sampled actions; 64 such steps are captured in one hipGraph and replayed.  actor_only:
+    the actor network alone (mean, sample, log prob; no value), the inference an env-only rollout needs.
+    Returns (env-steps/s, per-launch us of the inference kernel, its useful TFLOP/s)."""
     from generalizableracing_amd.rsl_rl import ActorCritic
     from generalizableracing_amd.rsl_rl.fused_inference import FusedPolicyInference
 
@@ -254,7 +255,7 @@ def policy_in_loop_fused(env, steps, device, precision="bf16"):
     fused = FusedPolicyInference(pol, n, device, env_id_offset=env.cfg.env_id_offset, precision=precision)
 
     def one_step(obs):
-        acts = fused.act(obs["policy"], obs["critic"])[0]
+        acts = fused.act(obs["policy"], None if actor_only else obs["critic"])[0]
         return env.step(acts)[0]
 
     obs = env.observe()
@@ -286,15 +287,17 @@ def policy_in_loop_fused(env, steps, device, precision="bf16"):
     # the inference kernel alone (events on the current stream, 64 back-to-back launches)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     x = obs["policy"].clone()
+    xc = None if actor_only else x
     for _ in range(4):
-        fused.act(x, x)
+        fused.act(x, xc)
     e0.record()
     for _ in range(64):
-        fused.act(x, x)
+        fused.act(x, xc)
     e1.record()
     e1.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / 64
-    flops = 2 * n * 2 * (16 * 256 + 256 * 256 + 256 * 4)  # actor + critic (critic out 1, padded rows free)
+    # useful flops: actor (+ critic; its 1-row output counted as 4, the padded rows are free)
+    flops = 2 * n * (1 if actor_only else 2) * (16 * 256 + 256 * 256 + 256 * 4)
     return rate, us, flops / (us * 1e-6) / 1e12
 
 
@@ -435,11 +438,22 @@ def main():
     extra = {"steady_state_env_steps_per_s_per_gpu": steady,
              "steady_state_note": "median of 3 timed runs of 1024 steps (16 replays of the 64-step graph), one rank"}
     if not a.no_extras:
+        rate_e, us_e, tfs_e = policy_in_loop_fused(env, 1024, device, precision="fp32", actor_only=True)
         extra["env_only_fp32"] = {
+            "env_steps_per_s": rate_e,
+            "launch": "hipgraph (64 x [fused fp32 actor inference 16-256-256-4 + Gaussian sample + gr_step])",
+            "inference_kernel": "gr::policy_f32_kernel<256> actor only (MFMA 16x16x4 f32), every CU",
+            "inference_kernel_us": us_e, "inference_TFLOPs": tfs_e,
+            "inference_roofline": {"bound": "mfma", "achieved": tfs_e, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                                   "frac": tfs_e / FP32_MFMA_PEAK_TFS},
+            "note": "SURVEY §8d env-only rate: gr_step + policy inference at the reference's fp32 (operands and "
+                    "accumulation fp32; mean within 1e-5 of the module)"}
+        progress("env_only_fp32")
+        extra["env_only_fp32_torch"] = {
             "env_steps_per_s": policy_in_loop_graphed(env, 1024, device),
             "launch": "hipgraph (64 x [PyTorch fp32 actor MLP 16-256-256-4 + Gaussian sample + gr_step])",
-            "note": "SURVEY §8d env-only rate: gr_step + policy inference at the reference's fp32"}
-        progress("env_only_fp32")
+            "note": "the same rate with the PyTorch (hipBLASLt) actor"}
+        progress("env_only_fp32_torch")
         extra["policy_in_loop_env_steps_per_s"] = policy_in_loop(env, 256, device)
         progress("policy_in_loop")
         rate, us_pol, tfs = policy_in_loop_fused(env, 512, device)

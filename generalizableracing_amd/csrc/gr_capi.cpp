@@ -634,7 +634,9 @@ int gr_policy_forward(const gr_policy_args* a, void* stream) {
       (a->activation != GR_POLICY_ACT_LRELU && a->activation != GR_POLICY_ACT_ELU) ||
       (a->precision != GR_POLICY_BF16 && a->precision != GR_POLICY_FP32))
     return GR_ERR_ARG;
-  for (int k = 0; k < 2; ++k) {
+  // net[1].obs == NULL: actor only (rollouts without a value estimate: play, the env-only rate)
+  const int nets = a->net[1].obs ? 2 : 1;
+  for (int k = 0; k < nets; ++k) {
     const gr_policy_net& n = a->net[k];
     if (!n.obs || !n.w1 || !n.b1 || !n.w2 || !n.b2 || !n.w3 || !n.b3 || !n.out || n.num_obs <= 0 || n.num_obs > 32 ||
         n.num_obs % 4 != 0 || !aligned16(n.obs) ||

@@ -1065,26 +1065,20 @@ enum { O_P = 0, O_Q = 1, O_MASK = 2, GR_OF4 = 3 };
 DEV void merge_handover(const float4* xch, int t, bool reset, Env& e) {
   // (field-wise selects: branch-dependent writes to different fields made the compiler
   // address the struct through scratch memory)
-  float4 p4 = xch[X_PA * GR_BLOCK + t], q4 = xch[X_Q * GR_BLOCK + t], v4 = xch[X_VD * GR_BLOCK + t];
-  int lvl = e.lvl, gate = e.gate;
-  float nl = e.nl;
-  if (reset) {
-    const float4* xr = xch + GR_XF4 * GR_BLOCK;
-    const float4 r0 = xr[R_POSQ * GR_BLOCK + t], r1 = xr[R_QV * GR_BLOCK + t], r2 = xr[R_VW * GR_BLOCK + t];
-    const float4 r3 = xr[R_W * GR_BLOCK + t], r4 = xr[R_RST0 * GR_BLOCK + t];
-    p4 = make_float4(r0.x, r0.y, r0.z, 0.0f);
-    q4 = make_float4(r0.w, r1.x, r1.y, r1.z);
-    v4 = make_float4(r1.w, r2.x, r2.y, 0.0f);
-    lvl = __float_as_int(r3.y);
-    gate = __float_as_int(r3.z);
-    nl = r4.y;
-  }
-  e.p[0] = p4.x; e.p[1] = p4.y; e.p[2] = p4.z;
-  e.q[0] = q4.x; e.q[1] = q4.y; e.q[2] = q4.z; e.q[3] = q4.w;
-  e.v[0] = v4.x; e.v[1] = v4.y; e.v[2] = v4.z;
-  e.lvl = lvl;
-  e.gate = gate;
-  e.nl = nl;
+  // every row is read unconditionally and merged by value selects: a conditional read let the compiler
+  // select between the LDS row and the Env field's address, which put the Env's integers in scratch and
+  // read them through a flat pointer on the post-handover path
+  const float4 p4 = xch[X_PA * GR_BLOCK + t], q4 = xch[X_Q * GR_BLOCK + t], v4 = xch[X_VD * GR_BLOCK + t];
+  const float4* xr = xch + GR_XF4 * GR_BLOCK;
+  const float4 r0 = xr[R_POSQ * GR_BLOCK + t], r1 = xr[R_QV * GR_BLOCK + t], r2 = xr[R_VW * GR_BLOCK + t];
+  const float4 r3 = xr[R_W * GR_BLOCK + t], r4 = xr[R_RST0 * GR_BLOCK + t];
+  e.p[0] = reset ? r0.x : p4.x; e.p[1] = reset ? r0.y : p4.y; e.p[2] = reset ? r0.z : p4.z;
+  e.q[0] = reset ? r0.w : q4.x; e.q[1] = reset ? r1.x : q4.y; e.q[2] = reset ? r1.y : q4.z;
+  e.q[3] = reset ? r1.z : q4.w;
+  e.v[0] = reset ? r1.w : v4.x; e.v[1] = reset ? r2.x : v4.y; e.v[2] = reset ? r2.y : v4.z;
+  e.lvl = reset ? __float_as_int(r3.y) : e.lvl;
+  e.gate = reset ? __float_as_int(r3.z) : e.gate;
+  e.nl = reset ? r4.y : e.nl;
   e.acc = reset ? 0 : e.acc;
   e.ep = reset ? 0 : e.ep + 1;
   e.epoch = reset ? e.epoch + 1 : e.epoch;

@@ -394,8 +394,9 @@ hipError_t read_policy_stamps(unsigned long long* host, int n) {
 hipError_t launch_policy(const gr_policy_args& a, hipStream_t s) {
   const int envs_per_block = POL_WAVES * POL_ENVS_PER_WAVE;
   const int tiles = (a.num_envs + envs_per_block - 1) / envs_per_block;
-  // one workgroup per CU (the weights fill its LDS), half of the CUs per network
-  const dim3 grid(tiles < POL_BLOCKS_PER_NET ? tiles : POL_BLOCKS_PER_NET, 2);
+  // one workgroup per CU (the weights fill its LDS), half of the CUs per network (all of them, actor only)
+  const int nets = a.net[1].obs ? 2 : 1, per_net = POL_BLOCKS_PER_NET * (3 - nets);
+  const dim3 grid(tiles < per_net ? tiles : per_net, nets);
   const size_t lds =
       ((size_t)a.hidden / 16 + (size_t)a.hidden * a.hidden / 512 + (size_t)a.hidden / 32) * 64 * 16 + 2 * 4 * (size_t)a.hidden;
   const bool elu = a.activation == GR_POLICY_ACT_ELU;

@@ -261,14 +261,16 @@ static hipError_t launch_policy_f32_t(const gr_policy_args& a, dim3 grid, hipStr
 template <int H, int ACT>
 static hipError_t launch_policy_f32_h(const gr_policy_args& a, dim3 grid, hipStream_t s) {
   // the layer-1 k depth: one 16-input group when both networks read <= 16 observations, else two
-  const int d = a.net[0].num_obs > a.net[1].num_obs ? a.net[0].num_obs : a.net[1].num_obs;
+  const int d1 = a.net[1].obs ? a.net[1].num_obs : 0;
+  const int d = a.net[0].num_obs > d1 ? a.net[0].num_obs : d1;
   return d <= 16 ? launch_policy_f32_t<H, ACT, 1>(a, grid, s) : launch_policy_f32_t<H, ACT, 2>(a, grid, s);
 }
 
 hipError_t launch_policy_f32(const gr_policy_args& a, hipStream_t s) {
   const int envs_per_block = 16 * PF_COLS;
   const int tiles = (a.num_envs + envs_per_block - 1) / envs_per_block;
-  const dim3 grid(tiles < PF_BLOCKS_PER_NET ? tiles : PF_BLOCKS_PER_NET, 2);
+  const int nets = a.net[1].obs ? 2 : 1, per_net = PF_BLOCKS_PER_NET * (3 - nets);  // actor only: every CU
+  const dim3 grid(tiles < per_net ? tiles : per_net, nets);
   const bool elu = a.activation == GR_POLICY_ACT_ELU;
   if (a.hidden == 256)
     return elu ? launch_policy_f32_h<256, GR_POLICY_ACT_ELU>(a, grid, s) : launch_policy_f32_h<256, GR_POLICY_ACT_LRELU>(a, grid, s);

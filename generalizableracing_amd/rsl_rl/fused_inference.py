@@ -185,20 +185,23 @@ class FusedPolicyInference:
         nt.num_obs, nt.num_out = num_obs, num_out
         return nt
 
-    def act(self, obs: torch.Tensor, critic_obs: torch.Tensor):
+    def act(self, obs: torch.Tensor, critic_obs: torch.Tensor | None):
         """-> (actions, values, log_prob, action_mean, action_sigma) for all envs (views of persistent
         buffers, overwritten by the next call).  Weights changed in place since the last packing (a PPO
-        update, a checkpoint load) are repacked first; inside a graph capture they must not change."""
+        update, a checkpoint load) are repacked first; inside a graph capture they must not change.
+        critic_obs None: the actor only (sampled actions, mean, log prob; `values` is not written)."""
         n = self.num_envs
         if self._param_version() != self._version:
             self.refresh()
-        for x, d in ((obs, self.num_obs[0]), (critic_obs, self.num_obs[1])):
+        checks = [(obs, self.num_obs[0])] + ([] if critic_obs is None else [(critic_obs, self.num_obs[1])])
+        for x, d in checks:
             if x.shape != (n, d) or x.dtype != torch.float32 or x.device != self.device or not x.is_contiguous():
                 raise ValueError(f"expected contiguous fp32 [{n}, {d}] observations on {self.device}, got "
                                  f"{tuple(x.shape)} {x.dtype} {x.device}")
         a = _abi.GrPolicyArgs()
         a.net[0] = self._net("actor", obs, self.action_mean, self.num_obs[0], self.num_actions)
-        a.net[1] = self._net("critic", critic_obs, self.values, self.num_obs[1], 1)
+        if critic_obs is not None:
+            a.net[1] = self._net("critic", critic_obs, self.values, self.num_obs[1], 1)
         a.std, a.actions, a.log_prob = self.std.data_ptr(), self.actions.data_ptr(), self.log_prob.data_ptr()
         a.counters, a.counter_index = self.counters.data_ptr(), self._calls % 2
         a.num_envs, a.hidden, a.activation, a.env_id_offset = n, self.hidden, self.activation, self.env_id_offset

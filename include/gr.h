@@ -359,7 +359,8 @@ typedef struct gr_policy_net {
   int32_t num_obs, num_out, reserved[2];
 } gr_policy_net;
 typedef struct gr_policy_args {
-  gr_policy_net net[2]; /* 0: actor (num_out = num_actions <= 4), 1: critic (num_out = 1) */
+  gr_policy_net net[2]; /* 0: actor (num_out = num_actions <= 4), 1: critic (num_out = 1); net[1].obs == NULL:
+                           actor only (no value; the actor's workgroups take every CU) */
   const float* std;     /* [num_actions] the policy's std */
   float* actions;       /* [num_envs][num_actions] sampled actions */
   float* log_prob;      /* [num_envs] */

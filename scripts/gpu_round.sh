@@ -15,4 +15,5 @@ timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > $OUT/bench_driver.j
 bash scripts/gpu_profile.sh ${TAG}_g 65536 0 || exit 12
 bash scripts/gpu_profile.sh ${TAG}_o 65536 1 || exit 13
 bash scripts/prof_policy.sh ${TAG}_p || exit 14
+bash scripts/prof_policy.sh ${TAG}_p32 --precision fp32 || exit 15
 echo done > $OUT/done

@@ -141,3 +141,23 @@ def test_ppo_rollout_fp32_old_log_prob_matches_update():
     kl = torch.sum(torch.log(sd / sd) + (sd**2 + (mu_st - mu) ** 2) / (2.0 * sd**2) - 0.5, dim=-1)
     assert float(kl.abs().max()) < 1e-9
     env.close()
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_actor_only_matches_both_networks(precision):
+    """critic_obs None: the actor alone (every CU), the same bits as the actor half of a two-network call;
+    the value buffer is left as it was."""
+    torch.manual_seed(4)
+    n = 20000
+    pol = ActorCritic(16, 16, 4, [256, 256], [256, 256], "lrelu").to(DEV)
+    both = FusedPolicyInference(pol, n, DEV, seed=9, precision=precision)
+    solo = FusedPolicyInference(pol, n, DEV, seed=9, precision=precision)
+    obs = torch.randn(n, 16, device=DEV)
+    both.act(obs, obs)
+    solo.values.fill_(123.0)
+    solo.act(obs, None)
+    torch.cuda.synchronize()
+    assert torch.equal(both.action_mean, solo.action_mean)
+    assert torch.equal(both.actions, solo.actions)
+    assert torch.equal(both.log_prob, solo.log_prob)
+    assert bool((solo.values == 123.0).all())
