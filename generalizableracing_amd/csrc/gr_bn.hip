@@ -1,0 +1,238 @@
+// gr_bn.hip — training-mode BatchNorm fused with its activation, on channels-last rows [M][C] (gfx950).
+//
+// The vision stem (VisionActorCritic, standalone/rsl_rl/ext/modules/vision_actor_critic.py:43-144, here
+// rsl_rl/vision_actor_critic.py) runs Conv -> BatchNorm2d -> LeakyReLU three times on [batch*H*W, C]
+// matrices with millions of rows and C = 16 / 32 / 64.  PyTorch spends 13 full passes over each such
+// matrix per forward + backward (statistics, transform, activation, activation backward, BN backward
+// reduce and element passes) and saves both the BN output and the activation output.  Here:
+//   forward:  one statistics pass (read x) + one apply pass (read x, write y = act(bn(x)));
+//   backward: one reduce pass (read gy, x) + one element pass (read gy, x, write gx);
+// the activation's derivative is recomputed from x, so only x is kept for the backward.
+//
+// Layout: a thread owns one float4 (4 channels) of a row per item and walks the rows with a stride that
+// is a multiple of C / 4, so its channel group is fixed (C / 4 must be a power of two dividing 256: C in
+// {4, 8, 16, 32, 64}).  Per-channel sums: fp32 per thread over its items, shifted by the channel's value in
+// row 0 (no cancellation in E[x^2] - E[x]^2), then fp64 across the block and across blocks in a fixed
+// order — deterministic, no atomics, graph-capturable.
+#include <hip/hip_runtime.h>
+
+#include "../../include/gr.h"
+#include "gr_kernels.h"
+
+namespace gr {
+
+constexpr int BN_THREADS = 256;
+constexpr int BN_MAX_BLOCKS = 1024;
+
+__host__ __device__ inline int bn_blocks(long long m, int c) {
+  const long long q = m * (c / 4);
+  long long b = (q + BN_THREADS * 8 - 1) / (BN_THREADS * 8);  // ~8 float4 per thread at least
+  if (b < 1) b = 1;
+  return (int)(b < BN_MAX_BLOCKS ? b : BN_MAX_BLOCKS);
+}
+
+template <int ACT>
+__device__ __forceinline__ float bn_act(float z, float slope) {
+  if constexpr (ACT == GR_POLICY_ACT_ELU) return z > 0.0f ? z : expm1f(z);
+  return z > 0.0f ? z : z * slope;
+}
+// d act / d z, from z (torch's leaky_relu_backward tests the input; ELU's uses the output y = expm1(z))
+template <int ACT>
+__device__ __forceinline__ float bn_dact(float z, float slope) {
+  if constexpr (ACT == GR_POLICY_ACT_ELU) return z > 0.0f ? 1.0f : expm1f(z) + 1.0f;
+  return z > 0.0f ? 1.0f : slope;
+}
+
+__device__ __forceinline__ float4 ld4f(const float* p, long long q) { return reinterpret_cast<const float4*>(p)[q]; }
+__device__ __forceinline__ float comp(const float4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
+
+// block reduction of 8 per-thread sums (two quantities x 4 channels) over the threads of each channel group,
+// in fp64, then one row of partials per block: part[block][2][C]
+__device__ void bn_block_partials(const float a[8], int c, double* part) {
+  __shared__ double red[BN_THREADS * 8];
+  const int t = threadIdx.x, c4 = c / 4;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[k * BN_THREADS + t] = (double)a[k];
+  __syncthreads();
+  // thread (quantity s, channel ch) sums the threads t' with t' % c4 == ch / 4 in index order
+  for (int j = t; j < 2 * c; j += BN_THREADS) {
+    const int s = j / c, ch = j % c, g = ch / 4, k = ch % 4;
+    double acc = 0.0;
+    for (int u = g; u < BN_THREADS; u += c4) acc += red[(s * 4 + k) * BN_THREADS + u];
+    part[(size_t)blockIdx.x * 2 * c + j] = acc;
+  }
+}
+
+// ---- forward: shifted channel sums of x
+__global__ __launch_bounds__(BN_THREADS) void bn_stats_partial(const float* __restrict__ x, long long m, int c,
+                                                               double* __restrict__ part) {
+  const int c4 = c / 4;
+  const long long q0 = (long long)blockIdx.x * BN_THREADS + threadIdx.x, stride = (long long)gridDim.x * BN_THREADS;
+  const long long nq = m * c4;
+  const float4 sh = ld4f(x, threadIdx.x & (c4 - 1));  // row 0 of this thread's channel group
+  float a[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  for (long long q = q0; q < nq; q += stride) {
+    const float4 v = ld4f(x, q);
+    const float d[4] = {v.x - sh.x, v.y - sh.y, v.z - sh.z, v.w - sh.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      a[k] += d[k];
+      a[4 + k] += d[k] * d[k];
+    }
+  }
+  bn_block_partials(a, c, part);
+}
+
+// the 2 c channel sums over the blocks' partials, in a fixed order: thread (pair j, lane k) of the 256 sums
+// the partials b = k (mod T), T = 256 / (2 c) threads per pair, then lane 0 of each pair adds the T lane sums
+// in order (out[j], j = s c + ch)
+__device__ void bn_final_sums(const double* __restrict__ part, int c, int blocks, double* out) {
+  __shared__ double red[BN_THREADS];
+  const int pairs = 2 * c, T = BN_THREADS / pairs, j = threadIdx.x / T, k = threadIdx.x % T;
+  double acc = 0.0;
+  if (j < pairs)
+    for (int b = k; b < blocks; b += T) acc += part[(size_t)b * pairs + j];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (j < pairs && k == 0) {
+    double s = 0.0;
+    for (int u = 0; u < T; ++u) s += red[j * T + u];
+    out[j] = s;
+  }
+  __syncthreads();
+}
+
+// stats[0][c] mean, [1][c] invstd = 1 / sqrt(var + eps), [2][c] biased var, [3][c] unbiased var
+__global__ __launch_bounds__(BN_THREADS) void bn_stats_final(const float* __restrict__ x, long long m, int c, int blocks,
+                                                             float eps, const double* __restrict__ part,
+                                                             float* __restrict__ stats) {
+  __shared__ double sums[128];
+  bn_final_sums(part, c, blocks, sums);
+  const int ch = threadIdx.x;
+  if (ch >= c) return;
+  const double md = (double)m, d1 = sums[ch] / md;
+  double var = sums[c + ch] / md - d1 * d1;
+  var = var > 0.0 ? var : 0.0;
+  const float varf = (float)var;
+  stats[ch] = (float)((double)x[ch] + d1);
+  stats[c + ch] = 1.0f / sqrtf(varf + eps);
+  stats[2 * c + ch] = varf;
+  stats[3 * c + ch] = m > 1 ? (float)(var * md / (md - 1.0)) : varf;
+}
+
+// ---- forward: y = act((x - mean) * invstd * w + b)
+template <int ACT>
+__global__ __launch_bounds__(BN_THREADS) void bn_apply(const float* __restrict__ x, long long m, int c,
+                                                       const float* __restrict__ w, const float* __restrict__ b,
+                                                       const float* __restrict__ stats, float slope, float* __restrict__ y) {
+  const int c4 = c / 4, g = threadIdx.x & (c4 - 1);
+  const float4 mu = ld4f(stats, g), is = ld4f(stats + c, g), wv = ld4f(w, g), bv = ld4f(b, g);
+  const long long nq = m * c4, stride = (long long)gridDim.x * BN_THREADS;
+  for (long long q = (long long)blockIdx.x * BN_THREADS + threadIdx.x; q < nq; q += stride) {
+    const float4 v = ld4f(x, q);
+    float4 o;
+    o.x = bn_act<ACT>((v.x - mu.x) * is.x * wv.x + bv.x, slope);
+    o.y = bn_act<ACT>((v.y - mu.y) * is.y * wv.y + bv.y, slope);
+    o.z = bn_act<ACT>((v.z - mu.z) * is.z * wv.z + bv.z, slope);
+    o.w = bn_act<ACT>((v.w - mu.w) * is.w * wv.w + bv.w, slope);
+    reinterpret_cast<float4*>(y)[q] = o;
+  }
+}
+
+// ---- backward: per channel sum(gz), sum(gz * xhat), gz = gy * act'(z)
+template <int ACT>
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial(const float* __restrict__ x, const float* __restrict__ gy,
+                                                             long long m, int c, const float* __restrict__ w,
+                                                             const float* __restrict__ b, const float* __restrict__ stats,
+                                                             float slope, double* __restrict__ part) {
+  const int c4 = c / 4, g = threadIdx.x & (c4 - 1);
+  const float4 mu = ld4f(stats, g), is = ld4f(stats + c, g), wv = ld4f(w, g), bv = ld4f(b, g);
+  const long long nq = m * c4, stride = (long long)gridDim.x * BN_THREADS;
+  float a[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  for (long long q = (long long)blockIdx.x * BN_THREADS + threadIdx.x; q < nq; q += stride) {
+    const float4 v = ld4f(x, q), dy = ld4f(gy, q);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float xh = (comp(v, k) - comp(mu, k)) * comp(is, k);
+      const float gz = comp(dy, k) * bn_dact<ACT>(xh * comp(wv, k) + comp(bv, k), slope);
+      a[k] += gz;
+      a[4 + k] += gz * xh;
+    }
+  }
+  bn_block_partials(a, c, part);
+}
+
+// sums[0][c] = sum gz (= grad bias), sums[1][c] = sum gz * xhat (= grad weight)
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_final(int c, int blocks, const double* __restrict__ part,
+                                                           float* __restrict__ gw, float* __restrict__ gb,
+                                                           float* __restrict__ sums) {
+  __shared__ double tot[128];
+  bn_final_sums(part, c, blocks, tot);
+  const int ch = threadIdx.x;
+  if (ch >= c) return;
+  sums[ch] = (float)tot[ch];
+  sums[c + ch] = (float)tot[c + ch];
+  gb[ch] = (float)tot[ch];
+  gw[ch] = (float)tot[c + ch];
+}
+
+// gx = (gz - sum(gz) / M - xhat * sum(gz xhat) / M) * invstd * w
+template <int ACT>
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_elemt(const float* __restrict__ x, const float* __restrict__ gy,
+                                                           long long m, int c, const float* __restrict__ w,
+                                                           const float* __restrict__ b, const float* __restrict__ stats,
+                                                           const float* __restrict__ sums, float slope,
+                                                           float* __restrict__ gx) {
+  const int c4 = c / 4, g = threadIdx.x & (c4 - 1);
+  const float4 mu = ld4f(stats, g), is = ld4f(stats + c, g), wv = ld4f(w, g), bv = ld4f(b, g);
+  const float inv_m = 1.0f / (float)m;
+  const float4 s1 = ld4f(sums, g), s2 = ld4f(sums + c, g);
+  const float mg[4] = {s1.x * inv_m, s1.y * inv_m, s1.z * inv_m, s1.w * inv_m};
+  const float mgx[4] = {s2.x * inv_m, s2.y * inv_m, s2.z * inv_m, s2.w * inv_m};
+  const long long nq = m * c4, stride = (long long)gridDim.x * BN_THREADS;
+  for (long long q = (long long)blockIdx.x * BN_THREADS + threadIdx.x; q < nq; q += stride) {
+    const float4 v = ld4f(x, q), dy = ld4f(gy, q);
+    float o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float xh = (comp(v, k) - comp(mu, k)) * comp(is, k);
+      const float gz = comp(dy, k) * bn_dact<ACT>(xh * comp(wv, k) + comp(bv, k), slope);
+      o[k] = (gz - mg[k] - xh * mgx[k]) * (comp(is, k) * comp(wv, k));
+    }
+    reinterpret_cast<float4*>(gx)[q] = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+int bn_scratch_doubles(long long m, int c) { return bn_blocks(m, c) * 2 * c + 2 * c; }
+
+hipError_t launch_bn_forward(const float* x, long long m, int c, const float* w, const float* b, float eps, int act,
+                             float slope, float* y, float* stats, double* part, hipStream_t s) {
+  const int nb = bn_blocks(m, c);
+  hipLaunchKernelGGL(bn_stats_partial, dim3(nb), dim3(BN_THREADS), 0, s, x, m, c, part);
+  hipLaunchKernelGGL(bn_stats_final, dim3(1), dim3(BN_THREADS), 0, s, x, m, c, nb, eps, part, stats);
+  if (act == GR_POLICY_ACT_ELU)
+    hipLaunchKernelGGL(bn_apply<GR_POLICY_ACT_ELU>, dim3(nb), dim3(BN_THREADS), 0, s, x, m, c, w, b, stats, slope, y);
+  else
+    hipLaunchKernelGGL(bn_apply<GR_POLICY_ACT_LRELU>, dim3(nb), dim3(BN_THREADS), 0, s, x, m, c, w, b, stats, slope, y);
+  return hipGetLastError();
+}
+
+hipError_t launch_bn_backward(const float* x, const float* gy, long long m, int c, const float* w, const float* b,
+                              const float* stats, int act, float slope, float* gx, float* gw, float* gb, double* part,
+                              hipStream_t s) {
+  const int nb = bn_blocks(m, c);
+  // the two channel sums live after the partials in the same workspace (as floats)
+  float* sums = reinterpret_cast<float*>(part + (size_t)nb * 2 * c);
+  if (act == GR_POLICY_ACT_ELU)
+    hipLaunchKernelGGL(bn_bwd_partial<GR_POLICY_ACT_ELU>, dim3(nb), dim3(BN_THREADS), 0, s, x, gy, m, c, w, b, stats, slope, part);
+  else
+    hipLaunchKernelGGL(bn_bwd_partial<GR_POLICY_ACT_LRELU>, dim3(nb), dim3(BN_THREADS), 0, s, x, gy, m, c, w, b, stats, slope, part);
+  hipLaunchKernelGGL(bn_bwd_final, dim3(1), dim3(BN_THREADS), 0, s, c, nb, part, gw, gb, sums);
+  if (act == GR_POLICY_ACT_ELU)
+    hipLaunchKernelGGL(bn_bwd_elemt<GR_POLICY_ACT_ELU>, dim3(nb), dim3(BN_THREADS), 0, s, x, gy, m, c, w, b, stats, sums, slope, gx);
+  else
+    hipLaunchKernelGGL(bn_bwd_elemt<GR_POLICY_ACT_LRELU>, dim3(nb), dim3(BN_THREADS), 0, s, x, gy, m, c, w, b, stats, sums, slope, gx);
+  return hipGetLastError();
+}
+
+}  // namespace gr

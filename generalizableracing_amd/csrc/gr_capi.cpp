@@ -651,6 +651,33 @@ int gr_policy_forward(const gr_policy_args* a, void* stream) {
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
+static bool bn_shape_ok(int64_t m, int32_t c) { return m >= 1 && (c == 4 || c == 8 || c == 16 || c == 32 || c == 64); }
+
+int64_t gr_bn_scratch_doubles(int64_t m, int32_t c) {
+  return bn_shape_ok(m, c) ? (int64_t)gr::bn_scratch_doubles(m, c) : (int64_t)GR_ERR_ARG;
+}
+
+int gr_bn_act_forward(const float* x, int64_t m, int32_t c, const float* w, const float* b, float eps, int32_t act,
+                      float slope, float* y, float* stats, double* part, void* stream) {
+  if (!bn_shape_ok(m, c) || !x || !w || !b || !y || !stats || !part || !aligned16(x) || !aligned16(y) ||
+      !aligned16(w) || !aligned16(b) || !aligned16(stats) || (act != GR_POLICY_ACT_LRELU && act != GR_POLICY_ACT_ELU))
+    return GR_ERR_ARG;
+  const hipError_t e = gr::launch_bn_forward(x, m, c, w, b, eps, act, slope, y, stats, part, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
+int gr_bn_act_backward(const float* x, const float* gy, int64_t m, int32_t c, const float* w, const float* b,
+                       const float* stats, int32_t act, float slope, float* gx, float* gw, float* gb, double* part,
+                       void* stream) {
+  if (!bn_shape_ok(m, c) || !x || !gy || !w || !b || !stats || !gx || !gw || !gb || !part || !aligned16(x) ||
+      !aligned16(gy) || !aligned16(gx) || !aligned16(w) || !aligned16(b) || !aligned16(stats) ||
+      (act != GR_POLICY_ACT_LRELU && act != GR_POLICY_ACT_ELU))
+    return GR_ERR_ARG;
+  const hipError_t e =
+      gr::launch_bn_backward(x, gy, m, c, w, b, stats, act, slope, gx, gw, gb, part, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
 int gr_column_sum_partials(int64_t rows) { return rows < 0 ? GR_ERR_ARG : gr::column_sum_blocks(rows); }
 
 int gr_column_sum(const void* x, int dtype, int64_t rows, int32_t cols, float* partial, float* out, void* stream) {

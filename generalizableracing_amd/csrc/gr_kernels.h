@@ -96,6 +96,12 @@ struct CamArgs {
 hipError_t launch_camera(const CamArgs& a, hipStream_t s);
 hipError_t launch_policy(const gr_policy_args& a, hipStream_t s);  // gr_policy.hip
 hipError_t launch_policy_f32(const gr_policy_args& a, hipStream_t s);  // gr_policy_f32.hip
+int bn_scratch_doubles(long long m, int c);                                                // gr_bn.hip
+hipError_t launch_bn_forward(const float* x, long long m, int c, const float* w, const float* b, float eps, int act,
+                             float slope, float* y, float* stats, double* part, hipStream_t s);
+hipError_t launch_bn_backward(const float* x, const float* gy, long long m, int c, const float* w, const float* b,
+                              const float* stats, int act, float slope, float* gx, float* gw, float* gb, double* part,
+                              hipStream_t s);
 int column_sum_blocks(long long m);                                                                       // gr_update.hip
 hipError_t launch_column_sum(const void* x, int dtype, long long m, int n, float* part, float* out, hipStream_t s);
 // obstacle slots per camera wave (the first GR_CAM_OBST_SLOTS obstacles in view; any further ones

@@ -24,6 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .actor_critic import ActorCritic, resolve_nn_activation
+from .fused_bn import batch_norm_act, fused_applicable
 
 
 def _conv_out(n: int, k: int, s: int) -> int:
@@ -68,6 +69,9 @@ def _gemm(x, w):
 
 class VisionActorCritic(ActorCritic):
     is_recurrent = False
+    # training-mode BatchNorm + activation of the stem as one HIP op on the GPU (rsl_rl/fused_bn.py); False:
+    # torch's batch_norm and activation ops (tests compare the two)
+    fused_bn = True
 
     def __init__(self, num_actor_obs: int, num_critic_obs: int, num_actions: int, img_res=(72, 96),
                  dim_hidden_input: int = 192, actor_hidden_dims=(256, 256, 256), critic_hidden_dims=(256, 256, 256),
@@ -119,6 +123,14 @@ class VisionActorCritic(ActorCritic):
                             bn.running_var if not bn.training or bn.track_running_stats else None,
                             bn.weight, bn.bias, use_batch, momentum, bn.eps)
 
+    def _bn_act(self, bn: nn.BatchNorm2d, act: nn.Module, x: torch.Tensor) -> torch.Tensor:
+        """act(bn(x)) on rows [M, C]: the fused HIP op in training mode on the GPU, else torch's ops."""
+        if self.fused_bn and fused_applicable(bn, act, x):
+            if bn.track_running_stats and bn.num_batches_tracked is not None:
+                bn.num_batches_tracked.add_(1)
+            return batch_norm_act(bn, act, x)
+        return act(self._bn(bn, x))
+
     def _patch_index(self, device):
         """Pixel indices of conv1's patches, rows ordered so that every later layer's input is a VIEW of
         the previous layer's output: conv1 rows feeding conv2 come grouped as conv2's 3x3 patches,
@@ -152,11 +164,11 @@ class VisionActorCritic(ActorCritic):
         x = flat.index_select(1, idx).view(B * n1, 9)
         if n1_left:
             x = torch.cat([x, flat.index_select(1, idx_left).view(B * n1_left, 9)])
-        y = act(self._bn(bn1, _gemm(x, conv1.weight.reshape(16, 9))))
+        y = self._bn_act(bn1, act, _gemm(x, conv1.weight.reshape(16, 9)))
         x = y[: B * n1].view(B * n2, 144)  # conv2's 3x3 patches (i, j, c): a view
-        y = act(self._bn(bn2, _gemm(x, conv2.weight.permute(0, 2, 3, 1).reshape(32, 144))))
+        y = self._bn_act(bn2, act, _gemm(x, conv2.weight.permute(0, 2, 3, 1).reshape(32, 144)))
         x = y.view(B, n2, 32)[:, :n3].reshape(B * h3 * w3, 128)  # conv3's 2x2 patches: a view at 72x96
-        y = act(self._bn(bn3, _gemm(x, conv3.weight.permute(0, 2, 3, 1).reshape(64, 128)))).view(B, h3 * w3 * 64)
+        y = self._bn_act(bn3, act, _gemm(x, conv3.weight.permute(0, 2, 3, 1).reshape(64, 128))).view(B, h3 * w3 * 64)
         # reference flatten is NCHW (c, h, w): permute the Linear's columns to (h, w, c) instead
         wl = lin.weight.view(-1, 64, h3, w3).permute(0, 2, 3, 1).reshape(lin.weight.shape[0], -1)
         return _gemm(y, wl) + lin.bias

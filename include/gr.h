@@ -373,6 +373,24 @@ typedef struct gr_policy_args {
 } gr_policy_args;
 int gr_policy_forward(const gr_policy_args* args, void* stream);
 
+/*
+ * Training-mode BatchNorm fused with its activation, on channels-last rows x [m][c] (fp32, 16-byte aligned,
+ * c in {4, 8, 16, 32, 64}): the Conv -> BatchNorm2d -> LeakyReLU / ELU blocks of the vision stem
+ * (standalone/rsl_rl/ext/modules/vision_actor_critic.py:43-144 as patch GEMMs, rsl_rl/vision_actor_critic.py),
+ * replacing torch's batch_norm (stats + transform) + activation passes and their backward (gr_bn.hip).
+ *   forward:  y = act((x - mean) * invstd * w + b) with the batch statistics; stats [4][c] = mean, invstd,
+ *             biased var, unbiased var (the caller updates the running statistics from them);
+ *   backward: gx, gw, gb from gy and x (the activation's derivative is recomputed).
+ * act: GR_POLICY_ACT_LRELU (negative slope `slope`) or GR_POLICY_ACT_ELU (alpha 1).  `part` is a device
+ * workspace of gr_bn_scratch_doubles(m, c) doubles.  Deterministic (fixed-order fp64 channel sums).
+ */
+int64_t gr_bn_scratch_doubles(int64_t m, int32_t c);
+int gr_bn_act_forward(const float* x, int64_t m, int32_t c, const float* w, const float* b, float eps, int32_t act,
+                      float slope, float* y, float* stats, double* part, void* stream);
+int gr_bn_act_backward(const float* x, const float* gy, int64_t m, int32_t c, const float* w, const float* b,
+                       const float* stats, int32_t act, float slope, float* gx, float* gw, float* gb, double* part,
+                       void* stream);
+
 /* Device status: the GR_STATUS_* bits the kernels of this context raised since the last clear (0: none).
  * Synchronises `stream` (the stream the steps ran on); clear != 0 resets the word.  A raised bit means the
  * outputs of some step since the last check are not trustworthy. */

@@ -41,7 +41,12 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--iters", type=int, default=2, help="training iterations (0: skip)")
     ap.add_argument("--storage-bf16", action="store_true", help="rollout storage observations in bf16")
-    args = ap.parse_args(argv)
+    ap.add_argument("--no-fused-bn", action="store_true", help="the stem's BatchNorm + activation on torch's ops")
+    print(json.dumps(run(ap.parse_args(argv))))
+
+
+def run(args):
+    """-> the measurements above as a dict (args: envs, steps, iters, storage_bf16, no_fused_bn)."""
     n = args.envs
     dev = "cuda:0"
     torch.manual_seed(0)
@@ -53,11 +58,12 @@ def main(argv=None):
         d["algorithm"]["storage_obs_dtype"] = torch.bfloat16
     runner = OnPolicyRunner(env, d, log_dir=None, device=dev)
     pol = runner.alg.policy
+    pol.fused_bn = not args.no_fused_bn
     obs, extras = env.get_observations()
     crit = extras["observations"]["critic"]
     g = torch.Generator(device=dev).manual_seed(1)
     acts = [torch.randn(n, 4, device=dev, generator=g) for _ in range(4)]
-    out = {"envs": n, "obs_dim": int(obs.shape[1]), "params": sum(p.numel() for p in pol.parameters())}
+    out = {"fused_bn": pol.fused_bn, "envs": n, "obs_dim": int(obs.shape[1]), "params": sum(p.numel() for p in pol.parameters())}
 
     for _ in range(4):
         env.step(acts[0])
@@ -90,7 +96,8 @@ def main(argv=None):
         out["last_log"] = {k: runner.last_log[k] for k in ("fps", "collection_time", "learn_time")
                            if k in runner.last_log}
         out["max_mem_GB"] = torch.cuda.max_memory_allocated() / 1e9
-    print(json.dumps(out))
+    env.close()
+    return out
 
 
 if __name__ == "__main__":

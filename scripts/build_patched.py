@@ -30,7 +30,7 @@ def build(name, patch):
     flags = ("--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt "
              "-fno-slp-vectorize")
     objs = []
-    for f in ("gr_kernels.hip", "gr_camera.hip", "gr_policy.hip", "gr_policy_f32.hip", "gr_update.hip", "gr_capi.cpp"):
+    for f in ("gr_kernels.hip", "gr_camera.hip", "gr_policy.hip", "gr_policy_f32.hip", "gr_bn.hip", "gr_update.hip", "gr_capi.cpp"):
         o = os.path.join(tmp, f + ".o")
         extra = " -fno-honor-nans" if f == "gr_policy.hip" else ""
         lang = " -x hip" if f.endswith(".cpp") else ""

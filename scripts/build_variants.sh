@@ -12,7 +12,7 @@ for spec in "$@"; do
   name=${spec%%=*}; flags=${spec#*=}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off \
     -fhip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize -fno-gpu-rdc $flags -shared \
-    -o $V/libgr_$name.so $C/gr_kernels.hip $C/gr_camera.hip $C/gr_policy.hip $C/gr_policy_f32.hip $C/gr_update.hip -x hip $C/gr_capi.cpp &
+    -o $V/libgr_$name.so $C/gr_kernels.hip $C/gr_camera.hip $C/gr_policy.hip $C/gr_policy_f32.hip $C/gr_bn.hip $C/gr_update.hip -x hip $C/gr_capi.cpp &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait $p; done

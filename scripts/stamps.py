@@ -26,7 +26,7 @@ def build():
     os.makedirs(OUT, exist_ok=True)
     cmd = (f"/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off "
            f"-fhip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize -DGR_STAMPS -shared -o {OUT}/libgr.so "
-           f"{CSRC}/gr_kernels.hip {CSRC}/gr_camera.hip {CSRC}/gr_policy.hip {CSRC}/gr_policy_f32.hip {CSRC}/gr_update.hip -x hip {CSRC}/gr_capi.cpp")
+           f"{CSRC}/gr_kernels.hip {CSRC}/gr_camera.hip {CSRC}/gr_policy.hip {CSRC}/gr_policy_f32.hip {CSRC}/gr_bn.hip {CSRC}/gr_update.hip -x hip {CSRC}/gr_capi.cpp")
     subprocess.run(cmd, shell=True, check=True)
 
 
