@@ -227,7 +227,8 @@ EXPORTS = [
     "gr_debug_read_stamps", "gr_debug_read_policy_stamps",
     "gr_camera_config_default", "gr_camera_config_size", "gr_enable_camera", "gr_bind_camera_buffers",
     "gr_camera_render", "gr_camera_bytes_per_env", "gr_policy_forward", "gr_column_sum_partials", "gr_column_sum",
-    "gr_bn_scratch_doubles", "gr_bn_act_forward", "gr_bn_act_backward",
+    "gr_bn_scratch_doubles", "gr_bn_act_forward", "gr_bn_act_backward", "gr_stem1_scratch_doubles",
+    "gr_stem1_forward", "gr_stem1_backward",
 ]
 
 _lib = None
@@ -277,6 +278,11 @@ def _declare(lib):
                                         vp]),
         "gr_bn_act_backward": (C.c_int, [vp, vp, C.c_int64, C.c_int32, vp, vp, vp, C.c_int32, C.c_float, vp, vp, vp,
                                          vp, vp]),
+        "gr_stem1_scratch_doubles": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
+        "gr_stem1_forward": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int32, vp, C.c_int32, C.c_int32, vp, C.c_int32,
+                                       vp, vp, C.c_float, C.c_int32, C.c_float, vp, vp, vp, vp]),
+        "gr_stem1_backward": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int32, vp, C.c_int32, C.c_int32, vp, C.c_int32,
+                                        vp, vp, vp, C.c_int32, C.c_float, vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name) and os.environ.get("GR_LIB_PATH"):

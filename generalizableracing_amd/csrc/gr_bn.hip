@@ -83,18 +83,29 @@ __global__ __launch_bounds__(BN_THREADS) void bn_stats_partial(const float* __re
   bn_block_partials(a, c, part);
 }
 
-// the 2 c channel sums over the blocks' partials, in a fixed order: thread (pair j, lane k) of the 256 sums
-// the partials b = k (mod T), T = 256 / (2 c) threads per pair, then lane 0 of each pair adds the T lane sums
-// in order (out[j], j = s c + ch)
-__device__ void bn_final_sums(const double* __restrict__ part, int c, int blocks, double* out) {
-  __shared__ double red[BN_THREADS];
-  const int pairs = 2 * c, T = BN_THREADS / pairs, j = threadIdx.x / T, k = threadIdx.x % T;
+// sums over the blocks' partials of `npairs` quantities (part[block][npairs]), in a fixed order: thread
+// (pair j, lane k) of the BN_FINAL_THREADS sums the partials b = k (mod T), T = BN_FINAL_THREADS / npairs
+// threads per pair, eight loads in flight at a time (the partials come from L2 / HBM: one load at a time left a
+// 1 024-block reduction latency-bound at ~70 us), then lane 0 of each pair adds the T lane sums in order
+constexpr int BN_FINAL_THREADS = 1024;
+__device__ void bn_final_sums(const double* __restrict__ part, int npairs, int blocks, double* out) {
+  __shared__ double red[BN_FINAL_THREADS];
+  const int T = BN_FINAL_THREADS / npairs, j = threadIdx.x / T, k = threadIdx.x % T;
   double acc = 0.0;
-  if (j < pairs)
-    for (int b = k; b < blocks; b += T) acc += part[(size_t)b * pairs + j];
+  if (j < npairs) {
+    int b = k;
+    for (; b + 7 * T < blocks; b += 8 * T) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(b + u * T) * npairs + j];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; b < blocks; b += T) acc += part[(size_t)b * npairs + j];
+  }
   red[threadIdx.x] = acc;
   __syncthreads();
-  if (j < pairs && k == 0) {
+  if (j < npairs && k == 0) {
     double s = 0.0;
     for (int u = 0; u < T; ++u) s += red[j * T + u];
     out[j] = s;
@@ -103,18 +114,19 @@ __device__ void bn_final_sums(const double* __restrict__ part, int c, int blocks
 }
 
 // stats[0][c] mean, [1][c] invstd = 1 / sqrt(var + eps), [2][c] biased var, [3][c] unbiased var
-__global__ __launch_bounds__(BN_THREADS) void bn_stats_final(const float* __restrict__ x, long long m, int c, int blocks,
+// shift[c]: the per-channel shift of the partial sums (row 0 of x)
+__global__ __launch_bounds__(BN_FINAL_THREADS) void bn_stats_final(const float* __restrict__ shift, long long m, int c, int blocks,
                                                              float eps, const double* __restrict__ part,
                                                              float* __restrict__ stats) {
   __shared__ double sums[128];
-  bn_final_sums(part, c, blocks, sums);
+  bn_final_sums(part, 2 * c, blocks, sums);
   const int ch = threadIdx.x;
   if (ch >= c) return;
   const double md = (double)m, d1 = sums[ch] / md;
   double var = sums[c + ch] / md - d1 * d1;
   var = var > 0.0 ? var : 0.0;
   const float varf = (float)var;
-  stats[ch] = (float)((double)x[ch] + d1);
+  stats[ch] = (float)((double)shift[ch] + d1);
   stats[c + ch] = 1.0f / sqrtf(varf + eps);
   stats[2 * c + ch] = varf;
   stats[3 * c + ch] = m > 1 ? (float)(var * md / (md - 1.0)) : varf;
@@ -163,11 +175,11 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial(const float* __rest
 }
 
 // sums[0][c] = sum gz (= grad bias), sums[1][c] = sum gz * xhat (= grad weight)
-__global__ __launch_bounds__(BN_THREADS) void bn_bwd_final(int c, int blocks, const double* __restrict__ part,
+__global__ __launch_bounds__(BN_FINAL_THREADS) void bn_bwd_final(int c, int blocks, const double* __restrict__ part,
                                                            float* __restrict__ gw, float* __restrict__ gb,
                                                            float* __restrict__ sums) {
   __shared__ double tot[128];
-  bn_final_sums(part, c, blocks, tot);
+  bn_final_sums(part, 2 * c, blocks, tot);
   const int ch = threadIdx.x;
   if (ch >= c) return;
   sums[ch] = (float)tot[ch];
@@ -209,7 +221,7 @@ hipError_t launch_bn_forward(const float* x, long long m, int c, const float* w,
                              float slope, float* y, float* stats, double* part, hipStream_t s) {
   const int nb = bn_blocks(m, c);
   hipLaunchKernelGGL(bn_stats_partial, dim3(nb), dim3(BN_THREADS), 0, s, x, m, c, part);
-  hipLaunchKernelGGL(bn_stats_final, dim3(1), dim3(BN_THREADS), 0, s, x, m, c, nb, eps, part, stats);
+  hipLaunchKernelGGL(bn_stats_final, dim3(1), dim3(BN_FINAL_THREADS), 0, s, x, m, c, nb, eps, part, stats);  // shift: row 0 of x
   if (act == GR_POLICY_ACT_ELU)
     hipLaunchKernelGGL(bn_apply<GR_POLICY_ACT_ELU>, dim3(nb), dim3(BN_THREADS), 0, s, x, m, c, w, b, stats, slope, y);
   else
@@ -227,11 +239,236 @@ hipError_t launch_bn_backward(const float* x, const float* gy, long long m, int 
     hipLaunchKernelGGL(bn_bwd_partial<GR_POLICY_ACT_ELU>, dim3(nb), dim3(BN_THREADS), 0, s, x, gy, m, c, w, b, stats, slope, part);
   else
     hipLaunchKernelGGL(bn_bwd_partial<GR_POLICY_ACT_LRELU>, dim3(nb), dim3(BN_THREADS), 0, s, x, gy, m, c, w, b, stats, slope, part);
-  hipLaunchKernelGGL(bn_bwd_final, dim3(1), dim3(BN_THREADS), 0, s, c, nb, part, gw, gb, sums);
+  hipLaunchKernelGGL(bn_bwd_final, dim3(1), dim3(BN_FINAL_THREADS), 0, s, c, nb, part, gw, gb, sums);
   if (act == GR_POLICY_ACT_ELU)
     hipLaunchKernelGGL(bn_bwd_elemt<GR_POLICY_ACT_ELU>, dim3(nb), dim3(BN_THREADS), 0, s, x, gy, m, c, w, b, stats, sums, slope, gx);
   else
     hipLaunchKernelGGL(bn_bwd_elemt<GR_POLICY_ACT_LRELU>, dim3(nb), dim3(BN_THREADS), 0, s, x, gy, m, c, w, b, stats, sums, slope, gx);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------- the stem's first block from the image
+// Conv2d(1, C, 3, stride 3, no bias) -> BatchNorm2d -> act of VisionActorCritic.stem_gemm, evaluated from
+// the depth image itself: row r of the conv output is W1 . patch(r), patch(r) the 9 pixels of a 3 x 3 cell
+// (pixel tables in the row order of stem_gemm: nimg x na rows of table a, then nimg x nb rows of table b, so
+// conv2's input stays a view of y).  Neither the patch matrix nor the conv output is ever written: the
+// statistics pass and the apply pass recompute the 36 FMAs of a thread's 4 channels, and so do the backward
+// passes, which end in the conv weight's gradient (the image needs none) instead of writing gx.
+constexpr int STEM_MAX_CELLS = 1024;  // na + nbt (768 at 72 x 96)
+
+__device__ __forceinline__ void stem_stage_table(const Stem1& s, short* tab) {
+  for (int i = threadIdx.x; i < (s.na + s.nbt) * 9; i += BN_THREADS) tab[i] = s.pix[i];
+  __syncthreads();
+}
+__device__ __forceinline__ void stem_pixels(const Stem1& s, const short* tab, unsigned r, float px[9]) {
+  const unsigned ra = (unsigned)s.nimg * (unsigned)s.na;
+  unsigned b, p;
+  if (r < ra) {
+    b = r / (unsigned)s.na;
+    p = r - b * (unsigned)s.na;
+  } else {
+    const unsigned q = r - ra;
+    b = q / (unsigned)s.nbt;
+    p = (unsigned)s.na + (q - b * (unsigned)s.nbt);
+  }
+  const float* img = s.obs + (long long)b * s.ld + s.off;
+  const short* t = tab + p * 9;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) px[k] = img[t[k]];
+}
+// the thread's 4 conv outputs (channels 4 g .. 4 g + 3), k-ordered fp32 FMA chains
+__device__ __forceinline__ void stem_conv(const float w[4][9], const float px[9], float x[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float a = w[j][0] * px[0];
+#pragma unroll
+    for (int k = 1; k < 9; ++k) a = __builtin_fmaf(w[j][k], px[k], a);
+    x[j] = a;
+  }
+}
+__device__ __forceinline__ void stem_load_w(const Stem1& s, int g, float w[4][9]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < 9; ++k) w[j][k] = s.w[(4 * g + j) * 9 + k];
+}
+
+// forward statistics: shifted channel sums of the conv output; block 0 also writes the shift (row 0)
+__global__ __launch_bounds__(BN_THREADS) void stem1_stats_partial(Stem1 s, double* __restrict__ part,
+                                                                  float* __restrict__ shift) {
+  __shared__ short tab[STEM_MAX_CELLS * 9];
+  stem_stage_table(s, tab);
+  const int c4 = s.c / 4, g = threadIdx.x & (c4 - 1);
+  float w[4][9], px[9], sh[4], x[4];
+  stem_load_w(s, g, w);
+  stem_pixels(s, tab, 0u, px);
+  stem_conv(w, px, sh);
+  if (blockIdx.x == 0 && threadIdx.x < c4)
+    for (int j = 0; j < 4; ++j) shift[4 * g + j] = sh[j];
+  const unsigned m = (unsigned)s.nimg * (unsigned)(s.na + s.nbt);
+  const unsigned step = gridDim.x * BN_THREADS / c4;
+  float a[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  for (unsigned r = (blockIdx.x * BN_THREADS + threadIdx.x) / c4; r < m; r += step) {
+    stem_pixels(s, tab, r, px);
+    stem_conv(w, px, x);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float d = x[j] - sh[j];
+      a[j] += d;
+      a[4 + j] += d * d;
+    }
+  }
+  bn_block_partials(a, s.c, part);
+}
+
+// forward apply: y[r][4 g + j] = act((x - mean) * invstd * w + b)
+template <int ACT>
+__global__ __launch_bounds__(BN_THREADS) void stem1_apply(Stem1 s, const float* __restrict__ bw, const float* __restrict__ bb,
+                                                          const float* __restrict__ stats, float slope, float* __restrict__ y) {
+  __shared__ short tab[STEM_MAX_CELLS * 9];
+  stem_stage_table(s, tab);
+  const int c4 = s.c / 4, g = threadIdx.x & (c4 - 1);
+  float w[4][9], px[9], x[4];
+  stem_load_w(s, g, w);
+  const float4 mu = ld4f(stats, g), is = ld4f(stats + s.c, g), wv = ld4f(bw, g), bv = ld4f(bb, g);
+  const unsigned m = (unsigned)s.nimg * (unsigned)(s.na + s.nbt);
+  const unsigned step = gridDim.x * BN_THREADS / c4;
+  for (unsigned r = (blockIdx.x * BN_THREADS + threadIdx.x) / c4; r < m; r += step) {
+    stem_pixels(s, tab, r, px);
+    stem_conv(w, px, x);
+    float4 o;
+    o.x = bn_act<ACT>((x[0] - mu.x) * is.x * wv.x + bv.x, slope);
+    o.y = bn_act<ACT>((x[1] - mu.y) * is.y * wv.y + bv.y, slope);
+    o.z = bn_act<ACT>((x[2] - mu.z) * is.z * wv.z + bv.z, slope);
+    o.w = bn_act<ACT>((x[3] - mu.w) * is.w * wv.w + bv.w, slope);
+    reinterpret_cast<float4*>(y)[(size_t)r * c4 + g] = o;
+  }
+}
+
+// backward reduce: per channel sum(gz), sum(gz xhat)
+template <int ACT>
+__global__ __launch_bounds__(BN_THREADS) void stem1_bwd_partial(Stem1 s, const float* __restrict__ gy,
+                                                                const float* __restrict__ bw, const float* __restrict__ bb,
+                                                                const float* __restrict__ stats, float slope,
+                                                                double* __restrict__ part) {
+  __shared__ short tab[STEM_MAX_CELLS * 9];
+  stem_stage_table(s, tab);
+  const int c4 = s.c / 4, g = threadIdx.x & (c4 - 1);
+  float w[4][9], px[9], x[4];
+  stem_load_w(s, g, w);
+  const float4 mu = ld4f(stats, g), is = ld4f(stats + s.c, g), wv = ld4f(bw, g), bv = ld4f(bb, g);
+  const unsigned m = (unsigned)s.nimg * (unsigned)(s.na + s.nbt);
+  const unsigned step = gridDim.x * BN_THREADS / c4;
+  float a[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  for (unsigned r = (blockIdx.x * BN_THREADS + threadIdx.x) / c4; r < m; r += step) {
+    stem_pixels(s, tab, r, px);
+    stem_conv(w, px, x);
+    const float4 dy = ld4f(gy, (long long)r * c4 + g);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float xh = (x[j] - comp(mu, j)) * comp(is, j);
+      const float gz = comp(dy, j) * bn_dact<ACT>(xh * comp(wv, j) + comp(bv, j), slope);
+      a[j] += gz;
+      a[4 + j] += gz * xh;
+    }
+  }
+  bn_block_partials(a, s.c, part);
+}
+
+// backward element + conv weight gradient: gx = (gz - sum gz / M - xhat sum gz xhat / M) invstd w (never
+// written), gW[4 g + j][k] += gx_j px_k; per block [C][9] partials in fp64
+template <int ACT>
+__global__ __launch_bounds__(BN_THREADS) void stem1_bwd_wgrad(Stem1 s, const float* __restrict__ gy,
+                                                              const float* __restrict__ bw, const float* __restrict__ bb,
+                                                              const float* __restrict__ stats, const float* __restrict__ sums,
+                                                              float slope, double* __restrict__ wpart) {
+  __shared__ short tab[STEM_MAX_CELLS * 9];
+  __shared__ float red[BN_THREADS * 36];
+  stem_stage_table(s, tab);
+  const int c4 = s.c / 4, g = threadIdx.x & (c4 - 1);
+  float w[4][9], px[9], x[4], acc[4][9];
+  stem_load_w(s, g, w);
+  const float4 mu = ld4f(stats, g), is = ld4f(stats + s.c, g), wv = ld4f(bw, g), bv = ld4f(bb, g);
+  const unsigned m = (unsigned)s.nimg * (unsigned)(s.na + s.nbt);
+  const float inv_m = 1.0f / (float)m;
+  const float4 s1 = ld4f(sums, g), s2 = ld4f(sums + s.c, g);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < 9; ++k) acc[j][k] = 0.0f;
+  const unsigned step = gridDim.x * BN_THREADS / c4;
+  for (unsigned r = (blockIdx.x * BN_THREADS + threadIdx.x) / c4; r < m; r += step) {
+    stem_pixels(s, tab, r, px);
+    stem_conv(w, px, x);
+    const float4 dy = ld4f(gy, (long long)r * c4 + g);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float xh = (x[j] - comp(mu, j)) * comp(is, j);
+      const float gz = comp(dy, j) * bn_dact<ACT>(xh * comp(wv, j) + comp(bv, j), slope);
+      const float gx = (gz - comp(s1, j) * inv_m - xh * (comp(s2, j) * inv_m)) * (comp(is, j) * comp(wv, j));
+#pragma unroll
+      for (int k = 0; k < 9; ++k) acc[j][k] = __builtin_fmaf(gx, px[k], acc[j][k]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < 9; ++k) red[(j * 9 + k) * BN_THREADS + threadIdx.x] = acc[j][k];
+  __syncthreads();
+  // (channel 4 gg + j, k) sums the threads of group gg in index order
+  for (int v = threadIdx.x; v < 9 * s.c; v += BN_THREADS) {
+    const int ch = v / 9, k = v % 9, gg = ch / 4, j = ch % 4;
+    double t = 0.0;
+    for (int u = gg; u < BN_THREADS; u += c4) t += (double)red[(j * 9 + k) * BN_THREADS + u];
+    wpart[(size_t)blockIdx.x * 9 * s.c + v] = t;
+  }
+}
+
+__global__ __launch_bounds__(BN_FINAL_THREADS) void stem1_wgrad_final(int n, int blocks, const double* __restrict__ wpart,
+                                                                      float* __restrict__ gw) {
+  __shared__ double tot[1024];
+  bn_final_sums(wpart, n, blocks, tot);
+  for (int v = threadIdx.x; v < n; v += BN_FINAL_THREADS) gw[v] = (float)tot[v];
+}
+
+static int stem_blocks(const Stem1& s) { return bn_blocks((long long)s.nimg * (s.na + s.nbt), s.c); }
+
+// workspace (doubles): BN partials [nb][2c] | shift + sums (2c floats, as c doubles) | wgrad partials [nb][9c]
+long long stem1_scratch_doubles(int nimg, int rows_per_img, int c) {
+  const long long nb = bn_blocks((long long)nimg * rows_per_img, c);
+  return nb * 2 * c + 2 * c + nb * 9 * c;
+}
+
+hipError_t launch_stem1_forward(const Stem1& s, const float* bw, const float* bb, float eps, int act, float slope,
+                                float* y, float* stats, double* part, hipStream_t st) {
+  const int nb = stem_blocks(s);
+  float* shift = reinterpret_cast<float*>(part + (size_t)nb * 2 * s.c);
+  const long long m = (long long)s.nimg * (s.na + s.nbt);
+  hipLaunchKernelGGL(stem1_stats_partial, dim3(nb), dim3(BN_THREADS), 0, st, s, part, shift);
+  hipLaunchKernelGGL(bn_stats_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, shift, m, s.c, nb, eps, part, stats);
+  if (act == GR_POLICY_ACT_ELU)
+    hipLaunchKernelGGL(stem1_apply<GR_POLICY_ACT_ELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, bw, bb, stats, slope, y);
+  else
+    hipLaunchKernelGGL(stem1_apply<GR_POLICY_ACT_LRELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, bw, bb, stats, slope, y);
+  return hipGetLastError();
+}
+
+hipError_t launch_stem1_backward(const Stem1& s, const float* bw, const float* bb, const float* stats, int act,
+                                 float slope, const float* gy, float* gconv, float* gbw, float* gbb, double* part,
+                                 hipStream_t st) {
+  const int nb = stem_blocks(s);
+  float* sums = reinterpret_cast<float*>(part + (size_t)nb * 2 * s.c);
+  double* wpart = part + (size_t)nb * 2 * s.c + 2 * s.c;
+  if (act == GR_POLICY_ACT_ELU)
+    hipLaunchKernelGGL(stem1_bwd_partial<GR_POLICY_ACT_ELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, gy, bw, bb, stats, slope, part);
+  else
+    hipLaunchKernelGGL(stem1_bwd_partial<GR_POLICY_ACT_LRELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, gy, bw, bb, stats, slope, part);
+  hipLaunchKernelGGL(bn_bwd_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, s.c, nb, part, gbw, gbb, sums);
+  if (act == GR_POLICY_ACT_ELU)
+    hipLaunchKernelGGL(stem1_bwd_wgrad<GR_POLICY_ACT_ELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, gy, bw, bb, stats, sums, slope, wpart);
+  else
+    hipLaunchKernelGGL(stem1_bwd_wgrad<GR_POLICY_ACT_LRELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, gy, bw, bb, stats, sums, slope, wpart);
+  hipLaunchKernelGGL(stem1_wgrad_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, 9 * s.c, nb, wpart, gconv);
   return hipGetLastError();
 }
 

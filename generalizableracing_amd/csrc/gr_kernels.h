@@ -97,6 +97,22 @@ hipError_t launch_camera(const CamArgs& a, hipStream_t s);
 hipError_t launch_policy(const gr_policy_args& a, hipStream_t s);  // gr_policy.hip
 hipError_t launch_policy_f32(const gr_policy_args& a, hipStream_t s);  // gr_policy_f32.hip
 int bn_scratch_doubles(long long m, int c);                                                // gr_bn.hip
+// the stem's first block from the image (gr_bn.hip): image b at obs + b * ld + off; rows nimg x na from
+// table a, then nimg x nbt from table b; pix [(na + nbt) * 9]; conv weight w [c][9]
+struct Stem1 {
+  const float* obs;
+  long long ld, off;
+  int nimg, na, nbt;
+  const short* pix;
+  const float* w;
+  int c;
+};
+long long stem1_scratch_doubles(int nimg, int rows_per_img, int c);
+hipError_t launch_stem1_forward(const Stem1& s, const float* bw, const float* bb, float eps, int act, float slope,
+                                float* y, float* stats, double* part, hipStream_t st);
+hipError_t launch_stem1_backward(const Stem1& s, const float* bw, const float* bb, const float* stats, int act,
+                                 float slope, const float* gy, float* gconv, float* gbw, float* gbb, double* part,
+                                 hipStream_t st);
 hipError_t launch_bn_forward(const float* x, long long m, int c, const float* w, const float* b, float eps, int act,
                              float slope, float* y, float* stats, double* part, hipStream_t s);
 hipError_t launch_bn_backward(const float* x, const float* gy, long long m, int c, const float* w, const float* b,

@@ -83,6 +83,77 @@ def batch_norm_act(bn: nn.BatchNorm2d, act: nn.Module, x: torch.Tensor) -> torch
     (the caller has already counted the batch in num_batches_tracked and passes the momentum it implies)."""
     code, slope = _act_code(act)
     y, stats = _BatchNormAct.apply(x, bn.weight, bn.bias, bn.eps, code, slope)
+    _update_running(bn, stats)
+    return y
+
+
+class _Stem1(torch.autograd.Function):
+    """Conv2d(1, C, 3, stride 3) -> BatchNorm2d (batch statistics) -> act from the depth images (gr_stem1_*)."""
+
+    @staticmethod
+    def forward(ctx, img, conv_w, bn_w, bn_b, pix, na, nb, eps, act, slope):
+        lib = _abi.load()
+        nimg = img.shape[0]
+        c = conv_w.shape[0]
+        rows = nimg * (na + nb)
+        y = torch.empty(rows, c, device=img.device, dtype=torch.float32)
+        stats = torch.empty(4, c, device=img.device, dtype=torch.float32)
+        part = torch.empty(int(lib.gr_stem1_scratch_doubles(nimg, na + nb, c)), device=img.device, dtype=torch.float64)
+        w = conv_w.detach().reshape(c, 9).contiguous()
+        bw, bb = bn_w.detach().contiguous(), bn_b.detach().contiguous()
+        rc = lib.gr_stem1_forward(img.data_ptr(), img.stride(0), 0, nimg, pix.data_ptr(), na, nb, w.data_ptr(), c,
+                                  bw.data_ptr(), bb.data_ptr(), float(eps), act, float(slope), y.data_ptr(),
+                                  stats.data_ptr(), part.data_ptr(), _stream(img))
+        if rc != 0:
+            raise RuntimeError(f"gr_stem1_forward failed (status {rc})")
+        ctx.save_for_backward(img, w, bw, bb, stats)
+        ctx.pix = pix  # a constant table (possibly made under inference mode): kept as an attribute
+        ctx.args = (na, nb, act, slope, conv_w.shape)
+        ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, gy, _gstats):
+        if ctx.needs_input_grad[0]:
+            raise RuntimeError("the fused stem computes no gradient for the image")
+        lib = _abi.load()
+        img, w, bw, bb, stats = ctx.saved_tensors
+        pix = ctx.pix
+        na, nb, act, slope, wshape = ctx.args
+        nimg, c = img.shape[0], w.shape[0]
+        gy = gy.contiguous()
+        gconv = torch.empty(c, 9, device=img.device, dtype=torch.float32)
+        gbw = torch.empty(c, device=img.device, dtype=torch.float32)
+        gbb = torch.empty(c, device=img.device, dtype=torch.float32)
+        part = torch.empty(int(lib.gr_stem1_scratch_doubles(nimg, na + nb, c)), device=img.device, dtype=torch.float64)
+        rc = lib.gr_stem1_backward(img.data_ptr(), img.stride(0), 0, nimg, pix.data_ptr(), na, nb, w.data_ptr(), c,
+                                   bw.data_ptr(), bb.data_ptr(), stats.data_ptr(), act, float(slope), gy.data_ptr(),
+                                   gconv.data_ptr(), gbw.data_ptr(), gbb.data_ptr(), part.data_ptr(), _stream(img))
+        if rc != 0:
+            raise RuntimeError(f"gr_stem1_backward failed (status {rc})")
+        return None, gconv.view(wshape), gbw, gbb, None, None, None, None, None, None
+
+
+def stem1_applicable(bn: nn.BatchNorm2d, act: nn.Module, img: torch.Tensor, conv_w: torch.Tensor) -> bool:
+    """The image-side HIP op: fp32 CUDA image rows (unit column stride), a 1-channel 3x3 conv without bias into
+    C in {4, 8, 16, 32, 64} channels, training-mode BN, LeakyReLU / ELU(1)."""
+    return (img.is_cuda and img.dtype == torch.float32 and img.dim() == 2 and img.stride(1) == 1
+            and not img.requires_grad and tuple(conv_w.shape[1:]) == (1, 3, 3) and conv_w.shape[0] in _CHANNELS
+            and conv_w.dtype == torch.float32 and bn.affine and bn.training and _act_code(act) is not None)
+
+
+def stem1_bn_act(bn: nn.BatchNorm2d, act: nn.Module, conv_w: torch.Tensor, img: torch.Tensor, pix: torch.Tensor,
+                 na: int, nb: int) -> torch.Tensor:
+    """act(bn(conv(img))) as the patch rows of VisionActorCritic.stem_gemm (img [B, H*W] rows; pix int16
+    [(na + nb) * 9] pixel offsets), running statistics updated as nn.BatchNorm2d does (the caller counts the
+    batch in num_batches_tracked)."""
+    code, slope = _act_code(act)
+    y, stats = _Stem1.apply(img, conv_w, bn.weight, bn.bias, pix, na, nb, bn.eps, code, slope)
+    _update_running(bn, stats)
+    return y
+
+
+def _update_running(bn: nn.BatchNorm2d, stats: torch.Tensor):
     if bn.track_running_stats and bn.running_mean is not None:
         momentum = 0.0 if bn.momentum is None else bn.momentum
         if bn.momentum is None and bn.num_batches_tracked is not None:
@@ -90,7 +161,6 @@ def batch_norm_act(bn: nn.BatchNorm2d, act: nn.Module, x: torch.Tensor) -> torch
         with torch.no_grad():
             bn.running_mean.mul_(1.0 - momentum).add_(stats[0], alpha=momentum)
             bn.running_var.mul_(1.0 - momentum).add_(stats[3], alpha=momentum)
-    return y
 
 
 def reference_batch_norm_act(bn: nn.BatchNorm2d, act: nn.Module, x: torch.Tensor) -> torch.Tensor:

@@ -24,7 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .actor_critic import ActorCritic, resolve_nn_activation
-from .fused_bn import batch_norm_act, fused_applicable
+from .fused_bn import batch_norm_act, fused_applicable, stem1_applicable, stem1_bn_act
 
 
 def _conv_out(n: int, k: int, s: int) -> int:
@@ -151,7 +151,11 @@ class VisionActorCritic(ActorCritic):
             return torch.tensor([(3 * v + i) * w + 3 * u + j for v, u in cells for i in range(3) for j in range(3)],
                                 dtype=torch.long, device=device)
 
-        self._pidx = (pix(l1), pix(l1_left), len(l1), len(l1_left), len(g3), len(g2))
+        with torch.inference_mode(False):  # cached across rollouts (inference mode) and updates
+            a, b = pix(l1), pix(l1_left)
+            # the same cells as int16 offsets, table a then table b, for the fused first block (gr_stem1_*)
+            pix16 = torch.cat([a, b]).to(torch.int16)
+        self._pidx = (a, b, len(l1), len(l1_left), len(g3), len(g2), pix16)
         return self._pidx
 
     def stem_gemm(self, img: torch.Tensor) -> torch.Tensor:
@@ -160,11 +164,17 @@ class VisionActorCritic(ActorCritic):
         h1, w1, h2, w2, h3, w3 = self._dims
         B = img.shape[0]
         flat = img.reshape(B, -1)
-        idx, idx_left, n1, n1_left, n3, n2 = self._patch_index(img.device)
-        x = flat.index_select(1, idx).view(B * n1, 9)
-        if n1_left:
-            x = torch.cat([x, flat.index_select(1, idx_left).view(B * n1_left, 9)])
-        y = self._bn_act(bn1, act, _gemm(x, conv1.weight.reshape(16, 9)))
+        idx, idx_left, n1, n1_left, n3, n2, pix16 = self._patch_index(img.device)
+        if self.fused_bn and stem1_applicable(bn1, act, flat, conv1.weight):
+            # conv1 + BN1 + act from the image itself: no patch matrix, no conv output (rsl_rl/fused_bn.py)
+            if bn1.track_running_stats and bn1.num_batches_tracked is not None:
+                bn1.num_batches_tracked.add_(1)
+            y = stem1_bn_act(bn1, act, conv1.weight, flat, pix16, n1, n1_left)
+        else:
+            x = flat.index_select(1, idx).view(B * n1, 9)
+            if n1_left:
+                x = torch.cat([x, flat.index_select(1, idx_left).view(B * n1_left, 9)])
+            y = self._bn_act(bn1, act, _gemm(x, conv1.weight.reshape(16, 9)))
         x = y[: B * n1].view(B * n2, 144)  # conv2's 3x3 patches (i, j, c): a view
         y = self._bn_act(bn2, act, _gemm(x, conv2.weight.permute(0, 2, 3, 1).reshape(32, 144)))
         x = y.view(B, n2, 32)[:, :n3].reshape(B * h3 * w3, 128)  # conv3's 2x2 patches: a view at 72x96

@@ -391,6 +391,24 @@ int gr_bn_act_backward(const float* x, const float* gy, int64_t m, int32_t c, co
                        const float* stats, int32_t act, float slope, float* gx, float* gw, float* gb, double* part,
                        void* stream);
 
+/*
+ * The vision stem's first block from the depth image itself: Conv2d(1, c, 3, stride 3, no bias) -> BatchNorm2d
+ * (training mode) -> act, for `nimg` images at obs + b * ld + off (fp32 pixels).  Output rows follow
+ * VisionActorCritic.stem_gemm: nimg x na rows whose 3x3 cells are pix[0 .. na) (int16 pixel offsets, 9 per
+ * row), then nimg x nb rows from pix[na .. na + nb); y [rows][c].  The patch matrix and the conv output are
+ * never written (recomputed per pass); the backward returns the conv weight's gradient [c][9] and the BN
+ * affine gradients (the image needs none).  c in {4, 8, 16, 32, 64}, na + nb <= 1024; `part`: a workspace of
+ * gr_stem1_scratch_doubles(nimg, na + nb, c) doubles; stats as gr_bn_act_forward.
+ */
+int64_t gr_stem1_scratch_doubles(int32_t nimg, int32_t rows_per_img, int32_t c);
+int gr_stem1_forward(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
+                     int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b, float eps,
+                     int32_t act, float slope, float* y, float* stats, double* part, void* stream);
+int gr_stem1_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
+                      int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b,
+                      const float* stats, int32_t act, float slope, const float* gy, float* g_conv_w, float* g_bn_w,
+                      float* g_bn_b, double* part, void* stream);
+
 /* Device status: the GR_STATUS_* bits the kernels of this context raised since the last clear (0: none).
  * Synchronises `stream` (the stream the steps ran on); clear != 0 resets the word.  A raised bit means the
  * outputs of some step since the last check are not trustworthy. */

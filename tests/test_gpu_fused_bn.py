@@ -27,10 +27,10 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
 
-def _close(got, want, tol):
-    scale = float(want.abs().max()) + 1e-6
-    err = float((got - want).abs().max())
-    assert err <= tol * scale, (err, scale)
+def _close(got, want, tol, what=""):
+    scale = float(want.detach().abs().max()) + 1e-6
+    err = float((got.detach() - want.detach()).abs().max())
+    assert err <= tol * scale, (what, err, scale)
 
 
 @pytest.mark.parametrize("m,c,act", [(2, 16, "lrelu"), (1000, 16, "lrelu"), (4097, 32, "elu"), (300000, 64, "lrelu"),
@@ -76,29 +76,42 @@ def test_deterministic():
         assert torch.equal(u, v)
 
 
-def test_vision_policy_fused_vs_torch():
-    """VisionActorCritic features and parameter gradients with the fused op == with torch's ops."""
+@pytest.mark.parametrize("activation,n", [("lrelu", 256), ("elu", 97)])
+def test_vision_policy_fused_vs_torch(activation, n):
+    """VisionActorCritic with the fused ops (conv1 + BN1 + act from the image, BN2 / BN3 + act) against torch's
+    ops (patch gather + GEMM + batch_norm + activation), both fp32, judged against a float64 evaluation of the
+    same module: the fused features, parameter gradients and running statistics must be at least as close to
+    float64 as torch's fp32 path is (within 2x, plus a 1e-5 floor).  The weight gradients reduce over 10^5-10^6
+    rows, and the BN backward makes them small differences of large sums, so fp32 paths differ from each
+    other by ~1e-3 of their norm; float64 is the arbiter.  The observation rows are a strided slice, as in
+    the rollout."""
     from generalizableracing_amd.rsl_rl.vision_actor_critic import VisionActorCritic
 
     torch.manual_seed(2)
-    n = 256
     pol = VisionActorCritic(16 + 72 * 96, 16 + 72 * 96, 4, actor_hidden_dims=[128, 128], critic_hidden_dims=[128, 128],
-                            activation="lrelu").to(DEV)
+                            activation=activation).to(DEV)
     ref = copy.deepcopy(pol)
     ref.fused_bn = False
-    obs = torch.rand(n, 16 + 72 * 96, device=DEV) * 5.0
-    f = pol.features(obs)
-    fr = ref.features(obs)
-    _close(f, fr, 1e-4)
-    (f.square().sum() + pol.actor(f).sum()).backward()
-    (fr.square().sum() + ref.actor(fr).sum()).backward()
-    for (name, p), (_, q) in zip(pol.named_parameters(), ref.named_parameters()):
-        if p.grad is None:
-            assert q.grad is None, name
-            continue
-        _close(p.grad, q.grad, 2e-3)
-    for (name, b), (_, c) in zip(pol.named_buffers(), ref.named_buffers()):
-        if b.dtype.is_floating_point:
-            assert float((b - c).abs().max()) <= 1e-5 * (float(c.abs().max()) + 1e-6), name
-        else:
-            assert torch.equal(b, c), name
+    r64 = copy.deepcopy(pol).double()
+    r64.fused_bn = False
+    obs = (torch.rand(n, 20 + 72 * 96, device=DEV) * 5.0)[:, 4:]  # row stride 6932: not a contiguous matrix
+    outs = []
+    for net, o in ((pol, obs), (ref, obs), (r64, obs.double())):
+        f = net.features(o)
+        (f.square().sum() + net.actor(f).sum()).backward()
+        outs.append((f.detach().double(), {k: p.grad.double() for k, p in net.named_parameters() if p.grad is not None},
+                     {k: b.double() for k, b in net.named_buffers() if b.dtype.is_floating_point}))
+    (f_fu, g_fu, b_fu), (f_t, g_t, b_t), (f_64, g_64, b_64) = outs
+
+    def rel(a, b):
+        return float((a - b).norm() / (b.norm() + 1e-30))
+
+    assert rel(f_fu, f_64) <= 2 * rel(f_t, f_64) + 1e-5, (rel(f_fu, f_64), rel(f_t, f_64))
+    assert g_fu.keys() == g_64.keys()
+    for k in g_64:
+        assert rel(g_fu[k], g_64[k]) <= 2 * rel(g_t[k], g_64[k]) + 1e-5, (k, rel(g_fu[k], g_64[k]), rel(g_t[k], g_64[k]))
+    for k in b_64:
+        assert rel(b_fu[k], b_64[k]) <= 2 * rel(b_t[k], b_64[k]) + 1e-6, (k, rel(b_fu[k], b_64[k]), rel(b_t[k], b_64[k]))
+    for (k, a), (_, b) in zip(pol.named_buffers(), ref.named_buffers()):
+        if not a.dtype.is_floating_point:
+            assert torch.equal(a, b), k
