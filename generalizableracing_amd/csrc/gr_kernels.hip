@@ -261,7 +261,7 @@ DEV void action_scale(const KArgs& a, float m_ctrl, float sc[4], float of[4]) {
 // compile-time lattice: after unrolling every offset is an inline constant (0, +-1, +-0.5)
 constexpr float c_lattice[17][3] = GR_LATTICE_INIT;
 #ifndef GR_OBST_BATCH
-#define GR_OBST_BATCH 4  // obstacle cull spheres loaded per batch
+#define GR_OBST_BATCH 8  // obstacle cull spheres loaded per batch (8: -0.15 us on obstacle tracks vs 4; 16 spills)
 #endif
 
 // ------------------------------------------------------------- obstacles
