@@ -328,7 +328,7 @@ def env_count_sweep(rank, device, a, sizes=(16384, 262144, 1048576)):
 
 
 def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False, graph_update=False, bf16_update=False,
-              obs_sink=True):
+              obs_sink=True, fused_precision="bf16"):
     """The reference's Perf/total_fps (24 steps x N / (collect + learn)) of rsl_rl PPO with MLP(256,256):
     config C2 at 4 096 envs fp32; at 65 536 envs also with the fused bf16 rollout inference and bf16
     rollout obs buffers (C5's training options; the update stays fp32)."""
@@ -338,6 +338,7 @@ def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False, graph_up
     venv = RslRlVecEnvWrapper(RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=device))))
     cfg = QuadcopterPPORunnerCfg(device=device)
     cfg.algorithm.fused_rollout_inference = bool(fused)
+    cfg.algorithm.fused_rollout_precision = fused_precision
     cfg.algorithm.storage_obs_dtype = "bfloat16" if bf16_storage else "float32"
     cfg.algorithm.graph_update = bool(graph_update)
     cfg.algorithm.update_autocast_bf16 = bool(bf16_update)
@@ -348,7 +349,7 @@ def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False, graph_up
     for _ in range(iters):
         runner.learn(1)
         fps.append(runner.last_log["fps"])
-    progress(f"train_fps n={n} fused={fused} bf16_storage={bf16_storage} graph_update={graph_update} "
+    progress(f"train_fps n={n} fused={fused}({fused_precision}) bf16_storage={bf16_storage} graph_update={graph_update} "
              f"obs_sink={obs_sink}: {np.median(fps):.4g}")
     venv.close()
     return float(np.median(fps))
@@ -535,6 +536,9 @@ def main():
         extra["train_total_fps_4096_envs_graph_update"] = train_fps(device, graph_update=True)
         extra["train_total_fps_65536_envs"] = {
             "fp32": train_fps(device, n),
+            "fp32_fused_fp32_rollout": train_fps(device, n, fused=True, fused_precision="fp32"),
+            "fp32_fused_fp32_rollout_graphed_update": train_fps(device, n, fused=True, fused_precision="fp32",
+                                                                graph_update=True),
             "fused_rollout_bf16_storage": train_fps(device, n, fused=True, bf16_storage=True),
             "fused_rollout_bf16_storage_no_obs_sink": train_fps(device, n, fused=True, bf16_storage=True,
                                                                 obs_sink=False),

@@ -1,5 +1,5 @@
 """Perf/total_fps of one training configuration, split into collection and learning time, plus the top
-device kernels of one iteration (torch.profiler).  N, FUSED, BF16, GRAPH, SINK env vars select the options."""
+device kernels of one iteration (torch.profiler).  N, FUSED (1 = bf16, fp32), BF16, GRAPH, SINK env vars select the options."""
 import os
 import sys
 
@@ -14,7 +14,8 @@ n = int(os.environ.get("N", "65536"))
 dev = "cuda:0"
 venv = RslRlVecEnvWrapper(RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=dev))))
 cfg = QuadcopterPPORunnerCfg(device=dev)
-cfg.algorithm.fused_rollout_inference = os.environ.get("FUSED", "0") == "1"
+cfg.algorithm.fused_rollout_inference = os.environ.get("FUSED", "0") in ("1", "fp32")
+cfg.algorithm.fused_rollout_precision = "fp32" if os.environ.get("FUSED") == "fp32" else "bf16"
 cfg.algorithm.storage_obs_dtype = "bfloat16" if os.environ.get("BF16", "0") == "1" else "float32"
 cfg.algorithm.graph_update = os.environ.get("GRAPH", "0") == "1"
 cfg.algorithm.obs_sink = os.environ.get("SINK", "1") == "1"
