@@ -251,7 +251,7 @@ int gr_create(const gr_config* cfg, gr_ctx** out) {
       g.num_levels > 255 || g.max_gates <= 0 || g.max_gates > 255 || g.decimation <= 0 ||
       (g.action_lag != 0 && g.action_lag != 1) || g.max_episode_length <= 0 || !(g.mass > 0.0f) ||
       (g.integrator != GR_INTEGRATOR_DD_EXPLICIT && g.integrator != GR_INTEGRATOR_SEMI_IMPLICIT) ||
-      g.num_types > g.num_envs || g.max_init_level < 0)
+      g.max_init_level < 0)  // (fewer envs than terrain columns is valid: IL's floor(i / (N / cols)) skips columns)
     return GR_ERR_ARG;
   gr_ctx* c = new (std::nothrow) gr_ctx();
   if (!c) return GR_ERR_STATE;

@@ -55,6 +55,17 @@ def test_create_destroy_and_bytes():
     assert lib.gr_destroy(ctx) == 0
 
 
+def test_create_accepts_fewer_envs_than_terrain_columns():
+    """IL assigns env i to column floor(i / (N / num_cols)): with N < num_cols some columns get no env."""
+    lib = _abi.load()
+    c = _abi.default_config()
+    c.num_envs = 1
+    ctx = C.c_void_p()
+    assert lib.gr_create(C.byref(c), C.byref(ctx)) == 0
+    assert lib.gr_num_blocks(ctx) == 1
+    assert lib.gr_destroy(ctx) == 0
+
+
 @pytest.mark.parametrize("field,value", [("num_envs", 0), ("num_types", 65), ("action_lag", 2), ("integrator", 7)])
 def test_create_rejects_bad_config(field, value):
     lib = _abi.load()

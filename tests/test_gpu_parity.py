@@ -131,6 +131,28 @@ def test_env_free_run_bit_exact(conf):
     env.close()
 
 
+@pytest.mark.parametrize("n", [1, 63, 257])
+def test_ragged_env_counts_bit_exact(n):
+    """Env counts that leave most of the last workgroup (and of its waves) empty: a single env, less than one
+    wave, one env past a whole workgroup.  Dead lanes must neither store nor disturb the live ones."""
+    env, orc = make(n, obstacles=True)
+    env.reset()
+    orc.reset(None)
+    g = torch.Generator().manual_seed(n)
+    for k in range(60):
+        a = (torch.randn(n, 4, generator=g) * 1.5).numpy().astype(np.float32)
+        _, rew, term, tout, _ = env.step(torch.from_numpy(a).to(DEV))
+        orc.step(a)
+        torch.cuda.synchronize()
+        where = f"n {n} step {k}"
+        assert np.array_equal(bits(rew.cpu().numpy()), bits(orc.reward)), where
+        assert np.array_equal(term.cpu().numpy().astype(np.uint8), orc.terminated), where
+        assert np.array_equal(tout.cpu().numpy().astype(np.uint8), orc.time_out), where
+        assert_envs_equal(kernel_envs(env), orc.envs, where)
+        compare_outputs(env, orc, where)
+    env.close()
+
+
 def test_full_size_teacher_forced_slices():
     """65 536 envs (BASELINE C3 size): every step, a slice of envs is re-stepped by the oracle from the
     kernel's own pre-step state (teacher forcing) and must match bit-for-bit; size-independent
