@@ -18,7 +18,7 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "gr::step_kernel<true, false>"  # <USE_LDS, OBST>; --obstacles selects <true, true>
+KERNEL = "gr::step_kernel<true, false>"  # <USE_LDS, OBST>; --obstacles selects <false, true> (table read from L2)
 
 
 def pmc_means(prof):
@@ -46,11 +46,11 @@ def main():
     p.add_argument("--gates", type=int, default=8)
     p.add_argument("--read-bytes", type=int, default=256, help="algorithmic bytes read per env-step")
     p.add_argument("--write-bytes", type=int, default=290, help="algorithmic bytes written per env-step")
-    p.add_argument("--obstacles", action="store_true", help="obstacle tracks (kernel <true, true>, +16 B r/w hint)")
+    p.add_argument("--obstacles", action="store_true", help="obstacle tracks (kernel <false, true>, +16 B r/w hint)")
     a = p.parse_args()
     global KERNEL
     if a.obstacles:
-        KERNEL = "gr::step_kernel<true, true>"
+        KERNEL = "gr::step_kernel<false, true>"
         a.read_bytes += 16
         a.write_bytes += 16
     prof = os.path.join(ROOT, "gpurun_out", f"prof_{a.tag}")
