@@ -1,0 +1,49 @@
+"""How much of a short timed region (the driver's K = 20) is launch / completion latency: the same 20-step graph
+replay timed with torch.cuda.synchronize() alone, and with a spin on an event query before it (the GPU work is
+the same; only the host's wake-up differs).  Prints one JSON line.
+
+    python scripts/time_short_region.py [--steps 20] [--reps 20]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    n = 65536
+    env = bench.make_env(n, 0, "cuda:0", 8, "dd_explicit", False)
+    g = torch.Generator(device="cuda:0").manual_seed(1234)
+    actions = torch.randn(bench.ACTION_RING, n, 4, device="cuda:0", generator=g)
+    graph = bench.capture_graph(env, actions, a.steps)
+    ev = torch.cuda.Event()
+    res = {"sync": [], "spin_then_sync": []}
+    for r in range(2 * a.reps):
+        mode = "sync" if r % 2 == 0 else "spin_then_sync"
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        graph.replay()
+        if mode == "spin_then_sync":
+            ev.record()
+            while not ev.query():
+                pass
+        torch.cuda.synchronize()
+        res[mode].append((time.perf_counter() - t0) * 1e6 / a.steps)
+    out = {k: {"median_us_per_step": float(np.median(v)), "min": float(np.min(v))} for k, v in res.items()}
+    out["steps"] = a.steps
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
