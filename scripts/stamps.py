@@ -71,6 +71,27 @@ def run(n=int(os.environ.get("N", "65536")), steps=200):
         "end_us_pcts(10,50,90,99,100)": [float(np.percentile((rt1 - rt0.min()) * 10 / 1e3, q))
                                          for q in (10, 50, 90, 99, 100)],
     }
+    # per XCD (stamp 11: XCC_ID << 32 | HW_ID): when its workgroups start and end, relative to the first start
+    xcc = (st[:, 11] >> 32) & 0xF
+    wg_end = (rt1.reshape(-1, 12).max(axis=1) - rt0.min()) * 10 / 1e3
+    wg_start = (rt0.reshape(-1, 12).min(axis=1) - rt0.min()) * 10 / 1e3
+    wg_xcc = xcc.reshape(-1, 12)[:, 0]
+    out["per_xcd_us"] = {int(x): {"start_p50": float(np.median(wg_start[wg_xcc == x])),
+                                  "end_p50": float(np.median(wg_end[wg_xcc == x])),
+                                  "end_max": float(wg_end[wg_xcc == x].max()),
+                                  "workgroups": int((wg_xcc == x).sum())} for x in np.unique(wg_xcc)}
+    wg_dur = wg_end - wg_start
+    out["workgroup_duration_us_pcts(10,50,90,100)"] = [float(np.percentile(wg_dur, q)) for q in (10, 50, 90, 100)]
+    # what the slowest tenth of the workgroups spend their extra time on: per role and phase, mean cycles of the
+    # workgroups above the 90th duration percentile minus those at or below the median
+    slow = np.repeat(wg_dur > np.percentile(wg_dur, 90), 12)
+    fast = np.repeat(wg_dur <= np.percentile(wg_dur, 50), 12)
+    out["slow_minus_fast_phase_cycles"] = {
+        name: {ph: float((st[slow & (role == r)][:, b_] - st[slow & (role == r)][:, a_]).mean()
+                         - (st[fast & (role == r)][:, b_] - st[fast & (role == r)][:, a_]).mean())
+               for ph, a_, b_ in ROLE_PHASES[name]}
+        for r, name in enumerate(("physics", "policy", "episode"))}
+    out["slow_workgroup_ids"] = [int(b) for b in np.nonzero(wg_dur > np.percentile(wg_dur, 90))[0]]
     for r, name in enumerate(("physics", "policy", "episode")):
         sel = st[role == r]
         life = sel[:, 8] - sel[:, 0]
