@@ -108,7 +108,7 @@ def test_bf16_autocast_update_follows_fp32():
     torch.manual_seed(9)
     lb = alg_b.update()
     for pe, pb, q in zip(alg.policy.parameters(), alg_b.policy.parameters(), p0):
-        de, db = (pe - q).flatten(), (pb - q).flatten()
+        de, db = (pe.detach() - q).flatten(), (pb.detach() - q).flatten()
         cos = float(torch.dot(de, db) / (de.norm() * db.norm() + 1e-20))
         assert cos > 0.9, cos
     assert all(torch.isfinite(torch.tensor(list(lb.values()))))
