@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgr.so")
 
 # ---- constants (include/gr.h) ----
-GR_ABI_VERSION = 1
+GR_ABI_VERSION = 2
 GR_INTEGRATOR_DD_EXPLICIT = 0
 GR_INTEGRATOR_SEMI_IMPLICIT = 1
 
@@ -226,7 +226,7 @@ EXPORTS = [
     "gr_test_philox",
     "gr_debug_read_stamps", "gr_debug_read_policy_stamps",
     "gr_camera_config_default", "gr_camera_config_size", "gr_enable_camera", "gr_bind_camera_buffers",
-    "gr_camera_render", "gr_camera_bytes_per_env", "gr_policy_forward", "gr_column_sum_partials", "gr_column_sum",
+    "gr_camera_render", "gr_camera_bytes_per_env", "gr_policy_forward", "gr_policy_args_size", "gr_column_sum_partials", "gr_column_sum",
     "gr_bn_scratch_doubles", "gr_bn_act_forward", "gr_bn_act_backward", "gr_stem1_scratch_doubles",
     "gr_stem1_forward", "gr_stem1_backward",
 ]
@@ -271,6 +271,7 @@ def _declare(lib):
         "gr_camera_render": (C.c_int, [vp, C.c_int, vp, vp]),
         "gr_camera_bytes_per_env": (C.c_int, [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
         "gr_policy_forward": (C.c_int, [C.POINTER(GrPolicyArgs), vp]),
+        "gr_policy_args_size": (C.c_size_t, []),
         "gr_column_sum_partials": (C.c_int, [C.c_int64]),
         "gr_column_sum": (C.c_int, [vp, C.c_int, C.c_int64, C.c_int32, vp, vp, vp]),
         "gr_bn_scratch_doubles": (C.c_int64, [C.c_int64, C.c_int32]),
@@ -311,6 +312,9 @@ def load(path: str | None = None):
         raise RuntimeError(f"gr_config size mismatch: C {lib.gr_config_size()} vs ctypes {C.sizeof(GrConfig)}")
     if lib.gr_camera_config_size() != C.sizeof(GrCameraConfig):
         raise RuntimeError("gr_camera_config size mismatch between libgr.so and the ctypes mirror")
+    if lib.gr_policy_args_size() != C.sizeof(GrPolicyArgs):
+        raise RuntimeError(f"gr_policy_args size mismatch: C {lib.gr_policy_args_size()} vs ctypes "
+                           f"{C.sizeof(GrPolicyArgs)}")
     if path is None:
         _lib = lib
     return lib

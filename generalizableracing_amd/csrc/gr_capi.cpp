@@ -160,6 +160,7 @@ extern "C" {
 
 int gr_abi_version(void) { return GR_ABI_VERSION; }
 size_t gr_config_size(void) { return sizeof(gr_config); }
+size_t gr_policy_args_size(void) { return sizeof(gr_policy_args); }
 
 int gr_config_default(gr_config* c) {
   if (!c) return GR_ERR_ARG;

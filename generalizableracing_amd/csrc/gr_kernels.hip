@@ -1184,7 +1184,10 @@ __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
           __builtin_amdgcn_s_sleep(1);
           ++spin;
         }
-        if (__builtin_expect(spin >= (1 << 22), 0) && (t & 63) == 0)
+        // the loop ends on the counter or on the flag: a flag that arrived on the last poll is not a timeout, so the
+        // status is raised only when one more read still finds it clear (this read runs only past the limit)
+        if (__builtin_expect(spin >= (1 << 22), 0) &&
+            __hip_atomic_load(oflag + (t >> 6), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0 && (t & 63) == 0)
           __hip_atomic_fetch_or(a.status, GR_STATUS_OBST_WAIT_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         cm |= (uint32_t)__float_as_int(obx[O_MASK * GR_BLOCK + t].x);
       }

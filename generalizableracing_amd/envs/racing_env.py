@@ -335,10 +335,17 @@ class RacingEnv:
     def check_device_status(self):
         """Raise if a kernel flagged an untrustworthy step since the last check (the runner calls this once per
         rollout, where it synchronises anyway)."""
+        from ..rsl_rl import distributed as gdist
+
         st = self.device_status(clear=True)
-        if st:
-            why = "; ".join(t for b, t in _abi.STATUS_TEXT.items() if st & b) or "unknown"
-            raise RuntimeError(f"gr step kernel status 0x{st:x}: {why}")
+        # data parallel: the bits are OR-ed over the ranks first (max of the words, which suffices for one bit;
+        # the local word is reported), so every rank raises together instead of one rank raising while the
+        # others block in the update's all-reduces until the collective timeout
+        any_st = gdist.allreduce_max_int(st, self.device) if gdist.is_dist() else st
+        if any_st:
+            why = "; ".join(t for b, t in _abi.STATUS_TEXT.items() if (st or any_st) & b) or "unknown"
+            where = "" if st else f" (raised on another rank; rank {gdist.rank()} is clean)"
+            raise RuntimeError(f"gr step kernel status 0x{any_st:x}{where}: {why}")
 
     def state_field(self, name: str) -> torch.Tensor:
         """Gather a named per-env state field ([N, k] copy) from the SoA planes."""

@@ -58,10 +58,13 @@ class FlatGrads:
     `flat` (~566 KB for the 256x256 MLPs: latency-bound on xGMI, one message), with no concatenation or
     scatter-back.  The graph-captured update writes its gradients into the same views."""
 
-    def __init__(self, params):
+    def __init__(self, params, extra: int = 1):
         self.params = list(params)
         p0 = self.params[0]
-        self.flat = torch.zeros(sum(p.numel() for p in self.params), device=p0.device, dtype=p0.dtype)
+        n = sum(p.numel() for p in self.params)
+        # `extra` trailing slots ride along in the same message: the graph-captured update's KL mean (ppo.py)
+        self.flat = torch.zeros(n + extra, device=p0.device, dtype=p0.dtype)
+        self.extra = self.flat[n:]
         self.views, off = [], 0
         for p in self.params:
             self.views.append(self.flat[off:off + p.numel()].view_as(p))
@@ -101,6 +104,17 @@ def allreduce_grads(params, flat: FlatGrads | None = None) -> None:
         n = g.numel()
         g.copy_(flat[off:off + n].view_as(g))
         off += n
+
+
+def allreduce_max_int(v: int, device) -> int:
+    """Max of an integer over ranks (the host value is exchanged in a one-element tensor on the backend's device:
+    CUDA for RCCL, CPU for gloo)."""
+    if not is_dist():
+        return int(v)
+    dev = device if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([int(v)], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return int(t.item())
 
 
 def allreduce_mean(t: torch.Tensor) -> torch.Tensor:

@@ -24,7 +24,8 @@ class PPO:
                  lam=0.95, value_loss_coef=1.0, entropy_coef=0.0, learning_rate=1e-3, max_grad_norm=1.0,
                  use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu",
                  normalize_advantage=True, storage_obs_dtype=torch.float32, fused_rollout_inference=False,
-                 fused_rollout_precision="bf16", graph_update=False, update_autocast_bf16=False, **kwargs):
+                 fused_rollout_precision="bf16", graph_update=False, update_autocast_bf16=False,
+                 graph_update_segmented=False, **kwargs):
         self.env = env
         self.device = device
         self.desired_kl = desired_kl
@@ -57,15 +58,24 @@ class PPO:
         # the update's mini-batch step (gather, forward, adaptive learning rate, losses, backward, clip,
         # Adam) captured once in a hipGraph and replayed per mini-batch (single rank, GPU): see _GraphedStep
         self.graph_update = bool(graph_update)
+        # two graph segments with the collectives run eagerly between them: always at world size > 1; this
+        # switch forces it on one rank (tests: the segmented step must equal the single graph)
+        self.graph_update_segmented = bool(graph_update_segmented)
         self._graphed = None
+        self._grads_checked = False  # which parameters the loss reaches (see _check_all_grads)
+        self._unused: set = set()
         # not in the reference (fp32 update): forward/backward of the update under torch.autocast(bf16);
         # the losses' exp / log / sums stay fp32 (autocast's fp32 list), parameters and Adam stay fp32
         self.update_autocast_bf16 = bool(update_autocast_bf16)
         self._flat = None  # gdist.FlatGrads: the parameters' gradients as views of one buffer
 
     def flat_grads(self) -> gdist.FlatGrads:
-        if self._flat is None or self._flat.params[0] is not next(self.policy.parameters()):
-            self._flat = gdist.FlatGrads(self.policy.parameters())
+        """The flat gradient buffer over the parameters the loss reaches (all of them until the first mini-batch
+        has been checked, see _check_all_grads)."""
+        used = [p for p in self.policy.parameters() if id(p) not in self._unused]
+        if self._flat is None or len(self._flat.params) != len(used) or \
+                any(a is not b for a, b in zip(self._flat.params, used)):
+            self._flat = gdist.FlatGrads(used)
         return self._flat
 
     def init_storage(self, training_type, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape,
@@ -158,9 +168,23 @@ class PPO:
             value_loss = (returns_batch - value_batch).pow(2).mean()
         return surrogate_loss, value_loss
 
+    def _check_all_grads(self, loss, params, grads=None):
+        """Find the parameters the loss does not reach (e.g. VisionActorCritic's aux_decoder) and take them out of
+        the flat gradient buffer, with `.grad` None: the reference's `zero_grad()` leaves their `.grad` None and
+        Adam skips them (ppo.py:178-181), where a bound zero `.grad` would count an Adam step for them (and step
+        them by their moments if they ever had any).  Checked once, on the first mini-batch."""
+        if grads is None:
+            grads = torch.autograd.grad(loss, params, retain_graph=True, allow_unused=True)
+        self._unused = {id(p) for p, g in zip(params, grads) if g is None}
+        for p in self.policy.parameters():
+            if id(p) in self._unused:
+                p.grad = None
+        self._grads_checked = True
+        return self.flat_grads()
+
     def update(self):
         if self.graph_update and self.storage is not None and str(self.device).startswith("cuda") \
-                and _graph_capturable_dist() and type(self).update is PPO.update:
+                and type(self).update is PPO.update:
             if self._graphed is None:
                 self._graphed = _GraphedStep(self)
             out = self._graphed.update()
@@ -190,6 +214,9 @@ class PPO:
                                                           returns_batch)
             loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_batch.float().mean()
             self.optimizer.zero_grad(set_to_none=False)  # (in place: the views of the flat buffer stay bound)
+            if not self._grads_checked:
+                flat = self._check_all_grads(loss, params)
+                flat.bind()
             loss.backward()
             gdist.allreduce_grads(params, flat)
             nn.utils.clip_grad_norm_(params, self.max_grad_norm)
@@ -204,18 +231,13 @@ class PPO:
         }
 
 
-def _graph_capturable_dist() -> bool:
-    """One rank, or ranks over RCCL (its collectives can be captured in a hipGraph; gloo's cannot)."""
-    return gdist.world_size() == 1 or dist.get_backend() == "nccl"
-
-
 class _GraphedStep:
-    """PPO.update's mini-batch step as one hipGraph (the same operations as the eager loop, in order).
+    """PPO.update's mini-batch step as hipGraph replays (the same operations as the eager loop).
 
     Per mini-batch the eager loop launches ~150 small kernels and reads the KL back to the host for the
     adaptive learning rate (ppo.py:133-150).  Here the learning-rate rule runs on the device (the same
-    comparisons, in fp32), Adam takes the rate as a device tensor (`capturable=True`), and the whole
-    step (mini-batch gathers from the storage by a static index buffer, forward, losses, backward, grad
+    comparisons, in fp32), Adam takes the rate as a device tensor (`capturable=True`), and the step
+    (mini-batch gathers from the storage by a static index buffer, forward, losses, backward, grad
     clipping, Adam) is captured once and replayed per mini-batch.  Capture needs warm-up steps; the
     parameters, the optimizer state and the rate are snapshotted before and restored after, so training
     is unchanged.  `learning_rate` is read back once per update, for the log.
@@ -223,8 +245,14 @@ class _GraphedStep:
     Gradients: `torch.autograd.grad` into the views of one flat buffer (gdist.FlatGrads, bound as the
     parameters' `.grad` before capture and never rebound), so the captured step does not depend on how
     autograd's gradient accumulation treats an existing `.grad` (an out-of-place accumulation during
-    capture rebinds `.grad` and leaves the graph writing a buffer nobody holds).  With several ranks (RCCL)
-    the gradient all-reduce and the KL mean of the adaptive learning rate are captured in the graph too."""
+    capture rebinds `.grad` and leaves the graph writing a buffer nobody holds).  The mini-batch's local KL
+    mean is written into the flat buffer's extra slot.
+
+    Two segments: A = gathers, forward, KL, losses, backward (into the flat buffer); B = learning-rate rule,
+    clip, Adam.  The rate only enters Adam, so computing it after the backward changes nothing.  With one
+    rank both segments are one graph.  With several ranks (any backend) they are two graphs and the exchange
+    runs eagerly between them: ONE in-place all-reduce of the flat buffer carries the gradients and the KL
+    mean together.  No collective is ever captured."""
 
     def __init__(self, alg: "PPO"):
         self.alg = alg
@@ -245,7 +273,9 @@ class _GraphedStep:
         self.idx = torch.zeros(self.mb, dtype=torch.long, device=dev)
         self.vloss = torch.zeros((), device=dev)
         self.sloss = torch.zeros((), device=dev)
-        self.graph = None
+        self.segmented = gdist.is_dist() or alg.graph_update_segmented
+        self.graph = None  # one rank: the whole step
+        self.graph_b = None  # segmented: graph = segment A, graph_b = segment B
 
     def _sources(self):
         st = self.alg.storage
@@ -255,7 +285,10 @@ class _GraphedStep:
                 st.returns.flatten(0, 1), st.actions_log_prob.flatten(0, 1), st.mu.flatten(0, 1),
                 st.sigma.flatten(0, 1))
 
-    def _step(self):
+    def _adaptive(self) -> bool:
+        return self.alg.desired_kl is not None and self.alg.schedule == "adaptive"
+
+    def _seg_a(self):
         alg, pol = self.alg, self.alg.policy
         obs, priv, act, val, adv, ret, logp, mu, sig = (x.index_select(0, self.idx) for x in self._sources())
         obs, priv = obs.float(), priv.float()
@@ -267,36 +300,42 @@ class _GraphedStep:
             value_b = pol.evaluate(priv)
             mu_b, sigma_b, entropy_b = pol.action_mean, pol.action_std, pol.entropy
         logp_b, value_b, mu_b, sigma_b, entropy_b = (t.float() for t in (logp_b, value_b, mu_b, sigma_b, entropy_b))
-        if alg.desired_kl is not None and alg.schedule == "adaptive":
+        if self._adaptive():
             with torch.no_grad():
                 kl = torch.sum(torch.log(sigma_b / sig + 1.0e-5)
                                + (torch.square(sig) + torch.square(mu - mu_b)) / (2.0 * torch.square(sigma_b)) - 0.5,
                                axis=-1)
-                k = torch.mean(kl)
-                if gdist.is_dist():
-                    dist.all_reduce(k, op=dist.ReduceOp.SUM)
-                    k = k / gdist.world_size()
+                self.flat.extra[0].copy_(torch.mean(kl))
+        surrogate_loss, value_loss = alg._ppo_losses(logp_b, logp, adv, value_b, val, ret)
+        loss = surrogate_loss + alg.value_loss_coef * value_loss - alg.entropy_coef * entropy_b.mean()
+        if not alg._grads_checked:  # (first warm-up step, before any capture)
+            grads = torch.autograd.grad(loss, self.params, retain_graph=True, allow_unused=True)
+            self.flat = alg._check_all_grads(loss, self.params, grads)
+            self.flat.bind()
+        grads = torch.autograd.grad(loss, self.flat.params)
+        torch._foreach_copy_(self.flat.views, list(grads))
+        self.vloss.add_(value_loss.detach())
+        self.sloss.add_(surrogate_loss.detach())
+
+    def _seg_b(self):
+        alg = self.alg
+        if self._adaptive():
+            with torch.no_grad():
+                k = self.flat.extra[0]  # the rank-averaged KL mean once the flat buffer has been all-reduced
                 lr = self.lr
                 up = torch.clamp(lr * 1.5, max=1e-2)
                 down = torch.clamp(lr / 1.5, min=1e-5)
                 lr_new = torch.where(k > alg.desired_kl * 2.0, down,
                                      torch.where((alg.desired_kl / 2.0 > k) & (k > 0.0), up, lr))
                 self.lr.copy_(lr_new)
-        surrogate_loss, value_loss = alg._ppo_losses(logp_b, logp, adv, value_b, val, ret)
-        loss = surrogate_loss + alg.value_loss_coef * value_loss - alg.entropy_coef * entropy_b.mean()
-        grads = torch.autograd.grad(loss, self.params, allow_unused=True)
-        torch._foreach_copy_(self.flat.views, [g if g is not None else torch.zeros_like(v)
-                                               for g, v in zip(grads, self.flat.views)])
-        self.flat.allreduce_()
         nn.utils.clip_grad_norm_(self.params, alg.max_grad_norm)
         self.opt.step()
-        self.vloss.add_(value_loss.detach())
-        self.sloss.add_(surrogate_loss.detach())
 
     def _capture(self):
         # snapshot (parameters, optimizer state, rate), warm up on a side stream, capture, restore
         snap_p = [p.detach().clone() for p in self.params]
         snap_lr = self.lr.clone()
+        snap_v, snap_s = self.vloss.clone(), self.sloss.clone()
         self.flat.bind()  # Adam and the clip read the gradients from these views (static addresses)
         snap_o = {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in self.opt.state[p].items()}
                   for p in self.params}
@@ -306,12 +345,21 @@ class _GraphedStep:
         _lin._FORCE_FN = True  # bias gradients by gr_column_sum in the captured step (linear.bias_grad)
         try:
             with torch.cuda.stream(s):
-                for _ in range(3):
-                    self._step()
+                for _ in range(3):  # (no collective in the warm-up: its results are discarded)
+                    self._seg_a()
+                    self._seg_b()
             torch.cuda.current_stream().wait_stream(s)
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph, stream=s):
-                self._step()
+            if self.segmented:
+                with torch.cuda.graph(self.graph, stream=s):
+                    self._seg_a()
+                self.graph_b = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph_b, stream=s, pool=self.graph.pool()):
+                    self._seg_b()
+            else:
+                with torch.cuda.graph(self.graph, stream=s):
+                    self._seg_a()
+                    self._seg_b()
         finally:
             _lin._FORCE_FN = False
         with torch.no_grad():
@@ -322,6 +370,8 @@ class _GraphedStep:
                     if torch.is_tensor(v):
                         self.opt.state[p][k].copy_(v)
             self.lr.copy_(snap_lr)
+            self.vloss.copy_(snap_v)
+            self.sloss.copy_(snap_s)
 
     def update(self):
         alg = self.alg
@@ -349,6 +399,9 @@ class _GraphedStep:
             for i in range(n):
                 self.idx.copy_(perm[i * self.mb:(i + 1) * self.mb])
                 self.graph.replay()
+                if self.graph_b is not None:
+                    self.flat.allreduce_()  # eager, on the current stream's order: gradients + KL mean, one message
+                    self.graph_b.replay()
         num_updates = alg.num_learning_epochs * n
         alg.learning_rate = float(self.lr)
         alg.storage.clear()

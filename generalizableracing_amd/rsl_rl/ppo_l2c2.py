@@ -105,6 +105,9 @@ class PPOL2C2(PPO):
             smooth_loss, _ = self.smooth_loss(obs_batch, next_obs_batch, cont_batch, mu_batch, value_batch)
             loss = loss + smooth_loss
             self.optimizer.zero_grad(set_to_none=False)
+            if not self._grads_checked:
+                flat = self._check_all_grads(loss, params)
+                flat.bind()
             loss.backward()
             gdist.allreduce_grads(params, flat)
             nn.utils.clip_grad_norm_(params, self.max_grad_norm)

@@ -35,7 +35,9 @@
 extern "C" {
 #endif
 
-#define GR_ABI_VERSION 1
+/* 2: GR_NUM_PLANES 17 (obstacle hint, rotor constants), gr_policy_args.precision, the observation sink and the
+ * status word; gr_policy_args_size */
+#define GR_ABI_VERSION 2
 
 /* ---- status codes ---- */
 #define GR_OK 0
@@ -372,6 +374,8 @@ typedef struct gr_policy_args {
   int32_t reserved;
 } gr_policy_args;
 int gr_policy_forward(const gr_policy_args* args, void* stream);
+/* sizeof(gr_policy_args): the binding checks its mirror against it at load time */
+size_t gr_policy_args_size(void);
 
 /*
  * Training-mode BatchNorm fused with its activation, on channels-last rows x [m][c] (fp32, 16-byte aligned,

@@ -25,3 +25,10 @@ def golden_env():
     import numpy as np
 
     return dict(np.load(os.path.join(ROOT, "tests", "golden", "golden_env.npz")))
+
+
+@pytest.fixture(scope="session")
+def golden_freerun():
+    import numpy as np
+
+    return dict(np.load(os.path.join(ROOT, "tests", "golden", "golden_freerun.npz")))

@@ -79,3 +79,40 @@ def check_step(g, stage, envs_after, reward, terminated, time_out, dones, obs_po
     assert (e["acc"][d] == 0).all()
     assert (e["ep_len"][d] == 0).all()
     assert np.array_equal(e["ep_len"][live], s("ep_len")[live] + 1)
+
+
+def freerun_envs(g, stage):
+    """gro_env records of the free run's initial state (tests/golden/make_golden_freerun.py)."""
+    return envs_from_fixture(g, stage)
+
+
+def check_free_step(g, stage, k, envs_after, reward, terminated, time_out, dones, obs_policy, obs_critic, obs_aux,
+                    start_gate):
+    """Assert step k of the reference free run on the envs its `valid` mask compares (first episode, away from
+    every threshold); returns the number of envs compared."""
+    o = lambda key: g[f"s{stage}_out_{key}"][k]  # noqa: E731
+    v = o("valid").astype(bool)
+    where = f"stage {stage} step {k}"
+    for name, got in (("terminated", terminated), ("time_out", time_out), ("dones", dones)):
+        assert np.array_equal(np.asarray(got).astype(np.uint8)[v], o(name)[v]), (where, name)
+    rscale = max(1.0, float(np.abs(o("reward")[v]).max()))
+    assert np.abs(reward[v].astype(np.float64) - o("reward")[v]).max() <= 2e-5 * rscale, (where, "reward")
+    assert np.array_equal(obs_aux.astype(np.float32)[v], o("obs_aux")[v]), (where, "aux")
+    live = v & (o("dones") == 0)
+    e = envs_after
+    for key, ref in (("p", "post_p"), ("q", "post_q"), ("v", "post_v"), ("w", "post_w")):
+        err = close(e[key][live], o(ref)[live])
+        assert err <= 1e-5, (where, key, err)
+    assert np.array_equal(e["gate_id"][live], o("gate_id_after")[live]), (where, "gate ids")
+    assert np.array_equal(e["acc"][live], o("acc_after")[live].astype(np.int32)), (where, "accumulated gates")
+    for name, got, ref in (("policy", obs_policy, o("obs_policy")), ("critic", obs_critic, o("obs_critic"))):
+        err = close(got[live], ref[live])
+        assert err <= 1e-5, (where, name, err)
+    d = v & (o("dones") != 0)
+    lv_ref = o("level_after")[d]
+    det = lv_ref >= 0
+    assert np.array_equal(e["level"][d][det], lv_ref[det]), (where, "curriculum levels")
+    assert close(e["noise_level"][d], o("noise_level_after")[d], 1e-6) <= 1e-6, (where, "noise level")
+    assert np.array_equal(e["gate_id"][d], start_gate[e["type"][d], e["level"][d]]), (where, "start gate")
+    assert (e["acc"][d] == 0).all() and (e["ep_len"][d] == 0).all()
+    return int(v.sum())

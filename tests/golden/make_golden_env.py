@@ -163,8 +163,10 @@ class Scene(dict):
     pass
 
 
-def reference_step(st, stage, gate_pose, start, origin_z, collide):
-    """One step of the reference composition from pre-state `st` (dict of numpy arrays)."""
+def reference_step(st, stage, gate_pose, start, origin_z, collide, carry=False):
+    """One step of the reference composition from pre-state `st` (dict of numpy arrays).  carry=True also returns
+    what the next step of a free run starts from (make_golden_freerun.py): the controller's filter state and the
+    body angular acceleration of the DroneDynamics step (the D-term input the simulator reports next step)."""
     mdp = il_shim.load_mdp()
     DroneDynamics = mdp["droneDynamics"].DroneDynamics
     DiffActions = mdp["diff_action"].DiffActions
@@ -220,6 +222,14 @@ def reference_step(st, stage, gate_pose, start, origin_z, collide):
     dd = DroneDynamics(n, f32(st["m_plant"]), plant_J, da.dt, 3, random_drag=False, device="cpu")
     dd.drag_coeffs, dd.h_force_drag_coeffs = f32(st["k2"]), f32(st["k1"])
     da.drone_dynamics = dd
+    if carry:  # record DroneDynamics.step's input wrench and pre-step body rate (droneDynamics.py:119-135)
+        dd_step = dd.step
+
+        def step_rec(tt):
+            step_rec.tt, step_rec.wb = tt.clone(), dd.ang_vel_b.clone()
+            return dd_step(tt)
+
+        dd.step = step_rec
     da.thr_est_error = f32(st["thr_err"])
     da.action_lag = 1
     a_prev, a = f32(st["a_prev"]), f32(st["a"])
@@ -328,6 +338,13 @@ def reference_step(st, stage, gate_pose, start, origin_z, collide):
            "gate_id_after": cmd.gate_id, "gate_id_reset": reset_gate,
            "acc_after": cmd.metrics["accumulate_gates"], "level_after": terrain.terrain_levels,
            "noise_level_after": cmd.noise_level[:, 0], "obs_policy": pol, "obs_critic": cri, "obs_aux": aux[:, 0]}
+    if carry:
+        tq, wb = step_rec.tt[:, 1:4], step_rec.wb
+        # alpha as DroneDynamics.step forms it from its own inertia matrices (droneDynamics.py:123)
+        jw = (dd.inertia @ wb.unsqueeze(-1)).squeeze(-1)
+        out["alpha_b"] = (dd.inertia_inv @ tq.unsqueeze(-1)).squeeze(-1) - \
+            (dd.inertia_inv @ torch.linalg.cross(wb, jw).unsqueeze(-1)).squeeze(-1)
+        out["ctrl_T"], out["ctrl_tau"] = ctl.gross_thrust[:, 0].clone(), ctl.torque.clone()
     return {k: v.detach().numpy() for k, v in out.items()}, {k: v.detach().numpy() for k, v in pre.items()}
 
 

@@ -1,0 +1,167 @@
+"""Shared replay of tests/golden/golden_ppo_c2.npz: the reference's PPO (standalone/rsl_rl/ext/algorithms/
+ppo.py:103-190, storage/rollout_storage.py:113-191) at BASELINE C2 size — 4 096 envs x 24 steps, MLP(256, 256),
+5 epochs x 4 mini-batches of 24 576 rows — over plain nn.Linear layers (tests/golden/make_golden_ppo_c2.py).
+
+The rollout (act / process_env_step / compute_returns) runs on the CPU with the reference's generator seeds, so the
+stored actions are the reference's draws; the update runs on `device` with the build's options (eager, or
+graph_update), i.e. TallLinear's split-K weight gradients, gr_column_sum bias gradients (captured step), capturable
+Adam.  Each update draws its mini-batch permutation from the CPU generator at the reference's seed point and moves
+it to the device (torch.randperm is redirected for the duration of update(): the build draws it on the device).
+Teacher forcing across iterations: the second rollout and update start from the reference's parameters.
+
+What is pinned, and how tightly (fp32; the reference's CPU GEMMs and the build's split-K / hipBLASLt GEMMs sum in
+different orders):
+  - the stored returns / advantages / actions / values: sums to 1e-6 of the absolute sum, the first 4 096 to 1e-5;
+  - the gradients Adam receives at the first update's first two mini-batches and at the second update's first one
+    (the same parameters as the reference's there): within 1e-5 of the gradient's norm and of its largest element
+    (measured on the CPU: 3e-7);
+  - the learning rate after each update, exactly (every adaptive decision agrees);
+  - the value loss within 1e-3 relative, the surrogate (a nearly cancelling mean of +-A * ratio, |A| ~ 1) within
+    2e-4 absolute;
+  - the parameters after each update: within 15 % (first update) and 75 % (second) of the update's norm.  These are
+    not loose copies of 1e-5: the reference is chaotic here.  Adam normalises each gradient element, so an element
+    whose gradient is round-off-small moves by up to a learning rate either way; perturbing the reference's own
+    initial parameters by 1e-7 relative moves its parameters by 7.4 % of the first update and 37 % of the second
+    (the build's CPU path: 3.5 % and, with the parameters teacher-forced but Adam's moments its own, 25 %), so 2x
+    the reference's own spread is the bound.  The gradients, the rate and the losses are the tight pins."""
+from __future__ import annotations
+
+import contextlib
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+
+import make_golden_ppo_c2 as mk  # noqa: E402  (rollout_inputs, sizes, hyper-parameters: no reference code)
+
+
+def load():
+    return dict(np.load(os.path.join(HERE, "golden", "golden_ppo_c2.npz")))
+
+
+@contextlib.contextmanager
+def cpu_randperm():
+    orig = torch.randperm
+
+    def rp(n, *args, device=None, **kw):
+        return orig(n, *args, **kw).to(device if device is not None else "cpu")
+
+    torch.randperm = rp
+    try:
+        yield
+    finally:
+        torch.randperm = orig
+
+
+@contextlib.contextmanager
+def record_grads(alg, out, count=2):
+    """Append the gradients Adam receives at the first `count` mini-batch steps of alg.update() to `out`: at the
+    optimizer step (eager) or, for the graph-captured step, from the flat gradient buffer after each replay that
+    ends a step."""
+    params = list(alg.policy.parameters())
+    step = alg.optimizer.step
+    replay = torch.cuda.CUDAGraph.replay
+
+    def step_rec(*a, **kw):
+        if len(out) < count:
+            out.append(torch.cat([p.grad.reshape(-1).detach().cpu() for p in params]))
+        return step(*a, **kw)
+
+    def replay_rec(graph):
+        replay(graph)
+        g = alg._graphed
+        if g is not None and len(out) < count and (g.graph_b is None or graph is g.graph_b):
+            n = sum(p.numel() for p in g.flat.params)
+            assert len(g.flat.params) == len(params)
+            out.append(g.flat.flat[:n].detach().cpu().clone())
+
+    alg.optimizer.step = step_rec
+    torch.cuda.CUDAGraph.replay = replay_rec
+    try:
+        yield
+    finally:
+        torch.cuda.CUDAGraph.replay = replay
+        if alg.optimizer.step is step_rec:
+            alg.optimizer.step = step
+
+
+def _params(alg):
+    return torch.cat([p.detach().reshape(-1).cpu() for p in alg.policy.parameters()]).double()
+
+
+def _set_params(alg, flat):
+    off = 0
+    with torch.no_grad():
+        for p in alg.policy.parameters():
+            p.copy_(torch.from_numpy(flat[off:off + p.numel()]).view_as(p))
+            off += p.numel()
+
+
+def replay(gp, device="cpu", **alg_kw):
+    """Two rollout + update iterations against the fixture; returns the measured deviations."""
+    from generalizableracing_amd.rsl_rl import ActorCritic
+    from generalizableracing_amd.rsl_rl.ppo import PPO
+
+    data = mk.rollout_inputs()
+    chk = np.array([float(x.double().sum()) for d in data for x in d])
+    assert np.array_equal(chk, gp["inputs_checksum"]), "the seeded rollout inputs differ from the fixture's"
+    roll = PPO(mk.make_policy(ActorCritic), None, device="cpu", **mk.HP)
+    assert any(type(m).__name__ == "TallLinear" for m in roll.policy.modules())
+    assert np.array_equal(_params(roll).float().numpy(), gp["init_params"])
+    roll.init_storage("rl", mk.N, mk.T, [mk.OBS], [mk.OBS], [4])
+    upd = PPO(mk.make_policy(ActorCritic), None, device=device, **mk.HP, **alg_kw)
+    upd.init_storage("rl", mk.N, mk.T, [mk.OBS], [mk.OBS], [4])
+    report = []
+    for it, (obs, cobs, rew, dones, tout, last) in enumerate(data):
+        torch.manual_seed(100 + it)
+        with torch.inference_mode():
+            for t in range(mk.T):
+                roll.act(obs[t], cobs[t])
+                roll.process_env_step(rew[t], dones[t], {"time_outs": tout[t]})
+            roll.compute_returns(last)
+        st = roll.storage
+        for k in ("returns", "advantages", "actions", "values"):
+            x = getattr(st, k).double()
+            want = float(gp[f"ppo_it{it}_{k}_sum"])
+            assert abs(float(x.sum()) - want) <= 1e-6 * float(gp[f"ppo_it{it}_{k}_abssum"]), (it, k)
+            np.testing.assert_allclose(getattr(st, k).flatten()[:4096].numpy(), gp[f"ppo_it{it}_{k}_head"],
+                                       rtol=1e-5, atol=1e-6, err_msg=f"it{it} {k}")
+        for name, v in vars(st).items():
+            if torch.is_tensor(v):
+                getattr(upd.storage, name).copy_(v)
+        upd.storage.step = st.step
+        p0 = _params(upd)
+        grads = []
+        torch.manual_seed(200 + it)
+        with cpu_randperm(), record_grads(upd, grads):
+            losses = upd.update()
+        lr_want = float(gp[f"ppo_it{it}_lr"])
+        assert abs(upd.learning_rate - lr_want) <= 1e-6 * lr_want, (it, upd.learning_rate, lr_want)
+        gerr = []
+        # mini-batch 1 of the second update starts from Adam moments that followed the build's own first update
+        for j in range(2 if it == 0 else 1):
+            g, w = grads[j].double(), torch.from_numpy(gp[f"ppo_it{it}_grad_mb{j}"]).double()
+            e_norm, e_max = float((g - w).norm() / w.norm()), float((g - w).abs().max() / w.abs().max())
+            assert e_norm <= 1e-5 and e_max <= 1e-5, (it, j, e_norm, e_max)
+            gerr.append(max(e_norm, e_max))
+        for k, v in losses.items():
+            want = float(gp[f"ppo_it{it}_loss_{k}"])
+            tol = 2e-4 if k == "surrogate" else 1e-3 * max(abs(want), 1e-3)
+            assert abs(v - want) <= tol, (it, k, v, want)
+        got, want = _params(upd), torch.from_numpy(gp[f"ppo_it{it}_params"]).double()
+        dev = float((got - want).norm() / (want - p0).norm())
+        assert dev <= (0.15, 0.75)[it], (it, dev)
+        report.append({"grad_err": max(gerr), "param_dev_of_update": dev,
+                       "value_loss_rel": abs(losses["value_function"] - float(gp[f"ppo_it{it}_loss_value_function"]))
+                       / abs(float(gp[f"ppo_it{it}_loss_value_function"]))})
+        # teacher forcing: the next rollout and update start from the reference's parameters (Adam's moments and
+        # the learning rate are the build's own)
+        for alg in (roll, upd):
+            _set_params(alg, gp[f"ppo_it{it}_params"])
+        roll.learning_rate = upd.learning_rate
+        roll.storage.clear()
+    return report
