@@ -355,6 +355,50 @@ def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False, graph_up
     return float(np.median(fps))
 
 
+def regeneration_cost(device, n, interval=256, plain=64):
+    """the interval step that regenerates the terrain (mdp/events.py:180-204) against a plain step,
+    both eager from Python with a device synchronisation after each (wall time).  The next generation is built on
+    the background thread from half-way through the interval and uploaded on a side stream; the regenerating step
+    swaps the tables on the stream (gr_swap_terrain) and resets every env.  The build's own duration (host, in the
+    background) is reported beside it."""
+    cfg = RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=device), stage=1,
+                       terrain=TerrainCfg(num_gates=8, obstacles=True, regen_interval_s=0.03 * interval))
+    env = RacingEnv(cfg)
+    env.reset()
+    g = torch.Generator(device=device).manual_seed(5)
+    acts = torch.randn(8, n, 4, device=device, generator=g)
+    for k in range(interval - 1 - plain):
+        env.step(acts[k % 8])
+    torch.cuda.synchronize()
+    t_build0 = time.perf_counter()
+    while env._next_terrain is not None and not env._next_terrain.done():
+        time.sleep(0.01)
+    build_wait = time.perf_counter() - t_build0
+    times = []
+    for k in range(plain):
+        t0 = time.perf_counter()
+        env.step(acts[k % 8])
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    assert env.common_step_counter % env._regen_steps == env._regen_steps - 1
+    t0 = time.perf_counter()
+    _, _, _, _, extras = env.step(acts[0])
+    torch.cuda.synchronize()
+    t_regen = time.perf_counter() - t0
+    assert extras.get("terrain_regenerated") and env.terrain_generation == 1
+    t0 = time.perf_counter()
+    env._build_terrain(env._terrain_seed(2))
+    t_build = time.perf_counter() - t0
+    env.close()
+    plain_us = float(np.median(times)) * 1e6
+    return {"plain_step_wall_us": plain_us, "regenerating_step_wall_us": t_regen * 1e6,
+            "ratio": t_regen * 1e6 / plain_us, "background_build_s": t_build,
+            "host_wait_for_build_s_before_timing": build_wait,
+            "note": f"{n} envs, obstacle tracks, eager env.step + synchronize per step; the build runs on a host "
+                    "thread from half-way through the interval, its upload on a side stream; the interval step swaps "
+                    "the tables on the stream and resets every env (reset + observation launches)"}
+
+
 def cpu_baseline(seconds: float, n: int = 65536, obstacles: bool = True):
     """The CPU oracle (C restatement of the reference step, OpenMP over envs) on a bounded sample
     of the same workload: n envs stepped for about `seconds`."""
@@ -532,6 +576,8 @@ def main():
         env_c5.close()
         progress("c5_32_gates")
     if not a.no_extras:
+        extra["terrain_regeneration"] = regeneration_cost(device, n)
+        progress("terrain_regeneration")
         extra["train_total_fps_4096_envs"] = train_fps(device)
         extra["train_total_fps_4096_envs_graph_update"] = train_fps(device, graph_update=True)
         extra["train_total_fps_65536_envs"] = {

@@ -221,7 +221,7 @@ STATUS_TEXT = {GR_STATUS_OBST_WAIT_TIMEOUT: "a physics wave gave up waiting for 
 
 EXPORTS = [
     "gr_abi_version", "gr_config_default", "gr_config_size", "gr_create", "gr_destroy", "gr_last_error",
-    "gr_num_blocks", "gr_num_log_rows", "gr_log_finalize", "gr_bytes_per_env_step", "gr_bind_tracks", "gr_bind_obstacles", "gr_bind_buffers", "gr_bind_obs_sink", "gr_init", "gr_reset",
+    "gr_num_blocks", "gr_num_log_rows", "gr_log_finalize", "gr_bytes_per_env_step", "gr_bind_tracks", "gr_bind_obstacles", "gr_swap_terrain", "gr_bind_buffers", "gr_bind_obs_sink", "gr_init", "gr_reset",
     "gr_step", "gr_observe", "gr_device_status", "gr_test_inject_fault", "gr_set_timing", "gr_read_timing", "gr_test_dynamics", "gr_test_math",
     "gr_test_philox",
     "gr_debug_read_stamps", "gr_debug_read_policy_stamps",
@@ -249,6 +249,7 @@ def _declare(lib):
         "gr_bytes_per_env_step": (C.c_int, [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
         "gr_bind_tracks": (C.c_int, [vp, vp, vp]),
         "gr_bind_obstacles": (C.c_int, [vp, C.POINTER(GrObstacles)]),
+        "gr_swap_terrain": (C.c_int, [vp, vp, vp, vp, C.POINTER(GrObstacles), C.POINTER(GrObstacles), vp]),
         "gr_bind_buffers": (C.c_int, [vp, C.POINTER(GrBuffers)]),
         "gr_bind_obs_sink": (C.c_int, [vp, vp, vp, C.c_int]),
         "gr_init": (C.c_int, [vp, vp]),

@@ -300,54 +300,120 @@ int gr_bytes_per_env_step(const gr_ctx* c, int64_t* rd, int64_t* wr) {
   return GR_OK;
 }
 
-int gr_bind_tracks(gr_ctx* c, const float* gates, const float* tracks) {
-  if (!c || !gates || !tracks) return fail(c, GR_ERR_ARG, "gr_bind_tracks: null pointer");
+// track records [ntr][GR_TRACK_FLOATS] (host copy): finite heights, 2 <= gates <= max_gates, start gate in range
+static int check_track_records(gr_ctx* c, const float* h, const char* who) {
   const gr_config& g = c->cfg;
   const int ntr = g.num_types * g.num_levels;
-  std::vector<float> h((size_t)ntr * GR_TRACK_FLOATS);
-  hipError_t e = hipMemcpy(h.data(), tracks, h.size() * sizeof(float), hipMemcpyDeviceToHost);
-  if (e != hipSuccess) return hip_fail(c, e, "gr_bind_tracks: copy track records");
   for (int t = 0; t < ntr; ++t) {
     const float* r = &h[(size_t)t * GR_TRACK_FLOATS];
     const int start = (int)r[2], ng = (int)r[3];
     if (!(std::isfinite(r[0]) && std::isfinite(r[1])) || ng < 2 || ng > g.max_gates || start < 0 || start >= ng ||
         (float)start != r[2] || (float)ng != r[3])
-      return fail(c, GR_ERR_ARG, "gr_bind_tracks: invalid track record " + std::to_string(t));
+      return fail(c, GR_ERR_ARG, std::string(who) + ": invalid track record " + std::to_string(t));
   }
+  return GR_OK;
+}
+
+// pack the device gate table + track records into the context's table (stream-ordered; allocated once)
+static int pack_tracks(gr_ctx* c, const float* gates, const float* tracks, hipStream_t s, const char* who) {
+  const gr_config& g = c->cfg;
+  const int ntr = g.num_types * g.num_levels;
   const size_t stride = (size_t)c->kc.track_stride;
+  hipError_t e = hipSuccess;
   if (!c->table) {
     e = hipMalloc(&c->table, (size_t)ntr * stride * sizeof(float));
-    if (e != hipSuccess) return hip_fail(c, e, "gr_bind_tracks: hipMalloc");
+    if (e != hipSuccess) return hip_fail(c, e, "hipMalloc (track table)");
   }
   const size_t gb = (size_t)g.max_gates * GR_GATE_FLOATS * sizeof(float);
-  e = hipMemcpy2D(c->table, stride * sizeof(float), gates, gb, gb, ntr, hipMemcpyDeviceToDevice);
-  if (e != hipSuccess) return hip_fail(c, e, "gr_bind_tracks: pack gates");
-  e = hipMemcpy2D(c->table + (size_t)g.max_gates * GR_GATE_FLOATS, stride * sizeof(float), tracks,
-                  GR_TRACK_FLOATS * sizeof(float), GR_TRACK_FLOATS * sizeof(float), ntr, hipMemcpyDeviceToDevice);
-  if (e != hipSuccess) return hip_fail(c, e, "gr_bind_tracks: pack track records");
-  e = hipDeviceSynchronize();
-  if (e != hipSuccess) return hip_fail(c, e, "gr_bind_tracks: sync");
+  e = hipMemcpy2DAsync(c->table, stride * sizeof(float), gates, gb, gb, ntr, hipMemcpyDeviceToDevice, s);
+  if (e == hipSuccess)
+    e = hipMemcpy2DAsync(c->table + (size_t)g.max_gates * GR_GATE_FLOATS, stride * sizeof(float), tracks,
+                         GR_TRACK_FLOATS * sizeof(float), GR_TRACK_FLOATS * sizeof(float), ntr,
+                         hipMemcpyDeviceToDevice, s);
+  if (e != hipSuccess) return hip_fail(c, e, who);
   c->args.table = c->table;
   c->have_tracks = true;
+  return GR_OK;
+}
+
+int gr_bind_tracks(gr_ctx* c, const float* gates, const float* tracks) {
+  if (!c || !gates || !tracks) return fail(c, GR_ERR_ARG, "gr_bind_tracks: null pointer");
+  const int ntr = c->cfg.num_types * c->cfg.num_levels;
+  std::vector<float> h((size_t)ntr * GR_TRACK_FLOATS);
+  hipError_t e = hipMemcpy(h.data(), tracks, h.size() * sizeof(float), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(c, e, "gr_bind_tracks: copy track records");
+  int rc = check_track_records(c, h.data(), "gr_bind_tracks");
+  if (rc != GR_OK) return rc;
+  rc = pack_tracks(c, gates, tracks, nullptr, "gr_bind_tracks: pack");
+  if (rc != GR_OK) return rc;
+  e = hipDeviceSynchronize();
+  return e == hipSuccess ? GR_OK : hip_fail(c, e, "gr_bind_tracks: sync");
+}
+
+// obstacle index arrays (host copies: counts [ntr], grid_f / grid_i [ntr][4], cells [num_cells][2]) against the sizes
+static int check_obstacles(gr_ctx* c, const gr_obstacles* o, const int32_t* cnt, const float* gf, const int32_t* gi,
+                           const int32_t* cells, const char* who) {
+  const int ntr = c->cfg.num_types * c->cfg.num_levels;
+  for (int t = 0; t < ntr; ++t) {
+    const int nx = gi[4 * t], ny = gi[4 * t + 1], first = gi[4 * t + 2];
+    if (cnt[t] < 0 || cnt[t] > o->max_obstacles || nx < 0 || ny < 0 || first < 0 ||
+        (long)first + (long)nx * ny > o->num_cells)
+      return fail(c, GR_ERR_ARG, std::string(who) + ": invalid count / grid of track " + std::to_string(t));
+  }
+  for (int k = 0; k < o->num_cells; ++k)
+    if (cells[2 * k] < 0 || cells[2 * k + 1] < 0 || (long)cells[2 * k] + cells[2 * k + 1] > o->num_items)
+      return fail(c, GR_ERR_ARG, std::string(who) + ": cell " + std::to_string(k) + " out of the item range");
+  // one cell size and margin for all tracks (the per-env hints carry only the grown cell's corner)
+  for (int t = 0; t < ntr; ++t)
+    if (!(gf[4 * t + 2] > 0.0f) || !(gf[4 * t + 3] >= 0.0f) || gf[4 * t + 2] != gf[2] || gf[4 * t + 3] != gf[3])
+      return fail(c, GR_ERR_ARG, std::string(who) + ": every track needs the same 1/cell > 0 and margin >= 0");
+  return GR_OK;
+}
+
+static int check_obstacle_arrays(gr_ctx* c, const gr_obstacles* o, const char* who) {
+  if (!o->records || !o->counts || !o->grid_f || !o->grid_i || !o->cells || !o->items || o->max_obstacles <= 0 ||
+      o->num_cells <= 0 || o->num_items <= 0)
+    return fail(c, GR_ERR_ARG, std::string(who) + ": null array or empty size");
+  if (!aligned16(o->records) || !aligned16(o->grid_f) || !aligned16(o->grid_i) || !aligned16(o->items) ||
+      (reinterpret_cast<uintptr_t>(o->cells) & 7u))
+    return fail(c, GR_ERR_ARG, std::string(who) + ": records / grids / items must be 16-byte aligned, cells 8-byte");
+  return GR_OK;
+}
+
+static void unbind_obstacles(gr_ctx* c) {
+  std::memset(&c->obst, 0, sizeof(c->obst));
+  c->args.obst_grid_f = nullptr;
+  c->args.obst_grid_i = nullptr;
+  c->args.obst_cells = nullptr;
+  c->args.obst_items = nullptr;
+}
+
+// bind validated obstacle arrays and clear the per-env hints (they refer to the previous table) on stream s
+static int attach_obstacles(gr_ctx* c, const gr_obstacles* o, float inv_cell, float margin_cells, hipStream_t s,
+                            const char* who) {
+  const float cell = 1.0f / inv_cell, margin = margin_cells * cell;
+  c->args.h.obst_span = cell + 2.0f * margin;
+  if (c->have_buf) {
+    hipError_t e = hipMemsetAsync(c->buf.state + (size_t)GR_P_OHINT * c->cfg.num_envs * 4, 0,
+                                  (size_t)c->cfg.num_envs * 16, s);
+    if (e != hipSuccess) return hip_fail(c, e, who);
+  }
+  c->obst = *o;
+  c->args.obst_grid_f = reinterpret_cast<const float4*>(o->grid_f);
+  c->args.obst_grid_i = reinterpret_cast<const int4*>(o->grid_i);
+  c->args.obst_cells = reinterpret_cast<const int2*>(o->cells);
+  c->args.obst_items = reinterpret_cast<const float4*>(o->items);
   return GR_OK;
 }
 
 int gr_bind_obstacles(gr_ctx* c, const gr_obstacles* o) {
   if (!c) return GR_ERR_ARG;
   if (!o) {
-    std::memset(&c->obst, 0, sizeof(c->obst));
-    c->args.obst_grid_f = nullptr;
-    c->args.obst_grid_i = nullptr;
-    c->args.obst_cells = nullptr;
-    c->args.obst_items = nullptr;
+    unbind_obstacles(c);
     return GR_OK;
   }
-  if (!o->records || !o->counts || !o->grid_f || !o->grid_i || !o->cells || !o->items || o->max_obstacles <= 0 ||
-      o->num_cells <= 0 || o->num_items <= 0)
-    return fail(c, GR_ERR_ARG, "gr_bind_obstacles: null array or empty size");
-  if (!aligned16(o->records) || !aligned16(o->grid_f) || !aligned16(o->grid_i) || !aligned16(o->items) ||
-      (reinterpret_cast<uintptr_t>(o->cells) & 7u))
-    return fail(c, GR_ERR_ARG, "gr_bind_obstacles: records / grids / items must be 16-byte aligned, cells 8-byte");
+  int rc = check_obstacle_arrays(c, o, "gr_bind_obstacles");
+  if (rc != GR_OK) return rc;
   const int ntr = c->cfg.num_types * c->cfg.num_levels;
   std::vector<int32_t> cnt(ntr), gi((size_t)ntr * 4), cells((size_t)o->num_cells * 2);
   std::vector<float> gf((size_t)ntr * 4);
@@ -356,32 +422,39 @@ int gr_bind_obstacles(gr_ctx* c, const gr_obstacles* o) {
   if (e == hipSuccess) e = hipMemcpy(gi.data(), o->grid_i, gi.size() * 4, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(cells.data(), o->cells, cells.size() * 4, hipMemcpyDeviceToHost);
   if (e != hipSuccess) return hip_fail(c, e, "gr_bind_obstacles: copy index arrays");
-  for (int t = 0; t < ntr; ++t) {
-    const int nx = gi[4 * t], ny = gi[4 * t + 1], first = gi[4 * t + 2];
-    if (cnt[t] < 0 || cnt[t] > o->max_obstacles || nx < 0 || ny < 0 || first < 0 ||
-        (long)first + (long)nx * ny > o->num_cells)
-      return fail(c, GR_ERR_ARG, "gr_bind_obstacles: invalid count / grid of track " + std::to_string(t));
+  rc = check_obstacles(c, o, cnt.data(), gf.data(), gi.data(), cells.data(), "gr_bind_obstacles");
+  if (rc != GR_OK) return rc;
+  rc = attach_obstacles(c, o, gf[2], gf[3], nullptr, "gr_bind_obstacles: clear hints");
+  if (rc != GR_OK) return rc;
+  e = hipDeviceSynchronize();
+  return e == hipSuccess ? GR_OK : hip_fail(c, e, "gr_bind_obstacles: sync");
+}
+
+int gr_swap_terrain(gr_ctx* c, const float* gates, const float* tracks, const float* tracks_host,
+                    const gr_obstacles* obst, const gr_obstacles* obst_host, void* stream) {
+  if (!c || !gates || !tracks || !tracks_host) return fail(c, GR_ERR_ARG, "gr_swap_terrain: null pointer");
+  int rc = check_track_records(c, tracks_host, "gr_swap_terrain");
+  if (rc != GR_OK) return rc;
+  if (obst) {
+    if (!obst_host || !obst_host->counts || !obst_host->grid_f || !obst_host->grid_i || !obst_host->cells)
+      return fail(c, GR_ERR_ARG, "gr_swap_terrain: obstacles need their host index arrays");
+    rc = check_obstacle_arrays(c, obst, "gr_swap_terrain");
+    if (rc != GR_OK) return rc;
+    if (obst_host->num_cells != obst->num_cells || obst_host->num_items != obst->num_items ||
+        obst_host->max_obstacles != obst->max_obstacles)
+      return fail(c, GR_ERR_ARG, "gr_swap_terrain: host and device obstacle sizes differ");
+    rc = check_obstacles(c, obst, obst_host->counts, obst_host->grid_f, obst_host->grid_i, obst_host->cells,
+                         "gr_swap_terrain");
+    if (rc != GR_OK) return rc;
   }
-  for (int k = 0; k < o->num_cells; ++k)
-    if (cells[2 * k] < 0 || cells[2 * k + 1] < 0 || (long)cells[2 * k] + cells[2 * k + 1] > o->num_items)
-      return fail(c, GR_ERR_ARG, "gr_bind_obstacles: cell " + std::to_string(k) + " out of the item range");
-  // one cell size and margin for all tracks (the per-env hints carry only the grown cell's corner)
-  for (int t = 0; t < ntr; ++t)
-    if (!(gf[4 * t + 2] > 0.0f) || !(gf[4 * t + 3] >= 0.0f) || gf[4 * t + 2] != gf[2] || gf[4 * t + 3] != gf[3])
-      return fail(c, GR_ERR_ARG, "gr_bind_obstacles: every track needs the same 1/cell > 0 and margin >= 0");
-  const float cell = 1.0f / gf[2], margin = gf[3] * cell;
-  c->args.h.obst_span = cell + 2.0f * margin;
-  // hints refer to the previous obstacle table: clear them (all-zero = no hint)
-  if (c->have_buf) {
-    e = hipMemset(c->buf.state + (size_t)GR_P_OHINT * c->cfg.num_envs * 4, 0, (size_t)c->cfg.num_envs * 16);
-    if (e != hipSuccess) return hip_fail(c, e, "gr_bind_obstacles: clear hints");
+  const hipStream_t s = (hipStream_t)stream;
+  rc = pack_tracks(c, gates, tracks, s, "gr_swap_terrain: pack");
+  if (rc != GR_OK) return rc;
+  if (!obst) {
+    unbind_obstacles(c);
+    return GR_OK;
   }
-  c->obst = *o;
-  c->args.obst_grid_f = reinterpret_cast<const float4*>(o->grid_f);
-  c->args.obst_grid_i = reinterpret_cast<const int4*>(o->grid_i);
-  c->args.obst_cells = reinterpret_cast<const int2*>(o->cells);
-  c->args.obst_items = reinterpret_cast<const float4*>(o->items);
-  return GR_OK;
+  return attach_obstacles(c, obst, obst_host->grid_f[2], obst_host->grid_f[3], s, "gr_swap_terrain: clear hints");
 }
 
 int gr_bind_buffers(gr_ctx* c, const gr_buffers* b) {

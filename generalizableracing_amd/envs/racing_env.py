@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes as C
 from collections.abc import Mapping
+from concurrent.futures import ThreadPoolExecutor
 
 import torch
 
@@ -111,9 +112,15 @@ class RacingEnv:
 
         # ---- track table + obstacles (host-generated, then device-resident) ----
         self.terrain_generation = 0
-        self._load_terrain(cfg.terrain.seed + cfg.track_seed_offset)
+        self._load_terrain(self._terrain_seed(0))
         interval = cfg.terrain.regen_interval_s
         self._regen_steps = None if interval is None else max(1, int(round(interval / self.step_dt)))
+        # periodic regeneration: the next generation's tables are built on a background host thread from half-way
+        # through the interval, so the interval step only swaps them in (gr_swap_terrain, no host synchronisation)
+        self._builder = ThreadPoolExecutor(max_workers=1, thread_name_prefix="gr-terrain") \
+            if self._regen_steps is not None else None
+        self._next_terrain = None
+        self._held_terrain = None  # the previous generation's device / pinned tensors (alive until the next swap)
 
         # ---- state (SoA float4 planes) and outputs ----
         n = self.num_envs
@@ -152,19 +159,54 @@ class RacingEnv:
                 self._cam_bufs.append(cb)
         self.extras: dict = {}
         self._sink = None  # (policy, critic) tensors of the bound observation sink
+        # fp32 sink = the calls' observation OUTPUT (set_obs_sink): the rows are written once, into the storage slot
+        self._sink_out = None
+        self._last_rows = None  # (policy, critic) rows the last call wrote, if not the output set's
         # startup (gr_init): nominal state, startup DR events, initial terrain levels
         self._bind(0)
         self._call("gr_init", self._stream())
         self._calls, self._cur = 1, 1  # gr_init wrote output set 1 (binding 0); counters zeroed
 
     # ------------------------------------------------------------------ terrain
+    def _terrain_seed(self, generation: int) -> int:
+        """The track seed of terrain generation g of this shard (generation 0 at start-up)."""
+        return self.cfg.terrain.seed + self.cfg.track_seed_offset + 1000003 * generation
+
+    def _build_terrain(self, seed: int):
+        t = self.cfg.terrain
+        return build_tracks(num_types=t.num_cols, num_levels=t.num_rows, num_gates=t.num_gates, seed=seed,
+                            obstacles=t.obstacles, cell=t.obstacle_cell)
+
+    def _start_next_terrain(self):
+        """Build generation terrain_generation + 1 on the background thread (host numpy, the reference's generator
+        restated: tracks.py), pinned for an asynchronous upload."""
+        if self._builder is None:
+            return
+        g = self.terrain_generation + 1
+
+        dev = self.device
+        side = self._upload_stream = getattr(self, "_upload_stream", None) or torch.cuda.Stream(dev)
+
+        def work():
+            gates, recs, obst = self._build_terrain(self._terrain_seed(g))
+            pin = {"gates": torch.from_numpy(gates).pin_memory(), "records": torch.from_numpy(recs).pin_memory()}
+            if obst is not None:
+                for k in ("records", "counts", "grid_f", "grid_i", "cells", "items"):
+                    pin["o_" + k] = torch.from_numpy(getattr(obst, k)).pin_memory()
+            # uploaded ahead on a side stream; the swap makes the env's stream wait for this event (no host wait)
+            with torch.cuda.stream(side):
+                dv = {k: v.to(dev, non_blocking=True) for k, v in pin.items()}
+                done = torch.cuda.Event()
+                done.record(side)
+            return g, gates, recs, obst, pin, dv, done
+
+        self._next_terrain = self._builder.submit(work)
+
     def _load_terrain(self, seed: int):
         """Generate the track table (gates + obstacles) for `seed` and bind it (gr_bind_tracks,
         gr_bind_obstacles).  The tables are copied / referenced by the context; the tensors stay
         alive on the env."""
-        t = self.cfg.terrain
-        gates, recs, obst = build_tracks(num_types=t.num_cols, num_levels=t.num_rows, num_gates=t.num_gates,
-                                         seed=seed, obstacles=t.obstacles, cell=t.obstacle_cell)
+        gates, recs, obst = self._build_terrain(seed)
         dev = self.device
         self.track_gates = torch.from_numpy(gates).to(dev).contiguous()
         self.track_records = torch.from_numpy(recs).to(dev).contiguous()
@@ -188,10 +230,52 @@ class RacingEnv:
 
     def regenerate_terrain(self):
         """EventCfg.reset_terrain -> reset_terrain_period (mdp/events.py:180-204): a new terrain
-        (next seed of this shard's stream), then env.reset() of every env."""
-        torch.cuda.current_stream(self.device).synchronize()  # the old tables may still be read
-        self.terrain_generation += 1
-        self._load_terrain(self.cfg.terrain.seed + self.cfg.track_seed_offset + 1000003 * self.terrain_generation)
+        (next seed of this shard's stream), then env.reset() of every env.
+
+        The tables come from the background builder (started when the previous generation bound); the swap is
+        ordered on the stream (gr_swap_terrain: asynchronous uploads from pinned memory, tables packed and hints
+        cleared on the device), so the host does not wait for the GPU and only waits for the builder if the
+        interval was shorter than a build."""
+        g = self.terrain_generation + 1
+        dev = self.device
+        if self._next_terrain is not None:
+            g_built, gates, recs, obst, pin, dv, done = self._next_terrain.result()
+            assert g_built == g
+            cur = torch.cuda.current_stream(dev)
+            cur.wait_event(done)
+            for v in dv.values():  # (allocated on the side stream, used on this one from now on)
+                v.record_stream(cur)
+        else:  # (not started: an interval of one step, or a direct call) built here
+            gates, recs, obst = self._build_terrain(self._terrain_seed(g))
+            pin = {"gates": torch.from_numpy(gates), "records": torch.from_numpy(recs)}
+            if obst is not None:
+                for k in ("records", "counts", "grid_f", "grid_i", "cells", "items"):
+                    pin["o_" + k] = torch.from_numpy(getattr(obst, k))
+            dv = {k: v.to(dev) for k, v in pin.items()}
+        self._next_terrain = None
+        self._held_terrain = (self.track_gates, self.track_records, self.obstacles, pin)
+        self.track_gates, self.track_records = dv["gates"], dv["records"]
+        recs_h = C.c_void_p(recs.ctypes.data)
+        if obst is None:
+            self.obstacles = None
+            self._call("gr_swap_terrain", self.track_gates.data_ptr(), self.track_records.data_ptr(), recs_h, None, None,
+                       self._stream())
+        else:
+            self.obstacles = {k: dv["o_" + k] for k in ("records", "counts", "grid_f", "grid_i", "cells", "items")}
+            o, oh = _abi.GrObstacles(), _abi.GrObstacles()
+            for k, v in self.obstacles.items():
+                setattr(o, k, v.data_ptr())
+            for k in ("counts", "grid_f", "grid_i", "cells"):
+                setattr(oh, k, getattr(obst, k).ctypes.data)
+            for x in (o, oh):
+                x.max_obstacles = obst.max_obstacles
+                x.num_cells = int(obst.cells.shape[0])
+                x.num_items = int(obst.items.shape[0])
+            self._obst_struct = o
+            self._call("gr_swap_terrain", self.track_gates.data_ptr(), self.track_records.data_ptr(), recs_h,
+                       C.byref(o), C.byref(oh), self._stream())
+        self.obstacle_table = obst
+        self.terrain_generation = g
         return self.reset()
 
     # ------------------------------------------------------------------ plumbing
@@ -230,7 +314,14 @@ class RacingEnv:
         return b
 
     def _bind(self, k: int):
-        self._call("gr_bind_buffers", C.byref(self._bufs[k % LOG_RING]))
+        b = self._bufs[k % LOG_RING]
+        if self._sink_out is not None or self._last_rows is not None:
+            b = _abi.GrBuffers.from_buffer_copy(b)
+            if self._last_rows is not None:  # gr_reset / gr_observe carry the last action from the rows last written
+                b.prev_obs_critic = self._last_rows[1].data_ptr()
+            if self._sink_out is not None:
+                b.obs_policy, b.obs_critic = self._sink_out[0].data_ptr(), self._sink_out[1].data_ptr()
+        self._call("gr_bind_buffers", C.byref(b))
         if getattr(self, "camera", None) is not None:
             self._call("gr_bind_camera_buffers", C.byref(self._cam_bufs[(k + 1) % 2]))
 
@@ -252,6 +343,7 @@ class RacingEnv:
         self._bind(k)
         self._calls += 1
         self._cur = (k + 1) % 2
+        self._last_rows = self._sink_out
         lg = _EpisodeLog(self, k, self._log_keys)
         self._logs[k % LOG_RING] = lg
         return self._sets[self._cur], lg
@@ -284,10 +376,14 @@ class RacingEnv:
         if self.camera is not None:
             img = self._img_sets[self._cur]
             return {"policy": img["policy"], "critic": img["critic"], "auxiliary": s["auxiliary"]}
+        if self._last_rows is not None:  # the last call wrote its rows into the bound fp32 sink
+            return {"policy": self._last_rows[0], "critic": self._last_rows[1], "auxiliary": s["auxiliary"]}
         return {"policy": s["policy"], "critic": s["critic"], "auxiliary": s["auxiliary"]}
 
     def state_obs(self) -> dict:
         """The 16 state terms of the last call (without the image)."""
+        if self._last_rows is not None:
+            return {"policy": self._last_rows[0], "critic": self._last_rows[1]}
         s = self._sets[self._cur]
         return {"policy": s["policy"], "critic": s["critic"]}
 
@@ -385,8 +481,12 @@ class RacingEnv:
         self._render(_abi.GR_CAM_STEP)
         self.common_step_counter += 1
         self.extras = {"log": log}
-        if self._regen_steps is not None and self.common_step_counter % self._regen_steps == 0:
-            self._regenerate_in_step()
+        if self._regen_steps is not None:
+            phase = self.common_step_counter % self._regen_steps
+            if phase == 0:
+                self._regenerate_in_step()
+            elif phase == self._regen_steps // 2 and self._next_terrain is None:
+                self._start_next_terrain()
         return self._obs_dict(out), out["reward"], out["terminated"], out["time_out"], self.extras
 
     def _regenerate_in_step(self):
@@ -401,7 +501,9 @@ class RacingEnv:
         observation rows only; set A's rows are then restored.  The next step (call k+3) writes set A and
         reads the post-reset rows of set B as its previous observation."""
         held = self._sets[(self._cur + 1) % 2]
-        keys = ("policy", "critic", "auxiliary")
+        # (with the fp32 sink as the output the reset and observation passes write the step's slot, which is what
+        # the step returns; the runner's previous slot is not touched)
+        keys = ("auxiliary",) if self._sink_out is not None else ("policy", "critic", "auxiliary")
         saved = [held[k].clone() for k in keys]
         if self.camera is not None:
             held_img = self._img_sets[(self._cur + 1) % 2]
@@ -433,12 +535,15 @@ class RacingEnv:
         return self._obs_dict(out), self.extras
 
     def set_obs_sink(self, policy: torch.Tensor | None, critic: torch.Tensor | None = None):
-        """gr_bind_obs_sink: the following step / reset / observe calls also write their policy and critic rows
-        into these [num_envs, 16] tensors (float32 or bfloat16; bf16 rounds to nearest even like torch's cast) —
-        the rollout storage's slot for the next transition (config C5's bf16 rollout buffers without a copy-cast
-        pass).  None unbinds.  State task only (the image rows of the camera task are not sunk)."""
+        """The following step / reset / observe calls put their policy and critic rows into these [num_envs, 16]
+        tensors — the rollout storage's slot for the next transition — instead of the storage copying them
+        (rollout_storage.py:74-88).  float32: the tensors become the calls' observation output (written once, and
+        returned by the calls); bfloat16 (config C5's bf16 rollout buffers): gr_bind_obs_sink, the kernel writes
+        the fp32 output rows and their round-to-nearest-even bf16 copy.  None unbinds.  State task only (the image
+        rows of the camera task are not sunk)."""
         if policy is None:
             self._sink = None
+            self._sink_out = None
             self._call("gr_bind_obs_sink", None, None, _abi.GR_DTYPE_F32)
             return
         if self.camera is not None:
@@ -451,9 +556,17 @@ class RacingEnv:
                                  f"float32 / bfloat16 tensors on {self.device}")
         if critic.dtype != policy.dtype:
             raise ValueError("set_obs_sink: policy and critic sinks must share a dtype")
-        dtype = _abi.GR_DTYPE_BF16 if policy.dtype == torch.bfloat16 else _abi.GR_DTYPE_F32
         self._sink = (policy, critic)  # kept alive while bound
-        self._call("gr_bind_obs_sink", policy.data_ptr(), critic.data_ptr(), dtype)
+        if policy.dtype == torch.float32:
+            # fp32: the tensors ARE the calls' observation output (the rows are written once; the calls return
+            # these tensors), rollout_storage.py:74-88's copy with no second write
+            self._sink_out = (policy, critic)
+            self._call("gr_bind_obs_sink", None, None, _abi.GR_DTYPE_F32)
+            return
+        # bf16: the fp32 rows stay the output (the rollout inference reads them) and the kernel also writes the
+        # rounded rows into the slot
+        self._sink_out = None
+        self._call("gr_bind_obs_sink", policy.data_ptr(), critic.data_ptr(), _abi.GR_DTYPE_BF16)
 
     def observe(self) -> dict:
         """ObservationManager.compute(): fresh observation noise, no state change."""
@@ -466,6 +579,9 @@ class RacingEnv:
         return seed
 
     def close(self):
+        if getattr(self, "_builder", None) is not None:
+            self._builder.shutdown(wait=False, cancel_futures=True)
+            self._builder = None
         if getattr(self, "_ctx", None):
             self._lib.gr_destroy(self._ctx)
             self._ctx = None

@@ -294,6 +294,15 @@ typedef struct gr_obstacles {
 /* obst == NULL unbinds (obstacle-free tracks).  Validates counts and the grid (host copies of
  * the small index arrays). */
 int gr_bind_obstacles(gr_ctx* ctx, const gr_obstacles* obst);
+/* Terrain swap of the periodic regeneration (EventCfg.reset_terrain -> reset_terrain_period,
+ * extensions/diff.lab_tasks/diff/lab_tasks/tasks/quadcopter_diff/mdp/events.py:180-204) without a host
+ * synchronisation: the new tables are validated from HOST copies (`tracks_host` [num_types*num_levels]
+ * [GR_TRACK_FLOATS]; `obst_host` with the host counts / grid_f / grid_i / cells, sizes as `obst`), then, ordered on
+ * `stream`, the device gate table is packed into the context's table and the obstacle hints are cleared; `obst`
+ * (device arrays, caller-owned, kept alive while bound) is bound, or NULL unbinds.  Launches enqueued earlier on
+ * `stream` run on the previous tables.  Same tables -> same steps as gr_bind_tracks + gr_bind_obstacles. */
+int gr_swap_terrain(gr_ctx* ctx, const float* gates, const float* tracks, const float* tracks_host,
+                    const gr_obstacles* obst, const gr_obstacles* obst_host, void* stream);
 int gr_bind_buffers(gr_ctx* ctx, const gr_buffers* bufs);
 
 /* Observation sink (config C5's bf16 rollout buffers): every following gr_step / gr_reset / gr_observe also

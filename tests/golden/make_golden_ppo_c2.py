@@ -10,8 +10,9 @@ mini-batches of 24 576 rows, adaptive KL rate, entropy 0).  Mini-batches of this
 device update path: TallLinear's split-K weight gradients (>= 2 * SPLIT rows), gr_column_sum bias gradients and,
 with graph_update, the captured step with capturable Adam — none of which the N = 64 fixture reaches.
 
-The rollout inputs are NOT stored (6 MB per tensor): `rollout_inputs` draws them from a seeded CPU
-torch.Generator, and the test draws the same ones (same torch build on both sides).  Stored per iteration: the
+The rollout inputs are NOT stored (6 MB per tensor): `rollout_inputs` draws them, and the policy's sampling noise,
+from a seeded numpy PCG64 stream, and the test draws the same ones (identical on every CPU, unlike torch's CPU
+normal_, which dispatches by instruction set).  Stored per iteration: the
 storage's returns / advantages (their sums and first 4 096 entries), the gradients Adam receives at the update's
 first two mini-batches, the losses, the learning rate and all parameters after the update; each update's
 mini-batch permutation is drawn after torch.manual_seed(200 + it), as in make_golden_ppo.py.
@@ -42,18 +43,41 @@ ITERS = 2
 
 def rollout_inputs(seed=11, iters=ITERS, n=N):
     """Per iteration: obs / critic obs [T, N, 16], rewards [T, N], dones [T, N] (long), time_outs [T, N] (bool),
-    the last critic obs [N, 16]."""
-    g = torch.Generator().manual_seed(seed)
+    the last critic obs [N, 16], and the policy's sampling noise [T, N, 4].  Drawn with numpy's PCG64 (the same
+    on every CPU: torch's CPU normal_ dispatches by instruction set), as torch tensors."""
+    rng = np.random.default_rng(seed)
     out = []
     for _ in range(iters):
-        obs = torch.randn(T, n, OBS, generator=g)
-        cobs = torch.randn(T, n, OBS, generator=g)
-        rew = torch.randn(T, n, generator=g) * 0.1
-        dones = (torch.rand(T, n, generator=g) < 0.02).long()
-        tout = (torch.rand(T, n, generator=g) < 0.5) & dones.bool()
-        last = torch.randn(n, OBS, generator=g)
-        out.append((obs, cobs, rew, dones, tout, last))
+        obs = rng.standard_normal((T, n, OBS), dtype=np.float32)
+        cobs = rng.standard_normal((T, n, OBS), dtype=np.float32)
+        rew = rng.standard_normal((T, n), dtype=np.float32) * np.float32(0.1)
+        u = rng.random((2, T, n))
+        dones = (u[0] < 0.02).astype(np.int64)
+        tout = (u[1] < 0.5) & dones.astype(bool)
+        last = rng.standard_normal((n, OBS), dtype=np.float32)
+        eps = rng.standard_normal((T, n, 4), dtype=np.float32)
+        out.append(tuple(torch.from_numpy(x) for x in (obs, cobs, rew, dones, tout, last, eps)))
     return out
+
+
+def checksum(data):
+    """Exact (fsum) sums of every input tensor."""
+    import math
+
+    return np.array([math.fsum(np.asarray(x, np.float64).ravel().tolist()) for d in data for x in d])
+
+
+def deterministic_sampling(policy):
+    """ActorCritic.act draws mean + std * eps with eps from the rollout inputs (set policy._eps before each act):
+    the same draws on every machine; the update's arithmetic, which the fixture pins, is untouched."""
+    def act(observations, **kwargs):
+        policy.update_distribution(observations)
+        if observations.shape[0] != policy._eps.shape[0]:  # PPO.update's act: only the distribution is used
+            return policy.distribution.mean
+        return policy.distribution.mean + policy.distribution.stddev * policy._eps
+
+    policy.act = act
+    return policy
 
 
 def make_policy(cls):
@@ -78,10 +102,10 @@ def plain_linear(policy):
 
 def run(alg, data, record, prefix):
     alg.init_storage("rl", N, T, [OBS], [OBS], [4])
-    for it, (obs, cobs, rew, dones, tout, last) in enumerate(data):
-        torch.manual_seed(100 + it)
+    for it, (obs, cobs, rew, dones, tout, last, eps) in enumerate(data):
         with torch.inference_mode():
             for t in range(T):
+                alg.policy._eps = eps[t]
                 alg.act(obs[t], cobs[t])
                 alg.process_env_step(rew[t], dones[t], {"time_outs": tout[t]})
             alg.compute_returns(last)
@@ -120,8 +144,8 @@ def main():
     pol = plain_linear(make_policy(ActorCritic))
     assert not any(type(m).__name__ == "TallLinear" for m in pol.modules())
     rec["init_params"] = torch.cat([p.detach().reshape(-1) for p in pol.parameters()])
-    rec["inputs_checksum"] = torch.tensor([float(x.double().sum()) for d in data for x in d], dtype=torch.float64)
-    run(RefPPO(copy.deepcopy(pol), None, device="cpu", **HP), data, rec, "ppo")
+    rec["inputs_checksum"] = torch.from_numpy(checksum(data))
+    run(RefPPO(deterministic_sampling(copy.deepcopy(pol)), None, device="cpu", **HP), data, rec, "ppo")
     out = {}
     for k, v in rec.items():
         a = v.detach().cpu().numpy()

@@ -2,8 +2,8 @@
 ppo.py:103-190, storage/rollout_storage.py:113-191) at BASELINE C2 size — 4 096 envs x 24 steps, MLP(256, 256),
 5 epochs x 4 mini-batches of 24 576 rows — over plain nn.Linear layers (tests/golden/make_golden_ppo_c2.py).
 
-The rollout (act / process_env_step / compute_returns) runs on the CPU with the reference's generator seeds, so the
-stored actions are the reference's draws; the update runs on `device` with the build's options (eager, or
+The rollout (act / process_env_step / compute_returns) runs on the CPU with the fixture's sampling noise (numpy
+PCG64, the same draws on every machine), so the stored actions are the reference's; the update runs on `device` with the build's options (eager, or
 graph_update), i.e. TallLinear's split-K weight gradients, gr_column_sum bias gradients (captured step), capturable
 Adam.  Each update draws its mini-batch permutation from the CPU generator at the reference's seed point and moves
 it to the device (torch.randperm is redirected for the duration of update(): the build draws it on the device).
@@ -13,11 +13,18 @@ What is pinned, and how tightly (fp32; the reference's CPU GEMMs and the build's
 different orders):
   - the stored returns / advantages / actions / values: sums to 1e-6 of the absolute sum, the first 4 096 to 1e-5;
   - the gradients Adam receives at the first update's first two mini-batches and at the second update's first one
-    (the same parameters as the reference's there): within 1e-5 of the gradient's norm and of its largest element
-    (measured on the CPU: 3e-7);
+    (the same parameters as the reference's there), per parameter tensor: within 1e-5 relative (the build's CPU
+    path: 3e-7-9e-7 against the reference, 1e-7-5e-7 against float64); hidden layers within 1e-3.  A hidden
+    layer's gradient passes through LeakyReLU's derivative, which jumps by 100x at 0: a pre-activation within fp32
+    rounding of 0 (one of the 6.3 M per layer on MI355X's fp32 GEMM, which sums in another order than the CPU's)
+    takes the other branch, and its row's term moves the layer's gradient by ~3e-4 (measured:
+    scripts/diag_c2_grads2.py: on cuda:0 every forward value and the output layer's gradients are within 5e-7 of
+    float64, the gradient below the second LeakyReLU 3e-4: one pre-activation of 6.3 M has the other sign than
+    float64's); the second mini-batch's gradients within 1e-2 only: it starts from one Adam step on the first
+    one's gradient, which Adam normalises per element (the kink row's 3e-4 becomes 2.6e-3 in the next gradient);
   - the learning rate after each update, exactly (every adaptive decision agrees);
   - the value loss within 1e-3 relative, the surrogate (a nearly cancelling mean of +-A * ratio, |A| ~ 1) within
-    2e-4 absolute;
+    2e-4 absolute (second update: 1e-3);
   - the parameters after each update: within 15 % (first update) and 75 % (second) of the update's norm.  These are
     not loose copies of 1e-5: the reference is chaotic here.  Adam normalises each gradient element, so an element
     whose gradient is round-off-small moves by up to a learning rate either way; perturbing the reference's own
@@ -89,6 +96,26 @@ def record_grads(alg, out, count=2):
             alg.optimizer.step = step
 
 
+KINK_TOL = 1e-3
+
+
+def _per_param(alg, g, w):
+    off = 0
+    for name, p in alg.policy.named_parameters():
+        yield name, g[off:off + p.numel()], w[off:off + p.numel()]
+        off += p.numel()
+
+
+def _behind_kink(alg, name):
+    """Parameters of a layer whose output passes through an activation (every MLP layer but the last): their
+    gradients go through LeakyReLU's derivative, which jumps from 1 to 0.01 at 0."""
+    net, idx = name.split(".")[0], name.split(".")[1] if "." in name else None
+    mod = getattr(alg.policy, net, None)
+    if not isinstance(mod, torch.nn.Sequential) or idx is None or not idx.isdigit():
+        return False
+    return int(idx) < len(mod) - 1
+
+
 def _params(alg):
     return torch.cat([p.detach().reshape(-1).cpu() for p in alg.policy.parameters()]).double()
 
@@ -107,19 +134,18 @@ def replay(gp, device="cpu", **alg_kw):
     from generalizableracing_amd.rsl_rl.ppo import PPO
 
     data = mk.rollout_inputs()
-    chk = np.array([float(x.double().sum()) for d in data for x in d])
-    assert np.array_equal(chk, gp["inputs_checksum"]), "the seeded rollout inputs differ from the fixture's"
-    roll = PPO(mk.make_policy(ActorCritic), None, device="cpu", **mk.HP)
+    assert np.array_equal(mk.checksum(data), gp["inputs_checksum"]), "the seeded rollout inputs differ from the fixture's"
+    roll = PPO(mk.deterministic_sampling(mk.make_policy(ActorCritic)), None, device="cpu", **mk.HP)
     assert any(type(m).__name__ == "TallLinear" for m in roll.policy.modules())
     assert np.array_equal(_params(roll).float().numpy(), gp["init_params"])
     roll.init_storage("rl", mk.N, mk.T, [mk.OBS], [mk.OBS], [4])
     upd = PPO(mk.make_policy(ActorCritic), None, device=device, **mk.HP, **alg_kw)
     upd.init_storage("rl", mk.N, mk.T, [mk.OBS], [mk.OBS], [4])
     report = []
-    for it, (obs, cobs, rew, dones, tout, last) in enumerate(data):
-        torch.manual_seed(100 + it)
+    for it, (obs, cobs, rew, dones, tout, last, eps) in enumerate(data):
         with torch.inference_mode():
             for t in range(mk.T):
+                roll.policy._eps = eps[t]
                 roll.act(obs[t], cobs[t])
                 roll.process_env_step(rew[t], dones[t], {"time_outs": tout[t]})
             roll.compute_returns(last)
@@ -145,12 +171,18 @@ def replay(gp, device="cpu", **alg_kw):
         # mini-batch 1 of the second update starts from Adam moments that followed the build's own first update
         for j in range(2 if it == 0 else 1):
             g, w = grads[j].double(), torch.from_numpy(gp[f"ppo_it{it}_grad_mb{j}"]).double()
-            e_norm, e_max = float((g - w).norm() / w.norm()), float((g - w).abs().max() / w.abs().max())
-            assert e_norm <= 1e-5 and e_max <= 1e-5, (it, j, e_norm, e_max)
-            gerr.append(max(e_norm, e_max))
+            for name, a, b in _per_param(upd, g, w):
+                e = float((a - b).norm() / max(float(b.norm()), 1e-30))
+                # mini-batch 1 starts from one Adam step on mini-batch 0's gradient, which Adam normalises per element:
+                # where that gradient differed by the kink row above, the step did too
+                tol = (KINK_TOL if _behind_kink(upd, name) else 1e-5) if j == 0 else 1e-2
+                assert e <= tol, (it, j, name, e)
+                gerr.append(e)
         for k, v in losses.items():
             want = float(gp[f"ppo_it{it}_loss_{k}"])
-            tol = 2e-4 if k == "surrogate" else 1e-3 * max(abs(want), 1e-3)
+            # (second update: the means over a trajectory that has left the reference's by up to 37 % of an update in
+            # the reference's own round-off spread, see below)
+            tol = (2e-4, 1e-3)[it] if k == "surrogate" else 1e-3 * max(abs(want), 1e-3)
             assert abs(v - want) <= tol, (it, k, v, want)
         got, want = _params(upd), torch.from_numpy(gp[f"ppo_it{it}_params"]).double()
         dev = float((got - want).norm() / (want - p0).norm())

@@ -327,8 +327,15 @@ def test_obs_sink_rows(dtype):
     venv = RslRlVecEnvWrapper(RacingEnv(cfg))
     sp = torch.full((n, 16), 7.0, device=DEV, dtype=dtype)
     sc = torch.full((n, 16), 7.0, device=DEV, dtype=dtype)
+    base_bytes = venv.env.bytes_per_env_step()
     venv.set_obs_sink(sp, sc)
+    if dtype == torch.float32:  # the slot IS the output: one write per row, no second (sink) row set
+        assert venv.env.bytes_per_env_step() == base_bytes
+    else:  # bf16: the rounded rows on top of the fp32 output rows
+        assert venv.env.bytes_per_env_step()[1] == base_bytes[1] + 64
     obs, ex = venv.get_observations()
+    if dtype == torch.float32:
+        assert obs.data_ptr() == sp.data_ptr() and ex["observations"]["critic"].data_ptr() == sc.data_ptr()
     torch.cuda.synchronize()
     assert torch.equal(sp, obs.to(dtype)) and torch.equal(sc, ex["observations"]["critic"].to(dtype))
     g = torch.Generator().manual_seed(4)
@@ -354,16 +361,18 @@ def test_obs_sink_rows(dtype):
 
 
 @pytest.mark.gpu
-def test_runner_obs_sink_matches_copy():
-    """OnPolicyRunner with the observation sink (bf16 rollout storage written by the step kernel) trains
-    exactly like the copy path: same stored observations, same parameters after two learn() calls."""
+@pytest.mark.parametrize("storage_dtype", ["bfloat16", "float32"])
+def test_runner_obs_sink_matches_copy(storage_dtype):
+    """OnPolicyRunner with the observation sink (bf16: the step kernel also writes the rounded rows into the storage
+    slot; fp32: the storage slot IS the step's observation output, each row written once) trains exactly like the
+    copy path: same stored observations, same parameters after two learn() calls."""
     from generalizableracing_amd.rsl_rl import OnPolicyRunner, QuadcopterPPORunnerCfg
 
     runs = []
     for sink in (True, False):
         torch.manual_seed(9)
         cfg = QuadcopterPPORunnerCfg(device=DEV, num_steps_per_env=8)
-        cfg.algorithm.storage_obs_dtype = "bfloat16"
+        cfg.algorithm.storage_obs_dtype = storage_dtype
         cfg.algorithm.obs_sink = sink
         env = RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=512), sim=SimCfg(device=DEV), stage=1))
         r = OnPolicyRunner(RslRlVecEnvWrapper(env), cfg.to_dict(), log_dir=None, device=DEV)
