@@ -40,6 +40,10 @@ from generalizableracing_amd.envs.racing_env import RacingEnv  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TFS = 157.3  # MI355X dense fp32 matrix peak (v_mfma_f32_16x16x4_f32; MI355X_MICROARCH.md)
+# the PPO update's useful flops per sample and epoch, MLP(256, 256) actor (16 -> 4) and critic (16 -> 1): forward
+# 140 544 MACs, weight gradients 140 544, input gradients below the first layer 132 352 (2 flops per MAC)
+UPDATE_FLOPS_PER_SAMPLE = 2 * (2 * (16 * 256 + 256 * 256 + 256 * 4 + 16 * 256 + 256 * 256 + 256)
+                               + (256 * 256 + 256 * 4 + 256 * 256 + 256))
 ACTION_RING = 64
 
 
@@ -344,15 +348,32 @@ def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False, graph_up
     cfg.algorithm.update_autocast_bf16 = bool(bf16_update)
     cfg.algorithm.obs_sink = bool(obs_sink)
     runner = OnPolicyRunner(venv, cfg.to_dict(), log_dir=None, device=device)
+    upd = runner.alg.update
+    upd_s = []
+
+    def timed_update():  # alg.update alone (learn_time also holds compute_returns)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = upd()
+        torch.cuda.synchronize()
+        upd_s.append(time.perf_counter() - t0)
+        return out
+
+    runner.alg.update = timed_update
     runner.learn(1, init_at_random_ep_len=True)  # warm-up iteration
     fps = []
     for _ in range(iters):
         runner.learn(1)
         fps.append(runner.last_log["fps"])
+    alg = runner.alg
+    samples = alg.num_learning_epochs * n * cfg.num_steps_per_env
+    upd_ms = float(np.median(upd_s[1:])) * 1e3
+    tfs = UPDATE_FLOPS_PER_SAMPLE * samples / (upd_ms * 1e-3) / 1e12
     progress(f"train_fps n={n} fused={fused}({fused_precision}) bf16_storage={bf16_storage} graph_update={graph_update} "
-             f"obs_sink={obs_sink}: {np.median(fps):.4g}")
+             f"obs_sink={obs_sink}: {np.median(fps):.4g} (update {upd_ms:.1f} ms, {tfs:.1f} TFLOP/s)")
     venv.close()
-    return float(np.median(fps))
+    return {"fps": float(np.median(fps)), "update_ms": upd_ms, "update_TFLOPs": tfs,
+            "update_frac_of_fp32_mfma_peak": tfs / FP32_MFMA_PEAK_TFS if not bf16_update else None}
 
 
 def regeneration_cost(device, n, interval=256, plain=64):

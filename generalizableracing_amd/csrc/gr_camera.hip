@@ -54,6 +54,34 @@ DEV_INLINE void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// the 16 state terms of both rows
+DEV_INLINE void state_terms(const CamArgs& a, int i, int lane, size_t row) {
+  if (lane < 4) {
+    const float4 sp = reinterpret_cast<const float4*>(a.obs_p16)[4 * i + lane];
+    const float4 sc = reinterpret_cast<const float4*>(a.obs_c16)[4 * i + lane];
+    reinterpret_cast<float4*>(a.out_p + i * row)[lane] = sp;
+    reinterpret_cast<float4*>(a.out_c + i * row)[lane] = sc;
+  }
+}
+
+// sensor up to date: stream the depth buffer into both rows, CAM_BATCH loads in flight per lane
+DEV_INLINE void reuse_rows(const CamArgs& a, const gr_cam_const* __restrict__ cc, const float4* dep4, float4* op4,
+                           float4* oc4, int nq, int lane, uint32_t gid, uint32_t cnt) {
+  for (int q0 = 0; q0 < nq; q0 += 64 * CAM_BATCH) {
+    float4 dd[CAM_BATCH];
+#pragma unroll
+    for (int j = 0; j < CAM_BATCH; ++j) {
+      const int q = q0 + 64 * j + lane;
+      dd[j] = q < nq ? dep4[q] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+#pragma unroll
+    for (int j = 0; j < CAM_BATCH; ++j) {
+      const int q = q0 + 64 * j + lane;
+      if (q < nq) emit_quad(a, cc, op4, oc4, q, dd[j], gid, cnt);
+    }
+  }
+}
+
 // obstacle slot from LDS (GR_CAM_OSLOT floats: frame and primitive = slot floats 0-15, window = 17-20)
 DEV_INLINE void load_oslot(const float4* src, float s[GR_CAM_SLOT]) {
 #pragma unroll
@@ -197,7 +225,8 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
         nv += nb;
       }
       const int ns = nv < GR_CAM_OBST_SLOTS ? nv : GR_CAM_OBST_SLOTS;
-      // per 8x32 tile: the slots whose window meets the tile's ray range (a_u, b_v decrease with u, v)
+      // per 8x32 tile: the slots whose window meets the tile's ray range (a_u, b_v decrease with u, v) and whose
+      // bounding box reaches into the tile's frustum (gr_cam_obst_outside)
       wave_lds_sync();
       for (int tl = lane; tl < ntx * nty; tl += 64) {
         const int v0 = 8 * (tl / ntx), u0 = 32 * (tl % ntx);
@@ -206,7 +235,12 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
         uint64_t tm = 0;
         for (int k = 0; k < ns; ++k) {
           const float4 wk = s_oslot[k * (GR_CAM_OSLOT / 4) + 4];
-          const bool meet = !(wk.y < a_lo || wk.x > a_hi || wk.w < b_lo || wk.z > b_hi);
+          bool meet = !(wk.y < a_lo || wk.x > a_hi || wk.w < b_lo || wk.z > b_hi);
+          if (meet) {
+            float sk[GR_CAM_SLOT];
+            load_oslot(s_oslot + k * (GR_CAM_OSLOT / 4), sk);
+            meet = !gr_cam_obst_outside(sk, a_lo, a_hi, b_lo, b_hi);
+          }
           tm |= (uint64_t)meet << k;
         }
         s_tmask[tl] = tm;
@@ -216,36 +250,17 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
   __syncthreads();
   if (!active) return;
 
-  // ---- the 16 state terms of both rows
   const uint32_t gid = (uint32_t)(a.env_id_offset + i);
   const uint32_t cnt = a.counters[a.counter_index];
   const size_t row = (size_t)(16 + npix);
-  if (lane < 4) {
-    const float4 sp = reinterpret_cast<const float4*>(a.obs_p16)[4 * i + lane];
-    const float4 sc = reinterpret_cast<const float4*>(a.obs_c16)[4 * i + lane];
-    reinterpret_cast<float4*>(a.out_p + i * row)[lane] = sp;
-    reinterpret_cast<float4*>(a.out_c + i * row)[lane] = sc;
-  }
+  state_terms(a, i, lane, row);
   float4* op4 = reinterpret_cast<float4*>(a.out_p + i * row + 16);
   float4* oc4 = reinterpret_cast<float4*>(a.out_c + i * row + 16);
   float4* dep4 = reinterpret_cast<float4*>(a.depth + (size_t)i * npix);
   const int nq = npix >> 2;
 
   if (!render) {
-    // ---- sensor up to date: stream the depth buffer into both rows, CAM_BATCH loads in flight per lane
-    for (int q0 = 0; q0 < nq; q0 += 64 * CAM_BATCH) {
-      float4 dd[CAM_BATCH];
-#pragma unroll
-      for (int j = 0; j < CAM_BATCH; ++j) {
-        const int q = q0 + 64 * j + lane;
-        dd[j] = q < nq ? dep4[q] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      }
-#pragma unroll
-      for (int j = 0; j < CAM_BATCH; ++j) {
-        const int q = q0 + 64 * j + lane;
-        if (q < nq) emit_quad(a, cc, op4, oc4, q, dd[j], gid, cnt);
-      }
-    }
+    reuse_rows(a, cc, dep4, op4, oc4, nq, lane, gid, cnt);
     return;
   }
 
@@ -284,14 +299,6 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
         }
       }
       if constexpr (obst) {
-        uint64_t mo = s_tmask[(v0 >> 3) * ntx + (u_t >> 5)];
-        while (mo) {
-          const int k = __builtin_ctzll(mo);
-          mo &= mo - 1;
-          float s[GR_CAM_SLOT];
-          load_oslot(s_oslot + k * (GR_CAM_OSLOT / 4), s);
-          quad_obst(s, av, b, d);
-        }
         for (int k = ofrom; k < nob; ++k) {  // beyond the slots: set up again (identical slot values)
           float r[GR_OBST_FLOATS], s[GR_CAM_SLOT];
           load_orec(orecs + (size_t)k * GR_OBST_FLOATS, r);
@@ -301,6 +308,46 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
       }
       s_stage[((v - v0) * W + u0) >> 2] =
           make_float4(gr_cam_clip(d[0], maxd), gr_cam_clip(d[1], maxd), gr_cam_clip(d[2], maxd), gr_cam_clip(d[3], maxd));
+    }
+    if constexpr (obst) {
+      // the obstacles of the LDS slots, per tile of the band: only the pixels inside a slot's window (a column
+      // range times a row range: a_u and b_v are monotonic), packed onto the lanes (one hit per lane and pass)
+      // and min-ed into the staged band (clip(min) = min(clip): the clip is monotonic)
+      float* st = reinterpret_cast<float*>(s_stage);
+      wave_lds_sync();
+      for (int u_t = 0; u_t < W; u_t += 32) {
+        uint64_t mo = s_tmask[(v0 >> 3) * ntx + (u_t >> 5)];
+        while (mo) {
+          const int k = __builtin_ctzll(mo);
+          mo &= mo - 1;
+          const float4 wk = s_oslot[k * (GR_CAM_OSLOT / 4) + 4];  // amin, amax, bmin, bmax
+          bool in = false;
+          if (lane < 32) {
+            const int u = u_t + lane;
+            in = u < W && s_ray_a[u] >= wk.x && s_ray_a[u] <= wk.y;
+          } else if (lane < 40) {
+            const int v = v0 + lane - 32;
+            in = v < H && s_ray_b[v] >= wk.z && s_ray_b[v] <= wk.w;
+          }
+          const uint64_t bal = __ballot(in);
+          const uint32_t cm = (uint32_t)bal, rm = (uint32_t)(bal >> 32) & 0xffu;
+          if (cm == 0u || rm == 0u) continue;
+          const int cu = u_t + __builtin_ctz(cm), wc = __popc(cm), rv = __builtin_ctz(rm), area = wc * __popc(rm);
+          const float inv_wc = 1.0f / (float)wc;
+          float s[GR_CAM_SLOT];
+          load_oslot(s_oslot + k * (GR_CAM_OSLOT / 4), s);
+          for (int base = 0; base < area; base += 64) {
+            const int idx = base + lane;
+            if (idx < area) {
+              // idx / wc exactly for idx < 256, wc <= 32 (the fraction of a non-integer quotient is <= 31/32)
+              const int r = (int)((float)idx * inv_wc + 1.0e-3f), c = idx - r * wc;
+              const int u = cu + c, pix = (rv + r) * W + u;
+              const float h = gr_cam_clip(gr_cam_obst_hit(s, s_ray_a[u], s_ray_b[v0 + rv + r]), maxd);
+              st[pix] = gr_minf(st[pix], h);
+            }
+          }
+        }
+      }
     }
     wave_lds_sync();
     const int qb = (v0 * W) >> 2, nqb = (rows * W) >> 2;

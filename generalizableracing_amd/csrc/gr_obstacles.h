@@ -126,6 +126,38 @@ GR_HD void gr_obst_local_box(const float* r, float l[3]) {
   l[2] = kind == GR_OBST_CAPSULE ? r[15] + r[7] : r[15];
 }
 
+/* One side plane of a frustum of pixel rays (y = a x or z = a x in camera coordinates, x forward): is the box
+ * (centre (x0, cp) in the plane's two coordinates, primitive axis j = (d0[j], dp[j]) in them, half sizes l) wholly
+ * on the outer side, sgn * (y - a x) > 0?  With a margin far above the rounding of any hit test. */
+GR_HD int gr_cam_box_beyond(float x0, float cp, const float* d0, const float* dp, const float l[3], float a,
+                            float sgn) {
+  const float v = sgn * (cp - a * x0);
+  const float r = (l[0] * gr_fabsf(dp[0] - a * d0[0]) + l[1] * gr_fabsf(dp[1] - a * d0[1])) +
+                  l[2] * gr_fabsf(dp[2] - a * d0[2]);
+  const float m = 1.0e-3f + 1.0e-4f * ((gr_fabsf(cp) + gr_fabsf(a * x0)) + r);
+  return v - r > m;
+}
+
+/* Kernel-only cull of a camera slot against a tile of pixel rays a in [a_lo, a_hi], b in [b_lo, b_hi] (the oracle
+ * tests every pixel of the slot's window, so this only skips pixels that cannot hit): the primitive's local
+ * bounding box lies wholly beyond one side plane of the tile's frustum.  A window spans the box's 8 projected
+ * corners, and is the whole screen when the box reaches behind the camera plane (a wall alongside the drone);
+ * the planes cut both down to the tiles the box can actually cover.  Camera coordinates from the slot: the
+ * centre is -(D0 . O, D1 . O, D2 . O), primitive axis j is (D0[j], D1[j], D2[j]). */
+GR_HD int gr_cam_obst_outside(const float* s, float a_lo, float a_hi, float b_lo, float b_hi) {
+  const float* O = s;
+  const float* D0 = s + 3;
+  const float* D1 = s + 6;
+  const float* D2 = s + 9;
+  const float x0 = -((D0[0] * O[0] + D0[1] * O[1]) + D0[2] * O[2]);
+  const float y0 = -((D1[0] * O[0] + D1[1] * O[1]) + D1[2] * O[2]);
+  const float z0 = -((D2[0] * O[0] + D2[1] * O[1]) + D2[2] * O[2]);
+  const int kind = (int)s[GR_OS_KIND];
+  const float l[3] = {s[GR_OS_E0], s[GR_OS_E1], kind == GR_OBST_CAPSULE ? s[GR_OS_E2] + s[GR_OS_E0] : s[GR_OS_E2]};
+  return gr_cam_box_beyond(x0, y0, D0, D1, l, a_hi, 1.0f) | gr_cam_box_beyond(x0, y0, D0, D1, l, a_lo, -1.0f) |
+         gr_cam_box_beyond(x0, z0, D0, D2, l, b_hi, 1.0f) | gr_cam_box_beyond(x0, z0, D0, D2, l, b_lo, -1.0f);
+}
+
 /* first crossing (s > 0) of the ray o + s d with the slab |x_j| <= h_j intersected with
  * the interval [t0, t1]; GR_CAM_FAR-style miss = 3e38 */
 GR_HD float gr_obst_first(float tin, float tout) {

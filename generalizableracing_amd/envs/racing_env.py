@@ -162,6 +162,9 @@ class RacingEnv:
         # fp32 sink = the calls' observation OUTPUT (set_obs_sink): the rows are written once, into the storage slot
         self._sink_out = None
         self._last_rows = None  # (policy, critic) rows the last call wrote, if not the output set's
+        # camera task: the fp32 sink is the camera kernel's [16 state terms | image] output instead
+        self._cam_sink_out = None
+        self._last_img = None
         # startup (gr_init): nominal state, startup DR events, initial terrain levels
         self._bind(0)
         self._call("gr_init", self._stream())
@@ -323,7 +326,11 @@ class RacingEnv:
                 b.obs_policy, b.obs_critic = self._sink_out[0].data_ptr(), self._sink_out[1].data_ptr()
         self._call("gr_bind_buffers", C.byref(b))
         if getattr(self, "camera", None) is not None:
-            self._call("gr_bind_camera_buffers", C.byref(self._cam_bufs[(k + 1) % 2]))
+            cb = self._cam_bufs[(k + 1) % 2]
+            if self._cam_sink_out is not None:
+                cb = _abi.GrCameraBuffers.from_buffer_copy(cb)
+                cb.obs_policy, cb.obs_critic = self._cam_sink_out[0].data_ptr(), self._cam_sink_out[1].data_ptr()
+            self._call("gr_bind_camera_buffers", C.byref(cb))
 
     def _render(self, mode: int, mask_ptr=None):
         if self.camera is not None:
@@ -344,6 +351,7 @@ class RacingEnv:
         self._calls += 1
         self._cur = (k + 1) % 2
         self._last_rows = self._sink_out
+        self._last_img = self._cam_sink_out
         lg = _EpisodeLog(self, k, self._log_keys)
         self._logs[k % LOG_RING] = lg
         return self._sets[self._cur], lg
@@ -375,6 +383,8 @@ class RacingEnv:
     def _obs_dict(self, s):
         if self.camera is not None:
             img = self._img_sets[self._cur]
+            if self._last_img is not None:  # the camera kernel wrote its rows into the bound fp32 sink
+                return {"policy": self._last_img[0], "critic": self._last_img[1], "auxiliary": s["auxiliary"]}
             return {"policy": img["policy"], "critic": img["critic"], "auxiliary": s["auxiliary"]}
         if self._last_rows is not None:  # the last call wrote its rows into the bound fp32 sink
             return {"policy": self._last_rows[0], "critic": self._last_rows[1], "auxiliary": s["auxiliary"]}
@@ -505,14 +515,15 @@ class RacingEnv:
         # the step returns; the runner's previous slot is not touched)
         keys = ("auxiliary",) if self._sink_out is not None else ("policy", "critic", "auxiliary")
         saved = [held[k].clone() for k in keys]
-        if self.camera is not None:
+        sink_img = self.camera is not None and self._cam_sink_out is not None
+        if self.camera is not None and not sink_img:  # (with the camera sink bound the held set is not written)
             held_img = self._img_sets[(self._cur + 1) % 2]
             saved_img = [held_img[k].clone() for k in ("policy", "critic")]
         _, extras = self.regenerate_terrain()
         self.observe()
         for k, v in zip(keys, saved):
             held[k].copy_(v)
-        if self.camera is not None:
+        if self.camera is not None and not sink_img:
             for k, v in zip(("policy", "critic"), saved_img):
                 held_img[k].copy_(v)
         self.extras = {"log": extras["log"], "terrain_regenerated": True}
@@ -539,24 +550,28 @@ class RacingEnv:
         tensors — the rollout storage's slot for the next transition — instead of the storage copying them
         (rollout_storage.py:74-88).  float32: the tensors become the calls' observation output (written once, and
         returned by the calls); bfloat16 (config C5's bf16 rollout buffers): gr_bind_obs_sink, the kernel writes
-        the fp32 output rows and their round-to-nearest-even bf16 copy.  None unbinds.  State task only (the image
-        rows of the camera task are not sunk)."""
+        the fp32 output rows and their round-to-nearest-even bf16 copy.  None unbinds.  Camera task: [num_envs,
+        16 + pixels] float32 tensors become the camera kernel's output ([16 state terms | image] rows,
+        observation.py:65-94 into rollout_storage.py:74-88's slot, written once)."""
         if policy is None:
             self._sink = None
             self._sink_out = None
+            self._cam_sink_out = None
             self._call("gr_bind_obs_sink", None, None, _abi.GR_DTYPE_F32)
             return
-        if self.camera is not None:
-            raise ValueError("set_obs_sink: the camera task's image observation rows have no sink")
+        width = self.num_obs
+        dtypes = (torch.float32,) if self.camera is not None else (torch.float32, torch.bfloat16)
         for t in (policy, critic):
-            if (t is None or t.device != self.device or tuple(t.shape) != (self.num_envs, _abi.OBS_DIM)
-                    or not t.is_contiguous() or t.dtype not in (torch.float32, torch.bfloat16)
-                    or t.data_ptr() % 16):
-                raise ValueError(f"set_obs_sink: need contiguous 16-byte aligned [{self.num_envs}, {_abi.OBS_DIM}] "
-                                 f"float32 / bfloat16 tensors on {self.device}")
+            if (t is None or t.device != self.device or tuple(t.shape) != (self.num_envs, width)
+                    or not t.is_contiguous() or t.dtype not in dtypes or t.data_ptr() % 16):
+                raise ValueError(f"set_obs_sink: need contiguous 16-byte aligned [{self.num_envs}, {width}] "
+                                 f"{' / '.join(str(d) for d in dtypes)} tensors on {self.device}")
         if critic.dtype != policy.dtype:
             raise ValueError("set_obs_sink: policy and critic sinks must share a dtype")
         self._sink = (policy, critic)  # kept alive while bound
+        if self.camera is not None:
+            self._cam_sink_out = (policy, critic)
+            return
         if policy.dtype == torch.float32:
             # fp32: the tensors ARE the calls' observation output (the rows are written once; the calls return
             # these tensors), rollout_storage.py:74-88's copy with no second write

@@ -49,8 +49,9 @@ class RslRlPpoAlgorithmCfg:
     # not in the reference: the update's forward/backward under torch.autocast(bfloat16) (ppo.py)
     update_autocast_bf16: bool = False
     # not in the reference: the env writes each transition's observations straight into the rollout storage
-    # slot (RacingEnv.set_obs_sink; PPO, state task, no empirical normalisation) instead of add_transitions
-    # copying them — with storage_obs_dtype "bfloat16" the kernel rounds them to bf16 itself
+    # slot (RacingEnv.set_obs_sink; PPO or PPOL2C2, state rows or fp32 camera rows, no empirical normalisation)
+    # instead of add_transitions copying them — with storage_obs_dtype "bfloat16" (state rows) the kernel rounds
+    # them to bf16 itself
     obs_sink: bool = True
 
 

@@ -60,20 +60,6 @@ def split_k_wgrad(gy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     return gw
 
 
-SMALL_K = 8  # input gradients gy @ W with at most this many output features take small_k_input_grad
-
-
-def small_k_input_grad(gy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """gy [M, K] @ w [K, N] for K <= SMALL_K as K fused multiply-add passes in fp32 (k = 0, 1, ... in order).  On the
-    GPU, hipBLASLt's fp32 GEMM of this shape (the actor head's input gradient, K = 4 actions) returned results 3e-4
-    off in relative terms on MI355X (the actor's hidden-layer gradients of the C2 update vs the reference's CPU fp32:
-    tests/test_gpu_ppo_c2_golden.py, scripts/diag_c2_grads.py); these passes are fp32-exact per term."""
-    gx = gy[:, 0:1] * w[0]
-    for k in range(1, gy.shape[1]):
-        gx.addcmul_(gy[:, k:k + 1], w[k])
-    return gx
-
-
 class _TallLinearFn(torch.autograd.Function):
     # custom_fwd / custom_bwd: under torch.autocast (PPO's opt-in bf16 update) the forward GEMM runs in
     # the autocast dtype and the backward runs under the same autocast state; gradients return in the
@@ -93,7 +79,7 @@ class _TallLinearFn(torch.autograd.Function):
         gx = None
         if ctx.needs_input_grad[0]:
             wg = w.to(gy.dtype)
-            gx = small_k_input_grad(gy, wg) if wg.shape[0] <= SMALL_K and gy.is_cuda else gy @ wg
+            gx = gy @ wg
         gw = split_k_wgrad(gy, x.to(gy.dtype)).to(ctx.wdtype) if ctx.needs_input_grad[1] else None
         gb = bias_grad(gy).to(ctx.wdtype) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return gx, gw, gb
@@ -109,7 +95,7 @@ class TallLinear(nn.Linear):
 
     @torch.jit.unused
     def _forward_eager(self, x: torch.Tensor) -> torch.Tensor:
-        if x.dim() == 2 and (x.shape[0] >= 2 * SPLIT or _FORCE_FN or (x.is_cuda and self.out_features <= SMALL_K)) \
+        if x.dim() == 2 and (x.shape[0] >= 2 * SPLIT or _FORCE_FN) \
                 and torch.is_grad_enabled() and self.weight.requires_grad:
             return _TallLinearFn.apply(x, self.weight, self.bias)
         return F.linear(x, self.weight, self.bias)

@@ -130,20 +130,24 @@ class OnPolicyRunner:
         self.last_log: dict = {}
 
     def _sink_supported(self, obs, extras) -> bool:
-        """The observation sink (RacingEnv.set_obs_sink: the step kernel writes each transition's observations
-        into the rollout storage slot) applies when the stored rows are exactly the env's rows: PPO (PPOL2C2's
-        storage pairs observations with their successors), no empirical normalisation, separate critic rows,
-        the env on the training device, state observations of the kernel's width."""
-        if type(self.alg) is not PPO or self.empirical_normalization or not hasattr(self.env, "set_obs_sink"):
+        """The observation sink (RacingEnv.set_obs_sink: the step kernel, or on the camera task the camera kernel,
+        writes each transition's observations into the rollout storage slot) applies when the stored rows are
+        exactly the env's rows: PPO or PPOL2C2 (whose successor pairs read the same slots), no empirical
+        normalisation, separate critic rows, the env on the training device; the camera task's rows with fp32
+        storage only."""
+        if not isinstance(self.alg, PPO) or self.empirical_normalization or not hasattr(self.env, "set_obs_sink"):
             return False
         st = self.alg.storage
         if st.privileged_observations is None or self.privileged_obs_type is None:
             return False
         unwrapped = getattr(self.env, "unwrapped", self.env)
-        if torch.device(self.env.device) != torch.device(self.device) or getattr(unwrapped, "camera", None) is not None:
+        if torch.device(self.env.device) != torch.device(self.device):
             return False
+        if getattr(unwrapped, "camera", None) is not None and st.observations.dtype != torch.float32:
+            return False
+        width = getattr(unwrapped, "num_obs", 16)
         crit = extras["observations"][self.privileged_obs_type]
-        return obs.dim() == 2 and obs.shape[1] == 16 and crit.dim() == 2 and crit.shape[1] == 16
+        return obs.dim() == 2 and obs.shape[1] == width and crit.dim() == 2 and crit.shape[1] == width
 
     def learn(self, num_learning_iterations: int, init_at_random_ep_len: bool = False):
         if self.log_dir is not None and self.writer is None and self.is_main:

@@ -16,7 +16,10 @@ Deviations (documented):
     ppo_l2c2.py:184,189 take `[0]`; on a plain ActorCritic `[0]` would pick the first
     ROW of the mean and broadcast it.  Here `_mean_of` takes [0] only of a tuple.
   * the transition is stored unless the whole observation batch is ~0
-    (ppo_l2c2.py:98), as in the reference; that test costs one host sync per step.
+    (ppo_l2c2.py:98), as in the reference; that test costs one host sync per step.  With the
+    observation sink (the camera kernel writes the rows into the storage slot) the test runs in act(),
+    on the same rows, and a skipped transition's successor rows move down into its slot
+    (RolloutStorage.sink_skipped).
 """
 from __future__ import annotations
 
@@ -55,14 +58,26 @@ class PPOL2C2(PPO):
         policy_coef = self.smoothness_upper_bound * eps
         return policy_coef, self.value_smoothness_coef * policy_coef
 
+    def act(self, obs, critic_obs):
+        actions = super().act(obs, critic_obs)
+        if getattr(self.storage, "sink", False):
+            # ppo_l2c2.py:98's zero-observation test on these rows, taken before the step: with the observation
+            # sink the rows of a skipped transition are moved down a slot and the env's next step writes the slot
+            # `obs` views
+            self._store = bool(torch.norm(obs).mean() > 1e-4)
+        return actions
+
     def process_env_step(self, rewards, dones, infos):
         self.transition.rewards = rewards.clone()
         self.transition.dones = dones
         if "time_outs" in infos:  # ppo_l2c2.py:91-95
             self.transition.rewards += self.gamma * torch.squeeze(
                 self.transition.values * infos["time_outs"].unsqueeze(1).to(self.device), 1)
-        if torch.norm(self.transition.observations).mean() > 1e-4:  # ppo_l2c2.py:98
+        sink = getattr(self.storage, "sink", False)
+        if self._store if sink else bool(torch.norm(self.transition.observations).mean() > 1e-4):  # ppo_l2c2.py:98
             self.storage.add_transitions(self.transition)
+        elif sink:
+            self.storage.sink_skipped()
         self.transition.clear()
         self.policy.reset(dones)
 

@@ -84,6 +84,18 @@ class RolloutStorage:
         priv = self.privileged_observations if self.privileged_observations is not None else self.observations
         return self.observations[t], priv[t]
 
+    def sink_skipped(self):
+        """A transition was not stored (PPOL2C2's zero-observation skip): the rows the env wrote for its successor
+        (slot step + 1) belong to the transition stored next, at slot step."""
+        t = self.step
+        if self.prefilled[t + 1]:
+            self.observations[t].copy_(self.observations[t + 1])
+            if self.privileged_observations is not None:
+                self.privileged_observations[t].copy_(self.privileged_observations[t + 1])
+            self.prefilled[t], self.prefilled[t + 1] = True, False
+        else:
+            self.prefilled[t] = False
+
     def discard_sink(self):
         """Slots marked filled by the env are stale (the runner observed afresh): copy on the next adds."""
         self.prefilled = [False] * (self.num_transitions_per_env + 1)

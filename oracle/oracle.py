@@ -54,6 +54,7 @@ def load():
             "gro_num_threads": [],
             "gro_camera": [vp, vp, vp, C.c_int, vp, C.c_int, vp, vp, vp, C.c_uint32, vp, vp, vp, vp, vp, vp],
             "gro_camera_frame": [vp, vp, vp, vp, vp],
+            "gro_camera_cull_check": [vp, vp, vp, C.c_int, vp, vp, vp],
         }.items():
             f = getattr(lib, name)
             f.restype = None
@@ -172,6 +173,14 @@ class Oracle:
                                   _p(np.ascontiguousarray(p, np.float32)), _p(np.ascontiguousarray(q, np.float32)),
                                   _p(out))
         return out[0:3], out[3:6], out[6:9], out[9:12], out[12:12 + W], out[12 + W:]
+
+    def camera_cull_check(self, track: int, p, q) -> np.ndarray:
+        """gro_camera_cull_check: [pairs, culled pairs, culled pairs with a hit (must be 0), culled window pixels]."""
+        out = np.zeros(4, np.int64)
+        self.lib.gro_camera_cull_check(C.byref(self.cfg), C.byref(self.cam_cfg), C.byref(self.tracks), track,
+                                       _p(np.ascontiguousarray(p, np.float32)), _p(np.ascontiguousarray(q, np.float32)),
+                                       _p(out))
+        return out
 
     def collision_count(self, track: int, p, q) -> int:
         p = np.ascontiguousarray(p, dtype=np.float32)

@@ -16,4 +16,6 @@ bash scripts/gpu_profile.sh ${TAG}_g 65536 0 || exit 12
 bash scripts/gpu_profile.sh ${TAG}_o 65536 1 || exit 13
 bash scripts/prof_policy.sh ${TAG}_p || exit 14
 bash scripts/prof_policy.sh ${TAG}_p32 --precision fp32 || exit 15
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/update -o update -- \
+    python3 $R/scripts/prof_update.py --fused --graph --iters 2 > $OUT/update.log 2>&1) || exit 16
 echo done > $OUT/done

@@ -21,6 +21,7 @@ if __name__ == "__main__":
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--fused", action="store_true")
     ap.add_argument("--iters", type=int, default=2)
+    ap.add_argument("--graph", action="store_true", help="graph-captured update (algorithm.graph_update)")
     ap.add_argument("--split", type=int, default=0, help="override rsl_rl/linear.py SPLIT (rows per chunk)")
     a = ap.parse_args()
     if a.split:
@@ -31,6 +32,8 @@ if __name__ == "__main__":
     venv = RslRlVecEnvWrapper(RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=a.envs), sim=SimCfg(device=dev))))
     cfg = QuadcopterPPORunnerCfg(device=dev)
     cfg.algorithm.fused_rollout_inference = a.fused
+    cfg.algorithm.fused_rollout_precision = "fp32"
+    cfg.algorithm.graph_update = a.graph
     runner = OnPolicyRunner(venv, cfg.to_dict(), log_dir=None, device=dev)
     runner.learn(1, init_at_random_ep_len=True)
     torch.cuda.synchronize()

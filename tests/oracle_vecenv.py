@@ -57,17 +57,21 @@ class OracleVecEnv:
 
     def set_obs_sink(self, policy, critic=None):
         """RacingEnv.set_obs_sink emulated: the rows are cast into the bound tensors (torch's cast rounds to
-        nearest even, as the kernel's bf16 sink does)."""
-        if policy is not None and self.camera is not None:
-            raise ValueError("set_obs_sink: no sink for the camera task")
+        nearest even, as the kernel's bf16 sink does); fp32 tensors are returned as the observations themselves
+        (the kernel's output), so the rows alias the storage slot as on the GPU."""
+        if policy is not None and self.camera is not None and policy.dtype != torch.float32:
+            raise ValueError("set_obs_sink: the camera task's rows sink into float32 tensors only")
         self._sink = None if policy is None else (policy, critic)
 
     def _obs(self):
         pol, cri = ((self.orc.img_policy, self.orc.img_critic) if self.camera is not None
                     else (self.orc.obs_policy, self.orc.obs_critic))
+        aux = torch.from_numpy(self.orc.obs_aux.copy()).unsqueeze(1)
         if self._sink is not None:
             self._sink[0].copy_(torch.from_numpy(pol))
             self._sink[1].copy_(torch.from_numpy(cri))
+            if self._sink[0].dtype == torch.float32:
+                return {"policy": self._sink[0], "critic": self._sink[1], "auxiliary": aux}
         return {"policy": torch.from_numpy(pol.copy()),
                 "critic": torch.from_numpy(cri.copy()),
                 "auxiliary": torch.from_numpy(self.orc.obs_aux.copy()).unsqueeze(1)}

@@ -173,3 +173,33 @@ def test_camera_obstacles_in_view_and_slot_overflow():
     assert (orc.depth < 4.0).mean() > 0.05
     assert ot.counts.max() > 64
     env.close()
+
+
+def test_vision_runner_camera_sink_matches_copy():
+    """The registered vision recipe (VisionActorCritic + PPOL2C2) with the camera observation sink (the camera
+    kernel writes its [16 state | image] rows straight into the rollout storage slot, fp32) stores the same rows
+    and trains to the same parameters as the copy path (rollout_storage.py:74-88)."""
+    from generalizableracing_amd.envs.racing_cfg import RacingVisionEnvCfg
+    from generalizableracing_amd.envs.racing_env import RslRlVecEnvWrapper
+    from generalizableracing_amd.rsl_rl import OnPolicyRunner, QuadcopterVisionPPORunnerCfg
+
+    runs = []
+    for sink in (True, False):
+        torch.manual_seed(4)
+        cfg = QuadcopterVisionPPORunnerCfg(device=DEV, num_steps_per_env=6)
+        cfg.algorithm.obs_sink = sink
+        env = RacingEnv(RacingVisionEnvCfg(scene=SceneCfg(num_envs=256), sim=SimCfg(device=DEV)))
+        r = OnPolicyRunner(RslRlVecEnvWrapper(env), cfg.to_dict(), log_dir=None, device=DEV)
+        assert r.obs_sink is sink
+        r.learn(2)
+        torch.cuda.synchronize()
+        runs.append(r)
+    a, b = runs
+    T = a.num_steps_per_env
+    assert a.alg.storage.observations.shape[0] == T + 1
+    assert torch.equal(a.alg.storage.observations[1:T], b.alg.storage.observations[1:T])
+    assert torch.equal(a.alg.storage.privileged_observations[1:T], b.alg.storage.privileged_observations[1:T])
+    for (k, x), (_, y) in zip(a.alg.policy.state_dict().items(), b.alg.policy.state_dict().items()):
+        assert torch.equal(x, y), k
+    for r in runs:
+        r.env.close()

@@ -120,3 +120,73 @@ def test_runner_trains_with_l2c2(tmp_path):
         assert math.isfinite(log[k]), k
     assert log["smooth_loss"] > 0.0
     assert (tmp_path / "model_1.pt").exists()
+
+
+def _drive(alg, obs_seq, sink):
+    """The runner's collection loop (on_policy_runner.py learn) over a scripted observation sequence; with `sink`
+    the env writes each step's rows into the storage slot and returns that slot (RacingEnv's fp32 sink)."""
+    st = alg.storage
+    obs = obs_seq[0].clone()
+    for t in range(1, len(obs_seq)):
+        alg.act(obs, obs * 2.0)
+        if sink:
+            p, c = st.sink_slot(st.step + 1)
+            p.copy_(obs_seq[t])
+            c.copy_(obs_seq[t] * 2.0)
+            obs = p
+        else:
+            obs = obs_seq[t].clone()
+        alg.process_env_step(torch.ones(obs.shape[0]), torch.zeros(obs.shape[0], dtype=torch.long), {})
+
+
+def test_observation_sink_with_zero_observation_skip():
+    """PPOL2C2 with the observation sink stores the same transitions as the copy path, also across
+    ppo_l2c2.py:98's skip of an all-zero observation batch (the skipped transition's successor rows move down a
+    slot: RolloutStorage.sink_skipped)."""
+    T, N, D = 6, 5, 4
+    g = torch.Generator().manual_seed(3)
+    obs_seq = [torch.randn(N, D, generator=g) for _ in range(T + 2)]
+    obs_seq[2] = torch.zeros(N, D)  # the transition acting on these rows is skipped
+    stores = []
+    for sink in (True, False):
+        torch.manual_seed(0)
+        alg = PPOL2C2(ActorCritic(D, D, 2, [8], [8], "lrelu"), device="cpu")
+        alg.init_storage("rl", N, T, [D], [D], [2])
+        if sink:
+            alg.storage.enable_obs_sink()
+        torch.manual_seed(1)
+        _drive(alg, obs_seq, sink)
+        stores.append(alg.storage)
+    a, b = stores
+    assert a.step == b.step == T
+    assert torch.equal(a.observations[:T], b.observations)
+    assert torch.equal(a.privileged_observations[:T], b.privileged_observations)
+    assert torch.equal(a.actions, b.actions)
+    # the stored rows are the scripted ones minus the skipped batch
+    want = torch.stack([o for k, o in enumerate(obs_seq[:T + 1]) if k != 2])
+    assert torch.equal(b.observations, want)
+
+
+def test_runner_l2c2_camera_sink_matches_copy():
+    """OnPolicyRunner + PPOL2C2 on the camera task (oracle env, [16 | image] rows): with the fp32 observation sink
+    the stored rows and the trained parameters equal the copy path's."""
+    from generalizableracing_amd.envs.racing_cfg import CameraCfg
+
+    runs = []
+    for sink in (True, False):
+        torch.manual_seed(0)
+        cfg = QuadcopterL2C2PPORunnerCfg(device="cpu", num_steps_per_env=4)
+        cfg.policy.actor_hidden_dims = [16]
+        cfg.policy.critic_hidden_dims = [16]
+        cfg.algorithm.obs_sink = sink
+        cam = CameraCfg(width=16, height=8)
+        r = OnPolicyRunner(OracleVecEnv(num_envs=8, camera=cam), cfg.to_dict(), log_dir=None, device="cpu")
+        assert r.obs_sink is sink
+        r.learn(2)
+        runs.append(r)
+    a, b = runs
+    T = a.num_steps_per_env
+    assert a.alg.storage.observations.shape[2] == 16 + 16 * 8
+    assert torch.equal(a.alg.storage.observations[1:T], b.alg.storage.observations[1:T])
+    for (k, x), (_, y) in zip(a.alg.policy.state_dict().items(), b.alg.policy.state_dict().items()):
+        assert torch.equal(x, y), k

@@ -133,8 +133,20 @@ def test_obs_sink_matches_copy(obs_dtype):
         assert torch.equal(x, y), k
 
 
-def test_obs_sink_not_used_for_l2c2():
-    cfg = small_cfg()
-    cfg.algorithm.class_name = "PPOL2C2"
-    r = OnPolicyRunner(OracleVecEnv(num_envs=16), cfg.to_dict(), log_dir=None, device="cpu")
-    assert not r.obs_sink
+def test_obs_sink_l2c2_matches_copy():
+    """PPOL2C2 (whose storage pairs slot t with slot t + 1) with the sink trains like the copy path."""
+    runs = []
+    for sink in (True, False):
+        torch.manual_seed(5)
+        cfg = small_cfg()
+        cfg.algorithm.class_name = "PPOL2C2"
+        cfg.algorithm.obs_sink = sink
+        r = OnPolicyRunner(OracleVecEnv(num_envs=16), cfg.to_dict(), log_dir=None, device="cpu")
+        assert r.obs_sink is sink
+        r.learn(2)
+        runs.append(r)
+    a, b = runs
+    T = a.num_steps_per_env
+    assert torch.equal(a.alg.storage.observations[1:T], b.alg.storage.observations[1:T])
+    for (k, x), (_, y) in zip(a.alg.policy.state_dict().items(), b.alg.policy.state_dict().items()):
+        assert torch.equal(x, y), k

@@ -65,7 +65,8 @@ def test_vision_runner_with_l2c2_on_the_oracle_camera_env(tmp_path):
     env = OracleVecEnv(num_envs=20, types=4, camera=CameraCfg())
     runner = OnPolicyRunner(env, d, log_dir=str(tmp_path), device="cpu")
     assert isinstance(runner.alg, PPOL2C2) and isinstance(runner.alg.policy, VisionActorCritic)
-    assert runner.alg.storage.observations.shape == (4, 20, OBS)
+    # (the camera rows sink into the storage: one more slot holds the rollout's last observations)
+    assert runner.obs_sink and runner.alg.storage.observations.shape == (4 + 1, 20, OBS)
     runner.learn(1)
     for k in ("value_function", "surrogate", "smooth_loss"):
         assert math.isfinite(runner.last_log[k]), k
