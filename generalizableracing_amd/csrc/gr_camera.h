@@ -166,6 +166,12 @@ GR_HD void gr_cam_gate_setup(const float* g, const float o[3], const float c0[3]
   s[GR_CS_HOH] = g[17];
 }
 
+/* kernel-only tile cull of a gate slot: its outer box (gr_cam_box_outside, gr_obstacles.h) */
+GR_HD int gr_cam_gate_outside(const float* s, float a_lo, float a_hi, float b_lo, float b_hi) {
+  const float l[3] = {s[GR_CS_HOW], s[GR_CS_HOH], s[GR_CS_HT]};
+  return gr_cam_box_outside(s, l, a_lo, a_hi, b_lo, b_hi);
+}
+
 /* One obstacle (GR_OBST_FLOATS record, gr_obstacles.h); hit by gr_cam_obst_hit. */
 GR_HD void gr_cam_obst_setup(const float* r, const float o[3], const float c0[3], const float c1[3],
                              const float c2[3], float max_distance, float* s) {

@@ -141,11 +141,14 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
   constexpr bool obst = OBST;
   const int ntx = (W + 31) / 32, nty = (H + 7) / 8;
   const int oslots = obst ? (int)camera_obst_floats(W, H) : 0;
-  float* wave_lds = smem + wpad + hpad + w * (G * GR_CAM_SLOT + oslots + 8 * W);
-  float4* s_slot = reinterpret_cast<float4*>(wave_lds);                             // [G][CAM_SLOT4]
-  float4* s_oslot = reinterpret_cast<float4*>(wave_lds + G * GR_CAM_SLOT);          // [64][GR_CAM_OSLOT / 4]
-  uint64_t* s_tmask = reinterpret_cast<uint64_t*>(wave_lds + G * GR_CAM_SLOT + GR_CAM_OBST_SLOTS * GR_CAM_OSLOT);
-  float4* s_stage = reinterpret_cast<float4*>(wave_lds + G * GR_CAM_SLOT + oslots);  // [8 * W / 4]
+  const int tmf = (int)camera_tile_mask_floats(W, H);
+  float* wave_lds = smem + wpad + hpad + w * (G * GR_CAM_SLOT + tmf + oslots + 8 * W);
+  float4* s_slot = reinterpret_cast<float4*>(wave_lds);                               // [G][CAM_SLOT4]
+  uint64_t* s_gmask = reinterpret_cast<uint64_t*>(wave_lds + G * GR_CAM_SLOT);        // [tiles]
+  float* olds = wave_lds + G * GR_CAM_SLOT + tmf;
+  float4* s_oslot = reinterpret_cast<float4*>(olds);                                  // [64][GR_CAM_OSLOT / 4]
+  uint64_t* s_tmask = reinterpret_cast<uint64_t*>(olds + GR_CAM_OBST_SLOTS * GR_CAM_OSLOT);  // [tiles]
+  float4* s_stage = reinterpret_cast<float4*>(olds + oslots);                         // [8 * W / 4]
 
   // ---- is the sensor outdated? (SensorBase.update / reset; wave-uniform)
   int render = 0;
@@ -171,6 +174,7 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
   uint64_t valid_mask = 0;
   const float* orecs = nullptr;  // this track's obstacle records
   int nob = 0, ofrom = 0;         // obstacles in the track; raw index of the first one beyond the slots
+  int ns = 0;                     // obstacle slots in LDS
   if (render) {
     const float4 posq = reinterpret_cast<const float4*>(a.state)[(size_t)GR_P_POSQ * N + i];
     const float4 qv = reinterpret_cast<const float4*>(a.state)[(size_t)GR_P_QV * N + i];
@@ -224,14 +228,30 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
         }
         nv += nb;
       }
-      const int ns = nv < GR_CAM_OBST_SLOTS ? nv : GR_CAM_OBST_SLOTS;
-      // per 8x32 tile: the slots whose window meets the tile's ray range (a_u, b_v decrease with u, v) and whose
-      // bounding box reaches into the tile's frustum (gr_cam_obst_outside)
-      wave_lds_sync();
-      for (int tl = lane; tl < ntx * nty; tl += 64) {
-        const int v0 = 8 * (tl / ntx), u0 = 32 * (tl % ntx);
-        const int v1 = (v0 + 7 < H ? v0 + 7 : H - 1), u1 = (u0 + 31 < W ? u0 + 31 : W - 1);
-        const float a_hi = cc->ray_a[u0], a_lo = cc->ray_a[u1], b_hi = cc->ray_b[v0], b_lo = cc->ray_b[v1];
+      ns = nv < GR_CAM_OBST_SLOTS ? nv : GR_CAM_OBST_SLOTS;
+    }
+    // per 8x32 tile: the gates and obstacle slots whose window meets the tile's ray range (a_u, b_v decrease
+    // with u, v) and whose bounding box reaches into the tile's frustum (gr_cam_gate_outside / _obst_outside)
+    wave_lds_sync();
+    for (int tl = lane; tl < ntx * nty; tl += 64) {
+      const int v0 = 8 * (tl / ntx), u0 = 32 * (tl % ntx);
+      const int v1 = (v0 + 7 < H ? v0 + 7 : H - 1), u1 = (u0 + 31 < W ? u0 + 31 : W - 1);
+      const float a_hi = cc->ray_a[u0], a_lo = cc->ray_a[u1], b_hi = cc->ray_b[v0], b_lo = cc->ray_b[v1];
+      uint64_t gm = 0;
+      for (uint64_t m = valid_mask; m; m &= m - 1) {
+        const int g = __builtin_ctzll(m);
+        float sg[GR_CAM_SLOT];
+#pragma unroll
+        for (int k = 0; k < CAM_SLOT4; ++k) {
+          const float4 q4 = s_slot[g * CAM_SLOT4 + k];
+          sg[4 * k] = q4.x; sg[4 * k + 1] = q4.y; sg[4 * k + 2] = q4.z; sg[4 * k + 3] = q4.w;
+        }
+        const bool meet = !(sg[GR_CS_AMAX] < a_lo || sg[GR_CS_AMIN] > a_hi || sg[GR_CS_BMAX] < b_lo ||
+                            sg[GR_CS_BMIN] > b_hi) && !gr_cam_gate_outside(sg, a_lo, a_hi, b_lo, b_hi);
+        gm |= (uint64_t)meet << g;
+      }
+      s_gmask[tl] = gm;
+      if constexpr (obst) {
         uint64_t tm = 0;
         for (int k = 0; k < ns; ++k) {
           const float4 wk = s_oslot[k * (GR_CAM_OSLOT / 4) + 4];
@@ -282,7 +302,7 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
         const float dz = gr_fmaf(b, c2[2], gr_fmaf(av[j], c1[2], c0[2]));
         d[j] = gr_cam_ground_hit(o[2], gz, dz);
       }
-      uint64_t m = valid_mask;
+      uint64_t m = s_gmask[(v0 >> 3) * ntx + (u_t >> 5)];
       while (m) {
         const int g = __builtin_ctzll(m);
         m &= m - 1;

@@ -124,16 +124,20 @@ hipError_t launch_column_sum(const void* x, int dtype, long long m, int n, float
 // are set up again per tile from their records)
 #define GR_CAM_OBST_SLOTS 64
 #define GR_CAM_OSLOT 20  // floats per obstacle slot in LDS: gate-slot floats 0-15, then the window (17-20)
-// dynamic LDS of the camera kernel: ray tables + per wave (gate slots [+ obstacle slots] + an 8-row
-// staging band)
-// obstacle slots + one 64-bit mask per 8x32 tile (the slots whose window meets the tile)
+// dynamic LDS of the camera kernel: ray tables + per wave (gate slots, one 64-bit gate mask per 8x32 tile
+// [+ obstacle slots and their tile masks] + an 8-row staging band); every part a multiple of 4 floats
+__host__ __device__ inline size_t camera_tile_mask_floats(int width, int height) {
+  return (2 * (size_t)((height + 7) / 8) * ((width + 31) / 32) + 3) & ~(size_t)3;
+}
+// obstacle slots + one 64-bit mask per 8x32 tile (the slots that can cover a pixel of the tile)
 __host__ __device__ inline size_t camera_obst_floats(int width, int height) {
-  return (size_t)GR_CAM_OBST_SLOTS * GR_CAM_OSLOT + 2 * (size_t)((height + 7) / 8) * ((width + 31) / 32);
+  return (size_t)GR_CAM_OBST_SLOTS * GR_CAM_OSLOT + camera_tile_mask_floats(width, height);
 }
 inline size_t camera_lds_bytes(int width, int height, int max_gates, bool obst) {
   const size_t wpad = (size_t)((width + 3) & ~3), hpad = (size_t)((height + 3) & ~3);
   const size_t os = obst ? camera_obst_floats(width, height) : 0;
-  return 4 * (wpad + hpad + 4 * ((size_t)max_gates * 24 + os + 8 * (size_t)width));
+  return 4 * (wpad + hpad +
+              4 * ((size_t)max_gates * 24 + camera_tile_mask_floats(width, height) + os + 8 * (size_t)width));
 }
 
 hipError_t launch_env(int mode, const KArgs& a, const float* actions, const uint8_t* mask, hipStream_t s,

@@ -139,12 +139,12 @@ GR_HD int gr_cam_box_beyond(float x0, float cp, const float* d0, const float* dp
 }
 
 /* Kernel-only cull of a camera slot against a tile of pixel rays a in [a_lo, a_hi], b in [b_lo, b_hi] (the oracle
- * tests every pixel of the slot's window, so this only skips pixels that cannot hit): the primitive's local
- * bounding box lies wholly beyond one side plane of the tile's frustum.  A window spans the box's 8 projected
- * corners, and is the whole screen when the box reaches behind the camera plane (a wall alongside the drone);
- * the planes cut both down to the tiles the box can actually cover.  Camera coordinates from the slot: the
- * centre is -(D0 . O, D1 . O, D2 . O), primitive axis j is (D0[j], D1[j], D2[j]). */
-GR_HD int gr_cam_obst_outside(const float* s, float a_lo, float a_hi, float b_lo, float b_hi) {
+ * tests every pixel of the slot's window, so this only skips pixels that cannot hit): the solid's local bounding
+ * box (half sizes l) lies wholly beyond one side plane of the tile's frustum.  A window spans the box's 8
+ * projected corners, and is the whole screen when the box reaches behind the camera plane (a wall alongside the
+ * drone, a gate being flown through); the planes cut both down to the tiles the box can actually cover.  Camera
+ * coordinates from the slot: the centre is -(D0 . O, D1 . O, D2 . O), local axis j is (D0[j], D1[j], D2[j]). */
+GR_HD int gr_cam_box_outside(const float* s, const float l[3], float a_lo, float a_hi, float b_lo, float b_hi) {
   const float* O = s;
   const float* D0 = s + 3;
   const float* D1 = s + 6;
@@ -152,10 +152,15 @@ GR_HD int gr_cam_obst_outside(const float* s, float a_lo, float a_hi, float b_lo
   const float x0 = -((D0[0] * O[0] + D0[1] * O[1]) + D0[2] * O[2]);
   const float y0 = -((D1[0] * O[0] + D1[1] * O[1]) + D1[2] * O[2]);
   const float z0 = -((D2[0] * O[0] + D2[1] * O[1]) + D2[2] * O[2]);
-  const int kind = (int)s[GR_OS_KIND];
-  const float l[3] = {s[GR_OS_E0], s[GR_OS_E1], kind == GR_OBST_CAPSULE ? s[GR_OS_E2] + s[GR_OS_E0] : s[GR_OS_E2]};
   return gr_cam_box_beyond(x0, y0, D0, D1, l, a_hi, 1.0f) | gr_cam_box_beyond(x0, y0, D0, D1, l, a_lo, -1.0f) |
          gr_cam_box_beyond(x0, z0, D0, D2, l, b_hi, 1.0f) | gr_cam_box_beyond(x0, z0, D0, D2, l, b_lo, -1.0f);
+}
+
+/* an obstacle slot (gr_cam_obst_setup): the primitive's local bounding box */
+GR_HD int gr_cam_obst_outside(const float* s, float a_lo, float a_hi, float b_lo, float b_hi) {
+  const int kind = (int)s[GR_OS_KIND];
+  const float l[3] = {s[GR_OS_E0], s[GR_OS_E1], kind == GR_OBST_CAPSULE ? s[GR_OS_E2] + s[GR_OS_E0] : s[GR_OS_E2]};
+  return gr_cam_box_outside(s, l, a_lo, a_hi, b_lo, b_hi);
 }
 
 /* first crossing (s > 0) of the ray o + s d with the slab |x_j| <= h_j intersected with

@@ -928,41 +928,48 @@ float gro_camera_ray(const gr_config* c, const gr_camera_config* kcfg, const gro
   return gr_cam_clip(d, K.max_distance);
 }
 
-/* Check of the camera kernel's per-tile obstacle cull (gr_cam_obst_outside, kernel-only): for the pose (p, q) on
- * `track`, over every (8 x 32 tile, obstacle in view) pair whose window meets the tile, out[0] = pairs, out[1] =
- * pairs the cull removes, out[2] = removed pairs with some pixel of the window that the oracle's per-pixel test
- * hits (must be 0), out[3] = window pixels of the removed pairs. */
+/* Check of the camera kernel's per-tile cull (gr_cam_gate_outside / gr_cam_obst_outside, kernel-only): for the
+ * pose (p, q) on `track`, over every (8 x 32 tile, gate or obstacle in view) pair whose window meets the tile,
+ * out[0] = pairs, out[1] = pairs the cull removes, out[2] = removed pairs with some pixel of the window that the
+ * oracle's per-pixel test hits (must be 0), out[3] = window pixels of the removed pairs; gates in out[0..3],
+ * obstacles in out[4..7]. */
 void gro_camera_cull_check(const gr_config* c, const gr_camera_config* kcfg, const gro_tracks* tr, int track,
-                           const float p[3], const float q[4], int64_t out[4]) {
+                           const float p[3], const float q[4], int64_t out[8]) {
   gr_cam_const K;
   gr_cam_derive(kcfg, c->step_dt, &K);
   float o[3], c0[3], c1[3], c2[3];
   gr_cam_pose(&K, p, q, o, c0, c1, c2);
   const int W = K.width, H = K.height;
-  const int no = track_num_obst(tr, track);
-  for (int j = 0; j < 4; ++j) out[j] = 0;
-  for (int j = 0; j < no; ++j) {
+  const int ng = track_num_gates(tr, track), no = track_num_obst(tr, track);
+  for (int j = 0; j < 8; ++j) out[j] = 0;
+  for (int j = 0; j < ng + no; ++j) {
+    const int gate = j < ng;
+    int64_t* ot = out + (gate ? 0 : 4);
     float sl[GR_CAM_SLOT];
-    gr_cam_obst_setup(obst_rec(tr, track, j), o, c0, c1, c2, K.max_distance, sl);
+    if (gate)
+      gr_cam_gate_setup(gate_rec(c, tr, track, j), o, c0, c1, c2, K.max_distance, sl);
+    else
+      gr_cam_obst_setup(obst_rec(tr, track, j - ng), o, c0, c1, c2, K.max_distance, sl);
     if (sl[GR_CS_VALID] == 0.0f) continue;
     for (int v0 = 0; v0 < H; v0 += 8) {
       for (int u0 = 0; u0 < W; u0 += 32) {
         const int v1 = v0 + 7 < H ? v0 + 7 : H - 1, u1 = u0 + 31 < W ? u0 + 31 : W - 1;
         const float a_hi = K.ray_a[u0], a_lo = K.ray_a[u1], b_hi = K.ray_b[v0], b_lo = K.ray_b[v1];
         if (sl[GR_CS_AMAX] < a_lo || sl[GR_CS_AMIN] > a_hi || sl[GR_CS_BMAX] < b_lo || sl[GR_CS_BMIN] > b_hi) continue;
-        out[0] += 1;
-        if (!gr_cam_obst_outside(sl, a_lo, a_hi, b_lo, b_hi)) continue;
-        out[1] += 1;
+        ot[0] += 1;
+        if (!(gate ? gr_cam_gate_outside(sl, a_lo, a_hi, b_lo, b_hi) : gr_cam_obst_outside(sl, a_lo, a_hi, b_lo, b_hi)))
+          continue;
+        ot[1] += 1;
         int hit = 0;
         for (int v = v0; v <= v1; ++v)
           for (int u = u0; u <= u1; ++u) {
             const float a = K.ray_a[u], b = K.ray_b[v];
             if (b >= sl[GR_CS_BMIN] && b <= sl[GR_CS_BMAX] && a >= sl[GR_CS_AMIN] && a <= sl[GR_CS_AMAX]) {
-              out[3] += 1;
-              hit |= gr_cam_obst_hit(sl, a, b) < 3.0e38f;
+              ot[3] += 1;
+              hit |= (gate ? gr_cam_gate_hit(sl, a, b) : gr_cam_obst_hit(sl, a, b)) < 3.0e38f;
             }
           }
-        out[2] += hit;
+        ot[2] += hit;
       }
     }
   }

@@ -77,7 +77,7 @@ void gro_camera(const gr_config* cfg, const gr_camera_config* kcfg, const gro_en
 float gro_camera_ray(const gr_config* cfg, const gr_camera_config* kcfg, const gro_tracks* tr, int track,
                      const float p[3], const float q[4], int u, int v);
 void gro_camera_cull_check(const gr_config* cfg, const gr_camera_config* kcfg, const gro_tracks* tr, int track,
-                           const float p[3], const float q[4], int64_t out[4]);
+                           const float p[3], const float q[4], int64_t out[8]);
 void gro_camera_frame(const gr_config* cfg, const gr_camera_config* kcfg, const float p[3], const float q[4],
                       float* out);
 /* OpenMP threads gro_step uses (1 without OpenMP) */

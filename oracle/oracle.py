@@ -175,12 +175,13 @@ class Oracle:
         return out[0:3], out[3:6], out[6:9], out[9:12], out[12:12 + W], out[12 + W:]
 
     def camera_cull_check(self, track: int, p, q) -> np.ndarray:
-        """gro_camera_cull_check: [pairs, culled pairs, culled pairs with a hit (must be 0), culled window pixels]."""
-        out = np.zeros(4, np.int64)
+        """gro_camera_cull_check: [[pairs, culled pairs, culled pairs with a hit (must be 0), culled window pixels]
+        of the gates, the same of the obstacles]."""
+        out = np.zeros(8, np.int64)
         self.lib.gro_camera_cull_check(C.byref(self.cfg), C.byref(self.cam_cfg), C.byref(self.tracks), track,
                                        _p(np.ascontiguousarray(p, np.float32)), _p(np.ascontiguousarray(q, np.float32)),
                                        _p(out))
-        return out
+        return out.reshape(2, 4)
 
     def collision_count(self, track: int, p, q) -> int:
         p = np.ascontiguousarray(p, dtype=np.float32)

@@ -351,22 +351,24 @@ def test_camera_obstacle_known_answers():
         assert orc.camera_ray(0, p, qb, u, v) == pytest.approx(cam.max_distance)
 
 
-def test_camera_tile_cull_is_conservative(gen):
-    """camera_kernel<true>'s per-tile obstacle cull (gr_cam_obst_outside: the bounding box beyond a side plane of
-    the 8x32 tile's frustum; kernel-only, the oracle tests every window pixel) never removes a (tile, obstacle)
-    pair with a pixel the per-pixel test hits, at poses all around the obstacles (close, grazing, inside the
-    window-is-the-whole-screen case of a box reaching behind the camera) — and it removes many pairs."""
-    _, tracks, ot = gen
-    orc = isolated_oracle(ot)
+def test_camera_tile_cull_is_conservative():
+    """camera_kernel's per-tile cull (gr_cam_gate_outside / gr_cam_obst_outside: the bounding box beyond a side
+    plane of the 8x32 tile's frustum; kernel-only, the oracle tests every window pixel) never removes a (tile,
+    gate or obstacle) pair with a pixel the per-pixel test hits, at poses all around the obstacles and through the
+    gates (close, grazing, the window-is-the-whole-screen case of a box reaching behind the camera) — and it
+    removes many pairs."""
+    gates, recs, ot = T.build_tracks(num_types=20, num_levels=10, num_gates=8, seed=42)
+    orc = oracle.Oracle(gr_cfg(16), gates, recs, ot.records, ot.counts)
     orc.enable_camera(CameraCfg().to_gr())
     rng = np.random.default_rng(5)
-    L = len(tracks[0])
-    tot = np.zeros(4, np.int64)
+    tot = np.zeros((2, 4), np.int64)
     for k in range(0, ot.records.shape[0], 7):
-        tr = tracks[k // L][k % L]
-        for _ in range(6):
-            o = tr.obstacles[rng.integers(len(tr.obstacles))]
-            p = (o.pos - tr.origin + rng.uniform(-1, 1, 3) * rng.choice([0.5, 1.5, 4.0])).astype(np.float32)
+        for j in range(8):
+            if j % 2:  # near an obstacle
+                centre = ot.records[k, rng.integers(ot.counts[k]), 0:3]
+            else:  # in or near a gate's frame
+                centre = gates[k, rng.integers(gates.shape[1]), 0:3]
+            p = (centre + rng.uniform(-1, 1, 3) * rng.choice([0.3, 1.5, 4.0])).astype(np.float32)
             roll, pitch, yaw = rng.uniform(-0.5, 0.5), rng.uniform(-0.5, 0.5), rng.uniform(-math.pi, math.pi)
             R = T.euler_matrix_rxyz(np.array([roll, pitch, yaw]))
             w = math.sqrt(max(1e-12, 1 + R[0, 0] + R[1, 1] + R[2, 2])) / 2
@@ -374,7 +376,7 @@ def test_camera_tile_cull_is_conservative(gen):
                          np.float32)
             q /= np.linalg.norm(q)
             r = orc.camera_cull_check(k, p, q)
-            assert r[2] == 0, (k, p, q, r)
+            assert r[0, 2] == 0 and r[1, 2] == 0, (k, p, q, r)
             tot += r
-    print("pairs, culled, culled with a hit, culled window pixels:", tot)
-    assert tot[1] > tot[0] // 4, tot  # (~half the pairs at training poses: scripts/diag_camera_windows.py)
+    print("[gates, obstacles] x [pairs, culled, culled with a hit, culled window pixels]:", tot.tolist())
+    assert tot[0, 1] > tot[0, 0] // 10 and tot[1, 1] > tot[1, 0] // 4, tot
