@@ -803,6 +803,35 @@ int gr_column_sum(const void* x, int dtype, int64_t rows, int32_t cols, float* p
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
+int64_t gr_head_partials(int64_t rows, int32_t k, int32_t h) {
+  if (rows < 0 || k < 1 || k > 8 || h < 4 || h > 256 || h % 4) return GR_ERR_ARG;
+  return (int64_t)gr::head_blocks(rows) * (k * h + k);
+}
+
+static bool head_args_ok(const float* z, int64_t rows, int32_t h, const float* w, int32_t k) {
+  return z && w && rows >= 0 && k >= 1 && k <= 8 && h >= 4 && h <= 256 && h % 4 == 0 &&
+         reinterpret_cast<uintptr_t>(z) % 16 == 0;
+}
+
+int gr_head_forward(const float* z, int64_t rows, int32_t h, const float* w, const float* b, int32_t k, float slope,
+                    float* y, void* stream) {
+  if (!head_args_ok(z, rows, h, w, k) || !b || !y) return GR_ERR_ARG;
+  if (rows == 0) return GR_OK;
+  const hipError_t e = gr::launch_head_forward(z, (long long)rows, h, w, b, k, slope, y, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
+int gr_head_backward(const float* z, const float* gy, int64_t rows, int32_t h, const float* w, int32_t k, float slope,
+                     float* gz, float* partial, float* gw, float* gb, void* stream) {
+  if (!head_args_ok(z, rows, h, w, k) || !gy || !gz || !partial || !gw || !gb ||
+      reinterpret_cast<uintptr_t>(gz) % 16 != 0)
+    return GR_ERR_ARG;
+  if (rows == 0) return GR_ERR_ARG;
+  const hipError_t e = gr::launch_head_backward(z, gy, (long long)rows, h, w, k, slope, gz, partial, gw, gb,
+                                                (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
 int gr_test_dynamics(gr_ctx* c, int n, int mode, const float* si, const float* ab, const float* cmd, const float* ci,
                      const float* par, const float* drag, float* so, float* co, float* xo, void* stream) {
   if (!c || n <= 0 || !si || !ab || !cmd || !ci || !par || !drag || !so || !co || !xo) return GR_ERR_ARG;

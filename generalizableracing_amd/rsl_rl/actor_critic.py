@@ -12,7 +12,7 @@ import torch
 import torch.nn as nn
 from torch.distributions import Normal
 
-from .linear import TallLinear
+from .linear import MLP, TallLinear
 
 
 def resolve_nn_activation(name: str) -> nn.Module:
@@ -26,7 +26,8 @@ def resolve_nn_activation(name: str) -> nn.Module:
 
 
 def _mlp(inp: int, hidden: list, out: int, act: str) -> nn.Sequential:
-    # TallLinear = nn.Linear (same parameters / state_dict keys) with a row-split weight gradient (linear.py)
+    # TallLinear = nn.Linear (same parameters / state_dict keys) with a row-split weight gradient; MLP =
+    # nn.Sequential whose last LeakyReLU + Linear fuse on the update's tall batches (linear.py)
     layers = [TallLinear(inp, hidden[0]), resolve_nn_activation(act)]
     for i in range(len(hidden)):
         if i == len(hidden) - 1:
@@ -34,7 +35,7 @@ def _mlp(inp: int, hidden: list, out: int, act: str) -> nn.Sequential:
         else:
             layers.append(TallLinear(hidden[i], hidden[i + 1]))
             layers.append(resolve_nn_activation(act))
-    return nn.Sequential(*layers)
+    return MLP(*layers)
 
 
 class ActorCritic(nn.Module):

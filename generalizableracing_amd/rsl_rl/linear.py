@@ -7,6 +7,12 @@ hipBLASLt tiles only its small [out, in] output, so a handful of workgroups stre
 split into chunks of SPLIT (a batched GEMM: one workgroup set per chunk) and the partial products are
 summed.  Same module tree, parameters and state_dict keys as nn.Linear (the reference's checkpoints
 and exporters are unaffected); small batches, inference and TorchScript take F.linear.
+
+`MLP` (the actor / critic Sequential) runs its last LeakyReLU and output Linear as ONE op on those
+batches (`leaky_head`: gr_head_forward / gr_head_backward, gr_update.hip): the activation pass, the
+small-N head GEMMs and the activation's backward pass each stream a [rows, 256] matrix through HBM
+(`profiles/round03_update65536_graphed_kernel_stats.csv`), the fused op reads the pre-activation once
+forward and once backward.
 """
 from __future__ import annotations
 
@@ -99,3 +105,88 @@ class TallLinear(nn.Linear):
                 and torch.is_grad_enabled() and self.weight.requires_grad:
             return _TallLinearFn.apply(x, self.weight, self.bias)
         return F.linear(x, self.weight, self.bias)
+
+
+# ------------------------------------------------------------------------------------------ fused head
+HEAD_MAX_OUT = 8      # gr_head_*: output features
+HEAD_MAX_IN = 256     # gr_head_*: input features (a multiple of 4)
+
+
+class _LeakyHeadFn(torch.autograd.Function):
+    """y = leaky_relu(z, slope) @ w^T + b on the device (gr_head_forward); backward gr_head_backward:
+    gz = (gy @ w) * leaky_relu'(z), gw = gy^T leaky_relu(z), gb = sum gy (fixed summation order)."""
+
+    @staticmethod
+    def forward(ctx, z, w, b, slope):
+        from .. import _abi
+
+        lib = _abi.load()
+        z, w, b = z.contiguous(), w.contiguous(), b.contiguous()
+        m, h = z.shape
+        k = w.shape[0]
+        y = torch.empty(m, k, device=z.device, dtype=torch.float32)
+        rc = lib.gr_head_forward(z.data_ptr(), m, h, w.data_ptr(), b.data_ptr(), k, float(slope), y.data_ptr(),
+                                 torch.cuda.current_stream(z.device).cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"gr_head_forward failed (status {rc})")
+        ctx.save_for_backward(z, w)
+        ctx.slope = float(slope)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from .. import _abi
+
+        lib = _abi.load()
+        z, w = ctx.saved_tensors
+        gy = gy.contiguous().float()
+        m, h = z.shape
+        k = w.shape[0]
+        gz = torch.empty_like(z)
+        part = torch.empty(lib.gr_head_partials(m, k, h), device=z.device, dtype=torch.float32)
+        gw = torch.empty_like(w)
+        gb = torch.empty(k, device=z.device, dtype=torch.float32)
+        rc = lib.gr_head_backward(z.data_ptr(), gy.data_ptr(), m, h, w.data_ptr(), k, ctx.slope, gz.data_ptr(),
+                                  part.data_ptr(), gw.data_ptr(), gb.data_ptr(),
+                                  torch.cuda.current_stream(z.device).cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"gr_head_backward failed (status {rc})")
+        return gz, gw, gb, None
+
+
+def leaky_head(z: torch.Tensor, w: torch.Tensor, b: torch.Tensor, slope: float) -> torch.Tensor:
+    """leaky_relu(z, slope) @ w^T + b as one device op with its own backward (HIP, gr_update.hip)."""
+    return _LeakyHeadFn.apply(z, w, b, slope)
+
+
+def head_fusable(x: torch.Tensor, act: nn.Module, lin: nn.Module) -> bool:
+    """The update's tall fp32 CUDA batches with LeakyReLU -> Linear(<= 256, <= 8) at the end of the MLP."""
+    return (isinstance(act, nn.LeakyReLU) and isinstance(lin, nn.Linear) and lin.bias is not None
+            and x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and lin.weight.dtype == torch.float32
+            and (x.shape[0] >= 2 * SPLIT or _FORCE_FN) and torch.is_grad_enabled() and lin.weight.requires_grad
+            and not torch.is_autocast_enabled("cuda")
+            and lin.out_features <= HEAD_MAX_OUT and lin.in_features <= HEAD_MAX_IN and lin.in_features % 4 == 0)
+
+
+class MLP(nn.Sequential):
+    """The actor / critic MLP: nn.Sequential with the same children and state_dict keys.  On the update's tall
+    CUDA mini-batches its last LeakyReLU + output Linear run fused (leaky_head); everywhere else (rollout,
+    inference, CPU, TorchScript) module by module."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if torch.jit.is_scripting():
+            for m in self:
+                x = m(x)
+            return x
+        return self._forward_eager(x)
+
+    @torch.jit.unused
+    def _forward_eager(self, x: torch.Tensor) -> torch.Tensor:
+        mods = list(self)
+        if len(mods) >= 2 and head_fusable(x, mods[-2], mods[-1]):
+            for m in mods[:-2]:
+                x = m(x)
+            return leaky_head(x, mods[-1].weight, mods[-1].bias, mods[-2].negative_slope)
+        for m in mods:
+            x = m(x)
+        return x

@@ -440,6 +440,21 @@ int gr_test_inject_fault(gr_ctx* ctx, int fault);
 int gr_column_sum_partials(int64_t rows);
 int gr_column_sum(const void* x, int dtype, int64_t rows, int32_t cols, float* partial, float* out, void* stream);
 
+/* The actor's / critic's output Linear fused with the LeakyReLU in front of it, for the PPO update's tall
+ * mini-batches (standalone/rsl_rl/ext/algorithms/ppo.py:103-190: update() -> policy.act / evaluate ->
+ * upstream rsl_rl ActorCritic's MLP [..., Linear(h, h), LeakyReLU, Linear(h, k)] and loss.backward() through it;
+ * generalizableracing_amd/rsl_rl/linear.py LeakyHead).  z [rows][h] fp32 row-major (16-byte aligned, h % 4 == 0,
+ * h <= 256) is the last hidden pre-activation, w [k][h] and b [k] the head (1 <= k <= 8), slope LeakyReLU's.
+ *   gr_head_forward : y [rows][k] = lrelu(z) w^T + b
+ *   gr_head_backward: gz [rows][h] = (gy w) * lrelu'(z), gw [k][h] = gy^T lrelu(z), gb [k] = sum gy
+ * Context-free, on `stream`, graph-capturable, no atomics, fixed summation order; `partial` is caller-owned
+ * scratch of gr_head_partials(rows, k, h) floats. */
+int64_t gr_head_partials(int64_t rows, int32_t k, int32_t h);
+int gr_head_forward(const float* z, int64_t rows, int32_t h, const float* w, const float* b, int32_t k, float slope,
+                    float* y, void* stream);
+int gr_head_backward(const float* z, const float* gy, int64_t rows, int32_t h, const float* w, int32_t k, float slope,
+                     float* gz, float* partial, float* gw, float* gb, void* stream);
+
 /* In-library HIP-event timing of the fused step kernel alone (not the log
  * finalize): when enabled, gr_step brackets the env kernel with a pair of
  * events on the caller's stream (ring of 4096 pairs; do not capture into a

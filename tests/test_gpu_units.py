@@ -185,3 +185,74 @@ def test_column_sum(rows, cols, dtype):
     assert got.dtype == torch.float32 and got.shape == (cols,)
     assert float(((got.double() - want).abs() / scale).max()) < 1e-6
     assert torch.equal(got, again)
+
+
+@pytest.mark.parametrize("rows,h,k", [(24576, 256, 4), (24576, 256, 1), (393216, 256, 4), (8193, 64, 8), (1, 4, 3),
+                                      (100003, 128, 2)])
+def test_leaky_head(rows, h, k):
+    """gr_head_forward / gr_head_backward (rsl_rl/linear.py leaky_head: the MLP's last LeakyReLU + output Linear on
+    the update's tall batches) against the same op in float64 torch: y, gz to 1e-6 of scale, gw / gb to a few ulps of the
+    absolute sums (4e-6); pre-activations exactly 0 take LeakyReLU's negative branch as torch does; repeats bit-identical."""
+    from generalizableracing_amd.rsl_rl.linear import leaky_head
+
+    dev = "cuda:0"
+    g = torch.Generator(device=dev).manual_seed(rows + 7 * h + k)
+    z = torch.randn(rows, h, device=dev, generator=g)
+    z[::7, ::5] = 0.0  # the kink
+    w = torch.randn(k, h, device=dev, generator=g) * 0.1
+    b = torch.randn(k, device=dev, generator=g)
+    gy = torch.randn(rows, k, device=dev, generator=g)
+    slope = 0.01
+    outs = []
+    for _ in range(2):
+        zz, ww, bb = (t.clone().requires_grad_(True) for t in (z, w, b))
+        y = leaky_head(zz, ww, bb, slope)
+        y.backward(gy)
+        outs.append((y.detach(), zz.grad, ww.grad, bb.grad))
+    torch.cuda.synchronize()
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)
+    y, gz, gw, gb = outs[0]
+    zd, wd, bd = (t.double().requires_grad_(True) for t in (z, w, b))
+    yd = torch.nn.functional.leaky_relu(zd, slope) @ wd.t() + bd
+    yd.backward(gy.double())
+    a = torch.nn.functional.leaky_relu(z.double(), slope)
+    assert float((y.double() - yd.detach()).abs().max()) <= 1e-6 * (1.0 + float((a.abs() @ wd.detach().abs().t()).max()))
+    assert float((gz.double() - zd.grad).abs().max()) <= 1e-6 * (1.0 + float(gy.abs().max() * w.abs().sum(0).max()))
+    # (fp32 running sums over a wave's rows, then the workgroups' partials in double: a few ulps of the absolute sum)
+    assert float((gw.double() - wd.grad).abs().max()) <= 4e-6 * float((gy.double().abs().t() @ a.abs()).max() + 1.0)
+    assert float((gb.double() - bd.grad).abs().max()) <= 4e-6 * float(gy.double().abs().sum(0).max() + 1.0)
+    # the kink: zero pre-activations take the negative branch (slope * gh), as torch's leaky_relu_backward
+    gh = (gy.double() @ w.double())
+    zero = z == 0
+    torch.testing.assert_close(gz[zero].double(), gh[zero] * slope, rtol=1e-5, atol=1e-9)
+
+
+def test_mlp_fused_head_matches_module_path():
+    """The actor / critic MLP with the fused head (tall CUDA batch) against the same module run layer by layer
+    (TallLinear + nn.LeakyReLU): outputs and every parameter gradient within fp32 summation-order noise."""
+    from generalizableracing_amd.rsl_rl import ActorCritic
+    from generalizableracing_amd.rsl_rl import linear
+
+    torch.manual_seed(3)
+    pol = ActorCritic(16, 16, 4, [256, 256], [256, 256], "lrelu").to("cuda:0")
+    x = torch.randn(3 * linear.SPLIT, 16, device="cuda:0")
+    assert linear.head_fusable(torch.empty(2 * linear.SPLIT, 256, device="cuda:0"), pol.actor[-2], pol.actor[-1])
+    res = []
+    for fused in (True, False):
+        pol.zero_grad()
+        if fused:
+            out = pol.actor(x).square().sum() + pol.critic(x).square().sum()
+        else:
+            def run(seq, v):
+                for m in seq:
+                    v = m(v)
+                return v
+            out = run(pol.actor, x).square().sum() + run(pol.critic, x).square().sum()
+        out.backward()
+        res.append((float(out), [p.grad.clone() for p in pol.parameters() if p.grad is not None]))
+    (oa, ga), (ob, gb_) = res
+    assert abs(oa - ob) <= 1e-5 * abs(ob)
+    assert len(ga) == len(gb_)
+    for a, b in zip(ga, gb_):
+        assert float((a - b).norm()) <= 1e-4 * float(b.norm()) + 1e-12
