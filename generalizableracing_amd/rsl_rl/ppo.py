@@ -271,26 +271,29 @@ class _GraphedStep:
         alg.optimizer = self.opt
         self.flat = alg.flat_grads()
         self.idx = torch.zeros(self.mb, dtype=torch.long, device=dev)
+        self.cols = st.sample_columns()  # packed sample rows (None: gathered field by field)
+        self.pack = st.pack_samples() if self.cols is not None else None  # persistent: the graphs read it
         self.vloss = torch.zeros((), device=dev)
         self.sloss = torch.zeros((), device=dev)
         self.segmented = gdist.is_dist() or alg.graph_update_segmented
         self.graph = None  # one rank: the whole step
         self.graph_b = None  # segmented: graph = segment A, graph_b = segment B
 
-    def _sources(self):
+    def _gather(self):
+        """The mini-batch's fields by the static index buffer: one row gather of the packed samples (refilled
+        before every update's replays, RolloutStorage.pack_samples), or one gather per field for wide rows."""
         st = self.alg.storage
-        obs = st.observations.flatten(0, 1)
-        priv = st.privileged_observations.flatten(0, 1) if st.privileged_observations is not None else obs
-        return (obs, priv, st.actions.flatten(0, 1), st.values.flatten(0, 1), st.advantages.flatten(0, 1),
-                st.returns.flatten(0, 1), st.actions_log_prob.flatten(0, 1), st.mu.flatten(0, 1),
-                st.sigma.flatten(0, 1))
+        if self.cols is not None:
+            g = self.pack.index_select(0, self.idx)
+            return tuple(g[:, a:b] for a, b in self.cols)
+        return tuple(x.index_select(0, self.idx) for x in st.sample_sources())
 
     def _adaptive(self) -> bool:
         return self.alg.desired_kl is not None and self.alg.schedule == "adaptive"
 
     def _seg_a(self):
         alg, pol = self.alg, self.alg.policy
-        obs, priv, act, val, adv, ret, logp, mu, sig = (x.index_select(0, self.idx) for x in self._sources())
+        obs, priv, act, val, adv, ret, logp, mu, sig = self._gather()
         obs, priv = obs.float(), priv.float()
         # the eager loop's policy.act also draws a sample it never uses; torch.normal's check of the std
         # reads back to the host, which a capture forbids, so only the distribution is set here
@@ -377,6 +380,8 @@ class _GraphedStep:
         alg = self.alg
         n = alg.num_mini_batches
         perm = torch.randperm(n * self.mb, device=self.idx.device)  # rollout_storage.py:152-191, drawn first
+        if self.pack is not None:  # this rollout's samples, packed in place (the graphs read the buffer)
+            alg.storage.pack_samples(out=self.pack)
         if self.graph is None:
             had_state = bool(self.opt.state)
             if not had_state:  # Adam's first step creates its state: take it with zero gradients, then undo

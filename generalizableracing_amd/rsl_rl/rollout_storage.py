@@ -156,6 +156,40 @@ class RolloutStorage:
         trajectory_lengths = done_indices[1:] - done_indices[:-1]
         return trajectory_lengths.float().mean(), self.rewards.mean()
 
+    PACK_MAX_COLS = 128  # sample rows up to this many floats are gathered as one packed row
+
+    def sample_sources(self):
+        """The per-sample fields the PPO mini-batches read, each [T * N, width]: observations, critic observations,
+        actions, values, advantages, returns, old log prob, old mean, old std."""
+        T = self.num_transitions_per_env
+        obs = self.observations[:T].flatten(0, 1)
+        priv = self.privileged_observations[:T].flatten(0, 1) if self.privileged_observations is not None else obs
+        return (obs, priv, self.actions.flatten(0, 1), self.values.flatten(0, 1), self.advantages.flatten(0, 1),
+                self.returns.flatten(0, 1), self.actions_log_prob.flatten(0, 1), self.mu.flatten(0, 1),
+                self.sigma.flatten(0, 1))
+
+    def sample_columns(self):
+        """Column ranges of the fields in a packed sample row (pack_samples), or None when the rows are too wide
+        to pack (the camera task's image rows: the fields are then gathered one by one)."""
+        widths = [x.shape[1] for x in self.sample_sources()]
+        if sum(widths) > self.PACK_MAX_COLS:
+            return None
+        cols, c = [], 0
+        for w in widths:
+            cols.append((c, c + w))
+            c += w
+        return cols
+
+    def pack_samples(self, out=None):
+        """[T * N, sum of widths] fp32: every field of a sample in one row, so a mini-batch is ONE row gather
+        (the fields one by one were nine gathers of 4-64-byte rows per mini-batch, each latency-bound:
+        profiles/round03_update65536_graphed_kernel_stats.csv).  Pure data movement: the mini-batches are
+        the same values."""
+        src = [x.float() for x in self.sample_sources()]
+        if out is None:
+            return torch.cat(src, dim=1)
+        return torch.cat(src, dim=1, out=out)
+
     def mini_batch_generator(self, num_mini_batches, num_epochs=8):
         """rollout_storage.py:152-191: one randperm, `num_epochs` passes of `num_mini_batches` chunks."""
         if self.training_type != "rl":
@@ -163,6 +197,14 @@ class RolloutStorage:
         batch_size = self.num_envs * self.num_transitions_per_env
         mini_batch_size = batch_size // num_mini_batches
         indices = torch.randperm(num_mini_batches * mini_batch_size, requires_grad=False, device=self.device)
+        cols = self.sample_columns()
+        if cols is not None:
+            pack = self.pack_samples()
+            for _ in range(num_epochs):
+                for i in range(num_mini_batches):
+                    g = pack.index_select(0, indices[i * mini_batch_size:(i + 1) * mini_batch_size])
+                    yield tuple(g[:, a:b] for a, b in cols) + ((None, None), None)
+            return
         observations = self.observations.flatten(0, 1)
         privileged = self.privileged_observations.flatten(0, 1) if self.privileged_observations is not None else observations
         actions = self.actions.flatten(0, 1)
