@@ -805,30 +805,54 @@ int gr_column_sum(const void* x, int dtype, int64_t rows, int32_t cols, float* p
 
 int64_t gr_head_partials(int64_t rows, int32_t k, int32_t h) {
   if (rows < 0 || k < 1 || k > 8 || h < 4 || h > 256 || h % 4) return GR_ERR_ARG;
-  return (int64_t)gr::head_blocks(rows) * (k * h + k);
+  return (int64_t)gr::head_partial_rows(rows) * ((k * h + k + h + 3) & ~3);
 }
 
-static bool head_args_ok(const float* z, int64_t rows, int32_t h, const float* w, int32_t k) {
-  return z && w && rows >= 0 && k >= 1 && k <= 8 && h >= 4 && h <= 256 && h % 4 == 0 &&
-         reinterpret_cast<uintptr_t>(z) % 16 == 0;
-}
+
 
 int gr_head_forward(const float* z, int64_t rows, int32_t h, const float* w, const float* b, int32_t k, float slope,
                     float* y, void* stream) {
-  if (!head_args_ok(z, rows, h, w, k) || !b || !y) return GR_ERR_ARG;
+  if (!z || !w || !b || !y || rows < 0 || k < 1 || k > 8 || h < 4 || h > 256 || h % 4 || !aligned16(z))
+    return GR_ERR_ARG;
   if (rows == 0) return GR_OK;
   const hipError_t e = gr::launch_head_forward(z, (long long)rows, h, w, b, k, slope, y, (hipStream_t)stream);
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
 int gr_head_backward(const float* z, const float* gy, int64_t rows, int32_t h, const float* w, int32_t k, float slope,
-                     float* gz, float* partial, float* gw, float* gb, void* stream) {
-  if (!head_args_ok(z, rows, h, w, k) || !gy || !gz || !partial || !gw || !gb ||
-      reinterpret_cast<uintptr_t>(gz) % 16 != 0)
+                     float* gz, float* partial, float* sums, void* stream) {
+  if (!z || !gy || !w || !gz || !partial || !sums || rows <= 0 || k < 1 || k > 8 || h < 4 || h > 256 || h % 4 ||
+      !aligned16(z) || !aligned16(gz) || !aligned16(partial))
     return GR_ERR_ARG;
-  if (rows == 0) return GR_ERR_ARG;
-  const hipError_t e = gr::launch_head_backward(z, gy, (long long)rows, h, w, k, slope, gz, partial, gw, gb,
-                                                (hipStream_t)stream);
+  const hipError_t e =
+      gr::launch_head_backward(z, gy, (long long)rows, h, w, k, slope, gz, partial, sums, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
+static bool in_args_ok(const float* x, int64_t rows, int32_t d, int32_t ldx, int32_t h) {
+  return x && rows > 0 && d >= 4 && d <= 32 && d % 4 == 0 && ldx >= d && ldx % 4 == 0 && h >= 4 && h <= 256 &&
+         h % 4 == 0 && aligned16(x);
+}
+
+int64_t gr_mlp_in_partials(int64_t rows, int32_t d, int32_t h) {
+  if (rows < 0 || d < 4 || d > 32 || d % 4 || h < 4 || h > 256 || h % 4) return GR_ERR_ARG;
+  return (int64_t)gr::head_partial_rows(rows) * (h * d + h);
+}
+
+int gr_mlp_in_forward(const float* x, int64_t rows, int32_t d, int32_t ldx, const float* w, const float* b, int32_t h,
+                      float slope, float* y, void* stream) {
+  if (!in_args_ok(x, rows, d, ldx, h) || !w || !b || !y || !aligned16(y)) return GR_ERR_ARG;
+  const hipError_t e = gr::launch_in_forward(x, (long long)rows, d, ldx, w, b, h, slope, y, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
+int gr_mlp_in_backward(const float* gh, const float* hv, const float* x, int64_t rows, int32_t d, int32_t ldx,
+                       int32_t h, float slope, float* partial, float* sums, void* stream) {
+  if (!in_args_ok(x, rows, d, ldx, h) || !gh || !hv || !partial || !sums || !aligned16(gh) || !aligned16(hv) ||
+      !aligned16(partial))
+    return GR_ERR_ARG;
+  const hipError_t e =
+      gr::launch_in_backward(gh, hv, x, (long long)rows, d, ldx, h, slope, partial, sums, (hipStream_t)stream);
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 

@@ -120,11 +120,15 @@ hipError_t launch_bn_backward(const float* x, const float* gy, long long m, int 
                               hipStream_t s);
 int column_sum_blocks(long long m);                                                                       // gr_update.hip
 hipError_t launch_column_sum(const void* x, int dtype, long long m, int n, float* part, float* out, hipStream_t s);
-int head_blocks(long long m);                                                                             // gr_update.hip
+int head_partial_rows(long long m);                                                                      // gr_update.hip
 hipError_t launch_head_forward(const float* z, long long m, int h, const float* w, const float* b, int k, float slope,
                                float* y, hipStream_t s);
 hipError_t launch_head_backward(const float* z, const float* gy, long long m, int h, const float* w, int k,
-                                float slope, float* gz, float* part, float* gw, float* gb, hipStream_t s);
+                                float slope, float* gz, float* part, float* sums, hipStream_t s);
+hipError_t launch_in_forward(const float* x, long long m, int d, int ldx, const float* w, const float* b, int h,
+                             float slope, float* y, hipStream_t s);
+hipError_t launch_in_backward(const float* gh, const float* hv, const float* x, long long m, int d, int ldx, int h,
+                              float slope, float* part, float* sums, hipStream_t s);
 // obstacle slots per camera wave (the first GR_CAM_OBST_SLOTS obstacles in view; any further ones
 // are set up again per tile from their records)
 #define GR_CAM_OBST_SLOTS 64

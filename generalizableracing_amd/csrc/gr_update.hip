@@ -109,25 +109,39 @@ hipError_t launch_column_sum(const void* x, int dtype, long long m, int n, float
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// The MLP head fused with the LeakyReLU in front of it (rsl_rl/linear.py LeakyHead): for the actor's / critic's last
-// Linear (out k <= 8 features, in h <= 256) on the update's tall mini-batches.  z [M][h] is the pre-activation of
-// the last hidden layer, W [k][h], b [k].
-//   forward : y = lrelu(z) W^T + b                                   (reads z once; no activation pass, no GEMM)
-//   backward: gz = (gy W) * lrelu'(z),  gW = gy^T lrelu(z),  gb = sum gy   (reads z and gy once, writes gz)
-// torch would run, per mini-batch and network: the LeakyReLU forward (read z, write h), the head GEMM (read h), the
-// head's input-gradient GEMM (write gh; a K <= 8 GEMM on general tiles), the LeakyReLU backward (read gh and z,
-// write gz), the head's weight-gradient GEMM (read gy, h) and its bias sum.  A wave owns a row at a time, lane l
-// columns 4l .. 4l + 3 (one 1 KB coalesced access per row); the weight / bias gradients are per-workgroup partial
-// sums reduced in a fixed order by head_final (deterministic, graph-capturable, no atomics).
+// The actor / critic MLP's memory-bound layers for the PPO update's tall mini-batches (rsl_rl/linear.py MLP):
+// the MLP is x -> L1 -> lrelu -> L2 -> lrelu -> L3 with L1: d -> h1 (d <= 32), L2: h1 -> h2 (the 256 x 256 GEMM, on
+// hipBLASLt), L3: h2 -> k (k <= 8).  Everything around the big GEMM runs here, each matrix read once:
+//   in_forward  : h1 = lrelu(x W1^T + b1)                          (K = d GEMM + bias + activation, writes h1)
+//   in_backward : gz1 = gh1 * lrelu'(h1); gW1 = gz1^T x, gb1 = sum gz1   (reads gh1, h1, x; gz1 never stored)
+//   head_forward: y = lrelu(z2) W3^T + b3                          (reads z2; no activation pass, no GEMM)
+//   head_backward: gz2 = (gy W3) * lrelu'(z2); gW3 = gy^T lrelu(z2), gb3 = sum gy, gb2 = sum gz2
+// (lrelu'(h) = lrelu'(z): a LeakyReLU keeps the sign, and maps 0 to 0.)  A wave owns a row at a time, lane l
+// columns 4 l .. 4 l + 3 (one 1 KB coalesced access per row of 256); four rows' loads are issued together.  Weight /
+// bias gradients: every wave writes its partial sums as one row of `part`, and partials_final adds the rows in a
+// fixed order (deterministic, graph-capturable, no atomics).
 constexpr int HD_WAVES = 4;
+constexpr int HD_U = 4;  // rows in flight per wave
 typedef float hd_v4 __attribute__((ext_vector_type(4)));
-constexpr int HD_MAXK = 8;
 
 __device__ __forceinline__ float hd_act(float z, float slope) { return z > 0.0f ? z : z * slope; }
 __device__ __forceinline__ float hd_der(float z, float slope) { return z > 0.0f ? 1.0f : slope; }
+__device__ __forceinline__ hd_v4 hd_ld(const float* p) { return __builtin_nontemporal_load(reinterpret_cast<const hd_v4*>(p)); }
 
-// forward: a wave takes 4 rows at a time, 16 lanes per row; lane q of a row holds columns 4 q + 64 j (j < 4), so
-// each load instruction reads 256 contiguous bytes of every row and a row's dot products reduce over 16 lanes
+// rows per wave for the backward kernels: enough waves to fill the chip, few enough partial rows
+__host__ __device__ inline long long hd_rows_per_wave(long long m) {
+  const long long waves = (m + 255) / 256;  // 256 rows per wave ...
+  const long long w = waves < 1 ? 1 : (waves > 4096 ? 4096 : waves);  // ... at most 4096 waves (partial rows)
+  return (m + w - 1) / w;
+}
+int head_partial_rows(long long m) {
+  const long long rpw = hd_rows_per_wave(m);
+  return (int)((m + rpw - 1) / rpw);
+}
+
+// ---- forward of the head: a wave takes 4 rows at a time, 16 lanes per row; lane q of a row holds columns
+// 4 q + 64 j (j < 4), so each load instruction reads 256 contiguous bytes of every row and a row's dot products
+// reduce over 16 lanes
 template <int K>
 __global__ __launch_bounds__(HD_WAVES * 64) void head_forward(const float* __restrict__ z, long long m, int h,
                                                               const float* __restrict__ w,
@@ -155,7 +169,7 @@ __global__ __launch_bounds__(HD_WAVES * 64) void head_forward(const float* __res
       for (int j = 0; j < 4; ++j) {
         const int c = 4 * q + 64 * j;
         hd_v4 zz = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (c < h) zz = __builtin_nontemporal_load(reinterpret_cast<const hd_v4*>(z + r * h + c));
+        if (c < h) zz = hd_ld(z + r * h + c);
         const float a[4] = {hd_act(zz.x, slope), hd_act(zz.y, slope), hd_act(zz.z, slope), hd_act(zz.w, slope)};
 #pragma unroll
         for (int k = 0; k < K; ++k)
@@ -175,13 +189,18 @@ __global__ __launch_bounds__(HD_WAVES * 64) void head_forward(const float* __res
   }
 }
 
+// ---- backward of the head; partial row of a wave: [gW3 (k h) | gb3 (k) | gb2 = column sums of gz2 (h)]
 template <int K>
 __global__ __launch_bounds__(HD_WAVES * 64) void head_backward(const float* __restrict__ z,
                                                                const float* __restrict__ gy, long long m, int h,
-                                                               const float* __restrict__ w, float slope, int rows,
+                                                               const float* __restrict__ w, float slope, long long rpw,
                                                                float* __restrict__ gz, float* __restrict__ part) {
-  __shared__ float sm[HD_WAVES][K * 256 + K];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  // (wave-uniform, so the per-row gy / x reads are scalar loads into SGPRs)
+  const long long wid = (long long)blockIdx.x * HD_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const long long r0 = wid * rpw;
+  if (r0 >= m) return;
+  const long long r1 = r0 + rpw < m ? r0 + rpw : m;
   const int c = 4 * lane;
   const bool on = c < h;
   float wr[K][4];
@@ -189,31 +208,28 @@ __global__ __launch_bounds__(HD_WAVES * 64) void head_backward(const float* __re
   for (int k = 0; k < K; ++k)
 #pragma unroll
     for (int j = 0; j < 4; ++j) wr[k][j] = on ? w[(size_t)k * h + c + j] : 0.0f;
-  float gw[K][4], gb[K];
+  float gw[K][4], gb[K], gs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     gb[k] = 0.0f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) gw[k][j] = 0.0f;
   }
-  const long long r0 = (long long)blockIdx.x * rows;
-  const long long r1 = r0 + rows < m ? r0 + rows : m;
-  constexpr int U = 4;  // rows in flight per wave (their loads issued together)
-  for (long long rb = r0 + wv; rb < r1; rb += U * HD_WAVES) {
-    float g[U][K];
-    hd_v4 zz[U];
+  for (long long rb = r0; rb < r1; rb += HD_U) {
+    float g[HD_U][K];
+    hd_v4 zz[HD_U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long long r = rb + (long long)u * HD_WAVES;
+    for (int u = 0; u < HD_U; ++u) {
+      const long long r = rb + u;
       const bool ok = r < r1;
 #pragma unroll
       for (int k = 0; k < K; ++k) g[u][k] = ok ? gy[r * K + k] : 0.0f;
       zz[u] = hd_v4{0.0f, 0.0f, 0.0f, 0.0f};
-      if (on && ok) zz[u] = __builtin_nontemporal_load(reinterpret_cast<const hd_v4*>(z + r * h + c));
+      if (on && ok) zz[u] = hd_ld(z + r * h + c);
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long long r = rb + (long long)u * HD_WAVES;
+    for (int u = 0; u < HD_U; ++u) {
+      const long long r = rb + u;
       const float zv[4] = {zz[u].x, zz[u].y, zz[u].z, zz[u].w};
       float o[4];
 #pragma unroll
@@ -222,6 +238,7 @@ __global__ __launch_bounds__(HD_WAVES * 64) void head_backward(const float* __re
 #pragma unroll
         for (int k = 1; k < K; ++k) gh += g[u][k] * wr[k][j];
         o[j] = gh * hd_der(zv[j], slope);
+        gs[j] += o[j];
         const float a = hd_act(zv[j], slope);
 #pragma unroll
         for (int k = 0; k < K; ++k) gw[k][j] += g[u][k] * a;
@@ -234,72 +251,185 @@ __global__ __launch_bounds__(HD_WAVES * 64) void head_backward(const float* __re
       }
     }
   }
-  // the workgroup's partial sums, waves combined in order: part[block][k * h + col], then part[block][k * h + k']
+  float* pr = part + (size_t)wid * ((K * h + K + h + 3) & ~3);  // (rows padded to 16 B: float4 stores)
+  if (on) {
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
+    for (int k = 0; k < K; ++k) *reinterpret_cast<hd_v4*>(pr + k * h + c) = hd_v4{gw[k][0], gw[k][1], gw[k][2], gw[k][3]};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) sm[wv][k * 256 + c + j] = gw[k][j];
-    if (lane == 0) sm[wv][K * 256 + k] = gb[k];
+    for (int j = 0; j < 4; ++j) pr[K * h + K + c + j] = gs[j];
   }
-  __syncthreads();
-  float* pb = part + (size_t)blockIdx.x * (K * h + K);
-  for (int i = threadIdx.x; i < K * 256 + K; i += HD_WAVES * 64) {
-    const bool bias = i >= K * 256;
-    const int k = bias ? i - K * 256 : i / 256, col = bias ? 0 : i % 256;
-    if (!bias && col >= h) continue;
-    float v = sm[0][i];
+  if (lane < K) {
+    float v = gb[0];
 #pragma unroll
-    for (int q = 1; q < HD_WAVES; ++q) v += sm[q][i];
-    pb[bias ? K * h + k : k * h + col] = v;
+    for (int k = 1; k < K; ++k) v = lane == k ? gb[k] : v;
+    pr[K * h + lane] = v;
   }
 }
 
-// gw [k][h] and gb [k] from the per-workgroup partials [blocks][k h + k]: 64 outputs per workgroup, its 16 waves
-// sum a sixteenth of the partial rows each (four loads in flight per lane), combined in LDS in wave order
-__global__ __launch_bounds__(CF_WAVES * 64) void head_final(const float* __restrict__ part, int blocks, int n,
-                                                            float* __restrict__ gw, float* __restrict__ gb, int nw) {
+// ---- first layer forward: h1 = lrelu(x W1^T + b1); lane l computes columns 4 l .. 4 l + 3 of each row
+template <int D>
+__global__ __launch_bounds__(HD_WAVES * 64) void in_forward(const float* __restrict__ x, long long m, int ldx,
+                                                            const float* __restrict__ w, const float* __restrict__ b,
+                                                            int h, float slope, float* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const int c = 4 * lane;
+  const bool on = c < h;
+  float wr[4][D], br[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    br[j] = on ? b[c + j] : 0.0f;
+#pragma unroll
+    for (int k = 0; k < D; ++k) wr[j][k] = on ? w[(size_t)(c + j) * D + k] : 0.0f;
+  }
+  const long long stride = (long long)gridDim.x * HD_WAVES * HD_U;
+  for (long long rb = ((long long)blockIdx.x * HD_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * HD_U;
+       rb < m; rb += stride) {
+    float xr[HD_U][D];
+#pragma unroll
+    for (int u = 0; u < HD_U; ++u) {
+      const long long r = rb + u < m ? rb + u : m - 1;
+#pragma unroll
+      for (int k = 0; k < D; k += 4) {
+        const hd_v4 v = *reinterpret_cast<const hd_v4*>(x + r * ldx + k);
+        xr[u][k] = v.x; xr[u][k + 1] = v.y; xr[u][k + 2] = v.z; xr[u][k + 3] = v.w;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < HD_U; ++u) {
+      const long long r = rb + u;
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float acc = xr[u][0] * wr[j][0];
+#pragma unroll
+        for (int k = 1; k < D; ++k) acc += xr[u][k] * wr[j][k];
+        o[j] = hd_act(acc + br[j], slope);
+      }
+      if (on && r < m) {
+        const hd_v4 ov = {o[0], o[1], o[2], o[3]};
+        __builtin_nontemporal_store(ov, reinterpret_cast<hd_v4*>(y + r * h + c));
+      }
+    }
+  }
+}
+
+// ---- first layer backward; partial row of a wave: [gW1 (h d, row-major [h][d]) | gb1 (h)]
+template <int D>
+__global__ __launch_bounds__(HD_WAVES * 64) void in_backward(const float* __restrict__ gh, const float* __restrict__ hv,
+                                                             const float* __restrict__ x, long long m, int ldx, int h,
+                                                             float slope, long long rpw, float* __restrict__ part) {
+  const int lane = threadIdx.x & 63;
+  // (wave-uniform, so the per-row gy / x reads are scalar loads into SGPRs)
+  const long long wid = (long long)blockIdx.x * HD_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const long long r0 = wid * rpw;
+  if (r0 >= m) return;
+  const long long r1 = r0 + rpw < m ? r0 + rpw : m;
+  const int c = 4 * lane;
+  const bool on = c < h;
+  float gw[4][D], gb[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < D; ++k) gw[j][k] = 0.0f;
+  for (long long rb = r0; rb < r1; rb += HD_U) {
+    hd_v4 gg[HD_U], hh[HD_U];
+    float xr[HD_U][D];
+#pragma unroll
+    for (int u = 0; u < HD_U; ++u) {
+      const long long r = rb + u;
+      const bool ok = r < r1;
+      const long long rr = ok ? r : r0;
+      gg[u] = hd_v4{0.0f, 0.0f, 0.0f, 0.0f};
+      hh[u] = hd_v4{0.0f, 0.0f, 0.0f, 0.0f};
+      if (on && ok) {
+        gg[u] = hd_ld(gh + r * h + c);
+        hh[u] = hd_ld(hv + r * h + c);
+      }
+#pragma unroll
+      for (int k = 0; k < D; k += 4) {
+        const hd_v4 v = *reinterpret_cast<const hd_v4*>(x + rr * ldx + k);
+        xr[u][k] = ok ? v.x : 0.0f; xr[u][k + 1] = ok ? v.y : 0.0f;
+        xr[u][k + 2] = ok ? v.z : 0.0f; xr[u][k + 3] = ok ? v.w : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < HD_U; ++u) {
+      const float gz[4] = {gg[u].x * hd_der(hh[u].x, slope), gg[u].y * hd_der(hh[u].y, slope),
+                           gg[u].z * hd_der(hh[u].z, slope), gg[u].w * hd_der(hh[u].w, slope)};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        gb[j] += gz[j];
+#pragma unroll
+        for (int k = 0; k < D; ++k) gw[j][k] += gz[j] * xr[u][k];
+      }
+    }
+  }
+  float* pr = part + (size_t)wid * (h * D + h);
+  if (on) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < D; k += 4)
+        *reinterpret_cast<hd_v4*>(pr + (size_t)(c + j) * D + k) = hd_v4{gw[j][k], gw[j][k + 1], gw[j][k + 2], gw[j][k + 3]};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pr[h * D + c + j] = gb[j];
+  }
+}
+
+// out[n] = sum over the `rows` partial rows [rows][n], in row order per 16-wave slice: 64 outputs per workgroup,
+// its 16 waves take every 16th partial row (four loads in flight per lane), combined in LDS in wave order
+__global__ __launch_bounds__(CF_WAVES * 64) void partials_final(const float* __restrict__ part, int rows, int n,
+                                                                int ld, float* __restrict__ out) {
   __shared__ float sm[CF_WAVES * 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + lane;
   float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
   if (i < n) {
     int b = wv;
-    for (; b + 3 * CF_WAVES < blocks; b += 4 * CF_WAVES) {
-      a0 += part[(size_t)b * n + i];
-      a1 += part[(size_t)(b + CF_WAVES) * n + i];
-      a2 += part[(size_t)(b + 2 * CF_WAVES) * n + i];
-      a3 += part[(size_t)(b + 3 * CF_WAVES) * n + i];
+    for (; b + 3 * CF_WAVES < rows; b += 4 * CF_WAVES) {
+      a0 += part[(size_t)b * ld + i];
+      a1 += part[(size_t)(b + CF_WAVES) * ld + i];
+      a2 += part[(size_t)(b + 2 * CF_WAVES) * ld + i];
+      a3 += part[(size_t)(b + 3 * CF_WAVES) * ld + i];
     }
-    for (; b < blocks; b += CF_WAVES) a0 += part[(size_t)b * n + i];
+    for (; b < rows; b += CF_WAVES) a0 += part[(size_t)b * ld + i];
   }
   sm[threadIdx.x] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (wv == 0 && i < n) {
     float s = 0.0f;
     for (int k = 0; k < CF_WAVES; ++k) s += sm[k * 64 + lane];
-    if (i < nw)
-      gw[i] = s;
-    else
-      gb[i - nw] = s;
+    out[i] = s;
   }
 }
 
-int head_blocks(long long m) {
-  long long b = (m + 255) / 256;
-  return (int)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
-}
-
-#define HD_DISPATCH(KK, ...)                   \
-  switch (KK) {                                \
-    case 1: __VA_ARGS__(1); break;             \
-    case 2: __VA_ARGS__(2); break;             \
-    case 3: __VA_ARGS__(3); break;             \
-    case 4: __VA_ARGS__(4); break;             \
-    case 5: __VA_ARGS__(5); break;             \
-    case 6: __VA_ARGS__(6); break;             \
-    case 7: __VA_ARGS__(7); break;             \
-    default: __VA_ARGS__(8); break;            \
+#define HD_DISPATCH_K(KK, F)          \
+  switch (KK) {                       \
+    case 1: F(1); break;              \
+    case 2: F(2); break;              \
+    case 3: F(3); break;              \
+    case 4: F(4); break;              \
+    case 5: F(5); break;              \
+    case 6: F(6); break;              \
+    case 7: F(7); break;              \
+    default: F(8); break;             \
   }
+#define HD_DISPATCH_D(DD, F)          \
+  switch (DD) {                       \
+    case 4: F(4); break;              \
+    case 8: F(8); break;              \
+    case 12: F(12); break;            \
+    case 16: F(16); break;            \
+    case 20: F(20); break;            \
+    case 24: F(24); break;            \
+    case 28: F(28); break;            \
+    default: F(32); break;            \
+  }
+
+static int hd_grid(long long waves) {
+  const long long b = (waves + HD_WAVES - 1) / HD_WAVES;
+  return (int)(b < 1 ? 1 : b);
+}
 
 hipError_t launch_head_forward(const float* z, long long m, int h, const float* w, const float* b, int k, float slope,
                                float* y, hipStream_t s) {
@@ -307,22 +437,47 @@ hipError_t launch_head_forward(const float* z, long long m, int h, const float* 
   const int blocks = (int)(fb < 1 ? 1 : (fb > 8192 ? 8192 : fb));
 #define HD_FWD(KK) \
   hipLaunchKernelGGL(head_forward<KK>, dim3(blocks), dim3(HD_WAVES * 64), 0, s, z, m, h, w, b, slope, y)
-  HD_DISPATCH(k, HD_FWD)
+  HD_DISPATCH_K(k, HD_FWD)
 #undef HD_FWD
   return hipGetLastError();
 }
 
 hipError_t launch_head_backward(const float* z, const float* gy, long long m, int h, const float* w, int k,
-                                float slope, float* gz, float* part, float* gw, float* gb, hipStream_t s) {
-  const int blocks = head_blocks(m);
-  const int rows = (int)((m + blocks - 1) / blocks);
-#define HD_BWD(KK)                                                                                               \
-  hipLaunchKernelGGL(head_backward<KK>, dim3(blocks), dim3(HD_WAVES * 64), 0, s, z, gy, m, h, w, slope, rows, gz, \
-                     part)
-  HD_DISPATCH(k, HD_BWD)
+                                float slope, float* gz, float* part, float* sums, hipStream_t s) {
+  const long long rpw = hd_rows_per_wave(m);
+  const int prow = head_partial_rows(m);
+  const int blocks = hd_grid(prow);
+#define HD_BWD(KK) \
+  hipLaunchKernelGGL(head_backward<KK>, dim3(blocks), dim3(HD_WAVES * 64), 0, s, z, gy, m, h, w, slope, rpw, gz, part)
+  HD_DISPATCH_K(k, HD_BWD)
 #undef HD_BWD
-  const int n = k * h + k;
-  hipLaunchKernelGGL(head_final, dim3((n + 63) / 64), dim3(CF_WAVES * 64), 0, s, part, blocks, n, gw, gb, k * h);
+  const int n = k * h + k + h;
+  hipLaunchKernelGGL(partials_final, dim3((n + 63) / 64), dim3(CF_WAVES * 64), 0, s, part, prow, n, (n + 3) & ~3, sums);
+  return hipGetLastError();
+}
+
+hipError_t launch_in_forward(const float* x, long long m, int d, int ldx, const float* w, const float* b, int h,
+                             float slope, float* y, hipStream_t s) {
+  const long long fb = (m + 8 * HD_WAVES * HD_U - 1) / (8 * HD_WAVES * HD_U);  // ~8 row groups per wave
+  const int blocks = (int)(fb < 1 ? 1 : (fb > 8192 ? 8192 : fb));
+#define IN_FWD(DD) \
+  hipLaunchKernelGGL(in_forward<DD>, dim3(blocks), dim3(HD_WAVES * 64), 0, s, x, m, ldx, w, b, h, slope, y)
+  HD_DISPATCH_D(d, IN_FWD)
+#undef IN_FWD
+  return hipGetLastError();
+}
+
+hipError_t launch_in_backward(const float* gh, const float* hv, const float* x, long long m, int d, int ldx, int h,
+                              float slope, float* part, float* sums, hipStream_t s) {
+  const long long rpw = hd_rows_per_wave(m);
+  const int prow = head_partial_rows(m);
+  const int blocks = hd_grid(prow);
+#define IN_BWD(DD) \
+  hipLaunchKernelGGL(in_backward<DD>, dim3(blocks), dim3(HD_WAVES * 64), 0, s, gh, hv, x, m, ldx, h, slope, rpw, part)
+  HD_DISPATCH_D(d, IN_BWD)
+#undef IN_BWD
+  const int n = h * d + h;
+  hipLaunchKernelGGL(partials_final, dim3((n + 63) / 64), dim3(CF_WAVES * 64), 0, s, part, prow, n, n, sums);
   return hipGetLastError();
 }
 

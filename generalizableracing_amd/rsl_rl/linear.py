@@ -107,9 +107,45 @@ class TallLinear(nn.Linear):
         return F.linear(x, self.weight, self.bias)
 
 
-# ------------------------------------------------------------------------------------------ fused head
+# ------------------------------------------------------------------------------------------ fused MLP layers
 HEAD_MAX_OUT = 8      # gr_head_*: output features
-HEAD_MAX_IN = 256     # gr_head_*: input features (a multiple of 4)
+HEAD_MAX_IN = 256     # gr_head_* / gr_mlp_in_*: hidden features (a multiple of 4)
+IN_MAX = 32           # gr_mlp_in_*: input features (a multiple of 4)
+
+
+def _lib_call(name, *args):
+    from .. import _abi
+
+    rc = getattr(_abi.load(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed (status {rc})")
+
+
+def _stream(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _head_backward(z, gy, w, slope):
+    """gr_head_backward -> (gz, gW, gb, column sums of gz)."""
+    from .. import _abi
+
+    m, h = z.shape
+    k = w.shape[0]
+    gz = torch.empty_like(z)
+    part = torch.empty(_abi.load().gr_head_partials(m, k, h), device=z.device, dtype=torch.float32)
+    sums = torch.empty(k * h + k + h, device=z.device, dtype=torch.float32)
+    _lib_call("gr_head_backward", z.data_ptr(), gy.data_ptr(), m, h, w.data_ptr(), k, float(slope), gz.data_ptr(),
+              part.data_ptr(), sums.data_ptr(), _stream(z))
+    return gz, sums[:k * h].view(k, h), sums[k * h:k * h + k], sums[k * h + k:]
+
+
+def _head_forward(z, w, b, slope):
+    m, h = z.shape
+    k = w.shape[0]
+    y = torch.empty(m, k, device=z.device, dtype=torch.float32)
+    _lib_call("gr_head_forward", z.data_ptr(), m, h, w.data_ptr(), b.data_ptr(), k, float(slope), y.data_ptr(),
+              _stream(z))
+    return y
 
 
 class _LeakyHeadFn(torch.autograd.Function):
@@ -118,39 +154,15 @@ class _LeakyHeadFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, z, w, b, slope):
-        from .. import _abi
-
-        lib = _abi.load()
         z, w, b = z.contiguous(), w.contiguous(), b.contiguous()
-        m, h = z.shape
-        k = w.shape[0]
-        y = torch.empty(m, k, device=z.device, dtype=torch.float32)
-        rc = lib.gr_head_forward(z.data_ptr(), m, h, w.data_ptr(), b.data_ptr(), k, float(slope), y.data_ptr(),
-                                 torch.cuda.current_stream(z.device).cuda_stream)
-        if rc != 0:
-            raise RuntimeError(f"gr_head_forward failed (status {rc})")
         ctx.save_for_backward(z, w)
         ctx.slope = float(slope)
-        return y
+        return _head_forward(z, w, b, slope)
 
     @staticmethod
     def backward(ctx, gy):
-        from .. import _abi
-
-        lib = _abi.load()
         z, w = ctx.saved_tensors
-        gy = gy.contiguous().float()
-        m, h = z.shape
-        k = w.shape[0]
-        gz = torch.empty_like(z)
-        part = torch.empty(lib.gr_head_partials(m, k, h), device=z.device, dtype=torch.float32)
-        gw = torch.empty_like(w)
-        gb = torch.empty(k, device=z.device, dtype=torch.float32)
-        rc = lib.gr_head_backward(z.data_ptr(), gy.data_ptr(), m, h, w.data_ptr(), k, ctx.slope, gz.data_ptr(),
-                                  part.data_ptr(), gw.data_ptr(), gb.data_ptr(),
-                                  torch.cuda.current_stream(z.device).cuda_stream)
-        if rc != 0:
-            raise RuntimeError(f"gr_head_backward failed (status {rc})")
+        gz, gw, gb, _ = _head_backward(z, gy.contiguous().float(), w, ctx.slope)
         return gz, gw, gb, None
 
 
@@ -159,18 +171,82 @@ def leaky_head(z: torch.Tensor, w: torch.Tensor, b: torch.Tensor, slope: float) 
     return _LeakyHeadFn.apply(z, w, b, slope)
 
 
+def _rows_ok(x: torch.Tensor) -> bool:
+    """x usable in place by gr_mlp_in_*: unit column stride, row stride a multiple of 4 floats, 16-byte aligned."""
+    return x.stride(1) == 1 and x.stride(0) % 4 == 0 and x.stride(0) >= x.shape[1] and x.data_ptr() % 16 == 0
+
+
+class _LeakyMLPFn(torch.autograd.Function):
+    """The whole MLP x -> L1 -> lrelu -> L2 -> lrelu -> L3 for an input that needs no gradient (the update's
+    observation rows): gr_mlp_in_forward (L1 + bias + activation), hipBLASLt for the h1 x h2 GEMM,
+    gr_head_forward (activation + L3).  Backward: gr_head_backward (gz2, gW3, gb3 and gb2 in one read of z2),
+    hipBLASLt for gh1 = gz2 W2, split-K for gW2, gr_mlp_in_backward (gW1, gb1 straight from gh1 and h1: gz1 is
+    never stored)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, w3, b3, slope):
+        if not _rows_ok(x):
+            x = x.contiguous()
+        m, d = x.shape
+        h1n = w1.shape[0]
+        h1 = torch.empty(m, h1n, device=x.device, dtype=torch.float32)
+        _lib_call("gr_mlp_in_forward", x.data_ptr(), m, d, x.stride(0), w1.data_ptr(), b1.data_ptr(), h1n,
+                  float(slope), h1.data_ptr(), _stream(x))
+        z2 = F.linear(h1, w2, b2)
+        y = _head_forward(z2, w3.contiguous(), b3, slope)
+        ctx.save_for_backward(x, h1, z2, w2, w3)
+        ctx.slope = float(slope)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from .. import _abi
+
+        x, h1, z2, w2, w3 = ctx.saved_tensors
+        gz2, gw3, gb3, gb2 = _head_backward(z2, gy.contiguous().float(), w3.contiguous(), ctx.slope)
+        gh1 = gz2 @ w2
+        gw2 = split_k_wgrad(gz2, h1)
+        m, d = x.shape
+        h1n = h1.shape[1]
+        part = torch.empty(_abi.load().gr_mlp_in_partials(m, d, h1n), device=x.device, dtype=torch.float32)
+        sums = torch.empty(h1n * d + h1n, device=x.device, dtype=torch.float32)
+        _lib_call("gr_mlp_in_backward", gh1.data_ptr(), h1.data_ptr(), x.data_ptr(), m, d, x.stride(0), h1n,
+                  ctx.slope, part.data_ptr(), sums.data_ptr(), _stream(x))
+        return None, sums[:h1n * d].view(h1n, d), sums[h1n * d:], gw2, gb2, gw3, gb3, None
+
+
+def _tall_cuda(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return (x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and w.dtype == torch.float32
+            and (x.shape[0] >= 2 * SPLIT or _FORCE_FN) and torch.is_grad_enabled() and w.requires_grad
+            and not torch.is_autocast_enabled("cuda"))
+
+
 def head_fusable(x: torch.Tensor, act: nn.Module, lin: nn.Module) -> bool:
     """The update's tall fp32 CUDA batches with LeakyReLU -> Linear(<= 256, <= 8) at the end of the MLP."""
     return (isinstance(act, nn.LeakyReLU) and isinstance(lin, nn.Linear) and lin.bias is not None
-            and x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and lin.weight.dtype == torch.float32
-            and (x.shape[0] >= 2 * SPLIT or _FORCE_FN) and torch.is_grad_enabled() and lin.weight.requires_grad
-            and not torch.is_autocast_enabled("cuda")
+            and _tall_cuda(x, lin.weight)
             and lin.out_features <= HEAD_MAX_OUT and lin.in_features <= HEAD_MAX_IN and lin.in_features % 4 == 0)
+
+
+def mlp_fusable(x: torch.Tensor, mods: list) -> bool:
+    """Linear(d <= 32) -> LeakyReLU -> Linear(h1, h2) -> LeakyReLU -> Linear(h2, <= 8), the input needing no
+    gradient, on the update's tall batches."""
+    if len(mods) != 5 or x.requires_grad:
+        return False
+    l1, a1, l2, a2, l3 = mods
+    return (all(isinstance(m, nn.Linear) and m.bias is not None for m in (l1, l2, l3))
+            and isinstance(a1, nn.LeakyReLU) and isinstance(a2, nn.LeakyReLU)
+            and a1.negative_slope == a2.negative_slope and head_fusable(x, a2, l3)
+            and l1.in_features <= IN_MAX and l1.in_features % 4 == 0 and x.shape[1] == l1.in_features
+            and l1.out_features <= HEAD_MAX_IN and l1.out_features % 4 == 0 and l2.in_features == l1.out_features
+            and l2.out_features == l3.in_features
+            and l1.weight.requires_grad and l2.weight.requires_grad)
 
 
 class MLP(nn.Sequential):
     """The actor / critic MLP: nn.Sequential with the same children and state_dict keys.  On the update's tall
-    CUDA mini-batches its last LeakyReLU + output Linear run fused (leaky_head); everywhere else (rollout,
+    CUDA mini-batches everything but the hidden GEMM runs in the fused HIP ops (_LeakyMLPFn; with an input that
+    needs a gradient, only the last LeakyReLU + output Linear fuse: leaky_head); everywhere else (rollout,
     inference, CPU, TorchScript) module by module."""
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -183,6 +259,10 @@ class MLP(nn.Sequential):
     @torch.jit.unused
     def _forward_eager(self, x: torch.Tensor) -> torch.Tensor:
         mods = list(self)
+        if mlp_fusable(x, mods):
+            l1, a1, l2, _, l3 = mods
+            return _LeakyMLPFn.apply(x, l1.weight, l1.bias, l2.weight, l2.bias, l3.weight, l3.bias,
+                                     a1.negative_slope)
         if len(mods) >= 2 and head_fusable(x, mods[-2], mods[-1]):
             for m in mods[:-2]:
                 x = m(x)

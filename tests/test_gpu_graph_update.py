@@ -60,8 +60,10 @@ def test_graphed_update_matches_eager():
             diff = float((pe.detach() - pg.detach()).abs().max())
             assert moved > 0.0 and diff <= 0.05 * moved, (rep, diff, moved)
         assert abs(alg.learning_rate - alg_g.learning_rate) <= 1e-6 * alg.learning_rate
-        for k in ("value_function", "surrogate"):
-            assert abs(le[k] - lg[k]) <= 1e-4 * (abs(le[k]) + 1e-6), (k, le[k], lg[k])
+        assert abs(le["value_function"] - lg["value_function"]) <= 1e-4 * abs(le["value_function"])
+        # the surrogate is a nearly cancelling mean of +-A * ratio (|A| ~ 1, mean ~ 0.02) over 20 mini-batches
+        # whose parameters differ by up to the 5 % above: an absolute bound, as tests/ppo_c2_golden.py's
+        assert abs(le["surrogate"] - lg["surrogate"]) <= 5e-5, (le["surrogate"], lg["surrogate"])
         # the next update (graph replay) starts from identical states: round-off differences would
         # otherwise grow through Adam's normalisation of near-zero gradients
         with torch.no_grad():

@@ -228,19 +228,66 @@ def test_leaky_head(rows, h, k):
     torch.testing.assert_close(gz[zero].double(), gh[zero] * slope, rtol=1e-5, atol=1e-9)
 
 
-def test_mlp_fused_head_matches_module_path():
-    """The actor / critic MLP with the fused head (tall CUDA batch) against the same module run layer by layer
-    (TallLinear + nn.LeakyReLU): outputs and every parameter gradient within fp32 summation-order noise."""
+@pytest.mark.parametrize("rows,d,ldx,h", [(24576, 16, 16, 256), (24576, 16, 48, 256), (393216, 16, 48, 256),
+                                          (8193, 32, 36, 64), (5, 4, 4, 8)])
+def test_mlp_in_layer(rows, d, ldx, h):
+    """gr_mlp_in_forward / gr_mlp_in_backward (the MLP's first Linear + bias + LeakyReLU and its weight / bias
+    gradients, rsl_rl/linear.py _LeakyMLPFn) against float64 torch, on strided input rows as the packed mini-batch
+    gives them (ldx > d); repeats bit-identical."""
+    from generalizableracing_amd import _abi
+
+    lib = _abi.load()
+    dev = "cuda:0"
+    g = torch.Generator(device=dev).manual_seed(rows + d + h)
+    xs = torch.randn(rows, ldx, device=dev, generator=g)
+    x = xs[:, :d]
+    w = torch.randn(h, d, device=dev, generator=g) * 0.3
+    b = torch.randn(h, device=dev, generator=g) * 0.1
+    gh = torch.randn(rows, h, device=dev, generator=g)
+    slope = 0.01
+    st = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for _ in range(2):
+        y = torch.empty(rows, h, device=dev)
+        assert lib.gr_mlp_in_forward(x.data_ptr(), rows, d, ldx, w.data_ptr(), b.data_ptr(), h, slope, y.data_ptr(),
+                                     st) == 0
+        part = torch.empty(lib.gr_mlp_in_partials(rows, d, h), device=dev)
+        sums = torch.empty(h * d + h, device=dev)
+        assert lib.gr_mlp_in_backward(gh.data_ptr(), y.data_ptr(), x.data_ptr(), rows, d, ldx, h, slope,
+                                      part.data_ptr(), sums.data_ptr(), st) == 0
+        outs.append((y, sums))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    y, sums = outs[0]
+    zd = x.double() @ w.double().t() + b.double()
+    yd = torch.nn.functional.leaky_relu(zd, slope)
+    assert float((y.double() - yd).abs().max()) <= 1e-6 * (1.0 + float((x.double().abs() @ w.double().abs().t()).max()))
+    gz = gh.double() * torch.where(zd > 0, 1.0, slope)
+    # (the float derivative is taken on y = lrelu(z): same sign as z except where z rounds across 0)
+    gz32 = gh.double() * torch.where(y > 0, 1.0, slope).double()
+    gw = gz32.t() @ x.double()
+    gb = gz32.sum(0)
+    scale_w = float((gz.abs().t() @ x.double().abs()).max()) + 1.0
+    assert float((sums[:h * d].view(h, d).double() - gw).abs().max()) <= 4e-6 * scale_w
+    assert float((sums[h * d:].double() - gb).abs().max()) <= 4e-6 * (float(gz.abs().sum(0).max()) + 1.0)
+
+
+@pytest.mark.parametrize("needs_input_grad", [False, True])
+def test_mlp_fused_matches_module_path(needs_input_grad):
+    """The actor / critic MLP on a tall CUDA batch — fully fused (_LeakyMLPFn: input needs no gradient, as the
+    update's observation rows) or with the fused head only (input needs a gradient) — against the same module run
+    layer by layer (TallLinear + nn.LeakyReLU): outputs and every parameter gradient within fp32 noise."""
     from generalizableracing_amd.rsl_rl import ActorCritic
     from generalizableracing_amd.rsl_rl import linear
 
     torch.manual_seed(3)
     pol = ActorCritic(16, 16, 4, [256, 256], [256, 256], "lrelu").to("cuda:0")
-    x = torch.randn(3 * linear.SPLIT, 16, device="cuda:0")
-    assert linear.head_fusable(torch.empty(2 * linear.SPLIT, 256, device="cuda:0"), pol.actor[-2], pol.actor[-1])
+    x0 = torch.randn(3 * linear.SPLIT, 48, device="cuda:0")[:, 8:24]  # a strided view, as the packed mini-batch
+    assert linear.mlp_fusable(x0, list(pol.actor)) and linear.mlp_fusable(x0, list(pol.critic))
     res = []
     for fused in (True, False):
         pol.zero_grad()
+        x = x0.clone().requires_grad_(True) if needs_input_grad else x0
         if fused:
             out = pol.actor(x).square().sum() + pol.critic(x).square().sum()
         else:
@@ -250,9 +297,12 @@ def test_mlp_fused_head_matches_module_path():
                 return v
             out = run(pol.actor, x).square().sum() + run(pol.critic, x).square().sum()
         out.backward()
-        res.append((float(out), [p.grad.clone() for p in pol.parameters() if p.grad is not None]))
-    (oa, ga), (ob, gb_) = res
+        gx = x.grad.clone() if needs_input_grad else None
+        res.append((float(out), [p.grad.clone() for p in pol.parameters() if p.grad is not None], gx))
+    (oa, ga, xa), (ob, gb_, xb) = res
     assert abs(oa - ob) <= 1e-5 * abs(ob)
-    assert len(ga) == len(gb_)
+    assert len(ga) == len(gb_) == len(list(pol.parameters())) - 1  # (std gets no gradient here)
     for a, b in zip(ga, gb_):
         assert float((a - b).norm()) <= 1e-4 * float(b.norm()) + 1e-12
+    if needs_input_grad:
+        assert float((xa - xb).norm()) <= 1e-4 * float(xb.norm())
