@@ -856,6 +856,31 @@ int gr_mlp_in_backward(const float* gh, const float* hv, const float* x, int64_t
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
+int64_t gr_ppo_loss_partials(int64_t rows) {
+  if (rows < 0) return GR_ERR_ARG;
+  return (int64_t)gr::ppo_loss_blocks(rows) * 8;
+}
+
+static bool loss_args_ok(const gr_ppo_loss_args* a) {
+  return a && a->rows > 0 && a->k >= 1 && a->k <= 8 && a->mu && a->std && a->value && a->act && a->logp_old &&
+         a->adv && a->value_old && a->ret && a->mu_old && a->sig_old && a->ld_mu >= a->k && a->ld_act >= a->k &&
+         a->ld_mu_old >= a->k && a->ld_sig_old >= a->k && a->ld_value >= 1 && a->ld_logp_old >= 1 && a->ld_adv >= 1 &&
+         a->ld_value_old >= 1 && a->ld_ret >= 1;
+}
+
+int gr_ppo_loss_forward(const gr_ppo_loss_args* a, float* partial, float* sums, void* stream) {
+  if (!loss_args_ok(a) || !partial || !sums) return GR_ERR_ARG;
+  const hipError_t e = gr::launch_ppo_loss_forward(*a, partial, sums, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
+int gr_ppo_loss_backward(const gr_ppo_loss_args* a, const float* g, float* dmu, float* dvalue, float* partial,
+                         float* dstd, void* stream) {
+  if (!loss_args_ok(a) || !g || !dmu || !dvalue || !partial || !dstd) return GR_ERR_ARG;
+  const hipError_t e = gr::launch_ppo_loss_backward(*a, g, dmu, dvalue, partial, dstd, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
 int gr_test_dynamics(gr_ctx* c, int n, int mode, const float* si, const float* ab, const float* cmd, const float* ci,
                      const float* par, const float* drag, float* so, float* co, float* xo, void* stream) {
   if (!c || n <= 0 || !si || !ab || !cmd || !ci || !par || !drag || !so || !co || !xo) return GR_ERR_ARG;

@@ -127,6 +127,10 @@ hipError_t launch_head_backward(const float* z, const float* gy, long long m, in
                                 float slope, float* gz, float* part, float* sums, hipStream_t s);
 hipError_t launch_in_forward(const float* x, long long m, int d, int ldx, const float* w, const float* b, int h,
                              float slope, float* y, hipStream_t s);
+int ppo_loss_blocks(long long rows);
+hipError_t launch_ppo_loss_forward(const gr_ppo_loss_args& a, float* part, float* sums, hipStream_t s);
+hipError_t launch_ppo_loss_backward(const gr_ppo_loss_args& a, const float* g, float* dmu, float* dvalue, float* part,
+                                    float* dstd, hipStream_t s);
 hipError_t launch_in_backward(const float* gh, const float* hv, const float* x, long long m, int d, int ldx, int h,
                               float slope, float* part, float* sums, hipStream_t s);
 // obstacle slots per camera wave (the first GR_CAM_OBST_SLOTS obstacles in view; any further ones

@@ -481,4 +481,142 @@ hipError_t launch_in_backward(const float* gh, const float* hv, const float* x, 
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// The PPO losses of a mini-batch (standalone/rsl_rl/ext/algorithms/ppo.py:152-169 with the adaptive-rate KL of
+// :133-150 and the Gaussian log prob of rsl_rl's ActorCritic), forward and backward, one thread per sample: ~50
+// tiny torch launches of [rows] / [rows, 4] tensors each way become one launch + one fixed-order reduction.
+// Forward sums [surrogate terms, value terms, KL terms]; backward d/dmu, d/dvalue per row and d/dstd (summed).
+// Semantics of the torch ops it replaces: Normal.log_prob = -(a - mu)^2 / (2 sigma^2) - log sigma - log sqrt(2 pi);
+// torch.max of two tensors splits the gradient in half on ties; clamp passes it on [lo, hi] inclusive.
+constexpr float LOG_SQRT_2PI = 0.918938533204672741780f;
+
+struct LossRow {
+  float logp, ratio, s1, s2, v, vc, ret, vdiff;
+};
+
+__device__ __forceinline__ float pl_at(const float* p, long long ld, long long i, int j) { return p[i * ld + j]; }
+
+__device__ __forceinline__ void pl_row(const gr_ppo_loss_args& a, long long i, const float* sd, LossRow& r,
+                                       float* kl) {
+  float lp = 0.0f, k = 0.0f;
+  for (int j = 0; j < a.k; ++j) {
+    const float mu = pl_at(a.mu, a.ld_mu, i, j), x = pl_at(a.act, a.ld_act, i, j);
+    const float d = x - mu, var = sd[j] * sd[j];
+    lp += (-(d * d) / (2.0f * var) - logf(sd[j])) - LOG_SQRT_2PI;
+    if (kl) {
+      const float so = pl_at(a.sig_old, a.ld_sig_old, i, j), mo = pl_at(a.mu_old, a.ld_mu_old, i, j);
+      const float dm = mo - mu;
+      k += (logf(sd[j] / so + 1.0e-5f) + (so * so + dm * dm) / (2.0f * (sd[j] * sd[j]))) - 0.5f;
+    }
+  }
+  if (kl) *kl = k;
+  r.logp = lp;
+  r.ratio = expf(lp - a.logp_old[i * a.ld_logp_old]);
+  const float A = a.adv[i * a.ld_adv];
+  const float rc = fminf(fmaxf(r.ratio, 1.0f - a.clip), 1.0f + a.clip);
+  r.s1 = -A * r.ratio;
+  r.s2 = -A * rc;
+  r.v = a.value[i * a.ld_value];
+  r.ret = a.ret[i * a.ld_ret];
+  const float vo = a.value_old[i * a.ld_value_old];
+  r.vdiff = r.v - vo;
+  r.vc = vo + fminf(fmaxf(r.vdiff, -a.clip), a.clip);
+}
+
+__device__ __forceinline__ float pl_wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void ppo_loss_forward(gr_ppo_loss_args a, float* __restrict__ part) {
+  __shared__ float sm[4][3];
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  float sd[8];
+  for (int j = 0; j < a.k; ++j) sd[j] = a.std[j];
+  float t[3] = {0.0f, 0.0f, 0.0f};
+  if (i < a.rows) {
+    LossRow r;
+    float kl;
+    pl_row(a, i, sd, r, &kl);
+    t[0] = fmaxf(r.s1, r.s2);
+    const float l1 = (r.v - r.ret) * (r.v - r.ret), l2 = (r.vc - r.ret) * (r.vc - r.ret);
+    t[1] = a.clipped_value ? fmaxf(l1, l2) : (r.ret - r.v) * (r.ret - r.v);
+    t[2] = kl;
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const float v = pl_wave_sum(t[q]);
+    if (lane == 0) sm[wv][q] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) part[(size_t)blockIdx.x * 4 + threadIdx.x] = ((sm[0][threadIdx.x] + sm[1][threadIdx.x]) + sm[2][threadIdx.x]) + sm[3][threadIdx.x];
+}
+
+// g[0], g[1]: the upstream gradients of the surrogate and value losses (device scalars; the means' 1 / rows is
+// applied here)
+__global__ __launch_bounds__(256) void ppo_loss_backward(gr_ppo_loss_args a, const float* __restrict__ g,
+                                                         float* __restrict__ dmu, float* __restrict__ dvalue,
+                                                         float* __restrict__ part) {
+  __shared__ float sm[4][8];
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  float sd[8];
+  for (int j = 0; j < a.k; ++j) sd[j] = a.std[j];
+  float ds[8];
+  for (int j = 0; j < 8; ++j) ds[j] = 0.0f;
+  if (i < a.rows) {
+    LossRow r;
+    pl_row(a, i, sd, r, nullptr);
+    const float inv_m = 1.0f / (float)a.rows;
+    const float gs = g[0] * inv_m, gv = g[1] * inv_m;
+    const float A = a.adv[i * a.ld_adv];
+    const float w1 = r.s1 > r.s2 ? 1.0f : (r.s1 == r.s2 ? 0.5f : 0.0f), w2 = 1.0f - w1;
+    const float inclip = (r.ratio >= 1.0f - a.clip && r.ratio <= 1.0f + a.clip) ? 1.0f : 0.0f;
+    const float dratio = gs * (w1 * -A + w2 * (-A * inclip));
+    const float dlogp = dratio * r.ratio;
+    for (int j = 0; j < a.k; ++j) {
+      const float mu = pl_at(a.mu, a.ld_mu, i, j), x = pl_at(a.act, a.ld_act, i, j);
+      const float d = x - mu, var = sd[j] * sd[j];
+      dmu[i * a.k + j] = dlogp * (d / var);
+      ds[j] = dlogp * (d * d / (var * sd[j]) - 1.0f / sd[j]);
+    }
+    float dv;
+    if (a.clipped_value) {
+      const float l1 = (r.v - r.ret) * (r.v - r.ret), l2 = (r.vc - r.ret) * (r.vc - r.ret);
+      const float u1 = l1 > l2 ? 1.0f : (l1 == l2 ? 0.5f : 0.0f), u2 = 1.0f - u1;
+      const float vin = (r.vdiff >= -a.clip && r.vdiff <= a.clip) ? 1.0f : 0.0f;
+      dv = gv * (u1 * 2.0f * (r.v - r.ret) + u2 * 2.0f * (r.vc - r.ret) * vin);
+    } else {
+      dv = gv * (2.0f * (r.v - r.ret));
+    }
+    dvalue[i] = dv;
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int j = 0; j < a.k; ++j) {
+    const float v = pl_wave_sum(ds[j]);
+    if (lane == 0) sm[wv][j] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < a.k)
+    part[(size_t)blockIdx.x * 8 + threadIdx.x] = ((sm[0][threadIdx.x] + sm[1][threadIdx.x]) + sm[2][threadIdx.x]) + sm[3][threadIdx.x];
+}
+
+int ppo_loss_blocks(long long rows) { return (int)((rows + 255) / 256); }
+
+hipError_t launch_ppo_loss_forward(const gr_ppo_loss_args& a, float* part, float* sums, hipStream_t s) {
+  const int blocks = ppo_loss_blocks(a.rows);
+  hipLaunchKernelGGL(ppo_loss_forward, dim3(blocks), dim3(256), 0, s, a, part);
+  hipLaunchKernelGGL(partials_final, dim3(1), dim3(CF_WAVES * 64), 0, s, part, blocks, 3, 4, sums);
+  return hipGetLastError();
+}
+
+hipError_t launch_ppo_loss_backward(const gr_ppo_loss_args& a, const float* g, float* dmu, float* dvalue, float* part,
+                                    float* dstd, hipStream_t s) {
+  const int blocks = ppo_loss_blocks(a.rows);
+  hipLaunchKernelGGL(ppo_loss_backward, dim3(blocks), dim3(256), 0, s, a, g, dmu, dvalue, part);
+  hipLaunchKernelGGL(partials_final, dim3(1), dim3(CF_WAVES * 64), 0, s, part, blocks, a.k, 8, dstd);
+  return hipGetLastError();
+}
+
 }  // namespace gr

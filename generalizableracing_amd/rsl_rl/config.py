@@ -53,6 +53,9 @@ class RslRlPpoAlgorithmCfg:
     # instead of add_transitions copying them — with storage_obs_dtype "bfloat16" (state rows) the kernel rounds
     # them to bf16 itself
     obs_sink: bool = True
+    # not in the reference: the update's mini-batch losses (log prob, KL, clipped surrogate and value loss) as one
+    # HIP op each way (rsl_rl/fused_loss.py); False keeps the torch ops
+    fused_losses: bool = True
 
 
 @dataclass

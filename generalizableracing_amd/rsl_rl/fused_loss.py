@@ -1,0 +1,116 @@
+"""The PPO losses of a mini-batch as one device op (gr_ppo_loss_forward / gr_ppo_loss_backward, gr_update.hip).
+
+PPO.update (standalone/rsl_rl/ext/algorithms/ppo.py:103-190) evaluates, per mini-batch, the Gaussian log prob of
+the stored actions under the new policy (rsl_rl ActorCritic.get_actions_log_prob), the adaptive-rate KL
+(ppo.py:133-150), the clipped surrogate and the clipped value loss (ppo.py:152-169): in torch some 50 launches of
+[rows] / [rows, 4] tensors forward and as many backward, each a few microseconds, together ~0.45 ms of every
+mini-batch step at 65 536 envs (profiles/round03_update65536_graphed_kernel_stats.csv).  Here: one launch and a
+fixed-order reduction each way, graph-capturable, on the row-strided columns of the packed mini-batch.  The
+arithmetic follows the torch ops it replaces (fp32; ties of torch.max split the gradient, clamp passes it on its
+closed interval); the entropy term depends on the std only and stays in torch.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import torch
+
+
+class GrPpoLossArgs(C.Structure):
+    """Mirror of gr_ppo_loss_args (include/gr.h)."""
+    _fields_ = [("rows", C.c_int64), ("k", C.c_int32), ("clipped_value", C.c_int32), ("clip", C.c_float)] + [
+        (n, C.c_void_p) for n in ("mu", "std", "value", "act", "logp_old", "adv", "value_old", "ret", "mu_old",
+                                  "sig_old")] + [
+        (n, C.c_int64) for n in ("ld_mu", "ld_value", "ld_act", "ld_logp_old", "ld_adv", "ld_value_old", "ld_ret",
+                                 "ld_mu_old", "ld_sig_old")]
+
+
+def _ld(t: torch.Tensor) -> int:
+    if t.dim() == 2 and t.stride(1) != 1:
+        raise ValueError("fused PPO loss: rows must have unit column stride")
+    return int(t.stride(0))
+
+
+def _args(mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old, clip, clipped_value):
+    a = GrPpoLossArgs()
+    a.rows, a.k = mu.shape[0], mu.shape[1]
+    a.clipped_value, a.clip = int(bool(clipped_value)), float(clip)
+    for name, t in (("mu", mu), ("std", std), ("value", value), ("act", act), ("logp_old", logp_old), ("adv", adv),
+                    ("value_old", value_old), ("ret", ret), ("mu_old", mu_old), ("sig_old", sig_old)):
+        setattr(a, name, t.data_ptr())
+        if name != "std":
+            setattr(a, "ld_" + name, _ld(t))
+    return a
+
+
+def _call(name, *args):
+    from .. import _abi
+
+    rc = getattr(_abi.load(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed (status {rc})")
+
+
+class _PPOLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old, clip, clipped_value):
+        from .. import _abi
+
+        std = std.contiguous()
+        a = _args(mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old, clip, clipped_value)
+        rows = mu.shape[0]
+        part = torch.empty(_abi.load().gr_ppo_loss_partials(rows), device=mu.device, dtype=torch.float32)
+        sums = torch.empty(3, device=mu.device, dtype=torch.float32)
+        stream = torch.cuda.current_stream(mu.device).cuda_stream
+        _call("gr_ppo_loss_forward", C.addressof(a), part.data_ptr(), sums.data_ptr(), stream)
+        ctx.save_for_backward(mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old)
+        ctx.clip, ctx.clipped_value = clip, clipped_value
+        out = sums / rows  # the means (torch's mean: sum / rows)
+        kl = out[2].clone()
+        ctx.mark_non_differentiable(kl)
+        return out[0].clone(), out[1].clone(), kl
+
+    @staticmethod
+    def backward(ctx, g_surr, g_value, g_kl):
+        from .. import _abi
+
+        mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old = ctx.saved_tensors
+        a = _args(mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old, ctx.clip, ctx.clipped_value)
+        rows, k = mu.shape
+        dev = mu.device
+        zero = torch.zeros((), device=dev)
+        g = torch.stack([g_surr if g_surr is not None else zero, g_value if g_value is not None else zero]).float()
+        dmu = torch.empty(rows, k, device=dev, dtype=torch.float32)
+        dvalue = torch.empty(rows, device=dev, dtype=torch.float32)
+        part = torch.empty(_abi.load().gr_ppo_loss_partials(rows), device=dev, dtype=torch.float32)
+        dstd = torch.empty(k, device=dev, dtype=torch.float32)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        _call("gr_ppo_loss_backward", C.addressof(a), g.data_ptr(), dmu.data_ptr(), dvalue.data_ptr(), part.data_ptr(),
+              dstd.data_ptr(), stream)
+        return (dmu, dstd, dvalue.view(value.shape), None, None, None, None, None, None, None, None, None)
+
+
+def fused_losses_ok(policy, obs: torch.Tensor) -> bool:
+    """rsl_rl's ActorCritic (state-independent std) with <= 8 actions, CUDA fp32 observations, outside autocast."""
+    from .actor_critic import ActorCritic
+
+    return (type(policy) is ActorCritic and obs.is_cuda and obs.dtype == torch.float32
+            and policy.actor[-1].out_features <= 8 and not torch.is_autocast_enabled("cuda"))
+
+
+def ppo_losses(alg, obs, critic_obs, act, value_old, adv, ret, logp_old, mu_old, sig_old):
+    """(surrogate_loss, value_loss, entropy_mean, kl_mean, mu, sigma) of one mini-batch, the losses differentiable:
+    the policy's actor and critic forward (the fused MLPs on tall batches), then gr_ppo_loss_*.  The same values
+    as PPO.update's policy.act / get_actions_log_prob / evaluate / _ppo_losses / _adapt_learning_rate (ppo.py
+    :103-169), without the unused action sample."""
+    pol = alg.policy
+    mu = pol.actor(obs)
+    std = pol._std(mu[:1])[0]  # [k]: the scalar or exp(log) std, differentiable
+    value = pol.critic(critic_obs)
+    surr, vloss, kl = _PPOLossFn.apply(mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old,
+                                       float(alg.clip_param), bool(alg.use_clipped_value_loss))
+    ent = None
+    if alg.entropy_coef != 0.0:  # Normal.entropy summed over the actions: the same for every sample
+        ent = (0.5 + 0.5 * math.log(2.0 * math.pi) + torch.log(std)).sum()
+    return surr, vloss, ent, kl, mu, std

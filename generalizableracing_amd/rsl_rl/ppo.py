@@ -15,6 +15,7 @@ import torch.optim as optim
 import torch.distributed as dist
 
 from . import distributed as gdist
+from . import fused_loss as _floss
 from . import linear as _lin
 from .rollout_storage import RolloutStorage
 
@@ -25,7 +26,7 @@ class PPO:
                  use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu",
                  normalize_advantage=True, storage_obs_dtype=torch.float32, fused_rollout_inference=False,
                  fused_rollout_precision="bf16", graph_update=False, update_autocast_bf16=False,
-                 graph_update_segmented=False, **kwargs):
+                 graph_update_segmented=False, fused_losses=True, **kwargs):
         self.env = env
         self.device = device
         self.desired_kl = desired_kl
@@ -68,6 +69,9 @@ class PPO:
         # the losses' exp / log / sums stay fp32 (autocast's fp32 list), parameters and Adam stay fp32
         self.update_autocast_bf16 = bool(update_autocast_bf16)
         self._flat = None  # gdist.FlatGrads: the parameters' gradients as views of one buffer
+        # the mini-batch losses (log prob, KL, surrogate, value loss) as one device op each way on CUDA
+        # (fused_loss.py); False: the torch ops
+        self.fused_losses = bool(fused_losses)
 
     def flat_grads(self) -> gdist.FlatGrads:
         """The flat gradient buffer over the parameters the loss reaches (all of them until the first mini-batch
@@ -201,18 +205,18 @@ class PPO:
                             str(self.device).startswith("cuda"))
         for (obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch, returns_batch,
              old_actions_log_prob_batch, old_mu_batch, old_sigma_batch, hid_states_batch, masks_batch) in generator:
-            with ac:
-                self.policy.act(obs_batch)
-                actions_log_prob_batch = self.policy.get_actions_log_prob(actions_batch)
-                value_batch = self.policy.evaluate(critic_obs_batch)
-                mu_batch = self.policy.action_mean
-                sigma_batch = self.policy.action_std
-                entropy_batch = self.policy.entropy
-            self._adapt_learning_rate(mu_batch.float(), sigma_batch.float(), old_mu_batch, old_sigma_batch)
-            surrogate_loss, value_loss = self._ppo_losses(actions_log_prob_batch.float(), old_actions_log_prob_batch,
-                                                          advantages_batch, value_batch.float(), target_values_batch,
-                                                          returns_batch)
-            loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_batch.float().mean()
+            if self._use_fused_losses(obs_batch):  # the same losses as one device op each way (fused_loss.py)
+                surrogate_loss, value_loss, ent, kl, _, _ = _floss.ppo_losses(
+                    self, obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch,
+                    returns_batch, old_actions_log_prob_batch, old_mu_batch, old_sigma_batch)
+                self._adapt_learning_rate_kl(kl)
+                loss = surrogate_loss + self.value_loss_coef * value_loss
+                if ent is not None:
+                    loss = loss - self.entropy_coef * ent
+            else:
+                surrogate_loss, value_loss, loss = self._torch_losses(
+                    ac, obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch,
+                    returns_batch, old_actions_log_prob_batch, old_mu_batch, old_sigma_batch)
             self.optimizer.zero_grad(set_to_none=False)  # (in place: the views of the flat buffer stay bound)
             if not self._grads_checked:
                 flat = self._check_all_grads(loss, params)
@@ -229,6 +233,39 @@ class PPO:
             "value_function": float(mean_value_loss) / num_updates,
             "surrogate": float(mean_surrogate_loss) / num_updates,
         }
+
+    def _use_fused_losses(self, obs) -> bool:
+        return (self.fused_losses and obs.is_cuda and not self.update_autocast_bf16
+                and _floss.fused_losses_ok(self.policy, obs))
+
+    def _adapt_learning_rate_kl(self, kl_mean):
+        """_adapt_learning_rate from the mini-batch's KL mean (computed by the fused losses)."""
+        if self.desired_kl is None or self.schedule != "adaptive":
+            return
+        kl_val = float(gdist.allreduce_mean(kl_mean.detach()))  # host decision, as in the reference
+        if kl_val > self.desired_kl * 2.0:
+            self.learning_rate = max(1e-5, self.learning_rate / 1.5)
+        elif self.desired_kl / 2.0 > kl_val > 0.0:
+            self.learning_rate = min(1e-2, self.learning_rate * 1.5)
+        for g in self.optimizer.param_groups:
+            g["lr"] = self.learning_rate
+
+    def _torch_losses(self, ac, obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch,
+                      returns_batch, old_actions_log_prob_batch, old_mu_batch, old_sigma_batch):
+        """ppo.py:103-169 as torch ops (CPU, autocast, other policies)."""
+        with ac:
+                self.policy.act(obs_batch)
+                actions_log_prob_batch = self.policy.get_actions_log_prob(actions_batch)
+                value_batch = self.policy.evaluate(critic_obs_batch)
+                mu_batch = self.policy.action_mean
+                sigma_batch = self.policy.action_std
+                entropy_batch = self.policy.entropy
+        self._adapt_learning_rate(mu_batch.float(), sigma_batch.float(), old_mu_batch, old_sigma_batch)
+        surrogate_loss, value_loss = self._ppo_losses(actions_log_prob_batch.float(), old_actions_log_prob_batch,
+                                                      advantages_batch, value_batch.float(), target_values_batch,
+                                                      returns_batch)
+        loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_batch.float().mean()
+        return surrogate_loss, value_loss, loss
 
 
 class _GraphedStep:
@@ -295,6 +332,16 @@ class _GraphedStep:
         alg, pol = self.alg, self.alg.policy
         obs, priv, act, val, adv, ret, logp, mu, sig = self._gather()
         obs, priv = obs.float(), priv.float()
+        if alg._use_fused_losses(obs):  # (fused_loss.py: one device op each way)
+            surrogate_loss, value_loss, ent, kl, _, _ = _floss.ppo_losses(alg, obs, priv, act, val, adv, ret, logp,
+                                                                        mu, sig)
+            if self._adaptive():
+                self.flat.extra[0].copy_(kl)
+            loss = surrogate_loss + alg.value_loss_coef * value_loss
+            if ent is not None:
+                loss = loss - alg.entropy_coef * ent
+            self._backward(loss, value_loss, surrogate_loss)
+            return
         # the eager loop's policy.act also draws a sample it never uses; torch.normal's check of the std
         # reads back to the host, which a capture forbids, so only the distribution is set here
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=alg.update_autocast_bf16):
@@ -311,6 +358,10 @@ class _GraphedStep:
                 self.flat.extra[0].copy_(torch.mean(kl))
         surrogate_loss, value_loss = alg._ppo_losses(logp_b, logp, adv, value_b, val, ret)
         loss = surrogate_loss + alg.value_loss_coef * value_loss - alg.entropy_coef * entropy_b.mean()
+        self._backward(loss, value_loss, surrogate_loss)
+
+    def _backward(self, loss, value_loss, surrogate_loss):
+        alg = self.alg
         if not alg._grads_checked:  # (first warm-up step, before any capture)
             grads = torch.autograd.grad(loss, self.params, retain_graph=True, allow_unused=True)
             self.flat = alg._check_all_grads(loss, self.params, grads)

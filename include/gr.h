@@ -462,6 +462,36 @@ int gr_mlp_in_forward(const float* x, int64_t rows, int32_t d, int32_t ldx, cons
 int gr_mlp_in_backward(const float* gh, const float* hv, const float* x, int64_t rows, int32_t d, int32_t ldx,
                        int32_t h, float slope, float* partial, float* sums, void* stream);
 
+/* The PPO losses of one mini-batch, forward and backward (standalone/rsl_rl/ext/algorithms/ppo.py:133-169: the
+ * adaptive-rate KL, the clipped surrogate, the (clipped) value loss; the Gaussian log prob of rsl_rl's
+ * ActorCritic with a state-independent std).  Row-strided fp32 inputs (ld_* in floats; the mini-batch's packed
+ * rows), k <= 8 actions, one thread per sample, fixed summation order, context-free and graph-capturable.
+ *   gr_ppo_loss_forward : sums [3] = [sum max(surrogate, clipped), sum value term, sum KL]  (means: / rows)
+ *   gr_ppo_loss_backward: g [2] = upstream gradients of the surrogate and value means (device scalars);
+ *                         dmu [rows][k], dvalue [rows], dstd [k] (summed over the rows)
+ * `partial` is caller-owned scratch of gr_ppo_loss_partials(rows) floats. */
+typedef struct {
+  int64_t rows;
+  int32_t k;
+  int32_t clipped_value; /* use_clipped_value_loss */
+  float clip;            /* clip_param */
+  const float* mu;       /* [rows] x ld_mu: the policy's action mean (the graph's output) */
+  const float* std;      /* [k]: the policy's action std */
+  const float* value;    /* the critic's value */
+  const float* act;      /* the stored actions */
+  const float* logp_old; /* the stored log probs */
+  const float* adv;
+  const float* value_old; /* the stored values (target_values_batch) */
+  const float* ret;
+  const float* mu_old;
+  const float* sig_old;
+  int64_t ld_mu, ld_value, ld_act, ld_logp_old, ld_adv, ld_value_old, ld_ret, ld_mu_old, ld_sig_old;
+} gr_ppo_loss_args;
+int64_t gr_ppo_loss_partials(int64_t rows);
+int gr_ppo_loss_forward(const gr_ppo_loss_args* args, float* partial, float* sums, void* stream);
+int gr_ppo_loss_backward(const gr_ppo_loss_args* args, const float* g, float* dmu, float* dvalue, float* partial,
+                         float* dstd, void* stream);
+
 /* In-library HIP-event timing of the fused step kernel alone (not the log
  * finalize): when enabled, gr_step brackets the env kernel with a pair of
  * events on the caller's stream (ring of 4096 pairs; do not capture into a

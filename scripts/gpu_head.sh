@@ -5,7 +5,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/${1:-head}
 mkdir -p $OUT
 cd $R
-timeout -k 10 600 python -u -m pytest tests/test_gpu_units.py tests/test_gpu_ppo_c2_golden.py tests/test_gpu_graph_update.py tests/test_gpu_graph_update_dp.py tests/test_gpu_parity.py -v -k "leaky_head or mlp_fused or mlp_in or column_sum or c2 or graph or runner" --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_units.py tests/test_gpu_ppo_c2_golden.py tests/test_gpu_graph_update.py tests/test_gpu_graph_update_dp.py tests/test_gpu_parity.py -v -k "leaky_head or mlp_fused or mlp_in or column_sum or fused_ppo or c2 or graph or runner" --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
 rc=$?; echo "pytest exit $rc" >> $OUT/pytest.log; [ $rc -ge 124 ] && exit 10
 timeout -k 10 400 python -u -c "
 import json, sys
