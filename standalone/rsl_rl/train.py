@@ -51,7 +51,8 @@ def build_parser() -> argparse.ArgumentParser:
                    help="The same launch with fp32 operands on fp32 MFMA, the reference's precision "
                         "(algorithm.fused_rollout_precision=fp32).")
     p.add_argument("--graph_update", action="store_true", default=False,
-                   help="PPO mini-batch step as one replayed hipGraph (algorithm.graph_update, single GPU).")
+                   help="PPO mini-batch step replayed from hipGraphs (algorithm.graph_update; at world size > 1 two graphs "
+                        "with the gradient all-reduce issued eagerly between them).")
     p.add_argument("--bf16_update", action="store_true", default=False,
                    help="PPO update forward/backward under bf16 autocast (algorithm.update_autocast_bf16).")
     p.add_argument("--bf16_storage", action="store_true", default=False,
