@@ -8,11 +8,13 @@ split into chunks of SPLIT (a batched GEMM: one workgroup set per chunk) and the
 summed.  Same module tree, parameters and state_dict keys as nn.Linear (the reference's checkpoints
 and exporters are unaffected); small batches, inference and TorchScript take F.linear.
 
-`MLP` (the actor / critic Sequential) runs its last LeakyReLU and output Linear as ONE op on those
-batches (`leaky_head`: gr_head_forward / gr_head_backward, gr_update.hip): the activation pass, the
-small-N head GEMMs and the activation's backward pass each stream a [rows, 256] matrix through HBM
-(`profiles/round03_update65536_graphed_kernel_stats.csv`), the fused op reads the pre-activation once
-forward and once backward.
+`MLP` (the actor / critic Sequential, same children and state_dict keys) runs everything around the hidden
+h1 x h2 GEMM in fused HIP ops on those batches (gr_update.hip): the first Linear (K = 16) with its bias and
+LeakyReLU (gr_mlp_in_forward) and, backward, its weight / bias gradients straight from the hidden gradient
+(gr_mlp_in_backward); the last LeakyReLU with the output Linear (gr_head_forward) and its backward, which also
+sums the hidden layer's bias gradient (gr_head_backward).  In torch each activation pass, the small-N head GEMMs
+and the bias sums streamed a [rows, 256] matrix through HBM (`profiles/round03_update65536_graphed_kernel_stats.csv`);
+DESIGN.md §4f has the before / after.
 """
 from __future__ import annotations
 

@@ -28,12 +28,24 @@ def main():
     actions = torch.randn(bench.ACTION_RING, n, 4, device="cuda:0", generator=g)
     graph = bench.capture_graph(env, actions, a.steps)
     ev = torch.cuda.Event()
-    res = {"sync": [], "spin_then_sync": []}
-    for r in range(2 * a.reps):
-        mode = "sync" if r % 2 == 0 else "spin_then_sync"
+    modes = ["sync", "spin_then_sync", "eager_env", "eager_raw"]
+    res = {m: [] for m in modes}
+    stream = env._stream()
+    ptrs = [actions[k].data_ptr() for k in range(bench.ACTION_RING)]
+    lib, ctx = env._lib, env._ctx
+    for r in range(len(modes) * a.reps):
+        mode = modes[r % len(modes)]
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        graph.replay()
+        if mode in ("sync", "spin_then_sync"):
+            graph.replay()
+        elif mode == "eager_env":
+            for k in range(a.steps):
+                env.step(actions[k % bench.ACTION_RING])
+        else:  # the binding rotation and the launch only (what a C-level launcher would do)
+            for k in range(a.steps):
+                env._advance()
+                lib.gr_step(ctx, ptrs[k % bench.ACTION_RING], stream)
         if mode == "spin_then_sync":
             ev.record()
             while not ev.query():

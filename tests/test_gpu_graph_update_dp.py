@@ -30,12 +30,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rollout(n_total):
-    """One seeded synthetic rollout (identical in every process), on the CPU."""
+def _rollout(n_total, act="elu"):
+    """One seeded synthetic rollout (identical in every process), on the CPU.  act="lrelu": the MLPs take the
+    fused device path of the update (rsl_rl/linear.py MLP) on the GPU."""
     from generalizableracing_amd.rsl_rl import ActorCritic
 
     torch.manual_seed(0)
-    pol = ActorCritic(16, 16, 4, [64, 64], [64, 64], "elu")
+    pol = ActorCritic(16, 16, 4, [64, 64], [64, 64], act)
     g = torch.Generator().manual_seed(1)
     obs = torch.randn(T, n_total, 16, generator=g)
     cobs = torch.randn(T, n_total, 16, generator=g)
@@ -53,10 +54,10 @@ def _rollout(n_total):
     return pol, data, last
 
 
-def _alg(sl, n_total, device, **kw):
+def _alg(sl, n_total, device, act="elu", **kw):
     from generalizableracing_amd.rsl_rl.ppo import PPO
 
-    pol, data, last = _rollout(n_total)
+    pol, data, last = _rollout(n_total, act)
     alg = PPO(pol, device=device, num_learning_epochs=3, num_mini_batches=1, clip_param=0.2, gamma=0.99, lam=0.95,
               value_loss_coef=1.0, entropy_coef=0.005, learning_rate=5e-4, max_grad_norm=1.0, schedule="adaptive",
               desired_kl=0.01, **kw)
@@ -88,21 +89,22 @@ def _updates(alg, data, last, sl, reps=2):
     return out
 
 
-def test_segmented_equals_single_graph():
+@pytest.mark.parametrize("act", ["elu", "lrelu"])
+def test_segmented_equals_single_graph(act):
     n = 512
     res = []
     for seg in (False, True):
-        alg, data, last, sl = _alg(slice(0, n), n, "cuda:0", graph_update=True, graph_update_segmented=seg)
+        alg, data, last, sl = _alg(slice(0, n), n, "cuda:0", act, graph_update=True, graph_update_segmented=seg)
         res.append(_updates(alg, data, last, sl))
         assert (alg._graphed.graph_b is not None) is seg
-    p0 = _params(_alg(slice(0, n), n, "cpu")[0])
+    p0 = _params(_alg(slice(0, n), n, "cpu", act)[0])
     for (pa, la), (pb, lb) in zip(*res):
         moved = float((pa - p0).abs().max())
         assert moved > 0 and float((pa - pb).abs().max()) <= 1e-6 * moved
         assert la == lb
 
 
-def _worker(rank, world, port, q, n_total):
+def _worker(rank, world, port, q, n_total, act):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0")
     try:
@@ -111,7 +113,7 @@ def _worker(rank, world, port, q, n_total):
 
         gdist.init_from_env("gloo")
         per = n_total // world
-        alg, data, last, sl = _alg(slice(rank * per, (rank + 1) * per), n_total, "cuda:0", graph_update=True)
+        alg, data, last, sl = _alg(slice(rank * per, (rank + 1) * per), n_total, "cuda:0", act, graph_update=True)
         out = _updates(alg, data, last, sl)
         assert alg._graphed.segmented and alg._graphed.graph_b is not None
         q.put((rank, [(p.tolist(), lr) for p, lr in out]))
@@ -123,15 +125,16 @@ def _worker(rank, world, port, q, n_total):
 
 
 @pytest.mark.timeout(300)
-def test_two_gloo_ranks_graphed_update_matches_single_rank():
+@pytest.mark.parametrize("act", ["elu", "lrelu"])
+def test_two_gloo_ranks_graphed_update_matches_single_rank(act):
     n_total = 1024
-    ref, data, last, sl = _alg(slice(0, n_total), n_total, "cpu")
+    ref, data, last, sl = _alg(slice(0, n_total), n_total, "cpu", act)
     p0 = _params(ref)
     want = _updates(ref, data, last, sl)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, n_total)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, n_total, act)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=280) for _ in procs)
