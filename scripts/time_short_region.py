@@ -52,6 +52,17 @@ def main():
                 pass
         torch.cuda.synchronize()
         res[mode].append((time.perf_counter() - t0) * 1e6 / a.steps)
+    # GPU-side duration of the same replay (events on the stream around it) vs the wall clock
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    gpu = []
+    for _ in range(a.reps):
+        torch.cuda.synchronize()
+        e0.record()
+        graph.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        gpu.append(e0.elapsed_time(e1) * 1e3 / a.steps)
+    res["gpu_events_per_step"] = gpu
     out = {k: {"median_us_per_step": float(np.median(v)), "min": float(np.min(v))} for k, v in res.items()}
     out["steps"] = a.steps
     print(json.dumps(out))
