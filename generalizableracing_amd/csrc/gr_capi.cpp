@@ -856,6 +856,39 @@ int gr_mlp_in_backward(const float* gh, const float* hv, const float* x, int64_t
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
+int gr_adam_prepare(gr_adam_segment* t, int32_t nseg, int32_t* nblocks) {
+  if (!t || !nblocks || nseg < 1 || nseg > GR_ADAM_MAX_SEGMENTS) return GR_ERR_ARG;
+  int64_t nb = 0;
+  for (int s = 0; s < nseg; ++s) {
+    gr_adam_segment& g = t[s];
+    if (!g.param || !g.grad || !g.exp_avg || !g.exp_avg_sq || g.numel <= 0 || g.step_slot < 0) return GR_ERR_ARG;
+    for (int r = 0; r < s; ++r)
+      if (t[r].step_slot == g.step_slot) return GR_ERR_ARG;  // one step counter per segment
+    g.block_start = (int32_t)nb;
+    nb += (g.numel + GR_ADAM_BLOCK - 1) / GR_ADAM_BLOCK;
+    if (nb > 0x7fffffff) return GR_ERR_ARG;
+  }
+  *nblocks = (int32_t)nb;
+  return GR_OK;
+}
+
+static bool adam_args_ok(const gr_adam_args* a) {
+  return a && a->nseg >= 1 && a->nseg <= GR_ADAM_MAX_SEGMENTS && a->nblocks >= 1 && a->seg && a->step && a->coef &&
+         a->part;
+}
+
+int gr_adam_clip(const gr_adam_args* a, float max_norm, float* norm_out, void* stream) {
+  if (!adam_args_ok(a) || !(max_norm > 0.0f)) return GR_ERR_ARG;
+  const hipError_t e = gr::launch_adam_clip(*a, max_norm, norm_out, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
+int gr_adam_step(const gr_adam_args* a, void* stream) {
+  if (!adam_args_ok(a)) return GR_ERR_ARG;
+  const hipError_t e = gr::launch_adam_step(*a, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
 int64_t gr_ppo_loss_partials(int64_t rows) {
   if (rows < 0) return GR_ERR_ARG;
   return (int64_t)gr::ppo_loss_blocks(rows) * 8;

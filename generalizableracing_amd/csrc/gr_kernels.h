@@ -127,6 +127,8 @@ hipError_t launch_head_backward(const float* z, const float* gy, long long m, in
                                 float slope, float* gz, float* part, float* sums, hipStream_t s);
 hipError_t launch_in_forward(const float* x, long long m, int d, int ldx, const float* w, const float* b, int h,
                              float slope, float* y, hipStream_t s);
+hipError_t launch_adam_clip(const gr_adam_args& a, float max_norm, float* norm_out, hipStream_t s);
+hipError_t launch_adam_step(const gr_adam_args& a, hipStream_t s);
 int ppo_loss_blocks(long long rows);
 hipError_t launch_ppo_loss_forward(const gr_ppo_loss_args& a, float* part, float* sums, hipStream_t s);
 hipError_t launch_ppo_loss_backward(const gr_ppo_loss_args& a, const float* g, float* dmu, float* dvalue, float* part,

@@ -619,4 +619,113 @@ hipError_t launch_ppo_loss_backward(const gr_ppo_loss_args& a, const float* g, f
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Adam and the gradient-norm clip of the PPO update over a device table of parameter segments
+// (rsl_rl/flat_adam.py): torch.nn.utils.clip_grad_norm_ + torch.optim.Adam (ppo.py:179-181) as 2 + 2 launches
+// instead of ~55 small per-tensor ones.  A workgroup of 256 threads owns GR_ADAM_BLOCK consecutive elements of one
+// segment, thread t elements t, t + 256, t + 512, t + 768 (coalesced; the segments need no alignment: gradients are
+// views of one flat buffer at any offset).
+
+// the workgroup's segment: ballot over the table's block_start (ascending); wave-uniform, readfirstlane'd so the
+// segment's fields are scalar loads
+__device__ __forceinline__ int adam_segment_of(const gr_adam_args& a, int b) {
+  const int l = threadIdx.x & 63;
+  const int bs = l < a.nseg ? a.seg[l].block_start : 0x7fffffff;
+  const unsigned long long m = __ballot(bs <= b);
+  return __builtin_amdgcn_readfirstlane(__popcll(m) - 1);
+}
+
+// per workgroup: the sum of squares of its elements in double -> part[b]
+__global__ __launch_bounds__(256) void adam_norm_part(gr_adam_args a) {
+  __shared__ double sm[4];
+  const int b = blockIdx.x, s = adam_segment_of(a, b);
+  const gr_adam_segment g = a.seg[s];  // (a copy: scalar loads, no reload after the stores)
+  const long long base = (long long)(b - g.block_start) * GR_ADAM_BLOCK;
+  double acc = 0.0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const long long j = base + k * 256 + threadIdx.x;
+    if (j < g.numel) {
+      const double x = g.grad[j];
+      acc += x * x;
+    }
+  }
+  for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) a.part[b] = (sm[0] + sm[1]) + (sm[2] + sm[3]);
+}
+
+// every workgroup sums part[] in the same order (the same coefficient everywhere), then scales its elements:
+// coefficient min(1, max_norm / (norm + 1e-6)) (torch: clip_coef_clamped, multiplied always); workgroup 0 writes
+// the norm
+__global__ __launch_bounds__(256) void adam_clip_apply(gr_adam_args a, float max_norm, float* __restrict__ norm_out) {
+  __shared__ double sm[4];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < a.nblocks; i += 256) acc += a.part[i];
+  for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  const float norm = (float)sqrt((sm[0] + sm[1]) + (sm[2] + sm[3]));
+  float c = max_norm / (norm + 1.0e-6f);
+  c = c < 1.0f ? c : 1.0f;
+  const int b = blockIdx.x, s = adam_segment_of(a, b);
+  if (b == 0 && threadIdx.x == 0 && norm_out) norm_out[0] = norm;
+  const gr_adam_segment g = a.seg[s];  // (a copy: scalar loads, no reload after the stores)
+  const long long base = (long long)(b - g.block_start) * GR_ADAM_BLOCK;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const long long j = base + k * 256 + threadIdx.x;
+    if (j < g.numel) g.grad[j] = g.grad[j] * c;
+  }
+}
+
+// step counters of the segments: +1, then the segment's coefficients in double (one thread per segment)
+__global__ __launch_bounds__(64) void adam_count(gr_adam_args a) {
+  const int s = threadIdx.x;
+  if (s >= a.nseg) return;
+  const int k = a.seg[s].step_slot;
+  const float t = a.step[k] + 1.0f;
+  a.step[k] = t;
+  const double lr = a.lr_ptr ? (double)a.lr_ptr[0] : a.lr;
+  a.coef[2 * k] = (float)(lr / (1.0 - pow(a.beta1, (double)t)));
+  a.coef[2 * k + 1] = (float)sqrt(1.0 - pow(a.beta2, (double)t));
+}
+
+// torch's lerp (weight < 0.5): m + w (g - m); addcmul: v + ((1 - b2) g) g; addcdiv: p + (-step_size) (m / denom)
+__global__ __launch_bounds__(256) void adam_update(gr_adam_args a) {
+  const int b = blockIdx.x, s = adam_segment_of(a, b);
+  const gr_adam_segment g = a.seg[s];  // (a copy: scalar loads, no reload after the stores)
+  const long long base = (long long)(b - g.block_start) * GR_ADAM_BLOCK;
+  const int k = g.step_slot;
+  const float step_size = a.coef[2 * k], bc2s = a.coef[2 * k + 1];
+  const float w1 = (float)(1.0 - a.beta1), b2 = (float)a.beta2, w2 = (float)(1.0 - a.beta2);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const long long j = base + q * 256 + threadIdx.x;
+    if (j >= g.numel) break;
+    const float gr = g.grad[j];
+    float m = g.exp_avg[j], v = g.exp_avg_sq[j];
+    m = m + w1 * (gr - m);
+    v = v * b2;
+    v = v + (w2 * gr) * gr;
+    g.exp_avg[j] = m;
+    g.exp_avg_sq[j] = v;
+    const float denom = sqrtf(v) / bc2s + a.eps;
+    g.param[j] = g.param[j] + (-step_size) * (m / denom);
+  }
+}
+
+hipError_t launch_adam_clip(const gr_adam_args& a, float max_norm, float* norm_out, hipStream_t s) {
+  hipLaunchKernelGGL(adam_norm_part, dim3(a.nblocks), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(adam_clip_apply, dim3(a.nblocks), dim3(256), 0, s, a, max_norm, norm_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_adam_step(const gr_adam_args& a, hipStream_t s) {
+  hipLaunchKernelGGL(adam_count, dim3(1), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(adam_update, dim3(a.nblocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
 }  // namespace gr

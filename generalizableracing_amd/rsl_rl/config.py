@@ -56,6 +56,9 @@ class RslRlPpoAlgorithmCfg:
     # not in the reference: the update's mini-batch losses (log prob, KL, clipped surrogate and value loss) as one
     # HIP op each way (rsl_rl/fused_loss.py); False keeps the torch ops
     fused_losses: bool = True
+    # not in the reference: the grad-norm clip and Adam as four HIP launches over the parameter table
+    # (rsl_rl/flat_adam.py); False keeps torch.optim.Adam + nn.utils.clip_grad_norm_
+    fused_adam: bool = True
 
 
 @dataclass

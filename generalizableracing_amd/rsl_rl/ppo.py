@@ -15,6 +15,7 @@ import torch.optim as optim
 import torch.distributed as dist
 
 from . import distributed as gdist
+from . import flat_adam as _fadam
 from . import fused_loss as _floss
 from . import linear as _lin
 from .rollout_storage import RolloutStorage
@@ -26,7 +27,7 @@ class PPO:
                  use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu",
                  normalize_advantage=True, storage_obs_dtype=torch.float32, fused_rollout_inference=False,
                  fused_rollout_precision="bf16", graph_update=False, update_autocast_bf16=False,
-                 graph_update_segmented=False, fused_losses=True, **kwargs):
+                 graph_update_segmented=False, fused_losses=True, fused_adam=True, **kwargs):
         self.env = env
         self.device = device
         self.desired_kl = desired_kl
@@ -36,7 +37,9 @@ class PPO:
         self.policy.to(self.device)
         gdist.broadcast_params(self.policy)
         self.storage: RolloutStorage | None = None
-        self.optimizer = optim.Adam(self.policy.parameters(), lr=learning_rate)
+        # Adam (ppo.py:39) and the grad-norm clip as four device launches over the parameter table on CUDA
+        # (flat_adam.py); torch.optim.Adam + nn.utils.clip_grad_norm_ on CPU or with fused_adam=False
+        self.optimizer = _fadam.make_adam(self.policy.parameters(), learning_rate, fused=fused_adam)
         self.transition = RolloutStorage.Transition()
         self.clip_param = clip_param
         self.num_learning_epochs = num_learning_epochs
@@ -223,7 +226,7 @@ class PPO:
                 flat.bind()
             loss.backward()
             gdist.allreduce_grads(params, flat)
-            nn.utils.clip_grad_norm_(params, self.max_grad_norm)
+            _fadam.clip_grad_norm_(self.optimizer, params, self.max_grad_norm)
             self.optimizer.step()
             mean_value_loss += value_loss.detach()
             mean_surrogate_loss += surrogate_loss.detach()
@@ -273,7 +276,8 @@ class _GraphedStep:
 
     Per mini-batch the eager loop launches ~150 small kernels and reads the KL back to the host for the
     adaptive learning rate (ppo.py:133-150).  Here the learning-rate rule runs on the device (the same
-    comparisons, in fp32), Adam takes the rate as a device tensor (`capturable=True`), and the step
+    comparisons, in fp32), Adam takes the rate as a device tensor (FlatAdam's lr pointer, or torch's
+    `capturable=True` with fused_adam off), and the step
     (mini-batch gathers from the storage by a static index buffer, forward, losses, backward, grad
     clipping, Adam) is captured once and replayed per mini-batch.  Capture needs warm-up steps; the
     parameters, the optimizer state and the rate are snapshotted before and restored after, so training
@@ -299,12 +303,16 @@ class _GraphedStep:
         self.params = list(alg.policy.parameters())
         self.lr = torch.tensor(float(alg.learning_rate), device=dev, dtype=torch.float32)
         old = alg.optimizer
-        self.opt = optim.Adam(self.params, lr=self.lr, capturable=True)
-        if old.state:  # resumed from a checkpoint: keep Adam's moments and step counts
-            self.opt.load_state_dict(old.state_dict())
-        for g in self.opt.param_groups:  # (load_state_dict brings the eager groups' settings)
-            g["lr"] = self.lr
-            g["capturable"] = True
+        if isinstance(old, _fadam.FlatAdam):  # the same launches eager or captured: the rate as a device tensor
+            self.opt = old
+            self.opt.param_groups[0]["lr"] = self.lr
+        else:
+            self.opt = optim.Adam(self.params, lr=self.lr, capturable=True)
+            if old.state:  # resumed from a checkpoint: keep Adam's moments and step counts
+                self.opt.load_state_dict(old.state_dict())
+            for g in self.opt.param_groups:  # (load_state_dict brings the eager groups' settings)
+                g["lr"] = self.lr
+                g["capturable"] = True
         alg.optimizer = self.opt
         self.flat = alg.flat_grads()
         self.idx = torch.zeros(self.mb, dtype=torch.long, device=dev)
@@ -382,7 +390,7 @@ class _GraphedStep:
                 lr_new = torch.where(k > alg.desired_kl * 2.0, down,
                                      torch.where((alg.desired_kl / 2.0 > k) & (k > 0.0), up, lr))
                 self.lr.copy_(lr_new)
-        nn.utils.clip_grad_norm_(self.params, alg.max_grad_norm)
+        _fadam.clip_grad_norm_(self.opt, self.params, alg.max_grad_norm)
         self.opt.step()
 
     def _capture(self):

@@ -27,6 +27,7 @@ import torch
 import torch.nn as nn
 
 from . import distributed as gdist
+from . import flat_adam as _fadam
 from .ppo import PPO
 from .rollout_storage_l2c2 import RolloutStorageL2C2
 
@@ -125,7 +126,7 @@ class PPOL2C2(PPO):
                 flat.bind()
             loss.backward()
             gdist.allreduce_grads(params, flat)
-            nn.utils.clip_grad_norm_(params, self.max_grad_norm)
+            _fadam.clip_grad_norm_(self.optimizer, params, self.max_grad_norm)
             self.optimizer.step()
             mean_value_loss += value_loss.detach()
             mean_surrogate_loss += surrogate_loss.detach()

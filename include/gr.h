@@ -492,6 +492,48 @@ int gr_ppo_loss_forward(const gr_ppo_loss_args* args, float* partial, float* sum
 int gr_ppo_loss_backward(const gr_ppo_loss_args* args, const float* g, float* dmu, float* dvalue, float* partial,
                          float* dstd, void* stream);
 
+/* Adam and the gradient-norm clip of the PPO update (standalone/rsl_rl/ext/algorithms/ppo.py:179-181:
+ * nn.utils.clip_grad_norm_(max_grad_norm) then torch.optim.Adam.step) over a table of parameter segments
+ * (generalizableracing_amd/rsl_rl/flat_adam.py).  The table lives in DEVICE memory (the kernels read it, so a
+ * launch's arguments stay small); gr_adam_prepare checks a host copy of it and numbers its blocks (1024 elements
+ * each, GR_ADAM_BLOCK) before the caller uploads it.  step[step_slot] is a segment's Adam step count (fp32,
+ * device; one slot per segment); lr_ptr (device) overrides lr when not null (the graph-captured update's rate
+ * tensor).  Context-free, graph-capturable, on `stream`.
+ *   gr_adam_prepare: fills block_start, *nblocks = the launch's blocks (the size of `part`); GR_ERR_ARG if a
+ *                    pointer is null, a size not positive, a slot negative or shared, or nseg outside 1..64
+ *   gr_adam_clip:    grads *= min(1, max_norm / (||all grads|| + 1e-6)); norm_out[0] = the norm (may be null);
+ *                    the norm in double, per block then in one fixed order (deterministic)
+ *   gr_adam_step:    step[slot] += 1 per segment (and its coefficients into coef), then the Adam update of every
+ *                    element.  Matches torch's foreach Adam (torch/optim/adam.py _multi_tensor_adam,
+ *                    non-capturable): m.lerp_(g, 1 - b1); v = v * b2 + (1 - b2) * g * g; step_size = lr / (1 - b1^t)
+ *                    and sqrt(1 - b2^t) in double, rounded to fp32; p += -step_size * m / (sqrt(v) / bc2_sqrt + eps) */
+#define GR_ADAM_MAX_SEGMENTS 64
+#define GR_ADAM_BLOCK 1024
+typedef struct {
+  float* param;
+  float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t numel;
+  int32_t step_slot;
+  int32_t block_start; /* gr_adam_prepare */
+} gr_adam_segment;
+typedef struct {
+  int32_t nseg;
+  int32_t nblocks;          /* gr_adam_prepare */
+  double lr, beta1, beta2;  /* host doubles as in torch's foreach Adam (bias corrections in double) */
+  float eps;
+  int32_t pad;
+  const float* lr_ptr;
+  float* step;                 /* [slots] */
+  float* coef;                 /* [slots][2] scratch: lr / (1 - b1^t), sqrt(1 - b2^t) */
+  double* part;                /* [nblocks] scratch of the clip */
+  const gr_adam_segment* seg;  /* device table [nseg] */
+} gr_adam_args;
+int gr_adam_prepare(gr_adam_segment* table, int32_t nseg, int32_t* nblocks);
+int gr_adam_clip(const gr_adam_args* args, float max_norm, float* norm_out, void* stream);
+int gr_adam_step(const gr_adam_args* args, void* stream);
+
 /* In-library HIP-event timing of the fused step kernel alone (not the log
  * finalize): when enabled, gr_step brackets the env kernel with a pair of
  * events on the caller's stream (ring of 4096 pairs; do not capture into a

@@ -74,7 +74,8 @@ def record_grads(alg, out, count=2):
     replay = torch.cuda.CUDAGraph.replay
 
     def step_rec(*a, **kw):
-        if len(out) < count:
+        # (the graph-captured update steps its optimizer in warm-ups and capture: recorded from the replays)
+        if len(out) < count and alg._graphed is None:
             out.append(torch.cat([p.grad.reshape(-1).detach().cpu() for p in params]))
         return step(*a, **kw)
 

@@ -78,3 +78,31 @@ def test_create_rejects_bad_config(field, value):
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         _abi.load(str(tmp_path / "libgr.so"))
+
+
+def test_adam_prepare_numbers_blocks_and_rejects_bad_tables():
+    """gr_adam_prepare (host only): block_start per segment in GR_ADAM_BLOCK = 1024 element blocks, the launch's
+    block count; null pointers, empty segments and a shared step slot are argument errors; ctypes layout of the
+    segment (48 B) and of the launch arguments (80 B) as in include/gr.h."""
+    from generalizableracing_amd.rsl_rl.flat_adam import GrAdamArgs, GrAdamSegment
+
+    assert C.sizeof(GrAdamSegment) == 48 and C.sizeof(GrAdamArgs) == 80
+    lib = _abi.load()
+    sizes = [4096, 256, 1, 1025, 3]
+    t = (GrAdamSegment * len(sizes))()
+    for i, n in enumerate(sizes):
+        t[i].param = t[i].grad = t[i].exp_avg = t[i].exp_avg_sq = 0x1000
+        t[i].numel, t[i].step_slot = n, len(sizes) - 1 - i
+    nb = C.c_int32()
+    assert lib.gr_adam_prepare(C.addressof(t), len(sizes), C.byref(nb)) == 0
+    assert [t[i].block_start for i in range(len(sizes))] == [0, 4, 5, 6, 8]
+    assert nb.value == 9
+    t[3].step_slot = t[0].step_slot
+    assert lib.gr_adam_prepare(C.addressof(t), len(sizes), C.byref(nb)) == -1  # GR_ERR_ARG
+    t[3].step_slot = 1
+    t[2].numel = 0
+    assert lib.gr_adam_prepare(C.addressof(t), len(sizes), C.byref(nb)) == -1  # GR_ERR_ARG
+    t[2].numel = 1
+    t[1].grad = None
+    assert lib.gr_adam_prepare(C.addressof(t), len(sizes), C.byref(nb)) == -1  # GR_ERR_ARG
+    assert lib.gr_adam_prepare(C.addressof(t), 65, C.byref(nb)) == -1  # GR_ERR_ARG
