@@ -889,6 +889,40 @@ int gr_adam_step(const gr_adam_args* a, void* stream) {
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
+static bool dones_bytes_ok(int b) { return b == 1 || b == 4 || b == 8; }
+
+int gr_store_transition(const gr_transition_args* a, void* stream) {
+  if (!a || a->n < 0 || a->k < 1 || a->k > 8 || !dones_bytes_ok(a->dones_bytes)) return GR_ERR_ARG;
+  if (a->n == 0) return GR_OK;
+  if (!a->reward || !a->dones || !a->value || !a->action || !a->logp || !a->mu || !a->sigma || !a->out_reward ||
+      !a->out_dones || !a->out_action || !a->out_value || !a->out_logp || !a->out_mu || !a->out_sigma)
+    return GR_ERR_ARG;
+  if (a->ld_value < 0 || a->ld_logp < 0 || a->ld_action < 0 || a->ld_mu < 0 || a->ld_sigma < 0) return GR_ERR_ARG;
+  const hipError_t e = gr::launch_store_transition(*a, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
+int gr_episode_accumulate(int64_t n, const float* reward, const void* dones, int32_t dones_bytes, float* cur_rew,
+                          float* cur_len, float* fin_rew, float* fin_len, uint8_t* fin_done, void* stream) {
+  if (n < 0 || !dones_bytes_ok(dones_bytes)) return GR_ERR_ARG;
+  if (n == 0) return GR_OK;
+  if (!reward || !dones || !cur_rew || !cur_len || !fin_rew || !fin_len || !fin_done) return GR_ERR_ARG;
+  const hipError_t e = gr::launch_episode_accumulate(n, reward, dones, dones_bytes, cur_rew, cur_len, fin_rew,
+                                                     fin_len, fin_done, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
+int gr_gae(int64_t n, int32_t t_steps, float gamma, float lam, const float* rewards, const uint8_t* dones,
+           const float* values, const float* last_values, int64_t ld_last, float* returns, float* advantages,
+           void* stream) {
+  if (n < 0 || t_steps < 1 || ld_last < 0) return GR_ERR_ARG;
+  if (n == 0) return GR_OK;
+  if (!rewards || !dones || !values || !last_values || !returns || !advantages) return GR_ERR_ARG;
+  const hipError_t e = gr::launch_gae(n, t_steps, gamma, lam, rewards, dones, values, last_values, ld_last, returns,
+                                      advantages, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
 int64_t gr_ppo_loss_partials(int64_t rows) {
   if (rows < 0) return GR_ERR_ARG;
   return (int64_t)gr::ppo_loss_blocks(rows) * 8;

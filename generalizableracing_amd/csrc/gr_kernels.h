@@ -129,6 +129,13 @@ hipError_t launch_in_forward(const float* x, long long m, int d, int ldx, const 
                              float slope, float* y, hipStream_t s);
 hipError_t launch_adam_clip(const gr_adam_args& a, float max_norm, float* norm_out, hipStream_t s);
 hipError_t launch_adam_step(const gr_adam_args& a, hipStream_t s);
+hipError_t launch_store_transition(const gr_transition_args& a, hipStream_t s);  // gr_rollout.hip
+hipError_t launch_episode_accumulate(long long n, const float* reward, const void* dones, int dones_bytes,
+                                     float* cur_rew, float* cur_len, float* fin_rew, float* fin_len,
+                                     uint8_t* fin_done, hipStream_t s);
+hipError_t launch_gae(long long n, int t_steps, float gamma, float lam, const float* rewards, const uint8_t* dones,
+                      const float* values, const float* last_values, long long ld_last, float* returns,
+                      float* advantages, hipStream_t s);
 int ppo_loss_blocks(long long rows);
 hipError_t launch_ppo_loss_forward(const gr_ppo_loss_args& a, float* part, float* sums, hipStream_t s);
 hipError_t launch_ppo_loss_backward(const gr_ppo_loss_args& a, const float* g, float* dmu, float* dvalue, float* part,

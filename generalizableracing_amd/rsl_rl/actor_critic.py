@@ -88,7 +88,14 @@ class ActorCritic(nn.Module):
 
     def act(self, observations, **kwargs):
         self.update_distribution(observations)
-        return self.distribution.sample()
+        d = self.distribution
+        if d.loc.is_cuda:
+            # Normal.sample is torch.normal(loc, scale), whose `std >= 0` check reads back to the host on every
+            # call; its draw is normal_(0, 1) into a fresh tensor, then mul_(std).add_(mean): the same bits here,
+            # without the synchronisation
+            with torch.no_grad():
+                return torch.randn(d.loc.shape, dtype=d.loc.dtype, device=d.loc.device).mul_(d.scale).add_(d.loc)
+        return d.sample()
 
     def get_actions_log_prob(self, actions):
         return self.distribution.log_prob(actions).sum(dim=-1)

@@ -21,6 +21,7 @@ from . import distributed as gdist
 from .actor_critic import ActorCritic, EmpiricalNormalization
 from .ppo import PPO
 from .ppo_l2c2 import PPOL2C2
+from .rollout_ops import EpisodeStats
 from .vision_actor_critic import VisionActorCritic
 
 ALGORITHMS = {"PPO": PPO, "PPOL2C2": PPOL2C2}
@@ -50,38 +51,8 @@ def _make_writer(log_dir, logger_type):
     return _CsvWriter(log_dir)
 
 
-class _EpisodeStats:
-    """Device-side replacement for the reference's rewbuffer/lenbuffer deques (maxlen 100)."""
-
-    def __init__(self, num_envs, device, maxlen=100):
-        self.cur_rew = torch.zeros(num_envs, device=device)
-        self.cur_len = torch.zeros(num_envs, device=device)
-        self.maxlen = maxlen
-        self.ring_rew = torch.zeros(maxlen + 1, device=device)
-        self.ring_len = torch.zeros(maxlen + 1, device=device)
-        self.head = torch.zeros((), dtype=torch.long, device=device)
-        self.count = torch.zeros((), dtype=torch.long, device=device)
-
-    def update(self, rewards, dones):
-        self.cur_rew += rewards
-        self.cur_len += 1
-        d = dones > 0
-        di = d.long()
-        pos = torch.cumsum(di, 0) - 1 + self.head
-        slot = torch.where(d, pos % self.maxlen, torch.full_like(pos, self.maxlen))
-        self.ring_rew.scatter_(0, slot, self.cur_rew)
-        self.ring_len.scatter_(0, slot, self.cur_len)
-        n = di.sum()
-        self.head = (self.head + n) % self.maxlen
-        self.count = torch.clamp(self.count + n, max=self.maxlen)
-        self.cur_rew = torch.where(d, torch.zeros_like(self.cur_rew), self.cur_rew)
-        self.cur_len = torch.where(d, torch.zeros_like(self.cur_len), self.cur_len)
-
-    def means(self):
-        c = int(self.count)
-        if c == 0:
-            return None
-        return float(self.ring_rew[:c].mean()), float(self.ring_len[:c].mean())
+# the reference's rewbuffer / lenbuffer deques and episode sums (on_policy_runner.py:128-173), on the device
+_EpisodeStats = EpisodeStats
 
 
 class OnPolicyRunner:
@@ -163,7 +134,7 @@ class OnPolicyRunner:
             storage.discard_sink()  # fresh observations: slot 0 is copied from them
         self.train_mode()
         ep_infos = []
-        stats = _EpisodeStats(self.env.num_envs, self.device)
+        stats = EpisodeStats(self.env.num_envs, self.device, steps=self.num_steps_per_env)
         start_iter = self.current_learning_iteration
         tot_iter = start_iter + num_learning_iterations
         for it in range(start_iter, tot_iter):

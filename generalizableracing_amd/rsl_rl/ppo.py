@@ -18,6 +18,7 @@ from . import distributed as gdist
 from . import flat_adam as _fadam
 from . import fused_loss as _floss
 from . import linear as _lin
+from . import rollout_ops as _rops
 from .rollout_storage import RolloutStorage
 
 
@@ -126,6 +127,14 @@ class PPO:
         return self.transition.actions
 
     def process_env_step(self, rewards, dones, infos):
+        tos = infos.get("time_outs")
+        tos = tos.to(self.device) if tos is not None else None
+        if _rops.store_ok(self.storage, self.transition, rewards, dones, tos):
+            # the bootstrap below and add_transitions as one launch (rollout_ops.py), the same bits
+            _rops.store_transition(self.storage, self.transition, rewards, dones, tos, self.gamma)
+            self.transition.clear()
+            self.policy.reset(dones)
+            return
         self.transition.rewards = rewards.clone()
         self.transition.dones = dones
         if "time_outs" in infos:  # bootstrapping on time outs (ppo.py:88-92)

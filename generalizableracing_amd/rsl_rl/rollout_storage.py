@@ -132,7 +132,15 @@ class RolloutStorage:
             self.prefilled[0] = True
 
     def compute_returns(self, last_values, gamma, lam, normalize_advantage: bool = True):
-        """GAE, rollout_storage.py:113-127."""
+        """GAE, rollout_storage.py:113-127 (CUDA fp32: one launch, rollout_ops.gae, the same bits)."""
+        from . import rollout_ops
+
+        if rollout_ops.gae_ok(self, last_values):
+            rollout_ops.gae(self, last_values, gamma, lam)
+            if normalize_advantage:
+                mean, std = gdist.global_mean_std(self.advantages)
+                self.advantages.sub_(mean).div_(std + 1e-8)
+            return
         advantage = 0
         for step in reversed(range(self.num_transitions_per_env)):
             next_values = last_values if step == self.num_transitions_per_env - 1 else self.values[step + 1]

@@ -534,6 +534,48 @@ int gr_adam_prepare(gr_adam_segment* table, int32_t nseg, int32_t* nblocks);
 int gr_adam_clip(const gr_adam_args* args, float max_norm, float* norm_out, void* stream);
 int gr_adam_step(const gr_adam_args* args, void* stream);
 
+/* The rollout loop's per-step bookkeeping (generalizableracing_amd/rsl_rl/rollout_ops.py), one launch each, the
+ * torch ops' arithmetic in their order (bit-identical stored rollouts).  Context-free, graph-capturable.
+ *   gr_store_transition: PPO.process_env_step + RolloutStorage.add_transitions (standalone/rsl_rl/ext/algorithms/
+ *       ppo.py:83-95, rsl_rl rollout_storage.py:74-98) for everything but the observations: out_reward = r +
+ *       gamma * (v * time_out) (time_out null: r), out_dones = dones != 0, and the action / value / log prob /
+ *       mean / std rows.  Inputs are row-strided (ld_* in floats; 0 repeats row 0, e.g. the expanded std); the
+ *       outputs are the storage slot's contiguous [n, k] / [n] rows.  k <= 8; dones_bytes 1 (bool, uint8), 4 or 8.
+ *   gr_episode_accumulate: the runner's episode sums (standalone/rsl_rl/ext/runners/on_policy_runner.py:167-173):
+ *       cur_rew += reward, cur_len += 1; fin_rew / fin_len = those sums and fin_done = dones != 0 (the finished
+ *       episodes go to the deques from there); cur_* of done envs zeroed.
+ *   gr_gae: RolloutStorage.compute_returns (rollout_storage.py:113-127) over [t_steps][n] planes (rewards, dones
+ *       as bytes, values), last_values row-strided by ld_last; writes returns and advantages = returns - values. */
+typedef struct {
+  int64_t n;
+  int32_t k;
+  int32_t dones_bytes;
+  float gamma;
+  int32_t pad;
+  const float* reward;
+  const void* dones;
+  const uint8_t* time_out; /* null: no bootstrap */
+  const float* value;
+  const float* action;
+  const float* logp;
+  const float* mu;
+  const float* sigma;
+  int64_t ld_value, ld_action, ld_logp, ld_mu, ld_sigma;
+  float* out_reward;
+  uint8_t* out_dones;
+  float* out_action;
+  float* out_value;
+  float* out_logp;
+  float* out_mu;
+  float* out_sigma;
+} gr_transition_args;
+int gr_store_transition(const gr_transition_args* args, void* stream);
+int gr_episode_accumulate(int64_t n, const float* reward, const void* dones, int32_t dones_bytes, float* cur_rew,
+                          float* cur_len, float* fin_rew, float* fin_len, uint8_t* fin_done, void* stream);
+int gr_gae(int64_t n, int32_t t_steps, float gamma, float lam, const float* rewards, const uint8_t* dones,
+           const float* values, const float* last_values, int64_t ld_last, float* returns, float* advantages,
+           void* stream);
+
 /* In-library HIP-event timing of the fused step kernel alone (not the log
  * finalize): when enabled, gr_step brackets the env kernel with a pair of
  * events on the caller's stream (ring of 4096 pairs; do not capture into a
