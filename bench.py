@@ -601,6 +601,10 @@ def main():
         progress("terrain_regeneration")
         extra["train_total_fps_4096_envs"] = train_fps(device)
         extra["train_total_fps_4096_envs_graph_update"] = train_fps(device, graph_update=True)
+        # C2 with the fp32 fused rollout inference (the reference's precision) and the graphed update
+        extra["train_total_fps_4096_envs_fused_fp32_graph_update"] = train_fps(device, fused=True,
+                                                                                 fused_precision="fp32",
+                                                                                 graph_update=True)
         extra["train_total_fps_65536_envs"] = {
             "fp32": train_fps(device, n),
             "fp32_fused_fp32_rollout": train_fps(device, n, fused=True, fused_precision="fp32"),

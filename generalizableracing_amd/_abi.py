@@ -231,6 +231,7 @@ EXPORTS = [
     "gr_mlp_in_backward", "gr_ppo_loss_partials", "gr_ppo_loss_forward", "gr_ppo_loss_backward",
     "gr_adam_prepare", "gr_adam_clip", "gr_adam_step",
     "gr_store_transition", "gr_episode_accumulate", "gr_gae",
+    "gr_ppo_loss_forward_loss", "gr_ppo_loss_backward_loss", "gr_adaptive_lr",
     "gr_bn_scratch_doubles", "gr_bn_act_forward", "gr_bn_act_backward", "gr_stem1_scratch_doubles",
     "gr_stem1_forward", "gr_stem1_backward",
 ]
@@ -286,6 +287,9 @@ def _declare(lib):
         "gr_ppo_loss_partials": (C.c_int64, [C.c_int64]),
         "gr_adam_prepare": (C.c_int, [vp, C.c_int32, vp]),
         "gr_store_transition": (C.c_int, [vp, vp]),
+        "gr_ppo_loss_forward_loss": (C.c_int, [vp, vp, vp, C.c_float, vp, vp, vp, vp, vp]),
+        "gr_ppo_loss_backward_loss": (C.c_int, [vp, vp, C.c_float, vp, vp, vp, vp, vp]),
+        "gr_adaptive_lr": (C.c_int, [vp, vp, C.c_double, C.c_double, C.c_double, vp]),
         "gr_episode_accumulate": (C.c_int, [C.c_int64, vp, vp, C.c_int32, vp, vp, vp, vp, vp, vp]),
         "gr_gae": (C.c_int, [C.c_int64, C.c_int32, C.c_float, C.c_float, vp, vp, vp, vp, C.c_int64, vp, vp, vp]),
         "gr_adam_clip": (C.c_int, [vp, C.c_float, vp, vp]),

@@ -944,7 +944,30 @@ int gr_ppo_loss_forward(const gr_ppo_loss_args* a, float* partial, float* sums, 
 int gr_ppo_loss_backward(const gr_ppo_loss_args* a, const float* g, float* dmu, float* dvalue, float* partial,
                          float* dstd, void* stream) {
   if (!loss_args_ok(a) || !g || !dmu || !dvalue || !partial || !dstd) return GR_ERR_ARG;
-  const hipError_t e = gr::launch_ppo_loss_backward(*a, g, dmu, dvalue, partial, dstd, (hipStream_t)stream);
+  const hipError_t e = gr::launch_ppo_loss_backward(*a, g, 1, 1.0f, dmu, dvalue, partial, dstd, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
+int gr_ppo_loss_forward_loss(const gr_ppo_loss_args* a, float* partial, float* sums, float value_coef, float* loss,
+                             float* stats, float* acc, float* kl_out, void* stream) {
+  if (!loss_args_ok(a) || !partial || !sums || !loss || !stats) return GR_ERR_ARG;
+  const hipError_t e = gr::launch_ppo_loss_forward_loss(*a, partial, sums, value_coef, loss, stats, acc, kl_out,
+                                                        (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
+int gr_ppo_loss_backward_loss(const gr_ppo_loss_args* a, const float* g_loss, float value_coef, float* dmu,
+                              float* dvalue, float* partial, float* dstd, void* stream) {
+  if (!loss_args_ok(a) || !g_loss || !dmu || !dvalue || !partial || !dstd) return GR_ERR_ARG;
+  const hipError_t e = gr::launch_ppo_loss_backward(*a, g_loss, 0, value_coef, dmu, dvalue, partial, dstd,
+                                                    (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
+int gr_adaptive_lr(const float* kl, float* lr, double desired_kl, double lr_min, double lr_max, void* stream) {
+  if (!kl || !lr || !(desired_kl > 0.0) || !(lr_min > 0.0) || !(lr_max >= lr_min)) return GR_ERR_ARG;
+  const hipError_t e = gr::launch_adaptive_lr(kl, lr, (float)(desired_kl * 2.0), (float)(desired_kl / 2.0),
+                                              (float)lr_min, (float)lr_max, (hipStream_t)stream);
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 

@@ -138,8 +138,12 @@ hipError_t launch_gae(long long n, int t_steps, float gamma, float lam, const fl
                       float* advantages, hipStream_t s);
 int ppo_loss_blocks(long long rows);
 hipError_t launch_ppo_loss_forward(const gr_ppo_loss_args& a, float* part, float* sums, hipStream_t s);
-hipError_t launch_ppo_loss_backward(const gr_ppo_loss_args& a, const float* g, float* dmu, float* dvalue, float* part,
-                                    float* dstd, hipStream_t s);
+hipError_t launch_ppo_loss_forward_loss(const gr_ppo_loss_args& a, float* part, float* sums, float value_coef,
+                                        float* loss, float* stats, float* acc, float* kl_out, hipStream_t s);
+hipError_t launch_ppo_loss_backward(const gr_ppo_loss_args& a, const float* g, int gv_index, float gv_coef, float* dmu,
+                                    float* dvalue, float* part, float* dstd, hipStream_t s);
+hipError_t launch_adaptive_lr(const float* kl, float* lr, float hi, float lo, float lr_min, float lr_max,
+                              hipStream_t s);
 hipError_t launch_in_backward(const float* gh, const float* hv, const float* x, long long m, int d, int ldx, int h,
                               float slope, float* part, float* sums, hipStream_t s);
 // obstacle slots per camera wave (the first GR_CAM_OBST_SLOTS obstacles in view; any further ones

@@ -128,10 +128,16 @@ __device__ __forceinline__ float hd_act(float z, float slope) { return z > 0.0f 
 __device__ __forceinline__ float hd_der(float z, float slope) { return z > 0.0f ? 1.0f : slope; }
 __device__ __forceinline__ hd_v4 hd_ld(const float* p) { return __builtin_nontemporal_load(reinterpret_cast<const hd_v4*>(p)); }
 
-// rows per wave for the backward kernels: enough waves to fill the chip, few enough partial rows
+// rows per wave for the backward kernels: enough waves to fill the chip, few enough partial rows.  256 rows per
+// wave, at most 4096 waves (partial rows); a batch that gives fewer than 1024 waves that way (e.g. 24 576 rows, config
+// C2's mini-batch: 96 waves, each a serial 256-row chain of ~100 us) is spread over up to 1024 waves of >= 16 rows
 __host__ __device__ inline long long hd_rows_per_wave(long long m) {
-  const long long waves = (m + 255) / 256;  // 256 rows per wave ...
-  const long long w = waves < 1 ? 1 : (waves > 4096 ? 4096 : waves);  // ... at most 4096 waves (partial rows)
+  long long w = (m + 255) / 256;
+  if (w < 1024) {
+    const long long w16 = (m + 15) / 16;
+    w = w16 < 1024 ? w16 : 1024;
+  }
+  w = w < 1 ? 1 : (w > 4096 ? 4096 : w);
   return (m + w - 1) / w;
 }
 int head_partial_rows(long long m) {
@@ -378,8 +384,8 @@ __global__ __launch_bounds__(HD_WAVES * 64) void in_backward(const float* __rest
 
 // out[n] = sum over the `rows` partial rows [rows][n], in row order per 16-wave slice: 64 outputs per workgroup,
 // its 16 waves take every 16th partial row (four loads in flight per lane), combined in LDS in wave order
-__global__ __launch_bounds__(CF_WAVES * 64) void partials_final(const float* __restrict__ part, int rows, int n,
-                                                                int ld, float* __restrict__ out) {
+__device__ __forceinline__ void partials_final_body(const float* __restrict__ part, int rows, int n, int ld,
+                                                    float* __restrict__ out) {
   __shared__ float sm[CF_WAVES * 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + lane;
@@ -401,6 +407,11 @@ __global__ __launch_bounds__(CF_WAVES * 64) void partials_final(const float* __r
     for (int k = 0; k < CF_WAVES; ++k) s += sm[k * 64 + lane];
     out[i] = s;
   }
+}
+
+__global__ __launch_bounds__(CF_WAVES * 64) void partials_final(const float* __restrict__ part, int rows, int n,
+                                                                int ld, float* __restrict__ out) {
+  partials_final_body(part, rows, n, ld, out);
 }
 
 #define HD_DISPATCH_K(KK, F)          \
@@ -556,9 +567,11 @@ __global__ __launch_bounds__(256) void ppo_loss_forward(gr_ppo_loss_args a, floa
 
 // g[0], g[1]: the upstream gradients of the surrogate and value losses (device scalars; the means' 1 / rows is
 // applied here)
+// (gr_ppo_loss_backward_loss: g[0] is the upstream gradient of the combined loss surrogate + value_coef * value,
+// gv_index 0 and gv_coef value_coef: torch's MulBackward gives the value mean g * value_coef)
 __global__ __launch_bounds__(256) void ppo_loss_backward(gr_ppo_loss_args a, const float* __restrict__ g,
-                                                         float* __restrict__ dmu, float* __restrict__ dvalue,
-                                                         float* __restrict__ part) {
+                                                         int gv_index, float gv_coef, float* __restrict__ dmu,
+                                                         float* __restrict__ dvalue, float* __restrict__ part) {
   __shared__ float sm[4][8];
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   float sd[8];
@@ -569,7 +582,7 @@ __global__ __launch_bounds__(256) void ppo_loss_backward(gr_ppo_loss_args a, con
     LossRow r;
     pl_row(a, i, sd, r, nullptr);
     const float inv_m = 1.0f / (float)a.rows;
-    const float gs = g[0] * inv_m, gv = g[1] * inv_m;
+    const float gs = g[0] * inv_m, gv = (gv_coef * g[gv_index]) * inv_m;
     const float A = a.adv[i * a.ld_adv];
     const float w1 = r.s1 > r.s2 ? 1.0f : (r.s1 == r.s2 ? 0.5f : 0.0f), w2 = 1.0f - w1;
     const float inclip = (r.ratio >= 1.0f - a.clip && r.ratio <= 1.0f + a.clip) ? 1.0f : 0.0f;
@@ -611,11 +624,64 @@ hipError_t launch_ppo_loss_forward(const gr_ppo_loss_args& a, float* part, float
   return hipGetLastError();
 }
 
-hipError_t launch_ppo_loss_backward(const gr_ppo_loss_args& a, const float* g, float* dmu, float* dvalue, float* part,
-                                    float* dstd, hipStream_t s) {
+// the forward's sums in partials_final's order, then the means and the combined loss (torch: sums / rows, then
+// surrogate + value_coef * value); acc[0..1] += (surrogate, value) and kl_out[0] = kl when given
+__global__ __launch_bounds__(CF_WAVES * 64) void ppo_loss_final(const float* __restrict__ part, int rows,
+                                                                float* __restrict__ sums, long long m, float value_coef,
+                                                                float* __restrict__ loss, float* __restrict__ stats,
+                                                                float* __restrict__ acc, float* __restrict__ kl_out) {
+  partials_final_body(part, rows, 3, 4, sums);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_block();
+    const float inv_m = 1.0f / (float)m;  // (torch's tensor / CPU scalar multiplies by the reciprocal)
+    const float surr = sums[0] * inv_m, val = sums[1] * inv_m, kl = sums[2] * inv_m;
+    loss[0] = surr + value_coef * val;
+    stats[0] = surr;
+    stats[1] = val;
+    stats[2] = kl;
+    if (acc) {
+      acc[0] = acc[0] + surr;
+      acc[1] = acc[1] + val;
+    }
+    if (kl_out) kl_out[0] = kl;
+  }
+}
+
+hipError_t launch_ppo_loss_forward_loss(const gr_ppo_loss_args& a, float* part, float* sums, float value_coef,
+                                        float* loss, float* stats, float* acc, float* kl_out, hipStream_t s) {
   const int blocks = ppo_loss_blocks(a.rows);
-  hipLaunchKernelGGL(ppo_loss_backward, dim3(blocks), dim3(256), 0, s, a, g, dmu, dvalue, part);
+  hipLaunchKernelGGL(ppo_loss_forward, dim3(blocks), dim3(256), 0, s, a, part);
+  hipLaunchKernelGGL(ppo_loss_final, dim3(1), dim3(CF_WAVES * 64), 0, s, part, blocks, sums, (long long)a.rows,
+                     value_coef, loss, stats, acc, kl_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_ppo_loss_backward(const gr_ppo_loss_args& a, const float* g, int gv_index, float gv_coef, float* dmu,
+                                    float* dvalue, float* part, float* dstd, hipStream_t s) {
+  const int blocks = ppo_loss_blocks(a.rows);
+  hipLaunchKernelGGL(ppo_loss_backward, dim3(blocks), dim3(256), 0, s, a, g, gv_index, gv_coef, dmu, dvalue, part);
   hipLaunchKernelGGL(partials_final, dim3(1), dim3(CF_WAVES * 64), 0, s, part, blocks, a.k, 8, dstd);
+  return hipGetLastError();
+}
+
+// the graph-captured update's adaptive learning-rate rule (ppo.py:133-150 on the device, ppo.py _GraphedStep):
+// kl > 2 desired: lr / 1.5 clamped below at lr_min; desired / 2 > kl > 0: lr * 1.5 clamped above at lr_max; in the
+// fp32 ops of the torch expression it replaces (the thresholds are the Python doubles rounded to fp32)
+__global__ void adaptive_lr(const float* __restrict__ kl, float* __restrict__ lr, float hi, float lo, float lr_min,
+                            float lr_max) {
+  if (threadIdx.x != 0) return;
+  const float k = kl[0], r = lr[0];
+  float up = r * 1.5f;
+  up = up > lr_max ? lr_max : up;
+  float down = r / 1.5f;
+  down = down < lr_min ? lr_min : down;
+  lr[0] = k > hi ? down : ((lo > k && k > 0.0f) ? up : r);
+}
+
+hipError_t launch_adaptive_lr(const float* kl, float* lr, float hi, float lo, float lr_min, float lr_max,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(adaptive_lr, dim3(1), dim3(64), 0, s, kl, lr, hi, lo, lr_min, lr_max);
   return hipGetLastError();
 }
 

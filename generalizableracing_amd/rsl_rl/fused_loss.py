@@ -91,6 +91,77 @@ class _PPOLossFn(torch.autograd.Function):
         return (dmu, dstd, dvalue.view(value.shape), None, None, None, None, None, None, None, None, None)
 
 
+class _PPOLossCombinedFn(torch.autograd.Function):
+    """The combined loss surrogate + value_coef * value (ppo.py:171-172) and its gradient, finished on the device
+    (gr_ppo_loss_forward_loss / gr_ppo_loss_backward_loss): no torch glue between the losses and autograd (the
+    means' division, the clones, the coefficient's multiply and add, the gradient stack).  Outputs: the loss and
+    the non-differentiable [surrogate, value, KL] means; `acc` [2] (optional) accumulates the surrogate and value
+    means, `kl_out` [1] (optional) receives the KL mean."""
+
+    @staticmethod
+    def forward(ctx, mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old, clip, clipped_value,
+                value_coef, acc, kl_out):
+        from .. import _abi
+
+        std = std.contiguous()
+        a = _args(mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old, clip, clipped_value)
+        rows = mu.shape[0]
+        dev = mu.device
+        part = torch.empty(_abi.load().gr_ppo_loss_partials(rows), device=dev, dtype=torch.float32)
+        sums = torch.empty(3, device=dev, dtype=torch.float32)
+        loss = torch.empty((), device=dev, dtype=torch.float32)
+        stats = torch.empty(3, device=dev, dtype=torch.float32)
+        _call("gr_ppo_loss_forward_loss", C.addressof(a), part.data_ptr(), sums.data_ptr(), C.c_float(value_coef),
+              loss.data_ptr(), stats.data_ptr(), acc.data_ptr() if acc is not None else None,
+              kl_out.data_ptr() if kl_out is not None else None, torch.cuda.current_stream(dev).cuda_stream)
+        ctx.save_for_backward(mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old)
+        ctx.clip, ctx.clipped_value, ctx.value_coef = clip, clipped_value, float(value_coef)
+        ctx.mark_non_differentiable(stats)
+        ctx.set_materialize_grads(False)  # (no zero gradient filled in for the stats)
+        return loss, stats
+
+    @staticmethod
+    def backward(ctx, g_loss, g_stats):
+        from .. import _abi
+
+        if g_loss is None:
+            return (None,) * 15
+        mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old = ctx.saved_tensors
+        a = _args(mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old, ctx.clip, ctx.clipped_value)
+        rows, k = mu.shape
+        dev = mu.device
+        g = g_loss.float().contiguous()
+        dmu = torch.empty(rows, k, device=dev, dtype=torch.float32)
+        dvalue = torch.empty(rows, device=dev, dtype=torch.float32)
+        part = torch.empty(_abi.load().gr_ppo_loss_partials(rows), device=dev, dtype=torch.float32)
+        dstd = torch.empty(k, device=dev, dtype=torch.float32)
+        _call("gr_ppo_loss_backward_loss", C.addressof(a), g.data_ptr(), C.c_float(ctx.value_coef), dmu.data_ptr(),
+              dvalue.data_ptr(), part.data_ptr(), dstd.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+        return (dmu, dstd, dvalue.view(value.shape)) + (None,) * 12
+
+
+def _policy_std(pol):
+    """The policy's action std [k] as a differentiable function of its parameter (ActorCritic._std without the
+    expand over the batch, whose backward would be a reduction)."""
+    return pol.std if pol.noise_std_type == "scalar" else torch.exp(pol.log_std)
+
+
+def ppo_loss(alg, obs, critic_obs, act, value_old, adv, ret, logp_old, mu_old, sig_old, acc=None, kl_out=None):
+    """(loss, [surrogate, value, KL] means) of one mini-batch: loss = surrogate + value_loss_coef * value
+    (- entropy_coef * entropy) as in ppo.py:171-172, differentiable; the same values as ppo_losses."""
+    pol = alg.policy
+    mu = pol.actor(obs)
+    std = _policy_std(pol)
+    value = pol.critic(critic_obs)
+    loss, stats = _PPOLossCombinedFn.apply(mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old,
+                                           float(alg.clip_param), bool(alg.use_clipped_value_loss),
+                                           float(alg.value_loss_coef), acc, kl_out)
+    if alg.entropy_coef != 0.0:  # Normal.entropy summed over the actions: the same for every sample
+        ent = (0.5 + 0.5 * math.log(2.0 * math.pi) + torch.log(std)).sum()
+        loss = loss - alg.entropy_coef * ent
+    return loss, stats
+
+
 def fused_losses_ok(policy, obs: torch.Tensor) -> bool:
     """rsl_rl's ActorCritic (state-independent std) with <= 8 actions, CUDA fp32 observations, outside autocast."""
     from .actor_critic import ActorCritic

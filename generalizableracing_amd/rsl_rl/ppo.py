@@ -9,6 +9,8 @@ applies the identical update.
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import torch
 import torch.nn as nn
 import torch.optim as optim
@@ -218,13 +220,11 @@ class PPO:
         for (obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch, returns_batch,
              old_actions_log_prob_batch, old_mu_batch, old_sigma_batch, hid_states_batch, masks_batch) in generator:
             if self._use_fused_losses(obs_batch):  # the same losses as one device op each way (fused_loss.py)
-                surrogate_loss, value_loss, ent, kl, _, _ = _floss.ppo_losses(
+                loss, stats = _floss.ppo_loss(
                     self, obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch,
                     returns_batch, old_actions_log_prob_batch, old_mu_batch, old_sigma_batch)
-                self._adapt_learning_rate_kl(kl)
-                loss = surrogate_loss + self.value_loss_coef * value_loss
-                if ent is not None:
-                    loss = loss - self.entropy_coef * ent
+                surrogate_loss, value_loss = stats[0], stats[1]
+                self._adapt_learning_rate_kl(stats[2])
             else:
                 surrogate_loss, value_loss, loss = self._torch_losses(
                     ac, obs_batch, critic_obs_batch, actions_batch, target_values_batch, advantages_batch,
@@ -327,8 +327,8 @@ class _GraphedStep:
         self.idx = torch.zeros(self.mb, dtype=torch.long, device=dev)
         self.cols = st.sample_columns()  # packed sample rows (None: gathered field by field)
         self.pack = st.pack_samples() if self.cols is not None else None  # persistent: the graphs read it
-        self.vloss = torch.zeros((), device=dev)
-        self.sloss = torch.zeros((), device=dev)
+        self.acc = torch.zeros(2, device=dev)  # the update's sums of the surrogate and value means
+        self.one = torch.ones((), device=dev)
         self.segmented = gdist.is_dist() or alg.graph_update_segmented
         self.graph = None  # one rank: the whole step
         self.graph_b = None  # segmented: graph = segment A, graph_b = segment B
@@ -349,15 +349,11 @@ class _GraphedStep:
         alg, pol = self.alg, self.alg.policy
         obs, priv, act, val, adv, ret, logp, mu, sig = self._gather()
         obs, priv = obs.float(), priv.float()
-        if alg._use_fused_losses(obs):  # (fused_loss.py: one device op each way)
-            surrogate_loss, value_loss, ent, kl, _, _ = _floss.ppo_losses(alg, obs, priv, act, val, adv, ret, logp,
-                                                                        mu, sig)
-            if self._adaptive():
-                self.flat.extra[0].copy_(kl)
-            loss = surrogate_loss + alg.value_loss_coef * value_loss
-            if ent is not None:
-                loss = loss - alg.entropy_coef * ent
-            self._backward(loss, value_loss, surrogate_loss)
+        if alg._use_fused_losses(obs):  # (fused_loss.py: one device op each way, the means and the loss finished
+            # there: the step's loss sums accumulate in self.acc, the KL mean lands in the flat buffer's extra slot)
+            loss, _ = _floss.ppo_loss(alg, obs, priv, act, val, adv, ret, logp, mu, sig, acc=self.acc,
+                                      kl_out=self.flat.extra[:1] if self._adaptive() else None)
+            self._backward(loss)
             return
         # the eager loop's policy.act also draws a sample it never uses; torch.normal's check of the std
         # reads back to the host, which a capture forbids, so only the distribution is set here
@@ -375,30 +371,25 @@ class _GraphedStep:
                 self.flat.extra[0].copy_(torch.mean(kl))
         surrogate_loss, value_loss = alg._ppo_losses(logp_b, logp, adv, value_b, val, ret)
         loss = surrogate_loss + alg.value_loss_coef * value_loss - alg.entropy_coef * entropy_b.mean()
-        self._backward(loss, value_loss, surrogate_loss)
+        self.acc.add_(torch.stack([surrogate_loss.detach(), value_loss.detach()]))
+        self._backward(loss)
 
-    def _backward(self, loss, value_loss, surrogate_loss):
+    def _backward(self, loss):
         alg = self.alg
         if not alg._grads_checked:  # (first warm-up step, before any capture)
             grads = torch.autograd.grad(loss, self.params, retain_graph=True, allow_unused=True)
             self.flat = alg._check_all_grads(loss, self.params, grads)
             self.flat.bind()
-        grads = torch.autograd.grad(loss, self.flat.params)
+        # (the seed gradient from a persistent 1: no fill launch in the captured step)
+        grads = torch.autograd.grad(loss, self.flat.params, grad_outputs=self.one)
         torch._foreach_copy_(self.flat.views, list(grads))
-        self.vloss.add_(value_loss.detach())
-        self.sloss.add_(surrogate_loss.detach())
 
     def _seg_b(self):
         alg = self.alg
-        if self._adaptive():
-            with torch.no_grad():
-                k = self.flat.extra[0]  # the rank-averaged KL mean once the flat buffer has been all-reduced
-                lr = self.lr
-                up = torch.clamp(lr * 1.5, max=1e-2)
-                down = torch.clamp(lr / 1.5, min=1e-5)
-                lr_new = torch.where(k > alg.desired_kl * 2.0, down,
-                                     torch.where((alg.desired_kl / 2.0 > k) & (k > 0.0), up, lr))
-                self.lr.copy_(lr_new)
+        if self._adaptive():  # on the rank-averaged KL mean once the flat buffer has been all-reduced: the
+            # comparisons of ppo.py:133-150 on the device, one launch (gr_adaptive_lr)
+            _lin._lib_call("gr_adaptive_lr", self.flat.extra.data_ptr(), self.lr.data_ptr(),
+                           C.c_double(alg.desired_kl), C.c_double(1e-5), C.c_double(1e-2), _lin._stream(self.lr))
         _fadam.clip_grad_norm_(self.opt, self.params, alg.max_grad_norm)
         self.opt.step()
 
@@ -406,7 +397,7 @@ class _GraphedStep:
         # snapshot (parameters, optimizer state, rate), warm up on a side stream, capture, restore
         snap_p = [p.detach().clone() for p in self.params]
         snap_lr = self.lr.clone()
-        snap_v, snap_s = self.vloss.clone(), self.sloss.clone()
+        snap_acc = self.acc.clone()
         self.flat.bind()  # Adam and the clip read the gradients from these views (static addresses)
         snap_o = {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in self.opt.state[p].items()}
                   for p in self.params}
@@ -441,8 +432,7 @@ class _GraphedStep:
                     if torch.is_tensor(v):
                         self.opt.state[p][k].copy_(v)
             self.lr.copy_(snap_lr)
-            self.vloss.copy_(snap_v)
-            self.sloss.copy_(snap_s)
+            self.acc.copy_(snap_acc)
 
     def update(self):
         alg = self.alg
@@ -466,8 +456,7 @@ class _GraphedStep:
                                 v.zero_()
             self._capture()
         self.lr.fill_(float(alg.learning_rate))
-        self.vloss.zero_()
-        self.sloss.zero_()
+        self.acc.zero_()
         for _ in range(alg.num_learning_epochs):
             for i in range(n):
                 self.idx.copy_(perm[i * self.mb:(i + 1) * self.mb])
@@ -478,4 +467,5 @@ class _GraphedStep:
         num_updates = alg.num_learning_epochs * n
         alg.learning_rate = float(self.lr)
         alg.storage.clear()
-        return {"value_function": float(self.vloss) / num_updates, "surrogate": float(self.sloss) / num_updates}
+        sl, vl = self.acc.tolist()
+        return {"value_function": vl / num_updates, "surrogate": sl / num_updates}

@@ -491,6 +491,19 @@ int64_t gr_ppo_loss_partials(int64_t rows);
 int gr_ppo_loss_forward(const gr_ppo_loss_args* args, float* partial, float* sums, void* stream);
 int gr_ppo_loss_backward(const gr_ppo_loss_args* args, const float* g, float* dmu, float* dvalue, float* partial,
                          float* dstd, void* stream);
+/* The same with the means and the combined loss finished on the device (rsl_rl/fused_loss.py; ppo.py:171-172
+ * `loss = surrogate_loss + value_loss_coef * value_loss`): gr_ppo_loss_forward_loss writes sums [3], loss [1] =
+ * sums[0] / rows + value_coef * (sums[1] / rows), stats [3] = the three means; acc [2] (may be null) += (surrogate,
+ * value) means; kl_out [1] (may be null) = the KL mean.  gr_ppo_loss_backward_loss takes the loss's upstream
+ * gradient g_loss [1]: the value mean's is value_coef * g_loss[0], as torch's MulBackward gives it. */
+int gr_ppo_loss_forward_loss(const gr_ppo_loss_args* args, float* partial, float* sums, float value_coef, float* loss,
+                             float* stats, float* acc, float* kl_out, void* stream);
+int gr_ppo_loss_backward_loss(const gr_ppo_loss_args* args, const float* g_loss, float value_coef, float* dmu,
+                              float* dvalue, float* partial, float* dstd, void* stream);
+/* The graph-captured update's adaptive learning-rate rule (ppo.py:133-150, device form): lr[0] = max(lr_min,
+ * lr / 1.5) if kl[0] > 2 desired_kl; min(lr_max, lr * 1.5) if desired_kl / 2 > kl[0] > 0; else unchanged (fp32
+ * arithmetic, the thresholds rounded to fp32 as torch's scalar comparisons do). */
+int gr_adaptive_lr(const float* kl, float* lr, double desired_kl, double lr_min, double lr_max, void* stream);
 
 /* Adam and the gradient-norm clip of the PPO update (standalone/rsl_rl/ext/algorithms/ppo.py:179-181:
  * nn.utils.clip_grad_norm_(max_grad_norm) then torch.optim.Adam.step) over a table of parameter segments

@@ -364,6 +364,48 @@ def test_fused_ppo_losses_match_torch(clipped):
         assert float((a - b).norm()) <= 1e-4 * float(b.norm()) + 1e-9
 
 
+def test_fused_combined_loss_matches_separate():
+    """fused_loss.ppo_loss (the loss finished on the device: gr_ppo_loss_forward_loss / backward_loss) against
+    ppo_losses composed in torch (ppo.py:171-172: surrogate + value_loss_coef * value - entropy_coef * entropy):
+    the loss, the means, the accumulators and every parameter gradient bit-identical (the same fp32 ops)."""
+    from generalizableracing_amd.rsl_rl import ActorCritic
+    from generalizableracing_amd.rsl_rl import fused_loss
+    from generalizableracing_amd.rsl_rl.ppo import PPO
+
+    torch.manual_seed(6)
+    dev = "cuda:0"
+    m = 12288
+    pol = ActorCritic(16, 16, 4, [64, 64], [64, 64], "lrelu", init_noise_std=0.7).to(dev)
+    alg = PPO(pol, device=dev, clip_param=0.2, entropy_coef=0.01, value_loss_coef=0.5)
+    obs, cobs = torch.randn(m, 16, device=dev), torch.randn(m, 16, device=dev)
+    with torch.no_grad():
+        mu0 = pol.actor(obs)
+        act = mu0 + 0.7 * torch.randn_like(mu0)
+        logp_old = torch.distributions.Normal(mu0, 0.7).log_prob(act).sum(-1, keepdim=True) \
+            + torch.randn(m, 1, device=dev) * 0.3
+        val_old = pol.critic(cobs) + torch.randn(m, 1, device=dev) * 0.3
+    adv, ret = torch.randn(m, 1, device=dev), torch.randn(m, 1, device=dev)
+    mu_old = mu0 + 0.05 * torch.randn_like(mu0)
+    sig_old = torch.full_like(mu0, 0.65)
+    args = (obs, cobs, act, val_old, adv, ret, logp_old, mu_old, sig_old)
+    pol.zero_grad()
+    acc = torch.tensor([1.0, 2.0], device=dev)
+    kl_out = torch.zeros(1, device=dev)
+    loss_a, stats = fused_loss.ppo_loss(alg, *args, acc=acc, kl_out=kl_out)
+    loss_a.backward()
+    ga = [p.grad.clone() for p in pol.parameters()]
+    pol.zero_grad()
+    s, v, ent, kl, _, _ = fused_loss.ppo_losses(alg, *args)
+    loss_b = s + alg.value_loss_coef * v - alg.entropy_coef * ent
+    loss_b.backward()
+    gb_ = [p.grad.clone() for p in pol.parameters()]
+    assert torch.equal(loss_a, loss_b)
+    assert torch.equal(stats, torch.stack([s, v, kl]).detach())
+    assert torch.equal(acc, torch.stack([1.0 + s, 2.0 + v]).detach()) and torch.equal(kl_out[0], kl)
+    for a, b in zip(ga, gb_):
+        assert torch.equal(a, b)
+
+
 def _actor_critic_shapes():
     # ActorCritic(16, 16, 4) with [256, 256, 256] hidden layers: weights, biases, std (ppo.py:39's parameters)
     sh = []
