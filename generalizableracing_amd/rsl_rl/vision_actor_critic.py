@@ -193,9 +193,7 @@ class VisionActorCritic(ActorCritic):
         mean = self.actor(self.features(observations))
         self.distribution = torch.distributions.Normal(mean, self._std(mean))
 
-    def act(self, observations, **kwargs):
-        self.update_distribution(observations)
-        return self.distribution.sample()
+    # act: ActorCritic.act (the distribution's draw without torch.normal's per-call host read, the same bits)
 
     def act_inference(self, observations):
         """-> (mean, feature), as the reference (its exporters and PPOL2C2 take [0])."""
