@@ -52,19 +52,28 @@ DEV float4 ld4(const float4* base, size_t idx) {
   return base[idx];
 #endif
 }
-template <typename T4>
+// GR_STATE_STORE_POLICY: the same choice for the state planes and istate alone (the only outputs the next step
+// re-reads, on the same XCD: workgroup b runs on XCD b % 8 in every launch).
+#ifndef GR_STATE_STORE_POLICY
+#define GR_STATE_STORE_POLICY GR_STORE_POLICY
+#endif
+template <int POL = GR_STORE_POLICY, typename T4>
 DEV void st4(T4* base, size_t idx, const T4& v) {
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   const u32x4 w = {__builtin_bit_cast(unsigned, v.x), __builtin_bit_cast(unsigned, v.y),
                    __builtin_bit_cast(unsigned, v.z), __builtin_bit_cast(unsigned, v.w)};
-#if GR_STORE_POLICY == 1
-  __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(base) + idx);
-#elif GR_STORE_POLICY >= 2
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b128(w, r, (int)(idx * 16), 0, GR_STORE_POLICY == 2 ? 16 : 18);
-#else
-  *reinterpret_cast<u32x4*>(base + idx) = w;
-#endif
+  if constexpr (POL == 1) {
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(base) + idx);
+  } else if constexpr (POL >= 2) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(w, r, (int)(idx * 16), 0, POL == 2 ? 16 : 18);
+  } else {
+    *reinterpret_cast<u32x4*>(base + idx) = w;
+  }
+}
+template <typename T4>
+DEV void st4s(T4* base, size_t idx, const T4& v) {  // state planes and istate
+  st4<GR_STATE_STORE_POLICY>(base, idx, v);
 }
 
 // ------------------------------------------------------------- IL math
@@ -193,20 +202,20 @@ DEV void load_env(const KArgs& a, int i, Env& e) {
 DEV void store_kin(const KArgs& a, int i, const Env& e) {
   float4* S = reinterpret_cast<float4*>(a.buf.state);
   const size_t n = (size_t)a.h.num_envs;
-  st4(S, GR_P_POSQ * n + i, make_float4(e.p[0], e.p[1], e.p[2], e.q[0]));
-  st4(S, GR_P_QV * n + i, make_float4(e.q[1], e.q[2], e.q[3], e.v[0]));
-  st4(S, GR_P_VW * n + i, make_float4(e.v[1], e.v[2], e.w[0], e.w[1]));
-  st4(S, GR_P_WA * n + i, make_float4(e.w[2], e.al[0], e.al[1], e.al[2]));
-  st4(S, GR_P_CTRL * n + i, make_float4(e.T, e.tau[0], e.tau[1], e.tau[2]));
-  st4(S, GR_P_LAG * n + i, make_float4(e.lag[0], e.lag[1], e.lag[2], e.lag[3]));
-  if (a.h.use_motor_model) st4(S, GR_P_MOTOR * n + i, make_float4(e.mw[0], e.mw[1], e.mw[2], e.mw[3]));
+  st4s(S, GR_P_POSQ * n + i, make_float4(e.p[0], e.p[1], e.p[2], e.q[0]));
+  st4s(S, GR_P_QV * n + i, make_float4(e.q[1], e.q[2], e.q[3], e.v[0]));
+  st4s(S, GR_P_VW * n + i, make_float4(e.v[1], e.v[2], e.w[0], e.w[1]));
+  st4s(S, GR_P_WA * n + i, make_float4(e.w[2], e.al[0], e.al[1], e.al[2]));
+  st4s(S, GR_P_CTRL * n + i, make_float4(e.T, e.tau[0], e.tau[1], e.tau[2]));
+  st4s(S, GR_P_LAG * n + i, make_float4(e.lag[0], e.lag[1], e.lag[2], e.lag[3]));
+  if (a.h.use_motor_model) st4s(S, GR_P_MOTOR * n + i, make_float4(e.mw[0], e.mw[1], e.mw[2], e.mw[3]));
 }
 // ... and episode sums
 DEV void store_eps(const KArgs& a, int i, const Env& e) {
   float4* S = reinterpret_cast<float4*>(a.buf.state);
   const size_t n = (size_t)a.h.num_envs;
-  st4(S, GR_P_EP0 * n + i, make_float4(e.es[0], e.es[1], e.es[2], e.es[3]));
-  st4(S, GR_P_EP1 * n + i, make_float4(e.es[4], e.es[5], e.es[6], e.mar));
+  st4s(S, GR_P_EP0 * n + i, make_float4(e.es[0], e.es[1], e.es[2], e.es[3]));
+  st4s(S, GR_P_EP1 * n + i, make_float4(e.es[4], e.es[5], e.es[6], e.mar));
 }
 DEV void store_dyn(const KArgs& a, int i, const Env& e) {
   store_kin(a, i, e);
@@ -217,13 +226,13 @@ DEV void store_dyn(const KArgs& a, int i, const Env& e) {
 DEV void store_rst(const KArgs& a, int i, const Env& e) {
   float4* S = reinterpret_cast<float4*>(a.buf.state);
   const size_t n = (size_t)a.h.num_envs;
-  st4(S, GR_P_RST0 * n + i, make_float4(e.thr, e.nl, e.k2[0], e.k2[1]));
-  st4(S, GR_P_RST1 * n + i, make_float4(e.k2[2], e.k1[0], e.k1[1], e.k1[2]));
+  st4s(S, GR_P_RST0 * n + i, make_float4(e.thr, e.nl, e.k2[0], e.k2[1]));
+  st4s(S, GR_P_RST1 * n + i, make_float4(e.k2[2], e.k1[0], e.k1[1], e.k1[2]));
 }
 
 DEV void store_istate(const KArgs& a, int i, const Env& e) {
   int packed = (e.gate & 0xff) | ((e.lvl & 0xff) << 8) | ((e.azero & 1) << 16) | ((e.type & 0xff) << 24);
-  st4(reinterpret_cast<int4*>(a.buf.istate), (size_t)i, make_int4(e.ep, e.acc, e.epoch, packed));
+  st4s(reinterpret_cast<int4*>(a.buf.istate), (size_t)i, make_int4(e.ep, e.acc, e.epoch, packed));
 }
 
 // ------------------------------------------------------------- track table view
@@ -1385,7 +1394,7 @@ __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
       if (a.sink_policy) store_rows_sink(a, a.sink_policy, blockIdx.x * GR_BLOCK + (t & ~63), n, stg + (t & ~63));
       if (live) st1(a.buf.obs_aux + i, aux);
     }
-    if (OBST && live) st4(reinterpret_cast<float4*>(a.buf.state), GR_P_OHINT * (size_t)n + i, next_hint);
+    if (OBST && live) st4s(reinterpret_cast<float4*>(a.buf.state), GR_P_OHINT * (size_t)n + i, next_hint);
     STAMP(8);
     RSTAMP(10);
   } else {

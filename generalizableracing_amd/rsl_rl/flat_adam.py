@@ -159,6 +159,11 @@ class FlatAdam(torch.optim.Optimizer):
         a = self._args()
         if a is not None:
             _call("gr_adam_step", C.addressof(a), self._stream())
+            # the kernel wrote the parameters through raw pointers: bump their version counters as torch's in-place
+            # Adam does, so caches keyed on them (the fused rollout inference's packed weights) see the update
+            for p in self.param_groups[0]["params"]:
+                if p.grad is not None:
+                    torch.autograd.graph.increment_version(p)
         return loss
 
     def load_state_dict(self, state_dict):

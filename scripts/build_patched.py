@@ -2,7 +2,10 @@
 ablation switches).  A patch is a JSON list of [file, old, new] text replacements; every `old` must occur
 exactly once.  Output: variants/<name>/libgr.so (GR_LIB_PATH selects it on the GPU box).
 
-    python scripts/build_patched.py NAME PATCH.json
+    python scripts/build_patched.py NAME PATCH.json [-DMACRO=VALUE ...]
+
+Extra arguments are passed to hipcc (cache-policy macros such as -DGR_STATE_STORE_POLICY=0); PATCH.json may be `-`
+for no text replacements.
 """
 import json
 import os
@@ -14,7 +17,7 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def build(name, patch):
+def build(name, patch, extra_flags=""):
     tmp = tempfile.mkdtemp(prefix="grvar_")
     src = os.path.join(tmp, "generalizableracing_amd", "csrc")
     shutil.copytree(os.path.join(ROOT, "generalizableracing_amd", "csrc"), src)
@@ -28,9 +31,9 @@ def build(name, patch):
     out = os.path.join(ROOT, "variants", name)
     os.makedirs(out, exist_ok=True)
     flags = ("--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt "
-             "-fno-slp-vectorize")
+             "-fno-slp-vectorize " + extra_flags)
     objs = []
-    for f in ("gr_kernels.hip", "gr_camera.hip", "gr_policy.hip", "gr_policy_f32.hip", "gr_bn.hip", "gr_update.hip", "gr_capi.cpp"):
+    for f in ("gr_kernels.hip", "gr_camera.hip", "gr_policy.hip", "gr_policy_f32.hip", "gr_bn.hip", "gr_update.hip", "gr_rollout.hip", "gr_capi.cpp"):
         o = os.path.join(tmp, f + ".o")
         extra = " -fno-honor-nans" if f == "gr_policy.hip" else ""
         lang = " -x hip" if f.endswith(".cpp") else ""
@@ -43,4 +46,4 @@ def build(name, patch):
 
 
 if __name__ == "__main__":
-    build(sys.argv[1], json.load(open(sys.argv[2])))
+    build(sys.argv[1], [] if sys.argv[2] == "-" else json.load(open(sys.argv[2])), " ".join(sys.argv[3:]))

@@ -450,9 +450,13 @@ def test_flat_adam_matches_torch(max_norm):
         torch.testing.assert_close(na, nb, rtol=1e-6, atol=0)
         torch.testing.assert_close([a.grad for a in pa if a.grad is not None],
                                    [b.grad for b in pb if b.grad is not None], rtol=2e-6, atol=1e-12)
+        vers = [a._version for a in pa]
         oa.step()
         ob.step()
         torch.cuda.synchronize()
+        # the stepped parameters' version counters move, as torch's in-place Adam moves them (the fused rollout
+        # inference repacks its weights on a version change); the one without a gradient keeps its version
+        assert [a._version > v for a, v in zip(pa, vers)] == [i != skip for i in range(len(pa))]
         for a, b in zip(pa, pb):
             torch.testing.assert_close(a.detach(), b.detach(), rtol=2e-6, atol=1e-6 * lr)
     assert pa[skip] not in oa.state or not oa.state[pa[skip]]
