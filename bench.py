@@ -410,10 +410,22 @@ def regeneration_cost(device, n, interval=256, plain=64):
     t0 = time.perf_counter()
     env._build_terrain(env._terrain_seed(2))
     t_build = time.perf_counter() - t0
+    # what the event implies besides the new tables (mdp/events.py:180-204 calls env.reset() of every env): a plain
+    # step followed by a full reset and an observation pass, the same way (eager, synchronised)
+    times_sr = []
+    for k in range(8):
+        t0 = time.perf_counter()
+        env.step(acts[k % 8])
+        env.reset()
+        env.observe()
+        torch.cuda.synchronize()
+        times_sr.append(time.perf_counter() - t0)
     env.close()
     plain_us = float(np.median(times)) * 1e6
+    sr_us = float(np.median(times_sr)) * 1e6
     return {"plain_step_wall_us": plain_us, "regenerating_step_wall_us": t_regen * 1e6,
-            "ratio": t_regen * 1e6 / plain_us, "background_build_s": t_build,
+            "ratio": t_regen * 1e6 / plain_us, "step_plus_full_reset_and_observe_wall_us": sr_us,
+            "ratio_to_step_plus_full_reset": t_regen * 1e6 / sr_us, "background_build_s": t_build,
             "host_wait_for_build_s_before_timing": build_wait,
             "note": f"{n} envs, obstacle tracks, eager env.step + synchronize per step; the build runs on a host "
                     "thread from half-way through the interval, its upload on a side stream; the interval step swaps "

@@ -120,19 +120,37 @@ hipError_t launch_column_sum(const void* x, int dtype, long long m, int n, float
 // columns 4 l .. 4 l + 3 (one 1 KB coalesced access per row of 256); four rows' loads are issued together.  Weight /
 // bias gradients: every wave writes its partial sums as one row of `part`, and partials_final adds the rows in a
 // fixed order (deterministic, graph-capturable, no atomics).
-constexpr int HD_WAVES = 4;
-constexpr int HD_U = 4;  // rows in flight per wave
+#ifndef GR_HD_WAVES
+#define GR_HD_WAVES 4
+#endif
+#ifndef GR_HD_U
+#define GR_HD_U 4
+#endif
+#ifndef GR_HD_RPW
+#define GR_HD_RPW 256
+#endif
+constexpr int HD_WAVES = GR_HD_WAVES;  // waves per workgroup
+constexpr int HD_U = GR_HD_U;          // rows in flight per wave
 typedef float hd_v4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float hd_act(float z, float slope) { return z > 0.0f ? z : z * slope; }
 __device__ __forceinline__ float hd_der(float z, float slope) { return z > 0.0f ? 1.0f : slope; }
-__device__ __forceinline__ hd_v4 hd_ld(const float* p) { return __builtin_nontemporal_load(reinterpret_cast<const hd_v4*>(p)); }
+#ifndef GR_HD_NT_LOAD
+#define GR_HD_NT_LOAD 1  // non-temporal loads of the once-read [rows, h] matrices
+#endif
+__device__ __forceinline__ hd_v4 hd_ld(const float* p) {
+#if GR_HD_NT_LOAD
+  return __builtin_nontemporal_load(reinterpret_cast<const hd_v4*>(p));
+#else
+  return *reinterpret_cast<const hd_v4*>(p);
+#endif
+}
 
 // rows per wave for the backward kernels: enough waves to fill the chip, few enough partial rows.  256 rows per
 // wave, at most 4096 waves (partial rows); a batch that gives fewer than 1024 waves that way (e.g. 24 576 rows, config
 // C2's mini-batch: 96 waves, each a serial 256-row chain of ~100 us) is spread over up to 1024 waves of >= 16 rows
 __host__ __device__ inline long long hd_rows_per_wave(long long m) {
-  long long w = (m + 255) / 256;
+  long long w = (m + GR_HD_RPW - 1) / GR_HD_RPW;
   if (w < 1024) {
     const long long w16 = (m + 15) / 16;
     w = w16 < 1024 ? w16 : 1024;
