@@ -836,7 +836,7 @@ static bool in_args_ok(const float* x, int64_t rows, int32_t d, int32_t ldx, int
 
 int64_t gr_mlp_in_partials(int64_t rows, int32_t d, int32_t h) {
   if (rows < 0 || d < 4 || d > 32 || d % 4 || h < 4 || h > 256 || h % 4) return GR_ERR_ARG;
-  return (int64_t)gr::head_partial_rows(rows) * (h * d + h);
+  return (int64_t)gr::in_partial_rows(rows) * (h * d + h);
 }
 
 int gr_mlp_in_forward(const float* x, int64_t rows, int32_t d, int32_t ldx, const float* w, const float* b, int32_t h,

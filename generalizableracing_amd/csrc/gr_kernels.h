@@ -121,6 +121,7 @@ hipError_t launch_bn_backward(const float* x, const float* gy, long long m, int 
 int column_sum_blocks(long long m);                                                                       // gr_update.hip
 hipError_t launch_column_sum(const void* x, int dtype, long long m, int n, float* part, float* out, hipStream_t s);
 int head_partial_rows(long long m);                                                                      // gr_update.hip
+int in_partial_rows(long long m);                                                                        // gr_update.hip
 hipError_t launch_head_forward(const float* z, long long m, int h, const float* w, const float* b, int k, float slope,
                                float* y, hipStream_t s);
 hipError_t launch_head_backward(const float* z, const float* gy, long long m, int h, const float* w, int k,

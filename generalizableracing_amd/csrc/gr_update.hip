@@ -117,7 +117,9 @@ hipError_t launch_column_sum(const void* x, int dtype, long long m, int n, float
 //   head_forward: y = lrelu(z2) W3^T + b3                          (reads z2; no activation pass, no GEMM)
 //   head_backward: gz2 = (gy W3) * lrelu'(z2); gW3 = gy^T lrelu(z2), gb3 = sum gy, gb2 = sum gz2
 // (lrelu'(h) = lrelu'(z): a LeakyReLU keeps the sign, and maps 0 to 0.)  A wave owns a row at a time, lane l
-// columns 4 l .. 4 l + 3 (one 1 KB coalesced access per row of 256); four rows' loads are issued together.  Weight /
+// columns 4 l .. 4 l + 3 (one 1 KB coalesced access per row of 256); four rows' loads are issued together.  Dot
+// products are fmaf chains (these ops are held to float64 at 1e-6 of scale, not to bits; with separate multiply and
+// add the first layer's 16-term dots were VALU-bound).  Weight /
 // bias gradients: every wave writes its partial sums as one row of `part`, and partials_final adds the rows in a
 // fixed order (deterministic, graph-capturable, no atomics).
 #ifndef GR_HD_WAVES
@@ -127,7 +129,10 @@ hipError_t launch_column_sum(const void* x, int dtype, long long m, int n, float
 #define GR_HD_U 4
 #endif
 #ifndef GR_HD_RPW
-#define GR_HD_RPW 256
+#define GR_HD_RPW 256  // head_backward rows per wave (128: +7 % at 393 216 rows, scripts/time_update_kernels.py)
+#endif
+#ifndef GR_IN_RPW
+#define GR_IN_RPW 128  // in_backward rows per wave (256: +13 %)
 #endif
 constexpr int HD_WAVES = GR_HD_WAVES;  // waves per workgroup
 constexpr int HD_U = GR_HD_U;          // rows in flight per wave
@@ -138,6 +143,16 @@ __device__ __forceinline__ float hd_der(float z, float slope) { return z > 0.0f 
 #ifndef GR_HD_NT_LOAD
 #define GR_HD_NT_LOAD 1  // non-temporal loads of the once-read [rows, h] matrices
 #endif
+#ifndef GR_HD_NT_STORE
+#define GR_HD_NT_STORE 1  // non-temporal stores of the [rows, h] outputs (h1, gz2)
+#endif
+__device__ __forceinline__ void hd_st(float* p, const hd_v4& v) {
+#if GR_HD_NT_STORE
+  __builtin_nontemporal_store(v, reinterpret_cast<hd_v4*>(p));
+#else
+  *reinterpret_cast<hd_v4*>(p) = v;
+#endif
+}
 __device__ __forceinline__ hd_v4 hd_ld(const float* p) {
 #if GR_HD_NT_LOAD
   return __builtin_nontemporal_load(reinterpret_cast<const hd_v4*>(p));
@@ -149,8 +164,8 @@ __device__ __forceinline__ hd_v4 hd_ld(const float* p) {
 // rows per wave for the backward kernels: enough waves to fill the chip, few enough partial rows.  256 rows per
 // wave, at most 4096 waves (partial rows); a batch that gives fewer than 1024 waves that way (e.g. 24 576 rows, config
 // C2's mini-batch: 96 waves, each a serial 256-row chain of ~100 us) is spread over up to 1024 waves of >= 16 rows
-__host__ __device__ inline long long hd_rows_per_wave(long long m) {
-  long long w = (m + GR_HD_RPW - 1) / GR_HD_RPW;
+__host__ __device__ inline long long hd_rows_per_wave(long long m, long long target = GR_HD_RPW) {
+  long long w = (m + target - 1) / target;
   if (w < 1024) {
     const long long w16 = (m + 15) / 16;
     w = w16 < 1024 ? w16 : 1024;
@@ -160,6 +175,10 @@ __host__ __device__ inline long long hd_rows_per_wave(long long m) {
 }
 int head_partial_rows(long long m) {
   const long long rpw = hd_rows_per_wave(m);
+  return (int)((m + rpw - 1) / rpw);
+}
+int in_partial_rows(long long m) {
+  const long long rpw = hd_rows_per_wave(m, GR_IN_RPW);
   return (int)((m + rpw - 1) / rpw);
 }
 
@@ -196,8 +215,12 @@ __global__ __launch_bounds__(HD_WAVES * 64) void head_forward(const float* __res
         if (c < h) zz = hd_ld(z + r * h + c);
         const float a[4] = {hd_act(zz.x, slope), hd_act(zz.y, slope), hd_act(zz.z, slope), hd_act(zz.w, slope)};
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-          acc[k] += ((a[0] * wr[k][4 * j] + a[1] * wr[k][4 * j + 1]) + a[2] * wr[k][4 * j + 2]) + a[3] * wr[k][4 * j + 3];
+        for (int k = 0; k < K; ++k) {
+          float t = __builtin_fmaf(a[0], wr[k][4 * j], acc[k]);
+          t = __builtin_fmaf(a[1], wr[k][4 * j + 1], t);
+          t = __builtin_fmaf(a[2], wr[k][4 * j + 2], t);
+          acc[k] = __builtin_fmaf(a[3], wr[k][4 * j + 3], t);
+        }
       }
     }
 #pragma unroll
@@ -260,18 +283,17 @@ __global__ __launch_bounds__(HD_WAVES * 64) void head_backward(const float* __re
       for (int j = 0; j < 4; ++j) {
         float gh = g[u][0] * wr[0][j];
 #pragma unroll
-        for (int k = 1; k < K; ++k) gh += g[u][k] * wr[k][j];
+        for (int k = 1; k < K; ++k) gh = __builtin_fmaf(g[u][k], wr[k][j], gh);
         o[j] = gh * hd_der(zv[j], slope);
         gs[j] += o[j];
         const float a = hd_act(zv[j], slope);
 #pragma unroll
-        for (int k = 0; k < K; ++k) gw[k][j] += g[u][k] * a;
+        for (int k = 0; k < K; ++k) gw[k][j] = __builtin_fmaf(g[u][k], a, gw[k][j]);
       }
 #pragma unroll
       for (int k = 0; k < K; ++k) gb[k] += g[u][k];
       if (on && r < r1) {
-        const hd_v4 ov = {o[0], o[1], o[2], o[3]};
-        __builtin_nontemporal_store(ov, reinterpret_cast<hd_v4*>(gz + r * h + c));
+        hd_st(gz + r * h + c, hd_v4{o[0], o[1], o[2], o[3]});
       }
     }
   }
@@ -326,12 +348,11 @@ __global__ __launch_bounds__(HD_WAVES * 64) void in_forward(const float* __restr
       for (int j = 0; j < 4; ++j) {
         float acc = xr[u][0] * wr[j][0];
 #pragma unroll
-        for (int k = 1; k < D; ++k) acc += xr[u][k] * wr[j][k];
+        for (int k = 1; k < D; ++k) acc = __builtin_fmaf(xr[u][k], wr[j][k], acc);
         o[j] = hd_act(acc + br[j], slope);
       }
       if (on && r < m) {
-        const hd_v4 ov = {o[0], o[1], o[2], o[3]};
-        __builtin_nontemporal_store(ov, reinterpret_cast<hd_v4*>(y + r * h + c));
+        hd_st(y + r * h + c, hd_v4{o[0], o[1], o[2], o[3]});
       }
     }
   }
@@ -384,7 +405,7 @@ __global__ __launch_bounds__(HD_WAVES * 64) void in_backward(const float* __rest
       for (int j = 0; j < 4; ++j) {
         gb[j] += gz[j];
 #pragma unroll
-        for (int k = 0; k < D; ++k) gw[j][k] += gz[j] * xr[u][k];
+        for (int k = 0; k < D; ++k) gw[j][k] = __builtin_fmaf(gz[j], xr[u][k], gw[j][k]);
       }
     }
   }
@@ -498,8 +519,8 @@ hipError_t launch_in_forward(const float* x, long long m, int d, int ldx, const 
 
 hipError_t launch_in_backward(const float* gh, const float* hv, const float* x, long long m, int d, int ldx, int h,
                               float slope, float* part, float* sums, hipStream_t s) {
-  const long long rpw = hd_rows_per_wave(m);
-  const int prow = head_partial_rows(m);
+  const long long rpw = hd_rows_per_wave(m, GR_IN_RPW);
+  const int prow = in_partial_rows(m);
   const int blocks = hd_grid(prow);
 #define IN_BWD(DD) \
   hipLaunchKernelGGL(in_backward<DD>, dim3(blocks), dim3(HD_WAVES * 64), 0, s, gh, hv, x, m, ldx, h, slope, rpw, part)
