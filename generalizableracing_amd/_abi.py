@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgr.so")
 
 # ---- constants (include/gr.h) ----
-GR_ABI_VERSION = 2
+GR_ABI_VERSION = 3
 GR_INTEGRATOR_DD_EXPLICIT = 0
 GR_INTEGRATOR_SEMI_IMPLICIT = 1
 
@@ -306,9 +306,9 @@ def _declare(lib):
                                          vp, vp]),
         "gr_stem1_scratch_doubles": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
         "gr_stem1_forward": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int32, vp, C.c_int32, C.c_int32, vp, C.c_int32,
-                                       vp, vp, C.c_float, C.c_int32, C.c_float, vp, vp, vp, vp]),
+                                       vp, vp, C.c_float, C.c_int32, C.c_float, vp, C.c_int64, vp, vp, vp]),
         "gr_stem1_backward": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int32, vp, C.c_int32, C.c_int32, vp, C.c_int32,
-                                        vp, vp, vp, C.c_int32, C.c_float, vp, vp, vp, vp, vp, vp]),
+                                        vp, vp, vp, C.c_int32, C.c_float, vp, C.c_int64, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name) and os.environ.get("GR_LIB_PATH"):

@@ -341,7 +341,7 @@ __global__ __launch_bounds__(BN_THREADS) void stem1_apply(Stem1 s, const float* 
     o.y = bn_act<ACT>((x[1] - mu.y) * is.y * wv.y + bv.y, slope);
     o.z = bn_act<ACT>((x[2] - mu.z) * is.z * wv.z + bv.z, slope);
     o.w = bn_act<ACT>((x[3] - mu.w) * is.w * wv.w + bv.w, slope);
-    reinterpret_cast<float4*>(y)[(size_t)r * c4 + g] = o;
+    if (r < s.rows_out) reinterpret_cast<float4*>(y)[(size_t)r * c4 + g] = o;
   }
 }
 
@@ -363,7 +363,7 @@ __global__ __launch_bounds__(BN_THREADS) void stem1_bwd_partial(Stem1 s, const f
   for (unsigned r = (blockIdx.x * BN_THREADS + threadIdx.x) / c4; r < m; r += step) {
     stem_pixels(s, tab, r, px);
     stem_conv(w, px, x);
-    const float4 dy = ld4f(gy, (long long)r * c4 + g);
+    const float4 dy = r < s.rows_out ? ld4f(gy, (long long)r * c4 + g) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float xh = (x[j] - comp(mu, j)) * comp(is, j);
@@ -400,7 +400,7 @@ __global__ __launch_bounds__(BN_THREADS) void stem1_bwd_wgrad(Stem1 s, const flo
   for (unsigned r = (blockIdx.x * BN_THREADS + threadIdx.x) / c4; r < m; r += step) {
     stem_pixels(s, tab, r, px);
     stem_conv(w, px, x);
-    const float4 dy = ld4f(gy, (long long)r * c4 + g);
+    const float4 dy = r < s.rows_out ? ld4f(gy, (long long)r * c4 + g) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float xh = (x[j] - comp(mu, j)) * comp(is, j);

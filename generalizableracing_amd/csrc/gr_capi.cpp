@@ -758,11 +758,14 @@ static bool stem1_args_ok(const float* obs, int32_t nimg, const int16_t* pix, in
          (int64_t)nimg * (na + nb) < (int64_t)1 << 31 && bn_shape_ok(1, c) && aligned16(bn_w) && aligned16(bn_b);
 }
 static gr::Stem1 stem1_of(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
-                          int32_t nb, const float* conv_w, int32_t c) {
+                          int32_t nb, const float* conv_w, int32_t c, int64_t rows_out) {
   gr::Stem1 s;
   s.obs = obs; s.ld = ld; s.off = off; s.nimg = nimg; s.na = na; s.nbt = nb;
-  s.pix = reinterpret_cast<const short*>(pix); s.w = conv_w; s.c = c;
+  s.pix = reinterpret_cast<const short*>(pix); s.w = conv_w; s.c = c; s.rows_out = rows_out;
   return s;
+}
+static bool stem1_rows_ok(int32_t nimg, int32_t na, int32_t nb, int64_t rows_out) {
+  return rows_out >= 1 && rows_out <= (int64_t)nimg * (na + nb);
 }
 
 int64_t gr_stem1_scratch_doubles(int32_t nimg, int32_t rows_per_img, int32_t c) {
@@ -772,23 +775,25 @@ int64_t gr_stem1_scratch_doubles(int32_t nimg, int32_t rows_per_img, int32_t c) 
 
 int gr_stem1_forward(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
                      int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b, float eps,
-                     int32_t act, float slope, float* y, float* stats, double* part, void* stream) {
+                     int32_t act, float slope, float* y, int64_t y_rows, float* stats, double* part, void* stream) {
   if (!stem1_args_ok(obs, nimg, pix, na, nb, conv_w, c, bn_w, bn_b) || !y || !stats || !part || !aligned16(y) ||
-      !aligned16(stats) || (act != GR_POLICY_ACT_LRELU && act != GR_POLICY_ACT_ELU))
+      !aligned16(stats) || (act != GR_POLICY_ACT_LRELU && act != GR_POLICY_ACT_ELU) ||
+      !stem1_rows_ok(nimg, na, nb, y_rows))
     return GR_ERR_ARG;
-  const gr::Stem1 s = stem1_of(obs, ld, off, nimg, pix, na, nb, conv_w, c);
+  const gr::Stem1 s = stem1_of(obs, ld, off, nimg, pix, na, nb, conv_w, c, y_rows);
   const hipError_t e = gr::launch_stem1_forward(s, bn_w, bn_b, eps, act, slope, y, stats, part, (hipStream_t)stream);
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
 int gr_stem1_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
                       int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b,
-                      const float* stats, int32_t act, float slope, const float* gy, float* g_conv_w, float* g_bn_w,
-                      float* g_bn_b, double* part, void* stream) {
+                      const float* stats, int32_t act, float slope, const float* gy, int64_t gy_rows, float* g_conv_w,
+                      float* g_bn_w, float* g_bn_b, double* part, void* stream) {
   if (!stem1_args_ok(obs, nimg, pix, na, nb, conv_w, c, bn_w, bn_b) || !stats || !gy || !g_conv_w || !g_bn_w ||
-      !g_bn_b || !part || !aligned16(gy) || !aligned16(stats) || (act != GR_POLICY_ACT_LRELU && act != GR_POLICY_ACT_ELU))
+      !g_bn_b || !part || !aligned16(gy) || !aligned16(stats) || (act != GR_POLICY_ACT_LRELU && act != GR_POLICY_ACT_ELU) ||
+      !stem1_rows_ok(nimg, na, nb, gy_rows))
     return GR_ERR_ARG;
-  const gr::Stem1 s = stem1_of(obs, ld, off, nimg, pix, na, nb, conv_w, c);
+  const gr::Stem1 s = stem1_of(obs, ld, off, nimg, pix, na, nb, conv_w, c, gy_rows);
   const hipError_t e = gr::launch_stem1_backward(s, bn_w, bn_b, stats, act, slope, gy, g_conv_w, g_bn_w, g_bn_b, part,
                                                  (hipStream_t)stream);
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;

@@ -106,6 +106,8 @@ struct Stem1 {
   const short* pix;
   const float* w;
   int c;
+  long long rows_out;  // rows of y / gy that exist: the forward stores rows [0, rows_out), the backward reads the
+                       // gradient of those rows and takes the rest (cells no later layer reads) as zero
 };
 long long stem1_scratch_doubles(int nimg, int rows_per_img, int c);
 hipError_t launch_stem1_forward(const Stem1& s, const float* bw, const float* bb, float eps, int act, float slope,

@@ -88,21 +88,23 @@ def batch_norm_act(bn: nn.BatchNorm2d, act: nn.Module, x: torch.Tensor) -> torch
 
 
 class _Stem1(torch.autograd.Function):
-    """Conv2d(1, C, 3, stride 3) -> BatchNorm2d (batch statistics) -> act from the depth images (gr_stem1_*)."""
+    """Conv2d(1, C, 3, stride 3) -> BatchNorm2d (batch statistics) -> act from the depth images (gr_stem1_*).
+    Returns the nimg x na table-a rows only (the next conv's input as it is): the nimg x nb table-b rows enter the
+    statistics but nothing reads them, so no zero-filled [rows, C] gradient is built for them in the backward."""
 
     @staticmethod
     def forward(ctx, img, conv_w, bn_w, bn_b, pix, na, nb, eps, act, slope):
         lib = _abi.load()
         nimg = img.shape[0]
         c = conv_w.shape[0]
-        rows = nimg * (na + nb)
+        rows = nimg * na
         y = torch.empty(rows, c, device=img.device, dtype=torch.float32)
         stats = torch.empty(4, c, device=img.device, dtype=torch.float32)
         part = torch.empty(int(lib.gr_stem1_scratch_doubles(nimg, na + nb, c)), device=img.device, dtype=torch.float64)
         w = conv_w.detach().reshape(c, 9).contiguous()
         bw, bb = bn_w.detach().contiguous(), bn_b.detach().contiguous()
         rc = lib.gr_stem1_forward(img.data_ptr(), img.stride(0), 0, nimg, pix.data_ptr(), na, nb, w.data_ptr(), c,
-                                  bw.data_ptr(), bb.data_ptr(), float(eps), act, float(slope), y.data_ptr(),
+                                  bw.data_ptr(), bb.data_ptr(), float(eps), act, float(slope), y.data_ptr(), rows,
                                   stats.data_ptr(), part.data_ptr(), _stream(img))
         if rc != 0:
             raise RuntimeError(f"gr_stem1_forward failed (status {rc})")
@@ -128,7 +130,8 @@ class _Stem1(torch.autograd.Function):
         part = torch.empty(int(lib.gr_stem1_scratch_doubles(nimg, na + nb, c)), device=img.device, dtype=torch.float64)
         rc = lib.gr_stem1_backward(img.data_ptr(), img.stride(0), 0, nimg, pix.data_ptr(), na, nb, w.data_ptr(), c,
                                    bw.data_ptr(), bb.data_ptr(), stats.data_ptr(), act, float(slope), gy.data_ptr(),
-                                   gconv.data_ptr(), gbw.data_ptr(), gbb.data_ptr(), part.data_ptr(), _stream(img))
+                                   gy.shape[0], gconv.data_ptr(), gbw.data_ptr(), gbb.data_ptr(), part.data_ptr(),
+                                   _stream(img))
         if rc != 0:
             raise RuntimeError(f"gr_stem1_backward failed (status {rc})")
         return None, gconv.view(wshape), gbw, gbb, None, None, None, None, None, None
@@ -144,9 +147,9 @@ def stem1_applicable(bn: nn.BatchNorm2d, act: nn.Module, img: torch.Tensor, conv
 
 def stem1_bn_act(bn: nn.BatchNorm2d, act: nn.Module, conv_w: torch.Tensor, img: torch.Tensor, pix: torch.Tensor,
                  na: int, nb: int) -> torch.Tensor:
-    """act(bn(conv(img))) as the patch rows of VisionActorCritic.stem_gemm (img [B, H*W] rows; pix int16
-    [(na + nb) * 9] pixel offsets), running statistics updated as nn.BatchNorm2d does (the caller counts the
-    batch in num_batches_tracked)."""
+    """act(bn(conv(img))) as the table-a patch rows of VisionActorCritic.stem_gemm (img [B, H*W] rows; pix int16
+    [(na + nb) * 9] pixel offsets; the B * nb table-b rows count in the statistics and are not returned), running
+    statistics updated as nn.BatchNorm2d does (the caller counts the batch in num_batches_tracked)."""
     code, slope = _act_code(act)
     y, stats = _Stem1.apply(img, conv_w, bn.weight, bn.bias, pix, na, nb, bn.eps, code, slope)
     _update_running(bn, stats)

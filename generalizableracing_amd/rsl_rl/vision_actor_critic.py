@@ -175,9 +175,12 @@ class VisionActorCritic(ActorCritic):
             if n1_left:
                 x = torch.cat([x, flat.index_select(1, idx_left).view(B * n1_left, 9)])
             y = self._bn_act(bn1, act, _gemm(x, conv1.weight.reshape(16, 9)))
-        x = y[: B * n1].view(B * n2, 144)  # conv2's 3x3 patches (i, j, c): a view
+        # conv2's 3x3 patches (i, j, c): a view (the fused block returns exactly these rows; a slice of the whole
+        # tensor would still cost a zero-filled gradient plus a copy in the backward)
+        x = (y if y.shape[0] == B * n1 else y[: B * n1]).view(B * n2, 144)
         y = self._bn_act(bn2, act, _gemm(x, conv2.weight.permute(0, 2, 3, 1).reshape(32, 144)))
-        x = y.view(B, n2, 32)[:, :n3].reshape(B * h3 * w3, 128)  # conv3's 2x2 patches: a view at 72x96
+        y = y.view(B, n2, 32)
+        x = (y if n3 == n2 else y[:, :n3]).reshape(B * h3 * w3, 128)  # conv3's 2x2 patches: a view at 72x96
         y = self._bn_act(bn3, act, _gemm(x, conv3.weight.permute(0, 2, 3, 1).reshape(64, 128))).view(B, h3 * w3 * 64)
         # reference flatten is NCHW (c, h, w): permute the Linear's columns to (h, w, c) instead
         wl = lin.weight.view(-1, 64, h3, w3).permute(0, 2, 3, 1).reshape(lin.weight.shape[0], -1)

@@ -37,7 +37,7 @@ extern "C" {
 
 /* 2: GR_NUM_PLANES 17 (obstacle hint, rotor constants), gr_policy_args.precision, the observation sink and the
  * status word; gr_policy_args_size */
-#define GR_ABI_VERSION 2
+#define GR_ABI_VERSION 3
 
 /* ---- status codes ---- */
 #define GR_OK 0
@@ -410,17 +410,20 @@ int gr_bn_act_backward(const float* x, const float* gy, int64_t m, int32_t c, co
  * VisionActorCritic.stem_gemm: nimg x na rows whose 3x3 cells are pix[0 .. na) (int16 pixel offsets, 9 per
  * row), then nimg x nb rows from pix[na .. na + nb); y [rows][c].  The patch matrix and the conv output are
  * never written (recomputed per pass); the backward returns the conv weight's gradient [c][9] and the BN
- * affine gradients (the image needs none).  c in {4, 8, 16, 32, 64}, na + nb <= 1024; `part`: a workspace of
+ * affine gradients (the image needs none).  Only the first y_rows rows of y are stored and only the first
+ * gy_rows of gy are read (ABI 3): the table-b rows (cells no later conv reads) still enter the BN statistics,
+ * their gradient is zero, so y [y_rows][c] can be exactly the next layer's input and no zero-padded gradient is
+ * ever built.  c in {4, 8, 16, 32, 64}, na + nb <= 1024; `part`: a workspace of
  * gr_stem1_scratch_doubles(nimg, na + nb, c) doubles; stats as gr_bn_act_forward.
  */
 int64_t gr_stem1_scratch_doubles(int32_t nimg, int32_t rows_per_img, int32_t c);
 int gr_stem1_forward(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
                      int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b, float eps,
-                     int32_t act, float slope, float* y, float* stats, double* part, void* stream);
+                     int32_t act, float slope, float* y, int64_t y_rows, float* stats, double* part, void* stream);
 int gr_stem1_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
                       int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b,
-                      const float* stats, int32_t act, float slope, const float* gy, float* g_conv_w, float* g_bn_w,
-                      float* g_bn_b, double* part, void* stream);
+                      const float* stats, int32_t act, float slope, const float* gy, int64_t gy_rows, float* g_conv_w,
+                      float* g_bn_w, float* g_bn_b, double* part, void* stream);
 
 /* Device status: the GR_STATUS_* bits the kernels of this context raised since the last clear (0: none).
  * Synchronises `stream` (the stream the steps ran on); clear != 0 resets the word.  A raised bit means the
