@@ -69,6 +69,9 @@ def main():
                                                                     gz.data_ptr(), part.data_ptr(), sums.data_ptr(), st),
               m * (2 * h * 4 + k * 4))
     res["sum_us"] = sum(v["us"] for v in res.values() if isinstance(v, dict))
+    # reference rates of the same matrix shape: torch's fill (write only) and copy (read + write)
+    timed("ref_torch_fill", lambda: h1.fill_(1.0), m * h * 4)
+    timed("ref_torch_copy", lambda: h1.copy_(gh), m * h * 8)
     print(json.dumps(res))
     if a.out:
         with open(a.out, "a") as f:
