@@ -917,6 +917,16 @@ int gr_episode_accumulate(int64_t n, const float* reward, const void* dones, int
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
+int gr_l2c2_mix(const float* obs, const float* next_obs, const float* w, int64_t rows, int32_t cols, float* out,
+                void* stream) {
+  if (!obs || !next_obs || !w || !out || rows < 0 || cols <= 0 || cols % 4 || !aligned16(obs) || !aligned16(next_obs) ||
+      !aligned16(out))
+    return GR_ERR_ARG;
+  if (rows == 0) return GR_OK;
+  const hipError_t e = gr::launch_l2c2_mix(obs, next_obs, w, (long long)rows, cols, out, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
 int gr_gae(int64_t n, int32_t t_steps, float gamma, float lam, const float* rewards, const uint8_t* dones,
            const float* values, const float* last_values, int64_t ld_last, float* returns, float* advantages,
            void* stream) {

@@ -124,6 +124,8 @@ int column_sum_blocks(long long m);                                             
 hipError_t launch_column_sum(const void* x, int dtype, long long m, int n, float* part, float* out, hipStream_t s);
 int head_partial_rows(long long m);                                                                      // gr_update.hip
 int in_partial_rows(long long m);                                                                        // gr_update.hip
+hipError_t launch_l2c2_mix(const float* o, const float* nx, const float* w, long long rows, int cols, float* out,
+                           hipStream_t s);  // gr_rollout.hip
 hipError_t launch_head_forward(const float* z, long long m, int h, const float* w, const float* b, int k, float slope,
                                float* y, hipStream_t s);
 hipError_t launch_head_backward(const float* z, const float* gy, long long m, int h, const float* w, int k,

@@ -105,4 +105,32 @@ hipError_t launch_gae(long long n, int t_steps, float gamma, float lam, const fl
   return hipGetLastError();
 }
 
+// PPOL2C2's mixed observations (ppo_l2c2.py:179-180): out = o + w * (n - o) with w one scalar per row, in the torch
+// expression's three roundings (sub, mul, add; no contraction): one pass (read o, n, write out) instead of three
+// elementwise kernels over [rows, cols] matrices of ~680 MB at 4 096 envs
+__global__ __launch_bounds__(256) void l2c2_mix(const float* __restrict__ o, const float* __restrict__ nx,
+                                                 const float* __restrict__ w, long long rows, int cols4,
+                                                 float* __restrict__ out) {
+  const long long n4 = rows * cols4;
+  for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < n4; q += (long long)gridDim.x * 256) {
+    const float wr = w[q / cols4];
+    const float4 a = reinterpret_cast<const float4*>(o)[q], b = reinterpret_cast<const float4*>(nx)[q];
+    float4 r;
+    r.x = a.x + wr * (b.x - a.x);
+    r.y = a.y + wr * (b.y - a.y);
+    r.z = a.z + wr * (b.z - a.z);
+    r.w = a.w + wr * (b.w - a.w);
+    reinterpret_cast<float4*>(out)[q] = r;
+  }
+}
+
+hipError_t launch_l2c2_mix(const float* o, const float* nx, const float* w, long long rows, int cols, float* out,
+                           hipStream_t s) {
+  const long long n4 = rows * (cols / 4);
+  long long blocks = (n4 + 256 * 8 - 1) / (256 * 8);
+  blocks = blocks < 1 ? 1 : (blocks > 8192 ? 8192 : blocks);
+  hipLaunchKernelGGL(l2c2_mix, dim3((unsigned)blocks), dim3(256), 0, s, o, nx, w, rows, cols / 4, out);
+  return hipGetLastError();
+}
+
 }  // namespace gr

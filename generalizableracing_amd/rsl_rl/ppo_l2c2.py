@@ -36,6 +36,26 @@ def _mean_of(out):
     return out[0] if isinstance(out, (tuple, list)) else out
 
 
+def _mix(obs, next_obs, w):
+    """obs + w * (next_obs - obs) (ppo_l2c2.py:179-180), w [rows, 1]: on the GPU one pass of gr_l2c2_mix (the same
+    three fp32 roundings as the torch expression), else the expression."""
+    fused = (obs.is_cuda and obs.dim() == 2 and obs.dtype == torch.float32 and next_obs.dtype == torch.float32
+             and obs.shape == next_obs.shape and obs.shape[1] % 4 == 0 and w.numel() == obs.shape[0]
+             and obs.is_contiguous() and next_obs.is_contiguous()
+             and not (obs.requires_grad or next_obs.requires_grad or w.requires_grad))
+    if fused:
+        from .. import _abi
+
+        w = w.reshape(-1).float().contiguous()
+        out = torch.empty_like(obs)
+        rc = _abi.load().gr_l2c2_mix(obs.data_ptr(), next_obs.data_ptr(), w.data_ptr(), obs.shape[0], obs.shape[1],
+                                     out.data_ptr(), torch.cuda.current_stream(obs.device).cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"gr_l2c2_mix failed (status {rc})")
+        return out
+    return obs + w * (next_obs - obs)
+
+
 class PPOL2C2(PPO):
     def __init__(self, policy, env=None, value_smoothness_coef=0.1, smoothness_upper_bound=1.0,
                  smoothness_lower_bound=0.1, **kwargs):
@@ -86,7 +106,7 @@ class PPOL2C2(PPO):
         """ppo_l2c2.py:176-188; returns (smooth_loss, action_smoothness)."""
         policy_coef, value_coef = self.smooth_coefs()
         mix_weights = cont_batch * (torch.rand_like(cont_batch) - 0.5) * 2.0
-        mix_obs_batch = obs_batch + mix_weights * (next_obs_batch - obs_batch)
+        mix_obs_batch = _mix(obs_batch, next_obs_batch, mix_weights)
         policy_smooth = torch.square(torch.norm(mu_batch - _mean_of(self.policy.act_inference(mix_obs_batch)),
                                                 dim=-1)).mean()
         value_smooth = torch.square(torch.norm(value_batch - self.policy.evaluate(mix_obs_batch), dim=-1)).mean()

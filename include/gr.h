@@ -588,6 +588,11 @@ typedef struct {
 int gr_store_transition(const gr_transition_args* args, void* stream);
 int gr_episode_accumulate(int64_t n, const float* reward, const void* dones, int32_t dones_bytes, float* cur_rew,
                           float* cur_len, float* fin_rew, float* fin_len, uint8_t* fin_done, void* stream);
+/* PPOL2C2's mixed observations (standalone/rsl_rl/ext/algorithms/ppo_l2c2.py:179-180, `obs + w * (next - obs)`):
+ * out [rows][cols] = obs + w[row] * (next_obs - obs), the torch expression's three fp32 roundings, one pass; contiguous
+ * rows, cols a multiple of 4, 16-byte aligned. */
+int gr_l2c2_mix(const float* obs, const float* next_obs, const float* w, int64_t rows, int32_t cols, float* out,
+                void* stream);
 int gr_gae(int64_t n, int32_t t_steps, float gamma, float lam, const float* rewards, const uint8_t* dones,
            const float* values, const float* last_values, int64_t ld_last, float* returns, float* advantages,
            void* stream);

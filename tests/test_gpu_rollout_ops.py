@@ -113,3 +113,18 @@ def test_actor_critic_act_draw_matches_torch_normal():
     pol.update_distribution(obs)
     b = torch.normal(pol.distribution.loc, pol.distribution.scale)
     assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_l2c2_mix_matches_torch():
+    """gr_l2c2_mix (PPOL2C2's mixed observations, ppo_l2c2.py:179-180) is bit-identical to the torch expression
+    obs + w * (next - obs) on the same device, zero weights (a reset) and negative ones included."""
+    from generalizableracing_amd.rsl_rl.ppo_l2c2 import _mix
+
+    g = torch.Generator(device="cuda").manual_seed(11)
+    for rows, cols in ((1, 4), (1000, 6928), (4097, 16)):
+        o = torch.randn(rows, cols, device="cuda", generator=g)
+        n = torch.randn(rows, cols, device="cuda", generator=g)
+        w = (torch.rand(rows, 1, device="cuda", generator=g) - 0.5) * 2.0
+        w[::5] = 0.0
+        assert torch.equal(_mix(o, n, w), o + w * (n - o))
