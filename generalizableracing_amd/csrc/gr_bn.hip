@@ -258,9 +258,6 @@ hipError_t launch_bn_backward(const float* x, const float* gy, long long m, int 
 // statistics pass and the apply pass recompute the 36 FMAs of a thread's 4 channels, and so do the backward
 // passes, which end in the conv weight's gradient (the image needs none) instead of writing gx.
 constexpr int STEM_MAX_CELLS = 1024;  // na + nbt (768 at 72 x 96)
-#ifndef GR_STEM_DPP
-#define GR_STEM_DPP 0
-#endif
 
 __device__ __forceinline__ void stem_stage_table(const Stem1& s, short* tab) {
   for (int i = threadIdx.x; i < (s.na + s.nbt) * 9; i += BN_THREADS) tab[i] = s.pix[i];
@@ -279,20 +276,6 @@ __device__ __forceinline__ void stem_pixels(const Stem1& s, const short* tab, un
   }
   const float* img = s.obs + (long long)b * s.ld + s.off;
   const short* t = tab + p * 9;
-#if GR_STEM_DPP
-  if (s.c == 16) {
-    // the 4 lanes of a row (one DPP quad, channel groups 0-3) share its 9 pixels: lane g loads pixels g, g + 4
-    // (and lane 0 pixel 8), the quad broadcasts them (quad_perm)
-    const int g = threadIdx.x & 3;
-    const float v0 = img[t[g]], v1 = img[t[g + 4]], v2 = img[t[8]];
-#define GR_QB(v, j) __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), (j) * 0x55, 0xf, 0xf, false))
-    px[0] = GR_QB(v0, 0); px[1] = GR_QB(v0, 1); px[2] = GR_QB(v0, 2); px[3] = GR_QB(v0, 3);
-    px[4] = GR_QB(v1, 0); px[5] = GR_QB(v1, 1); px[6] = GR_QB(v1, 2); px[7] = GR_QB(v1, 3);
-#undef GR_QB
-    px[8] = v2;
-    return;
-  }
-#endif
 #pragma unroll
   for (int k = 0; k < 9; ++k) px[k] = img[t[k]];
 }

@@ -358,6 +358,43 @@ __global__ __launch_bounds__(HD_WAVES * 64) void in_forward(const float* __restr
   }
 }
 
+// ---- the same on MFMA for d = 16, h a multiple of 16 (the actor / critic's 16 observations): a wave takes 16 rows at a
+// time and computes y^T = W1 x^T + b1 per 16-unit tile with four v_mfma_f32_16x16x4f32 (lane (g, j): W1 row 16 t + j
+// and x row j, elements 4 g .. 4 g + 3, so k step s contracts elements 4 g + s; its accumulator holds units
+// 16 t + 4 g .. + 3 of row j: one 16-byte store).  The VALU form is VALU-bound (256 x 16 MACs per row on 64 lanes);
+// this one moves only its bytes.  Summation order differs from the VALU form (both are held to float64).
+typedef float hd_f4 __attribute__((ext_vector_type(4)));
+template <int NT>
+__global__ __launch_bounds__(HD_WAVES * 64) void in_forward_mfma(const float* __restrict__ x, long long m, int ldx,
+                                                                 const float* __restrict__ w,
+                                                                 const float* __restrict__ b, float slope,
+                                                                 float* __restrict__ y) {
+  constexpr int H = 16 * NT;
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+  hd_f4 wr[NT], br[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    wr[t] = *reinterpret_cast<const hd_f4*>(w + (size_t)(16 * t + j) * 16 + 4 * g);
+    br[t] = *reinterpret_cast<const hd_f4*>(b + 16 * t + 4 * g);
+  }
+  const long long tiles = (m + 15) / 16;
+  for (long long tile = (long long)blockIdx.x * HD_WAVES + (threadIdx.x >> 6); tile < tiles;
+       tile += (long long)gridDim.x * HD_WAVES) {
+    const long long row = tile * 16 + j;
+    const long long rr = row < m ? row : m - 1;
+    const hd_f4 xv = *reinterpret_cast<const hd_f4*>(x + rr * ldx + 4 * g);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      hd_f4 acc = br[t];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[t][k], xv[k], acc, 0, 0, 0);
+      if (row < m)
+        hd_st(y + row * H + 16 * t + 4 * g,
+              hd_v4{hd_act(acc[0], slope), hd_act(acc[1], slope), hd_act(acc[2], slope), hd_act(acc[3], slope)});
+    }
+  }
+}
+
 // ---- first layer backward; partial row of a wave: [gW1 (h d, row-major [h][d]) | gb1 (h)]
 template <int D>
 __global__ __launch_bounds__(HD_WAVES * 64) void in_backward(const float* __restrict__ gh, const float* __restrict__ hv,
@@ -508,6 +545,16 @@ hipError_t launch_head_backward(const float* z, const float* gy, long long m, in
 
 hipError_t launch_in_forward(const float* x, long long m, int d, int ldx, const float* w, const float* b, int h,
                              float slope, float* y, hipStream_t s) {
+  if (d == 16 && (h == 256 || h == 128) && ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(b)) & 15) == 0) {
+    const long long tiles = (m + 15) / 16;
+    const long long fb = (tiles + 4 * HD_WAVES - 1) / (4 * HD_WAVES);  // ~4 row tiles per wave
+    const int blocks = (int)(fb < 1 ? 1 : (fb > 8192 ? 8192 : fb));
+    if (h == 256)
+      hipLaunchKernelGGL(in_forward_mfma<16>, dim3(blocks), dim3(HD_WAVES * 64), 0, s, x, m, ldx, w, b, slope, y);
+    else
+      hipLaunchKernelGGL(in_forward_mfma<8>, dim3(blocks), dim3(HD_WAVES * 64), 0, s, x, m, ldx, w, b, slope, y);
+    return hipGetLastError();
+  }
   const long long fb = (m + 8 * HD_WAVES * HD_U - 1) / (8 * HD_WAVES * HD_U);  // ~8 row groups per wave
   const int blocks = (int)(fb < 1 ? 1 : (fb > 8192 ? 8192 : fb));
 #define IN_FWD(DD) \

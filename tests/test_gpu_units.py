@@ -229,7 +229,7 @@ def test_leaky_head(rows, h, k):
 
 
 @pytest.mark.parametrize("rows,d,ldx,h", [(24576, 16, 16, 256), (24576, 16, 48, 256), (393216, 16, 48, 256),
-                                          (8193, 32, 36, 64), (5, 4, 4, 8)])
+                                          (1001, 16, 20, 128), (8193, 32, 36, 64), (5, 4, 4, 8)])
 def test_mlp_in_layer(rows, d, ldx, h):
     """gr_mlp_in_forward / gr_mlp_in_backward (the MLP's first Linear + bias + LeakyReLU and its weight / bias
     gradients, rsl_rl/linear.py _LeakyMLPFn) against float64 torch, on strided input rows as the packed mini-batch
