@@ -568,7 +568,7 @@ def main():
         del graph_o
         rd_o, wr_o = env_o.bytes_per_env_step()
         extra["with_obstacles"] = {
-            "value": n * ws * a.steps / secs_o, "unit": "env-steps/s", "kernel": "gr::step_kernel<false, true>",
+            "value": n * ws * a.steps / secs_o, "unit": "env-steps/s", "kernel": "gr::step_kernel<false, true, 0>",
             "kernel_us": kt_o["kernel_us"], "bytes_per_env_step": {"read": rd_o, "written": wr_o},
             "achieved_GBps": (rd_o + wr_o) * n / (kt_o["kernel_us"] * 1e-6) / 1e9,
             "frac": (rd_o + wr_o) * n / (kt_o["kernel_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS,
@@ -683,7 +683,8 @@ def main():
                          "read_achieved": rd * n / (us * 1e-6) / 1e9,
                          "read_frac": rd * n / (us * 1e-6) / 1e9 / HBM_PEAK_GBS,
                          "read_frac_definition": "the north star's HBM-read roofline: read bytes only",
-                         "kernel": f"gr::step_kernel<true, {'true' if a.obstacles else 'false'}> (fused step)", **kt,
+                         "kernel": ("gr::step_kernel<false, true, 0>" if a.obstacles else
+                                    f"gr::step_kernel<true, false, {8 if a.gates <= 8 else 0}>") + " (fused step)", **kt,
                          "algorithmic_bytes_per_launch": (rd + wr) * n,
                          "bytes_per_env_step": {"read": rd, "written": wr}},
             "cpu_baseline": cpu,

@@ -389,7 +389,8 @@ DEV void gate_frame(const float* g, const float v[3], float o[3]) {
 // lattice mask (17 bits) of the points inside a gate frame or under the ground, and with OBST inside
 // an obstacle looked up from the grid (the substep integrator; the explicit step hands obstacles to the
 // policy waves instead).  Replaces PhysX contact / Warp mesh_tools.py:128-233; see oracle.
-template <bool OBST>
+// MAXG > 0: tracks of at most MAXG gates (the launch checks max_gates), the sphere pass a fixed predicated sequence
+template <bool OBST, int MAXG = 0>
 DEV uint32_t collision_mask(const KArgs& a, const Tab& tab, int type, int lvl, const float p[3], const float q[4],
                             const ObstGrid& og) {
   const float* rec = tab.rec(type, lvl);
@@ -398,11 +399,22 @@ DEV uint32_t collision_mask(const KArgs& a, const Tab& tab, int type, int lvl, c
   const float reach = a.kc->lat_reach;  // > max |lattice offset| incl. rounding
   // ---- pass 1: bounding-sphere cull, one 16-byte read (centre, r^2) per gate ----
   uint32_t sph = 0u;
+  if constexpr (MAXG > 0) {
+#pragma unroll
+    for (int g = 0; g < MAXG; ++g) {
+      if (g < ng) {
+        const float4 c4 = *reinterpret_cast<const float4*>(tab.gate(type, lvl, g));
+        const float dx = p[0] - c4.x, dy = p[1] - c4.y, dz = p[2] - c4.z;
+        if ((dx * dx + dy * dy) + dz * dz <= c4.w) sph |= 1u << g;
+      }
+    }
+  } else {
 #pragma unroll 8
-  for (int g = 0; g < ng; ++g) {
-    const float4 c4 = *reinterpret_cast<const float4*>(tab.gate(type, lvl, g));
-    const float dx = p[0] - c4.x, dy = p[1] - c4.y, dz = p[2] - c4.z;
-    if ((dx * dx + dy * dy) + dz * dz <= c4.w) sph |= 1u << g;
+    for (int g = 0; g < ng; ++g) {
+      const float4 c4 = *reinterpret_cast<const float4*>(tab.gate(type, lvl, g));
+      const float dx = p[0] - c4.x, dy = p[1] - c4.y, dz = p[2] - c4.z;
+      if ((dx * dx + dy * dy) + dz * dz <= c4.w) sph |= 1u << g;
+    }
   }
   const bool ground_near = p[2] - ground < reach;
   int ocount = 0;
@@ -1099,7 +1111,9 @@ DEV void merge_handover(const float4* xch, int t, bool reset, Env& e) {
 #else
 #define GR_STEP_LB __launch_bounds__(3 * GR_BLOCK)
 #endif
-template <bool USE_LDS, bool OBST>
+// MAXG > 0: tracks of at most MAXG gates (checked at launch).  The 8-gate instantiation (the reference's tracks,
+// BASELINE C3 / C4) runs without scratch (the generic one spills 48 B / lane in its 32-gate sphere loop).
+template <bool USE_LDS, bool OBST, int MAXG = 0>
 __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
                                                              const float* __restrict__ actions) {
   a.kc = kc;
@@ -1181,7 +1195,7 @@ __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
       }
       commit();  // barrier 1: the table is first needed by the collision test
       STAMP(14);
-      uint32_t cm = collision_mask<false>(a, sl.tab, e.type, e.lvl, e.p, e.q, ObstGrid{});
+      uint32_t cm = collision_mask<false, MAXG>(a, sl.tab, e.type, e.lvl, e.p, e.q, ObstGrid{});
       STAMP(15);
       if (OBST) {
         // wait for the partner policy wave's obstacle mask (same 64 envs); it is resident and never waits on us
@@ -1210,7 +1224,7 @@ __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
       for (int k = 0; k < 3; ++k) fb[k] = (fb[k] - (e.k2[k] * vb[k]) * gr_fabsf(vb[k])) - e.k1[k] * vb[k];
       for (int s = 0; s < c.decimation; ++s) {
         si_substep(m, Jp, fb, tt + 1, c.sim_dt, c.gravity, e.p, e.q, e.v, e.w, accl, al);
-        int cc = __builtin_popcount(collision_mask<OBST>(a, sl.tab, e.type, e.lvl, e.p, e.q, og));
+        int cc = __builtin_popcount(collision_mask<OBST, MAXG>(a, sl.tab, e.type, e.lvl, e.p, e.q, og));
         ccount = cc > ccount ? cc : ccount;
       }
     }
@@ -1668,7 +1682,11 @@ static hipError_t launch_env_mode(const KArgs& a, const float* actions, const ui
       hipLaunchKernelGGL((step_kernel<false, true>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, b, b.kc, actions);
     } else {
       const size_t bytes = (size_t)a.h.lds_tab_vec * 16 + (size_t)(GR_XF4 + GR_RF4 + GR_SF4) * GR_BLOCK * 16;
-      if (lds)
+      // tracks of <= 8 gates (the reference's tracks, BASELINE C3 / C4): the sphere pass unrolled to a fixed 8, no
+      // scratch (same time as the generic kernel: 9.88-9.98 vs 9.82-9.98 us, gpurun_out/g8.txt)
+      if (lds && a.h.max_gates <= 8)
+        hipLaunchKernelGGL((step_kernel<true, false, 8>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
+      else if (lds)
         hipLaunchKernelGGL((step_kernel<true, false>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
       else
         hipLaunchKernelGGL((step_kernel<false, false>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
@@ -1730,6 +1748,7 @@ hipError_t launch_test_philox(int n, uint32_t c0, uint32_t c1, uint32_t c2, uint
 
 hipError_t allow_large_lds() {
   const void* ks[] = {reinterpret_cast<const void*>(&step_kernel<true, false>),
+                      reinterpret_cast<const void*>(&step_kernel<true, false, 8>),
                       reinterpret_cast<const void*>(&env_kernel<KMODE_RESET, true>),
                       reinterpret_cast<const void*>(&env_kernel<KMODE_OBSERVE, true>)};
   for (const void* k : ks) {
