@@ -568,7 +568,8 @@ def main():
         del graph_o
         rd_o, wr_o = env_o.bytes_per_env_step()
         extra["with_obstacles"] = {
-            "value": n * ws * a.steps / secs_o, "unit": "env-steps/s", "kernel": "gr::step_kernel<false, true, 0>",
+            "value": n * ws * a.steps / secs_o, "unit": "env-steps/s",
+            "kernel": "gr::step_kernel<false, true, 0>",
             "kernel_us": kt_o["kernel_us"], "bytes_per_env_step": {"read": rd_o, "written": wr_o},
             "achieved_GBps": (rd_o + wr_o) * n / (kt_o["kernel_us"] * 1e-6) / 1e9,
             "frac": (rd_o + wr_o) * n / (kt_o["kernel_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS,
