@@ -164,11 +164,14 @@ __device__ __forceinline__ hd_v4 hd_ld(const float* p) {
 // rows per wave for the backward kernels: enough waves to fill the chip, few enough partial rows.  256 rows per
 // wave, at most 4096 waves (partial rows); a batch that gives fewer than 1024 waves that way (e.g. 24 576 rows, config
 // C2's mini-batch: 96 waves, each a serial 256-row chain of ~100 us) is spread over up to 1024 waves of >= 16 rows
-__host__ __device__ inline long long hd_rows_per_wave(long long m, long long target = GR_HD_RPW) {
+#ifndef GR_IN_SMALL_WAVES
+#define GR_IN_SMALL_WAVES 1024  // in_backward: waves for batches below target x that (its partial rows are 17 KB each)
+#endif
+__host__ __device__ inline long long hd_rows_per_wave(long long m, long long target = GR_HD_RPW, long long small = 1024) {
   long long w = (m + target - 1) / target;
-  if (w < 1024) {
+  if (w < small) {
     const long long w16 = (m + 15) / 16;
-    w = w16 < 1024 ? w16 : 1024;
+    w = w16 < small ? w16 : small;
   }
   w = w < 1 ? 1 : (w > 4096 ? 4096 : w);
   return (m + w - 1) / w;
@@ -178,7 +181,7 @@ int head_partial_rows(long long m) {
   return (int)((m + rpw - 1) / rpw);
 }
 int in_partial_rows(long long m) {
-  const long long rpw = hd_rows_per_wave(m, GR_IN_RPW);
+  const long long rpw = hd_rows_per_wave(m, GR_IN_RPW, GR_IN_SMALL_WAVES);
   return (int)((m + rpw - 1) / rpw);
 }
 
@@ -566,7 +569,7 @@ hipError_t launch_in_forward(const float* x, long long m, int d, int ldx, const 
 
 hipError_t launch_in_backward(const float* gh, const float* hv, const float* x, long long m, int d, int ldx, int h,
                               float slope, float* part, float* sums, hipStream_t s) {
-  const long long rpw = hd_rows_per_wave(m, GR_IN_RPW);
+  const long long rpw = hd_rows_per_wave(m, GR_IN_RPW, GR_IN_SMALL_WAVES);
   const int prow = in_partial_rows(m);
   const int blocks = hd_grid(prow);
 #define IN_BWD(DD) \

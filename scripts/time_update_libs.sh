@@ -8,6 +8,6 @@ mkdir -p gpurun_out
 for rep in 1 2; do
   for lib in tree "$@"; do
     if [ "$lib" = tree ]; then env_lib=""; else env_lib="GR_LIB_PATH=$lib"; fi
-    env $env_lib timeout -k 10 120 python -u scripts/time_update_kernels.py --out gpurun_out/$OUT > /dev/null || exit 3
+    env $env_lib timeout -k 10 120 python -u scripts/time_update_kernels.py ${UPD_ARGS} --out gpurun_out/$OUT > /dev/null || exit 3
   done
 done
