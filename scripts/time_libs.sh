@@ -5,7 +5,7 @@ set -o pipefail
 OUT=$1; shift
 mkdir -p gpurun_out
 : > gpurun_out/$OUT
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   for lib in tree "$@"; do
     if [ "$lib" = tree ]; then env_lib=""; else env_lib="GR_LIB_PATH=$lib"; fi
     line=$(env $env_lib timeout -k 10 120 python -u bench.py --no-extras --steps 1024 --warmup 64 ${BENCH_ARGS} 2>/dev/null | tail -1) || exit 3
