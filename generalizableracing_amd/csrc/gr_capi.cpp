@@ -146,6 +146,7 @@ void derive(gr_ctx* c) {
   h.env_id_offset = g.env_id_offset;
   h.use_motor_model = g.use_motor_model;
   h.dr_rotor = g.dr_rotor;
+  h.integrator = g.integrator;
   h.obs_noise = g.obs_noise;
   h.lds_tab_vec = a.lds_bytes / 16;
   h.seed_lo = g.seed_lo;

@@ -48,6 +48,7 @@ struct KHot {
   float obs_lin_vel_noise, obs_att_noise;
   float obst_span;  // obstacle grid: cell + 2 margin (m), the side of a hinted grown cell
   int dr_rotor;     // per-env rotor constants (GR_P_ROTOR)
+  int integrator;   // GR_INTEGRATOR_* (the launch picks the lean step kernel for the explicit integrator)
   int test_fault;   // gr_test_inject_fault (0 in production)
 };
 

@@ -518,6 +518,8 @@ DEV void motor_update(const KArgs& a, const MotorK& m, float f[4], float mw[4]) 
 }
 
 // CTBRController.compute (controller_diff.py:120-144); rk: the env's rotor constants (dr_rotor) or null
+// NO_MOTOR: compiled for configurations without the motor model (the lean step kernel)
+template <bool NO_MOTOR = false>
 DEV void ctbr_compute(const KArgs& a, const float cmd[4], const float wb[3], const float ab[3], const float Kp[3],
                       const float Kd[3], float cT, const float ct[3], float& T, float tau[3], float mw[4],
                       float tt[4], const float4* rk = nullptr) {
@@ -535,7 +537,7 @@ DEV void ctbr_compute(const KArgs& a, const float cmd[4], const float wb[3], con
     tau[i] = (1.0f - ct[i]) * tdes + ct[i] * tau[i];
   }
   tt[0] = T; tt[1] = tau[0]; tt[2] = tau[1]; tt[3] = tau[2];
-  if (!a.h.use_motor_model) return;
+  if (NO_MOTOR || !a.h.use_motor_model) return;
   // allocation (controller_diff.py:56-69): rows 0-2 / columns 0-2 do not involve kappa; row / column 3 is
   // kappa * (1 -1 1 -1) and its inverse (1 -1 1 -1) / (4 kappa)
   const float sz[4] = {1.0f, -1.0f, 1.0f, -1.0f};
@@ -1113,7 +1115,9 @@ DEV void merge_handover(const float4* xch, int t, bool reset, Env& e) {
 #endif
 // MAXG > 0: tracks of at most MAXG gates (checked at launch).  The 8-gate instantiation (the reference's tracks,
 // BASELINE C3 / C4) runs without scratch (the generic one spills 48 B / lane in its 32-gate sphere loop).
-template <bool USE_LDS, bool OBST, int MAXG = 0>
+// LEAN: BASELINE C3 / C4's configuration compiled in (explicit integrator, no motor model, no rotor-constant DR; the
+// launch checks it)
+template <bool USE_LDS, bool OBST, int MAXG = 0, bool LEAN = false>
 __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
                                                              const float* __restrict__ actions) {
   a.kc = kc;
@@ -1174,18 +1178,18 @@ __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
     for (int k = 0; k < 4; ++k) cmd[k] = th_raw[k] * sc[k] + of[k];
     cmd[0] = cmd[0] * e.thr;
     float tt[4];
-    if (a.h.dr_rotor) {
+    if (!LEAN && a.h.dr_rotor) {
       const float4 rk = reinterpret_cast<const float4*>(a.buf.state)[GR_P_ROTOR * (size_t)n + ii];
       ctbr_compute(a, cmd, e.w, e.al, e.Kp, e.Kd, e.cT, e.ct, e.T, e.tau, e.mw, tt, &rk);
     } else {
-      ctbr_compute(a, cmd, e.w, e.al, e.Kp, e.Kd, e.cT, e.ct, e.T, e.tau, e.mw, tt);
+      ctbr_compute<LEAN>(a, cmd, e.w, e.al, e.Kp, e.Kd, e.cT, e.ct, e.T, e.tau, e.mw, tt);
     }
     const float m = c.dr_plant ? e.mp : e.mc;
     float Jp[3];
     for (int k = 0; k < 3; ++k) Jp[k] = c.dr_plant ? e.J[k] : c.inertia[k];
     float accl[3], al[3];
     int ccount = 0;
-    if (c.integrator == GR_INTEGRATOR_DD_EXPLICIT) {
+    if (LEAN || c.integrator == GR_INTEGRATOR_DD_EXPLICIT) {
       dd_explicit(m, Jp, e.k2, e.k1, tt, dt, c.gravity, e.p, e.q, e.v, e.w, accl, al);
       STAMP(3);
       if (OBST) {  // the policy waves test the obstacles on the post-step pose while this wave tests the gates
@@ -1685,7 +1689,10 @@ static hipError_t launch_env_mode(const KArgs& a, const float* actions, const ui
       const size_t bytes = (size_t)a.h.lds_tab_vec * 16 + (size_t)(GR_XF4 + GR_RF4 + GR_SF4) * GR_BLOCK * 16;
       // tracks of <= 8 gates (the reference's tracks, BASELINE C3 / C4): the sphere pass unrolled to a fixed 8, no
       // scratch (same time as the generic kernel: 9.88-9.98 vs 9.82-9.98 us, gpurun_out/g8.txt)
-      if (lds && a.h.max_gates <= 8)
+      const bool lean = a.h.integrator == GR_INTEGRATOR_DD_EXPLICIT && !a.h.use_motor_model && !a.h.dr_rotor;
+      if (lds && a.h.max_gates <= 8 && lean)
+        hipLaunchKernelGGL((step_kernel<true, false, 8, true>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
+      else if (lds && a.h.max_gates <= 8)
         hipLaunchKernelGGL((step_kernel<true, false, 8>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
       else if (lds)
         hipLaunchKernelGGL((step_kernel<true, false>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
@@ -1750,6 +1757,7 @@ hipError_t launch_test_philox(int n, uint32_t c0, uint32_t c1, uint32_t c2, uint
 hipError_t allow_large_lds() {
   const void* ks[] = {reinterpret_cast<const void*>(&step_kernel<true, false>),
                       reinterpret_cast<const void*>(&step_kernel<true, false, 8>),
+                      reinterpret_cast<const void*>(&step_kernel<true, false, 8, true>),
                       reinterpret_cast<const void*>(&env_kernel<KMODE_RESET, true>),
                       reinterpret_cast<const void*>(&env_kernel<KMODE_OBSERVE, true>)};
   for (const void* k : ks) {
