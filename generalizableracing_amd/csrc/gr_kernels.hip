@@ -1683,8 +1683,12 @@ static hipError_t launch_env_mode(const KArgs& a, const float* actions, const ui
       KArgs b = a;
       b.h.lds_tab_vec = 0;
       const size_t bytes = (size_t)(GR_XF4 + GR_RF4 + GR_SF4 + GR_OF4) * GR_BLOCK * 16 + 16;
-      // (the 8-gate instantiation, 28 B of scratch instead of 64, measured 0.15 us slower here: gpurun_out/o8.txt)
-      hipLaunchKernelGGL((step_kernel<false, true>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, b, b.kc, actions);
+      // (the 8-gate instantiation, 28 B of scratch instead of 64, measured 0.15 us slower here: gpurun_out/o8.txt; the
+      // lean one, C3's configuration compiled in, 12.14-12.17 vs 12.74-12.76 us: gpurun_out/olean.txt)
+      if (a.h.integrator == GR_INTEGRATOR_DD_EXPLICIT && !a.h.use_motor_model && !a.h.dr_rotor)
+        hipLaunchKernelGGL((step_kernel<false, true, 0, true>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, b, b.kc, actions);
+      else
+        hipLaunchKernelGGL((step_kernel<false, true>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, b, b.kc, actions);
     } else {
       const size_t bytes = (size_t)a.h.lds_tab_vec * 16 + (size_t)(GR_XF4 + GR_RF4 + GR_SF4) * GR_BLOCK * 16;
       // tracks of <= 8 gates (the reference's tracks, BASELINE C3 / C4): the sphere pass unrolled to a fixed 8, no
@@ -1758,6 +1762,7 @@ hipError_t allow_large_lds() {
   const void* ks[] = {reinterpret_cast<const void*>(&step_kernel<true, false>),
                       reinterpret_cast<const void*>(&step_kernel<true, false, 8>),
                       reinterpret_cast<const void*>(&step_kernel<true, false, 8, true>),
+                      reinterpret_cast<const void*>(&step_kernel<false, true, 0, true>),
                       reinterpret_cast<const void*>(&env_kernel<KMODE_RESET, true>),
                       reinterpret_cast<const void*>(&env_kernel<KMODE_OBSERVE, true>)};
   for (const void* k : ks) {
