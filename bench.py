@@ -569,7 +569,7 @@ def main():
         rd_o, wr_o = env_o.bytes_per_env_step()
         extra["with_obstacles"] = {
             "value": n * ws * a.steps / secs_o, "unit": "env-steps/s",
-            "kernel": "gr::step_kernel<false, true, 0, true>",
+            "kernel": "gr::step_kernel<false, true, 0, 1>",
             "kernel_us": kt_o["kernel_us"], "bytes_per_env_step": {"read": rd_o, "written": wr_o},
             "achieved_GBps": (rd_o + wr_o) * n / (kt_o["kernel_us"] * 1e-6) / 1e9,
             "frac": (rd_o + wr_o) * n / (kt_o["kernel_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS,
@@ -684,9 +684,9 @@ def main():
                          "read_achieved": rd * n / (us * 1e-6) / 1e9,
                          "read_frac": rd * n / (us * 1e-6) / 1e9 / HBM_PEAK_GBS,
                          "read_frac_definition": "the north star's HBM-read roofline: read bytes only",
-                         "kernel": ("gr::step_kernel<false, true, 0, true>" if a.obstacles else
-                                    "gr::step_kernel<true, false, 8, true>" if a.gates <= 8 and a.integrator == "dd_explicit"
-                                    else f"gr::step_kernel<true, false, {8 if a.gates <= 8 else 0}, false>")
+                         "kernel": ("gr::step_kernel<false, true, 0, 1>" if a.obstacles else
+                                    "gr::step_kernel<true, false, 8, 1>" if a.gates <= 8 and a.integrator == "dd_explicit"
+                                    else f"gr::step_kernel<true, false, {8 if a.gates <= 8 else 0}, 0>")
                                    + " (fused step)", **kt,
                          "algorithmic_bytes_per_launch": (rd + wr) * n,
                          "bytes_per_env_step": {"read": rd, "written": wr}},

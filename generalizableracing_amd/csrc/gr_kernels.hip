@@ -1115,9 +1115,9 @@ DEV void merge_handover(const float4* xch, int t, bool reset, Env& e) {
 #endif
 // MAXG > 0: tracks of at most MAXG gates (checked at launch).  The 8-gate instantiation (the reference's tracks,
 // BASELINE C3 / C4) runs without scratch (the generic one spills 48 B / lane in its 32-gate sphere loop).
-// LEAN: BASELINE C3 / C4's configuration compiled in (explicit integrator, no motor model, no rotor-constant DR; the
-// launch checks it)
-template <bool USE_LDS, bool OBST, int MAXG = 0, bool LEAN = false>
+// LEAN: a configuration compiled in (the launch checks it): 1 = BASELINE C3 / C4 (explicit integrator, no motor model,
+// no rotor-constant DR), 2 = C5's (the same with rotor-constant DR); 0 = every option read at run time
+template <bool USE_LDS, bool OBST, int MAXG = 0, int LEAN = 0>
 __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
                                                              const float* __restrict__ actions) {
   a.kc = kc;
@@ -1178,18 +1178,18 @@ __global__ GR_STEP_LB void step_kernel(KArgs a, const KConst* __restrict__ kc,
     for (int k = 0; k < 4; ++k) cmd[k] = th_raw[k] * sc[k] + of[k];
     cmd[0] = cmd[0] * e.thr;
     float tt[4];
-    if (!LEAN && a.h.dr_rotor) {
+    if (LEAN == 2 || (LEAN == 0 && a.h.dr_rotor)) {
       const float4 rk = reinterpret_cast<const float4*>(a.buf.state)[GR_P_ROTOR * (size_t)n + ii];
-      ctbr_compute(a, cmd, e.w, e.al, e.Kp, e.Kd, e.cT, e.ct, e.T, e.tau, e.mw, tt, &rk);
+      ctbr_compute<LEAN != 0>(a, cmd, e.w, e.al, e.Kp, e.Kd, e.cT, e.ct, e.T, e.tau, e.mw, tt, &rk);
     } else {
-      ctbr_compute<LEAN>(a, cmd, e.w, e.al, e.Kp, e.Kd, e.cT, e.ct, e.T, e.tau, e.mw, tt);
+      ctbr_compute<LEAN != 0>(a, cmd, e.w, e.al, e.Kp, e.Kd, e.cT, e.ct, e.T, e.tau, e.mw, tt);
     }
     const float m = c.dr_plant ? e.mp : e.mc;
     float Jp[3];
     for (int k = 0; k < 3; ++k) Jp[k] = c.dr_plant ? e.J[k] : c.inertia[k];
     float accl[3], al[3];
     int ccount = 0;
-    if (LEAN || c.integrator == GR_INTEGRATOR_DD_EXPLICIT) {
+    if (LEAN != 0 || c.integrator == GR_INTEGRATOR_DD_EXPLICIT) {
       dd_explicit(m, Jp, e.k2, e.k1, tt, dt, c.gravity, e.p, e.q, e.v, e.w, accl, al);
       STAMP(3);
       if (OBST) {  // the policy waves test the obstacles on the post-step pose while this wave tests the gates
@@ -1686,7 +1686,7 @@ static hipError_t launch_env_mode(const KArgs& a, const float* actions, const ui
       // (the 8-gate instantiation, 28 B of scratch instead of 64, measured 0.15 us slower here: gpurun_out/o8.txt; the
       // lean one, C3's configuration compiled in, 12.14-12.17 vs 12.74-12.76 us: gpurun_out/olean.txt)
       if (a.h.integrator == GR_INTEGRATOR_DD_EXPLICIT && !a.h.use_motor_model && !a.h.dr_rotor)
-        hipLaunchKernelGGL((step_kernel<false, true, 0, true>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, b, b.kc, actions);
+        hipLaunchKernelGGL((step_kernel<false, true, 0, 1>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, b, b.kc, actions);
       else
         hipLaunchKernelGGL((step_kernel<false, true>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, b, b.kc, actions);
     } else {
@@ -1695,7 +1695,9 @@ static hipError_t launch_env_mode(const KArgs& a, const float* actions, const ui
       // scratch (same time as the generic kernel: 9.88-9.98 vs 9.82-9.98 us, gpurun_out/g8.txt)
       const bool lean = a.h.integrator == GR_INTEGRATOR_DD_EXPLICIT && !a.h.use_motor_model && !a.h.dr_rotor;
       if (lds && a.h.max_gates <= 8 && lean)
-        hipLaunchKernelGGL((step_kernel<true, false, 8, true>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
+        hipLaunchKernelGGL((step_kernel<true, false, 8, 1>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
+      // (C5's configuration compiled in, LEAN = 2 on 32-gate tracks with rotor DR: 11.83-11.93 vs 11.77-11.93 us,
+      // gpurun_out/c5l.jsonl; not launched)
       else if (lds && a.h.max_gates <= 8)
         hipLaunchKernelGGL((step_kernel<true, false, 8>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
       else if (lds)
@@ -1761,8 +1763,8 @@ hipError_t launch_test_philox(int n, uint32_t c0, uint32_t c1, uint32_t c2, uint
 hipError_t allow_large_lds() {
   const void* ks[] = {reinterpret_cast<const void*>(&step_kernel<true, false>),
                       reinterpret_cast<const void*>(&step_kernel<true, false, 8>),
-                      reinterpret_cast<const void*>(&step_kernel<true, false, 8, true>),
-                      reinterpret_cast<const void*>(&step_kernel<false, true, 0, true>),
+                      reinterpret_cast<const void*>(&step_kernel<true, false, 8, 1>),
+                      reinterpret_cast<const void*>(&step_kernel<false, true, 0, 1>),
                       reinterpret_cast<const void*>(&env_kernel<KMODE_RESET, true>),
                       reinterpret_cast<const void*>(&env_kernel<KMODE_OBSERVE, true>)};
   for (const void* k : ks) {

@@ -18,7 +18,7 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "gr::step_kernel<true, false, 8, true>"  # <USE_LDS, OBST, MAXG, LEAN>; --obstacles: <false, true, 0, true>
+KERNEL = "gr::step_kernel<true, false, 8, 1>"  # <USE_LDS, OBST, MAXG, LEAN>; --obstacles: <false, true, 0, 1>
 
 
 def pmc_means(prof):
@@ -50,7 +50,7 @@ def main():
     a = p.parse_args()
     global KERNEL
     if a.obstacles:
-        KERNEL = "gr::step_kernel<false, true, 0, true>"
+        KERNEL = "gr::step_kernel<false, true, 0, 1>"
         a.read_bytes += 16
         a.write_bytes += 16
     prof = os.path.join(ROOT, "gpurun_out", f"prof_{a.tag}")
