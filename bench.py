@@ -244,12 +244,14 @@ def policy_in_loop_graphed(env, steps, device):
     return n * reps * ACTION_RING / (time.perf_counter() - t0)
 
 
-def policy_in_loop_fused(env, steps, device, precision="bf16", actor_only=False):
+def policy_in_loop_fused(env, steps, device, precision="bf16", actor_only=False, sink_ring=None):
     """C5 "hipGraph-captured step + inference": per step, the fused MFMA inference of both MLPs
     (FusedPolicyInference: actor mean + Gaussian sample + log prob, critic value; bf16 operands with fp32
     accumulation, or fp32 operands on fp32 MFMA = the reference's precision) on the step's observations,
     then gr_step on the sampled actions; 64 such steps are captured in one hipGraph and replayed.  actor_only:
     the actor network alone (mean, sample, log prob; no value), the inference an env-only rollout needs.
+    sink_ring: [ACTION_RING, 2, n, 16] bf16 rollout rows; step k of the graph writes its observation rows into slot
+    k (gr_bind_obs_sink rebound per step, as the runner rebinds it to the storage slot of each transition).
     Returns (env-steps/s, per-launch us of the inference kernel, its useful TFLOP/s)."""
     from generalizableracing_amd.rsl_rl import ActorCritic
     from generalizableracing_amd.rsl_rl.fused_inference import FusedPolicyInference
@@ -260,6 +262,9 @@ def policy_in_loop_fused(env, steps, device, precision="bf16", actor_only=False)
 
     def one_step(obs):
         acts = fused.act(obs["policy"], None if actor_only else obs["critic"])[0]
+        if sink_ring is not None:
+            slot = sink_ring[env._calls % ACTION_RING]
+            env.set_obs_sink(slot[0], slot[1])
         return env.step(acts)[0]
 
     obs = env.observe()
@@ -288,6 +293,8 @@ def policy_in_loop_fused(env, steps, device, precision="bf16", actor_only=False)
         g.replay()
     torch.cuda.synchronize()
     rate = n * reps * ACTION_RING / (time.perf_counter() - t0)
+    if sink_ring is not None:
+        env.set_obs_sink(None)
     # the inference kernel alone (events on the current stream, 64 back-to-back launches)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     x = obs["policy"].clone()
@@ -473,6 +480,40 @@ def load_traffic(n, gates, obstacles):
     return None
 
 
+# the PPO gradient exchange of one mini-batch step: actor 71 172 + critic 70 401 + std 4 parameters + the KL slot
+# (rsl_rl/distributed.py FlatGrads), 566 KB of fp32
+GRAD_ALLREDUCE_NUMEL = 71172 + 70401 + 4 + 1
+
+
+def device_identity(device) -> dict:
+    """This rank's device: torch's current device index, the PCI address (so a scaling line shows one distinct GPU
+    per rank) and the device name."""
+    idx = torch.cuda.current_device()
+    p = torch.cuda.get_device_properties(torch.device(device))
+    pci = None
+    if hasattr(p, "pci_bus_id"):
+        pci = f"{getattr(p, 'pci_domain_id', 0):04x}:{p.pci_bus_id:02x}:{getattr(p, 'pci_device_id', 0):02x}"
+    return {"current_device": idx, "pci": pci, "name": p.name, "uuid": str(getattr(p, "uuid", "")) or None}
+
+
+def allreduce_latency_us(device, reps=50, warm=10) -> float:
+    """Median wall latency of one in-place all_reduce of the PPO update's flat gradient buffer (566 KB fp32), each
+    call synchronised, after `warm` untimed calls: what every mini-batch step of a data-parallel update pays."""
+    dev = device if dist.get_backend() == "nccl" else "cpu"
+    buf = torch.ones(GRAD_ALLREDUCE_NUMEL, dtype=torch.float32, device=dev)
+    lat = []
+    for k in range(warm + reps):
+        if dev != "cpu":
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dist.all_reduce(buf)
+        if dev != "cpu":
+            torch.cuda.synchronize()
+        if k >= warm:
+            lat.append((time.perf_counter() - t0) * 1e6)
+    return float(np.median(lat))
+
+
 def main():
     a = parse()
     ws = int(os.environ.get("WORLD_SIZE", "1"))
@@ -495,6 +536,7 @@ def main():
         env.step(actions[k % ACTION_RING])
     torch.cuda.synchronize()
     secs, mode, graph = time_env_steps(env, actions, a.steps, not a.no_graph)
+    local_secs = secs
     secs = max_over_ranks(secs, device)
     value = n * ws * a.steps / secs
     if graph is None:  # --no-graph: the timed region ran eager, the kernel is still timed from graph replays
@@ -515,6 +557,20 @@ def main():
     progress(f"headline: {value:.4g} env-steps/s, kernel {us:.2f} us")
     extra = {"steady_state_env_steps_per_s_per_gpu": steady,
              "steady_state_note": "median of 3 timed runs of 1024 steps (16 replays of the 64-step graph), one rank"}
+    if ws > 1:
+        # a scaling line that proves what it ran: the backend, one record per rank (its device and PCI address, its
+        # own step rate over the timed region) and the latency of the update's one collective on this group
+        me = {"rank": rank, **device_identity(device), "env_steps_per_s": n * a.steps / local_secs,
+              "timed_region_s": local_secs}
+        ranks = [None] * ws
+        dist.all_gather_object(ranks, me)
+        extra["distributed"] = {
+            "world_size": ws, "backend": dist.get_backend(), "ranks": ranks,
+            "distinct_devices": len({(r["pci"], r["uuid"], r["current_device"]) for r in ranks}),
+            "grad_allreduce_bytes": GRAD_ALLREDUCE_NUMEL * 4,
+            "grad_allreduce_median_us": allreduce_latency_us(device),
+            "note": "value = world_size x envs x steps / max over ranks of the timed region; ranks[i].env_steps_per_s "
+                    "is rank i's own rate"}
     if not a.no_extras:
         rate_e, us_e, tfs_e = policy_in_loop_fused(env, 1024, device, precision="fp32", actor_only=True)
         extra["env_only_fp32"] = {
@@ -591,7 +647,6 @@ def main():
         graph_c5 = capture_graph(env_c5, actions)
         kt_c5 = kernel_timing(graph_c5)
         del graph_c5
-        rate_c5, us_c5, _ = policy_in_loop_fused(env_c5, 512, device)
         # the step kernel also writing the bf16 rollout rows (gr_bind_obs_sink: the runner's storage slot)
         sink = torch.empty(2, n, 16, device=device, dtype=torch.bfloat16)
         env_c5.set_obs_sink(sink[0], sink[1])
@@ -600,13 +655,32 @@ def main():
         del graph_c5s
         rd_c5s, wr_c5s = env_c5.bytes_per_env_step()
         env_c5.set_obs_sink(None)
+        del sink
+        # C5 as specified: bf16 BUFFERS (the step writes each transition's bf16 rows into its own storage slot of a
+        # 64-slot ring), the policy at the reference's fp32 (actor + critic on fp32 MFMA), hipGraph of 64 x
+        # [inference + step]
+        ring = torch.empty(ACTION_RING, 2, n, 16, device=device, dtype=torch.bfloat16)
+        rate_c5_32, us_c5_32, tfs_c5_32 = policy_in_loop_fused(env_c5, 512, device, precision="fp32", sink_ring=ring)
+        # option: the same with the bf16-operand MLP (not the reference's arithmetic)
+        rate_c5, us_c5, _ = policy_in_loop_fused(env_c5, 512, device, sink_ring=ring)
+        del ring
         extra["c5_32_gates"] = {"dr": "plant/controller mass, inertia, drag, thrust error, rotor constants "
                                       "(thrust map, kappa x U(0.9, 1.1))",
                                 "step_kernel_us": kt_c5["kernel_us"], "step_env_steps_per_s": n / (kt_c5["kernel_us"] * 1e-6),
-                                "step_plus_fused_inference_env_steps_per_s": rate_c5, "inference_kernel_us": us_c5,
-                                "launch": "hipgraph (64 x [fused inference + gr_step])",
+                                "step_plus_fused_fp32_inference_env_steps_per_s": rate_c5_32,
+                                "fp32_inference_kernel": "gr::policy_f32_kernel<256>, actor + critic (MFMA 16x16x4 "
+                                                         "f32: the reference's precision)",
+                                "fp32_inference_kernel_us": us_c5_32, "fp32_inference_TFLOPs": tfs_c5_32,
+                                "fp32_inference_frac_of_fp32_mfma_peak": tfs_c5_32 / FP32_MFMA_PEAK_TFS,
+                                "option_step_plus_fused_bf16_mlp_inference_env_steps_per_s": rate_c5,
+                                "option_bf16_mlp_inference_kernel_us": us_c5,
+                                "launch": "hipgraph (64 x [fused inference + gr_step writing its bf16 rows into "
+                                          "slot k of a 64-slot rollout ring])",
                                 "step_kernel_us_bf16_obs_sink": kt_c5s["kernel_us"],
-                                "bytes_per_env_step_bf16_obs_sink": {"read": rd_c5s, "written": wr_c5s}}
+                                "bytes_per_env_step_bf16_obs_sink": {"read": rd_c5s, "written": wr_c5s},
+                                "note": "C5 = bf16 obs / rollout buffers with the policy in fp32 (the headline "
+                                        "C5 figure); the bf16-MLP figure is an option, not the reference's "
+                                        "arithmetic"}
         env_c5.close()
         progress("c5_32_gates")
     if not a.no_extras:

@@ -215,6 +215,9 @@ GR_POLICY_BF16, GR_POLICY_FP32 = 0, 1
 GR_POLICY_LRELU_PRESCALE = 0.505
 GR_CAM_STEP, GR_CAM_RESET, GR_CAM_OBSERVE = 0, 1, 2
 GR_DTYPE_F32, GR_DTYPE_BF16 = 0, 1
+GR_STEP_L2, GR_STEP_LDS, GR_STEP_LDS8, GR_STEP_LDS8_LEAN, GR_STEP_OBST, GR_STEP_OBST_LEAN = range(6)
+STEP_KERNEL_NAMES = ["step_kernel<false, false>", "step_kernel<true, false>", "step_kernel<true, false, 8>",
+                     "step_kernel<true, false, 8, 1>", "step_kernel<false, true>", "step_kernel<false, true, 0, 1>"]
 GR_STATUS_OBST_WAIT_TIMEOUT = 1
 GR_FAULT_NONE, GR_FAULT_OBST_NO_SIGNAL = 0, 1
 STATUS_TEXT = {GR_STATUS_OBST_WAIT_TIMEOUT: "a physics wave gave up waiting for its obstacle mask (stale mask used)"}
@@ -222,7 +225,7 @@ STATUS_TEXT = {GR_STATUS_OBST_WAIT_TIMEOUT: "a physics wave gave up waiting for 
 EXPORTS = [
     "gr_abi_version", "gr_config_default", "gr_config_size", "gr_create", "gr_destroy", "gr_last_error",
     "gr_num_blocks", "gr_num_log_rows", "gr_log_finalize", "gr_bytes_per_env_step", "gr_bind_tracks", "gr_bind_obstacles", "gr_swap_terrain", "gr_bind_buffers", "gr_bind_obs_sink", "gr_init", "gr_reset",
-    "gr_step", "gr_observe", "gr_device_status", "gr_test_inject_fault", "gr_set_timing", "gr_read_timing", "gr_test_dynamics", "gr_test_math",
+    "gr_step", "gr_observe", "gr_step_kernel_variant", "gr_device_status", "gr_test_inject_fault", "gr_set_timing", "gr_read_timing", "gr_test_dynamics", "gr_test_math",
     "gr_test_philox",
     "gr_debug_read_stamps", "gr_debug_read_policy_stamps",
     "gr_camera_config_default", "gr_camera_config_size", "gr_enable_camera", "gr_bind_camera_buffers",
@@ -261,6 +264,7 @@ def _declare(lib):
         "gr_reset": (C.c_int, [vp, vp, vp]),
         "gr_step": (C.c_int, [vp, vp, vp]),
         "gr_observe": (C.c_int, [vp, vp]),
+        "gr_step_kernel_variant": (C.c_int, [vp]),
         "gr_device_status": (C.c_int, [vp, C.POINTER(C.c_uint32), C.c_int, vp]),
         "gr_test_inject_fault": (C.c_int, [vp, C.c_int]),
         "gr_set_timing": (C.c_int, [vp, C.c_int]),

@@ -532,6 +532,8 @@ int gr_step(gr_ctx* c, const float* actions, void* stream) {
   return e == hipSuccess ? GR_OK : hip_fail(c, e, "gr_step");
 }
 
+int gr_step_kernel_variant(const gr_ctx* c) { return c ? gr::step_variant(c->args) : GR_ERR_ARG; }
+
 int gr_device_status(gr_ctx* c, uint32_t* status, int clear, void* stream) {
   if (!c || !status) return fail(c, GR_ERR_ARG, "gr_device_status: null argument");
   *status = 0;

@@ -172,6 +172,8 @@ inline size_t camera_lds_bytes(int width, int height, int max_gates, bool obst) 
               4 * ((size_t)max_gates * 24 + camera_tile_mask_floats(width, height) + os + 8 * (size_t)width));
 }
 
+// which step_kernel instantiation gr_step launches for these arguments (GR_STEP_* of gr.h)
+int step_variant(const KArgs& a);
 hipError_t launch_env(int mode, const KArgs& a, const float* actions, const uint8_t* mask, hipStream_t s,
                       hipEvent_t t0, hipEvent_t t1);
 hipError_t launch_init(const KArgs& a, hipStream_t s);

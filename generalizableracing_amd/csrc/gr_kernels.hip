@@ -1670,13 +1670,21 @@ __global__ void test_philox_kernel(int n, uint32_t c0, uint32_t c1, uint32_t c2,
 // ------------------------------------------------------------- launchers
 static int grid_of(int n) { return (n + GR_BLOCK - 1) / GR_BLOCK; }
 
+int step_variant(const KArgs& a) {
+  const bool lean = a.h.integrator == GR_INTEGRATOR_DD_EXPLICIT && !a.h.use_motor_model && !a.h.dr_rotor;
+  if (a.obst_items != nullptr) return lean ? GR_STEP_OBST_LEAN : GR_STEP_OBST;
+  if (a.h.lds_tab_vec <= 0) return GR_STEP_L2;
+  if (a.h.max_gates <= 8) return lean ? GR_STEP_LDS8_LEAN : GR_STEP_LDS8;
+  return GR_STEP_LDS;
+}
+
 template <int MODE>
 static hipError_t launch_env_mode(const KArgs& a, const float* actions, const uint8_t* mask, hipStream_t s) {
   const int g = grid_of(a.h.num_envs);
   const bool lds = a.h.lds_tab_vec > 0;
   if constexpr (MODE == KMODE_STEP) {
-    const bool obst = a.obst_items != nullptr;
-    if (obst) {
+    const int v = step_variant(a);
+    if (v == GR_STEP_OBST_LEAN || v == GR_STEP_OBST) {
       // Obstacle tracks read the (L2-resident) track table directly: the workgroup barrier stays for the pose
       // hand-over, and without the slice staging a launch takes 12.3 us instead of 13.1 (65 536 envs).
       // Gate-only tracks time the same either way (9.8-9.9 us) and keep the LDS slice.
@@ -1685,7 +1693,7 @@ static hipError_t launch_env_mode(const KArgs& a, const float* actions, const ui
       const size_t bytes = (size_t)(GR_XF4 + GR_RF4 + GR_SF4 + GR_OF4) * GR_BLOCK * 16 + 16;
       // (the 8-gate instantiation, 28 B of scratch instead of 64, measured 0.15 us slower here: gpurun_out/o8.txt; the
       // lean one, C3's configuration compiled in, 12.14-12.17 vs 12.74-12.76 us: gpurun_out/olean.txt)
-      if (a.h.integrator == GR_INTEGRATOR_DD_EXPLICIT && !a.h.use_motor_model && !a.h.dr_rotor)
+      if (v == GR_STEP_OBST_LEAN)
         hipLaunchKernelGGL((step_kernel<false, true, 0, 1>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, b, b.kc, actions);
       else
         hipLaunchKernelGGL((step_kernel<false, true>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, b, b.kc, actions);
@@ -1693,14 +1701,13 @@ static hipError_t launch_env_mode(const KArgs& a, const float* actions, const ui
       const size_t bytes = (size_t)a.h.lds_tab_vec * 16 + (size_t)(GR_XF4 + GR_RF4 + GR_SF4) * GR_BLOCK * 16;
       // tracks of <= 8 gates (the reference's tracks, BASELINE C3 / C4): the sphere pass unrolled to a fixed 8, no
       // scratch (same time as the generic kernel: 9.88-9.98 vs 9.82-9.98 us, gpurun_out/g8.txt)
-      const bool lean = a.h.integrator == GR_INTEGRATOR_DD_EXPLICIT && !a.h.use_motor_model && !a.h.dr_rotor;
-      if (lds && a.h.max_gates <= 8 && lean)
+      if (v == GR_STEP_LDS8_LEAN)
         hipLaunchKernelGGL((step_kernel<true, false, 8, 1>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
       // (C5's configuration compiled in, LEAN = 2 on 32-gate tracks with rotor DR: 11.83-11.93 vs 11.77-11.93 us,
       // gpurun_out/c5l.jsonl; not launched)
-      else if (lds && a.h.max_gates <= 8)
+      else if (v == GR_STEP_LDS8)
         hipLaunchKernelGGL((step_kernel<true, false, 8>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
-      else if (lds)
+      else if (v == GR_STEP_LDS)
         hipLaunchKernelGGL((step_kernel<true, false>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);
       else
         hipLaunchKernelGGL((step_kernel<false, false>), dim3(g), dim3(3 * GR_BLOCK), bytes, s, a, a.kc, actions);

@@ -590,6 +590,12 @@ hipError_t launch_in_backward(const float* gh, const float* hv, const float* x, 
 // torch.max of two tensors splits the gradient in half on ties; clamp passes it on [lo, hi] inclusive.
 constexpr float LOG_SQRT_2PI = 0.918938533204672741780f;
 
+// torch.clamp / torch.max keep a NaN operand (fminf / fmaxf would drop it)
+__device__ __forceinline__ float clamp_keep_nan(float x, float lo, float hi) {
+  return x != x ? x : fminf(fmaxf(x, lo), hi);
+}
+__device__ __forceinline__ float max_keep_nan(float a, float b) { return (a != a || b != b) ? a + b : fmaxf(a, b); }
+
 struct LossRow {
   float logp, ratio, s1, s2, v, vc, ret, vdiff;
 };
@@ -613,14 +619,14 @@ __device__ __forceinline__ void pl_row(const gr_ppo_loss_args& a, long long i, c
   r.logp = lp;
   r.ratio = expf(lp - a.logp_old[i * a.ld_logp_old]);
   const float A = a.adv[i * a.ld_adv];
-  const float rc = fminf(fmaxf(r.ratio, 1.0f - a.clip), 1.0f + a.clip);
+  const float rc = clamp_keep_nan(r.ratio, 1.0f - a.clip, 1.0f + a.clip);
   r.s1 = -A * r.ratio;
   r.s2 = -A * rc;
   r.v = a.value[i * a.ld_value];
   r.ret = a.ret[i * a.ld_ret];
   const float vo = a.value_old[i * a.ld_value_old];
   r.vdiff = r.v - vo;
-  r.vc = vo + fminf(fmaxf(r.vdiff, -a.clip), a.clip);
+  r.vc = vo + clamp_keep_nan(r.vdiff, -a.clip, a.clip);
 }
 
 __device__ __forceinline__ float pl_wave_sum(float v) {
@@ -639,9 +645,9 @@ __global__ __launch_bounds__(256) void ppo_loss_forward(gr_ppo_loss_args a, floa
     LossRow r;
     float kl;
     pl_row(a, i, sd, r, &kl);
-    t[0] = fmaxf(r.s1, r.s2);
+    t[0] = max_keep_nan(r.s1, r.s2);
     const float l1 = (r.v - r.ret) * (r.v - r.ret), l2 = (r.vc - r.ret) * (r.vc - r.ret);
-    t[1] = a.clipped_value ? fmaxf(l1, l2) : (r.ret - r.v) * (r.ret - r.v);
+    t[1] = a.clipped_value ? max_keep_nan(l1, l2) : (r.ret - r.v) * (r.ret - r.v);
     t[2] = kl;
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -823,7 +829,7 @@ __global__ __launch_bounds__(256) void adam_clip_apply(gr_adam_args a, float max
   __syncthreads();
   const float norm = (float)sqrt((sm[0] + sm[1]) + (sm[2] + sm[3]));
   float c = max_norm / (norm + 1.0e-6f);
-  c = c < 1.0f ? c : 1.0f;
+  c = (c < 1.0f || c != c) ? c : 1.0f;  // torch.clamp(clip_coef, max=1.0) keeps a NaN (non-finite gradients)
   const int b = blockIdx.x, s = adam_segment_of(a, b);
   if (b == 0 && threadIdx.x == 0 && norm_out) norm_out[0] = norm;
   const gr_adam_segment g = a.seg[s];  // (a copy: scalar loads, no reload after the stores)

@@ -431,6 +431,13 @@ class RacingEnv:
         self._call("gr_bytes_per_env_step", C.byref(r), C.byref(w))
         return r.value, w.value
 
+    def step_kernel_name(self) -> str:
+        """The step_kernel instantiation gr_step launches with the current bindings (gr_step_kernel_variant)."""
+        v = self._lib.gr_step_kernel_variant(self._ctx)
+        if v < 0:
+            raise RuntimeError(f"gr_step_kernel_variant failed (status {v})")
+        return _abi.STEP_KERNEL_NAMES[v]
+
     def device_status(self, clear: bool = True) -> int:
         """gr_device_status: the GR_STATUS_* bits the step kernels raised since the last clear (synchronises the
         env's stream)."""

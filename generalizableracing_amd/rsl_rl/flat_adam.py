@@ -166,6 +166,23 @@ class FlatAdam(torch.optim.Optimizer):
                     torch.autograd.graph.increment_version(p)
         return loss
 
+    def state_dict(self):
+        """torch.optim.Adam's non-capturable layout, so the reference runner (on_policy_runner.py:319) can load a
+        checkpoint into torch.optim.Adam and step it: `lr` a Python float (the graphed update binds a device tensor
+        into the group), `capturable` False, each `step` a CPU fp32 scalar tensor and the moments standalone copies
+        (not views of the flat buffers, which torch.save would write whole for every view)."""
+        sd = super().state_dict()
+        for g in sd["param_groups"]:
+            lr = g["lr"]
+            g["lr"] = float(lr) if torch.is_tensor(lr) else lr
+            g["capturable"] = False
+        state = {}
+        for idx, st in sd["state"].items():
+            state[idx] = {"step": st["step"].detach().to("cpu", torch.float32).clone().reshape(()),
+                          "exp_avg": st["exp_avg"].detach().clone(), "exp_avg_sq": st["exp_avg_sq"].detach().clone()}
+        sd["state"] = state
+        return sd
+
     def load_state_dict(self, state_dict):
         """torch.optim.Adam's state_dict (or FlatAdam's): group settings and, per parameter with state, the step
         count and moments copied into the flat buffers (the state's tensors stay views of them)."""

@@ -190,7 +190,9 @@ class PPO:
         """Find the parameters the loss does not reach (e.g. VisionActorCritic's aux_decoder) and take them out of
         the flat gradient buffer, with `.grad` None: the reference's `zero_grad()` leaves their `.grad` None and
         Adam skips them (ppo.py:178-181), where a bound zero `.grad` would count an Adam step for them (and step
-        them by their moments if they ever had any).  Checked once, on the first mini-batch."""
+        them by their moments if they ever had any).  Checked once, on the first mini-batch: the set of parameters
+        the loss reaches must not change afterwards.  The eager update raises if a dropped parameter later receives a
+        gradient (PPO.update); the graphed update differentiates only the parameters kept here."""
         if grads is None:
             grads = torch.autograd.grad(loss, params, retain_graph=True, allow_unused=True)
         self._unused = {id(p) for p, g in zip(params, grads) if g is None}
@@ -234,6 +236,10 @@ class PPO:
                 flat = self._check_all_grads(loss, params)
                 flat.bind()
             loss.backward()
+            if self._unused and any(p.grad is not None for p in params if id(p) in self._unused):
+                raise RuntimeError("PPO.update: a parameter the loss did not reach on the first mini-batch now has a "
+                                   "gradient; the set of parameters the loss reaches must be fixed from the first "
+                                   "mini-batch (it is checked once: _check_all_grads)")
             gdist.allreduce_grads(params, flat)
             _fadam.clip_grad_norm_(self.optimizer, params, self.max_grad_norm)
             self.optimizer.step()
@@ -326,7 +332,8 @@ class _GraphedStep:
         self.flat = alg.flat_grads()
         self.idx = torch.zeros(self.mb, dtype=torch.long, device=dev)
         self.cols = st.sample_columns()  # packed sample rows (None: gathered field by field)
-        self.pack = st.pack_samples() if self.cols is not None else None  # persistent: the graphs read it
+        # persistent: the graphs read it (the storage's own packed buffer, shared with the eager generator)
+        self.pack = st.pack_samples(out=st.packed_buffer()) if self.cols is not None else None
         self.acc = torch.zeros(2, device=dev)  # the update's sums of the surrogate and value means
         self.one = torch.ones((), device=dev)
         self.segmented = gdist.is_dist() or alg.graph_update_segmented

@@ -193,10 +193,20 @@ class RolloutStorage:
         (the fields one by one were nine gathers of 4-64-byte rows per mini-batch, each latency-bound:
         profiles/round03_update65536_graphed_kernel_stats.csv).  Pure data movement: the mini-batches are
         the same values."""
-        src = [x.float() for x in self.sample_sources()]
-        if out is None:
-            return torch.cat(src, dim=1)
-        return torch.cat(src, dim=1, out=out)
+        src = [x.detach().float() for x in self.sample_sources()]
+        with torch.no_grad():
+            if out is None:
+                return torch.cat(src, dim=1)
+            return torch.cat(src, dim=1, out=out)
+
+    def packed_buffer(self):
+        """The persistent [T * N, packed width] fp32 buffer pack_samples fills (allocated on first use)."""
+        cols = self.sample_columns()
+        shape = (self.num_transitions_per_env * self.num_envs, cols[-1][1])
+        buf = getattr(self, "_packed", None)
+        if buf is None or tuple(buf.shape) != shape:
+            buf = self._packed = torch.empty(shape, dtype=torch.float32, device=self.device)
+        return buf
 
     def mini_batch_generator(self, num_mini_batches, num_epochs=8):
         """rollout_storage.py:152-191: one randperm, `num_epochs` passes of `num_mini_batches` chunks."""
@@ -206,8 +216,10 @@ class RolloutStorage:
         mini_batch_size = batch_size // num_mini_batches
         indices = torch.randperm(num_mini_batches * mini_batch_size, requires_grad=False, device=self.device)
         cols = self.sample_columns()
-        if cols is not None:
-            pack = self.pack_samples()
+        if cols is not None and self.observations.dtype == torch.float32:
+            # one persistent packed buffer (fp32 storage only: packing bf16 observations would upcast the whole
+            # rollout and undo what the bf16 storage saves; those are gathered field by field below)
+            pack = self.pack_samples(out=self.packed_buffer())
             for _ in range(num_epochs):
                 for i in range(num_mini_batches):
                     g = pack.index_select(0, indices[i * mini_batch_size:(i + 1) * mini_batch_size])

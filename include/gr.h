@@ -323,6 +323,15 @@ int gr_reset(gr_ctx* ctx, const uint8_t* mask, void* stream);
 int gr_step(gr_ctx* ctx, const float* actions, void* stream);
 /* recompute observations (fresh observation noise), no state change */
 int gr_observe(gr_ctx* ctx, void* stream);
+/* Which step_kernel instantiation gr_step launches with the current bindings (so a test can assert it checks the
+ * kernel a benchmark times).  Same selection as the launcher (gr_kernels.hip step_variant). */
+#define GR_STEP_L2 0          /* step_kernel<false, false>: track table read from L2 (too large for the LDS slice) */
+#define GR_STEP_LDS 1         /* step_kernel<true, false>: LDS track slice, any gate count */
+#define GR_STEP_LDS8 2        /* step_kernel<true, false, 8>: LDS slice, tracks of <= 8 gates */
+#define GR_STEP_LDS8_LEAN 3   /* step_kernel<true, false, 8, 1>: + C3's configuration compiled in (the bench headline) */
+#define GR_STEP_OBST 4        /* step_kernel<false, true>: obstacle tracks */
+#define GR_STEP_OBST_LEAN 5   /* step_kernel<false, true, 0, 1>: obstacle tracks, C3's configuration */
+int gr_step_kernel_variant(const gr_ctx* ctx);
 
 /* Depth camera.  gr_enable_camera validates the cfg and derives its constants (once);
  * gr_bind_camera_buffers binds the image outputs of the next render (rebind per call like

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 4, first GPU call: the new / changed GPU tests, then the default bench line.  Usage: gpu_r4a.sh TAG
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/${1:-r4a}
+mkdir -p $OUT
+cd $R
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+  "tests/test_gpu_parity.py::test_full_size_teacher_forced_slices" tests/test_gpu_bench_multirank.py \
+  tests/test_gpu_graph_update.py tests/test_gpu_units.py > $OUT/pytest_gpu.log 2>&1
+rc=$?; echo "pytest exit $rc" >> $OUT/pytest_gpu.log; [ $rc -ne 0 ] && exit 10
+timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || exit 12
+echo done > $OUT/done

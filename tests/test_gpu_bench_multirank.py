@@ -34,3 +34,11 @@ def test_bench_two_ranks_gloo():
     # the value counts both shards: 2 x 8192 envs x steps / max-over-ranks time
     assert abs(line["value"] - 2 * 8192 * 128 / (line["ms_per_step"] * 1e-3 * 128)) < 1e-6 * line["value"]
     assert line["cpu_baseline"] is None and "policy_in_loop_fused" not in line
+    # the line proves what ran: backend, per-rank device and rate, the update collective's latency on this group
+    d = line["distributed"]
+    assert d["world_size"] == 2 and d["backend"] == "gloo"
+    assert [r["rank"] for r in d["ranks"]] == [0, 1]
+    for r in d["ranks"]:
+        assert r["current_device"] == 0 and r["env_steps_per_s"] > 0 and "pci" in r and r["name"]
+        assert r["env_steps_per_s"] >= 8192 * 128 / (line["ms_per_step"] * 1e-3 * 128) * (1 - 1e-6)
+    assert d["grad_allreduce_bytes"] == 566_312 and d["grad_allreduce_median_us"] > 0

@@ -176,3 +176,65 @@ def test_graphed_update_across_iterations():
                 for key in ("exp_avg", "exp_avg_sq", "step"):
                     sg[key].copy_(se[key])
         alg_g.learning_rate = alg.learning_rate
+
+
+def test_graphed_checkpoint_loads_into_torch_adam(tmp_path):
+    """after a graphed update (FlatAdam's group holds the rate as a device tensor) a checkpoint's
+    optimizer state must load into a plain torch.optim.Adam — what the reference runner does on resume
+    (on_policy_runner.py:319) — and step it; and resume into FlatAdam with the same moments."""
+    from generalizableracing_amd.rsl_rl.flat_adam import FlatAdam
+
+    torch.manual_seed(6)
+    n = 1024
+    env = RslRlVecEnvWrapper(RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV))))
+    cfg = QuadcopterPPORunnerCfg(device=DEV, num_steps_per_env=8)
+    cfg.algorithm.graph_update = True
+    runner = OnPolicyRunner(env, cfg.to_dict(), log_dir=None, device=DEV)
+    runner.learn(2)
+    alg = runner.alg
+    assert isinstance(alg.optimizer, FlatAdam) and torch.is_tensor(alg.optimizer.param_groups[0]["lr"])
+    path = tmp_path / "model.pt"
+    runner.save(str(path))
+    ck = torch.load(str(path), weights_only=True)
+    osd = ck["optimizer_state_dict"]
+    g = osd["param_groups"][0]
+    assert isinstance(g["lr"], float) and g["capturable"] is False
+    for st in osd["state"].values():
+        assert st["step"].device.type == "cpu" and st["step"].dim() == 0 and float(st["step"]) >= 1
+    pol = copy.deepcopy(alg.policy)
+    adam = torch.optim.Adam(pol.parameters(), lr=1e-3)
+    adam.load_state_dict(osd)
+    for p in pol.parameters():
+        p.grad = torch.randn_like(p) * 1e-3
+    adam.step()  # the first foreach step raised 'lr as a Tensor is not supported' before the fix
+    assert all(torch.isfinite(p).all() for p in pol.parameters())
+    # and back into FlatAdam: same moments and step counts
+    fa = FlatAdam(list(alg.policy.parameters()), lr=1e-3)
+    fa.load_state_dict(osd)
+    for p, q in zip(alg.policy.parameters(), fa.param_groups[0]["params"]):
+        s0, s1 = alg.optimizer.state[p], fa.state[q]
+        assert torch.equal(s0["exp_avg"], s1["exp_avg"]) and torch.equal(s0["exp_avg_sq"], s1["exp_avg_sq"])
+        assert float(s0["step"]) == float(s1["step"])
+    env.close()
+
+
+def test_flat_adam_clip_keeps_nan_like_torch():
+    """a non-finite gradient makes torch's clip coefficient NaN and clip_grad_norm_ turns every gradient
+    NaN; FlatAdam's clip must fail the same way (not leave the finite tensors unscaled)."""
+    from generalizableracing_amd.rsl_rl.flat_adam import FlatAdam
+
+    torch.manual_seed(1)
+    ps = [torch.nn.Parameter(torch.randn(300, device=DEV)) for _ in range(3)]
+    qs = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    for p, q in zip(ps, qs):
+        p.grad = torch.randn_like(p)
+        q.grad = p.grad.clone()
+    ps[1].grad[7] = float("nan")
+    qs[1].grad[7] = float("nan")
+    fa = FlatAdam(ps, lr=1e-3)
+    n_fa = fa.clip_grad_norm_(1.0)
+    n_t = torch.nn.utils.clip_grad_norm_(qs, 1.0)
+    torch.cuda.synchronize()
+    assert torch.isnan(n_fa) and torch.isnan(n_t)
+    for p, q in zip(ps, qs):
+        assert torch.isnan(p.grad).all() and torch.isnan(q.grad).all()

@@ -153,41 +153,91 @@ def test_ragged_env_counts_bit_exact(n):
     env.close()
 
 
-def test_full_size_teacher_forced_slices():
-    """65 536 envs (BASELINE C3 size): every step, a slice of envs is re-stepped by the oracle from the
-    kernel's own pre-step state (teacher forcing) and must match bit-for-bit; size-independent
-    invariants are checked on all envs."""
-    n, steps, m = 65536, 220, 256
-    env, _ = make(n)
+GRAPH_LEN = 64  # bench.py ACTION_RING: the headline is timed as replays of a 64-step hipGraph
+
+
+def capture_step_graph(env, actions):
+    """The bench's capture (bench.py capture_graph): the host call counter aligned to a multiple of the ring,
+    then GRAPH_LEN consecutive env steps on actions[0..GRAPH_LEN) captured in one hipGraph."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for k in range(2):
+            env.step(actions[k])
+    torch.cuda.current_stream().wait_stream(s)
+    while env._calls % GRAPH_LEN != 0:
+        env.step(actions[env._calls % GRAPH_LEN])
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for k in range(GRAPH_LEN):
+            env.step(actions[k])
+    torch.cuda.synchronize()
+    return graph
+
+
+# slices of 256 envs at 65 536 envs: type t starts at env ceil(t * 3276.8), workgroups are 256 envs; each slice
+# below straddles a workgroup edge and a terrain-type boundary (workgroup 12 holds types 0|1 around env 3277,
+# workgroup 24 types 1|2 around 6554, workgroup 179 types 13|14 around 45876) or the last workgroup
+FULL_SIZE_SLICES = [3277 - 128, 6554 - 180, 32768 - 128, 45876 - 60, 65536 - 256]
+
+
+@pytest.mark.parametrize("obstacles", [False, True], ids=["gates_only_C3_headline", "obstacles"])
+def test_full_size_teacher_forced_slices(obstacles):
+    """65 536 envs (BASELINE C3 size), stepped the way bench.py steps them: replays of a captured 64-step hipGraph.
+    Before each replay the slices' state is read; the oracle re-steps each slice 64 times from it (teacher forcing
+    over the whole replay) and must match the kernel bit for bit: state, last step's policy row, reward and dones.
+    obstacles=False runs the headline instantiation step_kernel<true, false, 8, 1> (LDS track slice staged per
+    workgroup over its own terrain-type range); the test asserts that instantiation is the one launched."""
+    n, m, replays = 65536, 256, 6
+    env, _ = make(n, obstacles=obstacles)
+    want_kernel = "step_kernel<false, true, 0, 1>" if obstacles else "step_kernel<true, false, 8, 1>"
+    assert env.step_kernel_name() == want_kernel
     env.reset()
     g = torch.Generator().manual_seed(11)
     env.episode_length_buf = torch.randint(0, 200, (n,), generator=g, dtype=torch.int32).to(DEV)
-    slices = [0, 3200, 3276 * 5 - 100, 40000, n - m]
+    acts = torch.zeros(GRAPH_LEN, n, 4, device=DEV)
+    acts.copy_(torch.randn(GRAPH_LEN, n, 4, generator=g) * 1.2)
+    graph = capture_step_graph(env, acts)
     base = env.gr_config
-    seen_types = set()
-    for k in range(steps):
-        a = (torch.randn(n, 4, generator=g) * 1.2).numpy().astype(np.float32)
-        i0 = slices[k % len(slices)]
+    ot = env.obstacle_table
+    gates_h, recs_h = env.track_gates.cpu().numpy(), env.track_records.cpu().numpy()
+    seen_types, n_done = set(), 0
+    for r in range(replays):
+        a = (torch.randn(GRAPH_LEN, n, 4, generator=g) * 1.2)
+        acts.copy_(a)  # the graph reads the ring in place
+        a = a.numpy()
         torch.cuda.synchronize()
-        pre = oracle.planes_to_envs(env.state[:, i0:i0 + m].cpu().numpy(), env.istate[i0:i0 + m].cpu().numpy())
-        prev_crit = env.obs_buf["critic"][i0:i0 + m].cpu().numpy()
-        cnt = int(env._counters[env._calls % 2].item())
-        env.step(torch.from_numpy(a).to(DEV))
-        c = _abi.GrConfig.from_buffer_copy(base)
-        c.num_envs = m
-        c.env_id_offset = i0
-        ot = env.obstacle_table
-        orc = oracle.Oracle(c, env.track_gates.cpu().numpy(), env.track_records.cpu().numpy(), ot.records, ot.counts)
-        orc.envs[:] = pre
-        orc.obs_critic[:] = prev_crit
-        orc.counter[0] = cnt
-        orc.step(a[i0:i0 + m])
-        seen_types.update(pre["type"].tolist())
-        assert_envs_equal(kernel_envs(env)[i0:i0 + m], orc.envs, f"step {k} slice {i0}")
-        out = env.obs_buf
-        assert np.array_equal(bits(out["policy"][i0:i0 + m].cpu().numpy()), bits(orc.obs_policy))
-        assert np.array_equal(env._sets[env._cur]["dones"][i0:i0 + m].cpu().numpy(), orc.dones)
-    assert len(seen_types) >= 4
+        assert env._calls % GRAPH_LEN == 0 and env._cur == 0
+        pre_st = env.state.cpu().numpy()
+        pre_ist = env.istate.cpu().numpy()
+        prev_crit = env.obs_buf["critic"].cpu().numpy()
+        cnt = int(env._counters[0].item())
+        graph.replay()
+        torch.cuda.synchronize()
+        post = kernel_envs(env)
+        out = env._sets[env._cur]
+        for i0 in FULL_SIZE_SLICES:
+            c = _abi.GrConfig.from_buffer_copy(base)
+            c.num_envs = m
+            c.env_id_offset = i0
+            orc = oracle.Oracle(c, gates_h, recs_h, None if ot is None else ot.records, None if ot is None else ot.counts)
+            orc.envs[:] = oracle.planes_to_envs(pre_st[:, i0:i0 + m], pre_ist[i0:i0 + m])
+            orc.obs_critic[:] = prev_crit[i0:i0 + m]
+            orc.counter[0] = cnt
+            seen_types.update(orc.envs["type"].tolist())
+            for k in range(GRAPH_LEN):
+                orc.step(a[k, i0:i0 + m])
+                n_done += int(orc.dones.sum())
+            where = f"replay {r} slice {i0}"
+            assert_envs_equal(post[i0:i0 + m], orc.envs, where)
+            assert np.array_equal(bits(out["policy"][i0:i0 + m].cpu().numpy()), bits(orc.obs_policy)), where
+            assert np.array_equal(bits(out["critic"][i0:i0 + m].cpu().numpy()), bits(orc.obs_critic)), where
+            assert np.array_equal(bits(out["reward"][i0:i0 + m].cpu().numpy()), bits(orc.reward)), where
+            assert np.array_equal(out["dones"][i0:i0 + m].cpu().numpy(), orc.dones), where
+    del graph
+    assert len(seen_types) >= 4, seen_types
+    assert n_done > 100  # in-kernel resets were exercised inside the graph
     # invariants on all envs
     e = kernel_envs(env)
     assert np.isfinite(e["p"]).all() and np.isfinite(e["q"]).all() and np.isfinite(e["v"]).all()
