@@ -225,7 +225,7 @@ STATUS_TEXT = {GR_STATUS_OBST_WAIT_TIMEOUT: "a physics wave gave up waiting for 
 EXPORTS = [
     "gr_abi_version", "gr_config_default", "gr_config_size", "gr_create", "gr_destroy", "gr_last_error",
     "gr_num_blocks", "gr_num_log_rows", "gr_log_finalize", "gr_bytes_per_env_step", "gr_bind_tracks", "gr_bind_obstacles", "gr_swap_terrain", "gr_bind_buffers", "gr_bind_obs_sink", "gr_init", "gr_reset",
-    "gr_step", "gr_observe", "gr_step_kernel_variant", "gr_device_status", "gr_test_inject_fault", "gr_set_timing", "gr_read_timing", "gr_test_dynamics", "gr_test_math",
+    "gr_step", "gr_observe", "gr_device_status", "gr_test_inject_fault", "gr_set_timing", "gr_read_timing", "gr_test_dynamics", "gr_test_math",
     "gr_test_philox",
     "gr_debug_read_stamps", "gr_debug_read_policy_stamps",
     "gr_camera_config_default", "gr_camera_config_size", "gr_enable_camera", "gr_bind_camera_buffers",
@@ -236,7 +236,8 @@ EXPORTS = [
     "gr_store_transition", "gr_episode_accumulate", "gr_gae", "gr_l2c2_mix",
     "gr_ppo_loss_forward_loss", "gr_ppo_loss_backward_loss", "gr_adaptive_lr",
     "gr_bn_scratch_doubles", "gr_bn_act_forward", "gr_bn_act_backward", "gr_stem1_scratch_doubles",
-    "gr_stem1_forward", "gr_stem1_backward",
+    "gr_stem1_forward", "gr_stem1_backward", "gr_mlp_partials", "gr_mlp_forward", "gr_mlp_backward",
+    "gr_mlp_args_size", "gr_step_kernel_variant",
 ]
 
 _lib = None
@@ -304,6 +305,10 @@ def _declare(lib):
         "gr_mlp_in_forward": (C.c_int, [vp, C.c_int64, C.c_int32, C.c_int32, vp, vp, C.c_int32, C.c_float, vp, vp]),
         "gr_mlp_in_backward": (C.c_int, [vp, vp, vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_float, vp, vp,
                                          vp]),
+        "gr_mlp_partials": (C.c_int64, [C.c_int64, C.c_int32, C.c_int32]),
+        "gr_mlp_forward": (C.c_int, [vp, vp]),
+        "gr_mlp_backward": (C.c_int, [vp, vp]),
+        "gr_mlp_args_size": (C.c_size_t, []),
         "gr_bn_scratch_doubles": (C.c_int64, [C.c_int64, C.c_int32]),
         "gr_bn_act_forward": (C.c_int, [vp, C.c_int64, C.c_int32, vp, vp, C.c_float, C.c_int32, C.c_float, vp, vp, vp,
                                         vp]),
@@ -345,6 +350,11 @@ def load(path: str | None = None):
     if lib.gr_policy_args_size() != C.sizeof(GrPolicyArgs):
         raise RuntimeError(f"gr_policy_args size mismatch: C {lib.gr_policy_args_size()} vs ctypes "
                            f"{C.sizeof(GrPolicyArgs)}")
+    if hasattr(lib, "gr_mlp_args_size"):
+        from .rsl_rl.linear import GrMlpArgs
+
+        if lib.gr_mlp_args_size() != C.sizeof(GrMlpArgs):
+            raise RuntimeError("gr_mlp_args size mismatch between libgr.so and the ctypes mirror")
     if path is None:
         _lib = lib
     return lib

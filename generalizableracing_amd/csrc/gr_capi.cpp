@@ -864,6 +864,41 @@ int gr_mlp_in_backward(const float* gh, const float* hv, const float* x, int64_t
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
+size_t gr_mlp_args_size(void) { return sizeof(gr_mlp_args); }
+
+int64_t gr_mlp_partials(int64_t rows, int32_t hidden, int32_t nets) {
+  if (rows < 0 || (hidden != 128 && hidden != 256) || nets < 1 || nets > 2) return GR_ERR_ARG;
+  return gr::mlp_partial_floats(rows, hidden, nets, 32, 4);
+}
+
+// shapes and alignment of gr_mlp_args; `bwd` also checks the backward's buffers
+static bool mlp_args_ok(const gr_mlp_args* a, bool bwd) {
+  if (!a || a->rows <= 0 || a->nets < 1 || a->nets > 2 || (a->hidden != 128 && a->hidden != 256)) return false;
+  for (int i = 0; i < a->nets; ++i) {
+    const gr_mlp_net& n = a->net[i];
+    if (!n.x || !n.w1 || !n.b1 || !n.w2 || !n.b2 || !n.w3 || !n.b3 || !n.h1 || !n.z2 || n.d < 4 || n.d > 32 ||
+        n.d % 4 || n.k < 1 || n.k > 4 || n.ldx < n.d || n.ldx % 4 || !aligned16(n.x) || !aligned16(n.w1) ||
+        !aligned16(n.w2) || !aligned16(n.w3) || !aligned16(n.b1) || !aligned16(n.b2) || !aligned16(n.h1) ||
+        !aligned16(n.z2))
+      return false;
+    if (!bwd && !n.y) return false;
+    if (bwd && (!n.gy || !n.gz2 || !n.grads || !aligned16(n.gz2))) return false;
+  }
+  return !bwd || (a->partial && aligned16(a->partial));
+}
+
+int gr_mlp_forward(const gr_mlp_args* a, void* stream) {
+  if (!mlp_args_ok(a, false)) return GR_ERR_ARG;
+  const hipError_t e = gr::launch_mlp_forward(*a, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
+int gr_mlp_backward(const gr_mlp_args* a, void* stream) {
+  if (!mlp_args_ok(a, true)) return GR_ERR_ARG;
+  const hipError_t e = gr::launch_mlp_backward(*a, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
 int gr_adam_prepare(gr_adam_segment* t, int32_t nseg, int32_t* nblocks) {
   if (!t || !nblocks || nseg < 1 || nseg > GR_ADAM_MAX_SEGMENTS) return GR_ERR_ARG;
   int64_t nb = 0;

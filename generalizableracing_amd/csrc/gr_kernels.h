@@ -150,6 +150,10 @@ hipError_t launch_ppo_loss_backward(const gr_ppo_loss_args& a, const float* g, i
                                     float* dvalue, float* part, float* dstd, hipStream_t s);
 hipError_t launch_adaptive_lr(const float* kl, float* lr, float hi, float lo, float lr_min, float lr_max,
                               hipStream_t s);
+// gr_mlp.hip: the update's whole-network MLP kernels
+hipError_t launch_mlp_forward(const gr_mlp_args& a, hipStream_t s);
+hipError_t launch_mlp_backward(const gr_mlp_args& a, hipStream_t s);
+int64_t mlp_partial_floats(long long rows, int hidden, int nets, int max_d, int max_k);
 hipError_t launch_in_backward(const float* gh, const float* hv, const float* x, long long m, int d, int ldx, int h,
                               float slope, float* part, float* sums, hipStream_t s);
 // obstacle slots per camera wave (the first GR_CAM_OBST_SLOTS obstacles in view; any further ones

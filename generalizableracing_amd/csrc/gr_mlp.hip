@@ -1,0 +1,666 @@
+// gr_mlp.hip — the PPO update's actor and critic MLPs as whole-network fp32-MFMA kernels (gr_mlp_forward /
+// gr_mlp_backward, include/gr.h).
+//
+// Reference: PPO.update (standalone/rsl_rl/ext/algorithms/ppo.py:103-190) evaluates, per mini-batch, the actor
+// and the critic of upstream rsl_rl's ActorCritic (x -> Linear(d, H) -> LeakyReLU -> Linear(H, H) -> LeakyReLU ->
+// Linear(H, k)) and back-propagates the loss through both.  In round 3 that was, per network and direction, a
+// fused first layer, a hipBLASLt GEMM for the H x H layer, a fused head, a split-K batched GEMM + sum for the hidden
+// weight gradient and three partial-sum reductions: ~20 launches per mini-batch step, the GEMMs at 0.41-0.56 of the
+// fp32 MFMA peak on config C2's 24 576-row mini-batches (profiles/round03_train4096_fused_graphed_kernel_stats.csv).
+//
+// Here, for both networks at once (blockIdx.y = network):
+//   mlp_fwd   : per 64-row tile, layer 1 -> LDS (h1, also stored for the backward) -> layer 2 on MFMA with the
+//               wave's W2 rows in registers (z2 stored) -> activation -> layer 3 partials -> y.  The layout of
+//               policy_f32_kernel (gr_policy_f32.hip): 8 waves, wave w owns hidden units [H/8 w, H/8 (w + 1)).
+//   mlp_bwd   : per 64-row tile, gh2 = gy W3 (one MFMA per 16 x 16 tile, K = k <= 4) -> gz2 = gh2 lrelu'(z2) -> LDS
+//               -> gh1 = gz2 W2 on MFMA with the wave's W2 COLUMNS in registers -> gz1 = gh1 lrelu'(h1) -> LDS;
+//               the small weight gradients on MFMA contracting over the tile's rows (gW3 = gy^T h2, gW1 = gz1^T x)
+//               and the bias sums in registers, one partial row per workgroup; gz2 stored for mlp_wgrad.
+//   mlp_wgrad : gW2 = gz2^T h1, split over the rows (128 x 128 output blocks x row chunks), tiles staged in LDS
+//               transposed so every fragment is one ds_read_b128; the four blocks of a chunk share an XCD (L2).
+//   mlp_final : every partial row summed in a fixed order into the gradient vector [gW1 | gb1 | gW2 | gb2 | gW3 |
+//               gb3] of each network (deterministic, no atomics).
+// MFMA fragment convention (v_mfma_f32_16x16x4_f32): lane l = 16 g + j holds A[row j][k = g] and B[k = g][col j];
+// the C tile holds rows 4 g + r of column j in register r.  "k order": k step 4 q + r of a contraction over H
+// units is unit 16 q + 4 g + r, so a float4 of 4 consecutive units feeds 4 k steps.
+#include <hip/hip_runtime.h>
+
+#include "../../include/gr.h"
+#include "gr_kernels.h"
+
+namespace gr {
+
+typedef float m4 __attribute__((ext_vector_type(4)));
+
+constexpr int MW = 8;         // waves per workgroup (2 per SIMD)
+constexpr int MC = 4;         // 16-row column tiles per workgroup tile
+constexpr int ME = 16 * MC;   // rows per workgroup tile
+constexpr int M_BLOCKS = 256; // persistent workgroups (one per CU; their registers / LDS hold one)
+
+__device__ __forceinline__ m4 mf(float a, float b, m4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+__device__ __forceinline__ m4 ld4(const float* p) { return *reinterpret_cast<const m4*>(p); }
+__device__ __forceinline__ void st4(float* p, m4 v) { *reinterpret_cast<m4*>(p) = v; }
+__device__ __forceinline__ float lrelu(float z, float s) { return z > 0.0f ? z : z * s; }
+__device__ __forceinline__ float lrelu_d(float z, float s) { return z > 0.0f ? 1.0f : s; }
+__device__ __forceinline__ m4 zero4() { return (m4){0.0f, 0.0f, 0.0f, 0.0f}; }
+
+// ------------------------------------------------------------------------------------------------ forward
+// LDS (floats): h1 [2][ME][H + 4], layer-3 partials [2][MW][ME][4], b1 [H], b2 [H]
+constexpr size_t mlp_fwd_lds_bytes(int h) { return 4 * ((size_t)2 * ME * (h + 4) + 2 * MW * ME * 4 + 2 * h); }
+
+template <int H, int Q1>
+__global__ __launch_bounds__(MW * 64) void mlp_fwd(gr_mlp_args a) {
+  constexpr int TW = H / (16 * MW);  // 16-unit tiles per wave and layer
+  constexpr int Q = H / 16;
+  constexpr int HP = H + 4;  // row stride of the LDS h1 tile (float4 reads of 16 rows hit distinct bank quads)
+  const gr_mlp_net& net = a.net[blockIdx.y];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
+  const int n = (int)a.rows;  // (gr_mlp_* check rows * max(H, ldx) < 2^31: 32-bit offsets)
+  const int D = net.d, K = net.k;
+  const int ldx = (int)net.ldx;
+  const float slope = a.slope;
+  extern __shared__ float lds[];
+  float* h1s = lds;                            // [2][ME][HP]
+  float* parts = h1s + 2 * ME * HP;            // [2][MW][ME][4]
+  float* b1s = parts + 2 * MW * ME * 4;        // [H]
+  float* b2s = b1s + H;                        // [H]
+  const float* __restrict__ W1 = net.w1;
+  const float* __restrict__ W2 = net.w2;
+  const float* __restrict__ W3 = net.w3;
+
+  float w1r[TW][Q1][4], w2r[TW][4 * Q], w3r[TW][4];
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const int row = 16 * (wave * TW + t) + j;
+#pragma unroll
+    for (int q = 0; q < Q1; ++q) {
+      const int k = 16 * q + 4 * g;
+      const m4 v = k < D ? ld4(W1 + (size_t)row * D + k) : zero4();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w1r[t][q][r] = v[r];
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const m4 v = ld4(W2 + (size_t)row * H + 16 * q + 4 * g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w2r[t][4 * q + r] = v[r];
+    }
+    // layer 3 A operand: rows = outputs (j < K), k = the wave's units
+    const m4 v3 = j < K ? ld4(W3 + (size_t)j * H + 16 * (wave * TW + t) + 4 * g) : zero4();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) w3r[t][r] = v3[r];
+  }
+  for (int i = threadIdx.x; i < H; i += MW * 64) {
+    b1s[i] = net.b1[i];
+    b2s[i] = net.b2[i];
+  }
+  const float b3v = g < K ? net.b3[g] : 0.0f;
+
+  const int stride = gridDim.x * ME;
+  m4 xo[MC][Q1];
+  auto load_x = [&](int base) {
+#pragma unroll
+    for (int c = 0; c < MC; ++c) {
+      int r = base + 16 * c + j;
+      r = r < n ? r : n - 1;
+#pragma unroll
+      for (int q = 0; q < Q1; ++q) {
+        const int k = 16 * q + 4 * g;
+        xo[c][q] = k < D ? ld4(net.x + r * ldx + k) : zero4();
+      }
+    }
+  };
+  // the 8 waves' layer-3 partials of a tile -> y; column tile e by wave (2 kt + e) mod 8
+  auto epilogue = [&](int kt, int base) {
+    const int e = (wave - 2 * kt) & (MW - 1);
+    if (e >= MC) return;
+    const float* pp = parts + (size_t)(kt & 1) * MW * ME * 4 + (16 * e + j) * 4 + g;
+    float v = 0.0f;
+#pragma unroll
+    for (int w = 0; w < MW; ++w) v += pp[w * ME * 4];
+    const int r = base + 16 * e + j;
+    if (r < n && g < K) net.y[r * K + g] = v + b3v;
+  };
+
+  load_x(blockIdx.x * ME);
+  __syncthreads();  // biases staged
+  int kt = 0, prev_base = 0;
+  for (int base = blockIdx.x * ME; base < n; base += stride, ++kt) {
+    float* h1 = h1s + (kt & 1) * ME * HP;
+    m4 acc[TW][MC];
+    // ---- layer 1: the wave's h1 units of the tile -> LDS [row][unit] (the next tile's rows are loaded into the
+    // same registers once these MFMAs have read them)
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      const m4 bb = ld4(b1s + 16 * (wave * TW + t) + 4 * g);
+#pragma unroll
+      for (int c = 0; c < MC; ++c) acc[t][c] = bb;
+    }
+#pragma unroll
+    for (int kk = 0; kk < 4 * Q1; ++kk)
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+#pragma unroll
+        for (int c = 0; c < MC; ++c) acc[t][c] = mf(w1r[t][kk >> 2][kk & 3], xo[c][kk >> 2][kk & 3], acc[t][c]);
+    if (base + stride < n) load_x(base + stride);
+#pragma unroll
+    for (int t = 0; t < TW; ++t)
+#pragma unroll
+      for (int c = 0; c < MC; ++c) {
+        m4 v = acc[t][c];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = lrelu(v[r], slope);
+        st4(h1 + (16 * c + j) * HP + 16 * (wave * TW + t) + 4 * g, v);
+      }
+    __syncthreads();  // h1 of this tile complete; the layer-3 partials of the previous tile complete
+    if (kt > 0) epilogue(kt - 1, prev_base);
+    // h1 rows -> global for the backward (coalesced: wave w stores rows w, w + 8, ...; lane l units 4 l .. 4 l + 3)
+    if (4 * lane < H) {
+#pragma unroll
+      for (int rr = 0; rr < ME / MW; ++rr) {
+        const int row = wave + MW * rr;
+        if (base + row < n) st4(net.h1 + (base + row) * H + 4 * lane, ld4(h1 + row * HP + 4 * lane));
+      }
+    }
+    // ---- layer 2: the wave's z2 units from all of h1
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      const m4 bb = ld4(b2s + 16 * (wave * TW + t) + 4 * g);
+#pragma unroll
+      for (int c = 0; c < MC; ++c) acc[t][c] = bb;
+    }
+    m4 hb[2][MC];
+#pragma unroll
+    for (int c = 0; c < MC; ++c) hb[0][c] = ld4(h1 + (16 * c + j) * HP + 4 * g);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      if (q + 1 < Q) {
+#pragma unroll
+        for (int c = 0; c < MC; ++c) hb[(q + 1) & 1][c] = ld4(h1 + (16 * c + j) * HP + 16 * (q + 1) + 4 * g);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int t = 0; t < TW; ++t)
+#pragma unroll
+          for (int c = 0; c < MC; ++c) acc[t][c] = mf(w2r[t][4 * q + r], hb[q & 1][c][r], acc[t][c]);
+    }
+    // z2 -> global (lane (g, j): units 16 t' + 4 g .. + 3 of row 16 c + j; the wave's TW tiles fill whole lines)
+#pragma unroll
+    for (int c = 0; c < MC; ++c) {
+      const int r = base + 16 * c + j;
+      if (r < n) {
+#pragma unroll
+        for (int t = 0; t < TW; ++t) st4(net.z2 + r * H + 16 * (wave * TW + t) + 4 * g, acc[t][c]);
+      }
+    }
+    // ---- layer 3 partial over the wave's units -> LDS
+    m4 o[MC];
+#pragma unroll
+    for (int c = 0; c < MC; ++c) o[c] = zero4();
+#pragma unroll
+    for (int t = 0; t < TW; ++t)
+#pragma unroll
+      for (int c = 0; c < MC; ++c) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[c] = mf(w3r[t][r], lrelu(acc[t][c][r], slope), o[c]);
+      }
+    if (g == 0) {
+#pragma unroll
+      for (int c = 0; c < MC; ++c) st4(parts + ((size_t)((kt & 1) * MW + wave) * ME + 16 * c + j) * 4, o[c]);
+    }
+    prev_base = base;
+  }
+  __syncthreads();
+  if (kt > 0) epilogue(kt - 1, prev_base);
+}
+
+// ------------------------------------------------------------------------------------------------ backward
+// (32-row tiles: the W2 columns take 128 registers; with 64-row tiles the accumulators spilled)
+constexpr int BC = 2;
+constexpr int BE = 16 * BC;
+// per-workgroup partial row (floats): [gW1 (H D) | gb1 (H) | gb2 (H) | gW3 (k H) | gb3 (k)], padded to 4
+__host__ __device__ constexpr int mlp_bwd_row(int h, int d, int k) { return (h * d + h + h + k * h + k + 3) & ~3; }
+// LDS (floats): two [BE][H + 4] tiles (gz2; h2 then gz1) + gy rows [BE][4]
+constexpr size_t mlp_bwd_lds_bytes(int h) { return 4 * ((size_t)2 * BE * (h + 4) + BE * 4); }
+
+template <int H, int DT>
+__global__ __launch_bounds__(MW * 64) void mlp_bwd(gr_mlp_args a, int rows_per_net_part) {
+  constexpr int TW = H / (16 * MW);
+  constexpr int Q = H / 16;
+  constexpr int HP = H + 4;
+  const gr_mlp_net& net = a.net[blockIdx.y];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
+  const int n = (int)a.rows;  // (gr_mlp_* check rows * max(H, ldx) < 2^31: 32-bit offsets)
+  const int D = net.d, K = net.k;
+  const int ldx = (int)net.ldx;
+  const float slope = a.slope;
+  extern __shared__ float lds[];
+  float* gz2s = lds;               // [BE][HP]
+  float* bufb = gz2s + BE * HP;    // [BE][HP]: h2, then gz1
+  float* gys = bufb + BE * HP;     // [BE][4]
+  const float* __restrict__ W2 = net.w2;
+  const float* __restrict__ W3 = net.w3;
+
+  // A operands: gh1^T = W2^T gz2^T -> row j of tile t is hidden unit i = 16 (wave TW + t) + j of h1, k step 4 q + r
+  // is z2 unit 16 q + 4 g + r: W2[16 q + 4 g + r][i]
+  float w2c[TW][4 * Q], w3a[TW];
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const int i = 16 * (wave * TW + t) + j;
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w2c[t][4 * q + r] = W2[(size_t)(16 * q + 4 * g + r) * H + i];
+    // gh2^T = W3^T gy^T: row j = unit 16 (wave TW + t) + j, k = output g
+    w3a[t] = g < K ? W3[(size_t)g * H + i] : 0.0f;
+  }
+  m4 gw1[TW][DT], gw3[TW];
+  float gb1[TW][4], gb2[TW][4], gb3 = 0.0f;
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    gw3[t] = zero4();
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) gw1[t][dt] = zero4();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) gb1[t][r] = gb2[t][r] = 0.0f;
+  }
+
+  const int stride = gridDim.x * BE;
+  for (int base = blockIdx.x * BE; base < n; base += stride) {
+    // ---- gy rows of the tile -> LDS (rows past the end: 0, so they add nothing anywhere)
+    if (threadIdx.x < BE * 4) {
+      const int row = threadIdx.x >> 2, kk = threadIdx.x & 3;
+      const int r = base + row;
+      gys[threadIdx.x] = (r < n && kk < K) ? net.gy[r * K + kk] : 0.0f;
+    }
+    __syncthreads();  // (1) gy staged; the previous tile's readers of gz2s / bufb are done
+    // ---- gh2 = gy W3 (one MFMA per tile, K = k <= 4), gz2 = gh2 lrelu'(z2), h2 = lrelu(z2)
+#pragma unroll
+    for (int c = 0; c < BC; ++c) {
+      const int r = base + 16 * c + j;
+      const int rr = r < n ? r : n - 1;
+      const float gyv = gys[(16 * c + j) * 4 + g];  // B[k = g][row j]
+      if (wave == 0) gb3 += gyv;
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        const int u = 16 * (wave * TW + t) + 4 * g;
+        const m4 gh = mf(w3a[t], gyv, zero4());
+        const m4 z = ld4(net.z2 + rr * H + u);
+        m4 gz, h2;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          gz[q] = gh[q] * lrelu_d(z[q], slope);
+          h2[q] = lrelu(z[q], slope);
+          gb2[t][q] += gz[q];
+        }
+        st4(gz2s + (16 * c + j) * HP + u, gz);
+        st4(bufb + (16 * c + j) * HP + u, h2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();  // (2) gz2 and h2 of the tile in LDS
+    // ---- gW3 += gy^T h2: rows = outputs (j < k), contraction over the tile's rows (k step = rows 4 s + g)
+#pragma unroll 4
+    for (int s = 0; s < BE / 4; ++s) {
+      const int row = 4 * s + g;
+      const float av = j < 4 ? gys[row * 4 + j] : 0.0f;
+#pragma unroll
+      for (int t = 0; t < TW; ++t) gw3[t] = mf(av, bufb[row * HP + 16 * (wave * TW + t) + j], gw3[t]);
+    }
+    // ---- gh1 = gz2 W2 for the wave's h1 units, all rows of the tile
+    m4 acc[TW][BC];
+#pragma unroll
+    for (int t = 0; t < TW; ++t)
+#pragma unroll
+      for (int c = 0; c < BC; ++c) acc[t][c] = zero4();
+    // (B fragments single-buffered: the W2 columns take 128 registers; the SIMD's other wave covers the LDS latency)
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      m4 gb[BC];
+#pragma unroll
+      for (int c = 0; c < BC; ++c) gb[c] = ld4(gz2s + (16 * c + j) * HP + 16 * q + 4 * g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int t = 0; t < TW; ++t)
+#pragma unroll
+          for (int c = 0; c < BC; ++c) acc[t][c] = mf(w2c[t][4 * q + r], gb[c][r], acc[t][c]);
+      __builtin_amdgcn_sched_barrier(0);  // (no hoisting of later fragments' loads: registers)
+    }
+    // gz1 = gh1 lrelu'(h1) (h1 from the forward's saved rows)
+#pragma unroll
+    for (int c = 0; c < BC; ++c) {
+      const int r = base + 16 * c + j;
+      const int rr = r < n ? r : n - 1;
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        const m4 hv = ld4(net.h1 + rr * H + 16 * (wave * TW + t) + 4 * g);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc[t][c][q] *= lrelu_d(hv[q], slope);
+          gb1[t][q] += acc[t][c][q];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();  // (3) every wave is done with h2 (bufb) and gz2s
+    // gz1 -> bufb; gz2 rows -> global for mlp_wgrad (coalesced rows)
+#pragma unroll
+    for (int t = 0; t < TW; ++t)
+#pragma unroll
+      for (int c = 0; c < BC; ++c) st4(bufb + (16 * c + j) * HP + 16 * (wave * TW + t) + 4 * g, acc[t][c]);
+    if (4 * lane < H) {
+#pragma unroll
+      for (int rr = 0; rr < BE / MW; ++rr) {
+        const int row = wave + MW * rr;
+        if (base + row < n) st4(net.gz2 + (base + row) * H + 4 * lane, ld4(gz2s + row * HP + 4 * lane));
+      }
+    }
+    __syncthreads();  // (4) gz1 in LDS
+    // ---- gW1 += gz1^T x: rows = the wave's h1 units, cols = inputs (DT tiles of 16), k step = rows 4 s + g
+#pragma unroll 4
+    for (int s = 0; s < BE / 4; ++s) {
+      const int row = 4 * s + g;
+      int r = base + row;
+      r = r < n ? r : n - 1;  // (the tail rows' gz1 is 0)
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int dcol = 16 * dt + j;
+        const float xv = dcol < D ? net.x[r * ldx + dcol] : 0.0f;
+#pragma unroll
+        for (int t = 0; t < TW; ++t) gw1[t][dt] = mf(bufb[row * HP + 16 * (wave * TW + t) + j], xv, gw1[t][dt]);
+      }
+    }
+  }
+  // ---- the workgroup's partial row
+  float* pr = a.partial + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (size_t)rows_per_net_part;
+  // bias sums: over the 16 lanes j of each g group (fixed butterfly order)
+#pragma unroll
+  for (int t = 0; t < TW; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v1 = gb1[t][q], v2 = gb2[t][q];
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) {
+        v1 += __shfl_xor(v1, off);
+        v2 += __shfl_xor(v2, off);
+      }
+      gb1[t][q] = v1;
+      gb2[t][q] = v2;
+    }
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const int u0 = 16 * (wave * TW + t);
+    // gW1 [H][D]: C rows = units u0 + 4 g + q, col = input 16 dt + j
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (16 * dt + j < D) pr[(size_t)(u0 + 4 * g + q) * D + 16 * dt + j] = gw1[t][dt][q];
+    if (j == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        pr[H * D + u0 + 4 * g + q] = gb1[t][q];
+        pr[H * D + H + u0 + 4 * g + q] = gb2[t][q];
+      }
+    }
+    // gW3 [k][H]: C rows = outputs 4 g + q (g == 0, q < k), col = unit u0 + j
+    if (g == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (q < K) pr[H * D + 2 * H + q * H + u0 + j] = gw3[t][q];
+    }
+  }
+  if (wave == 0) {
+    float v = gb3;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) v += __shfl_xor(v, off);
+    if (j == 0 && g < K) pr[H * D + 2 * H + K * H + g] = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ gW2
+// gW2 [H][H] = gz2^T h1 per network: a workgroup takes a 128 x 128 output block (rows u of gW2 = gz2 columns,
+// cols i = h1 columns) over a chunk of the mini-batch rows; 8 waves as 2 (u) x 4 (i) of 64 x 32 (4 x 2 tiles).
+// The rows are staged 32 at a time, transposed into LDS ([col][row + 4]), so a fragment of 4 consecutive rows is
+// one ds_read_b128 (k order: k step 4 s + r of a 16-row group s is row 16 s + 4 g + r).
+constexpr int WG_BLK = 128;  // output block edge
+constexpr int WG_R = 32;     // rows per LDS stage
+constexpr int WG_RP = WG_R + 4;
+constexpr size_t mlp_wgrad_lds_bytes() { return 4 * (size_t)2 * 2 * WG_BLK * WG_RP; }
+
+template <int H>
+__global__ __launch_bounds__(MW * 64) void mlp_wgrad(gr_mlp_args a, int splits, long long rows_per_split,
+                                                     float* __restrict__ part) {
+  constexpr int NB = H / WG_BLK;  // blocks per edge
+  // XCD-aware: workgroup b runs on XCD b % 8; the NB * NB blocks of one (network, split) are b, b + 8, ... so they
+  // share that XCD's L2 (each stage of rows is read by NB blocks)
+  const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
+  const int blk = q % (NB * NB), grp = (q / (NB * NB)) * 8 + xcd;  // grp = net * splits + split
+  const int net_i = grp / splits, split = grp % splits;
+  if (net_i >= a.nets) return;
+  const gr_mlp_net& net = a.net[net_i];
+  const int bu = (blk / NB) * WG_BLK, bi = (blk % NB) * WG_BLK;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
+  const int wu = (wave >> 2) * 64, wi = (wave & 3) * 32;  // the wave's 64 x 32 sub-block
+  extern __shared__ float lds[];
+  const long long n = a.rows;
+  const long long r_begin = (long long)split * rows_per_split;
+  const long long r_end = r_begin + rows_per_split < n ? r_begin + rows_per_split : n;
+  m4 acc[4][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t][0] = acc[t][1] = zero4();
+  // staging: 32 rows x 32 float4 per matrix = 16 units of 8 rows x 8 float4 (one wave instruction: 8 rows x 128
+  // contiguous bytes; the transposed LDS writes of its 64 lanes then hit 32 distinct banks), 2 units per wave
+  auto stage = [&](float* dst, long long r0) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const float* src = m == 0 ? net.gz2 : net.h1;
+      const int col0 = m == 0 ? bu : bi;
+      float* d = dst + m * WG_BLK * WG_RP;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int unit = wave + MW * p;  // 0..15
+        const int row = 8 * (unit & 3) + (lane & 7), c4 = 4 * (8 * (unit >> 2) + (lane >> 3));
+        const long long r = r0 + row;
+        const m4 v = r < r_end ? ld4(src + r * H + col0 + c4) : zero4();
+#pragma unroll
+        for (int e = 0; e < 4; ++e) d[(c4 + e) * WG_RP + row] = v[e];
+      }
+    }
+  };
+  int buf = 0;
+  if (r_begin < r_end) stage(lds, r_begin);
+  for (long long r0 = r_begin; r0 < r_end; r0 += WG_R) {
+    __syncthreads();  // stage `buf` complete; the other buffer's readers are done
+    float* cur = lds + buf * 2 * WG_BLK * WG_RP;
+    if (r0 + WG_R < r_end) stage(lds + (buf ^ 1) * 2 * WG_BLK * WG_RP, r0 + WG_R);
+    const float* A = cur;                    // gz2 block, [u][row]
+    const float* B = cur + WG_BLK * WG_RP;   // h1 block, [i][row]
+#pragma unroll
+    for (int s = 0; s < WG_R / 16; ++s) {
+      m4 af[4], bf[2];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) af[t] = ld4(A + (wu + 16 * t + j) * WG_RP + 16 * s + 4 * g);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) bf[u] = ld4(B + (wi + 16 * u + j) * WG_RP + 16 * s + 4 * g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int u = 0; u < 2; ++u) acc[t][u] = mf(af[t][r], bf[u][r], acc[t][u]);
+    }
+    buf ^= 1;
+  }
+  // partial block -> part[net][split][H][H]
+  float* pp = part + ((size_t)net_i * splits + split) * H * H;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q2 = 0; q2 < 4; ++q2)
+        pp[(size_t)(bu + wu + 16 * t + 4 * g + q2) * H + bi + wi + 16 * u + j] = acc[t][u][q2];
+}
+
+// ------------------------------------------------------------------------------------------------ reductions
+// grads[net] = [gW1 (H D) | gb1 (H) | gW2 (H H) | gb2 (H) | gW3 (k H) | gb3 (k)]: element e of the vector is the
+// fixed-order sum of its partials (16 waves per 64 elements, every 16th partial row each, then wave order)
+__global__ __launch_bounds__(16 * 64) void mlp_final(gr_mlp_args a, int bwd_rows, int bwd_ld, int splits,
+                                                     const float* __restrict__ wpart) {
+  __shared__ float sm[16 * 64];
+  const gr_mlp_net& net = a.net[blockIdx.y];
+  const int H = a.hidden, D = net.d, K = net.k;
+  const int n_small = H * D + 2 * H + K * H + K;
+  const int total = n_small + H * H;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + lane;
+  // source: the backward's partial rows (small gradients) or the gW2 split partials
+  const float* src;
+  int rows, ld, out;
+  if (e < n_small) {
+    src = a.partial + (size_t)blockIdx.y * bwd_rows * bwd_ld + e;
+    rows = bwd_rows;
+    ld = bwd_ld;
+    // partial layout [gW1 | gb1 | gb2 | gW3 | gb3] -> grads layout [gW1 | gb1 | gW2 | gb2 | gW3 | gb3]
+    out = e < H * D + H ? e : e + H * H;
+  } else if (e < total) {
+    const int f = e - n_small;
+    src = wpart + (size_t)blockIdx.y * splits * H * H + f;
+    rows = splits;
+    ld = H * H;
+    out = H * D + H + f;
+  } else {
+    src = nullptr;
+    rows = 0;
+    ld = 0;
+    out = 0;
+  }
+  float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+  if (src) {
+    int b = wv;
+    for (; b + 48 < rows; b += 64) {
+      a0 += src[(size_t)b * ld];
+      a1 += src[(size_t)(b + 16) * ld];
+      a2 += src[(size_t)(b + 32) * ld];
+      a3 += src[(size_t)(b + 48) * ld];
+    }
+    for (; b < rows; b += 16) a0 += src[(size_t)b * ld];
+  }
+  sm[threadIdx.x] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (wv == 0 && src) {
+    float s = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += sm[k * 64 + lane];
+    net.grads[out] = s;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ launchers
+static int mlp_grid_x(long long rows, int nets, int tile = ME) {
+  const int t = (int)((rows + tile - 1) / tile), per = M_BLOCKS / nets;
+  return t < per ? (t < 1 ? 1 : t) : per;
+}
+// gW2 split count: enough workgroups for every CU (nets x blocks x splits >= 256), rows per split a multiple of the
+// stage, splits a multiple of 8 / (nets) so the XCD grouping is exact
+static int mlp_splits(long long rows, int hidden, int nets) {
+  const int nb = (hidden / WG_BLK) * (hidden / WG_BLK);
+  int s = (M_BLOCKS + nets * nb - 1) / (nets * nb);
+  const long long max_s = (rows + WG_R - 1) / WG_R;
+  if (s > max_s) s = (int)max_s;
+  if (s < 1) s = 1;
+  // (nets * s) must be a multiple of 8 for the b -> (grp, blk) mapping: round up
+  while ((nets * s) % 8) ++s;
+  return s;
+}
+static long long mlp_rows_per_split(long long rows, int splits) {
+  long long r = (rows + splits - 1) / splits;
+  return (r + WG_R - 1) / WG_R * WG_R;
+}
+
+int64_t mlp_partial_floats(long long rows, int hidden, int nets, int max_d, int max_k) {
+  const int bwd = mlp_grid_x(rows, nets, BE);
+  const int row = mlp_bwd_row(hidden, max_d, max_k);
+  const int s = mlp_splits(rows, hidden, nets);
+  return (int64_t)nets * bwd * row + (int64_t)nets * s * hidden * hidden;
+}
+
+template <typename F>
+static hipError_t set_lds(F* k, size_t bytes) {
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+template <int H, int Q1>
+static hipError_t launch_fwd_t(const gr_mlp_args& a, hipStream_t s) {
+  static bool attr = false;
+  const size_t lds = mlp_fwd_lds_bytes(H);
+  if (!attr) {
+    const hipError_t e = set_lds(&mlp_fwd<H, Q1>, lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((mlp_fwd<H, Q1>), dim3(mlp_grid_x(a.rows, a.nets), a.nets), dim3(MW * 64), lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_mlp_forward(const gr_mlp_args& a, hipStream_t s) {
+  int d = a.net[0].d;
+  if (a.nets > 1 && a.net[1].d > d) d = a.net[1].d;
+  if (a.hidden == 256) return d <= 16 ? launch_fwd_t<256, 1>(a, s) : launch_fwd_t<256, 2>(a, s);
+  return d <= 16 ? launch_fwd_t<128, 1>(a, s) : launch_fwd_t<128, 2>(a, s);
+}
+
+template <int H, int DT>
+static hipError_t launch_bwd_t(const gr_mlp_args& a, int row, hipStream_t s) {
+  static bool attr = false;
+  const size_t lds = mlp_bwd_lds_bytes(H);
+  if (!attr) {
+    const hipError_t e = set_lds(&mlp_bwd<H, DT>, lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((mlp_bwd<H, DT>), dim3(mlp_grid_x(a.rows, a.nets, BE), a.nets), dim3(MW * 64), lds, s, a, row);
+  return hipGetLastError();
+}
+
+template <int H>
+static hipError_t launch_wgrad_t(const gr_mlp_args& a, int splits, long long rps, float* wpart, hipStream_t s) {
+  static bool attr = false;
+  const size_t lds = mlp_wgrad_lds_bytes();
+  if (!attr) {
+    const hipError_t e = set_lds(&mlp_wgrad<H>, lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int nb = (H / WG_BLK) * (H / WG_BLK);
+  hipLaunchKernelGGL((mlp_wgrad<H>), dim3(a.nets * splits * nb), dim3(MW * 64), lds, s, a, splits, rps, wpart);
+  return hipGetLastError();
+}
+
+hipError_t launch_mlp_backward(const gr_mlp_args& a, hipStream_t s) {
+  int d = a.net[0].d, k = a.net[0].k;
+  if (a.nets > 1) {
+    d = a.net[1].d > d ? a.net[1].d : d;
+    k = a.net[1].k > k ? a.net[1].k : k;
+  }
+  const int row = mlp_bwd_row(a.hidden, d, k);
+  const int bwd_blocks = mlp_grid_x(a.rows, a.nets, BE);
+  hipError_t e;
+  if (a.hidden == 256) e = d <= 16 ? launch_bwd_t<256, 1>(a, row, s) : launch_bwd_t<256, 2>(a, row, s);
+  else e = d <= 16 ? launch_bwd_t<128, 1>(a, row, s) : launch_bwd_t<128, 2>(a, row, s);
+  if (e != hipSuccess) return e;
+  const int splits = mlp_splits(a.rows, a.hidden, a.nets);
+  const long long rps = mlp_rows_per_split(a.rows, splits);
+  float* wpart = a.partial + (size_t)a.nets * bwd_blocks * row;
+  e = a.hidden == 256 ? launch_wgrad_t<256>(a, splits, rps, wpart, s) : launch_wgrad_t<128>(a, splits, rps, wpart, s);
+  if (e != hipSuccess) return e;
+  const int total = a.hidden * d + 2 * a.hidden + k * a.hidden + k + a.hidden * a.hidden;
+  hipLaunchKernelGGL(mlp_final, dim3((total + 63) / 64, a.nets), dim3(16 * 64), 0, s, a, bwd_blocks, row, splits,
+                     (const float*)wpart);
+  return hipGetLastError();
+}
+
+}  // namespace gr

@@ -59,6 +59,10 @@ class RslRlPpoAlgorithmCfg:
     # not in the reference: the grad-norm clip and Adam as four HIP launches over the parameter table
     # (rsl_rl/flat_adam.py); False keeps torch.optim.Adam + nn.utils.clip_grad_norm_
     fused_adam: bool = True
+    # not in the reference: with fused_losses, the actor and critic MLPs of the update as whole-network fp32-MFMA
+    # kernels, one launch per direction for both networks (gr_mlp_forward / gr_mlp_backward, csrc/gr_mlp.hip);
+    # False keeps the per-layer path (fused first layer and head around hipBLASLt GEMMs, rsl_rl/linear.py MLP)
+    fused_mlp: bool = True
 
 
 @dataclass

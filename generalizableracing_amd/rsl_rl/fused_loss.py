@@ -146,13 +146,24 @@ def _policy_std(pol):
     return pol.std if pol.noise_std_type == "scalar" else torch.exp(pol.log_std)
 
 
+def policy_outputs(alg, obs, critic_obs):
+    """(action mean, value) of the mini-batch: both MLPs through the whole-network MFMA kernels when they cover
+    them (linear.fused_mlps: one launch per direction for actor and critic), else module by module."""
+    from . import linear as _lin
+
+    pol = alg.policy
+    nets, xs = [pol.actor, pol.critic], [obs, critic_obs]
+    if getattr(alg, "fused_mlp", False) and _lin.networks_fusable(nets, xs):
+        return _lin.fused_mlps(nets, xs)
+    return pol.actor(obs), pol.critic(critic_obs)
+
+
 def ppo_loss(alg, obs, critic_obs, act, value_old, adv, ret, logp_old, mu_old, sig_old, acc=None, kl_out=None):
     """(loss, [surrogate, value, KL] means) of one mini-batch: loss = surrogate + value_loss_coef * value
     (- entropy_coef * entropy) as in ppo.py:171-172, differentiable; the same values as ppo_losses."""
     pol = alg.policy
-    mu = pol.actor(obs)
+    mu, value = policy_outputs(alg, obs, critic_obs)
     std = _policy_std(pol)
-    value = pol.critic(critic_obs)
     loss, stats = _PPOLossCombinedFn.apply(mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old,
                                            float(alg.clip_param), bool(alg.use_clipped_value_loss),
                                            float(alg.value_loss_coef), acc, kl_out)
@@ -176,9 +187,8 @@ def ppo_losses(alg, obs, critic_obs, act, value_old, adv, ret, logp_old, mu_old,
     as PPO.update's policy.act / get_actions_log_prob / evaluate / _ppo_losses / _adapt_learning_rate (ppo.py
     :103-169), without the unused action sample."""
     pol = alg.policy
-    mu = pol.actor(obs)
+    mu, value = policy_outputs(alg, obs, critic_obs)
     std = pol._std(mu[:1])[0]  # [k]: the scalar or exp(log) std, differentiable
-    value = pol.critic(critic_obs)
     surr, vloss, kl = _PPOLossFn.apply(mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old,
                                        float(alg.clip_param), bool(alg.use_clipped_value_loss))
     ent = None

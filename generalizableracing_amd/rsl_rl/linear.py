@@ -18,6 +18,8 @@ DESIGN.md §4f has the before / after.
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -272,3 +274,142 @@ class MLP(nn.Sequential):
         for m in mods:
             x = m(x)
         return x
+
+
+# ------------------------------------------------------------------------------ whole-network MFMA kernels (round 4)
+class GrMlpNet(C.Structure):
+    """Mirror of gr_mlp_net (include/gr.h)."""
+    _fields_ = [(n, C.c_void_p) for n in ("x", "w1", "b1", "w2", "b2", "w3", "b3", "h1", "z2", "y", "gy", "gz2",
+                                          "grads")] + [("ldx", C.c_int64), ("d", C.c_int32), ("k", C.c_int32)]
+
+
+class GrMlpArgs(C.Structure):
+    """Mirror of gr_mlp_args (include/gr.h)."""
+    _fields_ = [("net", GrMlpNet * 2), ("rows", C.c_int64), ("nets", C.c_int32), ("hidden", C.c_int32),
+                ("slope", C.c_float), ("reserved", C.c_int32), ("partial", C.c_void_p)]
+
+
+def _mlp_layers(mlp: nn.Module):
+    """(l1, l2, l3, slope) of a Linear -> LeakyReLU -> Linear -> LeakyReLU -> Linear stack, else None."""
+    mods = list(mlp) if isinstance(mlp, nn.Sequential) else []
+    if len(mods) != 5:
+        return None
+    l1, a1, l2, a2, l3 = mods
+    if not (all(isinstance(m, nn.Linear) and m.bias is not None for m in (l1, l2, l3))
+            and isinstance(a1, nn.LeakyReLU) and isinstance(a2, nn.LeakyReLU) and a1.negative_slope == a2.negative_slope):
+        return None
+    return l1, l2, l3, float(a1.negative_slope)
+
+
+def networks_fusable(nets, xs) -> bool:
+    """gr_mlp_forward / _backward cover these networks on these inputs: the update's tall fp32 CUDA batches (inputs
+    without gradient, outside autocast) through Linear(d <= 32) -> LeakyReLU -> Linear(H, H) -> LeakyReLU ->
+    Linear(H, k <= 4) with H 128 or 256, one slope, 32-bit row offsets."""
+    if not torch.is_grad_enabled() or torch.is_autocast_enabled("cuda"):
+        return False
+    hs, slopes = set(), set()
+    for net, x in zip(nets, xs):
+        lay = _mlp_layers(net)
+        if lay is None:
+            return False
+        l1, l2, l3, slope = lay
+        if not (x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and not x.requires_grad
+                and (x.shape[0] >= 2 * SPLIT or _FORCE_FN) and x.shape[0] == xs[0].shape[0]):
+            return False
+        if not (l1.in_features == x.shape[1] and l1.in_features % 4 == 0 and l1.in_features <= 32
+                and l1.out_features == l2.in_features == l2.out_features == l3.in_features
+                and l3.out_features <= 4 and all(p.dtype == torch.float32 and p.is_cuda and p.requires_grad
+                                                  for m in (l1, l2, l3) for p in (m.weight, m.bias))):
+            return False
+        if x.stride(1) != 1 or x.stride(0) % 4 or x.data_ptr() % 16:
+            return False
+        if x.shape[0] * max(l1.out_features, x.stride(0)) >= 2 ** 31:
+            return False
+        hs.add(l1.out_features)
+        slopes.add(slope)
+    return len(hs) == 1 and hs.pop() in (128, 256) and len(slopes) == 1
+
+
+class _FusedMLPsFn(torch.autograd.Function):
+    """Up to two MLPs (the actor and the critic) on their input rows, forward and backward each as one set of
+    whole-network fp32-MFMA launches for both networks (gr_mlp_forward / gr_mlp_backward, gr_mlp.hip).  Forward
+    saves h1 and z2 per network; the backward writes the hidden layer's output gradient over z2 (each tile reads its
+    z2 rows before writing them) and returns every parameter gradient from one fixed-order reduction."""
+
+    @staticmethod
+    def forward(ctx, nnets, slope, *args):
+        xs, params = args[:nnets], args[nnets:]
+        rows = xs[0].shape[0]
+        dev = xs[0].device
+        a = GrMlpArgs()
+        a.rows, a.nets, a.slope = rows, nnets, float(slope)
+        keep, outs = [], []
+        for i in range(nnets):
+            w1, b1, w2, b2, w3, b3 = params[6 * i:6 * i + 6]
+            h = w1.shape[0]
+            h1 = torch.empty(rows, h, device=dev, dtype=torch.float32)
+            z2 = torch.empty(rows, h, device=dev, dtype=torch.float32)
+            y = torch.empty(rows, w3.shape[0], device=dev, dtype=torch.float32)
+            s = GrMlpNet()
+            s.x, s.ldx, s.d, s.k = xs[i].data_ptr(), xs[i].stride(0), w1.shape[1], w3.shape[0]
+            for name, t in (("w1", w1), ("b1", b1), ("w2", w2), ("b2", b2), ("w3", w3), ("b3", b3)):
+                setattr(s, name, t.data_ptr())
+            s.h1, s.z2, s.y = h1.data_ptr(), z2.data_ptr(), y.data_ptr()
+            a.net[i] = s
+            a.hidden = h
+            keep += [h1, z2]
+            outs.append(y)
+        _lib_call("gr_mlp_forward", C.byref(a), _stream(xs[0]))
+        ctx.nnets, ctx.slope = nnets, float(slope)
+        ctx.save_for_backward(*xs, *keep, *params)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gys):
+        from .. import _abi
+
+        nnets = ctx.nnets
+        saved = ctx.saved_tensors
+        xs, keep, params = saved[:nnets], saved[nnets:3 * nnets], saved[3 * nnets:]
+        rows = xs[0].shape[0]
+        dev = xs[0].device
+        a = GrMlpArgs()
+        a.rows, a.nets, a.slope = rows, nnets, ctx.slope
+        grads_out, gys_keep = [], []
+        for i in range(nnets):
+            w1, b1, w2, b2, w3, b3 = params[6 * i:6 * i + 6]
+            h, d, k = w1.shape[0], w1.shape[1], w3.shape[0]
+            h1, z2 = keep[2 * i], keep[2 * i + 1]
+            gy = gys[i]
+            gy = torch.zeros(rows, k, device=dev, dtype=torch.float32) if gy is None else gy.float().contiguous()
+            gys_keep.append(gy)
+            grads = torch.empty(h * d + h + h * h + h + k * h + k, device=dev, dtype=torch.float32)
+            s = GrMlpNet()
+            s.x, s.ldx, s.d, s.k = xs[i].data_ptr(), xs[i].stride(0), d, k
+            for name, t in (("w1", w1), ("b1", b1), ("w2", w2), ("b2", b2), ("w3", w3), ("b3", b3)):
+                setattr(s, name, t.data_ptr())
+            s.h1, s.z2, s.gy, s.gz2, s.grads = h1.data_ptr(), z2.data_ptr(), gy.data_ptr(), z2.data_ptr(), grads.data_ptr()
+            a.net[i] = s
+            a.hidden = h
+            o = 0
+            split = []
+            for shape in ((h, d), (h,), (h, h), (h,), (k, h), (k,)):
+                numel = 1
+                for e in shape:
+                    numel *= e
+                split.append(grads[o:o + numel].view(shape))
+                o += numel
+            grads_out += split
+        part = torch.empty(_abi.load().gr_mlp_partials(rows, a.hidden, nnets), device=dev, dtype=torch.float32)
+        a.partial = part.data_ptr()
+        _lib_call("gr_mlp_backward", C.byref(a), _stream(xs[0]))
+        return (None, None) + (None,) * nnets + tuple(grads_out)
+
+
+def fused_mlps(nets, xs):
+    """The outputs of `nets` (nn.Sequential MLPs) on `xs` through _FusedMLPsFn; call only when networks_fusable."""
+    params, slope = [], None
+    for net in nets:
+        l1, l2, l3, slope = _mlp_layers(net)
+        params += [l1.weight, l1.bias, l2.weight, l2.bias, l3.weight, l3.bias]
+    return _FusedMLPsFn.apply(len(nets), slope, *xs, *params)

@@ -30,7 +30,7 @@ class PPO:
                  use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu",
                  normalize_advantage=True, storage_obs_dtype=torch.float32, fused_rollout_inference=False,
                  fused_rollout_precision="bf16", graph_update=False, update_autocast_bf16=False,
-                 graph_update_segmented=False, fused_losses=True, fused_adam=True, **kwargs):
+                 graph_update_segmented=False, fused_losses=True, fused_adam=True, fused_mlp=True, **kwargs):
         self.env = env
         self.device = device
         self.desired_kl = desired_kl
@@ -78,6 +78,8 @@ class PPO:
         # the mini-batch losses (log prob, KL, surrogate, value loss) as one device op each way on CUDA
         # (fused_loss.py); False: the torch ops
         self.fused_losses = bool(fused_losses)
+        # with the fused losses: the actor and critic MLPs as whole-network fp32-MFMA kernels (linear.fused_mlps)
+        self.fused_mlp = bool(fused_mlp)
 
     def flat_grads(self) -> gdist.FlatGrads:
         """The flat gradient buffer over the parameters the loss reaches (all of them until the first mini-batch

@@ -474,6 +474,48 @@ int gr_mlp_in_forward(const float* x, int64_t rows, int32_t d, int32_t ldx, cons
 int gr_mlp_in_backward(const float* gh, const float* hv, const float* x, int64_t rows, int32_t d, int32_t ldx,
                        int32_t h, float slope, float* partial, float* sums, void* stream);
 
+/* The actor and critic MLPs of the PPO update as whole-network fp32-MFMA kernels (round 4): the mini-batch's
+ * forward and backward through x -> Linear(d, H) -> LeakyReLU -> Linear(H, H) -> LeakyReLU -> Linear(H, k) of both
+ * networks (upstream rsl_rl ActorCritic's MLPs as PPO.update runs them, standalone/rsl_rl/ext/algorithms/ppo.py:
+ * 103-190; loss.backward() through them), fp32 operands on v_mfma_f32_16x16x4_f32, one launch per direction for
+ * both networks (blockIdx.y = network) plus the weight gradient of the hidden layer and one fixed-order reduction:
+ *   gr_mlp_forward : y = MLP(x); saves h1 = lrelu(x W1^T + b1) and z2 = h1 W2^T + b2 for the backward
+ *   gr_mlp_backward: from gy [rows][k]: gz2 = (gy W3) * lrelu'(z2), gh1 = gz2 W2, gz1 = gh1 * lrelu'(h1);
+ *                    gW3 = gy^T lrelu(z2), gb3 = sum gy, gb2 = sum gz2, gW2 = gz2^T h1, gW1 = gz1^T x, gb1 = sum gz1
+ * H = 128 or 256, d <= 32 (a multiple of 4), k <= 4.  Row-major fp32, 16-byte aligned; the x rows may be strided
+ * (ldx floats: the update's packed mini-batch).  Context-free, graph-capturable, no atomics, fixed summation order;
+ * `partial` is caller-owned scratch of gr_mlp_partials(rows, H, nets) floats. */
+typedef struct gr_mlp_net {
+  const float* x;    /* [rows][ldx]: the first d columns are the input */
+  const float* w1;   /* [H][d] */
+  const float* b1;   /* [H] */
+  const float* w2;   /* [H][H] */
+  const float* b2;   /* [H] */
+  const float* w3;   /* [k][H] */
+  const float* b3;   /* [k] */
+  float* h1;         /* [rows][H]: forward output (saved), backward input */
+  float* z2;         /* [rows][H]: forward output (saved), backward input */
+  float* y;          /* [rows][k]: forward output */
+  const float* gy;   /* [rows][k]: backward input */
+  float* gz2;        /* [rows][H]: backward scratch (the hidden layer's output gradient) */
+  float* grads;      /* backward output [H d | H | H H | H | k H | k] = gW1, gb1, gW2, gb2, gW3, gb3 */
+  int64_t ldx;
+  int32_t d, k;
+} gr_mlp_net;
+typedef struct gr_mlp_args {
+  gr_mlp_net net[2];
+  int64_t rows;
+  int32_t nets;   /* 1 or 2 */
+  int32_t hidden; /* H */
+  float slope;    /* LeakyReLU negative slope */
+  int32_t reserved;
+  float* partial; /* scratch */
+} gr_mlp_args;
+int64_t gr_mlp_partials(int64_t rows, int32_t hidden, int32_t nets);
+int gr_mlp_forward(const gr_mlp_args* args, void* stream);
+int gr_mlp_backward(const gr_mlp_args* args, void* stream);
+size_t gr_mlp_args_size(void);
+
 /* The PPO losses of one mini-batch, forward and backward (standalone/rsl_rl/ext/algorithms/ppo.py:133-169: the
  * adaptive-rate KL, the clipped surrogate, the (clipped) value loss; the Gaussian log prob of rsl_rl's
  * ActorCritic with a state-independent std).  Row-strided fp32 inputs (ld_* in floats; the mini-batch's packed

@@ -1,0 +1,88 @@
+"""The update's whole-network MLP kernels (gr_mlp_forward / gr_mlp_backward, csrc/gr_mlp.hip; rsl_rl/linear.py
+fused_mlps) against a float64 evaluation of the same modules: the actor and critic outputs and every parameter
+gradient of both networks, on strided input rows (the packed mini-batch), ragged row counts (tails of the 64- and
+32-row tiles) and both hidden sizes.  Tolerance: the outputs within 1e-5 of their scale, the gradients within 1e-5 of
+each tensor's norm (fp32 sums over up to 2.5e4 rows; the round-3 per-layer path is held to the same bound), and
+repeat runs bit-identical (fixed summation order)."""
+import pytest
+import torch
+import torch.nn as nn
+
+from generalizableracing_amd.rsl_rl import linear as lin
+from generalizableracing_amd.rsl_rl.actor_critic import ActorCritic
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _packed(rows, d_a, d_c, width=48, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    buf = torch.randn(rows, width, generator=g).to(DEV)
+    return buf, buf[:, :d_a], buf[:, d_a:d_a + d_c]
+
+
+def _f64(net):
+    # plain nn.Linear (TallLinear's tall-batch backward would take fp32 column sums)
+    m = nn.Sequential(*[nn.Linear(x.in_features, x.out_features) if isinstance(x, nn.Linear) else x for x in net])
+    m.load_state_dict(net.state_dict())
+    return m.double()
+
+
+@pytest.mark.parametrize("rows,hidden,d", [(24576 + 13, 256, 16), (4096, 128, 16), (1, 256, 16), (77, 256, 8),
+                                          (9000, 256, 32)])
+def test_fused_mlps_match_float64(rows, hidden, d):
+    torch.manual_seed(rows + hidden)
+    pol = ActorCritic(d, d, 4, [hidden, hidden], [hidden, hidden], "lrelu").to(DEV)
+    nets = [pol.actor, pol.critic]
+    buf, xa, xc = _packed(rows, d, d, width=max(48, 2 * d + 16))
+    assert xa.stride(0) == buf.shape[1]
+    ya, yc = lin.fused_mlps(nets, [xa, xc])
+    ref = [_f64(n) for n in nets]
+    ra, rc = ref[0](xa.double()), ref[1](xc.double())
+    for y, r in ((ya, ra), (yc, rc)):
+        scale = float(r.abs().max())
+        assert float((y.double() - r).abs().max()) <= 1e-5 * scale, (float((y.double() - r).abs().max()), scale)
+    ga = torch.randn_like(ya) / rows
+    gc = torch.randn_like(yc) / rows
+    grads = torch.autograd.grad((ya * ga).sum() + (yc * gc).sum(), [p for n in nets for p in n.parameters()])
+    gref = torch.autograd.grad((ra * ga.double()).sum() + (rc * gc.double()).sum(),
+                               [p for n in ref for p in n.parameters()])
+    names = [f"{w}.{k}" for w, n in (("actor", pol.actor), ("critic", pol.critic)) for k, _ in n.named_parameters()]
+    for name, g, r in zip(names, grads, gref):
+        err, nrm = float((g.double() - r).norm()), float(r.norm())
+        assert err <= 1e-5 * nrm + 1e-12, (name, err, nrm)
+    # deterministic: the same bits again
+    ya2, yc2 = lin.fused_mlps(nets, [xa, xc])
+    grads2 = torch.autograd.grad((ya2 * ga).sum() + (yc2 * gc).sum(), [p for n in nets for p in n.parameters()])
+    assert torch.equal(ya, ya2) and torch.equal(yc, yc2)
+    for g, g2 in zip(grads, grads2):
+        assert torch.equal(g, g2)
+
+
+def test_fused_mlp_single_network_and_unused_output():
+    """One network (nets = 1), and a critic whose output gets no gradient (its gradients are zero)."""
+    torch.manual_seed(3)
+    pol = ActorCritic(16, 16, 4, [256, 256], [256, 256], "lrelu").to(DEV)
+    _, xa, xc = _packed(5000, 16, 16, seed=2)
+    (ya,) = lin.fused_mlps([pol.actor], [xa])
+    r = _f64(pol.actor)(xa.double())
+    assert float((ya.double() - r).abs().max()) <= 1e-5 * float(r.abs().max())
+    ya, yc = lin.fused_mlps([pol.actor, pol.critic], [xa, xc])
+    gs = torch.autograd.grad(ya.sum(), list(pol.actor.parameters()) + list(pol.critic.parameters()))
+    for g in gs[6:]:
+        assert torch.count_nonzero(g) == 0
+
+
+def test_fused_mlp_covers_the_update_and_falls_back():
+    """networks_fusable: the update's tall fp32 batches of the reference's MLP(256, 256) LeakyReLU policy; not ELU,
+    not inputs that need a gradient, not k > 4."""
+    pol = ActorCritic(16, 16, 4, [256, 256], [256, 256], "lrelu").to(DEV)
+    _, xa, xc = _packed(8192, 16, 16)
+    assert lin.networks_fusable([pol.actor, pol.critic], [xa, xc])
+    with torch.no_grad():
+        assert not lin.networks_fusable([pol.actor, pol.critic], [xa, xc])
+    assert not lin.networks_fusable([pol.actor, pol.critic], [xa.detach().clone().requires_grad_(), xc])
+    elu = ActorCritic(16, 16, 4, [256, 256], [256, 256], "elu").to(DEV)
+    assert not lin.networks_fusable([elu.actor, elu.critic], [xa, xc])
+    wide = ActorCritic(16, 16, 8, [256, 256], [256, 256], "lrelu").to(DEV)
+    assert not lin.networks_fusable([wide.actor, wide.critic], [xa, xc])
