@@ -45,6 +45,7 @@ FP32_MFMA_PEAK_TFS = 157.3  # MI355X dense fp32 matrix peak (v_mfma_f32_16x16x4_
 UPDATE_FLOPS_PER_SAMPLE = 2 * (2 * (16 * 256 + 256 * 256 + 256 * 4 + 16 * 256 + 256 * 256 + 256)
                                + (256 * 256 + 256 * 4 + 256 * 256 + 256))
 ACTION_RING = 64
+STREAM_FLOOR_US = 5.15  # 65 536 envs: the step's own bytes as a pure stream (BASELINE §2)
 
 
 def parse():
@@ -763,6 +764,10 @@ def main():
                                     else f"gr::step_kernel<true, false, {8 if a.gates <= 8 else 0}, 0>")
                                    + " (fused step)", **kt,
                          "algorithmic_bytes_per_launch": (rd + wr) * n,
+                         # the measured floor: a pure coalesced stream of exactly these bytes in the same launch shape
+                         # and hipGraph (tools/streambench.hip, profiles/round01_streambench.json), 65 536 envs
+                         "stream_floor_us": STREAM_FLOOR_US if n == 65536 and not a.obstacles else None,
+                         "frac_of_stream_floor": STREAM_FLOOR_US / us if n == 65536 and not a.obstacles else None,
                          "bytes_per_env_step": {"read": rd, "written": wr}},
             "cpu_baseline": cpu,
             **extra,

@@ -816,6 +816,41 @@ void gro_test_philox(int n, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, 
   }
 }
 
+/* The random values env i's step / reset / observation consume (tests/golden/make_golden_noise.py feeds them to the
+ * reference's own functions in place of torch's draws, so the arithmetic that APPLIES them is pinned):
+ *   kind 0: observation noise of call counter c1 (compute_obs): out[0..5] = the six N(0,1), velocity 0-2 then the
+ *           attitude euler angles 3-5 (before x obs_att_noise)
+ *   kind 1: gate-pose noise of (epoch c1, gates passed c3) (gate_noise): out[0..5] = the six U(0,1), gate x y z
+ *           then next gate x y z
+ *   kind 2: reset draws of epoch c1 (reset_env: the epoch AFTER the reset): out[0..23] = the 24 fields as U(0,1),
+ *           out[24] = the thrust-error N(0,1)
+ *   kind 3: startup draws (gro_init): out[0..13] = U(0,1) of Kp 0-2, Kd 3-5, thrust delay 6, torque delays 7-9,
+ *           mass add 10, inertia 11-13; out[14] = the initial-level U(0,1); out[15] = the thrust-error N(0,1) */
+void gro_draws(const gr_config* c, int i, int kind, uint32_t c1, uint32_t c3, float* out) {
+  const uint32_t gid = gid_of(c, i);
+  uint32_t f[24];
+  if (kind == 0) {
+    gr_fields6(draw(c, gid, c1, GR_TAG_OBS, 0), f);
+    for (int k = 0; k < 3; ++k) gr_box_muller21(f[2 * k], f[2 * k + 1], &out[2 * k], &out[2 * k + 1]);
+  } else if (kind == 1) {
+    gr_fields6(draw(c, gid, c1, GR_TAG_GATE, c3), f);
+    for (int k = 0; k < 6; ++k) out[k] = gr_f21(f[k]);
+  } else if (kind == 2) {
+    for (int b = 0; b < 4; ++b) gr_fields6(draw(c, gid, c1, GR_TAG_RESET, (uint32_t)b), f + 6 * b);
+    for (int k = 0; k < 24; ++k) out[k] = gr_f21(f[k]);
+    float z1;
+    gr_box_muller21(f[20], f[21], &out[24], &z1);
+  } else {
+    gr_u32x4 b0 = draw(c, gid, 0, GR_TAG_STATIC, 0), b1 = draw(c, gid, 0, GR_TAG_STATIC, 1);
+    gr_u32x4 b2 = draw(c, gid, 0, GR_TAG_STATIC, 2), b3 = draw(c, gid, 0, GR_TAG_STATIC, 3);
+    gr_u32x4 b4 = draw(c, gid, 0, GR_TAG_STATIC, 4);
+    const uint32_t w[15] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w, b2.x, b2.y, b2.z, b2.w, b3.x, b3.y, b3.z};
+    for (int k = 0; k < 15; ++k) out[k] = gr_u01(w[k]);
+    float z1;
+    gr_box_muller(b3.w, b4.x, &out[15], &z1);
+  }
+}
+
 void gro_test_fields6(int n, const uint32_t* in4, uint32_t* out6) {
   for (int i = 0; i < n; ++i) {
     gr_u32x4 r = {in4[i * 4], in4[i * 4 + 1], in4[i * 4 + 2], in4[i * 4 + 3]};

@@ -80,6 +80,8 @@ void gro_camera_cull_check(const gr_config* cfg, const gr_camera_config* kcfg, c
                            const float p[3], const float q[4], int64_t out[8]);
 void gro_camera_frame(const gr_config* cfg, const gr_camera_config* kcfg, const float p[3], const float q[4],
                       float* out);
+/* the random values env i consumes (kind 0 observation noise, 1 gate noise, 2 reset, 3 startup; gr_oracle.c) */
+void gro_draws(const gr_config* cfg, int i, int kind, uint32_t c1, uint32_t c3, float* out);
 /* OpenMP threads gro_step uses (1 without OpenMP) */
 int gro_num_threads(void);
 

@@ -55,6 +55,7 @@ def load():
             "gro_camera": [vp, vp, vp, C.c_int, vp, C.c_int, vp, vp, vp, C.c_uint32, vp, vp, vp, vp, vp, vp],
             "gro_camera_frame": [vp, vp, vp, vp, vp],
             "gro_camera_cull_check": [vp, vp, vp, C.c_int, vp, vp, vp],
+            "gro_draws": [vp, C.c_int, C.c_int, C.c_uint32, C.c_uint32, vp],
         }.items():
             f = getattr(lib, name)
             f.restype = None
@@ -214,6 +215,18 @@ def test_philox(n, c0, c1, c2, c3, k0, k1):
     out = np.zeros((n, 4), np.uint32)
     lib.gro_test_philox(n, c0, c1, c2, c3, k0, k1, _p(out))
     return out
+
+
+DRAW_OBS, DRAW_GATE, DRAW_RESET, DRAW_STATIC = 0, 1, 2, 3
+DRAW_LEN = {DRAW_OBS: 6, DRAW_GATE: 6, DRAW_RESET: 25, DRAW_STATIC: 16}
+
+
+def draws(cfg, i: int, kind: int, c1: int = 0, c3: int = 0) -> np.ndarray:
+    """gro_draws: the random values env i (of cfg's shard) consumes for `kind` (DRAW_*), as fp32."""
+    out = np.zeros(25, np.float32)
+    load().gro_draws(C.byref(cfg), int(i), int(kind), C.c_uint32(c1 & 0xFFFFFFFF), C.c_uint32(c3 & 0xFFFFFFFF),
+                     _p(out))
+    return out[:DRAW_LEN[kind]]
 
 
 def num_threads() -> int:

@@ -146,6 +146,98 @@ def yaw_quat(quat):
     return normalize(out)
 
 
+# IL sample_uniform: torch.rand(size) * (upper - lower) + lower.  SAMPLE_HOOK (a callable(size) -> tensor of U(0, 1), or
+# None) lets a fixture generator feed the draws (make_golden_noise.py injects the build's Philox values).
+SAMPLE_HOOK = None
+
+
+def sample_uniform(lower, upper, size, device=None):
+    if isinstance(size, int):
+        size = (size,)
+    u = SAMPLE_HOOK(tuple(size)) if SAMPLE_HOOK is not None else torch.rand(*size, device=device)
+    return u * (upper - lower) + lower
+
+
+def _randomize_prop_by_op(data, distribution_parameters, dim_0_ids, dim_1_ids, operation, distribution):
+    """omni.isaac.lab.envs.mdp.events._randomize_prop_by_op (IL 1.x), restated for the uniform distribution."""
+    if dim_0_ids is None:
+        n_dim_0 = data.shape[0]
+        dim_0_ids = slice(None)
+    else:
+        n_dim_0 = len(dim_0_ids)
+        if not isinstance(dim_1_ids, slice):
+            dim_0_ids = dim_0_ids[:, None]
+    n_dim_1 = data.shape[1] if isinstance(dim_1_ids, slice) else len(dim_1_ids)
+    if distribution != "uniform":
+        raise NotImplementedError("not restated: not on the fixture path")
+    v = sample_uniform(*distribution_parameters, (n_dim_0, n_dim_1), device=data.device)
+    if operation == "add":
+        data[dim_0_ids, dim_1_ids] += v
+    elif operation == "scale":
+        data[dim_0_ids, dim_1_ids] *= v
+    elif operation == "abs":
+        data[dim_0_ids, dim_1_ids] = v
+    else:
+        raise NotImplementedError(operation)
+    return data
+
+
+# ------------------------------------------------------------------ scripted draws (make_golden_noise.py)
+class TorchProxy:
+    """A reference module's `torch` with some call sites replaced (injected draws); everything else is torch."""
+
+    def __init__(self, **over):
+        self._over = over
+
+    def __getattr__(self, k):
+        return self._over[k] if k in self._over else getattr(torch, k)
+
+
+class Queue:
+    """Scripted draws: each call site takes the next tensor, which must have the requested shape."""
+
+    def __init__(self, items=()):
+        self.items = [torch.as_tensor(t, dtype=torch.float32) for t in items]
+
+    def push(self, t):
+        self.items.append(torch.as_tensor(t, dtype=torch.float32))
+
+    def take(self, shape):
+        t = self.items.pop(0)
+        assert tuple(t.shape) == tuple(shape), (tuple(t.shape), tuple(shape))
+        return t.clone()
+
+    def done(self):
+        assert not self.items, f"{len(self.items)} scripted draws unused"
+
+
+class ScriptedUniform:
+    """torch.empty(n) stand-in whose uniform_() yields the next scripted U(0, 1) tensor (commands.py's `r`)."""
+
+    def __init__(self, q, n):
+        self.q, self.n = q, n
+
+    def uniform_(self):
+        return self.q.take((self.n,))
+
+
+def size_of(size):
+    return tuple(size[0]) if len(size) == 1 and isinstance(size[0], (tuple, list)) else tuple(size)
+
+
+def push_gate_noise(q, u):
+    """The 12 uniform_ draws of one _resample_command / _update_command over envs with gate-noise draws u [m, 6] (gate
+    x y z, next gate x y z): gate x y z roll pitch yaw, next gate x y z roll pitch yaw; the orientation draws are 0.5
+    (zero angle: gate orientations are not observed)."""
+    u = torch.as_tensor(u, dtype=torch.float32)
+    half = torch.full((u.shape[0],), 0.5)
+    for base in (0, 3):
+        for k in range(3):
+            q.push(u[:, base + k])
+        for _ in range(3):
+            q.push(half)
+
+
 def _unsupported(*a, **k):
     raise NotImplementedError("not restated: not on the fixture path")
 
@@ -169,13 +261,15 @@ def install():
     mods = {}
     for n in ["omni", "omni.isaac", "omni.isaac.lab", "omni.isaac.lab.utils", "omni.isaac.lab.utils.math",
               "omni.isaac.lab.managers", "omni.isaac.lab.assets", "omni.isaac.lab.sensors", "omni.isaac.lab.markers",
-              "omni.isaac.lab.terrains", "omni.isaac.lab.envs", "diff", "diff.lab", "diff.lab.utils",
-              "diff.lab.controllers"]:
+              "omni.isaac.lab.terrains", "omni.isaac.lab.envs", "omni.isaac.lab.envs.mdp",
+              "omni.isaac.lab.envs.mdp.events", "diff", "diff.lab", "diff.lab.utils", "diff.lab.controllers",
+              "diff.lab.terrains"]:
         mods[n] = sys.modules.get(n) or types.ModuleType(n)
         sys.modules[n] = mods[n]
     m = mods["omni.isaac.lab.utils.math"]
     for f in (quat_mul, quat_rotate, quat_rotate_inverse, quat_conjugate, quat_inv, quat_from_euler_xyz, quat_unique,
-              matrix_from_quat, euler_xyz_from_quat, wrap_to_pi, compute_pose_error, yaw_quat, normalize):
+              matrix_from_quat, euler_xyz_from_quat, wrap_to_pi, compute_pose_error, yaw_quat, normalize,
+              sample_uniform):
         setattr(m, f.__name__, f)
     m.subtract_frame_transforms = _unsupported
     m.orthogonalize_perspective_depth = _unsupported
@@ -186,7 +280,10 @@ def install():
         setattr(mg, cname, type(cname, (_Base,), {}))
     for cname in ("Articulation", "RigidObject"):
         setattr(mods["omni.isaac.lab.assets"], cname, type(cname, (_Base,), {}))
-    for cname in ("ContactSensor", "FrameTransformerData", "TiledCamera", "Camera", "RayCasterCamera"):
+    mods["omni.isaac.lab.envs.mdp.events"]._randomize_prop_by_op = _randomize_prop_by_op
+    mods["diff.lab.terrains"].TerrainImporterCfg = type("TerrainImporterCfg", (_Base,), {})
+    for cname in ("ContactSensor", "FrameTransformerData", "TiledCamera", "Camera", "RayCasterCamera",
+                  "RayCasterCameraCfg"):
         setattr(mods["omni.isaac.lab.sensors"], cname, type(cname, (_Base,), {}))
     mods["omni.isaac.lab.markers"].VisualizationMarkers = type("VisualizationMarkers", (_Base,), {})
     mods["omni.isaac.lab.terrains"].TerrainImporter = type("TerrainImporter", (_Base,), {})
@@ -237,6 +334,6 @@ def load_mdp():
     synthetic_package("grref_mdp.dynamics", os.path.join(MDP_DIR, "dynamics"))
     out = {"droneDynamics": load("grref_mdp.dynamics.droneDynamics", os.path.join(MDP_DIR, "dynamics/droneDynamics.py"),
                                  "grref_mdp.dynamics")}
-    for name in ("diff_action", "rewards", "observation", "termination", "curriculums", "commands"):
+    for name in ("diff_action", "rewards", "observation", "termination", "curriculums", "commands", "events"):
         out[name] = load(f"grref_mdp.{name}", os.path.join(MDP_DIR, f"{name}.py"), "grref_mdp")
     return out

@@ -163,10 +163,13 @@ class Scene(dict):
     pass
 
 
-def reference_step(st, stage, gate_pose, start, origin_z, collide, carry=False):
+def reference_step(st, stage, gate_pose, start, origin_z, collide, carry=False, noise=None):
     """One step of the reference composition from pre-state `st` (dict of numpy arrays).  carry=True also returns
     what the next step of a free run starts from (make_golden_freerun.py): the controller's filter state and the
-    body angular acceleration of the DroneDynamics step (the D-term input the simulator reports next step)."""
+    body angular acceleration of the DroneDynamics step (the D-term input the simulator reports next step).
+    noise (make_golden_noise.py part G): the gate-pose and observation noise on, with injected draws: noise.gu_pre
+    [n, 6] = the noise of the gates each env holds, noise.gu_new / gu_rst = the draws of an update (gate passed) /
+    a resample (reset), noise.nz [n, 6] = the observation noise."""
     mdp = il_shim.load_mdp()
     DroneDynamics = mdp["droneDynamics"].DroneDynamics
     DiffActions = mdp["diff_action"].DiffActions
@@ -257,7 +260,7 @@ def reference_step(st, stage, gate_pose, start, origin_z, collide, carry=False):
 
     # ---- command term (RacingCommand without IL's __init__; fields as __init__ sets them)
     cmd = Cm.RacingCommand.__new__(Cm.RacingCommand)
-    cmd.cfg = NS(consecutive_commands=True, add_noise=False, make_quat_unique=False, update_threshold=0.35)
+    cmd.cfg = NS(consecutive_commands=True, add_noise=noise is not None, make_quat_unique=False, update_threshold=0.35)
     cmd.robot, cmd.env, cmd.num_envs, cmd.device = robot, env, n, "cpu"
     cmd.gate_pose = gp
     cmd.gate_id = torch.tensor(st["gate_id"], dtype=torch.long)
@@ -275,6 +278,16 @@ def reference_step(st, stage, gate_pose, start, origin_z, collide, carry=False):
     for nm in ("pos_x", "pos_y", "pos_z", "roll", "pitch", "yaw"):
         setattr(cmd, f"noise_range_{nm}", torch.tensor([[-0.1, 0.1]]).repeat(n, 1) * nl)
     cmd.noise_level = nl.clone()
+    if noise is not None:  # the noisy gates the envs hold from before the step (their (episode, gates passed) draws)
+        u = torch.tensor(noise.gu_pre, dtype=torch.float32)
+        for k, nm in enumerate(("pos_x", "pos_y", "pos_z")):
+            rg = getattr(cmd, f"noise_range_{nm}")
+            cmd.gate_pose_w[:, k] += rg[:, 0] + u[:, k] * (rg[:, 1] - rg[:, 0])
+            cmd.next_gate_pose_w[:, k] += rg[:, 0] + u[:, 3 + k] * (rg[:, 1] - rg[:, 0])
+        gq = il_shim.Queue()
+        cm_torch = Cm.torch
+        Cm.torch = il_shim.TorchProxy(empty=lambda *size, device=None, **kw: il_shim.ScriptedUniform(
+            gq, il_shim.size_of(size)[0]))
     env.command_manager = NS(get_term=lambda name: cmd, _terms={"next_gate_pose": cmd},
                              get_command=lambda name: cmd.command)
 
@@ -319,16 +332,37 @@ def reference_step(st, stage, gate_pose, start, origin_z, collide, carry=False):
         lv_tmp = terrain.terrain_levels.clone()
         lv_tmp[ids[~lv_ok]] = 0  # (the random level is not comparable; any level serves the resample)
         terrain.terrain_levels = lv_tmp
+        if noise is not None:
+            il_shim.push_gate_noise(gq, noise.gu_rst[ids.numpy()])
         cmd._resample_command(ids)
         terrain.terrain_levels[ids[~lv_ok]] = -1
     reset_gate = cmd.gate_id.clone()
     # ---- command compute: metrics, then gate progress (commands.py:247-260, 308-350)
     cmd._update_metrics()
+    if noise is not None:  # the envs _update_command will draw for (commands.py:309-310)
+        hit = torch.norm(cmd.gate_pose_gt_w[:, :3] - data.root_state_w[:, :3], dim=-1) < cmd.cfg.update_threshold
+        if hit.any():
+            il_shim.push_gate_noise(gq, noise.gu_new[hit.numpy()])
     cmd._update_command()
-    # ---- observations (noise-free policy group: obs_noise / gate noise off in the build too)
-    pol = torch.cat([O.modified_base_lin_vel(env, add_noise=False), O.base_orientation_r(env, add_noise=False),
-                     O.modified_generated_commands(env, "next_gate_pose"),
-                     O.modified_last_action(env, "force_torque")], 1)
+    if noise is not None:
+        Cm.torch = cm_torch
+        gq.done()
+    # ---- observations (noise-free policy group unless `noise`: then the injected observation noise)
+    if noise is None:
+        pol = torch.cat([O.modified_base_lin_vel(env, add_noise=False), O.base_orientation_r(env, add_noise=False),
+                         O.modified_generated_commands(env, "next_gate_pose"),
+                         O.modified_last_action(env, "force_torque")], 1)
+    else:
+        z = torch.tensor(noise.nz, dtype=torch.float32)
+        o_torch = O.torch
+        O.torch = il_shim.TorchProxy(randn_like=lambda x, **kw: z[:, 0:3].clone(),
+                                     randn=lambda *size, device=None, **kw: z[:, 3:6].clone())
+        try:
+            pol = torch.cat([O.modified_base_lin_vel(env, add_noise=True), O.base_orientation_r(env, add_noise=True),
+                             O.modified_generated_commands(env, "next_gate_pose"),
+                             O.modified_last_action(env, "force_torque")], 1)
+        finally:
+            O.torch = o_torch
     cri = torch.cat([O.modified_base_lin_vel(env, add_noise=False), O.base_orientation_r(env, add_noise=False),
                      O.modified_generated_commands_gt(env, "next_gate_pose"),
                      O.modified_last_action(env, "force_torque")], 1)
