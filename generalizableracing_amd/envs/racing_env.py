@@ -201,7 +201,9 @@ class RacingEnv:
                 dv = {k: v.to(dev, non_blocking=True) for k, v in pin.items()}
                 done = torch.cuda.Event()
                 done.record(side)
-            return g, gates, recs, obst, pin, dv, done
+            # the swap's arguments, built here too: the interval step only makes its launches
+            structs = self._terrain_structs(recs, obst, dv)
+            return g, gates, recs, obst, pin, dv, done, structs
 
         self._next_terrain = self._builder.submit(work)
 
@@ -231,7 +233,25 @@ class RacingEnv:
         self._obst_struct = o
         self._call("gr_bind_obstacles", C.byref(o))
 
-    def regenerate_terrain(self):
+    @staticmethod
+    def _terrain_structs(recs, obst, dv):
+        """gr_swap_terrain's arguments for a built generation: the host track records, and the device / host
+        gr_obstacles (None without obstacles)."""
+        recs_h = C.c_void_p(recs.ctypes.data)
+        if obst is None:
+            return recs_h, None, None
+        o, oh = _abi.GrObstacles(), _abi.GrObstacles()
+        for k in ("records", "counts", "grid_f", "grid_i", "cells", "items"):
+            setattr(o, k, dv["o_" + k].data_ptr())
+        for k in ("counts", "grid_f", "grid_i", "cells"):
+            setattr(oh, k, getattr(obst, k).ctypes.data)
+        for x in (o, oh):
+            x.max_obstacles = obst.max_obstacles
+            x.num_cells = int(obst.cells.shape[0])
+            x.num_items = int(obst.items.shape[0])
+        return recs_h, o, oh
+
+    def regenerate_terrain(self, out_set: dict | None = None):
         """EventCfg.reset_terrain -> reset_terrain_period (mdp/events.py:180-204): a new terrain
         (next seed of this shard's stream), then env.reset() of every env.
 
@@ -242,7 +262,7 @@ class RacingEnv:
         g = self.terrain_generation + 1
         dev = self.device
         if self._next_terrain is not None:
-            g_built, gates, recs, obst, pin, dv, done = self._next_terrain.result()
+            g_built, gates, recs, obst, pin, dv, done, structs = self._next_terrain.result()
             assert g_built == g
             cur = torch.cuda.current_stream(dev)
             cur.wait_event(done)
@@ -255,31 +275,23 @@ class RacingEnv:
                 for k in ("records", "counts", "grid_f", "grid_i", "cells", "items"):
                     pin["o_" + k] = torch.from_numpy(getattr(obst, k))
             dv = {k: v.to(dev) for k, v in pin.items()}
+            structs = self._terrain_structs(recs, obst, dv)
         self._next_terrain = None
         self._held_terrain = (self.track_gates, self.track_records, self.obstacles, pin)
         self.track_gates, self.track_records = dv["gates"], dv["records"]
-        recs_h = C.c_void_p(recs.ctypes.data)
+        recs_h, o, oh = structs
         if obst is None:
             self.obstacles = None
             self._call("gr_swap_terrain", self.track_gates.data_ptr(), self.track_records.data_ptr(), recs_h, None, None,
                        self._stream())
         else:
             self.obstacles = {k: dv["o_" + k] for k in ("records", "counts", "grid_f", "grid_i", "cells", "items")}
-            o, oh = _abi.GrObstacles(), _abi.GrObstacles()
-            for k, v in self.obstacles.items():
-                setattr(o, k, v.data_ptr())
-            for k in ("counts", "grid_f", "grid_i", "cells"):
-                setattr(oh, k, getattr(obst, k).ctypes.data)
-            for x in (o, oh):
-                x.max_obstacles = obst.max_obstacles
-                x.num_cells = int(obst.cells.shape[0])
-                x.num_items = int(obst.items.shape[0])
             self._obst_struct = o
             self._call("gr_swap_terrain", self.track_gates.data_ptr(), self.track_records.data_ptr(), recs_h,
                        C.byref(o), C.byref(oh), self._stream())
         self.obstacle_table = obst
         self.terrain_generation = g
-        return self.reset()
+        return self.reset(out_set=out_set)
 
     # ------------------------------------------------------------------ plumbing
     @staticmethod
@@ -316,13 +328,24 @@ class RacingEnv:
         b.counter_index = k % 2
         return b
 
-    def _bind(self, k: int):
+    def _bind(self, k: int, out_set: dict | None = None, prev_set: dict | None = None):
+        """Bind call k's buffers; out_set / prev_set (output-set dicts) replace the call's output / previous rows
+        (the terrain interval step's reset writes a scratch set: _regenerate_in_step)."""
         b = self._bufs[k % LOG_RING]
-        if self._sink_out is not None or self._last_rows is not None:
+        if self._sink_out is not None or self._last_rows is not None or out_set is not None or prev_set is not None:
             b = _abi.GrBuffers.from_buffer_copy(b)
             if self._last_rows is not None:  # gr_reset / gr_observe carry the last action from the rows last written
                 b.prev_obs_critic = self._last_rows[1].data_ptr()
-            if self._sink_out is not None:
+            if prev_set is not None:
+                b.prev_obs_critic = prev_set["critic"].data_ptr()
+                b.prev_obs_aux = prev_set["auxiliary"].data_ptr()
+                b.prev_time_out = prev_set["time_out"].data_ptr()
+            if out_set is not None:
+                for f, key in (("obs_policy", "policy"), ("obs_critic", "critic"), ("obs_aux", "auxiliary"),
+                               ("reward", "reward"), ("terminated", "terminated"), ("time_out", "time_out"),
+                               ("dones", "dones")):
+                    setattr(b, f, out_set[key].data_ptr())
+            elif self._sink_out is not None:
                 b.obs_policy, b.obs_critic = self._sink_out[0].data_ptr(), self._sink_out[1].data_ptr()
         self._call("gr_bind_buffers", C.byref(b))
         if getattr(self, "camera", None) is not None:
@@ -344,13 +367,13 @@ class RacingEnv:
         if rc != 0:
             raise RuntimeError(f"{name} failed (status {rc}): {self._lib.gr_last_error(self._ctx).decode()}")
 
-    def _advance(self):
+    def _advance(self, out_set: dict | None = None, prev_set: dict | None = None):
         """Bind the next output set + log slab; returns (output set, extras["log"] of this call)."""
         k = self._calls
-        self._bind(k)
+        self._bind(k, out_set, prev_set)
         self._calls += 1
         self._cur = (k + 1) % 2
-        self._last_rows = self._sink_out
+        self._last_rows = self._sink_out if out_set is None else None
         self._last_img = self._cam_sink_out
         lg = _EpisodeLog(self, k, self._log_keys)
         self._logs[k % LOG_RING] = lg
@@ -517,6 +540,17 @@ class RacingEnv:
         observation pass (call k+2) writes the post-reset observations back into set B, over the step's
         observation rows only; set A's rows are then restored.  The next step (call k+3) writes set A and
         reads the post-reset rows of set B as its previous observation."""
+        if self.camera is None:
+            # the reset's own observation (discarded by the reference: the step computes them again) goes to a scratch
+            # output set, so the runner's held set is never written and nothing is saved / restored: the interval step
+            # is gr_swap_terrain + gr_reset(all) + gr_observe on the stream
+            scratch = getattr(self, "_scratch_set", None)
+            if scratch is None:
+                scratch = self._scratch_set = self._alloc_outputs(self.num_envs, self.device)
+            _, extras = self.regenerate_terrain(out_set=scratch)
+            self._observe_after(scratch)
+            self.extras = {"log": extras["log"], "terrain_regenerated": True}
+            return
         held = self._sets[(self._cur + 1) % 2]
         # (with the fp32 sink as the output the reset and observation passes write the step's slot, which is what
         # the step returns; the runner's previous slot is not touched)
@@ -535,8 +569,9 @@ class RacingEnv:
                 held_img[k].copy_(v)
         self.extras = {"log": extras["log"], "terrain_regenerated": True}
 
-    def reset(self, seed: int | None = None, env_ids=None, options=None):
-        """ManagerBasedEnv.reset -> _reset_idx(env_ids) (+ curriculum), then observations."""
+    def reset(self, seed: int | None = None, env_ids=None, options=None, out_set: dict | None = None):
+        """ManagerBasedEnv.reset -> _reset_idx(env_ids) (+ curriculum), then observations.  out_set: write the
+        call's outputs into this output-set dict instead of the next ping-pong set (_regenerate_in_step)."""
         mask_t = None
         empty = False
         if env_ids is not None:
@@ -544,7 +579,9 @@ class RacingEnv:
             empty = ids.numel() == 0
             mask_t = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
             mask_t[ids] = 1
-        out, log = self._advance()
+        out, log = self._advance(out_set)
+        if out_set is not None:
+            out = out_set
         log._empty_reset = empty
         mp = mask_t.data_ptr() if mask_t is not None else None
         self._call("gr_reset", mp, self._stream())
@@ -596,6 +633,11 @@ class RacingEnv:
         self._call("gr_observe", self._stream())
         self._render(_abi.GR_CAM_OBSERVE)
         return self._obs_dict(out)
+
+    def _observe_after(self, prev_set: dict):
+        """observe() whose previous rows (the last action the rows carry) are prev_set's."""
+        self._advance(prev_set=prev_set)
+        self._call("gr_observe", self._stream())
 
     def seed(self, seed: int = -1) -> int:
         return seed
