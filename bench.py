@@ -62,10 +62,18 @@ def parse():
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="skip policy/train/cpu legs (profiling runs)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--legs", default="all",
+                   help="comma-separated extra legs to run (policy, obstacles, sweep, c5, regen, train4096, train65536, "
+                        "camera, vision, cpu) or 'all'; the headline step always runs")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL, one GPU per rank); gloo only to rehearse the multi-rank path with ranks "
                         "sharing one GPU")
     return p.parse_args()
+
+
+def want(a, leg: str) -> bool:
+    """Whether the extra leg `leg` runs (--legs; all by default, none with --no-extras)."""
+    return not a.no_extras and (a.legs == "all" or leg in a.legs.split(","))
 
 
 def barrier():
@@ -340,7 +348,7 @@ def env_count_sweep(rank, device, a, sizes=(16384, 262144, 1048576)):
 
 
 def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False, graph_update=False, bf16_update=False,
-              obs_sink=True, fused_precision="bf16"):
+              obs_sink=True, fused_precision="bf16", fused_mlp=True):
     """The reference's Perf/total_fps (24 steps x N / (collect + learn)) of rsl_rl PPO with MLP(256,256):
     config C2 at 4 096 envs fp32; at 65 536 envs also with the fused bf16 rollout inference and bf16
     rollout obs buffers (C5's training options; the update stays fp32)."""
@@ -355,6 +363,7 @@ def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False, graph_up
     cfg.algorithm.graph_update = bool(graph_update)
     cfg.algorithm.update_autocast_bf16 = bool(bf16_update)
     cfg.algorithm.obs_sink = bool(obs_sink)
+    cfg.algorithm.fused_mlp = bool(fused_mlp)
     runner = OnPolicyRunner(venv, cfg.to_dict(), log_dir=None, device=device)
     upd = runner.alg.update
     upd_s = []
@@ -378,7 +387,8 @@ def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False, graph_up
     upd_ms = float(np.median(upd_s[1:])) * 1e3
     tfs = UPDATE_FLOPS_PER_SAMPLE * samples / (upd_ms * 1e-3) / 1e12
     progress(f"train_fps n={n} fused={fused}({fused_precision}) bf16_storage={bf16_storage} graph_update={graph_update} "
-             f"obs_sink={obs_sink}: {np.median(fps):.4g} (update {upd_ms:.1f} ms, {tfs:.1f} TFLOP/s)")
+             f"obs_sink={obs_sink} fused_mlp={fused_mlp}: {np.median(fps):.4g} (update {upd_ms:.1f} ms, "
+             f"{tfs:.1f} TFLOP/s)")
     venv.close()
     return {"fps": float(np.median(fps)), "update_ms": upd_ms, "update_TFLOPs": tfs,
             "update_frac_of_fp32_mfma_peak": tfs / FP32_MFMA_PEAK_TFS if not bf16_update else None}
@@ -572,7 +582,7 @@ def main():
             "grad_allreduce_median_us": allreduce_latency_us(device),
             "note": "value = world_size x envs x steps / max over ranks of the timed region; ranks[i].env_steps_per_s "
                     "is rank i's own rate"}
-    if not a.no_extras:
+    if want(a, "policy"):
         rate_e, us_e, tfs_e = policy_in_loop_fused(env, 1024, device, precision="fp32", actor_only=True)
         extra["env_only_fp32"] = {
             "env_steps_per_s": rate_e,
@@ -610,7 +620,7 @@ def main():
                     "Gaussian sample + log prob: SURVEY §8d env-only rate at the reference's precision"}
         progress("policy_in_loop_fused_fp32")
     env.close()
-    if not a.no_extras and not a.obstacles:
+    if want(a, "obstacles") and not a.obstacles:
         # the reference task's terrain also carries walls / orbits / ground obstacles:
         # the same step over obstacle tracks (grid-listed collision, per-env cell hints)
         env_o = make_env(n, rank, device, a.gates, a.integrator, True)
@@ -636,9 +646,10 @@ def main():
             "obstacles_per_track_mean": float(env_o.obstacle_table.counts.mean())}
         progress("with_obstacles")
         env_o.close()
-    if not a.no_extras and not a.obstacles:
+    if want(a, "sweep") and not a.obstacles:
         extra["env_count_sweep"] = env_count_sweep(rank, device, a)
         progress("env_count_sweep")
+    if want(a, "c5") and not a.obstacles:
         # BASELINE config C5 on one GPU: 32-gate tracks, startup DR (plant vs controller mass, drag, thrust
         # error, rotor constants), hipGraph of [fused rollout inference + step]
         env_c5 = make_env(n, rank, device, 32, a.integrator, False, dr_rotor=1)
@@ -684,15 +695,22 @@ def main():
                                         "arithmetic"}
         env_c5.close()
         progress("c5_32_gates")
-    if not a.no_extras:
+    if want(a, "regen"):
         extra["terrain_regeneration"] = regeneration_cost(device, n)
         progress("terrain_regeneration")
+    if want(a, "train4096"):
         extra["train_total_fps_4096_envs"] = train_fps(device)
         extra["train_total_fps_4096_envs_graph_update"] = train_fps(device, graph_update=True)
         # C2 with the fp32 fused rollout inference (the reference's precision) and the graphed update
         extra["train_total_fps_4096_envs_fused_fp32_graph_update"] = train_fps(device, fused=True,
                                                                                  fused_precision="fp32",
                                                                                  graph_update=True)
+    if want(a, "mlp_ab"):  # the update's MLPs per layer (round 3: fused first layer / head around hipBLASLt)
+        extra["train_total_fps_4096_envs_fused_fp32_graph_update_per_layer_mlp"] = train_fps(
+            device, fused=True, fused_precision="fp32", graph_update=True, fused_mlp=False)
+        extra["train_total_fps_65536_envs_fused_fp32_graph_update_per_layer_mlp"] = train_fps(
+            device, n, fused=True, fused_precision="fp32", graph_update=True, fused_mlp=False)
+    if want(a, "train65536"):
         extra["train_total_fps_65536_envs"] = {
             "fp32": train_fps(device, n),
             "fp32_fused_fp32_rollout": train_fps(device, n, fused=True, fused_precision="fp32"),
@@ -705,8 +723,9 @@ def main():
                                                                 graph_update=True, bf16_update=True),
             "note": "Perf/total_fps, PPO 5 epochs x 4 mini-batches per 24-step rollout, obstacle tracks; the step "
                     "kernel writes the rollout storage rows (obs sink) unless marked no_obs_sink"}
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    if want(a, "camera"):
         # the depth camera of the vision task (separate kernel, same env shard size)
-        sys.path.insert(0, os.path.join(ROOT, "scripts"))
         import bench_camera
 
         for key, obst in (("vision_camera", False), ("vision_camera_with_obstacles", True)):
@@ -719,6 +738,7 @@ def main():
                 "frac": cam["hbm_frac_avg"],
                 "bytes_per_env_call": [cam["bytes_per_env_render"], cam["bytes_per_env_reuse"]],
                 "env_steps_per_s_step_plus_camera": cam["wall_env_steps_per_s_step_plus_camera"]}
+    if want(a, "vision"):
         # the reference's registered recipe end to end: depth camera + VisionActorCritic + PPOL2C2 (fused BN stem)
         import bench_vision
 
@@ -730,7 +750,7 @@ def main():
             "note": "Perf/total_fps of QuadcopterVisionPPORunnerCfg (VisionActorCritic 72x96 stem as patch GEMMs "
                     "with the fused HIP BatchNorm + LeakyReLU, PPOL2C2), obstacle tracks, fp32"}
     cpu = None
-    if rank == 0 and ws == 1 and not a.no_extras:
+    if rank == 0 and ws == 1 and want(a, "cpu"):
         cpu = cpu_baseline(a.cpu_seconds, obstacles=bool(a.obstacles))
         progress("cpu_baseline")
     traffic = load_traffic(n, a.gates, a.obstacles)

@@ -33,7 +33,8 @@ def build(name, patch, extra_flags=""):
     flags = ("--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt "
              "-fno-slp-vectorize " + extra_flags)
     objs = []
-    for f in ("gr_kernels.hip", "gr_camera.hip", "gr_policy.hip", "gr_policy_f32.hip", "gr_bn.hip", "gr_update.hip", "gr_rollout.hip", "gr_capi.cpp"):
+    for f in ("gr_kernels.hip", "gr_camera.hip", "gr_policy.hip", "gr_policy_f32.hip", "gr_bn.hip", "gr_update.hip",
+              "gr_mlp.hip", "gr_rollout.hip", "gr_capi.cpp"):
         o = os.path.join(tmp, f + ".o")
         extra = " -fno-honor-nans" if f == "gr_policy.hip" else ""
         lang = " -x hip" if f.endswith(".cpp") else ""
@@ -45,5 +46,17 @@ def build(name, patch, extra_flags=""):
     print(f"{out}/libgr.so")
 
 
+def load_patch(path):
+    """A patch file: a JSON list of [file, old, new] replacements, or {"replace": [...], "flags": "-D...",
+    "note": "..."} (variants/patches/*.json)."""
+    if path == "-":
+        return [], ""
+    p = json.load(open(path))
+    if isinstance(p, dict):
+        return p.get("replace", []), p.get("flags", "")
+    return p, ""
+
+
 if __name__ == "__main__":
-    build(sys.argv[1], [] if sys.argv[2] == "-" else json.load(open(sys.argv[2])), " ".join(sys.argv[3:]))
+    reps, flags = load_patch(sys.argv[2])
+    build(sys.argv[1], reps, " ".join([flags] + sys.argv[3:]))
