@@ -25,7 +25,7 @@ def _f64(net):
     # plain nn.Linear (TallLinear's tall-batch backward would take fp32 column sums)
     m = nn.Sequential(*[nn.Linear(x.in_features, x.out_features) if isinstance(x, nn.Linear) else x for x in net])
     m.load_state_dict(net.state_dict())
-    return m.double()
+    return m.double().to(DEV)
 
 
 @pytest.mark.parametrize("rows,hidden,d", [(24576 + 13, 256, 16), (4096, 128, 16), (1, 256, 16), (77, 256, 8),
