@@ -333,8 +333,8 @@ def networks_fusable(nets, xs) -> bool:
 class _FusedMLPsFn(torch.autograd.Function):
     """Up to two MLPs (the actor and the critic) on their input rows, forward and backward each as one set of
     whole-network fp32-MFMA launches for both networks (gr_mlp_forward / gr_mlp_backward, gr_mlp.hip).  Forward
-    saves h1 and z2 per network; the backward writes the hidden layer's output gradient over z2 (each tile reads its
-    z2 rows before writing them) and returns every parameter gradient from one fixed-order reduction."""
+    saves h1 and z2 per network; the backward returns every parameter gradient from one fixed-order reduction and
+    leaves the saved tensors intact (a retained graph may run it again)."""
 
     @staticmethod
     def forward(ctx, nnets, slope, *args):
@@ -388,7 +388,11 @@ class _FusedMLPsFn(torch.autograd.Function):
             s.x, s.ldx, s.d, s.k = xs[i].data_ptr(), xs[i].stride(0), d, k
             for name, t in (("w1", w1), ("b1", b1), ("w2", w2), ("b2", b2), ("w3", w3), ("b3", b3)):
                 setattr(s, name, t.data_ptr())
-            s.h1, s.z2, s.gy, s.gz2, s.grads = h1.data_ptr(), z2.data_ptr(), gy.data_ptr(), z2.data_ptr(), grads.data_ptr()
+            # (gz2 in its own buffer: a retained graph, e.g. PPO's first-mini-batch autograd.grad check, runs this
+            # backward twice over the same saved z2)
+            gz2 = torch.empty_like(z2)
+            gys_keep.append(gz2)
+            s.h1, s.z2, s.gy, s.gz2, s.grads = h1.data_ptr(), z2.data_ptr(), gy.data_ptr(), gz2.data_ptr(), grads.data_ptr()
             a.net[i] = s
             a.hidden = h
             o = 0

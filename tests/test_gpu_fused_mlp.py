@@ -86,3 +86,19 @@ def test_fused_mlp_covers_the_update_and_falls_back():
     assert not lin.networks_fusable([elu.actor, elu.critic], [xa, xc])
     wide = ActorCritic(16, 16, 8, [256, 256], [256, 256], "lrelu").to(DEV)
     assert not lin.networks_fusable([wide.actor, wide.critic], [xa, xc])
+
+
+def test_fused_mlp_backward_twice_on_a_retained_graph():
+    """PPO's first mini-batch runs autograd.grad(retain_graph=True) and then backward() on the same graph
+    (ppo.py _check_all_grads): the second backward must see the forward's saved tensors unchanged."""
+    torch.manual_seed(4)
+    pol = ActorCritic(16, 16, 4, [256, 256], [256, 256], "lrelu").to(DEV)
+    nets = [pol.actor, pol.critic]
+    _, xa, xc = _packed(3000, 16, 16, seed=5)
+    ya, yc = lin.fused_mlps(nets, [xa, xc])
+    loss = (ya ** 2).sum() + (yc ** 3).sum()
+    params = [p for n in nets for p in n.parameters()]
+    g1 = torch.autograd.grad(loss, params, retain_graph=True)
+    g2 = torch.autograd.grad(loss, params)
+    for a, b in zip(g1, g2):
+        assert torch.equal(a, b)
