@@ -203,7 +203,7 @@ def test_graphed_checkpoint_loads_into_torch_adam(tmp_path):
         assert st["step"].device.type == "cpu" and st["step"].dim() == 0 and float(st["step"]) >= 1
     pol = copy.deepcopy(alg.policy)
     adam = torch.optim.Adam(pol.parameters(), lr=1e-3)
-    adam.load_state_dict(osd)
+    adam.load_state_dict(copy.deepcopy(osd))  # (torch Adam adopts the loaded tensors and steps them in place)
     for p in pol.parameters():
         p.grad = torch.randn_like(p) * 1e-3
     adam.step()  # the first foreach step raised 'lr as a Tensor is not supported' before the fix
