@@ -121,12 +121,15 @@ class RacingEnv:
             if self._regen_steps is not None else None
         self._next_terrain = None
         self._held_terrain = None  # the previous generation's device / pinned tensors (alive until the next swap)
+        self._scratch_set = None  # the interval step's reset outputs (allocated with the output sets below)
 
         # ---- state (SoA float4 planes) and outputs ----
         n = self.num_envs
         self.state = torch.zeros(_abi.NUM_PLANES, n, 4, dtype=torch.float32, device=dev)
         self.istate = torch.zeros(n, 4, dtype=torch.int32, device=dev)
         self._sets = [self._alloc_outputs(n, dev) for _ in range(2)]
+        if self._regen_steps is not None:
+            self._scratch_set = self._alloc_outputs(n, dev)
         self._nrows = self._lib.gr_num_log_rows(ctx)
         self._log_slab = torch.zeros(LOG_RING, self._nrows, _abi.LOG_SLOTS, dtype=torch.float32, device=dev)
         self._logs: list = [None] * LOG_RING
@@ -544,8 +547,8 @@ class RacingEnv:
             # the reset's own observation (discarded by the reference: the step computes them again) goes to a scratch
             # output set, so the runner's held set is never written and nothing is saved / restored: the interval step
             # is gr_swap_terrain + gr_reset(all) + gr_observe on the stream
-            scratch = getattr(self, "_scratch_set", None)
-            if scratch is None:
+            scratch = self._scratch_set
+            if scratch is None:  # (a direct call on an env built without an interval)
                 scratch = self._scratch_set = self._alloc_outputs(self.num_envs, self.device)
             _, extras = self.regenerate_terrain(out_set=scratch)
             self._observe_after(scratch)
