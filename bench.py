@@ -394,39 +394,51 @@ def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False, graph_up
             "update_frac_of_fp32_mfma_peak": tfs / FP32_MFMA_PEAK_TFS if not bf16_update else None}
 
 
-def regeneration_cost(device, n, interval=256, plain=64):
+def regeneration_cost(device, n, interval=256, plain=64, regens=3, replays=20):
     """the interval step that regenerates the terrain (mdp/events.py:180-204) against a plain step,
-    both eager from Python with a device synchronisation after each (wall time).  The next generation is built on
-    the background thread from half-way through the interval and uploaded on a side stream; the regenerating step
-    swaps the tables on the stream (gr_swap_terrain) and resets every env.  The build's own duration (host, in the
-    background) is reported beside it."""
+    both eager from Python with a device synchronisation after each (wall time), over `regens` regenerations.  The
+    next generation is built on the background thread from half-way through the interval and staged into the
+    context's arrays on a side stream (gr_terrain_stage); the interval step commits it on the stream
+    (gr_terrain_commit) and resets every env.  The same interval step captured in a hipGraph and replayed, against
+    a captured step + full reset + observation.  The build's own duration (host, in the background) beside it."""
     cfg = RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=device), stage=1,
                        terrain=TerrainCfg(num_gates=8, obstacles=True, regen_interval_s=0.03 * interval))
     env = RacingEnv(cfg)
     env.reset()
     g = torch.Generator(device=device).manual_seed(5)
     acts = torch.randn(8, n, 4, device=device, generator=g)
-    for k in range(interval - 1 - plain):
-        env.step(acts[k % 8])
-    torch.cuda.synchronize()
-    t_build0 = time.perf_counter()
-    while env._next_terrain is not None and not env._next_terrain.done():
-        time.sleep(0.01)
-    build_wait = time.perf_counter() - t_build0
-    times = []
-    for k in range(plain):
+
+    def to_phase(ph):  # eager steps until the step counter is at phase ph of the interval
+        k = 0
+        while env.common_step_counter % env._regen_steps != ph:
+            env.step(acts[k % 8])
+            k += 1
+
+    def wait_build():
         t0 = time.perf_counter()
-        env.step(acts[k % 8])
+        if env._next_terrain is not None:
+            env._next_terrain.result()
         torch.cuda.synchronize()
-        times.append(time.perf_counter() - t0)
-    assert env.common_step_counter % env._regen_steps == env._regen_steps - 1
+        return time.perf_counter() - t0
+
+    times, t_regen, build_wait = [], [], 0.0
+    for r in range(regens):
+        to_phase(interval - 1 - (plain if r == 0 else 0))
+        build_wait += wait_build()
+        if r == 0:
+            for k in range(plain):
+                t0 = time.perf_counter()
+                env.step(acts[k % 8])
+                torch.cuda.synchronize()
+                times.append(time.perf_counter() - t0)
+        assert env.common_step_counter % env._regen_steps == env._regen_steps - 1
+        t0 = time.perf_counter()
+        _, _, _, _, extras = env.step(acts[0])
+        torch.cuda.synchronize()
+        t_regen.append(time.perf_counter() - t0)
+        assert extras.get("terrain_regenerated") and env.terrain_generation == r + 1
     t0 = time.perf_counter()
-    _, _, _, _, extras = env.step(acts[0])
-    torch.cuda.synchronize()
-    t_regen = time.perf_counter() - t0
-    assert extras.get("terrain_regenerated") and env.terrain_generation == 1
-    t0 = time.perf_counter()
-    env._build_terrain(env._terrain_seed(2))
+    env._build_terrain(env._terrain_seed(regens + 1))
     t_build = time.perf_counter() - t0
     # what the event implies besides the new tables (mdp/events.py:180-204 calls env.reset() of every env): a plain
     # step followed by a full reset and an observation pass, the same way (eager, synchronised)
@@ -438,16 +450,53 @@ def regeneration_cost(device, n, interval=256, plain=64):
         env.observe()
         torch.cuda.synchronize()
         times_sr.append(time.perf_counter() - t0)
+
+    # captured: the interval step as one graph, replayed (each replay: step, commit, reset, observe)
+    def replay_us(graph):
+        graph.replay()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(replays):
+            t0 = time.perf_counter()
+            graph.replay()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)) * 1e6
+
+    to_phase(interval - 1)
+    wait_build()
+    a_buf = acts[1].clone()
+    g_regen = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g_regen):
+        env.step(a_buf)
+    g_regen_us = replay_us(g_regen)
+    g_sr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g_sr):
+        env.step(a_buf)
+        env.reset()
+        env.observe()
+    g_sr_us = replay_us(g_sr)
+    g_plain = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g_plain):
+        env.step(a_buf)
+    g_plain_us = replay_us(g_plain)
+    del g_regen, g_sr, g_plain
     env.close()
     plain_us = float(np.median(times)) * 1e6
     sr_us = float(np.median(times_sr)) * 1e6
-    return {"plain_step_wall_us": plain_us, "regenerating_step_wall_us": t_regen * 1e6,
-            "ratio": t_regen * 1e6 / plain_us, "step_plus_full_reset_and_observe_wall_us": sr_us,
-            "ratio_to_step_plus_full_reset": t_regen * 1e6 / sr_us, "background_build_s": t_build,
-            "host_wait_for_build_s_before_timing": build_wait,
-            "note": f"{n} envs, obstacle tracks, eager env.step + synchronize per step; the build runs on a host "
-                    "thread from half-way through the interval, its upload on a side stream; the interval step swaps "
-                    "the tables on the stream and resets every env (reset + observation launches)"}
+    regen_us = float(np.median(t_regen)) * 1e6
+    return {"plain_step_wall_us": plain_us, "regenerating_step_wall_us": regen_us,
+            "regenerating_step_wall_us_each": [t * 1e6 for t in t_regen],
+            "ratio": regen_us / plain_us, "step_plus_full_reset_and_observe_wall_us": sr_us,
+            "ratio_to_step_plus_full_reset": regen_us / sr_us,
+            "graph": {"regenerating_step_us": g_regen_us, "step_plus_full_reset_and_observe_us": g_sr_us,
+                      "plain_step_us": g_plain_us, "ratio_to_step_plus_full_reset": g_regen_us / g_sr_us},
+            "background_build_s": t_build, "host_wait_for_build_s_before_timing": build_wait,
+            "note": f"{n} envs, obstacle tracks; eager: env.step + synchronize per step (median of {regens} "
+                    "regenerations); graph: the interval step captured once and replayed (synchronize per replay); "
+                    "the build runs on a host thread from half-way through the interval, its upload into the "
+                    "context's staging arrays on a side stream; the interval step commits them on the stream "
+                    "(gr_terrain_commit) and resets every env (reset + observation launches)"}
 
 
 def cpu_baseline(seconds: float, n: int = 65536, obstacles: bool = True):

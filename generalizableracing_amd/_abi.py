@@ -219,6 +219,7 @@ GR_STEP_L2, GR_STEP_LDS, GR_STEP_LDS8, GR_STEP_LDS8_LEAN, GR_STEP_OBST, GR_STEP_
 STEP_KERNEL_NAMES = ["step_kernel<false, false>", "step_kernel<true, false>", "step_kernel<true, false, 8>",
                      "step_kernel<true, false, 8, 1>", "step_kernel<false, true>", "step_kernel<false, true, 0, 1>"]
 GR_STATUS_OBST_WAIT_TIMEOUT = 1
+GR_ERR_CAPACITY = -4
 GR_FAULT_NONE, GR_FAULT_OBST_NO_SIGNAL = 0, 1
 STATUS_TEXT = {GR_STATUS_OBST_WAIT_TIMEOUT: "a physics wave gave up waiting for its obstacle mask (stale mask used)"}
 
@@ -237,7 +238,7 @@ EXPORTS = [
     "gr_ppo_loss_forward_loss", "gr_ppo_loss_backward_loss", "gr_adaptive_lr",
     "gr_bn_scratch_doubles", "gr_bn_act_forward", "gr_bn_act_backward", "gr_stem1_scratch_doubles",
     "gr_stem1_forward", "gr_stem1_backward", "gr_mlp_partials", "gr_mlp_forward", "gr_mlp_backward",
-    "gr_mlp_args_size", "gr_step_kernel_variant",
+    "gr_mlp_args_size", "gr_step_kernel_variant", "gr_terrain_reserve", "gr_terrain_stage", "gr_terrain_commit",
 ]
 
 _lib = None
@@ -259,6 +260,9 @@ def _declare(lib):
         "gr_bind_tracks": (C.c_int, [vp, vp, vp]),
         "gr_bind_obstacles": (C.c_int, [vp, C.POINTER(GrObstacles)]),
         "gr_swap_terrain": (C.c_int, [vp, vp, vp, vp, C.POINTER(GrObstacles), C.POINTER(GrObstacles), vp]),
+        "gr_terrain_reserve": (C.c_int, [vp, C.c_int32, C.c_int32, C.c_int32]),
+        "gr_terrain_stage": (C.c_int, [vp, vp, vp, C.POINTER(GrObstacles), vp]),
+        "gr_terrain_commit": (C.c_int, [vp, vp]),
         "gr_bind_buffers": (C.c_int, [vp, C.POINTER(GrBuffers)]),
         "gr_bind_obs_sink": (C.c_int, [vp, vp, vp, C.c_int]),
         "gr_init": (C.c_int, [vp, vp]),

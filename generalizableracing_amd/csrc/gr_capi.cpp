@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -42,6 +43,21 @@ struct gr_ctx {
   std::vector<hipEvent_t> ev;  // [2 * GR_TIMING_RING]
   int ev_next = 0;
   bool timing = false;
+  // resident terrain (gr_terrain_reserve / _stage / _commit): the live obstacle block the kernels read and a staging
+  // block [gates | tracks | obstacle block | header]; obstacle block (floats) = [records | counts | grid_f | grid_i |
+  // cells | items], every part 16-byte aligned
+  struct Resident {
+    bool on = false, staged = false, span_set = false;
+    int32_t cap_obst = 0, cap_cells = 0, cap_items = 0;
+    float* stage = nullptr;
+    float* live = nullptr;
+    size_t off_tracks = 0, off_obst = 0, off_hdr = 0, obst_floats = 0;
+    size_t o_cnt = 0, o_gf = 0, o_gi = 0, o_cells = 0, o_items = 0;
+    float inv_cell = 0.0f, margin = 0.0f;         // the obstacle grid's (same for every generation)
+    float staged_inv_cell = 0.0f, staged_margin = 0.0f;
+    int32_t hdr_host[4] = {0, 0, 0, 0};
+  } res;
+  std::mutex err_mu;  // gr_terrain_stage may fail on another host thread
 };
 
 #define GR_TIMING_RING 4096
@@ -49,7 +65,10 @@ struct gr_ctx {
 namespace {
 
 int fail(gr_ctx* c, int code, const std::string& msg) {
-  if (c) c->err = msg;
+  if (c) {
+    std::lock_guard<std::mutex> lk(c->err_mu);
+    c->err = msg;
+  }
   return code;
 }
 int hip_fail(gr_ctx* c, hipError_t e, const char* what) {
@@ -271,6 +290,8 @@ int gr_destroy(gr_ctx* c) {
   if (c->blk_dev) (void)hipFree(c->blk_dev);
   if (c->status_dev) (void)hipFree(c->status_dev);
   if (c->cam_dev) (void)hipFree(c->cam_dev);
+  if (c->res.stage) (void)hipFree(c->res.stage);
+  if (c->res.live) (void)hipFree(c->res.live);
   delete c;
   return GR_OK;
 }
@@ -456,6 +477,166 @@ int gr_swap_terrain(gr_ctx* c, const float* gates, const float* tracks, const fl
     return GR_OK;
   }
   return attach_obstacles(c, obst, obst_host->grid_f[2], obst_host->grid_f[3], s, "gr_swap_terrain: clear hints");
+}
+
+static size_t up4(size_t n) { return (n + 3) & ~(size_t)3; }
+
+// the resident live arrays as the kernels' terrain (reserve; again at every commit, after any gr_bind_* call)
+static void bind_resident(gr_ctx* c) {
+  gr_ctx::Resident& r = c->res;
+  c->args.table = c->table;
+  if (!r.live) {
+    unbind_obstacles(c);
+    return;
+  }
+  gr_obstacles o;
+  o.records = r.live;
+  o.counts = reinterpret_cast<const int32_t*>(r.live + r.o_cnt);
+  o.grid_f = r.live + r.o_gf;
+  o.grid_i = reinterpret_cast<const int32_t*>(r.live + r.o_gi);
+  o.cells = reinterpret_cast<const int32_t*>(r.live + r.o_cells);
+  o.items = r.live + r.o_items;
+  o.max_obstacles = r.cap_obst;
+  o.num_cells = r.cap_cells;
+  o.num_items = r.cap_items;
+  o.reserved = 0;
+  c->obst = o;
+  c->args.obst_grid_f = reinterpret_cast<const float4*>(o.grid_f);
+  c->args.obst_grid_i = reinterpret_cast<const int4*>(o.grid_i);
+  c->args.obst_cells = reinterpret_cast<const int2*>(o.cells);
+  c->args.obst_items = reinterpret_cast<const float4*>(o.items);
+}
+
+int gr_terrain_reserve(gr_ctx* c, int32_t max_obstacles, int32_t max_cells, int32_t max_items) {
+  if (!c) return GR_ERR_ARG;
+  if (max_obstacles < 0 || (max_obstacles > 0 && (max_cells <= 0 || max_items <= 0)))
+    return fail(c, GR_ERR_ARG, "gr_terrain_reserve: capacities");
+  int rc = ensure_dev(c, "gr_terrain_reserve");
+  if (rc != GR_OK) return rc;
+  const gr_config& g = c->cfg;
+  const size_t ntr = (size_t)g.num_types * g.num_levels;
+  hipError_t e = hipDeviceSynchronize();  // (a reallocation: nothing may still read the old arrays)
+  if (e != hipSuccess) return hip_fail(c, e, "gr_terrain_reserve: sync");
+  gr_ctx::Resident& r = c->res;
+  if (r.stage) (void)hipFree(r.stage);
+  if (r.live) (void)hipFree(r.live);
+  r = gr_ctx::Resident();
+  r.cap_obst = max_obstacles;
+  r.cap_cells = max_obstacles > 0 ? max_cells : 0;
+  r.cap_items = max_obstacles > 0 ? max_items : 0;
+  if (max_obstacles > 0) {
+    r.o_cnt = ntr * (size_t)max_obstacles * GR_OBST_FLOATS;
+    r.o_gf = r.o_cnt + up4(ntr);
+    r.o_gi = r.o_gf + 4 * ntr;
+    r.o_cells = r.o_gi + 4 * ntr;
+    r.o_items = r.o_cells + up4(2 * (size_t)max_cells);
+    r.obst_floats = r.o_items + (size_t)max_items * GR_OBST_FLOATS;
+  }
+  r.off_tracks = ntr * (size_t)g.max_gates * GR_GATE_FLOATS;
+  r.off_obst = r.off_tracks + ntr * GR_TRACK_FLOATS;
+  r.off_hdr = r.off_obst + r.obst_floats;
+  e = hipMalloc(&r.stage, (r.off_hdr + 4) * sizeof(float));
+  if (e == hipSuccess && r.obst_floats) e = hipMalloc(&r.live, r.obst_floats * sizeof(float));
+  if (e == hipSuccess && !c->table) e = hipMalloc(&c->table, ntr * (size_t)c->kc.track_stride * sizeof(float));
+  if (e != hipSuccess) {
+    if (r.stage) (void)hipFree(r.stage);
+    if (r.live) (void)hipFree(r.live);
+    r = gr_ctx::Resident();
+    return hip_fail(c, e, "gr_terrain_reserve: hipMalloc");
+  }
+  r.on = true;
+  bind_resident(c);  // (the contents arrive with the first commit)
+  c->have_tracks = false;  // until the first commit
+  return GR_OK;
+}
+
+int gr_terrain_stage(gr_ctx* c, const float* gates_h, const float* tracks_h, const gr_obstacles* o, void* stream) {
+  if (!c || !gates_h || !tracks_h) return fail(c, GR_ERR_ARG, "gr_terrain_stage: null pointer");
+  gr_ctx::Resident& r = c->res;
+  if (!r.on) return fail(c, GR_ERR_STATE, "gr_terrain_stage: gr_terrain_reserve first");
+  if ((o != nullptr) != (r.cap_obst > 0))
+    return fail(c, GR_ERR_ARG, "gr_terrain_stage: obstacles given iff reserved with obstacles");
+  int rc = check_track_records(c, tracks_h, "gr_terrain_stage");
+  if (rc != GR_OK) return rc;
+  const gr_config& g = c->cfg;
+  const size_t ntr = (size_t)g.num_types * g.num_levels;
+  if (o) {
+    if (!o->records || !o->counts || !o->grid_f || !o->grid_i || !o->cells || !o->items || o->max_obstacles <= 0 ||
+        o->num_cells <= 0 || o->num_items <= 0)
+      return fail(c, GR_ERR_ARG, "gr_terrain_stage: null obstacle array or empty size");
+    if (o->max_obstacles > r.cap_obst || o->num_cells > r.cap_cells || o->num_items > r.cap_items)
+      return fail(c, GR_ERR_CAPACITY, "gr_terrain_stage: the generation (" + std::to_string(o->max_obstacles) +
+                                          " obstacles per track, " + std::to_string(o->num_cells) + " cells, " +
+                                          std::to_string(o->num_items) + " items) exceeds the reservation");
+    rc = check_obstacles(c, o, o->counts, o->grid_f, o->grid_i, o->cells, "gr_terrain_stage");
+    if (rc != GR_OK) return rc;
+    if (r.span_set && (o->grid_f[2] != r.inv_cell || o->grid_f[3] != r.margin))
+      return fail(c, GR_ERR_ARG, "gr_terrain_stage: the obstacle grid's cell / margin changed between generations");
+  }
+  const hipStream_t s = (hipStream_t)stream;
+  float* st = r.stage;
+  hipError_t e = hipMemcpyAsync(st, gates_h, r.off_tracks * sizeof(float), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(st + r.off_tracks, tracks_h, ntr * GR_TRACK_FLOATS * sizeof(float), hipMemcpyHostToDevice, s);
+  if (o) {
+    float* ob = st + r.off_obst;
+    const size_t rec_b = (size_t)o->max_obstacles * GR_OBST_FLOATS * sizeof(float);
+    if (e == hipSuccess)
+      e = hipMemcpy2DAsync(ob, (size_t)r.cap_obst * GR_OBST_FLOATS * sizeof(float), o->records, rec_b, rec_b, ntr,
+                           hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(ob + r.o_cnt, o->counts, ntr * 4, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(ob + r.o_gf, o->grid_f, ntr * 16, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(ob + r.o_gi, o->grid_i, ntr * 16, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(ob + r.o_cells, o->cells, (size_t)o->num_cells * 8, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(ob + r.o_items, o->items, (size_t)o->num_items * GR_OBST_FLOATS * sizeof(float),
+                         hipMemcpyHostToDevice, s);
+    // header: float4s of the obstacle block the commit copies (through the last staged item)
+    r.hdr_host[0] = (int32_t)((r.o_items + (size_t)o->num_items * GR_OBST_FLOATS) / 4);
+    if (e == hipSuccess) e = hipMemcpyAsync(st + r.off_hdr, r.hdr_host, 16, hipMemcpyHostToDevice, s);
+    r.staged_inv_cell = o->grid_f[2];
+    r.staged_margin = o->grid_f[3];
+  }
+  if (e != hipSuccess) return hip_fail(c, e, "gr_terrain_stage: upload");
+  r.staged = true;
+  return GR_OK;
+}
+
+int gr_terrain_commit(gr_ctx* c, void* stream) {
+  if (!c) return GR_ERR_ARG;
+  gr_ctx::Resident& r = c->res;
+  if (!r.on || !r.staged) return fail(c, GR_ERR_STATE, "gr_terrain_commit: nothing staged");
+  const gr_config& g = c->cfg;
+  gr::TerrainCommitArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.s_gates = reinterpret_cast<const float4*>(r.stage);
+  a.s_tracks = reinterpret_cast<const float4*>(r.stage + r.off_tracks);
+  a.table = reinterpret_cast<float4*>(c->table);
+  a.ntr = g.num_types * g.num_levels;
+  a.g4 = g.max_gates * GR_GATE_FLOATS / 4;
+  a.stride4 = c->kc.track_stride / 4;
+  if (r.live) {
+    a.s_obst = reinterpret_cast<const float4*>(r.stage + r.off_obst);
+    a.l_obst = reinterpret_cast<float4*>(r.live);
+    a.hdr = reinterpret_cast<const int*>(r.stage + r.off_hdr);
+    a.max_obst4 = (long long)(r.obst_floats / 4);
+    if (c->have_buf) {
+      a.hints = reinterpret_cast<float4*>(c->buf.state) + (size_t)GR_P_OHINT * g.num_envs;
+      a.n_hints = g.num_envs;
+    }
+  }
+  hipError_t e = gr::launch_terrain_commit(a, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(c, e, "gr_terrain_commit");
+  if (r.live) {
+    r.inv_cell = r.staged_inv_cell;
+    r.margin = r.staged_margin;
+    r.span_set = true;
+    const float cell = 1.0f / r.inv_cell;
+    c->args.h.obst_span = cell + 2.0f * (r.margin * cell);
+  }
+  bind_resident(c);
+  c->have_tracks = true;
+  return GR_OK;
 }
 
 int gr_bind_buffers(gr_ctx* c, const gr_buffers* b) {

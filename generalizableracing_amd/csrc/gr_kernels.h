@@ -151,6 +151,20 @@ hipError_t launch_ppo_loss_backward(const gr_ppo_loss_args& a, const float* g, i
 hipError_t launch_adaptive_lr(const float* kl, float* lr, float hi, float lo, float lr_min, float lr_max,
                               hipStream_t s);
 // gr_mlp.hip: the update's whole-network MLP kernels
+// gr_terrain.hip: gr_terrain_commit (staged terrain -> live, gate table packed, obstacle hints cleared)
+struct TerrainCommitArgs {
+  const float4* s_gates;   // staged [ntr][g4]
+  const float4* s_tracks;  // staged [ntr] track records
+  float4* table;           // packed [ntr][stride4]
+  int ntr, g4, stride4;
+  const float4* s_obst;    // staged obstacle block (null: obstacle-free tracks)
+  float4* l_obst;          // live obstacle block
+  const int* hdr;          // staged header: [0] = float4s of the block to copy
+  long long max_obst4;     // float4s of the block (capacity)
+  float4* hints;           // GR_P_OHINT plane (null: buffers not bound)
+  int n_hints;
+};
+hipError_t launch_terrain_commit(const TerrainCommitArgs& a, hipStream_t s);
 hipError_t launch_mlp_forward(const gr_mlp_args& a, hipStream_t s);
 hipError_t launch_mlp_backward(const gr_mlp_args& a, hipStream_t s);
 int64_t mlp_partial_floats(long long rows, int hidden, int nets, int max_d, int max_k);

@@ -112,16 +112,19 @@ class RacingEnv:
 
         # ---- track table + obstacles (host-generated, then device-resident) ----
         self.terrain_generation = 0
-        self._load_terrain(self._terrain_seed(0))
         interval = cfg.terrain.regen_interval_s
         self._regen_steps = None if interval is None else max(1, int(round(interval / self.step_dt)))
-        # periodic regeneration: the next generation's tables are built on a background host thread from half-way
-        # through the interval, so the interval step only swaps them in (gr_swap_terrain, no host synchronisation)
+        # periodic regeneration: the context owns the terrain arrays (gr_terrain_reserve); the next generation is
+        # built on a background host thread from half-way through the interval and uploaded into the context's
+        # staging arrays on a side stream (gr_terrain_stage), so the interval step only commits it on the stream
+        # (gr_terrain_commit: fixed arguments, graph-capturable)
+        self._resident = False
         self._builder = ThreadPoolExecutor(max_workers=1, thread_name_prefix="gr-terrain") \
             if self._regen_steps is not None else None
         self._next_terrain = None
-        self._held_terrain = None  # the previous generation's device / pinned tensors (alive until the next swap)
+        self._held_terrain = None  # the live generation's pinned host arrays (resident: the last upload's source)
         self._scratch_set = None  # the interval step's reset outputs (allocated with the output sets below)
+        self._load_terrain(self._terrain_seed(0))
 
         # ---- state (SoA float4 planes) and outputs ----
         n = self.num_envs
@@ -183,39 +186,108 @@ class RacingEnv:
         return build_tracks(num_types=t.num_cols, num_levels=t.num_rows, num_gates=t.num_gates, seed=seed,
                             obstacles=t.obstacles, cell=t.obstacle_cell)
 
+    @staticmethod
+    def _pin_generation(gates, recs, obst) -> dict:
+        """Pinned host copies of a generation's arrays (the asynchronous upload's source)."""
+        pin = {"gates": torch.from_numpy(gates).pin_memory(), "records": torch.from_numpy(recs).pin_memory()}
+        if obst is not None:
+            for k in ("records", "counts", "grid_f", "grid_i", "cells", "items"):
+                pin["o_" + k] = torch.from_numpy(getattr(obst, k)).pin_memory()
+        return pin
+
+    @staticmethod
+    def _host_obstacles(pin, obst):
+        """gr_obstacles over the pinned host arrays (gr_terrain_stage)."""
+        if obst is None:
+            return None
+        o = _abi.GrObstacles()
+        for k in ("records", "counts", "grid_f", "grid_i", "cells", "items"):
+            setattr(o, k, pin["o_" + k].data_ptr())
+        o.max_obstacles = obst.max_obstacles
+        o.num_cells = int(obst.cells.shape[0])
+        o.num_items = int(obst.items.shape[0])
+        return o
+
+    def _reserve_terrain(self, obst):
+        """gr_terrain_reserve with room for generations somewhat larger than `obst` (the generator's sizes vary by
+        ~1 % between seeds; a larger one reallocates, outside any graph)."""
+        if obst is None:
+            caps = (0, 0, 0)
+        else:
+            caps = (obst.max_obstacles + max(8, obst.max_obstacles // 4), int(obst.cells.shape[0] * 1.25) + 64,
+                    int(obst.items.shape[0] * 1.25) + 256)
+        self._call("gr_terrain_reserve", *caps)
+        self._resident = True
+        self._capacity = caps
+
+    def _stage(self, pin, obst, stream) -> int:
+        """gr_terrain_stage (status returned: GR_ERR_CAPACITY is handled by the caller)."""
+        o = self._host_obstacles(pin, obst)
+        return self._lib.gr_terrain_stage(self._ctx, pin["gates"].data_ptr(), pin["records"].data_ptr(),
+                                          C.byref(o) if o is not None else None, stream)
+
+    def _stage_now(self, gates, recs, obst) -> dict:
+        """Stage a generation on the env's stream (start-up, or a regeneration the builder did not prepare); grows
+        the reservation if the generation does not fit."""
+        if not self._resident:
+            self._reserve_terrain(obst)
+        pin = self._pin_generation(gates, recs, obst)
+        rc = self._stage(pin, obst, self._stream())
+        if rc == _abi.GR_ERR_CAPACITY:
+            self._reserve_terrain(obst)
+            rc = self._stage(pin, obst, self._stream())
+        if rc != 0:
+            raise RuntimeError(f"gr_terrain_stage failed (status {rc}): {self._lib.gr_last_error(self._ctx).decode()}")
+        return pin
+
+    def _commit(self, pin, gates, recs, obst):
+        """gr_terrain_commit on the env's stream; the generation's host arrays become the env's track_gates /
+        track_records / obstacle_table."""
+        self._call("gr_terrain_commit", self._stream())
+        self._held_terrain = pin  # (alive until the next generation's upload has been ordered after this commit)
+        self.track_gates, self.track_records = pin["gates"], pin["records"]
+        self.obstacle_table = obst
+        self.obstacles = None
+
     def _start_next_terrain(self):
         """Build generation terrain_generation + 1 on the background thread (host numpy, the reference's generator
-        restated: tracks.py), pinned for an asynchronous upload."""
+        restated: tracks.py) and upload it into the context's staging arrays on a side stream, after the previous
+        commit (gr_terrain_stage)."""
         if self._builder is None:
             return
         g = self.terrain_generation + 1
-
         dev = self.device
         side = self._upload_stream = getattr(self, "_upload_stream", None) or torch.cuda.Stream(dev)
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("the terrain builder starts half-way through the interval: capture whole intervals "
+                               "outside this step, or only the interval step")
+        # the staging arrays are free once everything enqueued so far (the last commit, eager or a graph replay) ran
+        after = torch.cuda.Event()
+        after.record(torch.cuda.current_stream(dev))
 
         def work():
             gates, recs, obst = self._build_terrain(self._terrain_seed(g))
-            pin = {"gates": torch.from_numpy(gates).pin_memory(), "records": torch.from_numpy(recs).pin_memory()}
-            if obst is not None:
-                for k in ("records", "counts", "grid_f", "grid_i", "cells", "items"):
-                    pin["o_" + k] = torch.from_numpy(getattr(obst, k)).pin_memory()
-            # uploaded ahead on a side stream; the swap makes the env's stream wait for this event (no host wait)
+            pin = self._pin_generation(gates, recs, obst)
             with torch.cuda.stream(side):
-                dv = {k: v.to(dev, non_blocking=True) for k, v in pin.items()}
+                side.wait_event(after)
+                rc = self._stage(pin, obst, side.cuda_stream)
                 done = torch.cuda.Event()
                 done.record(side)
-            # the swap's arguments, built here too: the interval step only makes its launches
-            structs = self._terrain_structs(recs, obst, dv)
-            return g, gates, recs, obst, pin, dv, done, structs
+            return g, gates, recs, obst, pin, done, rc
 
         self._next_terrain = self._builder.submit(work)
 
     def _load_terrain(self, seed: int):
-        """Generate the track table (gates + obstacles) for `seed` and bind it (gr_bind_tracks,
-        gr_bind_obstacles).  The tables are copied / referenced by the context; the tensors stay
-        alive on the env."""
+        """Generate the track table (gates + obstacles) for `seed` and bind it: resident (gr_terrain_reserve / stage /
+        commit) when the env regenerates its terrain, else gr_bind_tracks + gr_bind_obstacles over env-owned device
+        tensors (track_gates / track_records / obstacles)."""
         gates, recs, obst = self._build_terrain(seed)
         dev = self.device
+        if self._regen_steps is not None:
+            pin = self._stage_now(gates, recs, obst)
+            self._commit(pin, gates, recs, obst)
+            torch.cuda.synchronize(dev)
+            return
         self.track_gates = torch.from_numpy(gates).to(dev).contiguous()
         self.track_records = torch.from_numpy(recs).to(dev).contiguous()
         self._call("gr_bind_tracks", self.track_gates.data_ptr(), self.track_records.data_ptr())
@@ -236,63 +308,39 @@ class RacingEnv:
         self._obst_struct = o
         self._call("gr_bind_obstacles", C.byref(o))
 
-    @staticmethod
-    def _terrain_structs(recs, obst, dv):
-        """gr_swap_terrain's arguments for a built generation: the host track records, and the device / host
-        gr_obstacles (None without obstacles)."""
-        recs_h = C.c_void_p(recs.ctypes.data)
-        if obst is None:
-            return recs_h, None, None
-        o, oh = _abi.GrObstacles(), _abi.GrObstacles()
-        for k in ("records", "counts", "grid_f", "grid_i", "cells", "items"):
-            setattr(o, k, dv["o_" + k].data_ptr())
-        for k in ("counts", "grid_f", "grid_i", "cells"):
-            setattr(oh, k, getattr(obst, k).ctypes.data)
-        for x in (o, oh):
-            x.max_obstacles = obst.max_obstacles
-            x.num_cells = int(obst.cells.shape[0])
-            x.num_items = int(obst.items.shape[0])
-        return recs_h, o, oh
-
     def regenerate_terrain(self, out_set: dict | None = None):
         """EventCfg.reset_terrain -> reset_terrain_period (mdp/events.py:180-204): a new terrain
         (next seed of this shard's stream), then env.reset() of every env.
 
-        The tables come from the background builder (started when the previous generation bound); the swap is
-        ordered on the stream (gr_swap_terrain: asynchronous uploads from pinned memory, tables packed and hints
-        cleared on the device), so the host does not wait for the GPU and only waits for the builder if the
-        interval was shorter than a build."""
+        The builder staged the generation ahead (validated on the host, uploaded on the side stream); here the
+        env's stream waits for that upload and commits it (gr_terrain_commit: one kernel with fixed arguments), so
+        the interval step is gr_terrain_commit + gr_reset + gr_observe, graph-capturable.  The host only waits for
+        the builder if the interval was shorter than a build.  Under a graph capture the staged generation must
+        be complete already (a replay commits whatever was staged last)."""
         g = self.terrain_generation + 1
-        dev = self.device
-        if self._next_terrain is not None:
-            g_built, gates, recs, obst, pin, dv, done, structs = self._next_terrain.result()
+        staged = None
+        if self._next_terrain is not None and self._resident:
+            g_built, gates, recs, obst, pin, done, rc = self._next_terrain.result()
             assert g_built == g
-            cur = torch.cuda.current_stream(dev)
-            cur.wait_event(done)
-            for v in dv.values():  # (allocated on the side stream, used on this one from now on)
-                v.record_stream(cur)
-        else:  # (not started: an interval of one step, or a direct call) built here
-            gates, recs, obst = self._build_terrain(self._terrain_seed(g))
-            pin = {"gates": torch.from_numpy(gates), "records": torch.from_numpy(recs)}
-            if obst is not None:
-                for k in ("records", "counts", "grid_f", "grid_i", "cells", "items"):
-                    pin["o_" + k] = torch.from_numpy(getattr(obst, k))
-            dv = {k: v.to(dev) for k, v in pin.items()}
-            structs = self._terrain_structs(recs, obst, dv)
+            if rc == 0:
+                if torch.cuda.is_current_stream_capturing():
+                    done.synchronize()
+                else:
+                    torch.cuda.current_stream(self.device).wait_event(done)
+                staged = (gates, recs, obst, pin)
+            elif rc != _abi.GR_ERR_CAPACITY:
+                raise RuntimeError(f"gr_terrain_stage failed (status {rc}): "
+                                   f"{self._lib.gr_last_error(self._ctx).decode()}")
         self._next_terrain = None
-        self._held_terrain = (self.track_gates, self.track_records, self.obstacles, pin)
-        self.track_gates, self.track_records = dv["gates"], dv["records"]
-        recs_h, o, oh = structs
-        if obst is None:
-            self.obstacles = None
-            self._call("gr_swap_terrain", self.track_gates.data_ptr(), self.track_records.data_ptr(), recs_h, None, None,
-                       self._stream())
-        else:
-            self.obstacles = {k: dv["o_" + k] for k in ("records", "counts", "grid_f", "grid_i", "cells", "items")}
-            self._obst_struct = o
-            self._call("gr_swap_terrain", self.track_gates.data_ptr(), self.track_records.data_ptr(), recs_h,
-                       C.byref(o), C.byref(oh), self._stream())
-        self.obstacle_table = obst
+        if staged is None:  # (not started, an interval of one step, a direct call, or a larger generation) here
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("regenerate_terrain under a graph capture needs the next generation staged "
+                                   "(the builder's upload complete)")
+            gates, recs, obst = self._build_terrain(self._terrain_seed(g))
+            pin = self._stage_now(gates, recs, obst)
+            staged = (gates, recs, obst, pin)
+        gates, recs, obst, pin = staged
+        self._commit(pin, gates, recs, obst)
         self.terrain_generation = g
         return self.reset(out_set=out_set)
 
@@ -647,7 +695,8 @@ class RacingEnv:
 
     def close(self):
         if getattr(self, "_builder", None) is not None:
-            self._builder.shutdown(wait=False, cancel_futures=True)
+            # (a running build stages into the context's arrays: wait for it before the context goes)
+            self._builder.shutdown(wait=True, cancel_futures=True)
             self._builder = None
         if getattr(self, "_ctx", None):
             self._lib.gr_destroy(self._ctx)

@@ -303,6 +303,28 @@ int gr_bind_obstacles(gr_ctx* ctx, const gr_obstacles* obst);
  * `stream` run on the previous tables.  Same tables -> same steps as gr_bind_tracks + gr_bind_obstacles. */
 int gr_swap_terrain(gr_ctx* ctx, const float* gates, const float* tracks, const float* tracks_host,
                     const gr_obstacles* obst, const gr_obstacles* obst_host, void* stream);
+
+/* Resident terrain: the periodic regeneration (EventCfg.reset_terrain -> reset_terrain_period, .../quadcopter_diff/
+ * mdp/events.py:180-204) as a swap with fixed device addresses, so the interval step can be captured in a hipGraph.
+ *   gr_terrain_reserve: the context allocates, once, the arrays the kernels read the terrain from (the packed gate
+ *     table; for obstacle tracks records [T*L][max_obstacles][GR_OBST_FLOATS], counts, grids, cells [max_cells][2],
+ *     items [max_items][GR_OBST_FLOATS]) and a staging copy of them, and binds the live ones (max_obstacles == 0:
+ *     obstacle-free tracks).  Synchronises the device.  Called again it reallocates (the kernel arguments change:
+ *     graphs captured before must be captured again).
+ *   gr_terrain_stage: validates a generation from HOST arrays (gates / tracks as gr_bind_tracks; obst_host: every
+ *     array a host pointer, max_obstacles / num_cells / num_items its sizes; NULL iff reserved obstacle-free) and
+ *     uploads it into the staging arrays on `stream` (asynchronous from pinned memory).  Touches only the staging
+ *     set: it may run on another host thread and stream while the env's calls run; the caller orders it after the
+ *     previous gr_terrain_commit (a stream wait).  GR_ERR_CAPACITY: the generation exceeds the reservation.
+ *   gr_terrain_commit: makes the last staged generation live, ordered on `stream`: one kernel copies the staged
+ *     arrays over the live ones (extents from the staged header, on the device), packs the gate table and clears
+ *     the per-env obstacle hints.  No host argument, check or synchronisation: capturable, and a graph replay
+ *     commits whatever was staged last.  Same tables -> same steps as gr_bind_tracks + gr_bind_obstacles. */
+#define GR_ERR_CAPACITY -4
+int gr_terrain_reserve(gr_ctx* ctx, int32_t max_obstacles, int32_t max_cells, int32_t max_items);
+int gr_terrain_stage(gr_ctx* ctx, const float* gates_host, const float* tracks_host, const gr_obstacles* obst_host,
+                     void* stream);
+int gr_terrain_commit(gr_ctx* ctx, void* stream);
 int gr_bind_buffers(gr_ctx* ctx, const gr_buffers* bufs);
 
 /* Observation sink (config C5's bf16 rollout buffers): every following gr_step / gr_reset / gr_observe also

@@ -34,7 +34,7 @@ def build(name, patch, extra_flags=""):
              "-fno-slp-vectorize " + extra_flags)
     objs = []
     for f in ("gr_kernels.hip", "gr_camera.hip", "gr_policy.hip", "gr_policy_f32.hip", "gr_bn.hip", "gr_update.hip",
-              "gr_mlp.hip", "gr_rollout.hip", "gr_capi.cpp"):
+              "gr_mlp.hip", "gr_rollout.hip", "gr_terrain.hip", "gr_capi.cpp"):
         o = os.path.join(tmp, f + ".o")
         extra = " -fno-honor-nans" if f == "gr_policy.hip" else ""
         lang = " -x hip" if f.endswith(".cpp") else ""

@@ -366,6 +366,67 @@ def test_wrapper_across_terrain_regeneration():
     venv.close()
 
 
+def test_terrain_regeneration_step_graph_captured():
+    """The interval step (gr_step + gr_terrain_commit + gr_reset + gr_observe, mdp/events.py:180-204) captured in a
+    hipGraph: one replay commits the generation the builder staged and equals the same step run eagerly on a twin
+    env bit for bit (state, observations, reward, terminated, dones); both then step on identically on the new
+    tracks, which the oracle confirms."""
+    n = 4096
+
+    def mk():
+        cfg = RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV), stage=1,
+                           terrain=TerrainCfg(regen_interval_s=0.03 * 8))
+        env = RacingEnv(cfg)
+        env.reset()
+        return env
+
+    ea, eb = mk(), mk()
+    g = torch.Generator().manual_seed(3)
+    acts = [torch.randn(n, 4, generator=g).to(DEV) for _ in range(12)]
+    for k in range(7):
+        ea.step(acts[k])
+        eb.step(acts[k])
+    for e in (ea, eb):
+        assert e._next_terrain.result()[-1] == 0  # generation 1 staged by the builder
+    torch.cuda.synchronize()
+    obs_a, rew_a, term_a, _, ex_a = ea.step(acts[7])
+    a_buf = acts[7].clone()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        obs_b, rew_b, term_b, _, ex_b = eb.step(a_buf)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert ex_a.get("terrain_regenerated") and ex_b.get("terrain_regenerated")
+    assert ea.terrain_generation == eb.terrain_generation == 1
+    assert torch.equal(ea.track_gates, eb.track_gates)
+
+    def same(where):
+        assert torch.equal(ea.state.view(torch.int32), eb.state.view(torch.int32)), where
+        assert torch.equal(ea.istate, eb.istate), where
+
+    same("interval step")
+    for k in ("policy", "critic"):
+        assert torch.equal(obs_a[k].view(torch.int32), obs_b[k].view(torch.int32)), k
+    assert torch.equal(rew_a.view(torch.int32), rew_b.view(torch.int32))
+    assert torch.equal(term_a, term_b)
+    assert torch.equal(ea._sets[ea._cur]["dones"], eb._sets[eb._cur]["dones"])
+    assert bool((eb.episode_length_buf == 0).all())
+    del graph
+    orc = oracle.from_env(eb)  # the new generation's tables (host copies of what was committed)
+    orc.envs[:] = kernel_envs(eb)
+    orc.obs_critic[:] = eb.obs_buf["critic"].cpu().numpy()
+    orc.counter[0] = int(eb._counters[eb._calls % 2].item())
+    for k in range(8, 11):
+        ea.step(acts[k])
+        eb.step(acts[k])
+        orc.step(acts[k].cpu().numpy())
+        torch.cuda.synchronize()
+        same(f"step {k}")
+        assert_envs_equal(kernel_envs(eb), orc.envs, f"after the captured regeneration, step {k}")
+    ea.close()
+    eb.close()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_obs_sink_rows(dtype):
