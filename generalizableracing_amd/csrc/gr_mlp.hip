@@ -420,6 +420,274 @@ __global__ __launch_bounds__(MW * 64) void mlp_bwd(gr_mlp_args a, int rows_per_n
   }
 }
 
+// ------------------------------------------------------------------------------------------------ backward, H = 256
+// mlp_bwd's arithmetic with the tile's inputs (z2, h1, x, gy rows) staged into LDS by LDS-DMA (global_load_lds) one
+// tile ahead.  At one workgroup per CU (the W2 columns hold 128 registers of each lane) the barriers keep the SIMD's
+// two waves in step, so mlp_bwd's global loads after its barriers stalled both: here they are issued while the
+// previous tile computes and waited for with counted vmcnt, behind raw barriers that do not drain them.
+//   per tile i, per wave, in issue order:  P_a (after barrier 2): z2 rows of tile i+1 (4 x 1 KB), gy of tile i+1
+//   (waves 6, 7: 1 each);  P_b (after barrier 3): gz2 row stores (4), h1 rows of tile i+1 (4), x of tile i+1
+//   (waves 0 .. 2 DT - 1: 1 each).  Loads, stores and LDS-DMA retire in issue order on vmcnt, so
+//   - end of tile i, before barrier 1 of i+1: vmcnt(8) leaves only P_b's 8-9 youngest -> z2 / gy of i+1 are in LDS;
+//   - tile i+1 before its gz1: vmcnt(4) leaves only what follows h1 (x, then P_a of i+1 with its 4 z2 rows) -> h1
+//     and x of i+1 are in; vmcnt(0) when there is no tile i+2 (no P_a).
+// Every DMA is issued for every row (past the end: row n - 1, finite data that the tail's zero gy cancels), so the
+// counts hold; the tail rows' gy is masked where it is read.
+constexpr int HB = 256, HBP = HB + 4;
+__host__ __device__ constexpr size_t mlp_bwd256_lds_bytes(int dt) {
+  return 4 * ((size_t)4 * BE * HBP + 2 * BE * 16 * dt + 2 * BE * 4);
+}
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glob_void_t;
+// LDS-DMA, one wave instruction: lane l's `size` bytes from g (per lane) to LDS at l_base (wave-uniform) + l * size
+__device__ __forceinline__ void glds16(const float* g, float* l_base) {
+  __builtin_amdgcn_global_load_lds((glob_void_t*)g, (lds_void_t*)l_base, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const float* g, float* l_base) {
+  __builtin_amdgcn_global_load_lds((glob_void_t*)g, (lds_void_t*)l_base, 4, 0, 0);
+}
+// workgroup barrier that leaves vector-memory operations in flight (__syncthreads() would wait for vmcnt(0))
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int DT>
+__global__ __launch_bounds__(MW * 64) void mlp_bwd256(gr_mlp_args a, int rows_per_net_part) {
+  constexpr int H = HB, HP = HBP, TW = H / (16 * MW), Q = H / 16;
+  constexpr int XW = 16 * DT;  // x row in LDS (floats)
+  const gr_mlp_net& net = a.net[blockIdx.y];
+  // (the wave index as a scalar: the DMA rows and LDS bases are wave-uniform, so they stay in SGPRs)
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4,
+            j = lane & 15;
+  const int n = (int)a.rows;  // (gr_mlp_* check rows * max(H, ldx) < 2^31: 32-bit offsets)
+  const int D = net.d, K = net.k;
+  const int ldx = (int)net.ldx;
+  const float slope = a.slope;
+  extern __shared__ float lds[];
+  float* gz2s = lds;             // [BE][HP]
+  float* bufb = gz2s + BE * HP;  // [BE][HP]: h2, then gz1
+  float* z2s = bufb + BE * HP;   // [BE][HP]: z2 rows of the tile (LDS-DMA)
+  float* h1s = z2s + BE * HP;    // [BE][HP]: h1 rows of the tile (LDS-DMA)
+  float* xs = h1s + BE * HP;     // [2][BE][XW]: x rows (LDS-DMA, by tile parity)
+  float* gys = xs + 2 * BE * XW; // [2][BE][4]: gy rows (LDS-DMA, by tile parity; outputs >= k stay 0)
+  const float* __restrict__ W2 = net.w2;
+  const float* __restrict__ W3 = net.w3;
+
+  float w2c[TW][4 * Q], w3a[TW];
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const int i = 16 * (wave * TW + t) + j;
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w2c[t][4 * q + r] = W2[(size_t)(16 * q + 4 * g + r) * H + i];
+    w3a[t] = g < K ? W3[(size_t)g * H + i] : 0.0f;
+  }
+  // the weights are consumed here, before any DMA: hipcc otherwise waits vmcnt(0) at their first use in the loop
+  // (a use of an ordinary load's result while an LDS-DMA is in flight), draining the next tile's DMA every tile
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+#pragma unroll
+    for (int k = 0; k < 4 * Q; ++k) asm volatile("" : "+v"(w2c[t][k]));
+    asm volatile("" : "+v"(w3a[t]));
+  }
+  m4 gw1[TW][DT], gw3[TW];
+  float gb1[TW][4], gb2[TW][4], gb3 = 0.0f;
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    gw3[t] = zero4();
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) gw1[t][dt] = zero4();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) gb1[t][r] = gb2[t][r] = 0.0f;
+  }
+  // the DMA targets start at 0: lanes it never writes (x columns >= d, gy outputs >= k) must read 0, and
+  // never-written LDS may hold NaN patterns
+  for (int i = threadIdx.x; i < 2 * BE * HP + 2 * BE * XW + 2 * BE * 4; i += MW * 64) z2s[i] = 0.0f;
+  __syncthreads();  // (no DMA in flight yet; also waits for the weight loads)
+
+  auto clamp_row = [&](int r) { return r < n ? r : n - 1; };
+  // P_a: z2 rows (wave w: rows w, w + 8, w + 16, w + 24) and gy (waves 6, 7: 16 rows x 4 outputs each)
+  auto issue_a = [&](int tb, int par) {
+#pragma unroll
+    for (int rr = 0; rr < BE / MW; ++rr) {
+      const int row = wave + MW * rr;
+      glds16(net.z2 + clamp_row(tb + row) * H + 4 * lane, z2s + row * HP);
+    }
+    if (wave >= MW - 2) {
+      const int row = 16 * (wave - (MW - 2)) + (lane >> 2), kk = lane & 3;
+      if (kk < K) glds4(net.gy + clamp_row(tb + row) * K + kk, gys + par * BE * 4 + 16 * (wave - (MW - 2)) * 4);
+    }
+  };
+  // P_b: h1 rows, x (waves 0 .. 2 DT - 1: 16 / DT rows x XW floats each)
+  auto issue_b = [&](int tb, int par) {
+#pragma unroll
+    for (int rr = 0; rr < BE / MW; ++rr) {
+      const int row = wave + MW * rr;
+      glds16(net.h1 + clamp_row(tb + row) * H + 4 * lane, h1s + row * HP);
+    }
+    if (wave < 2 * DT) {
+      constexpr int RPI = 16 / DT;  // rows per instruction
+      const int row = RPI * wave + lane / (4 * DT), c4 = 4 * (lane % (4 * DT));
+      if (c4 < D) glds16(net.x + clamp_row(tb + row) * ldx + c4, xs + par * BE * XW + RPI * wave * XW);
+    }
+  };
+
+  const int stride = gridDim.x * BE;
+  int base = blockIdx.x * BE;
+  if (base < n) {
+    issue_a(base, 0);
+    issue_b(base, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  raw_barrier();
+  for (int kt = 0; base < n; base += stride, ++kt) {
+    const bool has_next = base + stride < n;
+    const float* gyt = gys + (kt & 1) * BE * 4;
+    const float* xt = xs + (kt & 1) * BE * XW;
+    // ---- gh2 = gy W3, gz2 = gh2 lrelu'(z2), h2 = lrelu(z2)
+#pragma unroll
+    for (int c = 0; c < BC; ++c) {
+      const int row = 16 * c + j;
+      const float gyv = base + row < n ? gyt[row * 4 + g] : 0.0f;  // B[k = g][row j]
+      if (wave == 0) gb3 += gyv;
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        const int u = 16 * (wave * TW + t) + 4 * g;
+        const m4 gh = mf(w3a[t], gyv, zero4());
+        const m4 z = ld4(z2s + row * HP + u);
+        m4 gz, h2;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          gz[q] = gh[q] * lrelu_d(z[q], slope);
+          h2[q] = lrelu(z[q], slope);
+          gb2[t][q] += gz[q];
+        }
+        st4(gz2s + row * HP + u, gz);
+        st4(bufb + row * HP + u, h2);
+      }
+    }
+    raw_barrier();  // (2) gz2 and h2 of the tile in LDS; every wave is done with z2s
+    if (has_next) issue_a(base + stride, (kt + 1) & 1);
+    // ---- gW3 += gy^T h2 (k step = rows 4 s + g)
+#pragma unroll 4
+    for (int s = 0; s < BE / 4; ++s) {
+      const int row = 4 * s + g;
+      const float av = (j < 4 && base + row < n) ? gyt[row * 4 + j] : 0.0f;
+#pragma unroll
+      for (int t = 0; t < TW; ++t) gw3[t] = mf(av, bufb[row * HP + 16 * (wave * TW + t) + j], gw3[t]);
+    }
+    // ---- gh1 = gz2 W2 for the wave's h1 units
+    m4 acc[TW][BC];
+#pragma unroll
+    for (int t = 0; t < TW; ++t)
+#pragma unroll
+      for (int c = 0; c < BC; ++c) acc[t][c] = zero4();
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      m4 gb[BC];
+#pragma unroll
+      for (int c = 0; c < BC; ++c) gb[c] = ld4(gz2s + (16 * c + j) * HP + 16 * q + 4 * g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int t = 0; t < TW; ++t)
+#pragma unroll
+          for (int c = 0; c < BC; ++c) acc[t][c] = mf(w2c[t][4 * q + r], gb[c][r], acc[t][c]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // h1 (and x) of this tile: this wave's DMA retired, then every wave's (barrier)
+    if (has_next) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();  // (2b)
+#pragma unroll
+    for (int c = 0; c < BC; ++c) {
+      const int row = 16 * c + j;
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        const m4 hv = ld4(h1s + row * HP + 16 * (wave * TW + t) + 4 * g);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc[t][c][q] *= lrelu_d(hv[q], slope);
+          gb1[t][q] += acc[t][c][q];
+        }
+      }
+    }
+    raw_barrier();  // (3) every wave is done with h2 (bufb), gz2s and h1s
+#pragma unroll
+    for (int t = 0; t < TW; ++t)
+#pragma unroll
+      for (int c = 0; c < BC; ++c) st4(bufb + (16 * c + j) * HP + 16 * (wave * TW + t) + 4 * g, acc[t][c]);
+#pragma unroll
+    for (int rr = 0; rr < BE / MW; ++rr) {
+      const int row = wave + MW * rr;
+      if (base + row < n) st4(net.gz2 + (base + row) * H + 4 * lane, ld4(gz2s + row * HP + 4 * lane));
+    }
+    if (has_next) issue_b(base + stride, (kt + 1) & 1);
+    raw_barrier();  // (4) gz1 in LDS
+    // ---- gW1 += gz1^T x (k step = rows 4 s + g)
+#pragma unroll 4
+    for (int s = 0; s < BE / 4; ++s) {
+      const int row = 4 * s + g;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int dcol = 16 * dt + j;
+        const float xv = dcol < D ? xt[row * XW + dcol] : 0.0f;
+#pragma unroll
+        for (int t = 0; t < TW; ++t) gw1[t][dt] = mf(bufb[row * HP + 16 * (wave * TW + t) + j], xv, gw1[t][dt]);
+      }
+    }
+    if (has_next) {
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // z2 / gy of the next tile
+      raw_barrier();  // (1) of the next tile: its z2 / gy in LDS; the readers of bufb (gz1) and xt are done
+    }
+  }
+  // ---- the workgroup's partial row (as mlp_bwd)
+  float* pr = a.partial + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (size_t)rows_per_net_part;
+#pragma unroll
+  for (int t = 0; t < TW; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v1 = gb1[t][q], v2 = gb2[t][q];
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) {
+        v1 += __shfl_xor(v1, off);
+        v2 += __shfl_xor(v2, off);
+      }
+      gb1[t][q] = v1;
+      gb2[t][q] = v2;
+    }
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const int u0 = 16 * (wave * TW + t);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (16 * dt + j < D) pr[(size_t)(u0 + 4 * g + q) * D + 16 * dt + j] = gw1[t][dt][q];
+    if (j == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        pr[H * D + u0 + 4 * g + q] = gb1[t][q];
+        pr[H * D + H + u0 + 4 * g + q] = gb2[t][q];
+      }
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (q < K) pr[H * D + 2 * H + q * H + u0 + j] = gw3[t][q];
+    }
+  }
+  if (wave == 0) {
+    float v = gb3;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) v += __shfl_xor(v, off);
+    if (j == 0 && g < K) pr[H * D + 2 * H + K * H + g] = v;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ gW2
 // gW2 [H][H] = gz2^T h1 per network: a workgroup takes a 128 x 128 output block (rows u of gW2 = gz2 columns,
 // cols i = h1 columns) over a chunk of the mini-batch rows; 8 waves as 2 (u) x 4 (i) of 64 x 32 (4 x 2 tiles).
@@ -452,30 +720,47 @@ __global__ __launch_bounds__(MW * 64) void mlp_wgrad(gr_mlp_args a, int splits, 
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t][0] = acc[t][1] = zero4();
   // staging: 32 rows x 32 float4 per matrix = 16 units of 8 rows x 8 float4 (one wave instruction: 8 rows x 128
-  // contiguous bytes; the transposed LDS writes of its 64 lanes then hit 32 distinct banks), 2 units per wave
-  auto stage = [&](float* dst, long long r0) {
+  // contiguous bytes; the transposed LDS writes of its 64 lanes then hit 32 distinct banks), 2 units per wave.
+  // Split in two: the loads into registers are issued before the current stage's MFMAs, the transposed LDS writes
+  // after them (so the loads' latency is covered by the MFMAs instead of stalling both waves of the SIMD)
+  m4 sv[2][2];
+  auto stage_load = [&](long long r0) {
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
       const float* src = m == 0 ? net.gz2 : net.h1;
       const int col0 = m == 0 ? bu : bi;
-      float* d = dst + m * WG_BLK * WG_RP;
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         const int unit = wave + MW * p;  // 0..15
         const int row = 8 * (unit & 3) + (lane & 7), c4 = 4 * (8 * (unit >> 2) + (lane >> 3));
         const long long r = r0 + row;
-        const m4 v = r < r_end ? ld4(src + r * H + col0 + c4) : zero4();
+        sv[m][p] = r < r_end ? ld4(src + r * H + col0 + c4) : zero4();
+      }
+    }
+  };
+  auto stage_write = [&](float* dst) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) d[(c4 + e) * WG_RP + row] = v[e];
+    for (int m = 0; m < 2; ++m) {
+      float* d = dst + m * WG_BLK * WG_RP;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int unit = wave + MW * p;
+        const int row = 8 * (unit & 3) + (lane & 7), c4 = 4 * (8 * (unit >> 2) + (lane >> 3));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) d[(c4 + e) * WG_RP + row] = sv[m][p][e];
       }
     }
   };
   int buf = 0;
-  if (r_begin < r_end) stage(lds, r_begin);
+  if (r_begin < r_end) {
+    stage_load(r_begin);
+    stage_write(lds);
+  }
   for (long long r0 = r_begin; r0 < r_end; r0 += WG_R) {
     __syncthreads();  // stage `buf` complete; the other buffer's readers are done
     float* cur = lds + buf * 2 * WG_BLK * WG_RP;
-    if (r0 + WG_R < r_end) stage(lds + (buf ^ 1) * 2 * WG_BLK * WG_RP, r0 + WG_R);
+    const bool more = r0 + WG_R < r_end;
+    if (more) stage_load(r0 + WG_R);
     const float* A = cur;                    // gz2 block, [u][row]
     const float* B = cur + WG_BLK * WG_RP;   // h1 block, [i][row]
 #pragma unroll
@@ -492,6 +777,7 @@ __global__ __launch_bounds__(MW * 64) void mlp_wgrad(gr_mlp_args a, int splits, 
 #pragma unroll
           for (int u = 0; u < 2; ++u) acc[t][u] = mf(af[t][r], bf[u][r], acc[t][u]);
     }
+    if (more) stage_write(lds + (buf ^ 1) * 2 * WG_BLK * WG_RP);
     buf ^= 1;
   }
   // partial block -> part[net][split][H][H]
@@ -626,6 +912,19 @@ static hipError_t launch_bwd_t(const gr_mlp_args& a, int row, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int DT>
+static hipError_t launch_bwd256_t(const gr_mlp_args& a, int row, hipStream_t s) {
+  static bool attr = false;
+  const size_t lds = mlp_bwd256_lds_bytes(DT);
+  if (!attr) {
+    const hipError_t e = set_lds(&mlp_bwd256<DT>, lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((mlp_bwd256<DT>), dim3(mlp_grid_x(a.rows, a.nets, BE), a.nets), dim3(MW * 64), lds, s, a, row);
+  return hipGetLastError();
+}
+
 template <int H>
 static hipError_t launch_wgrad_t(const gr_mlp_args& a, int splits, long long rps, float* wpart, hipStream_t s) {
   static bool attr = false;
@@ -649,7 +948,7 @@ hipError_t launch_mlp_backward(const gr_mlp_args& a, hipStream_t s) {
   const int row = mlp_bwd_row(a.hidden, d, k);
   const int bwd_blocks = mlp_grid_x(a.rows, a.nets, BE);
   hipError_t e;
-  if (a.hidden == 256) e = d <= 16 ? launch_bwd_t<256, 1>(a, row, s) : launch_bwd_t<256, 2>(a, row, s);
+  if (a.hidden == 256) e = d <= 16 ? launch_bwd256_t<1>(a, row, s) : launch_bwd256_t<2>(a, row, s);
   else e = d <= 16 ? launch_bwd_t<128, 1>(a, row, s) : launch_bwd_t<128, 2>(a, row, s);
   if (e != hipSuccess) return e;
   const int splits = mlp_splits(a.rows, a.hidden, a.nets);

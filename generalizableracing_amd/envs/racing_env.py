@@ -244,7 +244,9 @@ class RacingEnv:
         """gr_terrain_commit on the env's stream; the generation's host arrays become the env's track_gates /
         track_records / obstacle_table."""
         self._call("gr_terrain_commit", self._stream())
-        self._held_terrain = pin  # (alive until the next generation's upload has been ordered after this commit)
+        # (alive until two commits later: the upload from it is long done, and no pinned block is released in
+        # the capture of an interval step)
+        self._held_prev, self._held_terrain = self._held_terrain, pin
         self.track_gates, self.track_records = pin["gates"], pin["records"]
         self.obstacle_table = obst
         self.obstacles = None
@@ -323,9 +325,8 @@ class RacingEnv:
             g_built, gates, recs, obst, pin, done, rc = self._next_terrain.result()
             assert g_built == g
             if rc == 0:
-                if torch.cuda.is_current_stream_capturing():
-                    done.synchronize()
-                else:
+                # (under a graph capture no event may be touched: the caller has synchronised the upload)
+                if not torch.cuda.is_current_stream_capturing():
                     torch.cuda.current_stream(self.device).wait_event(done)
                 staged = (gates, recs, obst, pin)
             elif rc != _abi.GR_ERR_CAPACITY:
