@@ -394,7 +394,7 @@ def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False, graph_up
             "update_frac_of_fp32_mfma_peak": tfs / FP32_MFMA_PEAK_TFS if not bf16_update else None}
 
 
-def regeneration_cost(device, n, interval=256, plain=64, regens=3, replays=20):
+def regeneration_cost(device, n, interval=256, plain=32, regens=5, replays=20):
     """the interval step that regenerates the terrain (mdp/events.py:180-204) against a plain step,
     both eager from Python with a device synchronisation after each (wall time), over `regens` regenerations.  The
     next generation is built on the background thread from half-way through the interval and staged into the
@@ -423,14 +423,15 @@ def regeneration_cost(device, n, interval=256, plain=64, regens=3, replays=20):
 
     times, t_regen, build_wait = [], [], 0.0
     for r in range(regens):
-        to_phase(interval - 1 - (plain if r == 0 else 0))
+        # plain steps between the wait for the build and the interval step (timed): the GPU idled while the host
+        # waited, and its first launches after an idle second run at lowered clocks
+        to_phase(interval - 1 - plain)
         build_wait += wait_build()
-        if r == 0:
-            for k in range(plain):
-                t0 = time.perf_counter()
-                env.step(acts[k % 8])
-                torch.cuda.synchronize()
-                times.append(time.perf_counter() - t0)
+        for k in range(plain):
+            t0 = time.perf_counter()
+            env.step(acts[k % 8])
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
         assert env.common_step_counter % env._regen_steps == env._regen_steps - 1
         t0 = time.perf_counter()
         _, _, _, _, extras = env.step(acts[0])
@@ -463,8 +464,10 @@ def regeneration_cost(device, n, interval=256, plain=64, regens=3, replays=20):
             ts.append(time.perf_counter() - t0)
         return float(np.median(ts)) * 1e6
 
-    to_phase(interval - 1)
+    to_phase(interval - 1 - plain)
     wait_build()
+    for k in range(plain):
+        env.step(acts[k % 8])
     a_buf = acts[1].clone()
     g_regen = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g_regen):

@@ -68,34 +68,6 @@ __global__ __launch_bounds__(MW * 64) void mlp_fwd(gr_mlp_args a) {
   const float* __restrict__ W2 = net.w2;
   const float* __restrict__ W3 = net.w3;
 
-  float w1r[TW][Q1][4], w2r[TW][4 * Q], w3r[TW][4];
-#pragma unroll
-  for (int t = 0; t < TW; ++t) {
-    const int row = 16 * (wave * TW + t) + j;
-#pragma unroll
-    for (int q = 0; q < Q1; ++q) {
-      const int k = 16 * q + 4 * g;
-      const m4 v = k < D ? ld4(W1 + (size_t)row * D + k) : zero4();
-#pragma unroll
-      for (int r = 0; r < 4; ++r) w1r[t][q][r] = v[r];
-    }
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const m4 v = ld4(W2 + (size_t)row * H + 16 * q + 4 * g);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) w2r[t][4 * q + r] = v[r];
-    }
-    // layer 3 A operand: rows = outputs (j < K), k = the wave's units
-    const m4 v3 = j < K ? ld4(W3 + (size_t)j * H + 16 * (wave * TW + t) + 4 * g) : zero4();
-#pragma unroll
-    for (int r = 0; r < 4; ++r) w3r[t][r] = v3[r];
-  }
-  for (int i = threadIdx.x; i < H; i += MW * 64) {
-    b1s[i] = net.b1[i];
-    b2s[i] = net.b2[i];
-  }
-  const float b3v = g < K ? net.b3[g] : 0.0f;
-
   const int stride = gridDim.x * ME;
   m4 xo[MC][Q1];
   auto load_x = [&](int base) {
@@ -106,10 +78,54 @@ __global__ __launch_bounds__(MW * 64) void mlp_fwd(gr_mlp_args a) {
 #pragma unroll
       for (int q = 0; q < Q1; ++q) {
         const int k = 16 * q + 4 * g;
-        xo[c][q] = k < D ? ld4(net.x + r * ldx + k) : zero4();
+        // (Q1 == 1 branch-free: a load inside a branch is waited for at the branch's end, which drains every
+        // older load; with two input tiles the branch-free form costs spills)
+        if constexpr (Q1 == 1) {
+          const m4 v = ld4(net.x + r * ldx + (k < D ? k : 0));
+          xo[c][q] = k < D ? v : zero4();
+        } else {
+          xo[c][q] = k < D ? ld4(net.x + r * ldx + k) : zero4();
+        }
       }
     }
   };
+  // issue order: what layer 1 of the first tile needs (biases, W1, x) before W2 / W3, so that layer 1 runs while
+  // the W2 rows (256 KB per workgroup) are still arriving
+  for (int i = threadIdx.x; i < H; i += MW * 64) {
+    b1s[i] = net.b1[i];
+    b2s[i] = net.b2[i];
+  }
+  float w1r[TW][Q1][4], w2r[TW][4 * Q], w3r[TW][4];
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const int row = 16 * (wave * TW + t) + j;
+#pragma unroll
+    for (int q = 0; q < Q1; ++q) {
+      const int k = 16 * q + 4 * g;
+      const m4 v0 = ld4(W1 + (size_t)row * D + (k < D ? k : 0));
+      const m4 v = k < D ? v0 : zero4();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w1r[t][q][r] = v[r];
+    }
+  }
+  load_x(blockIdx.x * ME);
+  const float b3l = net.b3[g < K ? g : 0];
+  const float b3v = g < K ? b3l : 0.0f;
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const int row = 16 * (wave * TW + t) + j;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const m4 v = ld4(W2 + (size_t)row * H + 16 * q + 4 * g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w2r[t][4 * q + r] = v[r];
+    }
+    // layer 3 A operand: rows = outputs (j < K), k = the wave's units
+    const m4 v3l = ld4(W3 + (size_t)(j < K ? j : 0) * H + 16 * (wave * TW + t) + 4 * g);
+    const m4 v3 = j < K ? v3l : zero4();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) w3r[t][r] = v3[r];
+  }
   // the 8 waves' layer-3 partials of a tile -> y; column tile e by wave (2 kt + e) mod 8
   auto epilogue = [&](int kt, int base) {
     const int e = (wave - 2 * kt) & (MW - 1);
@@ -121,8 +137,6 @@ __global__ __launch_bounds__(MW * 64) void mlp_fwd(gr_mlp_args a) {
     const int r = base + 16 * e + j;
     if (r < n && g < K) net.y[r * K + g] = v + b3v;
   };
-
-  load_x(blockIdx.x * ME);
   __syncthreads();  // biases staged
   int kt = 0, prev_base = 0;
   for (int base = blockIdx.x * ME; base < n; base += stride, ++kt) {
@@ -477,22 +491,45 @@ __global__ __launch_bounds__(MW * 64) void mlp_bwd256(gr_mlp_args a, int rows_pe
 
   float w2c[TW][4 * Q], w3a[TW];
 #pragma unroll
-  for (int t = 0; t < TW; ++t) {
-    const int i = 16 * (wave * TW + t) + j;
+  for (int t = 0; t < TW; ++t) w3a[t] = g < K ? W3[(size_t)g * H + 16 * (wave * TW + t) + j] : 0.0f;
+  // (consumed here, before any DMA: hipcc otherwise waits vmcnt(0) at the first use of an ordinary load's result
+  // while an LDS-DMA is in flight, draining the next tile's DMA every tile)
 #pragma unroll
-    for (int q = 0; q < Q; ++q)
+  for (int t = 0; t < TW; ++t) asm volatile("" : "+v"(w3a[t]));
+  // W2 columns (lane (g, j): W2[16 q + 4 g + r][unit i]), staged through LDS by LDS-DMA in 4 chunks of 64 W2 rows,
+  // two in flight, into the tiles' space ([64][HP] twice): one 1-KB row per wave instruction, instead of 128
+  // column loads per lane gathering 64-byte segments (8 x the L2 requests; ~10 us of a 24 576-row backward)
+  float* const stg0 = lds;                // gz2s + bufb
+  float* const stg1 = lds + 2 * BE * HP;  // z2s + h1s
+  auto issue_w2 = [&](int c, float* dst) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) w2c[t][4 * q + r] = W2[(size_t)(16 * q + 4 * g + r) * H + i];
-    w3a[t] = g < K ? W3[(size_t)g * H + i] : 0.0f;
+    for (int rr = 0; rr < 64 / MW; ++rr) {
+      const int row = wave + MW * rr;
+      glds16(W2 + (size_t)(64 * c + row) * H + 4 * lane, dst + row * HP);
+    }
+  };
+  issue_w2(0, stg0);
+  issue_w2(1, stg1);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if (c < 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // chunk c in (chunk c + 1 may be in flight)
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();
+    const float* src = (c & 1) ? stg1 : stg0;
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      const int i = 16 * (wave * TW + t) + j;
+#pragma unroll
+      for (int q = 4 * c; q < 4 * c + 4; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) w2c[t][4 * q + r] = src[(16 * (q - 4 * c) + 4 * g + r) * HP + i];
+    }
+    if (c + 2 < 4) {
+      raw_barrier();  // every wave has read chunk c
+      issue_w2(c + 2, (c & 1) ? stg1 : stg0);
+    }
   }
-  // the weights are consumed here, before any DMA: hipcc otherwise waits vmcnt(0) at their first use in the loop
-  // (a use of an ordinary load's result while an LDS-DMA is in flight), draining the next tile's DMA every tile
-#pragma unroll
-  for (int t = 0; t < TW; ++t) {
-#pragma unroll
-    for (int k = 0; k < 4 * Q; ++k) asm volatile("" : "+v"(w2c[t][k]));
-    asm volatile("" : "+v"(w3a[t]));
-  }
+  raw_barrier();  // every wave has read the last chunk (its space is the DMA targets, zeroed next)
   m4 gw1[TW][DT], gw3[TW];
   float gb1[TW][4], gb2[TW][4], gb3 = 0.0f;
 #pragma unroll

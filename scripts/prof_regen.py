@@ -36,7 +36,7 @@ def main():
     env.reset()
     g = torch.Generator(device=dev).manual_seed(5)
     acts = torch.randn(8, n, 4, device=dev, generator=g)
-    for k in range(a.interval - 1 - 16):
+    for k in range(a.interval - 1 - 15 - 16):  # (then 15 timed plain steps, 16 warm-up steps: phase R - 1)
         env.step(acts[k % 8])
     while env._next_terrain is not None and not env._next_terrain.done():
         time.sleep(0.01)
@@ -88,10 +88,13 @@ def main():
         setattr(obj, attr, w)
 
     res["full_reset_before_swap_us"] = wall(lambda: env.reset(), reps=4)
-    while env.common_step_counter % env._regen_steps != env._regen_steps - 1:
+    while env.common_step_counter % env._regen_steps != env._regen_steps - 17:
         env.step(acts[3])
     while env._next_terrain is not None and not env._next_terrain.done():
         time.sleep(0.01)
+    torch.cuda.synchronize()
+    for _ in range(16):  # (the GPU idled while the host waited: warm it up again)
+        env.step(acts[3])
     torch.cuda.synchronize()
     env._call = timed_call
     for attr in ("_regenerate_in_step", "regenerate_terrain", "reset", "observe", "_advance"):
@@ -114,10 +117,13 @@ def main():
         env.observe()
     res["step_plus_full_reset_and_observe_us"] = wall(step_reset_observe, reps=8)
     # a second interval: the regenerating step again, uninstrumented (the first one may carry one-time costs)
-    while env.common_step_counter % env._regen_steps != env._regen_steps - 1:
+    while env.common_step_counter % env._regen_steps != env._regen_steps - 17:
         env.step(acts[4])
     while env._next_terrain is not None and not env._next_terrain.done():
         time.sleep(0.01)
+    torch.cuda.synchronize()
+    for _ in range(16):
+        env.step(acts[4])
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     _, _, _, _, extras = env.step(acts[0])
