@@ -1113,6 +1113,17 @@ int gr_adam_step(const gr_adam_args* a, void* stream) {
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
+int gr_adam_clip_step(const gr_adam_args* a, float max_norm, float* norm_out, const float* kl, float* lr,
+                      double desired_kl, double lr_min, double lr_max, void* stream) {
+  if (!adam_args_ok(a) || !(max_norm > 0.0f)) return GR_ERR_ARG;
+  if (kl && (!lr || lr != a->lr_ptr || !(desired_kl > 0.0) || !(lr_min > 0.0) || !(lr_max >= lr_min)))
+    return GR_ERR_ARG;
+  const hipError_t e = gr::launch_adam_clip_step(*a, max_norm, norm_out, kl, kl ? lr : nullptr,
+                                                 (float)(desired_kl * 2.0), (float)(desired_kl / 2.0), (float)lr_min,
+                                                 (float)lr_max, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
 static bool dones_bytes_ok(int b) { return b == 1 || b == 4 || b == 8; }
 
 int gr_store_transition(const gr_transition_args* a, void* stream) {

@@ -135,6 +135,8 @@ hipError_t launch_in_forward(const float* x, long long m, int d, int ldx, const 
                              float slope, float* y, hipStream_t s);
 hipError_t launch_adam_clip(const gr_adam_args& a, float max_norm, float* norm_out, hipStream_t s);
 hipError_t launch_adam_step(const gr_adam_args& a, hipStream_t s);
+hipError_t launch_adam_clip_step(const gr_adam_args& a, float max_norm, float* norm_out, const float* kl, float* lr,
+                                 float hi, float lo, float lr_min, float lr_max, hipStream_t s);
 hipError_t launch_store_transition(const gr_transition_args& a, hipStream_t s);  // gr_rollout.hip
 hipError_t launch_episode_accumulate(long long n, const float* reward, const void* dones, int dones_bytes,
                                      float* cur_rew, float* cur_len, float* fin_rew, float* fin_len,

@@ -877,6 +877,87 @@ __global__ __launch_bounds__(256) void adam_update(gr_adam_args a) {
   }
 }
 
+// gr_adam_clip_step: the rate rule, the clip and Adam in 2 launches instead of 5 (adaptive_lr, norm_part, clip_apply,
+// count, update), the same arithmetic.  Launch 1: the per-block squared norms; workgroup 0 also applies the rate rule
+// (when kl is given) and each segment's first workgroup counts its step (nothing reads either before launch 2).
+// Launch 2: every workgroup sums the partial norms in the same order (clip coefficient), derives its segment's bias
+// corrections from the counted step (in double, as adam_count), then clips and updates its elements in one pass.
+__global__ __launch_bounds__(256) void adam_norm_count(gr_adam_args a, const float* __restrict__ kl, float* lr,
+                                                       float hi, float lo, float lr_min, float lr_max) {
+  __shared__ double sm[4];
+  const int b = blockIdx.x, s = adam_segment_of(a, b);
+  const gr_adam_segment g = a.seg[s];
+  const long long base = (long long)(b - g.block_start) * GR_ADAM_BLOCK;
+  double acc = 0.0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const long long j = base + k * 256 + threadIdx.x;
+    if (j < g.numel) {
+      const double x = g.grad[j];
+      acc += x * x;
+    }
+  }
+  for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    a.part[b] = (sm[0] + sm[1]) + (sm[2] + sm[3]);
+    if (b == g.block_start) a.step[g.step_slot] = a.step[g.step_slot] + 1.0f;
+    if (b == 0 && kl) {  // adaptive_lr's expression
+      const float k = kl[0], r = lr[0];
+      float up = r * 1.5f;
+      up = up > lr_max ? lr_max : up;
+      float down = r / 1.5f;
+      down = down < lr_min ? lr_min : down;
+      lr[0] = k > hi ? down : ((lo > k && k > 0.0f) ? up : r);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void adam_clip_update(gr_adam_args a, float max_norm, float* __restrict__ norm_out) {
+  __shared__ double sm[4];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < a.nblocks; i += 256) acc += a.part[i];
+  for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  const float norm = (float)sqrt((sm[0] + sm[1]) + (sm[2] + sm[3]));
+  float c = max_norm / (norm + 1.0e-6f);
+  c = (c < 1.0f || c != c) ? c : 1.0f;  // (as adam_clip_apply)
+  const int b = blockIdx.x, s = adam_segment_of(a, b);
+  if (b == 0 && threadIdx.x == 0 && norm_out) norm_out[0] = norm;
+  const gr_adam_segment g = a.seg[s];
+  const long long base = (long long)(b - g.block_start) * GR_ADAM_BLOCK;
+  // (as adam_count, from the step launch 1 counted)
+  const float t = a.step[g.step_slot];
+  const double lrd = a.lr_ptr ? (double)a.lr_ptr[0] : a.lr;
+  const float step_size = (float)(lrd / (1.0 - pow(a.beta1, (double)t)));
+  const float bc2s = (float)sqrt(1.0 - pow(a.beta2, (double)t));
+  const float w1 = (float)(1.0 - a.beta1), b2 = (float)a.beta2, w2 = (float)(1.0 - a.beta2);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const long long j = base + q * 256 + threadIdx.x;
+    if (j >= g.numel) break;
+    const float gr = g.grad[j] * c;
+    g.grad[j] = gr;  // (clip_grad_norm_ scales the gradients in place)
+    float m = g.exp_avg[j], v = g.exp_avg_sq[j];
+    m = m + w1 * (gr - m);
+    v = v * b2;
+    v = v + (w2 * gr) * gr;
+    g.exp_avg[j] = m;
+    g.exp_avg_sq[j] = v;
+    const float denom = sqrtf(v) / bc2s + a.eps;
+    g.param[j] = g.param[j] + (-step_size) * (m / denom);
+  }
+}
+
+hipError_t launch_adam_clip_step(const gr_adam_args& a, float max_norm, float* norm_out, const float* kl, float* lr,
+                                 float hi, float lo, float lr_min, float lr_max, hipStream_t s) {
+  hipLaunchKernelGGL(adam_norm_count, dim3(a.nblocks), dim3(256), 0, s, a, kl, lr, hi, lo, lr_min, lr_max);
+  hipLaunchKernelGGL(adam_clip_update, dim3(a.nblocks), dim3(256), 0, s, a, max_norm, norm_out);
+  return hipGetLastError();
+}
+
 hipError_t launch_adam_clip(const gr_adam_args& a, float max_norm, float* norm_out, hipStream_t s) {
   hipLaunchKernelGGL(adam_norm_part, dim3(a.nblocks), dim3(256), 0, s, a);
   hipLaunchKernelGGL(adam_clip_apply, dim3(a.nblocks), dim3(256), 0, s, a, max_norm, norm_out);

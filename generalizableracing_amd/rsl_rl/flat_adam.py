@@ -166,6 +166,26 @@ class FlatAdam(torch.optim.Optimizer):
                     torch.autograd.graph.increment_version(p)
         return loss
 
+    @torch.no_grad()
+    def clip_and_step(self, max_norm: float, kl: torch.Tensor | None = None, desired_kl: float | None = None,
+                      lr_min: float = 1e-5, lr_max: float = 1e-2) -> torch.Tensor:
+        """[the adaptive rate rule on the device, when kl is given (the rate is then the group's device tensor)] +
+        clip_grad_norm_(max_norm) + step(), as gr_adam_clip_step's two launches (the graph-captured update's
+        segment B); returns the norm (a device tensor)."""
+        a = self._args()
+        if a is None:
+            return self._norm[0].zero_()
+        lr = self.param_groups[0]["lr"]
+        if kl is not None and not (torch.is_tensor(lr) and lr.data_ptr() == a.lr_ptr):
+            raise ValueError("clip_and_step: the adaptive rule needs the group's rate as a device tensor")
+        _call("gr_adam_clip_step", C.addressof(a), C.c_float(float(max_norm)), self._norm.data_ptr(),
+              kl.data_ptr() if kl is not None else None, lr.data_ptr() if kl is not None else None,
+              C.c_double(float(desired_kl or 0.0)), C.c_double(lr_min), C.c_double(lr_max), self._stream())
+        for p in self.param_groups[0]["params"]:
+            if p.grad is not None:
+                torch.autograd.graph.increment_version(p)
+        return self._norm[0]
+
     def state_dict(self):
         """torch.optim.Adam's non-capturable layout, so the reference runner (on_policy_runner.py:319) can load a
         checkpoint into torch.optim.Adam and step it: `lr` a Python float (the graphed update binds a device tensor

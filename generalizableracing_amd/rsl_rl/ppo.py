@@ -395,6 +395,10 @@ class _GraphedStep:
 
     def _seg_b(self):
         alg = self.alg
+        if isinstance(self.opt, _fadam.FlatAdam):  # the rate rule, the clip and Adam: two launches (gr_adam_clip_step)
+            self.opt.clip_and_step(alg.max_grad_norm, kl=self.flat.extra if self._adaptive() else None,
+                                   desired_kl=alg.desired_kl)
+            return
         if self._adaptive():  # on the rank-averaged KL mean once the flat buffer has been all-reduced: the
             # comparisons of ppo.py:133-150 on the device, one launch (gr_adaptive_lr)
             _lin._lib_call("gr_adaptive_lr", self.flat.extra.data_ptr(), self.lr.data_ptr(),

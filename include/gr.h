@@ -622,6 +622,12 @@ typedef struct {
 int gr_adam_prepare(gr_adam_segment* table, int32_t nseg, int32_t* nblocks);
 int gr_adam_clip(const gr_adam_args* args, float max_norm, float* norm_out, void* stream);
 int gr_adam_step(const gr_adam_args* args, void* stream);
+/* gr_adaptive_lr (when kl is not null; lr must then be args->lr_ptr) + gr_adam_clip + gr_adam_step in two launches
+ * instead of five, the same arithmetic (the graph-captured update's segment B, generalizableracing_amd/rsl_rl/ppo.py
+ * _GraphedStep): the rate rule and the step counts ride in the launch of the per-block norms, the clip coefficient,
+ * the bias corrections and the clipped gradient (still written back) in the Adam pass. */
+int gr_adam_clip_step(const gr_adam_args* args, float max_norm, float* norm_out, const float* kl, float* lr,
+                      double desired_kl, double lr_min, double lr_max, void* stream);
 
 /* The rollout loop's per-step bookkeeping (generalizableracing_amd/rsl_rl/rollout_ops.py), one launch each, the
  * torch ops' arithmetic in their order (bit-identical stored rollouts).  Context-free, graph-capturable.

@@ -546,3 +546,65 @@ def test_flat_adam_graph_capture_reads_rate_tensor():
     torch.cuda.synchronize()
     for a, b in zip(pa, pb):
         assert torch.equal(a.detach(), b.detach())
+
+
+@pytest.mark.parametrize("adaptive", [False, True])
+def test_flat_adam_clip_and_step_equals_three_calls(adaptive):
+    """gr_adam_clip_step (FlatAdam.clip_and_step: two launches, the graphed update's segment B) is bit-identical to
+    gr_adaptive_lr + gr_adam_clip + gr_adam_step over 4 steps, captured and replayed, with the KL below, inside and
+    above the rule's band (the rate moves both ways), one parameter without a gradient, and the clip active."""
+    from generalizableracing_amd import _abi
+    from generalizableracing_amd.rsl_rl.flat_adam import FlatAdam
+
+    g = torch.Generator(device="cpu").manual_seed(5)
+    shapes = _actor_critic_shapes()
+    p0 = [torch.randn(s, generator=g) * 0.1 for s in shapes]
+    pa = [p.clone().to(DEV).requires_grad_() for p in p0]
+    pb = [p.clone().to(DEV).requires_grad_() for p in p0]
+    grads = [(torch.randn(s, generator=g)).to(DEV) for s in shapes]
+    skip = 3
+    for i, (a, b, gg) in enumerate(zip(pa, pb, grads)):
+        if i != skip:
+            a.grad, b.grad = gg.clone(), gg.clone()
+    lra, lrb = torch.tensor(1e-3, device=DEV), torch.tensor(1e-3, device=DEV)
+    kla, klb = torch.zeros(1, device=DEV), torch.zeros(1, device=DEV)
+    oa, ob = FlatAdam(pa, lr=lra), FlatAdam(pb, lr=lrb)
+    desired = 0.01
+    lib = _abi.load()
+
+    def three():
+        if adaptive:
+            assert lib.gr_adaptive_lr(klb.data_ptr(), lrb.data_ptr(), C.c_double(desired), C.c_double(1e-5),
+                                      C.c_double(1e-2), torch.cuda.current_stream().cuda_stream) == 0
+        ob.clip_grad_norm_(0.5)
+        ob.step()
+
+    oa.clip_and_step(0.5, kl=kla if adaptive else None, desired_kl=desired)  # (tables uploaded outside the capture)
+    three()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        oa.clip_and_step(0.5, kl=kla if adaptive else None, desired_kl=desired)
+    for it, kl in enumerate((0.05, 0.001, 0.0, 0.01)):
+        kla.fill_(kl)
+        klb.fill_(kl)
+        for i, (a, b, gg) in enumerate(zip(pa, pb, grads)):
+            if i != skip:
+                a.grad.copy_(gg * (it + 2))
+                b.grad.copy_(gg * (it + 2))
+        graph.replay()
+        three()
+        torch.cuda.synchronize()
+        assert torch.equal(lra, lrb), it
+        assert torch.equal(oa._norm, ob._norm), it
+        for a, b in zip(pa, pb):
+            assert torch.equal(a.detach(), b.detach()), it
+            if a.grad is not None:
+                assert torch.equal(a.grad, b.grad), it
+    if adaptive:
+        assert float(lra) != 1e-3
+    for a, b in zip(pa, pb):
+        if b in ob.state:
+            for k in ("step", "exp_avg", "exp_avg_sq"):
+                assert torch.equal(oa.state[a][k], ob.state[b][k]), k
