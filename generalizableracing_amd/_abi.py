@@ -233,7 +233,7 @@ EXPORTS = [
     "gr_camera_render", "gr_camera_bytes_per_env", "gr_policy_forward", "gr_policy_args_size", "gr_column_sum_partials", "gr_column_sum",
     "gr_head_partials", "gr_head_forward", "gr_head_backward", "gr_mlp_in_partials", "gr_mlp_in_forward",
     "gr_mlp_in_backward", "gr_ppo_loss_partials", "gr_ppo_loss_forward", "gr_ppo_loss_backward",
-    "gr_adam_prepare", "gr_adam_clip", "gr_adam_step", "gr_adam_clip_step",
+    "gr_adam_prepare", "gr_adam_clip", "gr_adam_step", "gr_adam_clip_step", "gr_ppo_loss_forward_backward",
     "gr_store_transition", "gr_episode_accumulate", "gr_gae", "gr_l2c2_mix",
     "gr_ppo_loss_forward_loss", "gr_ppo_loss_backward_loss", "gr_adaptive_lr",
     "gr_bn_scratch_doubles", "gr_bn_act_forward", "gr_bn_act_backward", "gr_stem1_scratch_doubles",
@@ -305,6 +305,7 @@ def _declare(lib):
         "gr_adam_clip": (C.c_int, [vp, C.c_float, vp, vp]),
         "gr_adam_step": (C.c_int, [vp, vp]),
         "gr_adam_clip_step": (C.c_int, [vp, C.c_float, vp, vp, vp, C.c_double, C.c_double, C.c_double, vp]),
+        "gr_ppo_loss_forward_backward": (C.c_int, [vp, vp, C.c_float, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "gr_ppo_loss_forward": (C.c_int, [vp, vp, vp, vp]),
         "gr_ppo_loss_backward": (C.c_int, [vp, vp, vp, vp, vp, vp, vp]),
         "gr_mlp_in_forward": (C.c_int, [vp, C.c_int64, C.c_int32, C.c_int32, vp, vp, C.c_int32, C.c_float, vp, vp]),

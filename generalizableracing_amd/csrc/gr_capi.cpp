@@ -1209,6 +1209,17 @@ int gr_ppo_loss_backward_loss(const gr_ppo_loss_args* a, const float* g_loss, fl
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
+int gr_ppo_loss_forward_backward(const gr_ppo_loss_args* a, const float* g_loss, float value_coef, float* partial,
+                                 float* sums, float* loss, float* stats, float* acc, float* kl_out, float* dmu,
+                                 float* dvalue, float* dpartial, float* dstd, void* stream) {
+  if (!loss_args_ok(a) || !g_loss || !partial || !sums || !loss || !stats || !dmu || !dvalue || !dpartial || !dstd ||
+      partial == dpartial)
+    return GR_ERR_ARG;
+  const hipError_t e = gr::launch_ppo_loss_forward_backward(*a, g_loss, value_coef, partial, sums, loss, stats, acc,
+                                                            kl_out, dmu, dvalue, dpartial, dstd, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
 int gr_adaptive_lr(const float* kl, float* lr, double desired_kl, double lr_min, double lr_max, void* stream) {
   if (!kl || !lr || !(desired_kl > 0.0) || !(lr_min > 0.0) || !(lr_max >= lr_min)) return GR_ERR_ARG;
   const hipError_t e = gr::launch_adaptive_lr(kl, lr, (float)(desired_kl * 2.0), (float)(desired_kl / 2.0),

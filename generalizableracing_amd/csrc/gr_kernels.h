@@ -148,6 +148,9 @@ int ppo_loss_blocks(long long rows);
 hipError_t launch_ppo_loss_forward(const gr_ppo_loss_args& a, float* part, float* sums, hipStream_t s);
 hipError_t launch_ppo_loss_forward_loss(const gr_ppo_loss_args& a, float* part, float* sums, float value_coef,
                                         float* loss, float* stats, float* acc, float* kl_out, hipStream_t s);
+hipError_t launch_ppo_loss_forward_backward(const gr_ppo_loss_args& a, const float* g, float value_coef, float* part,
+                                            float* sums, float* loss, float* stats, float* acc, float* kl_out,
+                                            float* dmu, float* dvalue, float* dpart, float* dstd, hipStream_t s);
 hipError_t launch_ppo_loss_backward(const gr_ppo_loss_args& a, const float* g, int gv_index, float gv_coef, float* dmu,
                                     float* dvalue, float* part, float* dstd, hipStream_t s);
 hipError_t launch_adaptive_lr(const float* kl, float* lr, float hi, float lo, float lr_min, float lr_max,

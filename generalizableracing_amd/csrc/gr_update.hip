@@ -752,6 +752,108 @@ hipError_t launch_ppo_loss_forward_loss(const gr_ppo_loss_args& a, float* part, 
   return hipGetLastError();
 }
 
+// gr_ppo_loss_forward_backward: ppo_loss_forward and ppo_loss_backward (combined-loss form) in one pass over the
+// rows, for a caller that knows the upstream gradient's device address before the backward runs (the graph-captured
+// step's persistent seed): the per-row gradients and the std gradient's partial rows come out of the forward pass,
+// and one final launch reduces both the loss sums and the std gradient, in the orders of the two-pass form
+// (bit-identical to gr_ppo_loss_forward_loss + gr_ppo_loss_backward_loss)
+__global__ __launch_bounds__(256) void ppo_loss_fwd_bwd(gr_ppo_loss_args a, const float* __restrict__ g,
+                                                        float value_coef, float* __restrict__ part,
+                                                        float* __restrict__ dmu, float* __restrict__ dvalue,
+                                                        float* __restrict__ dpart) {
+  __shared__ float sm[4][3];
+  __shared__ float smd[4][8];
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  float sd[8];
+  for (int j = 0; j < a.k; ++j) sd[j] = a.std[j];
+  float t[3] = {0.0f, 0.0f, 0.0f};
+  float ds[8];
+  for (int j = 0; j < 8; ++j) ds[j] = 0.0f;
+  if (i < a.rows) {
+    LossRow r;
+    float kl;
+    pl_row(a, i, sd, r, &kl);
+    // forward (ppo_loss_forward)
+    t[0] = max_keep_nan(r.s1, r.s2);
+    const float l1 = (r.v - r.ret) * (r.v - r.ret), l2 = (r.vc - r.ret) * (r.vc - r.ret);
+    t[1] = a.clipped_value ? max_keep_nan(l1, l2) : (r.ret - r.v) * (r.ret - r.v);
+    t[2] = kl;
+    // backward (ppo_loss_backward, gv_index 0, gv_coef value_coef)
+    const float inv_m = 1.0f / (float)a.rows;
+    const float gs = g[0] * inv_m, gv = (value_coef * g[0]) * inv_m;
+    const float A = a.adv[i * a.ld_adv];
+    const float w1 = r.s1 > r.s2 ? 1.0f : (r.s1 == r.s2 ? 0.5f : 0.0f), w2 = 1.0f - w1;
+    const float inclip = (r.ratio >= 1.0f - a.clip && r.ratio <= 1.0f + a.clip) ? 1.0f : 0.0f;
+    const float dratio = gs * (w1 * -A + w2 * (-A * inclip));
+    const float dlogp = dratio * r.ratio;
+    for (int j = 0; j < a.k; ++j) {
+      const float mu = pl_at(a.mu, a.ld_mu, i, j), x = pl_at(a.act, a.ld_act, i, j);
+      const float d = x - mu, var = sd[j] * sd[j];
+      dmu[i * a.k + j] = dlogp * (d / var);
+      ds[j] = dlogp * (d * d / (var * sd[j]) - 1.0f / sd[j]);
+    }
+    float dv;
+    if (a.clipped_value) {
+      const float u1 = l1 > l2 ? 1.0f : (l1 == l2 ? 0.5f : 0.0f), u2 = 1.0f - u1;
+      const float vin = (r.vdiff >= -a.clip && r.vdiff <= a.clip) ? 1.0f : 0.0f;
+      dv = gv * (u1 * 2.0f * (r.v - r.ret) + u2 * 2.0f * (r.vc - r.ret) * vin);
+    } else {
+      dv = gv * (2.0f * (r.v - r.ret));
+    }
+    dvalue[i] = dv;
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const float v = pl_wave_sum(t[q]);
+    if (lane == 0) sm[wv][q] = v;
+  }
+  for (int j = 0; j < a.k; ++j) {
+    const float v = pl_wave_sum(ds[j]);
+    if (lane == 0) smd[wv][j] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) part[(size_t)blockIdx.x * 4 + threadIdx.x] = ((sm[0][threadIdx.x] + sm[1][threadIdx.x]) + sm[2][threadIdx.x]) + sm[3][threadIdx.x];
+  if (threadIdx.x < a.k)
+    dpart[(size_t)blockIdx.x * 8 + threadIdx.x] = ((smd[0][threadIdx.x] + smd[1][threadIdx.x]) + smd[2][threadIdx.x]) + smd[3][threadIdx.x];
+}
+
+__global__ __launch_bounds__(CF_WAVES * 64) void ppo_loss_final_fb(const float* __restrict__ part,
+                                                                   const float* __restrict__ dpart, int rows, int k,
+                                                                   float* __restrict__ sums, long long m,
+                                                                   float value_coef, float* __restrict__ loss,
+                                                                   float* __restrict__ stats, float* __restrict__ acc,
+                                                                   float* __restrict__ kl_out, float* __restrict__ dstd) {
+  partials_final_body(part, rows, 3, 4, sums);
+  __syncthreads();
+  if (threadIdx.x == 0) {  // (as ppo_loss_final)
+    __threadfence_block();
+    const float inv_m = 1.0f / (float)m;
+    const float surr = sums[0] * inv_m, val = sums[1] * inv_m, kl = sums[2] * inv_m;
+    loss[0] = surr + value_coef * val;
+    stats[0] = surr;
+    stats[1] = val;
+    stats[2] = kl;
+    if (acc) {
+      acc[0] = acc[0] + surr;
+      acc[1] = acc[1] + val;
+    }
+    if (kl_out) kl_out[0] = kl;
+  }
+  __syncthreads();
+  partials_final_body(dpart, rows, k, 8, dstd);
+}
+
+hipError_t launch_ppo_loss_forward_backward(const gr_ppo_loss_args& a, const float* g, float value_coef, float* part,
+                                            float* sums, float* loss, float* stats, float* acc, float* kl_out,
+                                            float* dmu, float* dvalue, float* dpart, float* dstd, hipStream_t s) {
+  const int blocks = ppo_loss_blocks(a.rows);
+  hipLaunchKernelGGL(ppo_loss_fwd_bwd, dim3(blocks), dim3(256), 0, s, a, g, value_coef, part, dmu, dvalue, dpart);
+  hipLaunchKernelGGL(ppo_loss_final_fb, dim3(1), dim3(CF_WAVES * 64), 0, s, part, dpart, blocks, a.k, sums,
+                     (long long)a.rows, value_coef, loss, stats, acc, kl_out, dstd);
+  return hipGetLastError();
+}
+
 hipError_t launch_ppo_loss_backward(const gr_ppo_loss_args& a, const float* g, int gv_index, float gv_coef, float* dmu,
                                     float* dvalue, float* part, float* dstd, hipStream_t s) {
   const int blocks = ppo_loss_blocks(a.rows);

@@ -100,20 +100,35 @@ class _PPOLossCombinedFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old, clip, clipped_value,
-                value_coef, acc, kl_out):
+                value_coef, acc, kl_out, seed):
         from .. import _abi
 
         std = std.contiguous()
         a = _args(mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old, clip, clipped_value)
-        rows = mu.shape[0]
+        rows, k = mu.shape
         dev = mu.device
-        part = torch.empty(_abi.load().gr_ppo_loss_partials(rows), device=dev, dtype=torch.float32)
+        npart = _abi.load().gr_ppo_loss_partials(rows)
+        part = torch.empty(npart, device=dev, dtype=torch.float32)
         sums = torch.empty(3, device=dev, dtype=torch.float32)
         loss = torch.empty((), device=dev, dtype=torch.float32)
         stats = torch.empty(3, device=dev, dtype=torch.float32)
-        _call("gr_ppo_loss_forward_loss", C.addressof(a), part.data_ptr(), sums.data_ptr(), C.c_float(value_coef),
-              loss.data_ptr(), stats.data_ptr(), acc.data_ptr() if acc is not None else None,
-              kl_out.data_ptr() if kl_out is not None else None, torch.cuda.current_stream(dev).cuda_stream)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        accp, klp = (acc.data_ptr() if acc is not None else None), (kl_out.data_ptr() if kl_out is not None else None)
+        ctx.pre = None
+        if seed is not None:
+            # the backward's per-row gradients in the forward's pass (gr_ppo_loss_forward_backward), for the
+            # upstream gradient the caller will seed autograd with (the graph-captured step's persistent one)
+            dmu = torch.empty(rows, k, device=dev, dtype=torch.float32)
+            dvalue = torch.empty(rows, device=dev, dtype=torch.float32)
+            dpart = torch.empty(npart, device=dev, dtype=torch.float32)
+            dstd = _std_sink(std, k)
+            _call("gr_ppo_loss_forward_backward", C.addressof(a), seed.data_ptr(), C.c_float(value_coef),
+                  part.data_ptr(), sums.data_ptr(), loss.data_ptr(), stats.data_ptr(), accp, klp, dmu.data_ptr(),
+                  dvalue.data_ptr(), dpart.data_ptr(), dstd.data_ptr(), stream)
+            ctx.pre = (seed.data_ptr(), dmu, dstd, dvalue.view(value.shape))
+        else:
+            _call("gr_ppo_loss_forward_loss", C.addressof(a), part.data_ptr(), sums.data_ptr(), C.c_float(value_coef),
+                  loss.data_ptr(), stats.data_ptr(), accp, klp, stream)
         ctx.save_for_backward(mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old)
         ctx.clip, ctx.clipped_value, ctx.value_coef = clip, clipped_value, float(value_coef)
         ctx.mark_non_differentiable(stats)
@@ -125,7 +140,9 @@ class _PPOLossCombinedFn(torch.autograd.Function):
         from .. import _abi
 
         if g_loss is None:
-            return (None,) * 15
+            return (None,) * 16
+        if ctx.pre is not None and g_loss.data_ptr() == ctx.pre[0]:  # computed in the forward, for this seed
+            return ctx.pre[1:] + (None,) * 13
         mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old = ctx.saved_tensors
         a = _args(mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old, ctx.clip, ctx.clipped_value)
         rows, k = mu.shape
@@ -134,10 +151,21 @@ class _PPOLossCombinedFn(torch.autograd.Function):
         dmu = torch.empty(rows, k, device=dev, dtype=torch.float32)
         dvalue = torch.empty(rows, device=dev, dtype=torch.float32)
         part = torch.empty(_abi.load().gr_ppo_loss_partials(rows), device=dev, dtype=torch.float32)
-        dstd = torch.empty(k, device=dev, dtype=torch.float32)
+        dstd = _std_sink(std, k)
         _call("gr_ppo_loss_backward_loss", C.addressof(a), g.data_ptr(), C.c_float(ctx.value_coef), dmu.data_ptr(),
               dvalue.data_ptr(), part.data_ptr(), dstd.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
-        return (dmu, dstd, dvalue.view(value.shape)) + (None,) * 12
+        return (dmu, dstd, dvalue.view(value.shape)) + (None,) * 13
+
+
+def _std_sink(std, k):
+    """The std gradient's buffer: its view in the graph-captured step's flat gradient buffer when the std is the
+    parameter itself (linear._GRAD_SINK; the step then copies no gradient), else a new tensor."""
+    from . import linear as _lin
+
+    sink = _lin._GRAD_SINK.get(id(std)) if _lin._GRAD_SINK is not None else None
+    if sink is not None and sink.dtype == torch.float32 and sink.is_contiguous() and sink.numel() == k:
+        return sink.view(k)
+    return torch.empty(k, device=std.device, dtype=torch.float32)
 
 
 def _policy_std(pol):
@@ -158,15 +186,20 @@ def policy_outputs(alg, obs, critic_obs):
     return pol.actor(obs), pol.critic(critic_obs)
 
 
-def ppo_loss(alg, obs, critic_obs, act, value_old, adv, ret, logp_old, mu_old, sig_old, acc=None, kl_out=None):
+def ppo_loss(alg, obs, critic_obs, act, value_old, adv, ret, logp_old, mu_old, sig_old, acc=None, kl_out=None,
+             seed=None):
     """(loss, [surrogate, value, KL] means) of one mini-batch: loss = surrogate + value_loss_coef * value
-    (- entropy_coef * entropy) as in ppo.py:171-172, differentiable; the same values as ppo_losses."""
+    (- entropy_coef * entropy) as in ppo.py:171-172, differentiable; the same values as ppo_losses.  seed: the
+    device tensor autograd will be seeded with (the loss's gradient), when known now and the loss is the root: the
+    losses' backward then runs inside the forward's pass (gr_ppo_loss_forward_backward)."""
     pol = alg.policy
     mu, value = policy_outputs(alg, obs, critic_obs)
     std = _policy_std(pol)
+    if alg.entropy_coef != 0.0:  # (the loss is not the root then: its gradient is not the seed)
+        seed = None
     loss, stats = _PPOLossCombinedFn.apply(mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old,
                                            float(alg.clip_param), bool(alg.use_clipped_value_loss),
-                                           float(alg.value_loss_coef), acc, kl_out)
+                                           float(alg.value_loss_coef), acc, kl_out, seed)
     if alg.entropy_coef != 0.0:  # Normal.entropy summed over the actions: the same for every sample
         ent = (0.5 + 0.5 * math.log(2.0 * math.pi) + torch.log(std)).sum()
         loss = loss - alg.entropy_coef * ent

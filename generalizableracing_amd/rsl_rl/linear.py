@@ -28,6 +28,11 @@ SPLIT = 4096  # rows per chunk (scripts/prof_update.py --split: 2048-4096 best a
 # set by the graph-captured PPO step (ppo.py _GraphedStep): every Linear takes _TallLinearFn, whose bias
 # gradient is gr_column_sum (see bias_grad)
 _FORCE_FN = False
+# {id(parameter): gradient view} while the graph-captured PPO step differentiates into its flat gradient buffer
+# (ppo.py _GraphedStep._backward): _FusedMLPsFn's backward then writes a network's six gradients straight into
+# their views when they lie back to back in kernel order (gr_mlp_backward's [gW1 | gb1 | gW2 | gb2 | gW3 | gb3]),
+# so the step copies none of them
+_GRAD_SINK = None
 
 
 def bias_grad(gy: torch.Tensor) -> torch.Tensor:
@@ -383,7 +388,9 @@ class _FusedMLPsFn(torch.autograd.Function):
             gy = gys[i]
             gy = torch.zeros(rows, k, device=dev, dtype=torch.float32) if gy is None else gy.float().contiguous()
             gys_keep.append(gy)
-            grads = torch.empty(h * d + h + h * h + h + k * h + k, device=dev, dtype=torch.float32)
+            grads = _sink_region(params[6 * i:6 * i + 6])
+            if grads is None:
+                grads = torch.empty(h * d + h + h * h + h + k * h + k, device=dev, dtype=torch.float32)
             s = GrMlpNet()
             s.x, s.ldx, s.d, s.k = xs[i].data_ptr(), xs[i].stride(0), d, k
             for name, t in (("w1", w1), ("b1", b1), ("w2", w2), ("b2", b2), ("w3", w3), ("b3", b3)):
@@ -408,6 +415,23 @@ class _FusedMLPsFn(torch.autograd.Function):
         a.partial = part.data_ptr()
         _lib_call("gr_mlp_backward", C.byref(a), _stream(xs[0]))
         return (None, None) + (None,) * nnets + tuple(grads_out)
+
+
+def _sink_region(params):
+    """The span of the flat gradient buffer holding these six parameters' gradient views (_GRAD_SINK), when they
+    are contiguous, back to back and in this order; else None."""
+    if _GRAD_SINK is None:
+        return None
+    views = [_GRAD_SINK.get(id(p)) for p in params]
+    if any(v is None for v in views):
+        return None
+    base, off = views[0], 0
+    for p, v in zip(params, views):
+        if v.dtype != torch.float32 or not v.is_contiguous() or v.numel() != p.numel() or \
+                v.data_ptr() != base.data_ptr() + 4 * off:
+            return None
+        off += p.numel()
+    return torch.as_strided(base, (off,), (1,), base.storage_offset())
 
 
 def fused_mlps(nets, xs):

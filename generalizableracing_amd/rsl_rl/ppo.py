@@ -360,8 +360,13 @@ class _GraphedStep:
         obs, priv = obs.float(), priv.float()
         if alg._use_fused_losses(obs):  # (fused_loss.py: one device op each way, the means and the loss finished
             # there: the step's loss sums accumulate in self.acc, the KL mean lands in the flat buffer's extra slot)
-            loss, _ = _floss.ppo_loss(alg, obs, priv, act, val, adv, ret, logp, mu, sig, acc=self.acc,
-                                      kl_out=self.flat.extra[:1] if self._adaptive() else None)
+            # (the gradients land in the flat buffer's views directly while the sink is set: linear._GRAD_SINK)
+            _lin._GRAD_SINK = {id(p): v for p, v in zip(self.flat.params, self.flat.views)}
+            try:
+                loss, _ = _floss.ppo_loss(alg, obs, priv, act, val, adv, ret, logp, mu, sig, acc=self.acc,
+                                          kl_out=self.flat.extra[:1] if self._adaptive() else None, seed=self.one)
+            finally:
+                _lin._GRAD_SINK = None
             self._backward(loss)
             return
         # the eager loop's policy.act also draws a sample it never uses; torch.normal's check of the std
@@ -389,9 +394,16 @@ class _GraphedStep:
             grads = torch.autograd.grad(loss, self.params, retain_graph=True, allow_unused=True)
             self.flat = alg._check_all_grads(loss, self.params, grads)
             self.flat.bind()
-        # (the seed gradient from a persistent 1: no fill launch in the captured step)
-        grads = torch.autograd.grad(loss, self.flat.params, grad_outputs=self.one)
-        torch._foreach_copy_(self.flat.views, list(grads))
+        # (the seed gradient from a persistent 1: no fill launch in the captured step; the fused MLP backward writes
+        # its gradients into their flat views directly, linear._GRAD_SINK, and only the others are copied)
+        _lin._GRAD_SINK = {id(p): v for p, v in zip(self.flat.params, self.flat.views)}
+        try:
+            grads = torch.autograd.grad(loss, self.flat.params, grad_outputs=self.one)
+        finally:
+            _lin._GRAD_SINK = None
+        pairs = [(v, g) for v, g in zip(self.flat.views, grads) if g.data_ptr() != v.data_ptr()]
+        if pairs:
+            torch._foreach_copy_([v for v, _ in pairs], [g for _, g in pairs])
 
     def _seg_b(self):
         alg = self.alg

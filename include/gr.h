@@ -576,6 +576,14 @@ int gr_ppo_loss_forward_loss(const gr_ppo_loss_args* args, float* partial, float
                              float* stats, float* acc, float* kl_out, void* stream);
 int gr_ppo_loss_backward_loss(const gr_ppo_loss_args* args, const float* g_loss, float value_coef, float* dmu,
                               float* dvalue, float* partial, float* dstd, void* stream);
+/* gr_ppo_loss_forward_loss + gr_ppo_loss_backward_loss in one pass over the rows (+ one final reduction), for a caller
+ * that knows the upstream gradient's device address before the backward runs (the graph-captured update's persistent
+ * seed, generalizableracing_amd/rsl_rl/fused_loss.py): the per-row gradients dmu / dvalue and dstd come out of the
+ * forward pass, bit-identical to the two-pass form.  partial / dpartial: two distinct gr_ppo_loss_partials(rows)
+ * buffers. */
+int gr_ppo_loss_forward_backward(const gr_ppo_loss_args* args, const float* g_loss, float value_coef, float* partial,
+                                 float* sums, float* loss, float* stats, float* acc, float* kl_out, float* dmu,
+                                 float* dvalue, float* dpartial, float* dstd, void* stream);
 /* The graph-captured update's adaptive learning-rate rule (ppo.py:133-150, device form): lr[0] = max(lr_min,
  * lr / 1.5) if kl[0] > 2 desired_kl; min(lr_max, lr * 1.5) if desired_kl / 2 > kl[0] > 0; else unchanged (fp32
  * arithmetic, the thresholds rounded to fp32 as torch's scalar comparisons do). */
