@@ -30,7 +30,8 @@ class PPO:
                  use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu",
                  normalize_advantage=True, storage_obs_dtype=torch.float32, fused_rollout_inference=False,
                  fused_rollout_precision="bf16", graph_update=False, update_autocast_bf16=False,
-                 graph_update_segmented=False, fused_losses=True, fused_adam=True, fused_mlp=True, **kwargs):
+                 graph_update_segmented=False, fused_losses=True, fused_adam=True, fused_mlp=True,
+                 graph_update_per_step=False, **kwargs):
         self.env = env
         self.device = device
         self.desired_kl = desired_kl
@@ -68,6 +69,8 @@ class PPO:
         # two graph segments with the collectives run eagerly between them: always at world size > 1; this
         # switch forces it on one rank (tests: the segmented step must equal the single graph)
         self.graph_update_segmented = bool(graph_update_segmented)
+        # one graph per mini-batch step instead of one per epoch (the state between steps can be inspected: tests)
+        self.graph_update_per_step = bool(graph_update_per_step)
         self._graphed = None
         self._grads_checked = False  # which parameters the loss reaches (see _check_all_grads)
         self._unused: set = set()
@@ -308,7 +311,8 @@ class _GraphedStep:
 
     Two segments: A = gathers, forward, KL, losses, backward (into the flat buffer); B = learning-rate rule,
     clip, Adam.  The rate only enters Adam, so computing it after the backward changes nothing.  With one
-    rank both segments are one graph.  With several ranks (any backend) they are two graphs and the exchange
+    rank both segments of every mini-batch of an epoch are one graph (each step gathers by its own slice of the
+    update's permutation), replayed once per epoch.  With several ranks (any backend) they are two graphs and the exchange
     runs eagerly between them: ONE in-place all-reduce of the flat buffer carries the gradients and the KL
     mean together.  No collective is ever captured."""
 
@@ -332,31 +336,37 @@ class _GraphedStep:
                 g["capturable"] = True
         alg.optimizer = self.opt
         self.flat = alg.flat_grads()
-        self.idx = torch.zeros(self.mb, dtype=torch.long, device=dev)
+        self.nmb = alg.num_mini_batches
+        # the update's permutation (rollout_storage.py:152-191: one draw, the same mini-batch partition every epoch);
+        # one rank: ONE graph holds an epoch's mini-batch steps, each gathering by its own slice of this buffer (no
+        # per-step index copy or replay launch); several ranks: per-step graphs read `idx`, refilled per step
+        self.perm = torch.zeros(self.nmb * self.mb, dtype=torch.long, device=dev)
+        self.idx = self.perm[:self.mb]
         self.cols = st.sample_columns()  # packed sample rows (None: gathered field by field)
         # persistent: the graphs read it (the storage's own packed buffer, shared with the eager generator)
         self.pack = st.pack_samples(out=st.packed_buffer()) if self.cols is not None else None
         self.acc = torch.zeros(2, device=dev)  # the update's sums of the surrogate and value means
         self.one = torch.ones((), device=dev)
         self.segmented = gdist.is_dist() or alg.graph_update_segmented
-        self.graph = None  # one rank: the whole step
+        self.per_step = self.segmented or alg.graph_update_per_step
+        self.graph = None  # one rank: an epoch's steps (per_step: one step)
         self.graph_b = None  # segmented: graph = segment A, graph_b = segment B
 
-    def _gather(self):
-        """The mini-batch's fields by the static index buffer: one row gather of the packed samples (refilled
+    def _gather(self, idx):
+        """The mini-batch's fields by a static index buffer: one row gather of the packed samples (refilled
         before every update's replays, RolloutStorage.pack_samples), or one gather per field for wide rows."""
         st = self.alg.storage
         if self.cols is not None:
-            g = self.pack.index_select(0, self.idx)
+            g = self.pack.index_select(0, idx)
             return tuple(g[:, a:b] for a, b in self.cols)
-        return tuple(x.index_select(0, self.idx) for x in st.sample_sources())
+        return tuple(x.index_select(0, idx) for x in st.sample_sources())
 
     def _adaptive(self) -> bool:
         return self.alg.desired_kl is not None and self.alg.schedule == "adaptive"
 
-    def _seg_a(self):
+    def _seg_a(self, idx=None):
         alg, pol = self.alg, self.alg.policy
-        obs, priv, act, val, adv, ret, logp, mu, sig = self._gather()
+        obs, priv, act, val, adv, ret, logp, mu, sig = self._gather(self.idx if idx is None else idx)
         obs, priv = obs.float(), priv.float()
         if alg._use_fused_losses(obs):  # (fused_loss.py: one device op each way, the means and the loss finished
             # there: the step's loss sums accumulate in self.acc, the KL mean lands in the flat buffer's extra slot)
@@ -426,7 +436,7 @@ class _GraphedStep:
         self.flat.bind()  # Adam and the clip read the gradients from these views (static addresses)
         snap_o = {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in self.opt.state[p].items()}
                   for p in self.params}
-        self.idx.copy_(torch.arange(self.mb, device=self.idx.device))
+        self.perm.copy_(torch.arange(self.perm.numel(), device=self.perm.device))
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         _lin._FORCE_FN = True  # bias gradients by gr_column_sum in the captured step (linear.bias_grad)
@@ -443,10 +453,15 @@ class _GraphedStep:
                 self.graph_b = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(self.graph_b, stream=s, pool=self.graph.pool()):
                     self._seg_b()
-            else:
+            elif self.per_step:
                 with torch.cuda.graph(self.graph, stream=s):
                     self._seg_a()
                     self._seg_b()
+            else:  # an epoch: every mini-batch step, each on its slice of the permutation
+                with torch.cuda.graph(self.graph, stream=s):
+                    for i in range(self.nmb):
+                        self._seg_a(self.perm[i * self.mb:(i + 1) * self.mb])
+                        self._seg_b()
         finally:
             _lin._FORCE_FN = False
         with torch.no_grad():
@@ -462,7 +477,7 @@ class _GraphedStep:
     def update(self):
         alg = self.alg
         n = alg.num_mini_batches
-        perm = torch.randperm(n * self.mb, device=self.idx.device)  # rollout_storage.py:152-191, drawn first
+        perm = torch.randperm(n * self.mb, device=self.perm.device)  # rollout_storage.py:152-191, drawn first
         if self.pack is not None:  # this rollout's samples, packed in place (the graphs read the buffer)
             alg.storage.pack_samples(out=self.pack)
         if self.graph is None:
@@ -482,7 +497,12 @@ class _GraphedStep:
             self._capture()
         self.lr.fill_(float(alg.learning_rate))
         self.acc.zero_()
+        if not self.per_step:
+            self.perm.copy_(perm)
         for _ in range(alg.num_learning_epochs):
+            if not self.per_step:  # one replay per epoch
+                self.graph.replay()
+                continue
             for i in range(n):
                 self.idx.copy_(perm[i * self.mb:(i + 1) * self.mb])
                 self.graph.replay()

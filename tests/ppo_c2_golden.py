@@ -141,6 +141,10 @@ def replay(gp, device="cpu", **alg_kw):
     assert np.array_equal(_params(roll).float().numpy(), gp["init_params"])
     roll.init_storage("rl", mk.N, mk.T, [mk.OBS], [mk.OBS], [4])
     upd = PPO(mk.make_policy(ActorCritic), None, device=device, **mk.HP, **alg_kw)
+    # the gradients of single mini-batch steps are observable eagerly and with one graph per step; the default
+    # graph-captured form replays a whole epoch's steps at once (compared on the rate, losses and parameters)
+    record = not (alg_kw.get("graph_update") and not alg_kw.get("graph_update_per_step")
+                  and not alg_kw.get("graph_update_segmented"))
     upd.init_storage("rl", mk.N, mk.T, [mk.OBS], [mk.OBS], [4])
     report = []
     for it, (obs, cobs, rew, dones, tout, last, eps) in enumerate(data):
@@ -164,13 +168,13 @@ def replay(gp, device="cpu", **alg_kw):
         p0 = _params(upd)
         grads = []
         torch.manual_seed(200 + it)
-        with cpu_randperm(), record_grads(upd, grads):
+        with cpu_randperm(), record_grads(upd, grads, count=2 if record else 0):
             losses = upd.update()
         lr_want = float(gp[f"ppo_it{it}_lr"])
         assert abs(upd.learning_rate - lr_want) <= 1e-6 * lr_want, (it, upd.learning_rate, lr_want)
         gerr = []
         # mini-batch 1 of the second update starts from Adam moments that followed the build's own first update
-        for j in range(2 if it == 0 else 1):
+        for j in range((2 if it == 0 else 1) if record else 0):
             g, w = grads[j].double(), torch.from_numpy(gp[f"ppo_it{it}_grad_mb{j}"]).double()
             for name, a, b in _per_param(upd, g, w):
                 e = float((a - b).norm() / max(float(b.norm()), 1e-30))
@@ -188,7 +192,7 @@ def replay(gp, device="cpu", **alg_kw):
         got, want = _params(upd), torch.from_numpy(gp[f"ppo_it{it}_params"]).double()
         dev = float((got - want).norm() / (want - p0).norm())
         assert dev <= (0.15, 0.75)[it], (it, dev)
-        report.append({"grad_err": max(gerr), "param_dev_of_update": dev,
+        report.append({"grad_err": max(gerr) if gerr else None, "param_dev_of_update": dev,
                        "value_loss_rel": abs(losses["value_function"] - float(gp[f"ppo_it{it}_loss_value_function"]))
                        / abs(float(gp[f"ppo_it{it}_loss_value_function"]))})
         # teacher forcing: the next rollout and update start from the reference's parameters (Adam's moments and
