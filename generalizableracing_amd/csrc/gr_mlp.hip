@@ -488,6 +488,15 @@ __global__ __launch_bounds__(MW * 64) void mlp_bwd256(gr_mlp_args a, int rows_pe
   float* gys = xs + 2 * BE * XW; // [2][BE][4]: gy rows (LDS-DMA, by tile parity; outputs >= k stay 0)
   const float* __restrict__ W2 = net.w2;
   const float* __restrict__ W3 = net.w3;
+  // the row arrays' addresses in SGPRs for the whole kernel (opaque, so they are not re-loaded from the kernel
+  // arguments inside the tile loop: an outstanding scalar load there makes hipcc wait lgkmcnt(0) instead of the
+  // counted wait that keeps the next fragments' LDS reads in flight under the MFMAs)
+  const float* z2g = net.z2;
+  const float* h1g = net.h1;
+  const float* xg = net.x;
+  const float* gyg = net.gy;
+  float* gz2g = net.gz2;
+  asm volatile("" : "+s"(z2g), "+s"(h1g), "+s"(xg), "+s"(gyg), "+s"(gz2g));
 
   float w2c[TW][4 * Q], w3a[TW];
 #pragma unroll
@@ -551,11 +560,11 @@ __global__ __launch_bounds__(MW * 64) void mlp_bwd256(gr_mlp_args a, int rows_pe
 #pragma unroll
     for (int rr = 0; rr < BE / MW; ++rr) {
       const int row = wave + MW * rr;
-      glds16(net.z2 + clamp_row(tb + row) * H + 4 * lane, z2s + row * HP);
+      glds16(z2g + clamp_row(tb + row) * H + 4 * lane, z2s + row * HP);
     }
     if (wave >= MW - 2) {
       const int row = 16 * (wave - (MW - 2)) + (lane >> 2), kk = lane & 3;
-      if (kk < K) glds4(net.gy + clamp_row(tb + row) * K + kk, gys + par * BE * 4 + 16 * (wave - (MW - 2)) * 4);
+      if (kk < K) glds4(gyg + clamp_row(tb + row) * K + kk, gys + par * BE * 4 + 16 * (wave - (MW - 2)) * 4);
     }
   };
   // P_b: h1 rows, x (waves 0 .. 2 DT - 1: 16 / DT rows x XW floats each)
@@ -563,12 +572,12 @@ __global__ __launch_bounds__(MW * 64) void mlp_bwd256(gr_mlp_args a, int rows_pe
 #pragma unroll
     for (int rr = 0; rr < BE / MW; ++rr) {
       const int row = wave + MW * rr;
-      glds16(net.h1 + clamp_row(tb + row) * H + 4 * lane, h1s + row * HP);
+      glds16(h1g + clamp_row(tb + row) * H + 4 * lane, h1s + row * HP);
     }
     if (wave < 2 * DT) {
       constexpr int RPI = 16 / DT;  // rows per instruction
       const int row = RPI * wave + lane / (4 * DT), c4 = 4 * (lane % (4 * DT));
-      if (c4 < D) glds16(net.x + clamp_row(tb + row) * ldx + c4, xs + par * BE * XW + RPI * wave * XW);
+      if (c4 < D) glds16(xg + clamp_row(tb + row) * ldx + c4, xs + par * BE * XW + RPI * wave * XW);
     }
   };
 
@@ -622,17 +631,23 @@ __global__ __launch_bounds__(MW * 64) void mlp_bwd256(gr_mlp_args a, int rows_pe
     for (int t = 0; t < TW; ++t)
 #pragma unroll
       for (int c = 0; c < BC; ++c) acc[t][c] = zero4();
+    // (B fragments double-buffered: the next k block's LDS reads are in flight under this block's 16 MFMAs)
+    m4 gb[2][BC];
+#pragma unroll
+    for (int c = 0; c < BC; ++c) gb[0][c] = ld4(gz2s + (16 * c + j) * HP + 4 * g);
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-      m4 gb[BC];
+      if (q + 1 < Q) {
 #pragma unroll
-      for (int c = 0; c < BC; ++c) gb[c] = ld4(gz2s + (16 * c + j) * HP + 16 * q + 4 * g);
+        for (int c = 0; c < BC; ++c) gb[(q + 1) & 1][c] = ld4(gz2s + (16 * c + j) * HP + 16 * (q + 1) + 4 * g);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // (the reads first: their latency under the 16 MFMAs below)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int t = 0; t < TW; ++t)
 #pragma unroll
-          for (int c = 0; c < BC; ++c) acc[t][c] = mf(w2c[t][4 * q + r], gb[c][r], acc[t][c]);
+          for (int c = 0; c < BC; ++c) acc[t][c] = mf(w2c[t][4 * q + r], gb[q & 1][c][r], acc[t][c]);
       __builtin_amdgcn_sched_barrier(0);
     }
     // h1 (and x) of this tile: this wave's DMA retired, then every wave's (barrier)
@@ -660,7 +675,7 @@ __global__ __launch_bounds__(MW * 64) void mlp_bwd256(gr_mlp_args a, int rows_pe
 #pragma unroll
     for (int rr = 0; rr < BE / MW; ++rr) {
       const int row = wave + MW * rr;
-      if (base + row < n) st4(net.gz2 + (base + row) * H + 4 * lane, ld4(gz2s + row * HP + 4 * lane));
+      if (base + row < n) st4(gz2g + (base + row) * H + 4 * lane, ld4(gz2s + row * HP + 4 * lane));
     }
     if (has_next) issue_b(base + stride, (kt + 1) & 1);
     raw_barrier();  // (4) gz1 in LDS
@@ -830,55 +845,69 @@ __global__ __launch_bounds__(MW * 64) void mlp_wgrad(gr_mlp_args a, int splits, 
 
 // ------------------------------------------------------------------------------------------------ reductions
 // grads[net] = [gW1 (H D) | gb1 (H) | gW2 (H H) | gb2 (H) | gW3 (k H) | gb3 (k)]: element e of the vector is the
-// fixed-order sum of its partials (16 waves per 64 elements, every 16th partial row each, then wave order)
-__global__ __launch_bounds__(16 * 64) void mlp_final(gr_mlp_args a, int bwd_rows, int bwd_ld, int splits,
-                                                     const float* __restrict__ wpart) {
-  __shared__ float sm[16 * 64];
+// fixed-order sum of its partials.  A lane owns 4 consecutive elements (float4 loads of the partial rows); the 4
+// waves of a workgroup take every 4th partial row, 8 loads in flight per lane, and are summed in wave order.
+// (The small gradients come from the backward's partial rows [gW1 | gb1 | gb2 | gW3 | gb3], the hidden weight
+// gradient from mlp_wgrad's split partials.)
+constexpr int MF_WAVES = 4;
+__global__ __launch_bounds__(MF_WAVES * 64) void mlp_final(gr_mlp_args a, int bwd_rows, int bwd_ld, int splits,
+                                                          const float* __restrict__ wpart) {
+  __shared__ m4 sm[MF_WAVES * 64];
   const gr_mlp_net& net = a.net[blockIdx.y];
   const int H = a.hidden, D = net.d, K = net.k;
   const int n_small = H * D + 2 * H + K * H + K;
-  const int total = n_small + H * H;
+  const int q_small = (n_small + 3) / 4, q_total = q_small + H * H / 4;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int e = blockIdx.x * 64 + lane;
-  // source: the backward's partial rows (small gradients) or the gW2 split partials
+  const int q = blockIdx.x * 64 + lane;  // the lane's float4 of the (padded) small part, then of gW2
   const float* src;
-  int rows, ld, out;
-  if (e < n_small) {
-    src = a.partial + (size_t)blockIdx.y * bwd_rows * bwd_ld + e;
+  int rows, ldr;
+  if (q < q_small) {
+    src = a.partial + (size_t)blockIdx.y * bwd_rows * bwd_ld + 4 * q;
     rows = bwd_rows;
-    ld = bwd_ld;
-    // partial layout [gW1 | gb1 | gb2 | gW3 | gb3] -> grads layout [gW1 | gb1 | gW2 | gb2 | gW3 | gb3]
-    out = e < H * D + H ? e : e + H * H;
-  } else if (e < total) {
-    const int f = e - n_small;
-    src = wpart + (size_t)blockIdx.y * splits * H * H + f;
+    ldr = bwd_ld;
+  } else if (q < q_total) {
+    src = wpart + (size_t)blockIdx.y * splits * H * H + 4 * (q - q_small);
     rows = splits;
-    ld = H * H;
-    out = H * D + H + f;
+    ldr = H * H;
   } else {
     src = nullptr;
     rows = 0;
-    ld = 0;
-    out = 0;
+    ldr = 0;
   }
-  float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+  m4 acc0 = zero4(), acc1 = zero4();
   if (src) {
     int b = wv;
-    for (; b + 48 < rows; b += 64) {
-      a0 += src[(size_t)b * ld];
-      a1 += src[(size_t)(b + 16) * ld];
-      a2 += src[(size_t)(b + 32) * ld];
-      a3 += src[(size_t)(b + 48) * ld];
+    for (; b + 7 * MF_WAVES < rows; b += 8 * MF_WAVES) {
+      m4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = ld4(src + (size_t)(b + u * MF_WAVES) * ldr);
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        acc0 += v[u];
+        acc1 += v[u + 1];
+      }
     }
-    for (; b < rows; b += 16) a0 += src[(size_t)b * ld];
+    for (; b < rows; b += MF_WAVES) acc0 += ld4(src + (size_t)b * ldr);
   }
-  sm[threadIdx.x] = (a0 + a1) + (a2 + a3);
+  sm[threadIdx.x] = acc0 + acc1;
   __syncthreads();
   if (wv == 0 && src) {
-    float s = 0.0f;
+    m4 t = sm[lane];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) s += sm[k * 64 + lane];
-    net.grads[out] = s;
+    for (int w = 1; w < MF_WAVES; ++w) t += sm[w * 64 + lane];
+    if (q < q_small) {
+      // partial layout [gW1 | gb1 | gb2 | gW3 | gb3] -> grads [gW1 | gb1 | gW2 | gb2 | gW3 | gb3] (the boundary at
+      // H D + H is a multiple of 4: a float4 lies on one side)
+      const int e = 4 * q;
+      const int out = e < H * D + H ? e : e + H * H;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (e + r < n_small) net.grads[out + r] = t[r];
+    } else {
+      const int f = 4 * (q - q_small);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) net.grads[H * D + H + f + r] = t[r];
+    }
   }
 }
 
@@ -993,9 +1022,9 @@ hipError_t launch_mlp_backward(const gr_mlp_args& a, hipStream_t s) {
   float* wpart = a.partial + (size_t)a.nets * bwd_blocks * row;
   e = a.hidden == 256 ? launch_wgrad_t<256>(a, splits, rps, wpart, s) : launch_wgrad_t<128>(a, splits, rps, wpart, s);
   if (e != hipSuccess) return e;
-  const int total = a.hidden * d + 2 * a.hidden + k * a.hidden + k + a.hidden * a.hidden;
-  hipLaunchKernelGGL(mlp_final, dim3((total + 63) / 64, a.nets), dim3(16 * 64), 0, s, a, bwd_blocks, row, splits,
-                     (const float*)wpart);
+  const int q_total = (a.hidden * d + 2 * a.hidden + k * a.hidden + k + 3) / 4 + a.hidden * a.hidden / 4;
+  hipLaunchKernelGGL(mlp_final, dim3((q_total + 63) / 64, a.nets), dim3(MF_WAVES * 64), 0, s, a, bwd_blocks, row,
+                     splits, (const float*)wpart);
   return hipGetLastError();
 }
 
