@@ -16,6 +16,7 @@ the end of its 24-step rollout).
 from __future__ import annotations
 
 import ctypes as C
+import time
 from collections.abc import Mapping
 from concurrent.futures import ThreadPoolExecutor
 
@@ -26,6 +27,14 @@ from .racing_cfg import RacingEnvCfg
 from .tracks import build_tracks
 
 LOG_RING = 64
+# diagnostics (scripts/prof_regen.py): a list to append (label, time.perf_counter()) stamps to inside
+# regenerate_terrain; None = off
+REGEN_STAMPS = None
+
+
+def _stamp(label):
+    if REGEN_STAMPS is not None:
+        REGEN_STAMPS.append((label, time.perf_counter()))
 
 
 _EMPTY_MEAN_SLOTS = [_abi.LOG_EPSUM0 + j for j in range(7)] + [_abi.LOG_ACC, _abi.LOG_M_ACTRATE, _abi.LOG_M_LINSPD,
@@ -244,6 +253,7 @@ class RacingEnv:
         """gr_terrain_commit on the env's stream; the generation's host arrays become the env's track_gates /
         track_records / obstacle_table."""
         self._call("gr_terrain_commit", self._stream())
+        _stamp("commit_call")
         # (alive until two commits later: the upload from it is long done, and no pinned block is released in
         # the capture of an interval step)
         self._held_prev, self._held_terrain = self._held_terrain, pin
@@ -321,13 +331,16 @@ class RacingEnv:
         be complete already (a replay commits whatever was staged last)."""
         g = self.terrain_generation + 1
         staged = None
+        _stamp("enter")
         if self._next_terrain is not None and self._resident:
             g_built, gates, recs, obst, pin, done, rc = self._next_terrain.result()
+            _stamp("result")
             assert g_built == g
             if rc == 0:
                 # (under a graph capture no event may be touched: the caller has synchronised the upload)
                 if not torch.cuda.is_current_stream_capturing():
                     torch.cuda.current_stream(self.device).wait_event(done)
+                _stamp("wait_event")
                 staged = (gates, recs, obst, pin)
             elif rc != _abi.GR_ERR_CAPACITY:
                 raise RuntimeError(f"gr_terrain_stage failed (status {rc}): "
@@ -342,8 +355,11 @@ class RacingEnv:
             staged = (gates, recs, obst, pin)
         gates, recs, obst, pin = staged
         self._commit(pin, gates, recs, obst)
+        _stamp("commit")
         self.terrain_generation = g
-        return self.reset(out_set=out_set)
+        out = self.reset(out_set=out_set)
+        _stamp("reset")
+        return out
 
     # ------------------------------------------------------------------ plumbing
     @staticmethod

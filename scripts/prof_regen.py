@@ -96,6 +96,24 @@ def main():
     for _ in range(16):  # (the GPU idled while the host waited: warm it up again)
         env.step(acts[3])
     torch.cuda.synchronize()
+    from generalizableracing_amd.envs import racing_env as _re
+    _re.REGEN_STAMPS = []
+    # an uninstrumented interval step first, with stamps inside regenerate_terrain only (host time between them)
+    t0 = time.perf_counter()
+    env.step(acts[0])
+    torch.cuda.synchronize()
+    res["regenerating_step_stamped_us"] = (time.perf_counter() - t0) * 1e6
+    st = _re.REGEN_STAMPS
+    res["regenerate_terrain_host_us"] = {f"{a}->{b}": (tb - ta) * 1e6 for (a, ta), (b, tb) in zip(st, st[1:])}
+    _re.REGEN_STAMPS = None
+    while env.common_step_counter % env._regen_steps != env._regen_steps - 17:
+        env.step(acts[3])
+    while env._next_terrain is not None and not env._next_terrain.done():
+        time.sleep(0.01)
+    torch.cuda.synchronize()
+    for _ in range(16):
+        env.step(acts[3])
+    torch.cuda.synchronize()
     env._call = timed_call
     for attr in ("_regenerate_in_step", "regenerate_terrain", "reset", "observe", "_advance"):
         wrap(env, attr)
@@ -129,7 +147,7 @@ def main():
     _, _, _, _, extras = env.step(acts[0])
     torch.cuda.synchronize()
     res["second_regenerating_step_us"] = (time.perf_counter() - t0) * 1e6
-    assert extras.get("terrain_regenerated") and env.terrain_generation == 2
+    assert extras.get("terrain_regenerated") and env.terrain_generation == 3
     res["plain_step_after_us"] = wall(lambda: env.step(acts[5]), reps=8)
     env.close()
     print(json.dumps(res, indent=1))
