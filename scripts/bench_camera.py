@@ -87,8 +87,9 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=6)
     ap.add_argument("--no-noise", action="store_true", help="ablation: policy image without noise")
     ap.add_argument("--period", type=float, default=None, help="camera update_period override (0: every step)")
+    ap.add_argument("--gates-only", action="store_true", help="obstacle-free tracks")
     a = ap.parse_args(argv)
-    print(json.dumps(run(a.envs, a.steps, a.warmup, a.no_noise, a.period)))
+    print(json.dumps(run(a.envs, a.steps, a.warmup, a.no_noise, a.period, obstacles=not a.gates_only)))
 
 
 if __name__ == "__main__":
