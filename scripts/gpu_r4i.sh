@@ -20,6 +20,6 @@ step mlp_tests bash -c "timeout -k 10 300 python -u -m pytest -x -v --timeout 12
 step mlp_trace bash -c "cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/mlp -o mlp -- python3 $R/scripts/time_mlp.py --reps 10 > $OUT/mlp_trace.log 2>&1"
 step camsplit bash scripts/gpu_cam_split.sh ${T}_camsplit
 step b2 env REPS=4 bash scripts/time_libs.sh ${T}_b2.txt variants/barrier2_lds_only/libgr.so
-step gpu_suite bash -c "timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1"
+step gpu_suite bash -c "timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1"
 step bench bash -c "timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err"
 echo done > $OUT/done
