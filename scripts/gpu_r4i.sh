@@ -18,6 +18,7 @@ step() {
 step regen timeout -k 10 300 python -u scripts/prof_regen.py --out $OUT/regen.json > $OUT/regen.log 2>&1
 step mlp_tests bash -c "timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_fused_mlp.py tests/test_gpu_ppo_c2_golden.py tests/test_gpu_camera.py > $OUT/pytest_mlp_cam.log 2>&1"
 step mlp_trace bash -c "cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/mlp -o mlp -- python3 $R/scripts/time_mlp.py --reps 10 > $OUT/mlp_trace.log 2>&1"
+step mlp_wgrad512 bash -c "GR_LIB_PATH=$R/variants/wgrad_512/libgr.so timeout -k 10 200 python -u scripts/time_mlp.py > $OUT/time_mlp_wgrad512.jsonl 2>&1 && timeout -k 10 200 python -u scripts/time_mlp.py > $OUT/time_mlp_tree.jsonl 2>&1"
 step camsplit bash scripts/gpu_cam_split.sh ${T}_camsplit
 step b2 env REPS=4 bash scripts/time_libs.sh ${T}_b2.txt variants/barrier2_lds_only/libgr.so
 step gpu_suite bash -c "timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1"
