@@ -30,8 +30,7 @@ DEV_INLINE void nt_store4(float4* p, float4 v) {
 #define CAM_WAVES 4
 #define CAM_SLOT4 (GR_CAM_SLOT / 4)
 #ifndef CAM_BATCH
-#define CAM_BATCH 4  // reuse path: depth quad PAIRS loaded per lane before any is consumed (8 quads in flight; more
-                     // costs occupancy: 9 pairs took the gate-only kernel from 75 to 120 VGPRs)
+#define CAM_BATCH 9  // reuse path: depth quads loaded per lane before any is consumed (27 = 3 x 9 at 96x72)
 #endif
 
 // both observation rows of one pixel quad: its 4 noise values z, normalisation, streaming stores
