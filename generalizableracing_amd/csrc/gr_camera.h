@@ -242,23 +242,11 @@ GR_HD float gr_cam_obs(float d, float z, float std, float scale, float inv_scale
 /* the critic image: no noise */
 GR_HD float gr_cam_obs_clean(float d, float scale, float inv_scale) { return (d > scale ? scale : d) * inv_scale; }
 
-/* the eight standard normals of pixel-quad pair `pair` (pixels 8*pair .. 8*pair+7): one Philox block, eight
- * 16-bit fields, four Box-Muller pairs (u1 = (f + 1) 2^-16 in (0, 1]: the radius is truncated at 4.71 sigma; u2 =
- * f 2^-16: the angle in 2^-16 turns).  For the image's multiplicative noise (noise_std 0.02) both are far below
- * what the observation resolves; one block per 8 pixels halves the per-pixel Philox work of the camera kernel. */
-GR_HD void gr_cam_noise8(uint32_t gid, uint32_t cnt, uint32_t pair, uint32_t k0, uint32_t k1, float z[8]) {
-  const gr_u32x4 r = gr_philox4x32_10(gid, cnt, GR_TAG_IMG, pair, k0, k1);
-  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
-  for (int p = 0; p < 4; ++p)
-    gr_box_muller_u((float)((w[p] & 0xFFFFu) + 1u) * 1.52587891e-05f, (float)(w[p] >> 16) * 1.52587891e-05f,
-                    &z[2 * p], &z[2 * p + 1]);
-}
-
-/* the four standard normals of pixel quad `quad` (pixels 4*quad .. 4*quad+3): its half of gr_cam_noise8 */
+/* the four standard normals of pixel quad `quad` (pixels 4*quad .. 4*quad+3) */
 GR_HD void gr_cam_noise4(uint32_t gid, uint32_t cnt, uint32_t quad, uint32_t k0, uint32_t k1, float z[4]) {
-  float z8[8];
-  gr_cam_noise8(gid, cnt, quad >> 1, k0, k1, z8);
-  for (int j = 0; j < 4; ++j) z[j] = z8[4 * (quad & 1u) + j];
+  const gr_u32x4 r = gr_philox4x32_10(gid, cnt, GR_TAG_IMG, quad, k0, k1);
+  gr_box_muller(r.x, r.y, &z[0], &z[1]);
+  gr_box_muller(r.z, r.w, &z[2], &z[3]);
 }
 
 /* Isaac Lab sensor timing (SensorBase.update / _update_outdated_buffers): a sensor is

@@ -33,10 +33,12 @@ DEV_INLINE void nt_store4(float4* p, float4 v) {
 #define CAM_BATCH 9  // reuse path: depth quads loaded per lane before any is consumed (27 = 3 x 9 at 96x72)
 #endif
 
-// both observation rows of one pixel quad: its 4 noise values z, normalisation, streaming stores
-DEV_INLINE void emit_quad_z(const gr_cam_const* __restrict__ cc, float4* op4, float4* oc4, int q, float4 d4,
-                            const float z[4]) {
+// both observation rows of one pixel quad: fresh noise (quad index q), normalisation, streaming stores
+DEV_INLINE void emit_quad(const CamArgs& a, const gr_cam_const* __restrict__ cc, float4* op4, float4* oc4, int q,
+                          float4 d4, uint32_t gid, uint32_t cnt) {
   const float scale = cc->obs_scale, inv = cc->inv_obs_scale, nstd = cc->noise_std;
+  float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (cc->add_noise) gr_cam_noise4(gid, cnt, (uint32_t)q, a.seed_lo, a.seed_hi, z);
   float4 op, oc;
   op.x = gr_cam_obs(d4.x, z[0], nstd, scale, inv); oc.x = gr_cam_obs_clean(d4.x, scale, inv);
   op.y = gr_cam_obs(d4.y, z[1], nstd, scale, inv); oc.y = gr_cam_obs_clean(d4.y, scale, inv);
@@ -44,15 +46,6 @@ DEV_INLINE void emit_quad_z(const gr_cam_const* __restrict__ cc, float4* op4, fl
   op.w = gr_cam_obs(d4.w, z[3], nstd, scale, inv); oc.w = gr_cam_obs_clean(d4.w, scale, inv);
   nt_store4(op4 + q, op);
   nt_store4(oc4 + q, oc);
-}
-
-// both rows of pixel quads 2 p and 2 p + 1: fresh noise (one Philox block for the pair, gr_cam_noise8)
-DEV_INLINE void emit_pair(const CamArgs& a, const gr_cam_const* __restrict__ cc, float4* op4, float4* oc4, int p,
-                          float4 d0, float4 d1, uint32_t gid, uint32_t cnt) {
-  float z[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-  if (cc->add_noise) gr_cam_noise8(gid, cnt, (uint32_t)p, a.seed_lo, a.seed_hi, z);
-  emit_quad_z(cc, op4, oc4, 2 * p, d0, z);
-  emit_quad_z(cc, op4, oc4, 2 * p + 1, d1, z + 4);
 }
 
 DEV_INLINE void wave_lds_sync() {
@@ -71,22 +64,20 @@ DEV_INLINE void state_terms(const CamArgs& a, int i, int lane, size_t row) {
   }
 }
 
-// sensor up to date: stream the depth buffer into both rows, a lane per pixel-quad pair (32 contiguous bytes),
-// CAM_BATCH pairs' loads in flight per lane
+// sensor up to date: stream the depth buffer into both rows, CAM_BATCH loads in flight per lane
 DEV_INLINE void reuse_rows(const CamArgs& a, const gr_cam_const* __restrict__ cc, const float4* dep4, float4* op4,
-                           float4* oc4, int np, int lane, uint32_t gid, uint32_t cnt) {
-  for (int p0 = 0; p0 < np; p0 += 64 * CAM_BATCH) {
-    float4 dd[CAM_BATCH][2];
+                           float4* oc4, int nq, int lane, uint32_t gid, uint32_t cnt) {
+  for (int q0 = 0; q0 < nq; q0 += 64 * CAM_BATCH) {
+    float4 dd[CAM_BATCH];
 #pragma unroll
     for (int j = 0; j < CAM_BATCH; ++j) {
-      const int p = p0 + 64 * j + lane;
-      dd[j][0] = p < np ? dep4[2 * p] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      dd[j][1] = p < np ? dep4[2 * p + 1] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      const int q = q0 + 64 * j + lane;
+      dd[j] = q < nq ? dep4[q] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
 #pragma unroll
     for (int j = 0; j < CAM_BATCH; ++j) {
-      const int p = p0 + 64 * j + lane;
-      if (p < np) emit_pair(a, cc, op4, oc4, p, dd[j][0], dd[j][1], gid, cnt);
+      const int q = q0 + 64 * j + lane;
+      if (q < nq) emit_quad(a, cc, op4, oc4, q, dd[j], gid, cnt);
     }
   }
 }
@@ -289,7 +280,7 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
   const int nq = npix >> 2;
 
   if (!render) {
-    reuse_rows(a, cc, dep4, op4, oc4, nq >> 1, lane, gid, cnt);
+    reuse_rows(a, cc, dep4, op4, oc4, nq, lane, gid, cnt);
     return;
   }
 
@@ -379,13 +370,11 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
       }
     }
     wave_lds_sync();
-    // (a band's quads start at an even quad index and come in pairs: W is a multiple of 8, checked at enable)
     const int qb = (v0 * W) >> 2, nqb = (rows * W) >> 2;
-    for (int pp = lane; 2 * pp < nqb; pp += 64) {
-      const float4 d0 = s_stage[2 * pp], d1 = s_stage[2 * pp + 1];
-      nt_store4(dep4 + qb + 2 * pp, d0);
-      nt_store4(dep4 + qb + 2 * pp + 1, d1);
-      emit_pair(a, cc, op4, oc4, (qb >> 1) + pp, d0, d1, gid, cnt);
+    for (int qq = lane; qq < nqb; qq += 64) {
+      const float4 d4 = s_stage[qq];
+      nt_store4(dep4 + qb + qq, d4);
+      emit_quad(a, cc, op4, oc4, qb + qq, d4, gid, cnt);
     }
     wave_lds_sync();
   }

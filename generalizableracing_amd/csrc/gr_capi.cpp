@@ -802,9 +802,8 @@ int gr_enable_camera(gr_ctx* c, const gr_camera_config* k) {
   if (!c || !k) return fail(c, GR_ERR_ARG, "gr_enable_camera: null pointer");
   const float* r = k->offset_rot;
   const float qn = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
-  // (a multiple of 8: the kernel writes the image rows as pixel-quad pairs, band by band)
-  if (k->width <= 0 || k->width > GR_CAM_MAX_W || k->width % 8 != 0 || k->height <= 0 || k->height > GR_CAM_MAX_H)
-    return fail(c, GR_ERR_ARG, "gr_enable_camera: width must be a multiple of 8 in [8, 256], height in [1, 256]");
+  if (k->width <= 0 || k->width > GR_CAM_MAX_W || k->width % 4 != 0 || k->height <= 0 || k->height > GR_CAM_MAX_H)
+    return fail(c, GR_ERR_ARG, "gr_enable_camera: width must be a multiple of 4 in [4, 256], height in [1, 256]");
   if (!(k->fx > 0.0f) || !(k->fy > 0.0f) || !std::isfinite(k->cx) || !std::isfinite(k->cy) || !(qn > 0.0f) ||
       !(k->max_distance > 0.0f) || !(k->obs_scale > 0.0f) || !(k->update_period >= 0.0f) || !(k->noise_std >= 0.0f))
     return fail(c, GR_ERR_ARG, "gr_enable_camera: invalid intrinsics / offset / range / noise");

@@ -78,18 +78,15 @@ GR_HD float gr_u01_open0(uint32_t w) { return (float)((w >> 8) + 1u) * 5.9604645
 /* torch-style  U(lo, hi) = u * (hi - lo) + lo  (Isaac Lab sample_uniform op order) */
 GR_HD float gr_uniform(uint32_t w, float lo, float hi) { return gr_u01(w) * (hi - lo) + lo; }
 
-/* Box-Muller from u1 in (0, 1] and u2 in [0, 1) */
-GR_HD void gr_box_muller_u(float u1, float u2, float* z0, float* z1) {
+/* Box-Muller: two standard normals from two words */
+GR_HD void gr_box_muller(uint32_t w0, uint32_t w1, float* z0, float* z1) {
+  float u1 = gr_u01_open0(w0);
+  float u2 = gr_u01(w1);
   float rad = gr_sqrtf(-2.0f * gr_logf(u1));
   float s, c;
   gr_sincosf(6.28318548f * u2, &s, &c);
   *z0 = rad * c;
   *z1 = rad * s;
-}
-
-/* Box-Muller: two standard normals from two words */
-GR_HD void gr_box_muller(uint32_t w0, uint32_t w1, float* z0, float* z1) {
-  gr_box_muller_u(gr_u01_open0(w0), gr_u01(w1), z0, z1);
 }
 
 /* Six 21-bit fields from one 128-bit draw (bits 0..125; 126-127 unused).  The

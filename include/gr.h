@@ -223,7 +223,7 @@ typedef struct gr_buffers {
  * Defaults (gr_camera_config_default) are those of the reference cfg.
  */
 typedef struct gr_camera_config {
-  int32_t width, height;  /* 96, 72 (width a multiple of 8) */
+  int32_t width, height;  /* 96, 72 */
   float fx, fy, cx, cy;   /* pinhole intrinsics in pixels (from_intrinsic_matrix, :87-91) */
   float offset_pos[3];    /* (0.01, 0, 0) in the body frame */
   float offset_rot[4];    /* (0.991, 0, -0.131, 0) w,x,y,z, "world" convention; normalised */
