@@ -631,32 +631,19 @@ __global__ __launch_bounds__(MW * 64) void mlp_bwd256(gr_mlp_args a, int rows_pe
     for (int t = 0; t < TW; ++t)
 #pragma unroll
       for (int c = 0; c < BC; ++c) acc[t][c] = zero4();
-    // (B fragments double-buffered: the next k block's LDS reads are in flight under this block's 16 MFMAs.  The
-    // reads are inline asm with counted lgkmcnt waits: hipcc waits lgkmcnt(0) after issuing them, which exposes
-    // their latency every k block)
-    m4 gb[2][BC];
-    const uint32_t gz2_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)(gz2s + j * HP + 4 * g);
-#pragma unroll
-    for (int c = 0; c < BC; ++c)
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(gb[0][c]) : "v"(gz2_lds), "i"(4 * 16 * c * HP));
+    // (B fragments single-buffered, the next block's reads not hoisted: measured faster than double-buffered
+    // fragments, with hipcc's or with counted waits (mlp_bwd256 at 393 216 rows 1.06 vs 1.08-1.11 ms))
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-      if (q + 1 < Q) {
+      m4 gb[BC];
 #pragma unroll
-        for (int c = 0; c < BC; ++c)
-          asm volatile("ds_read_b128 %0, %1 offset:%2"
-                       : "=v"(gb[(q + 1) & 1][c])
-                       : "v"(gz2_lds), "i"(4 * (16 * c * HP + 16 * (q + 1))));
-        asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(gb[q & 1][0]), "+v"(gb[q & 1][1]));
-      } else {
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(gb[q & 1][0]), "+v"(gb[q & 1][1]));
-      }
+      for (int c = 0; c < BC; ++c) gb[c] = ld4(gz2s + (16 * c + j) * HP + 16 * q + 4 * g);
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int t = 0; t < TW; ++t)
 #pragma unroll
-          for (int c = 0; c < BC; ++c) acc[t][c] = mf(w2c[t][4 * q + r], gb[q & 1][c][r], acc[t][c]);
+          for (int c = 0; c < BC; ++c) acc[t][c] = mf(w2c[t][4 * q + r], gb[c][r], acc[t][c]);
       __builtin_amdgcn_sched_barrier(0);
     }
     // h1 (and x) of this tile: this wave's DMA retired, then every wave's (barrier)

@@ -131,7 +131,12 @@ class RacingEnv:
         self._builder = ThreadPoolExecutor(max_workers=1, thread_name_prefix="gr-terrain") \
             if self._regen_steps is not None else None
         self._next_terrain = None
-        self._held_terrain = None  # the live generation's pinned host arrays (resident: the last upload's source)
+        # the builder's pinned upload sources: two persistent sets with the reservation's capacities, generation g
+        # staged from set g % 2 (the interval step never allocates or frees pinned memory: a pinned free took
+        # ~0.5 ms of its host time)
+        self._pin_pool = [None, None]
+        # host objects of replaced generations, released on the builder thread when it starts the next build
+        self._retired = []
         self._scratch_set = None  # the interval step's reset outputs (allocated with the output sets below)
         self._load_terrain(self._terrain_seed(0))
 
@@ -217,6 +222,39 @@ class RacingEnv:
         o.num_items = int(obst.items.shape[0])
         return o
 
+    def _pinned_set(self, k, gates, recs, obst):
+        """Pinned set k of the pool holding this generation's arrays (views with its shapes into buffers with the
+        reservation's capacities; allocated on first use, reused every other generation).  None when the generation
+        does not fit (a new reservation follows in _stage_now)."""
+        caps = self._capacity
+        if obst is not None and (obst.max_obstacles > caps[0] or obst.cells.shape[0] > caps[1]
+                                 or obst.items.shape[0] > caps[2]):
+            return None
+        ps = self._pin_pool[k]
+        if ps is None or ps["gates"].shape != gates.shape or ps["caps"] != caps:
+            ps = {"caps": caps, "gates": torch.empty(gates.shape, dtype=torch.float32, pin_memory=True),
+                  "records": torch.empty(recs.shape, dtype=torch.float32, pin_memory=True)}
+            if obst is not None:
+                ntr = obst.counts.shape[0]
+                ps["o_records"] = torch.empty(ntr * caps[0] * obst.records.shape[2], dtype=torch.float32,
+                                              pin_memory=True)
+                ps["o_counts"] = torch.empty(ntr, dtype=torch.int32, pin_memory=True)
+                ps["o_grid_f"] = torch.empty(ntr, 4, dtype=torch.float32, pin_memory=True)
+                ps["o_grid_i"] = torch.empty(ntr, 4, dtype=torch.int32, pin_memory=True)
+                ps["o_cells"] = torch.empty(caps[1] * 2, dtype=torch.int32, pin_memory=True)
+                ps["o_items"] = torch.empty(caps[2] * obst.items.shape[1], dtype=torch.float32, pin_memory=True)
+            self._pin_pool[k] = ps
+        pin = {"gates": ps["gates"], "records": ps["records"]}
+        pin["gates"].copy_(torch.from_numpy(gates))
+        pin["records"].copy_(torch.from_numpy(recs))
+        if obst is not None:
+            for key in ("records", "counts", "grid_f", "grid_i", "cells", "items"):
+                a = getattr(obst, key)
+                v = ps["o_" + key].view(-1)[:a.size].view(a.shape)
+                v.copy_(torch.from_numpy(a))
+                pin["o_" + key] = v
+        return pin
+
     def _reserve_terrain(self, obst):
         """gr_terrain_reserve with room for generations somewhat larger than `obst` (the generator's sizes vary by
         ~1 % between seeds; a larger one reallocates, outside any graph)."""
@@ -254,10 +292,11 @@ class RacingEnv:
         track_records / obstacle_table."""
         self._call("gr_terrain_commit", self._stream())
         _stamp("commit_call")
-        # (alive until two commits later: the upload from it is long done, and no pinned block is released in
-        # the capture of an interval step)
-        self._held_prev, self._held_terrain = self._held_terrain, pin
-        self.track_gates, self.track_records = pin["gates"], pin["records"]
+        # the replaced generation's host objects (and a fresh pin set, _stage_now) are released by the builder when
+        # it starts the next build, not here: no host free in the interval step (nor in its graph capture)
+        self._retired.append((getattr(self, "track_gates", None), getattr(self, "track_records", None),
+                              getattr(self, "obstacle_table", None), pin))
+        self.track_gates, self.track_records = torch.from_numpy(gates), torch.from_numpy(recs)
         self.obstacle_table = obst
         self.obstacles = None
 
@@ -276,10 +315,14 @@ class RacingEnv:
         # the staging arrays are free once everything enqueued so far (the last commit, eager or a graph replay) ran
         after = torch.cuda.Event()
         after.record(torch.cuda.current_stream(dev))
+        retired, self._retired = self._retired, []
 
         def work():
+            retired.clear()  # (the previous generations' host objects, released here)
             gates, recs, obst = self._build_terrain(self._terrain_seed(g))
-            pin = self._pin_generation(gates, recs, obst)
+            pin = self._pinned_set(g % 2, gates, recs, obst)
+            if pin is None:  # larger than the reservation: staged again by the interval step (_stage_now)
+                return g, gates, recs, obst, None, None, _abi.GR_ERR_CAPACITY
             with torch.cuda.stream(side):
                 side.wait_event(after)
                 rc = self._stage(pin, obst, side.cuda_stream)
