@@ -434,6 +434,247 @@ __global__ __launch_bounds__(BN_FINAL_THREADS) void stem1_wgrad_final(int n, int
   for (int v = threadIdx.x; v < n; v += BN_FINAL_THREADS) gw[v] = (float)tot[v];
 }
 
+// ------------------------------------------------------------- the first block on fp32 MFMA (C = 16)
+// The per-row kernels above spend four threads per row (one per 4 channels), each re-deriving the row's image
+// and cell and gathering the same 9 pixels, plus 36 VALU FMAs; the four passes were VALU-bound at 1.7-2.4x their
+// HBM floors (profiles/round03_vision_update_kernel_stats.csv).  Here a wave takes 16 rows at a time and the conv
+// is three v_mfma_f32_16x16x4f32 (K = 9 padded to 12): lane l gathers pixels k = l/16, l/16 + 4 (and 8 for
+// l < 16) of row l % 16 — the A operand — against the weights W[l % 16][k] held as the B operand, and receives
+// x[row 4 (l/16) + v][channel l % 16], v = 0..3.  The MFMA is a k-ordered fmaf chain from 0 (padding adds exact
+// zeros), so every x is bit-identical to stem_conv's.  The conv weight's gradient is a second product on the same
+// tile, G[ch][k] += sum_rows gx[row][ch] px[row][k]: the lane's four gx (channel l % 16, rows 4 (l/16) + v) are
+// exactly the A operands of four 16x16x4 MFMAs over the rows 4 kk + v, their B operands the tile's pixels read
+// back from a per-wave LDS image of the A operands.  Per-lane sums are fp32 within a tile and fp64 across tiles
+// and in the fixed-order block reductions.
+typedef float sm4 __attribute__((ext_vector_type(4)));
+constexpr int SM_U = 4;  // tiles per wave per iteration (their gathers in flight together)
+
+__device__ __forceinline__ sm4 sm_mfma(float a, float b, sm4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+
+// the image pointer and cell of row r (r < m), as stem_pixels
+__device__ __forceinline__ const float* sm_locate(const Stem1& s, unsigned r, unsigned& p) {
+  const unsigned ra = (unsigned)s.nimg * (unsigned)s.na;
+  unsigned b;
+  if (r < ra) {
+    b = r / (unsigned)s.na;
+    p = r - b * (unsigned)s.na;
+  } else {
+    const unsigned q = r - ra;
+    b = q / (unsigned)s.nbt;
+    p = (unsigned)s.na + (q - b * (unsigned)s.nbt);
+  }
+  return s.obs + (long long)b * s.ld + s.off;
+}
+
+// gather the A operands of tile r0 (rows r0 .. r0 + 15): px[c] = pixel l/16 + 4 c of row r0 + l % 16, 0 for
+// k >= 9 and rows >= m (branch-free: the row is clamped, the value selected)
+__device__ __forceinline__ void sm_gather(const Stem1& s, const short* tab, unsigned r0, unsigned m, float px[3]) {
+  const unsigned l = threadIdx.x & 63, kq = l >> 4, r = r0 + (l & 15);
+  unsigned p;
+  const float* img = sm_locate(s, r < m ? r : m - 1, p);
+  const short* t = tab + p * 9;
+  const float v0 = img[t[kq]], v1 = img[t[kq + 4]], v2 = img[t[8]];
+  px[0] = r < m ? v0 : 0.0f;
+  px[1] = r < m ? v1 : 0.0f;
+  px[2] = (r < m && kq == 0) ? v2 : 0.0f;
+}
+__device__ __forceinline__ sm4 sm_conv(const float px[3], const float wb[3]) {
+  sm4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+  acc = sm_mfma(px[0], wb[0], acc);
+  acc = sm_mfma(px[1], wb[1], acc);
+  return sm_mfma(px[2], wb[2], acc);
+}
+// B operand of the conv: W[ch = l % 16][k = l / 16 + 4 c] (0 for k >= 9)
+__device__ __forceinline__ void sm_weights(const Stem1& s, float wb[3]) {
+  const unsigned l = threadIdx.x & 63, ch = l & 15, kq = l >> 4;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const unsigned k = kq + 4 * c;
+    wb[c] = k < 9 ? s.w[ch * 9 + k] : 0.0f;
+  }
+}
+__device__ __forceinline__ unsigned sm_wave() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// block partials of two per-lane fp64 sums over the lanes of each channel (waves in order, then l / 16 in
+// order): part[block][2][16]
+__device__ void sm_block_partials(double a0, double a1, double* part) {
+  __shared__ double red[BN_THREADS * 2];
+  red[threadIdx.x] = a0;
+  red[BN_THREADS + threadIdx.x] = a1;
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    const int q = threadIdx.x >> 4, ch = threadIdx.x & 15;
+    double acc = 0.0;
+    for (int w = 0; w < BN_THREADS / 64; ++w)
+      for (int kq = 0; kq < 4; ++kq) acc += red[q * BN_THREADS + w * 64 + kq * 16 + ch];
+    part[(size_t)blockIdx.x * 32 + threadIdx.x] = acc;
+  }
+}
+
+__global__ __launch_bounds__(BN_THREADS) void stem1m_stats_partial(Stem1 s, double* __restrict__ part,
+                                                                   float* __restrict__ shift) {
+  __shared__ short tab[STEM_MAX_CELLS * 9];
+  stem_stage_table(s, tab);
+  const unsigned m = (unsigned)s.nimg * (unsigned)(s.na + s.nbt), l = threadIdx.x & 63, ch = l & 15, kq = l >> 4;
+  float wb[3], px[SM_U][3];
+  sm_weights(s, wb);
+  sm_gather(s, tab, 0u, m, px[0]);
+  const sm4 x0 = sm_conv(px[0], wb);
+  const float sh = __shfl(x0[0], (int)ch);  // row 0, channel ch (lane ch holds row 0)
+  if (blockIdx.x == 0 && threadIdx.x < 16) shift[ch] = sh;
+  const unsigned ntiles = (m + 15) / 16, nw = gridDim.x * (BN_THREADS / 64);
+  double a0 = 0.0, a1 = 0.0;
+  for (unsigned tb = (blockIdx.x * (BN_THREADS / 64) + sm_wave()) * SM_U; tb < ntiles; tb += nw * SM_U) {
+#pragma unroll
+    for (int u = 0; u < SM_U; ++u) sm_gather(s, tab, (tb + u) * 16, m, px[u]);
+#pragma unroll
+    for (int u = 0; u < SM_U; ++u) {
+      const sm4 x = sm_conv(px[u], wb);
+      float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float d = (tb + u) * 16 + 4 * kq + v < m ? x[v] - sh : 0.0f;
+        s0 += d;
+        s1 += d * d;
+      }
+      a0 += (double)s0;
+      a1 += (double)s1;
+    }
+  }
+  sm_block_partials(a0, a1, part);
+}
+
+template <int ACT>
+__global__ __launch_bounds__(BN_THREADS) void stem1m_apply(Stem1 s, const float* __restrict__ bw, const float* __restrict__ bb,
+                                                           const float* __restrict__ stats, float slope, float* __restrict__ y) {
+  __shared__ short tab[STEM_MAX_CELLS * 9];
+  stem_stage_table(s, tab);
+  const unsigned m = (unsigned)s.nimg * (unsigned)(s.na + s.nbt), l = threadIdx.x & 63, ch = l & 15, kq = l >> 4;
+  const unsigned rows = (unsigned)s.rows_out;
+  float wb[3], px[SM_U][3];
+  sm_weights(s, wb);
+  const float mu = stats[ch], is = stats[16 + ch], wv = bw[ch], bv = bb[ch];
+  const unsigned ntiles = (rows + 15) / 16, nw = gridDim.x * (BN_THREADS / 64);  // rows past rows_out: not stored
+  for (unsigned tb = (blockIdx.x * (BN_THREADS / 64) + sm_wave()) * SM_U; tb < ntiles; tb += nw * SM_U) {
+#pragma unroll
+    for (int u = 0; u < SM_U; ++u) sm_gather(s, tab, (tb + u) * 16, m, px[u]);
+#pragma unroll
+    for (int u = 0; u < SM_U; ++u) {
+      const sm4 x = sm_conv(px[u], wb);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const unsigned r = (tb + u) * 16 + 4 * kq + v;
+        if (r < rows) y[(size_t)r * 16 + ch] = bn_act<ACT>((x[v] - mu) * is * wv + bv, slope);
+      }
+    }
+  }
+}
+
+// gy of the lane's four rows (0 past rows_out), gz = gy act'(z), xhat
+template <int ACT>
+__device__ __forceinline__ void sm_grad(const float* __restrict__ gy, unsigned r0, unsigned rows, const sm4& x, float mu,
+                                        float is, float wv, float bv, float slope, float gz[4], float xh[4]) {
+  const unsigned l = threadIdx.x & 63, ch = l & 15, kq = l >> 4;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const unsigned r = r0 + 4 * kq + v;
+    const float g = gy[(size_t)(r < rows ? r : rows - 1) * 16 + ch];
+    xh[v] = (x[v] - mu) * is;
+    gz[v] = (r < rows ? g : 0.0f) * bn_dact<ACT>(xh[v] * wv + bv, slope);
+  }
+}
+
+template <int ACT>
+__global__ __launch_bounds__(BN_THREADS) void stem1m_bwd_partial(Stem1 s, const float* __restrict__ gy,
+                                                                 const float* __restrict__ bw, const float* __restrict__ bb,
+                                                                 const float* __restrict__ stats, float slope,
+                                                                 double* __restrict__ part) {
+  __shared__ short tab[STEM_MAX_CELLS * 9];
+  stem_stage_table(s, tab);
+  const unsigned m = (unsigned)s.nimg * (unsigned)(s.na + s.nbt), l = threadIdx.x & 63, ch = l & 15;
+  const unsigned rows = (unsigned)s.rows_out;
+  float wb[3], px[SM_U][3];
+  sm_weights(s, wb);
+  const float mu = stats[ch], is = stats[16 + ch], wv = bw[ch], bv = bb[ch];
+  // rows past rows_out have gy = 0, so gz = 0: only the tiles holding stored rows contribute
+  const unsigned ntiles = (rows + 15) / 16, nw = gridDim.x * (BN_THREADS / 64);
+  double a0 = 0.0, a1 = 0.0;
+  for (unsigned tb = (blockIdx.x * (BN_THREADS / 64) + sm_wave()) * SM_U; tb < ntiles; tb += nw * SM_U) {
+#pragma unroll
+    for (int u = 0; u < SM_U; ++u) sm_gather(s, tab, (tb + u) * 16, m, px[u]);
+#pragma unroll
+    for (int u = 0; u < SM_U; ++u) {
+      const sm4 x = sm_conv(px[u], wb);
+      float gz[4], xh[4], s0 = 0.0f, s1 = 0.0f;
+      sm_grad<ACT>(gy, (tb + u) * 16, rows, x, mu, is, wv, bv, slope, gz, xh);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        s0 += gz[v];
+        s1 += gz[v] * xh[v];
+      }
+      a0 += (double)s0;
+      a1 += (double)s1;
+    }
+  }
+  sm_block_partials(a0, a1, part);
+}
+
+template <int ACT>
+__global__ __launch_bounds__(BN_THREADS) void stem1m_bwd_wgrad(Stem1 s, const float* __restrict__ gy,
+                                                               const float* __restrict__ bw, const float* __restrict__ bb,
+                                                               const float* __restrict__ stats, const float* __restrict__ sums,
+                                                               float slope, double* __restrict__ wpart) {
+  __shared__ short tab[STEM_MAX_CELLS * 9];
+  __shared__ float pimg[BN_THREADS / 64][SM_U][16][17];  // per wave: the tiles' A operands, [row][k] (+1: banks)
+  __shared__ double red[BN_THREADS * 4];
+  stem_stage_table(s, tab);
+  const unsigned m = (unsigned)s.nimg * (unsigned)(s.na + s.nbt), l = threadIdx.x & 63, ch = l & 15, kq = l >> 4;
+  const unsigned rows = (unsigned)s.rows_out, w = sm_wave();
+  float wb[3], px[SM_U][3];
+  sm_weights(s, wb);
+  const float mu = stats[ch], is = stats[16 + ch], wv = bw[ch], bv = bb[ch];
+  const float inv_m = 1.0f / (float)m;
+  const float mg = sums[ch] * inv_m, mgx = sums[16 + ch] * inv_m, isw = is * wv;
+#pragma unroll
+  for (int u = 0; u < SM_U; ++u) pimg[w][u][l & 15][12 + kq] = 0.0f;  // k = 12 .. 15: zero B operands
+  const unsigned ntiles = (m + 15) / 16, nw = gridDim.x * (BN_THREADS / 64);
+  double g[4] = {0.0, 0.0, 0.0, 0.0};
+  for (unsigned tb = (blockIdx.x * (BN_THREADS / 64) + w) * SM_U; tb < ntiles; tb += nw * SM_U) {
+#pragma unroll
+    for (int u = 0; u < SM_U; ++u) sm_gather(s, tab, (tb + u) * 16, m, px[u]);
+#pragma unroll
+    for (int u = 0; u < SM_U; ++u) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) pimg[w][u][l & 15][kq + 4 * c] = px[u][c];
+    }
+#pragma unroll
+    for (int u = 0; u < SM_U; ++u) {
+      const sm4 x = sm_conv(px[u], wb);
+      float gz[4], xh[4];
+      sm_grad<ACT>(gy, (tb + u) * 16, rows, x, mu, is, wv, bv, slope, gz, xh);
+      sm4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        // rows >= m: their pixels (the B operand) are 0
+        const float gx = (gz[v] - mg - xh[v] * mgx) * isw;
+        acc = sm_mfma(gx, pimg[w][u][4 * kq + v][ch], acc);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) g[q] += (double)acc[q];
+    }
+  }
+  // lane l holds G[channel 4 (l / 16) + q][k = l % 16]; per (channel, k) the waves' values in order
+#pragma unroll
+  for (int q = 0; q < 4; ++q) red[q * BN_THREADS + threadIdx.x] = g[q];
+  __syncthreads();
+  for (int v = threadIdx.x; v < 16 * 9; v += BN_THREADS) {
+    const int c2 = v / 9, k = v % 9, lane = (c2 >> 2) * 16 + k, q = c2 & 3;
+    double t = 0.0;
+    for (int ww = 0; ww < BN_THREADS / 64; ++ww) t += red[q * BN_THREADS + ww * 64 + lane];
+    wpart[(size_t)blockIdx.x * 144 + v] = t;
+  }
+}
+
 static int stem_blocks(const Stem1& s) { return bn_blocks((long long)s.nimg * (s.na + s.nbt), s.c); }
 
 // workspace (doubles): BN partials [nb][2c] | shift + sums (2c floats, as c doubles) | wgrad partials [nb][9c]
@@ -447,6 +688,15 @@ hipError_t launch_stem1_forward(const Stem1& s, const float* bw, const float* bb
   const int nb = stem_blocks(s);
   float* shift = reinterpret_cast<float*>(part + (size_t)nb * 2 * s.c);
   const long long m = (long long)s.nimg * (s.na + s.nbt);
+  if (s.c == 16) {  // the reference's stem: the MFMA kernels
+    hipLaunchKernelGGL(stem1m_stats_partial, dim3(nb), dim3(BN_THREADS), 0, st, s, part, shift);
+    hipLaunchKernelGGL(bn_stats_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, shift, m, s.c, nb, eps, part, stats);
+    if (act == GR_POLICY_ACT_ELU)
+      hipLaunchKernelGGL(stem1m_apply<GR_POLICY_ACT_ELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, bw, bb, stats, slope, y);
+    else
+      hipLaunchKernelGGL(stem1m_apply<GR_POLICY_ACT_LRELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, bw, bb, stats, slope, y);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(stem1_stats_partial, dim3(nb), dim3(BN_THREADS), 0, st, s, part, shift);
   hipLaunchKernelGGL(bn_stats_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, shift, m, s.c, nb, eps, part, stats);
   if (act == GR_POLICY_ACT_ELU)
@@ -462,6 +712,19 @@ hipError_t launch_stem1_backward(const Stem1& s, const float* bw, const float* b
   const int nb = stem_blocks(s);
   float* sums = reinterpret_cast<float*>(part + (size_t)nb * 2 * s.c);
   double* wpart = part + (size_t)nb * 2 * s.c + 2 * s.c;
+  if (s.c == 16) {
+    if (act == GR_POLICY_ACT_ELU)
+      hipLaunchKernelGGL(stem1m_bwd_partial<GR_POLICY_ACT_ELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, gy, bw, bb, stats, slope, part);
+    else
+      hipLaunchKernelGGL(stem1m_bwd_partial<GR_POLICY_ACT_LRELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, gy, bw, bb, stats, slope, part);
+    hipLaunchKernelGGL(bn_bwd_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, s.c, nb, part, gbw, gbb, sums);
+    if (act == GR_POLICY_ACT_ELU)
+      hipLaunchKernelGGL(stem1m_bwd_wgrad<GR_POLICY_ACT_ELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, gy, bw, bb, stats, sums, slope, wpart);
+    else
+      hipLaunchKernelGGL(stem1m_bwd_wgrad<GR_POLICY_ACT_LRELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, gy, bw, bb, stats, sums, slope, wpart);
+    hipLaunchKernelGGL(stem1_wgrad_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, 9 * s.c, nb, wpart, gconv);
+    return hipGetLastError();
+  }
   if (act == GR_POLICY_ACT_ELU)
     hipLaunchKernelGGL(stem1_bwd_partial<GR_POLICY_ACT_ELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, gy, bw, bb, stats, slope, part);
   else
