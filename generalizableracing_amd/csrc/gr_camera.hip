@@ -82,7 +82,8 @@ DEV_INLINE void reuse_rows(const CamArgs& a, const gr_cam_const* __restrict__ cc
   }
 }
 
-// obstacle slot from LDS (GR_CAM_OSLOT floats: frame and primitive = slot floats 0-15, window = 17-20)
+// obstacle slot from LDS (GR_CAM_OSLOT floats: frame and primitive = slot floats 0-15, window = 17-20, then the
+// hit constants of gr_cam_obst_prep)
 DEV_INLINE void load_oslot(const float4* src, float s[GR_CAM_SLOT]) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -91,6 +92,13 @@ DEV_INLINE void load_oslot(const float4* src, float s[GR_CAM_SLOT]) {
   }
   const float4 w4 = src[4];
   s[GR_CS_AMIN] = w4.x; s[GR_CS_AMAX] = w4.y; s[GR_CS_BMIN] = w4.z; s[GR_CS_BMAX] = w4.w;
+}
+DEV_INLINE void load_oconst(const float4* src, float k[GR_OK_N]) {
+#pragma unroll
+  for (int j = 0; j < GR_OK_N / 4; ++j) {
+    const float4 q4 = src[5 + j];
+    k[4 * j] = q4.x; k[4 * j + 1] = q4.y; k[4 * j + 2] = q4.z; k[4 * j + 3] = q4.w;
+  }
 }
 
 // the obstacle's record from global memory
@@ -146,7 +154,7 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
   float4* s_slot = reinterpret_cast<float4*>(wave_lds);                               // [G][CAM_SLOT4]
   uint64_t* s_gmask = reinterpret_cast<uint64_t*>(wave_lds + G * GR_CAM_SLOT);        // [tiles]
   float* olds = wave_lds + G * GR_CAM_SLOT + tmf;
-  float4* s_oslot = reinterpret_cast<float4*>(olds);                                  // [64][GR_CAM_OSLOT / 4]
+  float4* s_oslot = reinterpret_cast<float4*>(olds);                                  // [GR_CAM_OBST_SLOTS][GR_CAM_OSLOT / 4]
   uint64_t* s_tmask = reinterpret_cast<uint64_t*>(olds + GR_CAM_OBST_SLOTS * GR_CAM_OSLOT);  // [tiles]
   float4* s_stage = reinterpret_cast<float4*>(olds + oslots);                         // [8 * W / 4]
 
@@ -219,6 +227,11 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
           for (int q = 0; q < 4; ++q)
             s_oslot[pos * (GR_CAM_OSLOT / 4) + q] = make_float4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
           s_oslot[pos * (GR_CAM_OSLOT / 4) + 4] = make_float4(s[GR_CS_AMIN], s[GR_CS_AMAX], s[GR_CS_BMIN], s[GR_CS_BMAX]);
+          float kc[GR_OK_N];
+          gr_cam_obst_prep(s, kc);
+#pragma unroll
+          for (int q = 0; q < GR_OK_N / 4; ++q)
+            s_oslot[pos * (GR_CAM_OSLOT / 4) + 5 + q] = make_float4(kc[4 * q], kc[4 * q + 1], kc[4 * q + 2], kc[4 * q + 3]);
         }
         const int nb = __popcll(b);
         if (nv + nb > GR_CAM_OBST_SLOTS && ofrom == nob) {
@@ -354,15 +367,16 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
           if (cm == 0u || rm == 0u) continue;
           const int cu = u_t + __builtin_ctz(cm), wc = __popc(cm), rv = __builtin_ctz(rm), area = wc * __popc(rm);
           const float inv_wc = 1.0f / (float)wc;
-          float s[GR_CAM_SLOT];
+          float s[GR_CAM_SLOT], kc[GR_OK_N];
           load_oslot(s_oslot + k * (GR_CAM_OSLOT / 4), s);
+          load_oconst(s_oslot + k * (GR_CAM_OSLOT / 4), kc);
           for (int base = 0; base < area; base += 64) {
             const int idx = base + lane;
             if (idx < area) {
               // idx / wc exactly for idx < 256, wc <= 32 (the fraction of a non-integer quotient is <= 31/32)
               const int r = (int)((float)idx * inv_wc + 1.0e-3f), c = idx - r * wc;
               const int u = cu + c, pix = (rv + r) * W + u;
-              const float h = gr_cam_clip(gr_cam_obst_hit(s, s_ray_a[u], s_ray_b[v0 + rv + r]), maxd);
+              const float h = gr_cam_clip(gr_cam_obst_hit_k(s, kc, s_ray_a[u], s_ray_b[v0 + rv + r]), maxd);
               st[pix] = gr_minf(st[pix], h);
             }
           }

@@ -163,90 +163,134 @@ GR_HD int gr_cam_obst_outside(const float* s, float a_lo, float a_hi, float b_lo
   return gr_cam_box_outside(s, l, a_lo, a_hi, b_lo, b_hi);
 }
 
-/* first crossing (s > 0) of the ray o + s d with the slab |x_j| <= h_j intersected with
- * the interval [t0, t1]; GR_CAM_FAR-style miss = 3e38 */
-GR_HD float gr_obst_first(float tin, float tout) {
-  if (!(tin <= tout) || !(tout > 0.0f)) return 3.0e38f;
-  return tin > 0.0f ? tin : tout;
-}
-
 GR_HD float gr_obst_inv(float d) { return 1.0f / (gr_fabsf(d) < 1.0e-20f ? gr_copysignf(1.0e-20f, d) : d); }
 
-/* entry / exit of the sphere |x - (0,0,zc)| <= rad along o + s d (tin > tout: miss) */
-GR_HD void gr_obst_sphere_iv(const float o[3], const float d[3], float zc, float rad, float* tin, float* tout) {
-  const float oz = o[2] - zc;
-  const float A = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
-  const float Bh = (o[0] * d[0] + o[1] * d[1]) + oz * d[2];
-  const float Cc = ((o[0] * o[0] + o[1] * o[1]) + oz * oz) - rad * rad;
-  const float disc = Bh * Bh - A * Cc;
-  if (!(disc >= 0.0f)) {
-    *tin = 1.0f;
-    *tout = -1.0f;
-    return;
+/* ---- the per-pixel hit in inverse depth.  Along pixel ray (a, b) the direction in the primitive frame, d, is
+ * affine in (a, b), and the depth of the crossing with a plane x_j = p is s = (p - o_j) / d_j: its reciprocal
+ * u = d_j / (p - o_j) is d_j times a per-slot constant.  The slab tests therefore run on u (for s > 0 the order
+ * reverses: the latest entry is the smallest u, the earliest exit the largest), and so do the quadratics, whose
+ * roots satisfy s1 s2 = Cc / A (Vieta): u = (-Bh -/+ sq) / Cc, Cc = |o|^2 - r^2 a per-slot constant.  A hit
+ * costs one division, 1 / u of the first crossing, instead of one per slab or root (three for a box, up to
+ * five for a capsule).  The constants (gr_cam_obst_prep) come with the slot; gr_cam_obst_hit derives them
+ * itself. */
+#define GR_OK_N 12          /* floats of the per-slot constants */
+#define GR_U_NONE 3.0e38f   /* "no entry bound" (the camera is inside that slab / sphere) */
+
+/* slab |x| <= e seen from o: entry / exit constants (1 / (plane - o)); inside: o strictly between the planes */
+GR_HD void gr_obst_slab_prep(float o, float e, float* cE, float* cX, int* inside) {
+  const float lo = -e - o, hi = e - o;
+  *inside = lo < 0.0f && hi > 0.0f;
+  if (hi <= 0.0f) { /* beyond +e: entered through +e, left through -e */
+    *cE = gr_obst_inv(hi);
+    *cX = gr_obst_inv(lo);
+  } else { /* below -e (entered through -e), or inside */
+    *cE = gr_obst_inv(lo);
+    *cX = gr_obst_inv(hi);
   }
-  const float sq = gr_sqrtf(disc);
-  *tin = (-Bh - sq) / A;
-  *tout = (-Bh + sq) / A;
 }
 
-/* entry / exit of the finite cylinder x^2 + y^2 <= rad^2, |z| <= hh */
-GR_HD void gr_obst_cyl_iv(const float o[3], const float d[3], float rad, float hh, float* tin, float* tout) {
-  const float iz = gr_obst_inv(d[2]);
-  const float z0 = (-hh - o[2]) * iz, z1 = (hh - o[2]) * iz;
-  float lo = gr_minf(z0, z1), hi = gr_maxf(z0, z1);
-  const float A = d[0] * d[0] + d[1] * d[1];
-  const float Bh = o[0] * d[0] + o[1] * d[1];
-  const float Cc = (o[0] * o[0] + o[1] * o[1]) - rad * rad;
-  if (A < 1.0e-12f) {
-    /* parallel to the axis: inside the radius everywhere or nowhere */
-    if (!(Cc <= 0.0f)) hi = lo - 1.0f;
-  } else {
-    const float disc = Bh * Bh - A * Cc;
-    if (!(disc >= 0.0f)) {
-      hi = lo - 1.0f;
-    } else {
-      const float sq = gr_sqrtf(disc);
-      lo = gr_maxf(lo, (-Bh - sq) / A);
-      hi = gr_minf(hi, (-Bh + sq) / A);
-    }
-  }
-  *tin = lo;
-  *tout = hi;
-}
-
-/* first surface crossing (s > 0) of the pixel ray (a, b) with the obstacle of slot s:
- * from outside the entry, from inside the exit (a mesh ray cast reports the first face
- * it crosses).  The capsule is the union of its cylinder and two end spheres: the
- * nearest of their crossings. */
-GR_HD float gr_cam_obst_hit(const float* s, float a, float b) {
-  const float d[3] = {gr_fmaf(b, s[9], gr_fmaf(a, s[6], s[3])), gr_fmaf(b, s[10], gr_fmaf(a, s[7], s[4])),
-                      gr_fmaf(b, s[11], gr_fmaf(a, s[8], s[5]))};
-  const float o[3] = {s[0], s[1], s[2]};
+/* k[0..2] slab entry constants (x, y, z), k[4..6] exit constants, k[3] bit mask as a float: bits 0-2 the camera
+ * inside slab x / y / z, bit 3 inside the radius (cylinder, capsule) or sphere, bits 4 / 5 inside the capsule's
+ * top / bottom sphere; k[8], k[9] Cc and 1 / Cc of the radial / sphere quadratic; a capsule's top / bottom
+ * sphere keeps its Cc, 1 / Cc in k[0], k[1] / k[4], k[5] (it has no x / y slabs) */
+GR_HD void gr_cam_obst_prep(const float* s, float* k) {
   const int kind = (int)s[GR_OS_KIND];
   const float e0 = s[GR_OS_E0], e1 = s[GR_OS_E1], e2 = s[GR_OS_E2];
-  float tin, tout;
+  const float ox = s[0], oy = s[1], oz = s[2];
+  int m = 0, in = 0;
+  for (int i = 0; i < GR_OK_N; ++i) k[i] = 0.0f;
   if (kind == GR_OBST_BOX) {
-    const float ix = gr_obst_inv(d[0]), iy = gr_obst_inv(d[1]), iz = gr_obst_inv(d[2]);
-    const float tx0 = (-e0 - o[0]) * ix, tx1 = (e0 - o[0]) * ix;
-    const float ty0 = (-e1 - o[1]) * iy, ty1 = (e1 - o[1]) * iy;
-    const float tz0 = (-e2 - o[2]) * iz, tz1 = (e2 - o[2]) * iz;
-    tin = gr_maxf(gr_maxf(gr_minf(tx0, tx1), gr_minf(ty0, ty1)), gr_minf(tz0, tz1));
-    tout = gr_minf(gr_minf(gr_maxf(tx0, tx1), gr_maxf(ty0, ty1)), gr_maxf(tz0, tz1));
-    return gr_obst_first(tin, tout);
+    gr_obst_slab_prep(ox, e0, &k[0], &k[4], &in);
+    m |= in;
+    gr_obst_slab_prep(oy, e1, &k[1], &k[5], &in);
+    m |= in << 1;
   }
-  if (kind == GR_OBST_SPHERE) {
-    gr_obst_sphere_iv(o, d, 0.0f, e0, &tin, &tout);
-    return gr_obst_first(tin, tout);
+  if (kind != GR_OBST_SPHERE) {
+    gr_obst_slab_prep(oz, e2, &k[2], &k[6], &in);
+    m |= in << 2;
   }
-  gr_obst_cyl_iv(o, d, e0, e2, &tin, &tout);
-  float hit = gr_obst_first(tin, tout);
+  if (kind != GR_OBST_BOX) {
+    const float cc = kind == GR_OBST_SPHERE ? ((ox * ox + oy * oy) + oz * oz) - e0 * e0 : (ox * ox + oy * oy) - e0 * e0;
+    k[8] = cc;
+    k[9] = gr_obst_inv(cc);
+    m |= (cc < 0.0f) << 3;
+  }
   if (kind == GR_OBST_CAPSULE) {
-    gr_obst_sphere_iv(o, d, e2, e0, &tin, &tout);
-    hit = gr_minf(hit, gr_obst_first(tin, tout));
-    gr_obst_sphere_iv(o, d, -e2, e0, &tin, &tout);
-    hit = gr_minf(hit, gr_obst_first(tin, tout));
+    const float zt = oz - e2, zb = oz - (-e2);
+    const float ct = ((ox * ox + oy * oy) + zt * zt) - e0 * e0, cb = ((ox * ox + oy * oy) + zb * zb) - e0 * e0;
+    k[0] = ct;
+    k[1] = gr_obst_inv(ct);
+    k[4] = cb;
+    k[5] = gr_obst_inv(cb);
+    m |= (ct < 0.0f) << 4;
+    m |= (cb < 0.0f) << 5;
   }
-  return hit;
+  k[3] = (float)m;
+}
+
+/* one slab along the ray: the entry bound (outside only) and the exit */
+GR_HD void gr_u_slab(float d, float cE, float cX, int inside, float* uin, float* uout) {
+  const float p = d * cE, q = d * cX;
+  if (inside) {
+    *uout = gr_maxf(*uout, gr_maxf(p, q));
+  } else {
+    *uin = gr_minf(*uin, p);
+    *uout = gr_maxf(*uout, q);
+  }
+}
+/* the quadratic A s^2 + 2 Bh s + Cc = 0 (a sphere or the infinite cylinder): 0 if the ray misses it */
+GR_HD int gr_u_quad(float A, float Bh, float cc, float icc, int inside, float* uin, float* uout) {
+  const float disc = Bh * Bh - A * cc;
+  if (!(disc >= 0.0f)) return 0;
+  const float sq = gr_sqrtf(disc);
+  const float ux = (-Bh - sq) * icc;
+  if (!inside) *uin = gr_minf(*uin, (-Bh + sq) * icc);
+  *uout = gr_maxf(*uout, ux);
+  return 1;
+}
+/* u of the first crossing with s > 0 (0: none): the entry, or from inside every part the exit */
+GR_HD float gr_u_first(float uin, float uout) {
+  if (uin >= GR_U_NONE) return uout > 0.0f ? uout : 0.0f;
+  return (uin > 0.0f && uin >= uout) ? uin : 0.0f;
+}
+
+/* first surface crossing (s > 0) of the pixel ray (a, b) with the obstacle of slot s (constants k): from
+ * outside the entry, from inside the exit (a mesh ray cast reports the first face it crosses).  The capsule is
+ * the union of its cylinder and two end spheres: the nearest of their crossings (the largest u). */
+GR_HD float gr_cam_obst_hit_k(const float* s, const float* k, float a, float b) {
+  const float d0 = gr_fmaf(b, s[9], gr_fmaf(a, s[6], s[3])), d1 = gr_fmaf(b, s[10], gr_fmaf(a, s[7], s[4])),
+              d2 = gr_fmaf(b, s[11], gr_fmaf(a, s[8], s[5]));
+  const float ox = s[0], oy = s[1], oz = s[2];
+  const int kind = (int)s[GR_OS_KIND], m = (int)k[3];
+  float uin = GR_U_NONE, uout = 0.0f, u = 0.0f;
+  if (kind == GR_OBST_BOX) {
+    gr_u_slab(d0, k[0], k[4], m & 1, &uin, &uout);
+    gr_u_slab(d1, k[1], k[5], m & 2, &uin, &uout);
+    gr_u_slab(d2, k[2], k[6], m & 4, &uin, &uout);
+    u = gr_u_first(uin, uout);
+  } else if (kind == GR_OBST_SPHERE) {
+    const float A = (d0 * d0 + d1 * d1) + d2 * d2, Bh = (ox * d0 + oy * d1) + oz * d2;
+    if (gr_u_quad(A, Bh, k[8], k[9], m & 8, &uin, &uout)) u = gr_u_first(uin, uout);
+  } else {
+    const float A = d0 * d0 + d1 * d1, Bh = ox * d0 + oy * d1;
+    gr_u_slab(d2, k[2], k[6], m & 4, &uin, &uout);
+    if (gr_u_quad(A, Bh, k[8], k[9], m & 8, &uin, &uout)) u = gr_u_first(uin, uout);
+    if (kind == GR_OBST_CAPSULE) {
+      const float e2 = s[GR_OS_E2], A3 = A + d2 * d2;
+      float ui = GR_U_NONE, uo = 0.0f;
+      if (gr_u_quad(A3, Bh + (oz - e2) * d2, k[0], k[1], m & 16, &ui, &uo)) u = gr_maxf(u, gr_u_first(ui, uo));
+      ui = GR_U_NONE;
+      uo = 0.0f;
+      if (gr_u_quad(A3, Bh + (oz - (-e2)) * d2, k[4], k[5], m & 32, &ui, &uo)) u = gr_maxf(u, gr_u_first(ui, uo));
+    }
+  }
+  return u > 0.0f ? 1.0f / u : 3.0e38f;
+}
+
+GR_HD float gr_cam_obst_hit(const float* s, float a, float b) {
+  float k[GR_OK_N];
+  gr_cam_obst_prep(s, k);
+  return gr_cam_obst_hit_k(s, k, a, b);
 }
 
 #endif /* GR_OBSTACLES_H */
