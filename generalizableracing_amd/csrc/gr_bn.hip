@@ -436,243 +436,237 @@ __global__ __launch_bounds__(BN_FINAL_THREADS) void stem1_wgrad_final(int n, int
 
 // ------------------------------------------------------------- the first block on fp32 MFMA (C = 16)
 // The per-row kernels above spend four threads per row (one per 4 channels), each re-deriving the row's image
-// and cell and gathering the same 9 pixels, plus 36 VALU FMAs; the four passes were VALU-bound at 1.7-2.4x their
-// HBM floors (profiles/round03_vision_update_kernel_stats.csv).  Here a wave takes 16 rows at a time and the conv
-// is three v_mfma_f32_16x16x4f32 (K = 9 padded to 12): lane l gathers pixels k = l/16, l/16 + 4 (and 8 for
-// l < 16) of row l % 16 — the A operand — against the weights W[l % 16][k] held as the B operand, and receives
-// x[row 4 (l/16) + v][channel l % 16], v = 0..3.  The MFMA is a k-ordered fmaf chain from 0 (padding adds exact
-// zeros), so every x is bit-identical to stem_conv's.  The conv weight's gradient is a second product on the same
-// tile, G[ch][k] += sum_rows gx[row][ch] px[row][k]: the lane's four gx (channel l % 16, rows 4 (l/16) + v) are
-// exactly the A operands of four 16x16x4 MFMAs over the rows 4 kk + v, their B operands the tile's pixels read
-// back from a per-wave LDS image of the A operands.  Per-lane sums are fp32 within a tile and fp64 across tiles
-// and in the fixed-order block reductions.
+// and cell and gathering the same 9 pixels from global memory, plus 36 VALU FMAs; the four passes ran at
+// 1.7-2.4x their HBM floors (profiles/round03_vision_update_kernel_stats.csv).  Here a workgroup takes whole
+// images: it stages the image (27.6 KB at 72 x 96) in LDS with coalesced loads, and its four waves take the
+// image's rows 16 at a time (tiles of table a, then of table b; every tile lies within one image and one table).
+// The conv is three v_mfma_f32_16x16x4f32 (K = 9 padded to 12): lane l gathers pixels k = l/16, l/16 + 4 (and 8
+// for l < 16) of row l % 16 from the LDS image — the A operand — against the weights W[l % 16][k] held as the B
+// operand, and receives x[row 4 (l/16) + v][channel l % 16], v = 0..3.  The MFMA is a k-ordered fmaf chain from 0
+// (padding adds exact zeros), so every x is bit-identical to stem_conv's.  The conv weight's gradient is a second
+// product on the same tile, G[ch][k] += sum_rows gx[row][ch] px[row][k]: the lane's four gx (channel l % 16, rows
+// 4 (l/16) + v) are exactly the A operands of four 16x16x4 MFMAs over the rows 4 kk + v, their B operands the
+// tile's pixels read back from a per-wave LDS copy of the A operands.  Per-lane sums are fp32 within a tile and
+// fp64 across tiles and in the fixed-order block reductions.  A pixel table reaching beyond SM_IMG_CAP floats
+// (or beyond the row: ld - off) gathers from global memory instead (the same arithmetic).
 typedef float sm4 __attribute__((ext_vector_type(4)));
-constexpr int SM_U = 4;  // tiles per wave per iteration (their gathers in flight together)
+constexpr int SM_IMG_CAP = 8192;  // image floats staged in LDS per workgroup
+constexpr int SM_GRID = 768;      // workgroups: three per CU (LDS ~46 KB each), images strided over them
+enum { SM_STATS = 0, SM_APPLY = 1, SM_BWDP = 2, SM_WGRAD = 3 };
+
+struct SmArgs {
+  const float* bw;     // BN weight / bias
+  const float* bb;
+  const float* stats;  // [4][16] (mean, invstd, ...)
+  const float* sums;   // [2][16] sum gz, sum gz xhat (SM_WGRAD)
+  const float* gy;     // [rows_out][16]
+  float* y;            // [rows_out][16] (SM_APPLY)
+  double* part;        // block partials
+  float* shift;        // [16] (SM_STATS)
+  float slope;
+};
 
 __device__ __forceinline__ sm4 sm_mfma(float a, float b, sm4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
-
-// the image pointer and cell of row r (r < m), as stem_pixels
-__device__ __forceinline__ const float* sm_locate(const Stem1& s, unsigned r, unsigned& p) {
-  const unsigned ra = (unsigned)s.nimg * (unsigned)s.na;
-  unsigned b;
-  if (r < ra) {
-    b = r / (unsigned)s.na;
-    p = r - b * (unsigned)s.na;
-  } else {
-    const unsigned q = r - ra;
-    b = q / (unsigned)s.nbt;
-    p = (unsigned)s.na + (q - b * (unsigned)s.nbt);
-  }
-  return s.obs + (long long)b * s.ld + s.off;
-}
-
-// gather the A operands of tile r0 (rows r0 .. r0 + 15): px[c] = pixel l/16 + 4 c of row r0 + l % 16, 0 for
-// k >= 9 and rows >= m (branch-free: the row is clamped, the value selected)
-__device__ __forceinline__ void sm_gather(const Stem1& s, const short* tab, unsigned r0, unsigned m, float px[3]) {
-  const unsigned l = threadIdx.x & 63, kq = l >> 4, r = r0 + (l & 15);
-  unsigned p;
-  const float* img = sm_locate(s, r < m ? r : m - 1, p);
-  const short* t = tab + p * 9;
-  const float v0 = img[t[kq]], v1 = img[t[kq + 4]], v2 = img[t[8]];
-  px[0] = r < m ? v0 : 0.0f;
-  px[1] = r < m ? v1 : 0.0f;
-  px[2] = (r < m && kq == 0) ? v2 : 0.0f;
-}
 __device__ __forceinline__ sm4 sm_conv(const float px[3], const float wb[3]) {
   sm4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
   acc = sm_mfma(px[0], wb[0], acc);
   acc = sm_mfma(px[1], wb[1], acc);
   return sm_mfma(px[2], wb[2], acc);
 }
-// B operand of the conv: W[ch = l % 16][k = l / 16 + 4 c] (0 for k >= 9)
-__device__ __forceinline__ void sm_weights(const Stem1& s, float wb[3]) {
-  const unsigned l = threadIdx.x & 63, ch = l & 15, kq = l >> 4;
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const unsigned k = kq + 4 * c;
-    wb[c] = k < 9 ? s.w[ch * 9 + k] : 0.0f;
-  }
-}
 __device__ __forceinline__ unsigned sm_wave() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
-// block partials of two per-lane fp64 sums over the lanes of each channel (waves in order, then l / 16 in
-// order): part[block][2][16]
-__device__ void sm_block_partials(double a0, double a1, double* part) {
-  __shared__ double red[BN_THREADS * 2];
-  red[threadIdx.x] = a0;
-  red[BN_THREADS + threadIdx.x] = a1;
+// dynamic LDS: the pixel table (int16, padded to 16 B), then the image (max(cap, 2048) floats: the block
+// reductions reuse it at the end, 4 x 256 doubles)
+__host__ __device__ inline size_t sm_tab_floats(int ncell) { return (size_t)((ncell * 9 + 7) & ~7) / 2; }
+__host__ __device__ inline size_t sm_lds_bytes(int ncell, int cap) {
+  return 4 * (sm_tab_floats(ncell) + (size_t)(cap > 2048 ? cap : 2048));
+}
+
+template <int PASS, int ACT>
+__global__ __launch_bounds__(BN_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, int cap) {
+  extern __shared__ float4 sm_dyn4[];
+  __shared__ int s_span;
+  __shared__ float pimg[BN_THREADS / 64][16][17];  // SM_WGRAD: per wave, the tile's A operands [row][k] (+1: banks)
+  const int na = s.na, nbt = s.nbt, ncell = na + nbt;
+  short* tab = reinterpret_cast<short*>(sm_dyn4);
+  float* im = reinterpret_cast<float*>(sm_dyn4) + sm_tab_floats(ncell);
+  const unsigned l = threadIdx.x & 63, ch = l & 15, kq = l >> 4, w = sm_wave();
+  if (threadIdx.x == 0) s_span = 0;
   __syncthreads();
-  if (threadIdx.x < 32) {
-    const int q = threadIdx.x >> 4, ch = threadIdx.x & 15;
-    double acc = 0.0;
-    for (int w = 0; w < BN_THREADS / 64; ++w)
-      for (int kq = 0; kq < 4; ++kq) acc += red[q * BN_THREADS + w * 64 + kq * 16 + ch];
-    part[(size_t)blockIdx.x * 32 + threadIdx.x] = acc;
+  int mx = 0;
+  for (int i = threadIdx.x; i < ncell * 9; i += BN_THREADS) {
+    const short t = s.pix[i];
+    tab[i] = t;
+    mx = mx > (int)t + 1 ? mx : (int)t + 1;
   }
-}
-
-__global__ __launch_bounds__(BN_THREADS) void stem1m_stats_partial(Stem1 s, double* __restrict__ part,
-                                                                   float* __restrict__ shift) {
-  __shared__ short tab[STEM_MAX_CELLS * 9];
-  stem_stage_table(s, tab);
-  const unsigned m = (unsigned)s.nimg * (unsigned)(s.na + s.nbt), l = threadIdx.x & 63, ch = l & 15, kq = l >> 4;
-  float wb[3], px[SM_U][3];
-  sm_weights(s, wb);
-  sm_gather(s, tab, 0u, m, px[0]);
-  const sm4 x0 = sm_conv(px[0], wb);
-  const float sh = __shfl(x0[0], (int)ch);  // row 0, channel ch (lane ch holds row 0)
-  if (blockIdx.x == 0 && threadIdx.x < 16) shift[ch] = sh;
-  const unsigned ntiles = (m + 15) / 16, nw = gridDim.x * (BN_THREADS / 64);
-  double a0 = 0.0, a1 = 0.0;
-  for (unsigned tb = (blockIdx.x * (BN_THREADS / 64) + sm_wave()) * SM_U; tb < ntiles; tb += nw * SM_U) {
-#pragma unroll
-    for (int u = 0; u < SM_U; ++u) sm_gather(s, tab, (tb + u) * 16, m, px[u]);
-#pragma unroll
-    for (int u = 0; u < SM_U; ++u) {
-      const sm4 x = sm_conv(px[u], wb);
-      float s0 = 0.0f, s1 = 0.0f;
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const float d = (tb + u) * 16 + 4 * kq + v < m ? x[v] - sh : 0.0f;
-        s0 += d;
-        s1 += d * d;
-      }
-      a0 += (double)s0;
-      a1 += (double)s1;
-    }
-  }
-  sm_block_partials(a0, a1, part);
-}
-
-template <int ACT>
-__global__ __launch_bounds__(BN_THREADS) void stem1m_apply(Stem1 s, const float* __restrict__ bw, const float* __restrict__ bb,
-                                                           const float* __restrict__ stats, float slope, float* __restrict__ y) {
-  __shared__ short tab[STEM_MAX_CELLS * 9];
-  stem_stage_table(s, tab);
-  const unsigned m = (unsigned)s.nimg * (unsigned)(s.na + s.nbt), l = threadIdx.x & 63, ch = l & 15, kq = l >> 4;
-  const unsigned rows = (unsigned)s.rows_out;
-  float wb[3], px[SM_U][3];
-  sm_weights(s, wb);
-  const float mu = stats[ch], is = stats[16 + ch], wv = bw[ch], bv = bb[ch];
-  const unsigned ntiles = (rows + 15) / 16, nw = gridDim.x * (BN_THREADS / 64);  // rows past rows_out: not stored
-  for (unsigned tb = (blockIdx.x * (BN_THREADS / 64) + sm_wave()) * SM_U; tb < ntiles; tb += nw * SM_U) {
-#pragma unroll
-    for (int u = 0; u < SM_U; ++u) sm_gather(s, tab, (tb + u) * 16, m, px[u]);
-#pragma unroll
-    for (int u = 0; u < SM_U; ++u) {
-      const sm4 x = sm_conv(px[u], wb);
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const unsigned r = (tb + u) * 16 + 4 * kq + v;
-        if (r < rows) y[(size_t)r * 16 + ch] = bn_act<ACT>((x[v] - mu) * is * wv + bv, slope);
-      }
-    }
-  }
-}
-
-// gy of the lane's four rows (0 past rows_out), gz = gy act'(z), xhat
-template <int ACT>
-__device__ __forceinline__ void sm_grad(const float* __restrict__ gy, unsigned r0, unsigned rows, const sm4& x, float mu,
-                                        float is, float wv, float bv, float slope, float gz[4], float xh[4]) {
-  const unsigned l = threadIdx.x & 63, ch = l & 15, kq = l >> 4;
-#pragma unroll
-  for (int v = 0; v < 4; ++v) {
-    const unsigned r = r0 + 4 * kq + v;
-    const float g = gy[(size_t)(r < rows ? r : rows - 1) * 16 + ch];
-    xh[v] = (x[v] - mu) * is;
-    gz[v] = (r < rows ? g : 0.0f) * bn_dact<ACT>(xh[v] * wv + bv, slope);
-  }
-}
-
-template <int ACT>
-__global__ __launch_bounds__(BN_THREADS) void stem1m_bwd_partial(Stem1 s, const float* __restrict__ gy,
-                                                                 const float* __restrict__ bw, const float* __restrict__ bb,
-                                                                 const float* __restrict__ stats, float slope,
-                                                                 double* __restrict__ part) {
-  __shared__ short tab[STEM_MAX_CELLS * 9];
-  stem_stage_table(s, tab);
-  const unsigned m = (unsigned)s.nimg * (unsigned)(s.na + s.nbt), l = threadIdx.x & 63, ch = l & 15;
-  const unsigned rows = (unsigned)s.rows_out;
-  float wb[3], px[SM_U][3];
-  sm_weights(s, wb);
-  const float mu = stats[ch], is = stats[16 + ch], wv = bw[ch], bv = bb[ch];
-  // rows past rows_out have gy = 0, so gz = 0: only the tiles holding stored rows contribute
-  const unsigned ntiles = (rows + 15) / 16, nw = gridDim.x * (BN_THREADS / 64);
-  double a0 = 0.0, a1 = 0.0;
-  for (unsigned tb = (blockIdx.x * (BN_THREADS / 64) + sm_wave()) * SM_U; tb < ntiles; tb += nw * SM_U) {
-#pragma unroll
-    for (int u = 0; u < SM_U; ++u) sm_gather(s, tab, (tb + u) * 16, m, px[u]);
-#pragma unroll
-    for (int u = 0; u < SM_U; ++u) {
-      const sm4 x = sm_conv(px[u], wb);
-      float gz[4], xh[4], s0 = 0.0f, s1 = 0.0f;
-      sm_grad<ACT>(gy, (tb + u) * 16, rows, x, mu, is, wv, bv, slope, gz, xh);
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        s0 += gz[v];
-        s1 += gz[v] * xh[v];
-      }
-      a0 += (double)s0;
-      a1 += (double)s1;
-    }
-  }
-  sm_block_partials(a0, a1, part);
-}
-
-template <int ACT>
-__global__ __launch_bounds__(BN_THREADS) void stem1m_bwd_wgrad(Stem1 s, const float* __restrict__ gy,
-                                                               const float* __restrict__ bw, const float* __restrict__ bb,
-                                                               const float* __restrict__ stats, const float* __restrict__ sums,
-                                                               float slope, double* __restrict__ wpart) {
-  __shared__ short tab[STEM_MAX_CELLS * 9];
-  __shared__ float pimg[BN_THREADS / 64][SM_U][16][17];  // per wave: the tiles' A operands, [row][k] (+1: banks)
-  __shared__ double red[BN_THREADS * 4];
-  stem_stage_table(s, tab);
-  const unsigned m = (unsigned)s.nimg * (unsigned)(s.na + s.nbt), l = threadIdx.x & 63, ch = l & 15, kq = l >> 4;
-  const unsigned rows = (unsigned)s.rows_out, w = sm_wave();
-  float wb[3], px[SM_U][3];
-  sm_weights(s, wb);
-  const float mu = stats[ch], is = stats[16 + ch], wv = bw[ch], bv = bb[ch];
-  const float inv_m = 1.0f / (float)m;
-  const float mg = sums[ch] * inv_m, mgx = sums[16 + ch] * inv_m, isw = is * wv;
-#pragma unroll
-  for (int u = 0; u < SM_U; ++u) pimg[w][u][l & 15][12 + kq] = 0.0f;  // k = 12 .. 15: zero B operands
-  const unsigned ntiles = (m + 15) / 16, nw = gridDim.x * (BN_THREADS / 64);
-  double g[4] = {0.0, 0.0, 0.0, 0.0};
-  for (unsigned tb = (blockIdx.x * (BN_THREADS / 64) + w) * SM_U; tb < ntiles; tb += nw * SM_U) {
-#pragma unroll
-    for (int u = 0; u < SM_U; ++u) sm_gather(s, tab, (tb + u) * 16, m, px[u]);
-#pragma unroll
-    for (int u = 0; u < SM_U; ++u) {
-#pragma unroll
-      for (int c = 0; c < 3; ++c) pimg[w][u][l & 15][kq + 4 * c] = px[u][c];
-    }
-#pragma unroll
-    for (int u = 0; u < SM_U; ++u) {
-      const sm4 x = sm_conv(px[u], wb);
-      float gz[4], xh[4];
-      sm_grad<ACT>(gy, (tb + u) * 16, rows, x, mu, is, wv, bv, slope, gz, xh);
-      sm4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        // rows >= m: their pixels (the B operand) are 0
-        const float gx = (gz[v] - mg - xh[v] * mgx) * isw;
-        acc = sm_mfma(gx, pimg[w][u][4 * kq + v][ch], acc);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) g[q] += (double)acc[q];
-    }
-  }
-  // lane l holds G[channel 4 (l / 16) + q][k = l % 16]; per (channel, k) the waves' values in order
-#pragma unroll
-  for (int q = 0; q < 4; ++q) red[q * BN_THREADS + threadIdx.x] = g[q];
+  atomicMax(&s_span, mx);
   __syncthreads();
-  for (int v = threadIdx.x; v < 16 * 9; v += BN_THREADS) {
-    const int c2 = v / 9, k = v % 9, lane = (c2 >> 2) * 16 + k, q = c2 & 3;
-    double t = 0.0;
-    for (int ww = 0; ww < BN_THREADS / 64; ++ww) t += red[q * BN_THREADS + ww * 64 + lane];
-    wpart[(size_t)blockIdx.x * 144 + v] = t;
+  const int span = s_span;
+  const bool staged = span <= cap;  // (block-uniform)
+
+  float wb[3];  // B operand of the conv: W[ch][k = kq + 4 c] (0 for k >= 9)
+#pragma unroll
+  for (int c = 0; c < 3; ++c) wb[c] = kq + 4 * c < 9 ? s.w[ch * 9 + kq + 4 * c] : 0.0f;
+  float mu = 0.0f, is = 0.0f, wv = 0.0f, bv = 0.0f, mg = 0.0f, mgx = 0.0f, sh = 0.0f;
+  const unsigned m = (unsigned)s.nimg * (unsigned)ncell, rows = (unsigned)s.rows_out, ra = (unsigned)s.nimg * (unsigned)na;
+  if constexpr (PASS == SM_STATS) {
+    // the shift: row 0 (image 0, cell 0) of this lane's channel, from global memory (lane ch holds row 0)
+    const bool ok = (int)(l & 15) < ncell;
+    const short* t0 = tab + (ok ? (int)(l & 15) : 0) * 9;
+    const float v0 = s.obs[s.off + t0[kq]], v1 = s.obs[s.off + t0[kq + 4]], v2 = s.obs[s.off + t0[8]];
+    const float px[3] = {ok ? v0 : 0.0f, ok ? v1 : 0.0f, (ok && kq == 0) ? v2 : 0.0f};
+    const sm4 x0 = sm_conv(px, wb);
+    sh = __shfl(x0[0], (int)ch);
+    if (blockIdx.x == 0 && threadIdx.x < 16) q.shift[ch] = sh;
+  } else {
+    mu = q.stats[ch];
+    is = q.stats[16 + ch];
+    wv = q.bw[ch];
+    bv = q.bb[ch];
+    if constexpr (PASS == SM_WGRAD) {
+      const float inv_m = 1.0f / (float)m;
+      mg = q.sums[ch] * inv_m;
+      mgx = q.sums[16 + ch] * inv_m;
+      pimg[w][l & 15][12 + kq] = 0.0f;  // k = 12 .. 15: zero B operands
+    }
   }
+  const float isw = is * wv;
+  double a0 = 0.0, a1 = 0.0, g4[4] = {0.0, 0.0, 0.0, 0.0};
+  const int ta = (na + 15) / 16, T = ta + (nbt + 15) / 16;
+
+  for (int b = blockIdx.x; b < s.nimg; b += gridDim.x) {
+    const float* g = s.obs + (long long)b * s.ld + s.off;
+    if (staged) {
+      __syncthreads();  // the previous image's readers are done
+      int i = threadIdx.x;
+      for (; i + 7 * BN_THREADS < span; i += 8 * BN_THREADS) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = g[i + u * BN_THREADS];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) im[i + u * BN_THREADS] = v[u];
+      }
+      for (; i < span; i += BN_THREADS) im[i] = g[i];
+      __syncthreads();
+    }
+    for (int j = (int)w; j < T; j += BN_THREADS / 64) {
+      int cell0, nvalid;
+      unsigned r0;
+      if (j < ta) {
+        cell0 = 16 * j;
+        nvalid = na - cell0 < 16 ? na - cell0 : 16;
+        r0 = (unsigned)b * (unsigned)na + (unsigned)cell0;
+      } else {
+        const int jj = 16 * (j - ta);
+        cell0 = na + jj;
+        nvalid = nbt - jj < 16 ? nbt - jj : 16;
+        r0 = ra + (unsigned)b * (unsigned)nbt + (unsigned)jj;
+      }
+      const bool ok = (int)(l & 15) < nvalid;
+      const short* t = tab + (cell0 + (ok ? (int)(l & 15) : 0)) * 9;
+      float v0, v1, v2;
+      if (staged) {
+        v0 = im[t[kq]];
+        v1 = im[t[kq + 4]];
+        v2 = im[t[8]];
+      } else {
+        v0 = g[t[kq]];
+        v1 = g[t[kq + 4]];
+        v2 = g[t[8]];
+      }
+      const float px[3] = {ok ? v0 : 0.0f, ok ? v1 : 0.0f, (ok && kq == 0) ? v2 : 0.0f};
+      const sm4 x = sm_conv(px, wb);
+      if constexpr (PASS == SM_STATS) {
+        float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const float d = (int)(4 * kq + v) < nvalid ? x[v] - sh : 0.0f;
+          s0 += d;
+          s1 += d * d;
+        }
+        a0 += (double)s0;
+        a1 += (double)s1;
+      } else if constexpr (PASS == SM_APPLY) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const unsigned r = r0 + 4 * kq + v;
+          if ((int)(4 * kq + v) < nvalid && r < rows) q.y[(size_t)r * 16 + ch] = bn_act<ACT>((x[v] - mu) * is * wv + bv, q.slope);
+        }
+      } else {
+        // gy of the lane's rows (0 past rows_out: those rows enter the statistics only), gz = gy act'(z)
+        float gz[4], xh[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const unsigned r = r0 + 4 * kq + v;
+          const bool live = (int)(4 * kq + v) < nvalid && r < rows;
+          const float gv = q.gy[(size_t)(live ? r : 0u) * 16 + ch];
+          xh[v] = (x[v] - mu) * is;
+          gz[v] = (live ? gv : 0.0f) * bn_dact<ACT>(xh[v] * wv + bv, q.slope);
+        }
+        if constexpr (PASS == SM_BWDP) {
+          float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            s0 += gz[v];
+            s1 += gz[v] * xh[v];
+          }
+          a0 += (double)s0;
+          a1 += (double)s1;
+        } else {
+#pragma unroll
+          for (int c = 0; c < 3; ++c) pimg[w][l & 15][kq + 4 * c] = px[c];
+          sm4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            // rows past the tile's end: their pixels (the B operand) are 0
+            const float gx = (gz[v] - mg - xh[v] * mgx) * isw;
+            acc = sm_mfma(gx, pimg[w][4 * kq + v][ch], acc);
+          }
+#pragma unroll
+          for (int c = 0; c < 4; ++c) g4[c] += (double)acc[c];
+        }
+      }
+    }
+  }
+
+  // fixed-order block reductions through the (now free) image area
+  __syncthreads();
+  double* red = reinterpret_cast<double*>(im);
+  if constexpr (PASS == SM_STATS || PASS == SM_BWDP) {
+    // part[block][2][16]: per channel the waves in order, then l / 16 in order
+    red[threadIdx.x] = a0;
+    red[BN_THREADS + threadIdx.x] = a1;
+    __syncthreads();
+    if (threadIdx.x < 32) {
+      const int qq = threadIdx.x >> 4, c = threadIdx.x & 15;
+      double acc = 0.0;
+      for (int ww = 0; ww < BN_THREADS / 64; ++ww)
+        for (int k = 0; k < 4; ++k) acc += red[qq * BN_THREADS + ww * 64 + k * 16 + c];
+      q.part[(size_t)blockIdx.x * 32 + threadIdx.x] = acc;
+    }
+  } else if constexpr (PASS == SM_WGRAD) {
+    // lane l holds G[channel 4 (l / 16) + c][k = l % 16]; wpart[block][ch * 9 + k]: the waves' values in order
+#pragma unroll
+    for (int c = 0; c < 4; ++c) red[c * BN_THREADS + threadIdx.x] = g4[c];
+    __syncthreads();
+    for (int v = threadIdx.x; v < 16 * 9; v += BN_THREADS) {
+      const int c2 = v / 9, k = v % 9, lane = (c2 >> 2) * 16 + k, c = c2 & 3;
+      double t = 0.0;
+      for (int ww = 0; ww < BN_THREADS / 64; ++ww) t += red[c * BN_THREADS + ww * 64 + lane];
+      q.part[(size_t)blockIdx.x * 144 + v] = t;
+    }
+  }
+}
+
+template <int PASS>
+static void sm_launch(const Stem1& s, const SmArgs& q, int act, int grid, hipStream_t st) {
+  long long room = s.ld - s.off;
+  const int cap = (int)(room < 1 ? 1 : room < SM_IMG_CAP ? room : SM_IMG_CAP);
+  const size_t lds = sm_lds_bytes(s.na + s.nbt, cap);
+  if (act == GR_POLICY_ACT_ELU)
+    hipLaunchKernelGGL((stem1i_kernel<PASS, GR_POLICY_ACT_ELU>), dim3(grid), dim3(BN_THREADS), lds, st, s, q, cap);
+  else
+    hipLaunchKernelGGL((stem1i_kernel<PASS, GR_POLICY_ACT_LRELU>), dim3(grid), dim3(BN_THREADS), lds, st, s, q, cap);
 }
 
 static int stem_blocks(const Stem1& s) { return bn_blocks((long long)s.nimg * (s.na + s.nbt), s.c); }
@@ -688,13 +682,12 @@ hipError_t launch_stem1_forward(const Stem1& s, const float* bw, const float* bb
   const int nb = stem_blocks(s);
   float* shift = reinterpret_cast<float*>(part + (size_t)nb * 2 * s.c);
   const long long m = (long long)s.nimg * (s.na + s.nbt);
-  if (s.c == 16) {  // the reference's stem: the MFMA kernels
-    hipLaunchKernelGGL(stem1m_stats_partial, dim3(nb), dim3(BN_THREADS), 0, st, s, part, shift);
-    hipLaunchKernelGGL(bn_stats_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, shift, m, s.c, nb, eps, part, stats);
-    if (act == GR_POLICY_ACT_ELU)
-      hipLaunchKernelGGL(stem1m_apply<GR_POLICY_ACT_ELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, bw, bb, stats, slope, y);
-    else
-      hipLaunchKernelGGL(stem1m_apply<GR_POLICY_ACT_LRELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, bw, bb, stats, slope, y);
+  if (s.c == 16) {  // the reference's stem: the MFMA kernels, whole images per workgroup
+    const int grid = nb < SM_GRID ? nb : SM_GRID;
+    SmArgs q{bw, bb, stats, nullptr, nullptr, y, part, shift, slope};
+    sm_launch<SM_STATS>(s, q, act, grid, st);
+    hipLaunchKernelGGL(bn_stats_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, shift, m, s.c, grid, eps, part, stats);
+    sm_launch<SM_APPLY>(s, q, act, grid, st);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(stem1_stats_partial, dim3(nb), dim3(BN_THREADS), 0, st, s, part, shift);
@@ -713,16 +706,13 @@ hipError_t launch_stem1_backward(const Stem1& s, const float* bw, const float* b
   float* sums = reinterpret_cast<float*>(part + (size_t)nb * 2 * s.c);
   double* wpart = part + (size_t)nb * 2 * s.c + 2 * s.c;
   if (s.c == 16) {
-    if (act == GR_POLICY_ACT_ELU)
-      hipLaunchKernelGGL(stem1m_bwd_partial<GR_POLICY_ACT_ELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, gy, bw, bb, stats, slope, part);
-    else
-      hipLaunchKernelGGL(stem1m_bwd_partial<GR_POLICY_ACT_LRELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, gy, bw, bb, stats, slope, part);
-    hipLaunchKernelGGL(bn_bwd_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, s.c, nb, part, gbw, gbb, sums);
-    if (act == GR_POLICY_ACT_ELU)
-      hipLaunchKernelGGL(stem1m_bwd_wgrad<GR_POLICY_ACT_ELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, gy, bw, bb, stats, sums, slope, wpart);
-    else
-      hipLaunchKernelGGL(stem1m_bwd_wgrad<GR_POLICY_ACT_LRELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, gy, bw, bb, stats, sums, slope, wpart);
-    hipLaunchKernelGGL(stem1_wgrad_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, 9 * s.c, nb, wpart, gconv);
+    const int grid = nb < SM_GRID ? nb : SM_GRID;
+    SmArgs q{bw, bb, stats, sums, gy, nullptr, part, nullptr, slope};
+    sm_launch<SM_BWDP>(s, q, act, grid, st);
+    hipLaunchKernelGGL(bn_bwd_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, s.c, grid, part, gbw, gbb, sums);
+    q.part = wpart;
+    sm_launch<SM_WGRAD>(s, q, act, grid, st);
+    hipLaunchKernelGGL(stem1_wgrad_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, 9 * s.c, grid, wpart, gconv);
     return hipGetLastError();
   }
   if (act == GR_POLICY_ACT_ELU)
