@@ -37,7 +37,7 @@
 #define GR_CAM_MAX_W 256
 #define GR_CAM_MAX_H 256
 #define GR_CAM_MAX_GATES 64 /* one lane per gate sets a wave's gate slots up */
-#define GR_CAM_SLOT 24      /* floats per gate slot, see gr_cam_gate_setup */
+#define GR_CAM_SLOT 36      /* floats per gate slot, see gr_cam_gate_setup */
 #define GR_CAM_FAR 3.0e38f  /* "no hit" */
 
 /* slot layout */
@@ -55,6 +55,13 @@
 #define GR_CS_BMIN 19
 #define GR_CS_BMAX 20
 #define GR_CS_VALID 21 /* 1.0: may be hit by some pixel; 0.0: culled (behind, beyond range, or absent) */
+/* a gate's inverse-depth slab constants (gr_cam_gate_hit; gr_obst_slab_prep of gr_obstacles.h): entry / exit of
+ * the outer box's x, y, z slabs, of the hole's x, y slabs, and the camera-inside bits (as a float) */
+#define GR_CS_UE 24   /* outer x, y, z entry (3) */
+#define GR_CS_UX 27   /* outer x, y, z exit (3) */
+#define GR_CS_HE 30   /* hole x, y entry (2) */
+#define GR_CS_HX 32   /* hole x, y exit (2) */
+#define GR_CS_UM 34   /* bits 0-2: inside outer slab x / y / z; bits 3-4: inside hole slab x / y */
 
 /* Constants derived once from gr_camera_config (host side, identical on both sides). */
 typedef struct gr_cam_const {
@@ -164,6 +171,19 @@ GR_HD void gr_cam_gate_setup(const float* g, const float o[3], const float c0[3]
   s[GR_CS_HT] = g[15];
   s[GR_CS_HOW] = g[16];
   s[GR_CS_HOH] = g[17];
+  int m = 0, in = 0;
+  gr_obst_slab_prep(s[GR_CS_O], s[GR_CS_HOW], &s[GR_CS_UE], &s[GR_CS_UX], &in);
+  m |= in;
+  gr_obst_slab_prep(s[GR_CS_O + 1], s[GR_CS_HOH], &s[GR_CS_UE + 1], &s[GR_CS_UX + 1], &in);
+  m |= in << 1;
+  gr_obst_slab_prep(s[GR_CS_O + 2], s[GR_CS_HT], &s[GR_CS_UE + 2], &s[GR_CS_UX + 2], &in);
+  m |= in << 2;
+  gr_obst_slab_prep(s[GR_CS_O], s[GR_CS_HW], &s[GR_CS_HE], &s[GR_CS_HX], &in);
+  m |= in << 3;
+  gr_obst_slab_prep(s[GR_CS_O + 1], s[GR_CS_HH], &s[GR_CS_HE + 1], &s[GR_CS_HX + 1], &in);
+  m |= in << 4;
+  s[GR_CS_UM] = (float)m;
+  s[GR_CS_UM + 1] = 0.0f;
 }
 
 /* kernel-only tile cull of a gate slot: its outer box (gr_cam_box_outside, gr_obstacles.h) */
@@ -185,40 +205,41 @@ GR_HD void gr_cam_obst_setup(const float* r, const float o[3], const float c0[3]
   s[16] = 0.0f;
 }
 
-GR_HD float gr_cam_inv(float d) { return 1.0f / (gr_fabsf(d) < 1.0e-20f ? gr_copysignf(1.0e-20f, d) : d); }
-
 /* First surface crossing (s > 0) of the ray (a, b) with the gate solid
  * {|x| <= how, |y| <= hoh, |z| <= ht} minus the hole {|x| < hw, |y| < hh}; GR_CAM_FAR if none.
  * From outside the solid: the first entry; from inside a bar: the exit (a mesh ray cast
- * reports the first face it crosses either way). */
+ * reports the first face it crosses either way).  In inverse depth u = 1 / s, as
+ * gr_cam_obst_hit_k (gr_obstacles.h): the five slab tests are multiplies by the slot's constants,
+ * and the hit costs one division. */
 GR_HD float gr_cam_gate_hit(const float* s, float a, float b) {
   const float dx = gr_fmaf(b, s[GR_CS_D2], gr_fmaf(a, s[GR_CS_D1], s[GR_CS_D0]));
   const float dy = gr_fmaf(b, s[GR_CS_D2 + 1], gr_fmaf(a, s[GR_CS_D1 + 1], s[GR_CS_D0 + 1]));
   const float dz = gr_fmaf(b, s[GR_CS_D2 + 2], gr_fmaf(a, s[GR_CS_D1 + 2], s[GR_CS_D0 + 2]));
-  const float ix = gr_cam_inv(dx), iy = gr_cam_inv(dy), iz = gr_cam_inv(dz);
-  const float ox = s[GR_CS_O], oy = s[GR_CS_O + 1], oz = s[GR_CS_O + 2];
-  const float tx0 = (-s[GR_CS_HOW] - ox) * ix, tx1 = (s[GR_CS_HOW] - ox) * ix;
-  const float ty0 = (-s[GR_CS_HOH] - oy) * iy, ty1 = (s[GR_CS_HOH] - oy) * iy;
-  const float tz0 = (-s[GR_CS_HT] - oz) * iz, tz1 = (s[GR_CS_HT] - oz) * iz;
-  const float tin = gr_maxf(gr_maxf(gr_minf(tx0, tx1), gr_minf(ty0, ty1)), gr_minf(tz0, tz1));
-  const float tout = gr_minf(gr_minf(gr_maxf(tx0, tx1), gr_maxf(ty0, ty1)), gr_maxf(tz0, tz1));
-  if (!(tin <= tout) || !(tout > 0.0f)) return GR_CAM_FAR;
-  const float hx0 = (-s[GR_CS_HW] - ox) * ix, hx1 = (s[GR_CS_HW] - ox) * ix;
-  const float hy0 = (-s[GR_CS_HH] - oy) * iy, hy1 = (s[GR_CS_HH] - oy) * iy;
-  const float hin = gr_maxf(gr_minf(hx0, hx1), gr_minf(hy0, hy1));
-  const float hout = gr_minf(gr_maxf(hx0, hx1), gr_maxf(hy0, hy1));
-  const int hole = hin < hout;
-  const float t0 = tin > 0.0f ? tin : 0.0f;
-  const int start_in_hole = hole && hin < t0 && t0 < hout;
-  float hit;
-  if (tin > 0.0f || start_in_hole) {
-    /* outside the solid: enter at t0 unless t0 lies in the hole, then at the hole's exit */
-    hit = !start_in_hole ? t0 : (hout < tout ? hout : GR_CAM_FAR);
+  const int m = (int)s[GR_CS_UM];
+  float uin = GR_U_NONE, uout = 0.0f, hin = GR_U_NONE, hout = 0.0f;
+  gr_u_slab(dx, s[GR_CS_UE], s[GR_CS_UX], m & 1, &uin, &uout);
+  gr_u_slab(dy, s[GR_CS_UE + 1], s[GR_CS_UX + 1], m & 2, &uin, &uout);
+  gr_u_slab(dz, s[GR_CS_UE + 2], s[GR_CS_UX + 2], m & 4, &uin, &uout);
+  gr_u_slab(dx, s[GR_CS_HE], s[GR_CS_HX], m & 8, &hin, &hout);
+  gr_u_slab(dy, s[GR_CS_HE + 1], s[GR_CS_HX + 1], m & 16, &hin, &hout);
+  /* the hole's prism: around the camera (its entry behind), or crossed ahead (a prism interval behind the
+   * camera plays no part) */
+  const int prism = hin >= GR_U_NONE;
+  const int ahead = !prism && hin > 0.0f && hin > hout;
+  float u;
+  if (uin < GR_U_NONE) {
+    /* outside the solid's box: enter at its entry, unless that lies in the hole, then at the hole's exit */
+    if (!(uin > 0.0f && uin >= uout)) return GR_CAM_FAR;
+    const int in_hole = (prism || (ahead && hin > uin)) && uin > hout;
+    u = in_hole ? (hout > uout ? hout : 0.0f) : uin;
+  } else if (prism) {
+    /* inside the box, in the hole: the hole's exit if it leaves through a bar */
+    u = hout > uout ? hout : 0.0f;
   } else {
     /* inside a bar: leave through the hole wall or the outer box */
-    hit = (hole && hin > 0.0f && hin < tout) ? hin : tout;
+    u = (ahead && hin > uout) ? hin : uout;
   }
-  return hit;
+  return u > 0.0f ? 1.0f / u : GR_CAM_FAR;
 }
 
 /* ground plane z = gz seen along the ray with vertical component dz */

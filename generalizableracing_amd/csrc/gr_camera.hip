@@ -29,6 +29,7 @@ DEV_INLINE void nt_store4(float4* p, float4 v) {
 
 #define CAM_WAVES 4
 #define CAM_SLOT4 (GR_CAM_SLOT / 4)
+static_assert(GR_CAM_SLOT == GR_CAM_GATE_SLOT, "gate slot size (gr_camera.h / gr_kernels.h)");
 #ifndef CAM_BATCH
 #define CAM_BATCH 9  // reuse path: depth quads loaded per lane before any is consumed (27 = 3 x 9 at 96x72)
 #endif

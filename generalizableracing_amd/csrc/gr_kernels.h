@@ -177,7 +177,8 @@ hipError_t launch_in_backward(const float* gh, const float* hv, const float* x, 
                               float slope, float* part, float* sums, hipStream_t s);
 // obstacle slots per camera wave (the first GR_CAM_OBST_SLOTS obstacles in view; any further ones
 // are set up again per tile from their records)
-#define GR_CAM_OBST_SLOTS 48  // (in view per env at 65 536 envs: mean 18.7, max 49)
+#define GR_CAM_GATE_SLOT 36   // floats per gate slot in LDS (GR_CAM_SLOT of gr_camera.h)
+#define GR_CAM_OBST_SLOTS 40  // (in view per env at 65 536 envs: mean 18.7, max 49; 40 x 32 floats = the LDS of 64 x 20)
 #define GR_CAM_OSLOT 32  // floats per obstacle slot in LDS: slot floats 0-15, the window (17-20), gr_cam_obst_prep's 12
 // dynamic LDS of the camera kernel: ray tables + per wave (gate slots, one 64-bit gate mask per 8x32 tile
 // [+ obstacle slots and their tile masks] + an 8-row staging band); every part a multiple of 4 floats
@@ -192,7 +193,7 @@ inline size_t camera_lds_bytes(int width, int height, int max_gates, bool obst) 
   const size_t wpad = (size_t)((width + 3) & ~3), hpad = (size_t)((height + 3) & ~3);
   const size_t os = obst ? camera_obst_floats(width, height) : 0;
   return 4 * (wpad + hpad +
-              4 * ((size_t)max_gates * 24 + camera_tile_mask_floats(width, height) + os + 8 * (size_t)width));
+              4 * ((size_t)max_gates * GR_CAM_GATE_SLOT + camera_tile_mask_floats(width, height) + os + 8 * (size_t)width));
 }
 
 // which step_kernel instantiation gr_step launches for these arguments (GR_STEP_* of gr.h)

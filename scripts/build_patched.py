@@ -1,6 +1,7 @@
 """Timing-only variant builds of libgr.so from a patched copy of the sources (the product sources carry no
 ablation switches).  A patch is a JSON list of [file, old, new] text replacements; every `old` must occur
-exactly once.  Output: variants/<name>/libgr.so (GR_LIB_PATH selects it on the GPU box).
+exactly once; {"rev": COMMIT} builds that commit's sources instead of the tree's.  Output: variants/<name>/libgr.so
+(GR_LIB_PATH selects it on the GPU box).
 
     python scripts/build_patched.py NAME PATCH.json [-DMACRO=VALUE ...]
 
@@ -17,11 +18,15 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def build(name, patch, extra_flags=""):
+def build(name, patch, extra_flags="", rev=None):
     tmp = tempfile.mkdtemp(prefix="grvar_")
     src = os.path.join(tmp, "generalizableracing_amd", "csrc")
-    shutil.copytree(os.path.join(ROOT, "generalizableracing_amd", "csrc"), src)
-    shutil.copytree(os.path.join(ROOT, "include"), os.path.join(tmp, "include"))
+    if rev:  # the sources of an earlier commit (a before / after pair on the same box)
+        subprocess.run(f"git -C {ROOT} archive {rev} generalizableracing_amd/csrc include | tar -x -C {tmp}", shell=True,
+                       check=True)
+    else:
+        shutil.copytree(os.path.join(ROOT, "generalizableracing_amd", "csrc"), src)
+        shutil.copytree(os.path.join(ROOT, "include"), os.path.join(tmp, "include"))
     for fname, old, new in patch:
         p = os.path.join(src, fname)
         s = open(p).read()
@@ -50,13 +55,13 @@ def load_patch(path):
     """A patch file: a JSON list of [file, old, new] replacements, or {"replace": [...], "flags": "-D...",
     "note": "..."} (variants/patches/*.json)."""
     if path == "-":
-        return [], ""
+        return [], "", None
     p = json.load(open(path))
     if isinstance(p, dict):
-        return p.get("replace", []), p.get("flags", "")
-    return p, ""
+        return p.get("replace", []), p.get("flags", ""), p.get("rev")
+    return p, "", None
 
 
 if __name__ == "__main__":
-    reps, flags = load_patch(sys.argv[2])
-    build(sys.argv[1], reps, " ".join([flags] + sys.argv[3:]))
+    reps, flags, rev = load_patch(sys.argv[2])
+    build(sys.argv[1], reps, " ".join([flags] + sys.argv[3:]), rev)
