@@ -482,7 +482,29 @@ __host__ __device__ inline size_t sm_lds_bytes(int ncell, int cap) {
   return 4 * (sm_tab_floats(ncell) + (size_t)(cap > 2048 ? cap : 2048));
 }
 
-template <int PASS, int ACT>
+// the image's first `span` floats into LDS, every load of the thread in flight at once (T = float4 when the rows
+// are 16-B aligned, else float; span <= SM_IMG_CAP): 27.6 KB per image, ~80 KB per CU in flight
+template <typename T>
+__device__ __forceinline__ void sm_stage(const float* __restrict__ g, float* im, int span) {
+  constexpr int E = sizeof(T) / 4, N = SM_IMG_CAP / E / BN_THREADS;
+  const T* gs = reinterpret_cast<const T*>(g);
+  T* ls = reinterpret_cast<T*>(im);
+  const int n = span / E;
+  T v[N];
+#pragma unroll
+  for (int u = 0; u < N; ++u) {
+    const int i = threadIdx.x + u * BN_THREADS;
+    v[u] = gs[i < n ? i : (n > 0 ? n - 1 : 0)];  // (branch-free: all N loads issue before the first use)
+  }
+#pragma unroll
+  for (int u = 0; u < N; ++u) {
+    const int i = threadIdx.x + u * BN_THREADS;
+    if (i < n) ls[i] = v[u];
+  }
+  for (int i = n * E + (int)threadIdx.x; i < span; i += BN_THREADS) im[i] = g[i];
+}
+
+template <int PASS, int ACT, bool V4>
 __global__ __launch_bounds__(BN_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, int cap) {
   extern __shared__ float4 sm_dyn4[];
   __shared__ int s_span;
@@ -538,15 +560,10 @@ __global__ __launch_bounds__(BN_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, i
     const float* g = s.obs + (long long)b * s.ld + s.off;
     if (staged) {
       __syncthreads();  // the previous image's readers are done
-      int i = threadIdx.x;
-      for (; i + 7 * BN_THREADS < span; i += 8 * BN_THREADS) {
-        float v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = g[i + u * BN_THREADS];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) im[i + u * BN_THREADS] = v[u];
-      }
-      for (; i < span; i += BN_THREADS) im[i] = g[i];
+      if constexpr (V4)
+        sm_stage<float4>(g, im, span);
+      else
+        sm_stage<float>(g, im, span);
       __syncthreads();
     }
     for (int j = (int)w; j < T; j += BN_THREADS / 64) {
@@ -663,10 +680,18 @@ static void sm_launch(const Stem1& s, const SmArgs& q, int act, int grid, hipStr
   long long room = s.ld - s.off;
   const int cap = (int)(room < 1 ? 1 : room < SM_IMG_CAP ? room : SM_IMG_CAP);
   const size_t lds = sm_lds_bytes(s.na + s.nbt, cap);
-  if (act == GR_POLICY_ACT_ELU)
-    hipLaunchKernelGGL((stem1i_kernel<PASS, GR_POLICY_ACT_ELU>), dim3(grid), dim3(BN_THREADS), lds, st, s, q, cap);
-  else
-    hipLaunchKernelGGL((stem1i_kernel<PASS, GR_POLICY_ACT_LRELU>), dim3(grid), dim3(BN_THREADS), lds, st, s, q, cap);
+  const bool v4 = ((uintptr_t)(s.obs + s.off) & 15) == 0 && (s.ld & 3) == 0;  // every image row 16-B aligned
+  if (act == GR_POLICY_ACT_ELU) {
+    if (v4)
+      hipLaunchKernelGGL((stem1i_kernel<PASS, GR_POLICY_ACT_ELU, true>), dim3(grid), dim3(BN_THREADS), lds, st, s, q, cap);
+    else
+      hipLaunchKernelGGL((stem1i_kernel<PASS, GR_POLICY_ACT_ELU, false>), dim3(grid), dim3(BN_THREADS), lds, st, s, q, cap);
+  } else {
+    if (v4)
+      hipLaunchKernelGGL((stem1i_kernel<PASS, GR_POLICY_ACT_LRELU, true>), dim3(grid), dim3(BN_THREADS), lds, st, s, q, cap);
+    else
+      hipLaunchKernelGGL((stem1i_kernel<PASS, GR_POLICY_ACT_LRELU, false>), dim3(grid), dim3(BN_THREADS), lds, st, s, q, cap);
+  }
 }
 
 static int stem_blocks(const Stem1& s) { return bn_blocks((long long)s.nimg * (s.na + s.nbt), s.c); }

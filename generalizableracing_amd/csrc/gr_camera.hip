@@ -83,8 +83,7 @@ DEV_INLINE void reuse_rows(const CamArgs& a, const gr_cam_const* __restrict__ cc
   }
 }
 
-// obstacle slot from LDS (GR_CAM_OSLOT floats: frame and primitive = slot floats 0-15, window = 17-20, then the
-// hit constants of gr_cam_obst_prep)
+// obstacle slot from LDS (GR_CAM_OSLOT floats: frame and primitive = slot floats 0-15, window = 17-20)
 DEV_INLINE void load_oslot(const float4* src, float s[GR_CAM_SLOT]) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -93,13 +92,6 @@ DEV_INLINE void load_oslot(const float4* src, float s[GR_CAM_SLOT]) {
   }
   const float4 w4 = src[4];
   s[GR_CS_AMIN] = w4.x; s[GR_CS_AMAX] = w4.y; s[GR_CS_BMIN] = w4.z; s[GR_CS_BMAX] = w4.w;
-}
-DEV_INLINE void load_oconst(const float4* src, float k[GR_OK_N]) {
-#pragma unroll
-  for (int j = 0; j < GR_OK_N / 4; ++j) {
-    const float4 q4 = src[5 + j];
-    k[4 * j] = q4.x; k[4 * j + 1] = q4.y; k[4 * j + 2] = q4.z; k[4 * j + 3] = q4.w;
-  }
 }
 
 // the obstacle's record from global memory
@@ -123,7 +115,7 @@ DEV_INLINE void quad_obst(const float* s, const float av[4], float b, float d[4]
 }
 
 // Dynamic LDS: ray tables a_u[W], b_v[H] (padded to 4), then per wave: gate slots [max_gates][24], obstacle
-// slots [GR_CAM_OBST_SLOTS][24] (obstacle tracks only) and an 8-row depth staging band [8][W].
+// slots [GR_CAM_OBST_SLOTS][GR_CAM_OSLOT] (obstacle tracks only) and an 8-row depth staging band [8][W].
 #ifdef CAM_WAVES_PER_EU
 #define CAM_ATTR __attribute__((amdgpu_waves_per_eu(CAM_WAVES_PER_EU, CAM_WAVES_PER_EU)))
 #else
@@ -228,11 +220,6 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
           for (int q = 0; q < 4; ++q)
             s_oslot[pos * (GR_CAM_OSLOT / 4) + q] = make_float4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
           s_oslot[pos * (GR_CAM_OSLOT / 4) + 4] = make_float4(s[GR_CS_AMIN], s[GR_CS_AMAX], s[GR_CS_BMIN], s[GR_CS_BMAX]);
-          float kc[GR_OK_N];
-          gr_cam_obst_prep(s, kc);
-#pragma unroll
-          for (int q = 0; q < GR_OK_N / 4; ++q)
-            s_oslot[pos * (GR_CAM_OSLOT / 4) + 5 + q] = make_float4(kc[4 * q], kc[4 * q + 1], kc[4 * q + 2], kc[4 * q + 3]);
         }
         const int nb = __popcll(b);
         if (nv + nb > GR_CAM_OBST_SLOTS && ofrom == nob) {
@@ -278,6 +265,19 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
           tm |= (uint64_t)meet << k;
         }
         s_tmask[tl] = tm;
+      }
+    }
+    if constexpr (obst) {
+      // the tile masks are done with the slots' origins and extents: slot k becomes the 16 floats of the
+      // inverse-depth hit (gr_cam_obst_pack: the slab / quadratic constants replace what the hit no longer reads)
+      wave_lds_sync();
+      if (lane < ns) {
+        float s[GR_CAM_SLOT], pk[GR_OP_N];
+        load_oslot(s_oslot + lane * (GR_CAM_OSLOT / 4), s);
+        gr_cam_obst_pack(s, pk);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          s_oslot[lane * (GR_CAM_OSLOT / 4) + q] = make_float4(pk[4 * q], pk[4 * q + 1], pk[4 * q + 2], pk[4 * q + 3]);
       }
     }
   }
@@ -368,16 +368,19 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
           if (cm == 0u || rm == 0u) continue;
           const int cu = u_t + __builtin_ctz(cm), wc = __popc(cm), rv = __builtin_ctz(rm), area = wc * __popc(rm);
           const float inv_wc = 1.0f / (float)wc;
-          float s[GR_CAM_SLOT], kc[GR_OK_N];
-          load_oslot(s_oslot + k * (GR_CAM_OSLOT / 4), s);
-          load_oconst(s_oslot + k * (GR_CAM_OSLOT / 4), kc);
+          float pk[GR_OP_N];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 q4 = s_oslot[k * (GR_CAM_OSLOT / 4) + q];
+            pk[4 * q] = q4.x; pk[4 * q + 1] = q4.y; pk[4 * q + 2] = q4.z; pk[4 * q + 3] = q4.w;
+          }
           for (int base = 0; base < area; base += 64) {
             const int idx = base + lane;
             if (idx < area) {
               // idx / wc exactly for idx < 256, wc <= 32 (the fraction of a non-integer quotient is <= 31/32)
               const int r = (int)((float)idx * inv_wc + 1.0e-3f), c = idx - r * wc;
               const int u = cu + c, pix = (rv + r) * W + u;
-              const float h = gr_cam_clip(gr_cam_obst_hit_k(s, kc, s_ray_a[u], s_ray_b[v0 + rv + r]), maxd);
+              const float h = gr_cam_clip(gr_cam_obst_hit_p(pk, s_ray_a[u], s_ray_b[v0 + rv + r]), maxd);
               st[pix] = gr_minf(st[pix], h);
             }
           }

@@ -171,9 +171,9 @@ GR_HD float gr_obst_inv(float d) { return 1.0f / (gr_fabsf(d) < 1.0e-20f ? gr_co
  * reverses: the latest entry is the smallest u, the earliest exit the largest), and so do the quadratics, whose
  * roots satisfy s1 s2 = Cc / A (Vieta): u = (-Bh -/+ sq) / Cc, Cc = |o|^2 - r^2 a per-slot constant.  A hit
  * costs one division, 1 / u of the first crossing, instead of one per slab or root (three for a box, up to
- * five for a capsule).  The constants (gr_cam_obst_prep) come with the slot; gr_cam_obst_hit derives them
- * itself. */
-#define GR_OK_N 12          /* floats of the per-slot constants */
+ * five for a capsule).  gr_cam_obst_pack turns a slot into the 16 floats the hit reads (the constants replace
+ * the origin and extents a box's hit no longer needs); gr_cam_obst_hit packs and hits in one call. */
+#define GR_OP_N 16          /* floats of a packed obstacle slot */
 #define GR_U_NONE 3.0e38f   /* "no entry bound" (the camera is inside that slab / sphere) */
 
 /* slab |x| <= e seen from o: entry / exit constants (1 / (plane - o)); inside: o strictly between the planes */
@@ -188,45 +188,8 @@ GR_HD void gr_obst_slab_prep(float o, float e, float* cE, float* cX, int* inside
     *cX = gr_obst_inv(hi);
   }
 }
-
-/* k[0..2] slab entry constants (x, y, z), k[4..6] exit constants, k[3] bit mask as a float: bits 0-2 the camera
- * inside slab x / y / z, bit 3 inside the radius (cylinder, capsule) or sphere, bits 4 / 5 inside the capsule's
- * top / bottom sphere; k[8], k[9] Cc and 1 / Cc of the radial / sphere quadratic; a capsule's top / bottom
- * sphere keeps its Cc, 1 / Cc in k[0], k[1] / k[4], k[5] (it has no x / y slabs) */
-GR_HD void gr_cam_obst_prep(const float* s, float* k) {
-  const int kind = (int)s[GR_OS_KIND];
-  const float e0 = s[GR_OS_E0], e1 = s[GR_OS_E1], e2 = s[GR_OS_E2];
-  const float ox = s[0], oy = s[1], oz = s[2];
-  int m = 0, in = 0;
-  for (int i = 0; i < GR_OK_N; ++i) k[i] = 0.0f;
-  if (kind == GR_OBST_BOX) {
-    gr_obst_slab_prep(ox, e0, &k[0], &k[4], &in);
-    m |= in;
-    gr_obst_slab_prep(oy, e1, &k[1], &k[5], &in);
-    m |= in << 1;
-  }
-  if (kind != GR_OBST_SPHERE) {
-    gr_obst_slab_prep(oz, e2, &k[2], &k[6], &in);
-    m |= in << 2;
-  }
-  if (kind != GR_OBST_BOX) {
-    const float cc = kind == GR_OBST_SPHERE ? ((ox * ox + oy * oy) + oz * oz) - e0 * e0 : (ox * ox + oy * oy) - e0 * e0;
-    k[8] = cc;
-    k[9] = gr_obst_inv(cc);
-    m |= (cc < 0.0f) << 3;
-  }
-  if (kind == GR_OBST_CAPSULE) {
-    const float zt = oz - e2, zb = oz - (-e2);
-    const float ct = ((ox * ox + oy * oy) + zt * zt) - e0 * e0, cb = ((ox * ox + oy * oy) + zb * zb) - e0 * e0;
-    k[0] = ct;
-    k[1] = gr_obst_inv(ct);
-    k[4] = cb;
-    k[5] = gr_obst_inv(cb);
-    m |= (ct < 0.0f) << 4;
-    m |= (cb < 0.0f) << 5;
-  }
-  k[3] = (float)m;
-}
+/* Cc of the sphere / infinite cylinder of radius r around the axis, the camera at (x, y, z) (z = 0: cylinder) */
+GR_HD float gr_obst_cc(float x, float y, float z, float r) { return ((x * x + y * y) + z * z) - r * r; }
 
 /* one slab along the ray: the entry bound (outside only) and the exit */
 GR_HD void gr_u_slab(float d, float cE, float cX, int inside, float* uin, float* uout) {
@@ -239,13 +202,12 @@ GR_HD void gr_u_slab(float d, float cE, float cX, int inside, float* uin, float*
   }
 }
 /* the quadratic A s^2 + 2 Bh s + Cc = 0 (a sphere or the infinite cylinder): 0 if the ray misses it */
-GR_HD int gr_u_quad(float A, float Bh, float cc, float icc, int inside, float* uin, float* uout) {
+GR_HD int gr_u_quad(float A, float Bh, float cc, float icc, float* uin, float* uout) {
   const float disc = Bh * Bh - A * cc;
   if (!(disc >= 0.0f)) return 0;
   const float sq = gr_sqrtf(disc);
-  const float ux = (-Bh - sq) * icc;
-  if (!inside) *uin = gr_minf(*uin, (-Bh + sq) * icc);
-  *uout = gr_maxf(*uout, ux);
+  if (!(cc < 0.0f)) *uin = gr_minf(*uin, (-Bh + sq) * icc);
+  *uout = gr_maxf(*uout, (-Bh - sq) * icc);
   return 1;
 }
 /* u of the first crossing with s > 0 (0: none): the entry, or from inside every part the exit */
@@ -254,43 +216,90 @@ GR_HD float gr_u_first(float uin, float uout) {
   return (uin > 0.0f && uin >= uout) ? uin : 0.0f;
 }
 
-/* first surface crossing (s > 0) of the pixel ray (a, b) with the obstacle of slot s (constants k): from
- * outside the entry, from inside the exit (a mesh ray cast reports the first face it crosses).  The capsule is
- * the union of its cylinder and two end spheres: the nearest of their crossings (the largest u). */
-GR_HD float gr_cam_obst_hit_k(const float* s, const float* k, float a, float b) {
-  const float d0 = gr_fmaf(b, s[9], gr_fmaf(a, s[6], s[3])), d1 = gr_fmaf(b, s[10], gr_fmaf(a, s[7], s[4])),
-              d2 = gr_fmaf(b, s[11], gr_fmaf(a, s[8], s[5]));
+/* packed slot p[16]: camera axes in the primitive frame D0 D1 D2 (0-8), code = kind + 8 x inside bits (15), and
+ *   box:      9-11 slab entry constants x y z, 12-14 exit constants (inside bits 0-2: slabs x y z)
+ *   cylinder: 9-10 origin x y, 11 / 12 z-slab entry / exit, 13 Cc, 14 1 / Cc (bit 2: z slab)
+ *   sphere:   9-11 origin, 12 Cc, 13 1 / Cc
+ *   capsule:  9-11 origin, 12 radius, 13 half length (its constants are derived per call, gr_cam_obst_hit_p) */
+GR_HD void gr_cam_obst_pack(const float* s, float* p) {
+  const int kind = (int)s[GR_OS_KIND];
+  const float e0 = s[GR_OS_E0], e1 = s[GR_OS_E1], e2 = s[GR_OS_E2];
   const float ox = s[0], oy = s[1], oz = s[2];
-  const int kind = (int)s[GR_OS_KIND], m = (int)k[3];
+  int m = 0, in = 0;
+  for (int i = 0; i < 9; ++i) p[i] = s[3 + i];
+  for (int i = 9; i < GR_OP_N; ++i) p[i] = 0.0f;
+  if (kind == GR_OBST_BOX) {
+    gr_obst_slab_prep(ox, e0, &p[9], &p[12], &in);
+    m |= in;
+    gr_obst_slab_prep(oy, e1, &p[10], &p[13], &in);
+    m |= in << 1;
+    gr_obst_slab_prep(oz, e2, &p[11], &p[14], &in);
+    m |= in << 2;
+  } else if (kind == GR_OBST_CYLINDER) {
+    p[9] = ox;
+    p[10] = oy;
+    gr_obst_slab_prep(oz, e2, &p[11], &p[12], &in);
+    m |= in << 2;
+    p[13] = gr_obst_cc(ox, oy, 0.0f, e0);
+    p[14] = gr_obst_inv(p[13]);
+  } else if (kind == GR_OBST_SPHERE) {
+    p[9] = ox;
+    p[10] = oy;
+    p[11] = oz;
+    p[12] = gr_obst_cc(ox, oy, oz, e0);
+    p[13] = gr_obst_inv(p[12]);
+  } else {
+    p[9] = ox;
+    p[10] = oy;
+    p[11] = oz;
+    p[12] = e0;
+    p[13] = e2;
+  }
+  p[15] = (float)(kind + 8 * m);
+}
+
+/* first surface crossing (s > 0) of the pixel ray (a, b) with the packed obstacle p: from outside the entry,
+ * from inside the exit (a mesh ray cast reports the first face it crosses).  The capsule is the union of its
+ * cylinder and two end spheres: the nearest of their crossings (the largest u). */
+GR_HD float gr_cam_obst_hit_p(const float* p, float a, float b) {
+  const float d0 = gr_fmaf(b, p[6], gr_fmaf(a, p[3], p[0])), d1 = gr_fmaf(b, p[7], gr_fmaf(a, p[4], p[1])),
+              d2 = gr_fmaf(b, p[8], gr_fmaf(a, p[5], p[2]));
+  const int code = (int)p[15], kind = code & 7, m = code >> 3;
   float uin = GR_U_NONE, uout = 0.0f, u = 0.0f;
   if (kind == GR_OBST_BOX) {
-    gr_u_slab(d0, k[0], k[4], m & 1, &uin, &uout);
-    gr_u_slab(d1, k[1], k[5], m & 2, &uin, &uout);
-    gr_u_slab(d2, k[2], k[6], m & 4, &uin, &uout);
+    gr_u_slab(d0, p[9], p[12], m & 1, &uin, &uout);
+    gr_u_slab(d1, p[10], p[13], m & 2, &uin, &uout);
+    gr_u_slab(d2, p[11], p[14], m & 4, &uin, &uout);
     u = gr_u_first(uin, uout);
+  } else if (kind == GR_OBST_CYLINDER) {
+    gr_u_slab(d2, p[11], p[12], m & 4, &uin, &uout);
+    if (gr_u_quad(d0 * d0 + d1 * d1, p[9] * d0 + p[10] * d1, p[13], p[14], &uin, &uout)) u = gr_u_first(uin, uout);
   } else if (kind == GR_OBST_SPHERE) {
-    const float A = (d0 * d0 + d1 * d1) + d2 * d2, Bh = (ox * d0 + oy * d1) + oz * d2;
-    if (gr_u_quad(A, Bh, k[8], k[9], m & 8, &uin, &uout)) u = gr_u_first(uin, uout);
+    const float A = (d0 * d0 + d1 * d1) + d2 * d2, Bh = (p[9] * d0 + p[10] * d1) + p[11] * d2;
+    if (gr_u_quad(A, Bh, p[12], p[13], &uin, &uout)) u = gr_u_first(uin, uout);
   } else {
-    const float A = d0 * d0 + d1 * d1, Bh = ox * d0 + oy * d1;
-    gr_u_slab(d2, k[2], k[6], m & 4, &uin, &uout);
-    if (gr_u_quad(A, Bh, k[8], k[9], m & 8, &uin, &uout)) u = gr_u_first(uin, uout);
-    if (kind == GR_OBST_CAPSULE) {
-      const float e2 = s[GR_OS_E2], A3 = A + d2 * d2;
-      float ui = GR_U_NONE, uo = 0.0f;
-      if (gr_u_quad(A3, Bh + (oz - e2) * d2, k[0], k[1], m & 16, &ui, &uo)) u = gr_maxf(u, gr_u_first(ui, uo));
-      ui = GR_U_NONE;
-      uo = 0.0f;
-      if (gr_u_quad(A3, Bh + (oz - (-e2)) * d2, k[4], k[5], m & 32, &ui, &uo)) u = gr_maxf(u, gr_u_first(ui, uo));
-    }
+    const float ox = p[9], oy = p[10], oz = p[11], e0 = p[12], e2 = p[13];
+    float cE, cX;
+    int in = 0;
+    gr_obst_slab_prep(oz, e2, &cE, &cX, &in);
+    gr_u_slab(d2, cE, cX, in, &uin, &uout);
+    const float A = d0 * d0 + d1 * d1, Bh = ox * d0 + oy * d1, cc = gr_obst_cc(ox, oy, 0.0f, e0);
+    if (gr_u_quad(A, Bh, cc, gr_obst_inv(cc), &uin, &uout)) u = gr_u_first(uin, uout);
+    const float A3 = A + d2 * d2, zt = oz - e2, zb = oz - (-e2);
+    const float ct = gr_obst_cc(ox, oy, zt, e0), cb = gr_obst_cc(ox, oy, zb, e0);
+    float ui = GR_U_NONE, uo = 0.0f;
+    if (gr_u_quad(A3, Bh + zt * d2, ct, gr_obst_inv(ct), &ui, &uo)) u = gr_maxf(u, gr_u_first(ui, uo));
+    ui = GR_U_NONE;
+    uo = 0.0f;
+    if (gr_u_quad(A3, Bh + zb * d2, cb, gr_obst_inv(cb), &ui, &uo)) u = gr_maxf(u, gr_u_first(ui, uo));
   }
   return u > 0.0f ? 1.0f / u : 3.0e38f;
 }
 
 GR_HD float gr_cam_obst_hit(const float* s, float a, float b) {
-  float k[GR_OK_N];
-  gr_cam_obst_prep(s, k);
-  return gr_cam_obst_hit_k(s, k, a, b);
+  float p[GR_OP_N];
+  gr_cam_obst_pack(s, p);
+  return gr_cam_obst_hit_p(p, a, b);
 }
 
 #endif /* GR_OBSTACLES_H */
