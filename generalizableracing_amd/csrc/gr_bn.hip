@@ -451,7 +451,9 @@ __global__ __launch_bounds__(BN_FINAL_THREADS) void stem1_wgrad_final(int n, int
 // (or beyond the row: ld - off) gathers from global memory instead (the same arithmetic).
 typedef float sm4 __attribute__((ext_vector_type(4)));
 constexpr int SM_IMG_CAP = 8192;  // image floats staged in LDS per workgroup
-constexpr int SM_GRID = 768;      // workgroups: three per CU (LDS ~46 KB each), images strided over them
+constexpr int SM_GRID = 512;      // workgroups: two per CU (LDS ~73 KB each), images strided over them
+constexpr int SM_WAVES = 4;       // compute waves per workgroup; one more wave stages the next image (LDS-DMA)
+constexpr int SM_THREADS = 64 * (SM_WAVES + 1);
 enum { SM_STATS = 0, SM_APPLY = 1, SM_BWDP = 2, SM_WGRAD = 3 };
 
 struct SmArgs {
@@ -475,48 +477,47 @@ __device__ __forceinline__ sm4 sm_conv(const float px[3], const float wb[3]) {
 }
 __device__ __forceinline__ unsigned sm_wave() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
-// dynamic LDS: the pixel table (int16, padded to 16 B), then the image (max(cap, 2048) floats: the block
-// reductions reuse it at the end, 4 x 256 doubles)
+// dynamic LDS: the pixel table (int16, padded to 16 B), then two image buffers of sm_img_floats (the cap rounded
+// up to a DMA instruction's 256 floats; at least 1 024 each: the block reductions reuse them at the end)
 __host__ __device__ inline size_t sm_tab_floats(int ncell) { return (size_t)((ncell * 9 + 7) & ~7) / 2; }
-__host__ __device__ inline size_t sm_lds_bytes(int ncell, int cap) {
-  return 4 * (sm_tab_floats(ncell) + (size_t)(cap > 2048 ? cap : 2048));
-}
+__host__ __device__ inline size_t sm_img_floats(int cap) { const size_t c = ((size_t)cap + 255) & ~(size_t)255; return c > 1024 ? c : 1024; }
+__host__ __device__ inline size_t sm_lds_bytes(int ncell, int cap) { return 4 * (sm_tab_floats(ncell) + 2 * sm_img_floats(cap)); }
 
-// the image's first `span` floats into LDS, every load of the thread in flight at once (T = float4 when the rows
-// are 16-B aligned, else float; span <= SM_IMG_CAP): 27.6 KB per image, ~80 KB per CU in flight
-template <typename T>
-__device__ __forceinline__ void sm_stage(const float* __restrict__ g, float* im, int span) {
-  constexpr int E = sizeof(T) / 4, N = SM_IMG_CAP / E / BN_THREADS;
-  const T* gs = reinterpret_cast<const T*>(g);
-  T* ls = reinterpret_cast<T*>(im);
-  const int n = span / E;
-  T v[N];
-#pragma unroll
-  for (int u = 0; u < N; ++u) {
-    const int i = threadIdx.x + u * BN_THREADS;
-    v[u] = gs[i < n ? i : (n > 0 ? n - 1 : 0)];  // (branch-free: all N loads issue before the first use)
+typedef __attribute__((address_space(3))) void sm_lds_void_t;
+typedef __attribute__((address_space(1))) void sm_glob_void_t;
+// the image's first `span` floats into the LDS buffer dst by LDS-DMA (global_load_lds), issued by one wave: per
+// instruction lane l's 16 (or 4) bytes land at dst + o + 4 l (or + l); lanes past the span read the image's first
+// bytes (in bounds) into the buffer's padding.  v4: the image rows are 16-B aligned and span % 4 == 0.
+__device__ __forceinline__ void sm_dma_image(const float* g, float* dst, int span, bool v4) {
+  const int lane = threadIdx.x & 63;
+  if (v4) {
+    for (int o = 0; o < span; o += 256) {
+      const int i = o + 4 * lane;
+      __builtin_amdgcn_global_load_lds((sm_glob_void_t*)(g + (i < span ? i : 0)), (sm_lds_void_t*)(dst + o), 16, 0, 0);
+    }
+  } else {
+    for (int o = 0; o < span; o += 64) {
+      const int i = o + lane;
+      __builtin_amdgcn_global_load_lds((sm_glob_void_t*)(g + (i < span ? i : 0)), (sm_lds_void_t*)(dst + o), 4, 0, 0);
+    }
   }
-#pragma unroll
-  for (int u = 0; u < N; ++u) {
-    const int i = threadIdx.x + u * BN_THREADS;
-    if (i < n) ls[i] = v[u];
-  }
-  for (int i = n * E + (int)threadIdx.x; i < span; i += BN_THREADS) im[i] = g[i];
 }
 
 template <int PASS, int ACT, bool V4>
-__global__ __launch_bounds__(BN_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, int cap) {
+__global__ __launch_bounds__(SM_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, int cap) {
   extern __shared__ float4 sm_dyn4[];
   __shared__ int s_span;
-  __shared__ float pimg[BN_THREADS / 64][16][17];  // SM_WGRAD: per wave, the tile's A operands [row][k] (+1: banks)
+  __shared__ float pimg[SM_WAVES][16][17];  // SM_WGRAD: per wave, the tile's A operands [row][k] (+1: banks)
   const int na = s.na, nbt = s.nbt, ncell = na + nbt;
   short* tab = reinterpret_cast<short*>(sm_dyn4);
-  float* im = reinterpret_cast<float*>(sm_dyn4) + sm_tab_floats(ncell);
+  float* im0 = reinterpret_cast<float*>(sm_dyn4) + sm_tab_floats(ncell);
+  float* im1 = im0 + sm_img_floats(cap);
   const unsigned l = threadIdx.x & 63, ch = l & 15, kq = l >> 4, w = sm_wave();
+  const bool loader = w == SM_WAVES;  // (wave-uniform)
   if (threadIdx.x == 0) s_span = 0;
   __syncthreads();
   int mx = 0;
-  for (int i = threadIdx.x; i < ncell * 9; i += BN_THREADS) {
+  for (int i = threadIdx.x; i < ncell * 9; i += SM_THREADS) {
     const short t = s.pix[i];
     tab[i] = t;
     mx = mx > (int)t + 1 ? mx : (int)t + 1;
@@ -525,6 +526,7 @@ __global__ __launch_bounds__(BN_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, i
   __syncthreads();
   const int span = s_span;
   const bool staged = span <= cap;  // (block-uniform)
+  const bool v4 = V4 && (span & 3) == 0;
 
   float wb[3];  // B operand of the conv: W[ch][k = kq + 4 c] (0 for k >= 9)
 #pragma unroll
@@ -549,24 +551,26 @@ __global__ __launch_bounds__(BN_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, i
       const float inv_m = 1.0f / (float)m;
       mg = q.sums[ch] * inv_m;
       mgx = q.sums[16 + ch] * inv_m;
-      pimg[w][l & 15][12 + kq] = 0.0f;  // k = 12 .. 15: zero B operands
+      if (!loader) pimg[w][l & 15][12 + kq] = 0.0f;  // k = 12 .. 15: zero B operands
     }
   }
   const float isw = is * wv;
   double a0 = 0.0, a1 = 0.0, g4[4] = {0.0, 0.0, 0.0, 0.0};
   const int ta = (na + 15) / 16, T = ta + (nbt + 15) / 16;
 
-  for (int b = blockIdx.x; b < s.nimg; b += gridDim.x) {
+  // images b = blockIdx.x + k gridDim.x: the loader wave stages image k + 1 into the other buffer (LDS-DMA) while
+  // the compute waves run image k; the barrier at the end of each image drains the DMA (s_waitcnt vmcnt(0))
+  const int nmine = s.nimg > (int)blockIdx.x ? (s.nimg - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
+  if (staged && loader && nmine > 0) sm_dma_image(s.obs + (long long)blockIdx.x * s.ld + s.off, im0, span, v4);
+  __syncthreads();
+  for (int k = 0; k < nmine; ++k) {
+    const int b = (int)blockIdx.x + k * (int)gridDim.x;
     const float* g = s.obs + (long long)b * s.ld + s.off;
-    if (staged) {
-      __syncthreads();  // the previous image's readers are done
-      if constexpr (V4)
-        sm_stage<float4>(g, im, span);
-      else
-        sm_stage<float>(g, im, span);
-      __syncthreads();
-    }
-    for (int j = (int)w; j < T; j += BN_THREADS / 64) {
+    const float* im = (k & 1) ? im1 : im0;
+    if (loader) {
+      if (staged && k + 1 < nmine) sm_dma_image(g + (long long)gridDim.x * s.ld, (k & 1) ? im0 : im1, span, v4);
+    } else
+    for (int j = (int)w; j < T; j += SM_WAVES) {
       int cell0, nvalid;
       unsigned r0;
       if (j < ta) {
@@ -644,15 +648,17 @@ __global__ __launch_bounds__(BN_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, i
         }
       }
     }
+    __syncthreads();  // image k read, image k + 1 staged
   }
 
-  // fixed-order block reductions through the (now free) image area
-  __syncthreads();
-  double* red = reinterpret_cast<double*>(im);
+  // fixed-order block reductions of the compute waves' sums through the (now free) image buffers
+  double* red = reinterpret_cast<double*>(im0);
   if constexpr (PASS == SM_STATS || PASS == SM_BWDP) {
     // part[block][2][16]: per channel the waves in order, then l / 16 in order
-    red[threadIdx.x] = a0;
-    red[BN_THREADS + threadIdx.x] = a1;
+    if (!loader) {
+      red[threadIdx.x] = a0;
+      red[BN_THREADS + threadIdx.x] = a1;
+    }
     __syncthreads();
     if (threadIdx.x < 32) {
       const int qq = threadIdx.x >> 4, c = threadIdx.x & 15;
@@ -663,8 +669,10 @@ __global__ __launch_bounds__(BN_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, i
     }
   } else if constexpr (PASS == SM_WGRAD) {
     // lane l holds G[channel 4 (l / 16) + c][k = l % 16]; wpart[block][ch * 9 + k]: the waves' values in order
+    if (!loader) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) red[c * BN_THREADS + threadIdx.x] = g4[c];
+      for (int c = 0; c < 4; ++c) red[c * BN_THREADS + threadIdx.x] = g4[c];
+    }
     __syncthreads();
     for (int v = threadIdx.x; v < 16 * 9; v += BN_THREADS) {
       const int c2 = v / 9, k = v % 9, lane = (c2 >> 2) * 16 + k, c = c2 & 3;
@@ -683,14 +691,14 @@ static void sm_launch(const Stem1& s, const SmArgs& q, int act, int grid, hipStr
   const bool v4 = ((uintptr_t)(s.obs + s.off) & 15) == 0 && (s.ld & 3) == 0;  // every image row 16-B aligned
   if (act == GR_POLICY_ACT_ELU) {
     if (v4)
-      hipLaunchKernelGGL((stem1i_kernel<PASS, GR_POLICY_ACT_ELU, true>), dim3(grid), dim3(BN_THREADS), lds, st, s, q, cap);
+      hipLaunchKernelGGL((stem1i_kernel<PASS, GR_POLICY_ACT_ELU, true>), dim3(grid), dim3(SM_THREADS), lds, st, s, q, cap);
     else
-      hipLaunchKernelGGL((stem1i_kernel<PASS, GR_POLICY_ACT_ELU, false>), dim3(grid), dim3(BN_THREADS), lds, st, s, q, cap);
+      hipLaunchKernelGGL((stem1i_kernel<PASS, GR_POLICY_ACT_ELU, false>), dim3(grid), dim3(SM_THREADS), lds, st, s, q, cap);
   } else {
     if (v4)
-      hipLaunchKernelGGL((stem1i_kernel<PASS, GR_POLICY_ACT_LRELU, true>), dim3(grid), dim3(BN_THREADS), lds, st, s, q, cap);
+      hipLaunchKernelGGL((stem1i_kernel<PASS, GR_POLICY_ACT_LRELU, true>), dim3(grid), dim3(SM_THREADS), lds, st, s, q, cap);
     else
-      hipLaunchKernelGGL((stem1i_kernel<PASS, GR_POLICY_ACT_LRELU, false>), dim3(grid), dim3(BN_THREADS), lds, st, s, q, cap);
+      hipLaunchKernelGGL((stem1i_kernel<PASS, GR_POLICY_ACT_LRELU, false>), dim3(grid), dim3(SM_THREADS), lds, st, s, q, cap);
   }
 }
 

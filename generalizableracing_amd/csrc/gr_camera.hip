@@ -115,7 +115,7 @@ DEV_INLINE void quad_obst(const float* s, const float av[4], float b, float d[4]
 }
 
 // Dynamic LDS: ray tables a_u[W], b_v[H] (padded to 4), then per wave: gate slots [max_gates][24], obstacle
-// slots [GR_CAM_OBST_SLOTS][GR_CAM_OSLOT] (obstacle tracks only) and an 8-row depth staging band [8][W].
+// slots [GR_CAM_OBST_SLOTS][24] (obstacle tracks only) and an 8-row depth staging band [8][W].
 #ifdef CAM_WAVES_PER_EU
 #define CAM_ATTR __attribute__((amdgpu_waves_per_eu(CAM_WAVES_PER_EU, CAM_WAVES_PER_EU)))
 #else
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
   float4* s_slot = reinterpret_cast<float4*>(wave_lds);                               // [G][CAM_SLOT4]
   uint64_t* s_gmask = reinterpret_cast<uint64_t*>(wave_lds + G * GR_CAM_SLOT);        // [tiles]
   float* olds = wave_lds + G * GR_CAM_SLOT + tmf;
-  float4* s_oslot = reinterpret_cast<float4*>(olds);                                  // [GR_CAM_OBST_SLOTS][GR_CAM_OSLOT / 4]
+  float4* s_oslot = reinterpret_cast<float4*>(olds);                                  // [64][GR_CAM_OSLOT / 4]
   uint64_t* s_tmask = reinterpret_cast<uint64_t*>(olds + GR_CAM_OBST_SLOTS * GR_CAM_OSLOT);  // [tiles]
   float4* s_stage = reinterpret_cast<float4*>(olds + oslots);                         // [8 * W / 4]
 
@@ -267,19 +267,6 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
         s_tmask[tl] = tm;
       }
     }
-    if constexpr (obst) {
-      // the tile masks are done with the slots' origins and extents: slot k becomes the 16 floats of the
-      // inverse-depth hit (gr_cam_obst_pack: the slab / quadratic constants replace what the hit no longer reads)
-      wave_lds_sync();
-      if (lane < ns) {
-        float s[GR_CAM_SLOT], pk[GR_OP_N];
-        load_oslot(s_oslot + lane * (GR_CAM_OSLOT / 4), s);
-        gr_cam_obst_pack(s, pk);
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          s_oslot[lane * (GR_CAM_OSLOT / 4) + q] = make_float4(pk[4 * q], pk[4 * q + 1], pk[4 * q + 2], pk[4 * q + 3]);
-      }
-    }
   }
   __syncthreads();
   if (!active) return;
@@ -368,19 +355,15 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
           if (cm == 0u || rm == 0u) continue;
           const int cu = u_t + __builtin_ctz(cm), wc = __popc(cm), rv = __builtin_ctz(rm), area = wc * __popc(rm);
           const float inv_wc = 1.0f / (float)wc;
-          float pk[GR_OP_N];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float4 q4 = s_oslot[k * (GR_CAM_OSLOT / 4) + q];
-            pk[4 * q] = q4.x; pk[4 * q + 1] = q4.y; pk[4 * q + 2] = q4.z; pk[4 * q + 3] = q4.w;
-          }
+          float s[GR_CAM_SLOT];
+          load_oslot(s_oslot + k * (GR_CAM_OSLOT / 4), s);
           for (int base = 0; base < area; base += 64) {
             const int idx = base + lane;
             if (idx < area) {
               // idx / wc exactly for idx < 256, wc <= 32 (the fraction of a non-integer quotient is <= 31/32)
               const int r = (int)((float)idx * inv_wc + 1.0e-3f), c = idx - r * wc;
               const int u = cu + c, pix = (rv + r) * W + u;
-              const float h = gr_cam_clip(gr_cam_obst_hit_p(pk, s_ray_a[u], s_ray_b[v0 + rv + r]), maxd);
+              const float h = gr_cam_clip(gr_cam_obst_hit(s, s_ray_a[u], s_ray_b[v0 + rv + r]), maxd);
               st[pix] = gr_minf(st[pix], h);
             }
           }

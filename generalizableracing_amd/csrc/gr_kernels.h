@@ -178,8 +178,8 @@ hipError_t launch_in_backward(const float* gh, const float* hv, const float* x, 
 // obstacle slots per camera wave (the first GR_CAM_OBST_SLOTS obstacles in view; any further ones
 // are set up again per tile from their records)
 #define GR_CAM_GATE_SLOT 36   // floats per gate slot in LDS (GR_CAM_SLOT of gr_camera.h)
-#define GR_CAM_OBST_SLOTS 64  // (in view per env at 65 536 envs: mean 18.7, max 49)
-#define GR_CAM_OSLOT 20  // floats per obstacle slot in LDS: slot floats 0-15 (packed for the hit after the tile cull), window
+#define GR_CAM_OBST_SLOTS 64
+#define GR_CAM_OSLOT 20  // floats per obstacle slot in LDS: gate-slot floats 0-15, then the window (17-20)
 // dynamic LDS of the camera kernel: ray tables + per wave (gate slots, one 64-bit gate mask per 8x32 tile
 // [+ obstacle slots and their tile masks] + an 8-row staging band); every part a multiple of 4 floats
 __host__ __device__ inline size_t camera_tile_mask_floats(int width, int height) {

@@ -163,17 +163,97 @@ GR_HD int gr_cam_obst_outside(const float* s, float a_lo, float a_hi, float b_lo
   return gr_cam_box_outside(s, l, a_lo, a_hi, b_lo, b_hi);
 }
 
+/* first crossing (s > 0) of the ray o + s d with the slab |x_j| <= h_j intersected with
+ * the interval [t0, t1]; GR_CAM_FAR-style miss = 3e38 */
+GR_HD float gr_obst_first(float tin, float tout) {
+  if (!(tin <= tout) || !(tout > 0.0f)) return 3.0e38f;
+  return tin > 0.0f ? tin : tout;
+}
+
 GR_HD float gr_obst_inv(float d) { return 1.0f / (gr_fabsf(d) < 1.0e-20f ? gr_copysignf(1.0e-20f, d) : d); }
 
-/* ---- the per-pixel hit in inverse depth.  Along pixel ray (a, b) the direction in the primitive frame, d, is
- * affine in (a, b), and the depth of the crossing with a plane x_j = p is s = (p - o_j) / d_j: its reciprocal
- * u = d_j / (p - o_j) is d_j times a per-slot constant.  The slab tests therefore run on u (for s > 0 the order
- * reverses: the latest entry is the smallest u, the earliest exit the largest), and so do the quadratics, whose
- * roots satisfy s1 s2 = Cc / A (Vieta): u = (-Bh -/+ sq) / Cc, Cc = |o|^2 - r^2 a per-slot constant.  A hit
- * costs one division, 1 / u of the first crossing, instead of one per slab or root (three for a box, up to
- * five for a capsule).  gr_cam_obst_pack turns a slot into the 16 floats the hit reads (the constants replace
- * the origin and extents a box's hit no longer needs); gr_cam_obst_hit packs and hits in one call. */
-#define GR_OP_N 16          /* floats of a packed obstacle slot */
+/* entry / exit of the sphere |x - (0,0,zc)| <= rad along o + s d (tin > tout: miss) */
+GR_HD void gr_obst_sphere_iv(const float o[3], const float d[3], float zc, float rad, float* tin, float* tout) {
+  const float oz = o[2] - zc;
+  const float A = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
+  const float Bh = (o[0] * d[0] + o[1] * d[1]) + oz * d[2];
+  const float Cc = ((o[0] * o[0] + o[1] * o[1]) + oz * oz) - rad * rad;
+  const float disc = Bh * Bh - A * Cc;
+  if (!(disc >= 0.0f)) {
+    *tin = 1.0f;
+    *tout = -1.0f;
+    return;
+  }
+  const float sq = gr_sqrtf(disc);
+  *tin = (-Bh - sq) / A;
+  *tout = (-Bh + sq) / A;
+}
+
+/* entry / exit of the finite cylinder x^2 + y^2 <= rad^2, |z| <= hh */
+GR_HD void gr_obst_cyl_iv(const float o[3], const float d[3], float rad, float hh, float* tin, float* tout) {
+  const float iz = gr_obst_inv(d[2]);
+  const float z0 = (-hh - o[2]) * iz, z1 = (hh - o[2]) * iz;
+  float lo = gr_minf(z0, z1), hi = gr_maxf(z0, z1);
+  const float A = d[0] * d[0] + d[1] * d[1];
+  const float Bh = o[0] * d[0] + o[1] * d[1];
+  const float Cc = (o[0] * o[0] + o[1] * o[1]) - rad * rad;
+  if (A < 1.0e-12f) {
+    /* parallel to the axis: inside the radius everywhere or nowhere */
+    if (!(Cc <= 0.0f)) hi = lo - 1.0f;
+  } else {
+    const float disc = Bh * Bh - A * Cc;
+    if (!(disc >= 0.0f)) {
+      hi = lo - 1.0f;
+    } else {
+      const float sq = gr_sqrtf(disc);
+      lo = gr_maxf(lo, (-Bh - sq) / A);
+      hi = gr_minf(hi, (-Bh + sq) / A);
+    }
+  }
+  *tin = lo;
+  *tout = hi;
+}
+
+/* first surface crossing (s > 0) of the pixel ray (a, b) with the obstacle of slot s:
+ * from outside the entry, from inside the exit (a mesh ray cast reports the first face
+ * it crosses).  The capsule is the union of its cylinder and two end spheres: the
+ * nearest of their crossings. */
+GR_HD float gr_cam_obst_hit(const float* s, float a, float b) {
+  const float d[3] = {gr_fmaf(b, s[9], gr_fmaf(a, s[6], s[3])), gr_fmaf(b, s[10], gr_fmaf(a, s[7], s[4])),
+                      gr_fmaf(b, s[11], gr_fmaf(a, s[8], s[5]))};
+  const float o[3] = {s[0], s[1], s[2]};
+  const int kind = (int)s[GR_OS_KIND];
+  const float e0 = s[GR_OS_E0], e1 = s[GR_OS_E1], e2 = s[GR_OS_E2];
+  float tin, tout;
+  if (kind == GR_OBST_BOX) {
+    const float ix = gr_obst_inv(d[0]), iy = gr_obst_inv(d[1]), iz = gr_obst_inv(d[2]);
+    const float tx0 = (-e0 - o[0]) * ix, tx1 = (e0 - o[0]) * ix;
+    const float ty0 = (-e1 - o[1]) * iy, ty1 = (e1 - o[1]) * iy;
+    const float tz0 = (-e2 - o[2]) * iz, tz1 = (e2 - o[2]) * iz;
+    tin = gr_maxf(gr_maxf(gr_minf(tx0, tx1), gr_minf(ty0, ty1)), gr_minf(tz0, tz1));
+    tout = gr_minf(gr_minf(gr_maxf(tx0, tx1), gr_maxf(ty0, ty1)), gr_maxf(tz0, tz1));
+    return gr_obst_first(tin, tout);
+  }
+  if (kind == GR_OBST_SPHERE) {
+    gr_obst_sphere_iv(o, d, 0.0f, e0, &tin, &tout);
+    return gr_obst_first(tin, tout);
+  }
+  gr_obst_cyl_iv(o, d, e0, e2, &tin, &tout);
+  float hit = gr_obst_first(tin, tout);
+  if (kind == GR_OBST_CAPSULE) {
+    gr_obst_sphere_iv(o, d, e2, e0, &tin, &tout);
+    hit = gr_minf(hit, gr_obst_first(tin, tout));
+    gr_obst_sphere_iv(o, d, -e2, e0, &tin, &tout);
+    hit = gr_minf(hit, gr_obst_first(tin, tout));
+  }
+  return hit;
+}
+
+/* ---- slab tests in inverse depth (the camera's gate hit, gr_camera.h).  Along pixel ray (a, b) the direction in
+ * the primitive frame, d, is affine in (a, b), and the depth of the crossing with a plane x_j = p is
+ * s = (p - o_j) / d_j: its reciprocal u = d_j / (p - o_j) is d_j times a per-slot constant.  The slab tests
+ * therefore run on u (for s > 0 the order reverses: the latest entry is the smallest u, the earliest exit the
+ * largest), and a hit costs one division, 1 / u of the first crossing, instead of one per slab. */
 #define GR_U_NONE 3.0e38f   /* "no entry bound" (the camera is inside that slab / sphere) */
 
 /* slab |x| <= e seen from o: entry / exit constants (1 / (plane - o)); inside: o strictly between the planes */
@@ -188,9 +268,6 @@ GR_HD void gr_obst_slab_prep(float o, float e, float* cE, float* cX, int* inside
     *cX = gr_obst_inv(hi);
   }
 }
-/* Cc of the sphere / infinite cylinder of radius r around the axis, the camera at (x, y, z) (z = 0: cylinder) */
-GR_HD float gr_obst_cc(float x, float y, float z, float r) { return ((x * x + y * y) + z * z) - r * r; }
-
 /* one slab along the ray: the entry bound (outside only) and the exit */
 GR_HD void gr_u_slab(float d, float cE, float cX, int inside, float* uin, float* uout) {
   const float p = d * cE, q = d * cX;
@@ -201,105 +278,4 @@ GR_HD void gr_u_slab(float d, float cE, float cX, int inside, float* uin, float*
     *uout = gr_maxf(*uout, q);
   }
 }
-/* the quadratic A s^2 + 2 Bh s + Cc = 0 (a sphere or the infinite cylinder): 0 if the ray misses it */
-GR_HD int gr_u_quad(float A, float Bh, float cc, float icc, float* uin, float* uout) {
-  const float disc = Bh * Bh - A * cc;
-  if (!(disc >= 0.0f)) return 0;
-  const float sq = gr_sqrtf(disc);
-  if (!(cc < 0.0f)) *uin = gr_minf(*uin, (-Bh + sq) * icc);
-  *uout = gr_maxf(*uout, (-Bh - sq) * icc);
-  return 1;
-}
-/* u of the first crossing with s > 0 (0: none): the entry, or from inside every part the exit */
-GR_HD float gr_u_first(float uin, float uout) {
-  if (uin >= GR_U_NONE) return uout > 0.0f ? uout : 0.0f;
-  return (uin > 0.0f && uin >= uout) ? uin : 0.0f;
-}
-
-/* packed slot p[16]: camera axes in the primitive frame D0 D1 D2 (0-8), code = kind + 8 x inside bits (15), and
- *   box:      9-11 slab entry constants x y z, 12-14 exit constants (inside bits 0-2: slabs x y z)
- *   cylinder: 9-10 origin x y, 11 / 12 z-slab entry / exit, 13 Cc, 14 1 / Cc (bit 2: z slab)
- *   sphere:   9-11 origin, 12 Cc, 13 1 / Cc
- *   capsule:  9-11 origin, 12 radius, 13 half length (its constants are derived per call, gr_cam_obst_hit_p) */
-GR_HD void gr_cam_obst_pack(const float* s, float* p) {
-  const int kind = (int)s[GR_OS_KIND];
-  const float e0 = s[GR_OS_E0], e1 = s[GR_OS_E1], e2 = s[GR_OS_E2];
-  const float ox = s[0], oy = s[1], oz = s[2];
-  int m = 0, in = 0;
-  for (int i = 0; i < 9; ++i) p[i] = s[3 + i];
-  for (int i = 9; i < GR_OP_N; ++i) p[i] = 0.0f;
-  if (kind == GR_OBST_BOX) {
-    gr_obst_slab_prep(ox, e0, &p[9], &p[12], &in);
-    m |= in;
-    gr_obst_slab_prep(oy, e1, &p[10], &p[13], &in);
-    m |= in << 1;
-    gr_obst_slab_prep(oz, e2, &p[11], &p[14], &in);
-    m |= in << 2;
-  } else if (kind == GR_OBST_CYLINDER) {
-    p[9] = ox;
-    p[10] = oy;
-    gr_obst_slab_prep(oz, e2, &p[11], &p[12], &in);
-    m |= in << 2;
-    p[13] = gr_obst_cc(ox, oy, 0.0f, e0);
-    p[14] = gr_obst_inv(p[13]);
-  } else if (kind == GR_OBST_SPHERE) {
-    p[9] = ox;
-    p[10] = oy;
-    p[11] = oz;
-    p[12] = gr_obst_cc(ox, oy, oz, e0);
-    p[13] = gr_obst_inv(p[12]);
-  } else {
-    p[9] = ox;
-    p[10] = oy;
-    p[11] = oz;
-    p[12] = e0;
-    p[13] = e2;
-  }
-  p[15] = (float)(kind + 8 * m);
-}
-
-/* first surface crossing (s > 0) of the pixel ray (a, b) with the packed obstacle p: from outside the entry,
- * from inside the exit (a mesh ray cast reports the first face it crosses).  The capsule is the union of its
- * cylinder and two end spheres: the nearest of their crossings (the largest u). */
-GR_HD float gr_cam_obst_hit_p(const float* p, float a, float b) {
-  const float d0 = gr_fmaf(b, p[6], gr_fmaf(a, p[3], p[0])), d1 = gr_fmaf(b, p[7], gr_fmaf(a, p[4], p[1])),
-              d2 = gr_fmaf(b, p[8], gr_fmaf(a, p[5], p[2]));
-  const int code = (int)p[15], kind = code & 7, m = code >> 3;
-  float uin = GR_U_NONE, uout = 0.0f, u = 0.0f;
-  if (kind == GR_OBST_BOX) {
-    gr_u_slab(d0, p[9], p[12], m & 1, &uin, &uout);
-    gr_u_slab(d1, p[10], p[13], m & 2, &uin, &uout);
-    gr_u_slab(d2, p[11], p[14], m & 4, &uin, &uout);
-    u = gr_u_first(uin, uout);
-  } else if (kind == GR_OBST_CYLINDER) {
-    gr_u_slab(d2, p[11], p[12], m & 4, &uin, &uout);
-    if (gr_u_quad(d0 * d0 + d1 * d1, p[9] * d0 + p[10] * d1, p[13], p[14], &uin, &uout)) u = gr_u_first(uin, uout);
-  } else if (kind == GR_OBST_SPHERE) {
-    const float A = (d0 * d0 + d1 * d1) + d2 * d2, Bh = (p[9] * d0 + p[10] * d1) + p[11] * d2;
-    if (gr_u_quad(A, Bh, p[12], p[13], &uin, &uout)) u = gr_u_first(uin, uout);
-  } else {
-    const float ox = p[9], oy = p[10], oz = p[11], e0 = p[12], e2 = p[13];
-    float cE, cX;
-    int in = 0;
-    gr_obst_slab_prep(oz, e2, &cE, &cX, &in);
-    gr_u_slab(d2, cE, cX, in, &uin, &uout);
-    const float A = d0 * d0 + d1 * d1, Bh = ox * d0 + oy * d1, cc = gr_obst_cc(ox, oy, 0.0f, e0);
-    if (gr_u_quad(A, Bh, cc, gr_obst_inv(cc), &uin, &uout)) u = gr_u_first(uin, uout);
-    const float A3 = A + d2 * d2, zt = oz - e2, zb = oz - (-e2);
-    const float ct = gr_obst_cc(ox, oy, zt, e0), cb = gr_obst_cc(ox, oy, zb, e0);
-    float ui = GR_U_NONE, uo = 0.0f;
-    if (gr_u_quad(A3, Bh + zt * d2, ct, gr_obst_inv(ct), &ui, &uo)) u = gr_maxf(u, gr_u_first(ui, uo));
-    ui = GR_U_NONE;
-    uo = 0.0f;
-    if (gr_u_quad(A3, Bh + zb * d2, cb, gr_obst_inv(cb), &ui, &uo)) u = gr_maxf(u, gr_u_first(ui, uo));
-  }
-  return u > 0.0f ? 1.0f / u : 3.0e38f;
-}
-
-GR_HD float gr_cam_obst_hit(const float* s, float a, float b) {
-  float p[GR_OP_N];
-  gr_cam_obst_pack(s, p);
-  return gr_cam_obst_hit_p(p, a, b);
-}
-
 #endif /* GR_OBSTACLES_H */
