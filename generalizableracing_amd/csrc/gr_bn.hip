@@ -454,6 +454,7 @@ constexpr int SM_IMG_CAP = 8192;  // image floats staged in LDS per workgroup
 constexpr int SM_GRID = 512;      // workgroups: two per CU (LDS ~73 KB each), images strided over them
 constexpr int SM_WAVES = 4;       // compute waves per workgroup; one more wave stages the next image (LDS-DMA)
 constexpr int SM_THREADS = 64 * (SM_WAVES + 1);
+constexpr int SM_U = 4;           // tiles per compute wave in flight together
 enum { SM_STATS = 0, SM_APPLY = 1, SM_BWDP = 2, SM_WGRAD = 3 };
 
 struct SmArgs {
@@ -507,7 +508,8 @@ template <int PASS, int ACT, bool V4>
 __global__ __launch_bounds__(SM_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, int cap) {
   extern __shared__ float4 sm_dyn4[];
   __shared__ int s_span;
-  __shared__ float pimg[SM_WAVES][16][17];  // SM_WGRAD: per wave, the tile's A operands [row][k] (+1: banks)
+  __shared__ float pimg[SM_WAVES][16][17];  // SM_WGRAD: per wave, the tile's A operands [row][k] (+1: banks; one
+                                            // buffer per wave: its LDS accesses complete in order)
   const int na = s.na, nbt = s.nbt, ncell = na + nbt;
   short* tab = reinterpret_cast<short*>(sm_dyn4);
   float* im0 = reinterpret_cast<float*>(sm_dyn4) + sm_tab_floats(ncell);
@@ -570,81 +572,104 @@ __global__ __launch_bounds__(SM_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, i
     if (loader) {
       if (staged && k + 1 < nmine) sm_dma_image(g + (long long)gridDim.x * s.ld, (k & 1) ? im0 : im1, span, v4);
     } else
-    for (int j = (int)w; j < T; j += SM_WAVES) {
-      int cell0, nvalid;
-      unsigned r0;
-      if (j < ta) {
-        cell0 = 16 * j;
-        nvalid = na - cell0 < 16 ? na - cell0 : 16;
-        r0 = (unsigned)b * (unsigned)na + (unsigned)cell0;
-      } else {
-        const int jj = 16 * (j - ta);
-        cell0 = na + jj;
-        nvalid = nbt - jj < 16 ? nbt - jj : 16;
-        r0 = ra + (unsigned)b * (unsigned)nbt + (unsigned)jj;
+    for (int j0 = (int)w; j0 < T; j0 += SM_WAVES * SM_U) {
+      // SM_U tiles j0 + SM_WAVES u at a time: their gathers (and gradient loads) issue before any is consumed
+      int nvalid[SM_U];
+      unsigned r0[SM_U];
+      float px[SM_U][3], gv[SM_U][4];
+#pragma unroll
+      for (int u = 0; u < SM_U; ++u) {
+        const int j = j0 + SM_WAVES * u;
+        int cell0;
+        if (j < ta) {
+          cell0 = 16 * j;
+          nvalid[u] = na - cell0 < 16 ? na - cell0 : 16;
+          r0[u] = (unsigned)b * (unsigned)na + (unsigned)cell0;
+        } else if (j < T) {
+          const int jj = 16 * (j - ta);
+          cell0 = na + jj;
+          nvalid[u] = nbt - jj < 16 ? nbt - jj : 16;
+          r0[u] = ra + (unsigned)b * (unsigned)nbt + (unsigned)jj;
+        } else {  // past the image's last tile
+          cell0 = 0;
+          nvalid[u] = 0;
+          r0[u] = 0;
+        }
+        const bool ok = (int)(l & 15) < nvalid[u];
+        const short* t = tab + (cell0 + (ok ? (int)(l & 15) : 0)) * 9;
+        float v0, v1, v2;
+        if (staged) {
+          v0 = im[t[kq]];
+          v1 = im[t[kq + 4]];
+          v2 = im[t[8]];
+        } else {
+          v0 = g[t[kq]];
+          v1 = g[t[kq + 4]];
+          v2 = g[t[8]];
+        }
+        px[u][0] = ok ? v0 : 0.0f;
+        px[u][1] = ok ? v1 : 0.0f;
+        px[u][2] = (ok && kq == 0) ? v2 : 0.0f;
+        if constexpr (PASS == SM_BWDP || PASS == SM_WGRAD) {
+          // gy of the lane's rows (0 past rows_out: those rows enter the statistics only)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const unsigned r = r0[u] + 4 * kq + v;
+            const bool live = (int)(4 * kq + v) < nvalid[u] && r < rows;
+            const float gl = q.gy[(size_t)(live ? r : 0u) * 16 + ch];
+            gv[u][v] = live ? gl : 0.0f;
+          }
+        }
       }
-      const bool ok = (int)(l & 15) < nvalid;
-      const short* t = tab + (cell0 + (ok ? (int)(l & 15) : 0)) * 9;
-      float v0, v1, v2;
-      if (staged) {
-        v0 = im[t[kq]];
-        v1 = im[t[kq + 4]];
-        v2 = im[t[8]];
-      } else {
-        v0 = g[t[kq]];
-        v1 = g[t[kq + 4]];
-        v2 = g[t[8]];
-      }
-      const float px[3] = {ok ? v0 : 0.0f, ok ? v1 : 0.0f, (ok && kq == 0) ? v2 : 0.0f};
-      const sm4 x = sm_conv(px, wb);
-      if constexpr (PASS == SM_STATS) {
-        float s0 = 0.0f, s1 = 0.0f;
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const float d = (int)(4 * kq + v) < nvalid ? x[v] - sh : 0.0f;
-          s0 += d;
-          s1 += d * d;
-        }
-        a0 += (double)s0;
-        a1 += (double)s1;
-      } else if constexpr (PASS == SM_APPLY) {
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const unsigned r = r0 + 4 * kq + v;
-          if ((int)(4 * kq + v) < nvalid && r < rows) q.y[(size_t)r * 16 + ch] = bn_act<ACT>((x[v] - mu) * is * wv + bv, q.slope);
-        }
-      } else {
-        // gy of the lane's rows (0 past rows_out: those rows enter the statistics only), gz = gy act'(z)
-        float gz[4], xh[4];
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const unsigned r = r0 + 4 * kq + v;
-          const bool live = (int)(4 * kq + v) < nvalid && r < rows;
-          const float gv = q.gy[(size_t)(live ? r : 0u) * 16 + ch];
-          xh[v] = (x[v] - mu) * is;
-          gz[v] = (live ? gv : 0.0f) * bn_dact<ACT>(xh[v] * wv + bv, q.slope);
-        }
-        if constexpr (PASS == SM_BWDP) {
+      for (int u = 0; u < SM_U; ++u) {
+        const sm4 x = sm_conv(px[u], wb);
+        if constexpr (PASS == SM_STATS) {
           float s0 = 0.0f, s1 = 0.0f;
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
-            s0 += gz[v];
-            s1 += gz[v] * xh[v];
+            const float d = (int)(4 * kq + v) < nvalid[u] ? x[v] - sh : 0.0f;
+            s0 += d;
+            s1 += d * d;
           }
           a0 += (double)s0;
           a1 += (double)s1;
-        } else {
-#pragma unroll
-          for (int c = 0; c < 3; ++c) pimg[w][l & 15][kq + 4 * c] = px[c];
-          sm4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+        } else if constexpr (PASS == SM_APPLY) {
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
-            // rows past the tile's end: their pixels (the B operand) are 0
-            const float gx = (gz[v] - mg - xh[v] * mgx) * isw;
-            acc = sm_mfma(gx, pimg[w][4 * kq + v][ch], acc);
+            const unsigned r = r0[u] + 4 * kq + v;
+            if ((int)(4 * kq + v) < nvalid[u] && r < rows)
+              q.y[(size_t)r * 16 + ch] = bn_act<ACT>((x[v] - mu) * is * wv + bv, q.slope);
           }
+        } else {
+          float gz[4], xh[4];
 #pragma unroll
-          for (int c = 0; c < 4; ++c) g4[c] += (double)acc[c];
+          for (int v = 0; v < 4; ++v) {
+            xh[v] = (x[v] - mu) * is;
+            gz[v] = gv[u][v] * bn_dact<ACT>(xh[v] * wv + bv, q.slope);
+          }
+          if constexpr (PASS == SM_BWDP) {
+            float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              s0 += gz[v];
+              s1 += gz[v] * xh[v];
+            }
+            a0 += (double)s0;
+            a1 += (double)s1;
+          } else {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) pimg[w][l & 15][kq + 4 * c] = px[u][c];
+            sm4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              // rows past the tile's end: their pixels (the B operand) are 0
+              const float gx = (gz[v] - mg - xh[v] * mgx) * isw;
+              acc = sm_mfma(gx, pimg[w][4 * kq + v][ch], acc);
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) g4[c] += (double)acc[c];
+          }
         }
       }
     }
