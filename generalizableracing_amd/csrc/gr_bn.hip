@@ -454,7 +454,7 @@ constexpr int SM_IMG_CAP = 8192;  // image floats staged in LDS per workgroup
 constexpr int SM_GRID = 512;      // workgroups: two per CU (LDS ~73 KB each), images strided over them
 constexpr int SM_WAVES = 4;       // compute waves per workgroup; one more wave stages the next image (LDS-DMA)
 constexpr int SM_THREADS = 64 * (SM_WAVES + 1);
-constexpr int SM_U = 4;           // tiles per compute wave in flight together
+constexpr int SM_U = 6;           // tiles per compute wave in flight together
 enum { SM_STATS = 0, SM_APPLY = 1, SM_BWDP = 2, SM_WGRAD = 3 };
 
 struct SmArgs {
