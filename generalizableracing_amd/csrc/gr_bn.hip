@@ -454,7 +454,10 @@ constexpr int SM_IMG_CAP = 8192;  // image floats staged in LDS per workgroup
 constexpr int SM_GRID = 512;      // workgroups: two per CU (LDS ~73 KB each), images strided over them
 constexpr int SM_WAVES = 4;       // compute waves per workgroup; one more wave stages the next image (LDS-DMA)
 constexpr int SM_THREADS = 64 * (SM_WAVES + 1);
-constexpr int SM_U = 6;           // tiles per compute wave in flight together
+// tiles per compute wave in flight together: 12 in the forward passes, 6 in the backward ones (which also hold
+// the tiles' gradient rows); measured against 4 / 6 / 12 everywhere (gpurun_out/r4q)
+template <int PASS>
+constexpr int sm_tiles() { return PASS <= 1 ? 12 : 6; }
 enum { SM_STATS = 0, SM_APPLY = 1, SM_BWDP = 2, SM_WGRAD = 3 };
 
 struct SmArgs {
@@ -559,6 +562,7 @@ __global__ __launch_bounds__(SM_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, i
   const float isw = is * wv;
   double a0 = 0.0, a1 = 0.0, g4[4] = {0.0, 0.0, 0.0, 0.0};
   const int ta = (na + 15) / 16, T = ta + (nbt + 15) / 16;
+  constexpr int U = sm_tiles<PASS>();
 
   // images b = blockIdx.x + k gridDim.x: the loader wave stages image k + 1 into the other buffer (LDS-DMA) while
   // the compute waves run image k; the barrier at the end of each image drains the DMA (s_waitcnt vmcnt(0))
@@ -572,13 +576,13 @@ __global__ __launch_bounds__(SM_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, i
     if (loader) {
       if (staged && k + 1 < nmine) sm_dma_image(g + (long long)gridDim.x * s.ld, (k & 1) ? im0 : im1, span, v4);
     } else
-    for (int j0 = (int)w; j0 < T; j0 += SM_WAVES * SM_U) {
-      // SM_U tiles j0 + SM_WAVES u at a time: their gathers (and gradient loads) issue before any is consumed
-      int nvalid[SM_U];
-      unsigned r0[SM_U];
-      float px[SM_U][3], gv[SM_U][4];
+    for (int j0 = (int)w; j0 < T; j0 += SM_WAVES * U) {
+      // U tiles j0 + SM_WAVES u at a time: their gathers (and gradient loads) issue before any is consumed
+      int nvalid[U];
+      unsigned r0[U];
+      float px[U][3], gv[U][4];
 #pragma unroll
-      for (int u = 0; u < SM_U; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int j = j0 + SM_WAVES * u;
         int cell0;
         if (j < ta) {
@@ -622,7 +626,7 @@ __global__ __launch_bounds__(SM_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, i
         }
       }
 #pragma unroll
-      for (int u = 0; u < SM_U; ++u) {
+      for (int u = 0; u < U; ++u) {
         const sm4 x = sm_conv(px[u], wb);
         if constexpr (PASS == SM_STATS) {
           float s0 = 0.0f, s1 = 0.0f;
