@@ -23,6 +23,7 @@ camera.  Multi-rank runs report the headline step only.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -750,6 +751,24 @@ def main():
     if want(a, "regen"):
         extra["terrain_regeneration"] = regeneration_cost(device, n)
         progress("terrain_regeneration")
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    if want(a, "camera"):
+        # (before the training legs: measured in the same clean state as the headline, not after 65 536-env training)
+        gc.collect()
+        torch.cuda.empty_cache()
+        # SURVEY §8f next-1: the depth camera of the vision task (separate kernel, same env shard size)
+        import bench_camera
+
+        for key, obst in (("vision_camera", False), ("vision_camera_with_obstacles", True)):
+            cam = bench_camera.run(n, steps=24, warmup=4, device=device, obstacles=obst)
+            progress(key)
+            extra[key] = {
+                "kernel": cam["kernel"], "image": cam["image"], "render_fraction": cam["render_fraction"],
+                "ms_per_call": cam["ms_avg_call"], "ms_render_call": cam["ms_render_call"],
+                "ms_reuse_call": cam["ms_reuse_call"], "achieved_GBps": cam["gbs_avg"], "peak_GBps": HBM_PEAK_GBS,
+                "frac": cam["hbm_frac_avg"],
+                "bytes_per_env_call": [cam["bytes_per_env_render"], cam["bytes_per_env_reuse"]],
+                "env_steps_per_s_step_plus_camera": cam["wall_env_steps_per_s_step_plus_camera"]}
     if want(a, "train4096"):
         extra["train_total_fps_4096_envs"] = train_fps(device)
         extra["train_total_fps_4096_envs_graph_update"] = train_fps(device, graph_update=True)
@@ -775,21 +794,6 @@ def main():
                                                                 graph_update=True, bf16_update=True),
             "note": "Perf/total_fps, PPO 5 epochs x 4 mini-batches per 24-step rollout, obstacle tracks; the step "
                     "kernel writes the rollout storage rows (obs sink) unless marked no_obs_sink"}
-    sys.path.insert(0, os.path.join(ROOT, "scripts"))
-    if want(a, "camera"):
-        # SURVEY §8f next-1: the depth camera of the vision task (separate kernel, same env shard size)
-        import bench_camera
-
-        for key, obst in (("vision_camera", False), ("vision_camera_with_obstacles", True)):
-            cam = bench_camera.run(n, steps=24, warmup=4, device=device, obstacles=obst)
-            progress(key)
-            extra[key] = {
-                "kernel": cam["kernel"], "image": cam["image"], "render_fraction": cam["render_fraction"],
-                "ms_per_call": cam["ms_avg_call"], "ms_render_call": cam["ms_render_call"],
-                "ms_reuse_call": cam["ms_reuse_call"], "achieved_GBps": cam["gbs_avg"], "peak_GBps": HBM_PEAK_GBS,
-                "frac": cam["hbm_frac_avg"],
-                "bytes_per_env_call": [cam["bytes_per_env_render"], cam["bytes_per_env_reuse"]],
-                "env_steps_per_s_step_plus_camera": cam["wall_env_steps_per_s_step_plus_camera"]}
     if want(a, "vision"):
         # the reference's registered recipe end to end: depth camera + VisionActorCritic + PPOL2C2 (fused BN stem)
         import bench_vision
