@@ -16,6 +16,8 @@
 // order — deterministic, no atomics, graph-capturable.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "../../include/gr.h"
 #include "gr_kernels.h"
 
@@ -575,107 +577,130 @@ __global__ __launch_bounds__(SM_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, i
     const float* im = (k & 1) ? im1 : im0;
     if (loader) {
       if (staged && k + 1 < nmine) sm_dma_image(g + (long long)gridDim.x * s.ld, (k & 1) ? im0 : im1, span, v4);
-    } else
-    for (int j0 = (int)w; j0 < T; j0 += SM_WAVES * U) {
-      // U tiles j0 + SM_WAVES u at a time: their gathers (and gradient loads) issue before any is consumed
-      int nvalid[U];
-      unsigned r0[U];
-      float px[U][3], gv[U][4];
+    } else {
+      // one instantiation per source, so the gathers stay ds_read (LDS) or global_load: a pointer chosen at run time
+      // between the two became flat loads with full waits
+      auto tiles = [&](auto from_lds) {
+      for (int j0 = (int)w; j0 < T; j0 += SM_WAVES * U) {
+        // U tiles j0 + SM_WAVES u at a time: their gathers (and gradient loads) issue before any is consumed
+        int nvalid[U];
+        unsigned r0[U];
+        float px[U][3], gv[U][4];
+        int po[U][3];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int j = j0 + SM_WAVES * u;
-        int cell0;
-        if (j < ta) {
-          cell0 = 16 * j;
-          nvalid[u] = na - cell0 < 16 ? na - cell0 : 16;
-          r0[u] = (unsigned)b * (unsigned)na + (unsigned)cell0;
-        } else if (j < T) {
-          const int jj = 16 * (j - ta);
-          cell0 = na + jj;
-          nvalid[u] = nbt - jj < 16 ? nbt - jj : 16;
-          r0[u] = ra + (unsigned)b * (unsigned)nbt + (unsigned)jj;
-        } else {  // past the image's last tile
-          cell0 = 0;
-          nvalid[u] = 0;
-          r0[u] = 0;
-        }
-        const bool ok = (int)(l & 15) < nvalid[u];
-        const short* t = tab + (cell0 + (ok ? (int)(l & 15) : 0)) * 9;
-        float v0, v1, v2;
-        if (staged) {
-          v0 = im[t[kq]];
-          v1 = im[t[kq + 4]];
-          v2 = im[t[8]];
-        } else {
-          v0 = g[t[kq]];
-          v1 = g[t[kq + 4]];
-          v2 = g[t[8]];
-        }
-        px[u][0] = ok ? v0 : 0.0f;
-        px[u][1] = ok ? v1 : 0.0f;
-        px[u][2] = (ok && kq == 0) ? v2 : 0.0f;
-        if constexpr (PASS == SM_BWDP || PASS == SM_WGRAD) {
-          // gy of the lane's rows (0 past rows_out: those rows enter the statistics only)
+        for (int u = 0; u < U; ++u) {
+          const int j = j0 + SM_WAVES * u;
+          int cell0;
+          if (j < ta) {
+            cell0 = 16 * j;
+            nvalid[u] = na - cell0 < 16 ? na - cell0 : 16;
+            r0[u] = (unsigned)b * (unsigned)na + (unsigned)cell0;
+          } else if (j < T) {
+            const int jj = 16 * (j - ta);
+            cell0 = na + jj;
+            nvalid[u] = nbt - jj < 16 ? nbt - jj : 16;
+            r0[u] = ra + (unsigned)b * (unsigned)nbt + (unsigned)jj;
+          } else {  // past the image's last tile
+            cell0 = 0;
+            nvalid[u] = 0;
+            r0[u] = 0;
+          }
+          const bool ok = (int)(l & 15) < nvalid[u];
+          const short* t = tab + (cell0 + (ok ? (int)(l & 15) : 0)) * 9;
+          po[u][0] = t[kq];  // (all the tiles' table reads before any image read: one LDS wait, not one per tile)
+          po[u][1] = t[kq + 4];
+          po[u][2] = t[8];
+          if constexpr (PASS == SM_BWDP || PASS == SM_WGRAD) {
+            // gy of the lane's rows (0 past rows_out: those rows enter the statistics only)
 #pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            const unsigned r = r0[u] + 4 * kq + v;
-            const bool live = (int)(4 * kq + v) < nvalid[u] && r < rows;
-            const float gl = q.gy[(size_t)(live ? r : 0u) * 16 + ch];
-            gv[u][v] = live ? gl : 0.0f;
+            for (int v = 0; v < 4; ++v) {
+              const unsigned r = r0[u] + 4 * kq + v;
+              const bool live = (int)(4 * kq + v) < nvalid[u] && r < rows;
+              const float gl = q.gy[(size_t)(live ? r : 0u) * 16 + ch];
+              gv[u][v] = live ? gl : 0.0f;
+            }
           }
         }
-      }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const sm4 x = sm_conv(px[u], wb);
-        if constexpr (PASS == SM_STATS) {
-          float s0 = 0.0f, s1 = 0.0f;
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            const float d = (int)(4 * kq + v) < nvalid[u] ? x[v] - sh : 0.0f;
-            s0 += d;
-            s1 += d * d;
+        for (int u = 0; u < U; ++u) {
+          float v0, v1, v2;
+          if constexpr (decltype(from_lds)::value) {  // ds_read: the image in LDS
+            v0 = im[po[u][0]];
+            v1 = im[po[u][1]];
+            v2 = im[po[u][2]];
+          } else {
+            v0 = g[po[u][0]];
+            v1 = g[po[u][1]];
+            v2 = g[po[u][2]];
           }
-          a0 += (double)s0;
-          a1 += (double)s1;
-        } else if constexpr (PASS == SM_APPLY) {
+          // the A operand as loaded, no selects (a select let the compiler move the load under a branch, with a
+          // wait per tile): k = 9 .. 11 meet zero weights (fma(p, 0, acc) = acc for finite p), and rows past the
+          // tile's end (a clamped cell's pixels) give outputs every pass masks
+          px[u][0] = v0;
+          px[u][1] = v1;
+          px[u][2] = v2;
+        }
 #pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            const unsigned r = r0[u] + 4 * kq + v;
-            if ((int)(4 * kq + v) < nvalid[u] && r < rows)
-              q.y[(size_t)r * 16 + ch] = bn_act<ACT>((x[v] - mu) * is * wv + bv, q.slope);
-          }
-        } else {
-          float gz[4], xh[4];
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            xh[v] = (x[v] - mu) * is;
-            gz[v] = gv[u][v] * bn_dact<ACT>(xh[v] * wv + bv, q.slope);
-          }
-          if constexpr (PASS == SM_BWDP) {
+        for (int u = 0; u < U; ++u) {
+          const sm4 x = sm_conv(px[u], wb);
+          if constexpr (PASS == SM_STATS) {
             float s0 = 0.0f, s1 = 0.0f;
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
-              s0 += gz[v];
-              s1 += gz[v] * xh[v];
+              const float d = (int)(4 * kq + v) < nvalid[u] ? x[v] - sh : 0.0f;
+              s0 += d;
+              s1 += d * d;
             }
             a0 += (double)s0;
             a1 += (double)s1;
-          } else {
-#pragma unroll
-            for (int c = 0; c < 3; ++c) pimg[w][l & 15][kq + 4 * c] = px[u][c];
-            sm4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+          } else if constexpr (PASS == SM_APPLY) {
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
-              // rows past the tile's end: their pixels (the B operand) are 0
-              const float gx = (gz[v] - mg - xh[v] * mgx) * isw;
-              acc = sm_mfma(gx, pimg[w][4 * kq + v][ch], acc);
+              const unsigned r = r0[u] + 4 * kq + v;
+              if ((int)(4 * kq + v) < nvalid[u] && r < rows)
+                q.y[(size_t)r * 16 + ch] = bn_act<ACT>((x[v] - mu) * is * wv + bv, q.slope);
             }
+          } else {
+            float gz[4], xh[4];
 #pragma unroll
-            for (int c = 0; c < 4; ++c) g4[c] += (double)acc[c];
+            for (int v = 0; v < 4; ++v) {
+              xh[v] = (x[v] - mu) * is;
+              gz[v] = gv[u][v] * bn_dact<ACT>(xh[v] * wv + bv, q.slope);
+            }
+            if constexpr (PASS == SM_BWDP) {
+              float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+              for (int v = 0; v < 4; ++v) {
+                s0 += gz[v];
+                s1 += gz[v] * xh[v];
+              }
+              a0 += (double)s0;
+              a1 += (double)s1;
+            } else {
+#pragma unroll
+              for (int c = 0; c < 3; ++c) {
+              // the B operand: the tile's pixels, 0 past its rows and for k >= 9
+              const bool okc = (int)(l & 15) < nvalid[u] && (c < 2 || kq == 0);
+              pimg[w][l & 15][kq + 4 * c] = okc ? px[u][c] : 0.0f;
+            }
+              sm4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+              for (int v = 0; v < 4; ++v) {
+                // rows past the tile's end: their pixels (the B operand) are 0
+                const float gx = (gz[v] - mg - xh[v] * mgx) * isw;
+                acc = sm_mfma(gx, pimg[w][4 * kq + v][ch], acc);
+              }
+#pragma unroll
+              for (int c = 0; c < 4; ++c) g4[c] += (double)acc[c];
+            }
           }
         }
       }
+      };
+      if (staged)
+        tiles(std::true_type{});
+      else
+        tiles(std::false_type{});
     }
     __syncthreads();  // image k read, image k + 1 staged
   }
