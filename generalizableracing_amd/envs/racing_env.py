@@ -296,7 +296,8 @@ class RacingEnv:
         # it starts the next build, not here: no host free in the interval step (nor in its graph capture)
         self._retired.append((getattr(self, "track_gates", None), getattr(self, "track_records", None),
                               getattr(self, "obstacle_table", None), pin))
-        self.track_gates, self.track_records = torch.from_numpy(gates), torch.from_numpy(recs)
+        self.track_gates = gates if torch.is_tensor(gates) else torch.from_numpy(gates)
+        self.track_records = recs if torch.is_tensor(recs) else torch.from_numpy(recs)
         self.obstacle_table = obst
         self.obstacles = None
 
@@ -323,6 +324,7 @@ class RacingEnv:
             pin = self._pinned_set(g % 2, gates, recs, obst)
             if pin is None:  # larger than the reservation: staged again by the interval step (_stage_now)
                 return g, gates, recs, obst, None, None, _abi.GR_ERR_CAPACITY
+            gates, recs = torch.from_numpy(gates), torch.from_numpy(recs)  # (the env's track_gates / records, here)
             with torch.cuda.stream(side):
                 side.wait_event(after)
                 rc = self._stage(pin, obst, side.cuda_stream)
@@ -380,8 +382,9 @@ class RacingEnv:
             _stamp("result")
             assert g_built == g
             if rc == 0:
-                # (under a graph capture no event may be touched: the caller has synchronised the upload)
-                if not torch.cuda.is_current_stream_capturing():
+                # (under a graph capture no event may be touched: the caller has synchronised the upload; an upload
+                # that has completed — the usual case, half an interval later — needs no stream dependency)
+                if not torch.cuda.is_current_stream_capturing() and not done.query():
                     torch.cuda.current_stream(self.device).wait_event(done)
                 _stamp("wait_event")
                 staged = (gates, recs, obst, pin)
