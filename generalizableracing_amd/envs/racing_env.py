@@ -330,6 +330,7 @@ class RacingEnv:
                 rc = self._stage(pin, obst, side.cuda_stream)
                 done = torch.cuda.Event()
                 done.record(side)
+            done.synchronize()  # (on this thread: the interval step then finds the upload complete, no stream wait)
             return g, gates, recs, obst, pin, done, rc
 
         self._next_terrain = self._builder.submit(work)
@@ -369,10 +370,10 @@ class RacingEnv:
         """EventCfg.reset_terrain -> reset_terrain_period (mdp/events.py:180-204): a new terrain
         (next seed of this shard's stream), then env.reset() of every env.
 
-        The builder staged the generation ahead (validated on the host, uploaded on the side stream); here the
-        env's stream waits for that upload and commits it (gr_terrain_commit: one kernel with fixed arguments), so
-        the interval step is gr_terrain_commit + gr_reset + gr_observe, graph-capturable.  The host only waits for
-        the builder if the interval was shorter than a build.  Under a graph capture the staged generation must
+        The builder staged the generation ahead (validated on the host, uploaded on the side stream, its completion
+        awaited on the builder thread); here the env's stream commits it (gr_terrain_commit: one kernel with fixed
+        arguments), so the interval step is gr_terrain_commit + gr_reset + gr_observe, graph-capturable.  The host
+        only waits for the builder if the interval was shorter than a build and its upload.  Under a graph capture the staged generation must
         be complete already (a replay commits whatever was staged last)."""
         g = self.terrain_generation + 1
         staged = None
@@ -382,10 +383,8 @@ class RacingEnv:
             _stamp("result")
             assert g_built == g
             if rc == 0:
-                # (under a graph capture no event may be touched: the caller has synchronised the upload; an upload
-                # that has completed — the usual case, half an interval later — needs no stream dependency)
-                if not torch.cuda.is_current_stream_capturing() and not done.query():
-                    torch.cuda.current_stream(self.device).wait_event(done)
+                # the builder waited for its upload before returning: the staged arrays are complete, so the stream
+                # needs no dependency on it (and under a graph capture no event may be touched)
                 _stamp("wait_event")
                 staged = (gates, recs, obst, pin)
             elif rc != _abi.GR_ERR_CAPACITY:
