@@ -65,28 +65,20 @@ DEV_INLINE void state_terms(const CamArgs& a, int i, int lane, size_t row) {
   }
 }
 
-// the quads before the first 128-byte line of an observation row's image: the rows are 27 712 B apart, so every
-// other row's image starts half-way into a line.  The obs rows are written in 64-quad chunks that start on a line
-// (lane l of chunk k: quad sh - 64 + 64 k + l), so each non-temporal store instruction covers 8 whole lines rather
-// than 9 with two halves (the partial lines had cost ~13 % extra HBM writes)
-DEV_INLINE int row_line_shift(const float4* row4) { return (8 - (int)((reinterpret_cast<uintptr_t>(row4) >> 4) & 7)) & 7; }
-
 // sensor up to date: stream the depth buffer into both rows, CAM_BATCH loads in flight per lane
 DEV_INLINE void reuse_rows(const CamArgs& a, const gr_cam_const* __restrict__ cc, const float4* dep4, float4* op4,
                            float4* oc4, int nq, int lane, uint32_t gid, uint32_t cnt) {
-  // chunks start at quad sh - 64 (the first one writes only the head quads 0 .. sh - 1)
-  const unsigned unq = (unsigned)nq;
-  for (int q0 = row_line_shift(op4) - 64; q0 < nq; q0 += 64 * CAM_BATCH) {
+  for (int q0 = 0; q0 < nq; q0 += 64 * CAM_BATCH) {
     float4 dd[CAM_BATCH];
 #pragma unroll
     for (int j = 0; j < CAM_BATCH; ++j) {
-      const unsigned q = (unsigned)(q0 + 64 * j + lane);
-      dd[j] = q < unq ? dep4[q] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      const int q = q0 + 64 * j + lane;
+      dd[j] = q < nq ? dep4[q] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
 #pragma unroll
     for (int j = 0; j < CAM_BATCH; ++j) {
-      const unsigned q = (unsigned)(q0 + 64 * j + lane);
-      if (q < unq) emit_quad(a, cc, op4, oc4, (int)q, dd[j], gid, cnt);
+      const int q = q0 + 64 * j + lane;
+      if (q < nq) emit_quad(a, cc, op4, oc4, q, dd[j], gid, cnt);
     }
   }
 }
@@ -297,7 +289,6 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
   // row), so a gate's screen window culls whole tiles; the band is staged in LDS and written out in
   // row-major order (full, contiguous 1 KB stores per wave instruction).
   const float maxd = cc->max_distance;
-  const int rsh = (8 * W / 4) % 8 == 0 ? row_line_shift(op4) : 0;  // (a band of 8 rows must start on a line quad)
   for (int v0 = 0; v0 < H; v0 += 8) {
     const int rows = H - v0 < 8 ? H - v0 : 8;
     for (int u_t = 0; u_t < W; u_t += 32) {
@@ -381,11 +372,10 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
     }
     wave_lds_sync();
     const int qb = (v0 * W) >> 2, nqb = (rows * W) >> 2;
-    for (int qq = lane; qq < nqb; qq += 64) nt_store4(dep4 + qb + qq, s_stage[qq]);
-    // the obs rows in line-aligned chunks (row_line_shift; the band starts on a quad multiple of 8)
-    for (int base = rsh - 64; base < nqb; base += 64) {
-      const unsigned qq = (unsigned)(base + lane);
-      if (qq < (unsigned)nqb) emit_quad(a, cc, op4, oc4, qb + (int)qq, s_stage[qq], gid, cnt);
+    for (int qq = lane; qq < nqb; qq += 64) {
+      const float4 d4 = s_stage[qq];
+      nt_store4(dep4 + qb + qq, d4);
+      emit_quad(a, cc, op4, oc4, qb + qq, d4, gid, cnt);
     }
     wave_lds_sync();
   }
