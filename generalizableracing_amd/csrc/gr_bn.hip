@@ -459,7 +459,7 @@ constexpr int SM_THREADS = 64 * (SM_WAVES + 1);
 // tiles per compute wave in flight together: 12 in the forward passes, 6 in the backward ones (which also hold
 // the tiles' gradient rows); measured against 4 / 6 / 12 everywhere (gpurun_out/r4q)
 template <int PASS>
-constexpr int sm_tiles() { return PASS <= 1 ? 12 : 4; }
+constexpr int sm_tiles() { return PASS <= 1 ? 12 : 6; }
 enum { SM_STATS = 0, SM_APPLY = 1, SM_BWDP = 2, SM_WGRAD = 3 };
 
 struct SmArgs {
@@ -569,43 +569,6 @@ __global__ __launch_bounds__(SM_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, i
   // images b = blockIdx.x + k gridDim.x: the loader wave stages image k + 1 into the other buffer (LDS-DMA) while
   // the compute waves run image k; the barrier at the end of each image drains the DMA (s_waitcnt vmcnt(0))
   const int nmine = s.nimg > (int)blockIdx.x ? (s.nimg - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
-  // tile j of image b: its first table cell, its rows, its first global row
-  auto geom = [&](int b, int j, int& cell0, int& nvalid, unsigned& r0) {
-    if (j < ta) {
-      cell0 = 16 * j;
-      nvalid = na - cell0 < 16 ? na - cell0 : 16;
-      r0 = (unsigned)b * (unsigned)na + (unsigned)cell0;
-    } else if (j < T) {
-      const int jj = 16 * (j - ta);
-      cell0 = na + jj;
-      nvalid = nbt - jj < 16 ? nbt - jj : 16;
-      r0 = ra + (unsigned)b * (unsigned)nbt + (unsigned)jj;
-    } else {  // past the image's last tile
-      cell0 = 0;
-      nvalid = 0;
-      r0 = 0;
-    }
-  };
-  // the backward passes' gradient rows of a group of tiles (0 past rows_out: those rows enter the statistics only),
-  // loaded one group ahead of their use
-  float gvn[U][4];
-  auto load_gy = [&](int b, int j0) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      int cell0, nv;
-      unsigned r0;
-      geom(b, j0 + SM_WAVES * u, cell0, nv, r0);
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const unsigned r = r0 + 4 * kq + v;
-        const bool live = (int)(4 * kq + v) < nv && r < rows;
-        const float gl = q.gy[(size_t)(live ? r : 0u) * 16 + ch];
-        gvn[u][v] = live ? gl : 0.0f;
-      }
-    }
-  };
-  if constexpr (PASS == SM_BWDP || PASS == SM_WGRAD)
-    if (!loader && nmine > 0) load_gy((int)blockIdx.x, (int)w);
   if (staged && loader && nmine > 0) sm_dma_image(s.obs + (long long)blockIdx.x * s.ld + s.off, im0, span, v4);
   __syncthreads();
   for (int k = 0; k < nmine; ++k) {
@@ -624,27 +587,39 @@ __global__ __launch_bounds__(SM_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, i
         unsigned r0[U];
         float px[U][3], gv[U][4];
         int po[U][3];
-        if constexpr (PASS == SM_BWDP || PASS == SM_WGRAD) {
-#pragma unroll
-          for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int v = 0; v < 4; ++v) gv[u][v] = gvn[u][v];
-          // the next group's gradient rows: this image's next tiles, or the next image's first
-          const int jn = j0 + SM_WAVES * U;
-          if (jn < T)
-            load_gy(b, jn);
-          else if (k + 1 < nmine)
-            load_gy(b + (int)gridDim.x, (int)w);
-        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
+          const int j = j0 + SM_WAVES * u;
           int cell0;
-          geom(b, j0 + SM_WAVES * u, cell0, nvalid[u], r0[u]);
+          if (j < ta) {
+            cell0 = 16 * j;
+            nvalid[u] = na - cell0 < 16 ? na - cell0 : 16;
+            r0[u] = (unsigned)b * (unsigned)na + (unsigned)cell0;
+          } else if (j < T) {
+            const int jj = 16 * (j - ta);
+            cell0 = na + jj;
+            nvalid[u] = nbt - jj < 16 ? nbt - jj : 16;
+            r0[u] = ra + (unsigned)b * (unsigned)nbt + (unsigned)jj;
+          } else {  // past the image's last tile
+            cell0 = 0;
+            nvalid[u] = 0;
+            r0[u] = 0;
+          }
           const bool ok = (int)(l & 15) < nvalid[u];
           const short* t = tab + (cell0 + (ok ? (int)(l & 15) : 0)) * 9;
           po[u][0] = t[kq];  // (all the tiles' table reads before any image read: one LDS wait, not one per tile)
           po[u][1] = t[kq + 4];
           po[u][2] = t[8];
+          if constexpr (PASS == SM_BWDP || PASS == SM_WGRAD) {
+            // gy of the lane's rows (0 past rows_out: those rows enter the statistics only)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              const unsigned r = r0[u] + 4 * kq + v;
+              const bool live = (int)(4 * kq + v) < nvalid[u] && r < rows;
+              const float gl = q.gy[(size_t)(live ? r : 0u) * 16 + ch];
+              gv[u][v] = live ? gl : 0.0f;
+            }
+          }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
