@@ -32,6 +32,9 @@ LOG_RING = 64
 REGEN_STAMPS = None
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)  # (torch's own raw-stream accessor)
+
+
 def _stamp(label):
     if REGEN_STAMPS is not None:
         REGEN_STAMPS.append((label, time.perf_counter()))
@@ -473,6 +476,10 @@ class RacingEnv:
             self._call("gr_camera_render", mode, mask_ptr, self._stream())
 
     def _stream(self):
+        # the raw handle of the device's current stream: torch.cuda.current_stream(device) builds a Stream object
+        # under a device guard on every env call (a few µs of each step's host time)
+        if _RAW_STREAM is not None and self.device.index is not None:
+            return _RAW_STREAM(self.device.index)
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def _call(self, name, *args):
