@@ -386,3 +386,20 @@ def check(lib, ctx, rc: int, what: str):
     if rc != 0:
         msg = lib.gr_last_error(ctx) if ctx else b""
         raise RuntimeError(f"{what} failed (status {rc}): {msg.decode() if msg else ''}")
+
+
+_RAW_STREAM = None
+
+
+def raw_stream(device) -> int:
+    """The raw handle of `device`'s current HIP stream for the C ABI's `stream` argument: torch's accessor when the
+    device has an index (torch.cuda.current_stream(device) builds a Stream object under a device guard per call)."""
+    global _RAW_STREAM
+    import torch
+
+    if _RAW_STREAM is None:
+        _RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", False)
+    index = device.index if isinstance(device, torch.device) else None
+    if _RAW_STREAM and index is not None:
+        return _RAW_STREAM(index)
+    return torch.cuda.current_stream(device).cuda_stream

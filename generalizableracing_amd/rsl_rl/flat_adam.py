@@ -138,7 +138,9 @@ class FlatAdam(torch.optim.Optimizer):
         return a
 
     def _stream(self):
-        return torch.cuda.current_stream(self._m.device).cuda_stream
+        from .. import _abi
+
+        return _abi.raw_stream(self._m.device)
 
     @torch.no_grad()
     def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:

@@ -31,7 +31,7 @@ def _act_code(act: nn.Module):
 
 
 def _stream(x):
-    return C.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    return C.c_void_p(_abi.raw_stream(x.device))
 
 
 class _BatchNormAct(torch.autograd.Function):

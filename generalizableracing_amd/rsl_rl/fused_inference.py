@@ -207,7 +207,7 @@ class FusedPolicyInference:
         a.num_envs, a.hidden, a.activation, a.env_id_offset = n, self.hidden, self.activation, self.env_id_offset
         a.seed_lo, a.seed_hi = self.seed & 0xFFFFFFFF, (self.seed >> 32) & 0xFFFFFFFF
         a.precision = _abi.GR_POLICY_FP32 if self.precision == "fp32" else _abi.GR_POLICY_BF16
-        rc = self._lib.gr_policy_forward(C.byref(a), C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
+        rc = self._lib.gr_policy_forward(C.byref(a), C.c_void_p(_abi.raw_stream(self.device)))
         if rc != 0:
             raise RuntimeError(f"gr_policy_forward failed (status {rc})")
         self._calls += 1

@@ -62,7 +62,7 @@ class _PPOLossFn(torch.autograd.Function):
         rows = mu.shape[0]
         part = torch.empty(_abi.load().gr_ppo_loss_partials(rows), device=mu.device, dtype=torch.float32)
         sums = torch.empty(3, device=mu.device, dtype=torch.float32)
-        stream = torch.cuda.current_stream(mu.device).cuda_stream
+        stream = _abi.raw_stream(mu.device)
         _call("gr_ppo_loss_forward", C.addressof(a), part.data_ptr(), sums.data_ptr(), stream)
         ctx.save_for_backward(mu, std, value, act, logp_old, adv, value_old, ret, mu_old, sig_old)
         ctx.clip, ctx.clipped_value = clip, clipped_value
@@ -85,7 +85,7 @@ class _PPOLossFn(torch.autograd.Function):
         dvalue = torch.empty(rows, device=dev, dtype=torch.float32)
         part = torch.empty(_abi.load().gr_ppo_loss_partials(rows), device=dev, dtype=torch.float32)
         dstd = torch.empty(k, device=dev, dtype=torch.float32)
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = _abi.raw_stream(dev)
         _call("gr_ppo_loss_backward", C.addressof(a), g.data_ptr(), dmu.data_ptr(), dvalue.data_ptr(), part.data_ptr(),
               dstd.data_ptr(), stream)
         return (dmu, dstd, dvalue.view(value.shape), None, None, None, None, None, None, None, None, None)
@@ -112,7 +112,7 @@ class _PPOLossCombinedFn(torch.autograd.Function):
         sums = torch.empty(3, device=dev, dtype=torch.float32)
         loss = torch.empty((), device=dev, dtype=torch.float32)
         stats = torch.empty(3, device=dev, dtype=torch.float32)
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = _abi.raw_stream(dev)
         accp, klp = (acc.data_ptr() if acc is not None else None), (kl_out.data_ptr() if kl_out is not None else None)
         ctx.pre = None
         if seed is not None:
@@ -153,7 +153,7 @@ class _PPOLossCombinedFn(torch.autograd.Function):
         part = torch.empty(_abi.load().gr_ppo_loss_partials(rows), device=dev, dtype=torch.float32)
         dstd = _std_sink(std, k)
         _call("gr_ppo_loss_backward_loss", C.addressof(a), g.data_ptr(), C.c_float(ctx.value_coef), dmu.data_ptr(),
-              dvalue.data_ptr(), part.data_ptr(), dstd.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+              dvalue.data_ptr(), part.data_ptr(), dstd.data_ptr(), _abi.raw_stream(dev))
         return (dmu, dstd, dvalue.view(value.shape)) + (None,) * 13
 
 

@@ -57,7 +57,7 @@ def bias_grad(gy: torch.Tensor) -> torch.Tensor:
     part = torch.empty(lib.gr_column_sum_partials(m) * n, device=gy.device, dtype=torch.float32)
     out = torch.empty(n, device=gy.device, dtype=torch.float32)
     rc = lib.gr_column_sum(gy.data_ptr(), dtype, m, n, part.data_ptr(), out.data_ptr(),
-                           torch.cuda.current_stream(gy.device).cuda_stream)
+                           _abi.raw_stream(gy.device))
     if rc != 0:
         raise RuntimeError(f"gr_column_sum failed (status {rc})")
     return out
@@ -131,7 +131,9 @@ def _lib_call(name, *args):
 
 
 def _stream(t):
-    return torch.cuda.current_stream(t.device).cuda_stream
+    from .. import _abi
+
+    return _abi.raw_stream(t.device)
 
 
 def _head_backward(z, gy, w, slope):

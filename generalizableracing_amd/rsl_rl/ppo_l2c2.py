@@ -49,7 +49,7 @@ def _mix(obs, next_obs, w):
         w = w.reshape(-1).float().contiguous()
         out = torch.empty_like(obs)
         rc = _abi.load().gr_l2c2_mix(obs.data_ptr(), next_obs.data_ptr(), w.data_ptr(), obs.shape[0], obs.shape[1],
-                                     out.data_ptr(), torch.cuda.current_stream(obs.device).cuda_stream)
+                                     out.data_ptr(), _abi.raw_stream(obs.device))
         if rc != 0:
             raise RuntimeError(f"gr_l2c2_mix failed (status {rc})")
         return out

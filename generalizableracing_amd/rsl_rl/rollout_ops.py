@@ -39,7 +39,9 @@ def _call(name, *args):
 
 
 def _stream(t):
-    return torch.cuda.current_stream(t.device).cuda_stream
+    from .. import _abi
+
+    return _abi.raw_stream(t.device)
 
 
 def _flags_ok(t, n) -> bool:
