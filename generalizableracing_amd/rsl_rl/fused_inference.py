@@ -135,11 +135,17 @@ class FusedPolicyInference:
         self.env_id_offset = int(env_id_offset)
         self._packed = {}
         self._version = None
+        self._plist = None
         self.refresh()
 
     def _params(self):
-        ps = list(self.policy.actor.parameters()) + list(self.policy.critic.parameters())
-        return ps + [self.policy.std if self.policy.noise_std_type == "scalar" else self.policy.log_std]
+        # (collected once per packing: walking the module tree on every act call cost ~20 us of host time per step at
+        # 4 096 envs.  Optimizers, load_state_dict and FlatAdam write the parameters in place, which the version
+        # tuple sees; a module whose Parameter objects are replaced needs an explicit refresh())
+        if self._plist is None:
+            ps = list(self.policy.actor.parameters()) + list(self.policy.critic.parameters())
+            self._plist = ps + [self.policy.std if self.policy.noise_std_type == "scalar" else self.policy.log_std]
+        return self._plist
 
     def _param_version(self):
         # torch bumps a tensor's version on every in-place write (optimizer.step, load_state_dict, copy_)
@@ -165,6 +171,7 @@ class FusedPolicyInference:
                     self._packed[key] = v.clone()  # never an alias of the module's parameter
         std = self.policy.std if self.policy.noise_std_type == "scalar" else torch.exp(self.policy.log_std)
         self.std.copy_(std.detach().float())
+        self._plist = None  # (re-collected: a repack also follows a replaced parameter)
         self._version = self._param_version()
 
     def _pack_bf16(self, lin):
