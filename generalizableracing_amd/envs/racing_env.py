@@ -721,7 +721,7 @@ class RacingEnv:
             self._sink = None
             self._sink_out = None
             self._cam_sink_out = None
-            self._call("gr_bind_obs_sink", None, None, _abi.GR_DTYPE_F32)
+            self._bind_obs_sink(None, None, _abi.GR_DTYPE_F32)
             return
         width = self.num_obs
         dtypes = (torch.float32,) if self.camera is not None else (torch.float32, torch.bfloat16)
@@ -740,12 +740,20 @@ class RacingEnv:
             # fp32: the tensors ARE the calls' observation output (the rows are written once; the calls return
             # these tensors), rollout_storage.py:74-88's copy with no second write
             self._sink_out = (policy, critic)
-            self._call("gr_bind_obs_sink", None, None, _abi.GR_DTYPE_F32)
+            self._bind_obs_sink(None, None, _abi.GR_DTYPE_F32)
             return
         # bf16: the fp32 rows stay the output (the rollout inference reads them) and the kernel also writes the
         # rounded rows into the slot
         self._sink_out = None
-        self._call("gr_bind_obs_sink", policy.data_ptr(), critic.data_ptr(), _abi.GR_DTYPE_BF16)
+        self._bind_obs_sink(policy.data_ptr(), critic.data_ptr(), _abi.GR_DTYPE_BF16)
+
+    def _bind_obs_sink(self, p, c, dtype):
+        """gr_bind_obs_sink unless the context already holds exactly this binding (an fp32 sink rebinds nothing
+        per step: its tensors are the calls' outputs, set in _bind)."""
+        state = (p, c, dtype)
+        if getattr(self, "_obs_sink_state", None) != state:
+            self._call("gr_bind_obs_sink", p, c, dtype)
+            self._obs_sink_state = state
 
     def observe(self) -> dict:
         """ObservationManager.compute(): fresh observation noise, no state change."""
