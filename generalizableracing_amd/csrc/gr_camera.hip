@@ -332,9 +332,24 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
     }
     if constexpr (obst) {
       // the obstacles of the LDS slots, per tile of the band: only the pixels inside a slot's window (a column
-      // range times a row range: a_u and b_v are monotonic), packed onto the lanes (one hit per lane and pass)
-      // and min-ed into the staged band (clip(min) = min(clip): the clip is monotonic)
-      float* st = reinterpret_cast<float*>(s_stage);
+      // range times a row range: a_u and b_v are monotonic), packed onto the lanes across slots and tiles of
+      // the band (one hit per lane and batch of 64 pixels) and min-ed into the staged band (clip(min) =
+      // min(clip): the clip is monotonic). Two slots of one batch may share a pixel, so the min is an LDS
+      // integer atomic: a hit is > 0 and never NaN, the staged depth is clipped (not NaN), so the signed
+      // order of the bit patterns is the float order of the pairs compared and the result is the sequential
+      // min's bits whatever the order
+      int* sti = reinterpret_cast<int*>(s_stage);
+      int fill = 0;                      // lanes holding a pixel of the current batch (wave-uniform)
+      int my_k = 0, my_u = 0, my_r = 0;  // this lane's slot, column and band row
+      auto batch = [&](int nfill) {
+        if (lane < nfill) {
+          float s[GR_CAM_SLOT];
+          load_oslot(s_oslot + my_k * (GR_CAM_OSLOT / 4), s);
+          const float h = gr_cam_clip(gr_cam_obst_hit(s, s_ray_a[my_u], s_ray_b[v0 + my_r]), maxd);
+          __hip_atomic_fetch_min(sti + my_r * W + my_u, __float_as_int(h), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WAVEFRONT);
+        }
+      };
       wave_lds_sync();
       for (int u_t = 0; u_t < W; u_t += 32) {
         uint64_t mo = s_tmask[(v0 >> 3) * ntx + (u_t >> 5)];
@@ -355,20 +370,26 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
           if (cm == 0u || rm == 0u) continue;
           const int cu = u_t + __builtin_ctz(cm), wc = __popc(cm), rv = __builtin_ctz(rm), area = wc * __popc(rm);
           const float inv_wc = 1.0f / (float)wc;
-          float s[GR_CAM_SLOT];
-          load_oslot(s_oslot + k * (GR_CAM_OSLOT / 4), s);
-          for (int base = 0; base < area; base += 64) {
-            const int idx = base + lane;
-            if (idx < area) {
+          for (int done = 0; done < area;) {
+            const int take = area - done < 64 - fill ? area - done : 64 - fill;
+            if (lane >= fill && lane < fill + take) {
               // idx / wc exactly for idx < 256, wc <= 32 (the fraction of a non-integer quotient is <= 31/32)
-              const int r = (int)((float)idx * inv_wc + 1.0e-3f), c = idx - r * wc;
-              const int u = cu + c, pix = (rv + r) * W + u;
-              const float h = gr_cam_clip(gr_cam_obst_hit(s, s_ray_a[u], s_ray_b[v0 + rv + r]), maxd);
-              st[pix] = gr_minf(st[pix], h);
+              const int idx = done + lane - fill;
+              const int r = (int)((float)idx * inv_wc + 1.0e-3f);
+              my_k = k;
+              my_u = cu + idx - r * wc;
+              my_r = rv + r;
+            }
+            fill += take;
+            done += take;
+            if (fill == 64) {
+              batch(64);
+              fill = 0;
             }
           }
         }
       }
+      if (fill) batch(fill);
     }
     wave_lds_sync();
     const int qb = (v0 * W) >> 2, nqb = (rows * W) >> 2;
