@@ -4,6 +4,10 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+The first form with N > 1 starts the second itself, as a child process (launch_ranks).  Under
+torch.distributed.run, --gpus must equal WORLD_SIZE, and with the nccl (RCCL) backend every rank
+must own a distinct GPU; anything else exits non-zero rather than print a line for another world.
+
 A "step" is one pass of the hot path (ManagerBasedDiffRLEnv.step equivalent:
 action processing, CTBR controller, integrator, collision, gate progress,
 reward, termination, in-lane reset, observation, log reduction) over all envs
@@ -26,12 +30,40 @@ import argparse
 import gc
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
+
+def launch_ranks(argv) -> int | None:
+    """`python bench.py --gpus N` with N > 1 outside torch.distributed.run: start the N ranks ourselves, one per
+    GPU, as `python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ... bench.py
+    <the same arguments>` in a CHILD process, and return its exit status.  Rank 0's JSON line reaches our stdout
+    (inherited).  Called before torch or the package is imported, so this process never touches the GPU (no
+    exec, the launcher is a child).  Returns None when there is nothing to launch (N == 1, or already a rank)."""
+    p = argparse.ArgumentParser(add_help=False)
+    p.add_argument("--gpus", type=int, default=None)
+    known, _ = p.parse_known_args(argv)
+    if known.gpus is None or known.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(known.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    print(f"[bench] launching {known.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+
+
+if __name__ == "__main__":
+    _rc = launch_ranks(sys.argv[1:])
+    if _rc is not None:
+        sys.exit(_rc)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -51,7 +83,9 @@ STREAM_FLOOR_US = 5.15  # 65 536 envs: the step's own bytes as a pure stream (DE
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="number of GPUs = ranks; N > 1 outside torch.distributed.run launches the N ranks itself "
+                        "(launch_ranks); under torch.distributed.run it must equal WORLD_SIZE")
     p.add_argument("--steps", type=int, default=1024)
     p.add_argument("--warmup", type=int, default=64)
     p.add_argument("--num-envs", type=int, default=65536)
@@ -583,7 +617,14 @@ def main():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.dist_backend != "nccl":  # rehearsal: ranks may share a device
+    # a line must describe what ran: --gpus is the rank count, and with RCCL every rank owns a GPU of its own
+    if a.gpus is not None and a.gpus != ws:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={ws} (run `python bench.py --gpus N` to launch "
+                         f"N ranks, or torch.distributed.run --nproc-per-node N ... --gpus N)")
+    if a.dist_backend == "nccl":
+        if ws > 1 and torch.cuda.device_count() < ws:
+            raise SystemExit(f"bench.py: {ws} RCCL ranks need {ws} GPUs, {torch.cuda.device_count()} visible")
+    else:  # rehearsal: ranks may share a device
         local = local % max(1, torch.cuda.device_count())
     if ws > 1:
         # the scaling lines report the headline step only: the extras (policy, training, camera, sweep legs)
@@ -628,9 +669,12 @@ def main():
               "timed_region_s": local_secs}
         ranks = [None] * ws
         dist.all_gather_object(ranks, me)
+        distinct = len({(r["pci"], r["uuid"], r["current_device"]) for r in ranks})
+        if dist.get_backend() == "nccl" and distinct != ws:
+            raise SystemExit(f"bench.py: {ws} RCCL ranks ran on {distinct} distinct devices: {ranks}")
         extra["distributed"] = {
             "world_size": ws, "backend": dist.get_backend(), "ranks": ranks,
-            "distinct_devices": len({(r["pci"], r["uuid"], r["current_device"]) for r in ranks}),
+            "distinct_devices": distinct,
             "grad_allreduce_bytes": GRAD_ALLREDUCE_NUMEL * 4,
             "grad_allreduce_median_us": allreduce_latency_us(device),
             "note": "value = world_size x envs x steps / max over ranks of the timed region; ranks[i].env_steps_per_s "

@@ -58,6 +58,7 @@ struct gr_ctx {
     int32_t hdr_host[4] = {0, 0, 0, 0};
   } res;
   std::mutex err_mu;  // gr_terrain_stage may fail on another host thread
+  int64_t terrain_epoch = 0;  // gr_terrain_reserve calls: each one moves the terrain arrays a graph may have baked in
 };
 
 #define GR_TIMING_RING 4096
@@ -296,7 +297,16 @@ int gr_destroy(gr_ctx* c) {
   return GR_OK;
 }
 
-const char* gr_last_error(const gr_ctx* c) { return c ? c->err.c_str() : "null context"; }
+const char* gr_last_error(const gr_ctx* c) {
+  if (!c) return "null context";
+  // a copy per calling thread, taken under the lock: gr_terrain_stage may set the message on the builder thread
+  thread_local std::string copy;
+  std::lock_guard<std::mutex> lk(const_cast<gr_ctx*>(c)->err_mu);
+  copy = c->err;
+  return copy.c_str();
+}
+
+int64_t gr_terrain_epoch(const gr_ctx* c) { return c ? c->terrain_epoch : GR_ERR_ARG; }
 
 int gr_num_blocks(const gr_ctx* c) { return c ? (c->cfg.num_envs + GR_BLOCK - 1) / GR_BLOCK : GR_ERR_ARG; }
 int gr_num_log_rows(const gr_ctx* c) { return c ? gr_num_blocks(c) * GR_LOG_ROWS_PER_BLOCK : GR_ERR_ARG; }
@@ -545,6 +555,7 @@ int gr_terrain_reserve(gr_ctx* c, int32_t max_obstacles, int32_t max_cells, int3
     return hip_fail(c, e, "gr_terrain_reserve: hipMalloc");
   }
   r.on = true;
+  ++c->terrain_epoch;
   bind_resident(c);  // (the contents arrive with the first commit)
   c->have_tracks = false;  // until the first commit
   return GR_OK;
@@ -1057,6 +1068,8 @@ static bool mlp_args_ok(const gr_mlp_args* a, bool bwd) {
   if (!a || a->rows <= 0 || a->nets < 1 || a->nets > 2 || (a->hidden != 128 && a->hidden != 256)) return false;
   for (int i = 0; i < a->nets; ++i) {
     const gr_mlp_net& n = a->net[i];
+    // the kernels index rows and element offsets in 32 bits (gr_mlp.hip): rows * max(H, ldx) < 2^31 (GR_MLP_MAX_ELEMS)
+    if (n.ldx > 0 && a->rows > (int64_t)GR_MLP_MAX_ELEMS / (n.ldx > a->hidden ? n.ldx : a->hidden)) return false;
     if (!n.x || !n.w1 || !n.b1 || !n.w2 || !n.b2 || !n.w3 || !n.b3 || !n.h1 || !n.z2 || n.d < 4 || n.d > 32 ||
         n.d % 4 || n.k < 1 || n.k > 4 || n.ldx < n.d || n.ldx % 4 || !aligned16(n.x) || !aligned16(n.w1) ||
         !aligned16(n.w2) || !aligned16(n.w3) || !aligned16(n.b1) || !aligned16(n.b2) || !aligned16(n.h1) ||

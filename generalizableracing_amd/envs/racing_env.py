@@ -131,6 +131,7 @@ class RacingEnv:
         # staging arrays on a side stream (gr_terrain_stage), so the interval step only commits it on the stream
         # (gr_terrain_commit: fixed arguments, graph-capturable)
         self._resident = False
+        self._captured_epoch = None  # terrain epoch of the last call captured into a graph (_call)
         self._builder = ThreadPoolExecutor(max_workers=1, thread_name_prefix="gr-terrain") \
             if self._regen_steps is not None else None
         self._next_terrain = None
@@ -258,9 +259,25 @@ class RacingEnv:
                 pin["o_" + key] = v
         return pin
 
+    @property
+    def terrain_epoch(self) -> int:
+        """gr_terrain_epoch: how often the context (re)allocated its terrain arrays.  A hipGraph captured over this
+        env's calls bakes in the arrays of the epoch it was captured in."""
+        return int(self._lib.gr_terrain_epoch(self._ctx))
+
+    def forget_captures(self):
+        """The caller destroyed every graph it captured over this env's calls: the terrain arrays may move again."""
+        self._captured_epoch = None
+
     def _reserve_terrain(self, obst):
         """gr_terrain_reserve with room for generations somewhat larger than `obst` (the generator's sizes vary by
-        ~1 % between seeds; a larger one reallocates, outside any graph)."""
+        ~1 % between seeds; a larger one reallocates, outside any graph).  Refused while a graph captured over this
+        env's calls may still be replayed (it would read the freed arrays): forget_captures() first."""
+        if self._resident and getattr(self, "_captured_epoch", None) is not None:
+            raise RuntimeError(
+                "the terrain generation outgrew its reservation, and reallocating would leave the hipGraphs captured "
+                f"over this env (terrain epoch {self._captured_epoch}) pointing at freed arrays: destroy them and call "
+                "env.forget_captures(), then regenerate again")
         if obst is None:
             caps = (0, 0, 0)
         else:
@@ -288,7 +305,20 @@ class RacingEnv:
             rc = self._stage(pin, obst, self._stream())
         if rc != 0:
             raise RuntimeError(f"gr_terrain_stage failed (status {rc}): {self._lib.gr_last_error(self._ctx).decode()}")
+        # the upload is a raw hipMemcpyAsync that torch's pinned-memory cache does not track: the set is released only
+        # after this event (_release_retired), never back into the cache while the copy may still read it
+        pin["_uploaded"] = torch.cuda.Event()
+        pin["_uploaded"].record(torch.cuda.current_stream(self.device))
         return pin
+
+    @staticmethod
+    def _release_retired(retired: list):
+        """Drop replaced generations' host objects, after the uploads from their pinned sets (if any) completed."""
+        for entry in retired:
+            pin = entry[-1]
+            if isinstance(pin, dict) and pin.get("_uploaded") is not None:
+                pin["_uploaded"].synchronize()
+        retired.clear()
 
     def _commit(self, pin, gates, recs, obst):
         """gr_terrain_commit on the env's stream; the generation's host arrays become the env's track_gates /
@@ -299,6 +329,9 @@ class RacingEnv:
         # it starts the next build, not here: no host free in the interval step (nor in its graph capture)
         self._retired.append((getattr(self, "track_gates", None), getattr(self, "track_records", None),
                               getattr(self, "obstacle_table", None), pin))
+        if len(self._retired) > 2:  # (no builder ran in between: one-step intervals, direct regenerate_terrain calls)
+            old, self._retired = self._retired[:-2], self._retired[-2:]
+            self._release_retired(old)
         self.track_gates = gates if torch.is_tensor(gates) else torch.from_numpy(gates)
         self.track_records = recs if torch.is_tensor(recs) else torch.from_numpy(recs)
         self.obstacle_table = obst
@@ -322,7 +355,7 @@ class RacingEnv:
         retired, self._retired = self._retired, []
 
         def work():
-            retired.clear()  # (the previous generations' host objects, released here)
+            self._release_retired(retired)  # (the previous generations' host objects, released here)
             gates, recs, obst = self._build_terrain(self._terrain_seed(g))
             pin = self._pinned_set(g % 2, gates, recs, obst)
             if pin is None:  # larger than the reservation: staged again by the interval step (_stage_now)
@@ -483,6 +516,8 @@ class RacingEnv:
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def _call(self, name, *args):
+        if torch.cuda.is_current_stream_capturing():  # a graph now holds this epoch's terrain arrays (_reserve_terrain)
+            self._captured_epoch = self.terrain_epoch
         rc = getattr(self._lib, name)(self._ctx, *args)
         if rc != 0:
             raise RuntimeError(f"{name} failed (status {rc}): {self._lib.gr_last_error(self._ctx).decode()}")

@@ -255,6 +255,7 @@ int gr_config_default(gr_config* cfg);
 size_t gr_config_size(void);
 int gr_create(const gr_config* cfg, gr_ctx** out);
 int gr_destroy(gr_ctx* ctx);
+/* the last error's text; safe from any host thread (a copy per calling thread, valid until its next call) */
 const char* gr_last_error(const gr_ctx* ctx);
 /* number of workgroups of the step kernel */
 int gr_num_blocks(const gr_ctx* ctx);
@@ -310,12 +311,15 @@ int gr_swap_terrain(gr_ctx* ctx, const float* gates, const float* tracks, const 
  *     table; for obstacle tracks records [T*L][max_obstacles][GR_OBST_FLOATS], counts, grids, cells [max_cells][2],
  *     items [max_items][GR_OBST_FLOATS]) and a staging copy of them, and binds the live ones (max_obstacles == 0:
  *     obstacle-free tracks).  Synchronises the device.  Called again it reallocates (the kernel arguments change:
- *     graphs captured before must be captured again).
+ *     graphs captured before must be captured again).  Each call increments the terrain epoch (gr_terrain_epoch):
+ *     a graph owner records the epoch at capture and must not replay once it changed.
  *   gr_terrain_stage: validates a generation from HOST arrays (gates / tracks as gr_bind_tracks; obst_host: every
  *     array a host pointer, max_obstacles / num_cells / num_items its sizes; NULL iff reserved obstacle-free) and
  *     uploads it into the staging arrays on `stream` (asynchronous from pinned memory).  Touches only the staging
  *     set: it may run on another host thread and stream while the env's calls run; the caller orders it after the
- *     previous gr_terrain_commit (a stream wait).  GR_ERR_CAPACITY: the generation exceeds the reservation.
+ *     previous gr_terrain_commit (a stream wait).  The only context fields it writes are the staging set, its
+ *     staged header / grid scalars (read by the next commit) and, under a lock, the error text; the caller must not
+ *     run gr_terrain_reserve, _commit or another _stage concurrently with it.  GR_ERR_CAPACITY: the generation exceeds the reservation.
  *   gr_terrain_commit: makes the last staged generation live, ordered on `stream`: one kernel copies the staged
  *     arrays over the live ones (extents from the staged header, on the device), packs the gate table and clears
  *     the per-env obstacle hints.  No host argument, check or synchronisation: capturable, and a graph replay
@@ -325,6 +329,8 @@ int gr_terrain_reserve(gr_ctx* ctx, int32_t max_obstacles, int32_t max_cells, in
 int gr_terrain_stage(gr_ctx* ctx, const float* gates_host, const float* tracks_host, const gr_obstacles* obst_host,
                      void* stream);
 int gr_terrain_commit(gr_ctx* ctx, void* stream);
+/* number of gr_terrain_reserve calls so far (0: the terrain arrays are the caller's, gr_bind_tracks) */
+int64_t gr_terrain_epoch(const gr_ctx* ctx);
 int gr_bind_buffers(gr_ctx* ctx, const gr_buffers* bufs);
 
 /* Observation sink (config C5's bf16 rollout buffers): every following gr_step / gr_reset / gr_observe also
@@ -506,7 +512,9 @@ int gr_mlp_in_backward(const float* gh, const float* hv, const float* x, int64_t
  *                    gW3 = gy^T lrelu(z2), gb3 = sum gy, gb2 = sum gz2, gW2 = gz2^T h1, gW1 = gz1^T x, gb1 = sum gz1
  * H = 128 or 256, d <= 32 (a multiple of 4), k <= 4.  Row-major fp32, 16-byte aligned; the x rows may be strided
  * (ldx floats: the update's packed mini-batch).  Context-free, graph-capturable, no atomics, fixed summation order;
- * `partial` is caller-owned scratch of gr_mlp_partials(rows, H, nets) floats. */
+ * `partial` is caller-owned scratch of gr_mlp_partials(rows, H, nets) floats.
+ * Size limit: rows * max(H, ldx) < GR_MLP_MAX_ELEMS (2^31; the kernels use 32-bit offsets), else GR_ERR_ARG. */
+#define GR_MLP_MAX_ELEMS 2147483647LL
 typedef struct gr_mlp_net {
   const float* x;    /* [rows][ldx]: the first d columns are the input */
   const float* w1;   /* [H][d] */

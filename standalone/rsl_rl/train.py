@@ -4,10 +4,13 @@ Same command line as the reference (train.sh):
 
     python standalone/rsl_rl/train.py --task DiffLab-Quadcopter-CTBR-Racing-v0 --num_envs 1024 --headless
 
+trains the reference recipe for that id (depth camera + VisionActorCritic + PPOL2C2); the state-only MLP
+task of the BASELINE configs is DiffLab-Quadcopter-CTBR-Racing-State-v0.
+
 Multi-GPU (one env shard per GPU, PPO gradients all-reduced over RCCL):
 
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
-        standalone/rsl_rl/train.py --task DiffLab-Quadcopter-CTBR-Racing-v0 --num_envs 65536
+        standalone/rsl_rl/train.py --task DiffLab-Quadcopter-CTBR-Racing-State-v0 --num_envs 65536
 
 There is no simulator app to launch: `--headless` and the other AppLauncher
 flags are accepted and ignored; `--video` is rejected (no renderer).

@@ -106,3 +106,26 @@ def test_adam_prepare_numbers_blocks_and_rejects_bad_tables():
     t[1].grad = None
     assert lib.gr_adam_prepare(C.addressof(t), len(sizes), C.byref(nb)) == -1  # GR_ERR_ARG
     assert lib.gr_adam_prepare(C.addressof(t), 65, C.byref(nb)) == -1  # GR_ERR_ARG
+
+
+def test_mlp_rejects_rows_past_32_bit_offsets():
+    """gr_mlp_forward / _backward index rows * max(H, ldx) elements in 32 bits: a larger call is an argument error
+    (checked before any launch; no device needed), whoever the caller is."""
+    from generalizableracing_amd.rsl_rl.linear import GrMlpArgs, GrMlpNet
+
+    lib = _abi.load()
+    assert lib.gr_mlp_args_size() == C.sizeof(GrMlpArgs)
+    a = GrMlpArgs()
+    s = GrMlpNet()
+    for name in ("x", "w1", "b1", "w2", "b2", "w3", "b3", "h1", "z2", "y", "gy", "gz2", "grads"):
+        setattr(s, name, 0x10000)
+    s.ldx, s.d, s.k = 16, 16, 4
+    a.net[0] = s
+    a.nets, a.hidden, a.slope, a.partial = 1, 256, 0.01, 0x10000
+    for rows in (2 ** 31 // 256, 2 ** 40):  # rows * H = 2^31, and a row count past int32
+        a.rows = rows
+        assert lib.gr_mlp_forward(C.byref(a), None) == -1  # GR_ERR_ARG
+        assert lib.gr_mlp_backward(C.byref(a), None) == -1
+    a.rows, a.hidden = 2 ** 31 // 128 - 1, 128
+    a.net[0].ldx = 160  # the strided input dominates: rows * ldx >= 2^31
+    assert lib.gr_mlp_forward(C.byref(a), None) == -1

@@ -19,11 +19,21 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_bench_two_ranks_gloo():
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "128", "--warmup", "8", "--num-envs", "8192", "--dist-backend", "gloo"]
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+BENCH_ARGS = ["--gpus", "2", "--steps", "128", "--warmup", "8", "--num-envs", "8192", "--dist-backend", "gloo"]
+
+
+@pytest.mark.parametrize("launch", ["torchrun", "plain"])
+def test_bench_two_ranks_gloo(launch):
+    """torchrun: the driver's form for N > 1.  plain: `python bench.py --gpus 2`, which starts the two ranks itself
+    (bench.launch_ranks) and must print the same two-rank line."""
+    bench = os.path.join(ROOT, "bench.py")
+    if launch == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), bench, *BENCH_ARGS]
+    else:
+        cmd = [sys.executable, bench, *BENCH_ARGS]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["MASTER_ADDR"] = "127.0.0.1"
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -42,3 +52,18 @@ def test_bench_two_ranks_gloo():
         assert r["current_device"] == 0 and r["env_steps_per_s"] > 0 and "pci" in r and r["name"]
         assert r["env_steps_per_s"] >= 8192 * 128 / (line["ms_per_step"] * 1e-3 * 128) * (1 - 1e-6)
     assert d["grad_allreduce_bytes"] == 566_312 and d["grad_allreduce_median_us"] > 0
+    assert len(d["ranks"]) == 2
+
+
+def test_bench_refuses_a_world_it_cannot_describe():
+    """Two RCCL ranks on a one-GPU box: every rank must own a GPU, so the run exits non-zero without a line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    import torch
+
+    n = torch.cuda.device_count()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n + 1), "--steps", "8",
+                        "--num-envs", "8192", "--no-extras"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode != 0
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert "need" in r.stderr

@@ -238,3 +238,54 @@ def test_flat_adam_clip_keeps_nan_like_torch():
     assert torch.isnan(n_fa) and torch.isnan(n_t)
     for p, q in zip(ps, qs):
         assert torch.isnan(p.grad).all() and torch.isnan(q.grad).all()
+
+
+def test_epoch_graph_equals_per_step_graph_bitwise():
+    """The default graphed update (one graph per epoch, every mini-batch step on its slice of the permutation) runs
+    the same kernels in the same order as one graph per mini-batch step (graph_update_per_step): parameters, Adam
+    moments and step counts, learning rate and losses are identical bit for bit, at capture and at replay."""
+    torch.manual_seed(5)
+    n = 2048
+    env = RslRlVecEnvWrapper(RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV))))
+    cfg = QuadcopterPPORunnerCfg(device=DEV)
+    cfg.algorithm.obs_sink = False
+    cfg.algorithm.graph_update = True
+    runner = OnPolicyRunner(env, cfg.to_dict(), log_dir=None, device=DEV)
+    alg = runner.alg
+    kw = dict(cfg.to_dict()["algorithm"])
+    kw.pop("class_name")
+    kw["graph_update_per_step"] = True
+    alg_s = PPO(copy.deepcopy(alg.policy), device=DEV, **kw)
+    alg_s.init_storage("rl", n, cfg.num_steps_per_env, [16], [16], [4])
+    obs, extras = env.get_observations()
+    cobs = extras["observations"]["critic"]
+    with torch.inference_mode():
+        for _ in range(cfg.num_steps_per_env):
+            a = alg.act(obs, cobs)
+            obs, rew, dones, infos = env.step(a)
+            cobs = infos["observations"]["critic"]
+            alg.process_env_step(rew, dones, infos)
+        alg.compute_returns(cobs)
+    for name, v in vars(alg.storage).items():
+        if torch.is_tensor(v):
+            getattr(alg_s.storage, name).copy_(v)
+
+    def state_tensors(a):
+        sd = a.optimizer.state_dict()
+        out = [t for st in sd["state"].values() for t in st.values() if torch.is_tensor(t)]
+        return [p.detach() for p in a.policy.parameters()] + out
+
+    for rep in range(2):  # capture, then replay
+        alg_s.storage.step = alg.storage.step = cfg.num_steps_per_env
+        torch.manual_seed(11 + rep)
+        le = alg.update()
+        torch.manual_seed(11 + rep)
+        ls = alg_s.update()
+        assert not alg._graphed.per_step and alg_s._graphed.per_step
+        te, ts = state_tensors(alg), state_tensors(alg_s)
+        assert len(te) == len(ts) > 8
+        for k, (x, y) in enumerate(zip(te, ts)):
+            assert torch.equal(x, y), (rep, k)
+        assert alg.learning_rate == alg_s.learning_rate
+        assert le == ls, (le, ls)
+    env.close()

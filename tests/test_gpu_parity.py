@@ -427,6 +427,50 @@ def test_terrain_regeneration_step_graph_captured():
     eb.close()
 
 
+def test_terrain_reservation_does_not_move_under_a_captured_graph():
+    """A generation larger than the reservation reallocates the terrain arrays (gr_terrain_reserve): refused while a
+    graph captured over the env may still replay (it would read freed arrays); allowed after forget_captures(), and
+    the terrain epoch (gr_terrain_epoch) moves with it."""
+    from generalizableracing_amd.envs.tracks import ObstacleTable
+
+    n = 1024
+    env = RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV), stage=1,
+                                 terrain=TerrainCfg(regen_interval_s=0.03 * 1000)))
+    env.reset()
+    e0 = env.terrain_epoch
+    assert e0 >= 1
+    a = torch.zeros(n, 4, device=DEV)
+    env.step(a)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        env.step(a)
+    graph.replay()
+    torch.cuda.synchronize()
+    build = env._build_terrain
+
+    def bigger(seed):  # the same generation with twice the obstacle slots per track (counts unchanged)
+        gates, recs, obst = build(seed)
+        m = obst.max_obstacles
+        rec = np.zeros((obst.records.shape[0], 2 * m + 16, obst.records.shape[2]), dtype=np.float32)
+        rec[:, :m] = obst.records
+        return gates, recs, ObstacleTable(rec, obst.counts, obst.grid_f, obst.grid_i, obst.cells, obst.items)
+
+    env._build_terrain = bigger
+    if env._next_terrain is not None:
+        env._next_terrain.result()
+        env._next_terrain = None
+    with pytest.raises(RuntimeError, match="forget_captures"):
+        env.regenerate_terrain()
+    assert env.terrain_epoch == e0
+    del graph
+    env.forget_captures()
+    env.regenerate_terrain()
+    assert env.terrain_epoch == e0 + 1
+    env.step(a)
+    torch.cuda.synchronize()
+    env.close()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_obs_sink_rows(dtype):
