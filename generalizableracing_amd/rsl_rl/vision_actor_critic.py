@@ -119,9 +119,15 @@ class VisionActorCritic(ActorCritic):
             if bn.momentum is None:
                 momentum = 1.0 / float(bn.num_batches_tracked)
         use_batch = bn.training or (bn.running_mean is None and bn.running_var is None)
-        return F.batch_norm(x, bn.running_mean if not bn.training or bn.track_running_stats else None,
-                            bn.running_var if not bn.training or bn.track_running_stats else None,
-                            bn.weight, bn.bias, use_batch, momentum, bn.eps)
+        args = (bn.running_mean if not bn.training or bn.track_running_stats else None,
+                bn.running_var if not bn.training or bn.track_running_stats else None,
+                bn.weight, bn.bias, use_batch, momentum, bn.eps)
+        if use_batch and x.device.type == "cpu":
+            # torch's CPU batch_norm reduces an [M, C] (channels-last) input with ~1e-4 relative error at M ~ 2e5
+            # rows when |mean| >> std (depth-image activations); on [1, C, M] it reduces as it does the
+            # reference's NCHW tensors (~3e-7).  The GPU kernels are accurate in either layout.
+            return F.batch_norm(x.t().contiguous().unsqueeze(0), *args)[0].t().contiguous()
+        return F.batch_norm(x, *args)
 
     def _bn_act(self, bn: nn.BatchNorm2d, act: nn.Module, x: torch.Tensor) -> torch.Tensor:
         """act(bn(x)) on rows [M, C]: the fused HIP op in training mode on the GPU, else torch's ops."""
