@@ -239,7 +239,7 @@ EXPORTS = [
     "gr_bn_scratch_doubles", "gr_bn_act_forward", "gr_bn_act_backward", "gr_stem1_scratch_doubles",
     "gr_stem1_forward", "gr_stem1_backward", "gr_mlp_partials", "gr_mlp_forward", "gr_mlp_backward",
     "gr_mlp_args_size", "gr_step_kernel_variant", "gr_terrain_reserve", "gr_terrain_stage", "gr_terrain_commit",
-    "gr_terrain_epoch",
+    "gr_terrain_epoch", "gr_mlp_h1mask_words",
 ]
 
 _lib = None
@@ -265,6 +265,7 @@ def _declare(lib):
         "gr_terrain_stage": (C.c_int, [vp, vp, vp, C.POINTER(GrObstacles), vp]),
         "gr_terrain_commit": (C.c_int, [vp, vp]),
         "gr_terrain_epoch": (C.c_int64, [vp]),
+        "gr_mlp_h1mask_words": (C.c_int64, [C.c_int64, C.c_int32]),
         "gr_bind_buffers": (C.c_int, [vp, C.POINTER(GrBuffers)]),
         "gr_bind_obs_sink": (C.c_int, [vp, vp, vp, C.c_int]),
         "gr_init": (C.c_int, [vp, vp]),

@@ -1058,6 +1058,11 @@ int gr_mlp_in_backward(const float* gh, const float* hv, const float* x, int64_t
 
 size_t gr_mlp_args_size(void) { return sizeof(gr_mlp_args); }
 
+int64_t gr_mlp_h1mask_words(int64_t rows, int32_t hidden) {
+  if (rows < 0 || (hidden != 128 && hidden != 256)) return GR_ERR_ARG;
+  return (rows + 15) / 16 * (hidden / 16) * 4;
+}
+
 int64_t gr_mlp_partials(int64_t rows, int32_t hidden, int32_t nets) {
   if (rows < 0 || (hidden != 128 && hidden != 256) || nets < 1 || nets > 2) return GR_ERR_ARG;
   return gr::mlp_partial_floats(rows, hidden, nets, 32, 4);
@@ -1076,6 +1081,7 @@ static bool mlp_args_ok(const gr_mlp_args* a, bool bwd) {
         !aligned16(n.z2))
       return false;
     if (!bwd && !n.y) return false;
+    if (n.h1mask && !aligned16(n.h1mask)) return false;
     if (bwd && (!n.gy || !n.gz2 || !n.grads || !aligned16(n.gz2))) return false;
   }
   return !bwd || (a->partial && aligned16(a->partial));

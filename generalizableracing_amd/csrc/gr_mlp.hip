@@ -157,6 +157,26 @@ __global__ __launch_bounds__(MW * 64) void mlp_fwd(gr_mlp_args a) {
 #pragma unroll
         for (int c = 0; c < MC; ++c) acc[t][c] = mf(w1r[t][kk >> 2][kk & 3], xo[c][kk >> 2][kk & 3], acc[t][c]);
     if (base + stride < n) load_x(base + stride);
+    if (net.h1mask) {
+      // the sign of h1 for mlp_bwd256h (the only thing the backward needs of h1): per 16-row x 16-unit tile and
+      // register r the wave's ballot, bit 16 g + j = (unit 16 u16 + 4 g + r, row 16 c + j) > 0; lane
+      // (t MC + c) 4 + r stores word [row tile][u16][r] (a vector store per lane)
+      unsigned long long my = 0ull;
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+#pragma unroll
+        for (int c = 0; c < MC; ++c)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const unsigned long long b = __ballot(acc[t][c][r] > 0.0f);
+            if (lane == (t * MC + c) * 4 + r) my = b;
+          }
+      if (lane < TW * MC * 4) {
+        const int t = lane / (MC * 4), c = (lane / 4) % MC, r = lane & 3;
+        if (base + 16 * c < n)
+          net.h1mask[(((size_t)(base / 16 + c)) * (H / 16) + wave * TW + t) * 4 + r] = my;
+      }
+    }
 #pragma unroll
     for (int t = 0; t < TW; ++t)
 #pragma unroll
@@ -736,6 +756,275 @@ __global__ __launch_bounds__(MW * 64) void mlp_bwd256(gr_mlp_args a, int rows_pe
   }
 }
 
+// ------------------------------------------------------------------------------------------------ backward, H = 256,
+// two workgroups per CU (round 5)
+// mlp_bwd256 keeps all 8 waves of a CU in one workgroup: five barriers per 32-row tile hold the two waves of every
+// SIMD in step, so the non-MFMA phases of both (gz2, gz1, the small weight gradients' dependent MFMA chains, the
+// DMA waits) leave the matrix pipe idle at once (MFMA busy 56 % at 24 576 rows, 67 % at 393 216).  Here a workgroup
+// is 4 waves and owns HALF of the h1 units (128; wave w: units 128 h + 32 w .. + 31, the W2 columns of those in
+// registers as before), so two workgroups share a CU and drift apart: one's elementwise phase runs under the
+// other's GEMM.  Per tile, two barriers:
+//   B1  z2 / gy / x / h1-sign rows of the tile in LDS (LDS-DMA issued one tile ahead; z2 single-buffered, the
+//       small inputs double-buffered); every wave is done with the previous tile's gz2 (its GEMM operand).
+//       gW3 += gy^T h2 for the workgroup's half of the z2 units (B operand lrelu(z2) from LDS); gz2 = (gy W3) *
+//       lrelu'(z2) for ALL 256 z2 units (each workgroup of the pair computes the full tile: the GEMM contracts over
+//       it), wave w the units 32 w .. + 31 and 128 + 32 w .. + 31, of which the half's own ones feed gb2 and the
+//       global gz2 rows mlp_wgrad reads.
+//   B2  gz2 tile complete, z2 free: the next tile's DMA is issued.  GEMM gh1 = gz2 W2 as C[rows x units]
+//       (A = gz2 fragments from LDS, B = the W2 columns), so its output fragment is directly the A operand of
+//       gW1 = gz1^T x (k = the tile's rows) and gz1 = gh1 lrelu'(h1) needs only the SIGN of h1: 1 bit per element
+//       from mlp_fwd (gr_mlp_net.h1mask) instead of the h1 rows (1 KB per row and network).
+// LDS (floats): z2s [BE][HBP], gz2s [BE][HBP], xs [2][BE][16 DT], gys [2][BE][4], masks [2][2][8][4] x u64; the W2
+// staging at start-up (2 chunks of 64 W2 rows x 128 columns) reuses z2s + gz2s.
+constexpr int HWV = 4;          // waves per workgroup
+constexpr int HSP = 128 + 4;    // LDS row stride of the W2 staging chunks
+__host__ __device__ constexpr size_t mlp_bwd256h_lds_bytes(int dt) {
+  return 4 * ((size_t)2 * BE * HBP + 2 * BE * 16 * dt + 2 * BE * 4 + 2 * 2 * 8 * 4 * 2);
+}
+
+template <int DT>
+__global__ __launch_bounds__(HWV * 64, 2) void mlp_bwd256h(gr_mlp_args a, int rows_per_net_part) {
+  constexpr int H = HB, HP = HBP, Q = H / 16;
+  constexpr int XW = 16 * DT;
+  const gr_mlp_net& net = a.net[blockIdx.y];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4,
+            j = lane & 15;
+  const int half = blockIdx.x & 1, rg = blockIdx.x >> 1, groups = gridDim.x >> 1;
+  const int n = (int)a.rows;  // (gr_mlp_* check rows * max(H, ldx) < 2^31: 32-bit offsets)
+  const int D = net.d, K = net.k;
+  const int ldx = (int)net.ldx;
+  const float slope = a.slope;
+  extern __shared__ float lds[];
+  float* z2s = lds;                                           // [BE][HP]
+  float* gz2s = z2s + BE * HP;                                // [BE][HP]
+  float* xs = gz2s + BE * HP;                                 // [2][BE][XW]
+  float* gys = xs + 2 * BE * XW;                              // [2][BE][4]
+  unsigned long long* mks = reinterpret_cast<unsigned long long*>(gys + 2 * BE * 4);  // [2][2 c][8 u16][4 r]
+  const float* __restrict__ W2 = net.w2;
+  const float* __restrict__ W3 = net.w3;
+  const float* z2g = net.z2;
+  const float* xg = net.x;
+  const float* gyg = net.gy;
+  const unsigned long long* mkg = reinterpret_cast<const unsigned long long*>(net.h1mask);
+  float* gz2g = net.gz2;
+  asm volatile("" : "+s"(z2g), "+s"(xg), "+s"(gyg), "+s"(mkg), "+s"(gz2g));
+  const int U0 = 128 * half + 32 * wave;  // this wave's h1 units (GEMM output) U0 .. U0 + 31
+  // this wave's z2 unit tiles for gz2: o-tiles 2w, 2w + 1, 8 + 2w, 9 + 2w; the half's own ones are 8 half + 2w + e
+  float w3a[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int ot = (e < 2 ? 2 * wave + e : 8 + 2 * wave + (e - 2));
+    w3a[e] = g < K ? W3[(size_t)g * H + 16 * ot + j] : 0.0f;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(w3a[e]));  // (consumed before any DMA, as mlp_bwd256)
+  // W2 columns U0 .. U0 + 31 (lane (g, j): W2[16 q + 4 g + r][U0 + 16 t + j]), staged by LDS-DMA: 4 chunks of 64 W2
+  // rows x the half's 128 columns, two in flight, one 512-B row per wave instruction (lanes 0..31)
+  float w2c[2][4 * Q];
+  float* const stg0 = lds;
+  float* const stg1 = lds + 64 * HSP;
+  auto issue_w2 = [&](int c, float* dst) {
+#pragma unroll
+    for (int k = 0; k < 64 / HWV; ++k) {
+      const int row = wave + HWV * k;
+      if (lane < 32) glds16(W2 + (size_t)(64 * c + row) * H + 128 * half + 4 * lane, dst + row * HSP);
+    }
+  };
+  issue_w2(0, stg0);
+  issue_w2(1, stg1);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if (c < 3) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // chunk c in (chunk c + 1 may be in flight)
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();
+    const float* src = (c & 1) ? stg1 : stg0;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int i = 32 * wave + 16 * t + j;
+#pragma unroll
+      for (int q = 4 * c; q < 4 * c + 4; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) w2c[t][4 * q + r] = src[(16 * (q - 4 * c) + 4 * g + r) * HSP + i];
+    }
+    if (c + 2 < 4) {
+      raw_barrier();  // every wave has read chunk c
+      issue_w2(c + 2, (c & 1) ? stg1 : stg0);
+    }
+  }
+  raw_barrier();  // every wave has read the last chunk (its space is the DMA targets, zeroed next)
+  m4 gw1[2][DT], gw3[2];
+  float gb1[2], gb2[2][4], gb3 = 0.0f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    gw3[t] = zero4();
+    gb1[t] = 0.0f;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) gw1[t][dt] = zero4();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) gb2[t][r] = 0.0f;
+  }
+  // the small DMA targets start at 0 (x columns >= d, gy outputs >= k are never written; never-written LDS may
+  // hold NaN patterns)
+  for (int i = threadIdx.x; i < 2 * BE * XW + 2 * BE * 4; i += HWV * 64) xs[i] = 0.0f;
+  __syncthreads();
+
+  auto clamp_row = [&](int r) { return r < n ? r : n - 1; };
+  // one tile's inputs: z2 rows (wave w: rows w + 4 k), gy (wave 3), x (waves 0 .. 2 DT - 1), h1 signs (wave 2)
+  auto issue_in = [&](int tb, int par) {
+#pragma unroll
+    for (int k = 0; k < BE / HWV; ++k) {
+      const int row = wave + HWV * k;
+      glds16(z2g + (size_t)clamp_row(tb + row) * H + 4 * lane, z2s + row * HP);
+    }
+    if (wave == HWV - 1) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = 16 * h + (lane >> 2), kk = lane & 3;
+        if (kk < K) glds4(gyg + (size_t)clamp_row(tb + row) * K + kk, gys + par * BE * 4 + 16 * h * 4);
+      }
+    }
+    if (wave < 2 * DT) {
+      constexpr int RPI = 16 / DT;  // rows per instruction
+      const int row = RPI * wave + lane / (4 * DT), c4 = 4 * (lane % (4 * DT));
+      if (c4 < D) glds16(xg + (size_t)clamp_row(tb + row) * ldx + c4, xs + par * BE * XW + RPI * wave * XW);
+    }
+    if (wave == 2 && lane < 32) {
+      // [c][u16 8 half .. + 7][r]: 2 x 256 contiguous bytes (row tiles tb / 16 + c, clamped)
+      const int c = lane >> 4, rt = clamp_row(tb + 16 * c) >> 4;
+      glds16(reinterpret_cast<const float*>(mkg + ((size_t)rt * (H / 16) + 8 * half) * 4) + 4 * (lane & 15),
+             reinterpret_cast<float*>(mks + par * 64));
+    }
+  };
+
+  const int stride = groups * BE;
+  int base = rg * BE;
+  if (base < n) issue_in(base, 0);
+  for (int kt = 0; base < n; base += stride, ++kt) {
+    const int par = kt & 1;
+    const bool has_next = base + stride < n;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();  // (B1) this tile's inputs in LDS; every wave is done with the previous tile's gz2
+    const float* gyt = gys + par * BE * 4;
+    const float* xt = xs + par * BE * XW;
+    const unsigned long long* mkt = mks + par * 64;
+    // ---- gW3 += gy^T h2 for the half's z2 units 128 half + 32 w + 16 t + j (k step = rows 4 s + g)
+#pragma unroll 4
+    for (int s = 0; s < BE / 4; ++s) {
+      const int row = 4 * s + g;
+      const float av = (j < 4 && base + row < n) ? gyt[row * 4 + j] : 0.0f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        gw3[t] = mf(av, lrelu(z2s[row * HP + 128 * half + 32 * wave + 16 * t + j], slope), gw3[t]);
+    }
+    // ---- gz2 = (gy W3) lrelu'(z2) for the wave's four z2 unit tiles, all rows of the tile -> LDS; the half's own
+    // ones also -> gb2 and the global gz2 rows (mlp_wgrad)
+#pragma unroll
+    for (int c = 0; c < BC; ++c) {
+      const int row = 16 * c + j;
+      const bool live = base + row < n;
+      const float gyv = live ? gyt[row * 4 + g] : 0.0f;  // B[k = g][row j]
+      if (half == 0 && wave == 0) gb3 += gyv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int ot = (e < 2 ? 2 * wave + e : 8 + 2 * wave + (e - 2));
+        const int u = 16 * ot + 4 * g;
+        const m4 gh = mf(w3a[e], gyv, zero4());
+        const m4 z = ld4(z2s + row * HP + u);
+        m4 gz;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gz[q] = gh[q] * lrelu_d(z[q], slope);
+        st4(gz2s + row * HP + u, gz);
+        if ((e >> 1) == half) {  // (wave-uniform)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) gb2[e & 1][q] += gz[q];
+          if (live) st4(gz2g + (size_t)(base + row) * H + u, gz);
+        }
+      }
+    }
+    raw_barrier();  // (B2) gz2 of the tile in LDS; every wave is done with z2s
+    if (has_next) issue_in(base + stride, par ^ 1);
+    // ---- gh1 = gz2 W2 as C[rows 16 c .. + 15 x units U0 + 16 t .. + 15]
+    m4 acc[2][BC];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int c = 0; c < BC; ++c) acc[t][c] = zero4();
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      m4 gb[BC];
+#pragma unroll
+      for (int c = 0; c < BC; ++c) gb[c] = ld4(gz2s + (16 * c + j) * HP + 16 * q + 4 * g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int c = 0; c < BC; ++c) acc[t][c] = mf(gb[c][r], w2c[t][4 * q + r], acc[t][c]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- gz1 = gh1 lrelu'(h1) (sign bits from the forward), gb1, gW1 += gz1^T x: lane (g, j) holds rows
+    // 16 c + 4 g + r of unit U0 + 16 t + j, which is gW1's A fragment for k step (c, r) as it stands
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int c = 0; c < BC; ++c) {
+        // word [c][u16 = 2 w + t][r' = j % 4]: bit 16 (j / 4) + 4 g + r = (row 16 c + 4 g + r, unit 16 u16 + j)
+        const unsigned long long mw = mkt[(c * 8 + 2 * wave + t) * 4 + (j & 3)];
+        const uint32_t nib = (uint32_t)(mw >> (16 * (j >> 2) + 4 * g)) & 0xfu;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float gz1 = acc[t][c][r] * (((nib >> r) & 1u) ? 1.0f : slope);
+          gb1[t] += gz1;
+          const int row = 16 * c + 4 * g + r;
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            const int dcol = 16 * dt + j;
+            gw1[t][dt] = mf(gz1, dcol < D ? xt[row * XW + dcol] : 0.0f, gw1[t][dt]);
+          }
+        }
+      }
+    }
+  }
+  // ---- the workgroup's part of the partial row of its row group (the pair's two halves fill it)
+  float* pr = a.partial + ((size_t)blockIdx.y * groups + rg) * (size_t)rows_per_net_part;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int u0 = U0 + 16 * t;
+    // gW1 [H][D]: C rows = units u0 + 4 g + q, col = input 16 dt + j
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (16 * dt + j < D) pr[(size_t)(u0 + 4 * g + q) * D + 16 * dt + j] = gw1[t][dt][q];
+    // gb1: unit u0 + j, summed over the 4 row groups g
+    float v = gb1[t];
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (g == 0) pr[H * D + u0 + j] = v;
+    // gb2: z2 unit 128 half + 32 w + 16 t + 4 g + q, summed over the rows j
+    const int o0 = 128 * half + 32 * wave + 16 * t;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float b2 = gb2[t][q];
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) b2 += __shfl_xor(b2, off);
+      if (j == 0) pr[H * D + H + o0 + 4 * g + q] = b2;
+    }
+    // gW3 [k][H]: C rows = outputs 4 g + q (g == 0, q < k), col = z2 unit o0 + j
+    if (g == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (q < K) pr[H * D + 2 * H + q * H + o0 + j] = gw3[t][q];
+    }
+  }
+  if (half == 0 && wave == 0) {
+    float v = gb3;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) v += __shfl_xor(v, off);
+    if (j == 0 && g < K) pr[H * D + 2 * H + K * H + g] = v;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ gW2
 // gW2 [H][H] = gz2^T h1 per network: a workgroup takes a 128 x 128 output block (rows u of gW2 = gz2 columns,
 // cols i = h1 columns) over a chunk of the mini-batch rows; 8 waves as 2 (u) x 4 (i) of 64 x 32 (4 x 2 tiles).
@@ -987,6 +1276,20 @@ static hipError_t launch_bwd256_t(const gr_mlp_args& a, int row, hipStream_t s) 
   return hipGetLastError();
 }
 
+template <int DT>
+static hipError_t launch_bwd256h_t(const gr_mlp_args& a, int row, hipStream_t s) {
+  static bool attr = false;
+  const size_t lds = mlp_bwd256h_lds_bytes(DT);
+  if (!attr) {
+    const hipError_t e = set_lds(&mlp_bwd256h<DT>, lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((mlp_bwd256h<DT>), dim3(2 * mlp_grid_x(a.rows, a.nets, BE), a.nets), dim3(HWV * 64), lds, s, a,
+                     row);
+  return hipGetLastError();
+}
+
 template <int H>
 static hipError_t launch_wgrad_t(const gr_mlp_args& a, int splits, long long rps, float* wpart, hipStream_t s) {
   static bool attr = false;
@@ -1010,7 +1313,9 @@ hipError_t launch_mlp_backward(const gr_mlp_args& a, hipStream_t s) {
   const int row = mlp_bwd_row(a.hidden, d, k);
   const int bwd_blocks = mlp_grid_x(a.rows, a.nets, BE);
   hipError_t e;
-  if (a.hidden == 256) e = d <= 16 ? launch_bwd256_t<1>(a, row, s) : launch_bwd256_t<2>(a, row, s);
+  const bool masks = a.net[0].h1mask && (a.nets < 2 || a.net[1].h1mask);
+  if (a.hidden == 256 && masks) e = d <= 16 ? launch_bwd256h_t<1>(a, row, s) : launch_bwd256h_t<2>(a, row, s);
+  else if (a.hidden == 256) e = d <= 16 ? launch_bwd256_t<1>(a, row, s) : launch_bwd256_t<2>(a, row, s);
   else e = d <= 16 ? launch_bwd_t<128, 1>(a, row, s) : launch_bwd_t<128, 2>(a, row, s);
   if (e != hipSuccess) return e;
   const int splits = mlp_splits(a.rows, a.hidden, a.nets);

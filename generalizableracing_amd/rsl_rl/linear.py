@@ -287,7 +287,8 @@ class MLP(nn.Sequential):
 class GrMlpNet(C.Structure):
     """Mirror of gr_mlp_net (include/gr.h)."""
     _fields_ = [(n, C.c_void_p) for n in ("x", "w1", "b1", "w2", "b2", "w3", "b3", "h1", "z2", "y", "gy", "gz2",
-                                          "grads")] + [("ldx", C.c_int64), ("d", C.c_int32), ("k", C.c_int32)]
+                                          "grads")] + [("ldx", C.c_int64), ("d", C.c_int32), ("k", C.c_int32),
+                                                       ("h1mask", C.c_void_p)]
 
 
 class GrMlpArgs(C.Structure):
@@ -362,9 +363,12 @@ class _FusedMLPsFn(torch.autograd.Function):
             for name, t in (("w1", w1), ("b1", b1), ("w2", w2), ("b2", b2), ("w3", w3), ("b3", b3)):
                 setattr(s, name, t.data_ptr())
             s.h1, s.z2, s.y = h1.data_ptr(), z2.data_ptr(), y.data_ptr()
+            # the sign of h1 as bits (H = 256: the backward reads these instead of the h1 rows, mlp_bwd256h)
+            mask = torch.empty(_mask_words(rows, h), device=dev, dtype=torch.int64)
+            s.h1mask = mask.data_ptr() if mask.numel() else None
             a.net[i] = s
             a.hidden = h
-            keep += [h1, z2]
+            keep += [h1, z2, mask]
             outs.append(y)
         _lib_call("gr_mlp_forward", C.byref(a), _stream(xs[0]))
         ctx.nnets, ctx.slope = nnets, float(slope)
@@ -377,7 +381,7 @@ class _FusedMLPsFn(torch.autograd.Function):
 
         nnets = ctx.nnets
         saved = ctx.saved_tensors
-        xs, keep, params = saved[:nnets], saved[nnets:3 * nnets], saved[3 * nnets:]
+        xs, keep, params = saved[:nnets], saved[nnets:4 * nnets], saved[4 * nnets:]
         rows = xs[0].shape[0]
         dev = xs[0].device
         a = GrMlpArgs()
@@ -386,7 +390,7 @@ class _FusedMLPsFn(torch.autograd.Function):
         for i in range(nnets):
             w1, b1, w2, b2, w3, b3 = params[6 * i:6 * i + 6]
             h, d, k = w1.shape[0], w1.shape[1], w3.shape[0]
-            h1, z2 = keep[2 * i], keep[2 * i + 1]
+            h1, z2, mask = keep[3 * i], keep[3 * i + 1], keep[3 * i + 2]
             gy = gys[i]
             gy = torch.zeros(rows, k, device=dev, dtype=torch.float32) if gy is None else gy.float().contiguous()
             gys_keep.append(gy)
@@ -402,6 +406,7 @@ class _FusedMLPsFn(torch.autograd.Function):
             gz2 = torch.empty_like(z2)
             gys_keep.append(gz2)
             s.h1, s.z2, s.gy, s.gz2, s.grads = h1.data_ptr(), z2.data_ptr(), gy.data_ptr(), gz2.data_ptr(), grads.data_ptr()
+            s.h1mask = mask.data_ptr() if mask.numel() else None
             a.net[i] = s
             a.hidden = h
             o = 0
@@ -417,6 +422,15 @@ class _FusedMLPsFn(torch.autograd.Function):
         a.partial = part.data_ptr()
         _lib_call("gr_mlp_backward", C.byref(a), _stream(xs[0]))
         return (None, None) + (None,) * nnets + tuple(grads_out)
+
+
+def _mask_words(rows: int, hidden: int) -> int:
+    """gr_mlp_h1mask_words for H = 256 (mlp_bwd256h); 0 (no mask: the backward reads h1) for H = 128."""
+    if hidden != 256:
+        return 0
+    from .. import _abi
+
+    return int(_abi.load().gr_mlp_h1mask_words(rows, hidden))
 
 
 def _sink_region(params):

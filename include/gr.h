@@ -531,7 +531,12 @@ typedef struct gr_mlp_net {
   float* grads;      /* backward output [H d | H | H H | H | k H | k] = gW1, gb1, gW2, gb2, gW3, gb3 */
   int64_t ldx;
   int32_t d, k;
+  /* optional, 16-byte aligned, gr_mlp_h1mask_words(rows, H) words: the sign of h1 as bits, written by the forward
+   * when non-null; given to the backward (H = 256) it replaces the h1 rows there (mlp_bwd256h: 1/32 of their bytes,
+   * two workgroups per CU).  NULL in the backward: the h1 rows are read (mlp_bwd256 / mlp_bwd). */
+  uint64_t* h1mask;
 } gr_mlp_net;
+int64_t gr_mlp_h1mask_words(int64_t rows, int32_t hidden);
 typedef struct gr_mlp_args {
   gr_mlp_net net[2];
   int64_t rows;
