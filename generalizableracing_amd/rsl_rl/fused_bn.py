@@ -78,12 +78,13 @@ def fused_applicable(bn: nn.BatchNorm2d, act: nn.Module, x: torch.Tensor) -> boo
             and bn.weight.dtype == torch.float32)
 
 
-def batch_norm_act(bn: nn.BatchNorm2d, act: nn.Module, x: torch.Tensor) -> torch.Tensor:
+def batch_norm_act(bn: nn.BatchNorm2d, act: nn.Module, x: torch.Tensor, uses: int = 1) -> torch.Tensor:
     """act(bn(x)) for rows x [M, C] in training mode, running statistics updated as nn.BatchNorm2d does
-    (the caller has already counted the batch in num_batches_tracked and passes the momentum it implies)."""
+    (the caller has already counted the batch in num_batches_tracked and passes the momentum it implies);
+    uses > 1: as `uses` forwards of the same rows would (_update_running)."""
     code, slope = _act_code(act)
     y, stats = _BatchNormAct.apply(x, bn.weight, bn.bias, bn.eps, code, slope)
-    _update_running(bn, stats)
+    _update_running(bn, stats, uses)
     return y
 
 
@@ -146,24 +147,31 @@ def stem1_applicable(bn: nn.BatchNorm2d, act: nn.Module, img: torch.Tensor, conv
 
 
 def stem1_bn_act(bn: nn.BatchNorm2d, act: nn.Module, conv_w: torch.Tensor, img: torch.Tensor, pix: torch.Tensor,
-                 na: int, nb: int) -> torch.Tensor:
+                 na: int, nb: int, uses: int = 1) -> torch.Tensor:
     """act(bn(conv(img))) as the table-a patch rows of VisionActorCritic.stem_gemm (img [B, H*W] rows; pix int16
     [(na + nb) * 9] pixel offsets; the B * nb table-b rows count in the statistics and are not returned), running
     statistics updated as nn.BatchNorm2d does (the caller counts the batch in num_batches_tracked)."""
     code, slope = _act_code(act)
     y, stats = _Stem1.apply(img, conv_w, bn.weight, bn.bias, pix, na, nb, bn.eps, code, slope)
-    _update_running(bn, stats)
+    _update_running(bn, stats, uses)
     return y
 
 
-def _update_running(bn: nn.BatchNorm2d, stats: torch.Tensor):
-    if bn.track_running_stats and bn.running_mean is not None:
-        momentum = 0.0 if bn.momentum is None else bn.momentum
-        if bn.momentum is None and bn.num_batches_tracked is not None:
-            momentum = 1.0 / float(bn.num_batches_tracked)
-        with torch.no_grad():
-            bn.running_mean.mul_(1.0 - momentum).add_(stats[0], alpha=momentum)
-            bn.running_var.mul_(1.0 - momentum).add_(stats[3], alpha=momentum)
+def _update_running(bn: nn.BatchNorm2d, stats: torch.Tensor, uses: int = 1):
+    """The running-statistics update of one training-mode forward; uses > 1 replays it as `uses` forwards of the
+    same rows would, in sequence (the first already counted by the caller, each further one counted here)."""
+    for k in range(uses):
+        if k and bn.track_running_stats and bn.num_batches_tracked is not None:
+            bn.num_batches_tracked.add_(1)
+        if bn.track_running_stats and bn.running_mean is not None:
+            momentum = 0.0 if bn.momentum is None else bn.momentum
+            if bn.momentum is None and bn.num_batches_tracked is not None:
+                momentum = 1.0 / float(bn.num_batches_tracked)
+            with torch.no_grad():
+                # (through .data, as F.batch_norm updates them inside its kernel: no version bump, so a torch
+                # batch_norm of the same forward that saved them for its backward stays valid)
+                bn.running_mean.data.mul_(1.0 - momentum).add_(stats[0], alpha=momentum)
+                bn.running_var.data.mul_(1.0 - momentum).add_(stats[3], alpha=momentum)
 
 
 def reference_batch_norm_act(bn: nn.BatchNorm2d, act: nn.Module, x: torch.Tensor) -> torch.Tensor:

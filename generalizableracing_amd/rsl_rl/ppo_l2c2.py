@@ -58,8 +58,10 @@ def _mix(obs, next_obs, w):
 
 class PPOL2C2(PPO):
     def __init__(self, policy, env=None, value_smoothness_coef=0.1, smoothness_upper_bound=1.0,
-                 smoothness_lower_bound=0.1, **kwargs):
+                 smoothness_lower_bound=0.1, share_mix_features=True, **kwargs):
         kwargs.pop("normalize_advantage", None)
+        # one stem evaluation of the mixed batch for the actor and the critic (policies with shared_features)
+        self.share_mix_features = bool(share_mix_features)
         super().__init__(policy, env=env, normalize_advantage=True, **kwargs)
         self.transition = RolloutStorageL2C2.Transition()
         self.value_smoothness_coef = value_smoothness_coef
@@ -107,9 +109,17 @@ class PPOL2C2(PPO):
         policy_coef, value_coef = self.smooth_coefs()
         mix_weights = cont_batch * (torch.rand_like(cont_batch) - 0.5) * 2.0
         mix_obs_batch = _mix(obs_batch, next_obs_batch, mix_weights)
-        policy_smooth = torch.square(torch.norm(mu_batch - _mean_of(self.policy.act_inference(mix_obs_batch)),
-                                                dim=-1)).mean()
-        value_smooth = torch.square(torch.norm(value_batch - self.policy.evaluate(mix_obs_batch), dim=-1)).mean()
+        shared = getattr(self.policy, "shared_features", None)
+        if shared is not None and self.share_mix_features:
+            # the actor's and the critic's forward of the mixed batch share one stem evaluation (VisionActorCritic:
+            # the same features, BatchNorm running statistics updated as by the reference's two forwards)
+            feat = shared(mix_obs_batch, 2)
+            mix_mean, mix_value = self.policy.actor(feat), self.policy.critic(feat)
+        else:
+            mix_mean = _mean_of(self.policy.act_inference(mix_obs_batch))
+            mix_value = self.policy.evaluate(mix_obs_batch)
+        policy_smooth = torch.square(torch.norm(mu_batch - mix_mean, dim=-1)).mean()
+        value_smooth = torch.square(torch.norm(value_batch - mix_value, dim=-1)).mean()
         loss = policy_coef * policy_smooth + value_coef * value_smooth
         with torch.inference_mode():
             action_smoothness = torch.norm(mu_batch - _mean_of(self.policy.act_inference(next_obs_batch)),

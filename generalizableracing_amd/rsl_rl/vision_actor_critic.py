@@ -110,9 +110,27 @@ class VisionActorCritic(ActorCritic):
         if self.use_auxiliary_loss:
             self.aux_decoder = nn.Linear(dim_hidden_input, 1)
 
-    @staticmethod
-    def _bn(bn: nn.BatchNorm2d, x: torch.Tensor) -> torch.Tensor:
+    # how many forwards of the same rows one stem evaluation stands for (shared_features): each BatchNorm's running
+    # statistics are updated that many times, as that many training-mode forwards would
+    _bn_uses = 1
+
+    def _bn(self, bn: nn.BatchNorm2d, x: torch.Tensor) -> torch.Tensor:
         """nn.BatchNorm2d.forward on channels-last rows [M, C] (M = batch*height*width)."""
+        y = self._bn_once(bn, x)
+        if self._bn_uses > 1 and bn.training and bn.track_running_stats and bn.running_mean is not None:
+            from .fused_bn import _update_running
+
+            with torch.no_grad():
+                xd = x.detach().double()
+                stats = torch.stack([xd.mean(0), xd.var(0, unbiased=False), xd.var(0, unbiased=False),
+                                     xd.var(0, unbiased=True)]).float()
+            for _ in range(self._bn_uses - 1):  # (F.batch_norm made the first update)
+                if bn.num_batches_tracked is not None:
+                    bn.num_batches_tracked.add_(1)
+                _update_running(bn, stats)
+        return y
+
+    def _bn_once(self, bn: nn.BatchNorm2d, x: torch.Tensor) -> torch.Tensor:
         momentum = 0.0 if bn.momentum is None else bn.momentum
         if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
             bn.num_batches_tracked.add_(1)
@@ -134,7 +152,7 @@ class VisionActorCritic(ActorCritic):
         if self.fused_bn and fused_applicable(bn, act, x):
             if bn.track_running_stats and bn.num_batches_tracked is not None:
                 bn.num_batches_tracked.add_(1)
-            return batch_norm_act(bn, act, x)
+            return batch_norm_act(bn, act, x, self._bn_uses)
         return act(self._bn(bn, x))
 
     def _patch_index(self, device):
@@ -175,7 +193,7 @@ class VisionActorCritic(ActorCritic):
             # conv1 + BN1 + act from the image itself: no patch matrix, no conv output (rsl_rl/fused_bn.py)
             if bn1.track_running_stats and bn1.num_batches_tracked is not None:
                 bn1.num_batches_tracked.add_(1)
-            y = stem1_bn_act(bn1, act, conv1.weight, flat, pix16, n1, n1_left)
+            y = stem1_bn_act(bn1, act, conv1.weight, flat, pix16, n1, n1_left, self._bn_uses)
         else:
             x = flat.index_select(1, idx).view(B * n1, 9)
             if n1_left:
@@ -197,6 +215,17 @@ class VisionActorCritic(ActorCritic):
         img = observations[:, -self.num_pixels:].reshape(-1, 1, *self.img_res)
         state = observations[:, :-self.num_pixels]
         return self.activation(self.stem_gemm(img) + self.state_enc(state))
+
+    def shared_features(self, observations: torch.Tensor, uses: int) -> torch.Tensor:
+        """features(observations) evaluated once for `uses` consumers of the same rows (PPOL2C2's mixed batch feeds
+        both the actor and the critic, ppo_l2c2.py:184-186, which the reference evaluates as two stem forwards):
+        the same values, one backward through the stem for the summed feature gradient, and every BatchNorm's
+        running statistics updated `uses` times, as `uses` training-mode forwards of these rows do."""
+        self._bn_uses = int(uses)
+        try:
+            return self.features(observations)
+        finally:
+            self._bn_uses = 1
 
     def update_distribution(self, observations):
         mean = self.actor(self.features(observations))

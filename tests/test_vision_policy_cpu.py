@@ -117,3 +117,43 @@ def test_split_k_weight_gradient():
         _PatchGemm.apply(x, w).backward(gy)
         torch.testing.assert_close(w.grad, gy.t() @ x.detach(), rtol=1e-4, atol=1e-3)
         torch.testing.assert_close(x.grad, gy @ w.detach())
+
+
+def _l2c2_update(share: bool, steps: int = 3):
+    """One PPOL2C2 update of a vision policy on a fixed synthetic rollout (CPU)."""
+    torch.manual_seed(11)
+    p = policy()
+    for bn in (p.stem[1], p.stem[4], p.stem[7]):
+        bn.weight.data.uniform_(0.5, 1.5)
+        bn.bias.data.uniform_(-0.2, 0.2)
+    alg = PPOL2C2(p, device="cpu", num_learning_epochs=2, num_mini_batches=2, share_mix_features=share)
+    n = 6
+    alg.init_storage("rl", n, steps, [OBS], [OBS], [4])
+    g = torch.Generator().manual_seed(3)
+    obs = torch.rand(n, OBS, generator=g)
+    with torch.inference_mode():
+        for _ in range(steps):
+            alg.act(obs, obs + 0.01)
+            obs = torch.rand(n, OBS, generator=g)
+            alg.process_env_step(torch.randn(n, generator=g), torch.zeros(n, dtype=torch.long),
+                                 {"time_outs": torch.zeros(n)})
+        alg.compute_returns(obs)
+    torch.manual_seed(5)
+    out = alg.update()
+    return p, out
+
+
+def test_l2c2_shared_mix_features_match_two_stem_forwards():
+    """PPOL2C2's mixed batch through one shared stem evaluation (VisionActorCritic.shared_features) against the
+    reference's two forwards (act_inference + evaluate, ppo_l2c2.py:184-186): the same losses and parameters up to
+    fp32 summation order, and the BatchNorm running statistics and batch counts of two forwards."""
+    p1, o1 = _l2c2_update(share=False)
+    p2, o2 = _l2c2_update(share=True)
+    for k in ("value_function", "surrogate", "smooth_loss"):
+        assert abs(o1[k] - o2[k]) <= 1e-5 * max(1.0, abs(o1[k])), (k, o1[k], o2[k])
+    s1, s2 = p1.state_dict(), p2.state_dict()
+    for k in s1:
+        if "num_batches" in k:
+            assert torch.equal(s1[k], s2[k]), k
+        else:
+            torch.testing.assert_close(s2[k], s1[k], rtol=1e-4, atol=1e-6, msg=k)
