@@ -424,9 +424,12 @@ class _FusedMLPsFn(torch.autograd.Function):
         return (None, None) + (None,) * nnets + tuple(grads_out)
 
 
+_H1_MASKS = True  # (False: the backward reads the h1 rows, mlp_bwd256: timing A/B)
+
+
 def _mask_words(rows: int, hidden: int) -> int:
     """gr_mlp_h1mask_words for H = 256 (mlp_bwd256h); 0 (no mask: the backward reads h1) for H = 128."""
-    if hidden != 256:
+    if hidden != 256 or not _H1_MASKS:
         return 0
     from .. import _abi
 

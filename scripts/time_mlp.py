@@ -33,7 +33,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, nargs="+", default=[24576, 393216])
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--no-mask", action="store_true", help="the backward reads h1 (mlp_bwd256) instead of its sign bits")
+    ap.add_argument("--fused-only", action="store_true")
     a = ap.parse_args()
+    lin._H1_MASKS = not a.no_mask
     dev = "cuda:0"
     torch.manual_seed(0)
     pol = ActorCritic(16, 16, 4, [256, 256], [256, 256], "lrelu").to(dev)
@@ -43,7 +46,7 @@ def main():
         buf = torch.randn(rows, 48, device=dev)
         xa, xc = buf[:, :16], buf[:, 16:32]
         ga, gc = torch.randn(rows, 4, device=dev), torch.randn(rows, 1, device=dev)
-        for path in ("fused_mlp", "per_layer"):
+        for path in (("fused_mlp",) if a.fused_only else ("fused_mlp", "per_layer")):
             def step():
                 if path == "fused_mlp":
                     ya, yc = lin.fused_mlps(nets, [xa, xc])
