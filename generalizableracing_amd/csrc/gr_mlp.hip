@@ -898,9 +898,6 @@ __global__ __launch_bounds__(HWV * 64, 2) void mlp_bwd256h(gr_mlp_args a, int ro
 
   const int stride = groups * BE;
   int base = rg * BE;
-#ifdef GR_MLPV_NOLOOP  // (timing variant: the fixed cost alone)
-  base = n;
-#endif
   if (base < n) issue_in(base, 0);
   for (int kt = 0; base < n; base += stride, ++kt) {
     const int par = kt & 1;
@@ -952,7 +949,6 @@ __global__ __launch_bounds__(HWV * 64, 2) void mlp_bwd256h(gr_mlp_args a, int ro
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int c = 0; c < BC; ++c) acc[t][c] = zero4();
-#ifndef GR_MLPV_NOGEMM  // (timing variant: no main GEMM)
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       m4 gb[BC];
@@ -966,10 +962,6 @@ __global__ __launch_bounds__(HWV * 64, 2) void mlp_bwd256h(gr_mlp_args a, int ro
           for (int c = 0; c < BC; ++c) acc[t][c] = mf(gb[c][r], w2c[t][4 * q + r], acc[t][c]);
       __builtin_amdgcn_sched_barrier(0);
     }
-#else
-    for (int t = 0; t < 2; ++t)
-      for (int c = 0; c < BC; ++c) acc[t][c] = ld4(gz2s + (16 * c + j) * HP + 4 * g) * w2c[t][c];
-#endif
     // ---- gz1 = gh1 lrelu'(h1) (sign bits from the forward), gb1, gW1 += gz1^T x: lane (g, j) holds rows
     // 16 c + 4 g + r of unit U0 + 16 t + j, which is gW1's A fragment for k step (c, r) as it stands
 #pragma unroll

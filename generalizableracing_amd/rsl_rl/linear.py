@@ -424,7 +424,10 @@ class _FusedMLPsFn(torch.autograd.Function):
         return (None, None) + (None,) * nnets + tuple(grads_out)
 
 
-_H1_MASKS = True  # (False: the backward reads the h1 rows, mlp_bwd256: timing A/B)
+# True: the forward also writes the sign of h1 as bits and the backward (H = 256) reads those instead of the h1 rows
+# (mlp_bwd256h, two workgroups per CU).  Measured no faster than mlp_bwd256 (C2 +2 %, 393 216 rows -3 %, the
+# forward's mask +2 %; DESIGN §4f''), so off by default; tests run both.
+_H1_MASKS = False
 
 
 def _mask_words(rows: int, hidden: int) -> int:

@@ -33,10 +33,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, nargs="+", default=[24576, 393216])
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--no-mask", action="store_true", help="the backward reads h1 (mlp_bwd256) instead of its sign bits")
+    ap.add_argument("--mask", action="store_true", help="the backward reads h1's sign bits (mlp_bwd256h), not the rows")
     ap.add_argument("--fused-only", action="store_true")
     a = ap.parse_args()
-    lin._H1_MASKS = not a.no_mask
+    lin._H1_MASKS = a.mask
     dev = "cuda:0"
     torch.manual_seed(0)
     pol = ActorCritic(16, 16, 4, [256, 256], [256, 256], "lrelu").to(dev)

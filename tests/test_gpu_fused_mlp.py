@@ -28,9 +28,18 @@ def _f64(net):
     return m.double().to(DEV)
 
 
+@pytest.fixture(params=[False, True], ids=["h1_rows", "h1_sign_bits"])
+def h1_masks(request):
+    """Both backward kernels for H = 256: mlp_bwd256 (reads the h1 rows) and mlp_bwd256h (the forward's sign bits)."""
+    old = lin._H1_MASKS
+    lin._H1_MASKS = request.param
+    yield request.param
+    lin._H1_MASKS = old
+
+
 @pytest.mark.parametrize("rows,hidden,d", [(24576 + 13, 256, 16), (4096, 128, 16), (1, 256, 16), (77, 256, 8),
                                           (9000, 256, 32)])
-def test_fused_mlps_match_float64(rows, hidden, d):
+def test_fused_mlps_match_float64(rows, hidden, d, h1_masks):
     torch.manual_seed(rows + hidden)
     pol = ActorCritic(d, d, 4, [hidden, hidden], [hidden, hidden], "lrelu").to(DEV)
     nets = [pol.actor, pol.critic]
@@ -59,7 +68,7 @@ def test_fused_mlps_match_float64(rows, hidden, d):
         assert torch.equal(g, g2)
 
 
-def test_fused_mlp_single_network_and_unused_output():
+def test_fused_mlp_single_network_and_unused_output(h1_masks):
     """One network (nets = 1), and a critic whose output gets no gradient (its gradients are zero)."""
     torch.manual_seed(3)
     pol = ActorCritic(16, 16, 4, [256, 256], [256, 256], "lrelu").to(DEV)
@@ -88,7 +97,7 @@ def test_fused_mlp_covers_the_update_and_falls_back():
     assert not lin.networks_fusable([wide.actor, wide.critic], [xa, xc])
 
 
-def test_fused_mlp_backward_twice_on_a_retained_graph():
+def test_fused_mlp_backward_twice_on_a_retained_graph(h1_masks):
     """PPO's first mini-batch runs autograd.grad(retain_graph=True) and then backward() on the same graph
     (ppo.py _check_all_grads): the second backward must see the forward's saved tensors unchanged."""
     torch.manual_seed(4)
