@@ -90,8 +90,8 @@ __global__ __launch_bounds__(BN_THREADS) void bn_stats_partial(const float* __re
 
 // sums over the blocks' partials of `npairs` quantities (part[block][npairs]), in a fixed order: thread
 // (pair j, lane k) of the BN_FINAL_THREADS sums the partials b = k (mod T), T = BN_FINAL_THREADS / npairs
-// threads per pair, eight loads in flight at a time (the partials come from L2 / HBM: one load at a time left a
-// 1 024-block reduction latency-bound at ~70 us), then lane 0 of each pair adds the T lane sums in order
+// threads per pair, 32 (then 8) loads in flight at a time (the partials come from L2 / HBM: one load at a time left
+// a 1 024-block reduction latency-bound at ~70 us), then lane 0 of each pair adds the T lane sums in order
 constexpr int BN_FINAL_THREADS = 1024;
 __device__ void bn_final_sums(const double* __restrict__ part, int npairs, int blocks, double* out) {
   __shared__ double red[BN_FINAL_THREADS];
@@ -99,6 +99,15 @@ __device__ void bn_final_sums(const double* __restrict__ part, int npairs, int b
   double acc = 0.0;
   if (j < npairs) {
     int b = k;
+    // 32 loads in flight: the partials were just written by blocks on every XCD, so each round trip is a
+    // far-memory latency (8 at a time left the final at ~29 us for 1 024 partial rows, profiles/round05_*)
+    for (; b + 31 * T < blocks; b += 32 * T) {
+      double v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) v[u] = part[(size_t)(b + u * T) * npairs + j];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) acc += v[u];
+    }
     for (; b + 7 * T < blocks; b += 8 * T) {
       double v[8];
 #pragma unroll
