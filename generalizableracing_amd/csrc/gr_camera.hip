@@ -232,38 +232,39 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
       ns = nv < GR_CAM_OBST_SLOTS ? nv : GR_CAM_OBST_SLOTS;
     }
     // per 8x32 tile: the gates and obstacle slots whose window meets the tile's ray range (a_u, b_v decrease
-    // with u, v) and whose bounding box reaches into the tile's frustum (gr_cam_gate_outside / _obst_outside).
-    // Slot-major: lane g tests gate g (its set-up above) and lane k obstacle slot k against one tile per
-    // iteration, and the tile's masks are the two ballots (every lane busy, no per-slot loop per tile)
-    wave_lds_sync();  // (the gate and obstacle slots written above)
-    float sg[GR_CAM_SLOT], so[GR_CAM_SLOT];
-    const int g_ok = (int)((valid_mask >> lane) & 1ull);
-#pragma unroll
-    for (int k = 0; k < CAM_SLOT4; ++k) {
-      const float4 q4 = s_slot[(g_ok ? lane : 0) * CAM_SLOT4 + k];
-      sg[4 * k] = q4.x; sg[4 * k + 1] = q4.y; sg[4 * k + 2] = q4.z; sg[4 * k + 3] = q4.w;
-    }
-    int so_ok = 0;
-    if constexpr (obst) {
-      so_ok = lane < ns;
-      load_oslot(s_oslot + (so_ok ? lane : 0) * (GR_CAM_OSLOT / 4), so);
-    }
-    for (int tl = 0; tl < ntx * nty; ++tl) {
+    // with u, v) and whose bounding box reaches into the tile's frustum (gr_cam_gate_outside / _obst_outside)
+    wave_lds_sync();
+    for (int tl = lane; tl < ntx * nty; tl += 64) {
       const int v0 = 8 * (tl / ntx), u0 = 32 * (tl % ntx);
       const int v1 = (v0 + 7 < H ? v0 + 7 : H - 1), u1 = (u0 + 31 < W ? u0 + 31 : W - 1);
-      const float a_hi = s_ray_a[u0], a_lo = s_ray_a[u1], b_hi = s_ray_b[v0], b_lo = s_ray_b[v1];
-      const bool gmeet = g_ok && !(sg[GR_CS_AMAX] < a_lo || sg[GR_CS_AMIN] > a_hi || sg[GR_CS_BMAX] < b_lo ||
-                                   sg[GR_CS_BMIN] > b_hi) && !gr_cam_gate_outside(sg, a_lo, a_hi, b_lo, b_hi);
-      const uint64_t gm = __ballot(gmeet);
-      uint64_t tm = 0;
-      if constexpr (obst) {
-        const bool ometh = so_ok && !(so[GR_CS_AMAX] < a_lo || so[GR_CS_AMIN] > a_hi || so[GR_CS_BMAX] < b_lo ||
-                                      so[GR_CS_BMIN] > b_hi) && !gr_cam_obst_outside(so, a_lo, a_hi, b_lo, b_hi);
-        tm = __ballot(ometh);
+      const float a_hi = cc->ray_a[u0], a_lo = cc->ray_a[u1], b_hi = cc->ray_b[v0], b_lo = cc->ray_b[v1];
+      uint64_t gm = 0;
+      for (uint64_t m = valid_mask; m; m &= m - 1) {
+        const int g = __builtin_ctzll(m);
+        float sg[GR_CAM_SLOT];
+#pragma unroll
+        for (int k = 0; k < CAM_SLOT4; ++k) {
+          const float4 q4 = s_slot[g * CAM_SLOT4 + k];
+          sg[4 * k] = q4.x; sg[4 * k + 1] = q4.y; sg[4 * k + 2] = q4.z; sg[4 * k + 3] = q4.w;
+        }
+        const bool meet = !(sg[GR_CS_AMAX] < a_lo || sg[GR_CS_AMIN] > a_hi || sg[GR_CS_BMAX] < b_lo ||
+                            sg[GR_CS_BMIN] > b_hi) && !gr_cam_gate_outside(sg, a_lo, a_hi, b_lo, b_hi);
+        gm |= (uint64_t)meet << g;
       }
-      if (lane == 0) {
-        s_gmask[tl] = gm;
-        if constexpr (obst) s_tmask[tl] = tm;
+      s_gmask[tl] = gm;
+      if constexpr (obst) {
+        uint64_t tm = 0;
+        for (int k = 0; k < ns; ++k) {
+          const float4 wk = s_oslot[k * (GR_CAM_OSLOT / 4) + 4];
+          bool meet = !(wk.y < a_lo || wk.x > a_hi || wk.w < b_lo || wk.z > b_hi);
+          if (meet) {
+            float sk[GR_CAM_SLOT];
+            load_oslot(s_oslot + k * (GR_CAM_OSLOT / 4), sk);
+            meet = !gr_cam_obst_outside(sk, a_lo, a_hi, b_lo, b_hi);
+          }
+          tm |= (uint64_t)meet << k;
+        }
+        s_tmask[tl] = tm;
       }
     }
   }
