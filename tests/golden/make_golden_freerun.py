@@ -153,6 +153,10 @@ def main():
         out[f"s{stage}_actions"] = acts
         for key, v in recs_k.items():
             out[f"s{stage}_out_{key}"] = np.stack(v)
+        # observation noise is off in this run, so the policy rows equal the critic rows: stored once
+        # (tests/env_golden.py reads obs_critic when obs_policy is absent)
+        if np.array_equal(out[f"s{stage}_out_obs_policy"], out[f"s{stage}_out_obs_critic"]):
+            del out[f"s{stage}_out_obs_policy"]
         val = np.stack(recs_k["valid"])
         dn = np.stack(recs_k["dones"]).astype(bool)
         print(f"stage {stage}: compared at the last step {val[-1].sum()}/{N}; resets inside the run "
