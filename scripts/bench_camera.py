@@ -5,6 +5,11 @@ stream), separately for the calls that re-render every sensor (every 2nd step: u
 0.04 s at step_dt 0.03 s) and the calls that reuse the depth buffer, and reports algorithmic
 bytes per call (gr_camera_bytes_per_env) / time against the HBM peak.
 
+Phases: "synchronized" (default) starts every sensor on the same call, as right after one global reset, so the
+calls alternate between all-render and all-reuse.  "steady" spreads the sensors' ages uniformly over the update
+period first, as a long training run leaves them (each env's phase is set by its own last reset, and episodes end at
+different steps), so every call renders ~1/period of the envs and reuses the rest.
+
   python scripts/bench_camera.py --envs 65536 --steps 40
 """
 from __future__ import annotations
@@ -27,7 +32,8 @@ from generalizableracing_amd.envs.racing_env import RacingEnv  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
-def run(n=65536, steps=40, warmup=6, no_noise=False, period=None, device="cuda:0", obstacles=True) -> dict:
+def run(n=65536, steps=40, warmup=6, no_noise=False, period=None, device="cuda:0", obstacles=True,
+        phase="synchronized") -> dict:
     args = argparse.Namespace(envs=n, steps=steps, warmup=warmup, no_noise=no_noise, period=period)
     cam = CameraCfg(add_noise=not args.no_noise)
     if args.period is not None:
@@ -41,6 +47,14 @@ def run(n=65536, steps=40, warmup=6, no_noise=False, period=None, device="cuda:0
     env._call("gr_camera_bytes_per_env", C.byref(rb), C.byref(ub))
     for k in range(args.warmup):
         env.step(acts[k % 8])
+    if phase == "steady":
+        k_period = 1  # gr_cam_period_steps: renders every k_period steps
+        while k_period * env.cfg.step_dt + 1e-6 < env.cfg.camera.update_period:
+            k_period += 1
+        ages = torch.randint(0, k_period, (n,), generator=torch.Generator().manual_seed(7), dtype=torch.int32)
+        env.camera_age.copy_(ages.to(device))
+    elif phase != "synchronized":
+        raise ValueError(f"phase {phase!r}")
     torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     rendered = []
@@ -63,7 +77,7 @@ def run(n=65536, steps=40, warmup=6, no_noise=False, period=None, device="cuda:0
     bytes_call = n * (mean_frac * rb.value + (1 - mean_frac) * ub.value)
     out = {
         "kernel": "gr::camera_kernel",
-        "noise": not args.no_noise,
+        "noise": not args.no_noise, "phase": phase,
         "envs": n, "steps": args.steps,
         "image": [env.camera.height, env.camera.width],
         "render_fraction": mean_frac,
@@ -88,8 +102,10 @@ def main(argv=None):
     ap.add_argument("--no-noise", action="store_true", help="ablation: policy image without noise")
     ap.add_argument("--period", type=float, default=None, help="camera update_period override (0: every step)")
     ap.add_argument("--gates-only", action="store_true", help="obstacle-free tracks")
+    ap.add_argument("--phase", choices=["synchronized", "steady"], default="synchronized")
     a = ap.parse_args(argv)
-    print(json.dumps(run(a.envs, a.steps, a.warmup, a.no_noise, a.period, obstacles=not a.gates_only)))
+    print(json.dumps(run(a.envs, a.steps, a.warmup, a.no_noise, a.period, obstacles=not a.gates_only,
+                         phase=a.phase)))
 
 
 if __name__ == "__main__":

@@ -157,8 +157,8 @@ def replay(gp, device="cpu", **alg_kw):
         st = roll.storage
         for k in ("returns", "advantages", "actions", "values"):
             x = getattr(st, k).double()
-            want = float(gp[f"ppo_it{it}_{k}_sum"])
-            assert abs(float(x.sum()) - want) <= 1e-6 * float(gp[f"ppo_it{it}_{k}_abssum"]), (it, k)
+            want = float(gp[f"ppo_it{it}_{k}_sum"].item())
+            assert abs(float(x.sum()) - want) <= 1e-6 * float(gp[f"ppo_it{it}_{k}_abssum"].item()), (it, k)
             np.testing.assert_allclose(getattr(st, k).flatten()[:4096].numpy(), gp[f"ppo_it{it}_{k}_head"],
                                        rtol=1e-5, atol=1e-6, err_msg=f"it{it} {k}")
         for name, v in vars(st).items():
@@ -170,7 +170,7 @@ def replay(gp, device="cpu", **alg_kw):
         torch.manual_seed(200 + it)
         with cpu_randperm(), record_grads(upd, grads, count=2 if record else 0):
             losses = upd.update()
-        lr_want = float(gp[f"ppo_it{it}_lr"])
+        lr_want = float(gp[f"ppo_it{it}_lr"].item())
         assert abs(upd.learning_rate - lr_want) <= 1e-6 * lr_want, (it, upd.learning_rate, lr_want)
         gerr = []
         # mini-batch 1 of the second update starts from Adam moments that followed the build's own first update
@@ -184,7 +184,7 @@ def replay(gp, device="cpu", **alg_kw):
                 assert e <= tol, (it, j, name, e)
                 gerr.append(e)
         for k, v in losses.items():
-            want = float(gp[f"ppo_it{it}_loss_{k}"])
+            want = float(gp[f"ppo_it{it}_loss_{k}"].item())
             # (second update: the means over a trajectory that has left the reference's by up to 37 % of an update in
             # the reference's own round-off spread, see below)
             tol = (2e-4, 1e-3)[it] if k == "surrogate" else 1e-3 * max(abs(want), 1e-3)
@@ -193,8 +193,8 @@ def replay(gp, device="cpu", **alg_kw):
         dev = float((got - want).norm() / (want - p0).norm())
         assert dev <= (0.15, 0.75)[it], (it, dev)
         report.append({"grad_err": max(gerr) if gerr else None, "param_dev_of_update": dev,
-                       "value_loss_rel": abs(losses["value_function"] - float(gp[f"ppo_it{it}_loss_value_function"]))
-                       / abs(float(gp[f"ppo_it{it}_loss_value_function"]))})
+                       "value_loss_rel": abs(losses["value_function"] - float(gp[f"ppo_it{it}_loss_value_function"].item()))
+                       / abs(float(gp[f"ppo_it{it}_loss_value_function"].item()))})
         # teacher forcing: the next rollout and update start from the reference's parameters (Adam's moments and
         # the learning rate are the build's own)
         for alg in (roll, upd):
