@@ -263,11 +263,15 @@ GR_HD float gr_cam_obs(float d, float z, float std, float scale, float inv_scale
 /* the critic image: no noise */
 GR_HD float gr_cam_obs_clean(float d, float scale, float inv_scale) { return (d > scale ? scale : d) * inv_scale; }
 
-/* the four standard normals of pixel quad `quad` (pixels 4*quad .. 4*quad+3) */
-GR_HD void gr_cam_noise4(uint32_t gid, uint32_t cnt, uint32_t quad, uint32_t k0, uint32_t k1, float z[4]) {
+/* the four standard normals of pixel quad `quad` (pixels 4*quad .. 4*quad+3): one Philox block, one word per pixel
+ * through the inverse-CDF table (`tab` = GR_NORMAL_TABLE_INIT's floats, gr_normal24) */
+GR_HD void gr_cam_noise4(uint32_t gid, uint32_t cnt, uint32_t quad, uint32_t k0, uint32_t k1, const float* tab,
+                         float z[4]) {
   const gr_u32x4 r = gr_philox4x32_10(gid, cnt, GR_TAG_IMG, quad, k0, k1);
-  gr_box_muller(r.x, r.y, &z[0], &z[1]);
-  gr_box_muller(r.z, r.w, &z[2], &z[3]);
+  z[0] = gr_normal24(r.x, tab);
+  z[1] = gr_normal24(r.y, tab);
+  z[2] = gr_normal24(r.z, tab);
+  z[3] = gr_normal24(r.w, tab);
 }
 
 /* Isaac Lab sensor timing (SensorBase.update / _update_outdated_buffers): a sensor is

@@ -15,8 +15,14 @@
 // [16 state terms | image], the policy image with fresh multiplicative noise.
 #include "gr_camera.h"
 #include "gr_kernels.h"
+#include "gr_normal_table.h"
 
 namespace gr {
+
+static_assert(CAM_NORMAL_FLOATS == 4 * GR_NORMAL_TABLE_ENTRIES && GR_NORMAL_TABLE_ENTRIES % 64 == 0,
+              "normal table size (gr_kernels.h)");
+// the image noise's inverse-CDF table (gr_rng.h gr_normal24); each workgroup copies it into LDS
+__constant__ __attribute__((aligned(16))) float cam_normal_tab[4 * GR_NORMAL_TABLE_ENTRIES] = GR_NORMAL_TABLE_INIT;
 
 #define DEV_INLINE __device__ __forceinline__
 
@@ -35,11 +41,11 @@ static_assert(GR_CAM_SLOT == GR_CAM_GATE_SLOT, "gate slot size (gr_camera.h / gr
 #endif
 
 // both observation rows of one pixel quad: fresh noise (quad index q), normalisation, streaming stores
-DEV_INLINE void emit_quad(const CamArgs& a, const gr_cam_const* __restrict__ cc, float4* op4, float4* oc4, int q,
-                          float4 d4, uint32_t gid, uint32_t cnt) {
+DEV_INLINE void emit_quad(const CamArgs& a, const gr_cam_const* __restrict__ cc, const float* ntab, float4* op4,
+                          float4* oc4, int q, float4 d4, uint32_t gid, uint32_t cnt) {
   const float scale = cc->obs_scale, inv = cc->inv_obs_scale, nstd = cc->noise_std;
   float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  if (cc->add_noise) gr_cam_noise4(gid, cnt, (uint32_t)q, a.seed_lo, a.seed_hi, z);
+  if (cc->add_noise) gr_cam_noise4(gid, cnt, (uint32_t)q, a.seed_lo, a.seed_hi, ntab, z);
   float4 op, oc;
   op.x = gr_cam_obs(d4.x, z[0], nstd, scale, inv); oc.x = gr_cam_obs_clean(d4.x, scale, inv);
   op.y = gr_cam_obs(d4.y, z[1], nstd, scale, inv); oc.y = gr_cam_obs_clean(d4.y, scale, inv);
@@ -66,8 +72,8 @@ DEV_INLINE void state_terms(const CamArgs& a, int i, int lane, size_t row) {
 }
 
 // sensor up to date: stream the depth buffer into both rows, CAM_BATCH loads in flight per lane
-DEV_INLINE void reuse_rows(const CamArgs& a, const gr_cam_const* __restrict__ cc, const float4* dep4, float4* op4,
-                           float4* oc4, int nq, int lane, uint32_t gid, uint32_t cnt) {
+DEV_INLINE void reuse_rows(const CamArgs& a, const gr_cam_const* __restrict__ cc, const float* ntab, const float4* dep4,
+                           float4* op4, float4* oc4, int nq, int lane, uint32_t gid, uint32_t cnt) {
   for (int q0 = 0; q0 < nq; q0 += 64 * CAM_BATCH) {
     float4 dd[CAM_BATCH];
 #pragma unroll
@@ -78,7 +84,7 @@ DEV_INLINE void reuse_rows(const CamArgs& a, const gr_cam_const* __restrict__ cc
 #pragma unroll
     for (int j = 0; j < CAM_BATCH; ++j) {
       const int q = q0 + 64 * j + lane;
-      if (q < nq) emit_quad(a, cc, op4, oc4, q, dd[j], gid, cnt);
+      if (q < nq) emit_quad(a, cc, ntab, op4, oc4, q, dd[j], gid, cnt);
     }
   }
 }
@@ -125,10 +131,21 @@ DEV_INLINE void quad_obst(const float* s, const float av[4], float b, float d[4]
 template <bool OBST>
 __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs a) {
   extern __shared__ float4 smem4[];
-  float* smem = reinterpret_cast<float*>(smem4);
+  float* smem = reinterpret_cast<float*>(smem4);  // [normal table | ray tables | per-wave slots]
   const gr_cam_const* __restrict__ cc = a.cc;
   const int W = a.width, H = a.height, npix = W * H, G = a.max_gates;
   const int wpad = (W + 3) & ~3, hpad = (H + 3) & ~3;
+  // the normal table: in LDS on gate-only tracks; on obstacle tracks the LDS is full at 4 workgroups per CU (the
+  // obstacle slots), so a rendering wave reads the table from the constant segment (5 KB, cache-resident) and a
+  // reusing wave copies it into its own slot area
+  const float* s_ntab = cam_normal_tab;
+  if constexpr (!OBST) {
+    float4* s_ntab4 = smem4;
+    for (int k = threadIdx.x; k < GR_NORMAL_TABLE_ENTRIES; k += CAM_WAVES * 64)
+      s_ntab4[k] = reinterpret_cast<const float4*>(cam_normal_tab)[k];
+    s_ntab = smem;
+    smem += CAM_NORMAL_FLOATS;
+  }
   float* s_ray_a = smem;
   float* s_ray_b = smem + wpad;
   for (int k = threadIdx.x; k < W; k += CAM_WAVES * 64) s_ray_a[k] = cc->ray_a[k];
@@ -281,7 +298,18 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
   const int nq = npix >> 2;
 
   if (!render) {
-    reuse_rows(a, cc, dep4, op4, oc4, nq, lane, gid, cnt);
+    const float* ntab = s_ntab;
+    if constexpr (OBST) {
+      // a reusing wave has no obstacle slots to hold: its slot area takes a copy of the normal table
+      static_assert(CAM_NORMAL_FLOATS <= GR_CAM_OBST_SLOTS * GR_CAM_OSLOT, "normal table vs obstacle slot area");
+      float4* t4 = reinterpret_cast<float4*>(olds);
+#pragma unroll
+      for (int k = 0; k < GR_NORMAL_TABLE_ENTRIES / 64; ++k)
+        t4[64 * k + lane] = reinterpret_cast<const float4*>(cam_normal_tab)[64 * k + lane];
+      wave_lds_sync();
+      ntab = olds;
+    }
+    reuse_rows(a, cc, ntab, dep4, op4, oc4, nq, lane, gid, cnt);
     return;
   }
 
@@ -396,7 +424,7 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
     for (int qq = lane; qq < nqb; qq += 64) {
       const float4 d4 = s_stage[qq];
       nt_store4(dep4 + qb + qq, d4);
-      emit_quad(a, cc, op4, oc4, qb + qq, d4, gid, cnt);
+      emit_quad(a, cc, s_ntab, op4, oc4, qb + qq, d4, gid, cnt);
     }
     wave_lds_sync();
   }

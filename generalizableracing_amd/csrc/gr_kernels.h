@@ -189,10 +189,12 @@ __host__ __device__ inline size_t camera_tile_mask_floats(int width, int height)
 __host__ __device__ inline size_t camera_obst_floats(int width, int height) {
   return (size_t)GR_CAM_OBST_SLOTS * GR_CAM_OSLOT + camera_tile_mask_floats(width, height);
 }
+// (the normal table of the image noise, gr_normal_table.h: 4 floats per entry, first in LDS on gate-only tracks)
+#define CAM_NORMAL_FLOATS (4 * 320)
 inline size_t camera_lds_bytes(int width, int height, int max_gates, bool obst) {
   const size_t wpad = (size_t)((width + 3) & ~3), hpad = (size_t)((height + 3) & ~3);
   const size_t os = obst ? camera_obst_floats(width, height) : 0;
-  return 4 * (wpad + hpad +
+  return 4 * ((obst ? 0 : CAM_NORMAL_FLOATS) + wpad + hpad +
               4 * ((size_t)max_gates * GR_CAM_GATE_SLOT + camera_tile_mask_floats(width, height) + os + 8 * (size_t)width));
 }
 

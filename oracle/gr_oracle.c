@@ -29,6 +29,9 @@
 #include "../generalizableracing_amd/csrc/gr_math.h"
 #include "../generalizableracing_amd/csrc/gr_rng.h"
 #include "../generalizableracing_amd/csrc/gr_camera.h"
+#include "../generalizableracing_amd/csrc/gr_normal_table.h"
+
+static const float GRO_NORMAL_TAB[4 * GR_NORMAL_TABLE_ENTRIES] = GR_NORMAL_TABLE_INIT;
 
 size_t gro_env_size(void) { return sizeof(gro_env); }
 
@@ -851,6 +854,16 @@ void gro_draws(const gr_config* c, int i, int kind, uint32_t c1, uint32_t c3, fl
   }
 }
 
+/* gr_normal24 of n words (the camera noise's inverse-CDF table) */
+void gro_test_normal24(int n, const uint32_t* w, float* z) {
+  for (int i = 0; i < n; ++i) z[i] = gr_normal24(w[i], GRO_NORMAL_TAB);
+}
+
+/* the camera noise of env id gid, call counter cnt, pixel quads q0 .. q0 + nq - 1 (gr_cam_noise4): z[4 nq] */
+void gro_test_cam_noise(uint32_t gid, uint32_t cnt, uint32_t q0, int nq, uint32_t k0, uint32_t k1, float* z) {
+  for (int q = 0; q < nq; ++q) gr_cam_noise4(gid, cnt, q0 + (uint32_t)q, k0, k1, GRO_NORMAL_TAB, z + 4 * q);
+}
+
 void gro_test_fields6(int n, const uint32_t* in4, uint32_t* out6) {
   for (int i = 0; i < n; ++i) {
     gr_u32x4 r = {in4[i * 4], in4[i * 4 + 1], in4[i * 4 + 2], in4[i * 4 + 3]};
@@ -924,7 +937,7 @@ void gro_camera(const gr_config* c, const gr_camera_config* kcfg, const gro_env*
     const uint32_t gid = gid_of(c, i);
     for (int q = 0; q < npix / 4; ++q) {
       float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (K.add_noise) gr_cam_noise4(gid, cnt, (uint32_t)q, c->seed_lo, c->seed_hi, z);
+      if (K.add_noise) gr_cam_noise4(gid, cnt, (uint32_t)q, c->seed_lo, c->seed_hi, GRO_NORMAL_TAB, z);
       for (int j = 0; j < 4; ++j) {
         const float d = dep[4 * q + j];
         rp[16 + 4 * q + j] = gr_cam_obs(d, z[j], K.noise_std, K.obs_scale, K.inv_obs_scale);

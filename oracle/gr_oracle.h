@@ -68,6 +68,8 @@ void gro_test_math(int fn, int n, const float* x, const float* y, float* out);
 void gro_test_philox(int n, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
                      uint32_t* out4);
 void gro_test_fields6(int n, const uint32_t* in4, uint32_t* out6);
+void gro_test_normal24(int n, const uint32_t* w, float* z);
+void gro_test_cam_noise(uint32_t gid, uint32_t cnt, uint32_t q0, int nq, uint32_t k0, uint32_t k1, float* z);
 /* depth camera + depth_image observation, same contract as gr_camera_render (include/gr.h);
  * cnt = the observation counter of the call the images belong to */
 void gro_camera(const gr_config* cfg, const gr_camera_config* kcfg, const gro_env* envs, int n, const gro_tracks* tr,

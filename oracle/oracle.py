@@ -51,6 +51,8 @@ def load():
             "gro_test_math": [C.c_int, C.c_int, vp, vp, vp],
             "gro_test_philox": [C.c_int] + [C.c_uint32] * 6 + [vp],
             "gro_test_fields6": [C.c_int, vp, vp],
+            "gro_test_normal24": [C.c_int, vp, vp],
+            "gro_test_cam_noise": [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, vp],
             "gro_num_threads": [],
             "gro_camera": [vp, vp, vp, C.c_int, vp, C.c_int, vp, vp, vp, C.c_uint32, vp, vp, vp, vp, vp, vp],
             "gro_camera_frame": [vp, vp, vp, vp, vp],
@@ -296,3 +298,19 @@ def envs_to_planes(envs: np.ndarray, num_planes: int = 17):
     istate[:, 3] = (envs["gate_id"] & 0xFF) | ((envs["level"] & 0xFF) << 8) | ((envs["azero"] & 1) << 16) | \
         ((envs["type"] & 0xFF) << 24)
     return state, istate
+
+
+def test_normal24(words: np.ndarray) -> np.ndarray:
+    """gr_normal24 (the camera noise's inverse-CDF normal) of each uint32 word."""
+    w = np.ascontiguousarray(words, dtype=np.uint32).ravel()
+    out = np.zeros(w.size, np.float32)
+    load().gro_test_normal24(w.size, _p(w), _p(out))
+    return out
+
+
+def test_cam_noise(gid: int, cnt: int, q0: int, nq: int, k0: int, k1: int) -> np.ndarray:
+    """The camera's image noise (gr_cam_noise4) of env id gid, call counter cnt, quads q0 .. q0 + nq - 1: [4 nq]."""
+    out = np.zeros(4 * nq, np.float32)
+    load().gro_test_cam_noise(gid & 0xFFFFFFFF, cnt & 0xFFFFFFFF, q0 & 0xFFFFFFFF, nq, k0 & 0xFFFFFFFF,
+                              k1 & 0xFFFFFFFF, _p(out))
+    return out
