@@ -746,6 +746,232 @@ __global__ __launch_bounds__(SM_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, i
   }
 }
 
+// ------------------------------------------------------------- the first block's backward fused with conv2's dgrad
+// conv2 = Conv2d(16, 32, 3, stride 3) on the first block's output, whose rows come grouped as conv2's patches (cell
+// 9 p + j of table a is position j of patch p).  Its input gradient gy1[cell 9 p + j][c] = sum_o gz2[p][o] W2[o][j, c]
+// was a GEMM writing [rows, 144] (1.13 GB per 24 576-image mini-batch) that both backward passes then read back.
+// Here the passes form it themselves: a tile is 16 patches at one position j, so
+//   gy1 tile = gz2[16 patches][32] x W2[32][j, 16 channels]: eight v_mfma_f32_16x16x4f32, k step s of lane group g
+//   taking o = 8 g + s (A: the lane's patch row of gz2, two float4; B: W2 re-laid as w2t[j][g][c][s], two float4),
+// and the output fragment (patch 4 (l/16) + v, channel l % 16) is exactly the conv1 fragment of the same 16 cells
+// (cells 9 (16 chunk + i) + j as the tile's rows).  Table b's cells (not under conv2) have gy1 = 0: they add nothing
+// to the reduce pass and are still walked by the weight-gradient pass (their gx is not 0).
+struct Sm12Args {
+  const float* bw;
+  const float* bb;
+  const float* stats;
+  const float* sums;  // SM_WGRAD
+  const float* gz2;   // [nimg * n2][32]
+  const float* w2t;   // [9][4][16][8]: W2[o = 8 g + s][j * 16 + c] at ((j * 4 + g) * 16 + c) * 8 + s
+  double* part;
+  float slope;
+  int n2;             // conv2 patches per image (na = 9 n2)
+};
+
+template <int PASS, int ACT, bool V4>
+__global__ __launch_bounds__(SM_THREADS) void stem12b_kernel(Stem1 s, Sm12Args q, int cap) {
+  extern __shared__ float4 sm_dyn4[];
+  __shared__ int s_span;
+  __shared__ float pimg[SM_WAVES][16][17];
+  const int na = s.na, nbt = s.nbt, ncell = na + nbt, n2 = q.n2;
+  short* tab = reinterpret_cast<short*>(sm_dyn4);
+  float* im0 = reinterpret_cast<float*>(sm_dyn4) + sm_tab_floats(ncell);
+  float* im1 = im0 + sm_img_floats(cap);
+  const unsigned l = threadIdx.x & 63, ch = l & 15, kq = l >> 4, w = sm_wave();
+  const bool loader = w == SM_WAVES;
+  if (threadIdx.x == 0) s_span = 0;
+  __syncthreads();
+  int mx = 0;
+  for (int i = threadIdx.x; i < ncell * 9; i += SM_THREADS) {
+    const short t = s.pix[i];
+    tab[i] = t;
+    mx = mx > (int)t + 1 ? mx : (int)t + 1;
+  }
+  atomicMax(&s_span, mx);
+  __syncthreads();
+  const int span = s_span;
+  const bool staged = span <= cap;
+  const bool v4 = V4 && (span & 3) == 0;
+
+  float wb[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) wb[c] = kq + 4 * c < 9 ? s.w[ch * 9 + kq + 4 * c] : 0.0f;
+  const float mu = q.stats[ch], is = q.stats[16 + ch], wv = q.bw[ch], bv = q.bb[ch];
+  const unsigned m = (unsigned)s.nimg * (unsigned)ncell;
+  float mg = 0.0f, mgx = 0.0f;
+  if constexpr (PASS == SM_WGRAD) {
+    const float inv_m = 1.0f / (float)m;
+    mg = q.sums[ch] * inv_m;
+    mgx = q.sums[16 + ch] * inv_m;
+    if (!loader) pimg[w][l & 15][12 + kq] = 0.0f;
+  }
+  const float isw = is * wv;
+  double a0 = 0.0, a1 = 0.0, g4[4] = {0.0, 0.0, 0.0, 0.0};
+  const int nch = (n2 + 15) / 16, ta = 9 * nch;
+  const int T = ta + (PASS == SM_WGRAD ? (nbt + 15) / 16 : 0);
+  constexpr int U = 3;
+
+  const int nmine = s.nimg > (int)blockIdx.x ? (s.nimg - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
+  if (staged && loader && nmine > 0) sm_dma_image(s.obs + (long long)blockIdx.x * s.ld + s.off, im0, span, v4);
+  __syncthreads();
+  for (int k = 0; k < nmine; ++k) {
+    const int b = (int)blockIdx.x + k * (int)gridDim.x;
+    const float* g = s.obs + (long long)b * s.ld + s.off;
+    const float* im = (k & 1) ? im1 : im0;
+    if (loader) {
+      if (staged && k + 1 < nmine) sm_dma_image(g + (long long)gridDim.x * s.ld, (k & 1) ? im0 : im1, span, v4);
+    } else {
+      auto tiles = [&](auto from_lds) {
+      for (int j0 = (int)w; j0 < T; j0 += SM_WAVES * U) {
+        int nvalid[U];
+        bool conv2t[U];  // a table-a tile (gy1 from gz2); else table b (gy1 = 0)
+        float px[U][3];
+        int po[U][3];
+        float4 za[U][2], wf[U][2];  // gz2 A fragments, W2 B fragments
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int t = j0 + SM_WAVES * u;
+          int cell;
+          conv2t[u] = t < ta;
+          if (t < ta) {
+            const int chunk = t / 9, jj = t - 9 * chunk;
+            nvalid[u] = n2 - 16 * chunk < 16 ? n2 - 16 * chunk : 16;
+            const int p = 16 * chunk + ((int)(l & 15) < nvalid[u] ? (int)(l & 15) : 0);
+            cell = 9 * p + jj;
+            const float4* zr = reinterpret_cast<const float4*>(q.gz2 + ((size_t)b * n2 + p) * 32 + 8 * kq);
+            za[u][0] = zr[0];
+            za[u][1] = zr[1];
+            const float4* wr = reinterpret_cast<const float4*>(q.w2t + (size_t)((jj * 4 + (int)kq) * 16 + (int)ch) * 8);
+            wf[u][0] = wr[0];
+            wf[u][1] = wr[1];
+          } else if (t < T) {
+            const int jb = 16 * (t - ta);
+            nvalid[u] = nbt - jb < 16 ? nbt - jb : 16;
+            cell = na + jb + ((int)(l & 15) < nvalid[u] ? (int)(l & 15) : 0);
+            za[u][0] = za[u][1] = wf[u][0] = wf[u][1] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+          } else {
+            nvalid[u] = 0;
+            cell = 0;
+            za[u][0] = za[u][1] = wf[u][0] = wf[u][1] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+          }
+          const short* tt = tab + cell * 9;
+          po[u][0] = tt[kq];
+          po[u][1] = tt[kq + 4];
+          po[u][2] = tt[8];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if constexpr (decltype(from_lds)::value) {
+            px[u][0] = im[po[u][0]];
+            px[u][1] = im[po[u][1]];
+            px[u][2] = im[po[u][2]];
+          } else {
+            px[u][0] = g[po[u][0]];
+            px[u][1] = g[po[u][1]];
+            px[u][2] = g[po[u][2]];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const sm4 x = sm_conv(px[u], wb);
+          // gy1 of the tile's rows (patches 4 kq + v, channel ch): k step s of lane group kq is o = 8 kq + s
+          sm4 gyt = {0.0f, 0.0f, 0.0f, 0.0f};
+          if (conv2t[u]) {  // (wave-uniform)
+            const float a8[8] = {za[u][0].x, za[u][0].y, za[u][0].z, za[u][0].w, za[u][1].x, za[u][1].y, za[u][1].z, za[u][1].w};
+            const float b8[8] = {wf[u][0].x, wf[u][0].y, wf[u][0].z, wf[u][0].w, wf[u][1].x, wf[u][1].y, wf[u][1].z, wf[u][1].w};
+#pragma unroll
+            for (int ss = 0; ss < 8; ++ss) gyt = sm_mfma(a8[ss], b8[ss], gyt);
+          }
+          float gz[4], xh[4];
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const bool live = (int)(4 * kq + v) < nvalid[u];
+            xh[v] = (x[v] - mu) * is;
+            gz[v] = (live ? gyt[v] : 0.0f) * bn_dact<ACT>(xh[v] * wv + bv, q.slope);
+          }
+          if constexpr (PASS == SM_BWDP) {
+            float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              s0 += gz[v];
+              s1 += gz[v] * xh[v];
+            }
+            a0 += (double)s0;
+            a1 += (double)s1;
+          } else {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              const bool okc = (int)(l & 15) < nvalid[u] && (c < 2 || kq == 0);
+              pimg[w][l & 15][kq + 4 * c] = okc ? px[u][c] : 0.0f;
+            }
+            sm4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              const float gx = (gz[v] - mg - xh[v] * mgx) * isw;
+              acc = sm_mfma(gx, pimg[w][4 * kq + v][ch], acc);
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) g4[c] += (double)acc[c];
+          }
+        }
+      }
+      };
+      if (staged)
+        tiles(std::true_type{});
+      else
+        tiles(std::false_type{});
+    }
+    __syncthreads();
+  }
+
+  double* red = reinterpret_cast<double*>(im0);
+  if constexpr (PASS == SM_BWDP) {
+    if (!loader) {
+      red[threadIdx.x] = a0;
+      red[BN_THREADS + threadIdx.x] = a1;
+    }
+    __syncthreads();
+    if (threadIdx.x < 32) {
+      const int qq = threadIdx.x >> 4, c = threadIdx.x & 15;
+      double acc = 0.0;
+      for (int ww = 0; ww < BN_THREADS / 64; ++ww)
+        for (int k = 0; k < 4; ++k) acc += red[qq * BN_THREADS + ww * 64 + k * 16 + c];
+      q.part[(size_t)blockIdx.x * 32 + threadIdx.x] = acc;
+    }
+  } else {
+    if (!loader) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) red[c * BN_THREADS + threadIdx.x] = g4[c];
+    }
+    __syncthreads();
+    for (int v = threadIdx.x; v < 16 * 9; v += BN_THREADS) {
+      const int c2 = v / 9, k = v % 9, lane = (c2 >> 2) * 16 + k, c = c2 & 3;
+      double t = 0.0;
+      for (int ww = 0; ww < BN_THREADS / 64; ++ww) t += red[c * BN_THREADS + ww * 64 + lane];
+      q.part[(size_t)blockIdx.x * 144 + v] = t;
+    }
+  }
+}
+
+template <int PASS>
+static void sm12_launch(const Stem1& s, const Sm12Args& q, int act, int grid, hipStream_t st) {
+  long long room = s.ld - s.off;
+  const int cap = (int)(room < 1 ? 1 : room < SM_IMG_CAP ? room : SM_IMG_CAP);
+  const size_t lds = sm_lds_bytes(s.na + s.nbt, cap);
+  const bool v4 = ((uintptr_t)(s.obs + s.off) & 15) == 0 && (s.ld & 3) == 0;
+  if (act == GR_POLICY_ACT_ELU) {
+    if (v4)
+      hipLaunchKernelGGL((stem12b_kernel<PASS, GR_POLICY_ACT_ELU, true>), dim3(grid), dim3(SM_THREADS), lds, st, s, q, cap);
+    else
+      hipLaunchKernelGGL((stem12b_kernel<PASS, GR_POLICY_ACT_ELU, false>), dim3(grid), dim3(SM_THREADS), lds, st, s, q, cap);
+  } else {
+    if (v4)
+      hipLaunchKernelGGL((stem12b_kernel<PASS, GR_POLICY_ACT_LRELU, true>), dim3(grid), dim3(SM_THREADS), lds, st, s, q, cap);
+    else
+      hipLaunchKernelGGL((stem12b_kernel<PASS, GR_POLICY_ACT_LRELU, false>), dim3(grid), dim3(SM_THREADS), lds, st, s, q, cap);
+  }
+}
+
 template <int PASS>
 static void sm_launch(const Stem1& s, const SmArgs& q, int act, int grid, hipStream_t st) {
   long long room = s.ld - s.off;
@@ -821,6 +1047,22 @@ hipError_t launch_stem1_backward(const Stem1& s, const float* bw, const float* b
   else
     hipLaunchKernelGGL(stem1_bwd_wgrad<GR_POLICY_ACT_LRELU>, dim3(nb), dim3(BN_THREADS), 0, st, s, gy, bw, bb, stats, sums, slope, wpart);
   hipLaunchKernelGGL(stem1_wgrad_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, 9 * s.c, nb, wpart, gconv);
+  return hipGetLastError();
+}
+
+hipError_t launch_stem12_backward(const Stem1& s, const float* bw, const float* bb, const float* stats, int act,
+                                  float slope, const float* gz2, int n2, const float* w2t, float* gconv, float* gbw,
+                                  float* gbb, double* part, hipStream_t st) {
+  const int nb = stem_blocks(s);
+  float* sums = reinterpret_cast<float*>(part + (size_t)nb * 2 * s.c);
+  double* wpart = part + (size_t)nb * 2 * s.c + 2 * s.c;
+  const int grid = nb < SM_GRID ? nb : SM_GRID;
+  Sm12Args q{bw, bb, stats, sums, gz2, w2t, part, slope, n2};
+  sm12_launch<SM_BWDP>(s, q, act, grid, st);
+  hipLaunchKernelGGL(bn_bwd_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, s.c, grid, part, gbw, gbb, sums);
+  q.part = wpart;
+  sm12_launch<SM_WGRAD>(s, q, act, grid, st);
+  hipLaunchKernelGGL(stem1_wgrad_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, 9 * s.c, grid, wpart, gconv);
   return hipGetLastError();
 }
 

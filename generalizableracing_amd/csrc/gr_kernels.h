@@ -116,6 +116,10 @@ hipError_t launch_stem1_forward(const Stem1& s, const float* bw, const float* bb
 hipError_t launch_stem1_backward(const Stem1& s, const float* bw, const float* bb, const float* stats, int act,
                                  float slope, const float* gy, float* gconv, float* gbw, float* gbb, double* part,
                                  hipStream_t st);
+// the same backward with conv2's input gradient formed inside the passes (C = 16, na = 9 n2; gr_bn.hip stem12b_kernel)
+hipError_t launch_stem12_backward(const Stem1& s, const float* bw, const float* bb, const float* stats, int act,
+                                  float slope, const float* gz2, int n2, const float* w2t, float* gconv, float* gbw,
+                                  float* gbb, double* part, hipStream_t st);
 hipError_t launch_bn_forward(const float* x, long long m, int c, const float* w, const float* b, float eps, int act,
                              float slope, float* y, float* stats, double* part, hipStream_t s);
 hipError_t launch_bn_backward(const float* x, const float* gy, long long m, int c, const float* w, const float* b,

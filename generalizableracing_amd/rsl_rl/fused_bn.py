@@ -138,6 +138,88 @@ class _Stem1(torch.autograd.Function):
         return None, gconv.view(wshape), gbw, gbb, None, None, None, None, None, None
 
 
+class _Stem12(torch.autograd.Function):
+    """The first block (as _Stem1, C = 16) followed by conv2 as a patch GEMM: z2 = y1.view(-1, 144) @ w2^T, w2 [32, 144]
+    in (position j, channel) column order.  The forward is _Stem1's kernels plus the GEMM; the backward takes conv2's
+    output gradient straight into the first block's passes (gr_stem12_backward): conv2's input gradient, a
+    [rows, 144] matrix, is never written.  conv2's weight gradient is the split-K product of gz2 and y1 (saved)."""
+
+    @staticmethod
+    def forward(ctx, img, conv_w, bn_w, bn_b, w2, pix, na, nb, eps, act, slope):
+        lib = _abi.load()
+        nimg = img.shape[0]
+        rows = nimg * na
+        y = torch.empty(rows, 16, device=img.device, dtype=torch.float32)
+        stats = torch.empty(4, 16, device=img.device, dtype=torch.float32)
+        part = torch.empty(int(lib.gr_stem1_scratch_doubles(nimg, na + nb, 16)), device=img.device, dtype=torch.float64)
+        w = conv_w.detach().reshape(16, 9).contiguous()
+        bw, bb = bn_w.detach().contiguous(), bn_b.detach().contiguous()
+        rc = lib.gr_stem1_forward(img.data_ptr(), img.stride(0), 0, nimg, pix.data_ptr(), na, nb, w.data_ptr(), 16,
+                                  bw.data_ptr(), bb.data_ptr(), float(eps), act, float(slope), y.data_ptr(), rows,
+                                  stats.data_ptr(), part.data_ptr(), _stream(img))
+        if rc != 0:
+            raise RuntimeError(f"gr_stem1_forward failed (status {rc})")
+        w2d = w2.detach()
+        z2 = y.view(-1, 144) @ w2d.t()
+        ctx.save_for_backward(img, w, bw, bb, stats, y, w2d)
+        ctx.pix = pix
+        ctx.args = (na, nb, act, slope, conv_w.shape)
+        ctx.mark_non_differentiable(stats)
+        return z2, stats
+
+    @staticmethod
+    def backward(ctx, gz2, _gstats):
+        if ctx.needs_input_grad[0]:
+            raise RuntimeError("the fused stem computes no gradient for the image")
+        lib = _abi.load()
+        img, w, bw, bb, stats, y, w2d = ctx.saved_tensors
+        na, nb, act, slope, wshape = ctx.args
+        nimg = img.shape[0]
+        gz2 = gz2.contiguous()
+        gw2 = None
+        if ctx.needs_input_grad[4]:  # conv2's weight: gz2^T y1 patches, split over the rows (as _PatchGemm)
+            x = y.view(-1, 144)
+            m, c = x.shape[0], 8192
+            sp = m // c
+            if sp >= 2:
+                gw2 = torch.bmm(gz2[: sp * c].view(sp, c, -1).transpose(1, 2), x[: sp * c].view(sp, c, -1)).sum(0)
+                if m > sp * c:
+                    gw2 = gw2 + gz2[sp * c:].t() @ x[sp * c:]
+            else:
+                gw2 = gz2.t() @ x
+        # w2t[j][g][ch][s] = W2[o = 8 g + s][j * 16 + ch]
+        w2t = w2d.reshape(4, 8, 9, 16).permute(2, 0, 3, 1).contiguous()
+        gconv = torch.empty(16, 9, device=img.device, dtype=torch.float32)
+        gbw = torch.empty(16, device=img.device, dtype=torch.float32)
+        gbb = torch.empty(16, device=img.device, dtype=torch.float32)
+        part = torch.empty(int(lib.gr_stem1_scratch_doubles(nimg, na + nb, 16)), device=img.device, dtype=torch.float64)
+        rc = lib.gr_stem12_backward(img.data_ptr(), img.stride(0), 0, nimg, ctx.pix.data_ptr(), na, nb, w.data_ptr(), 16,
+                                    bw.data_ptr(), bb.data_ptr(), stats.data_ptr(), act, float(slope), gz2.data_ptr(),
+                                    na // 9, w2t.data_ptr(), gconv.data_ptr(), gbw.data_ptr(), gbb.data_ptr(),
+                                    part.data_ptr(), _stream(img))
+        if rc != 0:
+            raise RuntimeError(f"gr_stem12_backward failed (status {rc})")
+        return None, gconv.view(wshape), gbw, gbb, gw2, None, None, None, None, None, None
+
+
+def stem12_applicable(bn: nn.BatchNorm2d, act: nn.Module, img: torch.Tensor, conv_w: torch.Tensor,
+                      conv2_w: torch.Tensor, na: int) -> bool:
+    """The fused first block + conv2 backward: stem1_applicable with 16 channels, conv2 = Conv2d(16, 32, 3, stride 3)
+    without bias, and the table-a rows grouped as its patches (na = 9 n2)."""
+    return (stem1_applicable(bn, act, img, conv_w) and conv_w.shape[0] == 16 and
+            tuple(conv2_w.shape) == (32, 16, 3, 3) and conv2_w.dtype == torch.float32 and na % 9 == 0)
+
+
+def stem12_bn_act_conv(bn: nn.BatchNorm2d, act: nn.Module, conv_w: torch.Tensor, w2: torch.Tensor, img: torch.Tensor,
+                       pix: torch.Tensor, na: int, nb: int, uses: int = 1) -> torch.Tensor:
+    """conv2's output rows [B * na / 9, 32] = patches(act(bn(conv(img)))) @ w2^T (w2 [32, 144], columns (j, c)),
+    running statistics of the first BN updated as stem1_bn_act does."""
+    code, slope = _act_code(act)
+    z2, stats = _Stem12.apply(img, conv_w, bn.weight, bn.bias, w2, pix, na, nb, bn.eps, code, slope)
+    _update_running(bn, stats, uses)
+    return z2
+
+
 def stem1_applicable(bn: nn.BatchNorm2d, act: nn.Module, img: torch.Tensor, conv_w: torch.Tensor) -> bool:
     """The image-side HIP op: fp32 CUDA image rows (unit column stride), a 1-channel 3x3 conv without bias into
     C in {4, 8, 16, 32, 64} channels, training-mode BN, LeakyReLU / ELU(1)."""

@@ -24,7 +24,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .actor_critic import ActorCritic, resolve_nn_activation
-from .fused_bn import batch_norm_act, fused_applicable, stem1_applicable, stem1_bn_act
+from .fused_bn import (batch_norm_act, fused_applicable, stem1_applicable, stem1_bn_act, stem12_applicable,
+                       stem12_bn_act_conv)
 
 
 def _conv_out(n: int, k: int, s: int) -> int:
@@ -72,6 +73,9 @@ class VisionActorCritic(ActorCritic):
     # training-mode BatchNorm + activation of the stem as one HIP op on the GPU (rsl_rl/fused_bn.py); False:
     # torch's batch_norm and activation ops (tests compare the two)
     fused_bn = True
+    # with fused_bn: conv2's input gradient formed inside the first block's backward passes (fused_bn._Stem12); False:
+    # the first block alone, conv2 as a patch GEMM (tests and scripts/bench_vision.py --no-fused-conv2 compare the two)
+    fused_conv2 = True
 
     def __init__(self, num_actor_obs: int, num_critic_obs: int, num_actions: int, img_res=(72, 96),
                  dim_hidden_input: int = 192, actor_hidden_dims=(256, 256, 256), critic_hidden_dims=(256, 256, 256),
@@ -189,7 +193,15 @@ class VisionActorCritic(ActorCritic):
         B = img.shape[0]
         flat = img.reshape(B, -1)
         idx, idx_left, n1, n1_left, n3, n2, pix16 = self._patch_index(img.device)
-        if self.fused_bn and stem1_applicable(bn1, act, flat, conv1.weight):
+        w2m = conv2.weight.permute(0, 2, 3, 1).reshape(32, 144)  # conv2 on its 3x3 patches, columns (i, j, c)
+        block2 = None
+        if self.fused_bn and self.fused_conv2 and n1 == 9 * n2 and stem12_applicable(bn1, act, flat, conv1.weight, conv2.weight, n1):
+            # conv1 + BN1 + act + conv2: the backward forms conv2's input gradient inside the first block's passes
+            if bn1.track_running_stats and bn1.num_batches_tracked is not None:
+                bn1.num_batches_tracked.add_(1)
+            z2 = stem12_bn_act_conv(bn1, act, conv1.weight, w2m, flat, pix16, n1, n1_left, self._bn_uses)
+            block2 = self._bn_act(bn2, act, z2)
+        elif self.fused_bn and stem1_applicable(bn1, act, flat, conv1.weight):
             # conv1 + BN1 + act from the image itself: no patch matrix, no conv output (rsl_rl/fused_bn.py)
             if bn1.track_running_stats and bn1.num_batches_tracked is not None:
                 bn1.num_batches_tracked.add_(1)
@@ -199,11 +211,12 @@ class VisionActorCritic(ActorCritic):
             if n1_left:
                 x = torch.cat([x, flat.index_select(1, idx_left).view(B * n1_left, 9)])
             y = self._bn_act(bn1, act, _gemm(x, conv1.weight.reshape(16, 9)))
-        # conv2's 3x3 patches (i, j, c): a view (the fused block returns exactly these rows; a slice of the whole
-        # tensor would still cost a zero-filled gradient plus a copy in the backward)
-        x = (y if y.shape[0] == B * n1 else y[: B * n1]).view(B * n2, 144)
-        y = self._bn_act(bn2, act, _gemm(x, conv2.weight.permute(0, 2, 3, 1).reshape(32, 144)))
-        y = y.view(B, n2, 32)
+        if block2 is None:
+            # conv2's 3x3 patches (i, j, c): a view (the fused block returns exactly these rows; a slice of the whole
+            # tensor would still cost a zero-filled gradient plus a copy in the backward)
+            x = (y if y.shape[0] == B * n1 else y[: B * n1]).view(B * n2, 144)
+            block2 = self._bn_act(bn2, act, _gemm(x, w2m))
+        y = block2.view(B, n2, 32)
         x = (y if n3 == n2 else y[:, :n3]).reshape(B * h3 * w3, 128)  # conv3's 2x2 patches: a view at 72x96
         y = self._bn_act(bn3, act, _gemm(x, conv3.weight.permute(0, 2, 3, 1).reshape(64, 128))).view(B, h3 * w3 * 64)
         # reference flatten is NCHW (c, h, w): permute the Linear's columns to (h, w, c) instead

@@ -461,6 +461,16 @@ int gr_stem1_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, c
                       int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b,
                       const float* stats, int32_t act, float slope, const float* gy, int64_t gy_rows, float* g_conv_w,
                       float* g_bn_w, float* g_bn_b, double* part, void* stream);
+/* The same backward when the next layer is the stem's conv2, Conv2d(c = 16, 32, 3, stride 3, no bias), on the
+ * nimg x na table-a rows grouped as its patches (row 9 p + j of an image = position j of patch p, na = 9 n2): takes
+ * conv2's OUTPUT gradient gz2 [nimg * n2][32] (16-byte aligned) and forms conv2's input gradient inside the passes
+ * instead of reading a [nimg * na][16] gy (VisionActorCritic stem; reference vision_actor_critic.py:93-105).
+ * w2t: conv2's weight as [9][4][16][8] floats, w2t[((j * 4 + g) * 16 + ch) * 8 + s] = W[o = 8 g + s][ch][j / 3][j % 3]
+ * (16-byte aligned).  conv2's own weight gradient is not computed here.  Same workspace as gr_stem1_backward. */
+int gr_stem12_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
+                       int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b,
+                       const float* stats, int32_t act, float slope, const float* gz2, int32_t n2, const float* w2t,
+                       float* g_conv_w, float* g_bn_w, float* g_bn_b, double* part, void* stream);
 
 /* Device status: the GR_STATUS_* bits the kernels of this context raised since the last clear (0: none).
  * Synchronises `stream` (the stream the steps ran on); clear != 0 resets the word.  A raised bit means the

@@ -1,0 +1,115 @@
+"""The vision stem's first block + conv2 with conv2's input gradient formed inside the first block's backward passes
+(fused_bn._Stem12, gr_stem12_backward), against (a) the unfused path of the same module (first block kernels, conv2
+as a patch GEMM, hipBLASLt dgrad) and (b) a float64 evaluation of the whole stem (reference
+vision_actor_critic.py:93-105 as written: nn.Conv2d / BatchNorm2d / LeakyReLU on NCHW images).
+
+The forward is the same kernels and GEMM either way, so features and BatchNorm statistics must be bit-identical
+to (a).  Gradients reduce over ~10^6 rows in another order: held to 1e-4 of each tensor's largest magnitude against
+(a) and against (b)."""
+from __future__ import annotations
+
+import copy
+import os
+import sys
+
+import pytest
+import torch
+import torch.nn as nn
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _model(img_res, act, seed):
+    from generalizableracing_amd.rsl_rl.vision_actor_critic import VisionActorCritic
+
+    torch.manual_seed(seed)
+    h, w = img_res
+    pol = VisionActorCritic(16 + h * w, 16 + h * w, 4, img_res=img_res, dim_hidden_input=64,
+                            actor_hidden_dims=[32], critic_hidden_dims=[32], activation=act)
+    g = torch.Generator().manual_seed(seed + 1)
+    with torch.no_grad():
+        for m in pol.modules():
+            if isinstance(m, nn.BatchNorm2d):
+                m.weight.copy_(1.0 + 0.3 * torch.randn(m.num_features, generator=g))
+                m.bias.copy_(0.2 * torch.randn(m.num_features, generator=g))
+    return pol.to(DEV).train()
+
+
+def _grads(pol, obs, gfeat, fused):
+    pol = copy.deepcopy(pol)
+    pol.fused_conv2 = fused
+    pol.zero_grad(set_to_none=True)
+    f = pol.features(obs)
+    (f * gfeat).sum().backward()
+    g = {k: p.grad.detach().clone() for k, p in pol.named_parameters() if k.startswith("stem.") and p.grad is not None}
+    bufs = {k: v.detach().clone() for k, v in pol.state_dict().items() if ".running_" in k or "num_batches" in k}
+    return f.detach(), g, bufs
+
+
+def _reference64(pol, obs, gfeat):
+    """The reference's stem as written (NCHW convs, float64), its feature sum and activation."""
+    p64 = copy.deepcopy(pol).double().cpu()
+    p64.zero_grad(set_to_none=True)
+    o = obs.double().cpu()
+    img = o[:, -p64.num_pixels:].reshape(-1, 1, *p64.img_res)
+    f = p64.activation(p64.stem(img) + p64.state_enc(o[:, :-p64.num_pixels]))
+    (f * gfeat.double().cpu()).sum().backward()
+    return {k: p.grad for k, p in p64.named_parameters() if k.startswith("stem.") and p.grad is not None}
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("img_res,nimg,act", [((72, 96), 512, "lrelu"), ((36, 48), 300, "lrelu"),
+                                              ((72, 96), 97, "elu")])
+def test_stem12_backward_matches_unfused_and_float64(img_res, nimg, act):
+    pol = _model(img_res, act, seed=3)
+    h, w = img_res
+    g = torch.Generator(device=DEV).manual_seed(11)
+    obs = torch.rand(nimg, 16 + h * w, device=DEV, generator=g) * 8.0 + 0.5
+    gfeat = torch.randn(nimg, 64, device=DEV, generator=g)
+    pol_n1, pol_n2 = pol._patch_index(DEV)[2], pol._patch_index(DEV)[5]
+    assert pol_n1 == 9 * pol_n2
+    f_f, g_f, b_f = _grads(pol, obs, gfeat, fused=True)
+    f_u, g_u, b_u = _grads(pol, obs, gfeat, fused=False)
+    assert torch.equal(f_f, f_u)  # same forward kernels and GEMM
+    for k in b_u:
+        assert torch.equal(b_f[k], b_u[k]), k
+    assert set(g_f) == set(g_u)
+    g64 = _reference64(pol, obs, gfeat)
+    for k in g_u:
+        assert _rel(g_f[k], g_u[k]) <= 1e-4, (k, _rel(g_f[k], g_u[k]))
+        assert _rel(g_f[k], g64[k]) <= 1e-4, (k, "vs float64", _rel(g_f[k], g64[k]))
+
+
+def test_stem12_repeats_bit_identical():
+    pol = _model((72, 96), "lrelu", seed=5)
+    g = torch.Generator(device=DEV).manual_seed(2)
+    obs = torch.rand(256, 16 + 72 * 96, device=DEV, generator=g) * 8.0
+    gfeat = torch.randn(256, 64, device=DEV, generator=g)
+    _, g1, _ = _grads(pol, obs, gfeat, fused=True)
+    _, g2, _ = _grads(pol, obs, gfeat, fused=True)
+    for k in g1:
+        assert torch.equal(g1[k], g2[k]), k
+
+
+def test_stem12_is_the_path_taken():
+    """The fused Function is what a training-mode forward of the registered stem records."""
+    pol = _model((72, 96), "lrelu", seed=7)
+    obs = torch.rand(32, 16 + 72 * 96, device=DEV)
+    f = pol.features(obs)
+    names = set()
+    stack = [f.grad_fn]
+    while stack:
+        n = stack.pop()
+        if n is None or n in names:
+            continue
+        names.add(n)
+        stack.extend(x[0] for x in n.next_functions)
+    assert any("_Stem12" in type(n).__name__ for n in names)
