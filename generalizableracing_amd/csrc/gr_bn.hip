@@ -91,33 +91,36 @@ __global__ __launch_bounds__(BN_THREADS) void bn_stats_partial(const float* __re
 // sums over the blocks' partials of `npairs` quantities (part[block][npairs]), in a fixed order: thread
 // (pair j, lane k) of the BN_FINAL_THREADS sums the partials b = k (mod T), T = BN_FINAL_THREADS / npairs
 // threads per pair, 32 (then 8) loads in flight at a time (the partials come from L2 / HBM: one load at a time left
-// a 1 024-block reduction latency-bound at ~70 us), then lane 0 of each pair adds the T lane sums in order
+// a 1 024-block reduction latency-bound at ~70 us), then lane 0 of each pair adds the T lane sums in order.
+// Thread index = k * npairs + j: consecutive threads read consecutive pairs of one partial row (coalesced; with
+// j = t / T a wave's load touched 16 rows, and the final took ~30 us for 1 024 rows of 32 pairs)
 constexpr int BN_FINAL_THREADS = 1024;
-__device__ void bn_final_sums(const double* __restrict__ part, int npairs, int blocks, double* out) {
+__device__ void bn_final_sums(const double* __restrict__ part, int npairs, int blocks, double* out, int stride = 0) {
   __shared__ double red[BN_FINAL_THREADS];
-  const int T = BN_FINAL_THREADS / npairs, j = threadIdx.x / T, k = threadIdx.x % T;
+  if (stride == 0) stride = npairs;  // (the partial rows' length, when the pairs are a slice of a longer row)
+  const int T = BN_FINAL_THREADS / npairs, j = threadIdx.x % npairs, k = threadIdx.x / npairs;
   double acc = 0.0;
-  if (j < npairs) {
+  if (k < T) {
     int b = k;
     // 32 loads in flight: the partials were just written by blocks on every XCD, so each round trip is a
     // far-memory latency (8 at a time left the final at ~29 us for 1 024 partial rows, profiles/round05_*)
     for (; b + 31 * T < blocks; b += 32 * T) {
       double v[32];
 #pragma unroll
-      for (int u = 0; u < 32; ++u) v[u] = part[(size_t)(b + u * T) * npairs + j];
+      for (int u = 0; u < 32; ++u) v[u] = part[(size_t)(b + u * T) * stride + j];
 #pragma unroll
       for (int u = 0; u < 32; ++u) acc += v[u];
     }
     for (; b + 7 * T < blocks; b += 8 * T) {
       double v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(b + u * T) * npairs + j];
+      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(b + u * T) * stride + j];
 #pragma unroll
       for (int u = 0; u < 8; ++u) acc += v[u];
     }
-    for (; b < blocks; b += T) acc += part[(size_t)b * npairs + j];
+    for (; b < blocks; b += T) acc += part[(size_t)b * stride + j];
+    red[j * T + k] = acc;
   }
-  red[threadIdx.x] = acc;
   __syncthreads();
   if (j < npairs && k == 0) {
     double s = 0.0;
@@ -754,21 +757,24 @@ __global__ __launch_bounds__(SM_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, i
 //   gy1 tile = gz2[16 patches][32] x W2[32][j, 16 channels]: eight v_mfma_f32_16x16x4f32, k step s of lane group g
 //   taking o = 8 g + s (A: the lane's patch row of gz2, two float4; B: W2 re-laid as w2t[j][g][c][s], two float4),
 // and the output fragment (patch 4 (l/16) + v, channel l % 16) is exactly the conv1 fragment of the same 16 cells
-// (cells 9 (16 chunk + i) + j as the tile's rows).  Table b's cells (not under conv2) have gy1 = 0: they add nothing
-// to the reduce pass and are still walked by the weight-gradient pass (their gx is not 0).
+// (cells 9 (16 chunk + i) + j as the tile's rows).  Table b's cells (not under conv2) have gy1 = 0.
+// One pass instead of two: the conv weight's gradient sum_r gx[r][ch] px[r][k], gx = (gz - mg - xhat mgx) isw with
+// mg, mgx the batch means of gz and gz xhat, is isw (A1 - mg A2 - mgx A3) with A1 = sum gz px, A2 = sum px,
+// A3 = sum xhat px, none of which needs mg or mgx: the pass accumulates them with the BN sums (12 MFMAs per tile on
+// the pixels read back from LDS, as the weight-gradient pass did for gx) and stem12_final combines them in fp64.
 struct Sm12Args {
   const float* bw;
   const float* bb;
   const float* stats;
-  const float* sums;  // SM_WGRAD
   const float* gz2;   // [nimg * n2][32]
   const float* w2t;   // [9][4][16][8]: W2[o = 8 g + s][j * 16 + c] at ((j * 4 + g) * 16 + c) * 8 + s
-  double* part;
+  double* part;       // [grid][32] BN sums (as SM_BWDP)
+  double* wpart;      // [grid][3][144] A1, A2, A3 (channel 4 (l / 16) + c, tap l % 16 layout as SM_WGRAD's)
   float slope;
   int n2;             // conv2 patches per image (na = 9 n2)
 };
 
-template <int PASS, int ACT, bool V4>
+template <int ACT, bool V4>
 __global__ __launch_bounds__(SM_THREADS) void stem12b_kernel(Stem1 s, Sm12Args q, int cap) {
   extern __shared__ float4 sm_dyn4[];
   __shared__ int s_span;
@@ -797,18 +803,11 @@ __global__ __launch_bounds__(SM_THREADS) void stem12b_kernel(Stem1 s, Sm12Args q
 #pragma unroll
   for (int c = 0; c < 3; ++c) wb[c] = kq + 4 * c < 9 ? s.w[ch * 9 + kq + 4 * c] : 0.0f;
   const float mu = q.stats[ch], is = q.stats[16 + ch], wv = q.bw[ch], bv = q.bb[ch];
-  const unsigned m = (unsigned)s.nimg * (unsigned)ncell;
-  float mg = 0.0f, mgx = 0.0f;
-  if constexpr (PASS == SM_WGRAD) {
-    const float inv_m = 1.0f / (float)m;
-    mg = q.sums[ch] * inv_m;
-    mgx = q.sums[16 + ch] * inv_m;
-    if (!loader) pimg[w][l & 15][12 + kq] = 0.0f;
-  }
-  const float isw = is * wv;
-  double a0 = 0.0, a1 = 0.0, g4[4] = {0.0, 0.0, 0.0, 0.0};
+  if (!loader) pimg[w][l & 15][12 + kq] = 0.0f;  // k = 12 .. 15: zero B operands
+  // A2 (the pixel sums, the same for every channel) on the VALU: this lane's row, taps kq, kq + 4, kq + 8
+  double a0 = 0.0, a1 = 0.0, g1[4] = {0.0, 0.0, 0.0, 0.0}, g3[4] = {0.0, 0.0, 0.0, 0.0}, p2[3] = {0.0, 0.0, 0.0};
   const int nch = (n2 + 15) / 16, ta = 9 * nch;
-  const int T = ta + (PASS == SM_WGRAD ? (nbt + 15) / 16 : 0);
+  const int T = ta + (nbt + 15) / 16;
   constexpr int U = 3;
 
   const int nmine = s.nimg > (int)blockIdx.x ? (s.nimg - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
@@ -889,29 +888,33 @@ __global__ __launch_bounds__(SM_THREADS) void stem12b_kernel(Stem1 s, Sm12Args q
             xh[v] = (x[v] - mu) * is;
             gz[v] = (live ? gyt[v] : 0.0f) * bn_dact<ACT>(xh[v] * wv + bv, q.slope);
           }
-          if constexpr (PASS == SM_BWDP) {
-            float s0 = 0.0f, s1 = 0.0f;
+          float s0 = 0.0f, s1 = 0.0f;
 #pragma unroll
-            for (int v = 0; v < 4; ++v) {
-              s0 += gz[v];
-              s1 += gz[v] * xh[v];
-            }
-            a0 += (double)s0;
-            a1 += (double)s1;
-          } else {
+          for (int v = 0; v < 4; ++v) {
+            const bool row = (int)(4 * kq + v) < nvalid[u];  // (xhat of a row past the tile's end: its pixels are 0)
+            s0 += gz[v];
+            s1 += row ? gz[v] * xh[v] : 0.0f;
+          }
+          a0 += (double)s0;
+          a1 += (double)s1;
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-              const bool okc = (int)(l & 15) < nvalid[u] && (c < 2 || kq == 0);
-              pimg[w][l & 15][kq + 4 * c] = okc ? px[u][c] : 0.0f;
-            }
-            sm4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+          for (int c = 0; c < 3; ++c) {
+            const bool okc = (int)(l & 15) < nvalid[u] && (c < 2 || kq == 0);
+            const float pc = okc ? px[u][c] : 0.0f;
+            pimg[w][l & 15][kq + 4 * c] = pc;
+            p2[c] += (double)pc;
+          }
+          sm4 c1 = {0.0f, 0.0f, 0.0f, 0.0f}, c3 = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-            for (int v = 0; v < 4; ++v) {
-              const float gx = (gz[v] - mg - xh[v] * mgx) * isw;
-              acc = sm_mfma(gx, pimg[w][4 * kq + v][ch], acc);
-            }
+          for (int v = 0; v < 4; ++v) {
+            const float pv = pimg[w][4 * kq + v][ch];
+            c1 = sm_mfma(gz[v], pv, c1);
+            c3 = sm_mfma(xh[v], pv, c3);
+          }
 #pragma unroll
-            for (int c = 0; c < 4; ++c) g4[c] += (double)acc[c];
+          for (int c = 0; c < 4; ++c) {
+            g1[c] += (double)c1[c];
+            g3[c] += (double)c3[c];
           }
         }
       }
@@ -924,36 +927,67 @@ __global__ __launch_bounds__(SM_THREADS) void stem12b_kernel(Stem1 s, Sm12Args q
     __syncthreads();
   }
 
+  // fixed-order block reductions through the (now free) image buffers (>= 2 x 1 024 floats: 4 x 256 doubles a round)
   double* red = reinterpret_cast<double*>(im0);
-  if constexpr (PASS == SM_BWDP) {
-    if (!loader) {
-      red[threadIdx.x] = a0;
-      red[BN_THREADS + threadIdx.x] = a1;
-    }
+  if (!loader) {
+    red[threadIdx.x] = a0;
+    red[BN_THREADS + threadIdx.x] = a1;
+  }
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    const int qq = threadIdx.x >> 4, c = threadIdx.x & 15;
+    double acc = 0.0;
+    for (int ww = 0; ww < BN_THREADS / 64; ++ww)
+      for (int k = 0; k < 4; ++k) acc += red[qq * BN_THREADS + ww * 64 + k * 16 + c];
+    q.part[(size_t)blockIdx.x * 32 + threadIdx.x] = acc;
+  }
+#pragma unroll
+  for (int a = 0; a < 3; a += 2) {
     __syncthreads();
-    if (threadIdx.x < 32) {
-      const int qq = threadIdx.x >> 4, c = threadIdx.x & 15;
-      double acc = 0.0;
-      for (int ww = 0; ww < BN_THREADS / 64; ++ww)
-        for (int k = 0; k < 4; ++k) acc += red[qq * BN_THREADS + ww * 64 + k * 16 + c];
-      q.part[(size_t)blockIdx.x * 32 + threadIdx.x] = acc;
-    }
-  } else {
     if (!loader) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) red[c * BN_THREADS + threadIdx.x] = g4[c];
+      for (int c = 0; c < 4; ++c) red[c * BN_THREADS + threadIdx.x] = a == 0 ? g1[c] : g3[c];
     }
     __syncthreads();
     for (int v = threadIdx.x; v < 16 * 9; v += BN_THREADS) {
       const int c2 = v / 9, k = v % 9, lane = (c2 >> 2) * 16 + k, c = c2 & 3;
       double t = 0.0;
       for (int ww = 0; ww < BN_THREADS / 64; ++ww) t += red[c * BN_THREADS + ww * 64 + lane];
-      q.part[(size_t)blockIdx.x * 144 + v] = t;
+      q.wpart[((size_t)blockIdx.x * 3 + a) * 144 + v] = t;
     }
+  }
+  // A2[k]: the lanes holding tap k (lane group k % 4, register k / 4) summed over rows and waves in a fixed order,
+  // stored for every channel
+  __syncthreads();
+  if (!loader) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) red[c * BN_THREADS + threadIdx.x] = p2[c];
+  }
+  __syncthreads();
+  for (int v = threadIdx.x; v < 16 * 9; v += BN_THREADS) {
+    const int k = v % 9, c = k >> 2, g = k & 3;
+    double t = 0.0;
+    for (int ww = 0; ww < BN_THREADS / 64; ++ww)
+      for (int i = 0; i < 16; ++i) t += red[c * BN_THREADS + ww * 64 + g * 16 + i];
+    q.wpart[((size_t)blockIdx.x * 3 + 1) * 144 + v] = t;
   }
 }
 
-template <int PASS>
+// gconv[ch][k] = isw (A1 - mg A2 - mgx A3), the A sums over the blocks in a fixed order, mg / mgx from the BN sums
+__global__ __launch_bounds__(BN_FINAL_THREADS) void stem12_final(int blocks, const double* __restrict__ wpart,
+                                                                const float* __restrict__ sums, const float* __restrict__ stats,
+                                                                const float* __restrict__ bw, double m, float* __restrict__ gw) {
+  __shared__ double tot[3 * 144];
+  // the three sums one after the other (7 threads per column instead of 2 for all 432 at once)
+  for (int a = 0; a < 3; ++a) bn_final_sums(wpart + a * 144, 144, blocks, tot + a * 144, 3 * 144);
+  for (int v = threadIdx.x; v < 144; v += BN_FINAL_THREADS) {
+    const int ch = v / 9;
+    const double mg = (double)sums[ch] / m, mgx = (double)sums[16 + ch] / m;
+    const double isw = (double)stats[16 + ch] * (double)bw[ch];
+    gw[v] = (float)(isw * (tot[v] - mg * tot[144 + v] - mgx * tot[288 + v]));
+  }
+}
+
 static void sm12_launch(const Stem1& s, const Sm12Args& q, int act, int grid, hipStream_t st) {
   long long room = s.ld - s.off;
   const int cap = (int)(room < 1 ? 1 : room < SM_IMG_CAP ? room : SM_IMG_CAP);
@@ -961,14 +995,14 @@ static void sm12_launch(const Stem1& s, const Sm12Args& q, int act, int grid, hi
   const bool v4 = ((uintptr_t)(s.obs + s.off) & 15) == 0 && (s.ld & 3) == 0;
   if (act == GR_POLICY_ACT_ELU) {
     if (v4)
-      hipLaunchKernelGGL((stem12b_kernel<PASS, GR_POLICY_ACT_ELU, true>), dim3(grid), dim3(SM_THREADS), lds, st, s, q, cap);
+      hipLaunchKernelGGL((stem12b_kernel<GR_POLICY_ACT_ELU, true>), dim3(grid), dim3(SM_THREADS), lds, st, s, q, cap);
     else
-      hipLaunchKernelGGL((stem12b_kernel<PASS, GR_POLICY_ACT_ELU, false>), dim3(grid), dim3(SM_THREADS), lds, st, s, q, cap);
+      hipLaunchKernelGGL((stem12b_kernel<GR_POLICY_ACT_ELU, false>), dim3(grid), dim3(SM_THREADS), lds, st, s, q, cap);
   } else {
     if (v4)
-      hipLaunchKernelGGL((stem12b_kernel<PASS, GR_POLICY_ACT_LRELU, true>), dim3(grid), dim3(SM_THREADS), lds, st, s, q, cap);
+      hipLaunchKernelGGL((stem12b_kernel<GR_POLICY_ACT_LRELU, true>), dim3(grid), dim3(SM_THREADS), lds, st, s, q, cap);
     else
-      hipLaunchKernelGGL((stem12b_kernel<PASS, GR_POLICY_ACT_LRELU, false>), dim3(grid), dim3(SM_THREADS), lds, st, s, q, cap);
+      hipLaunchKernelGGL((stem12b_kernel<GR_POLICY_ACT_LRELU, false>), dim3(grid), dim3(SM_THREADS), lds, st, s, q, cap);
   }
 }
 
@@ -993,10 +1027,11 @@ static void sm_launch(const Stem1& s, const SmArgs& q, int act, int grid, hipStr
 
 static int stem_blocks(const Stem1& s) { return bn_blocks((long long)s.nimg * (s.na + s.nbt), s.c); }
 
-// workspace (doubles): BN partials [nb][2c] | shift + sums (2c floats, as c doubles) | wgrad partials [nb][9c]
+// workspace (doubles): BN partials [nb][2c] | shift + sums (2c floats, as c doubles) | wgrad partials [nb][3][9c]
+// (three sums per block for the fused conv2 backward, one for the first block's own)
 long long stem1_scratch_doubles(int nimg, int rows_per_img, int c) {
   const long long nb = bn_blocks((long long)nimg * rows_per_img, c);
-  return nb * 2 * c + 2 * c + nb * 9 * c;
+  return nb * 2 * c + 2 * c + nb * 27 * c;
 }
 
 hipError_t launch_stem1_forward(const Stem1& s, const float* bw, const float* bb, float eps, int act, float slope,
@@ -1057,12 +1092,11 @@ hipError_t launch_stem12_backward(const Stem1& s, const float* bw, const float* 
   float* sums = reinterpret_cast<float*>(part + (size_t)nb * 2 * s.c);
   double* wpart = part + (size_t)nb * 2 * s.c + 2 * s.c;
   const int grid = nb < SM_GRID ? nb : SM_GRID;
-  Sm12Args q{bw, bb, stats, sums, gz2, w2t, part, slope, n2};
-  sm12_launch<SM_BWDP>(s, q, act, grid, st);
+  Sm12Args q{bw, bb, stats, gz2, w2t, part, wpart, slope, n2};
+  sm12_launch(s, q, act, grid, st);
   hipLaunchKernelGGL(bn_bwd_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, s.c, grid, part, gbw, gbb, sums);
-  q.part = wpart;
-  sm12_launch<SM_WGRAD>(s, q, act, grid, st);
-  hipLaunchKernelGGL(stem1_wgrad_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, 9 * s.c, grid, wpart, gconv);
+  hipLaunchKernelGGL(stem12_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, grid, wpart, sums, stats, bw,
+                     (double)s.nimg * (double)(s.na + s.nbt), gconv);
   return hipGetLastError();
 }
 
