@@ -14,11 +14,15 @@
 
 #include "../../include/gr.h"
 #include "gr_kernels.h"
+#include "gr_normal_table.h"
 #include "gr_math.h"
 #include "gr_obstacles.h"
 #include "gr_rng.h"
 
 namespace gr {
+
+// the observation noise's inverse-CDF normals (gr_rng.h gr_normal21; gr_normal_table.h)
+__constant__ __attribute__((aligned(16))) float obs_normal_tab[4 * GR_NORMAL_TABLE_ENTRIES] = GR_NORMAL_TABLE_INIT;
 
 #define DEV __device__ __forceinline__
 
@@ -727,9 +731,7 @@ DEV void obs_noise(const KArgs& a, uint32_t gid, uint32_t cnt, ObsNoise& on) {
   {  // drawn unconditionally (one basic block for the scheduler), zeroed without obs noise
     uint32_t f[6];
     gr_fields6(draw(a, gid, cnt, GR_TAG_OBS, 0), f);
-    gr_box_muller21(f[0], f[1], &nz[0], &nz[1]);
-    gr_box_muller21(f[2], f[3], &nz[2], &nz[3]);
-    gr_box_muller21(f[4], f[5], &nz[4], &nz[5]);
+    for (int k = 0; k < 6; ++k) nz[k] = gr_normal21(f[k], obs_normal_tab);
     for (int k = 0; k < 6; ++k) nz[k] = a.h.obs_noise ? nz[k] : 0.0f;
   }
   for (int k = 0; k < 3; ++k) on.vfac[k] = 1.0f + nz[k] * a.h.obs_lin_vel_noise;

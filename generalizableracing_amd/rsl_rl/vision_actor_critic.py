@@ -43,14 +43,16 @@ class _PatchGemm(torch.autograd.Function):
     SPLIT = 8192
 
     @staticmethod
-    def forward(ctx, x, w):
+    def forward(ctx, x, w, b=None):
         ctx.save_for_backward(x, w)
-        return x @ w.t()
+        ctx.has_bias = b is not None
+        return x @ w.t() if b is None else torch.addmm(b, x, w.t())  # (the bias in the GEMM's epilogue)
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
         gx = gy @ w if ctx.needs_input_grad[0] else None
+        gb = gy.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
         gw = None
         if ctx.needs_input_grad[1]:
             m, c = x.shape[0], _PatchGemm.SPLIT
@@ -61,11 +63,14 @@ class _PatchGemm(torch.autograd.Function):
                     gw = gw + gy[s * c:].t() @ x[s * c:]
             else:
                 gw = gy.t() @ x
-        return gx, gw
+        return gx, gw, gb
 
 
-def _gemm(x, w):
-    return _PatchGemm.apply(x, w) if torch.is_grad_enabled() else x @ w.t()
+def _gemm(x, w, b=None):
+    """x @ w^T (+ b): the split-K weight gradient with autograd on, else one GEMM (bias in its epilogue)."""
+    if torch.is_grad_enabled():
+        return _PatchGemm.apply(x, w, b)
+    return x @ w.t() if b is None else torch.addmm(b, x, w.t())
 
 
 class VisionActorCritic(ActorCritic):
@@ -186,8 +191,9 @@ class VisionActorCritic(ActorCritic):
         self._pidx = (a, b, len(l1), len(l1_left), len(g3), len(g2), pix16)
         return self._pidx
 
-    def stem_gemm(self, img: torch.Tensor) -> torch.Tensor:
-        """The conv stem as patch GEMMs (identical math to self.stem(img), other summation order)."""
+    def stem_gemm(self, img: torch.Tensor, extra_bias: torch.Tensor | None = None) -> torch.Tensor:
+        """The conv stem as patch GEMMs (identical math to self.stem(img), other summation order); extra_bias is added
+        to the final Linear's bias (features() passes the state encoder's)."""
         conv1, bn1, act, conv2, bn2, _, conv3, bn3, _, _, lin = self.stem
         h1, w1, h2, w2, h3, w3 = self._dims
         B = img.shape[0]
@@ -221,13 +227,15 @@ class VisionActorCritic(ActorCritic):
         y = self._bn_act(bn3, act, _gemm(x, conv3.weight.permute(0, 2, 3, 1).reshape(64, 128))).view(B, h3 * w3 * 64)
         # reference flatten is NCHW (c, h, w): permute the Linear's columns to (h, w, c) instead
         wl = lin.weight.view(-1, 64, h3, w3).permute(0, 2, 3, 1).reshape(lin.weight.shape[0], -1)
-        return _gemm(y, wl) + lin.bias
+        return _gemm(y, wl, lin.bias if extra_bias is None else lin.bias + extra_bias)
 
     def features(self, observations: torch.Tensor) -> torch.Tensor:
         """act(stem(image) + state_enc(state)), vision_actor_critic.py:119-122."""
         img = observations[:, -self.num_pixels:].reshape(-1, 1, *self.img_res)
         state = observations[:, :-self.num_pixels]
-        return self.activation(self.stem_gemm(img) + self.state_enc(state))
+        # the state encoder's GEMM takes the stem's output (with both biases) as its addend: no [B, 192] adds
+        se = self.state_enc
+        return self.activation(torch.addmm(self.stem_gemm(img, se.bias), state, se.weight.t()))
 
     def shared_features(self, observations: torch.Tensor, uses: int) -> torch.Tensor:
         """features(observations) evaluated once for `uses` consumers of the same rows (PPOL2C2's mixed batch feeds

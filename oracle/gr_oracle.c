@@ -521,9 +521,7 @@ static void compute_obs(const gr_config* c, gro_env* e, uint32_t gid, uint32_t c
   if (c->obs_noise) { /* randn(N,3) for the velocity and for the attitude noise */
     uint32_t f[6];
     gr_fields6(draw(c, gid, cnt, GR_TAG_OBS, 0), f);
-    gr_box_muller21(f[0], f[1], &nz[0], &nz[1]);
-    gr_box_muller21(f[2], f[3], &nz[2], &nz[3]);
-    gr_box_muller21(f[4], f[5], &nz[4], &nz[5]);
+    for (int k = 0; k < 6; ++k) nz[k] = gr_normal21(f[k], GRO_NORMAL_TAB);
   }
   float qn[4], qq[4], r2n[3];
   quat_from_euler_xyz(nz[3] * c->obs_att_noise, nz[4] * c->obs_att_noise, nz[5] * c->obs_att_noise, qn);
@@ -834,7 +832,7 @@ void gro_draws(const gr_config* c, int i, int kind, uint32_t c1, uint32_t c3, fl
   uint32_t f[24];
   if (kind == 0) {
     gr_fields6(draw(c, gid, c1, GR_TAG_OBS, 0), f);
-    for (int k = 0; k < 3; ++k) gr_box_muller21(f[2 * k], f[2 * k + 1], &out[2 * k], &out[2 * k + 1]);
+    for (int k = 0; k < 6; ++k) out[k] = gr_normal21(f[k], GRO_NORMAL_TAB);
   } else if (kind == 1) {
     gr_fields6(draw(c, gid, c1, GR_TAG_GATE, c3), f);
     for (int k = 0; k < 6; ++k) out[k] = gr_f21(f[k]);
