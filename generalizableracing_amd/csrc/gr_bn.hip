@@ -762,6 +762,8 @@ __global__ __launch_bounds__(SM_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, i
 // mg, mgx the batch means of gz and gz xhat, is isw (A1 - mg A2 - mgx A3) with A1 = sum gz px, A2 = sum px,
 // A3 = sum xhat px, none of which needs mg or mgx: the pass accumulates them with the BN sums (12 MFMAs per tile on
 // the pixels read back from LDS, as the weight-gradient pass did for gx) and stem12_final combines them in fp64.
+// Per-lane sums are fp32 over one image's tiles, fp64 across images and in the block / final reductions (fp64 per
+// tile, as the first block's own passes do, took ~50 fp64 conversions and adds per tile).
 struct Sm12Args {
   const float* bw;
   const float* bb;
@@ -820,6 +822,9 @@ __global__ __launch_bounds__(SM_THREADS) void stem12b_kernel(Stem1 s, Sm12Args q
     if (loader) {
       if (staged && k + 1 < nmine) sm_dma_image(g + (long long)gridDim.x * s.ld, (k & 1) ? im0 : im1, span, v4);
     } else {
+      // fp32 sums over this image's tiles (<= 15 per wave), folded into the fp64 accumulators once per image
+      float f0 = 0.0f, f1 = 0.0f, fp2[3] = {0.0f, 0.0f, 0.0f};
+      sm4 fg1 = {0.0f, 0.0f, 0.0f, 0.0f}, fg3 = {0.0f, 0.0f, 0.0f, 0.0f};
       auto tiles = [&](auto from_lds) {
       for (int j0 = (int)w; j0 < T; j0 += SM_WAVES * U) {
         int nvalid[U];
@@ -895,14 +900,14 @@ __global__ __launch_bounds__(SM_THREADS) void stem12b_kernel(Stem1 s, Sm12Args q
             s0 += gz[v];
             s1 += row ? gz[v] * xh[v] : 0.0f;
           }
-          a0 += (double)s0;
-          a1 += (double)s1;
+          f0 += s0;
+          f1 += s1;
 #pragma unroll
           for (int c = 0; c < 3; ++c) {
             const bool okc = (int)(l & 15) < nvalid[u] && (c < 2 || kq == 0);
             const float pc = okc ? px[u][c] : 0.0f;
             pimg[w][l & 15][kq + 4 * c] = pc;
-            p2[c] += (double)pc;
+            fp2[c] += pc;
           }
           sm4 c1 = {0.0f, 0.0f, 0.0f, 0.0f}, c3 = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -911,11 +916,8 @@ __global__ __launch_bounds__(SM_THREADS) void stem12b_kernel(Stem1 s, Sm12Args q
             c1 = sm_mfma(gz[v], pv, c1);
             c3 = sm_mfma(xh[v], pv, c3);
           }
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            g1[c] += (double)c1[c];
-            g3[c] += (double)c3[c];
-          }
+          fg1 += c1;
+          fg3 += c3;
         }
       }
       };
@@ -923,6 +925,15 @@ __global__ __launch_bounds__(SM_THREADS) void stem12b_kernel(Stem1 s, Sm12Args q
         tiles(std::true_type{});
       else
         tiles(std::false_type{});
+      a0 += (double)f0;
+      a1 += (double)f1;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) p2[c] += (double)fp2[c];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        g1[c] += (double)fg1[c];
+        g3[c] += (double)fg3[c];
+      }
     }
     __syncthreads();
   }
