@@ -129,3 +129,22 @@ def test_mlp_rejects_rows_past_32_bit_offsets():
     a.rows, a.hidden = 2 ** 31 // 128 - 1, 128
     a.net[0].ldx = 160  # the strided input dominates: rows * ldx >= 2^31
     assert lib.gr_mlp_forward(C.byref(a), None) == -1
+
+
+def test_stem12_rejects_shapes_it_does_not_cover():
+    """gr_stem12_backward (the first block's backward with conv2's input gradient inside) covers 16 channels and table-a
+    rows grouped as conv2's patches (na = 9 n2) with 16-byte aligned gz2 / w2t: anything else is an argument error,
+    checked before any launch (no device needed)."""
+    lib = _abi.load()
+    p = 0x10000  # aligned dummy device pointers: the checks return before any launch
+
+    def call(c=16, na=720, nb=48, n2=80, gz2=p, w2t=p, act=_abi.GR_POLICY_ACT_LRELU):
+        return lib.gr_stem12_backward(p, 6928, 16, 8, p, na, nb, p, c, p, p, p, act, 0.01, gz2, n2, w2t, p, p, p, p,
+                                      None)
+
+    assert call(c=8) == -1
+    assert call(na=721) == -1          # na != 9 n2
+    assert call(n2=0, na=0) == -1
+    assert call(gz2=p + 4) == -1       # gz2 not 16-byte aligned
+    assert call(w2t=None) == -1
+    assert call(act=7) == -1
