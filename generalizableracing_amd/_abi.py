@@ -239,7 +239,7 @@ EXPORTS = [
     "gr_bn_scratch_doubles", "gr_bn_act_forward", "gr_bn_act_backward", "gr_stem1_scratch_doubles",
     "gr_stem1_forward", "gr_stem1_backward", "gr_mlp_partials", "gr_mlp_forward", "gr_mlp_backward",
     "gr_mlp_args_size", "gr_step_kernel_variant", "gr_terrain_reserve", "gr_terrain_stage", "gr_terrain_commit",
-    "gr_terrain_epoch", "gr_mlp_h1mask_words", "gr_stem12_backward",
+    "gr_terrain_epoch", "gr_mlp_h1mask_words", "gr_stem12_backward", "gr_stem12_forward",
 ]
 
 _lib = None
@@ -328,6 +328,8 @@ def _declare(lib):
                                        vp, vp, C.c_float, C.c_int32, C.c_float, vp, C.c_int64, vp, vp, vp]),
         "gr_stem1_backward": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int32, vp, C.c_int32, C.c_int32, vp, C.c_int32,
                                         vp, vp, vp, C.c_int32, C.c_float, vp, C.c_int64, vp, vp, vp, vp, vp]),
+        "gr_stem12_forward": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int32, vp, C.c_int32, C.c_int32, vp, C.c_int32,
+                                        vp, vp, C.c_float, C.c_int32, C.c_float, vp, C.c_int32, vp, vp, vp, vp, vp]),
         "gr_stem12_backward": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int32, vp, C.c_int32, C.c_int32, vp, C.c_int32,
                                          vp, vp, vp, C.c_int32, C.c_float, vp, C.c_int32, vp, vp, vp, vp, vp, vp]),
     }

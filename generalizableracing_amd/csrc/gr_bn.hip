@@ -1045,6 +1045,178 @@ long long stem1_scratch_doubles(int nimg, int rows_per_img, int c) {
   return nb * 2 * c + 2 * c + nb * 27 * c;
 }
 
+// ------------------------------------------------------------- the first block's apply pass fused with conv2
+// y1 = act(bn(conv1(image))) as SM_APPLY stores it, and conv2's output z2[p][o] = sum_{j, c} y1[9 p + j][c] W2[o][j, c]
+// from the same registers (conv2's patch GEMM read y1 back from HBM: 1.13 GB per 24 576-image mini-batch).  conv1 runs
+// transposed here, C[channel][cell] = W1 . pixels (A = the weights, B = the gathered pixels: the same k-ordered fmaf
+// chain, so y1 is bit-identical to SM_APPLY's), so a lane holds one cell (a patch of the tile) and four channels
+// 4 (l/16) + v: exactly conv2's A fragment with k step v of lane group g taking channel 4 g + v.  A wave owns whole
+// 16-patch chunks (its nine positions j accumulate in its registers, in j order: deterministic), so the workgroup
+// has SMF_WAVES = 5 compute waves (72 x 96: five chunks of 80 patches per image) and one loader wave.
+constexpr int SMF_WAVES = 5;
+constexpr int SMF_THREADS = 64 * (SMF_WAVES + 1);
+struct Sm12fArgs {
+  const float* bw;
+  const float* bb;
+  const float* stats;  // [4][16] (mean, invstd, ...)
+  const float* w2f;    // [9][4][32][4]: W2[o][j * 16 + 4 g + v] at ((j * 4 + g) * 32 + o) * 4 + v
+  float* y;            // [nimg * na][16]
+  float* z2;           // [nimg * n2][32]
+  float slope;
+  int n2;
+};
+
+template <int ACT, bool V4>
+__global__ __launch_bounds__(SMF_THREADS) void stem12f_kernel(Stem1 s, Sm12fArgs q, int cap) {
+  extern __shared__ float4 sm_dyn4[];
+  __shared__ int s_span;
+  const int na = s.na, nbt = s.nbt, ncell = na + nbt, n2 = q.n2;
+  short* tab = reinterpret_cast<short*>(sm_dyn4);
+  float* im0 = reinterpret_cast<float*>(sm_dyn4) + sm_tab_floats(ncell);
+  float* im1 = im0 + sm_img_floats(cap);
+  const unsigned l = threadIdx.x & 63, lo = l & 15, kq = l >> 4, w = sm_wave();
+  const bool loader = w == SMF_WAVES;
+  if (threadIdx.x == 0) s_span = 0;
+  __syncthreads();
+  int mx = 0;
+  for (int i = threadIdx.x; i < ncell * 9; i += SMF_THREADS) {
+    const short t = s.pix[i];
+    tab[i] = t;
+    mx = mx > (int)t + 1 ? mx : (int)t + 1;
+  }
+  atomicMax(&s_span, mx);
+  __syncthreads();
+  const int span = s_span;
+  const bool staged = span <= cap;
+  const bool v4 = V4 && (span & 3) == 0;
+
+  // conv1 as C[channel][cell]: A = W1[channel lo][k = kq + 4 c] (0 for k >= 9); the lane's output channels 4 kq + v
+  float wa[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) wa[c] = kq + 4 * c < 9 ? s.w[lo * 9 + kq + 4 * c] : 0.0f;
+  float mu[4], is[4], wv[4], bv[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int chn = 4 * (int)kq + v;
+    mu[v] = q.stats[chn];
+    is[v] = q.stats[16 + chn];
+    wv[v] = q.bw[chn];
+    bv[v] = q.bb[chn];
+  }
+  const unsigned rows = (unsigned)s.rows_out;
+  const int nch = (n2 + 15) / 16;
+
+  const int nmine = s.nimg > (int)blockIdx.x ? (s.nimg - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
+  if (staged && loader && nmine > 0) sm_dma_image(s.obs + (long long)blockIdx.x * s.ld + s.off, im0, span, v4);
+  __syncthreads();
+  for (int k = 0; k < nmine; ++k) {
+    const int b = (int)blockIdx.x + k * (int)gridDim.x;
+    const float* g = s.obs + (long long)b * s.ld + s.off;
+    const float* im = (k & 1) ? im1 : im0;
+    if (loader) {
+      if (staged && k + 1 < nmine) sm_dma_image(g + (long long)gridDim.x * s.ld, (k & 1) ? im0 : im1, span, v4);
+    } else {
+      auto chunks = [&](auto from_lds) {
+      for (int chunk = (int)w; chunk < nch; chunk += SMF_WAVES) {
+        const int nvalid = n2 - 16 * chunk < 16 ? n2 - 16 * chunk : 16;
+        const bool ok = (int)lo < nvalid;
+        const int p = 16 * chunk + (ok ? (int)lo : 0);
+        // the chunk's nine positions: table reads, then pixel gathers, all issued before any is consumed
+        int po[9][3];
+#pragma unroll
+        for (int jj = 0; jj < 9; ++jj) {
+          const short* tt = tab + (9 * p + jj) * 9;
+          po[jj][0] = tt[kq];
+          po[jj][1] = tt[kq + 4];
+          po[jj][2] = tt[8];
+        }
+        float px[9][3];
+#pragma unroll
+        for (int jj = 0; jj < 9; ++jj) {
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            if constexpr (decltype(from_lds)::value)
+              px[jj][c] = im[po[jj][c]];
+            else
+              px[jj][c] = g[po[jj][c]];
+          }
+        }
+        sm4 z0 = {0.0f, 0.0f, 0.0f, 0.0f}, z1 = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int jj = 0; jj < 9; ++jj) {
+          sm4 x = {0.0f, 0.0f, 0.0f, 0.0f};
+          x = sm_mfma(wa[0], px[jj][0], x);
+          x = sm_mfma(wa[1], px[jj][1], x);
+          x = sm_mfma(wa[2], px[jj][2], x);
+          float4 y4;
+          float yv[4];
+#pragma unroll
+          for (int v = 0; v < 4; ++v) yv[v] = bn_act<ACT>((x[v] - mu[v]) * is[v] * wv[v] + bv[v], q.slope);
+          y4.x = yv[0]; y4.y = yv[1]; y4.z = yv[2]; y4.w = yv[3];
+          const unsigned r = (unsigned)b * (unsigned)na + (unsigned)(9 * p + jj);
+          if (ok && r < rows) reinterpret_cast<float4*>(q.y + (size_t)r * 16)[kq] = y4;
+          // conv2: B fragment W2[o][jj, 4 kq + v] for o = lo (z0) and 16 + lo (z1)
+          const float4 b0 = reinterpret_cast<const float4*>(q.w2f)[(jj * 4 + (int)kq) * 32 + (int)lo];
+          const float4 b1 = reinterpret_cast<const float4*>(q.w2f)[(jj * 4 + (int)kq) * 32 + 16 + (int)lo];
+          z0 = sm_mfma(yv[0], b0.x, z0);
+          z0 = sm_mfma(yv[1], b0.y, z0);
+          z0 = sm_mfma(yv[2], b0.z, z0);
+          z0 = sm_mfma(yv[3], b0.w, z0);
+          z1 = sm_mfma(yv[0], b1.x, z1);
+          z1 = sm_mfma(yv[1], b1.y, z1);
+          z1 = sm_mfma(yv[2], b1.z, z1);
+          z1 = sm_mfma(yv[3], b1.w, z1);
+        }
+        // lane (o = lo, kq) holds z2[patch 16 chunk + 4 kq + v][o] (z0) and [16 + o] (z1)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int pp = 4 * (int)kq + v;
+          if (pp < nvalid) {
+            float* zr = q.z2 + ((size_t)b * n2 + 16 * chunk + pp) * 32;
+            zr[lo] = z0[v];
+            zr[16 + lo] = z1[v];
+          }
+        }
+      }
+      };
+      if (staged)
+        chunks(std::true_type{});
+      else
+        chunks(std::false_type{});
+    }
+    __syncthreads();
+  }
+}
+
+hipError_t launch_stem12_forward(const Stem1& s, const float* bw, const float* bb, float eps, int act, float slope,
+                                 const float* w2f, int n2, float* y, float* z2, float* stats, double* part,
+                                 hipStream_t st) {
+  const int nb = stem_blocks(s);
+  float* shift = reinterpret_cast<float*>(part + (size_t)nb * 2 * s.c);
+  const long long m = (long long)s.nimg * (s.na + s.nbt);
+  const int grid = nb < SM_GRID ? nb : SM_GRID;
+  SmArgs q{bw, bb, stats, nullptr, nullptr, y, part, shift, slope};
+  sm_launch<SM_STATS>(s, q, act, grid, st);
+  hipLaunchKernelGGL(bn_stats_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, shift, m, s.c, grid, eps, part, stats);
+  long long room = s.ld - s.off;
+  const int cap = (int)(room < 1 ? 1 : room < SM_IMG_CAP ? room : SM_IMG_CAP);
+  const size_t lds = sm_lds_bytes(s.na + s.nbt, cap);
+  const bool v4 = ((uintptr_t)(s.obs + s.off) & 15) == 0 && (s.ld & 3) == 0;
+  Sm12fArgs f{bw, bb, stats, w2f, y, z2, slope, n2};
+  if (act == GR_POLICY_ACT_ELU) {
+    if (v4)
+      hipLaunchKernelGGL((stem12f_kernel<GR_POLICY_ACT_ELU, true>), dim3(grid), dim3(SMF_THREADS), lds, st, s, f, cap);
+    else
+      hipLaunchKernelGGL((stem12f_kernel<GR_POLICY_ACT_ELU, false>), dim3(grid), dim3(SMF_THREADS), lds, st, s, f, cap);
+  } else {
+    if (v4)
+      hipLaunchKernelGGL((stem12f_kernel<GR_POLICY_ACT_LRELU, true>), dim3(grid), dim3(SMF_THREADS), lds, st, s, f, cap);
+    else
+      hipLaunchKernelGGL((stem12f_kernel<GR_POLICY_ACT_LRELU, false>), dim3(grid), dim3(SMF_THREADS), lds, st, s, f, cap);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_stem1_forward(const Stem1& s, const float* bw, const float* bb, float eps, int act, float slope,
                                 float* y, float* stats, double* part, hipStream_t st) {
   const int nb = stem_blocks(s);

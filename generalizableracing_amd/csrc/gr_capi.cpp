@@ -994,6 +994,21 @@ int gr_stem1_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, c
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
+int gr_stem12_forward(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
+                      int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b, float eps,
+                      int32_t act, float slope, const float* w2f, int32_t n2, float* y, float* z2, float* stats,
+                      double* part, void* stream) {
+  if (!stem1_args_ok(obs, nimg, pix, na, nb, conv_w, c, bn_w, bn_b) || c != 16 || !w2f || !y || !z2 || !stats ||
+      !part || !aligned16(w2f) || !aligned16(y) || !aligned16(z2) || !aligned16(stats) ||
+      (act != GR_POLICY_ACT_LRELU && act != GR_POLICY_ACT_ELU) || n2 < 1 || na != 9 * n2 ||
+      (int64_t)nimg * n2 * 32 >= (int64_t)1 << 31)
+    return GR_ERR_ARG;
+  const gr::Stem1 s = stem1_of(obs, ld, off, nimg, pix, na, nb, conv_w, c, (int64_t)nimg * na);
+  const hipError_t e = gr::launch_stem12_forward(s, bn_w, bn_b, eps, act, slope, w2f, n2, y, z2, stats, part,
+                                                 (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
 int gr_stem12_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
                        int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b,
                        const float* stats, int32_t act, float slope, const float* gz2, int32_t n2, const float* w2t,

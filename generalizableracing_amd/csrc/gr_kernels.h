@@ -116,6 +116,10 @@ hipError_t launch_stem1_forward(const Stem1& s, const float* bw, const float* bb
 hipError_t launch_stem1_backward(const Stem1& s, const float* bw, const float* bb, const float* stats, int act,
                                  float slope, const float* gy, float* gconv, float* gbw, float* gbb, double* part,
                                  hipStream_t st);
+// the first block's forward with conv2 (16 -> 32, 3x3 / 3) fused into its apply pass: y1 and z2 (gr_bn.hip stem12f_kernel)
+hipError_t launch_stem12_forward(const Stem1& s, const float* bw, const float* bb, float eps, int act, float slope,
+                                 const float* w2f, int n2, float* y, float* z2, float* stats, double* part,
+                                 hipStream_t st);
 // the same backward with conv2's input gradient formed inside the passes (C = 16, na = 9 n2; gr_bn.hip stem12b_kernel)
 hipError_t launch_stem12_backward(const Stem1& s, const float* bw, const float* bb, const float* stats, int act,
                                   float slope, const float* gz2, int n2, const float* w2t, float* gconv, float* gbw,

@@ -139,13 +139,14 @@ class _Stem1(torch.autograd.Function):
 
 
 class _Stem12(torch.autograd.Function):
-    """The first block (as _Stem1, C = 16) followed by conv2 as a patch GEMM: z2 = y1.view(-1, 144) @ w2^T, w2 [32, 144]
-    in (position j, channel) column order.  The forward is _Stem1's kernels plus the GEMM; the backward takes conv2's
-    output gradient straight into the first block's passes (gr_stem12_backward): conv2's input gradient, a
-    [rows, 144] matrix, is never written.  conv2's weight gradient is the split-K product of gz2 and y1 (saved)."""
+    """The first block (as _Stem1, C = 16) followed by conv2: z2 = y1.view(-1, 144) @ w2^T, w2 [32, 144] in (position j,
+    channel) column order.  The forward computes conv2 inside the first block's apply pass (gr_stem12_forward: y1 is
+    stored for conv2's weight gradient but not read back); the backward takes conv2's output gradient straight into
+    the first block's passes (gr_stem12_backward): conv2's input gradient, a [rows, 144] matrix, is never written.
+    conv2's weight gradient is the split-K product of gz2 and the saved y1."""
 
     @staticmethod
-    def forward(ctx, img, conv_w, bn_w, bn_b, w2, pix, na, nb, eps, act, slope):
+    def forward(ctx, img, conv_w, bn_w, bn_b, w2, pix, na, nb, eps, act, slope, fused_forward=True):
         lib = _abi.load()
         nimg = img.shape[0]
         rows = nimg * na
@@ -154,13 +155,22 @@ class _Stem12(torch.autograd.Function):
         part = torch.empty(int(lib.gr_stem1_scratch_doubles(nimg, na + nb, 16)), device=img.device, dtype=torch.float64)
         w = conv_w.detach().reshape(16, 9).contiguous()
         bw, bb = bn_w.detach().contiguous(), bn_b.detach().contiguous()
-        rc = lib.gr_stem1_forward(img.data_ptr(), img.stride(0), 0, nimg, pix.data_ptr(), na, nb, w.data_ptr(), 16,
-                                  bw.data_ptr(), bb.data_ptr(), float(eps), act, float(slope), y.data_ptr(), rows,
-                                  stats.data_ptr(), part.data_ptr(), _stream(img))
-        if rc != 0:
-            raise RuntimeError(f"gr_stem1_forward failed (status {rc})")
         w2d = w2.detach()
-        z2 = y.view(-1, 144) @ w2d.t()
+        if fused_forward:
+            # conv2 inside the first block's apply pass: w2f[j][g][o][v] = W2[o][j * 16 + 4 g + v]
+            w2f = w2d.reshape(32, 9, 4, 4).permute(1, 2, 0, 3).contiguous()
+            z2 = torch.empty(nimg * (na // 9), 32, device=img.device, dtype=torch.float32)
+            rc = lib.gr_stem12_forward(img.data_ptr(), img.stride(0), 0, nimg, pix.data_ptr(), na, nb, w.data_ptr(), 16,
+                                       bw.data_ptr(), bb.data_ptr(), float(eps), act, float(slope), w2f.data_ptr(),
+                                       na // 9, y.data_ptr(), z2.data_ptr(), stats.data_ptr(), part.data_ptr(),
+                                       _stream(img))
+        else:  # the first block's kernels, then conv2 as a GEMM (the A/B reference of the fused forward)
+            rc = lib.gr_stem1_forward(img.data_ptr(), img.stride(0), 0, nimg, pix.data_ptr(), na, nb, w.data_ptr(), 16,
+                                      bw.data_ptr(), bb.data_ptr(), float(eps), act, float(slope), y.data_ptr(), rows,
+                                      stats.data_ptr(), part.data_ptr(), _stream(img))
+            z2 = y.view(-1, 144) @ w2d.t() if rc == 0 else None
+        if rc != 0:
+            raise RuntimeError(f"gr_stem12_forward failed (status {rc})")
         ctx.save_for_backward(img, w, bw, bb, stats, y, w2d)
         ctx.pix = pix
         ctx.args = (na, nb, act, slope, conv_w.shape)
@@ -199,7 +209,7 @@ class _Stem12(torch.autograd.Function):
                                     part.data_ptr(), _stream(img))
         if rc != 0:
             raise RuntimeError(f"gr_stem12_backward failed (status {rc})")
-        return None, gconv.view(wshape), gbw, gbb, gw2, None, None, None, None, None, None
+        return None, gconv.view(wshape), gbw, gbb, gw2, None, None, None, None, None, None, None
 
 
 def stem12_applicable(bn: nn.BatchNorm2d, act: nn.Module, img: torch.Tensor, conv_w: torch.Tensor,
@@ -211,11 +221,11 @@ def stem12_applicable(bn: nn.BatchNorm2d, act: nn.Module, img: torch.Tensor, con
 
 
 def stem12_bn_act_conv(bn: nn.BatchNorm2d, act: nn.Module, conv_w: torch.Tensor, w2: torch.Tensor, img: torch.Tensor,
-                       pix: torch.Tensor, na: int, nb: int, uses: int = 1) -> torch.Tensor:
+                       pix: torch.Tensor, na: int, nb: int, uses: int = 1, fused_forward: bool = True) -> torch.Tensor:
     """conv2's output rows [B * na / 9, 32] = patches(act(bn(conv(img)))) @ w2^T (w2 [32, 144], columns (j, c)),
     running statistics of the first BN updated as stem1_bn_act does."""
     code, slope = _act_code(act)
-    z2, stats = _Stem12.apply(img, conv_w, bn.weight, bn.bias, w2, pix, na, nb, bn.eps, code, slope)
+    z2, stats = _Stem12.apply(img, conv_w, bn.weight, bn.bias, w2, pix, na, nb, bn.eps, code, slope, fused_forward)
     _update_running(bn, stats, uses)
     return z2
 

@@ -81,6 +81,8 @@ class VisionActorCritic(ActorCritic):
     # with fused_bn: conv2's input gradient formed inside the first block's backward passes (fused_bn._Stem12); False:
     # the first block alone, conv2 as a patch GEMM (tests and scripts/bench_vision.py --no-fused-conv2 compare the two)
     fused_conv2 = True
+    # with fused_conv2: conv2's forward inside the first block's apply pass too (False: conv2's forward as a GEMM)
+    fused_conv2_forward = True
 
     def __init__(self, num_actor_obs: int, num_critic_obs: int, num_actions: int, img_res=(72, 96),
                  dim_hidden_input: int = 192, actor_hidden_dims=(256, 256, 256), critic_hidden_dims=(256, 256, 256),
@@ -205,7 +207,8 @@ class VisionActorCritic(ActorCritic):
             # conv1 + BN1 + act + conv2: the backward forms conv2's input gradient inside the first block's passes
             if bn1.track_running_stats and bn1.num_batches_tracked is not None:
                 bn1.num_batches_tracked.add_(1)
-            z2 = stem12_bn_act_conv(bn1, act, conv1.weight, w2m, flat, pix16, n1, n1_left, self._bn_uses)
+            z2 = stem12_bn_act_conv(bn1, act, conv1.weight, w2m, flat, pix16, n1, n1_left, self._bn_uses,
+                                    self.fused_conv2_forward)
             block2 = self._bn_act(bn2, act, z2)
         elif self.fused_bn and stem1_applicable(bn1, act, flat, conv1.weight):
             # conv1 + BN1 + act from the image itself: no patch matrix, no conv output (rsl_rl/fused_bn.py)

@@ -461,6 +461,15 @@ int gr_stem1_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, c
                       int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b,
                       const float* stats, int32_t act, float slope, const float* gy, int64_t gy_rows, float* g_conv_w,
                       float* g_bn_w, float* g_bn_b, double* part, void* stream);
+/* The first block's forward with the stem's conv2, Conv2d(c = 16, 32, 3, stride 3, no bias), fused into its apply
+ * pass: y [nimg * na][16] as gr_stem1_forward stores it (y_rows = nimg * na: the table-a rows) and conv2's output
+ * z2 [nimg * n2][32] (na = 9 n2; row 9 p + j of an image = position j of patch p).  w2f: conv2's weight as
+ * [9][4][32][4] floats, w2f[((j * 4 + g) * 32 + o) * 4 + v] = W[o][4 g + v][j / 3][j % 3] (16-byte aligned).
+ * Same workspace and stats as gr_stem1_forward. */
+int gr_stem12_forward(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
+                      int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b, float eps,
+                      int32_t act, float slope, const float* w2f, int32_t n2, float* y, float* z2, float* stats,
+                      double* part, void* stream);
 /* The same backward when the next layer is the stem's conv2, Conv2d(c = 16, 32, 3, stride 3, no bias), on the
  * nimg x na table-a rows grouped as its patches (row 9 p + j of an image = position j of patch p, na = 9 n2): takes
  * conv2's OUTPUT gradient gz2 [nimg * n2][32] (16-byte aligned) and forms conv2's input gradient inside the passes

@@ -42,6 +42,8 @@ def main(argv=None):
     ap.add_argument("--iters", type=int, default=2, help="training iterations (0: skip)")
     ap.add_argument("--storage-bf16", action="store_true", help="rollout storage observations in bf16")
     ap.add_argument("--no-fused-bn", action="store_true", help="the stem's BatchNorm + activation on torch's ops")
+    ap.add_argument("--no-fused-conv2-forward", action="store_true",
+                    help="conv2's forward as a GEMM (not inside the first block's apply pass)")
     ap.add_argument("--no-fused-conv2", action="store_true",
                     help="conv2's input gradient as a GEMM (not inside the first block's backward passes)")
     ap.add_argument("--no-share", action="store_true", help="PPOL2C2's mixed batch through two stem forwards")
@@ -64,11 +66,12 @@ def run(args):
     pol = runner.alg.policy
     pol.fused_bn = not args.no_fused_bn
     pol.fused_conv2 = not getattr(args, "no_fused_conv2", False)
+    pol.fused_conv2_forward = not getattr(args, "no_fused_conv2_forward", False)
     obs, extras = env.get_observations()
     crit = extras["observations"]["critic"]
     g = torch.Generator(device=dev).manual_seed(1)
     acts = [torch.randn(n, 4, device=dev, generator=g) for _ in range(4)]
-    out = {"fused_bn": pol.fused_bn, "fused_conv2": pol.fused_conv2, "share_mix_features": runner.alg.share_mix_features, "envs": n, "obs_dim": int(obs.shape[1]), "params": sum(p.numel() for p in pol.parameters())}
+    out = {"fused_bn": pol.fused_bn, "fused_conv2": pol.fused_conv2, "fused_conv2_forward": pol.fused_conv2_forward, "share_mix_features": runner.alg.share_mix_features, "envs": n, "obs_dim": int(obs.shape[1]), "params": sum(p.numel() for p in pol.parameters())}
 
     for _ in range(4):
         env.step(acts[0])

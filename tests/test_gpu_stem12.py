@@ -3,9 +3,9 @@
 as a patch GEMM, hipBLASLt dgrad) and (b) a float64 evaluation of the whole stem (reference
 vision_actor_critic.py:93-105 as written: nn.Conv2d / BatchNorm2d / LeakyReLU on NCHW images).
 
-The forward is the same kernels and GEMM either way, so features and BatchNorm statistics must be bit-identical
-to (a).  Gradients reduce over ~10^6 rows in another order: held to 1e-4 of each tensor's largest magnitude against
-(a) and against (b)."""
+The first BatchNorm's statistics come from the same pass either way (bit-identical); conv2's output is summed in
+another order than hipBLASLt's (features and the later BatchNorm statistics within 1e-5).  Gradients reduce over
+~10^6 rows in another order: held to 1e-4 of each tensor's largest magnitude against (a) and against (b)."""
 from __future__ import annotations
 
 import copy
@@ -78,9 +78,13 @@ def test_stem12_backward_matches_unfused_and_float64(img_res, nimg, act):
     assert pol_n1 == 9 * pol_n2
     f_f, g_f, b_f = _grads(pol, obs, gfeat, fused=True)
     f_u, g_u, b_u = _grads(pol, obs, gfeat, fused=False)
-    assert torch.equal(f_f, f_u)  # same forward kernels and GEMM
+    # conv2 on MFMA in the apply pass vs the hipBLASLt GEMM: another summation order over its 144 inputs
+    assert _rel(f_f, f_u) <= 1e-5, _rel(f_f, f_u)
     for k in b_u:
-        assert torch.equal(b_f[k], b_u[k]), k
+        if "num_batches" in k or ".0." in k or k.startswith("stem.1."):  # the first BN's statistics: same pass
+            assert torch.equal(b_f[k], b_u[k]), k
+        else:
+            assert _rel(b_f[k], b_u[k]) <= 1e-5, (k, _rel(b_f[k], b_u[k]))
     assert set(g_f) == set(g_u)
     g64 = _reference64(pol, obs, gfeat)
     for k in g_u:
