@@ -148,3 +148,19 @@ def test_stem12_rejects_shapes_it_does_not_cover():
     assert call(gz2=p + 4) == -1       # gz2 not 16-byte aligned
     assert call(w2t=None) == -1
     assert call(act=7) == -1
+
+
+def test_stem12_forward_rejects_shapes_it_does_not_cover():
+    """gr_stem12_forward (conv2 inside the first block's apply pass): 16 channels, na = 9 n2, 16-byte aligned outputs
+    and weights; anything else is an argument error before any launch."""
+    lib = _abi.load()
+    p = 0x10000
+
+    def call(c=16, na=720, n2=80, w2f=p, z2=p, act=_abi.GR_POLICY_ACT_LRELU):
+        return lib.gr_stem12_forward(p, 6928, 16, 8, p, na, 48, p, c, p, p, 1e-5, act, 0.01, w2f, n2, p, z2, p, p, None)
+
+    assert call(c=32) == -1
+    assert call(na=718) == -1
+    assert call(w2f=p + 8) == -1
+    assert call(z2=None) == -1
+    assert call(act=5) == -1
