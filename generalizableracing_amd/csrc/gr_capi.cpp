@@ -994,6 +994,19 @@ int gr_stem1_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, c
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
+int64_t gr_patch_wgrad32_floats(int64_t m, int32_t k) {
+  if (m < 1 || (k != 128 && k != 144)) return GR_ERR_ARG;
+  return (int64_t)gr::patch_wgrad_blocks(m) * 32 * k;
+}
+
+int gr_patch_wgrad32(const float* x, const float* gy, int64_t m, int32_t k, float* part, float* gw, void* stream) {
+  if (!x || !gy || !part || !gw || m < 1 || (k != 128 && k != 144) || !aligned16(x) || !aligned16(gy) ||
+      m * (int64_t)k >= ((int64_t)1 << 40))
+    return GR_ERR_ARG;
+  const hipError_t e = gr::launch_patch_wgrad32(x, gy, (long long)m, k, part, gw, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
 int gr_stem12_forward(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
                       int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b, float eps,
                       int32_t act, float slope, const float* w2f, int32_t n2, float* y, float* z2, float* stats,

@@ -90,6 +90,134 @@ __global__ __launch_bounds__(CF_WAVES * 64) void colsum_final(const float* __res
   }
 }
 
+// ------------------------------------------------------------- weight gradient of a 32-output patch GEMM
+// gw[32][K] = gy[M][32]^T x[M][K] over millions of rows (the vision stem's conv2: x = its input patches, the first
+// block's output y1 [M][144]; hipBLASLt's split-K tiles streamed the 1.38 GB at ~3.7 TB/s).  A wave takes a run of
+// rows and holds the whole [32][K] product in MFMA accumulators (2 x K/16 tiles of v_mfma_f32_16x16x4f32): per four
+// rows (the k step), lane (i = l % 16, g = l / 16) supplies row g's gy columns 2 i, 2 i + 1 (A of tiles nt = 0, 1)
+// and x columns KT i .. KT i + KT - 1 (B of tiles kt), read as float2 / float4 loads; PW_DEPTH row quads per
+// register set, the next set's loads in flight under the current set's MFMAs.  The
+// workgroup's four wave sums are added in wave order through LDS, and pw_final sums the workgroup rows in order:
+// deterministic, no atomics.
+constexpr int PW_WAVES = 4;
+constexpr int PW_DEPTH = 2;  // (same-box A/B, r5pw6: depth 2 307 us, 3 319, 4 325; more workgroups no faster)
+typedef float pw4 __attribute__((ext_vector_type(4)));
+typedef float pw4u __attribute__((ext_vector_type(4), aligned(4)));
+
+template <int KT>
+__global__ __launch_bounds__(PW_WAVES * 64) void pw_partial(const float* __restrict__ x, const float* __restrict__ gy,
+                                                             long long m, long long rows_per_wave,
+                                                             float* __restrict__ part) {
+  constexpr int K = 16 * KT;
+  __shared__ float red[32 * K];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
+  pw4 acc[2][KT];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) acc[nt][kt] = pw4{0.0f, 0.0f, 0.0f, 0.0f};
+  const long long r0 = ((long long)blockIdx.x * PW_WAVES + w) * rows_per_wave;
+  const long long r1 = r0 + rows_per_wave < m ? r0 + rows_per_wave : m;
+  // two register sets of PW_DEPTH row quads: the next set's loads are in flight under this set's MFMAs (full sets
+  // only; the run's last, partial set is loaded with its dead rows' gy zeroed)
+  // lane i reads its KT consecutive columns KT i .. KT i + KT - 1 of x (tile kt holds column KT i + kt) and its two
+  // consecutive gy columns 2 i, 2 i + 1 (tile nt holds output row 2 i + nt): a few wide loads per row instead of one
+  // 4-byte load per tile (measured faster than float4 loads of columns 64 q + 4 i, which read each stretch whole)
+  auto load_row = [&](long long r, float (&a)[2], float (&b)[KT]) {
+    const float2 y2 = *reinterpret_cast<const float2*>(gy + r * 32 + 2 * i);
+    a[0] = y2.x;
+    a[1] = y2.y;
+    const float* xr = x + r * K + KT * i;
+#pragma unroll
+    for (int kt = 0; kt + 4 <= KT; kt += 4) {
+      const pw4u v = *reinterpret_cast<const pw4u*>(xr + kt);  // (4-byte aligned: still one dwordx4 load)
+      b[kt] = v.x; b[kt + 1] = v.y; b[kt + 2] = v.z; b[kt + 3] = v.w;
+    }
+#pragma unroll
+    for (int kt = KT / 4 * 4; kt < KT; ++kt) b[kt] = xr[kt];
+  };
+  auto load = [&](long long q, float (&a)[PW_DEPTH][2], float (&b)[PW_DEPTH][KT]) {
+#pragma unroll
+    for (int d = 0; d < PW_DEPTH; ++d) load_row(q + 4 * d + g, a[d], b[d]);
+  };
+  auto mma = [&](const float (&a)[PW_DEPTH][2], const float (&b)[PW_DEPTH][KT]) {
+#pragma unroll
+    for (int d = 0; d < PW_DEPTH; ++d)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt)
+          acc[nt][kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[d][nt], b[d][kt], acc[nt][kt], 0, 0, 0);
+  };
+  constexpr int STEP = 4 * PW_DEPTH;
+  const long long full = r0 + (r1 > r0 ? (r1 - r0) / STEP * STEP : 0);  // end of the full sets
+  float a0[PW_DEPTH][2], b0[PW_DEPTH][KT], a1[PW_DEPTH][2], b1[PW_DEPTH][KT];
+  long long q = r0;
+  if (q < full) load(q, a0, b0);
+  while (q < full) {
+    const bool more = q + STEP < full;
+    if (more) load(q + STEP, a1, b1);
+    __builtin_amdgcn_sched_barrier(0);  // (the next set's loads stay ahead of these MFMAs)
+    mma(a0, b0);
+    q += STEP;
+    if (!more) break;
+    const bool more2 = q + STEP < full;
+    if (more2) load(q + STEP, a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(a1, b1);
+    q += STEP;
+    if (!more2) break;
+  }
+  if (full < r1) {  // the partial set: rows past r1 read row r0 (in bounds) against a zero gy
+#pragma unroll
+    for (int d = 0; d < PW_DEPTH; ++d) {
+      const long long r = full + 4 * d + g;
+      const bool live = r < r1;
+      load_row(live ? r : r0, a0[d], b0[d]);
+      a0[d][0] = live ? a0[d][0] : 0.0f;
+      a0[d][1] = live ? a0[d][1] : 0.0f;
+    }
+    mma(a0, b0);
+  }
+  // lane (n = i, g) holds, for tile (nt, kt), output row 2 (4 g + v) + nt (the A row 4 g + v) and column
+  // KT i + kt
+  for (int ww = 0; ww < PW_WAVES; ++ww) {
+    if (w == ww) {
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            float* dst = red + (2 * (4 * g + v) + nt) * K + KT * i + kt;
+            *dst = ww == 0 ? acc[nt][kt][v] : *dst + acc[nt][kt][v];
+          }
+    }
+    __syncthreads();
+  }
+  for (int e = threadIdx.x; e < 32 * K; e += PW_WAVES * 64) part[(size_t)blockIdx.x * 32 * K + e] = red[e];
+}
+
+int patch_wgrad_blocks(long long m) {
+  const long long b = (m + 4095) / 4096;  // ~1 K rows per wave
+  return (int)(b < 1 ? 1 : (b > 512 ? 512 : b));
+}
+
+hipError_t launch_patch_wgrad32(const float* x, const float* gy, long long m, int k, float* part, float* gw,
+                                hipStream_t s) {
+  const int blocks = patch_wgrad_blocks(m);
+  long long rpw = (m + (long long)blocks * PW_WAVES - 1) / ((long long)blocks * PW_WAVES);
+  rpw = (rpw + 3) & ~3LL;
+  if (k == 144)
+    hipLaunchKernelGGL(pw_partial<9>, dim3(blocks), dim3(PW_WAVES * 64), 0, s, x, gy, m, rpw, part);
+  else if (k == 128)
+    hipLaunchKernelGGL(pw_partial<8>, dim3(blocks), dim3(PW_WAVES * 64), 0, s, x, gy, m, rpw, part);
+  else
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(colsum_final, dim3((32 * k + 63) / 64), dim3(CF_WAVES * 64), 0, s, part, blocks, 32 * k, gw);
+  return hipGetLastError();
+}
+
 int column_sum_blocks(long long m) {
   long long b = (m + 255) / 256;
   return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));

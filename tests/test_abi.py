@@ -164,3 +164,20 @@ def test_stem12_forward_rejects_shapes_it_does_not_cover():
     assert call(w2f=p + 8) == -1
     assert call(z2=None) == -1
     assert call(act=5) == -1
+
+
+def test_patch_wgrad32_rejects_shapes_it_does_not_cover():
+    """gr_patch_wgrad32 (conv2's weight gradient): k of 128 or 144 columns, 16-byte aligned x and gy, m >= 1."""
+    lib = _abi.load()
+    p = 0x10000
+    assert lib.gr_patch_wgrad32_floats(4096, 144) == 32 * 144
+    assert lib.gr_patch_wgrad32_floats(1, 100) == -1
+    assert lib.gr_patch_wgrad32_floats(0, 144) == -1
+
+    def call(x=p, gy=p, m=100, k=144):
+        return lib.gr_patch_wgrad32(x, gy, m, k, p, p, None)
+
+    assert call(k=64) == -1
+    assert call(m=0) == -1
+    assert call(x=p + 4) == -1
+    assert call(gy=None) == -1

@@ -117,3 +117,30 @@ def test_stem12_is_the_path_taken():
         names.add(n)
         stack.extend(x[0] for x in n.next_functions)
     assert any("_Stem12" in type(n).__name__ for n in names)
+
+
+@pytest.mark.parametrize("m,k", [(1, 144), (7, 128), (4099, 144), (1_966_080, 144), (491_527, 128)])
+def test_patch_wgrad32_matches_float64(m, k):
+    """gr_patch_wgrad32 (gw[32][k] = gy^T x, conv2's weight gradient) against float64 at ragged and full sizes
+    (1 966 080 rows = conv2's patches of a 24 576-image mini-batch); repeats bit-identical."""
+    from generalizableracing_amd import _abi
+    import ctypes as C
+
+    lib = _abi.load()
+    g = torch.Generator(device=DEV).manual_seed(m % 1000 + k)
+    x = torch.rand(m, k, device=DEV, generator=g) * 2.0
+    gy = torch.randn(m, 32, device=DEV, generator=g)
+    part = torch.empty(int(lib.gr_patch_wgrad32_floats(m, k)), device=DEV)
+    out = torch.empty(32, k, device=DEV)
+
+    def run():
+        rc = lib.gr_patch_wgrad32(x.data_ptr(), gy.data_ptr(), m, k, part.data_ptr(), out.data_ptr(),
+                                  C.c_void_p(_abi.raw_stream(x.device)))
+        assert rc == 0
+        torch.cuda.synchronize()
+        return out.clone()
+
+    o1 = run()
+    want = (gy.double().t() @ x.double()).cpu()
+    assert _rel(o1, want) <= 1e-5, _rel(o1, want)
+    assert torch.equal(o1, run())
