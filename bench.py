@@ -842,13 +842,16 @@ def main():
         # the reference's registered recipe end to end: depth camera + VisionActorCritic + PPOL2C2 (fused BN stem)
         import bench_vision
 
-        vis = bench_vision.run(argparse.Namespace(envs=4096, steps=8, iters=2, storage_bf16=False, no_fused_bn=False))
+        vis = bench_vision.run(argparse.Namespace(envs=4096, steps=8, iters=2, storage_bf16=False, no_fused_bn=False,
+                                                  graph_update=True))
         progress("vision_train")
         extra["vision_train_total_fps_4096_envs"] = {
             "value": vis["train_total_fps"], "train_iter_s": vis["train_iter_s"],
             "rollout_env_steps_per_s": vis["rollout_env_steps_per_s"], "max_mem_GB": vis["max_mem_GB"],
-            "note": "Perf/total_fps of QuadcopterVisionPPORunnerCfg (VisionActorCritic 72x96 stem as patch GEMMs "
-                    "with the fused HIP BatchNorm + LeakyReLU, PPOL2C2), obstacle tracks, fp32"}
+            "graph_update": vis["graph_update"],
+            "note": "Perf/total_fps of QuadcopterVisionPPORunnerCfg (VisionActorCritic 72x96 stem: fused HIP first "
+                    "block + conv2, BatchNorm + LeakyReLU passes, PPOL2C2 with the update's mini-batch steps as "
+                    "hipGraph replays), obstacle tracks, fp32"}
     cpu = None
     if rank == 0 and ws == 1 and want(a, "cpu"):
         cpu = cpu_baseline(a.cpu_seconds, obstacles=bool(a.obstacles))

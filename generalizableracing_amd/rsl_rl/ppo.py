@@ -431,6 +431,9 @@ class _GraphedStep:
     def _capture(self):
         # snapshot (parameters, optimizer state, rate), warm up on a side stream, capture, restore
         snap_p = [p.detach().clone() for p in self.params]
+        # (the module's buffers too: the warm-up and captured steps' BatchNorm running statistics and batch counts)
+        bufs = list(self.alg.policy.buffers())
+        snap_bufs = [b.detach().clone() for b in bufs]
         snap_lr = self.lr.clone()
         snap_acc = self.acc.clone()
         self.flat.bind()  # Adam and the clip read the gradients from these views (static addresses)
@@ -471,15 +474,25 @@ class _GraphedStep:
                 for k, v in snap_o[id(p)].items():
                     if torch.is_tensor(v):
                         self.opt.state[p][k].copy_(v)
+            for b, v in zip(bufs, snap_bufs):
+                b.copy_(v)
             self.lr.copy_(snap_lr)
             self.acc.copy_(snap_acc)
+
+    def _refresh_sources(self):
+        """Before an update's replays: this rollout's samples, packed in place (the graphs read the buffer)."""
+        if self.pack is not None:
+            self.alg.storage.pack_samples(out=self.pack)
+
+    def _stats(self, num_updates):
+        sl, vl = self.acc.tolist()
+        return {"value_function": vl / num_updates, "surrogate": sl / num_updates}
 
     def update(self):
         alg = self.alg
         n = alg.num_mini_batches
         perm = torch.randperm(n * self.mb, device=self.perm.device)  # rollout_storage.py:152-191, drawn first
-        if self.pack is not None:  # this rollout's samples, packed in place (the graphs read the buffer)
-            alg.storage.pack_samples(out=self.pack)
+        self._refresh_sources()
         if self.graph is None:
             had_state = bool(self.opt.state)
             if not had_state:  # Adam's first step creates its state: take it with zero gradients, then undo
@@ -512,5 +525,4 @@ class _GraphedStep:
         num_updates = alg.num_learning_epochs * n
         alg.learning_rate = float(self.lr)
         alg.storage.clear()
-        sl, vl = self.acc.tolist()
-        return {"value_function": vl / num_updates, "surrogate": sl / num_updates}
+        return self._stats(num_updates)

@@ -28,7 +28,7 @@ import torch.nn as nn
 
 from . import distributed as gdist
 from . import flat_adam as _fadam
-from .ppo import PPO
+from .ppo import PPO, _GraphedStep
 from .rollout_storage_l2c2 import RolloutStorageL2C2
 
 
@@ -64,6 +64,7 @@ class PPOL2C2(PPO):
         self.share_mix_features = bool(share_mix_features)
         super().__init__(policy, env=env, normalize_advantage=True, **kwargs)
         self.transition = RolloutStorageL2C2.Transition()
+        self._mix_uniform = torch.rand_like  # the smoothness loss's uniform draw (tests substitute a fixed one)
         self.value_smoothness_coef = value_smoothness_coef
         self.smoothness_upper_bound = smoothness_upper_bound
         self.smoothness_lower_bound = smoothness_lower_bound
@@ -107,7 +108,7 @@ class PPOL2C2(PPO):
     def smooth_loss(self, obs_batch, next_obs_batch, cont_batch, mu_batch, value_batch):
         """ppo_l2c2.py:176-188; returns (smooth_loss, action_smoothness)."""
         policy_coef, value_coef = self.smooth_coefs()
-        mix_weights = cont_batch * (torch.rand_like(cont_batch) - 0.5) * 2.0
+        mix_weights = cont_batch * (self._mix_uniform(cont_batch) - 0.5) * 2.0
         mix_obs_batch = _mix(obs_batch, next_obs_batch, mix_weights)
         shared = getattr(self.policy, "shared_features", None)
         if shared is not None and self.share_mix_features:
@@ -127,6 +128,13 @@ class PPOL2C2(PPO):
         return loss, action_smoothness
 
     def update(self):
+        if self.graph_update and self.storage is not None and str(self.device).startswith("cuda"):
+            if self._graphed is None:
+                self._graphed = _GraphedStepL2C2(self)
+            out = self._graphed.update()
+            if self.fused is not None:  # graph replays write the parameters without bumping their versions
+                self.fused.refresh()
+            return out
         mean_value_loss = torch.zeros((), device=self.device)
         mean_surrogate_loss = torch.zeros((), device=self.device)
         mean_smooth_loss = torch.zeros((), device=self.device)
@@ -168,3 +176,70 @@ class PPOL2C2(PPO):
             "surrogate": float(mean_surrogate_loss) / num_updates,
             "smooth_loss": float(mean_smooth_loss) / num_updates,
         }
+
+
+class _GraphedStepL2C2(_GraphedStep):
+    """PPOL2C2.update's mini-batch step as hipGraph replays (ppo.py _GraphedStep: one graph per epoch on one rank,
+    two segments around the eager all-reduce on several): the vision recipe's update is ~590 launches per
+    mini-batch, most of them small, and the eager loop reads the KL back to the host once per mini-batch.
+
+    Segment A is ppo_l2c2.py:127-191 on the mini-batch gathered by a static index buffer from the (T-1) N samples
+    (rollout_storage_l2c2.py:131-167; the continuation flags in a persistent buffer refreshed per update): the
+    distribution and values, the KL mean into the flat buffer's extra slot, the PPO losses, the smoothness loss
+    (its own uniform draw per replay: torch's graph-safe generator), and the backward into the flat gradient
+    views.  Segment B is the base class's: the rate rule on the device, the clip and Adam.  As in _GraphedStep the
+    learning rate is an fp32 device tensor and the eager loop's unused action draw is not made; the BatchNorm
+    running statistics of the warm-up and captured steps are restored after the capture."""
+
+    def __init__(self, alg: "PPOL2C2"):
+        super().__init__(alg)
+        st, dev = alg.storage, alg.device
+        if self.T < 2:
+            raise ValueError("L2C2 needs at least 2 transitions per env (pairs obs[t] with obs[t+1])")
+        self.mb = (self.T - 1) * self.N // self.nmb
+        self.perm = torch.zeros(self.nmb * self.mb, dtype=torch.long, device=dev)
+        self.idx = self.perm[:self.mb]
+        self.cols, self.pack = None, None
+        self.acc = torch.zeros(3, device=dev)  # the update's sums of the surrogate, value and smoothness means
+        self.cont = torch.zeros((self.T - 1) * self.N, 1, device=dev)
+
+    def _refresh_sources(self):
+        st = self.alg.storage
+        with torch.no_grad():
+            torch.sub(1.0, st.dones[:self.T - 1].float().flatten(0, 1), out=self.cont)
+
+    def _sources(self):
+        st, T = self.alg.storage, self.T
+        obs = st.observations[:T - 1].flatten(0, 1)
+        crit = st.privileged_observations[:T - 1].flatten(0, 1) if st.privileged_observations is not None else obs
+        return (obs, crit, st.observations[1:T].flatten(0, 1), self.cont) + tuple(
+            x[:T - 1].flatten(0, 1) for x in (st.actions, st.values, st.advantages, st.returns, st.actions_log_prob,
+                                               st.mu, st.sigma))
+
+    def _gather(self, idx):
+        return tuple(x.index_select(0, idx) for x in self._sources())
+
+    def _seg_a(self, idx=None):
+        alg, pol = self.alg, self.alg.policy
+        obs, crit, nxt, cont, act, val, adv, ret, logp, mu, sig = self._gather(self.idx if idx is None else idx)
+        obs, crit, nxt = obs.float(), crit.float(), nxt.float()
+        pol.update_distribution(obs)
+        logp_b = pol.get_actions_log_prob(act)
+        value_b = pol.evaluate(crit)
+        mu_b, sigma_b, entropy_b = pol.action_mean, pol.action_std, pol.entropy
+        if self._adaptive():
+            with torch.no_grad():
+                kl = torch.sum(torch.log(sigma_b / sig + 1.0e-5)
+                               + (torch.square(sig) + torch.square(mu - mu_b)) / (2.0 * torch.square(sigma_b)) - 0.5,
+                               axis=-1)
+                self.flat.extra[0].copy_(torch.mean(kl))
+        surrogate_loss, value_loss = alg._ppo_losses(logp_b, logp, adv, value_b, val, ret)
+        loss = surrogate_loss + alg.value_loss_coef * value_loss - alg.entropy_coef * entropy_b.mean()
+        smooth_loss, _ = alg.smooth_loss(obs, nxt, cont, mu_b, value_b)
+        loss = loss + smooth_loss
+        self.acc.add_(torch.stack([surrogate_loss.detach(), value_loss.detach(), smooth_loss.detach()]))
+        self._backward(loss)
+
+    def _stats(self, num_updates):
+        sl, vl, ml = self.acc.tolist()
+        return {"value_function": vl / num_updates, "surrogate": sl / num_updates, "smooth_loss": ml / num_updates}

@@ -47,6 +47,8 @@ def main(argv=None):
     ap.add_argument("--no-fused-conv2", action="store_true",
                     help="conv2's input gradient as a GEMM (not inside the first block's backward passes)")
     ap.add_argument("--no-share", action="store_true", help="PPOL2C2's mixed batch through two stem forwards")
+    ap.add_argument("--graph-update", action="store_true",
+                    help="the update's mini-batch steps as hipGraph replays (ppo_l2c2._GraphedStepL2C2)")
     print(json.dumps(run(ap.parse_args(argv))))
 
 
@@ -63,6 +65,7 @@ def run(args):
         d["algorithm"]["storage_obs_dtype"] = torch.bfloat16
     runner = OnPolicyRunner(env, d, log_dir=None, device=dev)
     runner.alg.share_mix_features = not getattr(args, "no_share", False)
+    runner.alg.graph_update = bool(getattr(args, "graph_update", False))
     pol = runner.alg.policy
     pol.fused_bn = not args.no_fused_bn
     pol.fused_conv2 = not getattr(args, "no_fused_conv2", False)
@@ -71,7 +74,7 @@ def run(args):
     crit = extras["observations"]["critic"]
     g = torch.Generator(device=dev).manual_seed(1)
     acts = [torch.randn(n, 4, device=dev, generator=g) for _ in range(4)]
-    out = {"fused_bn": pol.fused_bn, "fused_conv2": pol.fused_conv2, "fused_conv2_forward": pol.fused_conv2_forward, "share_mix_features": runner.alg.share_mix_features, "envs": n, "obs_dim": int(obs.shape[1]), "params": sum(p.numel() for p in pol.parameters())}
+    out = {"fused_bn": pol.fused_bn, "fused_conv2": pol.fused_conv2, "fused_conv2_forward": pol.fused_conv2_forward, "share_mix_features": runner.alg.share_mix_features, "graph_update": runner.alg.graph_update, "envs": n, "obs_dim": int(obs.shape[1]), "params": sum(p.numel() for p in pol.parameters())}
 
     for _ in range(4):
         env.step(acts[0])

@@ -1,0 +1,161 @@
+"""PPOL2C2 with algorithm.graph_update (ppo_l2c2._GraphedStepL2C2) on the reference's registered recipe (depth
+camera + VisionActorCritic with the fused stem + PPOL2C2): the update's mini-batch steps captured once per epoch
+and replayed must give the eager update's parameters, BatchNorm running statistics, learning rate and losses from
+the same rollout, at the first call (capture) and the next (replay) (the running statistics, like the parameters,
+within 5 % of how far the update moved them).
+
+The smoothness loss's uniform draw is the one input the two cannot share (the graphs draw from torch's graph-safe
+generator), so the comparison substitutes a fixed draw (u = 0.75: every mixed row 0.5 of the way to its successor)
+in both; a second test keeps the real draw and holds the graphed update to the eager one's direction.  Tolerance as
+tests/test_gpu_graph_update.py (fp32 device learning rate, another gradient accumulation order): parameters within
+5 % of their movement (norms), the value loss 1e-4 relative, the smoothness loss 2e-3."""
+import copy
+import os
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from generalizableracing_amd.envs.racing_cfg import CameraCfg, RacingEnvCfg, SceneCfg, SimCfg  # noqa: E402
+from generalizableracing_amd.envs.racing_env import RacingEnv, RslRlVecEnvWrapper  # noqa: E402
+from generalizableracing_amd.rsl_rl import OnPolicyRunner  # noqa: E402
+from generalizableracing_amd.rsl_rl.config import QuadcopterVisionPPORunnerCfg  # noqa: E402
+from generalizableracing_amd.rsl_rl.ppo_l2c2 import PPOL2C2  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _pair(n, steps, fixed_mix):
+    env = RslRlVecEnvWrapper(RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=DEV),
+                                                    camera=CameraCfg())))
+    cfg = QuadcopterVisionPPORunnerCfg(device=DEV, num_steps_per_env=steps)
+    cfg.algorithm.obs_sink = False  # the storages are copied slot for slot
+    runner = OnPolicyRunner(env, cfg.to_dict(), log_dir=None, device=DEV)
+    alg = runner.alg
+    kw = dict(cfg.to_dict()["algorithm"])
+    kw.pop("class_name")
+    kw.pop("obs_sink", None)
+    kw["graph_update"] = True
+    alg_g = PPOL2C2(copy.deepcopy(alg.policy), device=DEV, **kw)
+    od = env.num_obs
+    alg_g.init_storage("rl", n, steps, [od], [od], [4])
+    if fixed_mix:
+        for a in (alg, alg_g):
+            a._mix_uniform = lambda c: torch.full_like(c, 0.75)
+    obs, extras = env.get_observations()
+    cobs = extras["observations"]["critic"]
+    with torch.inference_mode():
+        for _ in range(steps):
+            a = alg.act(obs, cobs)
+            obs, rew, dones, infos = env.step(a)
+            cobs = infos["observations"]["critic"]
+            alg.process_env_step(rew, dones, infos)
+        alg.compute_returns(cobs)
+    for name, v in vars(alg.storage).items():
+        if torch.is_tensor(v):
+            getattr(alg_g.storage, name).copy_(v)
+    # (the rollout's train-mode forwards moved the BatchNorm running statistics of the eager policy)
+    alg_g.policy.load_state_dict(alg.policy.state_dict())
+    return env, alg, alg_g
+
+
+def _buffers(pol):
+    return {k: v for k, v in pol.state_dict().items() if "running" in k or "num_batches" in k}
+
+
+def test_graphed_l2c2_update_matches_eager():
+    torch.manual_seed(3)
+    n, steps = 512, 8
+    env, alg, alg_g = _pair(n, steps, fixed_mix=True)
+    assert alg.policy.fused_bn
+    for rep in range(2):  # capture, then replay
+        alg_g.storage.step = alg.storage.step = steps
+        p0 = [p.detach().clone() for p in alg.policy.parameters()]
+        b0 = {k: v.clone() for k, v in _buffers(alg.policy).items()}
+        torch.manual_seed(7 + rep)
+        le = alg.update()
+        torch.manual_seed(7 + rep)
+        lg = alg_g.update()
+        n_moved = 0
+        for (name, pe), pg, q in zip(alg.policy.named_parameters(), alg_g.policy.parameters(), p0):
+            # (the conv biases ahead of a BatchNorm get no gradient: those stay put in both)
+            moved = float((pe.detach() - q).norm())
+            diff = float((pe.detach() - pg.detach()).norm())
+            assert diff <= 0.05 * moved, (rep, name, diff, moved)
+            n_moved += moved > 0.0
+        assert n_moved >= len(p0) - 3, (n_moved, len(p0))
+        be, bg = _buffers(alg.policy), _buffers(alg_g.policy)
+        assert set(be) == set(bg) and len(be) >= 9
+        bad = []
+        for k in be:
+            if "num_batches" in k:
+                if not torch.equal(be[k], bg[k]):
+                    bad.append((k, int(be[k]), int(bg[k])))
+            else:
+                # as the parameters: within 5 % of how far the update moved them
+                moved, diff = float((be[k] - b0[k]).norm()), float((bg[k] - be[k]).norm())
+                if not (moved > 0.0 and diff <= 0.05 * moved):
+                    bad.append((k, diff, moved))
+        assert not bad, (rep, bad)
+        assert abs(alg.learning_rate - alg_g.learning_rate) <= 1e-6 * alg.learning_rate
+        assert abs(le["value_function"] - lg["value_function"]) <= 1e-4 * abs(le["value_function"]), (rep, le, lg)
+        # the smoothness loss is a mean of squared distances between two nearly equal policy outputs (~1e-3): the
+        # parameters' round-off differences of the later mini-batches show in it at ~1e-4 relative
+        assert abs(le["smooth_loss"] - lg["smooth_loss"]) <= 2e-3 * abs(le["smooth_loss"]), (rep, le, lg)
+        assert abs(le["surrogate"] - lg["surrogate"]) <= 5e-5, (le["surrogate"], lg["surrogate"])
+        with torch.no_grad():  # the next update starts from identical states
+            for pe, pg in zip(alg.policy.parameters(), alg_g.policy.parameters()):
+                pg.copy_(pe)
+                se, sg = alg.optimizer.state[pe], alg_g.optimizer.state[pg]
+                if not se:  # (a parameter the loss does not reach: no gradient, no eager Adam state; the graphed
+                    # update's zero-gradient first step gave it zero moments, never stepped again)
+                    assert not sg or (float(sg["exp_avg"].abs().max()) == 0.0 and float(pg.grad is None))
+                    continue
+                for key in ("exp_avg", "exp_avg_sq", "step"):
+                    sg[key].copy_(se[key])
+            for k, v in _buffers(alg.policy).items():
+                alg_g.policy.state_dict()[k].copy_(v)
+        alg_g.learning_rate = alg.learning_rate
+    assert alg_g._graphed is not None and alg_g._graphed.graph is not None
+    env.close()
+
+
+def test_graphed_l2c2_update_draws_fresh_uniforms():
+    """With the real draw the graphed steps take their uniforms from torch's graph-safe generator: every replayed
+    mini-batch step draws anew (four distinct draws per epoch graph, new ones on the next update), uniform on
+    [0, 1); the losses stay finite and the value loss near the eager update's."""
+    torch.manual_seed(4)
+    n, steps = 512, 8
+    env, alg, alg_g = _pair(n, steps, fixed_mix=False)
+    nmb, mb = alg_g.num_mini_batches, (steps - 1) * n // alg_g.num_mini_batches
+    rec = torch.zeros(nmb, mb, device=DEV)
+    calls = [0]
+
+    def recorder(c):
+        u = torch.rand_like(c)
+        rec[calls[0] % nmb].copy_(u.reshape(-1))
+        calls[0] += 1
+        return u
+
+    alg_g._mix_uniform = recorder
+    seen = []
+    for rep in range(2):
+        alg_g.storage.step = alg.storage.step = steps
+        le = alg.update()
+        lg = alg_g.update()
+        assert all(torch.isfinite(torch.tensor(list(lg.values())))), lg
+        assert abs(le["value_function"] - lg["value_function"]) <= 0.05 * abs(le["value_function"]), (le, lg)
+        r = rec.clone()
+        assert float(r.min()) >= 0.0 and float(r.max()) < 1.0
+        assert abs(float(r.mean()) - 0.5) < 0.02
+        for i in range(nmb):
+            for j in range(i):
+                assert not torch.equal(r[i], r[j]), (rep, i, j)
+        for prev in seen:
+            assert not torch.equal(prev, r), rep
+        seen.append(r)
+    env.close()
