@@ -234,6 +234,33 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_elemt(const float* __restri
 
 int bn_scratch_doubles(long long m, int c) { return bn_blocks(m, c) * 2 * c + 2 * c; }
 
+// the running-statistics update of `uses` training-mode forwards over the same rows (F.batch_norm's, as
+// fused_bn._update_running made it with torch's ops: r = r * keep, then r + momentum * batch stat, per forward), and
+// num_batches_tracked + count: one launch instead of five per BatchNorm and forward
+__global__ void bn_running_update(float* __restrict__ rm, float* __restrict__ rv, long long* __restrict__ nbt,
+                                  const float* __restrict__ stats, int c, float keep, float momentum, int uses,
+                                  int count) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < c) {
+    const float mean = stats[j], var = stats[3 * c + j];
+    float a = rm[j], v = rv[j];
+    for (int u = 0; u < uses; ++u) {
+      a = __fmaf_rn(momentum, mean, a * keep);
+      v = __fmaf_rn(momentum, var, v * keep);
+    }
+    rm[j] = a;
+    rv[j] = v;
+  }
+  if (j == 0 && nbt) nbt[0] += count;
+}
+
+hipError_t launch_bn_running_update(float* rm, float* rv, long long* nbt, const float* stats, int c, float keep,
+                                    float momentum, int uses, int count, hipStream_t s) {
+  hipLaunchKernelGGL(bn_running_update, dim3((c + 63) / 64), dim3(64), 0, s, rm, rv, nbt, stats, c, keep, momentum,
+                     uses, count);
+  return hipGetLastError();
+}
+
 hipError_t launch_bn_forward(const float* x, long long m, int c, const float* w, const float* b, float eps, int act,
                              float slope, float* y, float* stats, double* part, hipStream_t s) {
   const int nb = bn_blocks(m, c);

@@ -935,6 +935,15 @@ int gr_bn_act_forward(const float* x, int64_t m, int32_t c, const float* w, cons
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
+int gr_bn_running_update(float* running_mean, float* running_var, int64_t* num_batches, const float* stats, int32_t c,
+                         float keep, float momentum, int32_t uses, int32_t count, void* stream) {
+  if (!running_mean || !running_var || !stats || c < 1 || c > 4096 || uses < 1 || count < 0 || (count && !num_batches))
+    return GR_ERR_ARG;
+  const hipError_t e = gr::launch_bn_running_update(running_mean, running_var, reinterpret_cast<long long*>(num_batches),
+                                                    stats, c, keep, momentum, uses, count, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
 int gr_bn_act_backward(const float* x, const float* gy, int64_t m, int32_t c, const float* w, const float* b,
                        const float* stats, int32_t act, float slope, float* gx, float* gw, float* gb, double* part,
                        void* stream) {

@@ -124,6 +124,8 @@ hipError_t launch_stem12_forward(const Stem1& s, const float* bw, const float* b
 hipError_t launch_stem12_backward(const Stem1& s, const float* bw, const float* bb, const float* stats, int act,
                                   float slope, const float* gz2, int n2, const float* w2t, float* gconv, float* gbw,
                                   float* gbb, double* part, hipStream_t st);
+hipError_t launch_bn_running_update(float* rm, float* rv, long long* nbt, const float* stats, int c, float keep,
+                                    float momentum, int uses, int count, hipStream_t s);
 hipError_t launch_bn_forward(const float* x, long long m, int c, const float* w, const float* b, float eps, int act,
                              float slope, float* y, float* stats, double* part, hipStream_t s);
 hipError_t launch_bn_backward(const float* x, const float* gy, long long m, int c, const float* w, const float* b,

@@ -78,13 +78,14 @@ def fused_applicable(bn: nn.BatchNorm2d, act: nn.Module, x: torch.Tensor) -> boo
             and bn.weight.dtype == torch.float32)
 
 
-def batch_norm_act(bn: nn.BatchNorm2d, act: nn.Module, x: torch.Tensor, uses: int = 1) -> torch.Tensor:
+def batch_norm_act(bn: nn.BatchNorm2d, act: nn.Module, x: torch.Tensor, uses: int = 1,
+                   count_first: bool = False) -> torch.Tensor:
     """act(bn(x)) for rows x [M, C] in training mode, running statistics updated as nn.BatchNorm2d does
-    (the caller has already counted the batch in num_batches_tracked and passes the momentum it implies);
+    (the caller has already counted the batch in num_batches_tracked, unless count_first);
     uses > 1: as `uses` forwards of the same rows would (_update_running)."""
     code, slope = _act_code(act)
     y, stats = _BatchNormAct.apply(x, bn.weight, bn.bias, bn.eps, code, slope)
-    _update_running(bn, stats, uses)
+    _update_running(bn, stats, uses, count_first)
     return y
 
 
@@ -219,12 +220,13 @@ def stem12_applicable(bn: nn.BatchNorm2d, act: nn.Module, img: torch.Tensor, con
 
 
 def stem12_bn_act_conv(bn: nn.BatchNorm2d, act: nn.Module, conv_w: torch.Tensor, w2: torch.Tensor, img: torch.Tensor,
-                       pix: torch.Tensor, na: int, nb: int, uses: int = 1, fused_forward: bool = True) -> torch.Tensor:
+                       pix: torch.Tensor, na: int, nb: int, uses: int = 1, fused_forward: bool = True,
+                       count_first: bool = False) -> torch.Tensor:
     """conv2's output rows [B * na / 9, 32] = patches(act(bn(conv(img)))) @ w2^T (w2 [32, 144], columns (j, c)),
     running statistics of the first BN updated as stem1_bn_act does."""
     code, slope = _act_code(act)
     z2, stats = _Stem12.apply(img, conv_w, bn.weight, bn.bias, w2, pix, na, nb, bn.eps, code, slope, fused_forward)
-    _update_running(bn, stats, uses)
+    _update_running(bn, stats, uses, count_first)
     return z2
 
 
@@ -237,22 +239,40 @@ def stem1_applicable(bn: nn.BatchNorm2d, act: nn.Module, img: torch.Tensor, conv
 
 
 def stem1_bn_act(bn: nn.BatchNorm2d, act: nn.Module, conv_w: torch.Tensor, img: torch.Tensor, pix: torch.Tensor,
-                 na: int, nb: int, uses: int = 1) -> torch.Tensor:
+                 na: int, nb: int, uses: int = 1, count_first: bool = False) -> torch.Tensor:
     """act(bn(conv(img))) as the table-a patch rows of VisionActorCritic.stem_gemm (img [B, H*W] rows; pix int16
     [(na + nb) * 9] pixel offsets; the B * nb table-b rows count in the statistics and are not returned), running
     statistics updated as nn.BatchNorm2d does (the caller counts the batch in num_batches_tracked)."""
     code, slope = _act_code(act)
     y, stats = _Stem1.apply(img, conv_w, bn.weight, bn.bias, pix, na, nb, bn.eps, code, slope)
-    _update_running(bn, stats, uses)
+    _update_running(bn, stats, uses, count_first)
     return y
 
 
-def _update_running(bn: nn.BatchNorm2d, stats: torch.Tensor, uses: int = 1):
+def _update_running(bn: nn.BatchNorm2d, stats: torch.Tensor, uses: int = 1, count_first: bool = False):
     """The running-statistics update of one training-mode forward; uses > 1 replays it as `uses` forwards of the
-    same rows would, in sequence (the first already counted by the caller, each further one counted here)."""
+    same rows would, in sequence (each forward after the first counted here in num_batches_tracked, the first too
+    with count_first, else by the caller).  With a momentum on the GPU: one launch (gr_bn_running_update)."""
+    if not bn.track_running_stats or bn.running_mean is None:
+        return
+    nbt = bn.num_batches_tracked
+    count = uses if count_first else uses - 1
+    rm, rv = bn.running_mean, bn.running_var
+    if (bn.momentum is not None and stats.is_cuda and rm.is_cuda and rm.dtype == torch.float32
+            and rv.dtype == torch.float32 and rm.is_contiguous() and rv.is_contiguous() and stats.is_contiguous()
+            and (nbt is None or nbt.dtype == torch.int64)):
+        m = float(bn.momentum)
+        # (through raw pointers, as F.batch_norm updates them inside its kernel: no version bump, so a torch
+        # batch_norm of the same forward that saved them for its backward stays valid)
+        rc = _abi.load().gr_bn_running_update(rm.data_ptr(), rv.data_ptr(), nbt.data_ptr() if nbt is not None else None,
+                                              stats.data_ptr(), rm.numel(), float(1.0 - m), m, int(uses),
+                                              int(count) if nbt is not None else 0, _stream(stats))
+        if rc != 0:
+            raise RuntimeError(f"gr_bn_running_update failed (status {rc})")
+        return
     for k in range(uses):
-        if k and bn.track_running_stats and bn.num_batches_tracked is not None:
-            bn.num_batches_tracked.add_(1)
+        if (k or count_first) and nbt is not None:
+            nbt.add_(1)
         if bn.track_running_stats and bn.running_mean is not None:
             momentum = 0.0 if bn.momentum is None else bn.momentum
             if bn.momentum is None and bn.num_batches_tracked is not None:

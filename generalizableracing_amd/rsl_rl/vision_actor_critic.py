@@ -160,10 +160,8 @@ class VisionActorCritic(ActorCritic):
 
     def _bn_act(self, bn: nn.BatchNorm2d, act: nn.Module, x: torch.Tensor) -> torch.Tensor:
         """act(bn(x)) on rows [M, C]: the fused HIP op in training mode on the GPU, else torch's ops."""
-        if self.fused_bn and fused_applicable(bn, act, x):
-            if bn.track_running_stats and bn.num_batches_tracked is not None:
-                bn.num_batches_tracked.add_(1)
-            return batch_norm_act(bn, act, x, self._bn_uses)
+        if self.fused_bn and fused_applicable(bn, act, x):  # (the batch counted with the running statistics)
+            return batch_norm_act(bn, act, x, self._bn_uses, count_first=True)
         return act(self._bn(bn, x))
 
     def _patch_index(self, device):
@@ -205,16 +203,12 @@ class VisionActorCritic(ActorCritic):
         block2 = None
         if self.fused_bn and self.fused_conv2 and n1 == 9 * n2 and stem12_applicable(bn1, act, flat, conv1.weight, conv2.weight, n1):
             # conv1 + BN1 + act + conv2: the backward forms conv2's input gradient inside the first block's passes
-            if bn1.track_running_stats and bn1.num_batches_tracked is not None:
-                bn1.num_batches_tracked.add_(1)
             z2 = stem12_bn_act_conv(bn1, act, conv1.weight, w2m, flat, pix16, n1, n1_left, self._bn_uses,
-                                    self.fused_conv2_forward)
+                                    self.fused_conv2_forward, count_first=True)
             block2 = self._bn_act(bn2, act, z2)
         elif self.fused_bn and stem1_applicable(bn1, act, flat, conv1.weight):
             # conv1 + BN1 + act from the image itself: no patch matrix, no conv output (rsl_rl/fused_bn.py)
-            if bn1.track_running_stats and bn1.num_batches_tracked is not None:
-                bn1.num_batches_tracked.add_(1)
-            y = stem1_bn_act(bn1, act, conv1.weight, flat, pix16, n1, n1_left, self._bn_uses)
+            y = stem1_bn_act(bn1, act, conv1.weight, flat, pix16, n1, n1_left, self._bn_uses, count_first=True)
         else:
             x = flat.index_select(1, idx).view(B * n1, 9)
             if n1_left:

@@ -440,6 +440,12 @@ int gr_bn_act_forward(const float* x, int64_t m, int32_t c, const float* w, cons
 int gr_bn_act_backward(const float* x, const float* gy, int64_t m, int32_t c, const float* w, const float* b,
                        const float* stats, int32_t act, float slope, float* gx, float* gw, float* gb, double* part,
                        void* stream);
+/* The running-statistics update of `uses` training-mode forwards over the same rows from a forward's stats [4][c]
+ * (nn.BatchNorm2d / F.batch_norm with a momentum, torch/nn/modules/batchnorm.py; the reference's stem BatchNorms,
+ * vision_actor_critic.py:93-105): per forward running = running * keep + momentum * batch stat (mean; unbiased
+ * variance), keep = 1 - momentum as fp32; then num_batches += count (num_batches may be NULL when count is 0). */
+int gr_bn_running_update(float* running_mean, float* running_var, int64_t* num_batches, const float* stats, int32_t c,
+                         float keep, float momentum, int32_t uses, int32_t count, void* stream);
 
 /*
  * The vision stem's first block from the depth image itself: Conv2d(1, c, 3, stride 3, no bias) -> BatchNorm2d

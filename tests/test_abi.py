@@ -181,3 +181,19 @@ def test_patch_wgrad32_rejects_shapes_it_does_not_cover():
     assert call(m=0) == -1
     assert call(x=p + 4) == -1
     assert call(gy=None) == -1
+
+
+def test_bn_running_update_rejects_bad_arguments():
+    """gr_bn_running_update: non-null running buffers and stats, 1 <= c <= 4096, uses >= 1, a batch count needs its
+    counter."""
+    lib = _abi.load()
+    p = 0x10000
+
+    def call(rm=p, nbt=p, c=16, uses=1, count=1):
+        return lib.gr_bn_running_update(rm, p, nbt, p, c, 0.9, 0.1, uses, count, None)
+
+    assert call(rm=None) == -1
+    assert call(c=0) == -1
+    assert call(uses=0) == -1
+    assert call(nbt=None) == -1
+    assert call(count=-1) == -1

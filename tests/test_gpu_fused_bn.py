@@ -115,3 +115,30 @@ def test_vision_policy_fused_vs_torch(activation, n):
     for (k, a), (_, b) in zip(pol.named_buffers(), ref.named_buffers()):
         if not a.dtype.is_floating_point:
             assert torch.equal(a, b), k
+
+
+@pytest.mark.parametrize("uses,count_first", [(1, False), (1, True), (2, True), (3, False)])
+def test_running_update_one_launch_matches_torch_sequence(uses, count_first):
+    """gr_bn_running_update (fused_bn._update_running's GPU path) against the same update as torch's in-place ops
+    (`uses` times running * (1 - momentum) + momentum * stat, num_batches_tracked counted): within one fp32 rounding
+    per step (torch's add with alpha may or may not be contracted), batch counts equal."""
+    from generalizableracing_amd.rsl_rl.fused_bn import _update_running
+
+    torch.manual_seed(uses)
+    c = 32
+    bn = nn.BatchNorm2d(c).to(DEV)
+    bn.running_mean.uniform_(-1, 1)
+    bn.running_var.uniform_(0.5, 2)
+    bn.num_batches_tracked.fill_(5)
+    stats = torch.rand(4, c, device=DEV) + 0.1
+    ref = copy.deepcopy(bn)
+    _update_running(bn, stats, uses, count_first)
+    m = ref.momentum
+    for k in range(uses):
+        if k or count_first:
+            ref.num_batches_tracked.add_(1)
+        ref.running_mean.mul_(1.0 - m).add_(stats[0], alpha=m)
+        ref.running_var.mul_(1.0 - m).add_(stats[3], alpha=m)
+    assert int(bn.num_batches_tracked) == int(ref.num_batches_tracked) == 5 + uses - (0 if count_first else 1)
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, rtol=2e-7 * uses, atol=1e-7)
+    torch.testing.assert_close(bn.running_var, ref.running_var, rtol=2e-7 * uses, atol=1e-7)
