@@ -23,11 +23,14 @@ Deviations (documented):
 """
 from __future__ import annotations
 
+import math
+
 import torch
 import torch.nn as nn
 
 from . import distributed as gdist
 from . import flat_adam as _fadam
+from . import fused_loss as _floss
 from .ppo import PPO, _GraphedStep
 from .rollout_storage_l2c2 import RolloutStorageL2C2
 
@@ -219,10 +222,35 @@ class _GraphedStepL2C2(_GraphedStep):
     def _gather(self, idx):
         return tuple(x.index_select(0, idx) for x in self._sources())
 
+    def _fused_losses_ok(self, obs) -> bool:
+        """The PPO losses as one device op each way (fused_loss._PPOLossCombinedFn, as PPO's graphed step uses them):
+        a policy with actor / critic heads and a state-independent std over <= 8 actions, fp32 outside autocast."""
+        pol = self.alg.policy
+        return (self.alg.fused_losses and obs.is_cuda and obs.dtype == torch.float32 and hasattr(pol, "features")
+                and isinstance(pol.actor, torch.nn.Sequential) and pol.actor[-1].out_features <= 8
+                and getattr(pol, "noise_std_type", None) in ("scalar", "log")
+                and not torch.is_autocast_enabled("cuda"))
+
     def _seg_a(self, idx=None):
         alg, pol = self.alg, self.alg.policy
         obs, crit, nxt, cont, act, val, adv, ret, logp, mu, sig = self._gather(self.idx if idx is None else idx)
         obs, crit, nxt = obs.float(), crit.float(), nxt.float()
+        if self._fused_losses_ok(obs):
+            # ppo_l2c2.py:127-175 with the log prob, KL, surrogate and value losses in one launch each way; the KL
+            # mean lands in the flat buffer's extra slot, the surrogate and value means accumulate in acc[:2]
+            mu_b = pol.actor(pol.features(obs))
+            value_b = pol.critic(pol.features(crit))
+            std = _floss._policy_std(pol)
+            loss, _ = _floss._PPOLossCombinedFn.apply(
+                mu_b, std, value_b, act, logp, adv, val, ret, mu, sig, float(alg.clip_param),
+                bool(alg.use_clipped_value_loss), float(alg.value_loss_coef), self.acc[:2],
+                self.flat.extra[:1] if self._adaptive() else None, None)
+            if alg.entropy_coef != 0.0:  # Normal.entropy summed over the actions: the same for every sample
+                loss = loss - alg.entropy_coef * (0.5 + 0.5 * math.log(2.0 * math.pi) + torch.log(std)).sum()
+            smooth_loss, _ = alg.smooth_loss(obs, nxt, cont, mu_b, value_b)
+            self.acc[2:].add_(smooth_loss.detach())
+            self._backward(loss + smooth_loss)
+            return
         pol.update_distribution(obs)
         logp_b = pol.get_actions_log_prob(act)
         value_b = pol.evaluate(crit)
