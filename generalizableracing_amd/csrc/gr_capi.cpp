@@ -1003,16 +1003,18 @@ int gr_stem1_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, c
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
-int64_t gr_patch_wgrad32_floats(int64_t m, int32_t k) {
-  if (m < 1 || (k != 128 && k != 144)) return GR_ERR_ARG;
-  return (int64_t)gr::patch_wgrad_blocks(m) * 32 * k;
+int64_t gr_patch_wgrad_floats(int64_t m, int32_t n, int32_t k) {
+  if (m < 1) return GR_ERR_ARG;
+  const int blocks = gr::patch_wgrad_blocks(m, n, k);
+  return blocks ? (int64_t)blocks * n * k : GR_ERR_ARG;
 }
 
-int gr_patch_wgrad32(const float* x, const float* gy, int64_t m, int32_t k, float* part, float* gw, void* stream) {
-  if (!x || !gy || !part || !gw || m < 1 || (k != 128 && k != 144) || !aligned16(x) || !aligned16(gy) ||
-      m * (int64_t)k >= ((int64_t)1 << 40))
+int gr_patch_wgrad(const float* x, int64_t ld, const float* gy, int64_t m, int32_t n, int32_t k, float* part,
+                   float* gw, void* stream) {
+  if (!x || !gy || !part || !gw || m < 1 || gr::patch_wgrad_blocks(m, n, k) == 0 || ld < k || !aligned16(gy) ||
+      ((uintptr_t)x & 3) || m * ld >= ((int64_t)1 << 40))
     return GR_ERR_ARG;
-  const hipError_t e = gr::launch_patch_wgrad32(x, gy, (long long)m, k, part, gw, (hipStream_t)stream);
+  const hipError_t e = gr::launch_patch_wgrad(x, (long long)ld, gy, (long long)m, n, k, part, gw, (hipStream_t)stream);
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 

@@ -132,9 +132,9 @@ hipError_t launch_bn_backward(const float* x, const float* gy, long long m, int 
                               const float* stats, int act, float slope, float* gx, float* gw, float* gb, double* part,
                               hipStream_t s);
 int column_sum_blocks(long long m);                                                                       // gr_update.hip
-int patch_wgrad_blocks(long long m);  // gr_update.hip: gw[32][k] = gy^T x (k = 128 or 144)
-hipError_t launch_patch_wgrad32(const float* x, const float* gy, long long m, int k, float* part, float* gw,
-                                hipStream_t s);
+int patch_wgrad_blocks(long long m, int n, int k);  // gr_update.hip: gw[n][k] = gy^T x (0: (n, k) not covered)
+hipError_t launch_patch_wgrad(const float* x, long long ld, const float* gy, long long m, int n, int k, float* part,
+                              float* gw, hipStream_t s);
 hipError_t launch_column_sum(const void* x, int dtype, long long m, int n, float* part, float* out, hipStream_t s);
 int head_partial_rows(long long m);                                                                      // gr_update.hip
 int in_partial_rows(long long m);                                                                        // gr_update.hip

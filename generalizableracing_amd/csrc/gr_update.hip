@@ -90,44 +90,56 @@ __global__ __launch_bounds__(CF_WAVES * 64) void colsum_final(const float* __res
   }
 }
 
-// ------------------------------------------------------------- weight gradient of a 32-output patch GEMM
-// gw[32][K] = gy[M][32]^T x[M][K] over millions of rows (the vision stem's conv2: x = its input patches, the first
-// block's output y1 [M][144]; hipBLASLt's split-K tiles streamed the 1.38 GB at ~3.7 TB/s).  A wave takes a run of
-// rows and holds the whole [32][K] product in MFMA accumulators (2 x K/16 tiles of v_mfma_f32_16x16x4f32): per four
-// rows (the k step), lane (i = l % 16, g = l / 16) supplies row g's gy columns 2 i, 2 i + 1 (A of tiles nt = 0, 1)
-// and x columns KT i .. KT i + KT - 1 (B of tiles kt), read as float2 / float4 loads; PW_DEPTH row quads per
-// register set, the next set's loads in flight under the current set's MFMAs.  The
-// workgroup's four wave sums are added in wave order through LDS, and pw_final sums the workgroup rows in order:
-// deterministic, no atomics.
+// ------------------------------------------------------------------ weight gradient of a tall patch GEMM
+// gw[n][K] = gy[M][n]^T x[M][K] over up to millions of rows, in slabs of N = 16 NT outputs (32 or 64): the vision
+// stem's conv2 (x = its input patches [M][144], n 32), conv3 ([M][128], n 64) and its final Linear ([M][1280],
+// n 192): hipBLASLt's split-K tiles streamed them at 1.3-3.7 TB/s.  A workgroup takes a run of rows and one slab
+// of N outputs x 16 KT columns (blockIdx.y; x rows ld floats apart, gy rows n); each wave holds its rows' whole [N][16 KT] product in MFMA accumulators
+// (NT x KT tiles of v_mfma_f32_16x16x4f32).  Per four rows (the k step) lane (i = l % 16, g = l / 16) supplies row
+// g's gy columns NT i .. NT i + NT - 1 (A of tiles nt: output row NT i + nt) and the slab's x columns KT i .. KT i +
+// KT - 1 (B of tiles kt: column KT i + kt), read as float2 / float4 loads (measured faster than float4 loads of
+// columns 64 q + 4 i, which read each 256-byte stretch whole); pw_depth row quads per register set, the next set's
+// loads in flight under the current set's MFMAs.  The workgroup's wave sums are added in wave order through LDS
+// into its row of partials [N][K], and colsum_final sums the rows in order: deterministic, no atomics.
 constexpr int PW_WAVES = 4;
-constexpr int PW_DEPTH = 2;  // (same-box A/B, r5pw6: depth 2 307 us, 3 319, 4 325; more workgroups no faster)
+// row quads per register set: 2 for 32 outputs (same-box A/B, r5pw6: depth 2 307 us, 3 319, 4 325; more workgroups
+// no faster), 1 for 64 (the accumulators take 128 registers)
+template <int NT>
+constexpr int pw_depth() { return NT == 2 ? 2 : 1; }
 typedef float pw4 __attribute__((ext_vector_type(4)));
 typedef float pw4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef float pw2u __attribute__((ext_vector_type(2), aligned(4)));
 
-template <int KT>
-__global__ __launch_bounds__(PW_WAVES * 64) void pw_partial(const float* __restrict__ x, const float* __restrict__ gy,
-                                                             long long m, long long rows_per_wave,
+// (64 outputs: two waves per SIMD, which the compiler fits in 182 registers without spilling; same-box A/B r5pwi:
+// conv3 112 -> 96 us, the Linear 189 -> 164 us; the 32-output instances are faster as they are)
+template <int NT, int KT>
+__global__ __launch_bounds__(PW_WAVES * 64) __attribute__((amdgpu_waves_per_eu(NT == 4 ? 2 : 1)))
+void pw_partial(const float* __restrict__ x, long long ld,
+                                                             const float* __restrict__ gy, long long m, int n_total,
+                                                             int k_total, long long rows_per_wave,
                                                              float* __restrict__ part) {
-  constexpr int K = 16 * KT;
-  __shared__ float red[32 * K];
+  constexpr int N = 16 * NT, KS = 16 * KT, PW_DEPTH = pw_depth<NT>();
+  __shared__ float red[N * KS];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
-  pw4 acc[2][KT];
+  const int kslabs = k_total / KS;
+  const int col0 = (blockIdx.y % kslabs) * KS, n0 = (blockIdx.y / kslabs) * N;  // this workgroup's slab
+  pw4 acc[NT][KT];
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt)
+  for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) acc[nt][kt] = pw4{0.0f, 0.0f, 0.0f, 0.0f};
   const long long r0 = ((long long)blockIdx.x * PW_WAVES + w) * rows_per_wave;
   const long long r1 = r0 + rows_per_wave < m ? r0 + rows_per_wave : m;
-  // two register sets of PW_DEPTH row quads: the next set's loads are in flight under this set's MFMAs (full sets
-  // only; the run's last, partial set is loaded with its dead rows' gy zeroed)
-  // lane i reads its KT consecutive columns KT i .. KT i + KT - 1 of x (tile kt holds column KT i + kt) and its two
-  // consecutive gy columns 2 i, 2 i + 1 (tile nt holds output row 2 i + nt): a few wide loads per row instead of one
-  // 4-byte load per tile (measured faster than float4 loads of columns 64 q + 4 i, which read each stretch whole)
-  auto load_row = [&](long long r, float (&a)[2], float (&b)[KT]) {
-    const float2 y2 = *reinterpret_cast<const float2*>(gy + r * 32 + 2 * i);
-    a[0] = y2.x;
-    a[1] = y2.y;
-    const float* xr = x + r * K + KT * i;
+  auto load_row = [&](long long r, float (&a)[NT], float (&b)[KT]) {
+    const float* yr = gy + r * n_total + n0 + NT * i;
+    if constexpr (NT == 4) {
+      const pw4u v = *reinterpret_cast<const pw4u*>(yr);
+      a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
+    } else {
+      const pw2u v = *reinterpret_cast<const pw2u*>(yr);
+      a[0] = v.x; a[1] = v.y;
+    }
+    const float* xr = x + r * ld + col0 + KT * i;
 #pragma unroll
     for (int kt = 0; kt + 4 <= KT; kt += 4) {
       const pw4u v = *reinterpret_cast<const pw4u*>(xr + kt);  // (4-byte aligned: still one dwordx4 load)
@@ -136,22 +148,24 @@ __global__ __launch_bounds__(PW_WAVES * 64) void pw_partial(const float* __restr
 #pragma unroll
     for (int kt = KT / 4 * 4; kt < KT; ++kt) b[kt] = xr[kt];
   };
-  auto load = [&](long long q, float (&a)[PW_DEPTH][2], float (&b)[PW_DEPTH][KT]) {
+  auto load = [&](long long q, float (&a)[PW_DEPTH][NT], float (&b)[PW_DEPTH][KT]) {
 #pragma unroll
     for (int d = 0; d < PW_DEPTH; ++d) load_row(q + 4 * d + g, a[d], b[d]);
   };
-  auto mma = [&](const float (&a)[PW_DEPTH][2], const float (&b)[PW_DEPTH][KT]) {
+  auto mma = [&](const float (&a)[PW_DEPTH][NT], const float (&b)[PW_DEPTH][KT]) {
 #pragma unroll
     for (int d = 0; d < PW_DEPTH; ++d)
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
+      for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
         for (int kt = 0; kt < KT; ++kt)
           acc[nt][kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[d][nt], b[d][kt], acc[nt][kt], 0, 0, 0);
   };
+  // two register sets of PW_DEPTH row quads: the next set's loads are in flight under this set's MFMAs (full sets
+  // only; the run's last, partial set is loaded with its dead rows' gy zeroed)
   constexpr int STEP = 4 * PW_DEPTH;
   const long long full = r0 + (r1 > r0 ? (r1 - r0) / STEP * STEP : 0);  // end of the full sets
-  float a0[PW_DEPTH][2], b0[PW_DEPTH][KT], a1[PW_DEPTH][2], b1[PW_DEPTH][KT];
+  float a0[PW_DEPTH][NT], b0[PW_DEPTH][KT], a1[PW_DEPTH][NT], b1[PW_DEPTH][KT];
   long long q = r0;
   if (q < full) load(q, a0, b0);
   while (q < full) {
@@ -174,47 +188,66 @@ __global__ __launch_bounds__(PW_WAVES * 64) void pw_partial(const float* __restr
       const long long r = full + 4 * d + g;
       const bool live = r < r1;
       load_row(live ? r : r0, a0[d], b0[d]);
-      a0[d][0] = live ? a0[d][0] : 0.0f;
-      a0[d][1] = live ? a0[d][1] : 0.0f;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) a0[d][nt] = live ? a0[d][nt] : 0.0f;
     }
     mma(a0, b0);
   }
-  // lane (n = i, g) holds, for tile (nt, kt), output row 2 (4 g + v) + nt (the A row 4 g + v) and column
+  // lane (n = i, g) holds, for tile (nt, kt), output row NT (4 g + v) + nt (the A row 4 g + v) and slab column
   // KT i + kt
   for (int ww = 0; ww < PW_WAVES; ++ww) {
     if (w == ww) {
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
+      for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
         for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
-            float* dst = red + (2 * (4 * g + v) + nt) * K + KT * i + kt;
+            float* dst = red + (NT * (4 * g + v) + nt) * KS + KT * i + kt;
             *dst = ww == 0 ? acc[nt][kt][v] : *dst + acc[nt][kt][v];
           }
     }
     __syncthreads();
   }
-  for (int e = threadIdx.x; e < 32 * K; e += PW_WAVES * 64) part[(size_t)blockIdx.x * 32 * K + e] = red[e];
+  // this workgroup's row of partials [n_total][k_total], its slab
+  float* prow = part + ((size_t)blockIdx.x * n_total + n0) * k_total + col0;
+  for (int e = threadIdx.x; e < N * KS; e += PW_WAVES * 64) prow[(size_t)(e / KS) * k_total + e % KS] = red[e];
 }
 
-int patch_wgrad_blocks(long long m) {
-  const long long b = (m + 4095) / 4096;  // ~1 K rows per wave
+// the column slab width for (n, k): conv2's single 144-column slab, else 128-column slabs, with n in one 32-row slab
+// or 64-row slabs (0: not covered)
+static int pw_slab(int n, int k) {
+  if (n == 32 && (k == 144 || k == 128)) return k;
+  if (n % 64 == 0 && n <= 256 && k % 128 == 0 && k <= 4096) return 128;
+  return 0;
+}
+
+int patch_wgrad_blocks(long long m, int n, int k) {
+  const int slab = pw_slab(n, k);
+  if (!slab) return 0;
+  const long long slabs = (long long)(k / slab) * (n == 32 ? 1 : n / 64);
+  // about 512 workgroups over rows x slabs, 1 024 rows per wave at most (64 at least)
+  long long rpb = (m * slabs + 511) / 512;
+  rpb = rpb < 256 ? 256 : (rpb > 4096 ? 4096 : rpb);
+  const long long b = (m + rpb - 1) / rpb;
   return (int)(b < 1 ? 1 : (b > 512 ? 512 : b));
 }
 
-hipError_t launch_patch_wgrad32(const float* x, const float* gy, long long m, int k, float* part, float* gw,
-                                hipStream_t s) {
-  const int blocks = patch_wgrad_blocks(m);
+hipError_t launch_patch_wgrad(const float* x, long long ld, const float* gy, long long m, int n, int k, float* part,
+                              float* gw, hipStream_t s) {
+  const int slab = pw_slab(n, k);
+  const int blocks = patch_wgrad_blocks(m, n, k);
+  if (!slab || !blocks) return hipErrorInvalidValue;
   long long rpw = (m + (long long)blocks * PW_WAVES - 1) / ((long long)blocks * PW_WAVES);
   rpw = (rpw + 3) & ~3LL;
-  if (k == 144)
-    hipLaunchKernelGGL(pw_partial<9>, dim3(blocks), dim3(PW_WAVES * 64), 0, s, x, gy, m, rpw, part);
-  else if (k == 128)
-    hipLaunchKernelGGL(pw_partial<8>, dim3(blocks), dim3(PW_WAVES * 64), 0, s, x, gy, m, rpw, part);
+  const dim3 grid(blocks, (k / slab) * (n == 32 ? 1 : n / 64)), wg(PW_WAVES * 64);
+  if (n == 32 && k == 144)
+    hipLaunchKernelGGL((pw_partial<2, 9>), grid, wg, 0, s, x, ld, gy, m, n, k, rpw, part);
+  else if (n == 32)
+    hipLaunchKernelGGL((pw_partial<2, 8>), grid, wg, 0, s, x, ld, gy, m, n, k, rpw, part);
   else
-    return hipErrorInvalidValue;
-  hipLaunchKernelGGL(colsum_final, dim3((32 * k + 63) / 64), dim3(CF_WAVES * 64), 0, s, part, blocks, 32 * k, gw);
+    hipLaunchKernelGGL((pw_partial<4, 8>), grid, wg, 0, s, x, ld, gy, m, n, k, rpw, part);
+  hipLaunchKernelGGL(colsum_final, dim3((n * k + 63) / 64), dim3(CF_WAVES * 64), 0, s, part, blocks, n * k, gw);
   return hipGetLastError();
 }
 

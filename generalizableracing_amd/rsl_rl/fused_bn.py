@@ -188,14 +188,10 @@ class _Stem12(torch.autograd.Function):
         nimg = img.shape[0]
         gz2 = gz2.contiguous()
         gw2 = None
-        if ctx.needs_input_grad[4]:  # conv2's weight: gz2^T y1 patches (gr_patch_wgrad32: MFMA, fixed-order sums)
-            m = y.shape[0] // 9
-            gw2 = torch.empty(32, 144, device=img.device, dtype=torch.float32)
-            wpart = torch.empty(int(lib.gr_patch_wgrad32_floats(m, 144)), device=img.device, dtype=torch.float32)
-            rc = lib.gr_patch_wgrad32(y.data_ptr(), gz2.data_ptr(), m, 144, wpart.data_ptr(), gw2.data_ptr(),
-                                      _stream(img))
-            if rc != 0:
-                raise RuntimeError(f"gr_patch_wgrad32 failed (status {rc})")
+        if ctx.needs_input_grad[4]:  # conv2's weight: gz2^T y1 patches (gr_patch_wgrad: MFMA, fixed-order sums)
+            from .linear import tall_wgrad
+
+            gw2 = tall_wgrad(gz2, y.view(y.shape[0] // 9, 144))
         # w2t[j][g][ch][s] = W2[o = 8 g + s][j * 16 + ch]
         w2t = w2d.reshape(4, 8, 9, 16).permute(2, 0, 3, 1).contiguous()
         gconv = torch.empty(16, 9, device=img.device, dtype=torch.float32)

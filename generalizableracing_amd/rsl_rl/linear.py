@@ -75,6 +75,28 @@ def split_k_wgrad(gy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     return gw
 
 
+def tall_wgrad(gy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """gy^T x [N, K] for tall fp32 CUDA gy [M, N] and x [M, K] (x's rows may be strided): gr_patch_wgrad (one MFMA
+    pass over the rows, fixed-order partial sums) when it covers (N, K), else split_k_wgrad."""
+    m, n = gy.shape
+    k = x.shape[1]
+    if gy.is_cuda and gy.dtype == torch.float32 and x.dtype == torch.float32 and x.dim() == 2 and x.stride(1) == 1:
+        from .. import _abi
+
+        lib = _abi.load()
+        floats = int(lib.gr_patch_wgrad_floats(m, n, k))
+        if floats > 0:
+            gy = gy.contiguous()
+            gw = torch.empty(n, k, device=gy.device, dtype=torch.float32)
+            part = torch.empty(floats, device=gy.device, dtype=torch.float32)
+            rc = lib.gr_patch_wgrad(x.data_ptr(), x.stride(0), gy.data_ptr(), m, n, k, part.data_ptr(), gw.data_ptr(),
+                                    _abi.raw_stream(gy.device))
+            if rc != 0:
+                raise RuntimeError(f"gr_patch_wgrad failed (status {rc})")
+            return gw
+    return split_k_wgrad(gy, x)
+
+
 class _TallLinearFn(torch.autograd.Function):
     # custom_fwd / custom_bwd: under torch.autocast (PPO's opt-in bf16 update) the forward GEMM runs in
     # the autocast dtype and the backward runs under the same autocast state; gradients return in the

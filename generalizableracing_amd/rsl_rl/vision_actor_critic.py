@@ -23,6 +23,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import linear as _lin
 from .actor_critic import ActorCritic, resolve_nn_activation
 from .fused_bn import (batch_norm_act, fused_applicable, stem1_applicable, stem1_bn_act, stem12_applicable,
                        stem12_bn_act_conv)
@@ -52,18 +53,30 @@ class _PatchGemm(torch.autograd.Function):
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
         gx = gy @ w if ctx.needs_input_grad[0] else None
-        gb = gy.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        # (the bias gradient by gr_column_sum: a fixed-order pass, and graph-safe where torch's multi-block sum is
+        # not, linear.bias_grad)
+        gb = _lin.bias_grad(gy) if ctx.has_bias and ctx.needs_input_grad[2] else None
         gw = None
         if ctx.needs_input_grad[1]:
             m, c = x.shape[0], _PatchGemm.SPLIT
             s = m // c
-            if s >= 2:
+            if gy.is_cuda and _abi_wgrad_ok(gy, x):  # gr_patch_wgrad: one MFMA pass, fixed-order sums
+                gw = _lin.tall_wgrad(gy, x)
+            elif s >= 2:
                 gw = torch.bmm(gy[: s * c].view(s, c, -1).transpose(1, 2), x[: s * c].view(s, c, -1)).sum(0)
                 if m > s * c:
                     gw = gw + gy[s * c:].t() @ x[s * c:]
             else:
                 gw = gy.t() @ x
         return gx, gw, gb
+
+
+def _abi_wgrad_ok(gy, x) -> bool:
+    """gr_patch_wgrad covers the shape (conv3: 64 x 128, the final Linear: 192 x 1280, conv2: 32 x 144)."""
+    from .. import _abi
+
+    return (gy.dtype == torch.float32 and x.dtype == torch.float32 and x.stride(-1) == 1
+            and int(_abi.load().gr_patch_wgrad_floats(x.shape[0], gy.shape[1], x.shape[1])) > 0)
 
 
 def _gemm(x, w, b=None):

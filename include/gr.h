@@ -467,11 +467,15 @@ int gr_stem1_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, c
                       int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b,
                       const float* stats, int32_t act, float slope, const float* gy, int64_t gy_rows, float* g_conv_w,
                       float* g_bn_w, float* g_bn_b, double* part, void* stream);
-/* Weight gradient of a 32-output patch GEMM: gw[32][k] = gy[m][32]^T x[m][k] (k = 128 or 144; fp32, row-major,
- * 16-byte aligned), the vision stem's conv2 weight gradient (x = its input patches).  Deterministic (fixed-order
- * sums, no atomics).  `part`: a workspace of gr_patch_wgrad32_floats(m, k) floats. */
-int64_t gr_patch_wgrad32_floats(int64_t m, int32_t k);
-int gr_patch_wgrad32(const float* x, const float* gy, int64_t m, int32_t k, float* part, float* gw, void* stream);
+/* Weight gradient of a tall patch GEMM: gw[n][k] = gy[m][n]^T x[m][k] (fp32; gy row-major, 16-byte aligned; x rows
+ * `ld` floats apart, 4-byte aligned), the vision stem's conv2 (n 32, k 144), conv3 (n 64, k 128) and final Linear
+ * (n 192, k 1280) weight gradients (standalone/rsl_rl/ext/modules/vision_actor_critic.py:93-105; torch's
+ * Conv2d / Linear backward).  Covered: n 32 with k 128 or 144; n a multiple of 64 up to 256 with k a multiple of
+ * 128 up to 4096.
+ * Deterministic (fixed-order sums, no atomics).  `part`: a workspace of gr_patch_wgrad_floats(m, n, k) floats. */
+int64_t gr_patch_wgrad_floats(int64_t m, int32_t n, int32_t k);
+int gr_patch_wgrad(const float* x, int64_t ld, const float* gy, int64_t m, int32_t n, int32_t k, float* part,
+                   float* gw, void* stream);
 /* The first block's forward with the stem's conv2, Conv2d(c = 16, 32, 3, stride 3, no bias), fused into its apply
  * pass: y [nimg * na][16] as gr_stem1_forward stores it (y_rows = nimg * na: the table-a rows) and conv2's output
  * z2 [nimg * n2][32] (na = 9 n2; row 9 p + j of an image = position j of patch p).  w2f: conv2's weight as

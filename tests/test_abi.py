@@ -166,20 +166,28 @@ def test_stem12_forward_rejects_shapes_it_does_not_cover():
     assert call(act=5) == -1
 
 
-def test_patch_wgrad32_rejects_shapes_it_does_not_cover():
-    """gr_patch_wgrad32 (conv2's weight gradient): k of 128 or 144 columns, 16-byte aligned x and gy, m >= 1."""
+def test_patch_wgrad_rejects_shapes_it_does_not_cover():
+    """gr_patch_wgrad (the stem's conv2 / conv3 / Linear weight gradients): n 32 with k 128 or 144, n a multiple of
+    64 up to 256 with k a multiple of 128 up to 4096; ld >= k; 16-byte aligned gy, 4-byte aligned x; m >= 1."""
     lib = _abi.load()
     p = 0x10000
-    assert lib.gr_patch_wgrad32_floats(4096, 144) == 32 * 144
-    assert lib.gr_patch_wgrad32_floats(1, 100) == -1
-    assert lib.gr_patch_wgrad32_floats(0, 144) == -1
+    assert lib.gr_patch_wgrad_floats(4096, 32, 144) > 0
+    assert lib.gr_patch_wgrad_floats(491520, 64, 128) > 0
+    assert lib.gr_patch_wgrad_floats(24576, 192, 1280) > 0
+    assert lib.gr_patch_wgrad_floats(24576, 96, 128) == -1
+    assert lib.gr_patch_wgrad_floats(1, 32, 100) == -1
+    assert lib.gr_patch_wgrad_floats(100, 64, 144) == -1
+    assert lib.gr_patch_wgrad_floats(0, 32, 144) == -1
 
-    def call(x=p, gy=p, m=100, k=144):
-        return lib.gr_patch_wgrad32(x, gy, m, k, p, p, None)
+    def call(x=p, ld=144, gy=p, m=100, n=32, k=144):
+        return lib.gr_patch_wgrad(x, ld, gy, m, n, k, p, p, None)
 
     assert call(k=64) == -1
+    assert call(n=48) == -1
     assert call(m=0) == -1
-    assert call(x=p + 4) == -1
+    assert call(ld=100) == -1
+    assert call(x=p + 2) == -1
+    assert call(gy=p + 4) == -1
     assert call(gy=None) == -1
 
 

@@ -119,23 +119,27 @@ def test_stem12_is_the_path_taken():
     assert any("_Stem12" in type(n).__name__ for n in names)
 
 
-@pytest.mark.parametrize("m,k", [(1, 144), (7, 128), (4099, 144), (1_966_080, 144), (491_527, 128)])
-def test_patch_wgrad32_matches_float64(m, k):
-    """gr_patch_wgrad32 (gw[32][k] = gy^T x, conv2's weight gradient) against float64 at ragged and full sizes
-    (1 966 080 rows = conv2's patches of a 24 576-image mini-batch); repeats bit-identical."""
+@pytest.mark.parametrize("m,n,k,ld", [(1, 32, 144, 144), (7, 32, 128, 128), (4099, 32, 144, 144),
+                                      (1_966_080, 32, 144, 144), (491_527, 32, 128, 128), (491_520, 64, 128, 128),
+                                      (24_576, 192, 1280, 1280), (3001, 128, 256, 300), (5, 64, 128, 131)])
+def test_patch_wgrad_matches_float64(m, n, k, ld):
+    """gr_patch_wgrad (gw[n][k] = gy^T x: the stem's conv2, conv3 and final Linear weight gradients) against float64
+    at ragged and full sizes (1 966 080 rows = conv2's patches of a 24 576-image mini-batch, 491 520 conv3's,
+    24 576 the Linear's 1 280 columns into 192 outputs), strided x rows; repeats bit-identical."""
     from generalizableracing_amd import _abi
     import ctypes as C
 
     lib = _abi.load()
-    g = torch.Generator(device=DEV).manual_seed(m % 1000 + k)
-    x = torch.rand(m, k, device=DEV, generator=g) * 2.0
-    gy = torch.randn(m, 32, device=DEV, generator=g)
-    part = torch.empty(int(lib.gr_patch_wgrad32_floats(m, k)), device=DEV)
-    out = torch.empty(32, k, device=DEV)
+    g = torch.Generator(device=DEV).manual_seed(m % 1000 + k + n)
+    xs = torch.rand(m, ld, device=DEV, generator=g) * 2.0
+    x = xs[:, :k]
+    gy = torch.randn(m, n, device=DEV, generator=g)
+    part = torch.empty(int(lib.gr_patch_wgrad_floats(m, n, k)), device=DEV)
+    out = torch.empty(n, k, device=DEV)
 
     def run():
-        rc = lib.gr_patch_wgrad32(x.data_ptr(), gy.data_ptr(), m, k, part.data_ptr(), out.data_ptr(),
-                                  C.c_void_p(_abi.raw_stream(x.device)))
+        rc = lib.gr_patch_wgrad(x.data_ptr(), ld, gy.data_ptr(), m, n, k, part.data_ptr(), out.data_ptr(),
+                                C.c_void_p(_abi.raw_stream(x.device)))
         assert rc == 0
         torch.cuda.synchronize()
         return out.clone()
