@@ -1003,6 +1003,17 @@ int gr_stem1_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, c
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
+int gr_tsgemm(const float* a, int64_t lda, const float* b, int32_t b_nk, float* c, int64_t ldc, int64_t m, int32_t k,
+              int32_t n, void* stream) {
+  if (!a || !b || !c || m < 0 || !gr::tsgemm_covered(k, n, b_nk != 0) || lda < k || ldc < n || ((uintptr_t)a & 3) ||
+      m * (lda > ldc ? lda : ldc) >= ((int64_t)1 << 40))
+    return GR_ERR_ARG;
+  if (m == 0) return GR_OK;
+  const hipError_t e = gr::launch_tsgemm(a, (long long)lda, b, b_nk != 0, c, (long long)ldc, (long long)m, k, n,
+                                         (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
 int64_t gr_patch_wgrad_floats(int64_t m, int32_t n, int32_t k) {
   if (m < 1) return GR_ERR_ARG;
   const int blocks = gr::patch_wgrad_blocks(m, n, k);

@@ -251,6 +251,95 @@ hipError_t launch_patch_wgrad(const float* x, long long ld, const float* gy, lon
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------- tall-skinny patch GEMM, forward / dgrad
+// C[M][N] = A[M][K] B[K][N] for millions of rows and a small B (K x N <= 128 x 128): the vision stem's conv3 forward
+// (A = its 2 x 2 patches [M][128], B = W3^T, N 64) and its input gradient (A = gz3 [M][64], B = W3, N 128), where
+// hipBLASLt ran at 1.5-2.4 TB/s.  B lives in registers for the whole kernel: a wave's lane (n = l % 16, g = l / 16)
+// holds B[k(s, g)][16 nt + n] for every k step s and output tile nt (K / 4 x N / 16 values), so the rows stream with
+// no LDS.  The k order is permuted so that A is read as float4: k(s, g) = 16 (s / 4) + 4 g + s % 4, lane (i, g)
+// taking A[row i][16 q + 4 g .. + 3] for the four steps of quad q.  A wave walks 16-row tiles strided by the grid,
+// the next tile's A loaded under the current tile's MFMAs; lane (n, g) stores C[4 g + v][16 nt + n].  Each output is
+// one fixed-order fp32 MFMA chain over k: deterministic.
+typedef float ts4u __attribute__((ext_vector_type(4), aligned(4)));
+constexpr int TS_WAVES = 4;
+
+template <int K, int N, bool B_NK>
+__global__ __launch_bounds__(TS_WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
+void tsgemm_kernel(const float* __restrict__ a, long long lda, const float* __restrict__ bm,
+                   float* __restrict__ c, long long ldc, long long m) {
+  constexpr int S = K / 4, NT = N / 16, Q = K / 16;
+  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  float b[S][NT];
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int k = 16 * (s / 4) + 4 * g + (s % 4), n = 16 * nt + i;
+      b[s][nt] = B_NK ? bm[(size_t)n * K + k] : bm[(size_t)k * N + n];  // B_NK: bm is W [N][K] (B = W^T)
+    }
+  const long long tiles = (m + 15) / 16;
+  const long long wave = (long long)blockIdx.x * TS_WAVES + (threadIdx.x >> 6);
+  const long long stride = (long long)gridDim.x * TS_WAVES;
+  auto load = [&](long long t, float (&av)[S]) {
+    long long r = 16 * t + i;
+    r = r < m ? r : m - 1;  // (rows past the end read the last row; their outputs are not stored)
+    const float* ar = a + r * lda + 4 * g;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const ts4u v = *reinterpret_cast<const ts4u*>(ar + 16 * q);
+      av[4 * q] = v.x; av[4 * q + 1] = v.y; av[4 * q + 2] = v.z; av[4 * q + 3] = v.w;
+    }
+  };
+  auto tile = [&](long long t, const float (&av)[S]) {
+    pw4 acc[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[nt] = pw4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], b[s][nt], acc[nt], 0, 0, 0);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const long long r = 16 * t + 4 * g + v;
+      if (r < m) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) c[r * ldc + 16 * nt + i] = acc[nt][v];
+      }
+    }
+  };
+  // two register sets, the next tile's loads issued ahead of this tile's MFMAs (no copies between the sets)
+  float a0[S], a1[S];
+  long long t = wave;
+  if (t < tiles) load(t, a0);
+  while (t < tiles) {
+    const long long t1 = t + stride;
+    if (t1 < tiles) load(t1, a1);
+    __builtin_amdgcn_sched_barrier(0);
+    tile(t, a0);
+    if (t1 >= tiles) break;
+    const long long t2 = t1 + stride;
+    if (t2 < tiles) load(t2, a0);
+    __builtin_amdgcn_sched_barrier(0);
+    tile(t1, a1);
+    t = t2;
+  }
+}
+
+bool tsgemm_covered(int k, int n, bool b_nk) { return (k == 128 && n == 64 && b_nk) || (k == 64 && n == 128 && !b_nk); }
+
+hipError_t launch_tsgemm(const float* a, long long lda, const float* bm, bool b_nk, float* c, long long ldc,
+                         long long m, int k, int n, hipStream_t s) {
+  if (!tsgemm_covered(k, n, b_nk)) return hipErrorInvalidValue;
+  const long long tiles = (m + 15) / 16;
+  long long blocks = (tiles + TS_WAVES - 1) / TS_WAVES;
+  blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);  // 256 CUs x 2 waves per SIMD, walked in strides
+  if (k == 128)
+    hipLaunchKernelGGL((tsgemm_kernel<128, 64, true>), dim3(blocks), dim3(TS_WAVES * 64), 0, s, a, lda, bm, c, ldc, m);
+  else
+    hipLaunchKernelGGL((tsgemm_kernel<64, 128, false>), dim3(blocks), dim3(TS_WAVES * 64), 0, s, a, lda, bm, c, ldc, m);
+  return hipGetLastError();
+}
+
 int column_sum_blocks(long long m) {
   long long b = (m + 255) / 256;
   return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));

@@ -47,12 +47,18 @@ class _PatchGemm(torch.autograd.Function):
     def forward(ctx, x, w, b=None):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
-        return x @ w.t() if b is None else torch.addmm(b, x, w.t())  # (the bias in the GEMM's epilogue)
+        if b is None:
+            y = _tsgemm(x, w, True)
+            return y if y is not None else x @ w.t()
+        return torch.addmm(b, x, w.t())  # (the bias in the GEMM's epilogue)
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
-        gx = gy @ w if ctx.needs_input_grad[0] else None
+        gx = None
+        if ctx.needs_input_grad[0]:
+            gx = _tsgemm(gy, w, False)
+            gx = gx if gx is not None else gy @ w
         # (the bias gradient by gr_column_sum: a fixed-order pass, and graph-safe where torch's multi-block sum is
         # not, linear.bias_grad)
         gb = _lin.bias_grad(gy) if ctx.has_bias and ctx.needs_input_grad[2] else None
@@ -71,6 +77,26 @@ class _PatchGemm(torch.autograd.Function):
         return gx, gw, gb
 
 
+def _tsgemm(a, w, b_nk: bool):
+    """a @ w^T (b_nk) or a @ w on gr_tsgemm (the weight in registers, the rows streamed once) when it covers the shape
+    (conv3: [M, 128] x [64, 128]^T and [M, 64] x [64, 128]), else None."""
+    if not (a.is_cuda and a.dtype == torch.float32 and w.dtype == torch.float32 and a.dim() == 2 and a.stride(1) == 1):
+        return None
+    from .. import _abi
+
+    k = a.shape[1]
+    n = w.shape[0] if b_nk else w.shape[1]
+    if not ((k == 128 and n == 64 and b_nk) or (k == 64 and n == 128 and not b_nk)):
+        return None
+    w = w.contiguous()
+    out = torch.empty(a.shape[0], n, device=a.device, dtype=torch.float32)
+    rc = _abi.load().gr_tsgemm(a.data_ptr(), a.stride(0), w.data_ptr(), int(b_nk), out.data_ptr(), n, a.shape[0], k,
+                               n, _abi.raw_stream(a.device))
+    if rc != 0:
+        raise RuntimeError(f"gr_tsgemm failed (status {rc})")
+    return out
+
+
 def _abi_wgrad_ok(gy, x) -> bool:
     """gr_patch_wgrad covers the shape (conv3: 64 x 128, the final Linear: 192 x 1280, conv2: 32 x 144)."""
     from .. import _abi
@@ -80,10 +106,14 @@ def _abi_wgrad_ok(gy, x) -> bool:
 
 
 def _gemm(x, w, b=None):
-    """x @ w^T (+ b): the split-K weight gradient with autograd on, else one GEMM (bias in its epilogue)."""
+    """x @ w^T (+ b): _PatchGemm with autograd on, else one GEMM (gr_tsgemm where it covers the shape; the bias in
+    the GEMM's epilogue)."""
     if torch.is_grad_enabled():
         return _PatchGemm.apply(x, w, b)
-    return x @ w.t() if b is None else torch.addmm(b, x, w.t())
+    if b is None:
+        y = _tsgemm(x, w, True)
+        return y if y is not None else x @ w.t()
+    return torch.addmm(b, x, w.t())
 
 
 class VisionActorCritic(ActorCritic):

@@ -467,6 +467,13 @@ int gr_stem1_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, c
                       int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b,
                       const float* stats, int32_t act, float slope, const float* gy, int64_t gy_rows, float* g_conv_w,
                       float* g_bn_w, float* g_bn_b, double* part, void* stream);
+/* Tall-skinny patch GEMM: C[m][n] = A[m][k] B[k][n] (fp32; A rows `lda` floats apart, 4-byte aligned; C rows `ldc`
+ * apart), B small and held in registers: with b_nk B = b^T for b [n][k] (a Conv2d / Linear forward, x W^T), else B = b
+ * [k][n] (its input gradient, gy W).  The vision stem's conv3 forward (k 128, n 64, b_nk) and input gradient (k 64,
+ * n 128) (standalone/rsl_rl/ext/modules/vision_actor_critic.py:93-105 as patch GEMMs).  Each output one fixed-order
+ * fp32 MFMA chain over k. */
+int gr_tsgemm(const float* a, int64_t lda, const float* b, int32_t b_nk, float* c, int64_t ldc, int64_t m, int32_t k,
+              int32_t n, void* stream);
 /* Weight gradient of a tall patch GEMM: gw[n][k] = gy[m][n]^T x[m][k] (fp32; gy row-major, 16-byte aligned; x rows
  * `ld` floats apart, 4-byte aligned), the vision stem's conv2 (n 32, k 144), conv3 (n 64, k 128) and final Linear
  * (n 192, k 1280) weight gradients (standalone/rsl_rl/ext/modules/vision_actor_critic.py:93-105; torch's

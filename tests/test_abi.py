@@ -205,3 +205,21 @@ def test_bn_running_update_rejects_bad_arguments():
     assert call(uses=0) == -1
     assert call(nbt=None) == -1
     assert call(count=-1) == -1
+
+
+def test_tsgemm_rejects_shapes_it_does_not_cover():
+    """gr_tsgemm: (k 128, n 64, b as [n][k]) or (k 64, n 128, b as [k][n]); lda >= k, ldc >= n; 4-byte aligned A."""
+    lib = _abi.load()
+    p = 0x10000
+
+    def call(a=p, lda=128, b_nk=1, ldc=64, m=100, k=128, n=64):
+        return lib.gr_tsgemm(a, lda, p, b_nk, p, ldc, m, k, n, None)
+
+    assert call(m=0) == 0
+    assert call(b_nk=0) == -1
+    assert call(k=64, n=128, lda=64, ldc=128) == -1
+    assert call(n=32) == -1
+    assert call(lda=100) == -1
+    assert call(ldc=32) == -1
+    assert call(a=p + 2) == -1
+    assert call(a=None) == -1

@@ -148,3 +148,31 @@ def test_patch_wgrad_matches_float64(m, n, k, ld):
     want = (gy.double().t() @ x.double()).cpu()
     assert _rel(o1, want) <= 1e-5, _rel(o1, want)
     assert torch.equal(o1, run())
+
+
+@pytest.mark.parametrize("m,k,n,b_nk,lda", [(491_520, 128, 64, True, 128), (491_520, 64, 128, False, 64),
+                                            (1, 128, 64, True, 128), (37, 64, 128, False, 70), (4099, 128, 64, True, 131)])
+def test_tsgemm_matches_float64(m, k, n, b_nk, lda):
+    """gr_tsgemm (conv3's forward x W^T and input gradient gy W as patch GEMMs, the weight in registers) against
+    float64 at full (491 520 rows = conv3's patches of a 24 576-image mini-batch) and ragged sizes, strided rows;
+    repeats bit-identical."""
+    from generalizableracing_amd import _abi
+    import ctypes as C
+
+    lib = _abi.load()
+    g = torch.Generator(device=DEV).manual_seed(m % 997 + k)
+    a = (torch.rand(m, lda, device=DEV, generator=g) * 2.0 - 0.5)[:, :k]
+    w = torch.randn(n, k, device=DEV, generator=g) if b_nk else torch.randn(k, n, device=DEV, generator=g)
+    out = torch.empty(m, n, device=DEV)
+
+    def run():
+        rc = lib.gr_tsgemm(a.data_ptr(), lda, w.data_ptr(), int(b_nk), out.data_ptr(), n, m, k, n,
+                           C.c_void_p(_abi.raw_stream(a.device)))
+        assert rc == 0
+        torch.cuda.synchronize()
+        return out.clone()
+
+    o1 = run()
+    want = (a.double() @ (w.double().t() if b_nk else w.double())).cpu()
+    assert _rel(o1, want) <= 1e-5, _rel(o1, want)
+    assert torch.equal(o1, run())
