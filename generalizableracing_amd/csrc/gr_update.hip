@@ -254,29 +254,28 @@ hipError_t launch_patch_wgrad(const float* x, long long ld, const float* gy, lon
 // ------------------------------------------------------------------- tall-skinny patch GEMM, forward / dgrad
 // C[M][N] = A[M][K] B[K][N] for millions of rows and a small B (K x N <= 128 x 128): the vision stem's conv3 forward
 // (A = its 2 x 2 patches [M][128], B = W3^T, N 64) and its input gradient (A = gz3 [M][64], B = W3, N 128), where
-// hipBLASLt ran at 1.5-2.4 TB/s.  B lives in registers for the whole kernel: a wave's lane (n = l % 16, g = l / 16)
-// holds B[k(s, g)][16 nt + n] for every k step s and output tile nt (K / 4 x N / 16 values), so the rows stream with
-// no LDS.  The k order is permuted so that A is read as float4: k(s, g) = 16 (s / 4) + 4 g + s % 4, lane (i, g)
-// taking A[row i][16 q + 4 g .. + 3] for the four steps of quad q.  A wave walks 16-row tiles strided by the grid,
-// the next tile's A loaded under the current tile's MFMAs; lane (n, g) stores C[4 g + v][16 nt + n].  Each output is
-// one fixed-order fp32 MFMA chain over k: deterministic.
+// hipBLASLt ran at 1.5-2.4 TB/s.  The workgroup stages B once in LDS, transposed (Bt[n][k], rows padded by 4 floats);
+// the k order is permuted so that both operands are read four steps at a time: k(s, g) = 16 (s / 4) + 4 g + s % 4,
+// lane (i = l % 16, g = l / 16) taking A[row i][16 q + 4 g .. + 3] (a float4 from global) and Bt[16 nt + i][16 q +
+// 4 g .. + 3] (a 16-byte LDS read) for the four steps of quad q.  A wave walks 16-row tiles strided by the grid, the
+// next tile's A loaded under the current tile's MFMAs; lane (n, g) stores C[4 g + v][16 nt + n].  Each output is one
+// fixed-order fp32 MFMA chain over k: deterministic.  (Same-box A/B, r5ts2, 24 576 images: forward 124 -> 92 us,
+// input gradient 125 -> 109 us against B held in registers, 128 of them, two waves per SIMD; 172 / 157 us hipBLASLt.)
 typedef float ts4u __attribute__((ext_vector_type(4), aligned(4)));
 constexpr int TS_WAVES = 4;
 
 template <int K, int N, bool B_NK>
-__global__ __launch_bounds__(TS_WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
-void tsgemm_kernel(const float* __restrict__ a, long long lda, const float* __restrict__ bm,
-                   float* __restrict__ c, long long ldc, long long m) {
-  constexpr int S = K / 4, NT = N / 16, Q = K / 16;
+__global__ __launch_bounds__(TS_WAVES * 64) void tsgemm_kernel(const float* __restrict__ a, long long lda,
+                                                               const float* __restrict__ bm, float* __restrict__ c,
+                                                               long long ldc, long long m) {
+  constexpr int S = K / 4, NT = N / 16, Q = K / 16, LDK = K + 4;
+  __shared__ float bt[N * LDK];
+  for (int e = threadIdx.x; e < N * K; e += TS_WAVES * 64) {
+    const int n = e / K, k = e % K;
+    bt[n * LDK + k] = B_NK ? bm[e] : bm[(size_t)k * N + n];  // B_NK: bm is W [N][K] (B = W^T)
+  }
+  __syncthreads();
   const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
-  float b[S][NT];
-#pragma unroll
-  for (int s = 0; s < S; ++s)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const int k = 16 * (s / 4) + 4 * g + (s % 4), n = 16 * nt + i;
-      b[s][nt] = B_NK ? bm[(size_t)n * K + k] : bm[(size_t)k * N + n];  // B_NK: bm is W [N][K] (B = W^T)
-    }
   const long long tiles = (m + 15) / 16;
   const long long wave = (long long)blockIdx.x * TS_WAVES + (threadIdx.x >> 6);
   const long long stride = (long long)gridDim.x * TS_WAVES;
@@ -295,9 +294,16 @@ void tsgemm_kernel(const float* __restrict__ a, long long lda, const float* __re
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[nt] = pw4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int s = 0; s < S; ++s)
+    for (int q = 0; q < Q; ++q) {
+      pw4 bq[NT];
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], b[s][nt], acc[nt], 0, 0, 0);
+      for (int nt = 0; nt < NT; ++nt) bq[nt] = *reinterpret_cast<const pw4*>(bt + (16 * nt + i) * LDK + 16 * q + 4 * g);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[4 * q + e], bq[nt][e], acc[nt], 0, 0, 0);
+    }
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const long long r = 16 * t + 4 * g + v;
@@ -332,7 +338,7 @@ hipError_t launch_tsgemm(const float* a, long long lda, const float* bm, bool b_
   if (!tsgemm_covered(k, n, b_nk)) return hipErrorInvalidValue;
   const long long tiles = (m + 15) / 16;
   long long blocks = (tiles + TS_WAVES - 1) / TS_WAVES;
-  blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);  // 256 CUs x 2 waves per SIMD, walked in strides
+  blocks = blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks);  // 256 CUs x 4 workgroups, walked in strides
   if (k == 128)
     hipLaunchKernelGGL((tsgemm_kernel<128, 64, true>), dim3(blocks), dim3(TS_WAVES * 64), 0, s, a, lda, bm, c, ldc, m);
   else
