@@ -252,9 +252,9 @@ hipError_t launch_patch_wgrad(const float* x, long long ld, const float* gy, lon
 }
 
 // ------------------------------------------------------------------- tall-skinny patch GEMM, forward / dgrad
-// C[M][N] = A[M][K] B[K][N] for millions of rows and a small B (K x N <= 128 x 128): the vision stem's conv3 forward
-// (A = its 2 x 2 patches [M][128], B = W3^T, N 64) and its input gradient (A = gz3 [M][64], B = W3, N 128), where
-// hipBLASLt ran at 1.5-2.4 TB/s.  The workgroup stages B once in LDS, transposed (Bt[n][k], rows padded by 4 floats);
+// C[M][N] = A[M][K] B[K][N] for tall A and a small B: the vision stem's conv3 forward (A = its 2 x 2 patches [M][128],
+// B = W3^T, N 64), its input gradient (A = gz3 [M][64], B = W3, N 128) and the final Linear's input gradient (A = gy
+// [M][192], B = W [192][1280], in 64-output slabs, blockIdx.y), where hipBLASLt ran at 0.8-2.4 TB/s.  The workgroup stages B once in LDS, transposed (Bt[n][k], rows padded by 4 floats);
 // the k order is permuted so that both operands are read four steps at a time: k(s, g) = 16 (s / 4) + 4 g + s % 4,
 // lane (i = l % 16, g = l / 16) taking A[row i][16 q + 4 g .. + 3] (a float4 from global) and Bt[16 nt + i][16 q +
 // 4 g .. + 3] (a 16-byte LDS read) for the four steps of quad q.  A wave walks 16-row tiles strided by the grid, the
@@ -266,13 +266,16 @@ constexpr int TS_WAVES = 4;
 
 template <int K, int N, bool B_NK>
 __global__ __launch_bounds__(TS_WAVES * 64) void tsgemm_kernel(const float* __restrict__ a, long long lda,
-                                                               const float* __restrict__ bm, float* __restrict__ c,
-                                                               long long ldc, long long m) {
+                                                               const float* __restrict__ bm, int n_total,
+                                                               float* __restrict__ c, long long ldc, long long m) {
+  // N: this workgroup's slab of the n_total outputs (blockIdx.y)
   constexpr int S = K / 4, NT = N / 16, Q = K / 16, LDK = K + 4;
   __shared__ float bt[N * LDK];
+  const int n0 = blockIdx.y * N;
   for (int e = threadIdx.x; e < N * K; e += TS_WAVES * 64) {
     const int n = e / K, k = e % K;
-    bt[n * LDK + k] = B_NK ? bm[e] : bm[(size_t)k * N + n];  // B_NK: bm is W [N][K] (B = W^T)
+    // B_NK: bm is W [n_total][K] (B = W^T), else B [K][n_total]
+    bt[n * LDK + k] = B_NK ? bm[(size_t)(n0 + n) * K + k] : bm[(size_t)k * n_total + n0 + n];
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
@@ -309,7 +312,7 @@ __global__ __launch_bounds__(TS_WAVES * 64) void tsgemm_kernel(const float* __re
       const long long r = 16 * t + 4 * g + v;
       if (r < m) {
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) c[r * ldc + 16 * nt + i] = acc[nt][v];
+        for (int nt = 0; nt < NT; ++nt) c[r * ldc + n0 + 16 * nt + i] = acc[nt][v];
       }
     }
   };
@@ -331,7 +334,10 @@ __global__ __launch_bounds__(TS_WAVES * 64) void tsgemm_kernel(const float* __re
   }
 }
 
-bool tsgemm_covered(int k, int n, bool b_nk) { return (k == 128 && n == 64 && b_nk) || (k == 64 && n == 128 && !b_nk); }
+bool tsgemm_covered(int k, int n, bool b_nk) {
+  return (k == 128 && n == 64 && b_nk) || (k == 64 && n == 128 && !b_nk) ||
+         (k == 192 && !b_nk && n % 64 == 0 && n <= 4096);  // (the last in 64-output slabs: the final Linear's dgrad)
+}
 
 hipError_t launch_tsgemm(const float* a, long long lda, const float* bm, bool b_nk, float* c, long long ldc,
                          long long m, int k, int n, hipStream_t s) {
@@ -339,10 +345,17 @@ hipError_t launch_tsgemm(const float* a, long long lda, const float* bm, bool b_
   const long long tiles = (m + 15) / 16;
   long long blocks = (tiles + TS_WAVES - 1) / TS_WAVES;
   blocks = blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks);  // 256 CUs x 4 workgroups, walked in strides
+  const dim3 wg(TS_WAVES * 64);
   if (k == 128)
-    hipLaunchKernelGGL((tsgemm_kernel<128, 64, true>), dim3(blocks), dim3(TS_WAVES * 64), 0, s, a, lda, bm, c, ldc, m);
-  else
-    hipLaunchKernelGGL((tsgemm_kernel<64, 128, false>), dim3(blocks), dim3(TS_WAVES * 64), 0, s, a, lda, bm, c, ldc, m);
+    hipLaunchKernelGGL((tsgemm_kernel<128, 64, true>), dim3(blocks), wg, 0, s, a, lda, bm, n, c, ldc, m);
+  else if (k == 64)
+    hipLaunchKernelGGL((tsgemm_kernel<64, 128, false>), dim3(blocks), wg, 0, s, a, lda, bm, n, c, ldc, m);
+  else {  // 64-output slabs: about 1 024 workgroups over rows x slabs
+    const long long slabs = n / 64;
+    long long rb = (1024 + slabs - 1) / slabs;
+    rb = rb < blocks ? rb : blocks;
+    hipLaunchKernelGGL((tsgemm_kernel<192, 64, false>), dim3(rb, slabs), wg, 0, s, a, lda, bm, n, c, ldc, m);
+  }
   return hipGetLastError();
 }
 

@@ -78,15 +78,17 @@ class _PatchGemm(torch.autograd.Function):
 
 
 def _tsgemm(a, w, b_nk: bool):
-    """a @ w^T (b_nk) or a @ w on gr_tsgemm (the weight in registers, the rows streamed once) when it covers the shape
-    (conv3: [M, 128] x [64, 128]^T and [M, 64] x [64, 128]), else None."""
+    """a @ w^T (b_nk) or a @ w on gr_tsgemm (the weight staged in LDS, the rows streamed once) when it covers the shape
+    (conv3: [M, 128] x [64, 128]^T and [M, 64] x [64, 128]; the final Linear's input gradient [M, 192] x [192, 1280]),
+    else None."""
     if not (a.is_cuda and a.dtype == torch.float32 and w.dtype == torch.float32 and a.dim() == 2 and a.stride(1) == 1):
         return None
     from .. import _abi
 
     k = a.shape[1]
     n = w.shape[0] if b_nk else w.shape[1]
-    if not ((k == 128 and n == 64 and b_nk) or (k == 64 and n == 128 and not b_nk)):
+    if not ((k == 128 and n == 64 and b_nk) or (k == 64 and n == 128 and not b_nk)
+            or (k == 192 and not b_nk and n % 64 == 0 and n <= 4096)):
         return None
     w = w.contiguous()
     out = torch.empty(a.shape[0], n, device=a.device, dtype=torch.float32)

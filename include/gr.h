@@ -469,8 +469,9 @@ int gr_stem1_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, c
                       float* g_bn_w, float* g_bn_b, double* part, void* stream);
 /* Tall-skinny patch GEMM: C[m][n] = A[m][k] B[k][n] (fp32; A rows `lda` floats apart, 4-byte aligned; C rows `ldc`
  * apart), B small and held in registers: with b_nk B = b^T for b [n][k] (a Conv2d / Linear forward, x W^T), else B = b
- * [k][n] (its input gradient, gy W).  The vision stem's conv3 forward (k 128, n 64, b_nk) and input gradient (k 64,
- * n 128) (standalone/rsl_rl/ext/modules/vision_actor_critic.py:93-105 as patch GEMMs).  Each output one fixed-order
+ * [k][n] (its input gradient, gy W).  The vision stem's conv3 forward (k 128, n 64, b_nk), its input gradient (k 64,
+ * n 128) and the final Linear's input gradient (k 192, n a multiple of 64 up to 4096)
+ * (standalone/rsl_rl/ext/modules/vision_actor_critic.py:93-105 as patch GEMMs).  Each output one fixed-order
  * fp32 MFMA chain over k. */
 int gr_tsgemm(const float* a, int64_t lda, const float* b, int32_t b_nk, float* c, int64_t ldc, int64_t m, int32_t k,
               int32_t n, void* stream);

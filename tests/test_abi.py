@@ -219,6 +219,7 @@ def test_tsgemm_rejects_shapes_it_does_not_cover():
     assert call(b_nk=0) == -1
     assert call(k=64, n=128, lda=64, ldc=128) == -1
     assert call(n=32) == -1
+    assert call(k=192, n=100, b_nk=0, lda=192, ldc=100) == -1
     assert call(lda=100) == -1
     assert call(ldc=32) == -1
     assert call(a=p + 2) == -1

@@ -151,11 +151,12 @@ def test_patch_wgrad_matches_float64(m, n, k, ld):
 
 
 @pytest.mark.parametrize("m,k,n,b_nk,lda", [(491_520, 128, 64, True, 128), (491_520, 64, 128, False, 64),
-                                            (1, 128, 64, True, 128), (37, 64, 128, False, 70), (4099, 128, 64, True, 131)])
+                                            (1, 128, 64, True, 128), (37, 64, 128, False, 70), (4099, 128, 64, True, 131),
+                                            (24_576, 192, 1280, False, 192), (77, 192, 128, False, 200)])
 def test_tsgemm_matches_float64(m, k, n, b_nk, lda):
-    """gr_tsgemm (conv3's forward x W^T and input gradient gy W as patch GEMMs, the weight in registers) against
-    float64 at full (491 520 rows = conv3's patches of a 24 576-image mini-batch) and ragged sizes, strided rows;
-    repeats bit-identical."""
+    """gr_tsgemm (conv3's forward x W^T and input gradient gy W as patch GEMMs, the final Linear's input gradient in
+    64-output slabs) against float64 at full (491 520 rows = conv3's patches of a 24 576-image mini-batch; 24 576 rows
+    x 1 280 outputs) and ragged sizes, strided rows; repeats bit-identical."""
     from generalizableracing_amd import _abi
     import ctypes as C
 
