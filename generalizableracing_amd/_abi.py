@@ -240,7 +240,7 @@ EXPORTS = [
     "gr_stem1_forward", "gr_stem1_backward", "gr_mlp_partials", "gr_mlp_forward", "gr_mlp_backward",
     "gr_mlp_args_size", "gr_step_kernel_variant", "gr_terrain_reserve", "gr_terrain_stage", "gr_terrain_commit",
     "gr_terrain_epoch", "gr_mlp_h1mask_words", "gr_stem12_backward", "gr_stem12_forward",
-    "gr_patch_wgrad_floats", "gr_patch_wgrad", "gr_bn_running_update", "gr_tsgemm",
+    "gr_patch_wgrad_floats", "gr_patch_wgrad", "gr_bn_running_update", "gr_tsgemm", "gr_l2c2_mix_rows",
 ]
 
 _lib = None
@@ -306,6 +306,7 @@ def _declare(lib):
         "gr_episode_accumulate": (C.c_int, [C.c_int64, vp, vp, C.c_int32, vp, vp, vp, vp, vp, vp]),
         "gr_gae": (C.c_int, [C.c_int64, C.c_int32, C.c_float, C.c_float, vp, vp, vp, vp, C.c_int64, vp, vp, vp]),
         "gr_l2c2_mix": (C.c_int, [vp, vp, vp, C.c_int64, C.c_int32, vp, vp]),
+        "gr_l2c2_mix_rows": (C.c_int, [vp, vp, C.c_int64, vp, vp, vp, C.c_int64, C.c_int32, vp, vp]),
         "gr_adam_clip": (C.c_int, [vp, C.c_float, vp, vp]),
         "gr_adam_step": (C.c_int, [vp, vp]),
         "gr_adam_clip_step": (C.c_int, [vp, C.c_float, vp, vp, vp, C.c_double, C.c_double, C.c_double, vp]),
@@ -325,17 +326,17 @@ def _declare(lib):
         "gr_bn_act_backward": (C.c_int, [vp, vp, C.c_int64, C.c_int32, vp, vp, vp, C.c_int32, C.c_float, vp, vp, vp,
                                          vp, vp]),
         "gr_stem1_scratch_doubles": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
-        "gr_stem1_forward": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int32, vp, C.c_int32, C.c_int32, vp, C.c_int32,
+        "gr_stem1_forward": (C.c_int, [vp, C.c_int64, C.c_int64, vp, C.c_int32, vp, C.c_int32, C.c_int32, vp, C.c_int32,
                                        vp, vp, C.c_float, C.c_int32, C.c_float, vp, C.c_int64, vp, vp, vp]),
-        "gr_stem1_backward": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int32, vp, C.c_int32, C.c_int32, vp, C.c_int32,
+        "gr_stem1_backward": (C.c_int, [vp, C.c_int64, C.c_int64, vp, C.c_int32, vp, C.c_int32, C.c_int32, vp, C.c_int32,
                                         vp, vp, vp, C.c_int32, C.c_float, vp, C.c_int64, vp, vp, vp, vp, vp]),
         "gr_patch_wgrad_floats": (C.c_int64, [C.c_int64, C.c_int32, C.c_int32]),
         "gr_patch_wgrad": (C.c_int, [vp, C.c_int64, vp, C.c_int64, C.c_int32, C.c_int32, vp, vp, vp]),
         "gr_bn_running_update": (C.c_int, [vp, vp, vp, vp, C.c_int32, C.c_float, C.c_float, C.c_int32, C.c_int32, vp]),
         "gr_tsgemm": (C.c_int, [vp, C.c_int64, vp, C.c_int32, vp, C.c_int64, C.c_int64, C.c_int32, C.c_int32, vp]),
-        "gr_stem12_forward": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int32, vp, C.c_int32, C.c_int32, vp, C.c_int32,
+        "gr_stem12_forward": (C.c_int, [vp, C.c_int64, C.c_int64, vp, C.c_int32, vp, C.c_int32, C.c_int32, vp, C.c_int32,
                                         vp, vp, C.c_float, C.c_int32, C.c_float, vp, C.c_int32, vp, vp, vp, vp, vp]),
-        "gr_stem12_backward": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int32, vp, C.c_int32, C.c_int32, vp, C.c_int32,
+        "gr_stem12_backward": (C.c_int, [vp, C.c_int64, C.c_int64, vp, C.c_int32, vp, C.c_int32, C.c_int32, vp, C.c_int32,
                                          vp, vp, vp, C.c_int32, C.c_float, vp, C.c_int32, vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():

@@ -300,6 +300,10 @@ hipError_t launch_bn_backward(const float* x, const float* gy, long long m, int 
 // passes, which end in the conv weight's gradient (the image needs none) instead of writing gx.
 constexpr int STEM_MAX_CELLS = 1024;  // na + nbt (768 at 72 x 96)
 
+// image b's pixels: row rows[b] of obs when the batch is read through an index, else row b
+__device__ __forceinline__ const float* stem_img(const Stem1& s, long long b) {
+  return s.obs + (s.rows ? s.rows[b] : b) * s.ld + s.off;
+}
 __device__ __forceinline__ void stem_stage_table(const Stem1& s, short* tab) {
   for (int i = threadIdx.x; i < (s.na + s.nbt) * 9; i += BN_THREADS) tab[i] = s.pix[i];
   __syncthreads();
@@ -315,7 +319,7 @@ __device__ __forceinline__ void stem_pixels(const Stem1& s, const short* tab, un
     b = q / (unsigned)s.nbt;
     p = (unsigned)s.na + (q - b * (unsigned)s.nbt);
   }
-  const float* img = s.obs + (long long)b * s.ld + s.off;
+  const float* img = stem_img(s, b);
   const short* t = tab + p * 9;
 #pragma unroll
   for (int k = 0; k < 9; ++k) px[k] = img[t[k]];
@@ -583,7 +587,8 @@ __global__ __launch_bounds__(SM_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, i
     // the shift: row 0 (image 0, cell 0) of this lane's channel, from global memory (lane ch holds row 0)
     const bool ok = (int)(l & 15) < ncell;
     const short* t0 = tab + (ok ? (int)(l & 15) : 0) * 9;
-    const float v0 = s.obs[s.off + t0[kq]], v1 = s.obs[s.off + t0[kq + 4]], v2 = s.obs[s.off + t0[8]];
+    const float* im_0 = stem_img(s, 0);
+    const float v0 = im_0[t0[kq]], v1 = im_0[t0[kq + 4]], v2 = im_0[t0[8]];
     const float px[3] = {ok ? v0 : 0.0f, ok ? v1 : 0.0f, (ok && kq == 0) ? v2 : 0.0f};
     const sm4 x0 = sm_conv(px, wb);
     sh = __shfl(x0[0], (int)ch);
@@ -608,14 +613,14 @@ __global__ __launch_bounds__(SM_THREADS) void stem1i_kernel(Stem1 s, SmArgs q, i
   // images b = blockIdx.x + k gridDim.x: the loader wave stages image k + 1 into the other buffer (LDS-DMA) while
   // the compute waves run image k; the barrier at the end of each image drains the DMA (s_waitcnt vmcnt(0))
   const int nmine = s.nimg > (int)blockIdx.x ? (s.nimg - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
-  if (staged && loader && nmine > 0) sm_dma_image(s.obs + (long long)blockIdx.x * s.ld + s.off, im0, span, v4);
+  if (staged && loader && nmine > 0) sm_dma_image(stem_img(s, blockIdx.x), im0, span, v4);
   __syncthreads();
   for (int k = 0; k < nmine; ++k) {
     const int b = (int)blockIdx.x + k * (int)gridDim.x;
-    const float* g = s.obs + (long long)b * s.ld + s.off;
+    const float* g = stem_img(s, b);
     const float* im = (k & 1) ? im1 : im0;
     if (loader) {
-      if (staged && k + 1 < nmine) sm_dma_image(g + (long long)gridDim.x * s.ld, (k & 1) ? im0 : im1, span, v4);
+      if (staged && k + 1 < nmine) sm_dma_image(stem_img(s, b + (long long)gridDim.x), (k & 1) ? im0 : im1, span, v4);
     } else {
       // one instantiation per source, so the gathers stay ds_read (LDS) or global_load: a pointer chosen at run time
       // between the two became flat loads with full waits
@@ -840,14 +845,14 @@ __global__ __launch_bounds__(SM_THREADS) void stem12b_kernel(Stem1 s, Sm12Args q
   constexpr int U = 3;
 
   const int nmine = s.nimg > (int)blockIdx.x ? (s.nimg - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
-  if (staged && loader && nmine > 0) sm_dma_image(s.obs + (long long)blockIdx.x * s.ld + s.off, im0, span, v4);
+  if (staged && loader && nmine > 0) sm_dma_image(stem_img(s, blockIdx.x), im0, span, v4);
   __syncthreads();
   for (int k = 0; k < nmine; ++k) {
     const int b = (int)blockIdx.x + k * (int)gridDim.x;
-    const float* g = s.obs + (long long)b * s.ld + s.off;
+    const float* g = stem_img(s, b);
     const float* im = (k & 1) ? im1 : im0;
     if (loader) {
-      if (staged && k + 1 < nmine) sm_dma_image(g + (long long)gridDim.x * s.ld, (k & 1) ? im0 : im1, span, v4);
+      if (staged && k + 1 < nmine) sm_dma_image(stem_img(s, b + (long long)gridDim.x), (k & 1) ? im0 : im1, span, v4);
     } else {
       // fp32 sums over this image's tiles (<= 15 per wave), folded into the fp64 accumulators once per image
       float f0 = 0.0f, f1 = 0.0f, fp2[3] = {0.0f, 0.0f, 0.0f};
@@ -1134,14 +1139,14 @@ __global__ __launch_bounds__(SMF_THREADS) void stem12f_kernel(Stem1 s, Sm12fArgs
   const int nch = (n2 + 15) / 16;
 
   const int nmine = s.nimg > (int)blockIdx.x ? (s.nimg - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
-  if (staged && loader && nmine > 0) sm_dma_image(s.obs + (long long)blockIdx.x * s.ld + s.off, im0, span, v4);
+  if (staged && loader && nmine > 0) sm_dma_image(stem_img(s, blockIdx.x), im0, span, v4);
   __syncthreads();
   for (int k = 0; k < nmine; ++k) {
     const int b = (int)blockIdx.x + k * (int)gridDim.x;
-    const float* g = s.obs + (long long)b * s.ld + s.off;
+    const float* g = stem_img(s, b);
     const float* im = (k & 1) ? im1 : im0;
     if (loader) {
-      if (staged && k + 1 < nmine) sm_dma_image(g + (long long)gridDim.x * s.ld, (k & 1) ? im0 : im1, span, v4);
+      if (staged && k + 1 < nmine) sm_dma_image(stem_img(s, b + (long long)gridDim.x), (k & 1) ? im0 : im1, span, v4);
     } else {
       auto chunks = [&](auto from_lds) {
       for (int chunk = (int)w; chunk < nch; chunk += SMF_WAVES) {

@@ -961,10 +961,11 @@ static bool stem1_args_ok(const float* obs, int32_t nimg, const int16_t* pix, in
   return obs && pix && conv_w && bn_w && bn_b && nimg >= 1 && na >= 1 && nb >= 0 && na + nb <= 1024 &&
          (int64_t)nimg * (na + nb) < (int64_t)1 << 31 && bn_shape_ok(1, c) && aligned16(bn_w) && aligned16(bn_b);
 }
-static gr::Stem1 stem1_of(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
+static gr::Stem1 stem1_of(const float* obs, int64_t ld, int64_t off, const int64_t* rows, int32_t nimg, const int16_t* pix, int32_t na,
                           int32_t nb, const float* conv_w, int32_t c, int64_t rows_out) {
   gr::Stem1 s;
   s.obs = obs; s.ld = ld; s.off = off; s.nimg = nimg; s.na = na; s.nbt = nb;
+  s.rows = reinterpret_cast<const long long*>(rows);
   s.pix = reinterpret_cast<const short*>(pix); s.w = conv_w; s.c = c; s.rows_out = rows_out;
   return s;
 }
@@ -977,19 +978,19 @@ int64_t gr_stem1_scratch_doubles(int32_t nimg, int32_t rows_per_img, int32_t c) 
   return gr::stem1_scratch_doubles(nimg, rows_per_img, c);
 }
 
-int gr_stem1_forward(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
+int gr_stem1_forward(const float* obs, int64_t ld, int64_t off, const int64_t* rows, int32_t nimg, const int16_t* pix, int32_t na,
                      int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b, float eps,
                      int32_t act, float slope, float* y, int64_t y_rows, float* stats, double* part, void* stream) {
   if (!stem1_args_ok(obs, nimg, pix, na, nb, conv_w, c, bn_w, bn_b) || !y || !stats || !part || !aligned16(y) ||
       !aligned16(stats) || (act != GR_POLICY_ACT_LRELU && act != GR_POLICY_ACT_ELU) ||
       !stem1_rows_ok(nimg, na, nb, y_rows))
     return GR_ERR_ARG;
-  const gr::Stem1 s = stem1_of(obs, ld, off, nimg, pix, na, nb, conv_w, c, y_rows);
+  const gr::Stem1 s = stem1_of(obs, ld, off, rows, nimg, pix, na, nb, conv_w, c, y_rows);
   const hipError_t e = gr::launch_stem1_forward(s, bn_w, bn_b, eps, act, slope, y, stats, part, (hipStream_t)stream);
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
-int gr_stem1_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
+int gr_stem1_backward(const float* obs, int64_t ld, int64_t off, const int64_t* rows, int32_t nimg, const int16_t* pix, int32_t na,
                       int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b,
                       const float* stats, int32_t act, float slope, const float* gy, int64_t gy_rows, float* g_conv_w,
                       float* g_bn_w, float* g_bn_b, double* part, void* stream) {
@@ -997,7 +998,7 @@ int gr_stem1_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, c
       !g_bn_b || !part || !aligned16(gy) || !aligned16(stats) || (act != GR_POLICY_ACT_LRELU && act != GR_POLICY_ACT_ELU) ||
       !stem1_rows_ok(nimg, na, nb, gy_rows))
     return GR_ERR_ARG;
-  const gr::Stem1 s = stem1_of(obs, ld, off, nimg, pix, na, nb, conv_w, c, gy_rows);
+  const gr::Stem1 s = stem1_of(obs, ld, off, rows, nimg, pix, na, nb, conv_w, c, gy_rows);
   const hipError_t e = gr::launch_stem1_backward(s, bn_w, bn_b, stats, act, slope, gy, g_conv_w, g_bn_w, g_bn_b, part,
                                                  (hipStream_t)stream);
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
@@ -1029,7 +1030,7 @@ int gr_patch_wgrad(const float* x, int64_t ld, const float* gy, int64_t m, int32
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
-int gr_stem12_forward(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
+int gr_stem12_forward(const float* obs, int64_t ld, int64_t off, const int64_t* rows, int32_t nimg, const int16_t* pix, int32_t na,
                       int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b, float eps,
                       int32_t act, float slope, const float* w2f, int32_t n2, float* y, float* z2, float* stats,
                       double* part, void* stream) {
@@ -1038,13 +1039,13 @@ int gr_stem12_forward(const float* obs, int64_t ld, int64_t off, int32_t nimg, c
       (act != GR_POLICY_ACT_LRELU && act != GR_POLICY_ACT_ELU) || n2 < 1 || na != 9 * n2 ||
       (int64_t)nimg * n2 * 32 >= (int64_t)1 << 31)
     return GR_ERR_ARG;
-  const gr::Stem1 s = stem1_of(obs, ld, off, nimg, pix, na, nb, conv_w, c, (int64_t)nimg * na);
+  const gr::Stem1 s = stem1_of(obs, ld, off, rows, nimg, pix, na, nb, conv_w, c, (int64_t)nimg * na);
   const hipError_t e = gr::launch_stem12_forward(s, bn_w, bn_b, eps, act, slope, w2f, n2, y, z2, stats, part,
                                                  (hipStream_t)stream);
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
-int gr_stem12_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
+int gr_stem12_backward(const float* obs, int64_t ld, int64_t off, const int64_t* rows, int32_t nimg, const int16_t* pix, int32_t na,
                        int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b,
                        const float* stats, int32_t act, float slope, const float* gz2, int32_t n2, const float* w2t,
                        float* g_conv_w, float* g_bn_w, float* g_bn_b, double* part, void* stream) {
@@ -1053,7 +1054,7 @@ int gr_stem12_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, 
       (act != GR_POLICY_ACT_LRELU && act != GR_POLICY_ACT_ELU) || n2 < 1 || na != 9 * n2 ||
       (int64_t)nimg * n2 * 32 >= (int64_t)1 << 31)
     return GR_ERR_ARG;
-  const gr::Stem1 s = stem1_of(obs, ld, off, nimg, pix, na, nb, conv_w, c, (int64_t)nimg * na);
+  const gr::Stem1 s = stem1_of(obs, ld, off, rows, nimg, pix, na, nb, conv_w, c, (int64_t)nimg * na);
   const hipError_t e = gr::launch_stem12_backward(s, bn_w, bn_b, stats, act, slope, gz2, n2, w2t, g_conv_w, g_bn_w,
                                                   g_bn_b, part, (hipStream_t)stream);
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
@@ -1237,7 +1238,20 @@ int gr_l2c2_mix(const float* obs, const float* next_obs, const float* w, int64_t
       !aligned16(out))
     return GR_ERR_ARG;
   if (rows == 0) return GR_OK;
-  const hipError_t e = gr::launch_l2c2_mix(obs, next_obs, w, (long long)rows, cols, out, (hipStream_t)stream);
+  const hipError_t e = gr::launch_l2c2_mix(obs, next_obs, cols, nullptr, nullptr, w, (long long)rows, cols, out,
+                                           (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
+int gr_l2c2_mix_rows(const float* obs, const float* next_obs, int64_t ld, const int64_t* rows_obs,
+                     const int64_t* rows_next, const float* w, int64_t rows, int32_t cols, float* out, void* stream) {
+  if (!obs || !next_obs || !rows_obs || !rows_next || !w || !out || rows < 0 || cols <= 0 || cols % 4 || ld < cols ||
+      ld % 4 || !aligned16(obs) || !aligned16(next_obs) || !aligned16(out))
+    return GR_ERR_ARG;
+  if (rows == 0) return GR_OK;
+  const hipError_t e = gr::launch_l2c2_mix(obs, next_obs, ld, reinterpret_cast<const long long*>(rows_obs),
+                                           reinterpret_cast<const long long*>(rows_next), w, (long long)rows, cols, out,
+                                           (hipStream_t)stream);
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 

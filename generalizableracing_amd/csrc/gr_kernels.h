@@ -103,6 +103,7 @@ int bn_scratch_doubles(long long m, int c);                                     
 struct Stem1 {
   const float* obs;
   long long ld, off;
+  const long long* rows;  // image b is row rows[b] of obs (a mini-batch read through its permutation), or b if null
   int nimg, na, nbt;
   const short* pix;
   const float* w;
@@ -141,8 +142,8 @@ hipError_t launch_patch_wgrad(const float* x, long long ld, const float* gy, lon
 hipError_t launch_column_sum(const void* x, int dtype, long long m, int n, float* part, float* out, hipStream_t s);
 int head_partial_rows(long long m);                                                                      // gr_update.hip
 int in_partial_rows(long long m);                                                                        // gr_update.hip
-hipError_t launch_l2c2_mix(const float* o, const float* nx, const float* w, long long rows, int cols, float* out,
-                           hipStream_t s);  // gr_rollout.hip
+hipError_t launch_l2c2_mix(const float* o, const float* nx, long long ld, const long long* ra, const long long* rb,
+                           const float* w, long long rows, int cols, float* out, hipStream_t s);  // gr_rollout.hip
 hipError_t launch_head_forward(const float* z, long long m, int h, const float* w, const float* b, int k, float slope,
                                float* y, hipStream_t s);
 hipError_t launch_head_backward(const float* z, const float* gy, long long m, int h, const float* w, int k,

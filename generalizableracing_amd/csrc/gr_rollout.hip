@@ -107,29 +107,33 @@ hipError_t launch_gae(long long n, int t_steps, float gamma, float lam, const fl
 
 // PPOL2C2's mixed observations (ppo_l2c2.py:179-180): out = o + w * (n - o) with w one scalar per row, in the torch
 // expression's three roundings (sub, mul, add; no contraction): one pass (read o, n, write out) instead of three
-// elementwise kernels over [rows, cols] matrices of ~680 MB at 4 096 envs
-__global__ __launch_bounds__(256) void l2c2_mix(const float* __restrict__ o, const float* __restrict__ nx,
+// elementwise kernels over [rows, cols] matrices of ~680 MB at 4 096 envs.  With row indices the pair is read
+// straight from the rollout storage (row ra[r] of o, rb[r] of n, ld floats apart) instead of from gathered copies.
+__global__ __launch_bounds__(256) void l2c2_mix(const float* __restrict__ o, const float* __restrict__ nx, long long ld4,
+                                                 const long long* __restrict__ ra, const long long* __restrict__ rb,
                                                  const float* __restrict__ w, long long rows, int cols4,
                                                  float* __restrict__ out) {
   const long long n4 = rows * cols4;
   for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < n4; q += (long long)gridDim.x * 256) {
-    const float wr = w[q / cols4];
-    const float4 a = reinterpret_cast<const float4*>(o)[q], b = reinterpret_cast<const float4*>(nx)[q];
-    float4 r;
-    r.x = a.x + wr * (b.x - a.x);
-    r.y = a.y + wr * (b.y - a.y);
-    r.z = a.z + wr * (b.z - a.z);
-    r.w = a.w + wr * (b.w - a.w);
-    reinterpret_cast<float4*>(out)[q] = r;
+    const long long r = q / cols4, c = q - r * cols4;
+    const float wr = w[r];
+    const long long ia = (ra ? ra[r] : r) * ld4 + c, ib = (rb ? rb[r] : r) * ld4 + c;
+    const float4 a = reinterpret_cast<const float4*>(o)[ia], b = reinterpret_cast<const float4*>(nx)[ib];
+    float4 v;
+    v.x = a.x + wr * (b.x - a.x);
+    v.y = a.y + wr * (b.y - a.y);
+    v.z = a.z + wr * (b.z - a.z);
+    v.w = a.w + wr * (b.w - a.w);
+    reinterpret_cast<float4*>(out)[q] = v;
   }
 }
 
-hipError_t launch_l2c2_mix(const float* o, const float* nx, const float* w, long long rows, int cols, float* out,
-                           hipStream_t s) {
+hipError_t launch_l2c2_mix(const float* o, const float* nx, long long ld, const long long* ra, const long long* rb,
+                           const float* w, long long rows, int cols, float* out, hipStream_t s) {
   const long long n4 = rows * (cols / 4);
   long long blocks = (n4 + 256 * 8 - 1) / (256 * 8);
   blocks = blocks < 1 ? 1 : (blocks > 8192 ? 8192 : blocks);
-  hipLaunchKernelGGL(l2c2_mix, dim3((unsigned)blocks), dim3(256), 0, s, o, nx, w, rows, cols / 4, out);
+  hipLaunchKernelGGL(l2c2_mix, dim3((unsigned)blocks), dim3(256), 0, s, o, nx, ld / 4, ra, rb, w, rows, cols / 4, out);
   return hipGetLastError();
 }
 

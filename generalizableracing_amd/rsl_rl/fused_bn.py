@@ -95,23 +95,23 @@ class _Stem1(torch.autograd.Function):
     statistics but nothing reads them, so no zero-filled [rows, C] gradient is built for them in the backward."""
 
     @staticmethod
-    def forward(ctx, img, conv_w, bn_w, bn_b, pix, na, nb, eps, act, slope):
+    def forward(ctx, img, conv_w, bn_w, bn_b, pix, na, nb, eps, act, slope, rows=None):
         lib = _abi.load()
-        nimg = img.shape[0]
+        nimg = img.shape[0] if rows is None else rows.numel()
         c = conv_w.shape[0]
-        rows = nimg * na
-        y = torch.empty(rows, c, device=img.device, dtype=torch.float32)
+        y = torch.empty(nimg * na, c, device=img.device, dtype=torch.float32)
         stats = torch.empty(4, c, device=img.device, dtype=torch.float32)
         part = torch.empty(int(lib.gr_stem1_scratch_doubles(nimg, na + nb, c)), device=img.device, dtype=torch.float64)
         w = conv_w.detach().reshape(c, 9).contiguous()
         bw, bb = bn_w.detach().contiguous(), bn_b.detach().contiguous()
-        rc = lib.gr_stem1_forward(img.data_ptr(), img.stride(0), 0, nimg, pix.data_ptr(), na, nb, w.data_ptr(), c,
-                                  bw.data_ptr(), bb.data_ptr(), float(eps), act, float(slope), y.data_ptr(), rows,
-                                  stats.data_ptr(), part.data_ptr(), _stream(img))
+        rc = lib.gr_stem1_forward(img.data_ptr(), img.stride(0), 0, _rows_ptr(rows), nimg, pix.data_ptr(), na, nb,
+                                  w.data_ptr(), c, bw.data_ptr(), bb.data_ptr(), float(eps), act, float(slope),
+                                  y.data_ptr(), nimg * na, stats.data_ptr(), part.data_ptr(), _stream(img))
         if rc != 0:
             raise RuntimeError(f"gr_stem1_forward failed (status {rc})")
         ctx.save_for_backward(img, w, bw, bb, stats)
         ctx.pix = pix  # a constant table (possibly made under inference mode): kept as an attribute
+        ctx.rows = rows  # (the batch's row indices into img, or None)
         ctx.args = (na, nb, act, slope, conv_w.shape)
         ctx.mark_non_differentiable(stats)
         return y, stats
@@ -124,19 +124,21 @@ class _Stem1(torch.autograd.Function):
         img, w, bw, bb, stats = ctx.saved_tensors
         pix = ctx.pix
         na, nb, act, slope, wshape = ctx.args
-        nimg, c = img.shape[0], w.shape[0]
+        rows = ctx.rows
+        nimg, c = (img.shape[0] if rows is None else rows.numel()), w.shape[0]
         gy = gy.contiguous()
         gconv = torch.empty(c, 9, device=img.device, dtype=torch.float32)
         gbw = torch.empty(c, device=img.device, dtype=torch.float32)
         gbb = torch.empty(c, device=img.device, dtype=torch.float32)
         part = torch.empty(int(lib.gr_stem1_scratch_doubles(nimg, na + nb, c)), device=img.device, dtype=torch.float64)
-        rc = lib.gr_stem1_backward(img.data_ptr(), img.stride(0), 0, nimg, pix.data_ptr(), na, nb, w.data_ptr(), c,
-                                   bw.data_ptr(), bb.data_ptr(), stats.data_ptr(), act, float(slope), gy.data_ptr(),
+        rc = lib.gr_stem1_backward(img.data_ptr(), img.stride(0), 0, _rows_ptr(rows), nimg, pix.data_ptr(), na, nb,
+                                   w.data_ptr(), c, bw.data_ptr(), bb.data_ptr(), stats.data_ptr(), act, float(slope),
+                                   gy.data_ptr(),
                                    gy.shape[0], gconv.data_ptr(), gbw.data_ptr(), gbb.data_ptr(), part.data_ptr(),
                                    _stream(img))
         if rc != 0:
             raise RuntimeError(f"gr_stem1_backward failed (status {rc})")
-        return None, gconv.view(wshape), gbw, gbb, None, None, None, None, None, None
+        return None, gconv.view(wshape), gbw, gbb, None, None, None, None, None, None, None
 
 
 class _Stem12(torch.autograd.Function):
@@ -147,11 +149,10 @@ class _Stem12(torch.autograd.Function):
     conv2's weight gradient is the split-K product of gz2 and the saved y1."""
 
     @staticmethod
-    def forward(ctx, img, conv_w, bn_w, bn_b, w2, pix, na, nb, eps, act, slope, fused_forward=True):
+    def forward(ctx, img, conv_w, bn_w, bn_b, w2, pix, na, nb, eps, act, slope, fused_forward=True, rows=None):
         lib = _abi.load()
-        nimg = img.shape[0]
-        rows = nimg * na
-        y = torch.empty(rows, 16, device=img.device, dtype=torch.float32)
+        nimg = img.shape[0] if rows is None else rows.numel()
+        y = torch.empty(nimg * na, 16, device=img.device, dtype=torch.float32)
         stats = torch.empty(4, 16, device=img.device, dtype=torch.float32)
         part = torch.empty(int(lib.gr_stem1_scratch_doubles(nimg, na + nb, 16)), device=img.device, dtype=torch.float64)
         w = conv_w.detach().reshape(16, 9).contiguous()
@@ -161,19 +162,21 @@ class _Stem12(torch.autograd.Function):
             # conv2 inside the first block's apply pass: w2f[j][g][o][v] = W2[o][j * 16 + 4 g + v]
             w2f = w2d.reshape(32, 9, 4, 4).permute(1, 2, 0, 3).contiguous()
             z2 = torch.empty(nimg * (na // 9), 32, device=img.device, dtype=torch.float32)
-            rc = lib.gr_stem12_forward(img.data_ptr(), img.stride(0), 0, nimg, pix.data_ptr(), na, nb, w.data_ptr(), 16,
-                                       bw.data_ptr(), bb.data_ptr(), float(eps), act, float(slope), w2f.data_ptr(),
+            rc = lib.gr_stem12_forward(img.data_ptr(), img.stride(0), 0, _rows_ptr(rows), nimg, pix.data_ptr(), na, nb,
+                                       w.data_ptr(), 16, bw.data_ptr(), bb.data_ptr(), float(eps), act, float(slope),
+                                       w2f.data_ptr(),
                                        na // 9, y.data_ptr(), z2.data_ptr(), stats.data_ptr(), part.data_ptr(),
                                        _stream(img))
         else:  # the first block's kernels, then conv2 as a GEMM (the A/B reference of the fused forward)
-            rc = lib.gr_stem1_forward(img.data_ptr(), img.stride(0), 0, nimg, pix.data_ptr(), na, nb, w.data_ptr(), 16,
-                                      bw.data_ptr(), bb.data_ptr(), float(eps), act, float(slope), y.data_ptr(), rows,
-                                      stats.data_ptr(), part.data_ptr(), _stream(img))
+            rc = lib.gr_stem1_forward(img.data_ptr(), img.stride(0), 0, _rows_ptr(rows), nimg, pix.data_ptr(), na, nb,
+                                      w.data_ptr(), 16, bw.data_ptr(), bb.data_ptr(), float(eps), act, float(slope),
+                                      y.data_ptr(), nimg * na, stats.data_ptr(), part.data_ptr(), _stream(img))
             z2 = y.view(-1, 144) @ w2d.t() if rc == 0 else None
         if rc != 0:
             raise RuntimeError(f"gr_stem12_forward failed (status {rc})")
         ctx.save_for_backward(img, w, bw, bb, stats, y, w2d)
         ctx.pix = pix
+        ctx.rows = rows
         ctx.args = (na, nb, act, slope, conv_w.shape)
         ctx.mark_non_differentiable(stats)
         return z2, stats
@@ -185,7 +188,8 @@ class _Stem12(torch.autograd.Function):
         lib = _abi.load()
         img, w, bw, bb, stats, y, w2d = ctx.saved_tensors
         na, nb, act, slope, wshape = ctx.args
-        nimg = img.shape[0]
+        rows = ctx.rows
+        nimg = img.shape[0] if rows is None else rows.numel()
         gz2 = gz2.contiguous()
         gw2 = None
         if ctx.needs_input_grad[4]:  # conv2's weight: gz2^T y1 patches (gr_patch_wgrad: MFMA, fixed-order sums)
@@ -198,13 +202,14 @@ class _Stem12(torch.autograd.Function):
         gbw = torch.empty(16, device=img.device, dtype=torch.float32)
         gbb = torch.empty(16, device=img.device, dtype=torch.float32)
         part = torch.empty(int(lib.gr_stem1_scratch_doubles(nimg, na + nb, 16)), device=img.device, dtype=torch.float64)
-        rc = lib.gr_stem12_backward(img.data_ptr(), img.stride(0), 0, nimg, ctx.pix.data_ptr(), na, nb, w.data_ptr(), 16,
-                                    bw.data_ptr(), bb.data_ptr(), stats.data_ptr(), act, float(slope), gz2.data_ptr(),
+        rc = lib.gr_stem12_backward(img.data_ptr(), img.stride(0), 0, _rows_ptr(rows), nimg, ctx.pix.data_ptr(), na, nb,
+                                    w.data_ptr(), 16, bw.data_ptr(), bb.data_ptr(), stats.data_ptr(), act, float(slope),
+                                    gz2.data_ptr(),
                                     na // 9, w2t.data_ptr(), gconv.data_ptr(), gbw.data_ptr(), gbb.data_ptr(),
                                     part.data_ptr(), _stream(img))
         if rc != 0:
             raise RuntimeError(f"gr_stem12_backward failed (status {rc})")
-        return None, gconv.view(wshape), gbw, gbb, gw2, None, None, None, None, None, None, None
+        return None, gconv.view(wshape), gbw, gbb, gw2, None, None, None, None, None, None, None, None
 
 
 def stem12_applicable(bn: nn.BatchNorm2d, act: nn.Module, img: torch.Tensor, conv_w: torch.Tensor,
@@ -217,11 +222,13 @@ def stem12_applicable(bn: nn.BatchNorm2d, act: nn.Module, img: torch.Tensor, con
 
 def stem12_bn_act_conv(bn: nn.BatchNorm2d, act: nn.Module, conv_w: torch.Tensor, w2: torch.Tensor, img: torch.Tensor,
                        pix: torch.Tensor, na: int, nb: int, uses: int = 1, fused_forward: bool = True,
-                       count_first: bool = False) -> torch.Tensor:
+                       count_first: bool = False, rows: torch.Tensor | None = None) -> torch.Tensor:
     """conv2's output rows [B * na / 9, 32] = patches(act(bn(conv(img)))) @ w2^T (w2 [32, 144], columns (j, c)),
-    running statistics of the first BN updated as stem1_bn_act does."""
+    running statistics of the first BN updated as stem1_bn_act does.  rows: the batch is img[rows] (int64 device
+    indices), read through them instead of a gathered copy."""
     code, slope = _act_code(act)
-    z2, stats = _Stem12.apply(img, conv_w, bn.weight, bn.bias, w2, pix, na, nb, bn.eps, code, slope, fused_forward)
+    z2, stats = _Stem12.apply(img, conv_w, bn.weight, bn.bias, w2, pix, na, nb, bn.eps, code, slope, fused_forward,
+                              _rows_arg(rows))
     _update_running(bn, stats, uses, count_first)
     return z2
 
@@ -235,14 +242,28 @@ def stem1_applicable(bn: nn.BatchNorm2d, act: nn.Module, img: torch.Tensor, conv
 
 
 def stem1_bn_act(bn: nn.BatchNorm2d, act: nn.Module, conv_w: torch.Tensor, img: torch.Tensor, pix: torch.Tensor,
-                 na: int, nb: int, uses: int = 1, count_first: bool = False) -> torch.Tensor:
+                 na: int, nb: int, uses: int = 1, count_first: bool = False,
+                 rows: torch.Tensor | None = None) -> torch.Tensor:
     """act(bn(conv(img))) as the table-a patch rows of VisionActorCritic.stem_gemm (img [B, H*W] rows; pix int16
     [(na + nb) * 9] pixel offsets; the B * nb table-b rows count in the statistics and are not returned), running
     statistics updated as nn.BatchNorm2d does (the caller counts the batch in num_batches_tracked)."""
     code, slope = _act_code(act)
-    y, stats = _Stem1.apply(img, conv_w, bn.weight, bn.bias, pix, na, nb, bn.eps, code, slope)
+    y, stats = _Stem1.apply(img, conv_w, bn.weight, bn.bias, pix, na, nb, bn.eps, code, slope, _rows_arg(rows))
     _update_running(bn, stats, uses, count_first)
     return y
+
+
+def _rows_arg(rows):
+    """The batch's row indices as the kernels take them (contiguous int64 on the image's device), or None."""
+    if rows is None:
+        return None
+    if rows.dtype != torch.int64 or rows.dim() != 1:
+        raise ValueError("row indices: a 1-D int64 tensor")
+    return rows.contiguous()
+
+
+def _rows_ptr(rows):
+    return rows.data_ptr() if rows is not None else None
 
 
 def _update_running(bn: nn.BatchNorm2d, stats: torch.Tensor, uses: int = 1, count_first: bool = False):

@@ -59,12 +59,29 @@ def _mix(obs, next_obs, w):
     return obs + w * (next_obs - obs)
 
 
+def _mix_rows(src, rows_obs, rows_next, w):
+    """_mix(src[rows_obs], src[rows_next], w) in one pass over the storage rows (gr_l2c2_mix_rows): no gathered copies
+    of the pair."""
+    from .. import _abi
+
+    w = w.reshape(-1).float().contiguous()
+    out = torch.empty(rows_obs.numel(), src.shape[1], device=src.device, dtype=torch.float32)
+    rc = _abi.load().gr_l2c2_mix_rows(src.data_ptr(), src.data_ptr(), src.stride(0), rows_obs.data_ptr(),
+                                      rows_next.data_ptr(), w.data_ptr(), out.shape[0], out.shape[1], out.data_ptr(),
+                                      _abi.raw_stream(src.device))
+    if rc != 0:
+        raise RuntimeError(f"gr_l2c2_mix_rows failed (status {rc})")
+    return out
+
+
 class PPOL2C2(PPO):
     def __init__(self, policy, env=None, value_smoothness_coef=0.1, smoothness_upper_bound=1.0,
-                 smoothness_lower_bound=0.1, share_mix_features=True, **kwargs):
+                 smoothness_lower_bound=0.1, share_mix_features=True, rows_update=True, **kwargs):
         kwargs.pop("normalize_advantage", None)
         # one stem evaluation of the mixed batch for the actor and the critic (policies with shared_features)
         self.share_mix_features = bool(share_mix_features)
+        # the graphed update reads the mini-batch's image rows through its permutation (no gathered copies)
+        self.rows_update = bool(rows_update)
         super().__init__(policy, env=env, normalize_advantage=True, **kwargs)
         self.transition = RolloutStorageL2C2.Transition()
         self._mix_uniform = torch.rand_like  # the smoothness loss's uniform draw (tests substitute a fixed one)
@@ -108,11 +125,16 @@ class PPOL2C2(PPO):
         self.transition.clear()
         self.policy.reset(dones)
 
-    def smooth_loss(self, obs_batch, next_obs_batch, cont_batch, mu_batch, value_batch):
-        """ppo_l2c2.py:176-188; returns (smooth_loss, action_smoothness)."""
+    def smooth_loss(self, obs_batch, next_obs_batch, cont_batch, mu_batch, value_batch, rows=None):
+        """ppo_l2c2.py:176-188; returns (smooth_loss, action_smoothness).  rows (src, idx, next_idx): the pair is
+        src[idx], src[next_idx] (the rollout storage's rows, read through the indices; obs_batch / next_obs_batch
+        unused)."""
         policy_coef, value_coef = self.smooth_coefs()
         mix_weights = cont_batch * (self._mix_uniform(cont_batch) - 0.5) * 2.0
-        mix_obs_batch = _mix(obs_batch, next_obs_batch, mix_weights)
+        if rows is not None:
+            mix_obs_batch = _mix_rows(rows[0], rows[1], rows[2], mix_weights)
+        else:
+            mix_obs_batch = _mix(obs_batch, next_obs_batch, mix_weights)
         shared = getattr(self.policy, "shared_features", None)
         if shared is not None and self.share_mix_features:
             # the actor's and the critic's forward of the mixed batch share one stem evaluation (VisionActorCritic:
@@ -126,8 +148,11 @@ class PPOL2C2(PPO):
         value_smooth = torch.square(torch.norm(value_batch - mix_value, dim=-1)).mean()
         loss = policy_coef * policy_smooth + value_coef * value_smooth
         with torch.inference_mode():
-            action_smoothness = torch.norm(mu_batch - _mean_of(self.policy.act_inference(next_obs_batch)),
-                                           dim=-1).mean()
+            if rows is not None:
+                next_mean = self.policy.actor(self.policy.features_rows(rows[0], rows[2]))
+            else:
+                next_mean = _mean_of(self.policy.act_inference(next_obs_batch))
+            action_smoothness = torch.norm(mu_batch - next_mean, dim=-1).mean()
         return loss, action_smoothness
 
     def update(self):
@@ -231,9 +256,43 @@ class _GraphedStepL2C2(_GraphedStep):
                 and getattr(pol, "noise_std_type", None) in ("scalar", "log")
                 and not torch.is_autocast_enabled("cuda"))
 
+    def _rows_ok(self) -> bool:
+        """The mini-batch's image rows read through the permutation (VisionActorCritic.features_rows, the fused
+        first block's row indices, gr_l2c2_mix_rows) instead of gathered: fp32 storage rows, a policy with
+        features_rows, the fused losses."""
+        st, pol = self.alg.storage, self.alg.policy
+        srcs = [st.observations] + ([st.privileged_observations] if st.privileged_observations is not None else [])
+        return (self.alg.rows_update and hasattr(pol, "features_rows") and st.observations.is_cuda
+                and all(x.dtype == torch.float32 and x.is_contiguous() for x in srcs)
+                and st.observations.shape[-1] % 4 == 0 and self._fused_losses_ok(st.observations[0]))
+
+    def _seg_a_rows(self, idx):
+        """Segment A with the image rows read through `idx` (the same values as the gathered form)."""
+        alg, pol, st = self.alg, self.alg.policy, self.alg.storage
+        src = st.observations.flatten(0, 1)  # row j + N is the successor of row j
+        csrc = st.privileged_observations.flatten(0, 1) if st.privileged_observations is not None else src
+        nidx = idx + self.N
+        cont, act, val, adv, ret, logp, mu, sig = (x.index_select(0, idx) for x in self._sources()[3:])
+        mu_b = pol.actor(pol.features_rows(src, idx))
+        value_b = pol.critic(pol.features_rows(csrc, idx))
+        std = _floss._policy_std(pol)
+        loss, _ = _floss._PPOLossCombinedFn.apply(
+            mu_b, std, value_b, act, logp, adv, val, ret, mu, sig, float(alg.clip_param),
+            bool(alg.use_clipped_value_loss), float(alg.value_loss_coef), self.acc[:2],
+            self.flat.extra[:1] if self._adaptive() else None, None)
+        if alg.entropy_coef != 0.0:
+            loss = loss - alg.entropy_coef * (0.5 + 0.5 * math.log(2.0 * math.pi) + torch.log(std)).sum()
+        smooth_loss, _ = alg.smooth_loss(None, None, cont, mu_b, value_b, rows=(src, idx, nidx))
+        self.acc[2:].add_(smooth_loss.detach())
+        self._backward(loss + smooth_loss)
+
     def _seg_a(self, idx=None):
         alg, pol = self.alg, self.alg.policy
-        obs, crit, nxt, cont, act, val, adv, ret, logp, mu, sig = self._gather(self.idx if idx is None else idx)
+        idx = self.idx if idx is None else idx
+        if self._rows_ok():
+            self._seg_a_rows(idx)
+            return
+        obs, crit, nxt, cont, act, val, adv, ret, logp, mu, sig = self._gather(idx)
         obs, crit, nxt = obs.float(), crit.float(), nxt.float()
         if self._fused_losses_ok(obs):
             # ppo_l2c2.py:127-175 with the log prob, KL, surrogate and value losses in one launch each way; the KL

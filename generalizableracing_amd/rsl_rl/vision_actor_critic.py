@@ -236,24 +236,31 @@ class VisionActorCritic(ActorCritic):
         self._pidx = (a, b, len(l1), len(l1_left), len(g3), len(g2), pix16)
         return self._pidx
 
-    def stem_gemm(self, img: torch.Tensor, extra_bias: torch.Tensor | None = None) -> torch.Tensor:
+    def stem_gemm(self, img: torch.Tensor, extra_bias: torch.Tensor | None = None,
+                  rows: torch.Tensor | None = None) -> torch.Tensor:
         """The conv stem as patch GEMMs (identical math to self.stem(img), other summation order); extra_bias is added
-        to the final Linear's bias (features() passes the state encoder's)."""
+        to the final Linear's bias (features() passes the state encoder's).  rows: the batch is img[rows], read
+        through the indices by the fused first block (the other paths gather it)."""
         conv1, bn1, act, conv2, bn2, _, conv3, bn3, _, _, lin = self.stem
         h1, w1, h2, w2, h3, w3 = self._dims
-        B = img.shape[0]
-        flat = img.reshape(B, -1)
+        flat = img.reshape(img.shape[0], -1)
         idx, idx_left, n1, n1_left, n3, n2, pix16 = self._patch_index(img.device)
+        fused12 = (self.fused_bn and self.fused_conv2 and n1 == 9 * n2
+                   and stem12_applicable(bn1, act, flat, conv1.weight, conv2.weight, n1))
+        if rows is not None and not (fused12 or (self.fused_bn and stem1_applicable(bn1, act, flat, conv1.weight))):
+            flat, rows = flat.index_select(0, rows), None
+        B = flat.shape[0] if rows is None else rows.numel()
         w2m = conv2.weight.permute(0, 2, 3, 1).reshape(32, 144)  # conv2 on its 3x3 patches, columns (i, j, c)
         block2 = None
-        if self.fused_bn and self.fused_conv2 and n1 == 9 * n2 and stem12_applicable(bn1, act, flat, conv1.weight, conv2.weight, n1):
+        if fused12:
             # conv1 + BN1 + act + conv2: the backward forms conv2's input gradient inside the first block's passes
             z2 = stem12_bn_act_conv(bn1, act, conv1.weight, w2m, flat, pix16, n1, n1_left, self._bn_uses,
-                                    self.fused_conv2_forward, count_first=True)
+                                    self.fused_conv2_forward, count_first=True, rows=rows)
             block2 = self._bn_act(bn2, act, z2)
         elif self.fused_bn and stem1_applicable(bn1, act, flat, conv1.weight):
             # conv1 + BN1 + act from the image itself: no patch matrix, no conv output (rsl_rl/fused_bn.py)
-            y = stem1_bn_act(bn1, act, conv1.weight, flat, pix16, n1, n1_left, self._bn_uses, count_first=True)
+            y = stem1_bn_act(bn1, act, conv1.weight, flat, pix16, n1, n1_left, self._bn_uses, count_first=True,
+                             rows=rows)
         else:
             x = flat.index_select(1, idx).view(B * n1, 9)
             if n1_left:
@@ -278,6 +285,14 @@ class VisionActorCritic(ActorCritic):
         # the state encoder's GEMM takes the stem's output (with both biases) as its addend: no [B, 192] adds
         se = self.state_enc
         return self.activation(torch.addmm(self.stem_gemm(img, se.bias), state, se.weight.t()))
+
+    def features_rows(self, observations: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:
+        """features(observations[rows]) without the gathered copy of the image rows: the state columns are gathered,
+        the fused first block reads the images through `rows` (a PPO mini-batch straight from the rollout storage)."""
+        state = observations[:, :-self.num_pixels].index_select(0, rows)
+        img = observations[:, -self.num_pixels:]
+        se = self.state_enc
+        return self.activation(torch.addmm(self.stem_gemm(img, se.bias, rows=rows), state, se.weight.t()))
 
     def shared_features(self, observations: torch.Tensor, uses: int) -> torch.Tensor:
         """features(observations) evaluated once for `uses` consumers of the same rows (PPOL2C2's mixed batch feeds

@@ -449,7 +449,8 @@ int gr_bn_running_update(float* running_mean, float* running_var, int64_t* num_b
 
 /*
  * The vision stem's first block from the depth image itself: Conv2d(1, c, 3, stride 3, no bias) -> BatchNorm2d
- * (training mode) -> act, for `nimg` images at obs + b * ld + off (fp32 pixels).  Output rows follow
+ * (training mode) -> act, for `nimg` images at obs + b * ld + off (fp32 pixels), or at obs + rows[b] * ld + off
+ * when `rows` is not NULL (a mini-batch read through its permutation instead of a gathered copy).  Output rows follow
  * VisionActorCritic.stem_gemm: nimg x na rows whose 3x3 cells are pix[0 .. na) (int16 pixel offsets, 9 per
  * row), then nimg x nb rows from pix[na .. na + nb); y [rows][c].  The patch matrix and the conv output are
  * never written (recomputed per pass); the backward returns the conv weight's gradient [c][9] and the BN
@@ -460,10 +461,10 @@ int gr_bn_running_update(float* running_mean, float* running_var, int64_t* num_b
  * gr_stem1_scratch_doubles(nimg, na + nb, c) doubles; stats as gr_bn_act_forward.
  */
 int64_t gr_stem1_scratch_doubles(int32_t nimg, int32_t rows_per_img, int32_t c);
-int gr_stem1_forward(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
+int gr_stem1_forward(const float* obs, int64_t ld, int64_t off, const int64_t* rows, int32_t nimg, const int16_t* pix, int32_t na,
                      int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b, float eps,
                      int32_t act, float slope, float* y, int64_t y_rows, float* stats, double* part, void* stream);
-int gr_stem1_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
+int gr_stem1_backward(const float* obs, int64_t ld, int64_t off, const int64_t* rows, int32_t nimg, const int16_t* pix, int32_t na,
                       int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b,
                       const float* stats, int32_t act, float slope, const float* gy, int64_t gy_rows, float* g_conv_w,
                       float* g_bn_w, float* g_bn_b, double* part, void* stream);
@@ -489,7 +490,7 @@ int gr_patch_wgrad(const float* x, int64_t ld, const float* gy, int64_t m, int32
  * z2 [nimg * n2][32] (na = 9 n2; row 9 p + j of an image = position j of patch p).  w2f: conv2's weight as
  * [9][4][32][4] floats, w2f[((j * 4 + g) * 32 + o) * 4 + v] = W[o][4 g + v][j / 3][j % 3] (16-byte aligned).
  * Same workspace and stats as gr_stem1_forward. */
-int gr_stem12_forward(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
+int gr_stem12_forward(const float* obs, int64_t ld, int64_t off, const int64_t* rows, int32_t nimg, const int16_t* pix, int32_t na,
                       int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b, float eps,
                       int32_t act, float slope, const float* w2f, int32_t n2, float* y, float* z2, float* stats,
                       double* part, void* stream);
@@ -499,7 +500,7 @@ int gr_stem12_forward(const float* obs, int64_t ld, int64_t off, int32_t nimg, c
  * instead of reading a [nimg * na][16] gy (VisionActorCritic stem; reference vision_actor_critic.py:93-105).
  * w2t: conv2's weight as [9][4][16][8] floats, w2t[((j * 4 + g) * 16 + ch) * 8 + s] = W[o = 8 g + s][ch][j / 3][j % 3]
  * (16-byte aligned).  conv2's own weight gradient is not computed here.  Same workspace as gr_stem1_backward. */
-int gr_stem12_backward(const float* obs, int64_t ld, int64_t off, int32_t nimg, const int16_t* pix, int32_t na,
+int gr_stem12_backward(const float* obs, int64_t ld, int64_t off, const int64_t* rows, int32_t nimg, const int16_t* pix, int32_t na,
                        int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b,
                        const float* stats, int32_t act, float slope, const float* gz2, int32_t n2, const float* w2t,
                        float* g_conv_w, float* g_bn_w, float* g_bn_b, double* part, void* stream);
@@ -735,6 +736,11 @@ int gr_episode_accumulate(int64_t n, const float* reward, const void* dones, int
  * rows, cols a multiple of 4, 16-byte aligned. */
 int gr_l2c2_mix(const float* obs, const float* next_obs, const float* w, int64_t rows, int32_t cols, float* out,
                 void* stream);
+/* The same with the pair read through row indices: out[r] = obs[rows_obs[r]] + w[r] (next_obs[rows_next[r]] -
+ * obs[rows_obs[r]]), source rows `ld` floats apart (a multiple of 4): the mini-batch's rows straight from the rollout
+ * storage (rollout_storage_l2c2.py:131-167 gathers them first). */
+int gr_l2c2_mix_rows(const float* obs, const float* next_obs, int64_t ld, const int64_t* rows_obs,
+                     const int64_t* rows_next, const float* w, int64_t rows, int32_t cols, float* out, void* stream);
 int gr_gae(int64_t n, int32_t t_steps, float gamma, float lam, const float* rewards, const uint8_t* dones,
            const float* values, const float* last_values, int64_t ld_last, float* returns, float* advantages,
            void* stream);

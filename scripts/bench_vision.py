@@ -47,6 +47,7 @@ def main(argv=None):
     ap.add_argument("--no-fused-conv2", action="store_true",
                     help="conv2's input gradient as a GEMM (not inside the first block's backward passes)")
     ap.add_argument("--no-share", action="store_true", help="PPOL2C2's mixed batch through two stem forwards")
+    ap.add_argument("--no-rows", action="store_true", help="the graphed update gathers the mini-batch rows")
     ap.add_argument("--graph-update", action="store_true",
                     help="the update's mini-batch steps as hipGraph replays (ppo_l2c2._GraphedStepL2C2)")
     print(json.dumps(run(ap.parse_args(argv))))
@@ -66,6 +67,7 @@ def run(args):
     runner = OnPolicyRunner(env, d, log_dir=None, device=dev)
     runner.alg.share_mix_features = not getattr(args, "no_share", False)
     runner.alg.graph_update = bool(getattr(args, "graph_update", False))
+    runner.alg.rows_update = not getattr(args, "no_rows", False)
     pol = runner.alg.policy
     pol.fused_bn = not args.no_fused_bn
     pol.fused_conv2 = not getattr(args, "no_fused_conv2", False)

@@ -139,7 +139,7 @@ def test_stem12_rejects_shapes_it_does_not_cover():
     p = 0x10000  # aligned dummy device pointers: the checks return before any launch
 
     def call(c=16, na=720, nb=48, n2=80, gz2=p, w2t=p, act=_abi.GR_POLICY_ACT_LRELU):
-        return lib.gr_stem12_backward(p, 6928, 16, 8, p, na, nb, p, c, p, p, p, act, 0.01, gz2, n2, w2t, p, p, p, p,
+        return lib.gr_stem12_backward(p, 6928, 16, None, 8, p, na, nb, p, c, p, p, p, act, 0.01, gz2, n2, w2t, p, p, p, p,
                                       None)
 
     assert call(c=8) == -1
@@ -157,7 +157,7 @@ def test_stem12_forward_rejects_shapes_it_does_not_cover():
     p = 0x10000
 
     def call(c=16, na=720, n2=80, w2f=p, z2=p, act=_abi.GR_POLICY_ACT_LRELU):
-        return lib.gr_stem12_forward(p, 6928, 16, 8, p, na, 48, p, c, p, p, 1e-5, act, 0.01, w2f, n2, p, z2, p, p, None)
+        return lib.gr_stem12_forward(p, 6928, 16, None, 8, p, na, 48, p, c, p, p, 1e-5, act, 0.01, w2f, n2, p, z2, p, p, None)
 
     assert call(c=32) == -1
     assert call(na=718) == -1
@@ -224,3 +224,19 @@ def test_tsgemm_rejects_shapes_it_does_not_cover():
     assert call(ldc=32) == -1
     assert call(a=p + 2) == -1
     assert call(a=None) == -1
+
+
+def test_l2c2_mix_rows_rejects_bad_arguments():
+    """gr_l2c2_mix_rows: both row-index arrays, cols a multiple of 4, ld >= cols and a multiple of 4, 16-byte aligned
+    sources and output."""
+    lib = _abi.load()
+    p = 0x10000
+
+    def call(ra=p, ld=6928, cols=6928, out=p):
+        return lib.gr_l2c2_mix_rows(p, p, ld, ra, p, p, 8, cols, out, None)
+
+    assert call(ra=None) == -1
+    assert call(cols=6926) == -1
+    assert call(ld=6000) == -1
+    assert call(ld=6930) == -1
+    assert call(out=p + 4) == -1

@@ -177,3 +177,31 @@ def test_tsgemm_matches_float64(m, k, n, b_nk, lda):
     want = (a.double() @ (w.double().t() if b_nk else w.double())).cpu()
     assert _rel(o1, want) <= 1e-5, _rel(o1, want)
     assert torch.equal(o1, run())
+
+
+def test_features_through_row_indices_equal_gathered_rows():
+    """VisionActorCritic.features_rows(src, rows) (the fused first block reading the images through the indices, the
+    graphed L2C2 update's mini-batches) against features(src[rows]): features, every stem gradient and the BatchNorm
+    running statistics bit-identical; and gr_l2c2_mix_rows against the mix of gathered rows."""
+    from generalizableracing_amd.rsl_rl.ppo_l2c2 import _mix, _mix_rows
+
+    pol = _model((72, 96), "lrelu", seed=9)
+    g = torch.Generator(device=DEV).manual_seed(4)
+    src = torch.rand(700, 16 + 72 * 96, device=DEV, generator=g) * 8.0
+    rows = torch.randperm(700, device=DEV, generator=g)[:300]
+    gfeat = torch.randn(300, 64, device=DEV, generator=g)
+    out = []
+    for indexed in (False, True):
+        p = copy.deepcopy(pol)
+        p.zero_grad(set_to_none=True)
+        f = p.features_rows(src, rows) if indexed else p.features(src.index_select(0, rows))
+        (f * gfeat).sum().backward()
+        out.append((f.detach(), {k: q.grad.clone() for k, q in p.named_parameters() if q.grad is not None},
+                    {k: v.clone() for k, v in p.state_dict().items() if "running" in k or "num_batches" in k}))
+    (f0, g0, b0), (f1, g1, b1) = out
+    assert torch.equal(f0, f1)
+    assert set(g0) == set(g1) and all(torch.equal(g0[k], g1[k]) for k in g0)
+    assert all(torch.equal(b0[k], b1[k]) for k in b0)
+    nrows = (rows + 100) % 700
+    w = torch.rand(300, 1, device=DEV, generator=g) * 2.0 - 1.0
+    assert torch.equal(_mix_rows(src, rows, nrows, w), _mix(src.index_select(0, rows), src.index_select(0, nrows), w))
