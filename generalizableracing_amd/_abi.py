@@ -240,7 +240,8 @@ EXPORTS = [
     "gr_stem1_forward", "gr_stem1_backward", "gr_mlp_partials", "gr_mlp_forward", "gr_mlp_backward",
     "gr_mlp_args_size", "gr_step_kernel_variant", "gr_terrain_reserve", "gr_terrain_stage", "gr_terrain_commit",
     "gr_terrain_epoch", "gr_mlp_h1mask_words", "gr_stem12_backward", "gr_stem12_forward",
-    "gr_patch_wgrad_floats", "gr_patch_wgrad", "gr_bn_running_update", "gr_tsgemm", "gr_l2c2_mix_rows",
+    "gr_patch_wgrad_floats", "gr_patch_wgrad", "gr_bn_running_update", "gr_tsgemm", "gr_l2c2_mix_rows", "gr_tsgemm_bnact",
+    "gr_patch_wgrad_bnact", "gr_bn_stats",
 ]
 
 _lib = None
@@ -307,6 +308,11 @@ def _declare(lib):
         "gr_gae": (C.c_int, [C.c_int64, C.c_int32, C.c_float, C.c_float, vp, vp, vp, vp, C.c_int64, vp, vp, vp]),
         "gr_l2c2_mix": (C.c_int, [vp, vp, vp, C.c_int64, C.c_int32, vp, vp]),
         "gr_l2c2_mix_rows": (C.c_int, [vp, vp, C.c_int64, vp, vp, vp, C.c_int64, C.c_int32, vp, vp]),
+        "gr_tsgemm_bnact": (C.c_int, [vp, C.c_int64, vp, vp, C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int32, vp,
+                                      vp, vp, C.c_int32, C.c_float, vp]),
+        "gr_patch_wgrad_bnact": (C.c_int, [vp, C.c_int64, vp, C.c_int64, C.c_int32, C.c_int32, vp, vp, C.c_int32, vp,
+                                           vp, vp, C.c_int32, C.c_float, vp]),
+        "gr_bn_stats": (C.c_int, [vp, C.c_int64, C.c_int32, C.c_float, vp, vp, vp]),
         "gr_adam_clip": (C.c_int, [vp, C.c_float, vp, vp]),
         "gr_adam_step": (C.c_int, [vp, vp]),
         "gr_adam_clip_step": (C.c_int, [vp, C.c_float, vp, vp, vp, C.c_double, C.c_double, C.c_double, vp]),

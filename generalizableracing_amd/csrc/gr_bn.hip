@@ -273,6 +273,13 @@ hipError_t launch_bn_forward(const float* x, long long m, int c, const float* w,
   return hipGetLastError();
 }
 
+hipError_t launch_bn_stats(const float* x, long long m, int c, float eps, float* stats, double* part, hipStream_t s) {
+  const int nb = bn_blocks(m, c);
+  hipLaunchKernelGGL(bn_stats_partial, dim3(nb), dim3(BN_THREADS), 0, s, x, m, c, part);
+  hipLaunchKernelGGL(bn_stats_final, dim3(1), dim3(BN_FINAL_THREADS), 0, s, x, m, c, nb, eps, part, stats);
+  return hipGetLastError();
+}
+
 hipError_t launch_bn_backward(const float* x, const float* gy, long long m, int c, const float* w, const float* b,
                               const float* stats, int act, float slope, float* gx, float* gw, float* gb, double* part,
                               hipStream_t s) {

@@ -1011,7 +1011,34 @@ int gr_tsgemm(const float* a, int64_t lda, const float* b, int32_t b_nk, float* 
     return GR_ERR_ARG;
   if (m == 0) return GR_OK;
   const hipError_t e = gr::launch_tsgemm(a, (long long)lda, b, b_nk != 0, c, (long long)ldc, (long long)m, k, n,
+                                         nullptr, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
+static bool bnact_of(int32_t bn_c, const float* stats, const float* bn_w, const float* bn_b, int32_t act, float slope,
+                     gr::BnAct* p) {
+  if (!stats || !bn_w || !bn_b || !bn_shape_ok(1, bn_c) || (act != GR_POLICY_ACT_LRELU && act != GR_POLICY_ACT_ELU))
+    return false;
+  p->stats = stats; p->w = bn_w; p->b = bn_b; p->c = bn_c; p->act = act; p->slope = slope;
+  return true;
+}
+
+int gr_tsgemm_bnact(const float* z, int64_t lda, const float* b, float* c, int64_t ldc, int64_t m, int32_t k, int32_t n,
+                    int32_t bn_c, const float* stats, const float* bn_w, const float* bn_b, int32_t act, float slope,
+                    void* stream) {
+  gr::BnAct p;
+  if (!z || !b || !c || m < 0 || k != 128 || n != 64 || lda < k || ldc < n || ((uintptr_t)z & 3) || bn_c != 32 ||
+      !bnact_of(bn_c, stats, bn_w, bn_b, act, slope, &p) || m * (lda > ldc ? lda : ldc) >= ((int64_t)1 << 40))
+    return GR_ERR_ARG;
+  if (m == 0) return GR_OK;
+  const hipError_t e = gr::launch_tsgemm(z, (long long)lda, b, true, c, (long long)ldc, (long long)m, k, n, &p,
                                          (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
+int gr_bn_stats(const float* x, int64_t m, int32_t c, float eps, float* stats, double* part, void* stream) {
+  if (!bn_shape_ok(m, c) || !x || !stats || !part || !aligned16(x) || !aligned16(stats)) return GR_ERR_ARG;
+  const hipError_t e = gr::launch_bn_stats(x, m, c, eps, stats, part, (hipStream_t)stream);
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
@@ -1026,7 +1053,21 @@ int gr_patch_wgrad(const float* x, int64_t ld, const float* gy, int64_t m, int32
   if (!x || !gy || !part || !gw || m < 1 || gr::patch_wgrad_blocks(m, n, k) == 0 || ld < k || !aligned16(gy) ||
       ((uintptr_t)x & 3) || m * ld >= ((int64_t)1 << 40))
     return GR_ERR_ARG;
-  const hipError_t e = gr::launch_patch_wgrad(x, (long long)ld, gy, (long long)m, n, k, part, gw, (hipStream_t)stream);
+  const hipError_t e =
+      gr::launch_patch_wgrad(x, (long long)ld, gy, (long long)m, n, k, part, gw, nullptr, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
+int gr_patch_wgrad_bnact(const float* z, int64_t ld, const float* gy, int64_t m, int32_t n, int32_t k, float* part,
+                         float* gw, int32_t bn_c, const float* stats, const float* bn_w, const float* bn_b, int32_t act,
+                         float slope, void* stream) {
+  gr::BnAct p;
+  if (!z || !gy || !part || !gw || m < 1 || n % 64 || gr::patch_wgrad_blocks(m, n, k) == 0 || ld < k ||
+      !aligned16(gy) || ((uintptr_t)z & 3) || bn_c % 8 || 128 % bn_c || !bnact_of(bn_c, stats, bn_w, bn_b, act, slope, &p) ||
+      m * ld >= ((int64_t)1 << 40))
+    return GR_ERR_ARG;
+  const hipError_t e = gr::launch_patch_wgrad(z, (long long)ld, gy, (long long)m, n, k, part, gw, &p,
+                                              (hipStream_t)stream);
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 

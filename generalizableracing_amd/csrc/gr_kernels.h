@@ -134,11 +134,20 @@ hipError_t launch_bn_backward(const float* x, const float* gy, long long m, int 
                               hipStream_t s);
 int column_sum_blocks(long long m);                                                                       // gr_update.hip
 int patch_wgrad_blocks(long long m, int n, int k);  // gr_update.hip: gw[n][k] = gy^T x (0: (n, k) not covered)
+// a BatchNorm (batch statistics) + activation applied to a patch GEMM's input as it is loaded (gr_update.hip)
+struct BnAct {
+  const float* stats;  // [4][c]: mean, invstd, biased var, unbiased var (gr_bn_act_forward's)
+  const float* w;
+  const float* b;
+  int c, act;
+  float slope;
+};
 bool tsgemm_covered(int k, int n, bool b_nk);  // gr_update.hip: C[m][n] = A[m][k] B[k][n], B in registers
 hipError_t launch_tsgemm(const float* a, long long lda, const float* bm, bool b_nk, float* c, long long ldc,
-                         long long m, int k, int n, hipStream_t s);
+                         long long m, int k, int n, const BnAct* bna, hipStream_t s);
 hipError_t launch_patch_wgrad(const float* x, long long ld, const float* gy, long long m, int n, int k, float* part,
-                              float* gw, hipStream_t s);
+                              float* gw, const BnAct* bna, hipStream_t s);
+hipError_t launch_bn_stats(const float* x, long long m, int c, float eps, float* stats, double* part, hipStream_t s);
 hipError_t launch_column_sum(const void* x, int dtype, long long m, int n, float* part, float* out, hipStream_t s);
 int head_partial_rows(long long m);                                                                      // gr_update.hip
 int in_partial_rows(long long m);                                                                        // gr_update.hip

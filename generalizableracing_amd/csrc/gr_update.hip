@@ -90,6 +90,32 @@ __global__ __launch_bounds__(CF_WAVES * 64) void colsum_final(const float* __res
   }
 }
 
+// ------------------------------------------------------------- BatchNorm + activation applied on load
+// A patch GEMM whose input is act(bn(z)) (the vision stem's block 2 feeding conv3) can read z and apply the
+// BatchNorm's batch statistics and the activation as it loads, so act(bn(z)) is never written nor read back.  The
+// arithmetic is bn_apply's (gr_bn.hip): act(((z - mean) * invstd) * w + b), no contraction, so the values are
+// bit-identical to the materialised rows.  Column k of the patch rows is channel k % c.
+// (struct BnAct: gr_kernels.h)
+__device__ __forceinline__ float bnact_apply(float z, float mu, float is, float w, float b, int act, float slope) {
+  const float y = (z - mu) * is * w + b;
+  return act == GR_POLICY_ACT_ELU ? (y > 0.0f ? y : expm1f(y)) : (y > 0.0f ? y : y * slope);
+}
+// four consecutive channels' parameters c0 .. c0 + 3
+struct BnAct4 {
+  float mu[4], is[4], w[4], b[4];
+};
+__device__ __forceinline__ BnAct4 bnact_params(const BnAct& p, int c0) {
+  BnAct4 r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    r.mu[e] = p.stats[c0 + e];
+    r.is[e] = p.stats[p.c + c0 + e];
+    r.w[e] = p.w[c0 + e];
+    r.b[e] = p.b[c0 + e];
+  }
+  return r;
+}
+
 // ------------------------------------------------------------------ weight gradient of a tall patch GEMM
 // gw[n][K] = gy[M][n]^T x[M][K] over up to millions of rows, in slabs of N = 16 NT outputs (32 or 64): the vision
 // stem's conv2 (x = its input patches [M][144], n 32), conv3 ([M][128], n 64) and its final Linear ([M][1280],
@@ -112,12 +138,12 @@ typedef float pw2u __attribute__((ext_vector_type(2), aligned(4)));
 
 // (64 outputs: two waves per SIMD, which the compiler fits in 182 registers without spilling; same-box A/B r5pwi:
 // conv3 112 -> 96 us, the Linear 189 -> 164 us; the 32-output instances are faster as they are)
-template <int NT, int KT>
+template <int NT, int KT, bool BNA = false>
 __global__ __launch_bounds__(PW_WAVES * 64) __attribute__((amdgpu_waves_per_eu(NT == 4 ? 2 : 1)))
 void pw_partial(const float* __restrict__ x, long long ld,
                                                              const float* __restrict__ gy, long long m, int n_total,
                                                              int k_total, long long rows_per_wave,
-                                                             float* __restrict__ part) {
+                                                             float* __restrict__ part, BnAct bna) {
   constexpr int N = 16 * NT, KS = 16 * KT, PW_DEPTH = pw_depth<NT>();
   __shared__ float red[N * KS];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
@@ -128,6 +154,13 @@ void pw_partial(const float* __restrict__ x, long long ld,
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) acc[nt][kt] = pw4{0.0f, 0.0f, 0.0f, 0.0f};
+  // BNA: this lane's KT columns col0 + KT i .. + KT - 1 are channels (col0 + KT i) % c .. + KT - 1 (KT % 4 == 0,
+  // c a multiple of KT)
+  BnAct4 bp[BNA ? KT / 4 : 1];
+  if constexpr (BNA) {
+#pragma unroll
+    for (int u = 0; u < KT / 4; ++u) bp[u] = bnact_params(bna, (col0 + KT * i + 4 * u) % bna.c);
+  }
   const long long r0 = ((long long)blockIdx.x * PW_WAVES + w) * rows_per_wave;
   const long long r1 = r0 + rows_per_wave < m ? r0 + rows_per_wave : m;
   auto load_row = [&](long long r, float (&a)[NT], float (&b)[KT]) {
@@ -152,7 +185,18 @@ void pw_partial(const float* __restrict__ x, long long ld,
 #pragma unroll
     for (int d = 0; d < PW_DEPTH; ++d) load_row(q + 4 * d + g, a[d], b[d]);
   };
-  auto mma = [&](const float (&a)[PW_DEPTH][NT], const float (&b)[PW_DEPTH][KT]) {
+  // (BNA: the BatchNorm + activation is applied to a set when it is consumed, after the next set's loads were issued)
+  auto mma = [&](const float (&a)[PW_DEPTH][NT], float (&b)[PW_DEPTH][KT]) {
+    if constexpr (BNA) {
+#pragma unroll
+      for (int d = 0; d < PW_DEPTH; ++d)
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt) {
+          const BnAct4& q = bp[kt / 4];
+          const int e = kt % 4;
+          b[d][kt] = bnact_apply(b[d][kt], q.mu[e], q.is[e], q.w[e], q.b[e], bna.act, bna.slope);
+        }
+    }
 #pragma unroll
     for (int d = 0; d < PW_DEPTH; ++d)
 #pragma unroll
@@ -234,19 +278,23 @@ int patch_wgrad_blocks(long long m, int n, int k) {
 }
 
 hipError_t launch_patch_wgrad(const float* x, long long ld, const float* gy, long long m, int n, int k, float* part,
-                              float* gw, hipStream_t s) {
+                              float* gw, const BnAct* bna, hipStream_t s) {
   const int slab = pw_slab(n, k);
   const int blocks = patch_wgrad_blocks(m, n, k);
   if (!slab || !blocks) return hipErrorInvalidValue;
+  const BnAct none{};
   long long rpw = (m + (long long)blocks * PW_WAVES - 1) / ((long long)blocks * PW_WAVES);
   rpw = (rpw + 3) & ~3LL;
   const dim3 grid(blocks, (k / slab) * (n == 32 ? 1 : n / 64)), wg(PW_WAVES * 64);
-  if (n == 32 && k == 144)
-    hipLaunchKernelGGL((pw_partial<2, 9>), grid, wg, 0, s, x, ld, gy, m, n, k, rpw, part);
+  if (bna) {  // (covered: n 64 in 128-column slabs, c dividing 8 consecutive columns' channel run: c % 8 == 0)
+    if (n % 64 || bna->c % 8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((pw_partial<4, 8, true>), grid, wg, 0, s, x, ld, gy, m, n, k, rpw, part, *bna);
+  } else if (n == 32 && k == 144)
+    hipLaunchKernelGGL((pw_partial<2, 9>), grid, wg, 0, s, x, ld, gy, m, n, k, rpw, part, none);
   else if (n == 32)
-    hipLaunchKernelGGL((pw_partial<2, 8>), grid, wg, 0, s, x, ld, gy, m, n, k, rpw, part);
+    hipLaunchKernelGGL((pw_partial<2, 8>), grid, wg, 0, s, x, ld, gy, m, n, k, rpw, part, none);
   else
-    hipLaunchKernelGGL((pw_partial<4, 8>), grid, wg, 0, s, x, ld, gy, m, n, k, rpw, part);
+    hipLaunchKernelGGL((pw_partial<4, 8>), grid, wg, 0, s, x, ld, gy, m, n, k, rpw, part, none);
   hipLaunchKernelGGL(colsum_final, dim3((n * k + 63) / 64), dim3(CF_WAVES * 64), 0, s, part, blocks, n * k, gw);
   return hipGetLastError();
 }
@@ -264,10 +312,11 @@ hipError_t launch_patch_wgrad(const float* x, long long ld, const float* gy, lon
 typedef float ts4u __attribute__((ext_vector_type(4), aligned(4)));
 constexpr int TS_WAVES = 4;
 
-template <int K, int N, bool B_NK>
+template <int K, int N, bool B_NK, bool BNA = false>
 __global__ __launch_bounds__(TS_WAVES * 64) void tsgemm_kernel(const float* __restrict__ a, long long lda,
                                                                const float* __restrict__ bm, int n_total,
-                                                               float* __restrict__ c, long long ldc, long long m) {
+                                                               float* __restrict__ c, long long ldc, long long m,
+                                                               BnAct bna) {
   // N: this workgroup's slab of the n_total outputs (blockIdx.y)
   constexpr int S = K / 4, NT = N / 16, Q = K / 16, LDK = K + 4;
   __shared__ float bt[N * LDK];
@@ -279,6 +328,13 @@ __global__ __launch_bounds__(TS_WAVES * 64) void tsgemm_kernel(const float* __re
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  // BNA (c = 32 channels: the pattern repeats every two quads): quad q's four columns 16 q + 4 g .. + 3 are channels
+  // 16 (q % 2) + 4 g .. + 3
+  BnAct4 bp[BNA ? 2 : 1];
+  if constexpr (BNA) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) bp[u] = bnact_params(bna, 16 * u + 4 * g);
+  }
   const long long tiles = (m + 15) / 16;
   const long long wave = (long long)blockIdx.x * TS_WAVES + (threadIdx.x >> 6);
   const long long stride = (long long)gridDim.x * TS_WAVES;
@@ -292,7 +348,17 @@ __global__ __launch_bounds__(TS_WAVES * 64) void tsgemm_kernel(const float* __re
       av[4 * q] = v.x; av[4 * q + 1] = v.y; av[4 * q + 2] = v.z; av[4 * q + 3] = v.w;
     }
   };
-  auto tile = [&](long long t, const float (&av)[S]) {
+  // (BNA: the BatchNorm + activation is applied when the tile is consumed, a tile after its loads were issued, so the
+  // loads' latency stays hidden under the previous tile's MFMAs)
+  auto tile = [&](long long t, float (&av)[S]) {
+    if constexpr (BNA) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          av[4 * q + e] = bnact_apply(av[4 * q + e], bp[q % 2].mu[e], bp[q % 2].is[e], bp[q % 2].w[e], bp[q % 2].b[e],
+                                      bna.act, bna.slope);
+    }
     pw4 acc[NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[nt] = pw4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -340,21 +406,25 @@ bool tsgemm_covered(int k, int n, bool b_nk) {
 }
 
 hipError_t launch_tsgemm(const float* a, long long lda, const float* bm, bool b_nk, float* c, long long ldc,
-                         long long m, int k, int n, hipStream_t s) {
+                         long long m, int k, int n, const BnAct* bna, hipStream_t s) {
   if (!tsgemm_covered(k, n, b_nk)) return hipErrorInvalidValue;
+  const BnAct none{};
   const long long tiles = (m + 15) / 16;
   long long blocks = (tiles + TS_WAVES - 1) / TS_WAVES;
   blocks = blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks);  // 256 CUs x 4 workgroups, walked in strides
   const dim3 wg(TS_WAVES * 64);
-  if (k == 128)
-    hipLaunchKernelGGL((tsgemm_kernel<128, 64, true>), dim3(blocks), wg, 0, s, a, lda, bm, n, c, ldc, m);
+  if (bna) {  // (covered: conv3's forward from block 2's BatchNorm input, c dividing 4-column runs)
+    if (k != 128 || bna->c != 32) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((tsgemm_kernel<128, 64, true, true>), dim3(blocks), wg, 0, s, a, lda, bm, n, c, ldc, m, *bna);
+  } else if (k == 128)
+    hipLaunchKernelGGL((tsgemm_kernel<128, 64, true>), dim3(blocks), wg, 0, s, a, lda, bm, n, c, ldc, m, none);
   else if (k == 64)
-    hipLaunchKernelGGL((tsgemm_kernel<64, 128, false>), dim3(blocks), wg, 0, s, a, lda, bm, n, c, ldc, m);
+    hipLaunchKernelGGL((tsgemm_kernel<64, 128, false>), dim3(blocks), wg, 0, s, a, lda, bm, n, c, ldc, m, none);
   else {  // 64-output slabs: about 1 024 workgroups over rows x slabs
     const long long slabs = n / 64;
     long long rb = (1024 + slabs - 1) / slabs;
     rb = rb < blocks ? rb : blocks;
-    hipLaunchKernelGGL((tsgemm_kernel<192, 64, false>), dim3(rb, slabs), wg, 0, s, a, lda, bm, n, c, ldc, m);
+    hipLaunchKernelGGL((tsgemm_kernel<192, 64, false>), dim3(rb, slabs), wg, 0, s, a, lda, bm, n, c, ldc, m, none);
   }
   return hipGetLastError();
 }

@@ -212,6 +212,89 @@ class _Stem12(torch.autograd.Function):
         return None, gconv.view(wshape), gbw, gbb, gw2, None, None, None, None, None, None, None, None
 
 
+class _BnActPatchGemm(torch.autograd.Function):
+    """y = act(bn(z)).view(-1, k) @ w^T without writing act(bn(z)): the vision stem's block 2 (BatchNorm2d(32) ->
+    LeakyReLU on conv2's output rows z [M, 32]) feeding conv3 (w [64, 128], its 2 x 2 patches of four consecutive
+    rows).  Forward: the BatchNorm's statistics pass (gr_bn_stats), then conv3 with the BatchNorm and activation
+    applied as the rows are loaded (gr_tsgemm_bnact).  Backward: conv3's input gradient (gr_tsgemm), its weight
+    gradient recomputing act(bn(z)) on load (gr_patch_wgrad_bnact), and the BatchNorm + activation backward
+    (gr_bn_act_backward) on z.  The same values as batch_norm_act then the patch GEMM (the applied rows are
+    bit-identical to gr_bn_act_forward's)."""
+
+    @staticmethod
+    def forward(ctx, z, bn_w, bn_b, w, eps, act, slope):
+        lib = _abi.load()
+        m, c = z.shape
+        n, k = w.shape
+        stats = torch.empty(4, c, device=z.device, dtype=torch.float32)
+        part = torch.empty(int(lib.gr_bn_scratch_doubles(m, c)), device=z.device, dtype=torch.float64)
+        rc = lib.gr_bn_stats(z.data_ptr(), m, c, float(eps), stats.data_ptr(), part.data_ptr(), _stream(z))
+        if rc != 0:
+            raise RuntimeError(f"gr_bn_stats failed (status {rc})")
+        bw, bb, wd = bn_w.detach().contiguous(), bn_b.detach().contiguous(), w.detach().contiguous()
+        mp = m * c // k
+        y = torch.empty(mp, n, device=z.device, dtype=torch.float32)
+        rc = lib.gr_tsgemm_bnact(z.data_ptr(), k, wd.data_ptr(), y.data_ptr(), n, mp, k, n, c, stats.data_ptr(),
+                                 bw.data_ptr(), bb.data_ptr(), act, float(slope), _stream(z))
+        if rc != 0:
+            raise RuntimeError(f"gr_tsgemm_bnact failed (status {rc})")
+        ctx.save_for_backward(z, bw, bb, stats, wd)
+        ctx.act, ctx.slope = act, slope
+        ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, gy, _gstats):
+        lib = _abi.load()
+        z, bw, bb, stats, w = ctx.saved_tensors
+        m, c = z.shape
+        n, k = w.shape
+        mp = m * c // k
+        gy = gy.contiguous()
+        dev = z.device
+        gw = None
+        if ctx.needs_input_grad[3]:  # conv3's weight: gy^T act(bn(z)), recomputed on load
+            gw = torch.empty(n, k, device=dev, dtype=torch.float32)
+            wpart = torch.empty(int(lib.gr_patch_wgrad_floats(mp, n, k)), device=dev, dtype=torch.float32)
+            rc = lib.gr_patch_wgrad_bnact(z.data_ptr(), k, gy.data_ptr(), mp, n, k, wpart.data_ptr(), gw.data_ptr(), c,
+                                          stats.data_ptr(), bw.data_ptr(), bb.data_ptr(), ctx.act, float(ctx.slope),
+                                          _stream(z))
+            if rc != 0:
+                raise RuntimeError(f"gr_patch_wgrad_bnact failed (status {rc})")
+        # the gradient of act(bn(z)) = gy w, then the BatchNorm + activation backward on z
+        dblock = torch.empty(mp, k, device=dev, dtype=torch.float32)
+        rc = lib.gr_tsgemm(gy.data_ptr(), n, w.data_ptr(), 0, dblock.data_ptr(), k, mp, n, k, _stream(z))
+        if rc != 0:
+            raise RuntimeError(f"gr_tsgemm failed (status {rc})")
+        gx = torch.empty_like(z)
+        gbw = torch.empty(c, device=dev, dtype=torch.float32)
+        gbb = torch.empty(c, device=dev, dtype=torch.float32)
+        part = torch.empty(int(lib.gr_bn_scratch_doubles(m, c)), device=dev, dtype=torch.float64)
+        rc = lib.gr_bn_act_backward(z.data_ptr(), dblock.data_ptr(), m, c, bw.data_ptr(), bb.data_ptr(),
+                                    stats.data_ptr(), ctx.act, float(ctx.slope), gx.data_ptr(), gbw.data_ptr(),
+                                    gbb.data_ptr(), part.data_ptr(), _stream(z))
+        if rc != 0:
+            raise RuntimeError(f"gr_bn_act_backward failed (status {rc})")
+        return gx, gbw, gbb, gw, None, None, None
+
+
+def bn_act_conv_applicable(bn: nn.BatchNorm2d, act: nn.Module, z: torch.Tensor, w: torch.Tensor) -> bool:
+    """_BnActPatchGemm covers block 2 -> conv3: fused_applicable(bn, act, z) with 32 channels, w [64, 128] fp32, the
+    patches four consecutive rows."""
+    return (fused_applicable(bn, act, z) and z.shape[1] == 32 and tuple(w.shape) == (64, 128)
+            and w.dtype == torch.float32 and (z.shape[0] * 32) % 128 == 0)
+
+
+def bn_act_conv(bn: nn.BatchNorm2d, act: nn.Module, z: torch.Tensor, w: torch.Tensor, uses: int = 1,
+                count_first: bool = False) -> torch.Tensor:
+    """act(bn(z)).view(-1, 128) @ w^T (block 2 into conv3) without materialising act(bn(z)); running statistics updated
+    as batch_norm_act does."""
+    code, slope = _act_code(act)
+    y, stats = _BnActPatchGemm.apply(z, bn.weight, bn.bias, w, bn.eps, code, slope)
+    _update_running(bn, stats, uses, count_first)
+    return y
+
+
 def stem12_applicable(bn: nn.BatchNorm2d, act: nn.Module, img: torch.Tensor, conv_w: torch.Tensor,
                       conv2_w: torch.Tensor, na: int) -> bool:
     """The fused first block + conv2 backward: stem1_applicable with 16 channels, conv2 = Conv2d(16, 32, 3, stride 3)

@@ -25,8 +25,8 @@ import torch.nn.functional as F
 
 from . import linear as _lin
 from .actor_critic import ActorCritic, resolve_nn_activation
-from .fused_bn import (batch_norm_act, fused_applicable, stem1_applicable, stem1_bn_act, stem12_applicable,
-                       stem12_bn_act_conv)
+from .fused_bn import (batch_norm_act, bn_act_conv, bn_act_conv_applicable, fused_applicable, stem1_applicable,
+                       stem1_bn_act, stem12_applicable, stem12_bn_act_conv)
 
 
 def _conv_out(n: int, k: int, s: int) -> int:
@@ -128,6 +128,8 @@ class VisionActorCritic(ActorCritic):
     fused_conv2 = True
     # with fused_conv2: conv2's forward inside the first block's apply pass too (False: conv2's forward as a GEMM)
     fused_conv2_forward = True
+    # with fused_conv2: block 2's BatchNorm + activation applied as conv3 loads its rows (never written)
+    fused_conv3 = True
 
     def __init__(self, num_actor_obs: int, num_critic_obs: int, num_actions: int, img_res=(72, 96),
                  dim_hidden_input: int = 192, actor_hidden_dims=(256, 256, 256), critic_hidden_dims=(256, 256, 256),
@@ -252,11 +254,17 @@ class VisionActorCritic(ActorCritic):
         B = flat.shape[0] if rows is None else rows.numel()
         w2m = conv2.weight.permute(0, 2, 3, 1).reshape(32, 144)  # conv2 on its 3x3 patches, columns (i, j, c)
         block2 = None
+        w3m = conv3.weight.permute(0, 2, 3, 1).reshape(64, 128)  # conv3 on its 2x2 patches, columns (i, j, c)
+        z3 = None
         if fused12:
             # conv1 + BN1 + act + conv2: the backward forms conv2's input gradient inside the first block's passes
             z2 = stem12_bn_act_conv(bn1, act, conv1.weight, w2m, flat, pix16, n1, n1_left, self._bn_uses,
                                     self.fused_conv2_forward, count_first=True, rows=rows)
-            block2 = self._bn_act(bn2, act, z2)
+            if self.fused_conv3 and n3 == n2 and bn_act_conv_applicable(bn2, act, z2, w3m):
+                # block 2 straight into conv3: act(bn2(z2)) applied as conv3 loads its rows, never written
+                z3 = bn_act_conv(bn2, act, z2, w3m, self._bn_uses, count_first=True)
+            else:
+                block2 = self._bn_act(bn2, act, z2)
         elif self.fused_bn and stem1_applicable(bn1, act, flat, conv1.weight):
             # conv1 + BN1 + act from the image itself: no patch matrix, no conv output (rsl_rl/fused_bn.py)
             y = stem1_bn_act(bn1, act, conv1.weight, flat, pix16, n1, n1_left, self._bn_uses, count_first=True,
@@ -266,14 +274,16 @@ class VisionActorCritic(ActorCritic):
             if n1_left:
                 x = torch.cat([x, flat.index_select(1, idx_left).view(B * n1_left, 9)])
             y = self._bn_act(bn1, act, _gemm(x, conv1.weight.reshape(16, 9)))
-        if block2 is None:
+        if block2 is None and z3 is None:
             # conv2's 3x3 patches (i, j, c): a view (the fused block returns exactly these rows; a slice of the whole
             # tensor would still cost a zero-filled gradient plus a copy in the backward)
             x = (y if y.shape[0] == B * n1 else y[: B * n1]).view(B * n2, 144)
             block2 = self._bn_act(bn2, act, _gemm(x, w2m))
-        y = block2.view(B, n2, 32)
-        x = (y if n3 == n2 else y[:, :n3]).reshape(B * h3 * w3, 128)  # conv3's 2x2 patches: a view at 72x96
-        y = self._bn_act(bn3, act, _gemm(x, conv3.weight.permute(0, 2, 3, 1).reshape(64, 128))).view(B, h3 * w3 * 64)
+        if z3 is None:
+            y = block2.view(B, n2, 32)
+            x = (y if n3 == n2 else y[:, :n3]).reshape(B * h3 * w3, 128)  # conv3's 2x2 patches: a view at 72x96
+            z3 = _gemm(x, w3m)
+        y = self._bn_act(bn3, act, z3).view(B, h3 * w3 * 64)
         # reference flatten is NCHW (c, h, w): permute the Linear's columns to (h, w, c) instead
         wl = lin.weight.view(-1, 64, h3, w3).permute(0, 2, 3, 1).reshape(lin.weight.shape[0], -1)
         return _gemm(y, wl, lin.bias if extra_bias is None else lin.bias + extra_bias)

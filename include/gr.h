@@ -476,6 +476,22 @@ int gr_stem1_backward(const float* obs, int64_t ld, int64_t off, const int64_t* 
  * fp32 MFMA chain over k. */
 int gr_tsgemm(const float* a, int64_t lda, const float* b, int32_t b_nk, float* c, int64_t ldc, int64_t m, int32_t k,
               int32_t n, void* stream);
+/* The same GEMMs with a BatchNorm + activation applied to A as it is loaded: A = act(bn(z)) with the batch statistics
+ * `stats` [4][bn_c] (gr_bn_stats / gr_bn_act_forward's), affine bn_w / bn_b, act GR_POLICY_ACT_LRELU (slope) or ELU;
+ * column k of z is channel k % bn_c (bn_c 32 for gr_tsgemm_bnact).  The vision stem's block 2 feeds conv3 this way (vision_actor_critic.py:93-105:
+ * BatchNorm2d(32) -> LeakyReLU -> Conv2d(32, 64, 2, 2)): act(bn(z2)) is never written.  gr_tsgemm_bnact: conv3's
+ * forward (k 128, n 64, b = W3 [64][128]); gr_patch_wgrad_bnact: its weight gradient gy^T act(bn(z)) (n a multiple
+ * of 64, bn_c a multiple of 8 dividing 128).  Values bit-identical to the materialised act(bn(z)) (gr_bn_act_forward's
+ * arithmetic). */
+int gr_tsgemm_bnact(const float* z, int64_t lda, const float* b, float* c, int64_t ldc, int64_t m, int32_t k, int32_t n,
+                    int32_t bn_c, const float* stats, const float* bn_w, const float* bn_b, int32_t act, float slope,
+                    void* stream);
+int gr_patch_wgrad_bnact(const float* z, int64_t ld, const float* gy, int64_t m, int32_t n, int32_t k, float* part,
+                         float* gw, int32_t bn_c, const float* stats, const float* bn_w, const float* bn_b, int32_t act,
+                         float slope, void* stream);
+/* A training-mode BatchNorm's batch statistics alone (gr_bn_act_forward's stats pass): stats [4][c] = mean, invstd,
+ * biased var, unbiased var of x [m][c]; `part` as gr_bn_act_forward's. */
+int gr_bn_stats(const float* x, int64_t m, int32_t c, float eps, float* stats, double* part, void* stream);
 /* Weight gradient of a tall patch GEMM: gw[n][k] = gy[m][n]^T x[m][k] (fp32; gy row-major, 16-byte aligned; x rows
  * `ld` floats apart, 4-byte aligned), the vision stem's conv2 (n 32, k 144), conv3 (n 64, k 128) and final Linear
  * (n 192, k 1280) weight gradients (standalone/rsl_rl/ext/modules/vision_actor_critic.py:93-105; torch's

@@ -48,6 +48,7 @@ def main(argv=None):
                     help="conv2's input gradient as a GEMM (not inside the first block's backward passes)")
     ap.add_argument("--no-share", action="store_true", help="PPOL2C2's mixed batch through two stem forwards")
     ap.add_argument("--no-rows", action="store_true", help="the graphed update gathers the mini-batch rows")
+    ap.add_argument("--no-fused-conv3", action="store_true", help="block 2 materialised before conv3")
     ap.add_argument("--graph-update", action="store_true",
                     help="the update's mini-batch steps as hipGraph replays (ppo_l2c2._GraphedStepL2C2)")
     print(json.dumps(run(ap.parse_args(argv))))
@@ -72,6 +73,7 @@ def run(args):
     pol.fused_bn = not args.no_fused_bn
     pol.fused_conv2 = not getattr(args, "no_fused_conv2", False)
     pol.fused_conv2_forward = not getattr(args, "no_fused_conv2_forward", False)
+    pol.fused_conv3 = not getattr(args, "no_fused_conv3", False)
     obs, extras = env.get_observations()
     crit = extras["observations"]["critic"]
     g = torch.Generator(device=dev).manual_seed(1)

@@ -205,3 +205,46 @@ def test_features_through_row_indices_equal_gathered_rows():
     nrows = (rows + 100) % 700
     w = torch.rand(300, 1, device=DEV, generator=g) * 2.0 - 1.0
     assert torch.equal(_mix_rows(src, rows, nrows, w), _mix(src.index_select(0, rows), src.index_select(0, nrows), w))
+
+
+@pytest.mark.parametrize("m,act", [(24_576 * 80, "lrelu"), (4 * 777, "elu")])
+def test_block2_into_conv3_equals_materialised_block(m, act):
+    """fused_bn.bn_act_conv (block 2's BatchNorm + activation applied as conv3 loads its rows: gr_bn_stats,
+    gr_tsgemm_bnact; backward gr_tsgemm, gr_patch_wgrad_bnact, gr_bn_act_backward) against batch_norm_act then the
+    patch GEMM on the materialised rows: conv3's output, every gradient and the running statistics bit-identical
+    (the same kernels and arithmetic), and within 1e-5 / 1e-4 of float64."""
+    from generalizableracing_amd.rsl_rl.fused_bn import batch_norm_act, bn_act_conv
+    from generalizableracing_amd.rsl_rl.vision_actor_critic import _PatchGemm
+
+    torch.manual_seed(m % 1000)
+    a = nn.LeakyReLU(0.01) if act == "lrelu" else nn.ELU()
+    bn = nn.BatchNorm2d(32).to(DEV)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.3, 0.3)
+    w = (torch.randn(64, 128, device=DEV) * 0.1).requires_grad_()
+    z = (torch.randn(m, 32, device=DEV) * 2.0 + 0.5).requires_grad_()
+    gy = torch.randn(m // 4, 64, device=DEV)
+    res = []
+    for fused in (True, False):
+        b = copy.deepcopy(bn)
+        ww = w.detach().clone().requires_grad_()
+        zz = z.detach().clone().requires_grad_()
+        if fused:
+            y = bn_act_conv(b, a, zz, ww, count_first=True)
+        else:
+            b.num_batches_tracked.add_(1)
+            y = _PatchGemm.apply(batch_norm_act(b, a, zz).view(-1, 128), ww)
+        (y * gy).sum().backward()
+        res.append((y.detach(), zz.grad, ww.grad, b.weight.grad, b.bias.grad, b.running_mean.clone(),
+                    b.running_var.clone(), int(b.num_batches_tracked)))
+    for x0, x1 in zip(*res):
+        assert (x0 == x1) if isinstance(x0, int) else torch.equal(x0, x1)
+    # float64: y = act(bn(z)) patches @ w^T
+    zd = z.detach().double()
+    mu, var = zd.mean(0), zd.var(0, unbiased=False)
+    h = (zd - mu) / torch.sqrt(var + bn.eps) * bn.weight.double() + bn.bias.double()
+    h = torch.where(h > 0, h, h * 0.01) if act == "lrelu" else torch.where(h > 0, h, torch.expm1(h))
+    y64 = h.view(-1, 128) @ w.detach().double().t()
+    assert _rel(res[0][0], y64) <= 1e-5
+    assert _rel(res[0][2], gy.double().t() @ h.view(-1, 128)) <= 1e-4
