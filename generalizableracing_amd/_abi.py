@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgr.so")
 
 # ---- constants (include/gr.h) ----
-GR_ABI_VERSION = 3
+GR_ABI_VERSION = 4
 GR_INTEGRATOR_DD_EXPLICIT = 0
 GR_INTEGRATOR_SEMI_IMPLICIT = 1
 

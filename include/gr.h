@@ -36,8 +36,9 @@ extern "C" {
 #endif
 
 /* 2: GR_NUM_PLANES 17 (obstacle hint, rotor constants), gr_policy_args.precision, the observation sink and the
- * status word; gr_policy_args_size */
-#define GR_ABI_VERSION 3
+ * status word; gr_policy_args_size.  3: gr_stem1_* y_rows / gy_rows.  4: the gr_stem1_* / gr_stem12_* row indices
+ * (`rows` after `off`) */
+#define GR_ABI_VERSION 4
 
 /* ---- status codes ---- */
 #define GR_OK 0
