@@ -125,10 +125,13 @@ class PPOL2C2(PPO):
         self.transition.clear()
         self.policy.reset(dones)
 
-    def smooth_loss(self, obs_batch, next_obs_batch, cont_batch, mu_batch, value_batch, rows=None):
+    def smooth_loss(self, obs_batch, next_obs_batch, cont_batch, mu_batch, value_batch, rows=None,
+                    want_smoothness=True):
         """ppo_l2c2.py:176-188; returns (smooth_loss, action_smoothness).  rows (src, idx, next_idx): the pair is
         src[idx], src[next_idx] (the rollout storage's rows, read through the indices; obs_batch / next_obs_batch
-        unused)."""
+        unused).  want_smoothness False (the update, which never reads it, ppo_l2c2.py:188-191): action_smoothness is
+        None and the successor forward runs only for its side effects, the BatchNorm statistics of a training-mode
+        forward (policies with record_batch_statistics; none for the others)."""
         policy_coef, value_coef = self.smooth_coefs()
         mix_weights = cont_batch * (self._mix_uniform(cont_batch) - 0.5) * 2.0
         if rows is not None:
@@ -148,6 +151,11 @@ class PPOL2C2(PPO):
         value_smooth = torch.square(torch.norm(value_batch - mix_value, dim=-1)).mean()
         loss = policy_coef * policy_smooth + value_coef * value_smooth
         with torch.inference_mode():
+            if not want_smoothness:
+                record = getattr(self.policy, "record_batch_statistics", None)
+                if record is not None:
+                    record(*((rows[0], rows[2]) if rows is not None else (next_obs_batch,)))
+                return loss, None
             if rows is not None:
                 next_mean = self.policy.actor(self.policy.features_rows(rows[0], rows[2]))
             else:
@@ -184,7 +192,8 @@ class PPOL2C2(PPO):
                                                           advantages_batch, value_batch, target_values_batch,
                                                           returns_batch)
             loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_batch.mean()
-            smooth_loss, _ = self.smooth_loss(obs_batch, next_obs_batch, cont_batch, mu_batch, value_batch)
+            smooth_loss, _ = self.smooth_loss(obs_batch, next_obs_batch, cont_batch, mu_batch, value_batch,
+                                              want_smoothness=False)
             loss = loss + smooth_loss
             self.optimizer.zero_grad(set_to_none=False)
             if not self._grads_checked:
@@ -282,7 +291,8 @@ class _GraphedStepL2C2(_GraphedStep):
             self.flat.extra[:1] if self._adaptive() else None, None)
         if alg.entropy_coef != 0.0:
             loss = loss - alg.entropy_coef * (0.5 + 0.5 * math.log(2.0 * math.pi) + torch.log(std)).sum()
-        smooth_loss, _ = alg.smooth_loss(None, None, cont, mu_b, value_b, rows=(src, idx, nidx))
+        smooth_loss, _ = alg.smooth_loss(None, None, cont, mu_b, value_b, rows=(src, idx, nidx),
+                                         want_smoothness=False)
         self.acc[2:].add_(smooth_loss.detach())
         self._backward(loss + smooth_loss)
 
@@ -306,7 +316,7 @@ class _GraphedStepL2C2(_GraphedStep):
                 self.flat.extra[:1] if self._adaptive() else None, None)
             if alg.entropy_coef != 0.0:  # Normal.entropy summed over the actions: the same for every sample
                 loss = loss - alg.entropy_coef * (0.5 + 0.5 * math.log(2.0 * math.pi) + torch.log(std)).sum()
-            smooth_loss, _ = alg.smooth_loss(obs, nxt, cont, mu_b, value_b)
+            smooth_loss, _ = alg.smooth_loss(obs, nxt, cont, mu_b, value_b, want_smoothness=False)
             self.acc[2:].add_(smooth_loss.detach())
             self._backward(loss + smooth_loss)
             return
@@ -322,7 +332,7 @@ class _GraphedStepL2C2(_GraphedStep):
                 self.flat.extra[0].copy_(torch.mean(kl))
         surrogate_loss, value_loss = alg._ppo_losses(logp_b, logp, adv, value_b, val, ret)
         loss = surrogate_loss + alg.value_loss_coef * value_loss - alg.entropy_coef * entropy_b.mean()
-        smooth_loss, _ = alg.smooth_loss(obs, nxt, cont, mu_b, value_b)
+        smooth_loss, _ = alg.smooth_loss(obs, nxt, cont, mu_b, value_b, want_smoothness=False)
         loss = loss + smooth_loss
         self.acc.add_(torch.stack([surrogate_loss.detach(), value_loss.detach(), smooth_loss.detach()]))
         self._backward(loss)

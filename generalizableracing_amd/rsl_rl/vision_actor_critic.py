@@ -211,6 +211,37 @@ class VisionActorCritic(ActorCritic):
             return batch_norm_act(bn, act, x, self._bn_uses, count_first=True)
         return act(self._bn(bn, x))
 
+    def _bn_statistics(self, bn: nn.BatchNorm2d, x: torch.Tensor) -> None:
+        """A training-mode forward's effect on bn without its output: the running statistics and batch count."""
+        if not (bn.training and bn.track_running_stats):
+            return
+        if x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.is_contiguous() \
+                and x.shape[1] in (4, 8, 16, 32, 64) and x.shape[0] >= 2 and self.fused_bn:
+            from .. import _abi
+            from .fused_bn import _stream, _update_running
+
+            lib = _abi.load()
+            m, c = x.shape
+            stats = torch.empty(4, c, device=x.device, dtype=torch.float32)
+            part = torch.empty(int(lib.gr_bn_scratch_doubles(m, c)), device=x.device, dtype=torch.float64)
+            rc = lib.gr_bn_stats(x.data_ptr(), m, c, float(bn.eps), stats.data_ptr(), part.data_ptr(), _stream(x))
+            if rc != 0:
+                raise RuntimeError(f"gr_bn_stats failed (status {rc})")
+            _update_running(bn, stats, self._bn_uses, count_first=True)
+            return
+        self._bn(bn, x.detach())
+
+    def record_batch_statistics(self, observations: torch.Tensor, rows: torch.Tensor | None = None) -> None:
+        """What a training-mode forward of these rows changes besides its output: every BatchNorm's running
+        statistics and batch count (the stem up to block 3's statistics; no final Linear, state encoder or heads).
+        PPOL2C2's update evaluates the policy on the successor observations only for that side effect
+        (ppo_l2c2.py:188-189: `action_smoothness` is computed under inference mode and never used)."""
+        if rows is None:
+            img = observations[:, -self.num_pixels:].reshape(-1, 1, *self.img_res)
+        else:
+            img = observations[:, -self.num_pixels:]
+        self.stem_gemm(img, rows=rows, statistics_only=True)
+
     def _patch_index(self, device):
         """Pixel indices of conv1's patches, rows ordered so that every later layer's input is a VIEW of
         the previous layer's output: conv1 rows feeding conv2 come grouped as conv2's 3x3 patches,
@@ -239,7 +270,7 @@ class VisionActorCritic(ActorCritic):
         return self._pidx
 
     def stem_gemm(self, img: torch.Tensor, extra_bias: torch.Tensor | None = None,
-                  rows: torch.Tensor | None = None) -> torch.Tensor:
+                  rows: torch.Tensor | None = None, statistics_only: bool = False) -> torch.Tensor | None:
         """The conv stem as patch GEMMs (identical math to self.stem(img), other summation order); extra_bias is added
         to the final Linear's bias (features() passes the state encoder's).  rows: the batch is img[rows], read
         through the indices by the fused first block (the other paths gather it)."""
@@ -283,6 +314,9 @@ class VisionActorCritic(ActorCritic):
             y = block2.view(B, n2, 32)
             x = (y if n3 == n2 else y[:, :n3]).reshape(B * h3 * w3, 128)  # conv3's 2x2 patches: a view at 72x96
             z3 = _gemm(x, w3m)
+        if statistics_only:  # (record_batch_statistics: block 3's statistics are the last thing it needs)
+            self._bn_statistics(bn3, z3)
+            return None
         y = self._bn_act(bn3, act, z3).view(B, h3 * w3 * 64)
         # reference flatten is NCHW (c, h, w): permute the Linear's columns to (h, w, c) instead
         wl = lin.weight.view(-1, 64, h3, w3).permute(0, 2, 3, 1).reshape(lin.weight.shape[0], -1)

@@ -248,3 +248,25 @@ def test_block2_into_conv3_equals_materialised_block(m, act):
     y64 = h.view(-1, 128) @ w.detach().double().t()
     assert _rel(res[0][0], y64) <= 1e-5
     assert _rel(res[0][2], gy.double().t() @ h.view(-1, 128)) <= 1e-4
+
+
+@pytest.mark.parametrize("indexed", [False, True])
+def test_record_batch_statistics_gpu(indexed):
+    """record_batch_statistics on the fused GPU path (the stem to block 3's statistics, gr_bn_stats) leaves every
+    BatchNorm buffer bit-identical to a training-mode forward of the same rows (directly or through row indices)."""
+    pol = _model((72, 96), "lrelu", seed=12)
+    g = torch.Generator(device=DEV).manual_seed(6)
+    src = torch.rand(400, 16 + 72 * 96, device=DEV, generator=g) * 8.0
+    rows = torch.randperm(400, device=DEV, generator=g)[:256]
+    p1, p2 = copy.deepcopy(pol), copy.deepcopy(pol)
+    with torch.inference_mode():
+        if indexed:
+            p1.features_rows(src, rows)
+            p2.record_batch_statistics(src, rows)
+        else:
+            p1.features(src[rows])
+            p2.record_batch_statistics(src[rows])
+    s1, s2 = p1.state_dict(), p2.state_dict()
+    for k in s1:
+        if "running" in k or "num_batches" in k:
+            assert torch.equal(s1[k], s2[k]), k

@@ -1,5 +1,6 @@
 """VisionActorCritic (standalone/rsl_rl/ext/modules/vision_actor_critic.py:43-144) and the vision
 PPOL2C2 recipe (rsl_rl_ppo_cfg.py:43-52,80-104) on CPU, against the oracle camera VecEnv."""
+import copy
 import math
 
 import torch
@@ -157,3 +158,19 @@ def test_l2c2_shared_mix_features_match_two_stem_forwards():
             assert torch.equal(s1[k], s2[k]), k
         else:
             torch.testing.assert_close(s2[k], s1[k], rtol=1e-4, atol=1e-6, msg=k)
+
+
+def test_record_batch_statistics_equals_a_training_forward():
+    """VisionActorCritic.record_batch_statistics (what PPOL2C2's update keeps of its successor forward: the
+    BatchNorm running statistics and batch counts) leaves the buffers exactly as a training-mode forward does."""
+    torch.manual_seed(2)
+    p1 = policy()
+    p2 = copy.deepcopy(p1)
+    obs = torch.rand(5, OBS)
+    with torch.inference_mode():
+        p1.act_inference(obs)
+        p2.record_batch_statistics(obs)
+    s1, s2 = p1.state_dict(), p2.state_dict()
+    for k in s1:
+        if "running" in k or "num_batches" in k:
+            assert torch.equal(s1[k], s2[k]), k
