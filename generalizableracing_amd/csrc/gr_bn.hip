@@ -1193,7 +1193,7 @@ __global__ __launch_bounds__(SMF_THREADS) void stem12f_kernel(Stem1 s, Sm12fArgs
           for (int v = 0; v < 4; ++v) yv[v] = bn_act<ACT>((x[v] - mu[v]) * is[v] * wv[v] + bv[v], q.slope);
           y4.x = yv[0]; y4.y = yv[1]; y4.z = yv[2]; y4.w = yv[3];
           const unsigned r = (unsigned)b * (unsigned)na + (unsigned)(9 * p + jj);
-          if (ok && r < rows) reinterpret_cast<float4*>(q.y + (size_t)r * 16)[kq] = y4;
+          if (q.y && ok && r < rows) reinterpret_cast<float4*>(q.y + (size_t)r * 16)[kq] = y4;  // (null: no backward)
           // conv2: B fragment W2[o][jj, 4 kq + v] for o = lo (z0) and 16 + lo (z1)
           const float4 b0 = reinterpret_cast<const float4*>(q.w2f)[(jj * 4 + (int)kq) * 32 + (int)lo];
           const float4 b1 = reinterpret_cast<const float4*>(q.w2f)[(jj * 4 + (int)kq) * 32 + 16 + (int)lo];

@@ -1075,8 +1075,8 @@ int gr_stem12_forward(const float* obs, int64_t ld, int64_t off, const int64_t* 
                       int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b, float eps,
                       int32_t act, float slope, const float* w2f, int32_t n2, float* y, float* z2, float* stats,
                       double* part, void* stream) {
-  if (!stem1_args_ok(obs, nimg, pix, na, nb, conv_w, c, bn_w, bn_b) || c != 16 || !w2f || !y || !z2 || !stats ||
-      !part || !aligned16(w2f) || !aligned16(y) || !aligned16(z2) || !aligned16(stats) ||
+  if (!stem1_args_ok(obs, nimg, pix, na, nb, conv_w, c, bn_w, bn_b) || c != 16 || !w2f || !z2 || !stats ||
+      !part || !aligned16(w2f) || (y && !aligned16(y)) || !aligned16(z2) || !aligned16(stats) ||
       (act != GR_POLICY_ACT_LRELU && act != GR_POLICY_ACT_ELU) || n2 < 1 || na != 9 * n2 ||
       (int64_t)nimg * n2 * 32 >= (int64_t)1 << 31)
     return GR_ERR_ARG;

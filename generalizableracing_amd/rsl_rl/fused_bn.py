@@ -149,10 +149,13 @@ class _Stem12(torch.autograd.Function):
     conv2's weight gradient is the split-K product of gz2 and the saved y1."""
 
     @staticmethod
-    def forward(ctx, img, conv_w, bn_w, bn_b, w2, pix, na, nb, eps, act, slope, fused_forward=True, rows=None):
+    def forward(ctx, img, conv_w, bn_w, bn_b, w2, pix, na, nb, eps, act, slope, fused_forward=True, rows=None,
+                keep_y=True):
         lib = _abi.load()
         nimg = img.shape[0] if rows is None else rows.numel()
-        y = torch.empty(nimg * na, 16, device=img.device, dtype=torch.float32)
+        # (keep_y False: no backward will run, so y1 — kept only for conv2's weight gradient — is not stored)
+        keep_y = keep_y or not fused_forward
+        y = torch.empty(nimg * na if keep_y else 0, 16, device=img.device, dtype=torch.float32)
         stats = torch.empty(4, 16, device=img.device, dtype=torch.float32)
         part = torch.empty(int(lib.gr_stem1_scratch_doubles(nimg, na + nb, 16)), device=img.device, dtype=torch.float64)
         w = conv_w.detach().reshape(16, 9).contiguous()
@@ -165,8 +168,8 @@ class _Stem12(torch.autograd.Function):
             rc = lib.gr_stem12_forward(img.data_ptr(), img.stride(0), 0, _rows_ptr(rows), nimg, pix.data_ptr(), na, nb,
                                        w.data_ptr(), 16, bw.data_ptr(), bb.data_ptr(), float(eps), act, float(slope),
                                        w2f.data_ptr(),
-                                       na // 9, y.data_ptr(), z2.data_ptr(), stats.data_ptr(), part.data_ptr(),
-                                       _stream(img))
+                                       na // 9, y.data_ptr() if keep_y else None, z2.data_ptr(), stats.data_ptr(),
+                                       part.data_ptr(), _stream(img))
         else:  # the first block's kernels, then conv2 as a GEMM (the A/B reference of the fused forward)
             rc = lib.gr_stem1_forward(img.data_ptr(), img.stride(0), 0, _rows_ptr(rows), nimg, pix.data_ptr(), na, nb,
                                       w.data_ptr(), 16, bw.data_ptr(), bb.data_ptr(), float(eps), act, float(slope),
@@ -209,7 +212,7 @@ class _Stem12(torch.autograd.Function):
                                     part.data_ptr(), _stream(img))
         if rc != 0:
             raise RuntimeError(f"gr_stem12_backward failed (status {rc})")
-        return None, gconv.view(wshape), gbw, gbb, gw2, None, None, None, None, None, None, None, None
+        return None, gconv.view(wshape), gbw, gbb, gw2, None, None, None, None, None, None, None, None, None
 
 
 class _BnActPatchGemm(torch.autograd.Function):
@@ -310,8 +313,9 @@ def stem12_bn_act_conv(bn: nn.BatchNorm2d, act: nn.Module, conv_w: torch.Tensor,
     running statistics of the first BN updated as stem1_bn_act does.  rows: the batch is img[rows] (int64 device
     indices), read through them instead of a gathered copy."""
     code, slope = _act_code(act)
+    keep_y = torch.is_grad_enabled() and any(t.requires_grad for t in (conv_w, bn.weight, bn.bias, w2))
     z2, stats = _Stem12.apply(img, conv_w, bn.weight, bn.bias, w2, pix, na, nb, bn.eps, code, slope, fused_forward,
-                              _rows_arg(rows))
+                              _rows_arg(rows), keep_y)
     _update_running(bn, stats, uses, count_first)
     return z2
 

@@ -506,7 +506,8 @@ int gr_patch_wgrad(const float* x, int64_t ld, const float* gy, int64_t m, int32
  * pass: y [nimg * na][16] as gr_stem1_forward stores it (y_rows = nimg * na: the table-a rows) and conv2's output
  * z2 [nimg * n2][32] (na = 9 n2; row 9 p + j of an image = position j of patch p).  w2f: conv2's weight as
  * [9][4][32][4] floats, w2f[((j * 4 + g) * 32 + o) * 4 + v] = W[o][4 g + v][j / 3][j % 3] (16-byte aligned).
- * Same workspace and stats as gr_stem1_forward. */
+ * Same workspace and stats as gr_stem1_forward.  y may be NULL (a forward with no backward: y is only kept for
+ * conv2's weight gradient). */
 int gr_stem12_forward(const float* obs, int64_t ld, int64_t off, const int64_t* rows, int32_t nimg, const int16_t* pix, int32_t na,
                       int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b, float eps,
                       int32_t act, float slope, const float* w2f, int32_t n2, float* y, float* z2, float* stats,

@@ -270,3 +270,21 @@ def test_record_batch_statistics_gpu(indexed):
     for k in s1:
         if "running" in k or "num_batches" in k:
             assert torch.equal(s1[k], s2[k]), k
+
+
+def test_stem12_forward_without_backward_keeps_no_y1():
+    """Under inference mode the fused first block + conv2 does not store y1 (kept only for conv2's weight gradient):
+    the same conv2 output and statistics, bit for bit, as the training forward."""
+    from generalizableracing_amd.rsl_rl.fused_bn import stem12_bn_act_conv
+
+    pol = _model((72, 96), "lrelu", seed=13)
+    conv1, bn1, act, conv2 = pol.stem[0], pol.stem[1], pol.stem[2], pol.stem[3]
+    idx, idx_left, n1, n1_left, n3, n2, pix16 = pol._patch_index(DEV)
+    img = torch.rand(64, 72 * 96, device=DEV) * 8.0
+    w2m = conv2.weight.permute(0, 2, 3, 1).reshape(32, 144)
+    b1, b2 = copy.deepcopy(bn1), copy.deepcopy(bn1)
+    z_grad = stem12_bn_act_conv(b1, act, conv1.weight, w2m, img, pix16, n1, n1_left)
+    with torch.inference_mode():
+        z_inf = stem12_bn_act_conv(b2, act, conv1.weight, w2m, img, pix16, n1, n1_left)
+    assert torch.equal(z_grad.detach(), z_inf)
+    assert torch.equal(b1.running_mean, b2.running_mean) and torch.equal(b1.running_var, b2.running_var)
