@@ -451,7 +451,8 @@ int gr_bn_running_update(float* running_mean, float* running_var, int64_t* num_b
 /*
  * The vision stem's first block from the depth image itself: Conv2d(1, c, 3, stride 3, no bias) -> BatchNorm2d
  * (training mode) -> act, for `nimg` images at obs + b * ld + off (fp32 pixels), or at obs + rows[b] * ld + off
- * when `rows` is not NULL (a mini-batch read through its permutation instead of a gathered copy).  Output rows follow
+ * when `rows` is not NULL (a mini-batch read through its permutation instead of a gathered copy; the caller
+ * guarantees every rows[b] indexes a row of obs — the library cannot see the source's extent).  Output rows follow
  * VisionActorCritic.stem_gemm: nimg x na rows whose 3x3 cells are pix[0 .. na) (int16 pixel offsets, 9 per
  * row), then nimg x nb rows from pix[na .. na + nb); y [rows][c].  The patch matrix and the conv output are
  * never written (recomputed per pass); the backward returns the conv weight's gradient [c][9] and the BN
@@ -756,7 +757,7 @@ int gr_l2c2_mix(const float* obs, const float* next_obs, const float* w, int64_t
                 void* stream);
 /* The same with the pair read through row indices: out[r] = obs[rows_obs[r]] + w[r] (next_obs[rows_next[r]] -
  * obs[rows_obs[r]]), source rows `ld` floats apart (a multiple of 4): the mini-batch's rows straight from the rollout
- * storage (rollout_storage_l2c2.py:131-167 gathers them first). */
+ * storage (rollout_storage_l2c2.py:131-167 gathers them first); the caller guarantees the indices are in range. */
 int gr_l2c2_mix_rows(const float* obs, const float* next_obs, int64_t ld, const int64_t* rows_obs,
                      const int64_t* rows_next, const float* w, int64_t rows, int32_t cols, float* out, void* stream);
 int gr_gae(int64_t n, int32_t t_steps, float gamma, float lam, const float* rewards, const uint8_t* dones,
