@@ -102,14 +102,36 @@ class PPOL2C2(PPO):
         policy_coef = self.smoothness_upper_bound * eps
         return policy_coef, self.value_smoothness_coef * policy_coef
 
+    def _store_test(self, obs):
+        """ppo_l2c2.py:98's zero-observation test on these rows, issued before the policy forward and the env step
+        (stream order: the step cannot have touched them yet).  On the GPU its result is copied to pinned host
+        memory behind an event and read in process_env_step: the host never waits for the policy forward or the env
+        step, only for this reduction, long finished by then (the same decision, no per-step drain of the queue)."""
+        flag = torch.norm(obs).mean() > 1e-4
+        if not flag.is_cuda:
+            self._store_flag = bool(flag)
+            return
+        if getattr(self, "_flag_host", None) is None:
+            with torch.inference_mode(False):
+                self._flag_host = torch.zeros((), dtype=torch.bool, pin_memory=True)
+            self._flag_event = torch.cuda.Event()
+        self._flag_host.copy_(flag, non_blocking=True)
+        self._flag_event.record()
+        self._store_flag = None
+
+    def _stored(self) -> bool:
+        if not hasattr(self, "_store_flag"):  # (a transition stored without act: test its rows now)
+            self._store_test(self.transition.observations)
+        if self._store_flag is None:
+            self._flag_event.synchronize()
+            self._store_flag = bool(self._flag_host)
+        return self._store_flag
+
     def act(self, obs, critic_obs):
-        actions = super().act(obs, critic_obs)
-        if getattr(self.storage, "sink", False):
-            # ppo_l2c2.py:98's zero-observation test on these rows, taken before the step: with the observation
-            # sink the rows of a skipped transition are moved down a slot and the env's next step writes the slot
-            # `obs` views
-            self._store = bool(torch.norm(obs).mean() > 1e-4)
-        return actions
+        # (with the observation sink the rows of a skipped transition are moved down a slot and the env's next step
+        # writes the slot `obs` views: the test is on these rows as they are now)
+        self._store_test(obs)
+        return super().act(obs, critic_obs)
 
     def process_env_step(self, rewards, dones, infos):
         self.transition.rewards = rewards.clone()
@@ -118,7 +140,9 @@ class PPOL2C2(PPO):
             self.transition.rewards += self.gamma * torch.squeeze(
                 self.transition.values * infos["time_outs"].unsqueeze(1).to(self.device), 1)
         sink = getattr(self.storage, "sink", False)
-        if self._store if sink else bool(torch.norm(self.transition.observations).mean() > 1e-4):  # ppo_l2c2.py:98
+        store = self._stored()  # ppo_l2c2.py:98
+        del self._store_flag
+        if store:
             self.storage.add_transitions(self.transition)
         elif sink:
             self.storage.sink_skipped()
