@@ -285,7 +285,7 @@ class _GraphedStepL2C2(_GraphedStep):
         a policy with actor / critic heads and a state-independent std over <= 8 actions, fp32 outside autocast."""
         pol = self.alg.policy
         return (self.alg.fused_losses and obs.is_cuda and obs.dtype == torch.float32 and hasattr(pol, "features")
-                and isinstance(pol.actor, torch.nn.Sequential) and pol.actor[-1].out_features <= 8
+                and isinstance(pol.actor, nn.Sequential) and pol.actor[-1].out_features <= 8
                 and getattr(pol, "noise_std_type", None) in ("scalar", "log")
                 and not torch.is_autocast_enabled("cuda"))
 
