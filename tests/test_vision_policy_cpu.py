@@ -174,3 +174,15 @@ def test_record_batch_statistics_equals_a_training_forward():
     for k in s1:
         if "running" in k or "num_batches" in k:
             assert torch.equal(s1[k], s2[k]), k
+
+
+def test_features_rows_on_the_torch_path():
+    """features_rows(src, rows) on the CPU (the torch path gathers the rows itself): the features of src[rows],
+    bit for bit."""
+    torch.manual_seed(4)
+    p = policy()
+    src = torch.rand(9, OBS)
+    rows = torch.tensor([7, 2, 2, 5, 0], dtype=torch.int64)
+    p1, p2 = copy.deepcopy(p), copy.deepcopy(p)
+    with torch.no_grad():
+        assert torch.equal(p1.features_rows(src, rows), p2.features(src[rows]))
