@@ -22,7 +22,9 @@ N=1 only).  Single-GPU extras: policy-in-the-loop rates (PyTorch actor; fused
 MFMA inference in one hipGraph with the step), the step on obstacle tracks, an
 env-count sweep, config C5 (32-gate tracks), Perf/total_fps of PPO training at
 4 096 envs (C2, eager and graph-captured update) and 65 536 envs, and the depth
-camera.  Multi-rank runs report the headline step only.
+camera.  Every run, multi-rank included, also reports `distributed_train`: PPO training at the rank's envs with
+the per-mini-batch gradient all-reduce live (BASELINE C4), world-summed Perf/total_fps, per-rank update and
+all-reduce time, and a check that the ranks' parameters stay bit-identical.
 """
 from __future__ import annotations
 
@@ -98,8 +100,9 @@ def parse():
     p.add_argument("--no-extras", action="store_true", help="skip policy/train/cpu legs (profiling runs)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--legs", default="all",
-                   help="comma-separated extra legs to run (policy, obstacles, sweep, c5, regen, train4096, train65536, "
-                        "camera, vision, cpu) or 'all'; the headline step always runs")
+                   help="comma-separated extra legs to run (policy, obstacles, sweep, c5, regen, dtrain, train4096, "
+                        "train65536, camera, vision, cpu) or 'all'; the headline step always runs; at WORLD_SIZE > 1 "
+                        "'all' means dtrain (the data-parallel training leg) only")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL, one GPU per rank); gloo only to rehearse the multi-rank path with ranks "
                         "sharing one GPU")
@@ -429,6 +432,80 @@ def train_fps(device, n=4096, iters=3, fused=False, bf16_storage=False, graph_up
             "update_frac_of_fp32_mfma_peak": tfs / FP32_MFMA_PEAK_TFS if not bf16_update else None}
 
 
+def train_fps_distributed(device, n, rank, ws, iters=3):
+    """BASELINE config C4's exchange on the critical path: the reference's Perf/total_fps (on_policy_runner.py:229,
+    24 steps x n envs x world_size / iteration time) of PPO with MLP(256,256) at n envs per rank, each rank on its own
+    env shard (env ids and track seeds offset by rank), fp32 fused rollout inference, the graph-captured update.  At
+    world size > 1 every mini-batch step of the update (ppo.py:174-177) all-reduces the flat gradient + KL mean
+    (distributed.FlatGrads, 566 KB) eagerly between the step's two graphs, 20 exchanges per iteration.
+
+    World-summed fps = 24 x n x ws / (max over ranks of the iteration time), median over `iters` iterations after
+    one warm-up iteration.  Per rank: update_ms (alg.update alone) and the time the update's stream spends in the
+    exchanges (HIP events around each all-reduce, summed per iteration).  After the leg every rank's parameters are
+    hashed and compared: a data-parallel update must leave them bit-identical on every rank."""
+    import hashlib
+
+    from generalizableracing_amd.envs.racing_env import RslRlVecEnvWrapper
+    from generalizableracing_amd.rsl_rl import OnPolicyRunner, QuadcopterPPORunnerCfg
+    from generalizableracing_amd.rsl_rl import distributed as gdist
+
+    venv = RslRlVecEnvWrapper(RacingEnv(RacingEnvCfg(scene=SceneCfg(num_envs=n), sim=SimCfg(device=device),
+                                                     env_id_offset=rank * n, track_seed_offset=rank)))
+    cfg = QuadcopterPPORunnerCfg(device=device)
+    cfg.algorithm.fused_rollout_inference = True
+    cfg.algorithm.fused_rollout_precision = "fp32"
+    cfg.algorithm.graph_update = True
+    torch.manual_seed(1 + rank)  # rank 0's initial parameters are broadcast (PPO.__init__)
+    runner = OnPolicyRunner(venv, cfg.to_dict(), log_dir=None, device=device)
+    upd = runner.alg.update
+    upd_ms, ar_ms, n_ar = [], [], []
+
+    def timed_update():
+        gdist.FlatGrads.timings = []
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = upd()
+        torch.cuda.synchronize()
+        upd_ms.append((time.perf_counter() - t0) * 1e3)
+        ar_ms.append(sum(e0.elapsed_time(e1) for e0, e1 in gdist.FlatGrads.timings))
+        n_ar.append(len(gdist.FlatGrads.timings))
+        gdist.FlatGrads.timings = None
+        return out
+
+    runner.alg.update = timed_update
+    iter_s = []
+    try:
+        runner.learn(1, init_at_random_ep_len=True)  # warm-up iteration (graph capture)
+        for _ in range(iters):
+            barrier()
+            runner.learn(1)
+            iter_s.append(runner.last_log["collection_time"] + runner.last_log["learn_time"])
+    finally:
+        gdist.FlatGrads.timings = None
+    worst = [max_over_ranks(t, device) for t in iter_s]
+    fps = float(np.median([runner.num_steps_per_env * n * ws / t for t in worst]))
+    with torch.no_grad():
+        flat = torch.cat([p.detach().reshape(-1) for p in runner.alg.policy.parameters()]).cpu()
+    digest = hashlib.sha256(flat.numpy().tobytes()).hexdigest()
+    me = {"rank": rank, "update_ms": float(np.median(upd_ms[1:])), "allreduce_ms_per_iteration": float(np.median(ar_ms[1:])),
+          "allreduces_per_iteration": int(n_ar[-1]), "iteration_s": float(np.median(iter_s)), "param_sha256": digest}
+    ranks = [me]
+    if dist.is_initialized():
+        ranks = [None] * ws
+        dist.all_gather_object(ranks, me)
+    venv.close()
+    progress(f"train_fps_distributed n={n} ws={ws}: {fps:.4g} (update {me['update_ms']:.1f} ms, "
+             f"all-reduce {me['allreduce_ms_per_iteration']:.2f} ms / iteration)")
+    return {"train_total_fps": fps, "world_size": ws, "num_envs_per_rank": n,
+            "params_identical_on_all_ranks": len({r["param_sha256"] for r in ranks}) == 1,
+            "ranks": ranks,
+            "note": "Perf/total_fps = 24 x envs x world_size / max-over-ranks iteration time (median of "
+                    f"{iters}); PPO 5 epochs x 4 mini-batches, fp32 fused rollout inference, graphed update (at "
+                    "world size > 1: per mini-batch step two graphs with one eager in-place all-reduce of the "
+                    "flat gradient + KL mean between them); allreduce_ms = HIP events on the update's stream "
+                    "around each exchange, summed per iteration"}
+
+
 def regeneration_cost(device, n, interval=256, plain=32, regens=5, replays=20):
     """the interval step that regenerates the terrain (mdp/events.py:180-204) against a plain step,
     both eager from Python with a device synchronisation after each (wall time), over `regens` regenerations.  The
@@ -627,9 +704,14 @@ def main():
     else:  # rehearsal: ranks may share a device
         local = local % max(1, torch.cuda.device_count())
     if ws > 1:
-        # the scaling lines report the headline step only: the extras (policy, training, camera, sweep legs)
-        # are single-GPU measurements, and a rank-local leg must not hold the others at a collective
-        a.no_extras = True
+        # the scaling lines report the headline step and the data-parallel training leg (BASELINE C4: every rank
+        # trains on its own shard with the gradient all-reduce live); the other extras (policy, camera, sweep, C5,
+        # single-GPU training legs) are single-GPU measurements, and a rank-local leg must not hold the others at a
+        # collective
+        if a.legs == "all":
+            a.legs = "dtrain"
+        elif not set(a.legs.split(",")) <= {"dtrain", "none"}:
+            raise SystemExit(f"bench.py: --legs {a.legs}: at WORLD_SIZE > 1 only the dtrain leg runs")
         torch.cuda.set_device(local)
         dist.init_process_group(a.dist_backend, rank=rank, world_size=ws)
     device = f"cuda:{local}"
@@ -813,6 +895,11 @@ def main():
                 "frac": cam["hbm_frac_avg"],
                 "bytes_per_env_call": [cam["bytes_per_env_render"], cam["bytes_per_env_reuse"]],
                 "env_steps_per_s_step_plus_camera": cam["wall_env_steps_per_s_step_plus_camera"]}
+    if want(a, "dtrain"):
+        # BASELINE C4 (at world size 1 the same leg without an exchange: the per-N values the scaling run compares)
+        gc.collect()
+        torch.cuda.empty_cache()
+        extra["distributed_train"] = train_fps_distributed(device, n, rank, ws)
     if want(a, "train4096"):
         extra["train_total_fps_4096_envs"] = train_fps(device)
         extra["train_total_fps_4096_envs_graph_update"] = train_fps(device, graph_update=True)

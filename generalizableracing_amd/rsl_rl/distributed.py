@@ -78,11 +78,22 @@ class FlatGrads:
     def bound(self) -> bool:
         return all(p.grad is not None and p.grad.data_ptr() == v.data_ptr() for p, v in zip(self.params, self.views))
 
+    # measurement hook (bench.py): when a list, every exchange appends a (start, end) pair of events recorded on the
+    # current stream around the collective and the division, i.e. the time the update's stream waits for the exchange
+    timings: list | None = None
+
     def allreduce_(self):
         """Average over ranks in place (the views see the result)."""
         if is_dist():
+            ev = None
+            if FlatGrads.timings is not None and self.flat.is_cuda:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
             dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
             self.flat.div_(world_size())
+            if ev is not None:
+                ev[1].record()
+                FlatGrads.timings.append(ev)
 
 
 def allreduce_grads(params, flat: FlatGrads | None = None) -> None:

@@ -87,6 +87,8 @@ def tall_wgrad(gy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
         floats = int(lib.gr_patch_wgrad_floats(m, n, k))
         if floats > 0:
             gy = gy.contiguous()
+            if gy.data_ptr() % 16:  # (gr_patch_wgrad reads gy by 16-B vectors: a contiguous view at an odd storage
+                gy = gy.clone()     # offset is re-based, not sent to the fallback or rejected)
             gw = torch.empty(n, k, device=gy.device, dtype=torch.float32)
             part = torch.empty(floats, device=gy.device, dtype=torch.float32)
             rc = lib.gr_patch_wgrad(x.data_ptr(), x.stride(0), gy.data_ptr(), m, n, k, part.data_ptr(), gw.data_ptr(),

@@ -316,6 +316,8 @@ class _GraphedStep:
     runs eagerly between them: ONE in-place all-reduce of the flat buffer carries the gradients and the KL
     mean together.  No collective is ever captured."""
 
+    _PACK = True  # gather the mini-batch from the storage's packed sample rows when it has them
+
     def __init__(self, alg: "PPO"):
         self.alg = alg
         st, dev = alg.storage, alg.device
@@ -342,7 +344,9 @@ class _GraphedStep:
         # per-step index copy or replay launch); several ranks: per-step graphs read `idx`, refilled per step
         self.perm = torch.zeros(self.nmb * self.mb, dtype=torch.long, device=dev)
         self.idx = self.perm[:self.mb]
-        self.cols = st.sample_columns()  # packed sample rows (None: gathered field by field)
+        # packed sample rows (None: gathered field by field); a subclass gathering its own fields sets _PACK False and
+        # never allocates the buffer
+        self.cols = st.sample_columns() if self._PACK else None
         # persistent: the graphs read it (the storage's own packed buffer, shared with the eager generator)
         self.pack = st.pack_samples(out=st.packed_buffer()) if self.cols is not None else None
         self.acc = torch.zeros(2, device=dev)  # the update's sums of the surrogate and value means

@@ -252,6 +252,8 @@ class _GraphedStepL2C2(_GraphedStep):
     learning rate is an fp32 device tensor and the eager loop's unused action draw is not made; the BatchNorm
     running statistics of the warm-up and captured steps are restored after the capture."""
 
+    _PACK = False  # (the pairs are gathered field by field, _gather: no packed copy of the samples)
+
     def __init__(self, alg: "PPOL2C2"):
         super().__init__(alg)
         st, dev = alg.storage, alg.device
@@ -260,7 +262,6 @@ class _GraphedStepL2C2(_GraphedStep):
         self.mb = (self.T - 1) * self.N // self.nmb
         self.perm = torch.zeros(self.nmb * self.mb, dtype=torch.long, device=dev)
         self.idx = self.perm[:self.mb]
-        self.cols, self.pack = None, None
         self.acc = torch.zeros(3, device=dev)  # the update's sums of the surrogate, value and smoothness means
         self.cont = torch.zeros((self.T - 1) * self.N, 1, device=dev)
 

@@ -1,4 +1,4 @@
-"""The env-only chain's timeline from a rocprofv3 kernel trace of `bench.py --legs policy` (scripts/gpu_r4z.sh):
+"""The env-only chain's timeline from a rocprofv3 kernel trace of `bench.py --legs policy` (historically scripts/gpu_r4z.sh; today scripts/gpu.sh TAG 'trace 300 cd /tmp && rocprofv3 --kernel-trace ... -- python3 $R/bench.py --legs policy'):
 per rollout step the fused fp32 actor (policy_f32_kernel, actor only) and the env step (step_kernel), back to back
 in one hipGraph.  Prints and writes the per-step stamps (median actor / step / gap µs, the excerpt of one graph
 replay) — the measured form of DESIGN §4e''s argument that the chain is the actor's MFMA time plus the step.

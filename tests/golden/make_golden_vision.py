@@ -46,7 +46,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 import il_shim  # noqa: E402
-from vision_golden import randomise, run  # noqa: E402
+from vision_golden import observation_rows, randomise, run  # noqa: E402
 
 OUT = os.path.join(HERE, "golden_vision.npz")
 VAC = os.path.join(il_shim.REF, "standalone/rsl_rl/ext/modules/vision_actor_critic.py")
@@ -106,23 +106,6 @@ def policy_kwargs():
     """The registered recipe's policy (agents/rsl_rl_ppo_cfg.py:43-52, use_auxiliary_loss :103)."""
     return dict(img_res=(H, W), dim_hidden_input=192, actor_hidden_dims=[128, 128], critic_hidden_dims=[128, 128],
                 activation="lrelu", init_noise_std=1.0, noise_std_type="scalar", use_auxiliary_loss=True)
-
-
-def observation_rows():
-    from generalizableracing_amd.envs.racing_cfg import CameraCfg
-    from oracle_vecenv import OracleVecEnv
-
-    env = OracleVecEnv(num_envs=N, camera=CameraCfg())
-    g = torch.Generator().manual_seed(11)
-    obs, ex = env.get_observations()
-    for _ in range(6):
-        obs, _, _, ex = env.step(torch.randn(N, 4, generator=g))
-    o = ex["observations"]
-    # the policy group's image carries the camera noise (observation.py:84-92), which does not compress: both
-    # groups take the critic's clean image (the module does not care which), each with its own 16 state terms
-    cri = o["critic"].clone()
-    pol = torch.cat([o["policy"][:, :16], cri[:, 16:]], 1)
-    return pol, cri
 
 
 def main():

@@ -2,6 +2,7 @@
 two ranks share the one GPU of the test box over gloo, and rank 0 prints one JSON line whose value counts
 both shards.  The RCCL path differs only in the backend and one GPU per rank."""
 import json
+import math
 import os
 import socket
 import subprocess
@@ -53,6 +54,19 @@ def test_bench_two_ranks_gloo(launch):
         assert r["env_steps_per_s"] >= 8192 * 128 / (line["ms_per_step"] * 1e-3 * 128) * (1 - 1e-6)
     assert d["grad_allreduce_bytes"] == 566_312 and d["grad_allreduce_median_us"] > 0
     assert len(d["ranks"]) == 2
+    # BASELINE C4: the training leg ran on both ranks with the gradient exchange on the update's critical path
+    t = line["distributed_train"]
+    assert t["world_size"] == 2 and t["num_envs_per_rank"] == 8192
+    assert math.isfinite(t["train_total_fps"]) and t["train_total_fps"] > 0
+    assert [r["rank"] for r in t["ranks"]] == [0, 1]
+    for r in t["ranks"]:
+        # 5 epochs x 4 mini-batches, one in-place all-reduce of the flat gradient + KL mean each
+        assert r["allreduces_per_iteration"] == 20
+        assert 0 < r["allreduce_ms_per_iteration"] < r["update_ms"]
+        assert math.isfinite(r["iteration_s"]) and r["iteration_s"] > 0
+    # a data-parallel update leaves every rank's parameters bit-identical
+    assert t["params_identical_on_all_ranks"] is True
+    assert len({r["param_sha256"] for r in t["ranks"]}) == 1
 
 
 def test_bench_refuses_a_world_it_cannot_describe():

@@ -6,8 +6,9 @@ outputs (means, features, values, log probs, loss, BatchNorm running statistics)
 gradients within RTOL_GRAD, both relative to the largest magnitude of the reference tensor (the stem's
 convolutions run as patch GEMMs and its BatchNorm statistics reduce ~200 000 rows in another order, so exact
 bits are not expected; the fixture's own round-off scale is ~1e-7).  The fixture also holds the reference module
-evaluated in float64: the build is held to it with the same tolerances (the reference's fp32 conv1 weight
-gradient is itself ~7e-5 off it, the build's ~1e-5 on the CPU)."""
+evaluated in float64: the build is held to it with the same tolerances, and to the reference's fp32 tensor with
+the tolerance widened by exactly that tensor's own distance from float64 (the reference's fp32 conv1 weight
+gradient is ~1.3e-4 off float64, the build's ~2e-5 on the CPU)."""
 from __future__ import annotations
 
 import os
@@ -65,6 +66,26 @@ def run(model, pol, cri, actions, g_mu, w, g_v):
     return {k: v.detach().clone() for k, v in rec.items()}
 
 
+def observation_rows(n: int = 256):
+    """The fixture's observation inputs: n rows of the CPU oracle env with its depth camera (obstacle tracks)
+    after 6 seeded random-action steps -> (policy rows, critic rows).  The generator stores them; the CPU test
+    re-derives them and compares bit for bit, so a change of the oracle's draws fails loudly."""
+    from generalizableracing_amd.envs.racing_cfg import CameraCfg
+    from oracle_vecenv import OracleVecEnv
+
+    env = OracleVecEnv(num_envs=n, camera=CameraCfg())
+    g = torch.Generator().manual_seed(11)
+    obs, ex = env.get_observations()
+    for _ in range(6):
+        obs, _, _, ex = env.step(torch.randn(n, 4, generator=g))
+    o = ex["observations"]
+    # the policy group's image carries the camera noise (observation.py:84-92), which does not compress: both
+    # groups take the critic's clean image (the module does not care which), each with its own 16 state terms
+    cri = o["critic"].clone()
+    pol = torch.cat([o["policy"][:, :16], cri[:, 16:]], 1)
+    return pol, cri
+
+
 def load():
     z = np.load(GOLDEN)
     return {k: torch.from_numpy(z[k]) for k in z.files}
@@ -105,8 +126,14 @@ def check(got: dict, f: dict):
         rel = float((g - w).abs().max() / w.abs().max().clamp_min(1e-30))
         tol = RTOL_GRAD if k.startswith("grad:") else RTOL_OUT
         worst[k] = rel
-        assert rel <= tol, (k, rel, tol)
-        if k in f64:  # and the float64 evaluation of the same module: no worse than the reference's tolerance
+        if k in f64:
+            # the float64 evaluation of the same module is the exact answer: the build is held to it at `tol`, and
+            # to the reference's fp32 result at `tol` plus that result's own measured distance from float64 (the
+            # reference's fp32 conv1 weight gradient, a BatchNorm backward reduced over ~200 000 rows, is itself
+            # ~1.3e-4 off float64 on these inputs, while the build's is ~2e-5)
             d = f64[k].double().reshape(g.shape)
-            assert float((g - d).abs().max() / d.abs().max().clamp_min(1e-30)) <= tol, (k, "vs float64")
+            scale = d.abs().max().clamp_min(1e-30)
+            assert float((g - d).abs().max() / scale) <= tol, (k, "vs float64")
+            tol = tol + float((w - d).abs().max() / scale)
+        assert rel <= tol, (k, rel, tol)
     return worst
