@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgr.so")
 
 # ---- constants (include/gr.h) ----
-GR_ABI_VERSION = 4
+GR_ABI_VERSION = 5
 GR_INTEGRATOR_DD_EXPLICIT = 0
 GR_INTEGRATOR_SEMI_IMPLICIT = 1
 
@@ -241,7 +241,7 @@ EXPORTS = [
     "gr_mlp_args_size", "gr_step_kernel_variant", "gr_terrain_reserve", "gr_terrain_stage", "gr_terrain_commit",
     "gr_terrain_epoch", "gr_mlp_h1mask_words", "gr_stem12_backward", "gr_stem12_forward",
     "gr_patch_wgrad_floats", "gr_patch_wgrad", "gr_bn_running_update", "gr_tsgemm", "gr_l2c2_mix_rows", "gr_tsgemm_bnact",
-    "gr_patch_wgrad_bnact", "gr_bn_stats",
+    "gr_patch_wgrad_bnact", "gr_bn_stats", "gr_stem12_backward_w2_scratch_doubles", "gr_stem12_backward_w2",
 ]
 
 _lib = None
@@ -344,6 +344,10 @@ def _declare(lib):
                                         vp, vp, C.c_float, C.c_int32, C.c_float, vp, C.c_int32, vp, vp, vp, vp, vp]),
         "gr_stem12_backward": (C.c_int, [vp, C.c_int64, C.c_int64, vp, C.c_int32, vp, C.c_int32, C.c_int32, vp, C.c_int32,
                                          vp, vp, vp, C.c_int32, C.c_float, vp, C.c_int32, vp, vp, vp, vp, vp, vp]),
+        "gr_stem12_backward_w2_scratch_doubles": (C.c_int64, [C.c_int32]),
+        "gr_stem12_backward_w2": (C.c_int, [vp, C.c_int64, C.c_int64, vp, C.c_int32, vp, C.c_int32, C.c_int32, vp,
+                                            C.c_int32, vp, vp, vp, C.c_int32, C.c_float, vp, C.c_int32, vp, vp, vp, vp,
+                                            vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name) and os.environ.get("GR_LIB_PATH"):

@@ -1322,4 +1322,430 @@ hipError_t launch_stem12_backward(const Stem1& s, const float* bw, const float* 
   return hipGetLastError();
 }
 
+
+// ------------------------------------------------------------- the first block's backward with conv2's dgrad AND wgrad
+// stem12b_kernel above forms conv2's input gradient inside the first block's backward, but conv2's weight gradient
+// gW2[o][j, c] = sum_p gz2[p][o] y1[9 p + j][c] was a separate pass (gr_patch_wgrad) over a y1 [nimg * na][16] that
+// the forward had to write: 1.13 GB written + 1.13 GB read back per 24 576-image mini-batch, plus that pass's launch.
+// Here the backward recomputes y1 = act(bn(conv1)) from the registers it already holds (the same expression as the
+// forward's, so the same bits) and contracts it with gz2 on MFMA, and the forward stores no y1.
+//
+// Work split: position-major.  Wave w (8 per workgroup, 2 per SIMD) owns conv2 position j = w: its tiles are the
+// image's 16-patch chunks at that position (the rows 9 p + j of patches p = 16 c .. 16 c + 15), so the wave holds
+// conv2's weight fragments of ONE position and the conv2 weight-gradient accumulators of one position (plus
+// position 8's, whose chunks go to waves 0 .. nch - 1; table b's tiles to the others).  The tile list of a wave is
+// the same for every image, so every pixel offset it gathers is computed once, before the image loop (no table reads
+// or index arithmetic per tile).  All eight waves share the staging of the next image and its gz2 rows (LDS-DMA);
+// gz2's rows sit in LDS with their 16-float halves swapped on every second row group (the G2 operand reads of four
+// row groups hit two bank halves instead of one).
+//
+// Per table-a tile (lane l = 16 g + i; A operands by row i, C rows 4 g + v):
+//   x   = conv1 of patches 16 c + i at position j        3 MFMA (A = pixels, B = W1: as sm_conv, bit-identical x)
+//   gy1 = gz2[patch][0..31] x W2[0..31][j, ch]            8 MFMA (k step s of group g: o = 8 g + s)
+//   gz = gy1 act'(z), y1 = act(z), z = xhat w + b         VALU (rows past n2: 0)
+//   A1 += gz^T px, A3 += xhat^T px                         8 MFMA (B = the tile's pixels gathered a second time in
+//                                                                the B layout: rows 4 g + v, tap i)
+//   G2[ch][o] += y1^T gz2                                  8 MFMA (B = gz2[patch 4 g + v][o = i, 16 + i] from LDS)
+// 27 MFMA per tile.  Table-b tiles (cells under no conv2 patch: gz = 0) add only to A3 and A2.  Sums: fp32 within an
+// image, fp64 across images and in the fixed-order block / final reductions; deterministic.
+constexpr int SW_WAVES = 8;
+constexpr int SW_THREADS = 64 * SW_WAVES;
+constexpr int SW_MAX_CHUNKS = 5;  // conv2 patches per image <= 80 (72 x 96: exactly 80): offsets held in registers
+constexpr int SW_GRID = 256;      // one workgroup per CU (~200 VGPRs: two waves per SIMD)
+constexpr int SW_G2 = 9 * 16 * 32;  // conv2 weight-gradient partials per block: [position][channel][o]
+
+struct Sw12Args {
+  const float* bw;
+  const float* bb;
+  const float* stats;
+  const float* gz2;  // [nimg * n2][32]
+  const float* w2t;  // [9][4][16][8] (as Sm12Args)
+  double* part;      // [grid][32] BN sums
+  double* wpart;     // [grid][3][144] A1, A2, A3 (stem12_final's layout)
+  double* g2part;    // [grid][9][16][32]
+  float slope;
+  int n2;
+};
+
+__host__ __device__ inline int sw_gz_floats(int n2) { return (n2 * 32 + 255) & ~255; }
+__host__ __device__ inline size_t sw_lds_bytes(int n2, int cap) {
+  const size_t b = 4 * (2 * sm_img_floats(cap) + 2 * (size_t)sw_gz_floats(n2));
+  return b < 8 * 8 * SW_THREADS ? 8 * 8 * SW_THREADS : b;  // (the end's reductions: 8 doubles per thread)
+}
+// LDS float of gz2[row r][o]: the two 16-float halves of rows with r & 4 swapped
+__device__ __forceinline__ int sw_gz_at(int r, int o) { return r * 32 + (o ^ ((r & 4) << 2)); }
+
+// the image's first `span` floats into dst by LDS-DMA, the instructions shared by the eight waves
+__device__ __forceinline__ void sw_dma_image(const float* g, float* dst, int span, bool v4, int w) {
+  const int lane = threadIdx.x & 63;
+  if (v4) {
+    for (int o = 256 * w; o < span; o += 256 * SW_WAVES) {
+      const int i = o + 4 * lane;
+      __builtin_amdgcn_global_load_lds((sm_glob_void_t*)(g + (i < span ? i : 0)), (sm_lds_void_t*)(dst + o), 16, 0, 0);
+    }
+  } else {
+    for (int o = 64 * w; o < span; o += 64 * SW_WAVES) {
+      const int i = o + lane;
+      __builtin_amdgcn_global_load_lds((sm_glob_void_t*)(g + (i < span ? i : 0)), (sm_lds_void_t*)(dst + o), 4, 0, 0);
+    }
+  }
+}
+// the image's gz2 rows (n2 x 32 floats, 16-byte aligned) into dst in sw_gz_at's layout: lane L of an instruction fills
+// LDS float4 slot o / 4 + L (row R = slot / 8) from the global float4 the swap maps there
+__device__ __forceinline__ void sw_dma_gz2(const float* g, float* dst, int nflt, int w) {
+  const int lane = threadIdx.x & 63;
+  for (int o = 256 * w; o < nflt; o += 256 * SW_WAVES) {
+    const int slot = o / 4 + lane, r = slot >> 3, q4 = slot & 7;
+    const int i = 4 * (r * 8 + (q4 ^ (r & 4)));
+    __builtin_amdgcn_global_load_lds((sm_glob_void_t*)(g + (i < nflt ? i : 0)), (sm_lds_void_t*)(dst + o), 16, 0, 0);
+  }
+}
+
+template <int ACT, bool V4>
+__global__ __launch_bounds__(SW_THREADS) void stem12w_kernel(Stem1 s, Sw12Args q, int cap) {
+  extern __shared__ float4 sm_dyn4[];
+  __shared__ int s_span;
+  const int na = s.na, nbt = s.nbt, ncell = na + nbt, n2 = q.n2;
+  const int nch = (n2 + 15) / 16, ntb = (nbt + 15) / 16;
+  const int imgf = (int)sm_img_floats(cap), gzf = sw_gz_floats(n2);
+  float* im0 = reinterpret_cast<float*>(sm_dyn4);
+  float* im1 = im0 + imgf;
+  float* gz0 = im1 + imgf;
+  float* gz1 = gz0 + gzf;
+  const int l = (int)(threadIdx.x & 63), i = l & 15, g = l >> 4, w = (int)sm_wave();
+  if (threadIdx.x == 0) s_span = 0;
+  __syncthreads();
+  int mx = 0;
+  for (int k = threadIdx.x; k < ncell * 9; k += SW_THREADS) {
+    const int t = s.pix[k];
+    mx = mx > t + 1 ? mx : t + 1;
+  }
+  atomicMax(&s_span, mx);
+  __syncthreads();
+  const int span = s_span;
+  const bool staged = span <= cap;
+  const bool v4 = V4 && (span & 3) == 0;
+
+  float wb[3];  // B operand of conv1: W1[ch i][tap g + 4 c] (0 for taps >= 9)
+#pragma unroll
+  for (int c = 0; c < 3; ++c) wb[c] = g + 4 * c < 9 ? s.w[i * 9 + g + 4 * c] : 0.0f;
+  const float mu = q.stats[i], is = q.stats[16 + i], wv = q.bw[i], bv = q.bb[i];
+
+  // the wave's tiles: t < nch = (chunk t, position w); t == nch = (chunk w, position 8) when w < nch.  Per tile the
+  // A-layout pixel offsets (row i: cell 9 p + j, taps g, g + 4, 8), the B-layout ones (rows 4 g + v, tap i) and the
+  // live-row bits (patch < n2; B also tap i < 9)
+  constexpr int NT = SW_MAX_CHUNKS + 1;
+  int oa[NT][3], ob[NT][4];
+  unsigned live = 0u, bliv = 0u;
+  const bool extra = w < nch;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int c = t < nch ? t : w, j = t < nch ? w : 8;
+    const bool on = t < nch || (t == nch && extra);
+    const int pa = on ? (16 * c + i < n2 ? 16 * c + i : n2 - 1) : 0;
+    const short* ta = s.pix + (size_t)(9 * pa + j) * 9;
+    oa[t][0] = ta[g];
+    oa[t][1] = ta[g + 4];
+    oa[t][2] = ta[8];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int p = 16 * c + 4 * g + v;
+      const bool ok = on && p < n2;
+      ob[t][v] = (ok && i < 9) ? s.pix[(size_t)(9 * p + j) * 9 + i] : 0;
+      live |= (ok ? 1u : 0u) << (4 * t + v);
+      bliv |= ((ok && i < 9) ? 1u : 0u) << (4 * t + v);
+    }
+  }
+  // conv2's weight fragments (B of gy1 = gz2 W2): position w, and position 8 for the extra tile
+  float wf[8], wf8[8];
+  {
+    const float4* a = reinterpret_cast<const float4*>(q.w2t + (size_t)((w * 4 + g) * 16 + i) * 8);
+    const float4* b = reinterpret_cast<const float4*>(q.w2t + (size_t)((8 * 4 + g) * 16 + i) * 8);
+    const float4 a0 = a[0], a1 = a[1], b0 = b[0], b1 = b[1];
+    wf[0] = a0.x; wf[1] = a0.y; wf[2] = a0.z; wf[3] = a0.w; wf[4] = a1.x; wf[5] = a1.y; wf[6] = a1.z; wf[7] = a1.w;
+    wf8[0] = b0.x; wf8[1] = b0.y; wf8[2] = b0.z; wf8[3] = b0.w; wf8[4] = b1.x; wf8[5] = b1.y; wf8[6] = b1.z; wf8[7] = b1.w;
+  }
+
+  double d0 = 0.0, d1 = 0.0, da2 = 0.0, dc1[4] = {0.0, 0.0, 0.0, 0.0}, dc3[4] = {0.0, 0.0, 0.0, 0.0};
+  double dg[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, dg8[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+
+  const int nmine = s.nimg > (int)blockIdx.x ? (s.nimg - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
+  const int nflt = n2 * 32;
+  if (nmine > 0) {
+    if (staged) sw_dma_image(stem_img(s, blockIdx.x), im0, span, v4, w);
+    sw_dma_gz2(q.gz2 + (size_t)blockIdx.x * nflt, gz0, nflt, w);
+  }
+  __syncthreads();
+  for (int k = 0; k < nmine; ++k) {
+    const int b = (int)blockIdx.x + k * (int)gridDim.x;
+    const float* gim = stem_img(s, b);
+    const float* im = (k & 1) ? im1 : im0;
+    const float* gzs = (k & 1) ? gz1 : gz0;
+    if (k + 1 < nmine) {  // the next image and its gz2 rows into the other buffers, shared by the eight waves
+      const long long bn = b + (long long)gridDim.x;
+      if (staged) sw_dma_image(stem_img(s, bn), (k & 1) ? im0 : im1, span, v4, w);
+      sw_dma_gz2(q.gz2 + (size_t)bn * nflt, (k & 1) ? gz0 : gz1, nflt, w);
+    }
+    float f0 = 0.0f, f1 = 0.0f, fa2 = 0.0f;
+    sm4 c1 = {0.0f, 0.0f, 0.0f, 0.0f}, c3 = {0.0f, 0.0f, 0.0f, 0.0f};
+    sm4 ga = {0.0f, 0.0f, 0.0f, 0.0f}, gb = {0.0f, 0.0f, 0.0f, 0.0f};
+    sm4 ga8 = {0.0f, 0.0f, 0.0f, 0.0f}, gb8 = {0.0f, 0.0f, 0.0f, 0.0f};
+    auto run = [&](auto from_lds) {
+      const float* src = decltype(from_lds)::value ? im : gim;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        if (!(t < nch || (t == nch && extra))) continue;  // (wave-uniform)
+        const int c = t < nch ? t : w;
+        float pa[3], pb[4];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) pa[u] = src[oa[t][u]];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const float p = src[ob[t][v]];
+          pb[v] = (bliv >> (4 * t + v)) & 1u ? p : 0.0f;
+        }
+        // gz2 fragments: A of gy1 (row 16 c + i, o = 8 g .. 8 g + 7), B of G2 (rows 16 c + 4 g + v, o = i and 16 + i)
+        const int ra = 16 * c + i < n2 ? 16 * c + i : n2 - 1;
+        const float4 z0 = *reinterpret_cast<const float4*>(gzs + sw_gz_at(ra, 8 * g));
+        const float4 z1 = *reinterpret_cast<const float4*>(gzs + sw_gz_at(ra, 8 * g + 4));
+        float zb[4], zb2[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          int rb = 16 * c + 4 * g + v;
+          rb = rb < n2 ? rb : n2 - 1;
+          zb[v] = gzs[sw_gz_at(rb, i)];
+          zb2[v] = gzs[sw_gz_at(rb, 16 + i)];
+        }
+        const sm4 x = sm_conv(pa, wb);
+        auto gy1 = [&](const float (&f)[8]) {
+          sm4 a = {0.0f, 0.0f, 0.0f, 0.0f};
+          a = sm_mfma(z0.x, f[0], a);
+          a = sm_mfma(z0.y, f[1], a);
+          a = sm_mfma(z0.z, f[2], a);
+          a = sm_mfma(z0.w, f[3], a);
+          a = sm_mfma(z1.x, f[4], a);
+          a = sm_mfma(z1.y, f[5], a);
+          a = sm_mfma(z1.z, f[6], a);
+          return sm_mfma(z1.w, f[7], a);
+        };
+        const sm4 gyt = t < nch ? gy1(wf) : gy1(wf8);  // (wave-uniform)
+        float gz[4], xh[4], y1[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const bool lv = (live >> (4 * t + v)) & 1u;
+          xh[v] = (x[v] - mu) * is;
+          const float zz = xh[v] * wv + bv;
+          gz[v] = lv ? gyt[v] * bn_dact<ACT>(zz, q.slope) : 0.0f;
+          y1[v] = lv ? bn_act<ACT>(zz, q.slope) : 0.0f;
+          f0 += gz[v];
+          f1 += gz[v] * xh[v];
+          fa2 += pb[v];
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          c1 = sm_mfma(gz[v], pb[v], c1);
+          c3 = sm_mfma(xh[v], pb[v], c3);
+        }
+        if (t < nch) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            ga = sm_mfma(y1[v], zb[v], ga);
+            gb = sm_mfma(y1[v], zb2[v], gb);
+          }
+        } else {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            ga8 = sm_mfma(y1[v], zb[v], ga8);
+            gb8 = sm_mfma(y1[v], zb2[v], gb8);
+          }
+        }
+      }
+      // table b's tiles (cells under no conv2 patch: gz = 0; only A3 and A2), to the waves nch .. 7 in turn
+      for (int tb = w - nch; tb >= 0 && tb < ntb; tb += SW_WAVES - nch) {
+        const int r0 = 16 * tb, nv = nbt - r0 < 16 ? nbt - r0 : 16;
+        const short* ta = s.pix + (size_t)(na + r0 + (i < nv ? i : 0)) * 9;
+        float pa[3] = {src[ta[g]], src[ta[g + 4]], src[ta[8]]};
+        float pb[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const bool ok = 4 * g + v < nv && i < 9;
+          const float p = src[ok ? s.pix[(size_t)(na + r0 + 4 * g + v) * 9 + i] : 0];
+          pb[v] = ok ? p : 0.0f;
+          fa2 += pb[v];
+        }
+        const sm4 x = sm_conv(pa, wb);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) c3 = sm_mfma((x[v] - mu) * is, pb[v], c3);
+      }
+    };
+    if (staged)
+      run(std::true_type{});
+    else
+      run(std::false_type{});
+    d0 += (double)f0;
+    d1 += (double)f1;
+    da2 += (double)fa2;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      dc1[r] += (double)c1[r];
+      dc3[r] += (double)c3[r];
+      dg[r] += (double)ga[r];
+      dg[4 + r] += (double)gb[r];
+      dg8[r] += (double)ga8[r];
+      dg8[4 + r] += (double)gb8[r];
+    }
+    __syncthreads();  // image k read, image k + 1 staged
+  }
+
+  // fixed-order block reductions through the (now free) LDS buffers: >= 2 x 1 024 + 2 x 256 floats
+  double* red = reinterpret_cast<double*>(im0);
+  red[threadIdx.x] = d0;
+  red[SW_THREADS + threadIdx.x] = d1;
+  __syncthreads();
+  if (threadIdx.x < 32) {  // part[block][2][16]: per channel, the waves in order, then the lane groups in order
+    const int qq = threadIdx.x >> 4, c = threadIdx.x & 15;
+    double acc = 0.0;
+    for (int ww = 0; ww < SW_WAVES; ++ww)
+      for (int gg = 0; gg < 4; ++gg) acc += red[qq * SW_THREADS + ww * 64 + gg * 16 + c];
+    q.part[(size_t)blockIdx.x * 32 + threadIdx.x] = acc;
+  }
+#pragma unroll
+  for (int a = 0; a < 3; a += 2) {  // A1, A3: lane (g, i) holds [channel 4 g + r][tap i]
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[r * SW_THREADS + threadIdx.x] = a == 0 ? dc1[r] : dc3[r];
+    __syncthreads();
+    for (int v = threadIdx.x; v < 16 * 9; v += SW_THREADS) {
+      const int c2 = v / 9, tap = v % 9, lane = (c2 >> 2) * 16 + tap, r = c2 & 3;
+      double t = 0.0;
+      for (int ww = 0; ww < SW_WAVES; ++ww) t += red[r * SW_THREADS + ww * 64 + lane];
+      q.wpart[((size_t)blockIdx.x * 3 + a) * 144 + v] = t;
+    }
+  }
+  __syncthreads();
+  red[threadIdx.x] = da2;  // A2[tap i]: the lane groups and waves in order, stored for every channel
+  __syncthreads();
+  for (int v = threadIdx.x; v < 16 * 9; v += SW_THREADS) {
+    const int tap = v % 9;
+    double t = 0.0;
+    for (int ww = 0; ww < SW_WAVES; ++ww)
+      for (int gg = 0; gg < 4; ++gg) t += red[ww * 64 + gg * 16 + tap];
+    q.wpart[((size_t)blockIdx.x * 3 + 1) * 144 + v] = t;
+  }
+  // G2: wave w alone holds position w (written as is); position 8 sums waves 0 .. nch - 1 in order
+  double* g2 = q.g2part + (size_t)blockIdx.x * SW_G2;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int ch = 4 * g + r;
+    g2[(w * 16 + ch) * 32 + i] = dg[r];
+    g2[(w * 16 + ch) * 32 + 16 + i] = dg[4 + r];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 8; ++r) red[r * SW_THREADS + threadIdx.x] = dg8[r];
+  __syncthreads();
+  {
+    const int v = threadIdx.x;  // (channel, o) of position 8: v = ch * 32 + o, 512 of them
+    const int ch = v >> 5, o = v & 31, r = (ch & 3) + (o >= 16 ? 4 : 0), lane = (ch >> 2) * 16 + (o & 15);
+    double t = 0.0;
+    for (int ww = 0; ww < nch; ++ww) t += red[r * SW_THREADS + ww * 64 + lane];
+    g2[8 * 512 + v] = t;
+  }
+}
+
+// gconv as stem12_final; gw2[o][j * 16 + ch] = sum over the blocks (in order) of g2part[b][j][ch][o]: block 0 the former,
+// blocks 1 .. the latter, 128 columns per block, eight segments of the block range each summing 32 partials in flight
+__global__ __launch_bounds__(BN_FINAL_THREADS) void stem12w_final(int blocks, const double* __restrict__ wpart,
+                                                                 const double* __restrict__ g2part,
+                                                                 const float* __restrict__ sums,
+                                                                 const float* __restrict__ stats,
+                                                                 const float* __restrict__ bw, double m,
+                                                                 float* __restrict__ gw, float* __restrict__ gw2) {
+  if (blockIdx.x == 0) {
+    __shared__ double tot[3 * 144];
+    for (int a = 0; a < 3; ++a) bn_final_sums(wpart + a * 144, 144, blocks, tot + a * 144, 3 * 144);
+    for (int v = threadIdx.x; v < 144; v += BN_FINAL_THREADS) {
+      const int ch = v / 9;
+      const double mg = (double)sums[ch] / m, mgx = (double)sums[16 + ch] / m;
+      const double isw = (double)stats[16 + ch] * (double)bw[ch];
+      gw[v] = (float)(isw * (tot[v] - mg * tot[144 + v] - mgx * tot[288 + v]));
+    }
+    return;
+  }
+  __shared__ double seg[8][128];
+  const int col = (blockIdx.x - 1) * 128 + (threadIdx.x & 127), sg = threadIdx.x >> 7;
+  const int per = (blocks + 7) / 8, b0 = sg * per, b1 = b0 + per < blocks ? b0 + per : blocks;
+  double acc = 0.0;
+  if (col < SW_G2) {
+    int b = b0;
+    for (; b + 31 < b1; b += 32) {
+      double v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) v[u] = g2part[(size_t)(b + u) * SW_G2 + col];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) acc += v[u];
+    }
+    for (; b < b1; ++b) acc += g2part[(size_t)b * SW_G2 + col];
+  }
+  seg[sg][threadIdx.x & 127] = acc;
+  __syncthreads();
+  if (sg == 0 && col < SW_G2) {
+    double t = 0.0;
+    for (int u = 0; u < 8; ++u) t += seg[u][threadIdx.x];
+    const int o = col & 31, jc = col >> 5;  // jc = j * 16 + ch
+    gw2[o * 144 + jc] = (float)t;
+  }
+}
+
+int stem12w_grid(int nimg) { return nimg < SW_GRID ? (nimg < 1 ? 1 : nimg) : SW_GRID; }
+
+long long stem12w_scratch_doubles(int nimg) {
+  const long long gr = stem12w_grid(nimg);
+  return gr * 32 + 16 + gr * 3 * 144 + gr * SW_G2;
+}
+
+bool stem12w_covers(int n2) { return n2 >= 1 && n2 <= 16 * SW_MAX_CHUNKS; }
+
+hipError_t launch_stem12_backward_w2(const Stem1& s, const float* bw, const float* bb, const float* stats, int act,
+                                     float slope, const float* gz2, int n2, const float* w2t, float* gconv, float* gbw,
+                                     float* gbb, float* gw2, double* part, hipStream_t st) {
+  const int grid = stem12w_grid(s.nimg);
+  float* sums = reinterpret_cast<float*>(part + (size_t)grid * 32);
+  double* wpart = part + (size_t)grid * 32 + 16;
+  double* g2part = wpart + (size_t)grid * 3 * 144;
+  Sw12Args q{bw, bb, stats, gz2, w2t, part, wpart, g2part, slope, n2};
+  long long room = s.ld - s.off;
+  const int cap = (int)(room < 1 ? 1 : room < SM_IMG_CAP ? room : SM_IMG_CAP);
+  const size_t lds = sw_lds_bytes(n2, cap);
+  const bool v4 = ((uintptr_t)(s.obs + s.off) & 15) == 0 && (s.ld & 3) == 0;
+  static bool attr = false;
+  if (!attr) {  // (> 64 KB of dynamic LDS: every instantiation opts in once)
+    const void* ks[4] = {reinterpret_cast<const void*>(&stem12w_kernel<GR_POLICY_ACT_ELU, true>),
+                         reinterpret_cast<const void*>(&stem12w_kernel<GR_POLICY_ACT_ELU, false>),
+                         reinterpret_cast<const void*>(&stem12w_kernel<GR_POLICY_ACT_LRELU, true>),
+                         reinterpret_cast<const void*>(&stem12w_kernel<GR_POLICY_ACT_LRELU, false>)};
+    for (const void* k : ks) {
+      const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)sw_lds_bytes(16 * SW_MAX_CHUNKS, SM_IMG_CAP));  // (the largest)
+      if (e != hipSuccess) return e;
+    }
+    attr = true;
+  }
+  if (act == GR_POLICY_ACT_ELU) {
+    if (v4)
+      hipLaunchKernelGGL((stem12w_kernel<GR_POLICY_ACT_ELU, true>), dim3(grid), dim3(SW_THREADS), lds, st, s, q, cap);
+    else
+      hipLaunchKernelGGL((stem12w_kernel<GR_POLICY_ACT_ELU, false>), dim3(grid), dim3(SW_THREADS), lds, st, s, q, cap);
+  } else {
+    if (v4)
+      hipLaunchKernelGGL((stem12w_kernel<GR_POLICY_ACT_LRELU, true>), dim3(grid), dim3(SW_THREADS), lds, st, s, q, cap);
+    else
+      hipLaunchKernelGGL((stem12w_kernel<GR_POLICY_ACT_LRELU, false>), dim3(grid), dim3(SW_THREADS), lds, st, s, q, cap);
+  }
+  hipLaunchKernelGGL(bn_bwd_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, s.c, grid, part, gbw, gbb, sums);
+  hipLaunchKernelGGL(stem12w_final, dim3(1 + (SW_G2 + 127) / 128), dim3(BN_FINAL_THREADS), 0, st, grid, wpart, g2part,
+                     sums, stats, bw, (double)s.nimg * (double)(s.na + s.nbt), gconv, gw2);
+  return hipGetLastError();
+}
+
 }  // namespace gr

@@ -1101,6 +1101,25 @@ int gr_stem12_backward(const float* obs, int64_t ld, int64_t off, const int64_t*
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
+int64_t gr_stem12_backward_w2_scratch_doubles(int32_t nimg) {
+  return nimg < 1 ? GR_ERR_ARG : (int64_t)gr::stem12w_scratch_doubles(nimg);
+}
+
+int gr_stem12_backward_w2(const float* obs, int64_t ld, int64_t off, const int64_t* rows, int32_t nimg, const int16_t* pix,
+                          int32_t na, int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b,
+                          const float* stats, int32_t act, float slope, const float* gz2, int32_t n2, const float* w2t,
+                          float* g_conv_w, float* g_bn_w, float* g_bn_b, float* g_w2, double* part, void* stream) {
+  if (!stem1_args_ok(obs, nimg, pix, na, nb, conv_w, c, bn_w, bn_b) || c != 16 || !stats || !gz2 || !w2t ||
+      !g_conv_w || !g_bn_w || !g_bn_b || !g_w2 || !part || !aligned16(gz2) || !aligned16(w2t) || !aligned16(stats) ||
+      (act != GR_POLICY_ACT_LRELU && act != GR_POLICY_ACT_ELU) || !gr::stem12w_covers(n2) || na != 9 * n2 ||
+      (int64_t)nimg * n2 * 32 >= (int64_t)1 << 31)
+    return GR_ERR_ARG;
+  const gr::Stem1 s = stem1_of(obs, ld, off, rows, nimg, pix, na, nb, conv_w, c, (int64_t)nimg * na);
+  const hipError_t e = gr::launch_stem12_backward_w2(s, bn_w, bn_b, stats, act, slope, gz2, n2, w2t, g_conv_w, g_bn_w,
+                                                     g_bn_b, g_w2, part, (hipStream_t)stream);
+  return e == hipSuccess ? GR_OK : GR_ERR_HIP;
+}
+
 int gr_column_sum_partials(int64_t rows) { return rows < 0 ? GR_ERR_ARG : gr::column_sum_blocks(rows); }
 
 int gr_column_sum(const void* x, int dtype, int64_t rows, int32_t cols, float* partial, float* out, void* stream) {

@@ -141,20 +141,33 @@ class _Stem1(torch.autograd.Function):
         return None, gconv.view(wshape), gbw, gbb, None, None, None, None, None, None, None
 
 
+# conv2's weight gradient inside the first block's backward (gr_stem12_backward_w2: y1 recomputed there, so the forward
+# stores no y1 and no separate gz2^T y1 pass runs); False: the round-5 form (y1 stored, gr_patch_wgrad) for A/B
+STEM12_W2 = True
+STEM12_W2_MAX_N2 = 80  # (gr_stem12_backward_w2 covers conv2 patch counts up to 80 per image: 72 x 96 images)
+
+
+def _w2_path(fused_forward: bool, na: int) -> bool:
+    return STEM12_W2 and fused_forward and 1 <= na // 9 <= STEM12_W2_MAX_N2
+
+
 class _Stem12(torch.autograd.Function):
     """The first block (as _Stem1, C = 16) followed by conv2: z2 = y1.view(-1, 144) @ w2^T, w2 [32, 144] in (position j,
-    channel) column order.  The forward computes conv2 inside the first block's apply pass (gr_stem12_forward: y1 is
-    stored for conv2's weight gradient but not read back); the backward takes conv2's output gradient straight into
-    the first block's passes (gr_stem12_backward): conv2's input gradient, a [rows, 144] matrix, is never written.
-    conv2's weight gradient is the split-K product of gz2 and the saved y1."""
+    channel) column order.  The forward computes conv2 inside the first block's apply pass (gr_stem12_forward); the
+    backward takes conv2's output gradient straight into the first block's passes: conv2's input gradient, a
+    [rows, 144] matrix, is never written, and conv2's weight gradient gz2^T y1 is contracted there too from y1
+    recomputed in registers (gr_stem12_backward_w2), so y1 itself is never written either.  (STEM12_W2 False: y1 is
+    stored by the forward and conv2's weight gradient is the split-K product of gz2 and the saved y1.)"""
 
     @staticmethod
     def forward(ctx, img, conv_w, bn_w, bn_b, w2, pix, na, nb, eps, act, slope, fused_forward=True, rows=None,
                 keep_y=True):
         lib = _abi.load()
         nimg = img.shape[0] if rows is None else rows.numel()
-        # (keep_y False: no backward will run, so y1 — kept only for conv2's weight gradient — is not stored)
-        keep_y = keep_y or not fused_forward
+        # (keep_y False: no backward will run, so y1 — kept only for conv2's weight gradient — is not stored; nor when
+        # that gradient is formed inside the first block's backward)
+        w2_path = _w2_path(fused_forward, na)
+        keep_y = (keep_y and not w2_path) or not fused_forward
         y = torch.empty(nimg * na if keep_y else 0, 16, device=img.device, dtype=torch.float32)
         stats = torch.empty(4, 16, device=img.device, dtype=torch.float32)
         part = torch.empty(int(lib.gr_stem1_scratch_doubles(nimg, na + nb, 16)), device=img.device, dtype=torch.float64)
@@ -181,6 +194,7 @@ class _Stem12(torch.autograd.Function):
         ctx.pix = pix
         ctx.rows = rows
         ctx.args = (na, nb, act, slope, conv_w.shape)
+        ctx.w2_path = w2_path
         ctx.mark_non_differentiable(stats)
         return z2, stats
 
@@ -194,16 +208,30 @@ class _Stem12(torch.autograd.Function):
         rows = ctx.rows
         nimg = img.shape[0] if rows is None else rows.numel()
         gz2 = gz2.contiguous()
-        gw2 = None
-        if ctx.needs_input_grad[4]:  # conv2's weight: gz2^T y1 patches (gr_patch_wgrad: MFMA, fixed-order sums)
-            from .linear import tall_wgrad
-
-            gw2 = tall_wgrad(gz2, y.view(y.shape[0] // 9, 144))
+        if gz2.data_ptr() % 16:
+            gz2 = gz2.clone()
         # w2t[j][g][ch][s] = W2[o = 8 g + s][j * 16 + ch]
         w2t = w2d.reshape(4, 8, 9, 16).permute(2, 0, 3, 1).contiguous()
         gconv = torch.empty(16, 9, device=img.device, dtype=torch.float32)
         gbw = torch.empty(16, device=img.device, dtype=torch.float32)
         gbb = torch.empty(16, device=img.device, dtype=torch.float32)
+        if ctx.w2_path:  # the first block's backward with conv2's dgrad and wgrad (y1 recomputed)
+            gw2 = torch.empty(32, 144, device=img.device, dtype=torch.float32)
+            part = torch.empty(int(lib.gr_stem12_backward_w2_scratch_doubles(nimg)), device=img.device,
+                               dtype=torch.float64)
+            rc = lib.gr_stem12_backward_w2(img.data_ptr(), img.stride(0), 0, _rows_ptr(rows), nimg, ctx.pix.data_ptr(),
+                                           na, nb, w.data_ptr(), 16, bw.data_ptr(), bb.data_ptr(), stats.data_ptr(), act,
+                                           float(slope), gz2.data_ptr(), na // 9, w2t.data_ptr(), gconv.data_ptr(),
+                                           gbw.data_ptr(), gbb.data_ptr(), gw2.data_ptr(), part.data_ptr(), _stream(img))
+            if rc != 0:
+                raise RuntimeError(f"gr_stem12_backward_w2 failed (status {rc})")
+            return (None, gconv.view(wshape), gbw, gbb, gw2 if ctx.needs_input_grad[4] else None, None, None, None,
+                    None, None, None, None, None, None)
+        gw2 = None
+        if ctx.needs_input_grad[4]:  # conv2's weight: gz2^T y1 patches (gr_patch_wgrad: MFMA, fixed-order sums)
+            from .linear import tall_wgrad
+
+            gw2 = tall_wgrad(gz2, y.view(y.shape[0] // 9, 144))
         part = torch.empty(int(lib.gr_stem1_scratch_doubles(nimg, na + nb, 16)), device=img.device, dtype=torch.float64)
         rc = lib.gr_stem12_backward(img.data_ptr(), img.stride(0), 0, _rows_ptr(rows), nimg, ctx.pix.data_ptr(), na, nb,
                                     w.data_ptr(), 16, bw.data_ptr(), bb.data_ptr(), stats.data_ptr(), act, float(slope),

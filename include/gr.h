@@ -37,8 +37,8 @@ extern "C" {
 
 /* 2: GR_NUM_PLANES 17 (obstacle hint, rotor constants), gr_policy_args.precision, the observation sink and the
  * status word; gr_policy_args_size.  3: gr_stem1_* y_rows / gy_rows.  4: the gr_stem1_* / gr_stem12_* row indices
- * (`rows` after `off`) */
-#define GR_ABI_VERSION 4
+ * (`rows` after `off`).  5: gr_stem12_backward_w2 (conv2's weight gradient inside the first block's backward) */
+#define GR_ABI_VERSION 5
 
 /* ---- status codes ---- */
 #define GR_OK 0
@@ -523,6 +523,16 @@ int gr_stem12_backward(const float* obs, int64_t ld, int64_t off, const int64_t*
                        int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b,
                        const float* stats, int32_t act, float slope, const float* gz2, int32_t n2, const float* w2t,
                        float* g_conv_w, float* g_bn_w, float* g_bn_b, double* part, void* stream);
+/* gr_stem12_backward plus conv2's own weight gradient g_w2 [32][144] (columns (j, ch), w2's layout in
+ * VisionActorCritic's patch GEMM): y1 = act(bn(conv1)) is recomputed from the image (bit-identical to the forward's),
+ * so gr_stem12_forward may be called with y = NULL.  n2 <= 80 (72 x 96 images: 80).  Workspace:
+ * gr_stem12_backward_w2_scratch_doubles(nimg) doubles.  Deterministic (fixed-order sums).  Replaces the pair
+ * gr_stem12_backward + gr_patch_wgrad(gz2, y1) of the reference's conv2 backward (vision_actor_critic.py:93-105). */
+int64_t gr_stem12_backward_w2_scratch_doubles(int32_t nimg);
+int gr_stem12_backward_w2(const float* obs, int64_t ld, int64_t off, const int64_t* rows, int32_t nimg, const int16_t* pix,
+                          int32_t na, int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b,
+                          const float* stats, int32_t act, float slope, const float* gz2, int32_t n2, const float* w2t,
+                          float* g_conv_w, float* g_bn_w, float* g_bn_b, float* g_w2, double* part, void* stream);
 
 /* Device status: the GR_STATUS_* bits the kernels of this context raised since the last clear (0: none).
  * Synchronises `stream` (the stream the steps ran on); clear != 0 resets the word.  A raised bit means the

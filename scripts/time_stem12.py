@@ -23,7 +23,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nimg", type=int, default=24576)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--stored-y1", action="store_true", help="the round-5 backward (y1 stored, conv2's weight gradient "
+                    "by gr_patch_wgrad) instead of gr_stem12_backward_w2")
     a = ap.parse_args()
+    if a.stored_y1:
+        from generalizableracing_amd.rsl_rl import fused_bn
+
+        fused_bn.STEM12_W2 = False
     dev = "cuda:0"
     pol = VisionActorCritic(16 + 72 * 96, 16 + 72 * 96, 4, actor_hidden_dims=[32], critic_hidden_dims=[32])
     _, _, na, nb, _, n2, pix = pol._patch_index(dev)
@@ -50,7 +56,7 @@ def main():
         step()
     e1.record()
     torch.cuda.synchronize()
-    print(json.dumps({"nimg": a.nimg, "reps": a.reps, "ms_fwd_bwd": e0.elapsed_time(e1) / a.reps}))
+    print(json.dumps({"nimg": a.nimg, "reps": a.reps, "stored_y1": a.stored_y1, "ms_fwd_bwd": e0.elapsed_time(e1) / a.reps}))
 
 
 if __name__ == "__main__":

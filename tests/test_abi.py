@@ -150,6 +150,28 @@ def test_stem12_rejects_shapes_it_does_not_cover():
     assert call(act=7) == -1
 
 
+def test_stem12_w2_backward_rejects_shapes_it_does_not_cover():
+    """gr_stem12_backward_w2 (conv2's weight gradient inside the first block's backward) covers what gr_stem12_backward
+    covers with at most 80 conv2 patches per image (its offsets live in registers) and a gw2 output; anything else is
+    an argument error before any launch.  Its workspace: per workgroup (<= 256) the BN, conv1 and conv2 partials."""
+    lib = _abi.load()
+    p = 0x10000
+
+    def call(c=16, na=720, nb=48, n2=80, gz2=p, w2t=p, gw2=p, act=_abi.GR_POLICY_ACT_LRELU):
+        return lib.gr_stem12_backward_w2(p, 6928, 16, None, 8, p, na, nb, p, c, p, p, p, act, 0.01, gz2, n2, w2t, p, p,
+                                         p, gw2, p, None)
+
+    assert call(c=8) == -1
+    assert call(n2=81, na=729) == -1   # past the 80 patches the kernel holds
+    assert call(na=721) == -1
+    assert call(gz2=p + 4) == -1
+    assert call(gw2=None) == -1
+    assert call(act=7) == -1
+    assert lib.gr_stem12_backward_w2_scratch_doubles(0) == -1
+    assert lib.gr_stem12_backward_w2_scratch_doubles(1) == 32 + 16 + 432 + 4608
+    assert lib.gr_stem12_backward_w2_scratch_doubles(24576) == 256 * (32 + 432 + 4608) + 16
+
+
 def test_stem12_forward_rejects_shapes_it_does_not_cover():
     """gr_stem12_forward (conv2 inside the first block's apply pass): 16 channels, na = 9 n2, 16-byte aligned outputs
     and weights; anything else is an argument error before any launch."""

@@ -92,6 +92,54 @@ def test_stem12_backward_matches_unfused_and_float64(img_res, nimg, act):
         assert _rel(g_f[k], g64[k]) <= 1e-4, (k, "vs float64", _rel(g_f[k], g64[k]))
 
 
+@pytest.mark.parametrize("img_res,nimg,act,indexed", [((72, 96), 512, "lrelu", False), ((72, 96), 300, "elu", True),
+                                                      ((36, 48), 300, "lrelu", False), ((72, 96), 1, "lrelu", False),
+                                                      ((72, 96), 700, "lrelu", True)])
+def test_stem12_w2_backward_matches_the_stored_y1_path(img_res, nimg, act, indexed):
+    """gr_stem12_backward_w2 (conv2's weight gradient inside the first block's backward, y1 recomputed, the forward
+    storing no y1) against the round-5 pair (y1 stored by the forward, gr_stem12_backward + gr_patch_wgrad): conv2's
+    output bit-identical, every gradient within 1e-5 relative (the conv1 weight's within 1e-4: a cancelling
+    combination of three sums, reduced in another order), the same running statistics; repeats bit-identical.
+    Row-indexed batches (the graphed update's form) included; 700 images run 256 workgroups of 2-3 images."""
+    from generalizableracing_amd.rsl_rl import fused_bn
+    from generalizableracing_amd.rsl_rl.fused_bn import stem12_bn_act_conv
+
+    pol = _model(img_res, act, seed=21)
+    conv1, bn1, actm, conv2 = pol.stem[0], pol.stem[1], pol.stem[2], pol.stem[3]
+    idx, idx_left, n1, n1_left, n3, n2, pix16 = pol._patch_index(DEV)
+    h, w = img_res
+    g = torch.Generator(device=DEV).manual_seed(nimg)
+    src = torch.rand(nimg + 37, 16 + h * w, device=DEV, generator=g) * 8.0 + 0.5
+    rows = torch.randperm(nimg + 37, device=DEV, generator=g)[:nimg] if indexed else None
+    img = src[:, 16:] if indexed else src[:nimg, 16:]
+    gz = torch.randn(nimg * n2, 32, device=DEV, generator=g)
+
+    def run(w2_path):
+        old = fused_bn.STEM12_W2
+        fused_bn.STEM12_W2 = w2_path
+        try:
+            bn = copy.deepcopy(bn1)
+            cw = conv1.weight.detach().clone().requires_grad_(True)
+            w2 = conv2.weight.detach().permute(0, 2, 3, 1).reshape(32, 144).clone().requires_grad_(True)
+            z2 = stem12_bn_act_conv(bn, actm, cw, w2, img, pix16, n1, n1_left, rows=rows)
+            (z2 * gz).sum().backward()
+            return z2.detach(), {"conv1": cw.grad, "bn_w": bn.weight.grad, "bn_b": bn.bias.grad, "conv2": w2.grad}, bn
+        finally:
+            fused_bn.STEM12_W2 = old
+
+    z_new, g_new, bn_new = run(True)
+    z_old, g_old, bn_old = run(False)
+    assert torch.equal(z_new, z_old)
+    assert torch.equal(bn_new.running_mean, bn_old.running_mean)
+    assert torch.equal(bn_new.running_var, bn_old.running_var)
+    for k in g_old:
+        tol = 1e-4 if k == "conv1" else 1e-5
+        assert _rel(g_new[k], g_old[k]) <= tol, (k, _rel(g_new[k], g_old[k]))
+    _, g_again, _ = run(True)
+    for k in g_new:
+        assert torch.equal(g_new[k], g_again[k]), k
+
+
 def test_stem12_repeats_bit_identical():
     pol = _model((72, 96), "lrelu", seed=5)
     g = torch.Generator(device=DEV).manual_seed(2)
