@@ -1367,9 +1367,15 @@ struct Sw12Args {
   int n2;
 };
 
-__host__ __device__ inline int sw_gz_floats(int n2) { return (n2 * 32 + 255) & ~255; }
+// an image buffer: the staged floats (a DMA instruction's 256 rounded up) + 4 (a zero float, 16-byte aligned stride)
+__host__ __device__ inline int sw_img_stride(int cap) { return (int)sm_img_floats(cap) + 4; }
+// a gz2 buffer: 16 rows per chunk (rows n2 .. 16 nch zero), at least the DMA's 256-float granularity
+__host__ __device__ inline int sw_gz_stride(int n2) {
+  const int rows = (n2 + 15) / 16 * 16 * 32, dma = (n2 * 32 + 255) & ~255;
+  return rows > dma ? rows : dma;
+}
 __host__ __device__ inline size_t sw_lds_bytes(int n2, int cap) {
-  const size_t b = 4 * (2 * sm_img_floats(cap) + 2 * (size_t)sw_gz_floats(n2));
+  const size_t b = 4 * (2 * (size_t)sw_img_stride(cap) + 2 * (size_t)sw_gz_stride(n2));
   return b < 8 * 8 * SW_THREADS ? 8 * 8 * SW_THREADS : b;  // (the end's reductions: 8 doubles per thread)
 }
 // LDS float of gz2[row r][o]: the two 16-float halves of rows with r & 4 swapped
@@ -1397,23 +1403,34 @@ __device__ __forceinline__ void sw_dma_gz2(const float* g, float* dst, int nflt,
   for (int o = 256 * w; o < nflt; o += 256 * SW_WAVES) {
     const int slot = o / 4 + lane, r = slot >> 3, q4 = slot & 7;
     const int i = 4 * (r * 8 + (q4 ^ (r & 4)));
-    __builtin_amdgcn_global_load_lds((sm_glob_void_t*)(g + (i < nflt ? i : 0)), (sm_lds_void_t*)(dst + o), 16, 0, 0);
+    if (i < nflt)  // (lanes past the rows write nothing: the buffer's rows n2 .. keep their zeros)
+      __builtin_amdgcn_global_load_lds((sm_glob_void_t*)(g + i), (sm_lds_void_t*)(dst + o), 16, 0, 0);
   }
 }
 
-template <int ACT, bool V4>
+// NCH: the 16-patch chunks per image (n2 <= 16 NCH), a compile-time constant so every tile of a wave is straight-line
+// code (5 at 72 x 96); 0: taken from n2 at run time (other image sizes; the same arithmetic).  Image buffers carry one
+// zero float past their end and the gz2 buffers zero rows up to 16 nch: the gathers of rows past n2 and of taps past 9
+// read zeros there (gy1 = 0 and G2 += 0 on rows past n2, B operands 0), so no per-row masks are applied.
+template <int ACT, bool V4, int NCH>
 __global__ __launch_bounds__(SW_THREADS) void stem12w_kernel(Stem1 s, Sw12Args q, int cap) {
   extern __shared__ float4 sm_dyn4[];
   __shared__ int s_span;
   const int na = s.na, nbt = s.nbt, ncell = na + nbt, n2 = q.n2;
-  const int nch = (n2 + 15) / 16, ntb = (nbt + 15) / 16;
-  const int imgf = (int)sm_img_floats(cap), gzf = sw_gz_floats(n2);
+  const int nch = NCH > 0 ? NCH : (n2 + 15) / 16, ntb = (nbt + 15) / 16;
+  const int imgf = sw_img_stride(cap), gzf = sw_gz_stride(n2);
   float* im0 = reinterpret_cast<float*>(sm_dyn4);
   float* im1 = im0 + imgf;
   float* gz0 = im1 + imgf;
   float* gz1 = gz0 + gzf;
   const int l = (int)(threadIdx.x & 63), i = l & 15, g = l >> 4, w = (int)sm_wave();
   if (threadIdx.x == 0) s_span = 0;
+  // the zero float past each image buffer, the gz2 buffers' rows n2 .. 16 nch (never written by the DMA)
+  if (threadIdx.x < 2) (threadIdx.x ? im1 : im0)[imgf - 4] = 0.0f;
+  for (int k = n2 * 32 + (int)threadIdx.x; k < gzf; k += SW_THREADS) {
+    gz0[k] = 0.0f;
+    gz1[k] = 0.0f;
+  }
   __syncthreads();
   int mx = 0;
   for (int k = threadIdx.x; k < ncell * 9; k += SW_THREADS) {
@@ -1425,23 +1442,24 @@ __global__ __launch_bounds__(SW_THREADS) void stem12w_kernel(Stem1 s, Sw12Args q
   const int span = s_span;
   const bool staged = span <= cap;
   const bool v4 = V4 && (span & 3) == 0;
+  const int zero = staged ? imgf - 4 : 0;  // where a masked gather reads (LDS: the zero float; global: pixel 0, masked)
 
   float wb[3];  // B operand of conv1: W1[ch i][tap g + 4 c] (0 for taps >= 9)
 #pragma unroll
   for (int c = 0; c < 3; ++c) wb[c] = g + 4 * c < 9 ? s.w[i * 9 + g + 4 * c] : 0.0f;
   const float mu = q.stats[i], is = q.stats[16 + i], wv = q.bw[i], bv = q.bb[i];
 
-  // the wave's tiles: t < nch = (chunk t, position w); t == nch = (chunk w, position 8) when w < nch.  Per tile the
-  // A-layout pixel offsets (row i: cell 9 p + j, taps g, g + 4, 8), the B-layout ones (rows 4 g + v, tap i) and the
-  // live-row bits (patch < n2; B also tap i < 9)
-  constexpr int NT = SW_MAX_CHUNKS + 1;
-  int oa[NT][3], ob[NT][4];
-  unsigned live = 0u, bliv = 0u;
+  // the wave's tiles: t < nch = (chunk t, position w), and (chunk w, position 8) when w < nch (`extra`).  Per tile the
+  // A-layout pixel offsets (row i: cell 9 p + j, taps g, g + 4, 8; rows past n2 clamped: their outputs meet zero gy1
+  // and zero B operands) and the B-layout ones (rows 4 g + v, tap i; `zero` past n2 or for taps >= 9)
+  constexpr int NM = NCH > 0 ? NCH : SW_MAX_CHUNKS;
+  int oa[NM + 1][3], ob[NM + 1][4];
+  unsigned bliv = 0u;  // (global gathers only) B-operand bits
   const bool extra = w < nch;
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int c = t < nch ? t : w, j = t < nch ? w : 8;
-    const bool on = t < nch || (t == nch && extra);
+  for (int t = 0; t <= NM; ++t) {
+    const int c = t < NM ? t : w, j = t < NM ? w : 8;
+    const bool on = t < NM ? t < nch : extra;
     const int pa = on ? (16 * c + i < n2 ? 16 * c + i : n2 - 1) : 0;
     const short* ta = s.pix + (size_t)(9 * pa + j) * 9;
     oa[t][0] = ta[g];
@@ -1450,12 +1468,16 @@ __global__ __launch_bounds__(SW_THREADS) void stem12w_kernel(Stem1 s, Sw12Args q
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int p = 16 * c + 4 * g + v;
-      const bool ok = on && p < n2;
-      ob[t][v] = (ok && i < 9) ? s.pix[(size_t)(9 * p + j) * 9 + i] : 0;
-      live |= (ok ? 1u : 0u) << (4 * t + v);
-      bliv |= ((ok && i < 9) ? 1u : 0u) << (4 * t + v);
+      const bool ok = on && p < n2 && i < 9;
+      ob[t][v] = ok ? s.pix[(size_t)(9 * p + j) * 9 + i] : zero;
+      bliv |= (ok ? 1u : 0u) << (4 * t + v);
     }
   }
+  // gz2 in LDS (sw_gz_at): A of gy1 = row 16 c + i, floats 8 g .. 8 g + 7; B of G2 = rows 16 c + 4 g + v, o = i and
+  // 16 + i.  Row bit 2 is (i & 4) for the former and (g & 1) for the latter in every chunk: per-lane bases, the
+  // chunk (512 c) and v (32 v) as immediate offsets
+  const int zab = i * 32 + ((8 * g) ^ ((i & 4) << 2));
+  const int zbb = 128 * g + (i ^ ((g & 1) << 4));
   // conv2's weight fragments (B of gy1 = gz2 W2): position w, and position 8 for the extra tile
   float wf[8], wf8[8];
   {
@@ -1491,52 +1513,45 @@ __global__ __launch_bounds__(SW_THREADS) void stem12w_kernel(Stem1 s, Sw12Args q
     sm4 ga = {0.0f, 0.0f, 0.0f, 0.0f}, gb = {0.0f, 0.0f, 0.0f, 0.0f};
     sm4 ga8 = {0.0f, 0.0f, 0.0f, 0.0f}, gb8 = {0.0f, 0.0f, 0.0f, 0.0f};
     auto run = [&](auto from_lds) {
-      const float* src = decltype(from_lds)::value ? im : gim;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        if (!(t < nch || (t == nch && extra))) continue;  // (wave-uniform)
-        const int c = t < nch ? t : w;
+      constexpr bool LDS = decltype(from_lds)::value;
+      const float* src = LDS ? im : gim;
+      // one table-a tile: chunk base zc = 512 c (gz2 floats), pixel offsets oa / ob, the position's W2 fragments, its
+      // G2 accumulators
+      auto tile = [&](int t, int zc, const int (&oa_)[3], const int (&ob_)[4], const float (&f)[8], sm4& ha, sm4& hb) {
         float pa[3], pb[4];
 #pragma unroll
-        for (int u = 0; u < 3; ++u) pa[u] = src[oa[t][u]];
+        for (int u = 0; u < 3; ++u) pa[u] = src[oa_[u]];
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          const float p = src[ob[t][v]];
-          pb[v] = (bliv >> (4 * t + v)) & 1u ? p : 0.0f;
+          const float p = src[ob_[v]];
+          pb[v] = LDS || ((bliv >> (4 * t + v)) & 1u) ? p : 0.0f;
         }
-        // gz2 fragments: A of gy1 (row 16 c + i, o = 8 g .. 8 g + 7), B of G2 (rows 16 c + 4 g + v, o = i and 16 + i)
-        const int ra = 16 * c + i < n2 ? 16 * c + i : n2 - 1;
-        const float4 z0 = *reinterpret_cast<const float4*>(gzs + sw_gz_at(ra, 8 * g));
-        const float4 z1 = *reinterpret_cast<const float4*>(gzs + sw_gz_at(ra, 8 * g + 4));
+        const float* za = gzs + zc + zab;
+        const float4 z0 = *reinterpret_cast<const float4*>(za);
+        const float4 z1 = *reinterpret_cast<const float4*>(za + 4);
         float zb[4], zb2[4];
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          int rb = 16 * c + 4 * g + v;
-          rb = rb < n2 ? rb : n2 - 1;
-          zb[v] = gzs[sw_gz_at(rb, i)];
-          zb2[v] = gzs[sw_gz_at(rb, 16 + i)];
+          zb[v] = gzs[zc + zbb + 32 * v];
+          zb2[v] = gzs[zc + (zbb ^ 16) + 32 * v];
         }
         const sm4 x = sm_conv(pa, wb);
-        auto gy1 = [&](const float (&f)[8]) {
-          sm4 a = {0.0f, 0.0f, 0.0f, 0.0f};
-          a = sm_mfma(z0.x, f[0], a);
-          a = sm_mfma(z0.y, f[1], a);
-          a = sm_mfma(z0.z, f[2], a);
-          a = sm_mfma(z0.w, f[3], a);
-          a = sm_mfma(z1.x, f[4], a);
-          a = sm_mfma(z1.y, f[5], a);
-          a = sm_mfma(z1.z, f[6], a);
-          return sm_mfma(z1.w, f[7], a);
-        };
-        const sm4 gyt = t < nch ? gy1(wf) : gy1(wf8);  // (wave-uniform)
+        sm4 gyt = {0.0f, 0.0f, 0.0f, 0.0f};
+        gyt = sm_mfma(z0.x, f[0], gyt);
+        gyt = sm_mfma(z0.y, f[1], gyt);
+        gyt = sm_mfma(z0.z, f[2], gyt);
+        gyt = sm_mfma(z0.w, f[3], gyt);
+        gyt = sm_mfma(z1.x, f[4], gyt);
+        gyt = sm_mfma(z1.y, f[5], gyt);
+        gyt = sm_mfma(z1.z, f[6], gyt);
+        gyt = sm_mfma(z1.w, f[7], gyt);
         float gz[4], xh[4], y1[4];
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          const bool lv = (live >> (4 * t + v)) & 1u;
           xh[v] = (x[v] - mu) * is;
           const float zz = xh[v] * wv + bv;
-          gz[v] = lv ? gyt[v] * bn_dact<ACT>(zz, q.slope) : 0.0f;
-          y1[v] = lv ? bn_act<ACT>(zz, q.slope) : 0.0f;
+          gz[v] = gyt[v] * bn_dact<ACT>(zz, q.slope);
+          y1[v] = bn_act<ACT>(zz, q.slope);
           f0 += gz[v];
           f1 += gz[v] * xh[v];
           fa2 += pb[v];
@@ -1546,20 +1561,18 @@ __global__ __launch_bounds__(SW_THREADS) void stem12w_kernel(Stem1 s, Sw12Args q
           c1 = sm_mfma(gz[v], pb[v], c1);
           c3 = sm_mfma(xh[v], pb[v], c3);
         }
-        if (t < nch) {
 #pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            ga = sm_mfma(y1[v], zb[v], ga);
-            gb = sm_mfma(y1[v], zb2[v], gb);
-          }
-        } else {
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            ga8 = sm_mfma(y1[v], zb[v], ga8);
-            gb8 = sm_mfma(y1[v], zb2[v], gb8);
-          }
+        for (int v = 0; v < 4; ++v) {
+          ha = sm_mfma(y1[v], zb[v], ha);
+          hb = sm_mfma(y1[v], zb2[v], hb);
         }
+      };
+#pragma unroll
+      for (int t = 0; t < NM; ++t) {
+        if (NCH == 0 && t >= nch) break;  // (wave-uniform; compile-time when NCH > 0)
+        tile(t, 512 * t, oa[t], ob[t], wf, ga, gb);
       }
+      if (extra) tile(NM, 512 * w, oa[NM], ob[NM], wf8, ga8, gb8);
       // table b's tiles (cells under no conv2 patch: gz = 0; only A3 and A2), to the waves nch .. 7 in turn
       for (int tb = w - nch; tb >= 0 && tb < ntb; tb += SW_WAVES - nch) {
         const int r0 = 16 * tb, nv = nbt - r0 < 16 ? nbt - r0 : 16;
@@ -1706,6 +1719,27 @@ long long stem12w_scratch_doubles(int nimg) {
 
 bool stem12w_covers(int n2) { return n2 >= 1 && n2 <= 16 * SW_MAX_CHUNKS; }
 
+// every instantiation opts in to its > 64 KB of dynamic LDS once (the largest any shape needs)
+template <int ACT, bool V4, int NCH>
+static hipError_t sw_launch_t(int grid, size_t lds, hipStream_t st, const Stem1& s, const Sw12Args& q, int cap) {
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem12w_kernel<ACT, V4, NCH>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)sw_lds_bytes(16 * SW_MAX_CHUNKS, SM_IMG_CAP));
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((stem12w_kernel<ACT, V4, NCH>), dim3(grid), dim3(SW_THREADS), lds, st, s, q, cap);
+  return hipGetLastError();
+}
+// 72 x 96 images (five chunks) straight-line; other sizes with the chunk count at run time
+template <int ACT, bool V4>
+static hipError_t sw_launch(int nch, int grid, size_t lds, hipStream_t st, const Stem1& s, const Sw12Args& q, int cap) {
+  return nch == SW_MAX_CHUNKS ? sw_launch_t<ACT, V4, SW_MAX_CHUNKS>(grid, lds, st, s, q, cap)
+                              : sw_launch_t<ACT, V4, 0>(grid, lds, st, s, q, cap);
+}
+
 hipError_t launch_stem12_backward_w2(const Stem1& s, const float* bw, const float* bb, const float* stats, int act,
                                      float slope, const float* gz2, int n2, const float* w2t, float* gconv, float* gbw,
                                      float* gbb, float* gw2, double* part, hipStream_t st) {
@@ -1718,30 +1752,16 @@ hipError_t launch_stem12_backward_w2(const Stem1& s, const float* bw, const floa
   const int cap = (int)(room < 1 ? 1 : room < SM_IMG_CAP ? room : SM_IMG_CAP);
   const size_t lds = sw_lds_bytes(n2, cap);
   const bool v4 = ((uintptr_t)(s.obs + s.off) & 15) == 0 && (s.ld & 3) == 0;
-  static bool attr = false;
-  if (!attr) {  // (> 64 KB of dynamic LDS: every instantiation opts in once)
-    const void* ks[4] = {reinterpret_cast<const void*>(&stem12w_kernel<GR_POLICY_ACT_ELU, true>),
-                         reinterpret_cast<const void*>(&stem12w_kernel<GR_POLICY_ACT_ELU, false>),
-                         reinterpret_cast<const void*>(&stem12w_kernel<GR_POLICY_ACT_LRELU, true>),
-                         reinterpret_cast<const void*>(&stem12w_kernel<GR_POLICY_ACT_LRELU, false>)};
-    for (const void* k : ks) {
-      const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               (int)sw_lds_bytes(16 * SW_MAX_CHUNKS, SM_IMG_CAP));  // (the largest)
-      if (e != hipSuccess) return e;
-    }
-    attr = true;
-  }
+  const int nch = (n2 + 15) / 16;
+  hipError_t e = hipSuccess;
   if (act == GR_POLICY_ACT_ELU) {
-    if (v4)
-      hipLaunchKernelGGL((stem12w_kernel<GR_POLICY_ACT_ELU, true>), dim3(grid), dim3(SW_THREADS), lds, st, s, q, cap);
-    else
-      hipLaunchKernelGGL((stem12w_kernel<GR_POLICY_ACT_ELU, false>), dim3(grid), dim3(SW_THREADS), lds, st, s, q, cap);
+    e = v4 ? sw_launch<GR_POLICY_ACT_ELU, true>(nch, grid, lds, st, s, q, cap)
+           : sw_launch<GR_POLICY_ACT_ELU, false>(nch, grid, lds, st, s, q, cap);
   } else {
-    if (v4)
-      hipLaunchKernelGGL((stem12w_kernel<GR_POLICY_ACT_LRELU, true>), dim3(grid), dim3(SW_THREADS), lds, st, s, q, cap);
-    else
-      hipLaunchKernelGGL((stem12w_kernel<GR_POLICY_ACT_LRELU, false>), dim3(grid), dim3(SW_THREADS), lds, st, s, q, cap);
+    e = v4 ? sw_launch<GR_POLICY_ACT_LRELU, true>(nch, grid, lds, st, s, q, cap)
+           : sw_launch<GR_POLICY_ACT_LRELU, false>(nch, grid, lds, st, s, q, cap);
   }
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(bn_bwd_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, s.c, grid, part, gbw, gbb, sums);
   hipLaunchKernelGGL(stem12w_final, dim3(1 + (SW_G2 + 127) / 128), dim3(BN_FINAL_THREADS), 0, st, grid, wpart, g2part,
                      sums, stats, bw, (double)s.nimg * (double)(s.na + s.nbt), gconv, gw2);
