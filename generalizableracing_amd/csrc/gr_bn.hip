@@ -1227,6 +1227,8 @@ __global__ __launch_bounds__(SMF_THREADS) void stem12f_kernel(Stem1 s, Sm12fArgs
   }
 }
 
+hipError_t stem12g_launch(const Stem1& s, const Sm12fArgs& f, int act, hipStream_t st);  // (below, with stem12w)
+
 hipError_t launch_stem12_forward(const Stem1& s, const float* bw, const float* bb, float eps, int act, float slope,
                                  const float* w2f, int n2, float* y, float* z2, float* stats, double* part,
                                  hipStream_t st) {
@@ -1242,6 +1244,8 @@ hipError_t launch_stem12_forward(const Stem1& s, const float* bw, const float* b
   const size_t lds = sm_lds_bytes(s.na + s.nbt, cap);
   const bool v4 = ((uintptr_t)(s.obs + s.off) & 15) == 0 && (s.ld & 3) == 0;
   Sm12fArgs f{bw, bb, stats, w2f, y, z2, slope, n2};
+  // no y1 to store (the backward recomputes it, or no backward): the position-grouped kernel (stem12g_kernel)
+  if (!y && n2 <= 80) return stem12g_launch(s, f, act, st);
   if (act == GR_POLICY_ACT_ELU) {
     if (v4)
       hipLaunchKernelGGL((stem12f_kernel<GR_POLICY_ACT_ELU, true>), dim3(grid), dim3(SMF_THREADS), lds, st, s, f, cap);
@@ -1766,6 +1770,179 @@ hipError_t launch_stem12_backward_w2(const Stem1& s, const float* bw, const floa
   hipLaunchKernelGGL(stem12w_final, dim3(1 + (SW_G2 + 127) / 128), dim3(BN_FINAL_THREADS), 0, st, grid, wpart, g2part,
                      sums, stats, bw, (double)s.nimg * (double)(s.na + s.nbt), gconv, gw2);
   return hipGetLastError();
+}
+
+
+// ------------------------------------------------------------- the first block's apply pass + conv2, y1 not stored
+// stem12f_kernel gives each compute wave one 16-patch chunk and all nine positions (the conv2 sum over positions in
+// one MFMA chain): five compute waves per image (72 x 96: five chunks) on four SIMDs, two workgroups per CU.  Here a
+// unit is (chunk c, position group pg = positions 3 pg .. 3 pg + 2): 15 units per image over eight waves (two per
+// SIMD, the next image's staging shared), each unit's pixel offsets and W2 fragments held in registers for the whole
+// kernel.  A unit's partial z2 (its three positions) goes to LDS; after the image's barrier every thread sums the
+// three partials of its outputs in position-group order (fixed: deterministic) and stores z2.  Partials are double
+// buffered, so one barrier per image suffices.  y1 = act(bn(conv1)) exactly as stem12f_kernel computes it (conv1
+// transposed, the same expression), z2 = (j 0-2) + (j 3-5) + (j 6-8) in fp32.
+constexpr int SG_WAVES = 8;
+constexpr int SG_THREADS = 64 * SG_WAVES;
+constexpr int SG_UNITS = 3 * SW_MAX_CHUNKS;  // 15
+constexpr int SG_PLD = 36;                   // partial rows' stride (floats): 4 row groups on distinct banks
+constexpr int SG_PART = 16 * SG_PLD;         // floats per unit partial
+
+__host__ __device__ inline size_t sg_lds_bytes(int cap) {
+  return 4 * (2 * (size_t)sw_img_stride(cap) + 2 * (size_t)SG_UNITS * SG_PART);
+}
+
+template <int ACT, bool V4, int NCH>
+__global__ __launch_bounds__(SG_THREADS) void stem12g_kernel(Stem1 s, Sm12fArgs q, int cap) {
+  extern __shared__ float4 sm_dyn4[];
+  __shared__ int s_span;
+  const int ncell = s.na + s.nbt, n2 = q.n2;
+  const int nch = NCH > 0 ? NCH : (n2 + 15) / 16, nun = 3 * nch;
+  const int imgf = sw_img_stride(cap);
+  float* im0 = reinterpret_cast<float*>(sm_dyn4);
+  float* im1 = im0 + imgf;
+  float* pt0 = im1 + imgf;
+  float* pt1 = pt0 + SG_UNITS * SG_PART;
+  const int l = (int)(threadIdx.x & 63), lo = l & 15, kq = l >> 4, w = (int)sm_wave();
+  if (threadIdx.x == 0) s_span = 0;
+  __syncthreads();
+  int mx = 0;
+  for (int k = threadIdx.x; k < ncell * 9; k += SG_THREADS) {
+    const int t = s.pix[k];
+    mx = mx > t + 1 ? mx : t + 1;
+  }
+  atomicMax(&s_span, mx);
+  __syncthreads();
+  const int span = s_span;
+  const bool staged = span <= cap;
+  const bool v4 = V4 && (span & 3) == 0;
+
+  // conv1 as C[channel][cell]: A = W1[channel lo][tap kq + 4 c] (0 for taps >= 9); the lane's channels 4 kq + v
+  float wa[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) wa[c] = kq + 4 * c < 9 ? s.w[lo * 9 + kq + 4 * c] : 0.0f;
+  float mu[4], is[4], wv[4], bv[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int chn = 4 * kq + v;
+    mu[v] = q.stats[chn];
+    is[v] = q.stats[16 + chn];
+    wv[v] = q.bw[chn];
+    bv[v] = q.bb[chn];
+  }
+  // the wave's units w and w + 8: per position jj of the group, the pixel offsets (cell 9 p + j of patch
+  // p = 16 c + lo, clamped below n2: those rows' outputs are never stored) and W2's B fragments for o = lo, 16 + lo
+  const bool u1on = w + SG_WAVES < nun;
+  int po[2][3][3];
+  float4 b0[2][3], b1[2][3];
+#pragma unroll
+  for (int uu = 0; uu < 2; ++uu) {
+    const int u = w + SG_WAVES * uu;
+    const bool on = u < nun;
+    const int c = on ? u / 3 : 0, pg = on ? u % 3 : 0;
+    const int p = 16 * c + lo < n2 ? 16 * c + lo : n2 - 1;
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+      const int j = 3 * pg + jj;
+      const short* tt = s.pix + (size_t)(9 * p + j) * 9;
+      po[uu][jj][0] = tt[kq];
+      po[uu][jj][1] = tt[kq + 4];
+      po[uu][jj][2] = tt[8];
+      b0[uu][jj] = reinterpret_cast<const float4*>(q.w2f)[(j * 4 + kq) * 32 + lo];
+      b1[uu][jj] = reinterpret_cast<const float4*>(q.w2f)[(j * 4 + kq) * 32 + 16 + lo];
+    }
+  }
+  const int nmine = s.nimg > (int)blockIdx.x ? (s.nimg - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
+  if (staged && nmine > 0) sw_dma_image(stem_img(s, blockIdx.x), im0, span, v4, w);
+  __syncthreads();
+  for (int k = 0; k < nmine; ++k) {
+    const int b = (int)blockIdx.x + k * (int)gridDim.x;
+    const float* im = (k & 1) ? im1 : im0;
+    float* pt = (k & 1) ? pt1 : pt0;
+    if (staged && k + 1 < nmine) sw_dma_image(stem_img(s, b + (long long)gridDim.x), (k & 1) ? im0 : im1, span, v4, w);
+    auto run = [&](auto from_lds) {
+      const float* src = decltype(from_lds)::value ? im : stem_img(s, b);
+      auto unit = [&](int uu) {
+        float px[3][3];
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) px[jj][c] = src[po[uu][jj][c]];
+        sm4 z0 = {0.0f, 0.0f, 0.0f, 0.0f}, z1 = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) {
+          sm4 x = {0.0f, 0.0f, 0.0f, 0.0f};
+          x = sm_mfma(wa[0], px[jj][0], x);
+          x = sm_mfma(wa[1], px[jj][1], x);
+          x = sm_mfma(wa[2], px[jj][2], x);
+          float yv[4];
+#pragma unroll
+          for (int v = 0; v < 4; ++v) yv[v] = bn_act<ACT>((x[v] - mu[v]) * is[v] * wv[v] + bv[v], q.slope);
+          const float4 f0 = b0[uu][jj], f1 = b1[uu][jj];
+          z0 = sm_mfma(yv[0], f0.x, z0);
+          z0 = sm_mfma(yv[1], f0.y, z0);
+          z0 = sm_mfma(yv[2], f0.z, z0);
+          z0 = sm_mfma(yv[3], f0.w, z0);
+          z1 = sm_mfma(yv[0], f1.x, z1);
+          z1 = sm_mfma(yv[1], f1.y, z1);
+          z1 = sm_mfma(yv[2], f1.z, z1);
+          z1 = sm_mfma(yv[3], f1.w, z1);
+        }
+        // lane (o = lo, kq) holds the unit's partial z2[patch 4 kq + v][o] (z0) and [16 + o] (z1)
+        float* pr = pt + (w + SG_WAVES * uu) * SG_PART + 4 * kq * SG_PLD;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          pr[v * SG_PLD + lo] = z0[v];
+          pr[v * SG_PLD + 16 + lo] = z1[v];
+        }
+      };
+      if (NCH > 0 || w < nun) unit(0);
+      if (u1on) unit(1);
+    };
+    if (staged)
+      run(std::true_type{});
+    else
+      run(std::false_type{});
+    __syncthreads();  // the image's partials written, image k + 1 staged
+    // z2[b][p][o] = the three position groups' partials in order (consecutive threads: consecutive o, coalesced)
+    for (int qo = (int)threadIdx.x; qo < n2 * 32; qo += SG_THREADS) {
+      const int p = qo >> 5, o = qo & 31, c = p >> 4, pl = p & 15;
+      const float* a = pt + 3 * c * SG_PART + pl * SG_PLD + o;
+      q.z2[((size_t)b * n2 + p) * 32 + o] = (a[0] + a[SG_PART]) + a[2 * SG_PART];
+    }
+  }
+}
+
+template <int ACT, bool V4, int NCH>
+static hipError_t sg_launch_t(int grid, size_t lds, hipStream_t st, const Stem1& s, const Sm12fArgs& f, int cap) {
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem12g_kernel<ACT, V4, NCH>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)sg_lds_bytes(SM_IMG_CAP));
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((stem12g_kernel<ACT, V4, NCH>), dim3(grid), dim3(SG_THREADS), lds, st, s, f, cap);
+  return hipGetLastError();
+}
+template <int ACT, bool V4>
+static hipError_t sg_launch(int nch, int grid, size_t lds, hipStream_t st, const Stem1& s, const Sm12fArgs& f, int cap) {
+  return nch == SW_MAX_CHUNKS ? sg_launch_t<ACT, V4, SW_MAX_CHUNKS>(grid, lds, st, s, f, cap)
+                              : sg_launch_t<ACT, V4, 0>(grid, lds, st, s, f, cap);
+}
+
+hipError_t stem12g_launch(const Stem1& s, const Sm12fArgs& f, int act, hipStream_t st) {
+  const int grid = stem12w_grid(s.nimg);
+  long long room = s.ld - s.off;
+  const int cap = (int)(room < 1 ? 1 : room < SM_IMG_CAP ? room : SM_IMG_CAP);
+  const size_t lds = sg_lds_bytes(cap);
+  const bool v4 = ((uintptr_t)(s.obs + s.off) & 15) == 0 && (s.ld & 3) == 0;
+  const int nch = (f.n2 + 15) / 16;
+  if (act == GR_POLICY_ACT_ELU)
+    return v4 ? sg_launch<GR_POLICY_ACT_ELU, true>(nch, grid, lds, st, s, f, cap)
+              : sg_launch<GR_POLICY_ACT_ELU, false>(nch, grid, lds, st, s, f, cap);
+  return v4 ? sg_launch<GR_POLICY_ACT_LRELU, true>(nch, grid, lds, st, s, f, cap)
+            : sg_launch<GR_POLICY_ACT_LRELU, false>(nch, grid, lds, st, s, f, cap);
 }
 
 }  // namespace gr

@@ -97,8 +97,8 @@ def test_stem12_backward_matches_unfused_and_float64(img_res, nimg, act):
                                                       ((72, 96), 700, "lrelu", True)])
 def test_stem12_w2_backward_matches_the_stored_y1_path(img_res, nimg, act, indexed):
     """gr_stem12_backward_w2 (conv2's weight gradient inside the first block's backward, y1 recomputed, the forward
-    storing no y1) against the round-5 pair (y1 stored by the forward, gr_stem12_backward + gr_patch_wgrad): conv2's
-    output bit-identical, every gradient within 1e-5 relative (the conv1 weight's within 1e-4: a cancelling
+    storing no y1: stem12g_kernel) against the round-5 pair (y1 stored by stem12f_kernel, gr_stem12_backward +
+    gr_patch_wgrad): conv2's output within 1e-6, every gradient within 1e-5 relative (the conv1 weight's within 1e-4: a cancelling
     combination of three sums, reduced in another order), the same running statistics; repeats bit-identical.
     Row-indexed batches (the graphed update's form) included; 700 images run 256 workgroups of 2-3 images."""
     from generalizableracing_amd.rsl_rl import fused_bn
@@ -129,7 +129,8 @@ def test_stem12_w2_backward_matches_the_stored_y1_path(img_res, nimg, act, index
 
     z_new, g_new, bn_new = run(True)
     z_old, g_old, bn_old = run(False)
-    assert torch.equal(z_new, z_old)
+    # (the forward without y1 sums conv2's three position groups separately: another fp32 rounding of the same sum)
+    assert _rel(z_new, z_old) <= 1e-6, _rel(z_new, z_old)
     assert torch.equal(bn_new.running_mean, bn_old.running_mean)
     assert torch.equal(bn_new.running_var, bn_old.running_var)
     for k in g_old:
