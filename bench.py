@@ -932,10 +932,14 @@ def main():
         vis = bench_vision.run(argparse.Namespace(envs=4096, steps=8, iters=2, storage_bf16=False, no_fused_bn=False,
                                                   graph_update=True))
         progress("vision_train")
+        import time_stem12
+
+        stem = time_stem12.roofline(24576)  # one PPO mini-batch of images: the update's stem kernels against bounds
+        progress("vision_stem_roofline")
         extra["vision_train_total_fps_4096_envs"] = {
             "value": vis["train_total_fps"], "train_iter_s": vis["train_iter_s"],
             "rollout_env_steps_per_s": vis["rollout_env_steps_per_s"], "max_mem_GB": vis["max_mem_GB"],
-            "graph_update": vis["graph_update"],
+            "graph_update": vis["graph_update"], "stem_kernels_24576_images": stem,
             "note": "Perf/total_fps of QuadcopterVisionPPORunnerCfg (VisionActorCritic 72x96 stem: fused HIP first "
                     "block + conv2, BatchNorm + LeakyReLU passes, PPOL2C2 with the update's mini-batch steps as "
                     "hipGraph replays), obstacle tracks, fp32"}

@@ -353,13 +353,21 @@ class _GraphedStep:
         self.one = torch.ones((), device=dev)
         self.segmented = gdist.is_dist() or alg.graph_update_segmented
         self.per_step = self.segmented or alg.graph_update_per_step
+        # epoch graph + packed rows: the samples in the update's permutation order, gathered ONCE per update (every
+        # epoch uses the same partition, rollout_storage.py:152-191), so mini-batch i is the contiguous row slice i and
+        # the captured steps gather nothing (the per-step gathers were latency-bound launches, one per step)
+        self.pack_perm = torch.empty_like(self.pack) if self.pack is not None and not self.per_step else None
         self.graph = None  # one rank: an epoch's steps (per_step: one step)
         self.graph_b = None  # segmented: graph = segment A, graph_b = segment B
 
     def _gather(self, idx):
         """The mini-batch's fields by a static index buffer: one row gather of the packed samples (refilled
-        before every update's replays, RolloutStorage.pack_samples), or one gather per field for wide rows."""
+        before every update's replays, RolloutStorage.pack_samples), or one gather per field for wide rows.  idx a
+        (lo, hi) pair: rows lo .. hi of the permuted packed samples (pack_perm), views, no gather."""
         st = self.alg.storage
+        if isinstance(idx, tuple):
+            g = self.pack_perm[idx[0]:idx[1]]
+            return tuple(g[:, a:b] for a, b in self.cols)
         if self.cols is not None:
             g = self.pack.index_select(0, idx)
             return tuple(g[:, a:b] for a, b in self.cols)
@@ -444,6 +452,7 @@ class _GraphedStep:
         snap_o = {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in self.opt.state[p].items()}
                   for p in self.params}
         self.perm.copy_(torch.arange(self.perm.numel(), device=self.perm.device))
+        self._permute_pack()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         _lin._FORCE_FN = True  # bias gradients by gr_column_sum in the captured step (linear.bias_grad)
@@ -467,7 +476,8 @@ class _GraphedStep:
             else:  # an epoch: every mini-batch step, each on its slice of the permutation
                 with torch.cuda.graph(self.graph, stream=s):
                     for i in range(self.nmb):
-                        self._seg_a(self.perm[i * self.mb:(i + 1) * self.mb])
+                        lo, hi = i * self.mb, (i + 1) * self.mb
+                        self._seg_a((lo, hi) if self.pack_perm is not None else self.perm[lo:hi])
                         self._seg_b()
         finally:
             _lin._FORCE_FN = False
@@ -482,6 +492,10 @@ class _GraphedStep:
                 b.copy_(v)
             self.lr.copy_(snap_lr)
             self.acc.copy_(snap_acc)
+
+    def _permute_pack(self):
+        if self.pack_perm is not None:
+            torch.index_select(self.pack, 0, self.perm, out=self.pack_perm)
 
     def _refresh_sources(self):
         """Before an update's replays: this rollout's samples, packed in place (the graphs read the buffer)."""
@@ -516,6 +530,7 @@ class _GraphedStep:
         self.acc.zero_()
         if not self.per_step:
             self.perm.copy_(perm)
+            self._permute_pack()
         for _ in range(alg.num_learning_epochs):
             if not self.per_step:  # one replay per epoch
                 self.graph.replay()
