@@ -89,15 +89,14 @@ DEV_INLINE void reuse_rows(const CamArgs& a, const gr_cam_const* __restrict__ cc
   }
 }
 
-// obstacle slot from LDS (GR_CAM_OSLOT floats: frame and primitive = slot floats 0-15, window = 17-20)
+// obstacle slot from LDS (GR_CAM_OSLOT floats: frame and primitive = slot floats 0-15, what the hit and frustum tests
+// read; then the window's pixel rectangle u_lo, u_hi, v_lo, v_hi as ints, read by the tile masks and hit passes)
 DEV_INLINE void load_oslot(const float4* src, float s[GR_CAM_SLOT]) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const float4 q4 = src[k];
     s[4 * k] = q4.x; s[4 * k + 1] = q4.y; s[4 * k + 2] = q4.z; s[4 * k + 3] = q4.w;
   }
-  const float4 w4 = src[4];
-  s[GR_CS_AMIN] = w4.x; s[GR_CS_AMAX] = w4.y; s[GR_CS_BMIN] = w4.z; s[GR_CS_BMAX] = w4.w;
 }
 
 // the obstacle's record from global memory
@@ -108,6 +107,24 @@ DEV_INLINE void load_orec(const float* rec, float r[GR_OBST_FLOATS]) {
     const float4 v = r4[k];
     r[4 * k] = v.x; r[4 * k + 1] = v.y; r[4 * k + 2] = v.z; r[4 * k + 3] = v.w;
   }
+}
+
+// the pixel range {i : lo <= r[i] <= hi} of a decreasing ray table r[0 .. n) (a_u over u, b_v over v): [first, last],
+// empty when first > last.  Exactly the pixels a window test r[i] >= lo && r[i] <= hi admits
+DEV_INLINE void window_pixels(const float* __restrict__ r, int n, float lo, float hi, int& first, int& last) {
+  int a = 0, b = n;  // first i with r[i] <= hi
+  while (a < b) {
+    const int m = (a + b) >> 1;
+    if (r[m] <= hi) b = m; else a = m + 1;
+  }
+  first = a;
+  a = 0;
+  b = n;  // first i with r[i] < lo
+  while (a < b) {
+    const int m = (a + b) >> 1;
+    if (r[m] < lo) b = m; else a = m + 1;
+  }
+  last = a - 1;
 }
 
 // nearest obstacle crossing of the tile quad's four rays against one set-up slot
@@ -223,12 +240,19 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
       int nv = 0;
       for (int base = 0; base < nob; base += 64) {
         const int k = base + lane;
-        int ok = 0;
+        int ok = 0, u_lo = 0, u_hi = -1, v_lo = 0, v_hi = -1;
         if (k < nob) {
           float r[GR_OBST_FLOATS];
           load_orec(orecs + (size_t)k * GR_OBST_FLOATS, r);
           gr_cam_obst_setup(r, o, c0, c1, c2, cc->max_distance, s);
           ok = s[GR_CS_VALID] != 0.0f;
+          if (ok) {
+            // the window as the pixel rectangle it admits (a_u, b_v monotonic): the tile masks and the hit passes
+            // read it instead of testing rays; a window between pixel rays can be hit by none (dropped)
+            window_pixels(cc->ray_a, W, s[GR_CS_AMIN], s[GR_CS_AMAX], u_lo, u_hi);
+            window_pixels(cc->ray_b, H, s[GR_CS_BMIN], s[GR_CS_BMAX], v_lo, v_hi);
+            ok = u_lo <= u_hi && v_lo <= v_hi;
+          }
         }
         const uint64_t b = __ballot(ok);
         const int pos = nv + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
@@ -236,7 +260,8 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
 #pragma unroll
           for (int q = 0; q < 4; ++q)
             s_oslot[pos * (GR_CAM_OSLOT / 4) + q] = make_float4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
-          s_oslot[pos * (GR_CAM_OSLOT / 4) + 4] = make_float4(s[GR_CS_AMIN], s[GR_CS_AMAX], s[GR_CS_BMIN], s[GR_CS_BMAX]);
+          s_oslot[pos * (GR_CAM_OSLOT / 4) + 4] = make_float4(__int_as_float(u_lo), __int_as_float(u_hi),
+                                                              __int_as_float(v_lo), __int_as_float(v_hi));
         }
         const int nb = __popcll(b);
         if (nv + nb > GR_CAM_OBST_SLOTS && ofrom == nob) {
@@ -272,8 +297,9 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
       if constexpr (obst) {
         uint64_t tm = 0;
         for (int k = 0; k < ns; ++k) {
-          const float4 wk = s_oslot[k * (GR_CAM_OSLOT / 4) + 4];
-          bool meet = !(wk.y < a_lo || wk.x > a_hi || wk.w < b_lo || wk.z > b_hi);
+          const float4 wk = s_oslot[k * (GR_CAM_OSLOT / 4) + 4];  // pixel rectangle u_lo, u_hi, v_lo, v_hi
+          bool meet = !(__float_as_int(wk.y) < u0 || __float_as_int(wk.x) > u1 || __float_as_int(wk.w) < v0 ||
+                        __float_as_int(wk.z) > v1);
           if (meet) {
             float sk[GR_CAM_SLOT];
             load_oslot(s_oslot + k * (GR_CAM_OSLOT / 4), sk);
@@ -384,20 +410,16 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
         while (mo) {
           const int k = __builtin_ctzll(mo);
           mo &= mo - 1;
-          const float4 wk = s_oslot[k * (GR_CAM_OSLOT / 4) + 4];  // amin, amax, bmin, bmax
-          bool in = false;
-          if (lane < 32) {
-            const int u = u_t + lane;
-            in = u < W && s_ray_a[u] >= wk.x && s_ray_a[u] <= wk.y;
-          } else if (lane < 40) {
-            const int v = v0 + lane - 32;
-            in = v < H && s_ray_b[v] >= wk.z && s_ray_b[v] <= wk.w;
-          }
-          const uint64_t bal = __ballot(in);
-          const uint32_t cm = (uint32_t)bal, rm = (uint32_t)(bal >> 32) & 0xffu;
-          if (cm == 0u || rm == 0u) continue;
-          const int cu = u_t + __builtin_ctz(cm), wc = __popc(cm), rv = __builtin_ctz(rm), area = wc * __popc(rm);
-          const float inv_wc = 1.0f / (float)wc;
+          // the slot's pixel rectangle within this tile of the band (wave-uniform integer ranges)
+          const float4 wk = s_oslot[k * (GR_CAM_OSLOT / 4) + 4];
+          const int ulo = __float_as_int(wk.x), uhi = __float_as_int(wk.y), vlo = __float_as_int(wk.z),
+                    vhi = __float_as_int(wk.w);
+          const int cu = ulo > u_t ? ulo : u_t, cu1 = uhi < u_t + 31 ? uhi : u_t + 31;
+          const int rv = (vlo > v0 ? vlo : v0) - v0, rv1 = (vhi < v0 + 7 ? vhi : v0 + 7) - v0;
+          if (cu > cu1 || rv > rv1) continue;
+          const int wc = cu1 - cu + 1, area = wc * (rv1 - rv + 1);
+          // (idx / wc below exact for idx < 256, wc <= 32 with a 1-ulp reciprocal: see the 1e-3 margin)
+          const float inv_wc = __builtin_amdgcn_rcpf((float)wc);
           for (int done = 0; done < area;) {
             const int take = area - done < 64 - fill ? area - done : 64 - fill;
             if (lane >= fill && lane < fill + take) {
