@@ -37,7 +37,10 @@ DEV_INLINE void nt_store4(float4* p, float4 v) {
 #define CAM_SLOT4 (GR_CAM_SLOT / 4)
 static_assert(GR_CAM_SLOT == GR_CAM_GATE_SLOT, "gate slot size (gr_camera.h / gr_kernels.h)");
 #ifndef CAM_BATCH
-#define CAM_BATCH 9  // reuse path: depth quads loaded per lane before any is consumed (27 = 3 x 9 at 96x72)
+// reuse path: depth quads loaded per lane before any is consumed (27 = 14 + 13 at 96x72).  14 against 9: obstacle
+// reuse 1.271 -> 1.253 ms, gate-only 1.129 -> 1.114 ms, two alternations on one box (gpurun_out/r6m); the obstacle
+// kernel's VGPRs unchanged (98, its render path), the gate-only kernel's 69 -> 94 (7 -> 5 waves per SIMD)
+#define CAM_BATCH 14
 #endif
 
 // both observation rows of one pixel quad: fresh noise (quad index q), normalisation, streaming stores
