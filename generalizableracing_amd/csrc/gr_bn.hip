@@ -1228,6 +1228,7 @@ __global__ __launch_bounds__(SMF_THREADS) void stem12f_kernel(Stem1 s, Sm12fArgs
 }
 
 hipError_t stem12g_launch(const Stem1& s, const Sm12fArgs& f, int act, hipStream_t st);  // (below, with stem12w)
+int stem_stats_launch(const Stem1& s, double* part, float* shift, hipStream_t st);       // (below): blocks written
 
 hipError_t launch_stem12_forward(const Stem1& s, const float* bw, const float* bb, float eps, int act, float slope,
                                  const float* w2f, int n2, float* y, float* z2, float* stats, double* part,
@@ -1236,9 +1237,8 @@ hipError_t launch_stem12_forward(const Stem1& s, const float* bw, const float* b
   float* shift = reinterpret_cast<float*>(part + (size_t)nb * 2 * s.c);
   const long long m = (long long)s.nimg * (s.na + s.nbt);
   const int grid = nb < SM_GRID ? nb : SM_GRID;
-  SmArgs q{bw, bb, stats, nullptr, nullptr, y, part, shift, slope};
-  sm_launch<SM_STATS>(s, q, act, grid, st);
-  hipLaunchKernelGGL(bn_stats_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, shift, m, s.c, grid, eps, part, stats);
+  const int sgrid = stem_stats_launch(s, part, shift, st);
+  hipLaunchKernelGGL(bn_stats_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, shift, m, s.c, sgrid, eps, part, stats);
   long long room = s.ld - s.off;
   const int cap = (int)(room < 1 ? 1 : room < SM_IMG_CAP ? room : SM_IMG_CAP);
   const size_t lds = sm_lds_bytes(s.na + s.nbt, cap);
@@ -1268,8 +1268,8 @@ hipError_t launch_stem1_forward(const Stem1& s, const float* bw, const float* bb
   if (s.c == 16) {  // the reference's stem: the MFMA kernels, whole images per workgroup
     const int grid = nb < SM_GRID ? nb : SM_GRID;
     SmArgs q{bw, bb, stats, nullptr, nullptr, y, part, shift, slope};
-    sm_launch<SM_STATS>(s, q, act, grid, st);
-    hipLaunchKernelGGL(bn_stats_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, shift, m, s.c, grid, eps, part, stats);
+    const int sgrid = stem_stats_launch(s, part, shift, st);
+    hipLaunchKernelGGL(bn_stats_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, shift, m, s.c, sgrid, eps, part, stats);
     sm_launch<SM_APPLY>(s, q, act, grid, st);
     return hipGetLastError();
   }
@@ -1943,6 +1943,179 @@ hipError_t stem12g_launch(const Stem1& s, const Sm12fArgs& f, int act, hipStream
               : sg_launch<GR_POLICY_ACT_ELU, false>(nch, grid, lds, st, s, f, cap);
   return v4 ? sg_launch<GR_POLICY_ACT_LRELU, true>(nch, grid, lds, st, s, f, cap)
             : sg_launch<GR_POLICY_ACT_LRELU, false>(nch, grid, lds, st, s, f, cap);
+}
+
+
+// ------------------------------------------------------------- the first block's statistics from pixel moments
+// The BatchNorm statistics of conv1's output need, per channel, sum (x - sh) and sum (x - sh)^2 over every cell of
+// every image (sh: the channel's value at the first cell of image 0, the shift that keeps the second moment free of
+// cancellation).  With d = p - p0 the cell's 9 pixels less those of that first cell, x - sh = W d, so both sums are
+// linear in the cell moments: sum (x - sh) = W . sum d and sum (x - sh)^2 = W^T (sum d d^T) W.  A lane therefore
+// accumulates the 9 + 45 moments of its cells (63 VALU per cell instead of conv1's 144 FMAs + 48 for the sums), and
+// each block turns its fp64 moment sums into the 2 x 16 shifted channel sums bn_stats_final reads.  No LDS staging:
+// the workgroup ranks the table's cells by their first pixel (row-major on an image grid) and wave w owns ranks
+// 64 w .. 64 w + 63 for every image of its run (9 offsets per lane in registers; a 3 x 3 grid cell is three 12-byte
+// loads), four images' pixel loads in flight per lane.  The sums are exact algebra of round 5's (SM_STATS), in
+// another order: fp32 per lane, fp64 across lanes, waves and blocks in a fixed order.  24 576 images: 195 us with
+// round 5's LDS-staged pass, 176 us here (3.9 TB/s; the bound left is not the access order: strided and contiguous
+// image runs measure the same)
+// 256 workgroups, four images in flight per lane: measured against two / eight images and 512 / 1 024 workgroups
+// (199 / 237 / 205 / 244 vs 195 us before the row-major order, gpurun_out/r6o)
+constexpr int ST_GRID = 256;
+constexpr int ST_U = 4;  // images in flight per lane
+constexpr int ST_NM = 9 + 45;  // moments per lane: sum d_k, sum d_k d_l (l >= k)
+
+__global__ __launch_bounds__(1024) void stem_stats_kernel(Stem1 s, double* __restrict__ part, float* __restrict__ shift) {
+  __shared__ double red[16][ST_NM];
+  __shared__ double tot[ST_NM];
+  __shared__ int key[STEM_MAX_CELLS];
+  __shared__ short order[STEM_MAX_CELLS];
+  const int ncell = s.na + s.nbt, lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  // the cells in the order of their first pixel (the sums do not depend on the order; on an image grid it is
+  // row-major, so a wave's loads of one tap row touch a few consecutive lines instead of a scattered patch group):
+  // rank by counting (keys are distinct offsets, ties broken by cell index)
+  for (int c = threadIdx.x; c < ncell; c += blockDim.x) key[c] = s.pix[(size_t)c * 9];
+  __syncthreads();
+  for (int c = threadIdx.x; c < ncell; c += blockDim.x) {
+    const int kc = key[c];
+    int r = 0;
+    for (int e = 0; e < ncell; ++e) {
+      const int ke = key[e];
+      r += (ke < kc || (ke == kc && e < c)) ? 1 : 0;
+    }
+    order[r] = (short)c;
+  }
+  __syncthreads();
+  const int slot = 64 * w + lane;
+  const bool on = slot < ncell;
+  const int cell = on ? order[slot] : 0;
+  int off[9];
+  float p0[9];
+  {
+    const short* t = s.pix + (size_t)cell * 9;
+    const float* i0 = stem_img(s, 0);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      off[k] = t[k];
+      p0[k] = i0[s.pix[k]];  // the first cell of image 0 (the table's cell 0)
+    }
+  }
+  // a 3 x 3 pixel cell of an image row stride W: three 12-byte loads instead of nine (wave-uniform test)
+  const int rs = off[3] - off[0];
+  bool grid3 = true;
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) grid3 = grid3 && off[3 * r + c] == off[0] + r * rs + c;
+  grid3 = __all(grid3 || !on) != 0;
+  if (blockIdx.x == 0 && threadIdx.x < s.c) {  // sh = conv1 at that cell, stem_conv's k-ordered fmaf chain
+    float a = s.w[threadIdx.x * 9] * p0[0];
+#pragma unroll
+    for (int k = 1; k < 9; ++k) a = __builtin_fmaf(s.w[threadIdx.x * 9 + k], p0[k], a);
+    shift[threadIdx.x] = a;
+  }
+  float sd[9], mm[45];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) sd[k] = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 45; ++k) mm[k] = 0.0f;
+  // a contiguous run of images per workgroup (measured the same as images strided over the workgroups, r6q)
+  const int per = (s.nimg + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int bbeg = blockIdx.x * per, bend = bbeg + per < s.nimg ? bbeg + per : s.nimg, bstep = 1;
+  for (int b0 = bbeg; b0 < bend; b0 += ST_U * bstep) {
+    float px[ST_U][9];
+#pragma unroll
+    for (int u = 0; u < ST_U; ++u) {
+      const int b = b0 + u * bstep;
+      const bool ok = on && b < bend;
+      const float* img = stem_img(s, ok ? b : 0);
+      if (grid3) {
+        typedef float f3 __attribute__((ext_vector_type(3)));
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          f3 v;
+          __builtin_memcpy(&v, img + off[3 * r], 12);
+          px[u][3 * r] = v.x;
+          px[u][3 * r + 1] = v.y;
+          px[u][3 * r + 2] = v.z;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) px[u][k] = img[off[k]];
+      }
+      if (!ok) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) px[u][k] = p0[k];  // (d = 0: adds nothing)
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < ST_U; ++u) {
+      float d[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        d[k] = px[u][k] - p0[k];
+        sd[k] += d[k];
+      }
+      int q = 0;
+#pragma unroll
+      for (int k = 0; k < 9; ++k)
+#pragma unroll
+        for (int l = k; l < 9; ++l, ++q) mm[q] = __builtin_fmaf(d[k], d[l], mm[q]);
+    }
+  }
+  // fixed-order reductions: the wave's lanes by xor butterflies in fp64, then the waves in order
+  auto wave_sum = [&](float v) {
+    double x = (double)v;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+  };
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const double v = wave_sum(sd[k]);
+    if (lane == 0) red[w][k] = v;
+  }
+#pragma unroll
+  for (int k = 0; k < 45; ++k) {
+    const double v = wave_sum(mm[k]);
+    if (lane == 0) red[w][9 + k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < ST_NM) {
+    double t = 0.0;
+    for (int ww = 0; ww < nw; ++ww) t += red[ww][threadIdx.x];
+    tot[threadIdx.x] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * s.c) {  // part[block][0][ch] = W . S, [1][ch] = W^T M W (fp64)
+    const int ch = threadIdx.x % s.c;
+    double wk[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) wk[k] = (double)s.w[ch * 9 + k];
+    double r = 0.0;
+    if (threadIdx.x < s.c) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) r += wk[k] * tot[k];
+    } else {
+      int q = 0;
+#pragma unroll
+      for (int k = 0; k < 9; ++k)
+#pragma unroll
+        for (int l = k; l < 9; ++l, ++q) r += (l == k ? 1.0 : 2.0) * wk[k] * wk[l] * tot[9 + q];
+    }
+    part[(size_t)blockIdx.x * 2 * s.c + threadIdx.x] = r;
+  }
+}
+
+int stem_stats_launch(const Stem1& s, double* part, float* shift, hipStream_t st) {
+  const int ncell = s.na + s.nbt;
+  const int nw = (ncell + 63) / 64;
+  // (no more partial rows than the callers' workspace holds before the shift: stem_blocks(s), gr_stem1_scratch_doubles)
+  const int nb = stem_blocks(s);
+  int grid = s.nimg < ST_GRID ? (s.nimg < 1 ? 1 : s.nimg) : ST_GRID;
+  grid = grid < nb ? grid : nb;
+  hipLaunchKernelGGL(stem_stats_kernel, dim3(grid), dim3(64 * nw), 0, st, s, part, shift);
+  return grid;
 }
 
 }  // namespace gr
