@@ -297,20 +297,41 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
         gm |= (uint64_t)meet << g;
       }
       s_gmask[tl] = gm;
-      if constexpr (obst) {
+    }
+    if constexpr (obst) {
+      // the obstacle slots' tile masks on all 64 lanes when the image has <= 32 tiles (27 at 96 x 72): lane (h, tile)
+      // tests slots h, h + 2, ... of its tile, then the two halves' masks are OR-ed (a lane per tile left 37 of 64
+      // lanes idle through the longest loop of the set-up)
+      const int ntiles = ntx * nty;
+      const bool split = ntiles <= 32;
+      const int kstep = split ? 2 : 1;
+      for (int t0 = split ? (lane & 31) : lane; t0 < (split ? 32 : ntiles); t0 += 64) {
+        const int tl = t0, k0 = split ? (lane >> 5) : 0;
         uint64_t tm = 0;
-        for (int k = 0; k < ns; ++k) {
-          const float4 wk = s_oslot[k * (GR_CAM_OSLOT / 4) + 4];  // pixel rectangle u_lo, u_hi, v_lo, v_hi
-          bool meet = !(__float_as_int(wk.y) < u0 || __float_as_int(wk.x) > u1 || __float_as_int(wk.w) < v0 ||
-                        __float_as_int(wk.z) > v1);
-          if (meet) {
-            float sk[GR_CAM_SLOT];
-            load_oslot(s_oslot + k * (GR_CAM_OSLOT / 4), sk);
-            meet = !gr_cam_obst_outside(sk, a_lo, a_hi, b_lo, b_hi);
+        if (tl < ntiles) {
+          const int v0 = 8 * (tl / ntx), u0 = 32 * (tl % ntx);
+          const int v1 = (v0 + 7 < H ? v0 + 7 : H - 1), u1 = (u0 + 31 < W ? u0 + 31 : W - 1);
+          const float a_hi = cc->ray_a[u0], a_lo = cc->ray_a[u1], b_hi = cc->ray_b[v0], b_lo = cc->ray_b[v1];
+          for (int k = k0; k < ns; k += kstep) {
+            const float4 wk = s_oslot[k * (GR_CAM_OSLOT / 4) + 4];  // pixel rectangle u_lo, u_hi, v_lo, v_hi
+            bool meet = !(__float_as_int(wk.y) < u0 || __float_as_int(wk.x) > u1 || __float_as_int(wk.w) < v0 ||
+                          __float_as_int(wk.z) > v1);
+            if (meet) {
+              float sk[GR_CAM_SLOT];
+              load_oslot(s_oslot + k * (GR_CAM_OSLOT / 4), sk);
+              meet = !gr_cam_obst_outside(sk, a_lo, a_hi, b_lo, b_hi);
+            }
+            tm |= (uint64_t)meet << k;
           }
-          tm |= (uint64_t)meet << k;
         }
-        s_tmask[tl] = tm;
+        if (split) {  // (every lane: the shuffles are wave-wide)
+          const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)tm, 32);
+          const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(tm >> 32), 32);
+          tm |= ((uint64_t)hi << 32) | lo;
+          if (lane < 32 && tl < ntiles) s_tmask[tl] = tm;
+        } else if (tl < ntiles) {
+          s_tmask[tl] = tm;
+        }
       }
     }
   }

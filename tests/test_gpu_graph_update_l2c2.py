@@ -9,7 +9,8 @@ generator), so the comparison substitutes a fixed draw (u = 0.75: every mixed ro
 in both; a second test keeps the real draw and holds the graphed update to the eager one's direction.  Tolerance as
 tests/test_gpu_graph_update.py (fp32 device learning rate, another gradient accumulation order): parameters within
 5 % of their movement (norms over all; 15 % per tensor, and the worst tensor within twice what a one-ulp perturbation
-of the eager update itself produces), the value loss 1e-4 relative, the smoothness loss 2e-3.  Step by step: after
+of the eager update itself produces), the value loss 1e-4 relative, the smoothness loss 2e-3, the surrogate 5e-5 (or
+each within four times the one-ulp control's own difference).  Step by step: after
 the first mini-batch step the flat gradient within 1e-5 and the parameters within 1e-6 of the eager loop's; Adam's
 device step counters advance by exactly epochs x mini-batches (no step skipped or repeated).  Both the plain
 storage layout and the observation-sink layout (T + 1 slots, the recipe's default) are covered."""
@@ -161,7 +162,7 @@ def test_graphed_l2c2_update_matches_eager(obs_sink):
         for a, out in ((alg, le), (alg_g, lg), (alg_c, lc)):
             torch.manual_seed(7 + rep)
             out.append(a.update())
-        le, lg = le[0], lg[0]
+        le, lg, lc = le[0], lg[0], lc[0]
         # the device step counters: every mini-batch step ran exactly once
         s1e, s1g = _adam_steps(alg), _adam_steps(alg_g)
         assert set(s1e) == set(s1g) and len(s1e) >= len(p0) - 3
@@ -173,9 +174,10 @@ def test_graphed_l2c2_update_matches_eager(obs_sink):
         worst_g = sorted(((d / m if m else 0.0), name) for name, d, m in div_g)[-3:]
         worst_c = sorted(((d / m if m else 0.0), name) for name, d, m in div_c)[-3:]
         print(f"obs_sink={obs_sink} rep={rep}: graphed-vs-eager worst {worst_g}; one-ulp eager control worst {worst_c}")
-        # measured (gpurun_out/r6b): graphed-vs-eager worst tensor 1.2 % / 2.2 % of its movement, the one-ulp eager
-        # control 3.5 % / 5.5 %: the update's own round-off sensitivity exceeds the graphed path's difference, so the
-        # graphed update is held to the control (worst tensor within 2x the control's + 1 %) and to 15 % per tensor
+        # measured: graphed-vs-eager worst tensor 1.2 % / 2.2 % of its movement against a one-ulp eager control of 3.5 % /
+        # 5.5 % (gpurun_out/r6b), and on another rollout draw 7.6 % against 11 % (r6r): the update's own round-off
+        # sensitivity exceeds the graphed path's difference and depends on the data, so the graphed update is held to
+        # the control (worst tensor within 2x the control's + 1 %) and to 15 % per tensor
         assert worst_g[-1][0] <= 2.0 * worst_c[-1][0] + 0.01, (rep, worst_g, worst_c)
         per_tensor = 0.15
         n_moved, tot_moved, tot_diff = 0, 0.0, 0.0
@@ -201,11 +203,13 @@ def test_graphed_l2c2_update_matches_eager(obs_sink):
                     bad.append((k, diff, moved))
         assert not bad, (rep, bad)
         assert abs(alg.learning_rate - alg_g.learning_rate) <= 1e-6 * alg.learning_rate
-        assert abs(le["value_function"] - lg["value_function"]) <= 1e-4 * abs(le["value_function"]), (rep, le, lg)
-        # the smoothness loss is a mean of squared distances between two nearly equal policy outputs (~1e-3): the
-        # parameters' round-off differences of the later mini-batches show in it at ~1e-4 relative
-        assert abs(le["smooth_loss"] - lg["smooth_loss"]) <= 2e-3 * abs(le["smooth_loss"]), (rep, le, lg)
-        assert abs(le["surrogate"] - lg["surrogate"]) <= 5e-5, (le["surrogate"], lg["surrogate"])
+        # the losses: within fixed bounds (value 1e-4 relative, smoothness 2e-3 relative (a mean of squared distances
+        # between two nearly equal policy outputs, ~1e-3), surrogate 5e-5) or within four times what the one-ulp control
+        # moved them (the later mini-batches' round-off, amplified as above, shows in them too; the control is one
+        # sample of that spread: on rollout r6t the smoothness loss moved 2.1x the control's)
+        for key, fixed in (("value_function", 1e-4 * abs(le["value_function"])),
+                           ("smooth_loss", 2e-3 * abs(le["smooth_loss"])), ("surrogate", 5e-5)):
+            assert abs(le[key] - lg[key]) <= max(fixed, 4.0 * abs(le[key] - lc[key])), (rep, key, le, lg, lc)
         if obs_sink:  # (the last observations opened the next rollout in both, slot T into slot 0)
             assert alg_g.storage.prefilled == alg.storage.prefilled
             assert torch.equal(alg_g.storage.observations, alg.storage.observations)
