@@ -189,7 +189,7 @@ def test_graphed_l2c2_update_matches_eager(obs_sink):
             tot_diff += diff * diff
         assert n_moved >= len(p0) - 3, (n_moved, len(p0))
         assert tot_diff <= 0.05 ** 2 * tot_moved, (rep, tot_diff ** 0.5, tot_moved ** 0.5)
-        be, bg = _buffers(alg.policy), _buffers(alg_g.policy)
+        be, bg, bc = _buffers(alg.policy), _buffers(alg_g.policy), _buffers(alg_c.policy)
         assert set(be) == set(bg) and len(be) >= 9
         bad = []
         for k in be:
@@ -197,9 +197,12 @@ def test_graphed_l2c2_update_matches_eager(obs_sink):
                 if not torch.equal(be[k], bg[k]):
                     bad.append((k, int(be[k]), int(bg[k])))
             else:
-                # as the parameters: within 5 % of how far the update moved them
+                # as the parameters: within 5 % of how far the update moved them, or within twice the one-ulp
+                # control's difference (+1 %): the statistics are taken with the chaotic parameters (r6v:
+                # stem.4.running_var at 7 % of its movement)
                 moved, diff = float((be[k] - b0[k]).norm()), float((bg[k] - be[k]).norm())
-                if not (moved > 0.0 and diff <= 0.05 * moved):
+                ctrl = float((bc[k] - be[k]).norm())
+                if not (moved > 0.0 and diff <= max(0.05 * moved, 2.0 * ctrl + 0.01 * moved)):
                     bad.append((k, diff, moved))
         assert not bad, (rep, bad)
         assert abs(alg.learning_rate - alg_g.learning_rate) <= 1e-6 * alg.learning_rate
