@@ -92,8 +92,8 @@ DEV_INLINE void reuse_rows(const CamArgs& a, const gr_cam_const* __restrict__ cc
   }
 }
 
-// obstacle slot from LDS (GR_CAM_OSLOT floats: frame and primitive = slot floats 0-15, what the hit and frustum tests
-// read; then the window's pixel rectangle u_lo, u_hi, v_lo, v_hi as ints, read by the tile masks and hit passes)
+// obstacle slot from LDS (GR_CAM_OSLOT floats: frame, primitive and kind = slot floats 0-15, what the hit and frustum
+// tests read; the window's pixel rectangle, read by the tile masks and hit passes, is a packed word beside the slots)
 DEV_INLINE void load_oslot(const float4* src, float s[GR_CAM_SLOT]) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -140,8 +140,9 @@ DEV_INLINE void quad_obst(const float* s, const float av[4], float b, float d[4]
   }
 }
 
-// Dynamic LDS: ray tables a_u[W], b_v[H] (padded to 4), then per wave: gate slots [max_gates][24], obstacle
-// slots [GR_CAM_OBST_SLOTS][24] (obstacle tracks only) and an 8-row depth staging band [8][W].
+// Dynamic LDS: the normal table (workgroup), ray tables a_u[W], b_v[H] (padded to 4), then per wave: gate slots
+// [max_gates][36] and their tile masks, on obstacle tracks obstacle slots [GR_CAM_OBST_SLOTS][16], their pixel
+// rectangles and tile masks, and an 8-row depth staging band [8][W] (camera_lds_bytes, gr_kernels.h).
 #ifdef CAM_WAVES_PER_EU
 #define CAM_ATTR __attribute__((amdgpu_waves_per_eu(CAM_WAVES_PER_EU, CAM_WAVES_PER_EU)))
 #else
@@ -155,21 +156,20 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
   const gr_cam_const* __restrict__ cc = a.cc;
   const int W = a.width, H = a.height, npix = W * H, G = a.max_gates;
   const int wpad = (W + 3) & ~3, hpad = (H + 3) & ~3;
-  // the normal table: in LDS on gate-only tracks; on obstacle tracks the LDS is full at 4 workgroups per CU (the
-  // obstacle slots), so a rendering wave reads the table from the constant segment (5 KB, cache-resident) and a
-  // reusing wave copies it into its own slot area
-  const float* s_ntab = cam_normal_tab;
-  if constexpr (!OBST) {
+  // the normal table in LDS, shared by the workgroup's waves (read from the constant segment instead, a gate-only
+  // re-render measured 1.20 -> 1.41 ms: a per-pixel gather through the vector cache, gpurun_out/r6x)
+  {
     float4* s_ntab4 = smem4;
     for (int k = threadIdx.x; k < GR_NORMAL_TABLE_ENTRIES; k += CAM_WAVES * 64)
       s_ntab4[k] = reinterpret_cast<const float4*>(cam_normal_tab)[k];
-    s_ntab = smem;
-    smem += CAM_NORMAL_FLOATS;
   }
+  const float* s_ntab = smem;
+  smem += CAM_NORMAL_FLOATS;
   float* s_ray_a = smem;
   float* s_ray_b = smem + wpad;
   for (int k = threadIdx.x; k < W; k += CAM_WAVES * 64) s_ray_a[k] = cc->ray_a[k];
   for (int k = threadIdx.x; k < H; k += CAM_WAVES * 64) s_ray_b[k] = cc->ray_b[k];
+  __syncthreads();  // (the ray tables: read by the obstacle windows' searches and the tile masks below)
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -184,8 +184,10 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
   float4* s_slot = reinterpret_cast<float4*>(wave_lds);                               // [G][CAM_SLOT4]
   uint64_t* s_gmask = reinterpret_cast<uint64_t*>(wave_lds + G * GR_CAM_SLOT);        // [tiles]
   float* olds = wave_lds + G * GR_CAM_SLOT + tmf;
-  float4* s_oslot = reinterpret_cast<float4*>(olds);                                  // [64][GR_CAM_OSLOT / 4]
-  uint64_t* s_tmask = reinterpret_cast<uint64_t*>(olds + GR_CAM_OBST_SLOTS * GR_CAM_OSLOT);  // [tiles]
+  float4* s_oslot = reinterpret_cast<float4*>(olds);                                  // [slots][GR_CAM_OSLOT / 4]
+  // per slot: its window's pixel rectangle u_lo | u_hi << 8 | v_lo << 16 | v_hi << 24 (W, H <= 256)
+  uint32_t* s_orect = reinterpret_cast<uint32_t*>(olds + GR_CAM_OBST_SLOTS * GR_CAM_OSLOT);
+  uint64_t* s_tmask = reinterpret_cast<uint64_t*>(olds + GR_CAM_OBST_SLOTS * (GR_CAM_OSLOT + 1));  // [tiles]
   float4* s_stage = reinterpret_cast<float4*>(olds + oslots);                         // [8 * W / 4]
 
   // ---- is the sensor outdated? (SensorBase.update / reset; wave-uniform)
@@ -252,8 +254,8 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
           if (ok) {
             // the window as the pixel rectangle it admits (a_u, b_v monotonic): the tile masks and the hit passes
             // read it instead of testing rays; a window between pixel rays can be hit by none (dropped)
-            window_pixels(cc->ray_a, W, s[GR_CS_AMIN], s[GR_CS_AMAX], u_lo, u_hi);
-            window_pixels(cc->ray_b, H, s[GR_CS_BMIN], s[GR_CS_BMAX], v_lo, v_hi);
+            window_pixels(s_ray_a, W, s[GR_CS_AMIN], s[GR_CS_AMAX], u_lo, u_hi);
+            window_pixels(s_ray_b, H, s[GR_CS_BMIN], s[GR_CS_BMAX], v_lo, v_hi);
             ok = u_lo <= u_hi && v_lo <= v_hi;
           }
         }
@@ -263,8 +265,7 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
 #pragma unroll
           for (int q = 0; q < 4; ++q)
             s_oslot[pos * (GR_CAM_OSLOT / 4) + q] = make_float4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
-          s_oslot[pos * (GR_CAM_OSLOT / 4) + 4] = make_float4(__int_as_float(u_lo), __int_as_float(u_hi),
-                                                              __int_as_float(v_lo), __int_as_float(v_hi));
+          s_orect[pos] = (uint32_t)u_lo | (uint32_t)u_hi << 8 | (uint32_t)v_lo << 16 | (uint32_t)v_hi << 24;
         }
         const int nb = __popcll(b);
         if (nv + nb > GR_CAM_OBST_SLOTS && ofrom == nob) {
@@ -282,7 +283,7 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
     for (int tl = lane; tl < ntx * nty; tl += 64) {
       const int v0 = 8 * (tl / ntx), u0 = 32 * (tl % ntx);
       const int v1 = (v0 + 7 < H ? v0 + 7 : H - 1), u1 = (u0 + 31 < W ? u0 + 31 : W - 1);
-      const float a_hi = cc->ray_a[u0], a_lo = cc->ray_a[u1], b_hi = cc->ray_b[v0], b_lo = cc->ray_b[v1];
+      const float a_hi = s_ray_a[u0], a_lo = s_ray_a[u1], b_hi = s_ray_b[v0], b_lo = s_ray_b[v1];
       uint64_t gm = 0;
       for (uint64_t m = valid_mask; m; m &= m - 1) {
         const int g = __builtin_ctzll(m);
@@ -311,11 +312,11 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
         if (tl < ntiles) {
           const int v0 = 8 * (tl / ntx), u0 = 32 * (tl % ntx);
           const int v1 = (v0 + 7 < H ? v0 + 7 : H - 1), u1 = (u0 + 31 < W ? u0 + 31 : W - 1);
-          const float a_hi = cc->ray_a[u0], a_lo = cc->ray_a[u1], b_hi = cc->ray_b[v0], b_lo = cc->ray_b[v1];
+          const float a_hi = s_ray_a[u0], a_lo = s_ray_a[u1], b_hi = s_ray_b[v0], b_lo = s_ray_b[v1];
           for (int k = k0; k < ns; k += kstep) {
-            const float4 wk = s_oslot[k * (GR_CAM_OSLOT / 4) + 4];  // pixel rectangle u_lo, u_hi, v_lo, v_hi
-            bool meet = !(__float_as_int(wk.y) < u0 || __float_as_int(wk.x) > u1 || __float_as_int(wk.w) < v0 ||
-                          __float_as_int(wk.z) > v1);
+            const uint32_t wk = s_orect[k];  // pixel rectangle u_lo, u_hi, v_lo, v_hi
+            bool meet = !((int)(wk >> 8 & 0xffu) < u0 || (int)(wk & 0xffu) > u1 || (int)(wk >> 24) < v0 ||
+                          (int)(wk >> 16 & 0xffu) > v1);
             if (meet) {
               float sk[GR_CAM_SLOT];
               load_oslot(s_oslot + k * (GR_CAM_OSLOT / 4), sk);
@@ -349,16 +350,6 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
 
   if (!render) {
     const float* ntab = s_ntab;
-    if constexpr (OBST) {
-      // a reusing wave has no obstacle slots to hold: its slot area takes a copy of the normal table
-      static_assert(CAM_NORMAL_FLOATS <= GR_CAM_OBST_SLOTS * GR_CAM_OSLOT, "normal table vs obstacle slot area");
-      float4* t4 = reinterpret_cast<float4*>(olds);
-#pragma unroll
-      for (int k = 0; k < GR_NORMAL_TABLE_ENTRIES / 64; ++k)
-        t4[64 * k + lane] = reinterpret_cast<const float4*>(cam_normal_tab)[64 * k + lane];
-      wave_lds_sync();
-      ntab = olds;
-    }
     reuse_rows(a, cc, ntab, dep4, op4, oc4, nq, lane, gid, cnt);
     return;
   }
@@ -435,9 +426,9 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
           const int k = __builtin_ctzll(mo);
           mo &= mo - 1;
           // the slot's pixel rectangle within this tile of the band (wave-uniform integer ranges)
-          const float4 wk = s_oslot[k * (GR_CAM_OSLOT / 4) + 4];
-          const int ulo = __float_as_int(wk.x), uhi = __float_as_int(wk.y), vlo = __float_as_int(wk.z),
-                    vhi = __float_as_int(wk.w);
+          const uint32_t wk = s_orect[k];
+          const int ulo = (int)(wk & 0xffu), uhi = (int)(wk >> 8 & 0xffu), vlo = (int)(wk >> 16 & 0xffu),
+                    vhi = (int)(wk >> 24);
           const int cu = ulo > u_t ? ulo : u_t, cu1 = uhi < u_t + 31 ? uhi : u_t + 31;
           const int rv = (vlo > v0 ? vlo : v0) - v0, rv1 = (vhi < v0 + 7 ? vhi : v0 + 7) - v0;
           if (cu > cu1 || rv > rv1) continue;

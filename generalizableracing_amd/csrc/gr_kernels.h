@@ -211,23 +211,25 @@ hipError_t launch_in_backward(const float* gh, const float* hv, const float* x, 
 // obstacle slots per camera wave (the first GR_CAM_OBST_SLOTS obstacles in view; any further ones
 // are set up again per tile from their records)
 #define GR_CAM_GATE_SLOT 36   // floats per gate slot in LDS (GR_CAM_SLOT of gr_camera.h)
-#define GR_CAM_OBST_SLOTS 64
-#define GR_CAM_OSLOT 20  // floats per obstacle slot in LDS: gate-slot floats 0-15, then the window (17-20)
+#define GR_CAM_OBST_SLOTS 56
+#define GR_CAM_OSLOT 16  // floats per obstacle slot in LDS: slot floats 0-15 (frame, primitive, kind)
 // dynamic LDS of the camera kernel: ray tables + per wave (gate slots, one 64-bit gate mask per 8x32 tile
 // [+ obstacle slots and their tile masks] + an 8-row staging band); every part a multiple of 4 floats
 __host__ __device__ inline size_t camera_tile_mask_floats(int width, int height) {
   return (2 * (size_t)((height + 7) / 8) * ((width + 31) / 32) + 3) & ~(size_t)3;
 }
-// obstacle slots + one 64-bit mask per 8x32 tile (the slots that can cover a pixel of the tile)
+// obstacle slots + their windows' pixel rectangles (one packed word per slot) + one 64-bit mask per 8x32 tile (the
+// slots that can cover a pixel of the tile)
+static_assert(GR_CAM_OBST_SLOTS <= 64 && GR_CAM_OBST_SLOTS % 4 == 0, "obstacle slots: 64-bit tile masks, float4 parts");
 __host__ __device__ inline size_t camera_obst_floats(int width, int height) {
-  return (size_t)GR_CAM_OBST_SLOTS * GR_CAM_OSLOT + camera_tile_mask_floats(width, height);
+  return (size_t)GR_CAM_OBST_SLOTS * (GR_CAM_OSLOT + 1) + camera_tile_mask_floats(width, height);
 }
-// (the normal table of the image noise, gr_normal_table.h: 4 floats per entry, first in LDS on gate-only tracks)
+// (the normal table of the image noise, gr_normal_table.h: 4 floats per entry, first in LDS)
 #define CAM_NORMAL_FLOATS (4 * 320)
 inline size_t camera_lds_bytes(int width, int height, int max_gates, bool obst) {
   const size_t wpad = (size_t)((width + 3) & ~3), hpad = (size_t)((height + 3) & ~3);
   const size_t os = obst ? camera_obst_floats(width, height) : 0;
-  return 4 * ((obst ? 0 : CAM_NORMAL_FLOATS) + wpad + hpad +
+  return 4 * (CAM_NORMAL_FLOATS + wpad + hpad +
               4 * ((size_t)max_gates * GR_CAM_GATE_SLOT + camera_tile_mask_floats(width, height) + os + 8 * (size_t)width));
 }
 

@@ -101,6 +101,8 @@ def main():
     s = np.array(stats, np.float64)
     print(f"{n} envs at their post-reset pose, obstacle tracks")
     print(f"  obstacles in view per env: mean {s[:, 0].mean():.1f}, max {s[:, 0].max():.0f}")
+    print(f"  in view: p90 {np.percentile(s[:, 0], 90):.0f}, p99 {np.percentile(s[:, 0], 99):.0f}; envs over 48 / 56 / 64: "
+          f"{(s[:, 0] > 48).mean():.4f} / {(s[:, 0] > 56).mean():.4f} / {(s[:, 0] > 64).mean():.4f}")
     print(f"  (tile, slot) pairs per env: mean {s[:, 1].mean():.1f} (27 tiles)")
     print(f"  window pixels of those pairs per env: mean {s[:, 2].mean():.0f} (image 6912); "
           f"per pair {s[:, 2].sum() / max(s[:, 1].sum(), 1):.0f} of 256; whole-tile pairs {s[:, 3].sum() / max(s[:, 1].sum(), 1):.2f}")
