@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgr.so")
 
 # ---- constants (include/gr.h) ----
-GR_ABI_VERSION = 5
+GR_ABI_VERSION = 6
 GR_INTEGRATOR_DD_EXPLICIT = 0
 GR_INTEGRATOR_SEMI_IMPLICIT = 1
 
@@ -226,7 +226,7 @@ STATUS_TEXT = {GR_STATUS_OBST_WAIT_TIMEOUT: "a physics wave gave up waiting for 
 EXPORTS = [
     "gr_abi_version", "gr_config_default", "gr_config_size", "gr_create", "gr_destroy", "gr_last_error",
     "gr_num_blocks", "gr_num_log_rows", "gr_log_finalize", "gr_bytes_per_env_step", "gr_bind_tracks", "gr_bind_obstacles", "gr_swap_terrain", "gr_bind_buffers", "gr_bind_obs_sink", "gr_init", "gr_reset",
-    "gr_step", "gr_observe", "gr_device_status", "gr_test_inject_fault", "gr_set_timing", "gr_read_timing", "gr_test_dynamics", "gr_test_math",
+    "gr_step", "gr_observe", "gr_device_status", "gr_test_inject_fault", "gr_test_camera_slots", "gr_set_timing", "gr_read_timing", "gr_test_dynamics", "gr_test_math",
     "gr_test_philox",
     "gr_debug_read_stamps", "gr_debug_read_policy_stamps",
     "gr_camera_config_default", "gr_camera_config_size", "gr_enable_camera", "gr_bind_camera_buffers",
@@ -277,6 +277,7 @@ def _declare(lib):
         "gr_step_kernel_variant": (C.c_int, [vp]),
         "gr_device_status": (C.c_int, [vp, C.POINTER(C.c_uint32), C.c_int, vp]),
         "gr_test_inject_fault": (C.c_int, [vp, C.c_int]),
+        "gr_test_camera_slots": (C.c_int, [vp, C.c_int32]),
         "gr_set_timing": (C.c_int, [vp, C.c_int]),
         "gr_read_timing": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
         "gr_test_dynamics": (C.c_int, [vp, C.c_int, C.c_int] + [vp] * 9 + [vp]),

@@ -33,7 +33,6 @@ DEV_INLINE void nt_store4(float4* p, float4 v) {
   __builtin_nontemporal_store(x, reinterpret_cast<gr_v4f*>(p));
 }
 
-#define CAM_WAVES 4
 #define CAM_SLOT4 (GR_CAM_SLOT / 4)
 static_assert(GR_CAM_SLOT == GR_CAM_GATE_SLOT, "gate slot size (gr_camera.h / gr_kernels.h)");
 #ifndef CAM_BATCH
@@ -141,8 +140,8 @@ DEV_INLINE void quad_obst(const float* s, const float av[4], float b, float d[4]
 }
 
 // Dynamic LDS: the normal table (workgroup), ray tables a_u[W], b_v[H] (padded to 4), then per wave: gate slots
-// [max_gates][36] and their tile masks, on obstacle tracks obstacle slots [GR_CAM_OBST_SLOTS][16], their pixel
-// rectangles and tile masks, and an 8-row depth staging band [8][W] (camera_lds_bytes, gr_kernels.h).
+// [max_gates][36] and their tile masks, on obstacle tracks a.obst_slots obstacle slots of 16 floats, their pixel
+// rectangles and tile masks, and an 8-row depth staging band [8][W] (camera_launch_config, gr_kernels.h).
 #ifdef CAM_WAVES_PER_EU
 #define CAM_ATTR __attribute__((amdgpu_waves_per_eu(CAM_WAVES_PER_EU, CAM_WAVES_PER_EU)))
 #else
@@ -156,38 +155,40 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
   const gr_cam_const* __restrict__ cc = a.cc;
   const int W = a.width, H = a.height, npix = W * H, G = a.max_gates;
   const int wpad = (W + 3) & ~3, hpad = (H + 3) & ~3;
+  constexpr int nw = CAM_WAVES;
+  const int S = OBST ? a.obst_slots : 0;  // obstacle slots per wave
   // the normal table in LDS, shared by the workgroup's waves (read from the constant segment instead, a gate-only
   // re-render measured 1.20 -> 1.41 ms: a per-pixel gather through the vector cache, gpurun_out/r6x)
   {
     float4* s_ntab4 = smem4;
-    for (int k = threadIdx.x; k < GR_NORMAL_TABLE_ENTRIES; k += CAM_WAVES * 64)
+    for (int k = threadIdx.x; k < GR_NORMAL_TABLE_ENTRIES; k += nw * 64)
       s_ntab4[k] = reinterpret_cast<const float4*>(cam_normal_tab)[k];
   }
   const float* s_ntab = smem;
   smem += CAM_NORMAL_FLOATS;
   float* s_ray_a = smem;
   float* s_ray_b = smem + wpad;
-  for (int k = threadIdx.x; k < W; k += CAM_WAVES * 64) s_ray_a[k] = cc->ray_a[k];
-  for (int k = threadIdx.x; k < H; k += CAM_WAVES * 64) s_ray_b[k] = cc->ray_b[k];
-  __syncthreads();  // (the ray tables: read by the obstacle windows' searches and the tile masks below)
+  for (int k = threadIdx.x; k < W; k += nw * 64) s_ray_a[k] = cc->ray_a[k];
+  for (int k = threadIdx.x; k < H; k += nw * 64) s_ray_b[k] = cc->ray_b[k];
+  __syncthreads();  // (the only workgroup barrier: everything after it is per wave)
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int i = blockIdx.x * CAM_WAVES + w;
+  const int i = blockIdx.x * nw + w;
   const bool active = i < a.num_envs;
   const int N = a.num_envs;
   constexpr bool obst = OBST;
   const int ntx = (W + 31) / 32, nty = (H + 7) / 8;
-  const int oslots = obst ? (int)camera_obst_floats(W, H) : 0;
+  const int oslots = (int)camera_obst_floats(W, H, S);
   const int tmf = (int)camera_tile_mask_floats(W, H);
-  float* wave_lds = smem + wpad + hpad + w * (G * GR_CAM_SLOT + tmf + oslots + 8 * W);
+  float* wave_lds = smem + wpad + hpad + w * (int)camera_wave_floats(W, H, G, S);
   float4* s_slot = reinterpret_cast<float4*>(wave_lds);                               // [G][CAM_SLOT4]
   uint64_t* s_gmask = reinterpret_cast<uint64_t*>(wave_lds + G * GR_CAM_SLOT);        // [tiles]
   float* olds = wave_lds + G * GR_CAM_SLOT + tmf;
   float4* s_oslot = reinterpret_cast<float4*>(olds);                                  // [slots][GR_CAM_OSLOT / 4]
   // per slot: its window's pixel rectangle u_lo | u_hi << 8 | v_lo << 16 | v_hi << 24 (W, H <= 256)
-  uint32_t* s_orect = reinterpret_cast<uint32_t*>(olds + GR_CAM_OBST_SLOTS * GR_CAM_OSLOT);
-  uint64_t* s_tmask = reinterpret_cast<uint64_t*>(olds + GR_CAM_OBST_SLOTS * (GR_CAM_OSLOT + 1));  // [tiles]
+  uint32_t* s_orect = reinterpret_cast<uint32_t*>(olds + S * GR_CAM_OSLOT);
+  uint64_t* s_tmask = reinterpret_cast<uint64_t*>(olds + S * GR_CAM_OSLOT + ((S + 3) & ~3));  // [tiles]
   float4* s_stage = reinterpret_cast<float4*>(olds + oslots);                         // [8 * W / 4]
 
   // ---- is the sensor outdated? (SensorBase.update / reset; wave-uniform)
@@ -237,7 +238,7 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
     }
     valid_mask = __ballot(valid);
     if constexpr (obst) {
-      // obstacles in view: the first GR_CAM_OBST_SLOTS go to LDS slots (compacted by ballot); from the
+      // obstacles in view: the first S go to LDS slots (compacted by ballot); from the
       // next one on (rare) they are set up again per tile
       nob = a.obst_counts[track];
       orecs = a.obst + (size_t)track * a.max_obst * GR_OBST_FLOATS;
@@ -261,21 +262,21 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
         }
         const uint64_t b = __ballot(ok);
         const int pos = nv + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-        if (ok && pos < GR_CAM_OBST_SLOTS) {
+        if (ok && pos < S) {
 #pragma unroll
           for (int q = 0; q < 4; ++q)
             s_oslot[pos * (GR_CAM_OSLOT / 4) + q] = make_float4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
           s_orect[pos] = (uint32_t)u_lo | (uint32_t)u_hi << 8 | (uint32_t)v_lo << 16 | (uint32_t)v_hi << 24;
         }
         const int nb = __popcll(b);
-        if (nv + nb > GR_CAM_OBST_SLOTS && ofrom == nob) {
-          // raw index of valid obstacle number GR_CAM_OBST_SLOTS (wave-uniform)
-          const uint64_t over = __ballot(ok && pos == GR_CAM_OBST_SLOTS);
+        if (nv + nb > S && ofrom == nob) {
+          // raw index of valid obstacle number S (wave-uniform)
+          const uint64_t over = __ballot(ok && pos == S);
           ofrom = base + __builtin_ctzll(over);
         }
         nv += nb;
       }
-      ns = nv < GR_CAM_OBST_SLOTS ? nv : GR_CAM_OBST_SLOTS;
+      ns = nv < S ? nv : S;
     }
     // per 8x32 tile: the gates and obstacle slots whose window meets the tile's ray range (a_u, b_v decrease
     // with u, v) and whose bounding box reaches into the tile's frustum (gr_cam_gate_outside / _obst_outside)
@@ -336,7 +337,7 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
       }
     }
   }
-  __syncthreads();
+  wave_lds_sync();  // (this wave's slots and masks)
   if (!active) return;
 
   const uint32_t gid = (uint32_t)(a.env_id_offset + i);
@@ -467,15 +468,26 @@ __global__ __launch_bounds__(CAM_WAVES * 64) CAM_ATTR void camera_kernel(CamArgs
   }
 }
 
-hipError_t launch_camera(const CamArgs& a, hipStream_t s) {
-  const int blocks = (a.num_envs + CAM_WAVES - 1) / CAM_WAVES;
-  if (a.obst != nullptr)
-    hipLaunchKernelGGL(camera_kernel<true>, dim3(blocks), dim3(CAM_WAVES * 64),
-                       camera_lds_bytes(a.width, a.height, a.max_gates, true), s, a);
-  else
-    hipLaunchKernelGGL(camera_kernel<false>, dim3(blocks), dim3(CAM_WAVES * 64),
-                       camera_lds_bytes(a.width, a.height, a.max_gates, false), s, a);
+template <bool OBST>
+static hipError_t camera_launch_t(const CamArgs& b, const CamLaunch& L, hipStream_t s) {
+  if (L.lds > (size_t)CAM_LDS_PER_CU) return hipErrorInvalidValue;
+  static bool attr = false;  // (dynamic LDS above 64 KB: many gates)
+  if (L.lds > 65536 && !attr) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&camera_kernel<OBST>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, CAM_LDS_PER_CU);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(camera_kernel<OBST>, dim3((b.num_envs + L.waves - 1) / L.waves), dim3(L.waves * 64), L.lds, s, b);
   return hipGetLastError();
+}
+
+hipError_t launch_camera(const CamArgs& a, hipStream_t s) {
+  const bool obst = a.obst != nullptr;
+  const CamLaunch L = camera_launch_config(a.width, a.height, a.max_gates, obst, obst ? a.obst_slots : 0);
+  CamArgs b = a;
+  b.obst_slots = L.slots;
+  return obst ? camera_launch_t<true>(b, L, s) : camera_launch_t<false>(b, L, s);
 }
 
 }  // namespace gr

@@ -35,6 +35,7 @@ struct gr_ctx {
   std::string err;
   // optional depth camera
   bool cam_enabled = false;
+  int cam_test_slots = 0;  // gr_test_camera_slots (0: the launch's own choice)
   gr_cam_const cam_k;
   gr_cam_const* cam_dev = nullptr;
   gr_camera_buffers cam_buf;
@@ -748,6 +749,13 @@ int gr_test_inject_fault(gr_ctx* c, int fault) {
   return GR_OK;
 }
 
+int gr_test_camera_slots(gr_ctx* c, int32_t slots) {
+  if (!c) return GR_ERR_ARG;
+  if (slots < 0 || slots > GR_CAM_OBST_SLOTS_MAX) return fail(c, GR_ERR_ARG, "gr_test_camera_slots: slots in [0, 64]");
+  c->cam_test_slots = slots;
+  return GR_OK;
+}
+
 int gr_set_timing(gr_ctx* c, int enable) {
   if (!c) return GR_ERR_ARG;
   if (enable && c->ev.empty()) {
@@ -883,6 +891,7 @@ int gr_camera_render(gr_ctx* c, int mode, const uint8_t* mask, void* stream) {
   a.age = c->cam_buf.age;
   a.out_p = c->cam_buf.obs_policy;
   a.out_c = c->cam_buf.obs_critic;
+  a.obst_slots = c->cam_test_slots;
   hipError_t e = gr::launch_camera(a, (hipStream_t)stream);
   return e == hipSuccess ? GR_OK : hip_fail(c, e, "gr_camera_render");
 }

@@ -88,6 +88,7 @@ struct CamArgs {
   const int32_t* obst_counts;  // [T*L]
   int max_obst;
   int track_stride, num_levels, max_gates, num_envs, env_id_offset, mode, width, height;
+  int obst_slots;  // obstacle slots per wave in LDS (launch_camera sets it; > 0 on entry: a test's request)
   uint32_t seed_lo, seed_hi;
   float* depth;
   int32_t* age;
@@ -208,29 +209,45 @@ hipError_t launch_mlp_backward(const gr_mlp_args& a, hipStream_t s);
 int64_t mlp_partial_floats(long long rows, int hidden, int nets, int max_d, int max_k);
 hipError_t launch_in_backward(const float* gh, const float* hv, const float* x, long long m, int d, int ldx, int h,
                               float slope, float* part, float* sums, hipStream_t s);
-// obstacle slots per camera wave (the first GR_CAM_OBST_SLOTS obstacles in view; any further ones
-// are set up again per tile from their records)
-#define GR_CAM_GATE_SLOT 36   // floats per gate slot in LDS (GR_CAM_SLOT of gr_camera.h)
-#define GR_CAM_OBST_SLOTS 56
-#define GR_CAM_OSLOT 16  // floats per obstacle slot in LDS: slot floats 0-15 (frame, primitive, kind)
-// dynamic LDS of the camera kernel: ray tables + per wave (gate slots, one 64-bit gate mask per 8x32 tile
-// [+ obstacle slots and their tile masks] + an 8-row staging band); every part a multiple of 4 floats
+// Camera launch (camera_kernel, gr_camera.hip).  Dynamic LDS: the normal table and the ray tables (workgroup), then
+// per wave its gate slots, one 64-bit gate mask per 8x32 tile, on obstacle tracks its obstacle slots (the first
+// `slots` obstacles in view; any further ones are set up again per tile from their records), their windows' pixel
+// rectangles (one packed word per slot) and tile masks, and an 8-row staging band.  Every part a multiple of 4 floats.
+#define GR_CAM_GATE_SLOT 36     // floats per gate slot in LDS (GR_CAM_SLOT of gr_camera.h)
+#define GR_CAM_OSLOT 16         // floats per obstacle slot in LDS: slot floats 0-15 (frame, primitive, kind)
+#define GR_CAM_OBST_SLOTS_MAX 64  // (64-bit tile masks)
+#define GR_CAM_OBST_SLOTS 56    // obstacle slots per wave (obstacles in view per env: p99 41, max 53 over 1 024 envs)
+#define CAM_WAVES 4             // waves per workgroup
+#define CAM_LDS_PER_CU 163840
+// (the normal table of the image noise, gr_normal_table.h: 4 floats per entry)
+#define CAM_NORMAL_FLOATS (4 * 320)
 __host__ __device__ inline size_t camera_tile_mask_floats(int width, int height) {
   return (2 * (size_t)((height + 7) / 8) * ((width + 31) / 32) + 3) & ~(size_t)3;
 }
-// obstacle slots + their windows' pixel rectangles (one packed word per slot) + one 64-bit mask per 8x32 tile (the
-// slots that can cover a pixel of the tile)
-static_assert(GR_CAM_OBST_SLOTS <= 64 && GR_CAM_OBST_SLOTS % 4 == 0, "obstacle slots: 64-bit tile masks, float4 parts");
-__host__ __device__ inline size_t camera_obst_floats(int width, int height) {
-  return (size_t)GR_CAM_OBST_SLOTS * (GR_CAM_OSLOT + 1) + camera_tile_mask_floats(width, height);
+// obstacle slots + their pixel rectangles + their tile masks
+__host__ __device__ inline size_t camera_obst_floats(int width, int height, int slots) {
+  return slots > 0 ? (size_t)slots * GR_CAM_OSLOT + (((size_t)slots + 3) & ~(size_t)3) +
+                         camera_tile_mask_floats(width, height)
+                   : 0;
 }
-// (the normal table of the image noise, gr_normal_table.h: 4 floats per entry, first in LDS)
-#define CAM_NORMAL_FLOATS (4 * 320)
-inline size_t camera_lds_bytes(int width, int height, int max_gates, bool obst) {
+__host__ __device__ inline size_t camera_wave_floats(int width, int height, int max_gates, int slots) {
+  return (size_t)max_gates * GR_CAM_GATE_SLOT + camera_tile_mask_floats(width, height) +
+         camera_obst_floats(width, height, slots) + 8 * (size_t)width;
+}
+inline size_t camera_lds_bytes(int width, int height, int max_gates, int waves, int slots) {
   const size_t wpad = (size_t)((width + 3) & ~3), hpad = (size_t)((height + 3) & ~3);
-  const size_t os = obst ? camera_obst_floats(width, height) : 0;
-  return 4 * (CAM_NORMAL_FLOATS + wpad + hpad +
-              4 * ((size_t)max_gates * GR_CAM_GATE_SLOT + camera_tile_mask_floats(width, height) + os + 8 * (size_t)width));
+  return 4 * (CAM_NORMAL_FLOATS + wpad + hpad + (size_t)waves * camera_wave_floats(width, height, max_gates, slots));
+}
+struct CamLaunch {
+  int waves, slots;
+  size_t lds;
+};
+// 4-wave workgroups; on obstacle tracks GR_CAM_OBST_SLOTS slots per wave, or slots_req > 0 (tests: the path for
+// obstacles beyond the slots).  (Two 10-wave workgroups per CU with 43 slots, for 5 waves per SIMD, measured 1.68 ->
+// 1.93 ms per obstacle re-render: the second workgroup's waves do not fit beside the first's at 96 VGPRs, r6za)
+inline CamLaunch camera_launch_config(int width, int height, int max_gates, bool obst, int slots_req) {
+  const int slots = obst ? (slots_req > 0 ? slots_req : GR_CAM_OBST_SLOTS) : 0;
+  return {CAM_WAVES, slots, camera_lds_bytes(width, height, max_gates, CAM_WAVES, slots)};
 }
 
 // which step_kernel instantiation gr_step launches for these arguments (GR_STEP_* of gr.h)

@@ -37,8 +37,9 @@ extern "C" {
 
 /* 2: GR_NUM_PLANES 17 (obstacle hint, rotor constants), gr_policy_args.precision, the observation sink and the
  * status word; gr_policy_args_size.  3: gr_stem1_* y_rows / gy_rows.  4: the gr_stem1_* / gr_stem12_* row indices
- * (`rows` after `off`).  5: gr_stem12_backward_w2 (conv2's weight gradient inside the first block's backward) */
-#define GR_ABI_VERSION 5
+ * (`rows` after `off`).  5: gr_stem12_backward_w2 (conv2's weight gradient inside the first block's backward).
+ * 6: gr_test_camera_slots */
+#define GR_ABI_VERSION 6
 
 /* ---- status codes ---- */
 #define GR_OK 0
@@ -543,6 +544,9 @@ int gr_device_status(gr_ctx* ctx, uint32_t* status, int clear, void* stream);
 #define GR_FAULT_NONE 0
 #define GR_FAULT_OBST_NO_SIGNAL 1 /* the policy waves never signal the obstacle mask */
 int gr_test_inject_fault(gr_ctx* ctx, int fault);
+/* Obstacle slots per camera wave (tests: the path for obstacles beyond the slots; 0: the launch's own choice,
+ * 40-64 by the LDS; 1-64: that many). */
+int gr_test_camera_slots(gr_ctx* ctx, int32_t slots);
 
 /* Column sums of a row-major [rows][cols] matrix (fp32 or bf16 elements), fp32 out: the bias gradients of
  * the PPO update's tall mini-batches (standalone/rsl_rl/ext/algorithms/ppo.py:168-190 -> loss.backward()

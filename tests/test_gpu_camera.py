@@ -136,12 +136,16 @@ def test_camera_full_size_properties():
     env.close()
 
 
-def test_camera_obstacles_in_view_and_slot_overflow():
-    """Drones placed just behind obstacles looking at them (obstacles fill the image), on 32-gate tracks
-    whose obstacle count exceeds the LDS slots per wave (GR_CAM_OBST_SLOTS = 56): the re-setup path for obstacles beyond the
-    slots must give the oracle's bits too."""
+@pytest.mark.parametrize("gates,slots", [(32, 0), (8, 0), (8, 6), (32, 6)])
+def test_camera_obstacles_in_view_and_slot_overflow(gates, slots):
+    """Drones placed just behind obstacles looking at them (obstacles fill the image), on tracks whose obstacle count
+    exceeds the LDS slots per wave: the re-setup path for obstacles beyond the slots must give the oracle's bits too.
+    slots = 0: the launch's own choice (8 gates: two 10-wave workgroups per CU, 40-64 slots; 32 gates: 4-wave
+    workgroups, 56 slots); 6: gr_test_camera_slots forces the overflow path for most envs."""
     n = 256
-    env, orc = make(n, gates=32)
+    env, orc = make(n, gates=gates)
+    if slots:
+        env._call("gr_test_camera_slots", slots)
     env.reset()
     orc.reset(None)
     orc.camera(_abi.GR_CAM_RESET)
@@ -171,7 +175,7 @@ def test_camera_obstacles_in_view_and_slot_overflow():
     orc.camera(_abi.GR_CAM_OBSERVE)
     compare(env, orc, "placed observe")
     assert (orc.depth < 4.0).mean() > 0.05
-    assert ot.counts.max() > 56
+    assert ot.counts.max() > 64
     env.close()
 
 
