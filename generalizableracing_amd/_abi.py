@@ -342,13 +342,13 @@ def _declare(lib):
         "gr_bn_running_update": (C.c_int, [vp, vp, vp, vp, C.c_int32, C.c_float, C.c_float, C.c_int32, C.c_int32, vp]),
         "gr_tsgemm": (C.c_int, [vp, C.c_int64, vp, C.c_int32, vp, C.c_int64, C.c_int64, C.c_int32, C.c_int32, vp]),
         "gr_stem12_forward": (C.c_int, [vp, C.c_int64, C.c_int64, vp, C.c_int32, vp, C.c_int32, C.c_int32, vp, C.c_int32,
-                                        vp, vp, C.c_float, C.c_int32, C.c_float, vp, C.c_int32, vp, vp, vp, vp, vp]),
+                                        vp, vp, C.c_float, C.c_int32, C.c_float, vp, C.c_int32, vp, vp, vp, vp, vp, vp]),
         "gr_stem12_backward": (C.c_int, [vp, C.c_int64, C.c_int64, vp, C.c_int32, vp, C.c_int32, C.c_int32, vp, C.c_int32,
                                          vp, vp, vp, C.c_int32, C.c_float, vp, C.c_int32, vp, vp, vp, vp, vp, vp]),
         "gr_stem12_backward_w2_scratch_doubles": (C.c_int64, [C.c_int32]),
         "gr_stem12_backward_w2": (C.c_int, [vp, C.c_int64, C.c_int64, vp, C.c_int32, vp, C.c_int32, C.c_int32, vp,
-                                            C.c_int32, vp, vp, vp, C.c_int32, C.c_float, vp, C.c_int32, vp, vp, vp, vp,
-                                            vp, vp, vp]),
+                                            C.c_int32, vp, vp, vp, vp, C.c_int32, C.c_float, vp, C.c_int32, vp, vp, vp,
+                                            vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name) and os.environ.get("GR_LIB_PATH"):

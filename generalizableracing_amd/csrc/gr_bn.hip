@@ -1228,16 +1228,21 @@ __global__ __launch_bounds__(SMF_THREADS) void stem12f_kernel(Stem1 s, Sm12fArgs
 }
 
 hipError_t stem12g_launch(const Stem1& s, const Sm12fArgs& f, int act, hipStream_t st);  // (below, with stem12w)
-int stem_stats_launch(const Stem1& s, double* part, float* shift, hipStream_t st);       // (below): blocks written
+// (below): blocks written; mom (64 doubles, may be null): the pixel moments gr_stem12_backward_w2 takes A2 / A3 from,
+// through mpart (grid x 64 + 9 doubles of workspace)
+int stem_stats_launch(const Stem1& s, double* part, float* shift, hipStream_t st, double* mpart = nullptr,
+                      double* mom = nullptr);
 
 hipError_t launch_stem12_forward(const Stem1& s, const float* bw, const float* bb, float eps, int act, float slope,
-                                 const float* w2f, int n2, float* y, float* z2, float* stats, double* part,
-                                 hipStream_t st) {
+                                 const float* w2f, int n2, float* y, float* z2, float* stats, double* moments,
+                                 double* part, hipStream_t st) {
   const int nb = stem_blocks(s);
   float* shift = reinterpret_cast<float*>(part + (size_t)nb * 2 * s.c);
   const long long m = (long long)s.nimg * (s.na + s.nbt);
   const int grid = nb < SM_GRID ? nb : SM_GRID;
-  const int sgrid = stem_stats_launch(s, part, shift, st);
+  // (the moment partials in the workspace's wgrad region, unused by a forward: nb x 27 c >= grid x 64 + 9)
+  double* mpart = part + (size_t)nb * 2 * s.c + 2 * s.c;
+  const int sgrid = stem_stats_launch(s, part, shift, st, mpart, moments);
   hipLaunchKernelGGL(bn_stats_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, shift, m, s.c, sgrid, eps, part, stats);
   long long room = s.ld - s.off;
   const int cap = (int)(room < 1 ? 1 : room < SM_IMG_CAP ? room : SM_IMG_CAP);
@@ -1369,6 +1374,7 @@ struct Sw12Args {
   double* g2part;    // [grid][9][16][32]
   float slope;
   int n2;
+  const double* mom;  // the forward's pixel moments (stem_moments_final), or null: A2 / A3 summed here
 };
 
 // an image buffer: the staged floats (a DMA instruction's 256 rounded up) + 4 (a zero float, 16-byte aligned stride)
@@ -1416,7 +1422,9 @@ __device__ __forceinline__ void sw_dma_gz2(const float* g, float* dst, int nflt,
 // code (5 at 72 x 96); 0: taken from n2 at run time (other image sizes; the same arithmetic).  Image buffers carry one
 // zero float past their end and the gz2 buffers zero rows up to 16 nch: the gathers of rows past n2 and of taps past 9
 // read zeros there (gy1 = 0 and G2 += 0 on rows past n2, B operands 0), so no per-row masks are applied.
-template <int ACT, bool V4, int NCH>
+// MOM: A2 = sum px and A3 = sum xhat px come from the forward's pixel moments (stem12w_final), so the kernel skips
+// their 4 MFMA per table-a tile and table b's tiles altogether (23 MFMA per tile instead of 27)
+template <int ACT, bool V4, int NCH, bool MOM>
 __global__ __launch_bounds__(SW_THREADS) void stem12w_kernel(Stem1 s, Sw12Args q, int cap) {
   extern __shared__ float4 sm_dyn4[];
   __shared__ int s_span;
@@ -1558,12 +1566,12 @@ __global__ __launch_bounds__(SW_THREADS) void stem12w_kernel(Stem1 s, Sw12Args q
           y1[v] = bn_act<ACT>(zz, q.slope);
           f0 += gz[v];
           f1 += gz[v] * xh[v];
-          fa2 += pb[v];
+          if constexpr (!MOM) fa2 += pb[v];
         }
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
           c1 = sm_mfma(gz[v], pb[v], c1);
-          c3 = sm_mfma(xh[v], pb[v], c3);
+          if constexpr (!MOM) c3 = sm_mfma(xh[v], pb[v], c3);
         }
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
@@ -1578,7 +1586,7 @@ __global__ __launch_bounds__(SW_THREADS) void stem12w_kernel(Stem1 s, Sw12Args q
       }
       if (extra) tile(NM, 512 * w, oa[NM], ob[NM], wf8, ga8, gb8);
       // table b's tiles (cells under no conv2 patch: gz = 0; only A3 and A2), to the waves nch .. 7 in turn
-      for (int tb = w - nch; tb >= 0 && tb < ntb; tb += SW_WAVES - nch) {
+      for (int tb = w - nch; !MOM && tb >= 0 && tb < ntb; tb += SW_WAVES - nch) {
         const int r0 = 16 * tb, nv = nbt - r0 < 16 ? nbt - r0 : 16;
         const short* ta = s.pix + (size_t)(na + r0 + (i < nv ? i : 0)) * 9;
         float pa[3] = {src[ta[g]], src[ta[g + 4]], src[ta[8]]};
@@ -1677,10 +1685,36 @@ __global__ __launch_bounds__(BN_FINAL_THREADS) void stem12w_final(int blocks, co
                                                                  const float* __restrict__ sums,
                                                                  const float* __restrict__ stats,
                                                                  const float* __restrict__ bw, double m,
+                                                                 const double* __restrict__ mom,
+                                                                 const float* __restrict__ cw,
                                                                  float* __restrict__ gw, float* __restrict__ gw2) {
   if (blockIdx.x == 0) {
     __shared__ double tot[3 * 144];
-    for (int a = 0; a < 3; ++a) bn_final_sums(wpart + a * 144, 144, blocks, tot + a * 144, 3 * 144);
+    for (int a = 0; a < (mom ? 1 : 3); ++a) bn_final_sums(wpart + a * 144, 144, blocks, tot + a * 144, 3 * 144);
+    if (mom) {
+      // A2[tap] = sum p_tap and A3[ch][tap] = sum xhat_ch p_tap over every cell (xhat = (x - mu) is, x = W . p) from
+      // the moments of d = p - p0: with c = W . p0 - mu,  sum (x - mu) p_tap = sum_k W_k (M[k][tap] + p0_tap S_k)
+      // + c (S_tap + N p0_tap)
+      __syncthreads();
+      for (int v = threadIdx.x; v < 144; v += BN_FINAL_THREADS) {
+        const int ch = v / 9, tap = v % 9;
+        const double* S = mom;
+        const double* p0 = mom + 54;  // (ST_NM)
+        double wp0 = 0.0, acc = 0.0;
+        for (int k = 0; k < 9; ++k) {
+          const int a = k < tap ? k : tap, b = k < tap ? tap : k;  // M[k][tap] in the upper triangle
+          const double mkt = mom[9 + a * 9 - a * (a - 1) / 2 + (b - a)];
+          const double wk = (double)cw[ch * 9 + k];
+          wp0 += wk * p0[k];
+          acc += wk * (mkt + p0[tap] * S[k]);
+        }
+        const double a2 = S[tap] + m * p0[tap];
+        acc += (wp0 - (double)stats[ch]) * a2;
+        tot[144 + v] = a2;
+        tot[288 + v] = (double)stats[16 + ch] * acc;
+      }
+      __syncthreads();
+    }
     for (int v = threadIdx.x; v < 144; v += BN_FINAL_THREADS) {
       const int ch = v / 9;
       const double mg = (double)sums[ch] / m, mgx = (double)sums[16 + ch] / m;
@@ -1724,34 +1758,38 @@ long long stem12w_scratch_doubles(int nimg) {
 bool stem12w_covers(int n2) { return n2 >= 1 && n2 <= 16 * SW_MAX_CHUNKS; }
 
 // every instantiation opts in to its > 64 KB of dynamic LDS once (the largest any shape needs)
-template <int ACT, bool V4, int NCH>
+template <int ACT, bool V4, int NCH, bool MOM>
 static hipError_t sw_launch_t(int grid, size_t lds, hipStream_t st, const Stem1& s, const Sw12Args& q, int cap) {
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem12w_kernel<ACT, V4, NCH>),
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem12w_kernel<ACT, V4, NCH, MOM>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize,
                                              (int)sw_lds_bytes(16 * SW_MAX_CHUNKS, SM_IMG_CAP));
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL((stem12w_kernel<ACT, V4, NCH>), dim3(grid), dim3(SW_THREADS), lds, st, s, q, cap);
+  hipLaunchKernelGGL((stem12w_kernel<ACT, V4, NCH, MOM>), dim3(grid), dim3(SW_THREADS), lds, st, s, q, cap);
   return hipGetLastError();
 }
 // 72 x 96 images (five chunks) straight-line; other sizes with the chunk count at run time
 template <int ACT, bool V4>
 static hipError_t sw_launch(int nch, int grid, size_t lds, hipStream_t st, const Stem1& s, const Sw12Args& q, int cap) {
-  return nch == SW_MAX_CHUNKS ? sw_launch_t<ACT, V4, SW_MAX_CHUNKS>(grid, lds, st, s, q, cap)
-                              : sw_launch_t<ACT, V4, 0>(grid, lds, st, s, q, cap);
+  if (q.mom)
+    return nch == SW_MAX_CHUNKS ? sw_launch_t<ACT, V4, SW_MAX_CHUNKS, true>(grid, lds, st, s, q, cap)
+                                : sw_launch_t<ACT, V4, 0, true>(grid, lds, st, s, q, cap);
+  return nch == SW_MAX_CHUNKS ? sw_launch_t<ACT, V4, SW_MAX_CHUNKS, false>(grid, lds, st, s, q, cap)
+                              : sw_launch_t<ACT, V4, 0, false>(grid, lds, st, s, q, cap);
 }
 
-hipError_t launch_stem12_backward_w2(const Stem1& s, const float* bw, const float* bb, const float* stats, int act,
-                                     float slope, const float* gz2, int n2, const float* w2t, float* gconv, float* gbw,
-                                     float* gbb, float* gw2, double* part, hipStream_t st) {
+hipError_t launch_stem12_backward_w2(const Stem1& s, const float* bw, const float* bb, const float* stats,
+                                     const double* moments, int act, float slope, const float* gz2, int n2,
+                                     const float* w2t, float* gconv, float* gbw, float* gbb, float* gw2, double* part,
+                                     hipStream_t st) {
   const int grid = stem12w_grid(s.nimg);
   float* sums = reinterpret_cast<float*>(part + (size_t)grid * 32);
   double* wpart = part + (size_t)grid * 32 + 16;
   double* g2part = wpart + (size_t)grid * 3 * 144;
-  Sw12Args q{bw, bb, stats, gz2, w2t, part, wpart, g2part, slope, n2};
+  Sw12Args q{bw, bb, stats, gz2, w2t, part, wpart, g2part, slope, n2, moments};
   long long room = s.ld - s.off;
   const int cap = (int)(room < 1 ? 1 : room < SM_IMG_CAP ? room : SM_IMG_CAP);
   const size_t lds = sw_lds_bytes(n2, cap);
@@ -1768,7 +1806,7 @@ hipError_t launch_stem12_backward_w2(const Stem1& s, const float* bw, const floa
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(bn_bwd_final, dim3(1), dim3(BN_FINAL_THREADS), 0, st, s.c, grid, part, gbw, gbb, sums);
   hipLaunchKernelGGL(stem12w_final, dim3(1 + (SW_G2 + 127) / 128), dim3(BN_FINAL_THREADS), 0, st, grid, wpart, g2part,
-                     sums, stats, bw, (double)s.nimg * (double)(s.na + s.nbt), gconv, gw2);
+                     sums, stats, bw, (double)s.nimg * (double)(s.na + s.nbt), moments, s.w, gconv, gw2);
   return hipGetLastError();
 }
 
@@ -1964,8 +2002,11 @@ hipError_t stem12g_launch(const Stem1& s, const Sm12fArgs& f, int act, hipStream
 constexpr int ST_GRID = 256;
 constexpr int ST_U = 4;  // images in flight per lane
 constexpr int ST_NM = 9 + 45;  // moments per lane: sum d_k, sum d_k d_l (l >= k)
+constexpr int ST_MSTRIDE = 64;  // a block's moment row in the moment partials
+static_assert(ST_NM == 54 && ST_NM + 9 <= 64, "the moment layout stem12w_final reads");
 
-__global__ __launch_bounds__(1024) void stem_stats_kernel(Stem1 s, double* __restrict__ part, float* __restrict__ shift) {
+__global__ __launch_bounds__(1024) void stem_stats_kernel(Stem1 s, double* __restrict__ part, float* __restrict__ shift,
+                                                         double* __restrict__ mpart) {
   __shared__ double red[16][ST_NM];
   __shared__ double tot[ST_NM];
   __shared__ int key[STEM_MAX_CELLS];
@@ -2085,6 +2126,11 @@ __global__ __launch_bounds__(1024) void stem_stats_kernel(Stem1 s, double* __res
     double t = 0.0;
     for (int ww = 0; ww < nw; ++ww) t += red[ww][threadIdx.x];
     tot[threadIdx.x] = t;
+    if (mpart) mpart[(size_t)blockIdx.x * ST_MSTRIDE + threadIdx.x] = t;  // (the backward's A2 / A3, stem_moments_final)
+  }
+  if (mpart && blockIdx.x == 0 && threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) mpart[(size_t)gridDim.x * ST_MSTRIDE + k] = (double)p0[k];
   }
   __syncthreads();
   if (threadIdx.x < 2 * s.c) {  // part[block][0][ch] = W . S, [1][ch] = W^T M W (fp64)
@@ -2107,14 +2153,49 @@ __global__ __launch_bounds__(1024) void stem_stats_kernel(Stem1 s, double* __res
   }
 }
 
-int stem_stats_launch(const Stem1& s, double* part, float* shift, hipStream_t st) {
+// the moment totals for gr_stem12_backward_w2: mom[0 .. 8] = sum d, [9 .. 53] = sum d d^T (upper triangle, row-major),
+// [54 .. 62] = p0 (the first cell of image 0), all fp64.  Eight segments of the block range, each summing its blocks
+// in order with 32 loads in flight, then the segments in order (a single 64-lane loop over 256 blocks: 96 us)
+__global__ __launch_bounds__(512) void stem_moments_final(const double* __restrict__ mpart, int grid, double* __restrict__ mom) {
+  __shared__ double seg[8][ST_MSTRIDE];
+  const int t = threadIdx.x & 63, sg = threadIdx.x >> 6;
+  const int per = (grid + 7) / 8, b0 = sg * per, b1 = b0 + per < grid ? b0 + per : grid;
+  double acc = 0.0;
+  if (t < ST_NM) {
+    int b = b0;
+    for (; b + 31 < b1; b += 32) {
+      double v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) v[u] = mpart[(size_t)(b + u) * ST_MSTRIDE + t];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) acc += v[u];
+    }
+    for (; b < b1; ++b) acc += mpart[(size_t)b * ST_MSTRIDE + t];
+  }
+  seg[sg][t] = acc;
+  __syncthreads();
+  if (sg == 0) {
+    if (t < ST_NM) {
+      double a = 0.0;
+      for (int u = 0; u < 8; ++u) a += seg[u][t];
+      mom[t] = a;
+    } else if (t < ST_NM + 9) {
+      mom[t] = mpart[(size_t)grid * ST_MSTRIDE + (t - ST_NM)];
+    } else {
+      mom[t] = 0.0;
+    }
+  }
+}
+
+int stem_stats_launch(const Stem1& s, double* part, float* shift, hipStream_t st, double* mpart, double* mom) {
   const int ncell = s.na + s.nbt;
   const int nw = (ncell + 63) / 64;
   // (no more partial rows than the callers' workspace holds before the shift: stem_blocks(s), gr_stem1_scratch_doubles)
   const int nb = stem_blocks(s);
   int grid = s.nimg < ST_GRID ? (s.nimg < 1 ? 1 : s.nimg) : ST_GRID;
   grid = grid < nb ? grid : nb;
-  hipLaunchKernelGGL(stem_stats_kernel, dim3(grid), dim3(64 * nw), 0, st, s, part, shift);
+  hipLaunchKernelGGL(stem_stats_kernel, dim3(grid), dim3(64 * nw), 0, st, s, part, shift, mom ? mpart : nullptr);
+  if (mom) hipLaunchKernelGGL(stem_moments_final, dim3(1), dim3(512), 0, st, mpart, grid, mom);
   return grid;
 }
 

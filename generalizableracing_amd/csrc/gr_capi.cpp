@@ -1083,15 +1083,16 @@ int gr_patch_wgrad_bnact(const float* z, int64_t ld, const float* gy, int64_t m,
 int gr_stem12_forward(const float* obs, int64_t ld, int64_t off, const int64_t* rows, int32_t nimg, const int16_t* pix, int32_t na,
                       int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b, float eps,
                       int32_t act, float slope, const float* w2f, int32_t n2, float* y, float* z2, float* stats,
-                      double* part, void* stream) {
+                      double* moments, double* part, void* stream) {
   if (!stem1_args_ok(obs, nimg, pix, na, nb, conv_w, c, bn_w, bn_b) || c != 16 || !w2f || !z2 || !stats ||
       !part || !aligned16(w2f) || (y && !aligned16(y)) || !aligned16(z2) || !aligned16(stats) ||
+      (reinterpret_cast<uintptr_t>(moments) & 7u) ||
       (act != GR_POLICY_ACT_LRELU && act != GR_POLICY_ACT_ELU) || n2 < 1 || na != 9 * n2 ||
       (int64_t)nimg * n2 * 32 >= (int64_t)1 << 31)
     return GR_ERR_ARG;
   const gr::Stem1 s = stem1_of(obs, ld, off, rows, nimg, pix, na, nb, conv_w, c, (int64_t)nimg * na);
-  const hipError_t e = gr::launch_stem12_forward(s, bn_w, bn_b, eps, act, slope, w2f, n2, y, z2, stats, part,
-                                                 (hipStream_t)stream);
+  const hipError_t e = gr::launch_stem12_forward(s, bn_w, bn_b, eps, act, slope, w2f, n2, y, z2, stats, moments,
+                                                 part, (hipStream_t)stream);
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 
@@ -1116,16 +1117,18 @@ int64_t gr_stem12_backward_w2_scratch_doubles(int32_t nimg) {
 
 int gr_stem12_backward_w2(const float* obs, int64_t ld, int64_t off, const int64_t* rows, int32_t nimg, const int16_t* pix,
                           int32_t na, int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b,
-                          const float* stats, int32_t act, float slope, const float* gz2, int32_t n2, const float* w2t,
-                          float* g_conv_w, float* g_bn_w, float* g_bn_b, float* g_w2, double* part, void* stream) {
+                          const float* stats, const double* moments, int32_t act, float slope, const float* gz2,
+                          int32_t n2, const float* w2t, float* g_conv_w, float* g_bn_w, float* g_bn_b, float* g_w2,
+                          double* part, void* stream) {
   if (!stem1_args_ok(obs, nimg, pix, na, nb, conv_w, c, bn_w, bn_b) || c != 16 || !stats || !gz2 || !w2t ||
       !g_conv_w || !g_bn_w || !g_bn_b || !g_w2 || !part || !aligned16(gz2) || !aligned16(w2t) || !aligned16(stats) ||
+      (reinterpret_cast<uintptr_t>(moments) & 7u) ||
       (act != GR_POLICY_ACT_LRELU && act != GR_POLICY_ACT_ELU) || !gr::stem12w_covers(n2) || na != 9 * n2 ||
       (int64_t)nimg * n2 * 32 >= (int64_t)1 << 31)
     return GR_ERR_ARG;
   const gr::Stem1 s = stem1_of(obs, ld, off, rows, nimg, pix, na, nb, conv_w, c, (int64_t)nimg * na);
-  const hipError_t e = gr::launch_stem12_backward_w2(s, bn_w, bn_b, stats, act, slope, gz2, n2, w2t, g_conv_w, g_bn_w,
-                                                     g_bn_b, g_w2, part, (hipStream_t)stream);
+  const hipError_t e = gr::launch_stem12_backward_w2(s, bn_w, bn_b, stats, moments, act, slope, gz2, n2, w2t, g_conv_w,
+                                                     g_bn_w, g_bn_b, g_w2, part, (hipStream_t)stream);
   return e == hipSuccess ? GR_OK : GR_ERR_HIP;
 }
 

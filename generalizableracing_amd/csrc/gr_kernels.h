@@ -120,15 +120,16 @@ hipError_t launch_stem1_backward(const Stem1& s, const float* bw, const float* b
                                  hipStream_t st);
 // the first block's forward with conv2 (16 -> 32, 3x3 / 3) fused into its apply pass: y1 and z2 (gr_bn.hip stem12f_kernel)
 hipError_t launch_stem12_forward(const Stem1& s, const float* bw, const float* bb, float eps, int act, float slope,
-                                 const float* w2f, int n2, float* y, float* z2, float* stats, double* part,
-                                 hipStream_t st);
+                                 const float* w2f, int n2, float* y, float* z2, float* stats, double* moments,
+                                 double* part, hipStream_t st);
 // ... and with conv2's weight gradient gw2 [32][144] too (position-major waves, y1 recomputed: gr_bn.hip stem12w_kernel;
 // n2 <= 80), so the forward needs to store no y1
 long long stem12w_scratch_doubles(int nimg);
 bool stem12w_covers(int n2);
-hipError_t launch_stem12_backward_w2(const Stem1& s, const float* bw, const float* bb, const float* stats, int act,
-                                     float slope, const float* gz2, int n2, const float* w2t, float* gconv, float* gbw,
-                                     float* gbb, float* gw2, double* part, hipStream_t st);
+hipError_t launch_stem12_backward_w2(const Stem1& s, const float* bw, const float* bb, const float* stats,
+                                     const double* moments, int act, float slope, const float* gz2, int n2,
+                                     const float* w2t, float* gconv, float* gbw, float* gbb, float* gw2, double* part,
+                                     hipStream_t st);
 // the same backward with conv2's input gradient formed inside the passes (C = 16, na = 9 n2; gr_bn.hip stem12b_kernel)
 hipError_t launch_stem12_backward(const Stem1& s, const float* bw, const float* bb, const float* stats, int act,
                                   float slope, const float* gz2, int n2, const float* w2t, float* gconv, float* gbw,

@@ -145,6 +145,9 @@ class _Stem1(torch.autograd.Function):
 # stores no y1 and no separate gz2^T y1 pass runs); False: the round-5 form (y1 stored, gr_patch_wgrad) for A/B
 STEM12_W2 = True
 STEM12_W2_MAX_N2 = 80  # (gr_stem12_backward_w2 covers conv2 patch counts up to 80 per image: 72 x 96 images)
+# the backward's sums of the pixels and of xhat x pixels (conv1's weight gradient) from the forward's pixel moments
+# instead of 4 MFMA per tile and table b's tiles (gr_stem12_forward / gr_stem12_backward_w2 `moments`); False: A/B
+STEM12_MOMENTS = True
 
 
 def _w2_path(fused_forward: bool, na: int) -> bool:
@@ -174,6 +177,8 @@ class _Stem12(torch.autograd.Function):
         w = conv_w.detach().reshape(16, 9).contiguous()
         bw, bb = bn_w.detach().contiguous(), bn_b.detach().contiguous()
         w2d = w2.detach()
+        # the statistics pass's pixel moments, when the backward will take conv1's A2 / A3 sums from them
+        mom = torch.empty(64 if (w2_path and STEM12_MOMENTS) else 0, device=img.device, dtype=torch.float64)
         if fused_forward:
             # conv2 inside the first block's apply pass: w2f[j][g][o][v] = W2[o][j * 16 + 4 g + v]
             w2f = w2d.reshape(32, 9, 4, 4).permute(1, 2, 0, 3).contiguous()
@@ -182,7 +187,7 @@ class _Stem12(torch.autograd.Function):
                                        w.data_ptr(), 16, bw.data_ptr(), bb.data_ptr(), float(eps), act, float(slope),
                                        w2f.data_ptr(),
                                        na // 9, y.data_ptr() if keep_y else None, z2.data_ptr(), stats.data_ptr(),
-                                       part.data_ptr(), _stream(img))
+                                       mom.data_ptr() if mom.numel() else None, part.data_ptr(), _stream(img))
         else:  # the first block's kernels, then conv2 as a GEMM (the A/B reference of the fused forward)
             rc = lib.gr_stem1_forward(img.data_ptr(), img.stride(0), 0, _rows_ptr(rows), nimg, pix.data_ptr(), na, nb,
                                       w.data_ptr(), 16, bw.data_ptr(), bb.data_ptr(), float(eps), act, float(slope),
@@ -190,7 +195,7 @@ class _Stem12(torch.autograd.Function):
             z2 = y.view(-1, 144) @ w2d.t() if rc == 0 else None
         if rc != 0:
             raise RuntimeError(f"gr_stem12_forward failed (status {rc})")
-        ctx.save_for_backward(img, w, bw, bb, stats, y, w2d)
+        ctx.save_for_backward(img, w, bw, bb, stats, y, w2d, mom)
         ctx.pix = pix
         ctx.rows = rows
         ctx.args = (na, nb, act, slope, conv_w.shape)
@@ -203,7 +208,7 @@ class _Stem12(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             raise RuntimeError("the fused stem computes no gradient for the image")
         lib = _abi.load()
-        img, w, bw, bb, stats, y, w2d = ctx.saved_tensors
+        img, w, bw, bb, stats, y, w2d, mom = ctx.saved_tensors
         na, nb, act, slope, wshape = ctx.args
         rows = ctx.rows
         nimg = img.shape[0] if rows is None else rows.numel()
@@ -220,7 +225,8 @@ class _Stem12(torch.autograd.Function):
             part = torch.empty(int(lib.gr_stem12_backward_w2_scratch_doubles(nimg)), device=img.device,
                                dtype=torch.float64)
             rc = lib.gr_stem12_backward_w2(img.data_ptr(), img.stride(0), 0, _rows_ptr(rows), nimg, ctx.pix.data_ptr(),
-                                           na, nb, w.data_ptr(), 16, bw.data_ptr(), bb.data_ptr(), stats.data_ptr(), act,
+                                           na, nb, w.data_ptr(), 16, bw.data_ptr(), bb.data_ptr(), stats.data_ptr(),
+                                           mom.data_ptr() if mom.numel() else None, act,
                                            float(slope), gz2.data_ptr(), na // 9, w2t.data_ptr(), gconv.data_ptr(),
                                            gbw.data_ptr(), gbb.data_ptr(), gw2.data_ptr(), part.data_ptr(), _stream(img))
             if rc != 0:

@@ -38,7 +38,7 @@ extern "C" {
 /* 2: GR_NUM_PLANES 17 (obstacle hint, rotor constants), gr_policy_args.precision, the observation sink and the
  * status word; gr_policy_args_size.  3: gr_stem1_* y_rows / gy_rows.  4: the gr_stem1_* / gr_stem12_* row indices
  * (`rows` after `off`).  5: gr_stem12_backward_w2 (conv2's weight gradient inside the first block's backward).
- * 6: gr_test_camera_slots */
+ * 6: gr_test_camera_slots; gr_stem12_forward / gr_stem12_backward_w2 `moments` */
 #define GR_ABI_VERSION 6
 
 /* ---- status codes ---- */
@@ -509,11 +509,12 @@ int gr_patch_wgrad(const float* x, int64_t ld, const float* gy, int64_t m, int32
  * z2 [nimg * n2][32] (na = 9 n2; row 9 p + j of an image = position j of patch p).  w2f: conv2's weight as
  * [9][4][32][4] floats, w2f[((j * 4 + g) * 32 + o) * 4 + v] = W[o][4 g + v][j / 3][j % 3] (16-byte aligned).
  * Same workspace and stats as gr_stem1_forward.  y may be NULL (a forward with no backward: y is only kept for
- * conv2's weight gradient). */
+ * conv2's weight gradient).  moments (64 doubles, 8-byte aligned, may be NULL): the statistics pass's pixel moments
+ * over every cell (sums of d = p - p0 and of d d^T, and p0), for gr_stem12_backward_w2. */
 int gr_stem12_forward(const float* obs, int64_t ld, int64_t off, const int64_t* rows, int32_t nimg, const int16_t* pix, int32_t na,
                       int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b, float eps,
                       int32_t act, float slope, const float* w2f, int32_t n2, float* y, float* z2, float* stats,
-                      double* part, void* stream);
+                      double* moments, double* part, void* stream);
 /* The same backward when the next layer is the stem's conv2, Conv2d(c = 16, 32, 3, stride 3, no bias), on the
  * nimg x na table-a rows grouped as its patches (row 9 p + j of an image = position j of patch p, na = 9 n2): takes
  * conv2's OUTPUT gradient gz2 [nimg * n2][32] (16-byte aligned) and forms conv2's input gradient inside the passes
@@ -528,12 +529,15 @@ int gr_stem12_backward(const float* obs, int64_t ld, int64_t off, const int64_t*
  * VisionActorCritic's patch GEMM): y1 = act(bn(conv1)) is recomputed from the image (bit-identical to the forward's),
  * so gr_stem12_forward may be called with y = NULL.  n2 <= 80 (72 x 96 images: 80).  Workspace:
  * gr_stem12_backward_w2_scratch_doubles(nimg) doubles.  Deterministic (fixed-order sums).  Replaces the pair
- * gr_stem12_backward + gr_patch_wgrad(gz2, y1) of the reference's conv2 backward (vision_actor_critic.py:93-105). */
+ * gr_stem12_backward + gr_patch_wgrad(gz2, y1) of the reference's conv2 backward (vision_actor_critic.py:93-105).
+ * moments: the same forward's (gr_stem12_forward), or NULL: with them the conv1 weight gradient's sums of the pixels
+ * and of xhat x pixels come from the moments in fp64 and the pass skips those products. */
 int64_t gr_stem12_backward_w2_scratch_doubles(int32_t nimg);
 int gr_stem12_backward_w2(const float* obs, int64_t ld, int64_t off, const int64_t* rows, int32_t nimg, const int16_t* pix,
                           int32_t na, int32_t nb, const float* conv_w, int32_t c, const float* bn_w, const float* bn_b,
-                          const float* stats, int32_t act, float slope, const float* gz2, int32_t n2, const float* w2t,
-                          float* g_conv_w, float* g_bn_w, float* g_bn_b, float* g_w2, double* part, void* stream);
+                          const float* stats, const double* moments, int32_t act, float slope, const float* gz2,
+                          int32_t n2, const float* w2t, float* g_conv_w, float* g_bn_w, float* g_bn_b, float* g_w2,
+                          double* part, void* stream);
 
 /* Device status: the GR_STATUS_* bits the kernels of this context raised since the last clear (0: none).
  * Synchronises `stream` (the stream the steps ran on); clear != 0 resets the word.  A raised bit means the

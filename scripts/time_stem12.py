@@ -2,14 +2,14 @@
 gr_stem12_backward_w2's stem12w_kernel backward) at one PPO mini-batch of images (24 576 of 72 x 96): HIP events around
 `reps` forward + backward calls.  Run under rocprofv3 for the per-kernel split (or --pmc counters).
 
-    python scripts/time_stem12.py [--nimg 24576] [--reps 20] [--stored-y1]
+    python scripts/time_stem12.py [--nimg 24576] [--reps 20] [--stored-y1] [--no-moments] [--roofline]
 
 `roofline(nimg)` (bench.py's vision leg) times the forward and the backward separately and states each against its
 bound from the algorithmic bytes and flops per image:
   forward  = statistics pass (image read, conv1 of all 768 cells) + stem12g (image read, conv1 of the 720 table-a
              cells, BN + act, conv2; z2 written);
   backward = stem12w (image + gz2 read; conv1 recomputed, conv2's input and weight gradients, conv1's weight-gradient
-             sums) + its two small fixed-order reductions.
+             sums: with the forward's pixel moments only A1 = sum gz x pixels) + its two small fixed-order reductions.
 """
 import argparse
 import json
@@ -37,6 +37,9 @@ CONV2 = 2 * PATCHES * C2 * C1 * 9  # flops of conv2 (forward; each backward prod
 STATS = (IMG_BYTES, CELLS * CONV1)
 STEM12G = (IMG_BYTES + Z2_BYTES, CELLS_A * CONV1 + CONV2)
 STEM12W = (IMG_BYTES + Z2_BYTES, CELLS * CONV1 + 2 * CONV2 + CELLS_A * CONV1 + CELLS * CONV1)
+# with the forward's pixel moments (fused_bn.STEM12_MOMENTS): conv1 recomputed on the table-a cells, conv2's two
+# products, A1; A2 / A3 come from the moments
+STEM12W_MOM = (IMG_BYTES + Z2_BYTES, CELLS_A * CONV1 + 2 * CONV2 + CELLS_A * CONV1)
 
 
 def _setup(nimg, dev="cuda:0"):
@@ -84,7 +87,9 @@ def roofline(nimg=24576, reps=10):
     fwd = sum(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(reps)) * 1e3 / reps
     bwd = sum(ev[2 * r + 1].elapsed_time(ev[2 * r + 2]) for r in range(reps)) * 1e3 / reps
     f = _bound((STATS[0] + STEM12G[0], STATS[1] + STEM12G[1]), nimg, fwd)
-    b = _bound(STEM12W, nimg, bwd)
+    from generalizableracing_amd.rsl_rl import fused_bn
+
+    b = _bound(STEM12W_MOM if fused_bn.STEM12_MOMENTS else STEM12W, nimg, bwd)
     return {"images": nimg, "forward": f, "backward": b,
             "note": "forward = statistics pass + stem12g_kernel (+ bn_stats_final); backward = stem12w_kernel (+ its two "
                     "fixed-order reductions); bytes / flops algorithmic per image (scripts/time_stem12.py, DESIGN §4c), "
@@ -98,11 +103,15 @@ def main():
     ap.add_argument("--stored-y1", action="store_true", help="the round-5 pair (y1 stored by stem12f_kernel, conv2's "
                     "weight gradient by gr_patch_wgrad) instead of stem12g / gr_stem12_backward_w2")
     ap.add_argument("--roofline", action="store_true", help="the forward / backward split against their bounds")
+    ap.add_argument("--no-moments", action="store_true", help="the backward sums A2 / A3 itself (round-6 first form) "
+                    "instead of taking them from the forward's pixel moments")
     a = ap.parse_args()
-    if a.stored_y1:
-        from generalizableracing_amd.rsl_rl import fused_bn
+    from generalizableracing_amd.rsl_rl import fused_bn
 
+    if a.stored_y1:
         fused_bn.STEM12_W2 = False
+    if a.no_moments:
+        fused_bn.STEM12_MOMENTS = False
     if a.roofline:
         print(json.dumps(roofline(a.nimg)))
         return

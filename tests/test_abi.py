@@ -157,9 +157,9 @@ def test_stem12_w2_backward_rejects_shapes_it_does_not_cover():
     lib = _abi.load()
     p = 0x10000
 
-    def call(c=16, na=720, nb=48, n2=80, gz2=p, w2t=p, gw2=p, act=_abi.GR_POLICY_ACT_LRELU):
-        return lib.gr_stem12_backward_w2(p, 6928, 16, None, 8, p, na, nb, p, c, p, p, p, act, 0.01, gz2, n2, w2t, p, p,
-                                         p, gw2, p, None)
+    def call(c=16, na=720, nb=48, n2=80, gz2=p, w2t=p, gw2=p, act=_abi.GR_POLICY_ACT_LRELU, mom=None):
+        return lib.gr_stem12_backward_w2(p, 6928, 16, None, 8, p, na, nb, p, c, p, p, p, mom, act, 0.01, gz2, n2, w2t,
+                                         p, p, p, gw2, p, None)
 
     assert call(c=8) == -1
     assert call(n2=81, na=729) == -1   # past the 80 patches the kernel holds
@@ -167,6 +167,7 @@ def test_stem12_w2_backward_rejects_shapes_it_does_not_cover():
     assert call(gz2=p + 4) == -1
     assert call(gw2=None) == -1
     assert call(act=7) == -1
+    assert call(mom=p + 4) == -1  # (the forward's moments: 8-byte aligned doubles, or null)
     assert lib.gr_stem12_backward_w2_scratch_doubles(0) == -1
     assert lib.gr_stem12_backward_w2_scratch_doubles(1) == 32 + 16 + 432 + 4608
     assert lib.gr_stem12_backward_w2_scratch_doubles(24576) == 256 * (32 + 432 + 4608) + 16
@@ -178,14 +179,16 @@ def test_stem12_forward_rejects_shapes_it_does_not_cover():
     lib = _abi.load()
     p = 0x10000
 
-    def call(c=16, na=720, n2=80, w2f=p, z2=p, act=_abi.GR_POLICY_ACT_LRELU):
-        return lib.gr_stem12_forward(p, 6928, 16, None, 8, p, na, 48, p, c, p, p, 1e-5, act, 0.01, w2f, n2, p, z2, p, p, None)
+    def call(c=16, na=720, n2=80, w2f=p, z2=p, act=_abi.GR_POLICY_ACT_LRELU, mom=None):
+        return lib.gr_stem12_forward(p, 6928, 16, None, 8, p, na, 48, p, c, p, p, 1e-5, act, 0.01, w2f, n2, p, z2, p, mom,
+                                     p, None)
 
     assert call(c=32) == -1
     assert call(na=718) == -1
     assert call(w2f=p + 8) == -1
     assert call(z2=None) == -1
     assert call(act=5) == -1
+    assert call(mom=p + 4) == -1
 
 
 def test_patch_wgrad_rejects_shapes_it_does_not_cover():

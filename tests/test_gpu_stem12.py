@@ -92,15 +92,20 @@ def test_stem12_backward_matches_unfused_and_float64(img_res, nimg, act):
         assert _rel(g_f[k], g64[k]) <= 1e-4, (k, "vs float64", _rel(g_f[k], g64[k]))
 
 
-@pytest.mark.parametrize("img_res,nimg,act,indexed", [((72, 96), 512, "lrelu", False), ((72, 96), 300, "elu", True),
-                                                      ((36, 48), 300, "lrelu", False), ((72, 96), 1, "lrelu", False),
-                                                      ((72, 96), 700, "lrelu", True)])
-def test_stem12_w2_backward_matches_the_stored_y1_path(img_res, nimg, act, indexed):
+@pytest.mark.parametrize("img_res,nimg,act,indexed,moments", [((72, 96), 512, "lrelu", False, True),
+                                                              ((72, 96), 512, "lrelu", False, False),
+                                                              ((72, 96), 300, "elu", True, True),
+                                                              ((36, 48), 300, "lrelu", False, True),
+                                                              ((36, 48), 300, "lrelu", False, False),
+                                                              ((72, 96), 1, "lrelu", False, True),
+                                                              ((72, 96), 700, "lrelu", True, True)])
+def test_stem12_w2_backward_matches_the_stored_y1_path(img_res, nimg, act, indexed, moments):
     """gr_stem12_backward_w2 (conv2's weight gradient inside the first block's backward, y1 recomputed, the forward
     storing no y1: stem12g_kernel) against the round-5 pair (y1 stored by stem12f_kernel, gr_stem12_backward +
     gr_patch_wgrad): conv2's output within 1e-6, every gradient within 1e-5 relative (the conv1 weight's within 1e-4: a cancelling
     combination of three sums, reduced in another order), the same running statistics; repeats bit-identical.
-    Row-indexed batches (the graphed update's form) included; 700 images run 256 workgroups of 2-3 images."""
+    Row-indexed batches (the graphed update's form) included; 700 images run 256 workgroups of 2-3 images.  moments:
+    the conv1 weight gradient's pixel sums from the forward's pixel moments (fp64) instead of the pass's products."""
     from generalizableracing_amd.rsl_rl import fused_bn
     from generalizableracing_amd.rsl_rl.fused_bn import stem12_bn_act_conv
 
@@ -115,8 +120,8 @@ def test_stem12_w2_backward_matches_the_stored_y1_path(img_res, nimg, act, index
     gz = torch.randn(nimg * n2, 32, device=DEV, generator=g)
 
     def run(w2_path):
-        old = fused_bn.STEM12_W2
-        fused_bn.STEM12_W2 = w2_path
+        old, old_m = fused_bn.STEM12_W2, fused_bn.STEM12_MOMENTS
+        fused_bn.STEM12_W2, fused_bn.STEM12_MOMENTS = w2_path, moments
         try:
             bn = copy.deepcopy(bn1)
             cw = conv1.weight.detach().clone().requires_grad_(True)
@@ -125,7 +130,7 @@ def test_stem12_w2_backward_matches_the_stored_y1_path(img_res, nimg, act, index
             (z2 * gz).sum().backward()
             return z2.detach(), {"conv1": cw.grad, "bn_w": bn.weight.grad, "bn_b": bn.bias.grad, "conv2": w2.grad}, bn
         finally:
-            fused_bn.STEM12_W2 = old
+            fused_bn.STEM12_W2, fused_bn.STEM12_MOMENTS = old, old_m
 
     z_new, g_new, bn_new = run(True)
     z_old, g_old, bn_old = run(False)
