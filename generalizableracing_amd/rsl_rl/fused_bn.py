@@ -170,6 +170,7 @@ class _Stem12(torch.autograd.Function):
         # (keep_y False: no backward will run, so y1 — kept only for conv2's weight gradient — is not stored; nor when
         # that gradient is formed inside the first block's backward)
         w2_path = _w2_path(fused_forward, na)
+        backward_follows = keep_y
         keep_y = (keep_y and not w2_path) or not fused_forward
         y = torch.empty(nimg * na if keep_y else 0, 16, device=img.device, dtype=torch.float32)
         stats = torch.empty(4, 16, device=img.device, dtype=torch.float32)
@@ -178,7 +179,8 @@ class _Stem12(torch.autograd.Function):
         bw, bb = bn_w.detach().contiguous(), bn_b.detach().contiguous()
         w2d = w2.detach()
         # the statistics pass's pixel moments, when the backward will take conv1's A2 / A3 sums from them
-        mom = torch.empty(64 if (w2_path and STEM12_MOMENTS) else 0, device=img.device, dtype=torch.float64)
+        mom = torch.empty(64 if (w2_path and STEM12_MOMENTS and backward_follows) else 0, device=img.device,
+                          dtype=torch.float64)
         if fused_forward:
             # conv2 inside the first block's apply pass: w2f[j][g][o][v] = W2[o][j * 16 + 4 g + v]
             w2f = w2d.reshape(32, 9, 4, 4).permute(1, 2, 0, 3).contiguous()
