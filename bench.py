@@ -72,6 +72,7 @@ sys.path.insert(0, ROOT)
 
 from generalizableracing_amd.envs.racing_cfg import RacingEnvCfg, SceneCfg, SimCfg, TerrainCfg  # noqa: E402
 from generalizableracing_amd.envs.racing_env import RacingEnv  # noqa: E402
+from generalizableracing_amd import _abi as _abi_mod  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TFS = 157.3  # MI355X dense fp32 matrix peak (v_mfma_f32_16x16x4_f32; MI355X_MICROARCH.md)
@@ -984,11 +985,19 @@ def main():
                          "frac_of_stream_floor": STREAM_FLOOR_US / us if n == 65536 and not a.obstacles else None,
                          "bytes_per_env_step": {"read": rd, "written": wr}},
             "cpu_baseline": cpu,
+            # which binary ran: the sources libgr.so was built from, against this tree's (a stale build shows false)
+            "libgr": {"path": _abi_mod.LIB_PATH if not os.environ.get("GR_LIB_PATH") else os.environ["GR_LIB_PATH"],
+                      "source_sha256": _lib_sha(), "matches_tree": _lib_sha() == _abi_mod.tree_source_sha256()},
             **extra,
         }
         print(json.dumps(line))
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def _lib_sha():
+    f = getattr(_abi_mod.load(), "gr_source_sha256", None)
+    return f().decode() if f is not None else None
 
 
 if __name__ == "__main__":

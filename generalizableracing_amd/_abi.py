@@ -224,7 +224,7 @@ GR_FAULT_NONE, GR_FAULT_OBST_NO_SIGNAL = 0, 1
 STATUS_TEXT = {GR_STATUS_OBST_WAIT_TIMEOUT: "a physics wave gave up waiting for its obstacle mask (stale mask used)"}
 
 EXPORTS = [
-    "gr_abi_version", "gr_config_default", "gr_config_size", "gr_create", "gr_destroy", "gr_last_error",
+    "gr_abi_version", "gr_source_sha256", "gr_config_default", "gr_config_size", "gr_create", "gr_destroy", "gr_last_error",
     "gr_num_blocks", "gr_num_log_rows", "gr_log_finalize", "gr_bytes_per_env_step", "gr_bind_tracks", "gr_bind_obstacles", "gr_swap_terrain", "gr_bind_buffers", "gr_bind_obs_sink", "gr_init", "gr_reset",
     "gr_step", "gr_observe", "gr_device_status", "gr_test_inject_fault", "gr_test_camera_slots", "gr_set_timing", "gr_read_timing", "gr_test_dynamics", "gr_test_math",
     "gr_test_philox",
@@ -276,6 +276,7 @@ def _declare(lib):
         "gr_observe": (C.c_int, [vp, vp]),
         "gr_step_kernel_variant": (C.c_int, [vp]),
         "gr_device_status": (C.c_int, [vp, C.POINTER(C.c_uint32), C.c_int, vp]),
+        "gr_source_sha256": (C.c_char_p, []),
         "gr_test_inject_fault": (C.c_int, [vp, C.c_int]),
         "gr_test_camera_slots": (C.c_int, [vp, C.c_int32]),
         "gr_set_timing": (C.c_int, [vp, C.c_int]),
@@ -356,6 +357,30 @@ def _declare(lib):
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
+
+
+def tree_source_sha256() -> str | None:
+    """The SHA-256 gr_source_sha256() reports for a library built from this tree's sources: csrc/Makefile's SRCS then
+    HDRS, in its order, concatenated (None when the sources are not here)."""
+    import hashlib
+
+    csrc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc")
+    mk = os.path.join(csrc, "Makefile")
+    if not os.path.exists(mk):
+        return None
+    lists = {}
+    for line in open(mk):
+        for var in ("SRCS", "HDRS"):
+            if line.startswith(var + " :="):
+                lists[var] = line.split(":=", 1)[1].split()
+    h = hashlib.sha256()
+    for f in lists.get("SRCS", []) + lists.get("HDRS", []):
+        path = os.path.normpath(os.path.join(csrc, f.replace("$(HERE)", "")))
+        if not os.path.exists(path):
+            return None
+        with open(path, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
 
 
 def load(path: str | None = None):

@@ -253,6 +253,9 @@ typedef struct gr_camera_buffers {
 typedef struct gr_ctx gr_ctx;
 
 int gr_abi_version(void);
+/* SHA-256 (64 hex digits) of the sources this library was built from: generalizableracing_amd/csrc's SRCS then HDRS
+ * in the order its Makefile lists them, concatenated (a stale binary next to newer sources shows as a mismatch). */
+const char* gr_source_sha256(void);
 int gr_config_default(gr_config* cfg);
 size_t gr_config_size(void);
 int gr_create(const gr_config* cfg, gr_ctx** out);

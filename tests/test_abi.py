@@ -27,6 +27,13 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, name), name
 
 
+def test_library_was_built_from_these_sources():
+    """gr_source_sha256(): the in-tree libgr.so is the build of this tree's csrc sources (Makefile's SRCS + HDRS); a
+    stale binary beside edited sources fails here instead of testing old kernels."""
+    lib = _abi.load()
+    assert lib.gr_source_sha256().decode() == _abi.tree_source_sha256()
+
+
 def test_config_layout_and_defaults():
     lib = _abi.load()
     assert lib.gr_config_size() == C.sizeof(_abi.GrConfig)
